@@ -1,0 +1,479 @@
+"""Deterministic synthetic Delta tables (checkpoint Parquet + JSON commit tail).
+
+Test and benchmark input tooling, not product code. Writes tables whose `_delta_log` has the layout
+Delta Kernel reads:
+
+* a checkpoint at version ``ckpt_version`` — classic single-part
+  (``%020d.checkpoint.parquet``) or multi-part (``%020d.checkpoint.%010d.%010d.parquet``,
+  ``kernel-api/.../internal/util/FileNames.java:191-201``) — with the Spark checkpoint column
+  layout (optional ``add``/``remove``/``metaData``/``protocol`` structs, map<string,string>
+  partitionValues as ``key_value`` repeated groups);
+* ``n_commits`` newline-delimited JSON commits after it, mixing new adds, removes of checkpoint
+  files, re-adds of removed paths and duplicate adds;
+* ``_last_checkpoint``.
+
+Paths follow ``<part>/part-<i%1000:05d>-<uuid4>.c000.snappy.parquet`` with ``<part>`` =
+``date=2024-MM-DD``, seed 20250218 by default.
+"""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+import pyarrow as pa
+import pyarrow.parquet as pq
+
+SEED = 20250218
+HEX = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+Z85 = np.frombuffer(
+    b"0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ.-:+=^!/*?&<>()[]{}@%$#",
+    dtype=np.uint8)
+
+STR = pa.string()
+MAP_SS = pa.map_(pa.string(), pa.string())
+DV_TYPE = pa.struct([
+    ("storageType", STR), ("pathOrInlineDv", STR), ("offset", pa.int32()),
+    ("sizeInBytes", pa.int32()), ("cardinality", pa.int64()), ("maxRowIndex", pa.int64())])
+STATS_PARSED_TYPE = pa.struct([
+    ("numRecords", pa.int64()),
+    ("minValues", pa.struct([("id", pa.int64()), ("name", STR)])),
+    ("maxValues", pa.struct([("id", pa.int64()), ("name", STR)])),
+    ("nullCount", pa.struct([("id", pa.int64()), ("name", pa.int64())]))])
+
+
+@dataclass
+class TableSpec:
+    n_adds: int = 100_000
+    n_parts: int = 1
+    ckpt_version: int = 10
+    n_commits: int = 10
+    adds_per_commit: int = 50
+    removes_per_commit: int = 50
+    readd_frac: float = 0.1          # fraction of commit adds that re-add a removed path
+    dup_frac: float = 0.05           # fraction of commit adds that duplicate an earlier commit add
+    ckpt_removes: int = 0            # tombstone rows stored in the checkpoint (ignored by replay)
+    pv_keys: int = 1                 # 1: {date}, 2: {date, region}
+    with_stats: bool = False
+    with_stats_parsed: bool = False
+    dv_frac: float = 0.0
+    compression: str = "none"
+    data_page_version: str = "1.0"
+    use_dictionary: bool = True
+    delta_binary_packed: bool = False
+    row_group_size: int = 1 << 20
+    max_rows_per_page: int = 20_000  # parquet-mr 1.12 page row-count limit
+    write_page_index: bool = True
+    hot_frac: float = 0.0            # C5 skew: fraction of paths under one hot partition
+    variable_paths: bool = False     # add random suffixes / escapes so lengths vary
+    seed: int = SEED
+    extra: dict = field(default_factory=dict)
+
+
+def _uuid4(rng, n):
+    b = rng.integers(0, 256, size=(n, 16), dtype=np.uint8)
+    b[:, 6] = (b[:, 6] & 0x0F) | 0x40
+    b[:, 8] = (b[:, 8] & 0x3F) | 0x80
+    hx = np.empty((n, 32), dtype=np.uint8)
+    hx[:, 0::2] = HEX[b >> 4]
+    hx[:, 1::2] = HEX[b & 15]
+    out = np.full((n, 36), ord("-"), dtype=np.uint8)
+    out[:, 0:8] = hx[:, 0:8]
+    out[:, 9:13] = hx[:, 8:12]
+    out[:, 14:18] = hx[:, 12:16]
+    out[:, 19:23] = hx[:, 16:20]
+    out[:, 24:36] = hx[:, 20:32]
+    return out
+
+
+def _digits(vals, width):
+    out = np.empty((len(vals), width), dtype=np.uint8)
+    v = np.asarray(vals, dtype=np.int64).copy()
+    for i in range(width - 1, -1, -1):
+        out[:, i] = 48 + (v % 10)
+        v //= 10
+    return out
+
+
+_MDAYS = np.array([31, 29, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31])
+
+
+def _dates(day_idx):
+    """day index 0..365 in 2024 -> (n, 10) 'YYYY-MM-DD' bytes."""
+    cum = np.concatenate([[0], np.cumsum(_MDAYS)])
+    month = np.searchsorted(cum, day_idx, side="right") - 1
+    day = day_idx - cum[month] + 1
+    out = np.empty((len(day_idx), 10), dtype=np.uint8)
+    out[:, 0:4] = np.frombuffer(b"2024", dtype=np.uint8)
+    out[:, 4] = ord("-")
+    out[:, 5:7] = _digits(month + 1, 2)
+    out[:, 7] = ord("-")
+    out[:, 8:10] = _digits(day, 2)
+    return out
+
+
+def _strings_from_matrix(mat):
+    n, w = mat.shape
+    offs = np.arange(n + 1, dtype=np.int32) * w
+    return pa.StringArray.from_buffers(n, pa.py_buffer(offs.tobytes()),
+                                       pa.py_buffer(np.ascontiguousarray(mat).tobytes()))
+
+
+def _strings_from_list(lst):
+    return pa.array(lst, type=pa.string())
+
+
+def gen_paths(rng, n, start_index, spec: TableSpec):
+    """Returns (list-free) arrow string array of paths + the date-index per path."""
+    n_days = 366
+    day = rng.integers(0, n_days, size=n)
+    if spec.hot_frac > 0:
+        hot = rng.random(n) < spec.hot_frac
+        day[hot] = 77
+    prefix = np.frombuffer(b"date=", dtype=np.uint8)
+    mat = np.empty((n, 83), dtype=np.uint8)
+    mat[:, 0:5] = prefix
+    mat[:, 5:15] = _dates(day)
+    mat[:, 15:21] = np.frombuffer(b"/part-", dtype=np.uint8)
+    mat[:, 21:26] = _digits((np.arange(n) + start_index) % 1000, 5)
+    mat[:, 26] = ord("-")
+    mat[:, 27:63] = _uuid4(rng, n)
+    mat[:, 63:83] = np.frombuffer(b".c000.snappy.parquet", dtype=np.uint8)
+    if not spec.variable_paths:
+        return _strings_from_matrix(mat), day
+    # variable lengths: random extra segment, occasional escapes (still valid java.net.URI input)
+    base = [bytes(r).decode() for r in mat]
+    extra = rng.integers(0, 40, size=n)
+    kinds = rng.integers(0, 10, size=n)
+    out = []
+    for i, p in enumerate(base):
+        k = kinds[i]
+        if k == 0:
+            p = p.replace(".c000", "-" + "x" * int(extra[i]) + ".c000")
+        elif k == 1:
+            p = "s3://Bucket-A/tbl/" + p
+        elif k == 2:
+            p = p.replace("date=", "dt%3A=%2f")
+        elif k == 3:
+            p = "file:/tmp/t%20x/" + p
+        out.append(p)
+    return _strings_from_list(out), day
+
+
+def _pv_array(day, spec: TableSpec, rng):
+    n = len(day)
+    dates = _dates(np.asarray(day))
+    if spec.pv_keys == 1:
+        keys = _strings_from_matrix(np.tile(np.frombuffer(b"date", dtype=np.uint8), (n, 1)))
+        vals = _strings_from_matrix(dates)
+        offs = np.arange(n + 1, dtype=np.int32)
+    else:
+        regions = np.array([b"us-east", b"eu-west", b"ap-south"])
+        r = rng.integers(0, 3, size=n)
+        k = []
+        v = []
+        # interleave date/region per row
+        kmat = np.empty((2 * n, 6), dtype=np.uint8)
+        kmat[0::2] = np.frombuffer(b"date\0\0", dtype=np.uint8)
+        kmat[1::2] = np.frombuffer(b"region", dtype=np.uint8)
+        klen = np.empty(2 * n, dtype=np.int32)
+        klen[0::2] = 4
+        klen[1::2] = 6
+        vmat = np.zeros((2 * n, 10), dtype=np.uint8)
+        vmat[0::2] = dates
+        vlen = np.empty(2 * n, dtype=np.int32)
+        vlen[0::2] = 10
+        for j, reg in enumerate(regions):
+            m = np.where(r == j)[0]
+            vmat[2 * m + 1, :len(reg)] = np.frombuffer(reg, dtype=np.uint8)
+            vlen[2 * m + 1] = len(reg)
+        keys = _ragged(kmat, klen)
+        vals = _ragged(vmat, vlen)
+        offs = np.arange(n + 1, dtype=np.int32) * 2
+        del k, v
+    return pa.MapArray.from_arrays(pa.array(offs), keys, vals)
+
+
+def _ragged(mat, lens):
+    n = mat.shape[0]
+    offs = np.zeros(n + 1, dtype=np.int32)
+    np.cumsum(lens, out=offs[1:])
+    mask = np.arange(mat.shape[1])[None, :] < lens[:, None]
+    data = mat[mask]
+    return pa.StringArray.from_buffers(n, pa.py_buffer(offs.tobytes()), pa.py_buffer(data.tobytes()))
+
+
+def _dv_array(rng, n, frac):
+    present = rng.random(n) < frac
+    m = int(present.sum())
+    z = Z85[rng.integers(0, len(Z85), size=(m, 20))]
+    st = _strings_from_matrix(np.full((m, 1), ord("u"), dtype=np.uint8))
+    pid = _strings_from_matrix(z)
+    off = pa.array(np.ones(m, dtype=np.int32))
+    size = pa.array(rng.integers(30, 4000, size=m).astype(np.int32))
+    card = pa.array(rng.integers(1, 1000, size=m).astype(np.int64))
+    mri = pa.array([None] * m, type=pa.int64())
+    dense = pa.StructArray.from_arrays([st, pid, off, size, card, mri],
+                                       fields=list(DV_TYPE))
+    return _spread(dense, present), present
+
+
+def _spread(dense_arr, present):
+    """Expand a dense array of len sum(present) into len(present) with nulls where ~present."""
+    n = len(present)
+    idx = np.full(n, -1, dtype=np.int64)
+    idx[present] = np.arange(int(present.sum()))
+    take_idx = pa.array(np.where(present, idx, 0))
+    out = dense_arr.take(take_idx)
+    mask = pa.array(~present)
+    return _with_nulls(out, mask)
+
+
+def _with_nulls(arr, mask):
+    if isinstance(arr.type, pa.StructType):
+        return pa.StructArray.from_arrays([arr.field(i) for i in range(arr.type.num_fields)],
+                                          fields=list(arr.type), mask=mask)
+    return pa.compute.if_else(mask, pa.scalar(None, type=arr.type), arr)
+
+
+def _stats_json(ids_min, ids_max, names_min, names_max, nrec):
+    return [
+        '{"numRecords":%d,"minValues":{"id":%d,"name":"%s"},"maxValues":{"id":%d,"name":"%s"},'
+        '"nullCount":{"id":0,"name":0}}' % (nrec[i], ids_min[i], names_min[i], ids_max[i], names_max[i])
+        for i in range(len(nrec))]
+
+
+def _add_struct(rng, n, start_index, spec: TableSpec, data_change: bool, paths=None, day=None):
+    if paths is None:
+        paths, day = gen_paths(rng, n, start_index, spec)
+    pv = _pv_array(day, spec, rng)
+    size = pa.array(rng.integers(1 << 20, 1 << 28, size=n, dtype=np.int64))
+    mtime = pa.array(1_700_000_000_000 + rng.integers(0, 1_000_000_000, size=n, dtype=np.int64))
+    dc = pa.array(np.full(n, data_change))
+    tags = pa.nulls(n, type=MAP_SS)
+    if spec.dv_frac > 0:
+        dv, _ = _dv_array(rng, n, spec.dv_frac)
+    else:
+        dv = pa.nulls(n, type=DV_TYPE)
+    brid = pa.nulls(n, type=pa.int64())
+    drcv = pa.nulls(n, type=pa.int64())
+    arrays = [paths, pv, size, mtime, dc, tags, dv, brid, drcv]
+    fields = [("path", STR), ("partitionValues", MAP_SS), ("size", pa.int64()),
+              ("modificationTime", pa.int64()), ("dataChange", pa.bool_()), ("tags", MAP_SS),
+              ("deletionVector", DV_TYPE), ("baseRowId", pa.int64()),
+              ("defaultRowCommitVersion", pa.int64())]
+    if spec.with_stats or spec.with_stats_parsed:
+        idmin = rng.integers(0, 50_000_000, size=n)
+        idmax = idmin + rng.integers(0, 1_000_000, size=n)
+        nrec = rng.integers(1, 100_000, size=n)
+        names_min = ["n%06d" % x for x in rng.integers(0, 500_000, size=n)] if n < 2_000_000 else None
+    if spec.with_stats:
+        if names_min is None:
+            names_min = ["n%06d" % x for x in rng.integers(0, 500_000, size=n)]
+        stats = pa.array(_stats_json(idmin, idmax, names_min, names_min, nrec), type=STR)
+        arrays.append(stats)
+        fields.append(("stats", STR))
+    if spec.with_stats_parsed:
+        if names_min is None:
+            names_min = ["n%06d" % x for x in rng.integers(0, 500_000, size=n)]
+        nm = pa.array(names_min, type=STR)
+        sp = pa.StructArray.from_arrays([
+            pa.array(nrec.astype(np.int64)),
+            pa.StructArray.from_arrays([pa.array(idmin.astype(np.int64)), nm], names=["id", "name"]),
+            pa.StructArray.from_arrays([pa.array(idmax.astype(np.int64)), nm], names=["id", "name"]),
+            pa.StructArray.from_arrays([pa.array(np.zeros(n, np.int64)), pa.array(np.zeros(n, np.int64))],
+                                       names=["id", "name"])], fields=list(STATS_PARSED_TYPE))
+        arrays.append(sp)
+        fields.append(("stats_parsed", STATS_PARSED_TYPE))
+    return pa.StructArray.from_arrays(arrays, fields=[pa.field(a, t) for a, t in fields])
+
+
+def _remove_type():
+    return pa.struct([("path", STR), ("deletionTimestamp", pa.int64()), ("dataChange", pa.bool_()),
+                      ("extendedFileMetadata", pa.bool_()), ("partitionValues", MAP_SS),
+                      ("size", pa.int64()), ("deletionVector", DV_TYPE), ("baseRowId", pa.int64()),
+                      ("defaultRowCommitVersion", pa.int64())])
+
+
+METADATA_TYPE = pa.struct([
+    ("id", STR), ("name", STR), ("description", STR),
+    ("format", pa.struct([("provider", STR), ("options", MAP_SS)])),
+    ("schemaString", STR), ("partitionColumns", pa.list_(STR)), ("configuration", MAP_SS),
+    ("createdTime", pa.int64())])
+PROTOCOL_TYPE = pa.struct([
+    ("minReaderVersion", pa.int32()), ("minWriterVersion", pa.int32()),
+    ("readerFeatures", pa.list_(STR)), ("writerFeatures", pa.list_(STR))])
+
+SCHEMA_STRING = json.dumps({"type": "struct", "fields": [
+    {"name": "id", "type": "long", "nullable": True, "metadata": {}},
+    {"name": "name", "type": "string", "nullable": True, "metadata": {}},
+    {"name": "date", "type": "string", "nullable": True, "metadata": {}}]}, separators=(",", ":"))
+
+
+def _pm_rows(spec: TableSpec):
+    proto = {"minReaderVersion": 3, "minWriterVersion": 7,
+             "readerFeatures": ["deletionVectors", "v2Checkpoint"],
+             "writerFeatures": ["deletionVectors", "v2Checkpoint"]}
+    meta = {"id": "6f7a3d1e-2b0c-4c1e-9c4a-5a8e7d9b0c11", "name": None, "description": None,
+            "format": {"provider": "parquet", "options": []},
+            "schemaString": SCHEMA_STRING, "partitionColumns": ["date"],
+            "configuration": [("delta.enableDeletionVectors", "true")],
+            "createdTime": 1_700_000_000_000}
+    return proto, meta
+
+
+def build_checkpoint_tables(spec: TableSpec, rng):
+    """Returns (list of arrow tables, one per part, in part order; list of checkpoint add paths)."""
+    n = spec.n_adds
+    parts = []
+    per = [n // spec.n_parts + (1 if i < n % spec.n_parts else 0) for i in range(spec.n_parts)]
+    start = 0
+    all_paths = []
+    proto, meta = _pm_rows(spec)
+    for pi, cnt in enumerate(per):
+        adds = _add_struct(rng, cnt, start, spec, data_change=False)
+        all_paths.append(adds.field("path"))
+        n_pm = 2 if pi == 0 else 0
+        n_rm = spec.ckpt_removes if pi == 0 else 0
+        total = n_pm + cnt + n_rm
+        # row layout: [protocol, metaData] + adds + removes
+        add_col = pa.concat_arrays([pa.nulls(n_pm, type=adds.type), adds,
+                                    pa.nulls(n_rm, type=adds.type)]) if (n_pm or n_rm) else adds
+        rm_type = _remove_type()
+        if n_rm:
+            rpaths, rday = gen_paths(rng, n_rm, 10_000_000 + start, spec)
+            rm = pa.StructArray.from_arrays([
+                rpaths, pa.array(np.full(n_rm, 1_699_000_000_000, np.int64)), pa.array(np.ones(n_rm, bool)),
+                pa.array(np.ones(n_rm, bool)), _pv_array(rday, spec, rng),
+                pa.array(rng.integers(1 << 20, 1 << 28, size=n_rm, dtype=np.int64)),
+                pa.nulls(n_rm, type=DV_TYPE), pa.nulls(n_rm, type=pa.int64()),
+                pa.nulls(n_rm, type=pa.int64())], fields=list(rm_type))
+            rm_col = pa.concat_arrays([pa.nulls(n_pm + cnt, type=rm_type), rm])
+        else:
+            rm_col = pa.nulls(total, type=rm_type)
+        if n_pm:
+            meta_col = pa.concat_arrays([pa.array([None, meta], type=METADATA_TYPE),
+                                         pa.nulls(total - 2, type=METADATA_TYPE)])
+            proto_col = pa.concat_arrays([pa.array([proto, None], type=PROTOCOL_TYPE),
+                                          pa.nulls(total - 2, type=PROTOCOL_TYPE)])
+        else:
+            meta_col = pa.nulls(total, type=METADATA_TYPE)
+            proto_col = pa.nulls(total, type=PROTOCOL_TYPE)
+        t = pa.table({"add": add_col, "remove": rm_col, "metaData": meta_col, "protocol": proto_col})
+        parts.append(t)
+        start += cnt
+    return parts, all_paths
+
+
+def _write_parquet(table, path, spec: TableSpec):
+    kw = dict(compression=spec.compression, data_page_version=spec.data_page_version,
+              write_page_index=spec.write_page_index, row_group_size=spec.row_group_size,
+              max_rows_per_page=spec.max_rows_per_page, write_statistics=True)
+    if spec.delta_binary_packed:
+        kw["use_dictionary"] = False
+        kw["column_encoding"] = {c: "DELTA_BINARY_PACKED" for c in (
+            "add.size", "add.modificationTime")}
+    else:
+        kw["use_dictionary"] = spec.use_dictionary
+    pq.write_table(table, path, **kw)
+
+
+def _json_add(path, day, size, mtime, dv=None, stats=None, pv_keys=1, region=None):
+    d = {"path": path, "partitionValues": {"date": day}, "size": int(size),
+         "modificationTime": int(mtime), "dataChange": True}
+    if pv_keys == 2:
+        d["partitionValues"]["region"] = region or "us-east"
+    if stats is not None:
+        d["stats"] = stats
+    if dv is not None:
+        d["deletionVector"] = dv
+    return {"add": d}
+
+
+def _json_remove(path, day, ts, dv=None):
+    d = {"path": path, "deletionTimestamp": int(ts), "dataChange": True,
+         "extendedFileMetadata": True, "partitionValues": {"date": day}, "size": 1234}
+    if dv is not None:
+        d["deletionVector"] = dv
+    return {"remove": d}
+
+
+def write_table(root: str, spec: TableSpec):
+    """Write the synthetic table under ``root``. Returns a dict describing what was written."""
+    rng = np.random.Generator(np.random.PCG64(spec.seed))
+    log = os.path.join(root, "_delta_log")
+    os.makedirs(log, exist_ok=True)
+    parts, ck_paths = build_checkpoint_tables(spec, rng)
+    v = spec.ckpt_version
+    files = []
+    if spec.n_parts == 1:
+        fn = os.path.join(log, "%020d.checkpoint.parquet" % v)
+        _write_parquet(parts[0], fn, spec)
+        files.append(fn)
+    else:
+        for i, t in enumerate(parts):
+            fn = os.path.join(log, "%020d.checkpoint.%010d.%010d.parquet" % (v, i + 1, spec.n_parts))
+            _write_parquet(t, fn, spec)
+            files.append(fn)
+    lc = {"version": v, "size": int(sum(t.num_rows for t in parts))}
+    if spec.n_parts > 1:
+        lc["parts"] = spec.n_parts
+    with open(os.path.join(log, "_last_checkpoint"), "w") as f:
+        f.write(json.dumps(lc))
+
+    # ---- JSON commit tail ----
+    ck_all = pa.concat_arrays(ck_paths) if len(ck_paths) > 1 else ck_paths[0]
+    n_ck = len(ck_all)
+    new_serial = 0
+    added_in_tail = []      # paths added by commits (candidates for duplicates / removal)
+    removed = []            # paths removed by commits (candidates for re-add)
+    for c in range(spec.n_commits):
+        ver = v + 1 + c
+        lines = [json.dumps({"commitInfo": {"timestamp": 1_700_000_000_000 + ver,
+                                            "operation": "WRITE"}})]
+        # removes
+        for _ in range(spec.removes_per_commit):
+            pick = rng.random()
+            if pick < 0.5 or not added_in_tail:
+                i = int(rng.integers(0, n_ck))
+                p = ck_all[i].as_py()
+            else:
+                p = added_in_tail[int(rng.integers(0, len(added_in_tail)))]
+            removed.append(p)
+            lines.append(json.dumps(_json_remove(p, "2024-01-01", 1_700_000_000_000 + ver)))
+        # adds
+        n_readd = int(round(spec.adds_per_commit * spec.readd_frac))
+        n_dup = int(round(spec.adds_per_commit * spec.dup_frac))
+        n_new = spec.adds_per_commit - n_readd - n_dup
+        adds = []
+        for _ in range(n_readd):
+            if removed:
+                adds.append(removed[int(rng.integers(0, len(removed)))])
+        for _ in range(n_dup):
+            if added_in_tail:
+                adds.append(added_in_tail[int(rng.integers(0, len(added_in_tail)))])
+        if n_new > 0:
+            arr, day = gen_paths(rng, n_new, 5_000_000 + new_serial, spec)
+            new_serial += n_new
+            adds.extend(arr.to_pylist())
+        for p in adds:
+            dv = None
+            if spec.dv_frac > 0 and rng.random() < spec.dv_frac:
+                dv = {"storageType": "u",
+                      "pathOrInlineDv": bytes(Z85[rng.integers(0, len(Z85), 20)]).decode(),
+                      "offset": 1, "sizeInBytes": int(rng.integers(30, 4000)),
+                      "cardinality": int(rng.integers(1, 1000))}
+            stats = None
+            if spec.with_stats:
+                lo = int(rng.integers(0, 50_000_000))
+                stats = ('{"numRecords":10,"minValues":{"id":%d,"name":"a"},"maxValues":'
+                         '{"id":%d,"name":"z"},"nullCount":{"id":0,"name":0}}' % (lo, lo + 100))
+            lines.append(json.dumps(_json_add(p, "2024-01-01", rng.integers(1 << 20, 1 << 28),
+                                              1_700_000_000_000 + ver, dv=dv, stats=stats,
+                                              pv_keys=spec.pv_keys)))
+            added_in_tail.append(p)
+        with open(os.path.join(log, "%020d.json" % ver), "w") as f:
+            f.write("\n".join(lines) + "\n")
+    return {"checkpoint_files": files, "version": v + spec.n_commits,
+            "checkpoint_rows": lc["size"]}

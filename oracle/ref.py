@@ -1,0 +1,621 @@
+"""CPU ORACLE (test infrastructure only) — Delta Kernel log replay restated in Python over the C
+oracle ``oracle/_ref/libdk_ref.so``.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg may import this
+module, and only as the checker / CPU baseline. The product (``delta_amd``) never imports it.
+
+Restates, for the ``getScanFiles`` path:
+
+* log-segment selection and ordering: ``SnapshotManager.getLogSegmentForVersion``
+  (kernel-api/.../internal/snapshot/SnapshotManager.java:311-566, latest version only),
+  ``Checkpointer.getLatestCompleteCheckpointFromList`` (internal/checkpoints/Checkpointer.java:46-73),
+  ``LogSegment.allLogFilesReversed`` (internal/snapshot/LogSegment.java:166-178);
+* file sequencing: ``ActionsIterator.getNextActionsIter`` (internal/replay/ActionsIterator.java:291-362),
+  multi-part grouping ``retrieveRemainingCheckpointFiles`` (:395-417), V2 sidecars
+  ``extractSidecarsFromBatch`` (:256-283);
+* commit JSON decode: ``DefaultJsonHandler.readJsonFiles`` (kernel-defaults/.../engine/
+  DefaultJsonHandler.java:79-157, one batch = up to ``json_batch_size`` lines of ONE file) and
+  ``DefaultJsonRow.decodeElement/decodeField`` (internal/data/DefaultJsonRow.java:136-357);
+* reconciliation: ``ActiveAddFilesIterator.prepareNext`` (internal/replay/ActiveAddFilesIterator.java:146-275)
+  and ``ScanMetrics`` (internal/metrics/ScanMetrics.java:28-40);
+* keys: ``LogReplayUtils.pathToUri`` (internal/replay/LogReplayUtils.java:83-89) +
+  ``DeletionVectorDescriptor.getUniqueId`` (internal/actions/DeletionVectorDescriptor.java:167-174)
+  via the C restatement ``dkr_action_key``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import re
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_ref", "libdk_ref.so")
+_lib = None
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = C.CDLL(_LIB_PATH)
+        L.dkr_open.restype = C.c_void_p
+        L.dkr_open.argtypes = [C.c_char_p, C.c_int64]
+        L.dkr_errmsg.restype = C.c_char_p
+        L.dkr_num_rows.restype = C.c_int64
+        L.dkr_num_rows.argtypes = [C.c_void_p]
+        L.dkr_num_leaves.argtypes = [C.c_void_p]
+        L.dkr_num_row_groups.argtypes = [C.c_void_p]
+        L.dkr_leaf_path.restype = C.c_char_p
+        L.dkr_leaf_path.argtypes = [C.c_void_p, C.c_int]
+        L.dkr_leaf_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+        L.dkr_chunk_info.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int64)]
+        L.dkr_read_leaf.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+        L.dkr_col_free.argtypes = [C.c_void_p]
+        L.dkr_close.argtypes = [C.c_void_p]
+        L.dkr_uri_key.restype = C.c_int64
+        L.dkr_uri_key.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]
+        L.dkr_java_utf8.restype = C.c_int64
+        L.dkr_java_utf8.argtypes = [C.c_char_p, C.c_int64, C.c_char_p, C.c_int64]
+        L.dkr_action_key.restype = C.c_int64
+        L.dkr_action_key.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_char_p, C.c_int64,
+                                     C.c_char_p, C.c_int64, C.c_int, C.c_int32, C.c_char_p, C.c_int64]
+        L.dkr_keyset_new.restype = C.c_void_p
+        L.dkr_keyset_free.argtypes = [C.c_void_p]
+        L.dkr_keyset_or.argtypes = [C.c_void_p, C.c_char_p, C.c_int64, C.c_int]
+        L.dkr_keyset_get.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+        P = C.c_void_p
+        L.dkr_probe_checkpoint.argtypes = [P, C.c_int64, P, P, P, P, P, P, P, P, P, P, C.c_int, P, P, P]
+        _lib = L
+    return _lib
+
+
+class _Col(C.Structure):
+    _fields_ = [("n_rows", C.c_int64), ("n_entries", C.c_int64), ("n_chars", C.c_int64),
+                ("phys", C.c_int32), ("width", C.c_int32), ("max_def", C.c_int32),
+                ("max_rep", C.c_int32), ("rep_def", C.c_int32), ("_pad", C.c_int32),
+                ("row_def", C.c_void_p), ("row_offs", C.c_void_p), ("entry_def", C.c_void_p),
+                ("fixed", C.c_void_p), ("offs", C.c_void_p), ("chars", C.c_void_p)]
+
+
+def _np(ptr, n, dtype):
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    itemsize = np.dtype(dtype).itemsize
+    return np.frombuffer(C.string_at(ptr, n * itemsize), dtype=dtype).copy()
+
+
+@dataclass
+class Column:
+    """Assembled leaf column (same layout the product's dk_column uses)."""
+    path: str
+    phys: int
+    max_def: int
+    max_rep: int
+    rep_def: int
+    n_rows: int
+    row_def: np.ndarray
+    row_offs: np.ndarray | None = None
+    entry_def: np.ndarray | None = None
+    fixed: np.ndarray | None = None   # raw bytes (n * width)
+    width: int = 0
+    offs: np.ndarray | None = None
+    chars: np.ndarray | None = None
+
+    def values(self, dtype):
+        return self.fixed.view(dtype)
+
+    def string(self, i):
+        return bytes(self.chars[self.offs[i]:self.offs[i + 1]])
+
+
+class ParquetFile:
+    PHYS = {0: "BOOLEAN", 1: "INT32", 2: "INT64", 3: "INT96", 4: "FLOAT", 5: "DOUBLE",
+            6: "BYTE_ARRAY", 7: "FIXED_LEN_BYTE_ARRAY"}
+
+    def __init__(self, data: bytes):
+        self._buf = C.create_string_buffer(data, len(data))
+        self._h = lib().dkr_open(self._buf, len(data))
+        if not self._h:
+            raise OracleError(lib().dkr_errmsg().decode())
+        self.num_rows = lib().dkr_num_rows(self._h)
+        self.leaves = [lib().dkr_leaf_path(self._h, i).decode() for i in range(lib().dkr_num_leaves(self._h))]
+
+    @classmethod
+    def open(cls, path):
+        with open(path, "rb") as f:
+            return cls(f.read())
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().dkr_close(self._h)
+            self._h = None
+
+    def leaf_index(self, path):
+        """Field matching by exact name, then case-insensitive (ParquetSchemaUtils.java:92-119)."""
+        if path in self.leaves:
+            return self.leaves.index(path)
+        low = [p.lower() for p in self.leaves]
+        if path.lower() in low:
+            return low.index(path.lower())
+        return -1
+
+    def read(self, path) -> Column | None:
+        i = self.leaf_index(path)
+        if i < 0:
+            return None
+        c = _Col()
+        if lib().dkr_read_leaf(self._h, i, C.byref(c)) != 0:
+            raise OracleError("Error reading Parquet file: " + lib().dkr_errmsg().decode())
+        try:
+            n_val = c.n_entries if c.max_rep > 0 else c.n_rows
+            col = Column(path=path, phys=c.phys, max_def=c.max_def, max_rep=c.max_rep,
+                         rep_def=c.rep_def, n_rows=c.n_rows, width=c.width,
+                         row_def=_np(c.row_def, c.n_rows, np.uint8))
+            if c.max_rep > 0:
+                col.row_offs = _np(c.row_offs, c.n_rows + 1, np.int64)
+                col.entry_def = _np(c.entry_def, c.n_entries, np.uint8)
+            if c.phys == 6:
+                col.offs = _np(c.offs, n_val + 1, np.int64)
+                col.chars = _np(c.chars, c.n_chars, np.uint8)
+            else:
+                col.fixed = _np(c.fixed, n_val * c.width, np.uint8)
+            return col
+        finally:
+            lib().dkr_col_free(C.byref(c))
+
+
+def java_utf8(b: bytes) -> bytes:
+    out = C.create_string_buffer(len(b) * 3 + 8)
+    n = lib().dkr_java_utf8(b, len(b), out, len(out))
+    return out.raw[:n]
+
+
+def action_key(path: bytes, dv) -> bytes:
+    """dv: None or (storageType bytes, pathOrInlineDv bytes, offset int|None)."""
+    cap = len(path) * 3 + 256 + (0 if dv is None else 3 * (len(dv[0]) + len(dv[1])) + 64)
+    out = C.create_string_buffer(cap)
+    if dv is None:
+        n = lib().dkr_action_key(path, len(path), 0, None, 0, None, 0, 0, 0, out, cap)
+    else:
+        st, pid, off = dv
+        n = lib().dkr_action_key(path, len(path), 1, st, len(st), pid, len(pid),
+                                 0 if off is None else 1, 0 if off is None else off, out, cap)
+    if n < 0:
+        raise OracleError("java.net.URISyntaxException: " + path.decode("utf-8", "replace"))
+    return out.raw[:n]
+
+
+# --------------------------------------------------------------------------------------------
+# Log segment (SnapshotManager / Checkpointer / LogSegment restated for the latest snapshot)
+# --------------------------------------------------------------------------------------------
+DELTA_RE = re.compile(r"^(\d{20})\.json$")
+CLASSIC_RE = re.compile(r"^(\d{20})\.checkpoint\.parquet$")
+MULTI_RE = re.compile(r"^(\d{20})\.checkpoint\.(\d{10})\.(\d{10})\.parquet$")
+V2_RE = re.compile(r"^(\d{20})\.checkpoint\.([^.]+)\.(json|parquet)$")
+
+
+@dataclass
+class LogFile:
+    path: str
+    kind: str          # commit | classic | multipart | v2 | sidecar
+    version: int
+    part: int = 0
+    num_parts: int = 0
+
+
+@dataclass
+class LogSegment:
+    log_path: str
+    version: int
+    deltas: list
+    checkpoints: list
+
+    def all_files_reversed(self):
+        """LogSegment.java:171-177: sorted by file name, descending."""
+        return sorted(self.deltas + self.checkpoints, key=lambda f: os.path.basename(f.path), reverse=True)
+
+
+def _classify(name, full):
+    m = DELTA_RE.match(name)
+    if m:
+        return LogFile(full, "commit", int(m.group(1)))
+    m = CLASSIC_RE.match(name)
+    if m:
+        return LogFile(full, "classic", int(m.group(1)))
+    m = MULTI_RE.match(name)
+    if m:
+        return LogFile(full, "multipart", int(m.group(1)), int(m.group(2)), int(m.group(3)))
+    m = V2_RE.match(name)
+    if m:
+        return LogFile(full, "v2", int(m.group(1)))
+    return None
+
+
+def load_log_segment(table_root: str) -> LogSegment:
+    log = os.path.join(table_root, "_delta_log")
+    files = []
+    for name in os.listdir(log):
+        f = _classify(name, os.path.join(log, name))
+        if f:
+            files.append(f)
+    # complete checkpoints grouped by version (CheckpointInstance / Checkpointer.java:46-73)
+    ck = {}
+    for f in files:
+        if f.kind in ("classic", "multipart", "v2"):
+            ck.setdefault((f.version, f.kind, f.num_parts), []).append(f)
+    complete = []
+    for (v, kind, nparts), fs in ck.items():
+        if kind == "multipart":
+            if sorted(x.part for x in fs) == list(range(1, nparts + 1)):
+                complete.append((v, kind, fs))
+        else:
+            complete.append((v, kind, fs[:1]))
+    deltas = sorted([f for f in files if f.kind == "commit"], key=lambda f: f.version)
+    if not deltas and not complete:
+        raise OracleError("No delta files found in the directory: " + log)
+    latest = max([d.version for d in deltas] + [c[0] for c in complete])
+    cks = [c for c in complete if c[0] <= latest]
+    # preference at equal version: v2 > multipart(more parts) > classic (CheckpointInstance.compareTo)
+    rank = {"classic": 0, "multipart": 1, "v2": 2}
+    ckpt = max(cks, key=lambda c: (c[0], rank[c[1]], len(c[2])), default=None)
+    ck_version = ckpt[0] if ckpt else -1
+    tail = [d for d in deltas if d.version > ck_version]
+    expect = ck_version + 1
+    for d in tail:
+        if d.version != expect:
+            raise OracleError("Versions are not contiguous")
+        expect += 1
+    if ckpt is None and (not tail or tail[0].version != 0):
+        raise OracleError("Cannot compute snapshot. Missing delta file version 0.")
+    version = tail[-1].version if tail else ck_version
+    return LogSegment(log, version, tail, list(ckpt[2]) if ckpt else [])
+
+
+# --------------------------------------------------------------------------------------------
+# JSON decode (DefaultJsonRow semantics for the add/remove read schema)
+# --------------------------------------------------------------------------------------------
+def _is_long(v):
+    return isinstance(v, int) and not isinstance(v, bool) and -(1 << 63) <= v < (1 << 63)
+
+
+def _is_int(v):
+    return isinstance(v, int) and not isinstance(v, bool) and -(1 << 31) <= v < (1 << 31)
+
+
+def _dec(node, typ, name):
+    if node is None:
+        return None
+    if typ == "string":
+        if not isinstance(node, str):
+            raise OracleError("Couldn't decode %r, expected a string" % (node,))
+        return node
+    if typ == "long":
+        if not _is_long(node):
+            raise OracleError("Couldn't decode %r, expected a long" % (node,))
+        return node
+    if typ == "int":
+        if not _is_int(node):
+            raise OracleError("Couldn't decode %r, expected a integer" % (node,))
+        return node
+    if typ == "boolean":
+        if not isinstance(node, bool):
+            raise OracleError("Couldn't decode %r, expected a boolean" % (node,))
+        return node
+    if typ == "map":
+        if not isinstance(node, dict):
+            raise OracleError("Couldn't decode %r, expected a map" % (node,))
+        return [(k, _dec(v, "string", k)) for k, v in node.items()]
+    if isinstance(typ, list):
+        if not isinstance(node, dict):
+            raise OracleError("Couldn't decode %r, expected a object" % (node,))
+        return _dec_struct(node, typ)
+    raise OracleError("unsupported type " + str(typ))
+
+
+def _dec_struct(obj, schema):
+    out = {}
+    for name, typ, nullable in schema:
+        v = obj.get(name)
+        if v is None:
+            if not nullable:
+                raise OracleError("Root node at key %s is null but field isn't nullable. Root node: %s"
+                                  % (name, json.dumps(obj)))
+            out[name] = None
+        else:
+            out[name] = _dec(v, typ, name)
+    return out
+
+
+DV_SCHEMA = [("storageType", "string", False), ("pathOrInlineDv", "string", False),
+             ("offset", "int", True), ("sizeInBytes", "int", False), ("cardinality", "long", False)]
+ADD_SCHEMA = [("path", "string", False), ("partitionValues", "map", False), ("size", "long", False),
+              ("modificationTime", "long", False), ("dataChange", "boolean", False),
+              ("deletionVector", DV_SCHEMA, True), ("tags", "map", True), ("baseRowId", "long", True),
+              ("defaultRowCommitVersion", "long", True)]
+ADD_SCHEMA_STATS = ADD_SCHEMA + [("stats", "string", True)]
+REMOVE_SCHEMA = [("path", "string", False), ("deletionVector", DV_SCHEMA, True)]
+SIDECAR_SCHEMA = [("path", "string", False), ("sizeInBytes", "long", False),
+                  ("modificationTime", "long", False)]
+
+
+def read_json_batches(path, batch_size, with_stats=False, sidecars=False):
+    """Yields lists of rows {'add':..., 'remove':...} of at most batch_size lines of this file."""
+    add_s = ADD_SCHEMA_STATS if with_stats else ADD_SCHEMA
+    schema = [("add", add_s, True), ("remove", REMOVE_SCHEMA, True)]
+    if sidecars:
+        schema.append(("sidecar", SIDECAR_SCHEMA, True))
+    with open(path, "rb") as f:
+        data = f.read().decode("utf-8", errors="replace")
+    lines = data.splitlines()  # BufferedReader.readLine: \n, \r, \r\n
+    batch = []
+    for ln in lines:
+        obj = json.loads(ln)
+        batch.append(_dec_struct(obj, schema))
+        if len(batch) == batch_size:
+            yield batch
+            batch = []
+    if batch:
+        yield batch
+
+
+# --------------------------------------------------------------------------------------------
+# Replay
+# --------------------------------------------------------------------------------------------
+ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
+              "add.size", "add.modificationTime", "add.dataChange",
+              "add.deletionVector.storageType", "add.deletionVector.pathOrInlineDv",
+              "add.deletionVector.offset", "add.deletionVector.sizeInBytes",
+              "add.deletionVector.cardinality", "add.tags.key_value.key", "add.tags.key_value.value",
+              "add.baseRowId", "add.defaultRowCommitVersion"]
+STATS_LEAF = "add.stats"
+SIDECAR_LEAVES = ["sidecar.path", "sidecar.sizeInBytes", "sidecar.modificationTime"]
+
+
+@dataclass
+class Counters:
+    addFilesSeen: int = 0
+    addFilesSeenFromDeltaFiles: int = 0
+    activeAddFiles: int = 0
+    duplicateAddFiles: int = 0
+    removeFilesSeenFromDeltaFiles: int = 0
+
+    def as_tuple(self):
+        return (self.addFilesSeen, self.addFilesSeenFromDeltaFiles, self.activeAddFiles,
+                self.duplicateAddFiles, self.removeFilesSeenFromDeltaFiles)
+
+
+@dataclass
+class CheckpointBatch:
+    """One decoded checkpoint / sidecar file (all rows) with its selection."""
+    path: str
+    cols: dict
+    n_rows: int
+    selected: np.ndarray = None
+
+
+@dataclass
+class ReplayResult:
+    version: int
+    json_rows: list = field(default_factory=list)      # selected add dicts, in order
+    checkpoint: list = field(default_factory=list)     # CheckpointBatch in order
+    counters: Counters = field(default_factory=Counters)
+    table_root: str = ""
+
+    def scan_files(self):
+        """Ordered scan-file rows as canonical python tuples (App. B ordering)."""
+        out = [canon_add_from_json(r) for r in self.json_rows]
+        for b in self.checkpoint:
+            idx = np.nonzero(b.selected)[0]
+            out.extend(canon_add_from_cols(b.cols, int(i)) for i in idx)
+        return out
+
+
+def _dv_tuple(dv):
+    if dv is None:
+        return None
+    return (dv["storageType"].encode(), dv["pathOrInlineDv"].encode(), dv["offset"])
+
+
+def json_key(action):
+    return action_key(action["path"].encode("utf-8", "surrogatepass"), _dv_tuple(action["deletionVector"]))
+
+
+def canon_add_from_json(a):
+    dv = a["deletionVector"]
+    return (a["path"].encode("utf-8", "surrogatepass"),
+            tuple((k.encode(), None if v is None else v.encode()) for k, v in a["partitionValues"]),
+            a["size"], a["modificationTime"], a["dataChange"],
+            None if dv is None else (dv["storageType"].encode(), dv["pathOrInlineDv"].encode(), dv["offset"],
+                                     dv["sizeInBytes"], dv["cardinality"]),
+            None if a["tags"] is None else tuple((k.encode(), None if v is None else v.encode()) for k, v in a["tags"]),
+            a["baseRowId"], a["defaultRowCommitVersion"]) + ((a["stats"].encode() if a["stats"] is not None else None,) if "stats" in a else ())
+
+
+def _str_at(col, r, maxdef):
+    if col is None or col.row_def[r] < maxdef:
+        return None
+    return col.string(r)
+
+
+def _fixed_at(col, r, dtype):
+    if col is None or col.row_def[r] < col.max_def:
+        return None
+    w = np.dtype(dtype).itemsize
+    return col.fixed[r * w:(r + 1) * w].view(dtype)[0].item()
+
+
+def _map_at(kc, vc, r):
+    if kc is None:
+        return None
+    if kc.row_def[r] < kc.rep_def - 1:
+        return None
+    b, e = kc.row_offs[r], kc.row_offs[r + 1]
+    out = []
+    for j in range(b, e):
+        k = bytes(kc.chars[kc.offs[j]:kc.offs[j + 1]])
+        v = None
+        if vc is not None and vc.entry_def[j] == vc.max_def:
+            v = bytes(vc.chars[vc.offs[j]:vc.offs[j + 1]])
+        out.append((k, v))
+    return tuple(out)
+
+
+def canon_add_from_cols(cols, r):
+    g = cols.get
+    dvst = g("add.deletionVector.storageType")
+    dv = None
+    if dvst is not None and dvst.row_def[r] >= 2:
+        dv = (_str_at(dvst, r, 3), _str_at(g("add.deletionVector.pathOrInlineDv"), r, 3),
+              _fixed_at(g("add.deletionVector.offset"), r, np.int32),
+              _fixed_at(g("add.deletionVector.sizeInBytes"), r, np.int32),
+              _fixed_at(g("add.deletionVector.cardinality"), r, np.int64))
+    dc = g("add.dataChange")
+    row = (_str_at(g("add.path"), r, 2),
+           _map_at(g("add.partitionValues.key_value.key"), g("add.partitionValues.key_value.value"), r),
+           _fixed_at(g("add.size"), r, np.int64), _fixed_at(g("add.modificationTime"), r, np.int64),
+           None if dc is None or dc.row_def[r] < 2 else bool(dc.fixed[r]),
+           dv,
+           _map_at(g("add.tags.key_value.key"), g("add.tags.key_value.value"), r),
+           _fixed_at(g("add.baseRowId"), r, np.int64), _fixed_at(g("add.defaultRowCommitVersion"), r, np.int64))
+    if STATS_LEAF in cols:
+        row = row + (_str_at(cols[STATS_LEAF], r, 2),)
+    return row
+
+
+def decode_checkpoint_file(path, with_stats=False, extra_leaves=()):
+    pf = ParquetFile.open(path)
+    cols = {}
+    for leaf in ADD_LEAVES + ([STATS_LEAF] if with_stats else []) + list(extra_leaves):
+        cols[leaf] = pf.read(leaf)
+    return pf, cols
+
+
+def probe_checkpoint(cols, n_rows, keyset, counters: Counters):
+    """Checkpoint-batch branch of ActiveAddFilesIterator.prepareNext (isFromCheckpoint=true)."""
+    L = lib()
+    path = cols["add.path"]
+    sel = np.zeros(n_rows, dtype=np.uint8)
+    cnt = np.zeros(5, dtype=np.int64)
+    bad = np.zeros(1, dtype=np.int64)
+    if path is None:
+        return sel
+    st = cols.get("add.deletionVector.storageType")
+    pid = cols.get("add.deletionVector.pathOrInlineDv")
+    off = cols.get("add.deletionVector.offset")
+
+    def ptr(a):
+        return None if a is None else a.ctypes.data
+
+    if st is not None:
+        offv = off.fixed.view(np.int32) if off is not None else np.zeros(n_rows, np.int32)
+        offd = off.row_def if off is not None else np.zeros(n_rows, np.uint8)
+        args = (ptr(st.row_def), ptr(st.offs), ptr(st.chars), ptr(pid.offs), ptr(pid.chars),
+                ptr(offd), ptr(offv), 3)
+    else:
+        args = (None, None, None, None, None, None, None, 3)
+    rc = L.dkr_probe_checkpoint(keyset, n_rows, ptr(path.row_def), ptr(path.offs), ptr(path.chars),
+                                *args, ptr(sel), ptr(cnt), ptr(bad))
+    if rc != 0:
+        raise OracleError("java.net.URISyntaxException at checkpoint row %d" % bad[0])
+    counters.addFilesSeen += int(cnt[0])
+    counters.activeAddFiles += int(cnt[4])
+    counters.duplicateAddFiles += int(cnt[3])
+    return sel
+
+
+def replay(table_root: str, json_batch_size=1024, with_stats=False) -> ReplayResult:
+    """getLatestSnapshot + getScanFiles restated; returns the ordered active scan files + counters."""
+    seg = load_log_segment(table_root)
+    res = ReplayResult(version=seg.version, table_root=table_root)
+    c = res.counters
+    tomb = set()
+    added = set()
+    files = seg.all_files_reversed()
+    queue = list(files)
+    L = lib()
+    keyset = None
+    while queue:
+        f = queue.pop(0)
+        if f.kind == "commit":
+            for batch in read_json_batches(f.path, json_batch_size, with_stats):
+                for row in batch:                                  # :164-183
+                    rm = row["remove"]
+                    if rm is None:
+                        continue
+                    tomb.add(json_key(rm))
+                    c.removeFilesSeenFromDeltaFiles += 1
+                for row in batch:                                  # :192-234
+                    a = row["add"]
+                    if a is None:
+                        continue
+                    c.addFilesSeen += 1
+                    c.addFilesSeenFromDeltaFiles += 1
+                    k = json_key(a)
+                    if k not in added:
+                        added.add(k)
+                        if k not in tomb:
+                            res.json_rows.append(a)
+                            c.activeAddFiles += 1
+                    else:
+                        c.duplicateAddFiles += 1
+            continue
+        # checkpoint files: JSON sets are final from here on (checkpoint files come last)
+        if keyset is None:
+            keyset = L.dkr_keyset_new()
+            for k in added:
+                L.dkr_keyset_or(keyset, k, len(k), 1)
+            for k in tomb:
+                L.dkr_keyset_or(keyset, k, len(k), 2)
+        group = [f]
+        if f.kind in ("multipart", "sidecar"):
+            while queue and queue[0].kind == f.kind and queue[0].version == f.version:
+                group.append(queue.pop(0))
+        for g in group:
+            if g.kind == "v2" and g.path.endswith(".json"):
+                # V2 JSON manifest: rows are checkpoint rows (isFromCheckpoint=true)
+                for batch in read_json_batches(g.path, json_batch_size, with_stats, sidecars=True):
+                    for row in batch:
+                        sc = row.get("sidecar")
+                        if sc is not None:
+                            queue.append(LogFile(os.path.join(seg.log_path, "_sidecars", sc["path"]),
+                                                 "sidecar", g.version))
+                        a = row["add"]
+                        if a is None:
+                            continue
+                        c.addFilesSeen += 1
+                        k = json_key(a)
+                        if k in added:
+                            c.duplicateAddFiles += 1
+                        elif k not in tomb:
+                            res.json_rows.append(a)   # manifest rows precede sidecars
+                            c.activeAddFiles += 1
+                continue
+            extra = SIDECAR_LEAVES if g.kind == "v2" else ()
+            pf, cols = decode_checkpoint_file(g.path, with_stats, extra)
+            if g.kind == "v2":
+                sp = cols.get("sidecar.path")
+                if sp is not None:
+                    for r in range(pf.num_rows):
+                        if sp.row_def[r] >= 2:
+                            queue.append(LogFile(os.path.join(seg.log_path, "_sidecars",
+                                                              sp.string(r).decode()), "sidecar", g.version))
+            b = CheckpointBatch(g.path, cols, pf.num_rows)
+            b.selected = probe_checkpoint(cols, pf.num_rows, keyset, c)
+            res.checkpoint.append(b)
+    if keyset is not None:
+        L.dkr_keyset_free(keyset)
+    return res
