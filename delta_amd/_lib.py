@@ -1,0 +1,114 @@
+"""ctypes binding of libdkgpu.so (include/dkgpu.h). The library is built in-tree by
+delta_amd/build.py. There is no CPU fallback: if the library or a HIP device is missing, every
+entry point raises."""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdkgpu.so")
+_lib = None
+
+
+class DkError(RuntimeError):
+    """Mirrors io.delta.kernel.exceptions.KernelEngineException for errors raised by the engine."""
+
+
+class dk_config(C.Structure):
+    _fields_ = [("parquet_batch_size", C.c_int32), ("json_batch_size", C.c_int32),
+                ("device", C.c_int32), ("flags", C.c_int32)]
+
+
+class dk_column(C.Structure):
+    _fields_ = [("n_rows", C.c_int64), ("n_entries", C.c_int64), ("n_chars", C.c_int64),
+                ("phys", C.c_int32), ("width", C.c_int32), ("max_def", C.c_int32), ("max_rep", C.c_int32),
+                ("rep_def", C.c_int32), ("present", C.c_int32),
+                ("row_def", C.c_void_p), ("row_offs", C.c_void_p), ("entry_def", C.c_void_p),
+                ("fixed", C.c_void_p), ("offs", C.c_void_p), ("chars", C.c_void_p)]
+
+
+EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
+           "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
+           "dk_parquet_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
+           "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_run", "dk_replay_sync",
+           "dk_replay_counters", "dk_replay_json_selection", "dk_replay_ckpt_selection",
+           "dk_replay_kernel_stats", "dk_replay_free"]
+
+
+def lib(build_if_missing=True):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        if not build_if_missing:
+            raise DkError("libdkgpu.so is not built (run delta_amd/build.py)")
+        from . import build
+        build.build()
+    L = C.CDLL(LIB_PATH)
+    P, I32, I64 = C.c_void_p, C.c_int32, C.c_int64
+    sig = {
+        "dk_last_error": (C.c_char_p, []), "dk_version": (C.c_char_p, []),
+        "dk_engine_create": (C.c_int, [C.POINTER(dk_config), C.POINTER(P)]),
+        "dk_engine_destroy": (None, [P]),
+        "dk_parquet_open": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, C.POINTER(P)]),
+        "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),
+        "dk_parquet_num_rows": (I64, [P, I32]),
+        "dk_parquet_column": (C.c_int, [P, I32, I32, C.POINTER(dk_column)]),
+        "dk_parquet_traffic": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
+        "dk_parquet_close": (None, [P]),
+        "dk_json_tail_parse": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(I64), I32, I32, C.POINTER(P)]),
+        "dk_json_tail_rows": (I64, [P]),
+        "dk_json_tail_column": (C.c_int, [P, C.c_char_p, C.POINTER(dk_column)]),
+        "dk_json_tail_free": (None, [P]),
+        "dk_replay_create": (C.c_int, [P, P, P, C.POINTER(P)]),
+        "dk_replay_run": (C.c_int, [P]), "dk_replay_sync": (C.c_int, [P]),
+        "dk_replay_counters": (C.c_int, [P, C.POINTER(I64)]),
+        "dk_replay_json_selection": (C.c_int, [P, P, I64]),
+        "dk_replay_ckpt_selection": (C.c_int, [P, I32, P, I64]),
+        "dk_replay_kernel_stats": (C.c_int, [P, I32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(I64)]),
+        "dk_replay_free": (None, [P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise DkError(lib().dk_last_error().decode("utf-8", "replace"))
+
+
+def _arr(ptr, n, dtype):
+    if not ptr or n <= 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,)).copy()
+
+
+class Column:
+    """Host copy of a dk_column (same field names as the oracle's Column, by design)."""
+
+    def __init__(self, c: dk_column, path: str):
+        self.path = path
+        self.present = bool(c.present)
+        self.n_rows = c.n_rows
+        self.phys, self.width, self.max_def, self.max_rep, self.rep_def = c.phys, c.width, c.max_def, c.max_rep, c.rep_def
+        n_val = c.n_entries if c.max_rep > 0 else c.n_rows
+        self.row_def = _arr(c.row_def, c.n_rows, np.uint8) if c.present else np.zeros(c.n_rows, np.uint8)
+        self.row_offs = _arr(c.row_offs, c.n_rows + 1, np.int64) if c.max_rep > 0 else None
+        self.entry_def = _arr(c.entry_def, n_val, np.uint8) if c.max_rep > 0 else None
+        if c.present and c.phys == 6:
+            self.offs = _arr(c.offs, n_val + 1, np.int64)
+            self.chars = _arr(c.chars, c.n_chars, np.uint8)
+            self.fixed = None
+        elif c.present:
+            self.fixed = _arr(c.fixed, n_val * c.width, np.uint8)
+            self.offs = self.chars = None
+        else:
+            self.fixed = self.offs = self.chars = None
+
+    def string(self, i):
+        return bytes(self.chars[self.offs[i]:self.offs[i + 1]])

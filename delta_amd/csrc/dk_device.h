@@ -1,0 +1,96 @@
+// Device-side data model shared by the host orchestration (dk_host.cpp) and the kernels.
+#pragma once
+#include <stdint.h>
+
+namespace dk {
+
+// One column chunk (file part x projected leaf x row group).
+struct DChunk {
+  const uint8_t* file;   // device copy of the file bytes (padded)
+  int32_t col;           // output column (DColumn index)
+  int32_t phys, width, max_def, max_rep, rep_def, codec;
+  int32_t dict_page;     // page index of the dictionary page, -1 if none
+  int64_t dict_pos;      // string dictionaries: scratch offset (int32 per entry + 1)
+};
+
+enum : int32_t { PF_DICT = 1 };
+enum : int32_t { PS_OK = 0, PS_BAD_HEADER = 1, PS_BAD_LEVELS = 2, PS_BAD_VALUES = 3,
+                 PS_UNSUPPORTED = 4, PS_BAD_DICT = 5, PS_BAD_SNAPPY = 6 };
+
+struct DPage {
+  int64_t hdr_off;       // absolute file offset of the page header (input)
+  int32_t chunk;         // DChunk index (input)
+  int32_t flags;         // PF_* (input)
+  // parsed header (k_page_headers)
+  int32_t ptype, enc, num_values, dl_len, rl_len, csize, usize, hdr_len;
+  int32_t status, is_comp;
+  int64_t data_off;      // absolute offset of the page body in the file
+  int64_t unc_off;       // offset into the decompression arena, -1 = read in place (input)
+  // counts (k_page_count)
+  int32_t n_rows, n_entries, n_values, pad;
+  int64_t n_chars;
+  // bases within the column (k_column_scan)
+  int64_t row_base, entry_base, value_base, char_base;
+  int64_t pos_base;      // string positions scratch offset (input, int32 per value + 1)
+};
+
+struct DColumn {
+  int32_t first_page, n_pages;   // data pages, contiguous in the page table, in file order
+  int32_t phys, width, max_def, max_rep, rep_def, present;
+  int64_t n_rows;
+  uint8_t* row_def;
+  int64_t* row_offs;
+  uint8_t* entry_def;
+  uint8_t* fixed;
+  int64_t* offs;
+  uint8_t* chars;
+  int64_t n_entries, n_chars;    // totals (k_column_scan)
+  int64_t cap_entries, cap_chars;
+};
+
+// Commit-tail actions, one per JSON line, in replay order.
+enum : int32_t { JA_NONE = 0, JA_ADD = 1, JA_REMOVE = 2 };
+struct DJsonAction {
+  int32_t kind;          // JA_*
+  int32_t step;          // global batch index in replay order
+  int32_t row;           // row within its batch
+  int32_t has_dv, has_off, dv_off;
+  int64_t path_off; int32_t path_len, pad0;
+  int64_t st_off; int32_t st_len, pad1;
+  int64_t pid_off; int32_t pid_len, pad2;
+  int64_t canon_off;     // arena offset of the canonical path stream (cap path_len + 64)
+  int32_t canon_len, dv_len;   // canonical path bytes; dv stream bytes follow the path bytes
+  uint64_t h;
+  int32_t slot, status;
+};
+
+// Probe table slot (open addressing on the 64-bit key hash).
+struct Slot {
+  unsigned long long h;          // 0 = empty
+  unsigned long long first_add;  // min (step<<32 | row) over JSON adds, ~0 = none
+  int32_t rep;                   // representative action index
+  int32_t min_rm_step;           // min step over JSON removes, INT32_MAX = none
+};
+
+enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8 };
+
+// Device-side counters and error state of one replay.
+struct DState {
+  unsigned long long counters[5];
+  int32_t err_flags;
+  int32_t err_row_part;
+  long long err_row;
+};
+
+// Column pointers the checkpoint probe reads (one checkpoint file).
+struct ProbeCols {
+  const uint8_t* path_def; const int64_t* path_offs; const uint8_t* path_chars;
+  const uint8_t* st_def; const int64_t* st_offs; const uint8_t* st_chars;
+  const int64_t* pid_offs; const uint8_t* pid_chars;
+  const uint8_t* off_def; const int32_t* off_vals; int32_t off_maxdef;
+  int32_t has_dv;
+  int64_t n_rows;
+  int64_t row_tag;   // added to the row index in error reports
+};
+
+}  // namespace dk

@@ -1,0 +1,1283 @@
+// Host side of libdkgpu: file open (footer + offset index), page enumeration, device buffers,
+// kernel orchestration on one HIP stream, commit-tail JSON parsing, C ABI (include/dkgpu.h).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/dkgpu.h"
+#include "dk_device.h"
+#include "dk_thrift.h"
+#include "dk_uri.h"
+
+namespace dk {
+void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
+void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, hipStream_t);
+void launch_page_count(const DChunk*, DPage*, int, const uint8_t*, const int32_t*, hipStream_t);
+void launch_column_scan(DColumn*, int, DPage*, DState*, hipStream_t);
+void launch_page_decode(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, hipStream_t);
+void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, hipStream_t);
+void launch_json_canon(DJsonAction*, int, const uint8_t*, uint8_t*, uint32_t, DState*, hipStream_t);
+void launch_slots_init(Slot*, uint64_t, hipStream_t);
+void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
+void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
+void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
+void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint8_t*,
+                  DState*, hipStream_t);
+}  // namespace dk
+
+using namespace dk;
+
+static thread_local std::string g_err;
+static int fail(const std::string& m) { g_err = m; return 1; }
+
+#define HIPOK(x)                                                                              \
+  do {                                                                                        \
+    hipError_t _e = (x);                                                                      \
+    if (_e != hipSuccess) return fail(std::string("HIP error: ") + hipGetErrorString(_e) + " at " #x); \
+  } while (0)
+
+extern "C" const char* dk_last_error(void) { return g_err.c_str(); }
+extern "C" const char* dk_version(void) { return "libdkgpu 0.1 (gfx950)"; }
+
+// ------------------------------------------------------------------------------------------------
+// engine
+// ------------------------------------------------------------------------------------------------
+struct dk_engine {
+  dk_config cfg;
+  hipStream_t stream = nullptr;
+};
+
+extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
+  dk_config c = cfg ? *cfg : dk_config{1024, 1024, 0, 0};
+  if (c.parquet_batch_size <= 0) c.parquet_batch_size = 1024;
+  if (c.json_batch_size <= 0) return fail("invalid JSON reader batch size: " + std::to_string(c.json_batch_size));
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail("libdkgpu: no HIP device available (the GPU engine has no CPU fallback)");
+  if (c.device < 0 || c.device >= ndev) return fail("libdkgpu: bad device ordinal");
+  HIPOK(hipSetDevice(c.device));
+  auto* e = new dk_engine();
+  e->cfg = c;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return fail("stream"); }
+  *out = e;
+  return 0;
+}
+
+extern "C" void dk_engine_destroy(dk_engine* e) {
+  if (!e) return;
+  hipSetDevice(e->cfg.device);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+}
+
+// ------------------------------------------------------------------------------------------------
+// device buffer helper
+// ------------------------------------------------------------------------------------------------
+struct DBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~DBuf() { if (p) hipFree(p); }
+  int alloc(size_t bytes) {
+    if (p) { hipFree(p); p = nullptr; }
+    n = bytes;
+    if (bytes == 0) return 0;
+    if (hipMalloc(&p, bytes) != hipSuccess) { p = nullptr; return fail("hipMalloc failed for " + std::to_string(bytes) + " bytes"); }
+    return 0;
+  }
+  template <class T> T* as() const { return (T*)p; }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Parquet footer (FileMetaData) + offset index
+// ------------------------------------------------------------------------------------------------
+struct SchemaEl { std::string name; int type = -1, type_length = 0, repetition = 0, num_children = 0; };
+struct ColMeta {
+  int type = -1, codec = 0;
+  int64_t num_values = 0, total_compressed = 0, data_page_offset = 0, dict_page_offset = -1;
+  int64_t oi_off = -1; int32_t oi_len = 0;
+};
+struct RowGroupM { int64_t num_rows = 0; std::vector<ColMeta> cols; };
+struct LeafM { std::string path; int phys, type_length, max_def, max_rep, rep_def; };
+struct FileM {
+  std::string path;
+  std::vector<uint8_t> bytes;
+  int64_t num_rows = 0;
+  std::vector<SchemaEl> schema;
+  std::vector<LeafM> leaves;
+  std::vector<RowGroupM> rgs;
+};
+
+static std::string read_string(TReader& t) {
+  uint64_t n = t.varint();
+  if (t.bad || t.p + n > t.e) { t.bad = 1; return {}; }
+  std::string s((const char*)t.p, n);
+  t.p += n;
+  return s;
+}
+
+static void parse_col_meta(TReader& t, ColMeta& m) {
+  int last = 0, ty, id;
+  while ((id = t.field(&last, &ty))) {
+    switch (id) {
+      case 1: m.type = (int)t.zigzag(); break;
+      case 4: m.codec = (int)t.zigzag(); break;
+      case 5: m.num_values = t.zigzag(); break;
+      case 7: m.total_compressed = t.zigzag(); break;
+      case 9: m.data_page_offset = t.zigzag(); break;
+      case 11: m.dict_page_offset = t.zigzag(); break;
+      default: t.skip(ty);
+    }
+    if (t.bad) return;
+  }
+}
+
+static int parse_footer(FileM& f) {
+  const std::vector<uint8_t>& b = f.bytes;
+  if (b.size() < 12 || memcmp(b.data(), "PAR1", 4) || memcmp(b.data() + b.size() - 4, "PAR1", 4))
+    return fail("Error reading Parquet file: " + f.path + " (not a Parquet file)");
+  uint32_t flen;
+  memcpy(&flen, b.data() + b.size() - 8, 4);
+  if ((int64_t)flen > (int64_t)b.size() - 12) return fail("Error reading Parquet file: " + f.path + " (bad footer)");
+  TReader t{b.data() + b.size() - 8 - flen, b.data() + b.size() - 8, 0};
+  int last = 0, ty, id;
+  while ((id = t.field(&last, &ty))) {
+    if (id == 2 && ty == 9) {
+      int et;
+      int n = t.list_header(&et);
+      f.schema.resize(n);
+      for (int i = 0; i < n && !t.bad; i++) {
+        SchemaEl& s = f.schema[i];
+        int l2 = 0, t2, i2;
+        while ((i2 = t.field(&l2, &t2))) {
+          if (i2 == 1) s.type = (int)t.zigzag();
+          else if (i2 == 2) s.type_length = (int)t.zigzag();
+          else if (i2 == 3) s.repetition = (int)t.zigzag();
+          else if (i2 == 4) s.name = read_string(t);
+          else if (i2 == 5) s.num_children = (int)t.zigzag();
+          else t.skip(t2);
+          if (t.bad) break;
+        }
+      }
+    } else if (id == 3) {
+      f.num_rows = t.zigzag();
+    } else if (id == 4 && ty == 9) {
+      int et;
+      int n = t.list_header(&et);
+      f.rgs.resize(n);
+      for (int g = 0; g < n && !t.bad; g++) {
+        RowGroupM& rg = f.rgs[g];
+        int l2 = 0, t2, i2;
+        while ((i2 = t.field(&l2, &t2))) {
+          if (i2 == 1 && t2 == 9) {
+            int et2;
+            int nc = t.list_header(&et2);
+            rg.cols.resize(nc);
+            for (int c = 0; c < nc && !t.bad; c++) {
+              ColMeta& m = rg.cols[c];
+              int l3 = 0, t3, i3;
+              while ((i3 = t.field(&l3, &t3))) {
+                if (i3 == 3 && t3 == 12) parse_col_meta(t, m);
+                else if (i3 == 4) m.oi_off = t.zigzag();
+                else if (i3 == 5) m.oi_len = (int32_t)t.zigzag();
+                else t.skip(t3);
+                if (t.bad) break;
+              }
+            }
+          } else if (i2 == 3) {
+            rg.num_rows = t.zigzag();
+          } else t.skip(t2);
+          if (t.bad) break;
+        }
+      }
+    } else t.skip(ty);
+    if (t.bad) break;
+  }
+  if (t.bad || f.schema.empty()) return fail("Error reading Parquet file: " + f.path + " (corrupt footer)");
+  // leaves (DFS over the flattened schema)
+  struct Fr { int remaining, def, rep, rep_def; std::string path; };
+  std::vector<Fr> st;
+  st.push_back({f.schema[0].num_children, 0, 0, 0, ""});
+  size_t pos = 1;
+  while (!st.empty()) {
+    if (st.back().remaining == 0) { st.pop_back(); continue; }
+    st.back().remaining--;
+    if (pos >= f.schema.size()) return fail("Error reading Parquet file: " + f.path + " (bad schema)");
+    const SchemaEl& e = f.schema[pos++];
+    Fr& top = st.back();
+    int def = top.def + (e.repetition != 0 ? 1 : 0);
+    int rep = top.rep + (e.repetition == 2 ? 1 : 0);
+    int rep_def = e.repetition == 2 ? def : top.rep_def;
+    std::string path = top.path.empty() ? e.name : top.path + "." + e.name;
+    if (e.num_children > 0) st.push_back({e.num_children, def, rep, rep_def, path});
+    else f.leaves.push_back({path, e.type, e.type_length, def, rep, rep_def});
+  }
+  for (auto& rg : f.rgs)
+    if (rg.cols.size() != f.leaves.size()) return fail("Error reading Parquet file: " + f.path + " (column count)");
+  return 0;
+}
+
+// page offsets of one chunk: from the OffsetIndex when present, otherwise a host walk of headers
+struct PageRef { int64_t hdr_off; bool dict; };
+static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef>& out) {
+  const uint8_t* b = f.bytes.data();
+  const int64_t N = (int64_t)f.bytes.size();
+  int64_t start = m.data_page_offset;
+  if (m.dict_page_offset > 0 && m.dict_page_offset < start) start = m.dict_page_offset;
+  if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= N) {
+    TReader t{b + m.oi_off, b + m.oi_off + m.oi_len, 0};
+    std::vector<int64_t> offs;
+    int last = 0, ty, id;
+    while ((id = t.field(&last, &ty))) {
+      if (id == 1 && ty == 9) {
+        int et;
+        int n = t.list_header(&et);
+        for (int i = 0; i < n && !t.bad; i++) {
+          int l2 = 0, t2, i2;
+          int64_t off = -1;
+          while ((i2 = t.field(&l2, &t2))) {
+            if (i2 == 1) off = t.zigzag(); else t.skip(t2);
+            if (t.bad) break;
+          }
+          offs.push_back(off);
+        }
+      } else t.skip(ty);
+      if (t.bad) break;
+    }
+    if (!t.bad && !offs.empty()) {
+      if (offs[0] > start) out.push_back({start, true});   // dictionary page precedes the first data page
+      for (int64_t o : offs) out.push_back({o, false});
+      return 0;
+    }
+    out.clear();
+  }
+  // host walk (no offset index)
+  int64_t p = start, end = start + m.total_compressed;
+  if (end > N) return fail("Error reading Parquet file: " + f.path + " (chunk out of range)");
+  while (p < end) {
+    PageHeader h = parse_page_header(b + p, b + end);
+    if (!h.ok || h.csize < 0) return fail("Error reading Parquet file: " + f.path + " (bad page header)");
+    if (h.type != PAGE_INDEX) out.push_back({p, h.type == PAGE_DICT});
+    p += h.hdr_len + h.csize;
+  }
+  return 0;
+}
+
+static int leaf_index(const FileM& f, const std::string& want) {
+  for (size_t i = 0; i < f.leaves.size(); i++) if (f.leaves[i].path == want) return (int)i;
+  auto low = [](std::string s) { for (auto& c : s) c = (char)tolower((unsigned char)c); return s; };
+  std::string w = low(want);
+  for (size_t i = 0; i < f.leaves.size(); i++) if (low(f.leaves[i].path) == w) return (int)i;
+  return -1;
+}
+
+static int phys_width(int phys, int tl) {
+  switch (phys) { case PT_BOOLEAN: return 1; case PT_INT32: case PT_FLOAT: return 4; case PT_INT64: case PT_DOUBLE: return 8;
+    case PT_INT96: return 12; case PT_FIXED: return tl; default: return 0; }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernel timing (HIP events on the engine stream)
+// ------------------------------------------------------------------------------------------------
+struct KTimer {
+  static constexpr int K = 16;
+  const char* names[K] = {"k_page_headers", "k_string_positions_dict", "k_page_count", "k_column_scan",
+                          "k_string_positions", "k_page_decode", "k_string_copy", "k_json_canon",
+                          "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
+                          nullptr, nullptr, nullptr};
+  double sum_ms[K] = {0};
+  int64_t cnt[K] = {0};
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t get() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e; hipEventCreate(&e); return e;
+  }
+  struct Scope {
+    KTimer* t; int k; hipStream_t s; hipEvent_t a = nullptr, b = nullptr;
+    Scope(KTimer* t_, int k_, hipStream_t s_) : t(t_), k(k_), s(s_) { if (t->on) { a = t->get(); b = t->get(); hipEventRecord(a, s); } }
+    ~Scope() { if (t->on) { hipEventRecord(b, s); t->pending.push_back({k, {a, b}}); } }
+  };
+  void collect() {
+    for (auto& p : pending) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) { sum_ms[p.first] += ms; cnt[p.first]++; }
+      pool.push_back(p.second.first); pool.push_back(p.second.second);
+    }
+    pending.clear();
+  }
+  ~KTimer() { for (auto& p : pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
+              for (auto e : pool) hipEventDestroy(e); }
+};
+
+// ------------------------------------------------------------------------------------------------
+// dk_parquet: a set of files x projected leaves, decoded on the GPU
+// ------------------------------------------------------------------------------------------------
+struct HostCol {           // host mirror of one decoded column (filled on demand)
+  bool ready = false;
+  std::vector<uint8_t> row_def, entry_def, fixed, chars;
+  std::vector<int64_t> row_offs, offs;
+};
+
+struct dk_parquet {
+  dk_engine* eng = nullptr;
+  std::vector<FileM> files;
+  std::vector<std::string> leaves;
+  // per (file, leaf): column index or -1 (missing leaf)
+  std::vector<std::vector<int>> colmap;
+  std::vector<std::vector<int>> leafidx;  // file leaf index for (file, leaf)
+  std::vector<DBuf> dfile;
+  std::vector<DChunk> h_chunks;
+  std::vector<DPage> h_pages;
+  std::vector<DColumn> h_cols;
+  std::vector<int> col_file;
+  DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state;
+  std::vector<std::unique_ptr<DBuf>> outbufs;
+  std::vector<HostCol> host;
+  int n_pages = 0, n_cols = 0;
+  int64_t bytes_read = 0, bytes_written = 0;
+  KTimer timer;
+  bool prepared = false;
+};
+
+static int upload(DBuf& d, const void* src, size_t n, hipStream_t s) {
+  if (d.n < n || !d.p) if (d.alloc(n ? n : 16)) return 1;
+  if (n) HIPOK(hipMemcpyAsync(d.p, src, n, hipMemcpyHostToDevice, s));
+  return 0;
+}
+
+static int read_file(const std::string& path, std::vector<uint8_t>& out) {
+  FILE* fp = fopen(path.c_str(), "rb");
+  if (!fp) return fail("Error reading Parquet file: " + path + " (cannot open)");
+  fseek(fp, 0, SEEK_END);
+  long n = ftell(fp);
+  fseek(fp, 0, SEEK_SET);
+  out.resize(n > 0 ? n : 0);
+  size_t got = n > 0 ? fread(out.data(), 1, n, fp) : 0;
+  fclose(fp);
+  if ((long)got != n) return fail("Error reading Parquet file: " + path + " (short read)");
+  return 0;
+}
+
+// the decode pipeline (mode: 0 = prepare pass up to the scan; 1 = full step)
+static int run_pipeline(dk_parquet* p, int mode) {
+  hipStream_t s = p->eng->stream;
+  KTimer& T = p->timer;
+  const DChunk* C = p->d_chunks.as<DChunk>();
+  DPage* P = p->d_pages.as<DPage>();
+  int32_t* pos = p->d_pos.as<int32_t>();
+  const uint8_t* arena = p->d_arena.as<uint8_t>();
+  DState* st = p->d_state.as<DState>();
+  int n = p->n_pages;
+  { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
+  if (mode == -1) return 0;
+  { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, s); }  // dict pages (data pages exit: n_values unknown yet)
+  { KTimer::Scope sc(&T, 2, s); launch_page_count(C, P, n, arena, pos, s); }
+  { KTimer::Scope sc(&T, 3, s); launch_column_scan(p->d_cols.as<DColumn>(), p->n_cols, P, st, s); }
+  if (mode == 0) return 0;
+  { KTimer::Scope sc(&T, 4, s); launch_string_positions(C, P, n, arena, pos, s); }
+  { KTimer::Scope sc(&T, 5, s); launch_page_decode(C, P, n, p->d_cols.as<DColumn>(), arena, pos, s); }
+  { KTimer::Scope sc(&T, 6, s); launch_string_copy(C, P, n, p->d_cols.as<DColumn>(), arena, pos, s); }
+  return 0;
+}
+
+static std::string page_status_msg(const dk_parquet* p, const std::vector<DPage>& pages) {
+  for (const DPage& pg : pages)
+    if (pg.status != PS_OK) {
+      const DChunk& ck = p->h_chunks[pg.chunk];
+      int fi = p->col_file[ck.col];
+      static const char* why[] = {"ok", "bad page header", "bad levels", "bad values", "unsupported encoding/codec",
+                                  "bad dictionary", "bad snappy block"};
+      return "Error reading Parquet file: " + p->files[fi].path + " (" + why[pg.status < 7 ? pg.status : 4] +
+             " at offset " + std::to_string(pg.hdr_off) + ")";
+    }
+  return "";
+}
+
+static int prepare(dk_parquet* p) {
+  hipStream_t s = p->eng->stream;
+  // 1. parse headers once to size the scratch areas
+  if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;
+  if (upload(p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), s)) return 1;
+  DState st0{};
+  st0.err_row = LLONG_MAX;
+  if (upload(p->d_state, &st0, sizeof st0, s)) return 1;
+  if (p->d_pos.alloc(64)) return 1;
+  if (p->d_arena.alloc(64)) return 1;
+  run_pipeline(p, -1);
+  HIPOK(hipMemcpyAsync(p->h_pages.data(), p->d_pages.p, p->h_pages.size() * sizeof(DPage), hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  // header errors
+  for (DPage& pg : p->h_pages) if (pg.status != PS_OK && pg.status != PS_UNSUPPORTED) return fail(page_status_msg(p, p->h_pages));
+  int64_t posn = 0, arena_n = 0;
+  for (size_t i = 0; i < p->h_pages.size(); i++) {
+    DPage& pg = p->h_pages[i];
+    DChunk& ck = p->h_chunks[pg.chunk];
+    pg.unc_off = -1;
+    if (ck.codec != CODEC_NONE) {
+      if (ck.codec != CODEC_SNAPPY) return fail("Error reading Parquet file: unsupported compression codec " + std::to_string(ck.codec));
+      return fail("Error reading Parquet file: " + p->files[p->col_file[ck.col]].path + " (SNAPPY pages: GPU decompression not built in this version)");
+    }
+    if (ck.phys == PT_BYTE_ARRAY) {
+      if (pg.flags & PF_DICT) { ck.dict_pos = posn; }
+      else pg.pos_base = posn;
+      posn += (int64_t)pg.num_values + 1;
+    }
+  }
+  (void)arena_n;
+  if (p->d_pos.alloc((size_t)(posn + 16) * 4)) return 1;
+  if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;
+  if (upload(p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), s)) return 1;
+  // 2. count + scan to size the outputs (entries / chars are data dependent)
+  for (DColumn& c : p->h_cols) { c.cap_entries = LLONG_MAX; c.cap_chars = LLONG_MAX; c.offs = nullptr; c.row_offs = nullptr; }
+  if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
+  run_pipeline(p, 0);
+  std::vector<DColumn> got(p->h_cols.size());
+  HIPOK(hipMemcpyAsync(got.data(), p->d_cols.p, got.size() * sizeof(DColumn), hipMemcpyDeviceToHost, s));
+  HIPOK(hipMemcpyAsync(p->h_pages.data(), p->d_pages.p, p->h_pages.size() * sizeof(DPage), hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  std::string m = page_status_msg(p, p->h_pages);
+  if (!m.empty()) return fail(m);
+  // 3. allocate outputs
+  p->bytes_written = 0;
+  for (size_t i = 0; i < p->h_cols.size(); i++) {
+    DColumn& c = p->h_cols[i];
+    c.n_entries = got[i].n_entries;
+    c.n_chars = got[i].n_chars;
+    c.cap_entries = c.n_entries;
+    c.cap_chars = c.n_chars;
+    int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
+    auto mk = [&](size_t bytes) -> void* {
+      p->outbufs.emplace_back(new DBuf());
+      if (p->outbufs.back()->alloc(bytes + 16)) return nullptr;
+      p->bytes_written += bytes;
+      return p->outbufs.back()->p;
+    };
+    c.row_def = (uint8_t*)mk(c.n_rows);
+    c.row_offs = c.max_rep > 0 ? (int64_t*)mk((c.n_rows + 1) * 8) : nullptr;
+    c.entry_def = c.max_rep > 0 ? (uint8_t*)mk(nv) : nullptr;
+    if (c.phys == PT_BYTE_ARRAY) {
+      c.offs = (int64_t*)mk((nv + 1) * 8);
+      c.chars = (uint8_t*)mk(c.n_chars);
+      c.fixed = nullptr;
+    } else {
+      c.fixed = (uint8_t*)mk(nv * c.width);
+      c.offs = nullptr;
+      c.chars = nullptr;
+    }
+    if (!c.row_def) return 1;
+  }
+  if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
+  HIPOK(hipStreamSynchronize(s));
+  p->host.assign(p->h_cols.size(), HostCol());
+  p->prepared = true;
+  return 0;
+}
+
+extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                               int32_t n_leaves, dk_parquet** out) {
+  if (!e) return fail("null engine");
+  hipSetDevice(e->cfg.device);
+  std::unique_ptr<dk_parquet> p(new dk_parquet());
+  p->eng = e;
+  p->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
+  for (int i = 0; i < n_leaves; i++) p->leaves.push_back(leaves[i]);
+  p->files.resize(n_files);
+  p->colmap.assign(n_files, std::vector<int>(n_leaves, -1));
+  p->leafidx.assign(n_files, std::vector<int>(n_leaves, -1));
+  p->dfile.resize(n_files);
+  hipStream_t s = e->stream;
+  for (int fi = 0; fi < n_files; fi++) {
+    FileM& f = p->files[fi];
+    f.path = paths[fi];
+    if (read_file(f.path, f.bytes)) return 1;
+    if (parse_footer(f)) return 1;
+    if (p->dfile[fi].alloc(f.bytes.size() + 256)) return 1;
+    HIPOK(hipMemcpyAsync(p->dfile[fi].p, f.bytes.data(), f.bytes.size(), hipMemcpyHostToDevice, s));
+    for (int li = 0; li < n_leaves; li++) {
+      int idx = leaf_index(f, p->leaves[li]);
+      p->leafidx[fi][li] = idx;
+      if (idx < 0) continue;
+      const LeafM& L = f.leaves[idx];
+      if (L.max_rep > 1) return fail("Error reading Parquet file: " + f.path + " (nested repetition not supported: " + L.path + ")");
+      DColumn c{};
+      c.phys = L.phys; c.width = L.phys == PT_BYTE_ARRAY ? 0 : phys_width(L.phys, L.type_length);
+      c.max_def = L.max_def; c.max_rep = L.max_rep; c.rep_def = L.rep_def; c.present = 1;
+      c.n_rows = 0;
+      c.first_page = (int)p->h_pages.size();
+      int colid = (int)p->h_cols.size();
+      // chunks and pages in row-group order; data pages of a column stay contiguous
+      std::vector<DPage> dicts;
+      for (size_t g = 0; g < f.rgs.size(); g++) {
+        const ColMeta& m = f.rgs[g].cols[idx];
+        c.n_rows += f.rgs[g].num_rows;
+        DChunk ck{};
+        ck.file = p->dfile[fi].as<uint8_t>();
+        ck.col = colid;
+        ck.phys = L.phys; ck.width = c.width; ck.max_def = L.max_def; ck.max_rep = L.max_rep; ck.rep_def = L.rep_def;
+        ck.codec = m.codec; ck.dict_page = -1; ck.dict_pos = 0;
+        int chunk_id = (int)p->h_chunks.size();
+        std::vector<PageRef> refs;
+        if (enumerate_pages(f, m, refs)) return 1;
+        p->bytes_read += m.total_compressed;
+        for (const PageRef& r : refs) {
+          DPage pg{};
+          pg.hdr_off = r.hdr_off; pg.chunk = chunk_id; pg.flags = r.dict ? PF_DICT : 0; pg.unc_off = -1;
+          if (r.dict) { ck.dict_page = -2 - (int)dicts.size(); dicts.push_back(pg); }
+          else p->h_pages.push_back(pg);
+        }
+        p->h_chunks.push_back(ck);
+      }
+      c.n_pages = (int)p->h_pages.size() - c.first_page;
+      // dictionary pages go after the data pages (they are not part of the column's page range)
+      for (size_t d = 0; d < dicts.size(); d++) {
+        int at = (int)p->h_pages.size();
+        for (DChunk& ck : p->h_chunks) if (ck.col == colid && ck.dict_page == -2 - (int)d) ck.dict_page = at;
+        p->h_pages.push_back(dicts[d]);
+      }
+      p->colmap[fi][li] = colid;
+      p->h_cols.push_back(c);
+      p->col_file.push_back(fi);
+    }
+  }
+  p->n_pages = (int)p->h_pages.size();
+  p->n_cols = (int)p->h_cols.size();
+  if (prepare(p.get())) return 1;
+  *out = p.release();
+  return 0;
+}
+
+extern "C" int dk_parquet_decode(dk_parquet* p) {
+  hipSetDevice(p->eng->cfg.device);
+  DState st0{};
+  st0.err_row = LLONG_MAX;
+  HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, p->eng->stream));
+  KTimer::Scope sc(&p->timer, 12, p->eng->stream);
+  for (auto& h : p->host) h.ready = false;
+  return run_pipeline(p, 1);
+}
+
+static int check_state(dk_parquet* p) {
+  DState st;
+  HIPOK(hipMemcpy(&st, p->d_state.p, sizeof st, hipMemcpyDeviceToHost));
+  if (st.err_flags & E_PAGE) {
+    std::vector<DPage> pages(p->h_pages.size());
+    HIPOK(hipMemcpy(pages.data(), p->d_pages.p, pages.size() * sizeof(DPage), hipMemcpyDeviceToHost));
+    std::string m = page_status_msg(p, pages);
+    return fail(m.empty() ? std::string("Error reading Parquet file: decode size mismatch") : m);
+  }
+  return 0;
+}
+
+extern "C" int dk_parquet_sync(dk_parquet* p) {
+  HIPOK(hipStreamSynchronize(p->eng->stream));
+  p->timer.collect();
+  return check_state(p);
+}
+
+extern "C" int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file) {
+  if (!p || file < 0 || file >= (int)p->files.size()) return -1;
+  return p->files[file].num_rows;
+}
+
+extern "C" int dk_parquet_traffic(dk_parquet* p, int64_t* r, int64_t* w) {
+  *r = p->bytes_read; *w = p->bytes_written; return 0;
+}
+
+extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out) {
+  memset(out, 0, sizeof *out);
+  HIPOK(hipStreamSynchronize(p->eng->stream));
+  if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
+  int ci = p->colmap[file][leaf];
+  out->n_rows = p->files[file].num_rows;
+  if (ci < 0) { out->present = 0; return 0; }
+  const DColumn& c = p->h_cols[ci];
+  HostCol& h = p->host[ci];
+  int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
+  if (!h.ready) {
+    h.row_def.resize(c.n_rows);
+    HIPOK(hipMemcpy(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost));
+    if (c.max_rep > 0) {
+      h.row_offs.resize(c.n_rows + 1);
+      h.entry_def.resize(nv);
+      HIPOK(hipMemcpy(h.row_offs.data(), c.row_offs, (c.n_rows + 1) * 8, hipMemcpyDeviceToHost));
+      HIPOK(hipMemcpy(h.entry_def.data(), c.entry_def, nv, hipMemcpyDeviceToHost));
+    }
+    if (c.phys == PT_BYTE_ARRAY) {
+      h.offs.resize(nv + 1);
+      h.chars.resize(c.n_chars);
+      HIPOK(hipMemcpy(h.offs.data(), c.offs, (nv + 1) * 8, hipMemcpyDeviceToHost));
+      if (c.n_chars) HIPOK(hipMemcpy(h.chars.data(), c.chars, c.n_chars, hipMemcpyDeviceToHost));
+    } else {
+      h.fixed.resize(nv * c.width);
+      if (nv) HIPOK(hipMemcpy(h.fixed.data(), c.fixed, nv * c.width, hipMemcpyDeviceToHost));
+    }
+    h.ready = true;
+  }
+  out->n_entries = nv; out->n_chars = c.n_chars;
+  out->phys = c.phys; out->width = c.width; out->max_def = c.max_def; out->max_rep = c.max_rep;
+  out->rep_def = c.rep_def; out->present = 1;
+  out->row_def = h.row_def.data();
+  out->row_offs = c.max_rep > 0 ? h.row_offs.data() : nullptr;
+  out->entry_def = c.max_rep > 0 ? h.entry_def.data() : nullptr;
+  out->fixed = c.phys == PT_BYTE_ARRAY ? nullptr : h.fixed.data();
+  out->offs = c.phys == PT_BYTE_ARRAY ? h.offs.data() : nullptr;
+  out->chars = c.phys == PT_BYTE_ARRAY ? h.chars.data() : nullptr;
+  return 0;
+}
+
+extern "C" void dk_parquet_close(dk_parquet* p) {
+  if (!p) return;
+  hipSetDevice(p->eng->cfg.device);
+  hipStreamSynchronize(p->eng->stream);
+  delete p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// JSON commit tail (DefaultJsonHandler.readJsonFiles + DefaultJsonRow semantics, host side)
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+// Java UTF-8 decoding with replacement (InputStreamReader(UTF_8)): each maximal ill-formed
+// subsequence becomes U+FFFD.
+std::string java_utf8(const uint8_t* s, size_t n) {
+  std::string o;
+  o.reserve(n);
+  size_t i = 0;
+  while (i < n) {
+    uint32_t cp;
+    int l = utf8_len_valid(s, (int64_t)i, (int64_t)n, &cp);
+    if (l) { o.append((const char*)s + i, l); i += l; continue; }
+    // maximal subpart length
+    uint8_t b = s[i];
+    int need = 0; uint8_t lo = 0x80, hi = 0xBF;
+    if (b >= 0xC2 && b <= 0xDF) need = 1;
+    else if (b >= 0xE0 && b <= 0xEF) { need = 2; if (b == 0xE0) lo = 0xA0; if (b == 0xED) hi = 0x9F; }
+    else if (b >= 0xF0 && b <= 0xF4) { need = 3; if (b == 0xF0) lo = 0x90; if (b == 0xF4) hi = 0x8F; }
+    size_t j = i + 1;
+    for (int k = 0; k < need && j < n; k++, j++) {
+      uint8_t c = s[j];
+      uint8_t l2 = k == 0 ? lo : 0x80, h2 = k == 0 ? hi : 0xBF;
+      if (c < l2 || c > h2) break;
+    }
+    o.append("\xEF\xBF\xBD");
+    i = j;
+  }
+  return o;
+}
+
+enum JT { J_NULL, J_BOOL, J_NUM, J_STR, J_ARR, J_OBJ };
+struct JNode {
+  JT t = J_NULL;
+  bool b = false;
+  bool integral = false;
+  std::string s;                                   // string value or raw number text
+  std::vector<std::pair<std::string, int>> kv;      // object members (child node index)
+  std::vector<int> arr;
+};
+
+struct JParser {
+  const char* p; const char* e;
+  std::vector<JNode>& nodes;
+  std::string err;
+  JParser(const char* b, const char* en, std::vector<JNode>& n) : p(b), e(en), nodes(n) {}
+  void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
+  bool str(std::string& out) {
+    if (p >= e || *p != '"') return false;
+    p++;
+    out.clear();
+    while (p < e && *p != '"') {
+      unsigned char c = (unsigned char)*p;
+      if (c < 0x20) return false;
+      if (c != '\\') { out.push_back((char)c); p++; continue; }
+      p++;
+      if (p >= e) return false;
+      char x = *p++;
+      switch (x) {
+        case '"': out.push_back('"'); break; case '\\': out.push_back('\\'); break; case '/': out.push_back('/'); break;
+        case 'b': out.push_back('\b'); break; case 'f': out.push_back('\f'); break; case 'n': out.push_back('\n'); break;
+        case 'r': out.push_back('\r'); break; case 't': out.push_back('\t'); break;
+        case 'u': {
+          auto hex4 = [&](uint32_t* v) {
+            if (e - p < 4) return false;
+            uint32_t r = 0;
+            for (int k = 0; k < 4; k++) {
+              char h = p[k]; r <<= 4;
+              if (h >= '0' && h <= '9') r |= h - '0'; else if (h >= 'a' && h <= 'f') r |= h - 'a' + 10;
+              else if (h >= 'A' && h <= 'F') r |= h - 'A' + 10; else return false;
+            }
+            p += 4; *v = r; return true;
+          };
+          uint32_t cp;
+          if (!hex4(&cp)) return false;
+          if (cp >= 0xD800 && cp <= 0xDBFF && e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            const char* save = p;
+            p += 2;
+            uint32_t lo;
+            if (hex4(&lo) && lo >= 0xDC00 && lo <= 0xDFFF) cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            else p = save;
+          }
+          // lone surrogates are encoded as 3 bytes (invalid UTF-8); key builders report them
+          if (cp < 0x80) out.push_back((char)cp);
+          else if (cp < 0x800) { out.push_back((char)(0xC0 | (cp >> 6))); out.push_back((char)(0x80 | (cp & 63))); }
+          else if (cp < 0x10000) { out.push_back((char)(0xE0 | (cp >> 12))); out.push_back((char)(0x80 | ((cp >> 6) & 63))); out.push_back((char)(0x80 | (cp & 63))); }
+          else { out.push_back((char)(0xF0 | (cp >> 18))); out.push_back((char)(0x80 | ((cp >> 12) & 63))); out.push_back((char)(0x80 | ((cp >> 6) & 63))); out.push_back((char)(0x80 | (cp & 63))); }
+          break;
+        }
+        default: return false;
+      }
+    }
+    if (p >= e) return false;
+    p++;
+    return true;
+  }
+  int value(int depth) {
+    if (depth > 200) { err = "nesting too deep"; return -1; }
+    ws();
+    if (p >= e) { err = "unexpected end"; return -1; }
+    int id = (int)nodes.size();
+    nodes.emplace_back();
+    char c = *p;
+    if (c == '{') {
+      p++;
+      nodes[id].t = J_OBJ;
+      ws();
+      if (p < e && *p == '}') { p++; return id; }
+      for (;;) {
+        ws();
+        std::string k;
+        if (!str(k)) { err = "bad object key"; return -1; }
+        ws();
+        if (p >= e || *p != ':') { err = "expected ':'"; return -1; }
+        p++;
+        int v = value(depth + 1);
+        if (v < 0) return -1;
+        bool dup = false;
+        for (auto& m : nodes[id].kv) if (m.first == k) { m.second = v; dup = true; break; }   // ObjectNode.set: last wins, first position
+        if (!dup) nodes[id].kv.push_back({k, v});
+        ws();
+        if (p < e && *p == ',') { p++; continue; }
+        if (p < e && *p == '}') { p++; return id; }
+        err = "expected ',' or '}'"; return -1;
+      }
+    }
+    if (c == '[') {
+      p++;
+      nodes[id].t = J_ARR;
+      ws();
+      if (p < e && *p == ']') { p++; return id; }
+      for (;;) {
+        int v = value(depth + 1);
+        if (v < 0) return -1;
+        nodes[id].arr.push_back(v);
+        ws();
+        if (p < e && *p == ',') { p++; continue; }
+        if (p < e && *p == ']') { p++; return id; }
+        err = "expected ',' or ']'"; return -1;
+      }
+    }
+    if (c == '"') {
+      std::string s;
+      if (!str(s)) { err = "bad string"; return -1; }
+      nodes[id].t = J_STR; nodes[id].s = std::move(s);
+      return id;
+    }
+    if (e - p >= 4 && !memcmp(p, "null", 4)) { p += 4; nodes[id].t = J_NULL; return id; }
+    if (e - p >= 4 && !memcmp(p, "true", 4)) { p += 4; nodes[id].t = J_BOOL; nodes[id].b = true; return id; }
+    if (e - p >= 5 && !memcmp(p, "false", 5)) { p += 5; nodes[id].t = J_BOOL; nodes[id].b = false; return id; }
+    if (c == '-' || (c >= '0' && c <= '9')) {
+      const char* b = p;
+      if (*p == '-') p++;
+      if (p >= e || !(*p >= '0' && *p <= '9')) { err = "bad number"; return -1; }
+      if (*p == '0' && p + 1 < e && p[1] >= '0' && p[1] <= '9') { err = "leading zero"; return -1; }
+      while (p < e && *p >= '0' && *p <= '9') p++;
+      bool integral = true;
+      if (p < e && *p == '.') { integral = false; p++; if (p >= e || !(*p >= '0' && *p <= '9')) { err = "bad number"; return -1; } while (p < e && *p >= '0' && *p <= '9') p++; }
+      if (p < e && (*p == 'e' || *p == 'E')) { integral = false; p++; if (p < e && (*p == '+' || *p == '-')) p++; if (p >= e || !(*p >= '0' && *p <= '9')) { err = "bad number"; return -1; } while (p < e && *p >= '0' && *p <= '9') p++; }
+      nodes[id].t = J_NUM; nodes[id].integral = integral; nodes[id].s.assign(b, p - b);
+      return id;
+    }
+    err = "unexpected character";
+    return -1;
+  }
+};
+
+bool parse_i64(const std::string& s, int64_t lo, int64_t hi, int64_t* out) {
+  // integral text -> value if within [lo, hi]
+  size_t i = 0; bool neg = false;
+  if (s[0] == '-') { neg = true; i = 1; }
+  __int128 v = 0;
+  for (; i < s.size(); i++) { v = v * 10 + (s[i] - '0'); if (v > ((__int128)1 << 64)) return false; }
+  if (neg) v = -v;
+  if (v < lo || v > hi) return false;
+  *out = (int64_t)v;
+  return true;
+}
+
+// column builder in the dk_column layout
+struct CB {
+  int phys, width, max_def, max_rep, rep_def;
+  std::vector<uint8_t> row_def, entry_def, fixed, chars;
+  std::vector<int64_t> row_offs, offs;
+  void init(int ph, int w, int md, int mr, int rd) { phys = ph; width = w; max_def = md; max_rep = mr; rep_def = rd; if (mr) row_offs.push_back(0); if (ph == PT_BYTE_ARRAY) offs.push_back(0); }
+  // non-repeated
+  void null_row(int def) { row_def.push_back((uint8_t)def); if (phys == PT_BYTE_ARRAY) offs.push_back((int64_t)chars.size()); else fixed.insert(fixed.end(), width, 0); }
+  void str_row(const std::string& s) { row_def.push_back((uint8_t)max_def); chars.insert(chars.end(), s.begin(), s.end()); offs.push_back((int64_t)chars.size()); }
+  void fix_row(const void* v) { row_def.push_back((uint8_t)max_def); fixed.insert(fixed.end(), (const uint8_t*)v, (const uint8_t*)v + width); }
+  // repeated (map leaves): row begin / entry
+  void map_row(int def) { row_def.push_back((uint8_t)def); }
+  void map_end() { row_offs.push_back((int64_t)entry_def.size()); }
+  void entry_str(const std::string* s) {
+    if (s) { entry_def.push_back((uint8_t)max_def); chars.insert(chars.end(), s->begin(), s->end()); }
+    else entry_def.push_back((uint8_t)(max_def - 1));
+    offs.push_back((int64_t)chars.size());
+  }
+};
+
+}  // namespace
+
+static const char* JSON_LEAVES[] = {
+    "add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value", "add.size",
+    "add.modificationTime", "add.dataChange", "add.deletionVector.storageType", "add.deletionVector.pathOrInlineDv",
+    "add.deletionVector.offset", "add.deletionVector.sizeInBytes", "add.deletionVector.cardinality",
+    "add.tags.key_value.key", "add.tags.key_value.value", "add.baseRowId", "add.defaultRowCommitVersion", "add.stats",
+    "remove.path", "remove.deletionVector.storageType", "remove.deletionVector.pathOrInlineDv",
+    "remove.deletionVector.offset", "remove.deletionVector.sizeInBytes", "remove.deletionVector.cardinality"};
+enum { JL_PATH, JL_PVK, JL_PVV, JL_SIZE, JL_MTIME, JL_DC, JL_DVST, JL_DVPID, JL_DVOFF, JL_DVSIZE, JL_DVCARD,
+       JL_TGK, JL_TGV, JL_BRID, JL_DRCV, JL_STATS, JL_RPATH, JL_RDVST, JL_RDVPID, JL_RDVOFF, JL_RDVSIZE, JL_RDVCARD,
+       JL_N };
+
+struct dk_json_tail {
+  int64_t rows = 0;
+  bool with_stats = false;
+  CB col[JL_N];
+  std::vector<int32_t> step, rowin;   // per row: batch step and row within batch
+  int32_t n_steps = 0;
+};
+
+namespace {
+struct JErr { std::string msg; };
+
+const JNode* member(const std::vector<JNode>& N, const JNode& o, const char* k) {
+  for (auto& m : o.kv) if (m.first == k) return &N[m.second];
+  return nullptr;
+}
+std::string node_text(const std::vector<JNode>& N, const JNode& n);
+std::string node_text(const std::vector<JNode>& N, const JNode& n) {
+  switch (n.t) {
+    case J_NULL: return "null";
+    case J_BOOL: return n.b ? "true" : "false";
+    case J_NUM: return n.s;
+    case J_STR: return "\"" + n.s + "\"";
+    case J_ARR: { std::string r = "["; for (size_t i = 0; i < n.arr.size(); i++) { if (i) r += ","; r += node_text(N, N[n.arr[i]]); } return r + "]"; }
+    default: { std::string r = "{"; for (size_t i = 0; i < n.kv.size(); i++) { if (i) r += ","; r += "\"" + n.kv[i].first + "\":" + node_text(N, N[n.kv[i].second]); } return r + "}"; }
+  }
+}
+[[noreturn]] void mismatch(const std::vector<JNode>& N, const JNode& n, const char* what) {
+  throw JErr{"Couldn't decode " + node_text(N, n) + ", expected a " + what};
+}
+const JNode* field(const std::vector<JNode>& N, const JNode& o, const char* name, bool nullable) {
+  const JNode* v = member(N, o, name);
+  if (!v || v->t == J_NULL) {
+    if (nullable) return nullptr;
+    throw JErr{std::string("Root node at key ") + name + " is null but field isn't nullable. Root node: " + node_text(N, o)};
+  }
+  return v;
+}
+const std::string& as_str(const std::vector<JNode>& N, const JNode& n) { if (n.t != J_STR) mismatch(N, n, "string"); return n.s; }
+int64_t as_long(const std::vector<JNode>& N, const JNode& n) {
+  int64_t v;
+  if (n.t != J_NUM || !n.integral || !parse_i64(n.s, LLONG_MIN, LLONG_MAX, &v)) mismatch(N, n, "long");
+  return v;
+}
+int32_t as_int(const std::vector<JNode>& N, const JNode& n) {
+  int64_t v;
+  if (n.t != J_NUM || !n.integral || !parse_i64(n.s, INT_MIN, INT_MAX, &v)) mismatch(N, n, "integer");
+  return (int32_t)v;
+}
+bool as_bool(const std::vector<JNode>& N, const JNode& n) { if (n.t != J_BOOL) mismatch(N, n, "boolean"); return n.b; }
+
+void put_map(CB& k, CB& v, const std::vector<JNode>& N, const JNode* m, int null_def) {
+  if (!m) { k.map_row(null_def); v.map_row(null_def); k.map_end(); v.map_end(); return; }
+  if (m->t != J_OBJ) mismatch(N, *m, "map");
+  int present = k.rep_def - 1;   // map defined
+  k.map_row(m->kv.empty() ? present : k.rep_def);
+  v.map_row(m->kv.empty() ? present : v.rep_def);
+  for (auto& kv : m->kv) {
+    const JNode& val = N[kv.second];
+    k.entry_str(&kv.first);
+    if (val.t == J_NULL) v.entry_str(nullptr);
+    else v.entry_str(&as_str(N, val));
+  }
+  k.map_end(); v.map_end();
+}
+
+void put_dv(CB* c, const std::vector<JNode>& N, const JNode* dv, int add_def) {
+  // c[0..4] = storageType, pathOrInlineDv, offset, sizeInBytes, cardinality (leaf max_def 3)
+  if (!dv) { for (int i = 0; i < 5; i++) c[i].null_row(add_def); return; }
+  if (dv->t != J_OBJ) mismatch(N, *dv, "object");
+  const JNode* st = field(N, *dv, "storageType", false);
+  const JNode* pid = field(N, *dv, "pathOrInlineDv", false);
+  const JNode* off = field(N, *dv, "offset", true);
+  const JNode* sz = field(N, *dv, "sizeInBytes", false);
+  const JNode* card = field(N, *dv, "cardinality", false);
+  c[0].str_row(as_str(N, *st));
+  c[1].str_row(as_str(N, *pid));
+  if (off) { int32_t v = as_int(N, *off); c[2].fix_row(&v); } else c[2].null_row(2);
+  int32_t s = as_int(N, *sz); c[3].fix_row(&s);
+  int64_t cd = as_long(N, *card); c[4].fix_row(&cd);
+}
+}  // namespace
+
+extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
+                                  int32_t with_stats, dk_json_tail** out) {
+  (void)versions;
+  if (!e) return fail("null engine");
+  std::unique_ptr<dk_json_tail> t(new dk_json_tail());
+  t->with_stats = with_stats != 0;
+  CB* c = t->col;
+  c[JL_PATH].init(PT_BYTE_ARRAY, 0, 2, 0, 0);
+  c[JL_PVK].init(PT_BYTE_ARRAY, 0, 3, 1, 3);
+  c[JL_PVV].init(PT_BYTE_ARRAY, 0, 4, 1, 3);
+  c[JL_SIZE].init(PT_INT64, 8, 2, 0, 0);
+  c[JL_MTIME].init(PT_INT64, 8, 2, 0, 0);
+  c[JL_DC].init(PT_BOOLEAN, 1, 2, 0, 0);
+  c[JL_DVST].init(PT_BYTE_ARRAY, 0, 3, 0, 0);
+  c[JL_DVPID].init(PT_BYTE_ARRAY, 0, 3, 0, 0);
+  c[JL_DVOFF].init(PT_INT32, 4, 3, 0, 0);
+  c[JL_DVSIZE].init(PT_INT32, 4, 3, 0, 0);
+  c[JL_DVCARD].init(PT_INT64, 8, 3, 0, 0);
+  c[JL_TGK].init(PT_BYTE_ARRAY, 0, 3, 1, 3);
+  c[JL_TGV].init(PT_BYTE_ARRAY, 0, 4, 1, 3);
+  c[JL_BRID].init(PT_INT64, 8, 2, 0, 0);
+  c[JL_DRCV].init(PT_INT64, 8, 2, 0, 0);
+  c[JL_STATS].init(PT_BYTE_ARRAY, 0, 2, 0, 0);
+  c[JL_RPATH].init(PT_BYTE_ARRAY, 0, 2, 0, 0);
+  c[JL_RDVST].init(PT_BYTE_ARRAY, 0, 3, 0, 0);
+  c[JL_RDVPID].init(PT_BYTE_ARRAY, 0, 3, 0, 0);
+  c[JL_RDVOFF].init(PT_INT32, 4, 3, 0, 0);
+  c[JL_RDVSIZE].init(PT_INT32, 4, 3, 0, 0);
+  c[JL_RDVCARD].init(PT_INT64, 8, 3, 0, 0);
+  const int J = e->cfg.json_batch_size;
+  std::vector<JNode> N;
+  for (int fi = 0; fi < n_files; fi++) {
+    std::vector<uint8_t> raw;
+    FILE* fp = fopen(paths[fi], "rb");
+    if (!fp) return fail(std::string("Error reading JSON file: ") + paths[fi]);
+    fseek(fp, 0, SEEK_END); long n = ftell(fp); fseek(fp, 0, SEEK_SET);
+    raw.resize(n > 0 ? n : 0);
+    size_t got = n > 0 ? fread(raw.data(), 1, n, fp) : 0;
+    fclose(fp);
+    if ((long)got != n) return fail(std::string("Error reading JSON file: ") + paths[fi]);
+    std::string text = java_utf8(raw.data(), raw.size());
+    // BufferedReader.readLine: lines end at \n, \r or \r\n
+    size_t i = 0;
+    int in_batch = 0;
+    bool any = false;
+    while (i < text.size()) {
+      size_t j = i;
+      while (j < text.size() && text[j] != '\n' && text[j] != '\r') j++;
+      std::string line = text.substr(i, j - i);
+      if (j < text.size() && text[j] == '\r' && j + 1 < text.size() && text[j + 1] == '\n') j++;
+      i = j + 1;
+      N.clear();
+      JParser jp(line.data(), line.data() + line.size(), N);
+      int root = jp.value(0);
+      if (root >= 0) { jp.ws(); if (jp.p != jp.e) { root = -1; jp.err = "trailing characters"; } }
+      if (root < 0) return fail(std::string("Error reading JSON file: ") + paths[fi] + " (" + jp.err + ")");
+      if (in_batch == J) { t->n_steps++; in_batch = 0; }
+      t->step.push_back(t->n_steps);
+      t->rowin.push_back(in_batch++);
+      any = true;
+      try {
+        const JNode& R = N[root];
+        if (R.t != J_OBJ) mismatch(N, R, "object");
+        const JNode* add = field(N, R, "add", true);
+        const JNode* rm = field(N, R, "remove", true);
+        if (add) {
+          if (add->t != J_OBJ) mismatch(N, *add, "object");
+          const JNode& A = *add;
+          c[JL_PATH].str_row(as_str(N, *field(N, A, "path", false)));
+          put_map(c[JL_PVK], c[JL_PVV], N, field(N, A, "partitionValues", false), 1);
+          int64_t v = as_long(N, *field(N, A, "size", false)); c[JL_SIZE].fix_row(&v);
+          v = as_long(N, *field(N, A, "modificationTime", false)); c[JL_MTIME].fix_row(&v);
+          uint8_t b = as_bool(N, *field(N, A, "dataChange", false)); c[JL_DC].fix_row(&b);
+          put_dv(&c[JL_DVST], N, field(N, A, "deletionVector", true), 1);
+          put_map(c[JL_TGK], c[JL_TGV], N, field(N, A, "tags", true), 1);
+          const JNode* x = field(N, A, "baseRowId", true);
+          if (x) { v = as_long(N, *x); c[JL_BRID].fix_row(&v); } else c[JL_BRID].null_row(1);
+          x = field(N, A, "defaultRowCommitVersion", true);
+          if (x) { v = as_long(N, *x); c[JL_DRCV].fix_row(&v); } else c[JL_DRCV].null_row(1);
+          if (t->with_stats) { x = field(N, A, "stats", true); if (x) c[JL_STATS].str_row(as_str(N, *x)); else c[JL_STATS].null_row(1); }
+          else c[JL_STATS].null_row(1);
+        } else {
+          for (int k : {JL_PATH, JL_SIZE, JL_MTIME, JL_DC, JL_DVST, JL_DVPID, JL_DVOFF, JL_DVSIZE, JL_DVCARD, JL_BRID, JL_DRCV, JL_STATS})
+            c[k].null_row(0);
+          put_map(c[JL_PVK], c[JL_PVV], N, nullptr, 0);
+          put_map(c[JL_TGK], c[JL_TGV], N, nullptr, 0);
+        }
+        if (rm) {
+          if (rm->t != J_OBJ) mismatch(N, *rm, "object");
+          c[JL_RPATH].str_row(as_str(N, *field(N, *rm, "path", false)));
+          put_dv(&c[JL_RDVST], N, field(N, *rm, "deletionVector", true), 1);
+        } else {
+          for (int k : {JL_RPATH, JL_RDVST, JL_RDVPID, JL_RDVOFF, JL_RDVSIZE, JL_RDVCARD}) c[k].null_row(0);
+        }
+      } catch (const JErr& je) {
+        return fail(je.msg);
+      }
+      t->rows++;
+    }
+    if (any) { t->n_steps++; in_batch = 0; }
+  }
+  *out = t.release();
+  return 0;
+}
+
+extern "C" int64_t dk_json_tail_rows(dk_json_tail* t) { return t ? t->rows : -1; }
+
+extern "C" int dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out) {
+  memset(out, 0, sizeof *out);
+  out->n_rows = t->rows;
+  int k = -1;
+  for (int i = 0; i < JL_N; i++) if (!strcmp(JSON_LEAVES[i], leaf)) k = i;
+  if (k < 0 || (k == JL_STATS && !t->with_stats)) { out->present = 0; return 0; }
+  CB& c = t->col[k];
+  out->present = 1;
+  out->phys = c.phys; out->width = c.width; out->max_def = c.max_def; out->max_rep = c.max_rep; out->rep_def = c.rep_def;
+  out->n_entries = c.max_rep ? (int64_t)c.entry_def.size() : t->rows;
+  out->n_chars = (int64_t)c.chars.size();
+  out->row_def = c.row_def.data();
+  out->row_offs = c.max_rep ? c.row_offs.data() : nullptr;
+  out->entry_def = c.max_rep ? c.entry_def.data() : nullptr;
+  out->fixed = c.phys == PT_BYTE_ARRAY ? nullptr : c.fixed.data();
+  out->offs = c.phys == PT_BYTE_ARRAY ? c.offs.data() : nullptr;
+  out->chars = c.phys == PT_BYTE_ARRAY ? c.chars.data() : nullptr;
+  return 0;
+}
+
+extern "C" void dk_json_tail_free(dk_json_tail* t) { delete t; }
+
+// ------------------------------------------------------------------------------------------------
+// replay
+// ------------------------------------------------------------------------------------------------
+struct dk_replay {
+  dk_engine* eng = nullptr;
+  dk_json_tail* tail = nullptr;
+  dk_parquet* ck = nullptr;
+  std::vector<DJsonAction> acts;
+  std::vector<int64_t> act_row;        // tail row of each action
+  DBuf d_acts, d_jchars, d_canon, d_slots, d_state, d_jsel;
+  std::vector<std::unique_ptr<DBuf>> d_csel;   // per checkpoint file
+  std::vector<ProbeCols> probe;
+  uint64_t mask = 0;
+  uint32_t seed = 0;
+  KTimer timer;
+  std::vector<uint8_t> h_jsel;
+  DState h_state{};
+  bool have_result = false;
+};
+
+static const DColumn* find_col(dk_parquet* p, int fi, const char* leaf) {
+  for (size_t li = 0; li < p->leaves.size(); li++)
+    if (p->leaves[li] == leaf) { int ci = p->colmap[fi][li]; return ci >= 0 ? &p->h_cols[ci] : nullptr; }
+  return nullptr;
+}
+
+extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_replay** out) {
+  if (!e) return fail("null engine");
+  hipSetDevice(e->cfg.device);
+  std::unique_ptr<dk_replay> r(new dk_replay());
+  r->eng = e; r->tail = tail; r->ck = ckpt;
+  r->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
+  hipStream_t s = e->stream;
+  // actions: removes and adds of each tail row (a row may carry both)
+  std::vector<uint8_t> jchars;
+  int64_t canon_n = 0;
+  if (tail) {
+    const CB* c = tail->col;
+    auto add_str = [&](const CB& col, int64_t row, int64_t* off, int32_t* len) {
+      int64_t b = col.offs[row], en = col.offs[row + 1];
+      *off = (int64_t)jchars.size(); *len = (int32_t)(en - b);
+      jchars.insert(jchars.end(), col.chars.begin() + b, col.chars.begin() + en);
+    };
+    for (int64_t row = 0; row < tail->rows; row++) {
+      for (int kind : {JA_REMOVE, JA_ADD}) {
+        const CB& pc = c[kind == JA_ADD ? JL_PATH : JL_RPATH];
+        if (pc.row_def[row] < 1) continue;
+        DJsonAction a{};
+        a.kind = kind; a.step = tail->step[row]; a.row = tail->rowin[row];
+        add_str(pc, row, &a.path_off, &a.path_len);
+        const CB& st = c[kind == JA_ADD ? JL_DVST : JL_RDVST];
+        const CB& pid = c[kind == JA_ADD ? JL_DVPID : JL_RDVPID];
+        const CB& off = c[kind == JA_ADD ? JL_DVOFF : JL_RDVOFF];
+        a.has_dv = st.row_def[row] >= 2;
+        if (a.has_dv) {
+          add_str(st, row, &a.st_off, &a.st_len);
+          add_str(pid, row, &a.pid_off, &a.pid_len);
+          a.has_off = off.row_def[row] == 3;
+          if (a.has_off) memcpy(&a.dv_off, off.fixed.data() + row * 4, 4);
+        }
+        a.canon_off = canon_n;
+        canon_n += a.path_len + 64 + a.st_len + a.pid_len + 32;
+        r->acts.push_back(a);
+        r->act_row.push_back(row);
+      }
+    }
+  }
+  size_t na = r->acts.size();
+  uint64_t cap = 1024;
+  while (cap < 2 * na + 16) cap <<= 1;
+  r->mask = cap - 1;
+  if (upload(r->d_acts, r->acts.data(), na * sizeof(DJsonAction), s)) return 1;
+  if (upload(r->d_jchars, jchars.data(), jchars.size(), s)) return 1;
+  if (r->d_canon.alloc(canon_n + 64)) return 1;
+  if (r->d_slots.alloc(cap * sizeof(Slot))) return 1;
+  if (r->d_state.alloc(sizeof(DState))) return 1;
+  if (r->d_jsel.alloc(na + 16)) return 1;
+  if (ckpt) {
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      ProbeCols pc{};
+      const DColumn* path = find_col(ckpt, (int)fi, "add.path");
+      pc.n_rows = ckpt->files[fi].num_rows;
+      r->d_csel.emplace_back(new DBuf());
+      if (r->d_csel.back()->alloc(pc.n_rows + 16)) return 1;
+      if (!path) { pc.n_rows = 0; r->probe.push_back(pc); continue; }
+      if (path->phys != PT_BYTE_ARRAY || path->max_rep) return fail("add.path has an unexpected type");
+      pc.path_def = path->row_def; pc.path_offs = path->offs; pc.path_chars = path->chars;
+      const DColumn* st = find_col(ckpt, (int)fi, "add.deletionVector.storageType");
+      const DColumn* pid = find_col(ckpt, (int)fi, "add.deletionVector.pathOrInlineDv");
+      const DColumn* off = find_col(ckpt, (int)fi, "add.deletionVector.offset");
+      if (st && pid) {
+        pc.has_dv = 1;
+        pc.st_def = st->row_def; pc.st_offs = st->offs; pc.st_chars = st->chars;
+        pc.pid_offs = pid->offs; pc.pid_chars = pid->chars;
+        if (off) { pc.off_def = off->row_def; pc.off_vals = (const int32_t*)off->fixed; pc.off_maxdef = off->max_def; }
+      }
+      r->probe.push_back(pc);
+    }
+  }
+  HIPOK(hipStreamSynchronize(s));
+  *out = r.release();
+  return 0;
+}
+
+static int replay_launch(dk_replay* r) {
+  hipStream_t s = r->eng->stream;
+  KTimer& T = r->timer;
+  KTimer::Scope total(&T, 12, s);
+  DState st0{};
+  st0.err_row = LLONG_MAX;
+  HIPOK(hipMemcpyAsync(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
+  // probe table: h = 0 (empty), first_add = ~0, min_rm_step = INT32_MAX
+  launch_slots_init(r->d_slots.as<Slot>(), r->mask + 1, s);
+  int na = (int)r->acts.size();
+  DState* st = r->d_state.as<DState>();
+  DJsonAction* A = r->d_acts.as<DJsonAction>();
+  Slot* S = r->d_slots.as<Slot>();
+  { KTimer::Scope sc(&T, 7, s); launch_json_canon(A, na, r->d_jchars.as<uint8_t>(), r->d_canon.as<uint8_t>(), r->seed, st, s); }
+  { KTimer::Scope sc(&T, 8, s); launch_table_insert(A, na, S, r->mask, s); }
+  { KTimer::Scope sc(&T, 9, s); launch_table_update(A, na, S, r->mask, r->d_canon.as<uint8_t>(), st, s); }
+  { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->d_jsel.as<uint8_t>(), st, s); }
+  if (r->ck) {
+    dk_parquet* p = r->ck;
+    // decode errors are collected into the replay state too
+    HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
+    if (run_pipeline(p, 1)) return 1;
+    for (size_t fi = 0; fi < r->probe.size(); fi++) {
+      KTimer::Scope sc(&T, 11, s);
+      launch_probe(r->probe[fi], S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, r->d_csel[fi]->as<uint8_t>(), st, s);
+    }
+  }
+  return 0;
+}
+
+extern "C" int dk_replay_run(dk_replay* r) {
+  hipSetDevice(r->eng->cfg.device);
+  r->have_result = false;
+  if (r->ck) for (auto& h : r->ck->host) h.ready = false;
+  return replay_launch(r);
+}
+
+extern "C" int dk_replay_sync(dk_replay* r) {
+  hipStream_t s = r->eng->stream;
+  for (int attempt = 0; attempt < 8; attempt++) {
+    HIPOK(hipStreamSynchronize(s));
+    r->timer.collect();
+    if (r->ck) { r->ck->timer.collect(); if (check_state(r->ck)) return 1; }
+    HIPOK(hipMemcpy(&r->h_state, r->d_state.p, sizeof(DState), hipMemcpyDeviceToHost));
+    if (r->h_state.err_flags & E_COLLISION) {     // 64-bit key-hash collision: rebuild with a new seed
+      r->seed++;
+      if (replay_launch(r)) return 1;
+      continue;
+    }
+    if (r->h_state.err_flags & (E_URI | E_UTF8)) {
+      std::vector<DJsonAction> acts(r->acts.size());
+      if (!acts.empty()) HIPOK(hipMemcpy(acts.data(), r->d_acts.p, acts.size() * sizeof(DJsonAction), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < acts.size(); i++)
+        if (acts[i].status) {
+          const CB& pc = r->tail->col[acts[i].kind == JA_ADD ? JL_PATH : JL_RPATH];
+          int64_t row = r->act_row[i];
+          std::string path(pc.chars.begin() + pc.offs[row], pc.chars.begin() + pc.offs[row + 1]);
+          return fail((acts[i].status == -1 ? "java.net.URISyntaxException: Illegal character in path: "
+                                            : "malformed UTF-8 in action key (unsupported): ") + path);
+        }
+      return fail(std::string(r->h_state.err_flags & E_URI ? "java.net.URISyntaxException" : "malformed UTF-8 key") +
+                  " in checkpoint row " + std::to_string(r->h_state.err_row));
+    }
+    r->have_result = true;
+    return 0;
+  }
+  return fail("replay: repeated key-hash collisions");
+}
+
+extern "C" int dk_replay_counters(dk_replay* r, int64_t out[5]) {
+  if (!r->have_result) return fail("replay has no result (call dk_replay_sync)");
+  for (int i = 0; i < 5; i++) out[i] = (int64_t)r->h_state.counters[i];
+  return 0;
+}
+
+extern "C" int dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n) {
+  if (!r->have_result) return fail("replay has no result");
+  if (!r->tail || n != r->tail->rows) return fail("bad selection size");
+  memset(out, 0, n);
+  std::vector<uint8_t> sel(r->acts.size());
+  if (!sel.empty()) HIPOK(hipMemcpy(sel.data(), r->d_jsel.p, sel.size(), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < sel.size(); i++) if (r->acts[i].kind == JA_ADD && sel[i]) out[r->act_row[i]] = 1;
+  return 0;
+}
+
+extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out, int64_t n) {
+  if (!r->have_result) return fail("replay has no result");
+  if (!r->ck || file < 0 || file >= (int)r->d_csel.size()) return fail("bad checkpoint file index");
+  if (n != r->ck->files[file].num_rows) return fail("bad selection size");
+  if (r->probe[file].n_rows == 0) { memset(out, 0, n); return 0; }
+  HIPOK(hipMemcpy(out, r->d_csel[file]->p, n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {
+  if (i < 0 || i >= KTimer::K) return 1;
+  // decode kernels are timed by the parquet object's timer, the rest by the replay's
+  const KTimer* t = (r->ck && i <= 6) ? &r->ck->timer : &r->timer;
+  *name = t->names[i];
+  if (!*name) return 1;
+  *count = t->cnt[i];
+  *avg_us = t->cnt[i] ? 1000.0 * t->sum_ms[i] / (double)t->cnt[i] : 0.0;
+  return 0;
+}
+
+extern "C" void dk_replay_free(dk_replay* r) {
+  if (!r) return;
+  hipSetDevice(r->eng->cfg.device);
+  hipStreamSynchronize(r->eng->stream);
+  delete r;
+}

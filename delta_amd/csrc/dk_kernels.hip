@@ -1,0 +1,954 @@
+// CDNA4 (gfx950) kernels for checkpoint decode + log-replay reconciliation.
+//
+// Work unit = one Parquet page (one 256-thread workgroup, 4 wave64s). Everything here is
+// byte/integer work bounded by HBM bandwidth; there is no dense contraction, so no MFMA.
+// Pipeline per replay step:
+//   k_page_headers      Thrift PageHeader parse, one lane per page
+//   k_string_positions  PLAIN BYTE_ARRAY entry positions: speculative zero-run candidates +
+//                       exact chain verification, sequential fallback
+//   k_page_count        RLE/bit-packed hybrid level decode -> rows / entries / values / chars
+//   k_column_scan       per-column exclusive scan of page counts
+//   k_page_decode       levels + values -> row_def / row_offs / entry_def / fixed / offs
+//   k_string_copy       PLAIN string bytes -> contiguous chars (16 B aligned stores)
+//   k_json_canon / k_table_insert / k_table_update / k_json_select   commit-tail keys
+//   k_probe             checkpoint add rows: URI-canonical key hash, probe, verify, select
+#include <hip/hip_runtime.h>
+
+#include "dk_device.h"
+#include "dk_thrift.h"
+#include "dk_uri.h"
+
+namespace dk {
+
+constexpr int NT = 256;          // threads per workgroup
+constexpr int LW = 512;          // levels per window (2 per thread)
+constexpr int MAXSEG = 512;
+
+// --------------------------------------------------------------------------------------------
+// small helpers
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ const uint8_t* page_data(const DPage& pg, const DChunk& ck, const uint8_t* arena) {
+  return pg.unc_off >= 0 ? arena + pg.unc_off : ck.file + pg.data_off;
+}
+__device__ __forceinline__ int32_t page_len(const DPage& pg) { return pg.unc_off >= 0 ? pg.usize : pg.csize; }
+
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+__device__ __forceinline__ uint32_t read_bits(const uint8_t* p, int64_t bit, int bw, const uint8_t* e) {
+  if (bw == 0) return 0;
+  const uint8_t* q = p + (bit >> 3);
+  int sh = (int)(bit & 7);
+  int nb = (sh + bw + 7) >> 3;
+  uint64_t w = 0;
+  for (int k = 0; k < nb; k++) {
+    const uint8_t* a = q + k;
+    if (a < e) w |= (uint64_t)(*a) << (8 * k);
+  }
+  uint64_t mask = (bw >= 32) ? 0xffffffffull : ((1ull << bw) - 1);
+  return (uint32_t)((w >> sh) & mask);
+}
+
+// block-wide exclusive scan of up to 3 ints
+__device__ __forceinline__ void block_scan3(int a, int b, int c, int* ea, int* eb, int* ec,
+                                            int* ta, int* tb, int* tc, int* lds /*3*4*/) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = a, y = b, z = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int xa = __shfl_up(x, o, 64), ya = __shfl_up(y, o, 64), za = __shfl_up(z, o, 64);
+    if (lane >= o) { x += xa; y += ya; z += za; }
+  }
+  if (lane == 63) { lds[wid * 3] = x; lds[wid * 3 + 1] = y; lds[wid * 3 + 2] = z; }
+  __syncthreads();
+  int ba = 0, bb = 0, bc = 0, sa = 0, sb = 0, sc = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) {
+    int p = lds[w * 3], q = lds[w * 3 + 1], r = lds[w * 3 + 2];
+    if (w < wid) { ba += p; bb += q; bc += r; }
+    sa += p; sb += q; sc += r;
+  }
+  __syncthreads();
+  *ea = ba + x - a; *eb = bb + y - b; *ec = bc + z - c;
+  *ta = sa; *tb = sb; *tc = sc;
+}
+
+__device__ __forceinline__ long long block_scan64(long long v, long long* total, long long* lds) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  long long base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; w++) { long long s = lds[w]; if (w < wid) base += s; tot += s; }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// --------------------------------------------------------------------------------------------
+// RLE / bit-packed hybrid: one lane walks run headers, all lanes expand
+// --------------------------------------------------------------------------------------------
+struct Hyb {
+  const uint8_t* p;
+  const uint8_t* e;
+  const uint8_t* bp;
+  int32_t bw, left, is_bp, bp_idx;
+  uint32_t val;
+  int32_t err;
+};
+struct Seg {
+  int32_t start;     // first output index covered (window-local)
+  int32_t bp_idx;    // index within the bit-packed run, or -1 for an RLE run
+  uint32_t val;      // RLE value
+  uint32_t bp_off;   // bit-packed run data offset from Hyb.base
+};
+
+__device__ __forceinline__ void hyb_init(Hyb& h, const uint8_t* p, const uint8_t* e, int bw) {
+  h.p = p; h.e = e; h.bp = p; h.bw = bw; h.left = 0; h.is_bp = 0; h.bp_idx = 0; h.val = 0; h.err = 0;
+}
+
+// lane-serial: produce segments covering up to `want` values; returns number covered
+__device__ int hyb_fill(Hyb& h, const uint8_t* base, Seg* seg, int want, int* nseg) {
+  int got = 0, ns = 0;
+  while (got < want && ns < MAXSEG) {
+    if (h.left == 0) {
+      if (h.p >= h.e) { h.err = 1; break; }
+      uint64_t hdr = 0;
+      int s = 0;
+      for (;;) {
+        if (h.p >= h.e) { h.err = 1; *nseg = ns; return got; }
+        uint8_t b = *h.p++;
+        hdr |= (uint64_t)(b & 0x7f) << s;
+        if (!(b & 0x80)) break;
+        s += 7;
+        if (s > 35) { h.err = 1; *nseg = ns; return got; }
+      }
+      if (hdr & 1) {
+        int64_t groups = (int64_t)(hdr >> 1);
+        h.is_bp = 1; h.left = (int32_t)(groups * 8); h.bp = h.p; h.bp_idx = 0;
+        h.p += groups * h.bw;
+        if (h.p > h.e) h.p = h.e;   // truncated final run: values past the end are never used
+      } else {
+        h.is_bp = 0; h.left = (int32_t)(hdr >> 1);
+        int nb = (h.bw + 7) >> 3;
+        uint32_t v = 0;
+        for (int k = 0; k < nb; k++) {
+          if (h.p >= h.e) { h.err = 1; *nseg = ns; return got; }
+          v |= (uint32_t)(*h.p++) << (8 * k);
+        }
+        h.val = v;
+      }
+      if (h.left == 0) continue;
+    }
+    int take = min(h.left, want - got);
+    Seg sg;
+    sg.start = got;
+    sg.bp_idx = h.is_bp ? h.bp_idx : -1;
+    sg.val = h.val;
+    sg.bp_off = (uint32_t)(h.bp - base);
+    seg[ns++] = sg;
+    got += take;
+    h.left -= take;
+    if (h.is_bp) h.bp_idx += take;
+  }
+  *nseg = ns;
+  return got;
+}
+
+__device__ __forceinline__ uint32_t seg_value(const Seg* seg, int nseg, int i, int bw, const uint8_t* base,
+                                              const uint8_t* e) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (seg[mid].start <= i) lo = mid; else hi = mid - 1;
+  }
+  const Seg s = seg[lo];
+  if (s.bp_idx < 0) return s.val;
+  int64_t bit = (int64_t)(s.bp_idx + (i - s.start)) * bw;
+  return read_bits(base + s.bp_off, bit, bw, e);
+}
+
+// --------------------------------------------------------------------------------------------
+// page layout
+// --------------------------------------------------------------------------------------------
+struct Layout {
+  const uint8_t* d;      // page data start (base for segment offsets)
+  const uint8_t* e;
+  const uint8_t* rep_p; const uint8_t* rep_e;
+  const uint8_t* def_p; const uint8_t* def_e;
+  const uint8_t* val_p; const uint8_t* val_e;
+  int ok;
+};
+
+__device__ __forceinline__ Layout page_layout(const DPage& pg, const DChunk& ck, const uint8_t* arena) {
+  Layout L;
+  L.d = page_data(pg, ck, arena);
+  L.e = L.d + page_len(pg);
+  L.ok = 1;
+  const uint8_t* q = L.d;
+  if (pg.ptype == PAGE_DATA) {
+    L.rep_p = L.rep_e = q;
+    if (ck.max_rep > 0) {
+      if (q + 4 > L.e) { L.ok = 0; return L; }
+      uint32_t n = ld_u32(q);
+      L.rep_p = q + 4; L.rep_e = q + 4 + n; q = L.rep_e;
+    }
+    L.def_p = L.def_e = q;
+    if (ck.max_def > 0) {
+      if (q + 4 > L.e) { L.ok = 0; return L; }
+      uint32_t n = ld_u32(q);
+      L.def_p = q + 4; L.def_e = q + 4 + n; q = L.def_e;
+    }
+  } else {
+    L.rep_p = q; L.rep_e = q + pg.rl_len; q = L.rep_e;
+    L.def_p = q; L.def_e = q + pg.dl_len; q = L.def_e;
+  }
+  if (q > L.e) { L.ok = 0; return L; }
+  L.val_p = q; L.val_e = L.e;
+  return L;
+}
+
+__device__ __forceinline__ int bit_width(int v) { int w = 0; while ((1 << w) <= v) w++; return v == 0 ? 0 : w; }
+
+// --------------------------------------------------------------------------------------------
+// K1: page headers (one lane per page)
+// --------------------------------------------------------------------------------------------
+__global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restrict__ pages, int n_pages,
+                               const int64_t* __restrict__ file_len) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pages) return;
+  DPage pg = pages[i];
+  const DChunk& ck = chunks[pg.chunk];
+  const uint8_t* p = ck.file + pg.hdr_off;
+  // headers are small; bound the parse to 64 KiB (large min/max statistics are skipped)
+  PageHeader h = parse_page_header(p, p + 65536);
+  pg.status = PS_OK;
+  if (!h.ok) pg.status = PS_BAD_HEADER;
+  pg.ptype = h.type; pg.enc = h.enc; pg.num_values = h.num_values; pg.dl_len = h.dl_len; pg.rl_len = h.rl_len;
+  pg.csize = h.csize; pg.usize = h.usize; pg.hdr_len = h.hdr_len; pg.is_comp = h.is_comp;
+  pg.data_off = pg.hdr_off + h.hdr_len;
+  if (h.ok) {
+    bool dict = (pg.flags & PF_DICT) != 0;
+    if (dict != (h.type == PAGE_DICT)) pg.status = PS_BAD_HEADER;
+    if (!dict && h.type != PAGE_DATA && h.type != PAGE_DATA_V2) pg.status = PS_UNSUPPORTED;
+    if (h.type == PAGE_DATA && ((ck.max_def > 0 && h.dl_enc != ENC_RLE) || (ck.max_rep > 0 && h.rl_enc != ENC_RLE)))
+      pg.status = PS_UNSUPPORTED;
+    if (ck.codec != CODEC_NONE && pg.unc_off < 0 && !(h.type == PAGE_DATA_V2 && !h.is_comp)) pg.status = PS_UNSUPPORTED;
+  }
+  pages[i] = pg;
+}
+
+// --------------------------------------------------------------------------------------------
+// K2: PLAIN BYTE_ARRAY entry positions (data pages and string dictionaries)
+// P[k] = offset of entry k's 4-byte length prefix within the region, P[n] = region size.
+// Speculation: with non-empty, NUL-free string content and lengths < 2^16 whose low byte is
+// non-zero, every maximal run of zero bytes ends exactly at byte 3 of a length prefix. The
+// candidates are accepted only if they form the exact length chain from 0 to the region end;
+// otherwise one lane walks the chain (always exact).
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                         const uint8_t* __restrict__ arena, int32_t* __restrict__ pos) {
+  const DPage& pg = pages[blockIdx.x];
+  const DChunk& ck = chunks[pg.chunk];
+  if (ck.phys != PT_BYTE_ARRAY || pg.status != PS_OK) return;
+  const bool dict = (pg.flags & PF_DICT) != 0;
+  const uint8_t* r;
+  int64_t R;
+  int32_t n;
+  int32_t* P;
+  if (dict) {
+    r = page_data(pg, ck, arena);
+    R = page_len(pg);
+    n = pg.num_values;
+    P = pos + ck.dict_pos;
+  } else {
+    if (pg.enc != ENC_PLAIN) return;
+    Layout L = page_layout(pg, ck, arena);
+    if (!L.ok) return;
+    r = L.val_p;
+    R = L.val_e - L.val_p;
+    n = pg.n_values;
+    P = pos + pg.pos_base;
+  }
+  __shared__ int s_fail;
+  __shared__ int lds[12];
+  const int t = threadIdx.x;
+  if (t == 0) s_fail = 0;
+  __syncthreads();
+  int carry = 0;
+  for (int64_t w0 = 0; w0 < R; w0 += NT * 16) {
+    int64_t b = w0 + (int64_t)t * 16;
+    uint32_t m = 0;
+    int cnt = 0;
+    if (b < R) {
+      uint8_t by[20];
+#pragma unroll
+      for (int j = 0; j < 20; j++) by[j] = (b + j < R) ? r[b + j] : 1;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        int64_t q = b + j;
+        bool c = (q + 3 < R) && by[j + 3] == 0 && (q + 4 == R || by[j + 4] != 0);
+        if (c) { m |= 1u << j; cnt++; }
+      }
+    }
+    int base, d0, d1, tot, t1, t2;
+    block_scan3(cnt, 0, 0, &base, &d0, &d1, &tot, &t1, &t2, lds);
+    if (carry + tot > n) { if (t == 0) s_fail = 1; }
+    else {
+      int k = carry + base;
+      while (m) { int j = __ffs(m) - 1; m &= m - 1; P[k++] = (int32_t)(b + j); }
+    }
+    carry += tot;
+    if (carry > n) break;
+  }
+  __syncthreads();
+  if (carry != n) s_fail = 1;   // same value in every lane
+  __syncthreads();
+  if (!s_fail) {
+    for (int k = t; k < n; k += NT) {
+      int64_t pk = P[k];
+      int64_t nxt = (k + 1 < n) ? (int64_t)P[k + 1] : R;
+      if (k == 0 && pk != 0) s_fail = 1;
+      if (pk + 4 > R || pk + 4 + (int64_t)ld_u32(r + pk) != nxt) s_fail = 1;
+    }
+  }
+  __syncthreads();
+  if (s_fail && t == 0) {
+    int64_t q = 0;
+    int bad = 0;
+    for (int k = 0; k < n; k++) {
+      if (q + 4 > R) { bad = 1; break; }
+      P[k] = (int32_t)q;
+      q += 4 + (int64_t)ld_u32(r + q);
+      if (q > R) { bad = 1; break; }
+    }
+    if (bad) pages[blockIdx.x].status = dict ? PS_BAD_DICT : PS_BAD_VALUES;
+  }
+  if (t == 0) P[n] = (int32_t)R;
+}
+
+// --------------------------------------------------------------------------------------------
+// shared window machinery for the count / decode passes
+// --------------------------------------------------------------------------------------------
+struct WinLds {
+  Hyb hr, hd, hi;
+  Seg segr[MAXSEG];
+  Seg segd[MAXSEG];
+  Seg segi[MAXSEG];
+  int nr, nd, ni, win, err;
+  int scan[12];
+  long long scan64[4];
+};
+
+// lane 0: fill rep+def segments for the next window; sets W.win
+__device__ __forceinline__ void fill_levels(WinLds& W, const Layout& L, const DChunk& ck, int remaining) {
+  int want = min(LW, remaining);
+  int got = want;
+  if (ck.max_rep > 0) {
+    got = hyb_fill(W.hr, L.d, W.segr, want, &W.nr);
+  }
+  if (ck.max_def > 0) {
+    int gd = hyb_fill(W.hd, L.d, W.segd, got, &W.nd);
+    if (gd < got) {
+      if (ck.max_rep > 0) W.err = 1;   // rep stream over-advanced: unsupported pathological runs
+      got = gd;
+    }
+  }
+  if (got <= 0) W.err = 1;
+  W.win = got;
+}
+
+__device__ __forceinline__ void level_at(const WinLds& W, const Layout& L, const DChunk& ck, int i, int bwr, int bwd,
+                                         int* rep, int* def) {
+  *rep = ck.max_rep > 0 ? (int)seg_value(W.segr, W.nr, i, bwr, L.d, L.rep_e) : 0;
+  *def = ck.max_def > 0 ? (int)seg_value(W.segd, W.nd, i, bwd, L.d, L.def_e) : 0;
+}
+
+__device__ __forceinline__ const uint8_t* dict_data(const DChunk& ck, const DPage* pages, const uint8_t* arena,
+                                                    int32_t* dict_n) {
+  const DPage& dp = pages[ck.dict_page];
+  *dict_n = dp.num_values;
+  return page_data(dp, ck, arena);
+}
+
+// --------------------------------------------------------------------------------------------
+// K3: counts per data page
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_page_count(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                   const uint8_t* __restrict__ arena, const int32_t* __restrict__ pos) {
+  DPage& pg = pages[blockIdx.x];
+  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
+  const DChunk& ck = chunks[pg.chunk];
+  __shared__ WinLds W;
+  const int t = threadIdx.x;
+  Layout L = page_layout(pg, ck, arena);
+  if (!L.ok) { if (t == 0) pg.status = PS_BAD_LEVELS; return; }
+  const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
+  if (t == 0) {
+    hyb_init(W.hr, L.rep_p, L.rep_e, bwr);
+    hyb_init(W.hd, L.def_p, L.def_e, bwd);
+    W.err = 0;
+  }
+  __syncthreads();
+  int rows = 0, ents = 0, vals = 0;
+  const int nv = pg.num_values;
+  for (int w0 = 0; w0 < nv;) {
+    if (t == 0) fill_levels(W, L, ck, nv - w0);
+    __syncthreads();
+    const int win = W.win;
+    if (W.err) break;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      int i = t * 2 + k;
+      if (i < win) {
+        int rep, def;
+        level_at(W, L, ck, i, bwr, bwd, &rep, &def);
+        rows += (rep == 0);
+        ents += (def >= ck.rep_def);
+        vals += (def == ck.max_def);
+      }
+    }
+    w0 += win;
+    __syncthreads();
+  }
+  int er, ee, ev, tr, te, tv;
+  block_scan3(rows, ents, vals, &er, &ee, &ev, &tr, &te, &tv, W.scan);
+  if (W.err) { if (t == 0) pg.status = PS_BAD_LEVELS; return; }
+  // characters
+  long long nchars = 0;
+  bool bad = false;
+  if (ck.phys == PT_BYTE_ARRAY) {
+    if (pg.enc == ENC_PLAIN) {
+      nchars = (long long)(L.val_e - L.val_p) - 4ll * tv;
+      if (nchars < 0) bad = true;
+    } else if (pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) {
+      if (ck.dict_page < 0) { bad = true; }
+      else {
+        const int32_t* DP = pos + ck.dict_pos;
+        int32_t dn;
+        dict_data(ck, pages, arena, &dn);
+        const int ibw = tv > 0 ? (int)(*L.val_p) : 0;
+        if (t == 0) { hyb_init(W.hi, L.val_p + 1, L.val_e, ibw); }
+        __syncthreads();
+        long long local = 0;
+        for (int v0 = 0; v0 < tv;) {
+          if (t == 0) { W.win = hyb_fill(W.hi, L.d, W.segi, min(LW, tv - v0), &W.ni); if (W.win <= 0) W.err = 1; }
+          __syncthreads();
+          const int win = W.win;
+          if (W.err) break;
+          for (int i = t; i < win; i += NT) {
+            uint32_t ix = seg_value(W.segi, W.ni, i, ibw, L.d, L.val_e);
+            if ((int32_t)ix >= dn) { W.err = 1; continue; }
+            local += (long long)(DP[ix + 1] - DP[ix] - 4);
+          }
+          v0 += win;
+          __syncthreads();
+        }
+        long long tot;
+        block_scan64(local, &tot, W.scan64);
+        nchars = tot;
+        if (W.err) bad = true;
+      }
+    } else if (pg.enc != ENC_PLAIN || tv > 0) {
+      if (tv > 0) bad = true;
+    }
+  } else {
+    bool ok_enc = pg.enc == ENC_PLAIN || ((pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) && ck.dict_page >= 0) ||
+                  (pg.enc == ENC_RLE && ck.phys == PT_BOOLEAN);
+    if (!ok_enc && tv > 0) bad = true;
+  }
+  if (t == 0) {
+    pg.n_rows = ck.max_rep > 0 ? tr : nv;
+    pg.n_entries = ck.max_rep > 0 ? te : nv;
+    pg.n_values = tv;
+    pg.n_chars = nchars;
+    if (bad) pg.status = PS_UNSUPPORTED;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// K4: per-column exclusive scan over its data pages (one workgroup per column)
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_column_scan(DColumn* __restrict__ cols, DPage* __restrict__ pages,
+                                                    DState* __restrict__ st) {
+  DColumn& c = cols[blockIdx.x];
+  __shared__ int lds[12];
+  __shared__ long long l64[4];
+  long long rb = 0, eb = 0, vb = 0, cb = 0;
+  int bad = 0;
+  for (int p0 = 0; p0 < c.n_pages; p0 += NT) {
+    int i = p0 + threadIdx.x;
+    int r = 0, e = 0, v = 0;
+    long long ch = 0;
+    if (i < c.n_pages) {
+      const DPage& pg = pages[c.first_page + i];
+      if (pg.status != PS_OK) bad = 1;
+      r = pg.n_rows; e = pg.n_entries; v = pg.n_values; ch = pg.n_chars;
+    }
+    int er, ee, ev, tr, te, tv;
+    block_scan3(r, e, v, &er, &ee, &ev, &tr, &te, &tv, lds);
+    long long tc;
+    long long ec = block_scan64(ch, &tc, l64);
+    if (i < c.n_pages) {
+      DPage& pg = pages[c.first_page + i];
+      pg.row_base = rb + er; pg.entry_base = eb + ee; pg.value_base = vb + ev; pg.char_base = cb + ec;
+    }
+    rb += tr; eb += te; vb += tv; cb += tc;
+  }
+  if (bad) atomicOr(&st->err_flags, E_PAGE);
+  if (threadIdx.x == 0) {
+    c.n_entries = c.max_rep > 0 ? eb : rb;
+    c.n_chars = cb;
+    if (rb != c.n_rows || (c.max_rep > 0 && eb > c.cap_entries) || cb > c.cap_chars) atomicOr(&st->err_flags, E_PAGE);
+    if (c.phys == PT_BYTE_ARRAY && c.offs && !(cb > c.cap_chars)) c.offs[c.max_rep > 0 ? eb : rb] = cb;
+    if (c.max_rep > 0 && c.row_offs && eb <= c.cap_entries) c.row_offs[rb] = eb;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// K5: decode levels + values of one data page
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+                                                    const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
+                                                    const int32_t* __restrict__ pos) {
+  const DPage& pg = pages[blockIdx.x];
+  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
+  const DChunk& ck = chunks[pg.chunk];
+  const DColumn& col = cols[ck.col];
+  __shared__ WinLds W;
+  __shared__ int s_dict_n;
+  const int t = threadIdx.x;
+  Layout L = page_layout(pg, ck, arena);
+  const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
+  const bool rep = ck.max_rep > 0;
+  const bool is_str = ck.phys == PT_BYTE_ARRAY;
+  const bool is_dict = pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT;
+  const int w = ck.width;
+  const uint8_t* D = nullptr;
+  const int32_t* DP = nullptr;
+  int ibw = 0;
+  if (is_dict) {
+    int32_t dn;
+    D = dict_data(ck, pages, arena, &dn);
+    if (t == 0) s_dict_n = dn;
+    if (is_str) DP = pos + ck.dict_pos;
+    ibw = pg.n_values > 0 ? (int)(*L.val_p) : 0;
+  }
+  const int32_t* P = (is_str && pg.enc == ENC_PLAIN) ? pos + pg.pos_base : nullptr;
+  // RLE booleans: 4-byte length then hybrid (bw 1)
+  const uint8_t* bool_rle_p = nullptr;
+  if (ck.phys == PT_BOOLEAN && pg.enc == ENC_RLE) bool_rle_p = L.val_p + 4;
+  if (t == 0) {
+    hyb_init(W.hr, L.rep_p, L.rep_e, bwr);
+    hyb_init(W.hd, L.def_p, L.def_e, bwd);
+    if (is_dict) hyb_init(W.hi, L.val_p + 1, L.val_e, ibw);
+    else if (bool_rle_p) hyb_init(W.hi, bool_rle_p, L.val_e, 1);
+    W.err = 0;
+  }
+  __syncthreads();
+  int rows_c = 0, ents_c = 0, vals_c = 0;      // carries (page-local)
+  long long chars_c = 0;                        // dictionary string chars carry
+  const int nv = pg.num_values;
+  for (int w0 = 0; w0 < nv;) {
+    if (t == 0) fill_levels(W, L, ck, nv - w0);
+    __syncthreads();
+    const int win = W.win;
+    if (W.err) break;
+    int rp[2], df[2];
+    int nr = 0, ne = 0, nvl = 0;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      int i = t * 2 + k;
+      rp[k] = 1; df[k] = -1;
+      if (i < win) {
+        level_at(W, L, ck, i, bwr, bwd, &rp[k], &df[k]);
+        nr += (rp[k] == 0);
+        ne += (df[k] >= ck.rep_def);
+        nvl += (df[k] == ck.max_def);
+      }
+    }
+    int er, ee, ev, tr, te, tv;
+    block_scan3(nr, ne, nvl, &er, &ee, &ev, &tr, &te, &tv, W.scan);
+    // dictionary indices / RLE booleans for the values of this window
+    if ((is_dict || bool_rle_p) && tv > 0) {
+      if (t == 0) {
+        int got = hyb_fill(W.hi, L.d, W.segi, tv, &W.ni);
+        if (got < tv) W.err = 1;
+      }
+      __syncthreads();
+    }
+    // dictionary string lengths -> char offsets within the window
+    long long my_len = 0;
+    uint32_t ix[2] = {0, 0};
+    {
+      int v = ev;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        if (df[k] == ck.max_def && (is_dict || bool_rle_p)) {
+          ix[k] = seg_value(W.segi, W.ni, v, is_dict ? ibw : 1, L.d, L.val_e);
+          if (is_dict && (int32_t)ix[k] >= s_dict_n) { W.err = 1; ix[k] = 0; }
+          if (is_dict && is_str) my_len += (long long)(DP[ix[k] + 1] - DP[ix[k]] - 4);
+          v++;
+        }
+      }
+    }
+    long long ch_excl = 0, ch_tot = 0;
+    if (is_dict && is_str) ch_excl = block_scan64(my_len, &ch_tot, W.scan64);
+    // emit
+    {
+      int r_i = rows_c + er, e_i = ents_c + ee, v_i = vals_c + ev;
+      long long c_i = chars_c + ch_excl;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        int i = t * 2 + k;
+        if (i >= win) break;
+        const int d = df[k];
+        const bool is_row = (rp[k] == 0);
+        const bool is_ent = d >= ck.rep_def;
+        const bool is_val = d == ck.max_def;
+        const long long grow = pg.row_base + r_i;           // row of this level (if row start)
+        if (is_row) {
+          col.row_def[grow] = (uint8_t)d;
+          if (rep) col.row_offs[grow] = pg.entry_base + e_i;
+        }
+        long long dest = -1;
+        if (rep) {
+          if (is_ent) { dest = pg.entry_base + e_i; col.entry_def[dest] = (uint8_t)d; }
+        } else {
+          dest = grow;
+        }
+        if (dest >= 0) {
+          const long long vloc = v_i;                       // values before this level (page-local)
+          if (is_str) {
+            long long cpos;
+            if (P) cpos = (long long)P[vloc] - 4ll * vloc;
+            else cpos = c_i;
+            col.offs[dest] = pg.char_base + cpos;
+            if (is_val && is_dict) {
+              const uint8_t* src = D + DP[ix[k]] + 4;
+              int len = DP[ix[k] + 1] - DP[ix[k]] - 4;
+              uint8_t* o = col.chars + pg.char_base + cpos;
+              for (int j = 0; j < len; j++) o[j] = src[j];
+            }
+          } else if (col.fixed) {
+            uint8_t* o = col.fixed + dest * w;
+            if (!is_val) {
+              if (w == 8) *(uint64_t*)o = 0; else if (w == 4) *(uint32_t*)o = 0; else for (int j = 0; j < w; j++) o[j] = 0;
+            } else if (ck.phys == PT_BOOLEAN) {
+              uint8_t b;
+              if (bool_rle_p) b = (uint8_t)ix[k];
+              else b = (L.val_p[vloc >> 3] >> (vloc & 7)) & 1;
+              *o = b;
+            } else {
+              const uint8_t* src = is_dict ? D + (int64_t)ix[k] * w : L.val_p + vloc * w;
+              if (w == 8) {
+                uint64_t x = (uint64_t)ld_u32(src) | ((uint64_t)ld_u32(src + 4) << 32);
+                *(uint64_t*)o = x;
+              } else if (w == 4) {
+                *(uint32_t*)o = ld_u32(src);
+              } else {
+                for (int j = 0; j < w; j++) o[j] = src[j];
+              }
+            }
+          }
+        }
+        r_i += is_row; e_i += is_ent;
+        if (is_val) { if (is_dict && is_str) c_i += (long long)(DP[ix[k] + 1] - DP[ix[k]] - 4); v_i++; }
+      }
+    }
+    rows_c += tr; ents_c += te; vals_c += tv; chars_c += ch_tot;
+    w0 += win;
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// K6: PLAIN string bytes -> contiguous output chars (16-byte aligned global stores)
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k_string_copy(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+                                                    const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
+                                                    const int32_t* __restrict__ pos) {
+  const DPage& pg = pages[blockIdx.x];
+  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
+  const DChunk& ck = chunks[pg.chunk];
+  if (ck.phys != PT_BYTE_ARRAY || pg.enc != ENC_PLAIN || pg.n_chars == 0) return;
+  const DColumn& col = cols[ck.col];
+  Layout L = page_layout(pg, ck, arena);
+  const uint8_t* r = L.val_p;
+  const int32_t* P = pos + pg.pos_base;
+  const int n = pg.n_values;
+  uint8_t* ob = col.chars + pg.char_base;
+  const long long nc = pg.n_chars;
+  const uintptr_t a_lo = (uintptr_t)ob & ~(uintptr_t)15;
+  const uintptr_t a_hi = (uintptr_t)ob + nc;
+  for (uintptr_t a = a_lo + (uintptr_t)threadIdx.x * 16; a < a_hi; a += (uintptr_t)NT * 16) {
+    const uintptr_t lo = a < (uintptr_t)ob ? (uintptr_t)ob : a;
+    const uintptr_t hi = (a + 16 < a_hi) ? a + 16 : a_hi;
+    long long o = (long long)(lo - (uintptr_t)ob);
+    // largest v with charpos(v) <= o
+    int vlo = 0, vhi = n - 1;
+    while (vlo < vhi) {
+      int mid = (vlo + vhi + 1) >> 1;
+      if ((long long)P[mid] - 4ll * mid <= o) vlo = mid; else vhi = mid - 1;
+    }
+    int v = vlo;
+    long long cp = (long long)P[v] - 4ll * v;
+    long long cn = (long long)P[v + 1] - 4ll * (v + 1);
+    uint8_t buf[16];
+    int nb = 0;
+    for (uintptr_t x = lo; x < hi; x++, o++) {
+      while (o >= cn) { v++; cp = cn; cn = (long long)P[v + 1] - 4ll * (v + 1); }
+      buf[nb++] = r[(long long)P[v] + 4 + (o - cp)];
+    }
+    if (lo == a && hi == a + 16) {
+      uint4 q;
+      q.x = buf[0] | (buf[1] << 8) | (buf[2] << 16) | ((uint32_t)buf[3] << 24);
+      q.y = buf[4] | (buf[5] << 8) | (buf[6] << 16) | ((uint32_t)buf[7] << 24);
+      q.z = buf[8] | (buf[9] << 8) | (buf[10] << 16) | ((uint32_t)buf[11] << 24);
+      q.w = buf[12] | (buf[13] << 8) | (buf[14] << 16) | ((uint32_t)buf[15] << 24);
+      *(uint4*)a = q;
+    } else {
+      for (int j = 0; j < nb; j++) ((uint8_t*)lo)[j] = buf[j];
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Commit tail: canonical keys, probe-table build, JSON selection
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ void set_err(DState* st, int flag, long long row, int part) {
+  atomicOr(&st->err_flags, flag);
+  atomicMin((unsigned long long*)&st->err_row, (unsigned long long)row);
+  (void)part;
+}
+
+template <class Sink>
+__device__ __forceinline__ void feed(Sink& k, const uint8_t* p, int32_t n) { for (int32_t i = 0; i < n; i++) k.put(p[i]); }
+
+__device__ __forceinline__ uint64_t bytes_hash(const uint8_t* p, int32_t n, uint32_t seed) {
+  HashSink k; k.hs.init(kHashSeed(seed)); k.n = 0;
+  feed(k, p, n);
+  return k.hs.final_(k.n);
+}
+
+__global__ void k_json_canon(DJsonAction* __restrict__ acts, int n, const uint8_t* __restrict__ jchars,
+                             uint8_t* __restrict__ canon, uint32_t seed, DState* __restrict__ st) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DJsonAction a = acts[i];
+  if (a.kind == JA_NONE) return;
+  uint8_t* out = canon + a.canon_off;
+  WriteSink w{out, 0, (int64_t)a.path_len + 64};
+  int rc = uri_emit(jchars + a.path_off, a.path_len, w);
+  if (rc) { acts[i].status = rc; atomicOr(&st->err_flags, rc == -1 ? E_URI : E_UTF8); return; }
+  int32_t pl = (int32_t)w.n;
+  WriteSink w2{out + pl, 0, (int64_t)a.st_len + a.pid_len + 32};
+  rc = dv_emit(a.has_dv != 0, jchars + a.st_off, a.st_len, jchars + a.pid_off, a.pid_len, a.has_off != 0, a.dv_off, w2);
+  if (rc) { acts[i].status = rc; atomicOr(&st->err_flags, E_UTF8); return; }
+  uint64_t hp = bytes_hash(out, pl, seed);
+  uint64_t hd = bytes_hash(out + pl, (int32_t)w2.n, seed);
+  acts[i].canon_len = pl;
+  acts[i].dv_len = (int32_t)w2.n;
+  acts[i].h = hash_combine(hp, hd);
+  acts[i].status = 0;
+}
+
+__global__ void k_slots_init(Slot* __restrict__ slots, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Slot s;
+  s.h = 0ull; s.first_add = ~0ull; s.rep = 0; s.min_rm_step = 0x7fffffff;
+  slots[i] = s;
+}
+
+__global__ void k_table_insert(const DJsonAction* __restrict__ acts, int n, Slot* __restrict__ slots, uint64_t mask) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const DJsonAction& a = acts[i];
+  if (a.kind == JA_NONE || a.status) return;
+  unsigned long long h = a.h;
+  uint64_t s = h & mask;
+  for (;;) {
+    unsigned long long old = atomicCAS(&slots[s].h, 0ull, h);
+    if (old == 0ull) { slots[s].rep = i; break; }
+    if (old == h) break;
+    s = (s + 1) & mask;
+  }
+}
+
+__device__ __forceinline__ bool canon_equal(const DJsonAction& a, const DJsonAction& b, const uint8_t* canon) {
+  if (a.canon_len != b.canon_len || a.dv_len != b.dv_len) return false;
+  const uint8_t* x = canon + a.canon_off;
+  const uint8_t* y = canon + b.canon_off;
+  int32_t n = a.canon_len + a.dv_len;
+  for (int32_t k = 0; k < n; k++) if (x[k] != y[k]) return false;
+  return true;
+}
+
+__global__ void k_table_update(DJsonAction* __restrict__ acts, int n, Slot* __restrict__ slots, uint64_t mask,
+                               const uint8_t* __restrict__ canon, DState* __restrict__ st) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DJsonAction a = acts[i];
+  if (a.kind == JA_NONE || a.status) return;
+  uint64_t s = a.h & mask;
+  while (slots[s].h != a.h) s = (s + 1) & mask;
+  const DJsonAction& rp = acts[slots[s].rep];
+  if (!canon_equal(a, rp, canon)) { atomicOr(&st->err_flags, E_COLLISION); return; }
+  acts[i].slot = (int32_t)s;
+  if (a.kind == JA_ADD) atomicMin(&slots[s].first_add, ((unsigned long long)a.step << 32) | (unsigned)a.row);
+  else atomicMin(&slots[s].min_rm_step, a.step);
+}
+
+__device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
+  unsigned long long m = __ballot(pred);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(ctr, (unsigned long long)__popcll(m));
+}
+
+__global__ void k_json_select(const DJsonAction* __restrict__ acts, int n, const Slot* __restrict__ slots,
+                              uint8_t* __restrict__ sel, DState* __restrict__ st) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool is_add = false, is_rm = false, chosen = false, dup = false;
+  if (i < n) {
+    const DJsonAction a = acts[i];
+    is_add = a.kind == JA_ADD;
+    is_rm = a.kind == JA_REMOVE;
+    if (is_add && a.status == 0) {
+      const Slot s = slots[a.slot];
+      unsigned long long mypos = ((unsigned long long)a.step << 32) | (unsigned)a.row;
+      dup = s.first_add != mypos;                 // alreadyReturned (ActiveAddFilesIterator :210,227)
+      chosen = !dup && s.min_rm_step > a.step;    // not tombstoned by this or a newer batch (R2/R5)
+    }
+    sel[i] = chosen;
+  }
+  wave_count(&st->counters[0], is_add);
+  wave_count(&st->counters[1], is_add);
+  wave_count(&st->counters[2], chosen);
+  wave_count(&st->counters[3], dup);
+  wave_count(&st->counters[4], is_rm);
+}
+
+// --------------------------------------------------------------------------------------------
+// K7: checkpoint probe — one lane per checkpoint row
+// --------------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
+                                              const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
+                                              uint32_t seed, uint8_t* __restrict__ sel, DState* __restrict__ st) {
+  long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  bool seen = false, chosen = false, dup = false;
+  if (r < pc.n_rows) {
+    if (pc.path_def[r] >= 1) {
+      seen = true;
+      const uint8_t* p = pc.path_chars + pc.path_offs[r];
+      int32_t pl = (int32_t)(pc.path_offs[r + 1] - pc.path_offs[r]);
+      bool has_dv = pc.has_dv && pc.st_def[r] >= 2;
+      const uint8_t* sp = nullptr; const uint8_t* pp = nullptr;
+      int32_t sl = 0, ppl = 0, off = 0;
+      bool has_off = false;
+      if (has_dv) {
+        sp = pc.st_chars + pc.st_offs[r]; sl = (int32_t)(pc.st_offs[r + 1] - pc.st_offs[r]);
+        pp = pc.pid_chars + pc.pid_offs[r]; ppl = (int32_t)(pc.pid_offs[r + 1] - pc.pid_offs[r]);
+        has_off = pc.off_def != nullptr && pc.off_def[r] == pc.off_maxdef;
+        off = has_off ? pc.off_vals[r] : 0;
+      }
+      uint64_t hp;
+      int rc = path_hash(p, pl, seed, &hp);
+      HashSink kd; kd.hs.init(kHashSeed(seed)); kd.n = 0;
+      int rc2 = dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, kd);
+      if (rc || rc2) {
+        set_err(st, (rc == -1) ? E_URI : E_UTF8, pc.row_tag + r, 0);
+      } else {
+        uint64_t h = hash_combine(hp, kd.hs.final_(kd.n));
+        uint64_t s = h & mask;
+        int found = 0;
+        Slot sl_;
+        while (slots[s].h != 0ull) {
+          if (slots[s].h == h) {
+            sl_ = slots[s];
+            const DJsonAction& a = acts[sl_.rep];
+            CmpSink cmp{canon + a.canon_off, a.canon_len, 0, 1};
+            uri_emit(p, pl, cmp);
+            bool eq = cmp.eq && cmp.n == a.canon_len;
+            if (eq) {
+              CmpSink c2{canon + a.canon_off + a.canon_len, a.dv_len, 0, 1};
+              dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, c2);
+              eq = c2.eq && c2.n == a.dv_len;
+            }
+            if (eq) { found = 1; break; }
+          }
+          s = (s + 1) & mask;
+        }
+        if (found) {
+          dup = sl_.first_add != ~0ull;            // alreadyReturned -> duplicate
+        } else {
+          chosen = true;
+        }
+      }
+    }
+    sel[r] = chosen;
+  }
+  wave_count(&st->counters[0], seen);
+  wave_count(&st->counters[2], chosen);
+  wave_count(&st->counters[3], dup);
+}
+
+}  // namespace dk
+
+// ------------------------------------------------------------------------------------------------
+// launch wrappers (C++ linkage, used by dk_host.cpp)
+// ------------------------------------------------------------------------------------------------
+namespace dk {
+
+void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
+}
+void launch_string_positions(const DChunk* c, DPage* p, int n, const uint8_t* arena, int32_t* pos, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos);
+}
+void launch_page_count(const DChunk* c, DPage* p, int n, const uint8_t* arena, const int32_t* pos, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_page_count, dim3(n), dim3(NT), 0, s, c, p, arena, pos);
+}
+void launch_column_scan(DColumn* cols, int ncols, DPage* p, DState* st, hipStream_t s) {
+  if (ncols) hipLaunchKernelGGL(k_column_scan, dim3(ncols), dim3(NT), 0, s, cols, p, st);
+}
+void launch_page_decode(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
+                        const int32_t* pos, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_page_decode, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos);
+}
+void launch_string_copy(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
+                        const int32_t* pos, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_string_copy, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos);
+}
+void launch_json_canon(DJsonAction* a, int n, const uint8_t* jchars, uint8_t* canon, uint32_t seed, DState* st,
+                       hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_json_canon, dim3((n + 255) / 256), dim3(256), 0, s, a, n, jchars, canon, seed, st);
+}
+void launch_slots_init(Slot* slots, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_slots_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, n);
+}
+void launch_table_insert(const DJsonAction* a, int n, Slot* slots, uint64_t mask, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_table_insert, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, mask);
+}
+void launch_table_update(DJsonAction* a, int n, Slot* slots, uint64_t mask, const uint8_t* canon, DState* st,
+                         hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_table_update, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, mask, canon, st);
+}
+void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint8_t* sel, DState* st, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, sel, st);
+}
+void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const DJsonAction* acts,
+                  const uint8_t* canon, uint32_t seed, uint8_t* sel, DState* st, hipStream_t s) {
+  if (pc.n_rows)
+    hipLaunchKernelGGL(k_probe, dim3((unsigned)((pc.n_rows + NT - 1) / NT)), dim3(NT), 0, s, pc, slots, mask, acts,
+                       canon, seed, sel, st);
+}
+
+}  // namespace dk

@@ -1,0 +1,448 @@
+"""Python mirror of the Delta Kernel read surface over libdkgpu (the role JNI plays for Java).
+
+Reference surface (paths under /root/reference/kernel/kernel-api/src/main/java/io/delta/kernel/):
+  Table.forPath / getLatestSnapshot          Table.java:56-58,76; internal/TableImpl.java:65-103
+  SnapshotManager.getLogSegmentForVersion    internal/snapshot/SnapshotManager.java:311-566
+  LogSegment.allLogFilesReversed             internal/snapshot/LogSegment.java:166-178
+  Snapshot.getScanBuilder / ScanBuilder.build   Snapshot.java:69; internal/ScanBuilderImpl.java:77-86
+  Scan.getScanFiles -> FilteredColumnarBatch Scan.java:101; internal/ScanImpl.java:120-186
+  ScanMetrics counters                       internal/metrics/ScanMetrics.java:28-40
+
+Log-segment selection is Kernel host logic the GPU engine does not replace; it is
+restated here because the JVM is absent. Decode, key building and reconciliation all run in
+libdkgpu on the GPU; nothing here computes a selection.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import re
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._lib import Column, DkError, check, dk_column, dk_config, lib
+
+ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
+              "add.size", "add.modificationTime", "add.dataChange",
+              "add.deletionVector.storageType", "add.deletionVector.pathOrInlineDv",
+              "add.deletionVector.offset", "add.deletionVector.sizeInBytes",
+              "add.deletionVector.cardinality", "add.tags.key_value.key", "add.tags.key_value.value",
+              "add.baseRowId", "add.defaultRowCommitVersion"]
+STATS_LEAF = "add.stats"
+REMOVE_LEAVES = ["remove.path", "remove.deletionVector.storageType", "remove.deletionVector.pathOrInlineDv",
+                 "remove.deletionVector.offset", "remove.deletionVector.sizeInBytes",
+                 "remove.deletionVector.cardinality"]
+PM_LEAVES = ["protocol.minReaderVersion", "protocol.minWriterVersion",
+             "protocol.readerFeatures.list.element", "protocol.writerFeatures.list.element",
+             "metaData.id", "metaData.schemaString", "metaData.partitionColumns.list.element",
+             "metaData.configuration.key_value.key", "metaData.configuration.key_value.value",
+             "metaData.format.provider", "metaData.createdTime"]
+SIDECAR_LEAVES = ["sidecar.path", "sidecar.sizeInBytes", "sidecar.modificationTime"]
+
+TIMING = 1
+
+
+def _cstrs(items):
+    arr = (C.c_char_p * len(items))()
+    arr[:] = [s.encode() if isinstance(s, str) else s for s in items]
+    return arr
+
+
+class GpuEngine:
+    """Engine (engine/Engine.java:30-64) backed by one MI355X."""
+
+    def __init__(self, parquet_batch_size=1024, json_batch_size=1024, device=0, timing=False):
+        self.cfg = dk_config(parquet_batch_size, json_batch_size, device, TIMING if timing else 0)
+        self._h = C.c_void_p()
+        check(lib().dk_engine_create(C.byref(self.cfg), C.byref(self._h)))
+
+    create = classmethod(lambda cls, **kw: cls(**kw))
+
+    @property
+    def json_batch_size(self):
+        return self.cfg.json_batch_size
+
+    def close(self):
+        if self._h:
+            lib().dk_engine_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ParquetHandler.readParquetFiles (engine/ParquetHandler.java:64-68)
+    def read_parquet_files(self, paths, leaves):
+        return ParquetSet(self, paths, leaves)
+
+
+class ParquetSet:
+    """A set of Parquet files decoded on the GPU (one batch per file; batches in input order)."""
+
+    def __init__(self, engine: GpuEngine, paths, leaves):
+        self.engine = engine
+        self.paths = list(paths)
+        self.leaves = list(leaves)
+        self._h = C.c_void_p()
+        check(lib().dk_parquet_open(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
+                                    len(self.leaves), C.byref(self._h)))
+
+    def decode(self):
+        check(lib().dk_parquet_decode(self._h))
+        check(lib().dk_parquet_sync(self._h))
+        return self
+
+    def num_rows(self, file_idx):
+        return lib().dk_parquet_num_rows(self._h, file_idx)
+
+    def column(self, file_idx, leaf) -> Column:
+        c = dk_column()
+        check(lib().dk_parquet_column(self._h, file_idx, self.leaves.index(leaf), C.byref(c)))
+        return Column(c, leaf)
+
+    def columns(self, file_idx):
+        return {leaf: self.column(file_idx, leaf) for leaf in self.leaves}
+
+    def traffic(self):
+        r, w = C.c_int64(), C.c_int64()
+        check(lib().dk_parquet_traffic(self._h, C.byref(r), C.byref(w)))
+        return r.value, w.value
+
+    def close(self):
+        if self._h:
+            lib().dk_parquet_close(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class JsonTail:
+    """Commit files parsed on the host (DefaultJsonHandler.readJsonFiles semantics)."""
+
+    def __init__(self, engine: GpuEngine, commit_paths, versions, with_stats=False):
+        self._h = C.c_void_p()
+        vers = (C.c_int64 * max(1, len(versions)))(*versions)
+        check(lib().dk_json_tail_parse(engine._h, _cstrs(commit_paths), vers, len(commit_paths),
+                                       1 if with_stats else 0, C.byref(self._h)))
+        self.rows = lib().dk_json_tail_rows(self._h)
+
+    def column(self, leaf) -> Column:
+        c = dk_column()
+        check(lib().dk_json_tail_column(self._h, leaf.encode(), C.byref(c)))
+        return Column(c, leaf)
+
+    def close(self):
+        if self._h:
+            lib().dk_json_tail_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------------------------------
+# Log segment (SnapshotManager / Checkpointer / LogSegment)
+# ------------------------------------------------------------------------------------------------
+_DELTA = re.compile(r"^(\d{20})\.json$")
+_CLASSIC = re.compile(r"^(\d{20})\.checkpoint\.parquet$")
+_MULTI = re.compile(r"^(\d{20})\.checkpoint\.(\d{10})\.(\d{10})\.parquet$")
+_V2 = re.compile(r"^(\d{20})\.checkpoint\.([^.]+)\.(json|parquet)$")
+
+
+@dataclass
+class LogFile:
+    path: str
+    kind: str
+    version: int
+    part: int = 0
+    num_parts: int = 0
+
+
+@dataclass
+class LogSegment:
+    log_path: str
+    version: int
+    deltas: list
+    checkpoints: list
+
+    def all_files_reversed(self):
+        return sorted(self.deltas + self.checkpoints, key=lambda f: os.path.basename(f.path), reverse=True)
+
+
+def _classify(log, name):
+    full = os.path.join(log, name)
+    for rx, kind in ((_DELTA, "commit"), (_CLASSIC, "classic"), (_MULTI, "multipart"), (_V2, "v2")):
+        m = rx.match(name)
+        if m:
+            if kind == "multipart":
+                return LogFile(full, kind, int(m.group(1)), int(m.group(2)), int(m.group(3)))
+            return LogFile(full, kind, int(m.group(1)))
+    return None
+
+
+def build_log_segment(table_root: str) -> LogSegment:
+    log = os.path.join(table_root, "_delta_log")
+    if not os.path.isdir(log):
+        raise DkError("Table at path `%s` is not found" % table_root)
+    start = -1
+    lc = os.path.join(log, "_last_checkpoint")
+    if os.path.exists(lc):
+        try:
+            with open(lc) as f:
+                start = int(json.loads(f.readline())["version"])
+        except Exception:
+            start = -1          # corrupt hint: list everything (Checkpointer.readLastCheckpointFile)
+    files = [f for f in (_classify(log, n) for n in os.listdir(log)) if f and f.version >= max(start, 0)]
+    if not files and start >= 0:
+        files = [f for f in (_classify(log, n) for n in os.listdir(log)) if f]
+    groups = {}
+    for f in files:
+        if f.kind != "commit":
+            groups.setdefault((f.version, f.kind, f.num_parts), []).append(f)
+    complete = []
+    for (v, kind, nparts), fs in groups.items():
+        if kind == "multipart":
+            if sorted(x.part for x in fs) == list(range(1, nparts + 1)):
+                complete.append((v, kind, sorted(fs, key=lambda x: x.part)))
+        else:
+            complete.append((v, kind, fs[:1]))
+    deltas = sorted([f for f in files if f.kind == "commit"], key=lambda f: f.version)
+    if not deltas and not complete:
+        raise DkError("No delta files found in the directory: " + log)
+    rank = {"classic": 0, "multipart": 1, "v2": 2}
+    ck = max(complete, key=lambda c: (c[0], rank[c[1]], len(c[2])), default=None)
+    ckv = ck[0] if ck else -1
+    tail = [d for d in deltas if d.version > ckv]
+    for i, d in enumerate(tail):
+        if d.version != ckv + 1 + i:
+            raise DkError("Versions are not contiguous")
+    if ck is None and (not tail or tail[0].version != 0):
+        raise DkError("Cannot compute snapshot. Missing delta file version 0.")
+    return LogSegment(log, tail[-1].version if tail else ckv, tail, list(ck[2]) if ck else [])
+
+
+# ------------------------------------------------------------------------------------------------
+# Table / Snapshot / Scan
+# ------------------------------------------------------------------------------------------------
+class Table:
+    def __init__(self, path):
+        self.path = os.path.abspath(path)
+
+    @staticmethod
+    def forPath(engine, path):
+        return Table(path)
+
+    def getLatestSnapshot(self, engine):
+        seg = build_log_segment(self.path)
+        snap = Snapshot(self, seg)
+        snap._load_protocol_metadata(engine)
+        return snap
+
+
+@dataclass
+class ScanMetrics:
+    addFilesSeen: int = 0
+    addFilesSeenFromDeltaFiles: int = 0
+    activeAddFiles: int = 0
+    duplicateAddFiles: int = 0
+    removeFilesSeenFromDeltaFiles: int = 0
+
+    def as_tuple(self):
+        return (self.addFilesSeen, self.addFilesSeenFromDeltaFiles, self.activeAddFiles,
+                self.duplicateAddFiles, self.removeFilesSeenFromDeltaFiles)
+
+
+class Snapshot:
+    def __init__(self, table, seg):
+        self.table = table
+        self.log_segment = seg
+        self.protocol = None
+        self.metadata = None
+
+    def getVersion(self):
+        return self.log_segment.version
+
+    def getScanBuilder(self):
+        return ScanBuilder(self)
+
+    def _checkpoint_files(self, engine):
+        """Checkpoint data files in replay order: multi-part parts descending (LogSegment
+        ordering); V2 parquet manifest first, then its sidecars in manifest order."""
+        cks = self.log_segment.checkpoints
+        if not cks:
+            return []
+        if cks[0].kind == "v2":
+            man = cks[0].path
+            if man.endswith(".json"):
+                raise DkError("V2 checkpoint with a JSON manifest is not supported by this engine build")
+            ps = ParquetSet(engine, [man], SIDECAR_LEAVES).decode()
+            sp = ps.column(0, "sidecar.path")
+            side = []
+            if sp.present:
+                for r in range(sp.n_rows):
+                    if sp.row_def[r] >= sp.max_def:
+                        side.append(os.path.join(self.log_segment.log_path, "_sidecars", sp.string(r).decode()))
+            ps.close()
+            return [man] + side
+        return [f.path for f in sorted(cks, key=lambda f: os.path.basename(f.path), reverse=True)]
+
+    def _load_protocol_metadata(self, engine):
+        """LogReplay.loadTableProtocolAndMetadata (internal/replay/LogReplay.java:220-314): newest
+        commit first, then the checkpoint (decoded on the GPU)."""
+        for d in reversed(self.log_segment.deltas):
+            with open(d.path, "rb") as f:
+                for line in f.read().decode("utf-8", "replace").splitlines():
+                    obj = json.loads(line)
+                    if self.protocol is None and obj.get("protocol") is not None:
+                        self.protocol = obj["protocol"]
+                    if self.metadata is None and obj.get("metaData") is not None:
+                        self.metadata = obj["metaData"]
+            if self.protocol is not None and self.metadata is not None:
+                return
+        files = self._checkpoint_files(engine) if self.log_segment.checkpoints else []
+        if files and (self.protocol is None or self.metadata is None):
+            ps = ParquetSet(engine, files, PM_LEAVES).decode()
+            for fi in range(len(files)):
+                cols = ps.columns(fi)
+                rv = cols["protocol.minReaderVersion"]
+                if self.protocol is None and rv.present:
+                    idx = np.nonzero(rv.row_def >= 1)[0]
+                    if len(idx):
+                        r = int(idx[0])
+                        wv = cols["protocol.minWriterVersion"]
+                        self.protocol = {"minReaderVersion": int(rv.fixed.view(np.int32)[r]),
+                                         "minWriterVersion": int(wv.fixed.view(np.int32)[r])}
+                mid = cols["metaData.id"]
+                if self.metadata is None and mid.present:
+                    idx = np.nonzero(mid.row_def >= 1)[0]
+                    if len(idx):
+                        r = int(idx[0])
+                        ss = cols["metaData.schemaString"]
+                        self.metadata = {"id": mid.string(r).decode() if mid.row_def[r] >= 2 else None,
+                                         "schemaString": ss.string(r).decode() if ss.row_def[r] >= 2 else None}
+            ps.close()
+        if self.protocol is None:
+            raise DkError("No protocol found at version %d" % self.getVersion())
+        if self.metadata is None:
+            raise DkError("No metadata found at version %d" % self.getVersion())
+
+
+class ScanBuilder:
+    def __init__(self, snapshot):
+        self.snapshot = snapshot
+        self.read_stats = False
+
+    def withStats(self, flag=True):
+        self.read_stats = flag
+        return self
+
+    def build(self):
+        return GpuScan(self.snapshot, self.read_stats)
+
+
+@dataclass
+class FilteredColumnarBatch:
+    """data: leaf -> Column (add.* leaves) plus the constant tableRoot; selection: bool per row or
+    None when every row is selected (KA/data/FilteredColumnarBatch.java:37-111)."""
+    data: dict
+    table_root: str
+    size: int
+    selection: np.ndarray | None
+    source: str = ""
+
+    def selected_rows(self):
+        if self.selection is None:
+            return np.arange(self.size)
+        return np.nonzero(self.selection)[0]
+
+
+class GpuScan:
+    """Scan whose getScanFiles runs decode + reconciliation in libdkgpu (SURVEY.md §8(b) plugin
+    point 2)."""
+
+    def __init__(self, snapshot, read_stats=False):
+        self.snapshot = snapshot
+        self.read_stats = read_stats
+        self.metrics = ScanMetrics()
+        self.replay = None
+
+    def table_root(self):
+        # tableRoot = dataPath.toUri().toString() (ActiveAddFilesIterator.java:251)
+        p = self.snapshot.table.path
+        return "file:" + (p if p.endswith("/") else p + "/")
+
+    def prepare(self, engine):
+        """Host-side setup: parse the commit tail, open checkpoint files, upload to HBM."""
+        seg = self.snapshot.log_segment
+        commits = list(reversed(seg.deltas))
+        self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
+        self.ckpt_files = self.snapshot._checkpoint_files(engine)
+        leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
+        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves) if self.ckpt_files else None
+        self._rh = C.c_void_p()
+        check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
+                                     C.byref(self._rh)))
+        return self
+
+    def run(self):
+        """The device step: commit-tail keys + table, checkpoint decode, probe, selection."""
+        check(lib().dk_replay_run(self._rh))
+
+    def sync(self):
+        check(lib().dk_replay_sync(self._rh))
+        cnt = (C.c_int64 * 5)()
+        check(lib().dk_replay_counters(self._rh, cnt))
+        self.metrics = ScanMetrics(*[int(x) for x in cnt])
+
+    def kernel_stats(self):
+        out = {}
+        for i in range(16):
+            name, avg, cnt = C.c_char_p(), C.c_double(), C.c_int64()
+            if lib().dk_replay_kernel_stats(self._rh, i, C.byref(name), C.byref(avg), C.byref(cnt)) != 0:
+                continue
+            if cnt.value:
+                out[name.value.decode()] = (avg.value, cnt.value)
+        return out
+
+    def getScanFiles(self, engine):
+        if self.replay is None:
+            self.prepare(engine)
+            self.replay = True
+        self.run()
+        self.sync()
+        return self._batches()
+
+    def _batches(self):
+        root = self.table_root()
+        leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else [])
+        if self.tail.rows:
+            sel = np.zeros(self.tail.rows, dtype=np.uint8)
+            check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
+            cols = {leaf: self.tail.column(leaf) for leaf in leaves}
+            yield FilteredColumnarBatch(cols, root, int(self.tail.rows), sel.astype(bool), "json-tail")
+        for fi, path in enumerate(self.ckpt_files or []):
+            n = self.ckpt.num_rows(fi)
+            sel = np.zeros(n, dtype=np.uint8)
+            check(lib().dk_replay_ckpt_selection(self._rh, fi, sel.ctypes.data, n))
+            cols = {leaf: self.ckpt.column(fi, leaf) for leaf in leaves}
+            yield FilteredColumnarBatch(cols, root, int(n), sel.astype(bool), path)
+
+    def close(self):
+        if getattr(self, "_rh", None):
+            lib().dk_replay_free(self._rh)
+            self._rh = None
+        for o in ("ckpt", "tail"):
+            x = getattr(self, o, None)
+            if x is not None:
+                x.close()

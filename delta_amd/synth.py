@@ -267,17 +267,27 @@ def _add_struct(rng, n, start_index, spec: TableSpec, data_change: bool, paths=N
         idmin = rng.integers(0, 50_000_000, size=n)
         idmax = idmin + rng.integers(0, 1_000_000, size=n)
         nrec = rng.integers(1, 100_000, size=n)
-        names_min = ["n%06d" % x for x in rng.integers(0, 500_000, size=n)] if n < 2_000_000 else None
+        nmat = np.empty((n, 7), dtype=np.uint8)
+        nmat[:, 0] = ord("n")
+        nmat[:, 1:] = _digits(rng.integers(0, 500_000, size=n), 6)
     if spec.with_stats:
-        if names_min is None:
-            names_min = ["n%06d" % x for x in rng.integers(0, 500_000, size=n)]
-        stats = pa.array(_stats_json(idmin, idmax, names_min, names_min, nrec), type=STR)
+        # {"numRecords":N,"minValues":{"id":A,"name":"nXXXXXX"},"maxValues":{...},"nullCount":{...}}
+        parts = [b'{"numRecords":', None, b',"minValues":{"id":', None, b',"name":"', nmat,
+                 b'"},"maxValues":{"id":', None, b',"name":"', nmat, b'"},"nullCount":{"id":0,"name":0}}']
+        nums = {1: nrec, 3: idmin, 7: idmax}
+        cols = []
+        for i, p in enumerate(parts):
+            if isinstance(p, bytes):
+                cols.append(np.tile(np.frombuffer(p, dtype=np.uint8), (n, 1)))
+            elif p is None:
+                cols.append(_digits(nums[i], 8))
+            else:
+                cols.append(p)
+        stats = _strings_from_matrix(np.concatenate(cols, axis=1))
         arrays.append(stats)
         fields.append(("stats", STR))
     if spec.with_stats_parsed:
-        if names_min is None:
-            names_min = ["n%06d" % x for x in rng.integers(0, 500_000, size=n)]
-        nm = pa.array(names_min, type=STR)
+        nm = _strings_from_matrix(nmat)
         sp = pa.StructArray.from_arrays([
             pa.array(nrec.astype(np.int64)),
             pa.StructArray.from_arrays([pa.array(idmin.astype(np.int64)), nm], names=["id", "name"]),

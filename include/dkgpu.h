@@ -1,0 +1,111 @@
+/*
+ * libdkgpu — MI355X-native Delta Kernel snapshot state reconstruction (C ABI).
+ *
+ * This is the drop-in boundary a Kernel Engine binds through JNI/FFM. Every
+ * entry point is plain C: pointers, sizes, status codes. Status 0 = OK; non-zero = error, with
+ * the message from dk_last_error() (the Java side rethrows it as KernelEngineException, as
+ * DeltaErrors.wrapEngineException would: kernel-api/.../internal/DeltaErrors.java:315-345).
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/kernel/):
+ *   dk_engine_*          Engine / DefaultEngine.create
+ *                        (kernel-api/src/main/java/io/delta/kernel/engine/Engine.java:30-64,
+ *                         kernel-defaults/.../defaults/engine/DefaultEngine.java:62-64)
+ *   dk_parquet_*         ParquetHandler.readParquetFiles
+ *                        (kernel-api/.../engine/ParquetHandler.java:64-68;
+ *                         kernel-defaults/.../engine/DefaultParquetHandler.java:55-94)
+ *   dk_json_tail_*       JsonHandler.readJsonFiles over the commit tail
+ *                        (kernel-api/.../engine/JsonHandler.java:87-91;
+ *                         kernel-defaults/.../engine/DefaultJsonHandler.java:79-157)
+ *   dk_replay_*          the active-AddFile log replay behind Scan.getScanFiles
+ *                        (kernel-api/.../Scan.java:101; internal/replay/LogReplay.java:194-206,
+ *                         internal/replay/ActiveAddFilesIterator.java:146-275) and its
+ *                         ScanMetrics counters (internal/metrics/ScanMetrics.java:28-40)
+ */
+#ifndef DKGPU_H
+#define DKGPU_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dk_engine dk_engine;
+typedef struct dk_parquet dk_parquet;
+typedef struct dk_json_tail dk_json_tail;
+typedef struct dk_replay dk_replay;
+
+typedef struct dk_config {
+  int32_t parquet_batch_size;  /* delta.kernel.default.parquet.reader.batch-size (default 1024) */
+  int32_t json_batch_size;     /* delta.kernel.default.json.reader.batch-size (default 1024)    */
+  int32_t device;              /* HIP device ordinal                                           */
+  int32_t flags;               /* DK_FLAG_*                                                    */
+} dk_config;
+
+#define DK_FLAG_TIMING 1       /* record per-kernel HIP events on the engine stream */
+
+/* Assembled column, the layout both the device decoder and the CPU oracle produce.
+ *  non-repeated leaf : row_def[n_rows] (definition level per row); fixed[n_rows*width] (0 where
+ *                      null) or offs[n_rows+1] + chars (zero-length where null)
+ *  repeated leaf     : row_def[n_rows] (def of the row's first level: null vs empty map/list),
+ *                      row_offs[n_rows+1] entry offsets; entry_def[n_entries]; values entry-dense
+ *  present == 0      : the leaf is missing from the file -> every row null
+ *                      (ParquetColumnReaders.NonExistentColumnReader, :119-134) */
+typedef struct dk_column {
+  int64_t n_rows, n_entries, n_chars;
+  int32_t phys, width, max_def, max_rep, rep_def, present;
+  const uint8_t* row_def;
+  const int64_t* row_offs;
+  const uint8_t* entry_def;
+  const uint8_t* fixed;
+  const int64_t* offs;
+  const uint8_t* chars;
+} dk_column;
+
+const char* dk_last_error(void);
+const char* dk_version(void);
+
+int  dk_engine_create(const dk_config* cfg, dk_engine** out);
+void dk_engine_destroy(dk_engine* e);
+
+/* ---- ParquetHandler: open files (host read + footer/offset-index parse + H2D), decode on GPU --
+ * leaves: dotted projected leaf paths ("add.path", "add.partitionValues.key_value.key", ...);
+ * matched by exact name, then case-insensitively (ParquetSchemaUtils.java:92-119). */
+int  dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
+                     const char* const* leaves, int32_t n_leaves, dk_parquet** out);
+int  dk_parquet_decode(dk_parquet* p);                 /* async on the engine stream */
+int  dk_parquet_sync(dk_parquet* p);
+int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file);
+/* D2H copy of one decoded column into library-owned host memory (valid until close). */
+int  dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out);
+/* bytes read (projected column chunks) and written (decoded buffers) per decode, for roofline */
+int  dk_parquet_traffic(dk_parquet* p, int64_t* bytes_read, int64_t* bytes_written);
+void dk_parquet_close(dk_parquet* p);
+
+/* ---- Commit tail (host JSON parse, newest commit first, batches of json_batch_size lines) ----
+ * One row per JSON line, in replay order, with the add/remove read schema. Columns are addressed
+ * by the same dotted leaf names as the checkpoint (add.*, remove.path, remove.deletionVector.*). */
+int  dk_json_tail_parse(dk_engine* e, const char* const* commit_paths, const int64_t* versions,
+                        int32_t n_files, int32_t with_stats, dk_json_tail** out);
+int64_t dk_json_tail_rows(dk_json_tail* t);
+int  dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out);
+void dk_json_tail_free(dk_json_tail* t);
+
+/* ---- Replay: reconcile the tail and the checkpoint files on the GPU ----
+ * ckpt may be NULL (no checkpoint). Checkpoint files are given in replay order (multi-part:
+ * descending part number, LogSegment.java:171-177). */
+int  dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_replay** out);
+int  dk_replay_run(dk_replay* r);                      /* async: key build, probe, decode */
+int  dk_replay_sync(dk_replay* r);
+/* counters: addFilesSeen, addFilesSeenFromDeltaFiles, activeAddFiles, duplicateAddFiles,
+ * removeFilesSeenFromDeltaFiles */
+int  dk_replay_counters(dk_replay* r, int64_t out[5]);
+int  dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n);
+int  dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out, int64_t n);
+/* per-kernel average device time (us) over recorded runs (DK_FLAG_TIMING); names via index */
+int  dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count);
+void dk_replay_free(dk_replay* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
