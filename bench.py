@@ -1,0 +1,195 @@
+"""Benchmark: checkpoint actions reconciled/sec on MI355X (BASELINE.json metric), config C2.
+
+One "step" = the device half of Scan.getScanFiles over one checkpoint already resident in HBM:
+commit-tail key build + probe table, checkpoint page-header parse, level/value decode of every
+projected add/remove leaf, URI-canonical key hashing of every add row, probe, selection and
+ScanMetrics counters (delta_amd.kernel.GpuScan.run + sync).
+
+Workload (configs[1]): 10M-AddFile single-part checkpoint with 2-key
+partitionValues maps and stats_parsed (read schema: add without stats + remove), plus a 100-commit
+JSON tail (50 adds + 50 removes each). Synthetic, seed 20250218.
+
+Multi-GPU (one process per GPU, torch.distributed over RCCL for the barrier/max only): each rank
+owns one checkpoint part of the same size (part i -> rank i) and replicates the commit tail; the
+path has no data exchange, so scaling is weak and no collective runs inside the timed region.
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_table(root, rows, seed, compression):
+    from delta_amd import synth
+    spec = synth.TableSpec(n_adds=rows, pv_keys=2, with_stats_parsed=True, n_commits=100,
+                           adds_per_commit=50, removes_per_commit=50, compression=compression, seed=seed)
+    return synth.write_table(root, spec)
+
+
+def cpu_baseline(rows, reps, seed, compression):
+    """Oracle (plain C restatement, single thread) on a bounded sample of the same workload."""
+    from oracle import ref
+    d = tempfile.mkdtemp(prefix="dk_cpu_")
+    try:
+        make_table(d, rows, seed + 99, compression)
+        seg = ref.load_log_segment(d)
+        path = seg.checkpoints[0].path
+        leaves = ref.ADD_LEAVES + ["remove.path", "remove.deletionVector.storageType",
+                                   "remove.deletionVector.pathOrInlineDv", "remove.deletionVector.offset",
+                                   "remove.deletionVector.sizeInBytes", "remove.deletionVector.cardinality"]
+        with open(path, "rb") as f:
+            data = f.read()
+        total_rows, t_total = 0, 0.0
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            pf = ref.ParquetFile(data)
+            cols = {leaf: pf.read(leaf) for leaf in leaves}
+            ks = ref.lib().dkr_keyset_new()
+            ref.probe_checkpoint(cols, pf.num_rows, ks, ref.Counters())
+            ref.lib().dkr_keyset_free(ks)
+            t_total += time.perf_counter() - t0
+            total_rows += pf.num_rows
+        return {"value": total_rows / t_total, "unit": "actions/s", "cores": 1, "kind": "port",
+                "sample": "%d x %d-row C2-shaped checkpoint, decode (21 leaves) + key + probe, oracle/dk_ref.c"
+                          % (reps, rows)}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--compression", default="none")
+    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workdir", default=None)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from delta_amd import kernel as K
+
+    work = args.workdir or tempfile.mkdtemp(prefix="dk_bench_r%d_" % rank)
+    t0 = time.time()
+    info = make_table(work, args.rows, 20250218 + rank, args.compression)
+    log("[rank %d] generated %d-row table in %.1fs" % (rank, info["checkpoint_rows"], time.time() - t0))
+
+    eng = K.GpuEngine(device=local if world > 1 else 0, timing=True)
+    t0 = time.perf_counter()
+    snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
+    snapshot_ms = (time.perf_counter() - t0) * 1e3
+    scan = snap.getScanBuilder().build()
+    t0 = time.perf_counter()
+    scan.prepare(eng)
+    prepare_s = time.perf_counter() - t0
+    n_ckpt_rows = sum(scan.ckpt.num_rows(i) for i in range(len(scan.ckpt_files)))
+    n_tail = int(scan.tail.rows)
+    bytes_read, bytes_written = scan.ckpt.traffic()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        scan.run()
+        scan.sync()
+    counters = scan.metrics.as_tuple()
+    # reset kernel timers: only the timed steps count
+    barrier()
+    stats0 = scan.kernel_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        scan.run()
+        scan.sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stats1 = scan.kernel_stats()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel averages over the timed steps only
+    kern = {}
+    for name, (avg1, c1) in stats1.items():
+        avg0, c0 = stats0.get(name, (0.0, 0))
+        if c1 > c0:
+            kern[name] = (avg1 * c1 - avg0 * c0) / (c1 - c0)
+    step_us = kern.pop("step_total", None)
+    units = (n_ckpt_rows + n_tail) * world
+    value = units * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    dom = max(kern.items(), key=lambda kv: kv[1]) if kern else ("none", 0.0)
+    step_bytes = bytes_read + bytes_written
+    achieved = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
+
+    result = {
+        "metric": "checkpoint actions reconciled/sec (node) + snapshot load ms, 100M AddFile",
+        "value": value,
+        "unit": "actions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/int64",
+        "data": "synthetic (seed 20250218; delta_amd/synth.py)",
+        "config": {"workload": "C2: %d-AddFile single-part checkpoint per GPU, 2-key partitionValues, "
+                               "stats_parsed present, 100-commit JSON tail; read schema add(no stats)+remove"
+                               % n_ckpt_rows,
+                   "compression": args.compression, "parallelism": "weak: one checkpoint part per GPU",
+                   "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail},
+        "snapshot_load_ms": snapshot_ms,
+        "prepare_s": prepare_s,
+        "counters": counters,
+        "kernels_us": {k: round(v, 2) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])},
+        "roofline": {"bound": "hbm", "kernel": "device step (all kernels, HIP events on the engine stream)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": None, "algorithmic_bytes": step_bytes,
+                     "bytes_read": bytes_read, "bytes_written": bytes_written,
+                     "step_device_us": step_us, "dominant_kernel": dom[0], "dominant_kernel_us": dom[1]},
+    }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        result["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.cpu_reps, 20250218, args.compression)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    scan.close()
+    eng.close()
+    if not args.workdir:
+        shutil.rmtree(work, ignore_errors=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

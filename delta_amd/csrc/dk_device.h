@@ -37,6 +37,7 @@ struct DPage {
 struct DColumn {
   int32_t first_page, n_pages;   // data pages, contiguous in the page table, in file order
   int32_t phys, width, max_def, max_rep, rep_def, present;
+  int32_t null_only, pad0;   // null_only: no value anywhere -> no value buffers are materialised
   int64_t n_rows;
   uint8_t* row_def;
   int64_t* row_offs;

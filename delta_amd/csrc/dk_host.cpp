@@ -19,10 +19,12 @@
 
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
-void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, hipStream_t);
+void launch_snappy(const DChunk*, DPage*, int, uint8_t*, hipStream_t);
+void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, int, hipStream_t);
 void launch_page_count(const DChunk*, DPage*, int, const uint8_t*, const int32_t*, hipStream_t);
 void launch_column_scan(DColumn*, int, DPage*, DState*, hipStream_t);
-void launch_page_decode(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, hipStream_t);
+void launch_page_decode(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const long long*, hipStream_t);
+void launch_delta_decode(const DChunk*, DPage*, int, const uint8_t*, long long*, hipStream_t);
 void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, hipStream_t);
 void launch_json_canon(DJsonAction*, int, const uint8_t*, uint8_t*, uint32_t, DState*, hipStream_t);
 void launch_slots_init(Slot*, uint64_t, hipStream_t);
@@ -291,7 +293,7 @@ struct KTimer {
   const char* names[K] = {"k_page_headers", "k_string_positions_dict", "k_page_count", "k_column_scan",
                           "k_string_positions", "k_page_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
-                          nullptr, nullptr, nullptr};
+                          "k_snappy", "k_delta_decode", nullptr};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -339,11 +341,12 @@ struct dk_parquet {
   std::vector<DPage> h_pages;
   std::vector<DColumn> h_cols;
   std::vector<int> col_file;
-  DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state;
+  DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp;
   std::vector<std::unique_ptr<DBuf>> outbufs;
   std::vector<HostCol> host;
   int n_pages = 0, n_cols = 0;
-  int64_t bytes_read = 0, bytes_written = 0;
+  bool has_compressed = false, has_dbp = false;
+  int64_t bytes_read = 0, bytes_written = 0, bytes_arena = 0;
   KTimer timer;
   bool prepared = false;
 };
@@ -379,12 +382,14 @@ static int run_pipeline(dk_parquet* p, int mode) {
   int n = p->n_pages;
   { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
   if (mode == -1) return 0;
-  { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, s); }  // dict pages (data pages exit: n_values unknown yet)
+  if (p->has_compressed) { KTimer::Scope sc(&T, 13, s); launch_snappy(C, P, n, p->d_arena.as<uint8_t>(), s); }
+  { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, 1, s); }  // dictionary pages
   { KTimer::Scope sc(&T, 2, s); launch_page_count(C, P, n, arena, pos, s); }
   { KTimer::Scope sc(&T, 3, s); launch_column_scan(p->d_cols.as<DColumn>(), p->n_cols, P, st, s); }
   if (mode == 0) return 0;
-  { KTimer::Scope sc(&T, 4, s); launch_string_positions(C, P, n, arena, pos, s); }
-  { KTimer::Scope sc(&T, 5, s); launch_page_decode(C, P, n, p->d_cols.as<DColumn>(), arena, pos, s); }
+  { KTimer::Scope sc(&T, 4, s); launch_string_positions(C, P, n, arena, pos, 2, s); }
+  if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P, n, arena, p->d_dbp.as<long long>(), s); }
+  { KTimer::Scope sc(&T, 5, s); launch_page_decode(C, P, n, p->d_cols.as<DColumn>(), arena, pos, p->d_dbp.as<long long>(), s); }
   { KTimer::Scope sc(&T, 6, s); launch_string_copy(C, P, n, p->d_cols.as<DColumn>(), arena, pos, s); }
   return 0;
 }
@@ -417,14 +422,26 @@ static int prepare(dk_parquet* p) {
   HIPOK(hipStreamSynchronize(s));
   // header errors
   for (DPage& pg : p->h_pages) if (pg.status != PS_OK && pg.status != PS_UNSUPPORTED) return fail(page_status_msg(p, p->h_pages));
-  int64_t posn = 0, arena_n = 0;
+  int64_t posn = 0, arena_n = 0, dbp_n = 0;
   for (size_t i = 0; i < p->h_pages.size(); i++) {
     DPage& pg = p->h_pages[i];
     DChunk& ck = p->h_chunks[pg.chunk];
     pg.unc_off = -1;
     if (ck.codec != CODEC_NONE) {
-      if (ck.codec != CODEC_SNAPPY) return fail("Error reading Parquet file: unsupported compression codec " + std::to_string(ck.codec));
-      return fail("Error reading Parquet file: " + p->files[p->col_file[ck.col]].path + " (SNAPPY pages: GPU decompression not built in this version)");
+      if (ck.codec != CODEC_SNAPPY)
+        return fail("Error reading Parquet file: " + p->files[p->col_file[ck.col]].path +
+                    " (unsupported compression codec " + std::to_string(ck.codec) + ")");
+      if (!(pg.ptype == PAGE_DATA_V2 && !pg.is_comp)) {
+        pg.unc_off = arena_n;
+        arena_n += ((int64_t)pg.usize + 15) & ~(int64_t)15;
+        p->has_compressed = true;
+      }
+      pg.status = PS_OK;
+    }
+    if ((ck.phys == PT_INT32 || ck.phys == PT_INT64) && !(pg.flags & PF_DICT) && pg.enc == ENC_DELTA_BP) {
+      pg.pos_base = dbp_n;
+      dbp_n += (int64_t)pg.num_values + 1;
+      p->has_dbp = true;
     }
     if (ck.phys == PT_BYTE_ARRAY) {
       if (pg.flags & PF_DICT) { ck.dict_pos = posn; }
@@ -432,8 +449,10 @@ static int prepare(dk_parquet* p) {
       posn += (int64_t)pg.num_values + 1;
     }
   }
-  (void)arena_n;
   if (p->d_pos.alloc((size_t)(posn + 16) * 4)) return 1;
+  if (p->d_arena.alloc((size_t)arena_n + 256)) return 1;
+  if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
+  p->bytes_arena = arena_n;
   if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;
   if (upload(p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), s)) return 1;
   // 2. count + scan to size the outputs (entries / chars are data dependent)
@@ -461,17 +480,20 @@ static int prepare(dk_parquet* p) {
       p->bytes_written += bytes;
       return p->outbufs.back()->p;
     };
+    int64_t n_values = 0;
+    for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) n_values += p->h_pages[pi].n_values;
+    c.null_only = (n_values == 0 && (c.max_rep == 0 || c.n_entries == 0)) ? 1 : 0;
     c.row_def = (uint8_t*)mk(c.n_rows);
-    c.row_offs = c.max_rep > 0 ? (int64_t*)mk((c.n_rows + 1) * 8) : nullptr;
-    c.entry_def = c.max_rep > 0 ? (uint8_t*)mk(nv) : nullptr;
-    if (c.phys == PT_BYTE_ARRAY) {
-      c.offs = (int64_t*)mk((nv + 1) * 8);
-      c.chars = (uint8_t*)mk(c.n_chars);
-      c.fixed = nullptr;
-    } else {
-      c.fixed = (uint8_t*)mk(nv * c.width);
-      c.offs = nullptr;
-      c.chars = nullptr;
+    c.row_offs = (c.max_rep > 0 && !c.null_only) ? (int64_t*)mk((c.n_rows + 1) * 8) : nullptr;
+    c.entry_def = (c.max_rep > 0 && !c.null_only) ? (uint8_t*)mk(nv) : nullptr;
+    c.fixed = nullptr; c.offs = nullptr; c.chars = nullptr;
+    if (!c.null_only) {
+      if (c.phys == PT_BYTE_ARRAY) {
+        c.offs = (int64_t*)mk((nv + 1) * 8);
+        c.chars = (uint8_t*)mk(c.n_chars);
+      } else {
+        c.fixed = (uint8_t*)mk(nv * c.width);
+      }
     }
     if (!c.row_def) return 1;
   }
@@ -602,6 +624,16 @@ extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_c
   const DColumn& c = p->h_cols[ci];
   HostCol& h = p->host[ci];
   int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
+  if (!h.ready && c.null_only) {
+    h.row_def.resize(c.n_rows);
+    HIPOK(hipMemcpy(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost));
+    h.row_offs.assign(c.max_rep > 0 ? c.n_rows + 1 : 0, 0);
+    h.entry_def.assign(nv, 0);
+    h.offs.assign(c.phys == PT_BYTE_ARRAY ? nv + 1 : 0, 0);
+    h.chars.clear();
+    h.fixed.assign(c.phys == PT_BYTE_ARRAY ? 0 : nv * c.width, 0);
+    h.ready = true;
+  }
   if (!h.ready) {
     h.row_def.resize(c.n_rows);
     HIPOK(hipMemcpy(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost));
@@ -1267,7 +1299,7 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
 extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {
   if (i < 0 || i >= KTimer::K) return 1;
   // decode kernels are timed by the parquet object's timer, the rest by the replay's
-  const KTimer* t = (r->ck && i <= 6) ? &r->ck->timer : &r->timer;
+  const KTimer* t = (r->ck && (i <= 6 || i == 13 || i == 14)) ? &r->ck->timer : &r->timer;
   *name = t->names[i];
   if (!*name) return 1;
   *count = t->cnt[i];

@@ -246,6 +246,95 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
 }
 
 // --------------------------------------------------------------------------------------------
+// K1b: SNAPPY raw-block decompression, one wave64 per compressed page.
+// Every lane parses the same tag (uniform control flow; same-address loads coalesce into one
+// transaction), then the wave copies the literal / back-reference 64 bytes per step. Back
+// references read bytes other lanes stored earlier, so a workgroup-scope acq_rel fence orders
+// them whenever the source range reaches past the last fenced output position.
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                               uint8_t* __restrict__ arena) {
+  DPage& pg = pages[blockIdx.x];
+  if (pg.unc_off < 0 || pg.status != PS_OK) return;
+  const DChunk& ck = chunks[pg.chunk];
+  const int lane = threadIdx.x;
+  const uint8_t* in = ck.file + pg.data_off;
+  int64_t clen = pg.csize;
+  uint8_t* out = arena + pg.unc_off;
+  int64_t ulen = pg.usize;
+  const int64_t lv = (pg.ptype == PAGE_DATA_V2) ? (int64_t)pg.rl_len + pg.dl_len : 0;
+  if (lv > clen || lv > ulen) { if (lane == 0) pg.status = PS_BAD_SNAPPY; return; }
+  for (int64_t i = lane; i < lv; i += 64) out[i] = in[i];
+  in += lv; clen -= lv; out += lv; ulen -= lv;
+  if (pg.ptype == PAGE_DATA_V2 && !pg.is_comp) {
+    for (int64_t i = lane; i < clen; i += 64) out[i] = in[i];
+    return;
+  }
+  // preamble: varint uncompressed length
+  int64_t p = 0;
+  uint64_t n = 0;
+  for (int s = 0; s < 35; s += 7) {
+    if (p >= clen) break;
+    uint8_t b = in[p++];
+    n |= (uint64_t)(b & 0x7f) << s;
+    if (!(b & 0x80)) break;
+  }
+  bool bad = (int64_t)n != ulen;
+  int64_t o = 0, fenced = 0;
+  while (!bad && p < clen) {
+    const uint8_t tag = in[p++];
+    const int kind = tag & 3;
+    int64_t len, off = 0;
+    if (kind == 0) {
+      len = (tag >> 2) + 1;
+      if (len > 60) {
+        int nb = (int)len - 60;
+        if (p + nb > clen) { bad = true; break; }
+        len = 0;
+        for (int k = 0; k < nb; k++) len |= (int64_t)in[p + k] << (8 * k);
+        len += 1;
+        p += nb;
+      }
+      if (p + len > clen || o + len > ulen) { bad = true; break; }
+      for (int64_t i = lane; i < len; i += 64) out[o + i] = in[p + i];
+      p += len;
+    } else {
+      if (kind == 1) {
+        if (p + 1 > clen) { bad = true; break; }
+        len = ((tag >> 2) & 7) + 4;
+        off = ((int64_t)(tag >> 5) << 8) | in[p];
+        p += 1;
+      } else if (kind == 2) {
+        if (p + 2 > clen) { bad = true; break; }
+        len = (tag >> 2) + 1;
+        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8);
+        p += 2;
+      } else {
+        if (p + 4 > clen) { bad = true; break; }
+        len = (tag >> 2) + 1;
+        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8) | ((int64_t)in[p + 2] << 16) | ((int64_t)in[p + 3] << 24);
+        p += 4;
+      }
+      if (off == 0 || off > o || o + len > ulen) { bad = true; break; }
+      const int64_t src = o - off;
+      if (src + (off < len ? off : len) > fenced) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        fenced = o;
+      }
+      if (off >= len) {
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + i];
+      } else {
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + (i % off)];
+      }
+    }
+    o += len;
+  }
+  if (o != ulen) bad = true;
+  if (bad && lane == 0) pg.status = PS_BAD_SNAPPY;
+}
+
+// --------------------------------------------------------------------------------------------
 // K2: PLAIN BYTE_ARRAY entry positions (data pages and string dictionaries)
 // P[k] = offset of entry k's 4-byte length prefix within the region, P[n] = region size.
 // Speculation: with non-empty, NUL-free string content and lengths < 2^16 whose low byte is
@@ -254,11 +343,13 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
 // otherwise one lane walks the chain (always exact).
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                                         const uint8_t* __restrict__ arena, int32_t* __restrict__ pos) {
+                                                         const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
+                                                         int mode) {
   const DPage& pg = pages[blockIdx.x];
   const DChunk& ck = chunks[pg.chunk];
   if (ck.phys != PT_BYTE_ARRAY || pg.status != PS_OK) return;
   const bool dict = (pg.flags & PF_DICT) != 0;
+  if (dict != (mode == 1)) return;   // mode 1: dictionary pages, mode 2: data pages
   const uint8_t* r;
   int64_t R;
   int32_t n;
@@ -379,6 +470,153 @@ __device__ __forceinline__ const uint8_t* dict_data(const DChunk& ck, const DPag
 }
 
 // --------------------------------------------------------------------------------------------
+// K2b: DELTA_BINARY_PACKED (INT32/INT64) -> int64 scratch, one workgroup per page.
+// Lane 0 walks block headers for a window of deltas (block min-delta + miniblock bit widths and
+// data offsets into LDS); every lane unpacks its deltas; a block-wide 64-bit scan adds them to
+// the running value (wrapping, as parquet-mr's int arithmetic does).
+// --------------------------------------------------------------------------------------------
+constexpr int DBP_W = 1024;            // deltas per window (4 per thread)
+constexpr int DBP_MAXMINI = 256;
+struct DbpLds {
+  uint32_t mini_off[DBP_MAXMINI];      // miniblock data offset from the value region start
+  uint8_t mini_bw[DBP_MAXMINI];
+  long long mini_min[DBP_MAXMINI];     // min delta of the miniblock's block
+  int32_t mini_first[DBP_MAXMINI];     // first delta index (window-local) of the miniblock
+  int nmini, win, err;
+  long long carry;
+  long long scan64[4];
+  // walker state
+  const uint8_t* p;
+  long long block_min;
+  int mini_in_block, blk_left;         // next miniblock index in the current block
+  const uint8_t* bws;
+  const uint8_t* data;
+};
+
+__device__ __forceinline__ uint64_t uvarint(const uint8_t*& p, const uint8_t* e, int* err) {
+  uint64_t v = 0;
+  for (int s = 0; s < 64; s += 7) {
+    if (p >= e) { *err = 1; return 0; }
+    uint8_t b = *p++;
+    v |= (uint64_t)(b & 0x7f) << s;
+    if (!(b & 0x80)) return v;
+  }
+  *err = 1;
+  return 0;
+}
+
+__global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                     const uint8_t* __restrict__ arena, long long* __restrict__ dbp) {
+  DPage& pg = pages[blockIdx.x];
+  if ((pg.flags & PF_DICT) || pg.status != PS_OK || pg.enc != ENC_DELTA_BP) return;
+  const DChunk& ck = chunks[pg.chunk];
+  if (ck.phys != PT_INT32 && ck.phys != PT_INT64) return;
+  Layout L = page_layout(pg, ck, arena);
+  const int t = threadIdx.x;
+  const int n = pg.n_values;
+  long long* out = dbp + pg.pos_base;
+  __shared__ DbpLds S;
+  __shared__ uint64_t s_block, s_nmini, s_total;
+  if (t == 0) {
+    int err = 0;
+    const uint8_t* p = L.val_p;
+    s_block = uvarint(p, L.val_e, &err);
+    s_nmini = uvarint(p, L.val_e, &err);
+    s_total = uvarint(p, L.val_e, &err);
+    uint64_t z = uvarint(p, L.val_e, &err);
+    long long first = (long long)(z >> 1) ^ -(long long)(z & 1);
+    if (s_nmini == 0 || s_block % s_nmini || (s_block / s_nmini) % 32 || (long long)s_total < n ||
+        s_nmini > DBP_MAXMINI)
+      err = 1;
+    S.p = p; S.carry = first; S.err = err; S.blk_left = 0; S.mini_in_block = 0;
+    if (n > 0 && !err) out[0] = ck.phys == PT_INT32 ? (long long)(int32_t)first : first;
+  }
+  __syncthreads();
+  if (S.err) { if (t == 0) pg.status = PS_BAD_VALUES; return; }
+  const int per_mini = (int)(s_block / s_nmini);
+  const int nmini_blk = (int)s_nmini;
+  const long long ndelta = n > 0 ? n - 1 : 0;
+  for (long long d0 = 0; d0 < ndelta;) {
+    if (t == 0) {
+      // collect miniblocks covering up to DBP_W deltas
+      int got = 0, nm = 0;
+      int err = 0;
+      while (got < DBP_W && got < ndelta - d0 && nm < DBP_MAXMINI) {
+        if (S.mini_in_block == 0 || S.mini_in_block == nmini_blk) {
+          uint64_t z = uvarint(S.p, L.val_e, &err);
+          if (err) break;
+          S.block_min = (long long)(z >> 1) ^ -(long long)(z & 1);
+          if (S.p + nmini_blk > L.val_e) { err = 1; break; }
+          S.bws = S.p;
+          S.p += nmini_blk;
+          S.data = S.p;
+          S.mini_in_block = 0;
+        }
+        int bw = S.bws[S.mini_in_block];
+        S.mini_off[nm] = (uint32_t)(S.data - L.val_p);
+        S.mini_bw[nm] = (uint8_t)bw;
+        S.mini_min[nm] = S.block_min;
+        S.mini_first[nm] = got;
+        nm++;
+        S.data += (long long)per_mini * bw / 8;
+        S.mini_in_block++;
+        if (S.mini_in_block == nmini_blk) S.p = S.data;
+        got += per_mini;
+      }
+      long long rem = ndelta - d0;
+      S.win = (int)(got < rem ? got : rem);
+      S.nmini = nm;
+      S.err = err || S.win <= 0;
+    }
+    __syncthreads();
+    if (S.err) break;
+    const int win = S.win;
+    long long dsum = 0;
+    long long dv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int i = t * 4 + k;
+      dv[k] = 0;
+      if (i < win) {
+        int m = i / per_mini;
+        int pos = i - S.mini_first[m];
+        int bw = S.mini_bw[m];
+        uint64_t u = 0;
+        if (bw) {
+          const uint8_t* mp = L.val_p + S.mini_off[m];
+          int64_t bit = (int64_t)pos * bw;
+          const uint8_t* q = mp + (bit >> 3);
+          int sh = (int)(bit & 7);
+          int nb = (sh + bw + 7) >> 3;
+          unsigned __int128 w = 0;
+          for (int b = 0; b < nb; b++) if (q + b < L.val_e) w |= (unsigned __int128)q[b] << (8 * b);
+          u = (uint64_t)(w >> sh);
+          if (bw < 64) u &= ((1ull << bw) - 1);
+        }
+        dv[k] = (long long)((uint64_t)S.mini_min[m] + u);
+        dsum = (long long)((uint64_t)dsum + (uint64_t)dv[k]);
+      }
+    }
+    long long tot;
+    long long ex = block_scan64(dsum, &tot, S.scan64);
+    long long run = (long long)((uint64_t)S.carry + (uint64_t)ex);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int i = t * 4 + k;
+      if (i < win) {
+        run = (long long)((uint64_t)run + (uint64_t)dv[k]);
+        out[d0 + i + 1] = ck.phys == PT_INT32 ? (long long)(int32_t)run : run;
+      }
+    }
+    __syncthreads();
+    if (t == 0) S.carry = (long long)((uint64_t)S.carry + (uint64_t)tot);
+    d0 += win;
+    __syncthreads();
+  }
+  if (S.err && t == 0) pg.status = PS_BAD_VALUES;
+}
+
+// --------------------------------------------------------------------------------------------
 // K3: counts per data page
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_page_count(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
@@ -461,7 +699,8 @@ __global__ __launch_bounds__(NT) void k_page_count(const DChunk* __restrict__ ch
     }
   } else {
     bool ok_enc = pg.enc == ENC_PLAIN || ((pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) && ck.dict_page >= 0) ||
-                  (pg.enc == ENC_RLE && ck.phys == PT_BOOLEAN);
+                  (pg.enc == ENC_RLE && ck.phys == PT_BOOLEAN) ||
+                  (pg.enc == ENC_DELTA_BP && (ck.phys == PT_INT32 || ck.phys == PT_INT64));
     if (!ok_enc && tv > 0) bad = true;
   }
   if (t == 0) {
@@ -517,7 +756,7 @@ __global__ __launch_bounds__(NT) void k_column_scan(DColumn* __restrict__ cols, 
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                     const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
-                                                    const int32_t* __restrict__ pos) {
+                                                    const int32_t* __restrict__ pos, const long long* __restrict__ dbp) {
   const DPage& pg = pages[blockIdx.x];
   if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
   const DChunk& ck = chunks[pg.chunk];
@@ -616,15 +855,15 @@ __global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ c
         const long long grow = pg.row_base + r_i;           // row of this level (if row start)
         if (is_row) {
           col.row_def[grow] = (uint8_t)d;
-          if (rep) col.row_offs[grow] = pg.entry_base + e_i;
+          if (rep && col.row_offs) col.row_offs[grow] = pg.entry_base + e_i;
         }
         long long dest = -1;
         if (rep) {
-          if (is_ent) { dest = pg.entry_base + e_i; col.entry_def[dest] = (uint8_t)d; }
+          if (is_ent) { dest = pg.entry_base + e_i; if (col.entry_def) col.entry_def[dest] = (uint8_t)d; }
         } else {
           dest = grow;
         }
-        if (dest >= 0) {
+        if (dest >= 0 && !col.null_only) {
           const long long vloc = v_i;                       // values before this level (page-local)
           if (is_str) {
             long long cpos;
@@ -646,6 +885,9 @@ __global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ c
               if (bool_rle_p) b = (uint8_t)ix[k];
               else b = (L.val_p[vloc >> 3] >> (vloc & 7)) & 1;
               *o = b;
+            } else if (pg.enc == ENC_DELTA_BP) {
+              long long x = dbp[pg.pos_base + vloc];
+              if (w == 8) *(long long*)o = x; else *(int32_t*)o = (int32_t)x;
             } else {
               const uint8_t* src = is_dict ? D + (int64_t)ix[k] * w : L.val_p + vloc * w;
               if (w == 8) {
@@ -843,6 +1085,7 @@ __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restri
                                               const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
                                               uint32_t seed, uint8_t* __restrict__ sel, DState* __restrict__ st) {
   long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const SimpleSet ss;
   bool seen = false, chosen = false, dup = false;
   if (r < pc.n_rows) {
     if (pc.path_def[r] >= 1) {
@@ -860,7 +1103,20 @@ __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restri
         off = has_off ? pc.off_vals[r] : 0;
       }
       uint64_t hp;
-      int rc = path_hash(p, pl, seed, &hp);
+      int rc = 0;
+      {
+        // aligned 8-byte loads + funnel shift (no reliance on unaligned-access mode)
+        const uintptr_t pa = (uintptr_t)p;
+        const uint64_t* base = (const uint64_t*)(pa & ~(uintptr_t)7);
+        const int sh = (int)(pa & 7) * 8;
+        auto load8 = [&](int32_t j) -> uint64_t {
+          uint64_t w0 = base[j];
+          if (!sh) return w0;
+          uint64_t w1 = base[j + 1];
+          return (w0 >> sh) | (w1 << (64 - sh));
+        };
+        if (!simple_path_hash(pl, load8, ss, seed, &hp)) rc = path_hash(p, pl, seed, &hp);
+      }
       HashSink kd; kd.hs.init(kHashSeed(seed)); kd.n = 0;
       int rc2 = dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, kd);
       if (rc || rc2) {
@@ -910,8 +1166,12 @@ namespace dk {
 void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
 }
-void launch_string_positions(const DChunk* c, DPage* p, int n, const uint8_t* arena, int32_t* pos, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos);
+void launch_snappy(const DChunk* c, DPage* p, int n, uint8_t* arena, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_snappy, dim3(n), dim3(64), 0, s, c, p, arena);
+}
+void launch_string_positions(const DChunk* c, DPage* p, int n, const uint8_t* arena, int32_t* pos, int mode,
+                             hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos, mode);
 }
 void launch_page_count(const DChunk* c, DPage* p, int n, const uint8_t* arena, const int32_t* pos, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_count, dim3(n), dim3(NT), 0, s, c, p, arena, pos);
@@ -920,8 +1180,11 @@ void launch_column_scan(DColumn* cols, int ncols, DPage* p, DState* st, hipStrea
   if (ncols) hipLaunchKernelGGL(k_column_scan, dim3(ncols), dim3(NT), 0, s, cols, p, st);
 }
 void launch_page_decode(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
-                        const int32_t* pos, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_page_decode, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos);
+                        const int32_t* pos, const long long* dbp, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_page_decode, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos, dbp);
+}
+void launch_delta_decode(const DChunk* c, DPage* p, int n, const uint8_t* arena, long long* dbp, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_delta_decode, dim3(n), dim3(NT), 0, s, c, p, arena, dbp);
 }
 void launch_string_copy(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
                         const int32_t* pos, hipStream_t s) {

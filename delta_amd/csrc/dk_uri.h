@@ -436,8 +436,45 @@ DK_HD int dv_emit(bool has_dv, const uint8_t* st, int32_t stn, const uint8_t* pi
 
 DK_HD uint64_t kHashSeed(uint32_t seed) { return 0x243F6A8885A308D3ull * (uint64_t)(seed + 1); }
 
-// Hash of a path's canonical stream. Fast path processes 8 bytes per step (unaligned loads are
-// fine on CDNA global memory and on x86).
+// 128-bit membership bitmap of the fast-path class CC_SIMPLE (ASCII only).
+struct SimpleSet {
+  uint64_t lo, hi;
+  DK_HD SimpleSet() : lo(0), hi(0) {
+    for (int c = 1; c < 128; c++)
+      if (uri_class((uint8_t)c) & CC_SIMPLE) { if (c < 64) lo |= 1ull << c; else hi |= 1ull << (c - 64); }
+  }
+  DK_HD bool has(uint32_t c) const { return c < 64 ? ((lo >> c) & 1) : (c < 128 ? ((hi >> (c - 64)) & 1) : false); }
+};
+
+// Fast path of path_hash for plain relative paths: the stream is TAG_PATH followed by the raw
+// bytes, hashed one 8-byte word per step. `load8(i)` returns the little-endian bytes s[8i..8i+8)
+// (bytes past n are ignored). Returns false (nothing computed) when the string is not simple.
+template <class Load8>
+DK_HD bool simple_path_hash(int32_t n, const Load8& load8, const SimpleSet& ss, uint32_t seed, uint64_t* out) {
+  Hash64 hs; hs.init(kHashSeed(seed));
+  uint64_t prev = (uint64_t)TAG_PATH << 56;
+  const int32_t nchunks = (n + 7) >> 3;
+  for (int32_t j = 0; j < nchunks; j++) {
+    uint64_t c = load8(j);
+    int32_t valid = n - 8 * j < 8 ? n - 8 * j : 8;
+    for (int32_t b = 0; b < valid; b++) if (!ss.has((uint32_t)((c >> (8 * b)) & 0xff))) return false;
+    if (j == 0 && n >= 2 && (c & 0xffff) == 0x2f2f) return false;   // leading "//" = authority
+    if (valid == 8) { hs.word((prev >> 56) | (c << 8)); prev = c; }
+    else {
+      // final partial chunk: stream bytes left = 1 (carried) + valid
+      uint64_t tailw = (prev >> 56) | ((valid ? (c & ((1ull << (8 * valid)) - 1)) : 0) << 8);
+      hs.buf = tailw; hs.nb = valid + 1;
+      if (hs.nb == 8) { hs.word(hs.buf); hs.buf = 0; hs.nb = 0; }
+      *out = hs.final_((uint64_t)n + 1);
+      return true;
+    }
+  }
+  hs.buf = prev >> 56; hs.nb = 1;
+  *out = hs.final_((uint64_t)n + 1);
+  return true;
+}
+
+// Hash of a path's canonical stream (generic, byte at a time).
 DK_HD int path_hash(const uint8_t* s, int32_t n, uint32_t seed, uint64_t* out) {
   HashSink k; k.hs.init(kHashSeed(seed)); k.n = 0;
   int rc = uri_emit(s, n, k);

@@ -105,7 +105,12 @@ class ParquetSet:
         return Column(c, leaf)
 
     def columns(self, file_idx):
-        return {leaf: self.column(file_idx, leaf) for leaf in self.leaves}
+        """leaf -> Column, or None when the file lacks the leaf (all-null, NonExistentColumnReader)."""
+        out = {}
+        for leaf in self.leaves:
+            c = self.column(file_idx, leaf)
+            out[leaf] = c if c.present else None
+        return out
 
     def traffic(self):
         r, w = C.c_int64(), C.c_int64()
@@ -316,7 +321,7 @@ class Snapshot:
             for fi in range(len(files)):
                 cols = ps.columns(fi)
                 rv = cols["protocol.minReaderVersion"]
-                if self.protocol is None and rv.present:
+                if self.protocol is None and rv is not None:
                     idx = np.nonzero(rv.row_def >= 1)[0]
                     if len(idx):
                         r = int(idx[0])
@@ -324,13 +329,14 @@ class Snapshot:
                         self.protocol = {"minReaderVersion": int(rv.fixed.view(np.int32)[r]),
                                          "minWriterVersion": int(wv.fixed.view(np.int32)[r])}
                 mid = cols["metaData.id"]
-                if self.metadata is None and mid.present:
+                if self.metadata is None and mid is not None:
                     idx = np.nonzero(mid.row_def >= 1)[0]
                     if len(idx):
                         r = int(idx[0])
                         ss = cols["metaData.schemaString"]
                         self.metadata = {"id": mid.string(r).decode() if mid.row_def[r] >= 2 else None,
-                                         "schemaString": ss.string(r).decode() if ss.row_def[r] >= 2 else None}
+                                         "schemaString": (ss.string(r).decode()
+                                                          if ss is not None and ss.row_def[r] >= 2 else None)}
             ps.close()
         if self.protocol is None:
             raise DkError("No protocol found at version %d" % self.getVersion())
@@ -430,12 +436,14 @@ class GpuScan:
             sel = np.zeros(self.tail.rows, dtype=np.uint8)
             check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
             cols = {leaf: self.tail.column(leaf) for leaf in leaves}
+            cols = {k: (c if c.present else None) for k, c in cols.items()}
             yield FilteredColumnarBatch(cols, root, int(self.tail.rows), sel.astype(bool), "json-tail")
         for fi, path in enumerate(self.ckpt_files or []):
             n = self.ckpt.num_rows(fi)
             sel = np.zeros(n, dtype=np.uint8)
             check(lib().dk_replay_ckpt_selection(self._rh, fi, sel.ctypes.data, n))
             cols = {leaf: self.ckpt.column(fi, leaf) for leaf in leaves}
+            cols = {k: (c if c.present else None) for k, c in cols.items()}
             yield FilteredColumnarBatch(cols, root, int(n), sel.astype(bool), path)
 
     def close(self):

@@ -16,6 +16,11 @@ CASES = {
     "variable-paths": dict(variable_paths=True, dv_frac=0.2),
     "no-page-index": dict(write_page_index=False, max_rows_per_page=3000),
     "multi-rowgroup": dict(row_group_size=7000, max_rows_per_page=2500),
+    "snappy-v1": dict(compression="snappy", pv_keys=2, dv_frac=0.1),
+    "snappy-v2-plain": dict(compression="snappy", data_page_version="2.0", use_dictionary=False),
+    "snappy-stats-variable": dict(compression="snappy", variable_paths=True, with_stats=True),
+    "delta-binary-packed-v1": dict(delta_binary_packed=True, max_rows_per_page=4099),
+    "delta-binary-packed-v2-snappy": dict(delta_binary_packed=True, data_page_version="2.0", compression="snappy"),
 }
 
 

@@ -82,3 +82,21 @@ def test_fast_path_hash_matches_slow_stream(shim):
         h = C.c_uint64()
         assert shim.prod_path_hash(s, len(s), 0, C.byref(h)) == 0
         assert h.value != 0
+
+
+def test_simple_word_hash_equals_generic(shim):
+    shim.prod_simple_hash.argtypes = [C.c_char_p, C.c_int32, C.c_uint32, C.POINTER(C.c_uint64)]
+    rng = random.Random(7)
+    simple = "abcXYZ019-_.!~*'()/@&=+$,;"
+    for n in list(range(0, 40)) + [83, 87, 200]:
+        for _ in range(5):
+            s = "".join(rng.choice(simple) for _ in range(n)).encode()
+            if s.startswith(b"//"):
+                continue
+            a, b = C.c_uint64(), C.c_uint64()
+            assert shim.prod_simple_hash(s, len(s), 3, C.byref(a)) == 1
+            assert shim.prod_path_hash(s, len(s), 3, C.byref(b)) == 0
+            assert a.value == b.value, s
+    for s in [b"a:b", b"a%20", b"//x", b"a b", "é".encode()]:
+        a = C.c_uint64()
+        assert shim.prod_simple_hash(s, len(s), 3, C.byref(a)) == 0
