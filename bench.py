@@ -95,8 +95,11 @@ def main():
 
     work = args.workdir or tempfile.mkdtemp(prefix="dk_bench_r%d_" % rank)
     t0 = time.time()
-    info = make_table(work, args.rows, 20250218 + rank, args.compression)
-    log("[rank %d] generated %d-row table in %.1fs" % (rank, info["checkpoint_rows"], time.time() - t0))
+    if args.workdir and os.path.isdir(os.path.join(work, "_delta_log")):
+        log("[rank %d] reusing table in %s" % (rank, work))
+    else:
+        info = make_table(work, args.rows, 20250218 + rank, args.compression)
+        log("[rank %d] generated %d-row table in %.1fs" % (rank, info["checkpoint_rows"], time.time() - t0))
 
     eng = K.GpuEngine(device=local if world > 1 else 0, timing=True)
     t0 = time.perf_counter()

@@ -22,13 +22,24 @@ def build(force=False, verbose=False):
     if not force and not _stale():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value",
-           "-I", os.path.join(HERE, "..", "include"), "-o", OUT + ".tmp"]
-    cmd += [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+             "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value",
+             "-I", os.path.join(HERE, "..", "include")]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc] + flags + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    bad = [p.wait() for p in procs]
+    if any(bad):
+        raise subprocess.CalledProcessError(max(bad), "hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     subprocess.check_call(cmd)
+    for o in objs:
+        os.remove(o)
     os.replace(OUT + ".tmp", OUT)
     return OUT
 

@@ -37,7 +37,8 @@ struct DPage {
 struct DColumn {
   int32_t first_page, n_pages;   // data pages, contiguous in the page table, in file order
   int32_t phys, width, max_def, max_rep, rep_def, present;
-  int32_t null_only, pad0;   // null_only: no value anywhere -> no value buffers are materialised
+  int32_t null_only;         // no value anywhere -> no value buffers are materialised
+  int32_t key_hash;          // 1: this is the reconciliation key column (add.path) -> emit path hashes
   int64_t n_rows;
   uint8_t* row_def;
   int64_t* row_offs;
@@ -47,7 +48,15 @@ struct DColumn {
   uint8_t* chars;
   int64_t n_entries, n_chars;    // totals (k_column_scan)
   int64_t cap_entries, cap_chars;
+  // key_hash columns only: canonical-path hash (seed kDecodeSeed) per value (scratch, filled by
+  // k_string_copy for PLAIN pages, 0 = not computed) and per row (forwarded by k_page_decode;
+  // 0 = null row or "compute in the probe")
+  uint64_t* vhash;
+  uint64_t* hash;
 };
+
+constexpr uint32_t kDecodeSeed = 0;   // seed of the path hashes computed during decode
+constexpr int DK_COPY_TILE = 128;     // values per k_string_copy workgroup (host tile table step)
 
 // Commit-tail actions, one per JSON line, in replay order.
 enum : int32_t { JA_NONE = 0, JA_ADD = 1, JA_REMOVE = 2 };
@@ -86,6 +95,7 @@ struct DState {
 // Column pointers the checkpoint probe reads (one checkpoint file).
 struct ProbeCols {
   const uint8_t* path_def; const int64_t* path_offs; const uint8_t* path_chars;
+  const uint64_t* path_hash;   // per-row path hashes from decode (seed kDecodeSeed), or null
   const uint8_t* st_def; const int64_t* st_offs; const uint8_t* st_chars;
   const int64_t* pid_offs; const uint8_t* pid_chars;
   const uint8_t* off_def; const int32_t* off_vals; int32_t off_maxdef;

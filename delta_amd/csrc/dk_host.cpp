@@ -20,12 +20,12 @@
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const DChunk*, DPage*, int, uint8_t*, hipStream_t);
-void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, int, hipStream_t);
-void launch_page_count(const DChunk*, DPage*, int, const uint8_t*, const int32_t*, hipStream_t);
+void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, int, hipStream_t, int);
+void launch_page_count(const DChunk*, DPage*, int, const uint8_t*, const int32_t*, hipStream_t, int);
 void launch_column_scan(DColumn*, int, DPage*, DState*, hipStream_t);
-void launch_page_decode(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const long long*, hipStream_t);
+void launch_page_decode(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const long long*, hipStream_t, int);
 void launch_delta_decode(const DChunk*, DPage*, int, const uint8_t*, long long*, hipStream_t);
-void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, hipStream_t);
+void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const int2*, hipStream_t, int);
 void launch_json_canon(DJsonAction*, int, const uint8_t*, uint8_t*, uint32_t, DState*, hipStream_t);
 void launch_slots_init(Slot*, uint64_t, hipStream_t);
 void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
@@ -61,6 +61,11 @@ extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
   dk_config c = cfg ? *cfg : dk_config{1024, 1024, 0, 0};
   if (c.parquet_batch_size <= 0) c.parquet_batch_size = 1024;
   if (c.json_batch_size <= 0) return fail("invalid JSON reader batch size: " + std::to_string(c.json_batch_size));
+  {  // the compile-time fast-path character set must agree with the URI character classes
+    for (uint32_t ch = 0; ch < 256; ch++)
+      if (simple8(0x6161616161616100ull | ch) != (ch > 0 && ch < 128 && (uri_class((uint8_t)ch) & CC_SIMPLE) != 0))
+        return fail("libdkgpu: internal error: SimpleSet disagrees with uri_class");
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail("libdkgpu: no HIP device available (the GPU engine has no CPU fallback)");
@@ -341,7 +346,10 @@ struct dk_parquet {
   std::vector<DPage> h_pages;
   std::vector<DColumn> h_cols;
   std::vector<int> col_file;
-  DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp;
+  DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp, d_tiles;
+  // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
+  // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
+  std::vector<int> col_tile0;
   std::vector<std::unique_ptr<DBuf>> outbufs;
   std::vector<HostCol> host;
   int n_pages = 0, n_cols = 0;
@@ -370,6 +378,17 @@ static int read_file(const std::string& path, std::vector<uint8_t>& out) {
   return 0;
 }
 
+// Per-page kernels are launched once over every page, or -- with DK_SPLIT_LAUNCH=1, a profiling
+// aid -- once per column so that rocprofv3's kernel trace attributes time to columns.
+template <class F>
+static void per_column(const dk_parquet* p, int n, F&& f) {
+  static const bool split = getenv("DK_SPLIT_LAUNCH") && atoi(getenv("DK_SPLIT_LAUNCH")) != 0;
+  if (!split) { f(0, n); return; }
+  int covered = 0;
+  for (const DColumn& c : p->h_cols) { f(c.first_page, c.n_pages); covered += c.n_pages; }
+  if (covered < n) f(covered, n - covered);    // dictionary pages (after every data page)
+}
+
 // the decode pipeline (mode: 0 = prepare pass up to the scan; 1 = full step)
 static int run_pipeline(dk_parquet* p, int mode) {
   hipStream_t s = p->eng->stream;
@@ -379,18 +398,29 @@ static int run_pipeline(dk_parquet* p, int mode) {
   int32_t* pos = p->d_pos.as<int32_t>();
   const uint8_t* arena = p->d_arena.as<uint8_t>();
   DState* st = p->d_state.as<DState>();
+  DColumn* cols = p->d_cols.as<DColumn>();
+  const long long* dbp = p->d_dbp.as<long long>();
   int n = p->n_pages;
   { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
   if (mode == -1) return 0;
   if (p->has_compressed) { KTimer::Scope sc(&T, 13, s); launch_snappy(C, P, n, p->d_arena.as<uint8_t>(), s); }
-  { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, 1, s); }  // dictionary pages
-  { KTimer::Scope sc(&T, 2, s); launch_page_count(C, P, n, arena, pos, s); }
-  { KTimer::Scope sc(&T, 3, s); launch_column_scan(p->d_cols.as<DColumn>(), p->n_cols, P, st, s); }
+  { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, 1, s, 0); }  // dictionary pages
+  { KTimer::Scope sc(&T, 2, s); per_column(p, n, [&](int a, int k) { launch_page_count(C, P, k, arena, pos, s, a); }); }
+  { KTimer::Scope sc(&T, 3, s); launch_column_scan(cols, p->n_cols, P, st, s); }
   if (mode == 0) return 0;
-  { KTimer::Scope sc(&T, 4, s); launch_string_positions(C, P, n, arena, pos, 2, s); }
+  { KTimer::Scope sc(&T, 4, s); per_column(p, n, [&](int a, int k) { launch_string_positions(C, P, k, arena, pos, 2, s, a); }); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P, n, arena, p->d_dbp.as<long long>(), s); }
-  { KTimer::Scope sc(&T, 5, s); launch_page_decode(C, P, n, p->d_cols.as<DColumn>(), arena, pos, p->d_dbp.as<long long>(), s); }
-  { KTimer::Scope sc(&T, 6, s); launch_string_copy(C, P, n, p->d_cols.as<DColumn>(), arena, pos, s); }
+  // string copy first: it fills the key column's per-value hashes that k_page_decode forwards
+  {
+    KTimer::Scope sc(&T, 6, s);
+    static const bool split = getenv("DK_SPLIT_LAUNCH") && atoi(getenv("DK_SPLIT_LAUNCH")) != 0;
+    const int2* tiles = p->d_tiles.as<int2>();
+    if (!split) launch_string_copy(C, P, p->col_tile0.back(), cols, arena, pos, tiles, s, 0);
+    else
+      for (int c = 0; c < p->n_cols; c++)
+        launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c]);
+  }
+  { KTimer::Scope sc(&T, 5, s); per_column(p, n, [&](int a, int k) { launch_page_decode(C, P, k, cols, arena, pos, dbp, s, a); }); }
   return 0;
 }
 
@@ -465,7 +495,21 @@ static int prepare(dk_parquet* p) {
   HIPOK(hipStreamSynchronize(s));
   std::string m = page_status_msg(p, p->h_pages);
   if (!m.empty()) return fail(m);
-  // 3. allocate outputs
+  // 3. string-copy tile table (page counts are final after the count pass)
+  {
+    std::vector<int2> tiles;
+    p->col_tile0.assign(1, 0);
+    for (const DColumn& c : p->h_cols) {
+      for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
+        const DPage& pg = p->h_pages[pi];
+        if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN) continue;
+        for (int v0 = 0; v0 < pg.n_values; v0 += DK_COPY_TILE) tiles.push_back(make_int2(pi, v0));
+      }
+      p->col_tile0.push_back((int)tiles.size());
+    }
+    if (upload(p->d_tiles, tiles.data(), tiles.size() * sizeof(int2), s)) return 1;
+  }
+  // 4. allocate outputs
   p->bytes_written = 0;
   for (size_t i = 0; i < p->h_cols.size(); i++) {
     DColumn& c = p->h_cols[i];
@@ -484,6 +528,13 @@ static int prepare(dk_parquet* p) {
     for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) n_values += p->h_pages[pi].n_values;
     c.null_only = (n_values == 0 && (c.max_rep == 0 || c.n_entries == 0)) ? 1 : 0;
     c.row_def = (uint8_t*)mk(c.n_rows);
+    c.vhash = c.hash = nullptr;
+    if (c.key_hash && !c.null_only && c.phys == PT_BYTE_ARRAY && c.max_rep == 0) {
+      c.vhash = (uint64_t*)mk((n_values + 1) * 8);
+      p->bytes_written -= (n_values + 1) * 8;     // scratch, not an output (written + re-read once)
+      c.hash = (uint64_t*)mk(c.n_rows * 8);
+      if (!c.vhash || !c.hash) return 1;
+    }
     c.row_offs = (c.max_rep > 0 && !c.null_only) ? (int64_t*)mk((c.n_rows + 1) * 8) : nullptr;
     c.entry_def = (c.max_rep > 0 && !c.null_only) ? (uint8_t*)mk(nv) : nullptr;
     c.fixed = nullptr; c.offs = nullptr; c.chars = nullptr;
@@ -533,6 +584,7 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
       DColumn c{};
       c.phys = L.phys; c.width = L.phys == PT_BYTE_ARRAY ? 0 : phys_width(L.phys, L.type_length);
       c.max_def = L.max_def; c.max_rep = L.max_rep; c.rep_def = L.rep_def; c.present = 1;
+      c.key_hash = p->leaves[li] == "add.path";   // the reconciliation key (ActiveAddFilesIterator)
       c.n_rows = 0;
       c.first_page = (int)p->h_pages.size();
       int colid = (int)p->h_cols.size();
@@ -1185,6 +1237,7 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
       if (!path) { pc.n_rows = 0; r->probe.push_back(pc); continue; }
       if (path->phys != PT_BYTE_ARRAY || path->max_rep) return fail("add.path has an unexpected type");
       pc.path_def = path->row_def; pc.path_offs = path->offs; pc.path_chars = path->chars;
+      pc.path_hash = path->hash;
       const DColumn* st = find_col(ckpt, (int)fi, "add.deletionVector.storageType");
       const DColumn* pid = find_col(ckpt, (int)fi, "add.deletionVector.pathOrInlineDv");
       const DColumn* off = find_col(ckpt, (int)fi, "add.deletionVector.offset");
@@ -1226,7 +1279,9 @@ static int replay_launch(dk_replay* r) {
     if (run_pipeline(p, 1)) return 1;
     for (size_t fi = 0; fi < r->probe.size(); fi++) {
       KTimer::Scope sc(&T, 11, s);
-      launch_probe(r->probe[fi], S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, r->d_csel[fi]->as<uint8_t>(), st, s);
+      ProbeCols pc = r->probe[fi];
+      if (r->seed != kDecodeSeed) pc.path_hash = nullptr;   // collision retry: rehash from the chars
+      launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, r->d_csel[fi]->as<uint8_t>(), st, s);
     }
   }
   return 0;

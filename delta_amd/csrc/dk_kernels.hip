@@ -13,6 +13,7 @@
 //   k_json_canon / k_table_insert / k_table_update / k_json_select   commit-tail keys
 //   k_probe             checkpoint add rows: URI-canonical key hash, probe, verify, select
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "dk_device.h"
 #include "dk_thrift.h"
@@ -344,8 +345,8 @@ __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                          const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                         int mode) {
-  const DPage& pg = pages[blockIdx.x];
+                                                         int mode, int page0) {
+  const DPage& pg = pages[page0 + blockIdx.x];
   const DChunk& ck = chunks[pg.chunk];
   if (ck.phys != PT_BYTE_ARRAY || pg.status != PS_OK) return;
   const bool dict = (pg.flags & PF_DICT) != 0;
@@ -373,28 +374,43 @@ __global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restric
   const int t = threadIdx.x;
   if (t == 0) s_fail = 0;
   __syncthreads();
+  // Candidate scan over 16-byte ALIGNED blocks of the absolute address space (one dwordx4 per
+  // lane, the 4 look-ahead bytes come from the next lane's block): block i covers region bytes
+  // [16i - mis, 16i - mis + 16). A candidate is the last zero byte j of a zero run (byte j+1
+  // non-zero, or j+1 == R), giving the prefix start q = j - 3.
+  const uintptr_t abase = (uintptr_t)r & ~(uintptr_t)15;
+  const int64_t mis = (int64_t)((uintptr_t)r - abase);
+  const int64_t nblk = (mis + R + 15) >> 4;
+  const uint4* blk = (const uint4*)abase;
   int carry = 0;
-  for (int64_t w0 = 0; w0 < R; w0 += NT * 16) {
-    int64_t b = w0 + (int64_t)t * 16;
-    uint32_t m = 0;
-    int cnt = 0;
-    if (b < R) {
-      uint8_t by[20];
-#pragma unroll
-      for (int j = 0; j < 20; j++) by[j] = (b + j < R) ? r[b + j] : 1;
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        int64_t q = b + j;
-        bool c = (q + 3 < R) && by[j + 3] == 0 && (q + 4 == R || by[j + 4] != 0);
-        if (c) { m |= 1u << j; cnt++; }
-      }
-    }
+  for (int64_t i0 = 0; i0 < nblk; i0 += NT) {
+    const int64_t i = i0 + t;
+    uint4 q = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+    if (i < nblk) q = blk[i];
+    uint32_t nxt = __shfl_down(q.x, 1, 64);
+    if ((t & 63) == 63 && i + 1 < nblk) nxt = ((const uint32_t*)(blk + i + 1))[0];
+    auto zb = [](uint32_t x) -> uint32_t {      // bit k set iff byte k of x is zero
+      uint32_t y = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+      y = ~(y | x | 0x7F7F7F7Fu);               // 0x80 in every zero byte
+      return ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
+    };
+    uint32_t z = zb(q.x) | (zb(q.y) << 4) | (zb(q.z) << 8) | (zb(q.w) << 12);
+    const int64_t rb = 16 * i - mis;            // region index of byte 0 of this block
+    // the byte at region index R (past the region) counts as non-zero
+    uint32_t z16 = (zb(nxt) & 1u);
+    if (rb + 16 >= R) z16 = 0;
+    if (rb + 16 > R) { int64_t keep = R - rb; z &= keep <= 0 ? 0u : (uint32_t)((1u << keep) - 1u); }
+    uint32_t m = z & ~((z >> 1) | (z16 << 15));
+    // prefix start q = j - 3 must be >= 0
+    if (rb < 3) { int64_t drop = 3 - rb; m &= drop >= 16 ? 0u : ~((1u << drop) - 1u); }
+    if (i >= nblk) m = 0;
+    int cnt = __popc(m);
     int base, d0, d1, tot, t1, t2;
     block_scan3(cnt, 0, 0, &base, &d0, &d1, &tot, &t1, &t2, lds);
     if (carry + tot > n) { if (t == 0) s_fail = 1; }
     else {
       int k = carry + base;
-      while (m) { int j = __ffs(m) - 1; m &= m - 1; P[k++] = (int32_t)(b + j); }
+      while (m) { int j = __ffs(m) - 1; m &= m - 1; P[k++] = (int32_t)(rb + j - 3); }
     }
     carry += tot;
     if (carry > n) break;
@@ -420,7 +436,7 @@ __global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restric
       q += 4 + (int64_t)ld_u32(r + q);
       if (q > R) { bad = 1; break; }
     }
-    if (bad) pages[blockIdx.x].status = dict ? PS_BAD_DICT : PS_BAD_VALUES;
+    if (bad) pages[page0 + blockIdx.x].status = dict ? PS_BAD_DICT : PS_BAD_VALUES;
   }
   if (t == 0) P[n] = (int32_t)R;
 }
@@ -620,8 +636,8 @@ __global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ 
 // K3: counts per data page
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_page_count(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                                   const uint8_t* __restrict__ arena, const int32_t* __restrict__ pos) {
-  DPage& pg = pages[blockIdx.x];
+                                                   const uint8_t* __restrict__ arena, const int32_t* __restrict__ pos, int page0) {
+  DPage& pg = pages[page0 + blockIdx.x];
   if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
   const DChunk& ck = chunks[pg.chunk];
   __shared__ WinLds W;
@@ -756,8 +772,8 @@ __global__ __launch_bounds__(NT) void k_column_scan(DColumn* __restrict__ cols, 
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                     const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
-                                                    const int32_t* __restrict__ pos, const long long* __restrict__ dbp) {
-  const DPage& pg = pages[blockIdx.x];
+                                                    const int32_t* __restrict__ pos, const long long* __restrict__ dbp, int page0) {
+  const DPage& pg = pages[page0 + blockIdx.x];
   if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
   const DChunk& ck = chunks[pg.chunk];
   const DColumn& col = cols[ck.col];
@@ -856,6 +872,8 @@ __global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ c
         if (is_row) {
           col.row_def[grow] = (uint8_t)d;
           if (rep && col.row_offs) col.row_offs[grow] = pg.entry_base + e_i;
+          // key column: forward the value's path hash (PLAIN pages; 0 = the probe recomputes)
+          if (col.hash) col.hash[grow] = (is_val && P) ? col.vhash[pg.value_base + v_i] : 0ull;
         }
         long long dest = -1;
         if (rep) {
@@ -912,53 +930,125 @@ __global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ c
 }
 
 // --------------------------------------------------------------------------------------------
-// K6: PLAIN string bytes -> contiguous output chars (16-byte aligned global stores)
+// K6: PLAIN string bytes -> contiguous output chars, fused with the key-path hash.
+// One 128-thread workgroup per tile of CT values of one page (host-built tile table: a 1 MB page
+// spreads over ~90 workgroups). Per tile (split further if its input span exceeds CT_BYTES):
+//   1. stage the input span (length prefixes + bytes) into LDS `in` with aligned dwordx4 loads;
+//   2. lane k compacts value k into LDS `out` at its output position (dword stores, the source
+//      dword stream shifted with v_alignbyte; byte stores only at the value's two edges), and,
+//      for the key column (add.path), hashes it with the canonical fast-path hash
+//      (simple_path_hash, seed kDecodeSeed; 0 = "not simple, the probe recomputes");
+//   3. `out` is laid out congruent to the global destination mod 16, so the store pass is one
+//      ds_read_b128 + global dwordx4 store per lane (byte stores for the two edge chunks, which
+//      neighbouring tiles/pages share).
+// A single value larger than CT_BYTES is copied straight from global memory (hash 0).
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_string_copy(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+constexpr int CT = DK_COPY_TILE;       // threads = values per tile
+constexpr int CT_BYTES = 16384;        // LDS bytes per staging buffer
+
+__device__ __forceinline__ uint32_t lds_u32_at(const uint32_t* w, int32_t b) {   // 4 bytes at any byte offset
+  const int32_t i = b >> 2;
+  return __builtin_amdgcn_alignbyte(w[i + 1], w[i], (uint32_t)(b & 3));
+}
+
+__global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                     const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
-                                                    const int32_t* __restrict__ pos) {
-  const DPage& pg = pages[blockIdx.x];
+                                                    const int32_t* __restrict__ pos, const int2* __restrict__ tiles,
+                                                    int tile0, int dbg) {
+  const int2 tile = tiles[tile0 + blockIdx.x];     // (page, first value)
+  const DPage& pg = pages[tile.x];
   if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
   const DChunk& ck = chunks[pg.chunk];
-  if (ck.phys != PT_BYTE_ARRAY || pg.enc != ENC_PLAIN || pg.n_chars == 0) return;
+  if (ck.phys != PT_BYTE_ARRAY || pg.enc != ENC_PLAIN) return;
   const DColumn& col = cols[ck.col];
+  uint64_t* vh = (col.vhash && !(dbg & 2)) ? col.vhash + pg.value_base : nullptr;
+  const int n = min(pg.n_values, tile.y + CT);
+  if (n <= tile.y || (pg.n_chars == 0 && !vh)) return;
   Layout L = page_layout(pg, ck, arena);
   const uint8_t* r = L.val_p;
   const int32_t* P = pos + pg.pos_base;
-  const int n = pg.n_values;
-  uint8_t* ob = col.chars + pg.char_base;
-  const long long nc = pg.n_chars;
-  const uintptr_t a_lo = (uintptr_t)ob & ~(uintptr_t)15;
-  const uintptr_t a_hi = (uintptr_t)ob + nc;
-  for (uintptr_t a = a_lo + (uintptr_t)threadIdx.x * 16; a < a_hi; a += (uintptr_t)NT * 16) {
-    const uintptr_t lo = a < (uintptr_t)ob ? (uintptr_t)ob : a;
-    const uintptr_t hi = (a + 16 < a_hi) ? a + 16 : a_hi;
-    long long o = (long long)(lo - (uintptr_t)ob);
-    // largest v with charpos(v) <= o
-    int vlo = 0, vhi = n - 1;
-    while (vlo < vhi) {
-      int mid = (vlo + vhi + 1) >> 1;
-      if ((long long)P[mid] - 4ll * mid <= o) vlo = mid; else vhi = mid - 1;
+  uint8_t* ob = (col.chars && !(dbg & 1)) ? col.chars + pg.char_base : nullptr;
+  const int t = threadIdx.x;
+  __shared__ uint4 inw[CT_BYTES / 16 + 2];
+  __shared__ uint4 outw[CT_BYTES / 16 + 2];
+  const uint32_t* in32 = (const uint32_t*)inw;
+  const uint8_t* in8 = (const uint8_t*)inw;
+  uint32_t* out32 = (uint32_t*)outw;
+  uint8_t* out8 = (uint8_t*)outw;
+  for (int v0 = tile.y; v0 < n;) {
+    const int32_t a0 = P[v0];
+    const int v = v0 + t;
+    const int32_t pv = v < n ? P[v] : 0, pv1 = v < n ? P[v + 1] : 0;
+    const bool fits = v < n && (pv1 - a0) <= CT_BYTES - 32;
+    const int cnt = __syncthreads_count(fits);      // fits is monotone in t
+    if (cnt == 0) {
+      // one value larger than the staging buffer: plain global copy, no hash
+      const int32_t len = P[v0 + 1] - a0 - 4;
+      if (ob) {
+        uint8_t* o = ob + (a0 - 4ll * v0);
+        for (int32_t j = t; j < len; j += CT) o[j] = r[a0 + 4 + j];
+      }
+      if (vh && t == 0) vh[v0] = 0;
+      v0 += 1;
+      __syncthreads();
+      continue;
     }
-    int v = vlo;
-    long long cp = (long long)P[v] - 4ll * v;
-    long long cn = (long long)P[v + 1] - 4ll * (v + 1);
-    uint8_t buf[16];
-    int nb = 0;
-    for (uintptr_t x = lo; x < hi; x++, o++) {
-      while (o >= cn) { v++; cp = cn; cn = (long long)P[v + 1] - 4ll * (v + 1); }
-      buf[nb++] = r[(long long)P[v] + 4 + (o - cp)];
+    const int32_t a1 = P[v0 + cnt];
+    const uintptr_t g0 = (uintptr_t)(r + a0);
+    const uintptr_t gb = g0 & ~(uintptr_t)15;
+    const int32_t mis = (int32_t)(g0 - gb);
+    const int nw = (mis + (a1 - a0) + 15) >> 4;
+    for (int i = t; i < nw; i += CT) inw[i] = ((const uint4*)gb)[i];
+    // page-local char range of the tile and the LDS placement of the output stream
+    const int32_t c0 = a0 - 4 * v0, c1 = a1 - 4 * (v0 + cnt);
+    const int32_t opad = ob ? (int32_t)(((uintptr_t)ob + c0) & 15) : 0;
+    __syncthreads();
+    if (fits) {
+      const int32_t len = pv1 - pv - 4;
+      const int32_t src = pv + 4 - a0 + mis;                  // value bytes in `in`
+      if (ob && len > 0) {
+        int32_t d = (pv - 4 * v) - c0 + opad;                 // value bytes in `out`
+        int32_t sidx = src, k = 0;
+        const int32_t head = min(len, (4 - (d & 3)) & 3);
+        for (; k < head; k++) out8[d + k] = in8[sidx + k];
+        d += head; sidx += head;
+        const int32_t nd = (len - head) >> 2;
+        const uint32_t sb = (uint32_t)(sidx & 3);
+        int32_t si = sidx >> 2;
+        uint32_t lo = in32[si];
+        uint32_t* od = out32 + (d >> 2);
+        for (int32_t i = 0; i < nd; i++) {
+          const uint32_t hi = in32[si + i + 1];
+          od[i] = __builtin_amdgcn_alignbyte(hi, lo, sb);
+          lo = hi;
+        }
+        for (k = head + 4 * nd; k < len; k++) out8[(pv - 4 * v) - c0 + opad + k] = in8[src + k];
+      }
+      if (vh) {
+        auto load8 = [&](int32_t j) -> uint64_t {
+          const int32_t b = src + 8 * j;
+          return (uint64_t)lds_u32_at(in32, b) | ((uint64_t)lds_u32_at(in32, b + 4) << 32);
+        };
+        uint64_t h = 0;
+        if (!simple_path_hash(len, load8, kDecodeSeed, &h)) h = 0;
+        vh[v] = h;
+      }
     }
-    if (lo == a && hi == a + 16) {
-      uint4 q;
-      q.x = buf[0] | (buf[1] << 8) | (buf[2] << 16) | ((uint32_t)buf[3] << 24);
-      q.y = buf[4] | (buf[5] << 8) | (buf[6] << 16) | ((uint32_t)buf[7] << 24);
-      q.z = buf[8] | (buf[9] << 8) | (buf[10] << 16) | ((uint32_t)buf[11] << 24);
-      q.w = buf[12] | (buf[13] << 8) | (buf[14] << 16) | ((uint32_t)buf[15] << 24);
-      *(uint4*)a = q;
-    } else {
-      for (int j = 0; j < nb; j++) ((uint8_t*)lo)[j] = buf[j];
+    __syncthreads();
+    if (ob && c1 > c0) {
+      const int32_t nb = opad + (c1 - c0);                   // bytes of `out` in use
+      uint8_t* gbase = ob + c0 - opad;                         // 16-aligned
+      for (int32_t q = t; q * 16 < nb; q += CT) {
+        const int32_t lo = q * 16, hi = lo + 16;
+        if (lo >= opad && hi <= nb) {
+          *(uint4*)(gbase + lo) = outw[q];
+        } else {
+          for (int32_t j = max(lo, opad); j < min(hi, nb); j++) gbase[j] = out8[j];
+        }
+      }
     }
+    __syncthreads();
+    v0 += cnt;
   }
 }
 
@@ -1081,17 +1171,45 @@ __global__ void k_json_select(const DJsonAction* __restrict__ acts, int n, const
 // K7: checkpoint probe — one lane per checkpoint row
 // --------------------------------------------------------------------------------------------
 
+// per-workgroup reduction of three counters (ScanMetrics slots 0, 2, 3) -> one atomic each
+__device__ __forceinline__ void block_count3(DState* st, unsigned long long a, unsigned long long b,
+                                             unsigned long long c) {
+  __shared__ unsigned long long red[3][NT / 64];
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); c += __shfl_down(c, o, 64);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) { red[0][w] = a; red[1][w] = b; red[2][w] = c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long x = 0, y = 0, z = 0;
+    for (int i = 0; i < NT / 64; i++) { x += red[0][i]; y += red[1][i]; z += red[2][i]; }
+    if (x) atomicAdd(&st->counters[0], x);
+    if (y) atomicAdd(&st->counters[2], y);
+    if (z) atomicAdd(&st->counters[3], z);
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
                                               const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
                                               uint32_t seed, uint8_t* __restrict__ sel, DState* __restrict__ st) {
-  long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const SimpleSet ss;
-  bool seen = false, chosen = false, dup = false;
-  if (r < pc.n_rows) {
+  // grid-stride over rows; the three counters are reduced per workgroup (one atomic each per
+  // workgroup: per-wave atomics on three addresses serialise at ~10 ns apiece)
+  unsigned long long n_seen = 0, n_chosen = 0, n_dup = 0;
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < pc.n_rows;
+       r += (long long)gridDim.x * blockDim.x) {
+    bool seen = false, chosen = false, dup = false;
     if (pc.path_def[r] >= 1) {
       seen = true;
-      const uint8_t* p = pc.path_chars + pc.path_offs[r];
-      int32_t pl = (int32_t)(pc.path_offs[r + 1] - pc.path_offs[r]);
+      uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
+      const uint8_t* p = nullptr;      // path bytes: needed only to hash (hp == 0) or verify a hit
+      int32_t pl = 0;
+      auto load_path = [&]() {
+        if (p) return;
+        const int64_t o0 = pc.path_offs[r];
+        p = pc.path_chars + o0;
+        pl = (int32_t)(pc.path_offs[r + 1] - o0);
+      };
       bool has_dv = pc.has_dv && pc.st_def[r] >= 2;
       const uint8_t* sp = nullptr; const uint8_t* pp = nullptr;
       int32_t sl = 0, ppl = 0, off = 0;
@@ -1102,9 +1220,9 @@ __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restri
         has_off = pc.off_def != nullptr && pc.off_def[r] == pc.off_maxdef;
         off = has_off ? pc.off_vals[r] : 0;
       }
-      uint64_t hp;
       int rc = 0;
-      {
+      if (!hp) {
+        load_path();
         // aligned 8-byte loads + funnel shift (no reliance on unaligned-access mode)
         const uintptr_t pa = (uintptr_t)p;
         const uint64_t* base = (const uint64_t*)(pa & ~(uintptr_t)7);
@@ -1115,7 +1233,7 @@ __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restri
           uint64_t w1 = base[j + 1];
           return (w0 >> sh) | (w1 << (64 - sh));
         };
-        if (!simple_path_hash(pl, load8, ss, seed, &hp)) rc = path_hash(p, pl, seed, &hp);
+        if (!simple_path_hash(pl, load8, seed, &hp)) rc = path_hash(p, pl, seed, &hp);
       }
       HashSink kd; kd.hs.init(kHashSeed(seed)); kd.n = 0;
       int rc2 = dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, kd);
@@ -1129,6 +1247,7 @@ __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restri
         while (slots[s].h != 0ull) {
           if (slots[s].h == h) {
             sl_ = slots[s];
+            load_path();
             const DJsonAction& a = acts[sl_.rep];
             CmpSink cmp{canon + a.canon_off, a.canon_len, 0, 1};
             uri_emit(p, pl, cmp);
@@ -1150,10 +1269,9 @@ __global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restri
       }
     }
     sel[r] = chosen;
+    n_seen += seen; n_chosen += chosen; n_dup += dup;
   }
-  wave_count(&st->counters[0], seen);
-  wave_count(&st->counters[2], chosen);
-  wave_count(&st->counters[3], dup);
+  block_count3(st, n_seen, n_chosen, n_dup);
 }
 
 }  // namespace dk
@@ -1170,25 +1288,27 @@ void launch_snappy(const DChunk* c, DPage* p, int n, uint8_t* arena, hipStream_t
   if (n) hipLaunchKernelGGL(k_snappy, dim3(n), dim3(64), 0, s, c, p, arena);
 }
 void launch_string_positions(const DChunk* c, DPage* p, int n, const uint8_t* arena, int32_t* pos, int mode,
-                             hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos, mode);
+                             hipStream_t s, int page0) {
+  if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos, mode, page0);
 }
-void launch_page_count(const DChunk* c, DPage* p, int n, const uint8_t* arena, const int32_t* pos, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_page_count, dim3(n), dim3(NT), 0, s, c, p, arena, pos);
+void launch_page_count(const DChunk* c, DPage* p, int n, const uint8_t* arena, const int32_t* pos, hipStream_t s,
+                       int page0) {
+  if (n) hipLaunchKernelGGL(k_page_count, dim3(n), dim3(NT), 0, s, c, p, arena, pos, page0);
 }
 void launch_column_scan(DColumn* cols, int ncols, DPage* p, DState* st, hipStream_t s) {
   if (ncols) hipLaunchKernelGGL(k_column_scan, dim3(ncols), dim3(NT), 0, s, cols, p, st);
 }
 void launch_page_decode(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
-                        const int32_t* pos, const long long* dbp, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_page_decode, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos, dbp);
+                        const int32_t* pos, const long long* dbp, hipStream_t s, int page0) {
+  if (n) hipLaunchKernelGGL(k_page_decode, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos, dbp, page0);
 }
 void launch_delta_decode(const DChunk* c, DPage* p, int n, const uint8_t* arena, long long* dbp, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_delta_decode, dim3(n), dim3(NT), 0, s, c, p, arena, dbp);
 }
-void launch_string_copy(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
-                        const int32_t* pos, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_string_copy, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos);
+void launch_string_copy(const DChunk* c, const DPage* p, int ntiles, const DColumn* cols, const uint8_t* arena,
+                        const int32_t* pos, const int2* tiles, hipStream_t s, int tile0) {
+  static const int dbg = getenv("DK_COPY_DBG") ? atoi(getenv("DK_COPY_DBG")) : 0;
+  if (ntiles) hipLaunchKernelGGL(k_string_copy, dim3(ntiles), dim3(CT), 0, s, c, p, cols, arena, pos, tiles, tile0, dbg);
 }
 void launch_json_canon(DJsonAction* a, int n, const uint8_t* jchars, uint8_t* canon, uint32_t seed, DState* st,
                        hipStream_t s) {
@@ -1209,9 +1329,11 @@ void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint8_t*
 }
 void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const DJsonAction* acts,
                   const uint8_t* canon, uint32_t seed, uint8_t* sel, DState* st, hipStream_t s) {
-  if (pc.n_rows)
-    hipLaunchKernelGGL(k_probe, dim3((unsigned)((pc.n_rows + NT - 1) / NT)), dim3(NT), 0, s, pc, slots, mask, acts,
-                       canon, seed, sel, st);
+  if (pc.n_rows) {
+    const long long want = (pc.n_rows + NT - 1) / NT;
+    const unsigned grid = (unsigned)(want < 2048 ? want : 2048);   // 256 CUs x 8 workgroups
+    hipLaunchKernelGGL(k_probe, dim3(grid), dim3(NT), 0, s, pc, slots, mask, acts, canon, seed, sel, st);
+  }
 }
 
 }  // namespace dk

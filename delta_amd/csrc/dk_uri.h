@@ -55,26 +55,32 @@ DK_HD uint16_t uri_class(uint8_t c) {
 }
 DK_HD bool cc_unres(uint16_t k) { return (k & (CC_DIGIT | CC_ALPHA | CC_MARK)) != 0; }
 
-// ---- 64-bit streaming hash over 8-byte little-endian words ----
+DK_HD uint64_t kHashSeed(uint32_t seed) { return 0x243F6A8885A308D3ull * (uint64_t)(seed + 1); }
+
+// ---- 64-bit streaming hash of a canonical stream ----
+// The stream's first byte (always a TAG_* byte) is absorbed on its own, then the remaining bytes
+// as 8-byte little-endian words, so for a plain relative path (stream = TAG_PATH + raw bytes) the
+// words are exactly the raw 8-byte words of the path. One 64-bit multiply per word.
 struct Hash64 {
   uint64_t h, buf;
-  int nb;
-  DK_HD void init(uint64_t seed) { h = seed ^ 0x9E3779B97F4A7C15ull; buf = 0; nb = 0; }
+  int nb, started;
+  DK_HD void init(uint64_t seed) { h = seed ^ 0x9E3779B97F4A7C15ull; buf = 0; nb = 0; started = 0; }
   DK_HD static uint64_t mixw(uint64_t h, uint64_t w) {
-    h ^= w * 0xC2B2AE3D27D4EB4Full;
-    h = (h << 31) | (h >> 33);
-    return h * 0x9E3779B97F4A7C15ull + 0x165667B19E3779F9ull;
+    h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 29);
   }
   DK_HD void word(uint64_t w) { h = mixw(h, w); }
   DK_HD void put(uint8_t b) {
+    if (!started) { started = 1; h = mixw(h, 0x100u | b); return; }
     buf |= (uint64_t)b << (8 * nb);
     if (++nb == 8) { word(buf); buf = 0; nb = 0; }
   }
-  DK_HD uint64_t final_(uint64_t total_len) {
-    uint64_t x = mixw(h, buf ^ (total_len << 3));
+  DK_HD static uint64_t fin(uint64_t h, uint64_t tail, uint64_t total_len) {
+    uint64_t x = mixw(mixw(h, tail), total_len);
     x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
-    return x ? x : 1;   // 0 marks an empty table slot
+    return x ? x : 1;   // 0 marks an empty table slot / "not computed"
   }
+  DK_HD uint64_t final_(uint64_t total_len) { return fin(h, buf, total_len); }
 };
 
 DK_HD uint64_t hash_combine(uint64_t a, uint64_t b) {
@@ -434,43 +440,52 @@ DK_HD int dv_emit(bool has_dv, const uint8_t* st, int32_t stn, const uint8_t* pi
   return 0;
 }
 
-DK_HD uint64_t kHashSeed(uint32_t seed) { return 0x243F6A8885A308D3ull * (uint64_t)(seed + 1); }
 
-// 128-bit membership bitmap of the fast-path class CC_SIMPLE (ASCII only).
-struct SimpleSet {
-  uint64_t lo, hi;
-  DK_HD SimpleSet() : lo(0), hi(0) {
-    for (int c = 1; c < 128; c++)
-      if (uri_class((uint8_t)c) & CC_SIMPLE) { if (c < 64) lo |= 1ull << c; else hi |= 1ull << (c - 64); }
-  }
-  DK_HD bool has(uint32_t c) const { return c < 64 ? ((lo >> c) & 1) : (c < 128 ? ((hi >> (c - 64)) & 1) : false); }
-};
+// Fast-path character class CC_SIMPLE (unreserved = alnum + "-_.!~*'()", plus "@&=+$,;/"),
+// tested 4 bytes at a time: ok(c) = LO[c & 15] & HI[c >> 4] != 0 for c < 0x80, one bit per high
+// nibble 2..7 (tables built from the class; the engine re-checks them against uri_class() at
+// creation). On the device each 16-entry lookup is two v_perm_b32 + one bit-select for 4 bytes.
+DK_HD uint32_t perm8(uint32_t t1, uint32_t t0, uint32_t sel) {   // bytes of sel in 0..7 -> (t1:t0)
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(t1, t0, sel);
+#else
+  uint64_t t = ((uint64_t)t1 << 32) | t0;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) r |= (uint32_t)((t >> (8 * ((sel >> (8 * i)) & 7))) & 0xff) << (8 * i);
+  return r;
+#endif
+}
+DK_HD bool simple4(uint32_t x) {
+  if (x & 0x80808080u) return false;
+  const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x07070707u;
+  const uint32_t l7 = lo & 0x07070707u, m = ((lo >> 3) & 0x01010101u) * 0xFFu;
+  const uint32_t rl = (perm8(0x3f3f3e3fu, 0x3e3e3f2eu, l7) & ~m) | (perm8(0x1d351715u, 0x173d3f3fu, l7) & m);
+  const uint32_t v = rl & perm8(0x20100804u, 0x02010000u, hi);
+  return ((v - 0x01010101u) & ~v & 0x80808080u) == 0;      // every byte non-zero
+}
+DK_HD bool simple8(uint64_t w) { return simple4((uint32_t)w) && simple4((uint32_t)(w >> 32)); }
 
 // Fast path of path_hash for plain relative paths: the stream is TAG_PATH followed by the raw
-// bytes, hashed one 8-byte word per step. `load8(i)` returns the little-endian bytes s[8i..8i+8)
-// (bytes past n are ignored). Returns false (nothing computed) when the string is not simple.
+// bytes; `load8(j)` returns the little-endian bytes s[8j..8j+8) (bytes past n are ignored).
+// Returns false (nothing computed) when the string is not simple (the generic parser decides).
 template <class Load8>
-DK_HD bool simple_path_hash(int32_t n, const Load8& load8, const SimpleSet& ss, uint32_t seed, uint64_t* out) {
+DK_HD bool simple_path_hash(int32_t n, const Load8& load8, uint32_t seed, uint64_t* out) {
   Hash64 hs; hs.init(kHashSeed(seed));
-  uint64_t prev = (uint64_t)TAG_PATH << 56;
-  const int32_t nchunks = (n + 7) >> 3;
-  for (int32_t j = 0; j < nchunks; j++) {
-    uint64_t c = load8(j);
-    int32_t valid = n - 8 * j < 8 ? n - 8 * j : 8;
-    for (int32_t b = 0; b < valid; b++) if (!ss.has((uint32_t)((c >> (8 * b)) & 0xff))) return false;
-    if (j == 0 && n >= 2 && (c & 0xffff) == 0x2f2f) return false;   // leading "//" = authority
-    if (valid == 8) { hs.word((prev >> 56) | (c << 8)); prev = c; }
-    else {
-      // final partial chunk: stream bytes left = 1 (carried) + valid
-      uint64_t tailw = (prev >> 56) | ((valid ? (c & ((1ull << (8 * valid)) - 1)) : 0) << 8);
-      hs.buf = tailw; hs.nb = valid + 1;
-      if (hs.nb == 8) { hs.word(hs.buf); hs.buf = 0; hs.nb = 0; }
-      *out = hs.final_((uint64_t)n + 1);
-      return true;
-    }
+  hs.h = Hash64::mixw(hs.h, 0x100u | TAG_PATH);
+  const int32_t nfull = n >> 3;
+  for (int32_t j = 0; j < nfull; j++) {
+    const uint64_t c = load8(j);
+    if (!simple8(c) || (j == 0 && (c & 0xffff) == 0x2f2f)) return false;   // leading "//" = authority
+    hs.word(c);
   }
-  hs.buf = prev >> 56; hs.nb = 1;
-  *out = hs.final_((uint64_t)n + 1);
+  uint64_t tail = 0;
+  if (n & 7) {
+    const uint64_t mask = (1ull << (8 * (n & 7))) - 1;
+    tail = load8(nfull) & mask;
+    if (!simple8(tail | (0x6161616161616161ull & ~mask))) return false;     // pad with 'a'
+    if (nfull == 0 && n >= 2 && (tail & 0xffff) == 0x2f2f) return false;
+  }
+  *out = Hash64::fin(hs.h, tail, (uint64_t)n + 1);
   return true;
 }
 

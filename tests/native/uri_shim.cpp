@@ -13,11 +13,12 @@ extern "C" int prod_path_hash(const uint8_t* s, int32_t n, uint32_t seed, uint64
   return dk::path_hash(s, n, seed, h);
 }
 extern "C" int prod_simple_hash(const uint8_t* s, int32_t n, uint32_t seed, uint64_t* h) {
-  dk::SimpleSet ss;
   auto load8 = [&](int32_t j) -> uint64_t {
     uint64_t w = 0;
     for (int b = 0; b < 8 && 8 * j + b < n; b++) w |= (uint64_t)s[8 * j + b] << (8 * b);
     return w;
   };
-  return dk::simple_path_hash(n, load8, ss, seed, h) ? 1 : 0;
+  return dk::simple_path_hash(n, load8, seed, h) ? 1 : 0;
 }
+extern "C" int prod_simple8(uint64_t w) { return dk::simple8(w) ? 1 : 0; }
+extern "C" int prod_uri_class_simple(uint32_t c) { return (dk::uri_class((uint8_t)c) & dk::CC_SIMPLE) ? 1 : 0; }

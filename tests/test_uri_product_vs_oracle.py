@@ -100,3 +100,15 @@ def test_simple_word_hash_equals_generic(shim):
     for s in [b"a:b", b"a%20", b"//x", b"a b", "é".encode()]:
         a = C.c_uint64()
         assert shim.prod_simple_hash(s, len(s), 3, C.byref(a)) == 0
+
+
+def test_simple8_nibble_tables_match_uri_class(shim):
+    """simple8 (v_perm nibble-table classifier) agrees with uri_class()&CC_SIMPLE for every byte value
+    in every byte position of the 8-byte word (other positions padded with a simple char)."""
+    shim.prod_simple8.argtypes = [C.c_uint64]
+    shim.prod_uri_class_simple.argtypes = [C.c_uint32]
+    for pos in range(8):
+        for c in range(256):
+            w = 0x6161616161616161 & ~(0xff << (8 * pos)) | (c << (8 * pos))
+            want = 1 if (0 < c < 128 and shim.prod_uri_class_simple(c)) else 0
+            assert shim.prod_simple8(w) == want, (pos, c)
