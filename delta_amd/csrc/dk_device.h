@@ -26,16 +26,45 @@ struct DPage {
   int32_t status, is_comp;
   int64_t data_off;      // absolute offset of the page body in the file
   int64_t unc_off;       // offset into the decompression arena, -1 = read in place (input)
-  // counts (k_page_count)
+  // totals (k_tile_scan1 / k_tile_scan2: sums over the page's level tiles)
   int32_t n_rows, n_entries, n_values, pad;
   int64_t n_chars;
-  // bases within the column (k_column_scan)
+  // bases within the column (first tile's bases)
   int64_t row_base, entry_base, value_base, char_base;
   int64_t pos_base;      // string positions scratch offset (input, int32 per value + 1)
+  // run tables of the RLE/bit-packed hybrid streams (k_page_runs), offsets into the run scratch
+  // (input): rep levels, def levels, dictionary indices / RLE booleans; run_cap runs each
+  // (standard writers emit >= 8 values per run; more runs -> PS_UNSUPPORTED)
+  int64_t run_r, run_d, run_i;
+  int32_t run_cap, nrun_r, nrun_d, nrun_i;
+  int32_t idx_cover;     // values covered by the index stream's runs
+  int32_t first_tile, n_tiles;   // level tiles of this page (input)
+  int32_t pad2;
+  int64_t vbytes;        // bytes of the value section (after the levels)
 };
+
+// One run of an RLE/bit-packed hybrid stream: values [start, next.start) are `val` (RLE,
+// bp_idx < 0) or bit-packed from byte bp_off (relative to the page data start) on.
+struct Seg {
+  int32_t start;
+  int32_t bp_idx;
+  uint32_t val;
+  uint32_t bp_off;
+};
+
+// A level tile: DK_LEVEL_TILE consecutive levels of one data page (one workgroup per tile in
+// every level pass). Counts from k_tile_count / k_tile_chars, column bases from the scans.
+struct DTile {
+  int32_t page, lvl0;    // (input)
+  int32_t n_rows, n_entries, n_values, pad;
+  int64_t n_chars;
+  int64_t row_base, entry_base, value_base, char_base;
+};
+constexpr int DK_LEVEL_TILE = 2048;
 
 struct DColumn {
   int32_t first_page, n_pages;   // data pages, contiguous in the page table, in file order
+  int32_t first_tile, n_tiles;   // level tiles, contiguous, in page order
   int32_t phys, width, max_def, max_rep, rep_def, present;
   int32_t null_only;         // no value anywhere -> no value buffers are materialised
   int32_t key_hash;          // 1: this is the reconciliation key column (add.path) -> emit path hashes
@@ -46,10 +75,10 @@ struct DColumn {
   uint8_t* fixed;
   int64_t* offs;
   uint8_t* chars;
-  int64_t n_entries, n_chars;    // totals (k_column_scan)
+  int64_t n_entries, n_chars;    // totals (k_tile_scan1 / k_tile_scan2)
   int64_t cap_entries, cap_chars;
   // key_hash columns only: canonical-path hash (seed kDecodeSeed) per value (scratch, filled by
-  // k_string_copy for PLAIN pages, 0 = not computed) and per row (forwarded by k_page_decode;
+  // k_string_copy for PLAIN pages, 0 = not computed) and per row (forwarded by k_tile_decode;
   // 0 = null row or "compute in the probe")
   uint64_t* vhash;
   uint64_t* hash;

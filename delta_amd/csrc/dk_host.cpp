@@ -21,9 +21,12 @@ namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const DChunk*, DPage*, int, uint8_t*, hipStream_t);
 void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, int, hipStream_t, int);
-void launch_page_count(const DChunk*, DPage*, int, const uint8_t*, const int32_t*, hipStream_t, int);
-void launch_column_scan(DColumn*, int, DPage*, DState*, hipStream_t);
-void launch_page_decode(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const long long*, hipStream_t, int);
+void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
+void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
+void launch_tile_scan1(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
+void launch_tile_chars(const DChunk*, DPage*, const uint8_t*, const int32_t*, const Seg*, DTile*, int, int, hipStream_t);
+void launch_tile_scan2(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
+void launch_tile_decode(const DChunk*, DPage*, const DColumn*, const uint8_t*, const int32_t*, const long long*, const Seg*, const DTile*, int, int, DState*, hipStream_t);
 void launch_delta_decode(const DChunk*, DPage*, int, const uint8_t*, long long*, hipStream_t);
 void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const int2*, hipStream_t, int);
 void launch_json_canon(DJsonAction*, int, const uint8_t*, uint8_t*, uint32_t, DState*, hipStream_t);
@@ -294,11 +297,12 @@ static int phys_width(int phys, int tl) {
 // kernel timing (HIP events on the engine stream)
 // ------------------------------------------------------------------------------------------------
 struct KTimer {
-  static constexpr int K = 16;
-  const char* names[K] = {"k_page_headers", "k_string_positions_dict", "k_page_count", "k_column_scan",
-                          "k_string_positions", "k_page_decode", "k_string_copy", "k_json_canon",
+  static constexpr int K = 20;
+  const char* names[K] = {"k_page_headers", "k_string_positions_dict", "k_tile_count", "k_tile_scan",
+                          "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
-                          "k_snappy", "k_delta_decode", nullptr};
+                          "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", nullptr, nullptr,
+                          nullptr};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -347,6 +351,8 @@ struct dk_parquet {
   std::vector<DColumn> h_cols;
   std::vector<int> col_file;
   DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp, d_tiles;
+  DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
+  int n_ltiles = 0;
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
   std::vector<int> col_tile0;
@@ -378,18 +384,28 @@ static int read_file(const std::string& path, std::vector<uint8_t>& out) {
   return 0;
 }
 
-// Per-page kernels are launched once over every page, or -- with DK_SPLIT_LAUNCH=1, a profiling
-// aid -- once per column so that rocprofv3's kernel trace attributes time to columns.
+// Per-page and per-tile kernels are launched once over every page / tile, or -- with
+// DK_SPLIT_LAUNCH=1, a profiling aid -- once per column so that rocprofv3's kernel trace
+// attributes time to columns.
+static bool split_launch() {
+  static const bool split = getenv("DK_SPLIT_LAUNCH") && atoi(getenv("DK_SPLIT_LAUNCH")) != 0;
+  return split;
+}
 template <class F>
 static void per_column(const dk_parquet* p, int n, F&& f) {
-  static const bool split = getenv("DK_SPLIT_LAUNCH") && atoi(getenv("DK_SPLIT_LAUNCH")) != 0;
-  if (!split) { f(0, n); return; }
+  if (!split_launch()) { f(0, n); return; }
   int covered = 0;
   for (const DColumn& c : p->h_cols) { f(c.first_page, c.n_pages); covered += c.n_pages; }
   if (covered < n) f(covered, n - covered);    // dictionary pages (after every data page)
 }
+template <class F>
+static void per_column_tiles(const dk_parquet* p, F&& f) {
+  if (!split_launch()) { f(0, p->n_ltiles); return; }
+  for (const DColumn& c : p->h_cols) f(c.first_tile, c.n_tiles);
+}
 
-// the decode pipeline (mode: 0 = prepare pass up to the scan; 1 = full step)
+// the decode pipeline (mode: -1 = headers only; 0 = prepare pass through the scans, which size the
+// outputs; 1 = full step)
 static int run_pipeline(dk_parquet* p, int mode) {
   hipStream_t s = p->eng->stream;
   KTimer& T = p->timer;
@@ -400,27 +416,31 @@ static int run_pipeline(dk_parquet* p, int mode) {
   DState* st = p->d_state.as<DState>();
   DColumn* cols = p->d_cols.as<DColumn>();
   const long long* dbp = p->d_dbp.as<long long>();
+  DTile* LT = p->d_ltiles.as<DTile>();
+  Seg* runs = p->d_runs.as<Seg>();
   int n = p->n_pages;
   { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
   if (mode == -1) return 0;
   if (p->has_compressed) { KTimer::Scope sc(&T, 13, s); launch_snappy(C, P, n, p->d_arena.as<uint8_t>(), s); }
+  { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P, n, arena, runs, s); }
   { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, 1, s, 0); }  // dictionary pages
-  { KTimer::Scope sc(&T, 2, s); per_column(p, n, [&](int a, int k) { launch_page_count(C, P, k, arena, pos, s, a); }); }
-  { KTimer::Scope sc(&T, 3, s); launch_column_scan(cols, p->n_cols, P, st, s); }
-  if (mode == 0) return 0;
+  { KTimer::Scope sc(&T, 2, s); per_column_tiles(p, [&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols, p->n_cols, P, LT, st, s); }
   { KTimer::Scope sc(&T, 4, s); per_column(p, n, [&](int a, int k) { launch_string_positions(C, P, k, arena, pos, 2, s, a); }); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P, n, arena, p->d_dbp.as<long long>(), s); }
-  // string copy first: it fills the key column's per-value hashes that k_page_decode forwards
+  { KTimer::Scope sc(&T, 16, s); per_column_tiles(p, [&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols, p->n_cols, P, LT, st, s); }
+  if (mode == 0) return 0;
+  // string copy first: it fills the key column's per-value hashes that k_tile_decode forwards
   {
     KTimer::Scope sc(&T, 6, s);
-    static const bool split = getenv("DK_SPLIT_LAUNCH") && atoi(getenv("DK_SPLIT_LAUNCH")) != 0;
     const int2* tiles = p->d_tiles.as<int2>();
-    if (!split) launch_string_copy(C, P, p->col_tile0.back(), cols, arena, pos, tiles, s, 0);
+    if (!split_launch()) launch_string_copy(C, P, p->col_tile0.back(), cols, arena, pos, tiles, s, 0);
     else
       for (int c = 0; c < p->n_cols; c++)
         launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c]);
   }
-  { KTimer::Scope sc(&T, 5, s); per_column(p, n, [&](int a, int k) { launch_page_decode(C, P, k, cols, arena, pos, dbp, s, a); }); }
+  { KTimer::Scope sc(&T, 5, s); per_column_tiles(p, [&](int a, int k) { launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, k, a, st, s); }); }
   return 0;
 }
 
@@ -478,6 +498,34 @@ static int prepare(dk_parquet* p) {
       else pg.pos_base = posn;
       posn += (int64_t)pg.num_values + 1;
     }
+  }
+  // level tiles and run-table scratch (standard writers emit >= 8 values per hybrid run; a stream
+  // with more than num_values / 4 + 64 runs is reported as unsupported)
+  {
+    std::vector<DTile> tiles;
+    int64_t runs_n = 0;
+    for (DColumn& c : p->h_cols) {
+      c.first_tile = (int)tiles.size();
+      for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
+        DPage& pg = p->h_pages[pi];
+        const DChunk& ck = p->h_chunks[pg.chunk];
+        const int nv = pg.num_values > 0 ? pg.num_values : 0;
+        const int cap = nv / 4 + 64;
+        const bool idx = pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT || (ck.phys == PT_BOOLEAN && pg.enc == ENC_RLE);
+        pg.run_cap = cap;
+        pg.run_r = pg.run_d = pg.run_i = 0;
+        if (ck.max_rep > 0) { pg.run_r = runs_n; runs_n += cap; }
+        if (ck.max_def > 0) { pg.run_d = runs_n; runs_n += cap; }
+        if (idx) { pg.run_i = runs_n; runs_n += cap; }
+        pg.first_tile = (int)tiles.size();
+        for (int l0 = 0; l0 < nv; l0 += DK_LEVEL_TILE) { DTile tl{}; tl.page = pi; tl.lvl0 = l0; tiles.push_back(tl); }
+        pg.n_tiles = (int)tiles.size() - pg.first_tile;
+      }
+      c.n_tiles = (int)tiles.size() - c.first_tile;
+    }
+    p->n_ltiles = (int)tiles.size();
+    if (upload(p->d_ltiles, tiles.data(), tiles.size() * sizeof(DTile), s)) return 1;
+    if (p->d_runs.alloc((size_t)(runs_n + 1) * sizeof(Seg))) return 1;
   }
   if (p->d_pos.alloc((size_t)(posn + 16) * 4)) return 1;
   if (p->d_arena.alloc((size_t)arena_n + 256)) return 1;
@@ -1354,7 +1402,7 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
 extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {
   if (i < 0 || i >= KTimer::K) return 1;
   // decode kernels are timed by the parquet object's timer, the rest by the replay's
-  const KTimer* t = (r->ck && (i <= 6 || i == 13 || i == 14)) ? &r->ck->timer : &r->timer;
+  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16))) ? &r->ck->timer : &r->timer;
   *name = t->names[i];
   if (!*name) return 1;
   *count = t->cnt[i];

@@ -1,17 +1,20 @@
 // CDNA4 (gfx950) kernels for checkpoint decode + log-replay reconciliation.
 //
-// Work unit = one Parquet page (one 256-thread workgroup, 4 wave64s). Everything here is
-// byte/integer work bounded by HBM bandwidth; there is no dense contraction, so no MFMA.
-// Pipeline per replay step (see DESIGN.md §3):
+// Work units: level tiles of DK_LEVEL_TILE levels (level passes), 128-value tiles (string copy),
+// pages (header parse, snappy, string positions, run tables). Everything here is byte/integer
+// work bounded by HBM bandwidth; there is no dense contraction, so no MFMA.
+// Pipeline per replay step (see DESIGN.md):
 //   k_page_headers      Thrift PageHeader parse, one lane per page
+//   k_snappy            raw snappy blocks, one wave per compressed page
+//   k_page_runs         run tables of the rep / def / dictionary-index hybrid streams
 //   k_string_positions  PLAIN BYTE_ARRAY entry positions: speculative zero-run candidates +
 //                       exact chain verification, sequential fallback
-//   k_page_count        RLE/bit-packed hybrid level decode -> rows / entries / values / chars
-//   k_column_scan       per-column exclusive scan of page counts
-//   k_page_decode       levels + values -> row_def / row_offs / entry_def / fixed / offs
-//   k_string_copy       PLAIN string bytes -> contiguous chars (16 B aligned stores)
+//   k_tile_count / k_tile_scan1 / k_tile_chars / k_tile_scan2   rows, entries, values, chars
+//   k_delta_decode      DELTA_BINARY_PACKED
+//   k_string_copy       PLAIN string bytes -> contiguous chars + key-path hashes
+//   k_tile_decode       levels + values -> row_def / row_offs / entry_def / fixed / offs
 //   k_json_canon / k_table_insert / k_table_update / k_json_select   commit-tail keys
-//   k_probe             checkpoint add rows: URI-canonical key hash, probe, verify, select
+//   k_probe             checkpoint add rows: key hash, probe, verify, select
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -22,8 +25,6 @@
 namespace dk {
 
 constexpr int NT = 256;          // threads per workgroup
-constexpr int LW = 512;          // levels per window (2 per thread)
-constexpr int MAXSEG = 512;
 
 // --------------------------------------------------------------------------------------------
 // small helpers
@@ -33,21 +34,22 @@ __device__ __forceinline__ const uint8_t* page_data(const DPage& pg, const DChun
 }
 __device__ __forceinline__ int32_t page_len(const DPage& pg) { return pg.unc_off >= 0 ? pg.usize : pg.csize; }
 
+// 4 bytes at any address: two aligned dword loads + v_alignbyte (buffers are padded past the end)
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
-  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3);
+  return sh ? __builtin_amdgcn_alignbyte(w[1], w[0], sh) : w[0];
 }
 
 __device__ __forceinline__ uint32_t read_bits(const uint8_t* p, int64_t bit, int bw, const uint8_t* e) {
   if (bw == 0) return 0;
   const uint8_t* q = p + (bit >> 3);
-  int sh = (int)(bit & 7);
-  int nb = (sh + bw + 7) >> 3;
+  const int sh = (int)(bit & 7);
   uint64_t w = 0;
-  for (int k = 0; k < nb; k++) {
-    const uint8_t* a = q + k;
-    if (a < e) w |= (uint64_t)(*a) << (8 * k);
-  }
-  uint64_t mask = (bw >= 32) ? 0xffffffffull : ((1ull << bw) - 1);
+  if (q + 8 <= e) w = (uint64_t)ld_u32(q) | ((uint64_t)ld_u32(q + 4) << 32);
+  else for (int k = 0; k < 8 && q + k < e; k++) w |= (uint64_t)q[k] << (8 * k);
+  const uint64_t mask = (bw >= 32) ? 0xffffffffull : ((1ull << bw) - 1);
   return (uint32_t)((w >> sh) & mask);
 }
 
@@ -91,89 +93,6 @@ __device__ __forceinline__ long long block_scan64(long long v, long long* total,
   __syncthreads();
   *total = tot;
   return base + x - v;
-}
-
-// --------------------------------------------------------------------------------------------
-// RLE / bit-packed hybrid: one lane walks run headers, all lanes expand
-// --------------------------------------------------------------------------------------------
-struct Hyb {
-  const uint8_t* p;
-  const uint8_t* e;
-  const uint8_t* bp;
-  int32_t bw, left, is_bp, bp_idx;
-  uint32_t val;
-  int32_t err;
-};
-struct Seg {
-  int32_t start;     // first output index covered (window-local)
-  int32_t bp_idx;    // index within the bit-packed run, or -1 for an RLE run
-  uint32_t val;      // RLE value
-  uint32_t bp_off;   // bit-packed run data offset from Hyb.base
-};
-
-__device__ __forceinline__ void hyb_init(Hyb& h, const uint8_t* p, const uint8_t* e, int bw) {
-  h.p = p; h.e = e; h.bp = p; h.bw = bw; h.left = 0; h.is_bp = 0; h.bp_idx = 0; h.val = 0; h.err = 0;
-}
-
-// lane-serial: produce segments covering up to `want` values; returns number covered
-__device__ int hyb_fill(Hyb& h, const uint8_t* base, Seg* seg, int want, int* nseg) {
-  int got = 0, ns = 0;
-  while (got < want && ns < MAXSEG) {
-    if (h.left == 0) {
-      if (h.p >= h.e) { h.err = 1; break; }
-      uint64_t hdr = 0;
-      int s = 0;
-      for (;;) {
-        if (h.p >= h.e) { h.err = 1; *nseg = ns; return got; }
-        uint8_t b = *h.p++;
-        hdr |= (uint64_t)(b & 0x7f) << s;
-        if (!(b & 0x80)) break;
-        s += 7;
-        if (s > 35) { h.err = 1; *nseg = ns; return got; }
-      }
-      if (hdr & 1) {
-        int64_t groups = (int64_t)(hdr >> 1);
-        h.is_bp = 1; h.left = (int32_t)(groups * 8); h.bp = h.p; h.bp_idx = 0;
-        h.p += groups * h.bw;
-        if (h.p > h.e) h.p = h.e;   // truncated final run: values past the end are never used
-      } else {
-        h.is_bp = 0; h.left = (int32_t)(hdr >> 1);
-        int nb = (h.bw + 7) >> 3;
-        uint32_t v = 0;
-        for (int k = 0; k < nb; k++) {
-          if (h.p >= h.e) { h.err = 1; *nseg = ns; return got; }
-          v |= (uint32_t)(*h.p++) << (8 * k);
-        }
-        h.val = v;
-      }
-      if (h.left == 0) continue;
-    }
-    int take = min(h.left, want - got);
-    Seg sg;
-    sg.start = got;
-    sg.bp_idx = h.is_bp ? h.bp_idx : -1;
-    sg.val = h.val;
-    sg.bp_off = (uint32_t)(h.bp - base);
-    seg[ns++] = sg;
-    got += take;
-    h.left -= take;
-    if (h.is_bp) h.bp_idx += take;
-  }
-  *nseg = ns;
-  return got;
-}
-
-__device__ __forceinline__ uint32_t seg_value(const Seg* seg, int nseg, int i, int bw, const uint8_t* base,
-                                              const uint8_t* e) {
-  int lo = 0, hi = nseg - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (seg[mid].start <= i) lo = mid; else hi = mid - 1;
-  }
-  const Seg s = seg[lo];
-  if (s.bp_idx < 0) return s.val;
-  int64_t bit = (int64_t)(s.bp_idx + (i - s.start)) * bw;
-  return read_bits(base + s.bp_off, bit, bw, e);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -255,16 +174,17 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
 // --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                uint8_t* __restrict__ arena) {
-  DPage& pg = pages[blockIdx.x];
+  DPage& pgw = pages[blockIdx.x];
+  const DPage pg = pgw;                            // by value: byte stores below may alias
   if (pg.unc_off < 0 || pg.status != PS_OK) return;
-  const DChunk& ck = chunks[pg.chunk];
+  const DChunk ck = chunks[pg.chunk];
   const int lane = threadIdx.x;
   const uint8_t* in = ck.file + pg.data_off;
   int64_t clen = pg.csize;
   uint8_t* out = arena + pg.unc_off;
   int64_t ulen = pg.usize;
   const int64_t lv = (pg.ptype == PAGE_DATA_V2) ? (int64_t)pg.rl_len + pg.dl_len : 0;
-  if (lv > clen || lv > ulen) { if (lane == 0) pg.status = PS_BAD_SNAPPY; return; }
+  if (lv > clen || lv > ulen) { if (lane == 0) pgw.status = PS_BAD_SNAPPY; return; }
   for (int64_t i = lane; i < lv; i += 64) out[i] = in[i];
   in += lv; clen -= lv; out += lv; ulen -= lv;
   if (pg.ptype == PAGE_DATA_V2 && !pg.is_comp) {
@@ -332,7 +252,7 @@ __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks
     o += len;
   }
   if (o != ulen) bad = true;
-  if (bad && lane == 0) pg.status = PS_BAD_SNAPPY;
+  if (bad && lane == 0) pgw.status = PS_BAD_SNAPPY;
 }
 
 // --------------------------------------------------------------------------------------------
@@ -346,8 +266,8 @@ __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks
 __global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                          const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
                                                          int mode, int page0) {
-  const DPage& pg = pages[page0 + blockIdx.x];
-  const DChunk& ck = chunks[pg.chunk];
+  const DPage pg = pages[page0 + blockIdx.x];      // by value: byte stores below may alias
+  const DChunk ck = chunks[pg.chunk];
   if (ck.phys != PT_BYTE_ARRAY || pg.status != PS_OK) return;
   const bool dict = (pg.flags & PF_DICT) != 0;
   if (dict != (mode == 1)) return;   // mode 1: dictionary pages, mode 2: data pages
@@ -441,43 +361,6 @@ __global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restric
   if (t == 0) P[n] = (int32_t)R;
 }
 
-// --------------------------------------------------------------------------------------------
-// shared window machinery for the count / decode passes
-// --------------------------------------------------------------------------------------------
-struct WinLds {
-  Hyb hr, hd, hi;
-  Seg segr[MAXSEG];
-  Seg segd[MAXSEG];
-  Seg segi[MAXSEG];
-  int nr, nd, ni, win, err;
-  int scan[12];
-  long long scan64[4];
-};
-
-// lane 0: fill rep+def segments for the next window; sets W.win
-__device__ __forceinline__ void fill_levels(WinLds& W, const Layout& L, const DChunk& ck, int remaining) {
-  int want = min(LW, remaining);
-  int got = want;
-  if (ck.max_rep > 0) {
-    got = hyb_fill(W.hr, L.d, W.segr, want, &W.nr);
-  }
-  if (ck.max_def > 0) {
-    int gd = hyb_fill(W.hd, L.d, W.segd, got, &W.nd);
-    if (gd < got) {
-      if (ck.max_rep > 0) W.err = 1;   // rep stream over-advanced: unsupported pathological runs
-      got = gd;
-    }
-  }
-  if (got <= 0) W.err = 1;
-  W.win = got;
-}
-
-__device__ __forceinline__ void level_at(const WinLds& W, const Layout& L, const DChunk& ck, int i, int bwr, int bwd,
-                                         int* rep, int* def) {
-  *rep = ck.max_rep > 0 ? (int)seg_value(W.segr, W.nr, i, bwr, L.d, L.rep_e) : 0;
-  *def = ck.max_def > 0 ? (int)seg_value(W.segd, W.nd, i, bwd, L.d, L.def_e) : 0;
-}
-
 __device__ __forceinline__ const uint8_t* dict_data(const DChunk& ck, const DPage* pages, const uint8_t* arena,
                                                     int32_t* dict_n) {
   const DPage& dp = pages[ck.dict_page];
@@ -523,9 +406,10 @@ __device__ __forceinline__ uint64_t uvarint(const uint8_t*& p, const uint8_t* e,
 
 __global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                      const uint8_t* __restrict__ arena, long long* __restrict__ dbp) {
-  DPage& pg = pages[blockIdx.x];
+  DPage& pgw = pages[blockIdx.x];
+  const DPage pg = pgw;                            // by value: stores below may alias
   if ((pg.flags & PF_DICT) || pg.status != PS_OK || pg.enc != ENC_DELTA_BP) return;
-  const DChunk& ck = chunks[pg.chunk];
+  const DChunk ck = chunks[pg.chunk];
   if (ck.phys != PT_INT32 && ck.phys != PT_INT64) return;
   Layout L = page_layout(pg, ck, arena);
   const int t = threadIdx.x;
@@ -548,7 +432,7 @@ __global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ 
     if (n > 0 && !err) out[0] = ck.phys == PT_INT32 ? (long long)(int32_t)first : first;
   }
   __syncthreads();
-  if (S.err) { if (t == 0) pg.status = PS_BAD_VALUES; return; }
+  if (S.err) { if (t == 0) pgw.status = PS_BAD_VALUES; return; }
   const int per_mini = (int)(s_block / s_nmini);
   const int nmini_blk = (int)s_nmini;
   const long long ndelta = n > 0 ? n - 1 : 0;
@@ -629,304 +513,513 @@ __global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ 
     d0 += win;
     __syncthreads();
   }
-  if (S.err && t == 0) pg.status = PS_BAD_VALUES;
+  if (S.err && t == 0) pgw.status = PS_BAD_VALUES;
 }
 
 // --------------------------------------------------------------------------------------------
-// K3: counts per data page
+// Level pipeline, tile-parallel. Every data page is cut into level tiles of TL levels and every
+// level pass runs one workgroup per tile (a 10M-row column is ~5k workgroups, so the chip fills):
+//   k_page_runs    one lane per data page walks the run headers of its rep / def level streams
+//                  and of its dictionary-index (or RLE boolean) stream into run tables (Seg)
+//   k_tile_count   rows / entries / values of each tile
+//   k_tile_scan1   one workgroup per column: exclusive scan over its tiles -> tile bases; page
+//                  totals and bases
+//   k_tile_chars   BYTE_ARRAY tiles: chars of the tile's values (PLAIN: from the positions,
+//                  dictionary: sum of the entry lengths)
+//   k_tile_scan2   chars scan -> char bases, column totals and checks
+//   k_tile_decode  levels + values -> row_def / row_offs / entry_def / fixed / offs; dictionary
+//                  strings are copied cooperatively into 16-byte aligned output chunks
+// Record assembly follows kernel-defaults' converters (RowColumnReader.java:106-131,
+// RepeatedValueConverter.java:65-81, ParquetColumnReaders.java:155-478): a row starts at rep 0,
+// an entry exists at def >= rep_def, a value at def == max_def.
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_page_count(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                                   const uint8_t* __restrict__ arena, const int32_t* __restrict__ pos, int page0) {
-  DPage& pg = pages[page0 + blockIdx.x];
-  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
-  const DChunk& ck = chunks[pg.chunk];
-  __shared__ WinLds W;
-  const int t = threadIdx.x;
-  Layout L = page_layout(pg, ck, arena);
-  if (!L.ok) { if (t == 0) pg.status = PS_BAD_LEVELS; return; }
-  const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
-  if (t == 0) {
-    hyb_init(W.hr, L.rep_p, L.rep_e, bwr);
-    hyb_init(W.hd, L.def_p, L.def_e, bwd);
-    W.err = 0;
+constexpr int TL = DK_LEVEL_TILE;
+constexpr int LPT = TL / NT;           // levels per thread
+
+// lane-serial walk of one hybrid stream's run headers; returns the number of runs, *cover = values
+// covered. strict: the stream must cover `limit` values (levels), else PS_BAD_LEVELS.
+__device__ int walk_runs(const uint8_t* p, const uint8_t* e, const uint8_t* base, int bw, int64_t limit,
+                         Seg* out, int cap, bool strict, int* bad, int* cover) {
+  int64_t got = 0;
+  int n = 0;
+  const int nb = (bw + 7) >> 3;
+  while (got < limit) {
+    if (p >= e) { if (strict) *bad = PS_BAD_LEVELS; break; }
+    int err = 0;
+    const uint64_t hdr = uvarint(p, e, &err);
+    if (err) { if (strict) *bad = PS_BAD_LEVELS; break; }
+    Seg sg;
+    int64_t cnt;
+    if (hdr & 1) {
+      cnt = (int64_t)(hdr >> 1) * 8;
+      sg.bp_idx = 0; sg.val = 0; sg.bp_off = (uint32_t)(p - base);
+      const int64_t adv = (int64_t)(hdr >> 1) * bw;
+      p = (e - p) < adv ? e : p + adv;     // truncated final run: values past the end are unused
+    } else {
+      cnt = (int64_t)(hdr >> 1);
+      if (p + nb > e) { if (strict) *bad = PS_BAD_LEVELS; break; }
+      uint32_t v = 0;
+      for (int k = 0; k < nb; k++) v |= (uint32_t)p[k] << (8 * k);
+      p += nb;
+      sg.bp_idx = -1; sg.val = v; sg.bp_off = 0;
+    }
+    if (cnt == 0) continue;
+    if (n >= cap) { *bad = PS_UNSUPPORTED; break; }
+    sg.start = (int32_t)got;
+    out[n++] = sg;
+    got += cnt;
   }
-  __syncthreads();
-  int rows = 0, ents = 0, vals = 0;
+  *cover = (int)(got < 0x7fffffff ? got : 0x7fffffff);
+  return n;
+}
+
+// cursor over a run table for non-decreasing indices
+struct RunCur {
+  const Seg* R;
+  int n, k, next;
+  Seg cur;
+  __device__ __forceinline__ void init(const Seg* R_, int n_, int i) {
+    R = R_; n = n_;
+    int lo = 0, hi = n_ - 1;
+    while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (R_[mid].start <= i) lo = mid; else hi = mid - 1; }
+    k = lo;
+    cur = R_[k];
+    next = k + 1 < n_ ? R_[k + 1].start : 0x7fffffff;
+  }
+  __device__ __forceinline__ uint32_t get(int i, int bw, const uint8_t* base, const uint8_t* e) {
+    while (i >= next) { k++; cur = R[k]; next = k + 1 < n ? R[k + 1].start : 0x7fffffff; }
+    if (cur.bp_idx < 0) return cur.val;
+    return read_bits(base + cur.bp_off, (int64_t)(i - cur.start) * bw, bw, e);
+  }
+};
+
+__global__ void k_page_runs(const DChunk* __restrict__ chunks, DPage* __restrict__ pages, int n_pages,
+                            const uint8_t* __restrict__ arena, Seg* __restrict__ runs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pages) return;
+  const DPage pg = pages[i];
+  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
+  const DChunk ck = chunks[pg.chunk];
+  const Layout L = page_layout(pg, ck, arena);
+  int nr = 0, nd = 0, ni = 0, bad = 0, cov = 0, icov = 0;
+  if (!L.ok) bad = PS_BAD_LEVELS;
   const int nv = pg.num_values;
-  for (int w0 = 0; w0 < nv;) {
-    if (t == 0) fill_levels(W, L, ck, nv - w0);
-    __syncthreads();
-    const int win = W.win;
-    if (W.err) break;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      int i = t * 2 + k;
-      if (i < win) {
-        int rep, def;
-        level_at(W, L, ck, i, bwr, bwd, &rep, &def);
-        rows += (rep == 0);
-        ents += (def >= ck.rep_def);
-        vals += (def == ck.max_def);
+  if (!bad && ck.max_rep > 0)
+    nr = walk_runs(L.rep_p, L.rep_e, L.d, bit_width(ck.max_rep), nv, runs + pg.run_r, pg.run_cap, true, &bad, &cov);
+  if (!bad && ck.max_def > 0)
+    nd = walk_runs(L.def_p, L.def_e, L.d, bit_width(ck.max_def), nv, runs + pg.run_d, pg.run_cap, true, &bad, &cov);
+  if (!bad && L.val_p < L.val_e) {
+    if (pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) {
+      const int ibw = *L.val_p;
+      if (ibw > 32) bad = PS_BAD_VALUES;
+      else ni = walk_runs(L.val_p + 1, L.val_e, L.d, ibw, nv, runs + pg.run_i, pg.run_cap, false, &bad, &icov);
+    } else if (ck.phys == PT_BOOLEAN && pg.enc == ENC_RLE && L.val_p + 4 <= L.val_e) {
+      ni = walk_runs(L.val_p + 4, L.val_e, L.d, 1, nv, runs + pg.run_i, pg.run_cap, false, &bad, &icov);
+    }
+  }
+  DPage& o = pages[i];
+  o.nrun_r = nr; o.nrun_d = nd; o.nrun_i = ni; o.idx_cover = icov;
+  o.vbytes = L.ok ? (int64_t)(L.val_e - L.val_p) : 0;
+  if (bad) o.status = bad;
+}
+
+// encodings the value decoder supports for this page (values present)
+__device__ __forceinline__ bool enc_supported(const DPage& pg, const DChunk& ck) {
+  const bool dict = (pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) && ck.dict_page >= 0;
+  if (ck.phys == PT_BYTE_ARRAY) return pg.enc == ENC_PLAIN || dict;
+  return pg.enc == ENC_PLAIN || dict || (pg.enc == ENC_RLE && ck.phys == PT_BOOLEAN) ||
+         (pg.enc == ENC_DELTA_BP && (ck.phys == PT_INT32 || ck.phys == PT_INT64));
+}
+
+__global__ __launch_bounds__(NT) void k_tile_count(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                   const uint8_t* __restrict__ arena, const Seg* __restrict__ runs,
+                                                   DTile* __restrict__ tiles, int tile0) {
+  DTile& T = tiles[tile0 + blockIdx.x];
+  const int pi = T.page;
+  const DPage pg = pages[pi];
+  const int t = threadIdx.x;
+  __shared__ int lds[12];
+  int rows = 0, ents = 0, vals = 0;
+  const DChunk ck = chunks[pg.chunk];
+  if (pg.status == PS_OK) {
+    const Layout L = page_layout(pg, ck, arena);
+    const int l_end = min(T.lvl0 + TL, pg.num_values);
+    const int a = T.lvl0 + t * LPT, b = min(a + LPT, l_end);
+    if (a < b) {
+      const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
+      RunCur cr, cd;
+      if (ck.max_rep > 0) cr.init(runs + pg.run_r, pg.nrun_r, a);
+      if (ck.max_def > 0) cd.init(runs + pg.run_d, pg.nrun_d, a);
+      for (int i = a; i < b; i++) {
+        const int rep = ck.max_rep > 0 ? (int)cr.get(i, bwr, L.d, L.rep_e) : 0;
+        const int def = ck.max_def > 0 ? (int)cd.get(i, bwd, L.d, L.def_e) : 0;
+        rows += rep == 0; ents += def >= ck.rep_def; vals += def == ck.max_def;
       }
     }
-    w0 += win;
-    __syncthreads();
   }
   int er, ee, ev, tr, te, tv;
-  block_scan3(rows, ents, vals, &er, &ee, &ev, &tr, &te, &tv, W.scan);
-  if (W.err) { if (t == 0) pg.status = PS_BAD_LEVELS; return; }
-  // characters
-  long long nchars = 0;
-  bool bad = false;
-  if (ck.phys == PT_BYTE_ARRAY) {
-    if (pg.enc == ENC_PLAIN) {
-      nchars = (long long)(L.val_e - L.val_p) - 4ll * tv;
-      if (nchars < 0) bad = true;
-    } else if (pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) {
-      if (ck.dict_page < 0) { bad = true; }
-      else {
-        const int32_t* DP = pos + ck.dict_pos;
-        int32_t dn;
-        dict_data(ck, pages, arena, &dn);
-        const int ibw = tv > 0 ? (int)(*L.val_p) : 0;
-        if (t == 0) { hyb_init(W.hi, L.val_p + 1, L.val_e, ibw); }
-        __syncthreads();
-        long long local = 0;
-        for (int v0 = 0; v0 < tv;) {
-          if (t == 0) { W.win = hyb_fill(W.hi, L.d, W.segi, min(LW, tv - v0), &W.ni); if (W.win <= 0) W.err = 1; }
-          __syncthreads();
-          const int win = W.win;
-          if (W.err) break;
-          for (int i = t; i < win; i += NT) {
-            uint32_t ix = seg_value(W.segi, W.ni, i, ibw, L.d, L.val_e);
-            if ((int32_t)ix >= dn) { W.err = 1; continue; }
-            local += (long long)(DP[ix + 1] - DP[ix] - 4);
-          }
-          v0 += win;
-          __syncthreads();
-        }
-        long long tot;
-        block_scan64(local, &tot, W.scan64);
-        nchars = tot;
-        if (W.err) bad = true;
-      }
-    } else if (pg.enc != ENC_PLAIN || tv > 0) {
-      if (tv > 0) bad = true;
-    }
-  } else {
-    bool ok_enc = pg.enc == ENC_PLAIN || ((pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) && ck.dict_page >= 0) ||
-                  (pg.enc == ENC_RLE && ck.phys == PT_BOOLEAN) ||
-                  (pg.enc == ENC_DELTA_BP && (ck.phys == PT_INT32 || ck.phys == PT_INT64));
-    if (!ok_enc && tv > 0) bad = true;
-  }
+  block_scan3(rows, ents, vals, &er, &ee, &ev, &tr, &te, &tv, lds);
   if (t == 0) {
-    pg.n_rows = ck.max_rep > 0 ? tr : nv;
-    pg.n_entries = ck.max_rep > 0 ? te : nv;
-    pg.n_values = tv;
-    pg.n_chars = nchars;
-    if (bad) pg.status = PS_UNSUPPORTED;
+    T.n_rows = tr; T.n_entries = te; T.n_values = tv; T.n_chars = 0;
+    if (tv > 0 && pg.status == PS_OK && !enc_supported(pg, ck)) pages[pi].status = PS_UNSUPPORTED;
   }
 }
 
-// --------------------------------------------------------------------------------------------
-// K4: per-column exclusive scan over its data pages (one workgroup per column)
-// --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_column_scan(DColumn* __restrict__ cols, DPage* __restrict__ pages,
-                                                    DState* __restrict__ st) {
+__global__ __launch_bounds__(NT) void k_tile_scan1(DColumn* __restrict__ cols, DPage* __restrict__ pages,
+                                                   DTile* __restrict__ tiles, DState* __restrict__ st) {
   DColumn& c = cols[blockIdx.x];
+  const int ft = c.first_tile, nt = c.n_tiles;
   __shared__ int lds[12];
-  __shared__ long long l64[4];
-  long long rb = 0, eb = 0, vb = 0, cb = 0;
-  int bad = 0;
-  for (int p0 = 0; p0 < c.n_pages; p0 += NT) {
-    int i = p0 + threadIdx.x;
+  long long rb = 0, eb = 0, vb = 0;
+  for (int p0 = 0; p0 < nt; p0 += NT) {
+    const int i = p0 + threadIdx.x;
     int r = 0, e = 0, v = 0;
-    long long ch = 0;
-    if (i < c.n_pages) {
-      const DPage& pg = pages[c.first_page + i];
-      if (pg.status != PS_OK) bad = 1;
-      r = pg.n_rows; e = pg.n_entries; v = pg.n_values; ch = pg.n_chars;
-    }
+    if (i < nt) { const DTile& T = tiles[ft + i]; r = T.n_rows; e = T.n_entries; v = T.n_values; }
     int er, ee, ev, tr, te, tv;
     block_scan3(r, e, v, &er, &ee, &ev, &tr, &te, &tv, lds);
-    long long tc;
-    long long ec = block_scan64(ch, &tc, l64);
-    if (i < c.n_pages) {
-      DPage& pg = pages[c.first_page + i];
-      pg.row_base = rb + er; pg.entry_base = eb + ee; pg.value_base = vb + ev; pg.char_base = cb + ec;
+    if (i < nt) { DTile& T = tiles[ft + i]; T.row_base = rb + er; T.entry_base = eb + ee; T.value_base = vb + ev; }
+    rb += tr; eb += te; vb += tv;
+  }
+  __syncthreads();
+  int bad = 0;
+  for (int j = threadIdx.x; j < c.n_pages; j += NT) {
+    DPage& pg = pages[c.first_page + j];
+    if (pg.status != PS_OK) bad = 1;
+    if (pg.n_tiles > 0) {
+      const DTile& a = tiles[pg.first_tile];
+      const DTile& z = tiles[pg.first_tile + pg.n_tiles - 1];
+      pg.row_base = a.row_base; pg.entry_base = a.entry_base; pg.value_base = a.value_base;
+      pg.n_rows = (int32_t)(z.row_base + z.n_rows - a.row_base);
+      pg.n_entries = (int32_t)(z.entry_base + z.n_entries - a.entry_base);
+      pg.n_values = (int32_t)(z.value_base + z.n_values - a.value_base);
+    } else {
+      pg.n_rows = pg.n_entries = pg.n_values = 0;
+      pg.row_base = pg.entry_base = pg.value_base = 0;
     }
-    rb += tr; eb += te; vb += tv; cb += tc;
   }
   if (bad) atomicOr(&st->err_flags, E_PAGE);
   if (threadIdx.x == 0) {
     c.n_entries = c.max_rep > 0 ? eb : rb;
-    c.n_chars = cb;
-    if (rb != c.n_rows || (c.max_rep > 0 && eb > c.cap_entries) || cb > c.cap_chars) atomicOr(&st->err_flags, E_PAGE);
-    if (c.phys == PT_BYTE_ARRAY && c.offs && !(cb > c.cap_chars)) c.offs[c.max_rep > 0 ? eb : rb] = cb;
+    if (rb != c.n_rows || (c.max_rep > 0 && eb > c.cap_entries)) atomicOr(&st->err_flags, E_PAGE);
     if (c.max_rep > 0 && c.row_offs && eb <= c.cap_entries) c.row_offs[rb] = eb;
   }
 }
 
-// --------------------------------------------------------------------------------------------
-// K5: decode levels + values of one data page
-// --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_page_decode(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
-                                                    const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
-                                                    const int32_t* __restrict__ pos, const long long* __restrict__ dbp, int page0) {
-  const DPage& pg = pages[page0 + blockIdx.x];
-  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
-  const DChunk& ck = chunks[pg.chunk];
-  const DColumn& col = cols[ck.col];
-  __shared__ WinLds W;
-  __shared__ int s_dict_n;
+__global__ __launch_bounds__(NT) void k_tile_chars(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                   const uint8_t* __restrict__ arena, const int32_t* __restrict__ pos,
+                                                   const Seg* __restrict__ runs, DTile* __restrict__ tiles, int tile0) {
+  DTile& T = tiles[tile0 + blockIdx.x];
+  const int pi = T.page;
+  const DPage pg = pages[pi];
+  const DChunk ck = chunks[pg.chunk];
   const int t = threadIdx.x;
-  Layout L = page_layout(pg, ck, arena);
-  const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
+  if (ck.phys != PT_BYTE_ARRAY) return;
+  const int nvt = T.n_values;
+  const int vb = (int)(T.value_base - pg.value_base);     // page-local index of the tile's first value
+  if (pg.status != PS_OK || nvt == 0) { if (t == 0) T.n_chars = 0; return; }
+  if (pg.enc == ENC_PLAIN) {
+    if (t == 0) {
+      const int32_t* P = pos + pg.pos_base;
+      T.n_chars = (long long)(P[vb + nvt] - P[vb]) - 4ll * nvt;
+    }
+    return;
+  }
+  __shared__ long long l64[4];
+  __shared__ int s_bad;
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  long long sum = 0;
+  const bool dict = (pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT) && ck.dict_page >= 0;
+  if (!dict || vb + nvt > pg.idx_cover || pg.nrun_i == 0 || pages[ck.dict_page].status != PS_OK) {
+    if (t == 0) s_bad = 1;
+  } else {
+    const Layout L = page_layout(pg, ck, arena);
+    int32_t dn;
+    dict_data(ck, pages, arena, &dn);
+    const int32_t* DP = pos + ck.dict_pos;
+    const int ibw = *L.val_p;
+    const int per = (nvt + NT - 1) / NT;
+    const int a = vb + t * per, b = min(a + per, vb + nvt);
+    if (a < b) {
+      RunCur ci;
+      ci.init(runs + pg.run_i, pg.nrun_i, a);
+      for (int v = a; v < b; v++) {
+        const uint32_t ix = ci.get(v, ibw, L.d, L.val_e);
+        if ((int32_t)ix >= dn) { s_bad = 1; break; }
+        sum += DP[ix + 1] - DP[ix] - 4;
+      }
+    }
+  }
+  long long tot;
+  block_scan64(sum, &tot, l64);
+  if (t == 0) {
+    T.n_chars = tot;
+    if (s_bad) pages[pi].status = PS_BAD_VALUES;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_tile_scan2(DColumn* __restrict__ cols, DPage* __restrict__ pages,
+                                                   DTile* __restrict__ tiles, DState* __restrict__ st) {
+  DColumn& c = cols[blockIdx.x];
+  __shared__ long long l64[4];
+  int bad = 0;
+  for (int j = threadIdx.x; j < c.n_pages; j += NT)
+    if (pages[c.first_page + j].status != PS_OK) bad = 1;
+  if (bad) atomicOr(&st->err_flags, E_PAGE);
+  if (c.phys != PT_BYTE_ARRAY) return;
+  const int ft = c.first_tile, nt = c.n_tiles;
+  long long cb = 0;
+  for (int p0 = 0; p0 < nt; p0 += NT) {
+    const int i = p0 + threadIdx.x;
+    const long long ch = i < nt ? tiles[ft + i].n_chars : 0;
+    long long tc;
+    const long long ec = block_scan64(ch, &tc, l64);
+    if (i < nt) tiles[ft + i].char_base = cb + ec;
+    cb += tc;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < c.n_pages; j += NT) {
+    DPage& pg = pages[c.first_page + j];
+    if (pg.n_tiles > 0) {
+      const DTile& a = tiles[pg.first_tile];
+      const DTile& z = tiles[pg.first_tile + pg.n_tiles - 1];
+      pg.char_base = a.char_base;
+      pg.n_chars = z.char_base + z.n_chars - a.char_base;
+    } else {
+      pg.char_base = 0; pg.n_chars = 0;
+    }
+  }
+  if (threadIdx.x == 0) {
+    c.n_chars = cb;
+    if (cb > c.cap_chars) atomicOr(&st->err_flags, E_PAGE);
+    else if (c.offs) c.offs[c.n_entries] = cb;
+  }
+}
+
+// k_tile_decode: the tile's levels are dealt to lanes STRIDED (level lvl0 + k*NT + t, k < LPT) so
+// that every store instruction of the emit phase writes consecutive addresses across the wave
+// (coalesced row_def / offs / fixed / hash stores). Ranks within the tile come from wave ballots
+// + mbcnt, plus an exclusive scan over the LPT x NW (k, wave) counts in LDS.
+__device__ __forceinline__ int lane_rank(uint64_t m) {   // set bits of m below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                    const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
+                                                    const int32_t* __restrict__ pos, const long long* __restrict__ dbp,
+                                                    const Seg* __restrict__ runs, const DTile* __restrict__ tiles,
+                                                    int tile0, DState* __restrict__ st) {
+  constexpr int NW = NT / 64;
+  const DTile T = tiles[tile0 + blockIdx.x];       // by value: the stores below may alias
+  const DPage pg = pages[T.page];
+  if (pg.status != PS_OK) return;
+  const DChunk ck = chunks[pg.chunk];
+  const DColumn col = cols[ck.col];
+  const Layout L = page_layout(pg, ck, arena);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int l_end = min(T.lvl0 + TL, pg.num_values);
   const bool rep = ck.max_rep > 0;
   const bool is_str = ck.phys == PT_BYTE_ARRAY;
   const bool is_dict = pg.enc == ENC_PLAIN_DICT || pg.enc == ENC_RLE_DICT;
+  const bool bool_rle = ck.phys == PT_BOOLEAN && pg.enc == ENC_RLE;
+  const bool dict_str = is_dict && is_str;
   const int w = ck.width;
+  const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
   const uint8_t* D = nullptr;
   const int32_t* DP = nullptr;
-  int ibw = 0;
+  int32_t dict_n = 0;
+  int ibw = 1;
   if (is_dict) {
-    int32_t dn;
-    D = dict_data(ck, pages, arena, &dn);
-    if (t == 0) s_dict_n = dn;
+    D = dict_data(ck, pages, arena, &dict_n);
     if (is_str) DP = pos + ck.dict_pos;
-    ibw = pg.n_values > 0 ? (int)(*L.val_p) : 0;
+    ibw = L.val_p < L.val_e ? (int)(*L.val_p) : 0;
   }
   const int32_t* P = (is_str && pg.enc == ENC_PLAIN) ? pos + pg.pos_base : nullptr;
-  // RLE booleans: 4-byte length then hybrid (bw 1)
-  const uint8_t* bool_rle_p = nullptr;
-  if (ck.phys == PT_BOOLEAN && pg.enc == ENC_RLE) bool_rle_p = L.val_p + 4;
-  if (t == 0) {
-    hyb_init(W.hr, L.rep_p, L.rep_e, bwr);
-    hyb_init(W.hd, L.def_p, L.def_e, bwd);
-    if (is_dict) hyb_init(W.hi, L.val_p + 1, L.val_e, ibw);
-    else if (bool_rle_p) hyb_init(W.hi, bool_rle_p, L.val_e, 1);
-    W.err = 0;
+  __shared__ int wcnt[3][LPT][NW];          // per (k, wave): rows, entries, values
+  __shared__ int wbase[3][LPT][NW];         // their exclusive scan in level order
+  __shared__ long long wch[LPT][NW];        // dictionary strings: chars per (k, wave)
+  __shared__ long long wchb[LPT][NW];
+  __shared__ int s_tot[3];
+  __shared__ long long s_chtot;
+  __shared__ int32_t vsrc[TL];              // dictionary strings: source offset in the dictionary page
+  __shared__ int32_t vcoff[TL + 1];         // and tile-relative output offset of each value
+  // 1. levels (strided) and their ballots
+  int rp[LPT], df[LPT];
+  uint64_t mr[LPT], me[LPT], mv[LPT];
+  {
+    RunCur cr, cd;
+    const int i0 = T.lvl0 + t;
+    if (i0 < l_end) {
+      if (rep) cr.init(runs + pg.run_r, pg.nrun_r, i0);
+      if (ck.max_def > 0) cd.init(runs + pg.run_d, pg.nrun_d, i0);
+    }
+#pragma unroll
+    for (int k = 0; k < LPT; k++) {
+      const int i = i0 + k * NT;
+      rp[k] = 1; df[k] = -1;
+      if (i < l_end) {
+        rp[k] = rep ? (int)cr.get(i, bwr, L.d, L.rep_e) : 0;
+        df[k] = ck.max_def > 0 ? (int)cd.get(i, bwd, L.d, L.def_e) : 0;
+      }
+      mr[k] = __ballot(rp[k] == 0);
+      me[k] = __ballot(df[k] >= ck.rep_def && df[k] >= 0);
+      mv[k] = __ballot(df[k] == ck.max_def);
+      if (lane == 0) { wcnt[0][k][wv] = __popcll(mr[k]); wcnt[1][k][wv] = __popcll(me[k]); wcnt[2][k][wv] = __popcll(mv[k]); }
+    }
   }
   __syncthreads();
-  int rows_c = 0, ents_c = 0, vals_c = 0;      // carries (page-local)
-  long long chars_c = 0;                        // dictionary string chars carry
-  const int nv = pg.num_values;
-  for (int w0 = 0; w0 < nv;) {
-    if (t == 0) fill_levels(W, L, ck, nv - w0);
+  if (t < 3) {
+    int run = 0;
+    for (int k = 0; k < LPT; k++)
+      for (int q = 0; q < NW; q++) { wbase[t][k][q] = run; run += wcnt[t][k][q]; }
+    s_tot[t] = run;
+  }
+  __syncthreads();
+  const int tv = s_tot[2];
+  const int vt0 = (int)(T.value_base - pg.value_base);   // page-local index of the tile's first value
+  // 2. dictionary indices / RLE booleans of the thread's values (value order = level order)
+  uint32_t ix[LPT];
+  bool bad = false;
+  {
+    const bool need = is_dict || bool_rle;
+    RunCur ci;
+    bool ci_on = false;
+#pragma unroll
+    for (int k = 0; k < LPT; k++) {
+      ix[k] = 0;
+      if (need && df[k] == ck.max_def && !bad) {
+        const int v = vt0 + wbase[2][k][wv] + lane_rank(mv[k]);
+        if (v >= pg.idx_cover || pg.nrun_i == 0) { bad = true; continue; }
+        if (!ci_on) { ci.init(runs + pg.run_i, pg.nrun_i, v); ci_on = true; }
+        ix[k] = ci.get(v, ibw, L.d, L.val_e);
+        if (is_dict && (int32_t)ix[k] >= dict_n) { bad = true; ix[k] = 0; }
+      }
+    }
+  }
+  // PLAIN fixed-width values must lie inside the value section
+  if (!is_dict && !is_str && !bool_rle && pg.enc == ENC_PLAIN && tv > 0) {
+    const long long end_v = (long long)vt0 + tv;
+    const long long need_b = ck.phys == PT_BOOLEAN ? (end_v + 7) / 8 : end_v * w;
+    if (need_b > pg.vbytes) bad = true;
+  }
+  // 3. dictionary strings: exclusive scan of the value lengths in level order
+  long long cex[LPT];
+  if (dict_str) {
+#pragma unroll
+    for (int k = 0; k < LPT; k++) {
+      const long long len = (df[k] == ck.max_def && !bad) ? (long long)(DP[ix[k] + 1] - DP[ix[k]] - 4) : 0;
+      long long x = len;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      cex[k] = x - len;
+      if (lane == 63) wch[k][wv] = x;
+    }
     __syncthreads();
-    const int win = W.win;
-    if (W.err) break;
-    int rp[2], df[2];
-    int nr = 0, ne = 0, nvl = 0;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-      int i = t * 2 + k;
-      rp[k] = 1; df[k] = -1;
-      if (i < win) {
-        level_at(W, L, ck, i, bwr, bwd, &rp[k], &df[k]);
-        nr += (rp[k] == 0);
-        ne += (df[k] >= ck.rep_def);
-        nvl += (df[k] == ck.max_def);
-      }
+    if (t == 0) {
+      long long run = 0;
+      for (int k = 0; k < LPT; k++)
+        for (int q = 0; q < NW; q++) { wchb[k][q] = run; run += wch[k][q]; }
+      s_chtot = run;
     }
-    int er, ee, ev, tr, te, tv;
-    block_scan3(nr, ne, nvl, &er, &ee, &ev, &tr, &te, &tv, W.scan);
-    // dictionary indices / RLE booleans for the values of this window
-    if ((is_dict || bool_rle_p) && tv > 0) {
-      if (t == 0) {
-        int got = hyb_fill(W.hi, L.d, W.segi, tv, &W.ni);
-        if (got < tv) W.err = 1;
-      }
-      __syncthreads();
-    }
-    // dictionary string lengths -> char offsets within the window
-    long long my_len = 0;
-    uint32_t ix[2] = {0, 0};
-    {
-      int v = ev;
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        if (df[k] == ck.max_def && (is_dict || bool_rle_p)) {
-          ix[k] = seg_value(W.segi, W.ni, v, is_dict ? ibw : 1, L.d, L.val_e);
-          if (is_dict && (int32_t)ix[k] >= s_dict_n) { W.err = 1; ix[k] = 0; }
-          if (is_dict && is_str) my_len += (long long)(DP[ix[k] + 1] - DP[ix[k]] - 4);
-          v++;
-        }
-      }
-    }
-    long long ch_excl = 0, ch_tot = 0;
-    if (is_dict && is_str) ch_excl = block_scan64(my_len, &ch_tot, W.scan64);
-    // emit
-    {
-      int r_i = rows_c + er, e_i = ents_c + ee, v_i = vals_c + ev;
-      long long c_i = chars_c + ch_excl;
-#pragma unroll
-      for (int k = 0; k < 2; k++) {
-        int i = t * 2 + k;
-        if (i >= win) break;
-        const int d = df[k];
-        const bool is_row = (rp[k] == 0);
-        const bool is_ent = d >= ck.rep_def;
-        const bool is_val = d == ck.max_def;
-        const long long grow = pg.row_base + r_i;           // row of this level (if row start)
-        if (is_row) {
-          col.row_def[grow] = (uint8_t)d;
-          if (rep && col.row_offs) col.row_offs[grow] = pg.entry_base + e_i;
-          // key column: forward the value's path hash (PLAIN pages; 0 = the probe recomputes)
-          if (col.hash) col.hash[grow] = (is_val && P) ? col.vhash[pg.value_base + v_i] : 0ull;
-        }
-        long long dest = -1;
-        if (rep) {
-          if (is_ent) { dest = pg.entry_base + e_i; if (col.entry_def) col.entry_def[dest] = (uint8_t)d; }
-        } else {
-          dest = grow;
-        }
-        if (dest >= 0 && !col.null_only) {
-          const long long vloc = v_i;                       // values before this level (page-local)
-          if (is_str) {
-            long long cpos;
-            if (P) cpos = (long long)P[vloc] - 4ll * vloc;
-            else cpos = c_i;
-            col.offs[dest] = pg.char_base + cpos;
-            if (is_val && is_dict) {
-              const uint8_t* src = D + DP[ix[k]] + 4;
-              int len = DP[ix[k] + 1] - DP[ix[k]] - 4;
-              uint8_t* o = col.chars + pg.char_base + cpos;
-              for (int j = 0; j < len; j++) o[j] = src[j];
-            }
-          } else if (col.fixed) {
-            uint8_t* o = col.fixed + dest * w;
-            if (!is_val) {
-              if (w == 8) *(uint64_t*)o = 0; else if (w == 4) *(uint32_t*)o = 0; else for (int j = 0; j < w; j++) o[j] = 0;
-            } else if (ck.phys == PT_BOOLEAN) {
-              uint8_t b;
-              if (bool_rle_p) b = (uint8_t)ix[k];
-              else b = (L.val_p[vloc >> 3] >> (vloc & 7)) & 1;
-              *o = b;
-            } else if (pg.enc == ENC_DELTA_BP) {
-              long long x = dbp[pg.pos_base + vloc];
-              if (w == 8) *(long long*)o = x; else *(int32_t*)o = (int32_t)x;
-            } else {
-              const uint8_t* src = is_dict ? D + (int64_t)ix[k] * w : L.val_p + vloc * w;
-              if (w == 8) {
-                uint64_t x = (uint64_t)ld_u32(src) | ((uint64_t)ld_u32(src + 4) << 32);
-                *(uint64_t*)o = x;
-              } else if (w == 4) {
-                *(uint32_t*)o = ld_u32(src);
-              } else {
-                for (int j = 0; j < w; j++) o[j] = src[j];
-              }
-            }
-          }
-        }
-        r_i += is_row; e_i += is_ent;
-        if (is_val) { if (is_dict && is_str) c_i += (long long)(DP[ix[k] + 1] - DP[ix[k]] - 4); v_i++; }
-      }
-    }
-    rows_c += tr; ents_c += te; vals_c += tv; chars_c += ch_tot;
-    w0 += win;
     __syncthreads();
   }
+  // 4. emit (every store instruction covers consecutive levels across the wave)
+#pragma unroll
+  for (int k = 0; k < LPT; k++) {
+    const int i = T.lvl0 + t + k * NT;
+    if (i >= l_end) continue;
+    const int d = df[k];
+    const bool is_row = rp[k] == 0, is_ent = d >= ck.rep_def, is_val = d == ck.max_def;
+    const int r_i = wbase[0][k][wv] + lane_rank(mr[k]);
+    const int e_i = wbase[1][k][wv] + lane_rank(me[k]);
+    const int v_i = wbase[2][k][wv] + lane_rank(mv[k]);   // tile-local index of this / the next value
+    const long long grow = T.row_base + r_i;
+    const int vloc = vt0 + v_i;                           // page-local
+    if (is_row) {
+      col.row_def[grow] = (uint8_t)d;
+      if (rep && col.row_offs) col.row_offs[grow] = T.entry_base + e_i;
+      // key column: forward the value's path hash (PLAIN pages; 0 = the probe recomputes)
+      if (col.hash) col.hash[grow] = (is_val && P) ? col.vhash[pg.value_base + vloc] : 0ull;
+    }
+    long long dest = -1;
+    if (rep) {
+      if (is_ent) { dest = T.entry_base + e_i; if (col.entry_def) col.entry_def[dest] = (uint8_t)d; }
+    } else {
+      dest = grow;
+    }
+    if (dest < 0 || col.null_only || bad) continue;
+    if (is_str) {
+      const long long c_i = dict_str ? wchb[k][wv] + cex[k] : 0;
+      col.offs[dest] = P ? pg.char_base + ((long long)P[vloc] - 4ll * vloc) : T.char_base + c_i;
+      if (is_val && is_dict) { vsrc[v_i] = DP[ix[k]] + 4; vcoff[v_i] = (int32_t)c_i; }
+    } else if (col.fixed) {
+      uint8_t* o = col.fixed + dest * w;
+      if (!is_val) {
+        if (w == 8) *(uint64_t*)o = 0; else if (w == 4) *(uint32_t*)o = 0; else for (int j = 0; j < w; j++) o[j] = 0;
+      } else if (ck.phys == PT_BOOLEAN) {
+        *o = bool_rle ? (uint8_t)ix[k] : (uint8_t)((L.val_p[vloc >> 3] >> (vloc & 7)) & 1);
+      } else if (pg.enc == ENC_DELTA_BP) {
+        const long long x = dbp[pg.pos_base + vloc];
+        if (w == 8) *(long long*)o = x; else *(int32_t*)o = (int32_t)x;
+      } else {
+        const uint8_t* src = is_dict ? D + (int64_t)ix[k] * w : L.val_p + (int64_t)vloc * w;
+        if (w == 8) *(uint64_t*)o = (uint64_t)ld_u32(src) | ((uint64_t)ld_u32(src + 4) << 32);
+        else if (w == 4) *(uint32_t*)o = ld_u32(src);
+        else for (int j = 0; j < w; j++) o[j] = src[j];
+      }
+    }
+  }
+  // 5. dictionary strings: cooperative copy of the tile's chars into 16-byte aligned output chunks
+  //    (one dwordx4 store each; byte stores only for the two edge chunks shared with neighbours).
+  //    A chunk's 16 source addresses are resolved from LDS first, so its 16 loads issue together.
+  if (dict_str && !col.null_only && __syncthreads_or(bad) == 0 && s_chtot > 0) {
+    const int32_t nch = (int32_t)s_chtot;
+    if (t == 0) vcoff[tv] = nch;
+    __syncthreads();
+    uint8_t* ob = col.chars + T.char_base;
+    const uintptr_t lo_a = (uintptr_t)ob & ~(uintptr_t)15, hi_a = (uintptr_t)ob + nch;
+    for (uintptr_t ca = lo_a + (uintptr_t)t * 16; ca < hi_a; ca += (uintptr_t)NT * 16) {
+      const int32_t oa = (int32_t)((intptr_t)ca - (intptr_t)ob);
+      const int32_t lo = oa < 0 ? 0 : oa;
+      const int32_t hi = oa + 16 < nch ? oa + 16 : nch;
+      int kk = 0, kh = tv - 1;
+      while (kk < kh) { const int mid = (kk + kh + 1) >> 1; if (vcoff[mid] <= lo) kk = mid; else kh = mid - 1; }
+      int32_t nb = vcoff[kk + 1];
+      int32_t src[16];
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const int32_t o = oa + j;
+        src[j] = -1;
+        if (o >= lo && o < hi) {
+          while (o >= nb) { kk++; nb = vcoff[kk + 1]; }
+          src[j] = vsrc[kk] + (o - vcoff[kk]);
+        }
+      }
+      uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t by = src[j] >= 0 ? (uint32_t)D[src[j]] : 0u;
+        if (j < 4) q0 |= by << (8 * j);
+        else if (j < 8) q1 |= by << (8 * (j - 4));
+        else if (j < 12) q2 |= by << (8 * (j - 8));
+        else q3 |= by << (8 * (j - 12));
+      }
+      if (lo == oa && hi == oa + 16) {
+        *(uint4*)ca = make_uint4(q0, q1, q2, q3);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          if (src[j] < 0) continue;
+          const uint32_t q = j < 4 ? q0 : j < 8 ? q1 : j < 12 ? q2 : q3;
+          ((uint8_t*)ca)[j] = (uint8_t)(q >> (8 * (j & 3)));
+        }
+      }
+    }
+  }
+  if (bad) { pages[T.page].status = PS_BAD_VALUES; atomicOr(&st->err_flags, E_PAGE); }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -956,11 +1049,11 @@ __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ c
                                                     const int32_t* __restrict__ pos, const int2* __restrict__ tiles,
                                                     int tile0, int dbg) {
   const int2 tile = tiles[tile0 + blockIdx.x];     // (page, first value)
-  const DPage& pg = pages[tile.x];
+  const DPage pg = pages[tile.x];                  // by value: byte stores below may alias
   if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
-  const DChunk& ck = chunks[pg.chunk];
+  const DChunk ck = chunks[pg.chunk];
   if (ck.phys != PT_BYTE_ARRAY || pg.enc != ENC_PLAIN) return;
-  const DColumn& col = cols[ck.col];
+  const DColumn col = cols[ck.col];
   uint64_t* vh = (col.vhash && !(dbg & 2)) ? col.vhash + pg.value_base : nullptr;
   const int n = min(pg.n_values, tile.y + CT);
   if (n <= tile.y || (pg.n_chars == 0 && !vh)) return;
@@ -1291,16 +1384,28 @@ void launch_string_positions(const DChunk* c, DPage* p, int n, const uint8_t* ar
                              hipStream_t s, int page0) {
   if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos, mode, page0);
 }
-void launch_page_count(const DChunk* c, DPage* p, int n, const uint8_t* arena, const int32_t* pos, hipStream_t s,
-                       int page0) {
-  if (n) hipLaunchKernelGGL(k_page_count, dim3(n), dim3(NT), 0, s, c, p, arena, pos, page0);
+void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_page_runs, dim3((n + 63) / 64), dim3(64), 0, s, c, p, n, arena, runs);
 }
-void launch_column_scan(DColumn* cols, int ncols, DPage* p, DState* st, hipStream_t s) {
-  if (ncols) hipLaunchKernelGGL(k_column_scan, dim3(ncols), dim3(NT), 0, s, cols, p, st);
+void launch_tile_count(const DChunk* c, DPage* p, const uint8_t* arena, const Seg* runs, DTile* t, int ntiles,
+                       int tile0, hipStream_t s) {
+  if (ntiles) hipLaunchKernelGGL(k_tile_count, dim3(ntiles), dim3(NT), 0, s, c, p, arena, runs, t, tile0);
 }
-void launch_page_decode(const DChunk* c, const DPage* p, int n, const DColumn* cols, const uint8_t* arena,
-                        const int32_t* pos, const long long* dbp, hipStream_t s, int page0) {
-  if (n) hipLaunchKernelGGL(k_page_decode, dim3(n), dim3(NT), 0, s, c, p, cols, arena, pos, dbp, page0);
+void launch_tile_scan1(DColumn* cols, int ncols, DPage* p, DTile* t, DState* st, hipStream_t s) {
+  if (ncols) hipLaunchKernelGGL(k_tile_scan1, dim3(ncols), dim3(NT), 0, s, cols, p, t, st);
+}
+void launch_tile_chars(const DChunk* c, DPage* p, const uint8_t* arena, const int32_t* pos, const Seg* runs, DTile* t,
+                       int ntiles, int tile0, hipStream_t s) {
+  if (ntiles) hipLaunchKernelGGL(k_tile_chars, dim3(ntiles), dim3(NT), 0, s, c, p, arena, pos, runs, t, tile0);
+}
+void launch_tile_scan2(DColumn* cols, int ncols, DPage* p, DTile* t, DState* st, hipStream_t s) {
+  if (ncols) hipLaunchKernelGGL(k_tile_scan2, dim3(ncols), dim3(NT), 0, s, cols, p, t, st);
+}
+void launch_tile_decode(const DChunk* c, DPage* p, const DColumn* cols, const uint8_t* arena, const int32_t* pos,
+                        const long long* dbp, const Seg* runs, const DTile* t, int ntiles, int tile0, DState* st,
+                        hipStream_t s) {
+  if (ntiles)
+    hipLaunchKernelGGL(k_tile_decode, dim3(ntiles), dim3(NT), 0, s, c, p, cols, arena, pos, dbp, runs, t, tile0, st);
 }
 void launch_delta_decode(const DChunk* c, DPage* p, int n, const uint8_t* arena, long long* dbp, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_delta_decode, dim3(n), dim3(NT), 0, s, c, p, arena, dbp);

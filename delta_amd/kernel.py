@@ -413,7 +413,7 @@ class GpuScan:
 
     def kernel_stats(self):
         out = {}
-        for i in range(16):
+        for i in range(20):
             name, avg, cnt = C.c_char_p(), C.c_double(), C.c_int64()
             if lib().dk_replay_kernel_stats(self._rh, i, C.byref(name), C.byref(avg), C.byref(cnt)) != 0:
                 continue
