@@ -11,6 +11,7 @@ struct DChunk {
   int32_t phys, width, max_def, max_rep, rep_def, codec;
   int32_t dict_page;     // page index of the dictionary page, -1 if none
   int64_t dict_pos;      // string dictionaries: scratch offset (int32 per entry + 1)
+  int64_t dict_hash_off; // key columns: offset of this chunk's dictionary entries in DColumn.dhash
 };
 
 enum : int32_t { PF_DICT = 1 };
@@ -41,7 +42,18 @@ struct DPage {
   int32_t first_tile, n_tiles;   // level tiles of this page (input)
   int32_t pad2;
   int64_t vbytes;        // bytes of the value section (after the levels)
+  // string positions (BYTE_ARRAY PLAIN data pages and dictionary pages): 16 KiB chunks (input)
+  int32_t pchunk0, npchunk;
+  int32_t pos_fail;      // speculative positions rejected -> serial walk (k_pos_fallback)
+  int32_t pad3;
 };
+
+// One 16 KiB chunk of a string region for the chunk-parallel position scan.
+struct DPosChunk {
+  int32_t page, blk0;    // (input) page, first aligned 16-byte block of the region
+  int32_t cnt, base;     // candidates in the chunk, their first index
+};
+constexpr int DK_POS_CHUNK = 16384;
 
 // One run of an RLE/bit-packed hybrid stream: values [start, next.start) are `val` (RLE,
 // bp_idx < 0) or bit-packed from byte bp_off (relative to the page data start) on.
@@ -82,6 +94,7 @@ struct DColumn {
   // 0 = null row or "compute in the probe")
   uint64_t* vhash;
   uint64_t* hash;
+  uint64_t* dhash;       // key columns: path hash of every dictionary entry (k_string_copy)
 };
 
 constexpr uint32_t kDecodeSeed = 0;   // seed of the path hashes computed during decode

@@ -20,7 +20,7 @@
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const DChunk*, DPage*, int, uint8_t*, hipStream_t);
-void launch_string_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, int, hipStream_t, int);
+void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
 void launch_tile_scan1(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
@@ -34,8 +34,8 @@ void launch_slots_init(Slot*, uint64_t, hipStream_t);
 void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
-void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint8_t*,
-                  DState*, hipStream_t);
+void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
+                  uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
 
 using namespace dk;
@@ -298,7 +298,7 @@ static int phys_width(int phys, int tl) {
 // ------------------------------------------------------------------------------------------------
 struct KTimer {
   static constexpr int K = 20;
-  const char* names[K] = {"k_page_headers", "k_string_positions_dict", "k_tile_count", "k_tile_scan",
+  const char* names[K] = {"k_page_headers", "unused", "k_tile_count", "k_tile_scan",
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
                           "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", nullptr, nullptr,
@@ -353,6 +353,8 @@ struct dk_parquet {
   DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp, d_tiles;
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
   int n_ltiles = 0;
+  DBuf d_pchunks;            // string-position chunks (DPosChunk)
+  int n_pchunks = 0;
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
   std::vector<int> col_tile0;
@@ -423,10 +425,9 @@ static int run_pipeline(dk_parquet* p, int mode) {
   if (mode == -1) return 0;
   if (p->has_compressed) { KTimer::Scope sc(&T, 13, s); launch_snappy(C, P, n, p->d_arena.as<uint8_t>(), s); }
   { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P, n, arena, runs, s); }
-  { KTimer::Scope sc(&T, 1, s); launch_string_positions(C, P, n, arena, pos, 1, s, 0); }  // dictionary pages
   { KTimer::Scope sc(&T, 2, s); per_column_tiles(p, [&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols, p->n_cols, P, LT, st, s); }
-  { KTimer::Scope sc(&T, 4, s); per_column(p, n, [&](int a, int k) { launch_string_positions(C, P, k, arena, pos, 2, s, a); }); }
+  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, n, arena, pos, p->d_pchunks.as<DPosChunk>(), p->n_pchunks, s); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P, n, arena, p->d_dbp.as<long long>(), s); }
   { KTimer::Scope sc(&T, 16, s); per_column_tiles(p, [&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols, p->n_cols, P, LT, st, s); }
@@ -524,6 +525,22 @@ static int prepare(dk_parquet* p) {
       c.n_tiles = (int)tiles.size() - c.first_tile;
     }
     p->n_ltiles = (int)tiles.size();
+    // string-position chunks of every BYTE_ARRAY PLAIN data page and dictionary page (the region
+    // is at most the page body; chunks past the region's end find nothing)
+    std::vector<DPosChunk> pcs;
+    for (size_t pi = 0; pi < p->h_pages.size(); pi++) {
+      DPage& pg = p->h_pages[pi];
+      const DChunk& ck = p->h_chunks[pg.chunk];
+      pg.pchunk0 = (int)pcs.size();
+      pg.npchunk = 0;
+      pg.pos_fail = 0;
+      if (ck.phys != PT_BYTE_ARRAY || (!(pg.flags & PF_DICT) && pg.enc != ENC_PLAIN)) continue;
+      const int64_t body = (pg.unc_off >= 0 ? pg.usize : pg.csize) + 16;
+      for (int64_t b0 = 0; b0 * 16 < body; b0 += DK_POS_CHUNK / 16) { DPosChunk c{}; c.page = (int)pi; c.blk0 = (int32_t)b0; pcs.push_back(c); }
+      pg.npchunk = (int)pcs.size() - pg.pchunk0;
+    }
+    p->n_pchunks = (int)pcs.size();
+    if (upload(p->d_pchunks, pcs.data(), pcs.size() * sizeof(DPosChunk), s)) return 1;
     if (upload(p->d_ltiles, tiles.data(), tiles.size() * sizeof(DTile), s)) return 1;
     if (p->d_runs.alloc((size_t)(runs_n + 1) * sizeof(Seg))) return 1;
   }
@@ -547,12 +564,19 @@ static int prepare(dk_parquet* p) {
   {
     std::vector<int2> tiles;
     p->col_tile0.assign(1, 0);
-    for (const DColumn& c : p->h_cols) {
+    for (size_t ci = 0; ci < p->h_cols.size(); ci++) {
+      const DColumn& c = p->h_cols[ci];
       for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
         const DPage& pg = p->h_pages[pi];
         if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN) continue;
         for (int v0 = 0; v0 < pg.n_values; v0 += DK_COPY_TILE) tiles.push_back(make_int2(pi, v0));
       }
+      // key column: its dictionary pages are hashed entry by entry (hash-only tiles)
+      if (c.key_hash && c.phys == PT_BYTE_ARRAY && c.max_rep == 0)
+        for (const DChunk& ck : p->h_chunks)
+          if (ck.col == (int)ci && ck.dict_page >= 0)
+            for (int v0 = 0; v0 < p->h_pages[ck.dict_page].num_values; v0 += DK_COPY_TILE)
+              tiles.push_back(make_int2(ck.dict_page, v0));
       p->col_tile0.push_back((int)tiles.size());
     }
     if (upload(p->d_tiles, tiles.data(), tiles.size() * sizeof(int2), s)) return 1;
@@ -576,8 +600,16 @@ static int prepare(dk_parquet* p) {
     for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) n_values += p->h_pages[pi].n_values;
     c.null_only = (n_values == 0 && (c.max_rep == 0 || c.n_entries == 0)) ? 1 : 0;
     c.row_def = (uint8_t*)mk(c.n_rows);
-    c.vhash = c.hash = nullptr;
+    c.vhash = c.hash = c.dhash = nullptr;
     if (c.key_hash && !c.null_only && c.phys == PT_BYTE_ARRAY && c.max_rep == 0) {
+      int64_t dn = 0;        // dictionary entries of the column's chunks
+      for (DChunk& ck : p->h_chunks)
+        if (ck.col == (int)i && ck.dict_page >= 0) { ck.dict_hash_off = dn; dn += p->h_pages[ck.dict_page].num_values; }
+      if (dn) {
+        c.dhash = (uint64_t*)mk(dn * 8);
+        p->bytes_written -= dn * 8;               // scratch
+        if (!c.dhash) return 1;
+      }
       c.vhash = (uint64_t*)mk((n_values + 1) * 8);
       p->bytes_written -= (n_values + 1) * 8;     // scratch, not an output (written + re-read once)
       c.hash = (uint64_t*)mk(c.n_rows * 8);
@@ -597,6 +629,7 @@ static int prepare(dk_parquet* p) {
     if (!c.row_def) return 1;
   }
   if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
+  if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;   // dict_hash_off
   HIPOK(hipStreamSynchronize(s));
   p->host.assign(p->h_cols.size(), HostCol());
   p->prepared = true;
@@ -1208,6 +1241,7 @@ struct dk_replay {
   std::vector<DJsonAction> acts;
   std::vector<int64_t> act_row;        // tail row of each action
   DBuf d_acts, d_jchars, d_canon, d_slots, d_state, d_jsel;
+  DBuf d_cand, d_cand_n;      // probe candidates (rows needing the full key path)
   std::vector<std::unique_ptr<DBuf>> d_csel;   // per checkpoint file
   std::vector<ProbeCols> probe;
   uint64_t mask = 0;
@@ -1276,6 +1310,10 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   if (r->d_state.alloc(sizeof(DState))) return 1;
   if (r->d_jsel.alloc(na + 16)) return 1;
   if (ckpt) {
+    int64_t max_rows = 1;
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) max_rows = std::max<int64_t>(max_rows, ckpt->files[fi].num_rows);
+    if (r->d_cand.alloc((size_t)max_rows * 4 + 64)) return 1;
+    if (r->d_cand_n.alloc(64)) return 1;
     for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
       ProbeCols pc{};
       const DColumn* path = find_col(ckpt, (int)fi, "add.path");
@@ -1329,7 +1367,10 @@ static int replay_launch(dk_replay* r) {
       KTimer::Scope sc(&T, 11, s);
       ProbeCols pc = r->probe[fi];
       if (r->seed != kDecodeSeed) pc.path_hash = nullptr;   // collision retry: rehash from the chars
-      launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, r->d_csel[fi]->as<uint8_t>(), st, s);
+      HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;     // dvUniqueId stream of "no DV"
+      dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
+      launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, kd.hs.final_(kd.n),
+                   r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
     }
   }
   return 0;
@@ -1369,6 +1410,11 @@ extern "C" int dk_replay_sync(dk_replay* r) {
                   " in checkpoint row " + std::to_string(r->h_state.err_row));
     }
     r->have_result = true;
+    if (getenv("DK_PROBE_STATS") && r->ck) {   // diagnostics: candidates of the last probed file
+      unsigned int nc = 0;
+      HIPOK(hipMemcpy(&nc, r->d_cand_n.p, sizeof nc, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[dk] probe candidates (last file): %u\n", nc);
+    }
     return 0;
   }
   return fail("replay: repeated key-hash collisions");

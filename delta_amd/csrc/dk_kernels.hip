@@ -7,14 +7,14 @@
 //   k_page_headers      Thrift PageHeader parse, one lane per page
 //   k_snappy            raw snappy blocks, one wave per compressed page
 //   k_page_runs         run tables of the rep / def / dictionary-index hybrid streams
-//   k_string_positions  PLAIN BYTE_ARRAY entry positions: speculative zero-run candidates +
-//                       exact chain verification, sequential fallback
+//   k_pos_*             PLAIN BYTE_ARRAY entry positions, 16 KiB chunks: speculative zero-run
+//                       candidates + exact chain verification, sequential fallback
 //   k_tile_count / k_tile_scan1 / k_tile_chars / k_tile_scan2   rows, entries, values, chars
 //   k_delta_decode      DELTA_BINARY_PACKED
 //   k_string_copy       PLAIN string bytes -> contiguous chars + key-path hashes
 //   k_tile_decode       levels + values -> row_def / row_offs / entry_def / fixed / offs
 //   k_json_canon / k_table_insert / k_table_update / k_json_select   commit-tail keys
-//   k_probe             checkpoint add rows: key hash, probe, verify, select
+//   k_probe_fast / k_probe_cand   checkpoint add rows: key hash, probe, verify, select
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -256,109 +256,188 @@ __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks
 }
 
 // --------------------------------------------------------------------------------------------
-// K2: PLAIN BYTE_ARRAY entry positions (data pages and string dictionaries)
+// K2: PLAIN BYTE_ARRAY entry positions (data pages and string dictionaries), chunk-parallel.
 // P[k] = offset of entry k's 4-byte length prefix within the region, P[n] = region size.
 // Speculation: with non-empty, NUL-free string content and lengths < 2^16 whose low byte is
-// non-zero, every maximal run of zero bytes ends exactly at byte 3 of a length prefix. The
-// candidates are accepted only if they form the exact length chain from 0 to the region end;
-// otherwise one lane walks the chain (always exact).
+// non-zero, every maximal run of zero bytes ends exactly at byte 3 of a length prefix. Regions are
+// cut into 16 KiB chunks (one workgroup each, one dwordx4 per lane per step):
+//   k_pos_count    candidates per chunk
+//   k_pos_scan     per page: exclusive scan over its chunks; count != n -> fallback
+//   k_pos_write    candidates -> P in order
+//   k_pos_verify   the exact length chain: P[0] = 0, P[k] + 4 + len(P[k]) = P[k+1], P[n] = R
+//   k_pos_fallback pages that failed: one lane walks the chain (always exact)
 // --------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(NT) void k_string_positions(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                                         const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                         int mode, int page0) {
-  const DPage pg = pages[page0 + blockIdx.x];      // by value: byte stores below may alias
-  const DChunk ck = chunks[pg.chunk];
-  if (ck.phys != PT_BYTE_ARRAY || pg.status != PS_OK) return;
-  const bool dict = (pg.flags & PF_DICT) != 0;
-  if (dict != (mode == 1)) return;   // mode 1: dictionary pages, mode 2: data pages
+constexpr int POS_CHB = DK_POS_CHUNK / 16;   // aligned 16-byte blocks per chunk
+constexpr int POS_BPT = POS_CHB / NT;        // blocks per thread (strided by NT)
+
+struct StrRegion {
   const uint8_t* r;
   int64_t R;
   int32_t n;
   int32_t* P;
-  if (dict) {
-    r = page_data(pg, ck, arena);
-    R = page_len(pg);
-    n = pg.num_values;
-    P = pos + ck.dict_pos;
+  uintptr_t abase;
+  int64_t mis, nblk;
+};
+
+__device__ __forceinline__ bool str_region(const DPage& pg, const DChunk& ck, const uint8_t* arena, int32_t* pos,
+                                           StrRegion& S) {
+  if (ck.phys != PT_BYTE_ARRAY || pg.status != PS_OK) return false;
+  if (pg.flags & PF_DICT) {
+    S.r = page_data(pg, ck, arena);
+    S.R = page_len(pg);
+    S.n = pg.num_values;
+    S.P = pos + ck.dict_pos;
   } else {
-    if (pg.enc != ENC_PLAIN) return;
-    Layout L = page_layout(pg, ck, arena);
-    if (!L.ok) return;
-    r = L.val_p;
-    R = L.val_e - L.val_p;
-    n = pg.n_values;
-    P = pos + pg.pos_base;
+    if (pg.enc != ENC_PLAIN) return false;
+    const Layout L = page_layout(pg, ck, arena);
+    if (!L.ok) return false;
+    S.r = L.val_p;
+    S.R = L.val_e - L.val_p;
+    S.n = pg.n_values;
+    S.P = pos + pg.pos_base;
   }
-  __shared__ int s_fail;
+  S.abase = (uintptr_t)S.r & ~(uintptr_t)15;
+  S.mis = (int64_t)((uintptr_t)S.r - S.abase);
+  S.nblk = (S.mis + S.R + 15) >> 4;
+  return true;
+}
+
+// candidate bits of aligned block i (block i covers region bytes [16i - mis, 16i - mis + 16)); a
+// candidate is the last zero byte j of a zero run (byte j+1 non-zero, or j+1 == R), giving the
+// prefix start q = j - 3. Consecutive lanes must hold consecutive blocks (look-ahead via shfl).
+__device__ __forceinline__ uint32_t pos_cand_mask(const StrRegion& S, int64_t i) {
+  const uint4* blk = (const uint4*)S.abase;
+  uint4 q = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
+  if (i < S.nblk) q = blk[i];
+  uint32_t nxt = __shfl_down(q.x, 1, 64);
+  if ((threadIdx.x & 63) == 63 && i + 1 < S.nblk) nxt = ((const uint32_t*)(blk + i + 1))[0];
+  auto zb = [](uint32_t x) -> uint32_t {      // bit k set iff byte k of x is zero
+    uint32_t y = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    y = ~(y | x | 0x7F7F7F7Fu);               // 0x80 in every zero byte
+    return ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
+  };
+  uint32_t z = zb(q.x) | (zb(q.y) << 4) | (zb(q.z) << 8) | (zb(q.w) << 12);
+  const int64_t rb = 16 * i - S.mis;           // region index of byte 0 of this block
+  uint32_t z16 = (zb(nxt) & 1u);               // the byte at region index R counts as non-zero
+  if (rb + 16 >= S.R) z16 = 0;
+  if (rb + 16 > S.R) { const int64_t keep = S.R - rb; z &= keep <= 0 ? 0u : (uint32_t)((1u << keep) - 1u); }
+  uint32_t m = z & ~((z >> 1) | (z16 << 15));
+  if (rb < 3) { const int64_t drop = 3 - rb; m &= drop >= 16 ? 0u : ~((1u << drop) - 1u); }
+  if (i >= S.nblk) m = 0;
+  return m;
+}
+
+__global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+                                                  const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
+                                                  DPosChunk* __restrict__ pcs) {
+  DPosChunk& C = pcs[blockIdx.x];
+  const DPage pg = pages[C.page];
+  const DChunk ck = chunks[pg.chunk];
+  StrRegion S;
   __shared__ int lds[12];
-  const int t = threadIdx.x;
-  if (t == 0) s_fail = 0;
-  __syncthreads();
-  // Candidate scan over 16-byte ALIGNED blocks of the absolute address space (one dwordx4 per
-  // lane, the 4 look-ahead bytes come from the next lane's block): block i covers region bytes
-  // [16i - mis, 16i - mis + 16). A candidate is the last zero byte j of a zero run (byte j+1
-  // non-zero, or j+1 == R), giving the prefix start q = j - 3.
-  const uintptr_t abase = (uintptr_t)r & ~(uintptr_t)15;
-  const int64_t mis = (int64_t)((uintptr_t)r - abase);
-  const int64_t nblk = (mis + R + 15) >> 4;
-  const uint4* blk = (const uint4*)abase;
-  int carry = 0;
-  for (int64_t i0 = 0; i0 < nblk; i0 += NT) {
-    const int64_t i = i0 + t;
-    uint4 q = make_uint4(0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u);
-    if (i < nblk) q = blk[i];
-    uint32_t nxt = __shfl_down(q.x, 1, 64);
-    if ((t & 63) == 63 && i + 1 < nblk) nxt = ((const uint32_t*)(blk + i + 1))[0];
-    auto zb = [](uint32_t x) -> uint32_t {      // bit k set iff byte k of x is zero
-      uint32_t y = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
-      y = ~(y | x | 0x7F7F7F7Fu);               // 0x80 in every zero byte
-      return ((y >> 7) & 1u) | ((y >> 14) & 2u) | ((y >> 21) & 4u) | ((y >> 28) & 8u);
-    };
-    uint32_t z = zb(q.x) | (zb(q.y) << 4) | (zb(q.z) << 8) | (zb(q.w) << 12);
-    const int64_t rb = 16 * i - mis;            // region index of byte 0 of this block
-    // the byte at region index R (past the region) counts as non-zero
-    uint32_t z16 = (zb(nxt) & 1u);
-    if (rb + 16 >= R) z16 = 0;
-    if (rb + 16 > R) { int64_t keep = R - rb; z &= keep <= 0 ? 0u : (uint32_t)((1u << keep) - 1u); }
-    uint32_t m = z & ~((z >> 1) | (z16 << 15));
-    // prefix start q = j - 3 must be >= 0
-    if (rb < 3) { int64_t drop = 3 - rb; m &= drop >= 16 ? 0u : ~((1u << drop) - 1u); }
-    if (i >= nblk) m = 0;
-    int cnt = __popc(m);
-    int base, d0, d1, tot, t1, t2;
-    block_scan3(cnt, 0, 0, &base, &d0, &d1, &tot, &t1, &t2, lds);
-    if (carry + tot > n) { if (t == 0) s_fail = 1; }
-    else {
-      int k = carry + base;
-      while (m) { int j = __ffs(m) - 1; m &= m - 1; P[k++] = (int32_t)(rb + j - 3); }
-    }
-    carry += tot;
-    if (carry > n) break;
+  int cnt = 0;
+  if (str_region(pg, ck, arena, pos, S) && (int64_t)C.blk0 < S.nblk) {
+#pragma unroll
+    for (int j = 0; j < POS_BPT; j++) cnt += __popc(pos_cand_mask(S, (int64_t)C.blk0 + j * NT + threadIdx.x));
   }
-  __syncthreads();
-  if (carry != n) s_fail = 1;   // same value in every lane
-  __syncthreads();
-  if (!s_fail) {
-    for (int k = t; k < n; k += NT) {
-      int64_t pk = P[k];
-      int64_t nxt = (k + 1 < n) ? (int64_t)P[k + 1] : R;
-      if (k == 0 && pk != 0) s_fail = 1;
-      if (pk + 4 > R || pk + 4 + (int64_t)ld_u32(r + pk) != nxt) s_fail = 1;
-    }
+  int e0, e1, e2, tot, t1, t2;
+  block_scan3(cnt, 0, 0, &e0, &e1, &e2, &tot, &t1, &t2, lds);
+  if (threadIdx.x == 0) C.cnt = tot;
+}
+
+__global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                 const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
+                                                 DPosChunk* __restrict__ pcs) {
+  DPage& pgw = pages[blockIdx.x];
+  const DPage pg = pgw;
+  if (pg.npchunk == 0) return;
+  const DChunk ck = chunks[pg.chunk];
+  StrRegion S;
+  if (!str_region(pg, ck, arena, pos, S)) return;
+  __shared__ int lds[12];
+  int run = 0;
+  for (int c0 = 0; c0 < pg.npchunk; c0 += NT) {
+    const int c = c0 + threadIdx.x;
+    const int v = c < pg.npchunk ? pcs[pg.pchunk0 + c].cnt : 0;
+    int ex, e1, e2, tot, t1, t2;
+    block_scan3(v, 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
+    if (c < pg.npchunk) pcs[pg.pchunk0 + c].base = run + ex;
+    run += tot;
   }
-  __syncthreads();
-  if (s_fail && t == 0) {
-    int64_t q = 0;
-    int bad = 0;
-    for (int k = 0; k < n; k++) {
-      if (q + 4 > R) { bad = 1; break; }
-      P[k] = (int32_t)q;
-      q += 4 + (int64_t)ld_u32(r + q);
-      if (q > R) { bad = 1; break; }
-    }
-    if (bad) pages[page0 + blockIdx.x].status = dict ? PS_BAD_DICT : PS_BAD_VALUES;
+  if (threadIdx.x == 0) {
+    pgw.pos_fail = run != S.n;
+    S.P[S.n] = (int32_t)S.R;
   }
-  if (t == 0) P[n] = (int32_t)R;
+}
+
+__global__ __launch_bounds__(NT) void k_pos_write(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+                                                  const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
+                                                  const DPosChunk* __restrict__ pcs) {
+  const DPosChunk C = pcs[blockIdx.x];
+  const DPage pg = pages[C.page];
+  if (pg.pos_fail || C.cnt == 0) return;
+  const DChunk ck = chunks[pg.chunk];
+  StrRegion S;
+  if (!str_region(pg, ck, arena, pos, S)) return;
+  __shared__ int lds[12];
+  int run = C.base;
+#pragma unroll
+  for (int j = 0; j < POS_BPT; j++) {
+    const int64_t i = (int64_t)C.blk0 + j * NT + threadIdx.x;
+    uint32_t m = pos_cand_mask(S, i);
+    int ex, e1, e2, tot, t1, t2;
+    block_scan3(__popc(m), 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
+    int k = run + ex;
+    const int64_t rb = 16 * i - S.mis;
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      if (k < S.n) S.P[k] = (int32_t)(rb + b - 3);
+      k++;
+    }
+    run += tot;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_pos_verify(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
+                                                   const DPosChunk* __restrict__ pcs) {
+  const DPosChunk C = pcs[blockIdx.x];
+  const DPage pg = pages[C.page];
+  if (pg.pos_fail || C.cnt == 0) return;
+  const DChunk ck = chunks[pg.chunk];
+  StrRegion S;
+  if (!str_region(pg, ck, arena, pos, S)) return;
+  bool bad = false;
+  const int kend = min(C.base + C.cnt, S.n);
+  for (int k = C.base + threadIdx.x; k < kend; k += NT) {
+    const int64_t pk = S.P[k];
+    const int64_t nx = k + 1 < S.n ? (int64_t)S.P[k + 1] : S.R;
+    if (k == 0 && pk != 0) bad = true;
+    if (pk + 4 > S.R || pk + 4 + (int64_t)ld_u32(S.r + pk) != nx) bad = true;
+  }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) pages[C.page].pos_fail = 1;
+}
+
+__global__ void k_pos_fallback(const DChunk* __restrict__ chunks, DPage* __restrict__ pages, int n_pages,
+                               const uint8_t* __restrict__ arena, int32_t* __restrict__ pos) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pages) return;
+  const DPage pg = pages[i];
+  if (!pg.pos_fail || pg.npchunk == 0) return;
+  const DChunk ck = chunks[pg.chunk];
+  StrRegion S;
+  if (!str_region(pg, ck, arena, pos, S)) return;
+  int64_t q = 0;
+  bool bad = false;
+  for (int k = 0; k < S.n; k++) {
+    if (q + 4 > S.R) { bad = true; break; }
+    S.P[k] = (int32_t)q;
+    q += 4 + (int64_t)ld_u32(S.r + q);
+    if (q > S.R) { bad = true; break; }
+  }
+  S.P[S.n] = (int32_t)S.R;
+  if (bad) pages[i].status = (pg.flags & PF_DICT) ? PS_BAD_DICT : PS_BAD_VALUES;
 }
 
 __device__ __forceinline__ const uint8_t* dict_data(const DChunk& ck, const DPage* pages, const uint8_t* arena,
@@ -535,6 +614,7 @@ __global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ 
 // --------------------------------------------------------------------------------------------
 constexpr int TL = DK_LEVEL_TILE;
 constexpr int LPT = TL / NT;           // levels per thread
+constexpr int DSTAGE = 8192;          // dictionary bytes staged in LDS by k_tile_decode
 
 // lane-serial walk of one hybrid stream's run headers; returns the number of runs, *cover = values
 // covered. strict: the stream must cover `limit` values (levels), else PS_BAD_LEVELS.
@@ -796,6 +876,21 @@ __global__ __launch_bounds__(NT) void k_tile_scan2(DColumn* __restrict__ cols, D
   }
 }
 
+// block-cooperative byte fill: aligned dwordx4 stores, byte stores for the two edges
+__device__ __forceinline__ void fill_bytes(uint8_t* p, int64_t n, uint8_t v) {
+  const uintptr_t a = (uintptr_t)p, e = a + n;
+  const uintptr_t a16 = (a + 15) & ~(uintptr_t)15, e16 = e & ~(uintptr_t)15;
+  const uint32_t w = 0x01010101u * v;
+  if (a16 >= e16) {
+    for (uintptr_t x = a + threadIdx.x; x < e; x += blockDim.x) *(uint8_t*)x = v;
+    return;
+  }
+  for (uintptr_t x = a + threadIdx.x; x < a16; x += blockDim.x) *(uint8_t*)x = v;
+  for (uintptr_t x = e16 + threadIdx.x; x < e; x += blockDim.x) *(uint8_t*)x = v;
+  for (uintptr_t x = a16 + (uintptr_t)threadIdx.x * 16; x < e16; x += (uintptr_t)blockDim.x * 16)
+    *(uint4*)x = make_uint4(w, w, w, w);
+}
+
 // k_tile_decode: the tile's levels are dealt to lanes STRIDED (level lvl0 + k*NT + t, k < LPT) so
 // that every store instruction of the emit phase writes consecutive addresses across the wave
 // (coalesced row_def / offs / fixed / hash stores). Ranks within the tile come from wave ballots
@@ -835,6 +930,21 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
     ibw = L.val_p < L.val_e ? (int)(*L.val_p) : 0;
   }
   const int32_t* P = (is_str && pg.enc == ENC_PLAIN) ? pos + pg.pos_base : nullptr;
+  __shared__ int s_fill;
+  // null-only column whose def levels over the whole tile are ONE RLE run: every level is a row
+  // with the same def level and nothing but row_def is materialised -> a vectorised fill
+  if (col.null_only && !rep && ck.max_def > 0) {
+    if (t == 0) {
+      RunCur c0;
+      c0.init(runs + pg.run_d, pg.nrun_d, T.lvl0);
+      s_fill = (c0.cur.bp_idx < 0 && c0.next >= l_end) ? (int)c0.cur.val : -1;
+    }
+    __syncthreads();
+    if (s_fill >= 0) {
+      fill_bytes(col.row_def + T.row_base, l_end - T.lvl0, (uint8_t)s_fill);
+      return;
+    }
+  }
   __shared__ int wcnt[3][LPT][NW];          // per (k, wave): rows, entries, values
   __shared__ int wbase[3][LPT][NW];         // their exclusive scan in level order
   __shared__ long long wch[LPT][NW];        // dictionary strings: chars per (k, wave)
@@ -843,6 +953,7 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
   __shared__ long long s_chtot;
   __shared__ int32_t vsrc[TL];              // dictionary strings: source offset in the dictionary page
   __shared__ int32_t vcoff[TL + 1];         // and tile-relative output offset of each value
+  __shared__ uint4 dstage[DSTAGE / 16];     // small dictionary pages
   // 1. levels (strided) and their ballots
   int rp[LPT], df[LPT];
   uint64_t mr[LPT], me[LPT], mv[LPT];
@@ -942,7 +1053,10 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
       col.row_def[grow] = (uint8_t)d;
       if (rep && col.row_offs) col.row_offs[grow] = T.entry_base + e_i;
       // key column: forward the value's path hash (PLAIN pages; 0 = the probe recomputes)
-      if (col.hash) col.hash[grow] = (is_val && P) ? col.vhash[pg.value_base + vloc] : 0ull;
+      if (col.hash)
+        col.hash[grow] = !is_val ? 0ull
+                       : P ? col.vhash[pg.value_base + vloc]
+                       : (is_dict && col.dhash) ? col.dhash[ck.dict_hash_off + ix[k]] : 0ull;
     }
     long long dest = -1;
     if (rep) {
@@ -978,6 +1092,15 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
   if (dict_str && !col.null_only && __syncthreads_or(bad) == 0 && s_chtot > 0) {
     const int32_t nch = (int32_t)s_chtot;
     if (t == 0) vcoff[tv] = nch;
+    // a small dictionary (partition values, tags) is staged in LDS for the gather
+    const DPage& dpg = pages[ck.dict_page];
+    const int32_t dlen = page_len(dpg);
+    const uintptr_t dbase = (uintptr_t)D & ~(uintptr_t)15;
+    const int32_t dmis = (int32_t)((uintptr_t)D - dbase);
+    const bool dstaged = dmis + dlen <= DSTAGE;
+    if (dstaged)
+      for (int q = t; q * 16 < dmis + dlen; q += NT) dstage[q] = ((const uint4*)dbase)[q];
+    const uint8_t* dst8 = (const uint8_t*)dstage + dmis;
     __syncthreads();
     uint8_t* ob = col.chars + T.char_base;
     const uintptr_t lo_a = (uintptr_t)ob & ~(uintptr_t)15, hi_a = (uintptr_t)ob + nch;
@@ -1001,7 +1124,7 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
       uint32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
 #pragma unroll
       for (int j = 0; j < 16; j++) {
-        const uint32_t by = src[j] >= 0 ? (uint32_t)D[src[j]] : 0u;
+        const uint32_t by = src[j] >= 0 ? (uint32_t)(dstaged ? dst8[src[j]] : D[src[j]]) : 0u;
         if (j < 4) q0 |= by << (8 * j);
         else if (j < 8) q1 |= by << (8 * (j - 4));
         else if (j < 12) q2 |= by << (8 * (j - 8));
@@ -1050,17 +1173,34 @@ __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ c
                                                     int tile0, int dbg) {
   const int2 tile = tiles[tile0 + blockIdx.x];     // (page, first value)
   const DPage pg = pages[tile.x];                  // by value: byte stores below may alias
-  if ((pg.flags & PF_DICT) || pg.status != PS_OK) return;
+  if (pg.status != PS_OK) return;
   const DChunk ck = chunks[pg.chunk];
-  if (ck.phys != PT_BYTE_ARRAY || pg.enc != ENC_PLAIN) return;
+  if (ck.phys != PT_BYTE_ARRAY) return;
+  const bool dict = (pg.flags & PF_DICT) != 0;
+  if (!dict && pg.enc != ENC_PLAIN) return;
   const DColumn col = cols[ck.col];
-  uint64_t* vh = (col.vhash && !(dbg & 2)) ? col.vhash + pg.value_base : nullptr;
-  const int n = min(pg.n_values, tile.y + CT);
-  if (n <= tile.y || (pg.n_chars == 0 && !vh)) return;
-  Layout L = page_layout(pg, ck, arena);
-  const uint8_t* r = L.val_p;
-  const int32_t* P = pos + pg.pos_base;
-  uint8_t* ob = (col.chars && !(dbg & 1)) ? col.chars + pg.char_base : nullptr;
+  // data page: chars + key hashes per value; dictionary page of a key column: entry hashes only
+  uint64_t* vh;
+  const uint8_t* r;
+  const int32_t* P;
+  uint8_t* ob;
+  int nvals;
+  if (dict) {
+    if (!col.dhash) return;
+    vh = (dbg & 2) ? nullptr : col.dhash + ck.dict_hash_off;
+    r = page_data(pg, ck, arena);
+    P = pos + ck.dict_pos;
+    ob = nullptr;
+    nvals = pg.num_values;
+  } else {
+    vh = (col.vhash && !(dbg & 2)) ? col.vhash + pg.value_base : nullptr;
+    r = page_layout(pg, ck, arena).val_p;
+    P = pos + pg.pos_base;
+    ob = (col.chars && !(dbg & 1) && pg.n_chars > 0) ? col.chars + pg.char_base : nullptr;
+    nvals = pg.n_values;
+  }
+  const int n = min(nvals, tile.y + CT);
+  if (n <= tile.y || (!ob && !vh)) return;
   const int t = threadIdx.x;
   __shared__ uint4 inw[CT_BYTES / 16 + 2];
   __shared__ uint4 outw[CT_BYTES / 16 + 2];
@@ -1145,6 +1285,32 @@ __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ c
   }
 }
 
+// Byte-exact key verification for a SIMPLE checkpoint path p (the common case): its canonical
+// stream is TAG_PATH + raw bytes, and no non-simple path canonicalises to such a stream (escapes,
+// ':' / '?' / '#' / authority tags and non-ASCII bytes survive canonicalisation), so the streams are
+// equal iff the stored key is TAG_PATH + the same bytes. 8-byte words, aligned loads + funnel
+// shifts. Returns 1 equal, 0 different, -1 p is not simple (use the generic comparator).
+__device__ __forceinline__ uint64_t load8_any(const uint8_t* p, int32_t j) {
+  const uintptr_t pa = (uintptr_t)p + 8 * (uintptr_t)j;
+  const uint64_t* b = (const uint64_t*)(pa & ~(uintptr_t)7);
+  const int sh = (int)(pa & 7) * 8;
+  const uint64_t w0 = b[0];
+  return sh ? (w0 >> sh) | (b[1] << (64 - sh)) : w0;
+}
+__device__ int simple_key_equal(const uint8_t* p, int32_t pl, const uint8_t* key, int32_t key_len) {
+  const int32_t nw = (pl + 7) >> 3;
+  bool eq = key_len == pl + 1 && key[0] == TAG_PATH;
+  for (int32_t j = 0; j < nw; j++) {
+    uint64_t a = load8_any(p, j);
+    const int32_t valid = pl - 8 * j;
+    const uint64_t mask = valid >= 8 ? ~0ull : ((1ull << (8 * valid)) - 1);
+    a &= mask;
+    if (!simple8(a | (0x6161616161616161ull & ~mask)) || (j == 0 && pl >= 2 && (a & 0xffff) == 0x2f2f)) return -1;
+    if (eq) eq = (load8_any(key + 1, j) & mask) == a;
+  }
+  return eq ? 1 : 0;
+}
+
 // --------------------------------------------------------------------------------------------
 // Commit tail: canonical keys, probe-table build, JSON selection
 // --------------------------------------------------------------------------------------------
@@ -1170,15 +1336,31 @@ __global__ void k_json_canon(DJsonAction* __restrict__ acts, int n, const uint8_
   DJsonAction a = acts[i];
   if (a.kind == JA_NONE) return;
   uint8_t* out = canon + a.canon_off;
-  WriteSink w{out, 0, (int64_t)a.path_len + 64};
-  int rc = uri_emit(jchars + a.path_off, a.path_len, w);
-  if (rc) { acts[i].status = rc; atomicOr(&st->err_flags, rc == -1 ? E_URI : E_UTF8); return; }
-  int32_t pl = (int32_t)w.n;
+  const uint8_t* src = jchars + a.path_off;
+  int32_t pl;
+  uint64_t hp = 0;
+  // fast path (plain relative path): stream = TAG_PATH + raw bytes, copied and hashed by 8-byte words
+  auto load8 = [&](int32_t j) -> uint64_t { return load8_any(src, j); };
+  if (simple_path_hash(a.path_len, load8, seed, &hp)) {
+    out[0] = TAG_PATH;
+    for (int32_t j = 0; 8 * j < a.path_len; j++) {
+      const uint64_t wd = load8_any(src, j);
+      const int32_t nb = a.path_len - 8 * j < 8 ? a.path_len - 8 * j : 8;
+      for (int b = 0; b < nb; b++) out[1 + 8 * j + b] = (uint8_t)(wd >> (8 * b));
+    }
+    pl = a.path_len + 1;
+  } else {
+    WriteSink w{out, 0, (int64_t)a.path_len + 64};
+    const int rc = uri_emit(src, a.path_len, w);
+    if (rc) { acts[i].status = rc; atomicOr(&st->err_flags, rc == -1 ? E_URI : E_UTF8); return; }
+    pl = (int32_t)w.n;
+    hp = bytes_hash(out, pl, seed);
+  }
+  int rc;
   WriteSink w2{out + pl, 0, (int64_t)a.st_len + a.pid_len + 32};
   rc = dv_emit(a.has_dv != 0, jchars + a.st_off, a.st_len, jchars + a.pid_off, a.pid_len, a.has_off != 0, a.dv_off, w2);
   if (rc) { acts[i].status = rc; atomicOr(&st->err_flags, E_UTF8); return; }
-  uint64_t hp = bytes_hash(out, pl, seed);
-  uint64_t hd = bytes_hash(out + pl, (int32_t)w2.n, seed);
+  const uint64_t hd = bytes_hash(out + pl, (int32_t)w2.n, seed);
   acts[i].canon_len = pl;
   acts[i].dv_len = (int32_t)w2.n;
   acts[i].h = hash_combine(hp, hd);
@@ -1283,88 +1465,128 @@ __device__ __forceinline__ void block_count3(DState* st, unsigned long long a, u
   }
 }
 
-__global__ __launch_bounds__(NT) void k_probe(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
-                                              const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
-                                              uint32_t seed, uint8_t* __restrict__ sel, DState* __restrict__ st) {
-  // grid-stride over rows; the three counters are reduced per workgroup (one atomic each per
-  // workgroup: per-wave atomics on three addresses serialise at ~10 ns apiece)
-  unsigned long long n_seen = 0, n_chosen = 0, n_dup = 0;
-  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < pc.n_rows;
-       r += (long long)gridDim.x * blockDim.x) {
-    bool seen = false, chosen = false, dup = false;
-    if (pc.path_def[r] >= 1) {
+// Checkpoint add rows are probed in two passes:
+//   k_probe_fast  branch-light: path-def, the decode-time path hash, one table walk. A row whose
+//                 hash misses the table is decided here (selected: its key is not in the commit
+//                 tail). Rows that hit a slot (need byte verification), carry a deletion vector, or
+//                 have no fast-path hash (dictionary pages, non-simple URIs) are appended to a
+//                 candidate list (wave-aggregated atomic).
+//   k_probe_cand  the full key path for the candidates: canonical URI hash (java.net.URI rules),
+//                 dvUniqueId stream, byte-exact verification against the tail key, counters.
+__global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
+                                                   uint64_t h_nodv, uint8_t* __restrict__ sel,
+                                                   int32_t* __restrict__ cand, unsigned int* __restrict__ cand_n,
+                                                   DState* __restrict__ st) {
+  unsigned long long n_seen = 0, n_chosen = 0;
+  const int lane = threadIdx.x & 63;
+  for (long long r0 = (long long)blockIdx.x * blockDim.x; r0 < pc.n_rows; r0 += (long long)gridDim.x * blockDim.x) {
+    const long long r = r0 + threadIdx.x;
+    bool seen = false, chosen = false, defer = false;
+    if (r < pc.n_rows && pc.path_def[r] >= 1) {
       seen = true;
-      uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
-      const uint8_t* p = nullptr;      // path bytes: needed only to hash (hp == 0) or verify a hit
-      int32_t pl = 0;
-      auto load_path = [&]() {
-        if (p) return;
-        const int64_t o0 = pc.path_offs[r];
-        p = pc.path_chars + o0;
-        pl = (int32_t)(pc.path_offs[r + 1] - o0);
-      };
-      bool has_dv = pc.has_dv && pc.st_def[r] >= 2;
-      const uint8_t* sp = nullptr; const uint8_t* pp = nullptr;
-      int32_t sl = 0, ppl = 0, off = 0;
-      bool has_off = false;
-      if (has_dv) {
-        sp = pc.st_chars + pc.st_offs[r]; sl = (int32_t)(pc.st_offs[r + 1] - pc.st_offs[r]);
-        pp = pc.pid_chars + pc.pid_offs[r]; ppl = (int32_t)(pc.pid_offs[r + 1] - pc.pid_offs[r]);
-        has_off = pc.off_def != nullptr && pc.off_def[r] == pc.off_maxdef;
-        off = has_off ? pc.off_vals[r] : 0;
-      }
-      int rc = 0;
-      if (!hp) {
-        load_path();
-        // aligned 8-byte loads + funnel shift (no reliance on unaligned-access mode)
-        const uintptr_t pa = (uintptr_t)p;
-        const uint64_t* base = (const uint64_t*)(pa & ~(uintptr_t)7);
-        const int sh = (int)(pa & 7) * 8;
-        auto load8 = [&](int32_t j) -> uint64_t {
-          uint64_t w0 = base[j];
-          if (!sh) return w0;
-          uint64_t w1 = base[j + 1];
-          return (w0 >> sh) | (w1 << (64 - sh));
-        };
-        if (!simple_path_hash(pl, load8, seed, &hp)) rc = path_hash(p, pl, seed, &hp);
-      }
-      HashSink kd; kd.hs.init(kHashSeed(seed)); kd.n = 0;
-      int rc2 = dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, kd);
-      if (rc || rc2) {
-        set_err(st, (rc == -1) ? E_URI : E_UTF8, pc.row_tag + r, 0);
+      const uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
+      if (hp == 0 || (pc.has_dv && pc.st_def[r] >= 2)) {
+        defer = true;
       } else {
-        uint64_t h = hash_combine(hp, kd.hs.final_(kd.n));
-        uint64_t s = h & mask;
-        int found = 0;
-        Slot sl_;
-        while (slots[s].h != 0ull) {
-          if (slots[s].h == h) {
-            sl_ = slots[s];
-            load_path();
-            const DJsonAction& a = acts[sl_.rep];
-            CmpSink cmp{canon + a.canon_off, a.canon_len, 0, 1};
-            uri_emit(p, pl, cmp);
-            bool eq = cmp.eq && cmp.n == a.canon_len;
-            if (eq) {
-              CmpSink c2{canon + a.canon_off + a.canon_len, a.dv_len, 0, 1};
-              dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, c2);
-              eq = c2.eq && c2.n == a.dv_len;
-            }
-            if (eq) { found = 1; break; }
-          }
-          s = (s + 1) & mask;
+        const uint64_t h = hash_combine(hp, h_nodv);
+        uint64_t q = h & mask;
+        unsigned long long k;
+        while ((k = slots[q].h) != 0ull) {
+          if (k == h) { defer = true; break; }
+          q = (q + 1) & mask;
         }
-        if (found) {
-          dup = sl_.first_add != ~0ull;            // alreadyReturned -> duplicate
-        } else {
-          chosen = true;
-        }
+        chosen = !defer;
       }
     }
-    sel[r] = chosen;
-    n_seen += seen; n_chosen += chosen; n_dup += dup;
+    if (r < pc.n_rows && !defer) sel[r] = chosen;
+    const uint64_t m = __ballot(defer);
+    if (m) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(cand_n, (unsigned int)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (defer) cand[base + lane_rank(m)] = (int32_t)r;
+    }
+    n_seen += seen; n_chosen += chosen;
   }
-  block_count3(st, n_seen, n_chosen, n_dup);
+  block_count3(st, n_seen, n_chosen, 0);
+}
+
+__global__ __launch_bounds__(NT) void k_probe_cand(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
+                                                   const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
+                                                   uint32_t seed, uint8_t* __restrict__ sel,
+                                                   const int32_t* __restrict__ cand, const unsigned int* __restrict__ cand_n,
+                                                   DState* __restrict__ st) {
+  unsigned long long n_chosen = 0, n_dup = 0;
+  const long long nc = *cand_n;
+  for (long long ci = (long long)blockIdx.x * blockDim.x + threadIdx.x; ci < nc; ci += (long long)gridDim.x * blockDim.x) {
+    const long long r = cand[ci];
+    bool chosen = false, dup = false;
+    uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
+    const int64_t o0 = pc.path_offs[r];
+    const uint8_t* p = pc.path_chars + o0;
+    const int32_t pl = (int32_t)(pc.path_offs[r + 1] - o0);
+    const bool has_dv = pc.has_dv && pc.st_def[r] >= 2;
+    const uint8_t* sp = nullptr; const uint8_t* pp = nullptr;
+    int32_t sl = 0, ppl = 0, off = 0;
+    bool has_off = false;
+    if (has_dv) {
+      sp = pc.st_chars + pc.st_offs[r]; sl = (int32_t)(pc.st_offs[r + 1] - pc.st_offs[r]);
+      pp = pc.pid_chars + pc.pid_offs[r]; ppl = (int32_t)(pc.pid_offs[r + 1] - pc.pid_offs[r]);
+      has_off = pc.off_def != nullptr && pc.off_def[r] == pc.off_maxdef;
+      off = has_off ? pc.off_vals[r] : 0;
+    }
+    int rc = 0;
+    if (!hp) {
+      // aligned 8-byte loads + funnel shift (no reliance on unaligned-access mode)
+      const uintptr_t pa = (uintptr_t)p;
+      const uint64_t* base = (const uint64_t*)(pa & ~(uintptr_t)7);
+      const int sh = (int)(pa & 7) * 8;
+      auto load8 = [&](int32_t j) -> uint64_t {
+        uint64_t w0 = base[j];
+        if (!sh) return w0;
+        uint64_t w1 = base[j + 1];
+        return (w0 >> sh) | (w1 << (64 - sh));
+      };
+      if (!simple_path_hash(pl, load8, seed, &hp)) rc = path_hash(p, pl, seed, &hp);
+    }
+    HashSink kd; kd.hs.init(kHashSeed(seed)); kd.n = 0;
+    const int rc2 = dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, kd);
+    if (rc || rc2) {
+      set_err(st, (rc == -1) ? E_URI : E_UTF8, pc.row_tag + r, 0);
+    } else {
+      const uint64_t h = hash_combine(hp, kd.hs.final_(kd.n));
+      uint64_t q = h & mask;
+      int found = 0;
+      Slot sl_;
+      while (slots[q].h != 0ull) {
+        if (slots[q].h == h) {
+          sl_ = slots[q];
+          const DJsonAction& a = acts[sl_.rep];
+          int fe = simple_key_equal(p, pl, canon + a.canon_off, a.canon_len);
+          if (fe < 0) {
+            CmpSink cmp{canon + a.canon_off, a.canon_len, 0, 1};
+            uri_emit(p, pl, cmp);
+            fe = cmp.eq && cmp.n == a.canon_len;
+          }
+          bool eq = fe == 1;
+          if (eq && !has_dv) {
+            eq = a.dv_len == 1 && canon[a.canon_off + a.canon_len] == 0;   // "no DV" stream = one 0 byte
+          } else if (eq) {
+            CmpSink c2{canon + a.canon_off + a.canon_len, a.dv_len, 0, 1};
+            dv_emit(has_dv, sp, sl, pp, ppl, has_off, off, c2);
+            eq = c2.eq && c2.n == a.dv_len;
+          }
+          if (eq) { found = 1; break; }
+        }
+        q = (q + 1) & mask;
+      }
+      if (found) dup = sl_.first_add != ~0ull;      // alreadyReturned -> duplicate
+      else chosen = true;
+    }
+    sel[r] = chosen;
+    n_chosen += chosen; n_dup += dup;
+  }
+  block_count3(st, 0, n_chosen, n_dup);
 }
 
 }  // namespace dk
@@ -1380,9 +1602,14 @@ void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
 void launch_snappy(const DChunk* c, DPage* p, int n, uint8_t* arena, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_snappy, dim3(n), dim3(64), 0, s, c, p, arena);
 }
-void launch_string_positions(const DChunk* c, DPage* p, int n, const uint8_t* arena, int32_t* pos, int mode,
-                             hipStream_t s, int page0) {
-  if (n) hipLaunchKernelGGL(k_string_positions, dim3(n), dim3(NT), 0, s, c, p, arena, pos, mode, page0);
+void launch_positions(const DChunk* c, DPage* p, int n_pages, const uint8_t* arena, int32_t* pos, DPosChunk* pcs,
+                      int npc, hipStream_t s) {
+  if (!npc) return;
+  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_verify, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p, n_pages, arena, pos);
 }
 void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_runs, dim3((n + 63) / 64), dim3(64), 0, s, c, p, n, arena, runs);
@@ -1433,12 +1660,14 @@ void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint8_t*
   if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, sel, st);
 }
 void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const DJsonAction* acts,
-                  const uint8_t* canon, uint32_t seed, uint8_t* sel, DState* st, hipStream_t s) {
-  if (pc.n_rows) {
-    const long long want = (pc.n_rows + NT - 1) / NT;
-    const unsigned grid = (unsigned)(want < 2048 ? want : 2048);   // 256 CUs x 8 workgroups
-    hipLaunchKernelGGL(k_probe, dim3(grid), dim3(NT), 0, s, pc, slots, mask, acts, canon, seed, sel, st);
-  }
+                  const uint8_t* canon, uint32_t seed, uint64_t h_nodv, uint8_t* sel, int32_t* cand,
+                  unsigned int* cand_n, DState* st, hipStream_t s) {
+  if (!pc.n_rows) return;
+  const long long want = (pc.n_rows + NT - 1) / NT;
+  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);   // 256 CUs x 8 workgroups
+  hipMemsetAsync(cand_n, 0, sizeof(unsigned int), s);
+  hipLaunchKernelGGL(k_probe_fast, dim3(grid), dim3(NT), 0, s, pc, slots, mask, h_nodv, sel, cand, cand_n, st);
+  hipLaunchKernelGGL(k_probe_cand, dim3(grid), dim3(NT), 0, s, pc, slots, mask, acts, canon, seed, sel, cand, cand_n, st);
 }
 
 }  // namespace dk
