@@ -38,6 +38,21 @@ def make_table(root, rows, seed, compression):
     return synth.write_table(root, spec)
 
 
+def pmc_traffic(kernel, rows, compression):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same workload
+    (tools/pmc.sh + tools/pmc_summary.py --json: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
+    doubled for gfx950's half-count of wide loads, KB -> bytes), or None when no profile matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("rows") != rows or d.get("compression") != compression or kernel not in d.get("kernels", {}):
+        return None
+    return {"bytes": d["kernels"][kernel], "source": "profiles/pmc_traffic.json (%s)" % d.get("profile", "?")}
+
+
 def cpu_baseline(rows, reps, seed, compression):
     """Oracle (plain C restatement, single thread) on a bounded sample of the same workload."""
     from oracle import ref
@@ -151,7 +166,15 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     dom = max(kern.items(), key=lambda kv: kv[1]) if kern else ("none", 0.0)
     step_bytes = bytes_read + bytes_written
-    achieved = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
+    step_gbs = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
+    # roofline of the dominant decode kernel: algorithmic bytes of one launch (byte model in
+    # dk_parquet_kernel_traffic) / its average launch time (HIP events, engine stream)
+    modelled = [k for k in ("k_tile_decode", "k_string_copy") if k in kern]
+    rk = max(modelled, key=lambda k: kern[k]) if modelled else None
+    k_read, k_written = scan.ckpt.kernel_traffic(rk) if rk else (0, 0)
+    k_bytes = k_read + k_written
+    achieved = k_bytes / (kern[rk] * 1e-6) / 1e9 if rk else None
+    pmc = pmc_traffic(rk, n_ckpt_rows, args.compression) if rk else None
 
     result = {
         "metric": "checkpoint actions reconciled/sec (node) + snapshot load ms, 100M AddFile",
@@ -175,12 +198,16 @@ def main():
         "prepare_s": prepare_s,
         "counters": counters,
         "kernels_us": {k: round(v, 2) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])},
-        "roofline": {"bound": "hbm", "kernel": "device step (all kernels, HIP events on the engine stream)",
+        "roofline": {"bound": "hbm", "kernel": rk, "kernel_us": kern.get(rk),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": None, "algorithmic_bytes": step_bytes,
-                     "bytes_read": bytes_read, "bytes_written": bytes_written,
-                     "step_device_us": step_us, "dominant_kernel": dom[0], "dominant_kernel_us": dom[1]},
+                     "traffic": pmc["bytes"] if pmc else None,
+                     "traffic_source": pmc["source"] if pmc else None,
+                     "algorithmic_bytes": k_bytes, "algorithmic_read": k_read, "algorithmic_written": k_written,
+                     "dominant_kernel": dom[0], "dominant_kernel_us": dom[1],
+                     "step": {"device_us": step_us, "algorithmic_bytes": step_bytes, "bytes_read": bytes_read,
+                              "bytes_written": bytes_written, "achieved_gbs": step_gbs,
+                              "frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None}},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         result["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.cpu_reps, 20250218, args.compression)

@@ -30,7 +30,7 @@ class dk_column(C.Structure):
 
 EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
-           "dk_parquet_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
+           "dk_parquet_traffic", "dk_parquet_kernel_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_run", "dk_replay_sync",
            "dk_replay_counters", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free"]
@@ -56,6 +56,7 @@ def lib(build_if_missing=True):
         "dk_parquet_num_rows": (I64, [P, I32]),
         "dk_parquet_column": (C.c_int, [P, I32, I32, C.POINTER(dk_column)]),
         "dk_parquet_traffic": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
+        "dk_parquet_kernel_traffic": (C.c_int, [P, C.c_char_p, C.POINTER(I64), C.POINTER(I64)]),
         "dk_parquet_close": (None, [P]),
         "dk_json_tail_parse": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(I64), I32, I32, C.POINTER(P)]),
         "dk_json_tail_rows": (I64, [P]),

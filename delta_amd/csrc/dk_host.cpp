@@ -747,6 +747,48 @@ extern "C" int dk_parquet_traffic(dk_parquet* p, int64_t* r, int64_t* w) {
   *r = p->bytes_read; *w = p->bytes_written; return 0;
 }
 
+// Algorithmic bytes of one launch of a decode kernel ("Roofline"): what the kernel must
+// read and write at minimum, from the page / column metadata of the last prepare.
+extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int64_t* r, int64_t* w) {
+  if (!p || !kernel || !p->prepared) return fail("dk_parquet_kernel_traffic: not prepared");
+  const std::string k = kernel;
+  int64_t rd = 0, wr = 0;
+  for (size_t ci = 0; ci < p->h_cols.size(); ci++) {
+    const DColumn& c = p->h_cols[ci];
+    const bool key = c.hash != nullptr;
+    for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
+      const DPage& pg = p->h_pages[pi];
+      const int64_t body = pg.unc_off >= 0 ? pg.usize : pg.csize;
+      const bool plain_str = c.phys == PT_BYTE_ARRAY && pg.enc == ENC_PLAIN;
+      if (k == "k_string_copy") {
+        if (plain_str) { rd += pg.vbytes; wr += pg.n_chars + (key ? 8ll * pg.n_values : 0); }
+      } else if (k == "k_tile_decode") {
+        rd += body - pg.vbytes;                                   // level streams
+        if (!plain_str) rd += pg.vbytes;                          // values / dictionary indices
+        else rd += 4ll * pg.n_values + (key ? 8ll * pg.n_values : 0);   // positions (+ value hashes)
+        wr += pg.n_rows;                                          // row_def
+        if (c.max_rep > 0) wr += 8ll * pg.n_rows + pg.n_entries;  // row_offs, entry_def
+        if (!c.null_only) {
+          const int64_t nv = c.max_rep > 0 ? pg.n_entries : pg.n_rows;
+          if (c.phys == PT_BYTE_ARRAY) wr += 8ll * nv + (plain_str ? 0 : pg.n_chars);   // offs (+ dict chars)
+          else wr += (int64_t)c.width * nv;
+        }
+        if (key) wr += 8ll * pg.n_rows;                           // key hash per row
+      } else {
+        return fail("dk_parquet_kernel_traffic: no byte model for " + k);
+      }
+    }
+    if (k == "k_tile_decode")                                     // dictionary pages (read once)
+      for (const DChunk& ck : p->h_chunks)
+        if (ck.col == (int)ci && ck.dict_page >= 0) {
+          const DPage& d = p->h_pages[ck.dict_page];
+          rd += d.unc_off >= 0 ? d.usize : d.csize;
+        }
+  }
+  *r = rd; *w = wr;
+  return 0;
+}
+
 extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out) {
   memset(out, 0, sizeof *out);
   HIPOK(hipStreamSynchronize(p->eng->stream));

@@ -117,6 +117,12 @@ class ParquetSet:
         check(lib().dk_parquet_traffic(self._h, C.byref(r), C.byref(w)))
         return r.value, w.value
 
+    def kernel_traffic(self, kernel):
+        """Algorithmic (read, written) bytes of one launch of a decode kernel."""
+        r, w = C.c_int64(), C.c_int64()
+        check(lib().dk_parquet_kernel_traffic(self._h, kernel.encode(), C.byref(r), C.byref(w)))
+        return r.value, w.value
+
     def close(self):
         if self._h:
             lib().dk_parquet_close(self._h)

@@ -79,6 +79,8 @@ int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file);
 int  dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out);
 /* bytes read (projected column chunks) and written (decoded buffers) per decode, for roofline */
 int  dk_parquet_traffic(dk_parquet* p, int64_t* bytes_read, int64_t* bytes_written);
+/* algorithmic bytes one launch of a decode kernel must move ("k_string_copy", "k_tile_decode") */
+int  dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int64_t* bytes_read, int64_t* bytes_written);
 void dk_parquet_close(dk_parquet* p);
 
 /* ---- Commit tail (host JSON parse, newest commit first, batches of json_batch_size lines) ----

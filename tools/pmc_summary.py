@@ -1,24 +1,42 @@
-"""Summarise tools/pmc.sh output: per kernel, the counters averaged per dispatch (FETCH_SIZE and
-WRITE_SIZE in KB as rocprofv3 reports them). Usage: python tools/pmc_summary.py gpurun_out/<tag>"""
+"""Summarise tools/pmc.sh output: per kernel, each counter averaged over the kernel's dispatches.
+
+    python tools/pmc_summary.py gpurun_out/<tag>                      # table
+    python tools/pmc_summary.py gpurun_out/<tag> --json OUT --rows N --compression none --profile NAME
+
+--json writes the per-launch HBM traffic bench.py reports as roofline.traffic:
+    bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide coalesced
+reads (MI355X_MICROARCH.md, HBM), hence the factor 2 (an upper estimate for narrower loads).
+"""
+import argparse
 import collections
 import csv
 import glob
+import json
 import os
-import sys
 
-root = sys.argv[1]
+ap = argparse.ArgumentParser()
+ap.add_argument("root")
+ap.add_argument("--json")
+ap.add_argument("--rows", type=int)
+ap.add_argument("--compression", default="none")
+ap.add_argument("--profile", default="")
+args = ap.parse_args()
+
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in sorted(glob.glob(os.path.join(root, "p*", "*counter_collection.csv"))):
+for f in sorted(glob.glob(os.path.join(args.root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0]
-        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-names = sorted({c for k in acc.values() for c in k})
-print("kernel".ljust(28), " ".join(n[:14].rjust(14) for n in names))
-for k, d in sorted(acc.items()):
-    row = []
-    for n in names:
-        v = d.get(n)
-        # each dispatch may report one value per (dimension) instance; sum per dispatch is not
-        # recoverable here, so report the mean of all samples times samples-per-dispatch
-        row.append(("%.4g" % (sum(v) / max(1, len(v)))).rjust(14) if v else "-".rjust(14))
-    print(k[:28].ljust(28), " ".join(row))
+        acc[r["Kernel_Name"].split("(")[0].replace("dk::", "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
+mean = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+names = sorted({c for d in mean.values() for c in d})
+print("kernel".ljust(26), " ".join(n[:14].rjust(14) for n in names))
+for k, d in sorted(mean.items()):
+    print(k[:26].ljust(26), " ".join(("%.4g" % d[n]).rjust(14) if n in d else "-".rjust(14) for n in names))
+if args.json:
+    ker = {k: int((2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024) for k, d in mean.items()
+           if "FETCH_SIZE" in d and "WRITE_SIZE" in d}
+    with open(args.json, "w") as f:
+        json.dump({"rows": args.rows, "compression": args.compression, "profile": args.profile,
+                   "formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 per launch", "kernels": ker}, f, indent=1,
+                  sort_keys=True)
+    print("wrote", args.json)
