@@ -32,7 +32,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
            "dk_parquet_traffic", "dk_parquet_kernel_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_run", "dk_replay_sync",
-           "dk_replay_counters", "dk_replay_json_selection", "dk_replay_ckpt_selection",
+           "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free"]
 
 
@@ -65,6 +65,7 @@ def lib(build_if_missing=True):
         "dk_replay_create": (C.c_int, [P, P, P, C.POINTER(P)]),
         "dk_replay_run": (C.c_int, [P]), "dk_replay_sync": (C.c_int, [P]),
         "dk_replay_counters": (C.c_int, [P, C.POINTER(I64)]),
+        "dk_replay_counters_split": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
         "dk_replay_json_selection": (C.c_int, [P, P, I64]),
         "dk_replay_ckpt_selection": (C.c_int, [P, I32, P, I64]),
         "dk_replay_kernel_stats": (C.c_int, [P, I32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(I64)]),

@@ -128,7 +128,8 @@ enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8 };
 
 // Device-side counters and error state of one replay.
 struct DState {
-  unsigned long long counters[5];
+  unsigned long long counters[5];        // commit-tail part (k_json_select)
+  unsigned long long ckpt_counters[5];   // checkpoint part (k_probe_fast / k_probe_cand)
   int32_t err_flags;
   int32_t err_row_part;
   long long err_row;

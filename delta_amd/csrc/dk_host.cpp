@@ -1464,7 +1464,13 @@ extern "C" int dk_replay_sync(dk_replay* r) {
 
 extern "C" int dk_replay_counters(dk_replay* r, int64_t out[5]) {
   if (!r->have_result) return fail("replay has no result (call dk_replay_sync)");
-  for (int i = 0; i < 5; i++) out[i] = (int64_t)r->h_state.counters[i];
+  for (int i = 0; i < 5; i++) out[i] = (int64_t)(r->h_state.counters[i] + r->h_state.ckpt_counters[i]);
+  return 0;
+}
+
+extern "C" int dk_replay_counters_split(dk_replay* r, int64_t tail[5], int64_t ckpt[5]) {
+  if (!r->have_result) return fail("replay has no result (call dk_replay_sync)");
+  for (int i = 0; i < 5; i++) { tail[i] = (int64_t)r->h_state.counters[i]; ckpt[i] = (int64_t)r->h_state.ckpt_counters[i]; }
   return 0;
 }
 

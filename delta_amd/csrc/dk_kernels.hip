@@ -1446,7 +1446,7 @@ __global__ void k_json_select(const DJsonAction* __restrict__ acts, int n, const
 // K7: checkpoint probe — one lane per checkpoint row
 // --------------------------------------------------------------------------------------------
 
-// per-workgroup reduction of three counters (ScanMetrics slots 0, 2, 3) -> one atomic each
+// per-workgroup reduction of three checkpoint counters (ScanMetrics slots 0, 2, 3) -> one atomic each
 __device__ __forceinline__ void block_count3(DState* st, unsigned long long a, unsigned long long b,
                                              unsigned long long c) {
   __shared__ unsigned long long red[3][NT / 64];
@@ -1459,9 +1459,9 @@ __device__ __forceinline__ void block_count3(DState* st, unsigned long long a, u
   if (threadIdx.x == 0) {
     unsigned long long x = 0, y = 0, z = 0;
     for (int i = 0; i < NT / 64; i++) { x += red[0][i]; y += red[1][i]; z += red[2][i]; }
-    if (x) atomicAdd(&st->counters[0], x);
-    if (y) atomicAdd(&st->counters[2], y);
-    if (z) atomicAdd(&st->counters[3], z);
+    if (x) atomicAdd(&st->ckpt_counters[0], x);
+    if (y) atomicAdd(&st->ckpt_counters[2], y);
+    if (z) atomicAdd(&st->ckpt_counters[3], z);
   }
 }
 

@@ -354,13 +354,19 @@ class ScanBuilder:
     def __init__(self, snapshot):
         self.snapshot = snapshot
         self.read_stats = False
+        self.shard = None
 
     def withStats(self, flag=True):
         self.read_stats = flag
         return self
 
+    def withShard(self, world, rank):
+        """Reconcile only this rank's checkpoint files (delta_amd/shard.py)."""
+        self.shard = (int(world), int(rank))
+        return self
+
     def build(self):
-        return GpuScan(self.snapshot, self.read_stats)
+        return GpuScan(self.snapshot, self.read_stats, self.shard)
 
 
 @dataclass
@@ -372,6 +378,7 @@ class FilteredColumnarBatch:
     size: int
     selection: np.ndarray | None
     source: str = ""
+    file_index: int = -1          # replay-order checkpoint file index; -1 = commit tail
 
     def selected_rows(self):
         if self.selection is None:
@@ -383,10 +390,13 @@ class GpuScan:
     """Scan whose getScanFiles runs decode + reconciliation in libdkgpu (SURVEY.md §8(b) plugin
     point 2)."""
 
-    def __init__(self, snapshot, read_stats=False):
+    def __init__(self, snapshot, read_stats=False, shard=None):
         self.snapshot = snapshot
         self.read_stats = read_stats
+        self.shard = shard
         self.metrics = ScanMetrics()
+        self.tail_metrics = ScanMetrics()
+        self.ckpt_metrics = ScanMetrics()
         self.replay = None
 
     def table_root(self):
@@ -399,7 +409,13 @@ class GpuScan:
         seg = self.snapshot.log_segment
         commits = list(reversed(seg.deltas))
         self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
-        self.ckpt_files = self.snapshot._checkpoint_files(engine)
+        all_files = self.snapshot._checkpoint_files(engine)
+        if self.shard:
+            from .shard import owned_files
+            self.ckpt_index = owned_files(len(all_files), *self.shard)
+        else:
+            self.ckpt_index = list(range(len(all_files)))
+        self.ckpt_files = [all_files[i] for i in self.ckpt_index]
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves) if self.ckpt_files else None
         self._rh = C.c_void_p()
@@ -416,6 +432,10 @@ class GpuScan:
         cnt = (C.c_int64 * 5)()
         check(lib().dk_replay_counters(self._rh, cnt))
         self.metrics = ScanMetrics(*[int(x) for x in cnt])
+        tail, ck = (C.c_int64 * 5)(), (C.c_int64 * 5)()
+        check(lib().dk_replay_counters_split(self._rh, tail, ck))
+        self.tail_metrics = ScanMetrics(*[int(x) for x in tail])
+        self.ckpt_metrics = ScanMetrics(*[int(x) for x in ck])
 
     def kernel_stats(self):
         out = {}
@@ -450,7 +470,7 @@ class GpuScan:
             check(lib().dk_replay_ckpt_selection(self._rh, fi, sel.ctypes.data, n))
             cols = {leaf: self.ckpt.column(fi, leaf) for leaf in leaves}
             cols = {k: (c if c.present else None) for k, c in cols.items()}
-            yield FilteredColumnarBatch(cols, root, int(n), sel.astype(bool), path)
+            yield FilteredColumnarBatch(cols, root, int(n), sel.astype(bool), path, self.ckpt_index[fi])
 
     def close(self):
         if getattr(self, "_rh", None):

@@ -101,6 +101,9 @@ int  dk_replay_sync(dk_replay* r);
 /* counters: addFilesSeen, addFilesSeenFromDeltaFiles, activeAddFiles, duplicateAddFiles,
  * removeFilesSeenFromDeltaFiles */
 int  dk_replay_counters(dk_replay* r, int64_t out[5]);
+/* the same counters split into the commit-tail part and the checkpoint part (the part a shard of
+ * the checkpoint contributes; ranks sum checkpoint parts and take the tail part once) */
+int  dk_replay_counters_split(dk_replay* r, int64_t tail[5], int64_t ckpt[5]);
 int  dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n);
 int  dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out, int64_t n);
 /* per-kernel average device time (us) over recorded runs (DK_FLAG_TIMING); names via index */

@@ -405,6 +405,7 @@ class CheckpointBatch:
     cols: dict
     n_rows: int
     selected: np.ndarray = None
+    file_index: int = 0          # position among the checkpoint files in replay order
 
 
 @dataclass
@@ -414,6 +415,8 @@ class ReplayResult:
     checkpoint: list = field(default_factory=list)     # CheckpointBatch in order
     counters: Counters = field(default_factory=Counters)
     table_root: str = ""
+    tail_counters: Counters = field(default_factory=Counters)   # commit-tail part of `counters`
+    ckpt_counters: Counters = field(default_factory=Counters)   # checkpoint part (this shard's)
 
     def scan_files(self):
         """Ordered scan-file rows as canonical python tuples (App. B ordering)."""
@@ -537,11 +540,18 @@ def probe_checkpoint(cols, n_rows, keyset, counters: Counters):
     return sel
 
 
-def replay(table_root: str, json_batch_size=1024, with_stats=False) -> ReplayResult:
-    """getLatestSnapshot + getScanFiles restated; returns the ordered active scan files + counters."""
+def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None) -> ReplayResult:
+    """getLatestSnapshot + getScanFiles restated; returns the ordered active scan files + counters.
+
+    shard=(world, rank): reconcile only the checkpoint files whose replay-order index i has
+    i % world == rank (every rank still reads the commit tail and any V2 manifest to discover
+    sidecars); res.tail_counters / res.ckpt_counters hold the two parts of the counters."""
+    world, rank = shard if shard else (1, 0)
     seg = load_log_segment(table_root)
     res = ReplayResult(version=seg.version, table_root=table_root)
-    c = res.counters
+    c = res.tail_counters
+    cc = res.ckpt_counters
+    ckpt_idx = 0
     tomb = set()
     added = set()
     files = seg.all_files_reversed()
@@ -585,6 +595,9 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False) -> ReplayRes
             while queue and queue[0].kind == f.kind and queue[0].version == f.version:
                 group.append(queue.pop(0))
         for g in group:
+            idx = ckpt_idx
+            ckpt_idx += 1
+            mine = idx % world == rank
             if g.kind == "v2" and g.path.endswith(".json"):
                 # V2 JSON manifest: rows are checkpoint rows (isFromCheckpoint=true)
                 for batch in read_json_batches(g.path, json_batch_size, with_stats, sidecars=True):
@@ -594,15 +607,17 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False) -> ReplayRes
                             queue.append(LogFile(os.path.join(seg.log_path, "_sidecars", sc["path"]),
                                                  "sidecar", g.version))
                         a = row["add"]
-                        if a is None:
+                        if a is None or not mine:
                             continue
-                        c.addFilesSeen += 1
+                        cc.addFilesSeen += 1
                         k = json_key(a)
                         if k in added:
-                            c.duplicateAddFiles += 1
+                            cc.duplicateAddFiles += 1
                         elif k not in tomb:
                             res.json_rows.append(a)   # manifest rows precede sidecars
-                            c.activeAddFiles += 1
+                            cc.activeAddFiles += 1
+                continue
+            if not mine and g.kind != "v2":
                 continue
             extra = SIDECAR_LEAVES if g.kind == "v2" else ()
             pf, cols = decode_checkpoint_file(g.path, with_stats, extra)
@@ -613,9 +628,12 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False) -> ReplayRes
                         if sp.row_def[r] >= 2:
                             queue.append(LogFile(os.path.join(seg.log_path, "_sidecars",
                                                               sp.string(r).decode()), "sidecar", g.version))
-            b = CheckpointBatch(g.path, cols, pf.num_rows)
-            b.selected = probe_checkpoint(cols, pf.num_rows, keyset, c)
+            if not mine:
+                continue
+            b = CheckpointBatch(g.path, cols, pf.num_rows, file_index=idx)
+            b.selected = probe_checkpoint(cols, pf.num_rows, keyset, cc)
             res.checkpoint.append(b)
     if keyset is not None:
         L.dkr_keyset_free(keyset)
+    res.counters = Counters(*[a + b for a, b in zip(c.as_tuple(), cc.as_tuple())])
     return res
