@@ -124,7 +124,37 @@ struct Slot {
   int32_t min_rm_step;           // min step over JSON removes, INT32_MAX = none
 };
 
-enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8 };
+enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8, E_STATS = 16 };
+
+// Data-skipping program (layout of dk_skip_program in include/dkgpu.h): the stats fields to
+// extract from each row's add.stats JSON and a postfix program over them (delta_amd/skipping.py).
+constexpr int SK_MAX_PATHS = 8, SK_MAX_DEPTH = 4, SK_MAX_OPS = 64, SK_NAMES = 512;
+enum : int32_t { SK_LONG = 0, SK_INT = 1, SK_SHORT = 2, SK_BYTE = 3 };
+enum : int32_t { OP_STAT = 0, OP_LIT = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_EQ = 6, OP_AND = 7, OP_OR = 8 };
+struct DSkipProg {
+  int32_t n_paths;
+  int32_t path_type[SK_MAX_PATHS];
+  int32_t path_depth[SK_MAX_PATHS];
+  int32_t name_off[SK_MAX_PATHS][SK_MAX_DEPTH];
+  int32_t name_len[SK_MAX_PATHS][SK_MAX_DEPTH];
+  char names[SK_NAMES];
+  int32_t n_ops;
+  int32_t op[SK_MAX_OPS];
+  int32_t arg[SK_MAX_OPS];
+  int64_t lit[SK_MAX_OPS];
+};
+
+// Rows whose stats the skipping kernel reads: a decoded string column (row_def / offs / chars)
+// or, for the commit tail, explicit (offset, length) pairs per action (length < 0 = null).
+struct StatsRows {
+  int64_t n;
+  const uint8_t* row_def; int32_t max_def; int32_t pad;
+  const int64_t* offs;          // column mode: n + 1 offsets
+  const int64_t* soff;          // action mode: offset per row
+  const int32_t* slen;          // action mode: length per row (< 0: null)
+  const uint8_t* chars;
+  int64_t row_tag;
+};
 
 // Device-side counters and error state of one replay.
 struct DState {

@@ -34,6 +34,7 @@ void launch_slots_init(Slot*, uint64_t, hipStream_t);
 void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
+void launch_stats_eval(const StatsRows&, const DSkipProg&, uint8_t*, DState*, hipStream_t);
 void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
@@ -301,7 +302,7 @@ struct KTimer {
   const char* names[K] = {"k_page_headers", "unused", "k_tile_count", "k_tile_scan",
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
-                          "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", nullptr, nullptr,
+                          "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", nullptr,
                           nullptr};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
@@ -1284,6 +1285,11 @@ struct dk_replay {
   std::vector<int64_t> act_row;        // tail row of each action
   DBuf d_acts, d_jchars, d_canon, d_slots, d_state, d_jsel;
   DBuf d_cand, d_cand_n;      // probe candidates (rows needing the full key path)
+  // data skipping (dk_replay_set_skipping): program + the tail's stats strings per action
+  bool has_skip = false;
+  DSkipProg skip{};
+  DBuf d_tstats_chars, d_tstats_off, d_tstats_len;
+  std::vector<StatsRows> ck_stats;      // per checkpoint file (n = 0: no stats column)
   std::vector<std::unique_ptr<DBuf>> d_csel;   // per checkpoint file
   std::vector<ProbeCols> probe;
   uint64_t mask = 0;
@@ -1378,8 +1384,66 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
       r->probe.push_back(pc);
     }
   }
+  // stats strings for data skipping: the tail's per action (adds only), the checkpoint's column
+  if (tail && tail->with_stats) {
+    const CB& sc = tail->col[JL_STATS];
+    std::vector<int64_t> soff(na + 1, 0);
+    std::vector<int32_t> slen(na + 1, -1);
+    for (size_t i = 0; i < na; i++) {
+      const int64_t row = r->act_row[i];
+      if (r->acts[i].kind != JA_ADD || sc.row_def[row] < 2) continue;
+      soff[i] = sc.offs[row];
+      slen[i] = (int32_t)(sc.offs[row + 1] - sc.offs[row]);
+    }
+    if (upload(r->d_tstats_chars, sc.chars.data(), sc.chars.size(), s)) return 1;
+    if (upload(r->d_tstats_off, soff.data(), soff.size() * 8, s)) return 1;
+    if (upload(r->d_tstats_len, slen.data(), slen.size() * 4, s)) return 1;
+  }
+  if (ckpt) {
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      StatsRows R{};
+      const DColumn* sc = find_col(ckpt, (int)fi, "add.stats");
+      if (sc && !sc->null_only && sc->offs) {
+        R.n = ckpt->files[fi].num_rows;
+        R.row_def = sc->row_def; R.max_def = sc->max_def;
+        R.offs = sc->offs; R.chars = sc->chars;
+      }
+      r->ck_stats.push_back(R);
+    }
+  }
   HIPOK(hipStreamSynchronize(s));
   *out = r.release();
+  return 0;
+}
+
+extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog) {
+  static_assert(sizeof(dk_skip_program) == sizeof(DSkipProg), "dk_skip_program layout");
+  if (!r) return fail("null replay");
+  if (!prog) { r->has_skip = false; return 0; }
+  DSkipProg P;
+  memcpy(&P, prog, sizeof P);
+  if (P.n_paths < 0 || P.n_paths > SK_MAX_PATHS || P.n_ops <= 0 || P.n_ops > SK_MAX_OPS)
+    return fail("dk_replay_set_skipping: bad program size");
+  for (int p = 0; p < P.n_paths; p++) {
+    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_BYTE)
+      return fail("dk_replay_set_skipping: bad stats path");
+    for (int d = 0; d < P.path_depth[p]; d++)
+      if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
+        return fail("dk_replay_set_skipping: bad stats path name");
+  }
+  int depth = 0;
+  for (int k = 0; k < P.n_ops; k++) {
+    const int op = P.op[k];
+    if (op == OP_STAT) { if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail("dk_replay_set_skipping: bad stat"); depth++; }
+    else if (op == OP_LIT) depth++;
+    else if (op >= OP_LT && op <= OP_OR) { if (depth < 2) return fail("dk_replay_set_skipping: stack underflow"); depth--; }
+    else return fail("dk_replay_set_skipping: bad opcode");
+    if (depth > 16) return fail("dk_replay_set_skipping: program too deep");
+  }
+  if (depth != 1) return fail("dk_replay_set_skipping: program must leave one value");
+  if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
+  r->skip = P;
+  r->has_skip = true;
   return 0;
 }
 
@@ -1400,6 +1464,13 @@ static int replay_launch(dk_replay* r) {
   { KTimer::Scope sc(&T, 8, s); launch_table_insert(A, na, S, r->mask, s); }
   { KTimer::Scope sc(&T, 9, s); launch_table_update(A, na, S, r->mask, r->d_canon.as<uint8_t>(), st, s); }
   { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->d_jsel.as<uint8_t>(), st, s); }
+  if (r->has_skip && na) {                 // data skipping on the tail's selected adds
+    KTimer::Scope sc(&T, 17, s);
+    StatsRows R{};
+    R.n = na; R.soff = r->d_tstats_off.as<int64_t>(); R.slen = r->d_tstats_len.as<int32_t>();
+    R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
+    launch_stats_eval(R, r->skip, r->d_jsel.as<uint8_t>(), st, s);
+  }
   if (r->ck) {
     dk_parquet* p = r->ck;
     // decode errors are collected into the replay state too
@@ -1413,6 +1484,11 @@ static int replay_launch(dk_replay* r) {
       dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
       launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, kd.hs.final_(kd.n),
                    r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
+    }
+    if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
+      for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
+        KTimer::Scope sc(&T, 17, s);
+        launch_stats_eval(r->ck_stats[fi], r->skip, r->d_csel[fi]->as<uint8_t>(), st, s);
     }
   }
   return 0;
@@ -1436,6 +1512,12 @@ extern "C" int dk_replay_sync(dk_replay* r) {
       r->seed++;
       if (replay_launch(r)) return 1;
       continue;
+    }
+    if (r->h_state.err_flags & E_STATS) {
+      const long long row = r->h_state.err_row;
+      return fail(std::string("Evaluating the data skipping filter: couldn't decode add.stats of ") +
+                  (row < 0 ? "commit-tail action " + std::to_string(row + 1000000000000ll)
+                           : "checkpoint row " + std::to_string(row)));
     }
     if (r->h_state.err_flags & (E_URI | E_UTF8)) {
       std::vector<DJsonAction> acts(r->acts.size());

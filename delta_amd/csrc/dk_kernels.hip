@@ -1311,14 +1311,352 @@ __device__ int simple_key_equal(const uint8_t* p, int32_t pl, const uint8_t* key
   return eq ? 1 : 0;
 }
 
-// --------------------------------------------------------------------------------------------
-// Commit tail: canonical keys, probe-table build, JSON selection
-// --------------------------------------------------------------------------------------------
 __device__ __forceinline__ void set_err(DState* st, int flag, long long row, int part) {
   atomicOr(&st->err_flags, flag);
   atomicMin((unsigned long long*)&st->err_row, (unsigned long long)row);
   (void)part;
 }
+
+// --------------------------------------------------------------------------------------------
+// K11: data skipping over add.stats JSON (ScanImpl.applyDataSkipping, ScanImpl.java:304-352).
+// One lane per selected scan-file row: a JSON scanner extracts the program's stats fields with
+// the semantics of DefaultJsonHandler.parseJson / DefaultJsonRow (kernel-defaults/.../internal/data/
+// DefaultJsonRow.java:136-357): a missing field or JSON null is null; a long must be an integral
+// JSON number that fits (isIntegralNumber && canConvertToLong, :176-180; integer/short/byte the
+// same within their ranges); any other token for a numeric field, or a non-object where a struct is
+// expected, is a decode error; the last of duplicate keys wins (Jackson ObjectNode); trailing
+// content after the top-level object is ignored (readTree). The postfix program is then evaluated
+// with Kleene logic (DefaultExpressionEvaluator.visitAnd/visitOr, :384-436; comparators are null if
+// either side is null) and the row stays selected iff COALESCE(result, true).
+// --------------------------------------------------------------------------------------------
+constexpr int JS_MAXD = 16;
+
+__device__ __forceinline__ bool js_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+__device__ __forceinline__ bool js_hex(uint8_t c) {
+  return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F');
+}
+__device__ __forceinline__ uint32_t js_hexv(uint8_t c) {
+  return c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10;
+}
+
+// skip a string token starting at s[i] == '"'; returns the index after the closing quote or -1
+__device__ int32_t js_skip_string(const uint8_t* s, int32_t n, int32_t i, bool* has_esc) {
+  i++;
+  *has_esc = false;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c == '"') return i + 1;
+    if (c < 0x20) return -1;
+    if (c == '\\') {
+      *has_esc = true;
+      if (i + 1 >= n) return -1;
+      const uint8_t e = s[i + 1];
+      if (e == 'u') {
+        if (i + 5 >= n || !js_hex(s[i + 2]) || !js_hex(s[i + 3]) || !js_hex(s[i + 4]) || !js_hex(s[i + 5])) return -1;
+        i += 6;
+        continue;
+      }
+      if (!(e == '"' || e == '\\' || e == '/' || e == 'b' || e == 'f' || e == 'n' || e == 'r' || e == 't')) return -1;
+      i += 2;
+      continue;
+    }
+    i++;
+  }
+  return -1;
+}
+
+// does the key s[a, b) (string body, escapes allowed) equal the UTF-8 name nm[0, nl)?
+__device__ bool js_key_eq(const uint8_t* s, int32_t a, int32_t b, bool esc, const char* nm, int32_t nl) {
+  if (!esc) {
+    if (b - a != nl) return false;
+    for (int32_t k = 0; k < nl; k++) if (s[a + k] != (uint8_t)nm[k]) return false;
+    return true;
+  }
+  int32_t j = 0;
+  for (int32_t i = a; i < b;) {
+    uint32_t cp;
+    if (s[i] != '\\') {
+      if (j >= nl || s[i] != (uint8_t)nm[j]) return false;
+      i++; j++;
+      continue;
+    }
+    const uint8_t e = s[i + 1];
+    if (e != 'u') {
+      const uint8_t m = e == 'b' ? 8 : e == 'f' ? 12 : e == 'n' ? 10 : e == 'r' ? 13 : e == 't' ? 9 : e;
+      if (j >= nl || (uint8_t)nm[j] != m) return false;
+      i += 2; j++;
+      continue;
+    }
+    cp = (js_hexv(s[i + 2]) << 12) | (js_hexv(s[i + 3]) << 8) | (js_hexv(s[i + 4]) << 4) | js_hexv(s[i + 5]);
+    i += 6;
+    if (cp >= 0xD800 && cp < 0xDC00 && i + 5 < b && s[i] == '\\' && s[i + 1] == 'u') {
+      const uint32_t lo = (js_hexv(s[i + 2]) << 12) | (js_hexv(s[i + 3]) << 8) | (js_hexv(s[i + 4]) << 4) | js_hexv(s[i + 5]);
+      if (lo >= 0xDC00 && lo < 0xE000) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); i += 6; }
+    }
+    if (cp >= 0xD800 && cp < 0xE000) cp = 0xFFFD;    // lone surrogate -> replacement on UTF-8 encode
+    uint8_t u[4];
+    int ul;
+    if (cp < 0x80) { u[0] = (uint8_t)cp; ul = 1; }
+    else if (cp < 0x800) { u[0] = 0xC0 | (cp >> 6); u[1] = 0x80 | (cp & 63); ul = 2; }
+    else if (cp < 0x10000) { u[0] = 0xE0 | (cp >> 12); u[1] = 0x80 | ((cp >> 6) & 63); u[2] = 0x80 | (cp & 63); ul = 3; }
+    else { u[0] = 0xF0 | (cp >> 18); u[1] = 0x80 | ((cp >> 12) & 63); u[2] = 0x80 | ((cp >> 6) & 63); u[3] = 0x80 | (cp & 63); ul = 4; }
+    for (int k = 0; k < ul; k++) { if (j >= nl || (uint8_t)nm[j] != u[k]) return false; j++; }
+  }
+  return j == nl;
+}
+
+// number token at s[i]: returns the index after it or -1 (JSON grammar, no leading zeros); *integral
+// = no fraction / exponent; *v = value when integral and within int64 (*fits)
+__device__ int32_t js_number(const uint8_t* s, int32_t n, int32_t i, bool* integral, bool* fits, long long* v) {
+  bool neg = false;
+  if (s[i] == '-') { neg = true; i++; }
+  if (i >= n || s[i] < '0' || s[i] > '9') return -1;
+  unsigned long long mag = 0;
+  bool ok = true;
+  if (s[i] == '0') {
+    i++;
+    if (i < n && s[i] >= '0' && s[i] <= '9') return -1;
+  } else {
+    while (i < n && s[i] >= '0' && s[i] <= '9') {
+      const unsigned d = s[i] - '0';
+      if (mag > (0xFFFFFFFFFFFFFFFFull - d) / 10) ok = false;
+      else mag = mag * 10 + d;
+      i++;
+    }
+  }
+  *integral = true;
+  if (i < n && s[i] == '.') {
+    *integral = false;
+    i++;
+    if (i >= n || s[i] < '0' || s[i] > '9') return -1;
+    while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+  }
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    *integral = false;
+    i++;
+    if (i < n && (s[i] == '+' || s[i] == '-')) i++;
+    if (i >= n || s[i] < '0' || s[i] > '9') return -1;
+    while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+  }
+  *fits = ok && (neg ? mag <= 0x8000000000000000ull : mag <= 0x7FFFFFFFFFFFFFFFull);
+  *v = neg ? (long long)(0ull - mag) : (long long)mag;
+  return i;
+}
+
+// byte/short fields accept any JSON number whose exact decimal value is an integer in range: the
+// reference parses non-integer tokens as BigDecimal (USE_BIG_DECIMAL_FOR_FLOATS, DefaultJsonHandler
+// .java:48) and checks canConvertToExactIntegral (DefaultJsonRow.java:146-167), so "5.0" and "5E0"
+// are 5 while "5.5" is an error. Token [i, e) is already validated by js_number.
+__device__ bool js_small_exact(const uint8_t* s, int32_t i, int32_t e, long long* v) {
+  bool neg = false;
+  if (s[i] == '-') { neg = true; i++; }
+  int32_t m_end = i, int_digits = 0;
+  bool dot = false;
+  while (m_end < e && s[m_end] != 'e' && s[m_end] != 'E') {
+    if (s[m_end] == '.') dot = true;
+    else if (!dot) int_digits++;
+    m_end++;
+  }
+  long long ex = 0;
+  if (m_end < e) {                                    // exponent (clamped: only its sign region matters)
+    int32_t k = m_end + 1;
+    bool eneg = false;
+    if (s[k] == '+' || s[k] == '-') { eneg = s[k] == '-'; k++; }
+    for (; k < e; k++) ex = ex < 100000000ll ? ex * 10 + (s[k] - '0') : ex;
+    if (eneg) ex = -ex;
+  }
+  // digit j (0-based over the mantissa digits) has decimal place int_digits - 1 - j + ex
+  long long acc = 0;
+  int32_t j = 0;
+  for (int32_t k = i; k < m_end; k++) {
+    if (s[k] == '.') continue;
+    const int d = s[k] - '0';
+    const long long place = (long long)int_digits - 1 - j + ex;
+    j++;
+    if (d == 0) continue;
+    if (place < 0) return false;                      // a nonzero fractional digit: not integral
+    if (place > 5) return false;                      // |value| >= 10^6: outside short range
+    long long pw = 1;
+    for (long long q = 0; q < place; q++) pw *= 10;
+    acc += d * pw;
+  }
+  *v = neg ? -acc : acc;
+  return true;
+}
+
+// extract the program's stats fields from one JSON object; returns false on a decode error
+__device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long long* val, uint32_t* set) {
+  uint32_t mstack[JS_MAXD];
+  uint8_t is_obj[JS_MAXD];
+  uint32_t leafmask[SK_MAX_DEPTH + 2];
+  for (int d = 0; d < SK_MAX_DEPTH + 2; d++) leafmask[d] = 0;
+  uint32_t all = 0;
+  for (int p = 0; p < P.n_paths; p++) { leafmask[P.path_depth[p]] |= 1u << p; all |= 1u << p; }
+  *set = 0;
+  int32_t i = 0;
+  while (i < n && js_ws(s[i])) i++;
+  if (i >= n || s[i] != '{') return false;          // the stats row must be an object (struct)
+  i++;
+  int depth = 1;
+  is_obj[1] = 1;
+  mstack[1] = all;
+  // states: 0 = key or '}' (after '{'), 1 = key (after ','), 2 = value, 3 = after value, 4 = value or ']'
+  int state = 0;
+  uint32_t m = 0;                                     // paths matching the current member's key chain
+  while (true) {
+    while (i < n && js_ws(s[i])) i++;
+    if (i >= n) return false;
+    const uint8_t c = s[i];
+    if (state == 0 || state == 1) {
+      if (c == '}' && state == 0) { state = 3; goto close; }
+      if (c != '"') return false;
+      bool esc;
+      const int32_t e = js_skip_string(s, n, i, &esc);
+      if (e < 0) return false;
+      m = 0;
+      const uint32_t cand = depth <= SK_MAX_DEPTH ? mstack[depth] : 0;
+      for (int p = 0; p < P.n_paths; p++)
+        if ((cand >> p) & 1) {
+          if (js_key_eq(s, i + 1, e - 1, esc, P.names + P.name_off[p][depth - 1], P.name_len[p][depth - 1]))
+            m |= 1u << p;
+        }
+      i = e;
+      while (i < n && js_ws(s[i])) i++;
+      if (i >= n || s[i] != ':') return false;
+      i++;
+      state = 2;
+      continue;
+    }
+    if (state == 2 || state == 4) {
+      if (state == 4 && c == ']') { state = 3; goto close; }
+      const uint32_t leaf = depth <= SK_MAX_DEPTH ? (m & leafmask[depth]) : 0;
+      const uint32_t pre = m & ~leaf;
+      if (c == '{' || c == '[') {
+        if (leaf) return false;                       // number expected
+        if (c == '[' && pre) return false;            // struct expected
+        if (pre) *set &= ~pre;                        // a (repeated) parent object: its fields restart
+        if (depth + 1 >= JS_MAXD) return false;       // deeper than supported
+        depth++;
+        is_obj[depth] = c == '{';
+        mstack[depth] = c == '{' ? pre : 0;
+        i++;
+        state = c == '{' ? 0 : 4;
+        m = 0;
+        continue;
+      }
+      if (c == '"') {
+        if (leaf || pre) return false;                // a string where a number / struct is expected
+        bool esc;
+        const int32_t e = js_skip_string(s, n, i, &esc);
+        if (e < 0) return false;
+        i = e;
+      } else if (c == '-' || (c >= '0' && c <= '9')) {
+        if (pre) return false;
+        bool integral, fits;
+        long long v;
+        const int32_t e = js_number(s, n, i, &integral, &fits, &v);
+        if (e < 0) return false;
+        if (leaf) {
+          for (int p = 0; p < P.n_paths; p++)
+            if ((leaf >> p) & 1) {
+              const int t = P.path_type[p];
+              if (t == SK_SHORT || t == SK_BYTE) {
+                if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
+              } else if (!integral || !fits) {
+                return false;                         // long/integer need an integral token
+              }
+              const bool in = t == SK_LONG ? true
+                            : t == SK_INT ? (v >= -2147483648ll && v <= 2147483647ll)
+                            : t == SK_SHORT ? (v >= -32768 && v <= 32767) : (v >= -128 && v <= 127);
+              if (!in) return false;
+              val[p] = v;
+              *set |= 1u << p;
+            }
+        }
+        i = e;
+      } else if (c == 't' || c == 'f' || c == 'n') {
+        const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
+        const int ll = c == 'f' ? 5 : 4;
+        if (i + ll > n) return false;
+        for (int k = 0; k < ll; k++) if (s[i + k] != (uint8_t)lit[k]) return false;
+        if (c != 'n' && (leaf || pre)) return false;  // boolean where a number / struct is expected
+        if (c == 'n') *set &= ~(leaf | pre);          // JSON null: the field (and its children) null
+        i += ll;
+      } else {
+        return false;
+      }
+      state = 3;
+      continue;
+    }
+    // state 3: after a value
+    if (c == ',') { state = is_obj[depth] ? 1 : 4; i++; continue; }
+    if ((c == '}' && is_obj[depth]) || (c == ']' && !is_obj[depth])) goto close;
+    return false;
+  close:
+    i++;
+    depth--;
+    if (depth == 0) return true;                      // trailing content is ignored (readTree)
+    state = 3;
+  }
+}
+
+// Kleene evaluation of the postfix program; returns 1 true, 0 false, -1 null
+__device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set) {
+  long long sv[16];
+  int8_t sn[16];      // -1 null, else 0/1 for booleans (values: 0 = non-null)
+  int sp = 0;
+  for (int k = 0; k < P.n_ops && k < SK_MAX_OPS; k++) {
+    const int op = P.op[k];
+    if (op == OP_STAT) {
+      const int p = P.arg[k];
+      sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1; sp++;
+    } else if (op == OP_LIT) {
+      sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sp++;
+    } else if (op >= OP_LT && op <= OP_EQ) {
+      const long long b = sv[--sp]; const int8_t bn = sn[sp];
+      const long long a = sv[--sp]; const int8_t an = sn[sp];
+      int8_t r;
+      if (an < 0 || bn < 0) r = -1;
+      else r = op == OP_LT ? a < b : op == OP_LE ? a <= b : op == OP_GT ? a > b : op == OP_GE ? a >= b : a == b;
+      sn[sp] = r; sv[sp] = 0; sp++;
+    } else {
+      const int8_t b = sn[--sp];
+      const int8_t a = sn[--sp];
+      int8_t r;
+      if (op == OP_AND) r = (a == 0 || b == 0) ? 0 : (a == 1 && b == 1) ? 1 : -1;
+      else r = (a == 1 || b == 1) ? 1 : (a == 0 && b == 0) ? 0 : -1;
+      sn[sp] = r; sv[sp] = 0; sp++;
+    }
+  }
+  return sp == 1 ? sn[0] : -1;
+}
+
+__global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg P, uint8_t* __restrict__ sel,
+                                                   DState* __restrict__ st) {
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
+       r += (long long)gridDim.x * blockDim.x) {
+    if (!sel[r]) continue;
+    const uint8_t* s;
+    int32_t len;
+    if (R.offs) {
+      if (R.row_def[r] < R.max_def) continue;                     // null stats -> kept
+      s = R.chars + R.offs[r];
+      len = (int32_t)(R.offs[r + 1] - R.offs[r]);
+    } else {
+      if (R.slen[r] < 0) continue;
+      s = R.chars + R.soff[r];
+      len = R.slen[r];
+    }
+    long long val[SK_MAX_PATHS];
+    uint32_t set = 0;
+    if (!js_extract(s, len, P, val, &set)) { set_err(st, E_STATS, R.row_tag + r, 0); continue; }
+    if (sk_eval(P, val, set) == 0) sel[r] = 0;                    // COALESCE(skip, true)
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Commit tail: canonical keys, probe-table build, JSON selection
+// --------------------------------------------------------------------------------------------
 
 template <class Sink>
 __device__ __forceinline__ void feed(Sink& k, const uint8_t* p, int32_t n) { for (int32_t i = 0; i < n; i++) k.put(p[i]); }
@@ -1670,4 +2008,13 @@ void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const D
   hipLaunchKernelGGL(k_probe_cand, dim3(grid), dim3(NT), 0, s, pc, slots, mask, acts, canon, seed, sel, cand, cand_n, st);
 }
 
+}  // namespace dk
+
+namespace dk {
+void launch_stats_eval(const StatsRows& R, const DSkipProg& P, uint8_t* sel, DState* st, hipStream_t s) {
+  if (R.n <= 0) return;
+  const long long want = (R.n + NT - 1) / NT;
+  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
+  hipLaunchKernelGGL(k_stats_eval, dim3(grid), dim3(NT), 0, s, R, P, sel, st);
+}
 }  // namespace dk

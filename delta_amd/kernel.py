@@ -22,7 +22,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import Column, DkError, check, dk_column, dk_config, lib
+from ._lib import Column, DkError, check, dk_column, dk_config, dk_skip_program, lib
 
 ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
               "add.size", "add.modificationTime", "add.dataChange",
@@ -342,7 +342,8 @@ class Snapshot:
                         ss = cols["metaData.schemaString"]
                         self.metadata = {"id": mid.string(r).decode() if mid.row_def[r] >= 2 else None,
                                          "schemaString": (ss.string(r).decode()
-                                                          if ss is not None and ss.row_def[r] >= 2 else None)}
+                                                          if ss is not None and ss.row_def[r] >= 2 else None),
+                                         "partitionColumns": _list_at(cols["metaData.partitionColumns.list.element"], r)}
             ps.close()
         if self.protocol is None:
             raise DkError("No protocol found at version %d" % self.getVersion())
@@ -350,11 +351,28 @@ class Snapshot:
             raise DkError("No metadata found at version %d" % self.getVersion())
 
 
+def _list_at(col, r):
+    """list<string> value of row r of a decoded list leaf (None when the list is null)."""
+    if col is None or not col.present or col.row_def[r] < col.rep_def - 1:
+        return None
+    a, b = int(col.row_offs[r]), int(col.row_offs[r + 1])
+    return [col.string(i).decode() if col.entry_def[i] >= col.max_def else None for i in range(a, b)]
+
+
 class ScanBuilder:
     def __init__(self, snapshot):
         self.snapshot = snapshot
         self.read_stats = False
         self.shard = None
+        self.predicate = None
+
+    def withFilter(self, predicate):
+        """ScanBuilderImpl.withFilter (internal/ScanBuilderImpl.java:61-67). The data part of the
+        filter becomes a GPU data-skipping program (K11); partition pruning is not in this build."""
+        if self.predicate is not None:
+            raise ValueError("There already exists a filter in current builder")
+        self.predicate = predicate
+        return self
 
     def withStats(self, flag=True):
         self.read_stats = flag
@@ -366,7 +384,7 @@ class ScanBuilder:
         return self
 
     def build(self):
-        return GpuScan(self.snapshot, self.read_stats, self.shard)
+        return GpuScan(self.snapshot, self.read_stats, self.shard, self.predicate)
 
 
 @dataclass
@@ -390,10 +408,27 @@ class GpuScan:
     """Scan whose getScanFiles runs decode + reconciliation in libdkgpu (SURVEY.md §8(b) plugin
     point 2)."""
 
-    def __init__(self, snapshot, read_stats=False, shard=None):
+    def __init__(self, snapshot, read_stats=False, shard=None, predicate=None):
         self.snapshot = snapshot
-        self.read_stats = read_stats
         self.shard = shard
+        self.predicate = predicate
+        self.skipping = None          # (planner node, paths, types) when a data-skipping filter applies
+        self.partition_filter, self.data_filter = None, None
+        if predicate is not None:
+            from . import skipping as sk
+            md = snapshot.metadata or {}
+            parts = md.get("partitionColumns") or []
+            self.partition_filter, self.data_filter = sk.split_filters(predicate, parts)
+            if self.partition_filter is not None:
+                raise DkError("partition pruning (filter %r) is not supported by this engine build"
+                              % (self.partition_filter,))
+            if self.data_filter is not None:
+                leaves = sk.data_schema_leaves(md["schemaString"], parts)
+                node = sk.construct(self.data_filter, leaves)
+                if node is not None:
+                    self.skipping = (node,) + sk.compile_program(node, leaves)
+        # ScanImpl.getScanFiles: shouldReadStats = hasDataSkippingFilter || includeStats (:128-130)
+        self.read_stats = read_stats or self.skipping is not None
         self.metrics = ScanMetrics()
         self.tail_metrics = ScanMetrics()
         self.ckpt_metrics = ScanMetrics()
@@ -421,7 +456,16 @@ class GpuScan:
         self._rh = C.c_void_p()
         check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
                                      C.byref(self._rh)))
+        if self.skipping is not None:
+            from . import skipping as sk
+            prog = sk.pack(self.skipping[1:], dk_skip_program)
+            check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
         return self
+
+    def getRemainingFilter(self):
+        """ScanImpl.getRemainingFilter (:221-223): the data filter, which skipping never fully
+        applies."""
+        return self.data_filter
 
     def run(self):
         """The device step: commit-tail keys + table, checkpoint decode, probe, selection."""

@@ -1,0 +1,308 @@
+"""Data-skipping planning (host side of K11), restating
+kernel-api/.../internal/skipping/DataSkippingUtils.java:74-456 and StatsSchemaHelper.java:71-232,
+and compiling the skipping predicate into a postfix program that the GPU evaluates per scan-file
+row over the row's ``add.stats`` JSON (k_stats_eval; ScanImpl.applyDataSkipping, ScanImpl.java:304-352).
+
+A skipping predicate node is one of
+    ("AND", a, b) / ("OR", a, b)
+    (cmp, left, right)   cmp in "<", "<=", ">", ">=", "="; operands ("stat", path) or ("lit", int)
+where path is a tuple like ("maxValues", "id") or ("numRecords",). IS NOT DISTINCT FROM is rewritten
+as in the reference (rewriteEqualNullSafe, :528-534).
+"""
+from __future__ import annotations
+
+import json
+
+from .expressions import ALWAYS_TRUE, Column, Literal, Predicate
+
+MIN, MAX, NULL_COUNT, NUM_RECORDS = "minValues", "maxValues", "nullCount", "numRecords"
+SKIPPING_ELIGIBLE = {"byte", "short", "integer", "long", "float", "double", "date", "timestamp",
+                     "timestamp_ntz", "string"}          # StatsSchemaHelper.java:209-222 (+ decimal)
+GPU_TYPES = {"byte", "short", "integer", "long"}          # stats value types k_stats_eval decodes
+REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
+           "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}   # DataSkippingUtils.java:346-356
+NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
+
+
+class UnsupportedSkipping(RuntimeError):
+    pass
+
+
+def data_schema_leaves(schema_string: str, partition_columns=()) -> dict:
+    """Logical leaf column -> (type name, physical column) over the table's data schema (partition
+    columns excluded, Metadata.getDataSchema; StatsSchemaHelper.getLogicalToPhysicalColumnAndDataType
+    :297-319; physical names from delta.columnMapping.physicalName, ColumnMapping.getPhysicalName)."""
+    schema = json.loads(schema_string)
+    parts = {p.lower() for p in partition_columns}
+    out = {}
+
+    def walk(fields, prefix, phys):
+        for f in fields:
+            t = f["type"]
+            name = prefix + (f["name"],)
+            pname = phys + ((f.get("metadata") or {}).get("delta.columnMapping.physicalName", f["name"]),)
+            if not prefix and f["name"].lower() in parts:
+                continue
+            if isinstance(t, dict) and t.get("type") == "struct":
+                walk(t["fields"], name, pname)
+            elif isinstance(t, str):
+                out[name] = (t, pname)
+            else:
+                out[name] = (t.get("type", "complex") if isinstance(t, dict) else str(t), pname)
+    walk(schema["fields"], (), ())
+    return out
+
+
+def _refs_non_partition(children, parts) -> bool:
+    """PartitionUtils.hasNonPartitionColumns (util/PartitionUtils.java:398-415)."""
+    for ch in children:
+        if isinstance(ch, Column):
+            if len(ch.names) != 1 or ch.names[0].lower() not in parts:
+                return True
+        elif isinstance(ch, Predicate) and _refs_non_partition(ch.children, parts):
+            return True
+    return False
+
+
+def _and(a, b):
+    """combineWithAndOp (PartitionUtils.java:417-430)."""
+    if a.name.upper() == "ALWAYS_FALSE" or b.name.upper() == "ALWAYS_FALSE":
+        return Predicate("ALWAYS_FALSE")
+    if a.name.upper() == "ALWAYS_TRUE":
+        return b
+    if b.name.upper() == "ALWAYS_TRUE":
+        return a
+    return Predicate("AND", a, b)
+
+
+def split_filters(pred: Predicate, partition_columns=()):
+    """(partition predicate, data predicate), each None when ALWAYS_TRUE
+    (PartitionUtils.splitMetadataAndDataPredicates :242-263; ScanImpl.removeAlwaysTrue :236-245)."""
+    parts = {p.lower() for p in partition_columns}
+
+    def split(p):
+        if p.name.upper() == "AND":
+            l1, l2 = split(p.children[0])
+            r1, r2 = split(p.children[1])
+            return _and(l1, r1), _and(l2, r2)
+        if _refs_non_partition(p.children, parts):
+            return ALWAYS_TRUE, p
+        return p, ALWAYS_TRUE
+    a, b = split(pred)
+    drop = lambda x: None if x.name.upper() == "ALWAYS_TRUE" else x  # noqa: E731
+    return drop(a), drop(b)
+
+
+def _eligible_minmax(leaves, col):
+    t = leaves[col.names][0] if col.names in leaves else None
+    return t is not None and (t in SKIPPING_ELIGIBLE or t.startswith("decimal"))
+
+
+def _eligible_literal(lit):                               # isSkippingEligibleLiteral (StatsSchemaHelper :50-52)
+    return lit.type in SKIPPING_ELIGIBLE or lit.type.startswith("decimal")
+
+
+def construct(pred: Predicate, leaves: dict):
+    """constructDataSkippingFilter (DataSkippingUtils.java:156-283); None = no skipping filter."""
+    n = pred.name.upper()
+    c = pred.children
+    if n == "AND":                                                              # :178-190
+        a, b = construct(c[0], leaves), construct(c[1], leaves)
+        if a and b:
+            return ("AND", a, b)
+        return a or b
+    if n == "OR":                                                               # :204-213
+        a, b = construct(c[0], leaves), construct(c[1], leaves)
+        return ("OR", a, b) if a and b else None
+    if n == "IS_NOT_NULL":                                                      # :216-235
+        if isinstance(c[0], Column) and c[0].names in leaves:
+            return ("<", ("stat", (NULL_COUNT,) + leaves[c[0].names][1]), ("stat", (NUM_RECORDS,)))
+        return None
+    if n == "IS_NULL":                                                          # :240-252
+        if isinstance(c[0], Column) and c[0].names in leaves:
+            return (">", ("stat", (NULL_COUNT,) + leaves[c[0].names][1]), ("lit", 0))
+        return None
+    if n in ("=", "<", "<=", ">", ">=", "IS NOT DISTINCT FROM"):               # :254-274
+        left, right = c
+        if isinstance(left, Column) and isinstance(right, Literal):
+            if _eligible_minmax(leaves, left) and _eligible_literal(right):
+                return _comparator(n, left, right, leaves)
+            return None
+        if isinstance(right, Column) and isinstance(left, Literal):
+            return construct(Predicate(REVERSE[n], right, left), leaves)
+        return None
+    if n == "NOT":                                                              # :276-278
+        return _construct_not(c[0], leaves)
+    return None
+
+
+def _comparator(n, col, lit, leaves):
+    """constructComparatorDataSkippingFilters (:286-331)."""
+    mn = ("stat", (MIN,) + leaves[col.names][1])
+    mx = _max(col, leaves)
+    v = ("lit", lit.value)
+    if n == "=":
+        return ("AND", ("<=", mn, v), (">=", mx, v))
+    if n == "<":
+        return ("<", mn, v)
+    if n == "<=":
+        return ("<=", mn, v)
+    if n == ">":
+        return (">", mx, v)
+    if n == ">=":
+        return (">=", mx, v)
+    # IS NOT DISTINCT FROM (rewriteEqualNullSafe :528-534)
+    if lit.value is None:
+        return construct(Predicate("IS_NULL", col), leaves)
+    return construct(Predicate("AND", Predicate("IS_NOT_NULL", col), Predicate("=", col, lit)), leaves)
+
+
+def _max(col, leaves):
+    t, phys = leaves[col.names]
+    if t in ("timestamp", "timestamp_ntz"):              # getMaxColumn TIMEADD(+1 ms), StatsSchemaHelper :154-159
+        return ("timeadd", ("stat", (MAX,) + phys))
+    return ("stat", (MAX,) + phys)
+
+
+def _construct_not(child: Predicate, leaves):
+    """constructNotDataSkippingFilters (:366-487)."""
+    n = child.name.upper()
+    c = child.children
+    if n == "AND":
+        return construct(Predicate("OR", Predicate("NOT", c[0]), Predicate("NOT", c[1])), leaves)
+    if n == "OR":
+        return construct(Predicate("AND", Predicate("NOT", c[0]), Predicate("NOT", c[1])), leaves)
+    if n == "IS_NOT_NULL":
+        return construct(Predicate("IS_NULL", c[0]), leaves)
+    if n == "IS_NULL":
+        return construct(Predicate("IS_NOT_NULL", c[0]), leaves)
+    if n == "=":
+        # NOT(a = x) -> OR(min < x, max > x)   (constructDataSkippingFiltersForNotEqual :537-560)
+        return construct(Predicate("OR", Predicate("<", c[0], c[1]), Predicate(">", c[0], c[1])), leaves)
+    if n in NOT_CMP:
+        return construct(Predicate(NOT_CMP[n], c[0], c[1]), leaves)
+    if n == "IS NOT DISTINCT FROM":
+        left, right = c
+        if isinstance(left, Column) and isinstance(right, Literal):
+            if right.value is None:
+                return construct(Predicate("IS_NOT_NULL", left), leaves)
+            return construct(Predicate("OR", Predicate("IS_NULL", left),
+                                       Predicate("NOT", Predicate("=", left, right))), leaves)
+        if isinstance(right, Column) and isinstance(left, Literal):
+            return _construct_not(Predicate(n, right, left), leaves)
+        return None
+    if n == "NOT":
+        return construct(c[0], leaves)
+    return None
+
+
+def referenced_stats(node, out=None):
+    out = [] if out is None else out
+    if node[0] in ("AND", "OR"):
+        referenced_stats(node[1], out)
+        referenced_stats(node[2], out)
+    elif node[0] == "stat":
+        if node[1] not in out:
+            out.append(node[1])
+    elif node[0] == "timeadd":
+        referenced_stats(node[1], out)
+    elif node[0] != "lit":
+        referenced_stats(node[1], out)
+        referenced_stats(node[2], out)
+    return out
+
+
+# ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
+OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR = range(9)
+_CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
+TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3}
+
+
+def stat_type(path, leaves):
+    """Type of a stats field: numRecords / nullCount.* are long (getNullCountSchema :255-273),
+    min/max take the column's type."""
+    if path[0] in (NUM_RECORDS, NULL_COUNT):
+        return "long"
+    for t, phys in leaves.values():
+        if phys == path[1:]:
+            return t
+    raise KeyError(path)
+
+
+def compile_program(node, leaves):
+    """(paths, path type codes, ops) for the device evaluator; raises UnsupportedSkipping for stats
+    types the GPU evaluator does not decode (the reference would skip with them: refusing keeps
+    results identical instead of silently keeping more files)."""
+    paths = referenced_stats(node)
+    if len(paths) > MAX_PATHS:
+        raise UnsupportedSkipping("data skipping filter references %d stats fields (max %d)" % (len(paths), MAX_PATHS))
+    for p in paths:
+        t = stat_type(p, leaves)
+        if t not in GPU_TYPES:
+            raise UnsupportedSkipping("data skipping on %s column %s is not supported by this engine build"
+                                      % (t, ".".join(p[1:])))
+    ops = []
+
+    def emit(n):
+        if n[0] in ("AND", "OR"):
+            emit(n[1])
+            emit(n[2])
+            ops.append((OP_AND if n[0] == "AND" else OP_OR, 0, 0))
+        elif n[0] == "stat":
+            ops.append((OP_STAT, paths.index(n[1]), 0))
+        elif n[0] == "lit":
+            v = n[1]
+            if v is None:
+                ops.append((OP_LIT, 1, 0))                   # null literal: comparisons yield null
+            elif isinstance(v, bool) or not isinstance(v, int):
+                raise UnsupportedSkipping("data skipping with a %r literal is not supported" % (v,))
+            elif not -(1 << 63) <= v < (1 << 63):
+                raise UnsupportedSkipping("literal %d does not fit a long" % v)
+            else:
+                ops.append((OP_LIT, 0, int(v)))
+        elif n[0] == "timeadd":
+            raise UnsupportedSkipping("timestamp data skipping is not supported by this engine build")
+        else:
+            emit(n[1])
+            emit(n[2])
+            ops.append((_CMP[n[0]], 0, 0))
+    emit(node)
+    if len(ops) > MAX_OPS or _stack_depth(ops) > MAX_STACK:
+        raise UnsupportedSkipping("data skipping filter is too large for the device evaluator")
+    return paths, [TYPE_CODE[stat_type(p, leaves)] for p in paths], ops
+
+
+MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 512
+
+
+def _stack_depth(ops):
+    d = hi = 0
+    for op, _, _ in ops:
+        d += 1 if op in (OP_STAT, OP_LIT) else -1
+        hi = max(hi, d)
+    return hi
+
+
+def pack(program, struct_type):
+    """Fill a dk_skip_program ctypes struct (include/dkgpu.h) from compile_program's output."""
+    paths, types, ops = program
+    prog = struct_type()
+    names = bytearray()
+    prog.n_paths = len(paths)
+    for i, (p, t) in enumerate(zip(paths, types)):
+        if not 1 <= len(p) <= MAX_DEPTH:
+            raise UnsupportedSkipping("stats field %s is nested deeper than %d" % (".".join(p), MAX_DEPTH))
+        prog.path_type[i] = t
+        prog.path_depth[i] = len(p)
+        for d, comp in enumerate(p):
+            b = comp.encode("utf-8")
+            prog.name_off[i][d] = len(names)
+            prog.name_len[i][d] = len(b)
+            names += b
+    if len(names) > NAMES_BYTES:
+        raise UnsupportedSkipping("stats field names exceed %d bytes" % NAMES_BYTES)
+    prog.names = bytes(names)
+    prog.n_ops = len(ops)
+    for k, (op, arg, lit) in enumerate(ops):
+        prog.op[k], prog.arg[k], prog.lit[k] = op, arg, lit
+    return prog

@@ -264,9 +264,10 @@ def _add_struct(rng, n, start_index, spec: TableSpec, data_change: bool, paths=N
               ("deletionVector", DV_TYPE), ("baseRowId", pa.int64()),
               ("defaultRowCommitVersion", pa.int64())]
     if spec.with_stats or spec.with_stats_parsed:
-        idmin = rng.integers(0, 50_000_000, size=n)
+        # 8-digit values (no leading zeros: stats must be valid JSON for Jackson)
+        idmin = rng.integers(10_000_000, 50_000_000, size=n)
         idmax = idmin + rng.integers(0, 1_000_000, size=n)
-        nrec = rng.integers(1, 100_000, size=n)
+        nrec = rng.integers(10_000_000, 100_000_000, size=n)
         nmat = np.empty((n, 7), dtype=np.uint8)
         nmat[:, 0] = ord("n")
         nmat[:, 1:] = _digits(rng.integers(0, 500_000, size=n), 6)
@@ -475,10 +476,11 @@ def write_table(root: str, spec: TableSpec):
                       "offset": 1, "sizeInBytes": int(rng.integers(30, 4000)),
                       "cardinality": int(rng.integers(1, 1000))}
             stats = None
-            if spec.with_stats:
+            if spec.with_stats and rng.random() >= 0.05:      # ~5% of commit adds carry no stats
                 lo = int(rng.integers(0, 50_000_000))
                 stats = ('{"numRecords":10,"minValues":{"id":%d,"name":"a"},"maxValues":'
-                         '{"id":%d,"name":"z"},"nullCount":{"id":0,"name":0}}' % (lo, lo + 100))
+                         '{"id":%d,"name":"z"},"nullCount":{"id":%d,"name":0}}'
+                         % (lo, lo + 100, int(rng.integers(0, 3))))
             lines.append(json.dumps(_json_add(p, "2024-01-01", rng.integers(1 << 20, 1 << 28),
                                               1_700_000_000_000 + ver, dv=dv, stats=stats,
                                               pv_keys=spec.pv_keys)))

@@ -92,10 +92,31 @@ int64_t dk_json_tail_rows(dk_json_tail* t);
 int  dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out);
 void dk_json_tail_free(dk_json_tail* t);
 
+/* ---- Data skipping (ScanImpl.applyDataSkipping, KA/internal/ScanImpl.java:304-352) ----
+ * A skipping predicate compiled by the host planner (delta_amd/skipping.py, restating
+ * DataSkippingUtils.constructDataSkippingFilter) into the stats fields to read from each selected
+ * row's add.stats JSON and a postfix program over them. A row stays selected iff
+ * COALESCE(program(stats), true); null / absent stats keep the row. */
+typedef struct dk_skip_program {
+  int32_t n_paths;                 /* <= 8 stats fields                                        */
+  int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte                       */
+  int32_t path_depth[8];           /* name components, 1..4 ("maxValues","id" -> 2)             */
+  int32_t name_off[8][4];          /* component names: offsets / lengths into names (UTF-8)     */
+  int32_t name_len[8][4];
+  char names[512];
+  int32_t n_ops;                   /* <= 64                                                     */
+  int32_t op[64];                  /* 0 STAT(arg=path), 1 LIT(arg=1: null), 2 <, 3 <=, 4 >, 5 >=, 6 =, 7 AND, 8 OR */
+  int32_t arg[64];
+  int64_t lit[64];
+} dk_skip_program;
+
 /* ---- Replay: reconcile the tail and the checkpoint files on the GPU ----
  * ckpt may be NULL (no checkpoint). Checkpoint files are given in replay order (multi-part:
  * descending part number, LogSegment.java:171-177). */
 int  dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_replay** out);
+/* install (prog != NULL) or clear the data-skipping program applied after reconciliation; the
+ * tail must have been parsed with stats and the checkpoint projection must include add.stats */
+int  dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog);
 int  dk_replay_run(dk_replay* r);                      /* async: key build, probe, decode */
 int  dk_replay_sync(dk_replay* r);
 /* counters: addFilesSeen, addFilesSeenFromDeltaFiles, activeAddFiles, duplicateAddFiles,

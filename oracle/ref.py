@@ -540,12 +540,17 @@ def probe_checkpoint(cols, n_rows, keyset, counters: Counters):
     return sel
 
 
-def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None) -> ReplayResult:
+def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, skipping=None) -> ReplayResult:
     """getLatestSnapshot + getScanFiles restated; returns the ordered active scan files + counters.
 
     shard=(world, rank): reconcile only the checkpoint files whose replay-order index i has
     i % world == rank (every rank still reads the commit tail and any V2 manifest to discover
-    sidecars); res.tail_counters / res.ckpt_counters hold the two parts of the counters."""
+    sidecars); res.tail_counters / res.ckpt_counters hold the two parts of the counters.
+
+    skipping=(predicate node, {stats path: type}): ScanImpl.applyDataSkipping on the reconciled
+    rows (oracle/skipping.py); implies with_stats, leaves the counters unchanged."""
+    if skipping is not None:
+        with_stats = True
     world, rank = shard if shard else (1, 0)
     seg = load_log_segment(table_root)
     res = ReplayResult(version=seg.version, table_root=table_root)
@@ -636,4 +641,14 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None) 
     if keyset is not None:
         L.dkr_keyset_free(keyset)
     res.counters = Counters(*[a + b for a, b in zip(c.as_tuple(), cc.as_tuple())])
+    if skipping is not None:
+        from . import skipping as sk
+        node, types = skipping
+        res.json_rows = [a for a in res.json_rows if sk.keep(a.get("stats"), node, types)]
+        for b in res.checkpoint:
+            sc = b.cols.get(STATS_LEAF)
+            for i in np.nonzero(b.selected)[0]:
+                st = _str_at(sc, int(i), 2)
+                if not sk.keep(None if st is None else st.decode("utf-8", "replace"), node, types):
+                    b.selected[i] = False
     return res

@@ -1,0 +1,112 @@
+"""CPU ORACLE (test infrastructure only) for K11 data skipping: a restatement of what the reference
+does with a data-skipping predicate once the scan files are reconciled.
+
+  ScanImpl.applyDataSkipping            kernel-api/.../internal/ScanImpl.java:304-352
+      filter = COALESCE(skippingPredicate, true); rows selected = existing selection AND filter
+  DataSkippingUtils.parseJsonStats      kernel-api/.../internal/skipping/DataSkippingUtils.java:41-52
+      only selected rows with non-null stats are parsed (DefaultJsonHandler.parseJson :60-76)
+  DefaultJsonHandler.parseJson(String)  kernel-defaults/.../engine/DefaultJsonHandler.java:193-200
+      Jackson readTree with USE_BIG_DECIMAL_FOR_FLOATS (:48); trailing content ignored; the root
+      must be an object
+  DefaultJsonRow.decodeElement          kernel-defaults/.../internal/data/DefaultJsonRow.java:136-270
+      long/integer: an integral token in range; short/byte: any number whose exact value is an
+      integer in range (canConvertToExactIntegral); struct: an object; JSON null = null
+  DefaultExpressionEvaluator            kernel-defaults/.../internal/expressions/
+      comparators are null when either side is null; AND/OR are Kleene (visitAnd/visitOr)
+
+The predicate tree is the planner's (delta_amd/skipping.py, itself restating DataSkippingUtils
+.constructDataSkippingFilter); `types` maps each referenced stats path to its Kernel type name.
+Nothing here is used by the product path.
+"""
+from __future__ import annotations
+
+import json
+from decimal import Decimal
+
+RANGES = {"long": (-(1 << 63), (1 << 63) - 1), "integer": (-(1 << 31), (1 << 31) - 1),
+          "short": (-(1 << 15), (1 << 15) - 1), "byte": (-(1 << 7), (1 << 7) - 1)}
+
+
+class StatsDecodeError(RuntimeError):
+    pass
+
+
+def _reject_constant(tok):
+    raise StatsDecodeError("non-standard JSON token %s" % tok)
+
+
+_DECODER = json.JSONDecoder(parse_float=Decimal, parse_constant=_reject_constant)
+
+
+def parse_root(s: str):
+    i = 0
+    while i < len(s) and s[i] in " \t\r\n":
+        i += 1
+    try:
+        obj, _ = _DECODER.raw_decode(s, i)          # trailing content is ignored, as readTree does
+    except json.JSONDecodeError as e:
+        raise StatsDecodeError("Could not parse JSON: %s" % s) from e
+    if not isinstance(obj, dict):
+        raise StatsDecodeError("stats root is not an object: %s" % s)
+    return obj
+
+
+def _leaf(v, typ):
+    if v is None:
+        return None
+    lo, hi = RANGES[typ]
+    if isinstance(v, bool) or not isinstance(v, (int, Decimal)):
+        raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))
+    if isinstance(v, Decimal):
+        if typ in ("long", "integer") or v != v.to_integral_value():
+            raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))
+        v = int(v)
+    if not lo <= v <= hi:
+        raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))
+    return v
+
+
+def decode_stats(s: str, types: dict) -> dict:
+    """path tuple -> python int or None, for every referenced path."""
+    root = parse_root(s)
+    out = {}
+    for path, typ in types.items():
+        node = root
+        for comp in path[:-1]:
+            node = node.get(comp)
+            if node is None:
+                break
+            if not isinstance(node, dict):
+                raise StatsDecodeError("Couldn't decode %r, expected a object" % (node,))
+        out[path] = None if node is None else _leaf(node.get(path[-1]), typ)
+    return out
+
+
+def evaluate(node, vals):
+    """True / False / None (null) for a planner node over decoded stats."""
+    k = node[0]
+    if k == "stat":
+        return vals[node[1]]
+    if k == "lit":
+        return node[1]
+    if k == "AND":
+        a, b = evaluate(node[1], vals), evaluate(node[2], vals)
+        if a is False or b is False:
+            return False
+        return True if (a is True and b is True) else None
+    if k == "OR":
+        a, b = evaluate(node[1], vals), evaluate(node[2], vals)
+        if a is True or b is True:
+            return True
+        return False if (a is False and b is False) else None
+    a, b = evaluate(node[1], vals), evaluate(node[2], vals)
+    if a is None or b is None:
+        return None
+    return {"<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b, "=": a == b}[k]
+
+
+def keep(stats: str | None, node, types) -> bool:
+    """COALESCE(skippingPredicate, true) for one selected row (null stats -> kept)."""
+    if stats is None:
+        return True
+    return evaluate(node, decode_stats(stats, types)) is not False

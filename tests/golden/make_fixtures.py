@@ -22,6 +22,9 @@ TABLES = {
     "delete-re-add-same-file-different-transactions": GOLD, "multi-part-checkpoint": GOLD,
     "basic-with-inserts-deletes-checkpoint": GOLD, "only-checkpoint-files": GOLD, "v2-checkpoint-parquet": GOLD,
     "dv-partitioned-with-checkpoint": GOLD, "data-skipping-basic-stats-all-types-checkpoint": GOLD,
+    "data-skipping-basic-stats-all-types": GOLD, "data-skipping-basic-stats-all-types-columnmapping-name": GOLD,
+    "data-skipping-basic-stats-all-types-columnmapping-id": GOLD,
+    "data-skipping-change-stats-collected-across-versions": GOLD, "data-skipping-partition-and-data-column": GOLD,
     "basic-dv-with-checkpoint": KDRES, "basic-with-checkpoint": KDRES,
 }
 

@@ -1,0 +1,389 @@
+"""K11 data skipping (delta_amd/skipping.py planner, k_stats_eval on the GPU, oracle/skipping.py).
+
+Pinned to the reference's own expectations on its golden tables (KDT = kernel-defaults/src/test/scala/
+io/delta/kernel/defaults):
+  ScanSuite.scala:1150-1196  basic data skipping for all types (+ column mapping name/id, checkpoint):
+                             hits / misses for int, long, byte, short (the integral types the GPU
+                             evaluator decodes; float/double/string/date/decimal filters are refused)
+  ScanSuite.scala:1233-1239  filter on a non-existent column -> no skipping
+  ScanSuite.scala:1243-1253  AND of two data columns -> 1 file
+  ScanSuite.scala:1255-1267  stats collected changing across versions -> 1 / 2 / 1 files
+  ScanSuite.scala:1508-1545  referenced stats columns per predicate
+GPU tests compare the product's ordered scan files and counters with the oracle on the same tables,
+on synthetic tables with stats (commit tail + checkpoint), and on hand-written stats JSON edge cases.
+"""
+import json
+import os
+
+import pytest
+
+from delta_amd import skipping as sk
+from delta_amd import synth
+from delta_amd.expressions import ALWAYS_TRUE, And, Column, Literal, Or, Predicate
+from tests.golden_util import TABLES
+
+ALL_TYPES = ["data-skipping-basic-stats-all-types", "data-skipping-basic-stats-all-types-columnmapping-name",
+             "data-skipping-basic-stats-all-types-columnmapping-id",
+             "data-skipping-basic-stats-all-types-checkpoint"]
+INTEGRAL = {"as_int": Literal.ofInt, "as_long": Literal.ofLong, "as_byte": Literal.ofByte,
+            "as_short": Literal.ofShort}
+
+
+def col(n):
+    return Column(n)
+
+
+def cmp(op, c, v):
+    return Predicate(op, c, v)
+
+
+def all_types_hits_misses():
+    """ScanSuite.scala:1150-1183: value in table 0, smaller -1, bigger 1."""
+    hits, misses = [], []
+    for name, lit in INTEGRAL.items():
+        c, value, small, big = col(name), lit(0), lit(-1), lit(1)
+        misses += [cmp("=", c, small), cmp(">", c, value), cmp(">=", c, big), cmp("<", c, value),
+                   cmp("<=", c, small)]
+        hits += [cmp("=", c, value), cmp(">", c, small), cmp(">=", c, value), cmp("<", c, big),
+                 cmp("<=", c, value)]
+    return hits, misses
+
+
+def table_metadata(root):
+    """(schemaString, partitionColumns) of the latest metaData in the table's commits (or its
+    checkpoint when the commits carry none)."""
+    log = os.path.join(root, "_delta_log")
+    md = None
+    for f in sorted(os.listdir(log)):
+        if f.endswith(".json"):
+            with open(os.path.join(log, f)) as fh:
+                for line in fh:
+                    o = json.loads(line)
+                    if o.get("metaData"):
+                        md = o["metaData"]
+    if md is None:
+        import pyarrow.parquet as pq
+        for f in sorted(os.listdir(log)):
+            if ".checkpoint" in f and f.endswith(".parquet"):
+                t = pq.read_table(os.path.join(log, f), columns=["metaData"]).column(0).to_pylist()
+                md = next((x for x in t if x), md)
+    return md["schemaString"], md.get("partitionColumns") or []
+
+
+def oracle_skipping(root, predicate):
+    schema, parts = table_metadata(root)
+    pf, data = sk.split_filters(predicate, parts)
+    assert pf is None
+    if data is None:
+        return None
+    leaves = sk.data_schema_leaves(schema, parts)
+    node = sk.construct(data, leaves)
+    if node is None:
+        return None
+    paths, types, _ = sk.compile_program(node, leaves)
+    names = {v: k for k, v in sk.TYPE_CODE.items()}
+    return node, {p: names[t] for p, t in zip(paths, types)}
+
+
+def oracle_files(root, predicate, bs=1024):
+    from oracle import ref
+    r = ref.replay(root, json_batch_size=bs, with_stats=True, skipping=oracle_skipping(root, predicate))
+    return r.scan_files(), r.counters.as_tuple()
+
+
+# ---------------------------------------------------------------- planner (host logic, CPU)
+def test_split_filters():
+    p = And(cmp(">", col("part"), Literal.ofInt(0)), cmp(">", col("id"), Literal.ofInt(0)))
+    a, b = sk.split_filters(p, ["PART"])
+    assert a == cmp(">", col("part"), Literal.ofInt(0)) and b == cmp(">", col("id"), Literal.ofInt(0))
+    a, b = sk.split_filters(Or(cmp(">", col("part"), Literal.ofInt(0)), cmp(">", col("id"), Literal.ofInt(0))),
+                            ["part"])
+    assert a is None and b.name == "OR"
+    assert sk.split_filters(ALWAYS_TRUE, []) == (None, None)
+    # literal-only predicates have no non-partition column: they go to the partition side
+    assert sk.split_filters(cmp("=", Literal.ofInt(1), Literal.ofInt(1)), [])[1] is None
+
+
+def test_referenced_stats_match_reference():
+    # ScanSuite.scala:1527-1538
+    schema, parts = table_metadata(os.path.join(TABLES, "data-skipping-basic-stats-all-types"))
+    leaves = sk.data_schema_leaves(schema, parts)
+    z = Literal.ofInt(0)
+    cases = [(cmp("=", col("as_int"), z), {("minValues", "as_int"), ("maxValues", "as_int")}),
+             (cmp("<", col("as_int"), z), {("minValues", "as_int")}),
+             (cmp(">", col("as_int"), z), {("maxValues", "as_int")}),
+             (cmp(">=", col("as_int"), z), {("maxValues", "as_int")}),
+             (cmp("<=", col("as_int"), z), {("minValues", "as_int")}),
+             (And(cmp("<", col("as_int"), z), cmp(">", col("as_long"), z)),
+              {("minValues", "as_int"), ("maxValues", "as_long")})]
+    for p, want in cases:
+        assert set(sk.referenced_stats(sk.construct(p, leaves))) == want
+
+
+def test_construct_rules():
+    leaves = {("a",): ("long", ("a",)), ("b",): ("integer", ("col-b",)), ("m",): ("map", ("m",))}
+    v = Literal.ofLong(5)
+    # literal on the left is reversed; OR needs both sides; AND keeps one side
+    assert sk.construct(cmp("<", v, col("a")), leaves) == (">", ("stat", ("maxValues", "a")), ("lit", 5))
+    assert sk.construct(Or(cmp("<", col("a"), v), cmp("<", col("m"), v)), leaves) is None
+    assert sk.construct(And(cmp("<", col("a"), v), cmp("<", col("m"), v)), leaves) == \
+        ("<", ("stat", ("minValues", "a")), ("lit", 5))
+    # physical names; IS_NULL / IS_NOT_NULL use nullCount and numRecords
+    assert sk.construct(Predicate("IS_NOT_NULL", col("b")), leaves) == \
+        ("<", ("stat", ("nullCount", "col-b")), ("stat", ("numRecords",)))
+    assert sk.construct(Predicate("NOT", Predicate("IS_NOT_NULL", col("b"))), leaves) == \
+        (">", ("stat", ("nullCount", "col-b")), ("lit", 0))
+    # NOT(a = 5) -> min < 5 OR max > 5; NOT(a < 5) -> max >= 5
+    assert sk.construct(Predicate("NOT", cmp("=", col("a"), v)), leaves) == \
+        ("OR", ("<", ("stat", ("minValues", "a")), ("lit", 5)), (">", ("stat", ("maxValues", "a")), ("lit", 5)))
+    assert sk.construct(Predicate("NOT", cmp("<", col("a"), v)), leaves) == \
+        (">=", ("stat", ("maxValues", "a")), ("lit", 5))
+    # IS NOT DISTINCT FROM null -> IS_NULL
+    assert sk.construct(cmp("IS NOT DISTINCT FROM", col("a"), Literal.ofNull("long")), leaves) == \
+        (">", ("stat", ("nullCount", "a")), ("lit", 0))
+    # non-existent column: no skipping (ScanSuite.scala:1233-1239)
+    assert sk.construct(cmp("=", col("foo"), Literal.ofInt(1)), leaves) is None
+
+
+def test_compile_refuses_unsupported():
+    leaves = {("f",): ("float", ("f",)), ("s",): ("string", ("s",)), ("a",): ("long", ("a",))}
+    for p in (cmp("=", col("f"), Literal(0.0, "float")), cmp("=", col("s"), Literal.ofString("x")),
+              cmp("=", col("a"), Literal(0.5, "double"))):
+        node = sk.construct(p, leaves)
+        assert node is not None
+        with pytest.raises(sk.UnsupportedSkipping):
+            sk.compile_program(node, leaves)
+    node = sk.construct(cmp("=", col("a"), Literal.ofLong(3)), leaves)
+    paths, types, ops = sk.compile_program(node, leaves)
+    assert paths == [("minValues", "a"), ("maxValues", "a")] and types == [0, 0]
+    assert [o[0] for o in ops] == [sk.OP_STAT, sk.OP_LIT, sk.OP_LE, sk.OP_STAT, sk.OP_LIT, sk.OP_GE, sk.OP_AND]
+
+
+def test_pack_layout():
+    from delta_amd._lib import dk_skip_program
+    import ctypes
+    assert ctypes.sizeof(dk_skip_program) == 4 + 32 + 32 + 128 + 128 + 512 + 4 + 256 + 256 + 512
+    leaves = {("s", "x"): ("short", ("col-s", "col-x"))}
+    prog = sk.pack(sk.compile_program(sk.construct(cmp(">", col("s", "x") if False else Column("s", "x"),
+                                                       Literal.ofShort(3)), leaves), leaves), dk_skip_program)
+    assert prog.n_paths == 1 and prog.path_depth[0] == 3 and prog.path_type[0] == 2
+    names = bytes(prog.names)
+    assert [names[prog.name_off[0][d]:prog.name_off[0][d] + prog.name_len[0][d]] for d in range(3)] == \
+        [b"maxValues", b"col-s", b"col-x"]
+
+
+# ---------------------------------------------------------------- oracle (pinned to the reference)
+def test_oracle_stats_decoding_rules():
+    from oracle import skipping as osk
+    t = {("minValues", "x"): "short", ("maxValues", "y"): "long", ("numRecords",): "long"}
+    d = osk.decode_stats('{"numRecords":7,"minValues":{"x":5.0E0},"maxValues":{"y":-3}} trailing', t)
+    assert d == {("minValues", "x"): 5, ("maxValues", "y"): -3, ("numRecords",): 7}
+    assert osk.decode_stats('{"minValues":null,"numRecords":1,"numRecords":2}', t) == \
+        {("minValues", "x"): None, ("maxValues", "y"): None, ("numRecords",): 2}
+    for bad in ('{"maxValues":{"y":1.0}}', '{"minValues":{"x":5.5}}', '{"minValues":{"x":40000}}',
+                '{"minValues":3}', '{"numRecords":"1"}', '[]', '', '{"numRecords":true}',
+                '{"maxValues":{"y":9223372036854775808}}', '{"numRecords":01}'):
+        with pytest.raises(osk.StatsDecodeError):
+            osk.decode_stats(bad, t)
+
+
+@pytest.mark.parametrize("name", ALL_TYPES)
+def test_oracle_all_types_hits_and_misses(name):
+    root = os.path.join(TABLES, name)
+    hits, misses = all_types_hits_misses()
+    for p in hits:
+        assert oracle_files(root, p, bs=2)[0], ("expected hit", name, p)
+    for p in misses:
+        assert not oracle_files(root, p, bs=2)[0], ("expected miss", name, p)
+
+
+def test_oracle_non_existent_column_and_counts():
+    root = os.path.join(TABLES, "data-skipping-basic-stats-all-types")
+    assert oracle_files(root, cmp("=", col("foo"), Literal.ofInt(1)))[0]
+    root = os.path.join(TABLES, "data-skipping-partition-and-data-column")
+    p = And(cmp(">", col("part"), Literal.ofInt(0)), cmp(">", col("id"), Literal.ofInt(0)))
+    assert len(oracle_files(root, p)[0]) == 1
+    root = os.path.join(TABLES, "data-skipping-change-stats-collected-across-versions")
+    for p, n in ((cmp("=", col("col1"), Literal.ofInt(1)), 1), (cmp("=", col("col2"), Literal.ofInt(1)), 2),
+                 (And(cmp("=", col("col1"), Literal.ofInt(1)), cmp("=", col("col2"), Literal.ofInt(1))), 1)):
+        assert len(oracle_files(root, p)[0]) == n, p
+
+
+def test_oracle_skipping_leaves_counters_unchanged(tmp_path):
+    from oracle import ref
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=3_000, n_parts=2, n_commits=4, dv_frac=0.1,
+                                                     ckpt_removes=20, with_stats=True))
+    full = ref.replay(str(tmp_path), with_stats=True)
+    files, counters = oracle_files(str(tmp_path), cmp(">", col("id"), Literal.ofLong(30_000_000)))
+    assert counters == full.counters.as_tuple()
+    assert 0 < len(files) < len(full.scan_files())
+
+
+# ---------------------------------------------------------------- GPU parity
+def _gpu_files(root, predicate, eng):
+    from delta_amd import kernel as K
+    from oracle import ref
+    snap = K.Table.forPath(eng, root).getLatestSnapshot(eng)
+    scan = snap.getScanBuilder().withFilter(predicate).build()
+    try:
+        rows = [ref.canon_add_from_cols(b.data, int(i)) for b in scan.getScanFiles(eng) for i in b.selected_rows()]
+        return rows, scan.metrics.as_tuple()
+    finally:
+        scan.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ALL_TYPES)
+def test_gpu_all_types_hits_and_misses(name):
+    from delta_amd import kernel as K
+    root = os.path.join(TABLES, name)
+    eng = K.GpuEngine(json_batch_size=2)
+    hits, misses = all_types_hits_misses()
+    for p in hits + misses:
+        g = _gpu_files(root, p, eng)
+        o = oracle_files(root, p, bs=2)
+        assert g == o, (name, p)
+        assert bool(g[0]) == (p in hits), (name, p)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_golden_counts():
+    from delta_amd import kernel as K
+    eng = K.GpuEngine()
+    root = os.path.join(TABLES, "data-skipping-partition-and-data-column")
+    p = And(cmp(">", col("part"), Literal.ofInt(0)), cmp(">", col("id"), Literal.ofInt(0)))
+    assert len(_gpu_files(root, p, eng)[0]) == 1
+    root = os.path.join(TABLES, "data-skipping-change-stats-collected-across-versions")
+    for p, n in ((cmp("=", col("col1"), Literal.ofInt(1)), 1), (cmp("=", col("col2"), Literal.ofInt(1)), 2),
+                 (And(cmp("=", col("col1"), Literal.ofInt(1)), cmp("=", col("col2"), Literal.ofInt(1))), 1)):
+        g = _gpu_files(root, p, eng)
+        assert len(g[0]) == n and g == oracle_files(root, p), p
+    eng.close()
+
+
+SYNTH_PREDICATES = [
+    cmp(">", col("id"), Literal.ofLong(30_000_000)),
+    cmp("<=", col("id"), Literal.ofInt(20_000_000)),
+    cmp("=", col("id"), Literal.ofLong(25_000_123)),
+    And(cmp(">=", col("id"), Literal.ofLong(15_000_000)), cmp("<", col("id"), Literal.ofLong(35_000_000))),
+    Or(cmp("<", col("id"), Literal.ofLong(12_000_000)), cmp(">", col("id"), Literal.ofLong(48_000_000))),
+    Predicate("NOT", cmp("<", col("id"), Literal.ofLong(40_000_000))),
+    Predicate("IS_NOT_NULL", col("id")),
+    Predicate("IS_NULL", col("id")),
+    cmp("IS NOT DISTINCT FROM", col("id"), Literal.ofLong(33_333_333)),
+]
+
+
+@pytest.mark.gpu
+def test_gpu_synthetic_parity(tmp_path):
+    from delta_amd import kernel as K
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=40_000, n_parts=3, n_commits=6, dv_frac=0.2,
+                                                     ckpt_removes=200, with_stats=True))
+    eng = K.GpuEngine()
+    for p in SYNTH_PREDICATES:
+        g = _gpu_files(str(tmp_path), p, eng)
+        o = oracle_files(str(tmp_path), p)
+        assert g[1] == o[1], p
+        assert len(g[0]) == len(o[0]) and g[0] == o[0], p
+    eng.close()
+
+
+def _write_edge_table(root, stats_list):
+    """A commit-only table whose adds carry the given raw stats strings (None = no stats)."""
+    log = os.path.join(root, "_delta_log")
+    os.makedirs(log)
+    schema = {"type": "struct", "fields": [{"name": "x", "type": "short", "nullable": True, "metadata": {}},
+                                           {"name": "id", "type": "long", "nullable": True, "metadata": {}}]}
+    with open(os.path.join(log, "%020d.json" % 0), "w") as f:
+        f.write(json.dumps({"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}) + "\n")
+        f.write(json.dumps({"metaData": {"id": "t", "format": {"provider": "parquet", "options": {}},
+                                         "schemaString": json.dumps(schema), "partitionColumns": [],
+                                         "configuration": {}, "createdTime": 0}}) + "\n")
+        for i, st in enumerate(stats_list):
+            a = {"path": "f%d.parquet" % i, "partitionValues": {}, "size": 1, "modificationTime": 0,
+                 "dataChange": True}
+            if st is not None:
+                a["stats"] = st
+            f.write(json.dumps({"add": a}) + "\n")
+
+
+EDGE_STATS = [
+    '{"numRecords":3,"minValues":{"x":2,"id":10},"maxValues":{"x":9,"id":20},"nullCount":{"x":0,"id":0}}',
+    '{"numRecords":3,"minValues":{"x":2.0,"id":10},"maxValues":{"x":9E0,"id":20}}',
+    '{"numRecords":3,"minValues":{"x":-0.0e3,"id":-5},"maxValues":{"x":1.50e1,"id":5}}',
+    '{"numRecords":3,"minValues":{"x":7},"maxValues":{"x":8}} {"ignored": 1}',
+    '{"numRecords":3,"minValues":{"x":1,"x":7},"maxValues":{"x":3,"x":8}}',
+    '{"numRecords":3,"minValues":null,"maxValues":{"x":null}}',
+    '{"numRecords":3,"min\\u0056alues":{"x":100},"maxValues":{"\\u0078":200}}',
+    '{"numRecords":3,"minValues":{"x":4,"other":[1,{"a":"}"}]},"maxValues":{"x":6,"s":"\\"x\\""}}',
+    '{ "numRecords" : 3 , "minValues" : { "x" : 4 } , "maxValues" : { "x" : 4 } }',
+    '{"numRecords":3,"nullCount":{"x":3,"id":1},"minValues":{"x":4,"id":0},"maxValues":{"x":4,"id":0}}',
+    None,
+    '{}',
+]
+EDGE_PREDICATES = [cmp("=", col("x"), Literal.ofShort(4)), cmp(">", col("x"), Literal.ofShort(8)),
+                   cmp("<", col("x"), Literal.ofInt(2)), Predicate("IS_NULL", col("x")),
+                   Predicate("IS_NOT_NULL", col("id")), cmp("=", col("id"), Literal.ofLong(15)),
+                   Or(cmp("=", col("x"), Literal.ofShort(7)), cmp("=", col("id"), Literal.ofLong(0)))]
+
+
+@pytest.mark.gpu
+def test_gpu_stats_json_edge_cases(tmp_path):
+    from delta_amd import kernel as K
+    root = str(tmp_path / "t")
+    _write_edge_table(root, EDGE_STATS)
+    eng = K.GpuEngine()
+    for p in EDGE_PREDICATES:
+        g = _gpu_files(root, p, eng)
+        o = oracle_files(root, p)
+        assert g == o, p
+    eng.close()
+
+
+def test_oracle_edge_cases_expected():
+    """The oracle's answers on the edge-case table, written out by hand from the decoding rules."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        root = os.path.join(d, "t")
+        _write_edge_table(root, EDGE_STATS)
+        got = {i: sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0])
+               for i, p in enumerate(EDGE_PREDICATES)}
+    every = list(range(len(EDGE_STATS)))
+    assert got[0] == [0, 1, 2, 5, 7, 8, 9, 10, 11]      # min.x <= 4 AND max.x >= 4 (row 4: last key wins)
+    assert got[1] == [0, 1, 2, 5, 6, 10, 11]            # max.x > 8 (row 6: escaped key names)
+    assert got[2] == [2, 5, 10, 11]                     # min.x < 2 (row 2: -0.0e3 is 0)
+    assert got[3] == every[1:]                          # nullCount.x > 0: only row 0 is provably false
+    assert got[4] == every                              # nullCount.id < numRecords
+    assert got[5] == [i for i in every if i not in (2, 9)]
+    assert got[6] == every                              # F OR null = null -> kept
+
+
+BAD_STATS = ['{"numRecords":3,"minValues":{"x":4.5}}', '{"numRecords":3,"minValues":{"x":40000}}',
+             '{"numRecords":3,"minValues":{"id":1.0}}', '{"numRecords":3,"minValues":3}',
+             '{"numRecords":3,"minValues":{"x":"4"}}', '[1]', '{"numRecords":3,"minValues":{"x":4}',
+             '{"numRecords":3,"minValues":{"x":04}}']
+BAD_PREDICATE = And(cmp("<=", col("x"), Literal.ofShort(100)), cmp("<=", col("id"), Literal.ofLong(100)))
+
+
+def test_oracle_bad_stats_raise(tmp_path):
+    from oracle import skipping as osk
+    for i, bad in enumerate(BAD_STATS):
+        root = str(tmp_path / str(i))
+        _write_edge_table(root, [EDGE_STATS[0], bad])
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(root, BAD_PREDICATE)
+
+
+@pytest.mark.gpu
+def test_gpu_stats_decode_errors_raise(tmp_path):
+    """A stats string the reference cannot decode fails the scan on the GPU too."""
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    eng = K.GpuEngine()
+    for i, bad in enumerate(BAD_STATS):
+        root = str(tmp_path / str(i))
+        _write_edge_table(root, [EDGE_STATS[0], bad])
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(root, BAD_PREDICATE, eng)
+    eng.close()
