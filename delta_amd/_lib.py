@@ -7,7 +7,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdkgpu.so")
+# DK_LIB_PATH: load another build of the same ABI (A/B of kernel variants; tools/build_variant.py)
+LIB_PATH = os.environ.get("DK_LIB_PATH") or os.path.join(_HERE, "libdkgpu.so")
 _lib = None
 
 
