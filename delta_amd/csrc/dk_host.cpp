@@ -28,7 +28,8 @@ void launch_tile_chars(const DChunk*, DPage*, const uint8_t*, const int32_t*, co
 void launch_tile_scan2(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
 void launch_tile_decode(const DChunk*, DPage*, const DColumn*, const uint8_t*, const int32_t*, const long long*, const Seg*, const DTile*, int, int, DState*, hipStream_t);
 void launch_delta_decode(const DChunk*, DPage*, int, const uint8_t*, long long*, hipStream_t);
-void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const int2*, hipStream_t, int);
+void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const uint8_t*, const int32_t*, const int2*, hipStream_t,
+                        int, int);
 void launch_json_canon(DJsonAction*, int, const uint8_t*, uint8_t*, uint32_t, DState*, hipStream_t);
 void launch_slots_init(Slot*, uint64_t, hipStream_t);
 void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
@@ -359,6 +360,7 @@ struct dk_parquet {
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
   std::vector<int> col_tile0;
+  int copy_cb = 16384;       // k_string_copy staging buffer bytes (sized to the data in prepare)
   std::vector<std::unique_ptr<DBuf>> outbufs;
   std::vector<HostCol> host;
   int n_pages = 0, n_cols = 0;
@@ -437,10 +439,11 @@ static int run_pipeline(dk_parquet* p, int mode) {
   {
     KTimer::Scope sc(&T, 6, s);
     const int2* tiles = p->d_tiles.as<int2>();
-    if (!split_launch()) launch_string_copy(C, P, p->col_tile0.back(), cols, arena, pos, tiles, s, 0);
+    if (!split_launch()) launch_string_copy(C, P, p->col_tile0.back(), cols, arena, pos, tiles, s, 0, p->copy_cb);
     else
       for (int c = 0; c < p->n_cols; c++)
-        launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c]);
+        launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c],
+                           p->copy_cb);
   }
   { KTimer::Scope sc(&T, 5, s); per_column_tiles(p, [&](int a, int k) { launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, k, a, st, s); }); }
   return 0;
@@ -565,6 +568,15 @@ static int prepare(dk_parquet* p) {
   {
     std::vector<int2> tiles;
     p->col_tile0.assign(1, 0);
+    // staging buffer: the busiest PLAIN page's mean span of DK_COPY_TILE values (+5%), so a typical
+    // tile is one pass while the two buffers stay small enough for high occupancy
+    double span = 0;
+    for (const DPage& pg : p->h_pages) {
+      const DChunk& ck = p->h_chunks[pg.chunk];
+      if (ck.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN || pg.n_values <= 0) continue;
+      span = std::max(span, (double)pg.vbytes / pg.n_values * DK_COPY_TILE * 1.05 + 64);
+    }
+    p->copy_cb = span > 0 ? (int)span : 16384;
     for (size_t ci = 0; ci < p->h_cols.size(); ci++) {
       const DColumn& c = p->h_cols[ci];
       for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {

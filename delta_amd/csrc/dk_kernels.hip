@@ -1148,7 +1148,10 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
 // --------------------------------------------------------------------------------------------
 // K6: PLAIN string bytes -> contiguous output chars, fused with the key-path hash.
 // One 128-thread workgroup per tile of CT values of one page (host-built tile table: a 1 MB page
-// spreads over ~90 workgroups). Per tile (split further if its input span exceeds CT_BYTES):
+// spreads over ~90 workgroups). Per tile (split further if its input span exceeds cb, the staging
+// buffer size the host sizes per launch to the data: just above a typical tile span, because the two
+// LDS buffers set the occupancy -- 16 KiB buffers hold 4 workgroups per CU, 12 KiB six, and at 91 B
+// per path value the copy ran 868 -> 639 us):
 //   1. stage the input span (length prefixes + bytes) into LDS `in` with aligned dwordx4 loads;
 //   2. lane k compacts value k into LDS `out` at its output position (dword stores, the source
 //      dword stream shifted with v_alignbyte; byte stores only at the value's two edges), and,
@@ -1157,10 +1160,10 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
 //   3. `out` is laid out congruent to the global destination mod 16, so the store pass is one
 //      ds_read_b128 + global dwordx4 store per lane (byte stores for the two edge chunks, which
 //      neighbouring tiles/pages share).
-// A single value larger than CT_BYTES is copied straight from global memory (hash 0).
+// A single value larger than the buffer is copied straight from global memory (hash 0).
 // --------------------------------------------------------------------------------------------
 constexpr int CT = DK_COPY_TILE;       // threads = values per tile
-constexpr int CT_BYTES = 16384;        // LDS bytes per staging buffer
+constexpr int CT_BYTES_MAX = 16384;    // largest staging buffer (bytes; dynamic LDS holds two)
 
 __device__ __forceinline__ uint32_t lds_u32_at(const uint32_t* w, int32_t b) {   // 4 bytes at any byte offset
   const int32_t i = b >> 2;
@@ -1170,7 +1173,7 @@ __device__ __forceinline__ uint32_t lds_u32_at(const uint32_t* w, int32_t b) {  
 __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                     const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
                                                     const int32_t* __restrict__ pos, const int2* __restrict__ tiles,
-                                                    int tile0, int dbg) {
+                                                    int tile0, int cb, int dbg) {
   const int2 tile = tiles[tile0 + blockIdx.x];     // (page, first value)
   const DPage pg = pages[tile.x];                  // by value: byte stores below may alias
   if (pg.status != PS_OK) return;
@@ -1202,8 +1205,9 @@ __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ c
   const int n = min(nvals, tile.y + CT);
   if (n <= tile.y || (!ob && !vh)) return;
   const int t = threadIdx.x;
-  __shared__ uint4 inw[CT_BYTES / 16 + 2];
-  __shared__ uint4 outw[CT_BYTES / 16 + 2];
+  extern __shared__ uint4 smem_copy[];             // 2 x (cb + 32) bytes: input image, output image
+  uint4* inw = smem_copy;
+  uint4* outw = smem_copy + cb / 16 + 2;
   const uint32_t* in32 = (const uint32_t*)inw;
   const uint8_t* in8 = (const uint8_t*)inw;
   uint32_t* out32 = (uint32_t*)outw;
@@ -1212,7 +1216,7 @@ __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ c
     const int32_t a0 = P[v0];
     const int v = v0 + t;
     const int32_t pv = v < n ? P[v] : 0, pv1 = v < n ? P[v + 1] : 0;
-    const bool fits = v < n && (pv1 - a0) <= CT_BYTES - 32;
+    const bool fits = v < n && (pv1 - a0) <= cb - 32;
     const int cnt = __syncthreads_count(fits);      // fits is monotone in t
     if (cnt == 0) {
       // one value larger than the staging buffer: plain global copy, no hash
@@ -1976,9 +1980,14 @@ void launch_delta_decode(const DChunk* c, DPage* p, int n, const uint8_t* arena,
   if (n) hipLaunchKernelGGL(k_delta_decode, dim3(n), dim3(NT), 0, s, c, p, arena, dbp);
 }
 void launch_string_copy(const DChunk* c, const DPage* p, int ntiles, const DColumn* cols, const uint8_t* arena,
-                        const int32_t* pos, const int2* tiles, hipStream_t s, int tile0) {
+                        const int32_t* pos, const int2* tiles, hipStream_t s, int tile0, int cb) {
   static const int dbg = getenv("DK_COPY_DBG") ? atoi(getenv("DK_COPY_DBG")) : 0;
-  if (ntiles) hipLaunchKernelGGL(k_string_copy, dim3(ntiles), dim3(CT), 0, s, c, p, cols, arena, pos, tiles, tile0, dbg);
+  // the two buffers' LDS sets how many workgroups share a CU (12 KiB: six, 16 KiB: four), so the host
+  // sizes them to the data; never grow them toward an occupancy edge (allocation granularity)
+  cb = cb < 2048 ? 2048 : cb > CT_BYTES_MAX ? CT_BYTES_MAX : (cb + 255) & ~255;
+  if (ntiles)
+    hipLaunchKernelGGL(k_string_copy, dim3(ntiles), dim3(CT), 2 * (cb + 32), s, c, p, cols, arena, pos, tiles, tile0, cb,
+                       dbg);
 }
 void launch_json_canon(DJsonAction* a, int n, const uint8_t* jchars, uint8_t* canon, uint32_t seed, DState* st,
                        hipStream_t s) {
