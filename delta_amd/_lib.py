@@ -21,6 +21,12 @@ class dk_config(C.Structure):
                 ("device", C.c_int32), ("flags", C.c_int32)]
 
 
+class dk_part_program(C.Structure):
+    _fields_ = [("n_fields", C.c_int32), ("field_type", C.c_int32 * 8), ("name_off", C.c_int32 * 8),
+                ("name_len", C.c_int32 * 8), ("n_ops", C.c_int32), ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64),
+                ("lit", C.c_int64 * 64), ("pool", C.c_char * 1024)]
+
+
 class dk_column(C.Structure):
     _fields_ = [("n_rows", C.c_int64), ("n_entries", C.c_int64), ("n_chars", C.c_int64),
                 ("phys", C.c_int32), ("width", C.c_int32), ("max_def", C.c_int32), ("max_rep", C.c_int32),
@@ -38,7 +44,7 @@ class dk_skip_program(C.Structure):
 EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
            "dk_parquet_traffic", "dk_parquet_kernel_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
-           "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_run",
+           "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free"]
@@ -72,6 +78,7 @@ def lib(build_if_missing=True):
         "dk_json_tail_free": (None, [P]),
         "dk_replay_create": (C.c_int, [P, P, P, C.POINTER(P)]),
         "dk_replay_set_skipping": (C.c_int, [P, P]),
+        "dk_replay_set_partition_filter": (C.c_int, [P, P]),
         "dk_replay_run": (C.c_int, [P]), "dk_replay_sync": (C.c_int, [P]),
         "dk_replay_counters": (C.c_int, [P, C.POINTER(I64)]),
         "dk_replay_counters_split": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),

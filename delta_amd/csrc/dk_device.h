@@ -124,7 +124,7 @@ struct Slot {
   int32_t min_rm_step;           // min step over JSON removes, INT32_MAX = none
 };
 
-enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8, E_STATS = 16 };
+enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8, E_STATS = 16, E_PART = 32 };
 
 // Data-skipping program (layout of dk_skip_program in include/dkgpu.h): the stats fields to
 // extract from each row's add.stats JSON and a postfix program over them (delta_amd/skipping.py).
@@ -142,6 +142,38 @@ struct DSkipProg {
   int32_t op[SK_MAX_OPS];
   int32_t arg[SK_MAX_OPS];
   int64_t lit[SK_MAX_OPS];
+};
+
+// Partition-pruning program (layout of dk_part_program in include/dkgpu.h; delta_amd/partitions.py):
+// the partition columns it reads (physical names, looked up in each row's partitionValues map) and
+// a postfix program over their deserialized values.
+constexpr int PP_MAX_FIELDS = 8, PP_MAX_OPS = 64, PP_POOL = 1024;
+enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING = 4 };
+enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, PO_LT = 4, PO_LE = 5, PO_GT = 6,
+                 PO_GE = 7, PO_EQ = 8, PO_NSEQ = 9, PO_ISNULL = 10, PO_ISNOTNULL = 11, PO_NOT = 12, PO_AND = 13,
+                 PO_OR = 14 };
+struct DPartProg {
+  int32_t n_fields;
+  int32_t field_type[PP_MAX_FIELDS];
+  int32_t name_off[PP_MAX_FIELDS];
+  int32_t name_len[PP_MAX_FIELDS];
+  int32_t n_ops;
+  int32_t op[PP_MAX_OPS];
+  int32_t arg[PP_MAX_OPS];       // PO_FIELD: field; PO_LIT_STR: length
+  int64_t lit[PP_MAX_OPS];       // PO_LIT_INT: value; PO_LIT_STR: offset into pool
+  char pool[PP_POOL];            // field names and string literals (UTF-8)
+};
+
+// partitionValues map rows: repeated key / value leaves (row_offs over entries), per action for the
+// commit tail (act_row maps an action to its row) or per row for a checkpoint file
+struct MapRows {
+  int64_t n;
+  const int64_t* act_row;        // null: row r is action r
+  const uint8_t* row_def; int32_t rep_def; int32_t v_max_def;
+  const int64_t* row_offs;
+  const int64_t* k_offs; const uint8_t* k_chars;
+  const uint8_t* v_def; const int64_t* v_offs; const uint8_t* v_chars;
+  int64_t row_tag;
 };
 
 // Rows whose stats the skipping kernel reads: a decoded string column (row_def / offs / chars)

@@ -36,6 +36,7 @@ void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
 void launch_stats_eval(const StatsRows&, const DSkipProg&, uint8_t*, DState*, hipStream_t);
+void launch_part_eval(const MapRows&, const DPartProg&, uint8_t*, DState*, hipStream_t);
 void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
@@ -303,7 +304,7 @@ struct KTimer {
   const char* names[K] = {"k_page_headers", "unused", "k_tile_count", "k_tile_scan",
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
-                          "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", nullptr,
+                          "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", "k_part_eval",
                           nullptr};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
@@ -1302,6 +1303,12 @@ struct dk_replay {
   DSkipProg skip{};
   DBuf d_tstats_chars, d_tstats_off, d_tstats_len;
   std::vector<StatsRows> ck_stats;      // per checkpoint file (n = 0: no stats column)
+  // partition pruning (dk_replay_set_partition_filter): program + partitionValues maps
+  bool has_part = false;
+  DPartProg part{};
+  MapRows tail_maps{};
+  std::vector<MapRows> ck_maps;         // per checkpoint file (n = 0: no partitionValues leaves)
+  std::vector<std::unique_ptr<DBuf>> map_bufs;
   std::vector<std::unique_ptr<DBuf>> d_csel;   // per checkpoint file
   std::vector<ProbeCols> probe;
   uint64_t mask = 0;
@@ -1396,6 +1403,50 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
       r->probe.push_back(pc);
     }
   }
+  // partitionValues maps for partition pruning: the tail's (rows mapped from add actions) and the
+  // checkpoint's decoded key / value leaves
+  auto up = [&](const void* src, size_t n) -> void* {
+    r->map_bufs.emplace_back(new DBuf());
+    if (upload(*r->map_bufs.back(), src, n, s)) return nullptr;
+    return r->map_bufs.back()->p;
+  };
+  if (tail) {
+    const CB& kc = tail->col[JL_PVK];
+    const CB& vc = tail->col[JL_PVV];
+    std::vector<int64_t> arow(na);
+    for (size_t i = 0; i < na; i++) arow[i] = r->acts[i].kind == JA_ADD ? r->act_row[i] : -1;
+    MapRows M{};
+    M.n = (int64_t)na;
+    M.act_row = (const int64_t*)up(arow.data(), arow.size() * 8);
+    M.row_def = (const uint8_t*)up(kc.row_def.data(), kc.row_def.size());
+    M.rep_def = kc.rep_def; M.v_max_def = vc.max_def;
+    M.row_offs = (const int64_t*)up(kc.row_offs.data(), kc.row_offs.size() * 8);
+    M.k_offs = (const int64_t*)up(kc.offs.data(), kc.offs.size() * 8);
+    M.k_chars = (const uint8_t*)up(kc.chars.data(), kc.chars.size());
+    M.v_def = (const uint8_t*)up(vc.entry_def.data(), vc.entry_def.size());
+    M.v_offs = (const int64_t*)up(vc.offs.data(), vc.offs.size() * 8);
+    M.v_chars = (const uint8_t*)up(vc.chars.data(), vc.chars.size());
+    M.row_tag = -1000000000000ll;
+    if (!M.act_row || !M.row_def || !M.row_offs || !M.k_offs || !M.k_chars || !M.v_def || !M.v_offs || !M.v_chars)
+      return 1;
+    r->tail_maps = M;
+  }
+  if (ckpt) {
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      MapRows M{};
+      const DColumn* kc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.key");
+      const DColumn* vc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.value");
+      if (kc && vc && kc->row_offs && kc->offs && vc->entry_def && vc->offs) {
+        M.n = ckpt->files[fi].num_rows;
+        M.row_def = kc->row_def; M.rep_def = kc->rep_def; M.v_max_def = vc->max_def;
+        M.row_offs = kc->row_offs; M.k_offs = kc->offs; M.k_chars = kc->chars;
+        M.v_def = vc->entry_def; M.v_offs = vc->offs; M.v_chars = vc->chars;
+      } else {                  // no map entry anywhere (or no map leaf): every field is null
+        M.n = ckpt->files[fi].num_rows;
+      }
+      r->ck_maps.push_back(M);
+    }
+  }
   // stats strings for data skipping: the tail's per action (adds only), the checkpoint's column
   if (tail && tail->with_stats) {
     const CB& sc = tail->col[JL_STATS];
@@ -1459,6 +1510,42 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   return 0;
 }
 
+extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_program* prog) {
+  static_assert(sizeof(dk_part_program) == sizeof(DPartProg), "dk_part_program layout");
+  if (!r) return fail("null replay");
+  if (!prog) { r->has_part = false; return 0; }
+  DPartProg P;
+  memcpy(&P, prog, sizeof P);
+  if (P.n_fields < 0 || P.n_fields > PP_MAX_FIELDS || P.n_ops <= 0 || P.n_ops > PP_MAX_OPS)
+    return fail("dk_replay_set_partition_filter: bad program size");
+  for (int f = 0; f < P.n_fields; f++)
+    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_STRING || P.name_off[f] < 0 || P.name_len[f] < 0 ||
+        P.name_off[f] + P.name_len[f] > PP_POOL)
+      return fail("dk_replay_set_partition_filter: bad field");
+  int depth = 0;
+  for (int k = 0; k < P.n_ops; k++) {
+    const int op = P.op[k];
+    if (op == PO_FIELD) { if (P.arg[k] < 0 || P.arg[k] >= P.n_fields) return fail("dk_replay_set_partition_filter: bad field ref"); depth++; }
+    else if (op == PO_LIT_INT || op == PO_LIT_NULL) depth++;
+    else if (op == PO_LIT_STR) {
+      if (P.lit[k] < 0 || P.arg[k] < 0 || P.lit[k] + P.arg[k] > PP_POOL) return fail("dk_replay_set_partition_filter: bad literal");
+      depth++;
+    } else if ((op >= PO_LT && op <= PO_NSEQ) || op == PO_AND || op == PO_OR) {
+      if (depth < 2) return fail("dk_replay_set_partition_filter: stack underflow");
+      depth--;
+    } else if (op == PO_ISNULL || op == PO_ISNOTNULL || op == PO_NOT) {
+      if (depth < 1) return fail("dk_replay_set_partition_filter: stack underflow");
+    } else {
+      return fail("dk_replay_set_partition_filter: bad opcode");
+    }
+    if (depth > 16) return fail("dk_replay_set_partition_filter: program too deep");
+  }
+  if (depth != 1) return fail("dk_replay_set_partition_filter: program must leave one value");
+  r->part = P;
+  r->has_part = true;
+  return 0;
+}
+
 static int replay_launch(dk_replay* r) {
   hipStream_t s = r->eng->stream;
   KTimer& T = r->timer;
@@ -1476,6 +1563,10 @@ static int replay_launch(dk_replay* r) {
   { KTimer::Scope sc(&T, 8, s); launch_table_insert(A, na, S, r->mask, s); }
   { KTimer::Scope sc(&T, 9, s); launch_table_update(A, na, S, r->mask, r->d_canon.as<uint8_t>(), st, s); }
   { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->d_jsel.as<uint8_t>(), st, s); }
+  if (r->has_part && na) {                 // partition pruning on the tail's adds (before skipping)
+    KTimer::Scope sc(&T, 18, s);
+    launch_part_eval(r->tail_maps, r->part, r->d_jsel.as<uint8_t>(), st, s);
+  }
   if (r->has_skip && na) {                 // data skipping on the tail's selected adds
     KTimer::Scope sc(&T, 17, s);
     StatsRows R{};
@@ -1497,6 +1588,11 @@ static int replay_launch(dk_replay* r) {
       launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, kd.hs.final_(kd.n),
                    r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
     }
+    if (r->has_part)                        // partition pruning on the checkpoint files' rows
+      for (size_t fi = 0; fi < r->ck_maps.size(); fi++) {
+        KTimer::Scope sc(&T, 18, s);
+        launch_part_eval(r->ck_maps[fi], r->part, r->d_csel[fi]->as<uint8_t>(), st, s);
+      }
     if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
       for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
         KTimer::Scope sc(&T, 17, s);
@@ -1524,6 +1620,13 @@ extern "C" int dk_replay_sync(dk_replay* r) {
       r->seed++;
       if (replay_launch(r)) return 1;
       continue;
+    }
+    if (r->h_state.err_flags & E_PART) {
+      const long long row = r->h_state.err_row;
+      return fail(std::string("Evaluating the partition expression: java.lang.NumberFormatException for a partition "
+                              "value of ") +
+                  (row < 0 ? "commit-tail action " + std::to_string(row + 1000000000000ll)
+                           : "checkpoint row " + std::to_string(row)));
     }
     if (r->h_state.err_flags & E_STATS) {
       const long long row = r->h_state.err_row;

@@ -1659,6 +1659,144 @@ __global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg 
 }
 
 // --------------------------------------------------------------------------------------------
+// Partition pruning (ScanImpl.applyPartitionPruning, ScanImpl.java:247-294). One lane per row of the
+// scan-file batch. Each program field is element_at(add.partitionValues, physical name) -- null when
+// the map or the key is absent (the first entry with the key; keys are unique in valid logs) --
+// deserialized as PartitionValueEvaluator does (kernel-defaults/.../expressions/
+// PartitionValueEvaluator.java:50-90: Long/Integer/Short/Byte.parseX; a malformed value fails the
+// scan). Like DefaultExpressionEvaluator, every row with a map is evaluated, selected or not (AND and
+// OR do not short-circuit, DefaultExpressionEvaluator.java:384-436), so a malformed value anywhere in
+// the batch is an error. Comparators are null when a side is null; strings compare as unsigned
+// bytes, then length (DefaultExpressionUtils.java:39-56); the row stays selected iff the predicate is
+// TRUE (DefaultPredicateEvaluator: (sel = true) AND predicate, null -> dropped).
+// --------------------------------------------------------------------------------------------
+__device__ bool java_parse_long(const uint8_t* s, int32_t n, long long lo, long long hi, long long* out) {
+  if (n <= 0) return false;
+  int32_t i = 0;
+  bool neg = false;
+  if (s[0] == '-' || s[0] == '+') {
+    neg = s[0] == '-';
+    i = 1;
+    if (n == 1) return false;
+  }
+  const unsigned long long lim = neg ? (unsigned long long)(-(lo + 1)) + 1ull : (unsigned long long)hi;
+  unsigned long long mag = 0;
+  for (; i < n; i++) {
+    const uint32_t d = (uint32_t)s[i] - (uint32_t)'0';
+    if (d > 9) return false;
+    if (mag > (lim - d) / 10) return false;            // outside the type's range
+    mag = mag * 10 + d;
+  }
+  *out = neg ? (long long)(0ull - mag) : (long long)mag;
+  return true;
+}
+
+__device__ __forceinline__ int bytes_cmp(const uint8_t* a, int32_t na, const uint8_t* b, int32_t nb) {
+  const int32_t m = na < nb ? na : nb;
+  for (int32_t i = 0; i < m; i++)
+    if (a[i] != b[i]) return (int)a[i] - (int)b[i];
+  return na < nb ? -1 : na > nb ? 1 : 0;
+}
+
+struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean
+  int32_t kind, len;
+  long long v;
+  const uint8_t* p;
+};
+
+// 1 true, 0 false, -1 null; *err on a malformed partition value
+__device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bool* err) {
+  PVal f[PP_MAX_FIELDS];
+  for (int k = 0; k < P.n_fields && k < PP_MAX_FIELDS; k++) f[k].kind = 0;
+  if (M.row_offs && M.row_def[row] >= M.rep_def - 1) {   // the map is not null (and has entries somewhere)
+    const int64_t e0 = M.row_offs[row], e1 = M.row_offs[row + 1];
+    for (int k = 0; k < P.n_fields && k < PP_MAX_FIELDS; k++) {
+      const uint8_t* nm = (const uint8_t*)P.pool + P.name_off[k];
+      for (int64_t e = e0; e < e1; e++) {
+        const int64_t ko = M.k_offs[e];
+        if (bytes_cmp(M.k_chars + ko, (int32_t)(M.k_offs[e + 1] - ko), nm, P.name_len[k]) != 0) continue;
+        if (M.v_def[e] >= M.v_max_def) {
+          const uint8_t* vp = M.v_chars + M.v_offs[e];
+          const int32_t vl = (int32_t)(M.v_offs[e + 1] - M.v_offs[e]);
+          const int ty = P.field_type[k];
+          if (ty == PT_STRING) {
+            f[k].kind = 2; f[k].p = vp; f[k].len = vl;
+          } else {
+            const long long lo = ty == PT_LONG ? (-9223372036854775807ll - 1) : ty == PT_INT ? -2147483648ll
+                               : ty == PT_SHORT ? -32768 : -128;
+            const long long hi = ty == PT_LONG ? 9223372036854775807ll : ty == PT_INT ? 2147483647ll
+                               : ty == PT_SHORT ? 32767 : 127;
+            if (!java_parse_long(vp, vl, lo, hi, &f[k].v)) { *err = true; return -1; }
+            f[k].kind = 1;
+          }
+        }
+        break;
+      }
+    }
+  }
+  PVal st[16];
+  int sp = 0;
+  for (int i = 0; i < P.n_ops && i < PP_MAX_OPS; i++) {
+    const int op = P.op[i];
+    if (op == PO_FIELD) {
+      st[sp++] = f[P.arg[i]];
+    } else if (op == PO_LIT_INT) {
+      st[sp].kind = 1; st[sp].v = P.lit[i]; sp++;
+    } else if (op == PO_LIT_STR) {
+      st[sp].kind = 2; st[sp].p = (const uint8_t*)P.pool + P.lit[i]; st[sp].len = P.arg[i]; sp++;
+    } else if (op == PO_LIT_NULL) {
+      st[sp++].kind = 0;
+    } else if (op >= PO_LT && op <= PO_NSEQ) {
+      const PVal b = st[--sp];
+      const PVal a = st[--sp];
+      PVal r;
+      r.kind = 3;
+      if (op == PO_NSEQ && (a.kind == 0 || b.kind == 0)) {
+        r.v = a.kind == 0 && b.kind == 0;
+      } else if (a.kind == 0 || b.kind == 0) {
+        r.kind = 0;
+      } else {
+        const int c = a.kind == 2 ? bytes_cmp(a.p, a.len, b.p, b.len) : (a.v < b.v ? -1 : a.v > b.v ? 1 : 0);
+        r.v = op == PO_LT ? c < 0 : op == PO_LE ? c <= 0 : op == PO_GT ? c > 0 : op == PO_GE ? c >= 0 : c == 0;
+      }
+      st[sp++] = r;
+    } else if (op == PO_ISNULL || op == PO_ISNOTNULL) {
+      PVal& a = st[sp - 1];
+      const bool isnull = a.kind == 0;
+      a.kind = 3; a.v = op == PO_ISNULL ? isnull : !isnull;
+    } else if (op == PO_NOT) {
+      PVal& a = st[sp - 1];
+      if (a.kind != 0) a.v = !a.v;
+    } else {                                             // AND / OR, Kleene
+      const PVal b = st[--sp];
+      const PVal a = st[--sp];
+      const int av = a.kind == 0 ? -1 : (int)a.v, bv = b.kind == 0 ? -1 : (int)b.v;
+      int rv;
+      if (op == PO_AND) rv = (av == 0 || bv == 0) ? 0 : (av == 1 && bv == 1) ? 1 : -1;
+      else rv = (av == 1 || bv == 1) ? 1 : (av == 0 && bv == 0) ? 0 : -1;
+      PVal r;
+      r.kind = rv < 0 ? 0 : 3; r.v = rv > 0;
+      st[sp++] = r;
+    }
+  }
+  if (sp != 1 || st[0].kind == 0) return -1;
+  return st[0].v ? 1 : 0;
+}
+
+__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg P, uint8_t* __restrict__ sel,
+                                                  DState* __restrict__ st) {
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < M.n;
+       r += (long long)gridDim.x * blockDim.x) {
+    const long long row = M.act_row ? M.act_row[r] : r;
+    if (row < 0) continue;                              // not an add action
+    bool err = false;
+    const int res = part_eval(P, M, row, &err);
+    if (err) { set_err(st, E_PART, M.row_tag + r, 0); continue; }
+    if (res != 1 && sel[r]) sel[r] = 0;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
 // Commit tail: canonical keys, probe-table build, JSON selection
 // --------------------------------------------------------------------------------------------
 
@@ -2025,5 +2163,14 @@ void launch_stats_eval(const StatsRows& R, const DSkipProg& P, uint8_t* sel, DSt
   const long long want = (R.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
   hipLaunchKernelGGL(k_stats_eval, dim3(grid), dim3(NT), 0, s, R, P, sel, st);
+}
+}  // namespace dk
+
+namespace dk {
+void launch_part_eval(const MapRows& M, const DPartProg& P, uint8_t* sel, DState* st, hipStream_t s) {
+  if (M.n <= 0) return;
+  const long long want = (M.n + NT - 1) / NT;
+  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
+  hipLaunchKernelGGL(k_part_eval, dim3(grid), dim3(NT), 0, s, M, P, sel, st);
 }
 }  // namespace dk

@@ -22,7 +22,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import Column, DkError, check, dk_column, dk_config, dk_skip_program, lib
+from ._lib import Column, DkError, check, dk_column, dk_config, dk_part_program, dk_skip_program, lib
 
 ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
               "add.size", "add.modificationTime", "add.dataChange",
@@ -367,8 +367,9 @@ class ScanBuilder:
         self.predicate = None
 
     def withFilter(self, predicate):
-        """ScanBuilderImpl.withFilter (internal/ScanBuilderImpl.java:61-67). The data part of the
-        filter becomes a GPU data-skipping program (K11); partition pruning is not in this build."""
+        """ScanBuilderImpl.withFilter (internal/ScanBuilderImpl.java:61-67). The partition part of the
+        filter becomes a GPU partition-pruning program (delta_amd/partitions.py), the data part a GPU
+        data-skipping program (K11, delta_amd/skipping.py)."""
         if self.predicate is not None:
             raise ValueError("There already exists a filter in current builder")
         self.predicate = predicate
@@ -413,15 +414,18 @@ class GpuScan:
         self.shard = shard
         self.predicate = predicate
         self.skipping = None          # (planner node, paths, types) when a data-skipping filter applies
+        self.partition = None
         self.partition_filter, self.data_filter = None, None
         if predicate is not None:
             from . import skipping as sk
             md = snapshot.metadata or {}
             parts = md.get("partitionColumns") or []
             self.partition_filter, self.data_filter = sk.split_filters(predicate, parts)
+            self.partition = None     # compiled partition-pruning program (delta_amd/partitions.py)
             if self.partition_filter is not None:
-                raise DkError("partition pruning (filter %r) is not supported by this engine build"
-                              % (self.partition_filter,))
+                from . import partitions as pp
+                self.partition = pp.compile_program(
+                    self.partition_filter, pp.partition_fields(md["schemaString"], parts))
             if self.data_filter is not None:
                 leaves = sk.data_schema_leaves(md["schemaString"], parts)
                 node = sk.construct(self.data_filter, leaves)
@@ -456,6 +460,10 @@ class GpuScan:
         self._rh = C.c_void_p()
         check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
                                      C.byref(self._rh)))
+        if self.partition is not None:
+            from . import partitions as pp
+            pprog = pp.pack(self.partition, dk_part_program)
+            check(lib().dk_replay_set_partition_filter(self._rh, C.byref(pprog)))
         if self.skipping is not None:
             from . import skipping as sk
             prog = sk.pack(self.skipping[1:], dk_skip_program)

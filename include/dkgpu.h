@@ -110,6 +110,24 @@ typedef struct dk_skip_program {
   int64_t lit[64];
 } dk_skip_program;
 
+/* Partition-pruning program (ScanImpl.applyPartitionPruning, ScanImpl.java:247-294): the predicate on
+ * partition columns, rewritten over the scan file's partitionValues map
+ * (PartitionUtils.rewritePartitionPredicateOnScanFileSchema, PartitionUtils.java:324-358), in postfix.
+ * A row stays selected iff the predicate is TRUE (null and false drop it). */
+typedef struct dk_part_program {
+  int32_t n_fields;                /* <= 8 partition columns                                      */
+  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string                 */
+  int32_t name_off[8];             /* physical column name (map key): offset / length in pool      */
+  int32_t name_len[8];
+  int32_t n_ops;                   /* <= 64                                                       */
+  int32_t op[64];                  /* 0 FIELD(arg) 1 LIT_INT(lit) 2 LIT_STR(pool[lit], arg bytes) 3 LIT_NULL
+                                      4 < 5 <= 6 > 7 >= 8 = 9 IS NOT DISTINCT FROM 10 IS_NULL
+                                      11 IS_NOT_NULL 12 NOT 13 AND 14 OR                          */
+  int32_t arg[64];
+  int64_t lit[64];
+  char pool[1024];
+} dk_part_program;
+
 /* ---- Replay: reconcile the tail and the checkpoint files on the GPU ----
  * ckpt may be NULL (no checkpoint). Checkpoint files are given in replay order (multi-part:
  * descending part number, LogSegment.java:171-177). */
@@ -117,6 +135,9 @@ int  dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_rep
 /* install (prog != NULL) or clear the data-skipping program applied after reconciliation; the
  * tail must have been parsed with stats and the checkpoint projection must include add.stats */
 int  dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog);
+/* install (prog != NULL) or clear the partition-pruning program, applied before data skipping; the
+ * checkpoint projection must include add.partitionValues */
+int  dk_replay_set_partition_filter(dk_replay* r, const dk_part_program* prog);
 int  dk_replay_run(dk_replay* r);                      /* async: key build, probe, decode */
 int  dk_replay_sync(dk_replay* r);
 /* counters: addFilesSeen, addFilesSeenFromDeltaFiles, activeAddFiles, duplicateAddFiles,

@@ -1,0 +1,86 @@
+"""CPU ORACLE (test infrastructure only) for partition pruning: ScanImpl.applyPartitionPruning
+(kernel-api/.../internal/ScanImpl.java:247-294) restated on the predicate tree itself.
+
+  PartitionUtils.rewritePartitionPredicateOnScanFileSchema (util/PartitionUtils.java:324-358):
+      a partition column becomes element_at(add.partitionValues, physical name), deserialized by
+      PartitionValueEvaluator (kernel-defaults/.../expressions/PartitionValueEvaluator.java:50-90:
+      Long/Integer/Short/Byte.parseX -- a malformed value fails the scan) unless it is a string
+  DefaultExpressionEvaluator: comparators are null if a side is null (IS NOT DISTINCT FROM is
+      null-safe), AND/OR/NOT are Kleene and are evaluated on every row of the batch; strings compare
+      as unsigned UTF-8 bytes, then length (DefaultExpressionUtils.java:39-56)
+  DefaultPredicateEvaluator: selection = (selection = true) AND predicate; null drops the row
+Nothing here is used by the product path.
+"""
+from __future__ import annotations
+
+import re
+
+RANGES = {"long": (-(1 << 63), (1 << 63) - 1), "integer": (-(1 << 31), (1 << 31) - 1),
+          "short": (-(1 << 15), (1 << 15) - 1), "byte": (-(1 << 7), (1 << 7) - 1)}
+_INT = re.compile(rb"^[+-]?[0-9]+$")
+
+
+class PartitionValueError(RuntimeError):
+    pass
+
+
+def _b(x):
+    return x if isinstance(x, bytes) else str(x).encode("utf-8")
+
+
+def element_at(pv, key: bytes):
+    """pv: None (null map) or list of (key, value) with bytes/str items; first match wins."""
+    if pv is None:
+        return None
+    for k, v in pv:
+        if _b(k) == key:
+            return None if v is None else _b(v)
+    return None
+
+
+def deserialize(v, typ):
+    if v is None or typ == "string":
+        return v
+    if not _INT.match(v):
+        raise PartitionValueError("For input string: %r" % v)
+    x = int(v)
+    lo, hi = RANGES[typ]
+    if not lo <= x <= hi:
+        raise PartitionValueError("Value out of range: %r" % v)
+    return x
+
+
+def evaluate(node, pv, fields):
+    """True / False / None. `node` is a delta_amd.expressions node; fields: lower name -> (type, phys)."""
+    kind = type(node).__name__
+    if kind == "Column":
+        t, phys = fields[node.names[0].lower()]
+        return deserialize(element_at(pv, phys.encode("utf-8")), t)
+    if kind == "Literal":
+        return None if node.value is None else (_b(node.value) if node.type == "string" else node.value)
+    n = node.name.upper()
+    c = node.children
+    if n in ("AND", "OR"):
+        a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
+        if n == "AND":
+            return False if (a is False or b is False) else (True if (a is True and b is True) else None)
+        return True if (a is True or b is True) else (False if (a is False and b is False) else None)
+    if n == "NOT":
+        a = evaluate(c[0], pv, fields)
+        return None if a is None else (not a)
+    if n in ("IS_NULL", "IS_NOT_NULL"):
+        a = evaluate(c[0], pv, fields)
+        return (a is None) if n == "IS_NULL" else (a is not None)
+    a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
+    if n == "IS NOT DISTINCT FROM":
+        if a is None or b is None:
+            return a is None and b is None
+        return a == b
+    if a is None or b is None:
+        return None
+    return {"<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b, "=": a == b}[n]
+
+
+def json_map(add: dict):
+    pv = add.get("partitionValues")
+    return None if pv is None else list(pv.items()) if isinstance(pv, dict) else pv

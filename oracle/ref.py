@@ -540,7 +540,8 @@ def probe_checkpoint(cols, n_rows, keyset, counters: Counters):
     return sel
 
 
-def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, skipping=None) -> ReplayResult:
+def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, skipping=None,
+           partition=None) -> ReplayResult:
     """getLatestSnapshot + getScanFiles restated; returns the ordered active scan files + counters.
 
     shard=(world, rank): reconcile only the checkpoint files whose replay-order index i has
@@ -548,7 +549,9 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
     sidecars); res.tail_counters / res.ckpt_counters hold the two parts of the counters.
 
     skipping=(predicate node, {stats path: type}): ScanImpl.applyDataSkipping on the reconciled
-    rows (oracle/skipping.py); implies with_stats, leaves the counters unchanged."""
+    rows (oracle/skipping.py); implies with_stats, leaves the counters unchanged.
+    partition=(predicate, {lower name: (type, physical name)}): ScanImpl.applyPartitionPruning
+    (oracle/partitions.py), applied before data skipping, on every add row of every batch."""
     if skipping is not None:
         with_stats = True
     world, rank = shard if shard else (1, 0)
@@ -560,6 +563,7 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
     tomb = set()
     added = set()
     files = seg.all_files_reversed()
+    tail_adds = []          # every add row of the tail's batches (partition filters see them all)
     queue = list(files)
     L = lib()
     keyset = None
@@ -577,6 +581,7 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                     a = row["add"]
                     if a is None:
                         continue
+                    tail_adds.append(a)
                     c.addFilesSeen += 1
                     c.addFilesSeenFromDeltaFiles += 1
                     k = json_key(a)
@@ -614,6 +619,7 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                         a = row["add"]
                         if a is None or not mine:
                             continue
+                        tail_adds.append(a)
                         cc.addFilesSeen += 1
                         k = json_key(a)
                         if k in added:
@@ -641,6 +647,19 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
     if keyset is not None:
         L.dkr_keyset_free(keyset)
     res.counters = Counters(*[a + b for a, b in zip(c.as_tuple(), cc.as_tuple())])
+    if partition is not None:
+        from . import partitions as pp
+        pred, fields = partition
+        keep = {id(a): pp.evaluate(pred, pp.json_map(a), fields) is True for a in tail_adds}
+        res.json_rows = [a for a in res.json_rows if keep[id(a)]]
+        for b in res.checkpoint:
+            kc, vc, pc = b.cols.get(ADD_LEAVES[1]), b.cols.get(ADD_LEAVES[2]), b.cols.get("add.path")
+            for i in range(b.n_rows):
+                if pc is None or pc.row_def[i] < 1:
+                    continue                    # no add in this row: its map is null
+                pv = _map_at(kc, vc, i) if kc is not None else None
+                if pp.evaluate(pred, pv, fields) is not True:
+                    b.selected[i] = False
     if skipping is not None:
         from . import skipping as sk
         node, types = skipping

@@ -1,0 +1,222 @@
+"""Partition pruning (delta_amd/partitions.py planner, k_part_eval on the GPU, oracle/partitions.py).
+
+The oracle is cross-checked against an independent filter over the reference golden table
+dv-partitioned-with-checkpoint's expected scan files (tests/golden/expected.json, integer partition
+column `part`, a checkpoint plus a commit tail), then the GPU path is compared with the oracle there,
+on a synthetic table with a string partition column, together with data skipping, and on
+hand-written logs with null, missing, malformed and out-of-range partition values.
+"""
+import json
+import os
+
+import pytest
+
+from delta_amd import partitions as pp
+from delta_amd import synth
+from delta_amd.expressions import And, Column, Literal, Or, Predicate
+from tests.golden_util import TABLES, load_expected
+from tests.test_skipping import oracle_skipping, table_metadata
+
+DV_PART = os.path.join(TABLES, "dv-partitioned-with-checkpoint")
+
+
+def col(n):
+    return Column(n)
+
+
+def cmp(op, c, v):
+    return Predicate(op, c, v)
+
+
+def fields_of(root):
+    schema, parts = table_metadata(root)
+    return pp.partition_fields(schema, parts)
+
+
+def oracle_files(root, predicate, bs=1024):
+    from delta_amd import skipping as sk
+    from oracle import ref
+    schema, parts = table_metadata(root)
+    pf, df = sk.split_filters(predicate, parts)
+    part = (pf, pp.partition_fields(schema, parts)) if pf is not None else None
+    skip = oracle_skipping(root, df) if df is not None else None
+    r = ref.replay(root, json_batch_size=bs, with_stats=skip is not None, skipping=skip, partition=part)
+    return r.scan_files(), r.counters.as_tuple()
+
+
+# ---------------------------------------------------------------- planner (host logic, CPU)
+def test_partition_fields_and_compile():
+    schema = json.dumps({"type": "struct", "fields": [
+        {"name": "P", "type": "integer", "metadata": {"delta.columnMapping.physicalName": "col-p"}},
+        {"name": "s", "type": "string", "metadata": {}}, {"name": "d", "type": "date", "metadata": {}},
+        {"name": "x", "type": "long", "metadata": {}}]})
+    f = pp.partition_fields(schema, ["p", "S", "d"])
+    assert f == {"p": ("integer", "col-p"), "s": ("string", "s"), "d": ("date", "d")}
+    flist, ops, pool = pp.compile_program(And(cmp(">=", col("P"), Literal.ofInt(3)),
+                                              cmp("=", col("s"), Literal.ofString("a b"))), f)
+    assert [pool[o:o + n] for o, n, _ in flist] == [b"col-p", b"s"] and [t for _, _, t in flist] == [1, 4]
+    assert [o[0] for o in ops] == [pp.PO_FIELD, pp.PO_LIT_INT, pp.PO_GE, pp.PO_FIELD, pp.PO_LIT_STR, pp.PO_EQ,
+                                   pp.PO_AND]
+    for bad in (cmp("=", col("d"), Literal(1, "date")), cmp("=", col("s"), Literal.ofInt(1)),
+                Predicate("STARTS_WITH", col("s"), Literal.ofString("a"))):
+        with pytest.raises(pp.UnsupportedPartitionFilter):
+            pp.compile_program(bad, f)
+    with pytest.raises(ValueError):
+        pp.compile_program(cmp("=", col("zz"), Literal.ofInt(1)), f)
+
+
+def test_pack_layout():
+    import ctypes
+    from delta_amd._lib import dk_part_program
+    assert ctypes.sizeof(dk_part_program) == 4 + 32 * 3 + 4 + 256 + 256 + 512 + 1024
+    f = {"p": ("integer", "p")}
+    prog = pp.pack(pp.compile_program(Predicate("IS_NULL", col("p")), f), dk_part_program)
+    assert prog.n_fields == 1 and prog.n_ops == 2 and bytes(prog.pool)[:1] == b"p"
+
+
+# ---------------------------------------------------------------- oracle (cross-checked)
+PART_PREDICATES = [
+    cmp(">=", col("part"), Literal.ofInt(7)),
+    cmp("=", col("part"), Literal.ofInt(3)),
+    Or(cmp("<", col("part"), Literal.ofInt(2)), cmp(">", col("part"), Literal.ofLong(8))),
+    Predicate("NOT", cmp("<", col("part"), Literal.ofInt(5))),
+    Predicate("IS_NULL", col("part")),
+    Predicate("IS_NOT_NULL", col("part")),
+    cmp("IS NOT DISTINCT FROM", col("part"), Literal.ofNull("integer")),
+    cmp("IS NOT DISTINCT FROM", col("PART"), Literal.ofInt(4)),
+    cmp("=", col("part"), Literal.ofNull("integer")),
+]
+
+
+def _pv_part(row):
+    """`part` of an expected.json scan-file row (index 1 = partitionValues pairs)."""
+    for k, v in row[1] or []:
+        if (k["b"] if isinstance(k, dict) else k) == "part":
+            return None if v is None else int(v["b"] if isinstance(v, dict) else v)
+    return None
+
+
+def _reference_filter(pred, part):
+    """The same predicates written out directly over one integer value (None = null)."""
+    n = pred.name.upper()
+    c = pred.children
+    if n == "OR":
+        a, b = _reference_filter(c[0], part), _reference_filter(c[1], part)
+        return True if (a or b) else (False if (a is False and b is False) else None)
+    if n == "NOT":
+        a = _reference_filter(c[0], part)
+        return None if a is None else not a
+    if n == "IS_NULL":
+        return part is None
+    if n == "IS_NOT_NULL":
+        return part is not None
+    lit = c[1].value
+    if n == "IS NOT DISTINCT FROM":
+        return part == lit
+    if part is None or lit is None:
+        return None
+    return {"<": part < lit, ">": part > lit, ">=": part >= lit, "=": part == lit}[n]
+
+
+@pytest.mark.parametrize("pred", PART_PREDICATES)
+def test_oracle_partition_pruning_golden(pred):
+    rows = load_expected()["dv-partitioned-with-checkpoint"]["1024-0"]["rows"]
+    want = sorted(r[0]["b"] for r in rows if _reference_filter(pred, _pv_part(r)) is True)
+    got, counters = oracle_files(DV_PART, pred)
+    assert sorted(r[0].decode() for r in got) == want
+    assert list(counters) == load_expected()["dv-partitioned-with-checkpoint"]["1024-0"]["counters"]
+
+
+def _write_pv_table(root, pvs, schema_type="integer"):
+    log = os.path.join(root, "_delta_log")
+    os.makedirs(log)
+    schema = {"type": "struct", "fields": [{"name": "p", "type": schema_type, "nullable": True, "metadata": {}},
+                                           {"name": "id", "type": "long", "nullable": True, "metadata": {}}]}
+    with open(os.path.join(log, "%020d.json" % 0), "w") as f:
+        f.write(json.dumps({"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}) + "\n")
+        f.write(json.dumps({"metaData": {"id": "t", "format": {"provider": "parquet", "options": {}},
+                                         "schemaString": json.dumps(schema), "partitionColumns": ["p"],
+                                         "configuration": {}, "createdTime": 0}}) + "\n")
+        for i, pv in enumerate(pvs):
+            f.write(json.dumps({"add": {"path": "p%d.parquet" % i, "partitionValues": pv, "size": 1,
+                                        "modificationTime": 0, "dataChange": True}}) + "\n")
+
+
+EDGE_PVS = [{"p": "5"}, {"p": None}, {}, {"p": "+7"}, {"p": "-3"}, {"p": "0005"}, {"q": "5"}, {"p": "2147483647"}]
+
+
+def test_oracle_edge_values(tmp_path):
+    root = str(tmp_path / "t")
+    _write_pv_table(root, EDGE_PVS)
+    got = lambda p: sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0])   # noqa: E731
+    assert got(cmp("=", col("p"), Literal.ofInt(5))) == [0, 5]
+    assert got(Predicate("IS_NULL", col("p"))) == [1, 2, 6]
+    assert got(cmp(">", col("p"), Literal.ofInt(0))) == [0, 3, 5, 7]
+    assert got(Predicate("NOT", cmp(">", col("p"), Literal.ofInt(0)))) == [4]
+
+
+@pytest.mark.parametrize("bad", ["x", "", "1.0", "2147483648", " 1", "0x10"])
+def test_oracle_malformed_value_raises(tmp_path, bad):
+    from oracle import partitions as opp
+    root = str(tmp_path / "t")
+    _write_pv_table(root, [{"p": "1"}, {"p": bad}])
+    with pytest.raises(opp.PartitionValueError):
+        oracle_files(root, cmp("=", col("p"), Literal.ofInt(1)))
+
+
+# ---------------------------------------------------------------- GPU parity
+def _gpu_files(root, predicate, eng):
+    from tests.test_skipping import _gpu_files as gf
+    return gf(root, predicate, eng)
+
+
+@pytest.mark.gpu
+def test_gpu_partition_pruning_golden():
+    from delta_amd import kernel as K
+    eng = K.GpuEngine()
+    for pred in PART_PREDICATES + [And(cmp(">=", col("part"), Literal.ofInt(7)), cmp(">=", col("col1"), Literal.ofInt(0))),
+                                   And(cmp(">=", col("part"), Literal.ofInt(7)), cmp("=", col("col1"), Literal.ofInt(28)))]:
+        assert _gpu_files(DV_PART, pred, eng) == oracle_files(DV_PART, pred), pred
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_partition_pruning_synthetic(tmp_path):
+    from delta_amd import kernel as K
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=30_000, n_parts=2, n_commits=5, dv_frac=0.1,
+                                                     ckpt_removes=100, with_stats=True, pv_keys=2))
+    eng = K.GpuEngine()
+    day = Literal.ofString("2024-06-01")
+    for pred in (cmp(">=", col("date"), day), cmp("=", col("date"), Literal.ofString("2024-01-01")),
+                 Or(cmp("<", col("date"), day), Predicate("IS_NULL", col("date"))),
+                 And(cmp("<", col("date"), day), cmp(">", col("id"), Literal.ofLong(30_000_000)))):
+        g = _gpu_files(str(tmp_path), pred, eng)
+        o = oracle_files(str(tmp_path), pred)
+        assert g[1] == o[1] and len(g[0]) == len(o[0]) and g[0] == o[0], pred
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_partition_edge_values(tmp_path):
+    from delta_amd import kernel as K
+    root = str(tmp_path / "t")
+    _write_pv_table(root, EDGE_PVS)
+    eng = K.GpuEngine()
+    for pred in (cmp("=", col("p"), Literal.ofInt(5)), Predicate("IS_NULL", col("p")),
+                 cmp(">", col("p"), Literal.ofInt(0)), Predicate("NOT", cmp(">", col("p"), Literal.ofInt(0))),
+                 cmp("IS NOT DISTINCT FROM", col("p"), Literal.ofNull("integer"))):
+        assert _gpu_files(root, pred, eng) == oracle_files(root, pred), pred
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_malformed_value_raises(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    eng = K.GpuEngine()
+    for i, bad in enumerate(["x", "", "1.0", "2147483648", " 1", "0x10"]):
+        root = str(tmp_path / str(i))
+        _write_pv_table(root, [{"p": "1"}, {"p": bad}])
+        with pytest.raises(DkError, match="partition"):
+            _gpu_files(root, cmp("=", col("p"), Literal.ofInt(1)), eng)
+    eng.close()
