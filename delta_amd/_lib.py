@@ -43,6 +43,7 @@ class dk_skip_program(C.Structure):
 
 EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
+           "dk_parquet_first_row", "dk_parquet_column_rows",
            "dk_parquet_traffic", "dk_parquet_kernel_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
            "dk_replay_sync",
@@ -69,6 +70,8 @@ def lib(build_if_missing=True):
         "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),
         "dk_parquet_num_rows": (I64, [P, I32]),
         "dk_parquet_column": (C.c_int, [P, I32, I32, C.POINTER(dk_column)]),
+        "dk_parquet_first_row": (C.c_int, [P, I32, I32, I32, C.POINTER(I64)]),
+        "dk_parquet_column_rows": (C.c_int, [P, I32, I32, I64, I64, C.POINTER(dk_column)]),
         "dk_parquet_traffic": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
         "dk_parquet_kernel_traffic": (C.c_int, [P, C.c_char_p, C.POINTER(I64), C.POINTER(I64)]),
         "dk_parquet_close": (None, [P]),

@@ -6,7 +6,7 @@ namespace dk {
 
 // One column chunk (file part x projected leaf x row group).
 struct DChunk {
-  const uint8_t* file;   // device copy of the file bytes (padded)
+  const uint8_t* file;   // device copy of the file's projected chunks (padded)
   int32_t col;           // output column (DColumn index)
   int32_t phys, width, max_def, max_rep, rep_def, codec;
   int32_t dict_page;     // page index of the dictionary page, -1 if none
@@ -19,13 +19,13 @@ enum : int32_t { PS_OK = 0, PS_BAD_HEADER = 1, PS_BAD_LEVELS = 2, PS_BAD_VALUES 
                  PS_UNSUPPORTED = 4, PS_BAD_DICT = 5, PS_BAD_SNAPPY = 6 };
 
 struct DPage {
-  int64_t hdr_off;       // absolute file offset of the page header (input)
+  int64_t hdr_off;       // offset of the page header in the packed chunk image (input)
   int32_t chunk;         // DChunk index (input)
   int32_t flags;         // PF_* (input)
   // parsed header (k_page_headers)
   int32_t ptype, enc, num_values, dl_len, rl_len, csize, usize, hdr_len;
   int32_t status, is_comp;
-  int64_t data_off;      // absolute offset of the page body in the file
+  int64_t data_off;      // offset of the page body in the packed chunk image
   int64_t unc_off;       // offset into the decompression arena, -1 = read in place (input)
   // totals (k_tile_scan1 / k_tile_scan2: sums over the page's level tiles)
   int32_t n_rows, n_entries, n_values, pad;

@@ -33,6 +33,7 @@ void launch_string_copy(const DChunk*, const DPage*, int, const DColumn*, const 
 void launch_json_canon(DJsonAction*, int, const uint8_t*, uint8_t*, uint32_t, DState*, hipStream_t);
 void launch_slots_init(Slot*, uint64_t, hipStream_t);
 void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
+void launch_first_row(const uint8_t*, long long, int, unsigned long long*, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
 void launch_stats_eval(const StatsRows&, const DSkipProg&, uint8_t*, DState*, hipStream_t);
@@ -119,9 +120,17 @@ struct ColMeta {
 };
 struct RowGroupM { int64_t num_rows = 0; std::vector<ColMeta> cols; };
 struct LeafM { std::string path; int phys, type_length, max_def, max_rep, rep_def; };
+// A checkpoint file as the decoder sees it: the footer, plus only the byte ranges of the
+// projected column chunks (and their offset indexes), read with pread -- parquet-mr's column
+// projection (ParquetFileReader reads the chunks of the requested schema only). `bytes` holds the
+// packed chunks; `spans` maps file offsets to positions in it.
+struct Span { int64_t file_off, len, packed_off; };
 struct FileM {
   std::string path;
-  std::vector<uint8_t> bytes;
+  int64_t size = 0;
+  std::vector<uint8_t> footer;            // the FileMetaData bytes
+  std::vector<uint8_t> bytes;             // packed column-chunk / offset-index bytes
+  std::vector<Span> spans;
   int64_t num_rows = 0;
   std::vector<SchemaEl> schema;
   std::vector<LeafM> leaves;
@@ -152,14 +161,69 @@ static void parse_col_meta(TReader& t, ColMeta& m) {
   }
 }
 
-static int parse_footer(FileM& f) {
-  const std::vector<uint8_t>& b = f.bytes;
-  if (b.size() < 12 || memcmp(b.data(), "PAR1", 4) || memcmp(b.data() + b.size() - 4, "PAR1", 4))
+// bytes [off, off+len) of the file, when they were read (a projected chunk or offset index)
+static const uint8_t* span_ptr(const FileM& f, int64_t off, int64_t len) {
+  for (const Span& sp : f.spans)
+    if (off >= sp.file_off && off + len <= sp.file_off + sp.len) return f.bytes.data() + sp.packed_off + (off - sp.file_off);
+  return nullptr;
+}
+
+static int read_footer(FileM& f) {
+  FILE* fp = fopen(f.path.c_str(), "rb");
+  if (!fp) return fail("Error reading Parquet file: " + f.path + " (cannot open)");
+  fseek(fp, 0, SEEK_END);
+  f.size = ftell(fp);
+  uint8_t head[4] = {0}, tail[8] = {0};
+  bool ok = f.size >= 12 && fseek(fp, 0, SEEK_SET) == 0 && fread(head, 1, 4, fp) == 4 &&
+            fseek(fp, f.size - 8, SEEK_SET) == 0 && fread(tail, 1, 8, fp) == 8;
+  if (!ok || memcmp(head, "PAR1", 4) || memcmp(tail + 4, "PAR1", 4)) {
+    fclose(fp);
     return fail("Error reading Parquet file: " + f.path + " (not a Parquet file)");
+  }
   uint32_t flen;
-  memcpy(&flen, b.data() + b.size() - 8, 4);
-  if ((int64_t)flen > (int64_t)b.size() - 12) return fail("Error reading Parquet file: " + f.path + " (bad footer)");
-  TReader t{b.data() + b.size() - 8 - flen, b.data() + b.size() - 8, 0};
+  memcpy(&flen, tail, 4);
+  if ((int64_t)flen > f.size - 12) { fclose(fp); return fail("Error reading Parquet file: " + f.path + " (bad footer)"); }
+  f.footer.resize(flen);
+  ok = fseek(fp, f.size - 8 - (int64_t)flen, SEEK_SET) == 0 && fread(f.footer.data(), 1, flen, fp) == flen;
+  fclose(fp);
+  if (!ok) return fail("Error reading Parquet file: " + f.path + " (short read)");
+  return 0;
+}
+
+// Read the projected spans (file order) into f.bytes. Each span keeps its file offset modulo 64 so
+// that the kernels see the same alignment as in a whole-file image.
+static int read_spans(FileM& f, std::vector<Span> want) {
+  std::sort(want.begin(), want.end(), [](const Span& a, const Span& b) { return a.file_off < b.file_off; });
+  f.spans.clear();
+  for (const Span& w : want) {   // merge overlapping / adjacent ranges
+    if (w.len <= 0) continue;
+    if (w.file_off < 0 || w.file_off + w.len > f.size) return fail("Error reading Parquet file: " + f.path + " (chunk out of range)");
+    if (!f.spans.empty() && w.file_off <= f.spans.back().file_off + f.spans.back().len) {
+      Span& b = f.spans.back();
+      b.len = std::max(b.len, w.file_off + w.len - b.file_off);
+    } else f.spans.push_back({w.file_off, w.len, 0});
+  }
+  int64_t cur = 0;
+  for (Span& sp : f.spans) {
+    cur = (cur + 63) / 64 * 64 + (sp.file_off % 64);
+    sp.packed_off = cur;
+    cur += sp.len;
+  }
+  f.bytes.resize(cur);
+  FILE* fp = fopen(f.path.c_str(), "rb");
+  if (!fp) return fail("Error reading Parquet file: " + f.path + " (cannot open)");
+  for (const Span& sp : f.spans)
+    if (fseek(fp, sp.file_off, SEEK_SET) || fread(f.bytes.data() + sp.packed_off, 1, sp.len, fp) != (size_t)sp.len) {
+      fclose(fp);
+      return fail("Error reading Parquet file: " + f.path + " (short read)");
+    }
+  fclose(fp);
+  return 0;
+}
+
+static int parse_footer(FileM& f) {
+  const std::vector<uint8_t>& b = f.footer;
+  TReader t{b.data(), b.data() + b.size(), 0};
   int last = 0, ty, id;
   while ((id = t.field(&last, &ty))) {
     if (id == 2 && ty == 9) {
@@ -239,13 +303,18 @@ static int parse_footer(FileM& f) {
 
 // page offsets of one chunk: from the OffsetIndex when present, otherwise a host walk of headers
 struct PageRef { int64_t hdr_off; bool dict; };
-static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef>& out) {
-  const uint8_t* b = f.bytes.data();
-  const int64_t N = (int64_t)f.bytes.size();
+static int64_t chunk_start(const ColMeta& m) {
   int64_t start = m.data_page_offset;
   if (m.dict_page_offset > 0 && m.dict_page_offset < start) start = m.dict_page_offset;
-  if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= N) {
-    TReader t{b + m.oi_off, b + m.oi_off + m.oi_len, 0};
+  return start;
+}
+
+static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef>& out) {
+  const int64_t N = f.size;
+  int64_t start = chunk_start(m);
+  const uint8_t* oi = (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= N) ? span_ptr(f, m.oi_off, m.oi_len) : nullptr;
+  if (oi) {
+    TReader t{oi, oi + m.oi_len, 0};
     std::vector<int64_t> offs;
     int last = 0, ty, id;
     while ((id = t.field(&last, &ty))) {
@@ -273,7 +342,9 @@ static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef
   }
   // host walk (no offset index)
   int64_t p = start, end = start + m.total_compressed;
-  if (end > N) return fail("Error reading Parquet file: " + f.path + " (chunk out of range)");
+  const uint8_t* cb = end <= N ? span_ptr(f, start, m.total_compressed) : nullptr;
+  if (!cb) return fail("Error reading Parquet file: " + f.path + " (chunk out of range)");
+  const uint8_t* b = cb - start;   // file-offset view of the chunk
   while (p < end) {
     PageHeader h = parse_page_header(b + p, b + end);
     if (!h.ok || h.csize < 0) return fail("Error reading Parquet file: " + f.path + " (bad page header)");
@@ -364,6 +435,8 @@ struct dk_parquet {
   int copy_cb = 16384;       // k_string_copy staging buffer bytes (sized to the data in prepare)
   std::vector<std::unique_ptr<DBuf>> outbufs;
   std::vector<HostCol> host;
+  std::vector<HostCol> slice;   // dk_parquet_column_rows: one row range per column, offsets rebased
+  DBuf d_first;                 // dk_parquet_first_row result
   int n_pages = 0, n_cols = 0;
   bool has_compressed = false, has_dbp = false;
   int64_t bytes_read = 0, bytes_written = 0, bytes_arena = 0;
@@ -377,18 +450,6 @@ static int upload(DBuf& d, const void* src, size_t n, hipStream_t s) {
   return 0;
 }
 
-static int read_file(const std::string& path, std::vector<uint8_t>& out) {
-  FILE* fp = fopen(path.c_str(), "rb");
-  if (!fp) return fail("Error reading Parquet file: " + path + " (cannot open)");
-  fseek(fp, 0, SEEK_END);
-  long n = ftell(fp);
-  fseek(fp, 0, SEEK_SET);
-  out.resize(n > 0 ? n : 0);
-  size_t got = n > 0 ? fread(out.data(), 1, n, fp) : 0;
-  fclose(fp);
-  if ((long)got != n) return fail("Error reading Parquet file: " + path + " (short read)");
-  return 0;
-}
 
 // Per-page and per-tile kernels are launched once over every page / tile, or -- with
 // DK_SPLIT_LAUNCH=1, a profiling aid -- once per column so that rocprofv3's kernel trace
@@ -450,6 +511,12 @@ static int run_pipeline(dk_parquet* p, int mode) {
   return 0;
 }
 
+static int64_t file_offset(const FileM& f, int64_t packed) {
+  for (const Span& sp : f.spans)
+    if (packed >= sp.packed_off && packed < sp.packed_off + sp.len) return sp.file_off + (packed - sp.packed_off);
+  return packed;
+}
+
 static std::string page_status_msg(const dk_parquet* p, const std::vector<DPage>& pages) {
   for (const DPage& pg : pages)
     if (pg.status != PS_OK) {
@@ -458,7 +525,7 @@ static std::string page_status_msg(const dk_parquet* p, const std::vector<DPage>
       static const char* why[] = {"ok", "bad page header", "bad levels", "bad values", "unsupported encoding/codec",
                                   "bad dictionary", "bad snappy block"};
       return "Error reading Parquet file: " + p->files[fi].path + " (" + why[pg.status < 7 ? pg.status : 4] +
-             " at offset " + std::to_string(pg.hdr_off) + ")";
+             " at offset " + std::to_string(file_offset(p->files[fi], pg.hdr_off)) + ")";
     }
   return "";
 }
@@ -478,6 +545,12 @@ static int prepare(dk_parquet* p) {
   HIPOK(hipStreamSynchronize(s));
   // header errors
   for (DPage& pg : p->h_pages) if (pg.status != PS_OK && pg.status != PS_UNSUPPORTED) return fail(page_status_msg(p, p->h_pages));
+  for (const DPage& pg : p->h_pages) {   // every page body must lie inside the bytes that were read
+    const FileM& f = p->files[p->col_file[p->h_chunks[pg.chunk].col]];
+    if (pg.csize < 0 || pg.data_off + (int64_t)pg.csize > (int64_t)f.bytes.size())
+      return fail("Error reading Parquet file: " + f.path + " (bad page header at offset " +
+                  std::to_string(file_offset(f, pg.hdr_off)) + ")");
+  }
   int64_t posn = 0, arena_n = 0, dbp_n = 0;
   for (size_t i = 0; i < p->h_pages.size(); i++) {
     DPage& pg = p->h_pages[i];
@@ -646,6 +719,7 @@ static int prepare(dk_parquet* p) {
   if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;   // dict_hash_off
   HIPOK(hipStreamSynchronize(s));
   p->host.assign(p->h_cols.size(), HostCol());
+  p->slice.assign(p->h_cols.size(), HostCol());
   p->prepared = true;
   return 0;
 }
@@ -666,10 +740,22 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
   for (int fi = 0; fi < n_files; fi++) {
     FileM& f = p->files[fi];
     f.path = paths[fi];
-    if (read_file(f.path, f.bytes)) return 1;
-    if (parse_footer(f)) return 1;
+    if (read_footer(f) || parse_footer(f)) return 1;
+    {   // projection: only the chunks (and offset indexes) of the requested leaves travel to HBM
+      std::vector<Span> want;
+      for (int li = 0; li < n_leaves; li++) {
+        int idx = leaf_index(f, p->leaves[li]);
+        if (idx < 0) continue;
+        for (const RowGroupM& rg : f.rgs) {
+          const ColMeta& m = rg.cols[idx];
+          want.push_back({chunk_start(m), m.total_compressed, 0});
+          if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= f.size) want.push_back({m.oi_off, m.oi_len, 0});
+        }
+      }
+      if (read_spans(f, want)) return 1;
+    }
     if (p->dfile[fi].alloc(f.bytes.size() + 256)) return 1;
-    HIPOK(hipMemcpyAsync(p->dfile[fi].p, f.bytes.data(), f.bytes.size(), hipMemcpyHostToDevice, s));
+    if (!f.bytes.empty()) HIPOK(hipMemcpyAsync(p->dfile[fi].p, f.bytes.data(), f.bytes.size(), hipMemcpyHostToDevice, s));
     for (int li = 0; li < n_leaves; li++) {
       int idx = leaf_index(f, p->leaves[li]);
       p->leafidx[fi][li] = idx;
@@ -699,7 +785,9 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
         p->bytes_read += m.total_compressed;
         for (const PageRef& r : refs) {
           DPage pg{};
-          pg.hdr_off = r.hdr_off; pg.chunk = chunk_id; pg.flags = r.dict ? PF_DICT : 0; pg.unc_off = -1;
+          const uint8_t* hp = span_ptr(f, r.hdr_off, 1);
+          if (!hp) return fail("Error reading Parquet file: " + f.path + " (page outside its column chunk)");
+          pg.hdr_off = hp - f.bytes.data(); pg.chunk = chunk_id; pg.flags = r.dict ? PF_DICT : 0; pg.unc_off = -1;
           if (r.dict) { ck.dict_page = -2 - (int)dicts.size(); dicts.push_back(pg); }
           else p->h_pages.push_back(pg);
         }
@@ -844,6 +932,75 @@ extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_c
     h.ready = true;
   }
   out->n_entries = nv; out->n_chars = c.n_chars;
+  out->phys = c.phys; out->width = c.width; out->max_def = c.max_def; out->max_rep = c.max_rep;
+  out->rep_def = c.rep_def; out->present = 1;
+  out->row_def = h.row_def.data();
+  out->row_offs = c.max_rep > 0 ? h.row_offs.data() : nullptr;
+  out->entry_def = c.max_rep > 0 ? h.entry_def.data() : nullptr;
+  out->fixed = c.phys == PT_BYTE_ARRAY ? nullptr : h.fixed.data();
+  out->offs = c.phys == PT_BYTE_ARRAY ? h.offs.data() : nullptr;
+  out->chars = c.phys == PT_BYTE_ARRAY ? h.chars.data() : nullptr;
+  return 0;
+}
+
+extern "C" int dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, int32_t min_def, int64_t* row) {
+  *row = -1;
+  if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
+  int ci = p->colmap[file][leaf];
+  if (ci < 0) return 0;
+  const DColumn& c = p->h_cols[ci];
+  if (!c.n_rows) return 0;
+  hipSetDevice(p->eng->cfg.device);
+  hipStream_t s = p->eng->stream;
+  if (!p->d_first.p && p->d_first.alloc(8)) return 1;
+  const unsigned long long none = ~0ull;
+  HIPOK(hipMemcpyAsync(p->d_first.p, &none, 8, hipMemcpyHostToDevice, s));
+  launch_first_row(c.row_def, c.n_rows, min_def, p->d_first.as<unsigned long long>(), s);
+  unsigned long long got = none;
+  HIPOK(hipMemcpyAsync(&got, p->d_first.p, 8, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  if (check_state(p)) return 1;
+  *row = got == none ? -1 : (int64_t)got;
+  return 0;
+}
+
+extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf, int64_t row0, int64_t n,
+                                      dk_column* out) {
+  memset(out, 0, sizeof *out);
+  HIPOK(hipStreamSynchronize(p->eng->stream));
+  if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
+  if (row0 < 0 || n < 0 || row0 + n > p->files[file].num_rows) return fail("bad row range");
+  int ci = p->colmap[file][leaf];
+  out->n_rows = n;
+  if (ci < 0) { out->present = 0; return 0; }
+  const DColumn& c = p->h_cols[ci];
+  HostCol& h = p->slice[ci];
+  h = HostCol();
+  h.row_def.resize(n);
+  if (n) HIPOK(hipMemcpy(h.row_def.data(), c.row_def + row0, n, hipMemcpyDeviceToHost));
+  int64_t v0 = row0, v1 = row0 + n;   // value range
+  if (c.max_rep > 0) {
+    h.row_offs.resize(n + 1);
+    if (c.null_only) std::fill(h.row_offs.begin(), h.row_offs.end(), 0);
+    else HIPOK(hipMemcpy(h.row_offs.data(), c.row_offs + row0, (n + 1) * 8, hipMemcpyDeviceToHost));
+    v0 = h.row_offs[0]; v1 = h.row_offs[n];
+    for (auto& o : h.row_offs) o -= v0;
+    h.entry_def.resize(v1 - v0);
+    if (v1 > v0) HIPOK(hipMemcpy(h.entry_def.data(), c.entry_def + v0, v1 - v0, hipMemcpyDeviceToHost));
+  }
+  const int64_t nv = v1 - v0;
+  if (c.phys == PT_BYTE_ARRAY) {
+    h.offs.assign(nv + 1, 0);
+    if (!c.null_only) HIPOK(hipMemcpy(h.offs.data(), c.offs + v0, (nv + 1) * 8, hipMemcpyDeviceToHost));
+    const int64_t c0 = h.offs[0];
+    for (auto& o : h.offs) o -= c0;
+    h.chars.resize(h.offs[nv]);
+    if (!h.chars.empty()) HIPOK(hipMemcpy(h.chars.data(), c.chars + c0, h.chars.size(), hipMemcpyDeviceToHost));
+  } else {
+    h.fixed.assign(nv * c.width, 0);
+    if (!c.null_only && nv) HIPOK(hipMemcpy(h.fixed.data(), c.fixed + v0 * c.width, nv * c.width, hipMemcpyDeviceToHost));
+  }
+  out->n_entries = nv; out->n_chars = (int64_t)h.chars.size();
   out->phys = c.phys; out->width = c.width; out->max_def = c.max_def; out->max_rep = c.max_rep;
   out->rep_def = c.rep_def; out->present = 1;
   out->row_def = h.row_def.data();

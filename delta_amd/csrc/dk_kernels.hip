@@ -2173,4 +2173,23 @@ void launch_part_eval(const MapRows& M, const DPartProg& P, uint8_t* sel, DState
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
   hipLaunchKernelGGL(k_part_eval, dim3(grid), dim3(NT), 0, s, M, P, sel, st);
 }
+// First row whose definition level reaches min_def (LogReplay.loadTableProtocolAndMetadata takes
+// the first non-null protocol / metaData row, internal/replay/LogReplay.java:247-296): a grid-stride
+// scan with a wave-level min and one atomicMin per wave.
+__global__ void k_first_row(const uint8_t* __restrict__ row_def, long long n, int min_def, unsigned long long* out) {
+  unsigned long long best = ~0ull;
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x)
+    if (row_def[r] >= min_def) { best = (unsigned long long)r; break; }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long v = __shfl_xor(best, o);
+    best = v < best ? v : best;
+  }
+  if ((threadIdx.x & 63) == 0 && best != ~0ull) atomicMin(out, best);
+}
+void launch_first_row(const uint8_t* row_def, long long n, int min_def, unsigned long long* out, hipStream_t s) {
+  const long long want = (n + 255) / 256;
+  const unsigned grid = (unsigned)(want < 1024 ? (want > 0 ? want : 1) : 1024);
+  hipLaunchKernelGGL(k_first_row, dim3(grid), dim3(256), 0, s, row_def, n, min_def, out);
+}
+
 }  // namespace dk

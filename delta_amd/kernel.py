@@ -18,6 +18,7 @@ import ctypes as C
 import json
 import os
 import re
+import time
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -102,6 +103,18 @@ class ParquetSet:
     def column(self, file_idx, leaf) -> Column:
         c = dk_column()
         check(lib().dk_parquet_column(self._h, file_idx, self.leaves.index(leaf), C.byref(c)))
+        return Column(c, leaf)
+
+    def first_row(self, file_idx, leaf, min_def=1):
+        """Index of the first row whose definition level is >= min_def, or -1 (device scan)."""
+        r = C.c_int64()
+        check(lib().dk_parquet_first_row(self._h, file_idx, self.leaves.index(leaf), min_def, C.byref(r)))
+        return r.value
+
+    def column_rows(self, file_idx, leaf, row0, n) -> Column:
+        """Rows [row0, row0 + n) of a decoded column, offsets rebased to the slice."""
+        c = dk_column()
+        check(lib().dk_parquet_column_rows(self._h, file_idx, self.leaves.index(leaf), row0, n, C.byref(c)))
         return Column(c, leaf)
 
     def columns(self, file_idx):
@@ -255,8 +268,10 @@ class Table:
         return Table(path)
 
     def getLatestSnapshot(self, engine):
+        t0 = time.perf_counter()
         seg = build_log_segment(self.path)
         snap = Snapshot(self, seg)
+        snap.load_ms["log_segment"] = (time.perf_counter() - t0) * 1e3
         snap._load_protocol_metadata(engine)
         return snap
 
@@ -280,6 +295,7 @@ class Snapshot:
         self.log_segment = seg
         self.protocol = None
         self.metadata = None
+        self.load_ms = {}   # snapshot-load phases (ms): log_segment, commits_pm, checkpoint_pm
 
     def getVersion(self):
         return self.log_segment.version
@@ -311,9 +327,31 @@ class Snapshot:
     def _load_protocol_metadata(self, engine):
         """LogReplay.loadTableProtocolAndMetadata (internal/replay/LogReplay.java:220-314): newest
         commit first, then the checkpoint (decoded on the GPU)."""
+        t0 = time.perf_counter()
+        try:
+            self._pm_from_commits()
+        finally:
+            self.load_ms["commits_pm"] = (time.perf_counter() - t0) * 1e3
+        if self.protocol is not None and self.metadata is not None:
+            return
+        t0 = time.perf_counter()
+        try:
+            self._pm_from_checkpoint(engine)
+        finally:
+            self.load_ms["checkpoint_pm"] = (time.perf_counter() - t0) * 1e3
+        if self.protocol is None:
+            raise DkError("No protocol found at version %d" % self.getVersion())
+        if self.metadata is None:
+            raise DkError("No metadata found at version %d" % self.getVersion())
+
+    def _pm_from_commits(self):
         for d in reversed(self.log_segment.deltas):
             with open(d.path, "rb") as f:
-                for line in f.read().decode("utf-8", "replace").splitlines():
+                raw = f.read()
+            for line in raw.decode("utf-8", "replace").splitlines():
+                # only a line naming one of the two actions can hold it (a "\u"-escaped key
+                # is the one way to spell it otherwise)
+                if '"protocol"' in line or '"metaData"' in line or "\\u" in line:
                     obj = json.loads(line)
                     if self.protocol is None and obj.get("protocol") is not None:
                         self.protocol = obj["protocol"]
@@ -321,34 +359,30 @@ class Snapshot:
                         self.metadata = obj["metaData"]
             if self.protocol is not None and self.metadata is not None:
                 return
+
+    def _pm_from_checkpoint(self, engine):
         files = self._checkpoint_files(engine) if self.log_segment.checkpoints else []
         if files and (self.protocol is None or self.metadata is None):
             ps = ParquetSet(engine, files, PM_LEAVES).decode()
             for fi in range(len(files)):
-                cols = ps.columns(fi)
-                rv = cols["protocol.minReaderVersion"]
-                if self.protocol is None and rv is not None:
-                    idx = np.nonzero(rv.row_def >= 1)[0]
-                    if len(idx):
-                        r = int(idx[0])
-                        wv = cols["protocol.minWriterVersion"]
-                        self.protocol = {"minReaderVersion": int(rv.fixed.view(np.int32)[r]),
-                                         "minWriterVersion": int(wv.fixed.view(np.int32)[r])}
-                mid = cols["metaData.id"]
-                if self.metadata is None and mid is not None:
-                    idx = np.nonzero(mid.row_def >= 1)[0]
-                    if len(idx):
-                        r = int(idx[0])
-                        ss = cols["metaData.schemaString"]
-                        self.metadata = {"id": mid.string(r).decode() if mid.row_def[r] >= 2 else None,
-                                         "schemaString": (ss.string(r).decode()
-                                                          if ss is not None and ss.row_def[r] >= 2 else None),
-                                         "partitionColumns": _list_at(cols["metaData.partitionColumns.list.element"], r)}
+                # the first non-null protocol / metaData row of the batch, found on the device;
+                # only that row's values come back to the host
+                r = ps.first_row(fi, "protocol.minReaderVersion") if self.protocol is None else -1
+                if r >= 0:
+                    rv = ps.column_rows(fi, "protocol.minReaderVersion", r, 1)
+                    wv = ps.column_rows(fi, "protocol.minWriterVersion", r, 1)
+                    self.protocol = {"minReaderVersion": int(rv.fixed.view(np.int32)[0]),
+                                     "minWriterVersion": int(wv.fixed.view(np.int32)[0]) if wv.present else 0}
+                r = ps.first_row(fi, "metaData.id") if self.metadata is None else -1
+                if r >= 0:
+                    mid = ps.column_rows(fi, "metaData.id", r, 1)
+                    ss = ps.column_rows(fi, "metaData.schemaString", r, 1)
+                    pc = ps.column_rows(fi, "metaData.partitionColumns.list.element", r, 1)
+                    self.metadata = {"id": mid.string(0).decode() if mid.row_def[0] >= 2 else None,
+                                     "schemaString": (ss.string(0).decode()
+                                                      if ss.present and ss.row_def[0] >= 2 else None),
+                                     "partitionColumns": _list_at(pc if pc.present else None, 0)}
             ps.close()
-        if self.protocol is None:
-            raise DkError("No protocol found at version %d" % self.getVersion())
-        if self.metadata is None:
-            raise DkError("No metadata found at version %d" % self.getVersion())
 
 
 def _list_at(col, r):

@@ -69,7 +69,8 @@ void dk_engine_destroy(dk_engine* e);
 
 /* ---- ParquetHandler: open files (host read + footer/offset-index parse + H2D), decode on GPU --
  * leaves: dotted projected leaf paths ("add.path", "add.partitionValues.key_value.key", ...);
- * matched by exact name, then case-insensitively (ParquetSchemaUtils.java:92-119). */
+ * matched by exact name, then case-insensitively (ParquetSchemaUtils.java:92-119). Only the
+ * projected column chunks (and their offset indexes) are read from the file and copied to HBM. */
 int  dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
                      const char* const* leaves, int32_t n_leaves, dk_parquet** out);
 int  dk_parquet_decode(dk_parquet* p);                 /* async on the engine stream */
@@ -77,6 +78,13 @@ int  dk_parquet_sync(dk_parquet* p);
 int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file);
 /* D2H copy of one decoded column into library-owned host memory (valid until close). */
 int  dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out);
+/* Snapshot-load P&M pass (LogReplay.loadTableProtocolAndMetadata, internal/replay/LogReplay.java:
+ * 220-314, which takes the first row whose protocol / metaData is non-null): index of the first row
+ * of a decoded column with definition level >= min_def, found on the device; -1 when none. */
+int  dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, int32_t min_def, int64_t* row);
+/* D2H copy of rows [row0, row0+n) of one decoded column; row_offs / offs rebased to the slice
+ * (valid until the next call for the same column or close). */
+int  dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf, int64_t row0, int64_t n, dk_column* out);
 /* bytes read (projected column chunks) and written (decoded buffers) per decode, for roofline */
 int  dk_parquet_traffic(dk_parquet* p, int64_t* bytes_read, int64_t* bytes_written);
 /* algorithmic bytes one launch of a decode kernel must move ("k_string_copy", "k_tile_decode") */

@@ -671,3 +671,53 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                 if not sk.keep(None if st is None else st.decode("utf-8", "replace"), node, types):
                     b.selected[i] = False
     return res
+
+
+def load_protocol_metadata(table_root: str):
+    """``LogReplay.loadTableProtocolAndMetadata`` (internal/replay/LogReplay.java:220-314), no hint:
+    files newest first (``LogSegment.allLogFilesReversed``); the first row whose ``protocol`` /
+    ``metaData`` struct is non-null wins. Returns ((minReaderVersion, minWriterVersion),
+    (id, schemaString, partitionColumns)) with the checkpoint decoded by the C oracle."""
+    seg = load_log_segment(table_root)
+    prot = meta = None
+    for f in seg.all_files_reversed():
+        if f.kind == "commit":
+            with open(f.path, "rb") as fh:
+                lines = fh.read().decode("utf-8", "replace").splitlines()
+            for line in lines:
+                obj = json.loads(line)
+                if prot is None and obj.get("protocol") is not None:
+                    p = obj["protocol"]
+                    prot = (p.get("minReaderVersion"), p.get("minWriterVersion"))
+                if meta is None and obj.get("metaData") is not None:
+                    m = obj["metaData"]
+                    meta = (m.get("id"), m.get("schemaString"), m.get("partitionColumns"))
+        else:
+            if f.path.endswith(".json"):
+                continue
+            pf = ParquetFile.open(f.path)
+            rv, wv = pf.read("protocol.minReaderVersion"), pf.read("protocol.minWriterVersion")
+            if prot is None and rv is not None:
+                idx = np.nonzero(rv.row_def >= 1)[0]
+                if len(idx):
+                    r = int(idx[0])
+                    prot = (int(rv.fixed.view(np.int32)[r]), int(wv.fixed.view(np.int32)[r]) if wv is not None else 0)
+            mid = pf.read("metaData.id")
+            if meta is None and mid is not None:
+                idx = np.nonzero(mid.row_def >= 1)[0]
+                if len(idx):
+                    r = int(idx[0])
+                    ss = pf.read("metaData.schemaString")
+                    pc = pf.read("metaData.partitionColumns.list.element")
+                    plist = None
+                    if pc is not None and pc.row_def[r] >= pc.rep_def - 1:
+                        a, b = int(pc.row_offs[r]), int(pc.row_offs[r + 1])
+                        plist = [bytes(pc.chars[pc.offs[i]:pc.offs[i + 1]]).decode() if pc.entry_def[i] >= pc.max_def
+                                 else None for i in range(a, b)]
+                    meta = (bytes(mid.chars[mid.offs[r]:mid.offs[r + 1]]).decode() if mid.row_def[r] >= 2 else None,
+                            bytes(ss.chars[ss.offs[r]:ss.offs[r + 1]]).decode()
+                            if ss is not None and ss.row_def[r] >= 2 else None,
+                            plist)
+        if prot is not None and meta is not None:
+            return prot, meta
+    raise OracleError("No %s found at version %d" % ("protocol" if prot is None else "metadata", seg.version))
