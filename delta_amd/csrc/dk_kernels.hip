@@ -673,48 +673,6 @@ struct RunCur {
   }
 };
 
-// Tile-local run tables. A level pass reads, per stream, the few runs that cover its tile; each
-// lane binary-searching the page's whole table in global memory and then chasing R[k+1] put ~10-20
-// dependent global loads on every lane's critical path. Instead one lane per stream finds the
-// slice [k0, k1] covering [a, b), the workgroup copies it into LDS (RCAP runs at most, else the
-// global table is used), and cursors search / advance in LDS.
-constexpr int RCAP = 64;
-struct RunSlice { const Seg* R; int n; };
-
-__device__ __forceinline__ void find_slice(const Seg* R, int n, int a, int b, int* k0, int* k1) {
-  int lo = 0, hi = n - 1;
-  while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (R[mid].start <= a) lo = mid; else hi = mid - 1; }
-  *k0 = lo;
-  hi = n - 1;
-  const int last = b - 1 > a ? b - 1 : a;
-  while (lo < hi) { const int mid = (lo + hi + 1) >> 1; if (R[mid].start <= last) lo = mid; else hi = mid - 1; }
-  *k1 = lo;
-}
-
-// Workgroup-cooperative: streams q < nq with tables (R[q], n[q]) and ranges [a[q], b[q]).
-// s_k: 2 * nq ints of LDS; lds: nq * RCAP Segs of LDS. Must be reached by every thread.
-template <int NQ>
-__device__ __forceinline__ void stage_slices(const Seg* const* R, const int* n, const int* a, const int* b,
-                                             int* s_k, Seg* lds, RunSlice* out) {
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < NQ; q++)
-    if (t == q * 64) {
-      int k0 = 0, k1 = -1;
-      if (n[q] > 0 && b[q] > a[q]) find_slice(R[q], n[q], a[q], b[q], &k0, &k1);
-      s_k[2 * q] = k0; s_k[2 * q + 1] = k1;
-    }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const int k0 = s_k[2 * q], cnt = s_k[2 * q + 1] - k0 + 1;
-    if (cnt > 0 && cnt <= RCAP)
-      for (int j = t; j < cnt; j += blockDim.x) lds[q * RCAP + j] = R[q][k0 + j];
-    out[q] = cnt <= 0 ? RunSlice{R[q], 0} : cnt <= RCAP ? RunSlice{lds + q * RCAP, cnt} : RunSlice{R[q], n[q]};
-  }
-  __syncthreads();
-}
-
 __global__ void k_page_runs(const DChunk* __restrict__ chunks, DPage* __restrict__ pages, int n_pages,
                             const uint8_t* __restrict__ arena, Seg* __restrict__ runs) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -763,24 +721,15 @@ __global__ __launch_bounds__(NT) void k_tile_count(const DChunk* __restrict__ ch
   __shared__ int lds[12];
   int rows = 0, ents = 0, vals = 0;
   const DChunk ck = chunks[pg.chunk];
-  __shared__ int s_k[4];
-  __shared__ Seg s_runs[2 * RCAP];
   if (pg.status == PS_OK) {
     const Layout L = page_layout(pg, ck, arena);
     const int l_end = min(T.lvl0 + TL, pg.num_values);
-    RunSlice sl[2];
-    {
-      const Seg* R[2] = {runs + pg.run_r, runs + pg.run_d};
-      const int n[2] = {ck.max_rep > 0 ? pg.nrun_r : 0, ck.max_def > 0 ? pg.nrun_d : 0};
-      const int a[2] = {T.lvl0, T.lvl0}, b[2] = {l_end, l_end};
-      stage_slices<2>(R, n, a, b, s_k, s_runs, sl);
-    }
     const int a = T.lvl0 + t * LPT, b = min(a + LPT, l_end);
     if (a < b) {
       const int bwr = bit_width(ck.max_rep), bwd = bit_width(ck.max_def);
       RunCur cr, cd;
-      if (ck.max_rep > 0) cr.init(sl[0].R, sl[0].n, a);
-      if (ck.max_def > 0) cd.init(sl[1].R, sl[1].n, a);
+      if (ck.max_rep > 0) cr.init(runs + pg.run_r, pg.nrun_r, a);
+      if (ck.max_def > 0) cd.init(runs + pg.run_d, pg.nrun_d, a);
       for (int i = a; i < b; i++) {
         const int rep = ck.max_rep > 0 ? (int)cr.get(i, bwr, L.d, L.rep_e) : 0;
         const int def = ck.max_def > 0 ? (int)cd.get(i, bwd, L.d, L.def_e) : 0;
@@ -869,19 +818,11 @@ __global__ __launch_bounds__(NT) void k_tile_chars(const DChunk* __restrict__ ch
     dict_data(ck, pages, arena, &dn);
     const int32_t* DP = pos + ck.dict_pos;
     const int ibw = *L.val_p;
-    __shared__ int s_k[2];
-    __shared__ Seg s_runs[RCAP];
-    RunSlice sl[1];
-    {
-      const Seg* R[1] = {runs + pg.run_i};
-      const int n[1] = {pg.nrun_i}, a1[1] = {vb}, b1[1] = {vb + nvt};
-      stage_slices<1>(R, n, a1, b1, s_k, s_runs, sl);
-    }
     const int per = (nvt + NT - 1) / NT;
     const int a = vb + t * per, b = min(a + per, vb + nvt);
     if (a < b) {
       RunCur ci;
-      ci.init(sl[0].R, sl[0].n, a);
+      ci.init(runs + pg.run_i, pg.nrun_i, a);
       for (int v = a; v < b; v++) {
         const uint32_t ix = ci.get(v, ibw, L.d, L.val_e);
         if ((int32_t)ix >= dn) { s_bad = 1; break; }
@@ -1013,19 +954,6 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
   __shared__ int32_t vsrc[TL];              // dictionary strings: source offset in the dictionary page
   __shared__ int32_t vcoff[TL + 1];         // and tile-relative output offset of each value
   __shared__ uint4 dstage[DSTAGE / 16];     // small dictionary pages
-  // 0. the run-table slices of the tile (levels: [lvl0, l_end); indices: the tile's values)
-  const int vt0 = (int)(T.value_base - pg.value_base);   // page-local index of the tile's first value
-  __shared__ int s_k[6];
-  __shared__ Seg s_runs[3 * RCAP];
-  RunSlice sl[3];
-  {
-    const bool need_i = (is_dict || bool_rle) && pg.nrun_i > 0;
-    const Seg* R[3] = {runs + pg.run_r, runs + pg.run_d, runs + pg.run_i};
-    const int n[3] = {rep ? pg.nrun_r : 0, ck.max_def > 0 ? pg.nrun_d : 0, need_i ? pg.nrun_i : 0};
-    const int a[3] = {T.lvl0, T.lvl0, vt0};
-    const int b[3] = {l_end, l_end, min(vt0 + T.n_values, pg.idx_cover)};
-    stage_slices<3>(R, n, a, b, s_k, s_runs, sl);
-  }
   // 1. levels (strided) and their ballots
   int rp[LPT], df[LPT];
   uint64_t mr[LPT], me[LPT], mv[LPT];
@@ -1033,8 +961,8 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
     RunCur cr, cd;
     const int i0 = T.lvl0 + t;
     if (i0 < l_end) {
-      if (rep) cr.init(sl[0].R, sl[0].n, i0);
-      if (ck.max_def > 0) cd.init(sl[1].R, sl[1].n, i0);
+      if (rep) cr.init(runs + pg.run_r, pg.nrun_r, i0);
+      if (ck.max_def > 0) cd.init(runs + pg.run_d, pg.nrun_d, i0);
     }
 #pragma unroll
     for (int k = 0; k < LPT; k++) {
@@ -1044,9 +972,6 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
         rp[k] = rep ? (int)cr.get(i, bwr, L.d, L.rep_e) : 0;
         df[k] = ck.max_def > 0 ? (int)cd.get(i, bwd, L.d, L.def_e) : 0;
       }
-    }
-#pragma unroll
-    for (int k = 0; k < LPT; k++) {
       mr[k] = __ballot(rp[k] == 0);
       me[k] = __ballot(df[k] >= ck.rep_def && df[k] >= 0);
       mv[k] = __ballot(df[k] == ck.max_def);
@@ -1062,6 +987,7 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
   }
   __syncthreads();
   const int tv = s_tot[2];
+  const int vt0 = (int)(T.value_base - pg.value_base);   // page-local index of the tile's first value
   // 2. dictionary indices / RLE booleans of the thread's values (value order = level order)
   uint32_t ix[LPT];
   bool bad = false;
@@ -1075,7 +1001,7 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
       if (need && df[k] == ck.max_def && !bad) {
         const int v = vt0 + wbase[2][k][wv] + lane_rank(mv[k]);
         if (v >= pg.idx_cover || pg.nrun_i == 0) { bad = true; continue; }
-        if (!ci_on) { ci.init(sl[2].R, sl[2].n, v); ci_on = true; }
+        if (!ci_on) { ci.init(runs + pg.run_i, pg.nrun_i, v); ci_on = true; }
         ix[k] = ci.get(v, ibw, L.d, L.val_e);
         if (is_dict && (int32_t)ix[k] >= dict_n) { bad = true; ix[k] = 0; }
       }
