@@ -31,11 +31,47 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_table(root, rows, seed, compression):
+# BASELINE.json configs. "shared": one table sharded over the ranks by checkpoint
+# file (strong scaling); otherwise every rank reconciles its own table (weak scaling).
+CONFIGS = {
+    "c1": dict(rows=1_000_000, shared=False, stats=False, predicate=None,
+               spec=dict(pv_keys=1, n_commits=100, adds_per_commit=50, removes_per_commit=50),
+               desc="C1: %d-AddFile single-part uncompressed checkpoint per GPU, 100-commit JSON tail; "
+                    "read schema add(no stats)+remove"),
+    "c2": dict(rows=10_000_000, shared=False, stats=False, predicate=None,
+               spec=dict(pv_keys=2, with_stats_parsed=True, n_commits=100, adds_per_commit=50, removes_per_commit=50),
+               desc="C2: %d-AddFile single-part checkpoint per GPU, 2-key partitionValues, stats_parsed present, "
+                    "100-commit JSON tail; read schema add(no stats)+remove"),
+    "c3": dict(rows=100_000_000, shared=True, stats=False, predicate=None,
+               spec=dict(n_parts=64, compression="snappy", n_commits=1000, adds_per_commit=100,
+                         removes_per_commit=100, readd_frac=0.1, dup_frac=0.05),
+               desc="C3: %d-AddFile 64-part snappy checkpoint sharded over the GPUs by part, 1k commits "
+                    "(100 adds + 100 removes each); read schema add(no stats)+remove"),
+    "c4": dict(rows=50_000_000, shared=False, stats=True, predicate=("id", ">", 25_000_000),
+               spec=dict(dv_frac=0.3, with_stats=True, n_commits=100, adds_per_commit=50, removes_per_commit=50),
+               desc="C4: %d-AddFile checkpoint per GPU, 30%% with deletion vectors, predicate id > 25000000 "
+                    "over stats; read schema add(with stats)+remove"),
+    "c5": dict(rows=10_000_000, shared=True, stats=False, predicate=None,
+               spec=dict(n_parts=16, v2_sidecars=16, compression="snappy", data_page_version="2.0",
+                         delta_binary_packed=True, hot_frac=0.6, n_commits=100, adds_per_commit=50,
+                         removes_per_commit=50),
+               desc="C5: %d-AddFile V2 checkpoint (manifest + 16 sidecars, snappy, v2 pages, DELTA_BINARY_PACKED, "
+                    "60%% of paths under one hot partition) sharded over the GPUs by file; "
+                    "read schema add(no stats)+remove+sidecar"),
+}
+
+
+def table_spec(cfg, rows, seed, compression=None):
     from delta_amd import synth
-    spec = synth.TableSpec(n_adds=rows, pv_keys=2, with_stats_parsed=True, n_commits=100,
-                           adds_per_commit=50, removes_per_commit=50, compression=compression, seed=seed)
-    return synth.write_table(root, spec)
+    kw = dict(cfg["spec"])
+    if compression is not None:
+        kw["compression"] = compression
+    return synth.TableSpec(n_adds=rows, seed=seed, **kw)
+
+
+def make_table(root, rows, seed, compression, cfg=None):
+    from delta_amd import synth
+    return synth.write_table(root, table_spec(cfg or CONFIGS["c2"], rows, seed, compression))
 
 
 def pmc_traffic(kernel, rows, compression):
@@ -53,15 +89,18 @@ def pmc_traffic(kernel, rows, compression):
     return {"bytes": d["kernels"][kernel], "source": "profiles/pmc_traffic.json (%s)" % d.get("profile", "?")}
 
 
-def cpu_baseline(rows, reps, seed, compression):
-    """Oracle (plain C restatement, single thread) on a bounded sample of the same workload."""
+def cpu_baseline(rows, reps, seed, compression, cfg_name="c2"):
+    """Oracle (plain C restatement, single thread) on a bounded sample of the same workload: one
+    single-part checkpoint with the config's encodings."""
     from oracle import ref
     d = tempfile.mkdtemp(prefix="dk_cpu_")
     try:
-        make_table(d, rows, seed + 99, compression)
+        cfg = dict(CONFIGS[cfg_name])
+        cfg["spec"] = dict(cfg["spec"], n_parts=1, v2_sidecars=0)
+        make_table(d, rows, seed + 99, compression, cfg)
         seg = ref.load_log_segment(d)
         path = seg.checkpoints[0].path
-        leaves = ref.ADD_LEAVES + ["remove.path", "remove.deletionVector.storageType",
+        leaves = ref.ADD_LEAVES + (["add.stats"] if cfg["stats"] else []) + ["remove.path", "remove.deletionVector.storageType",
                                    "remove.deletionVector.pathOrInlineDv", "remove.deletionVector.offset",
                                    "remove.deletionVector.sizeInBytes", "remove.deletionVector.cardinality"]
         with open(path, "rb") as f:
@@ -77,8 +116,8 @@ def cpu_baseline(rows, reps, seed, compression):
             t_total += time.perf_counter() - t0
             total_rows += pf.num_rows
         return {"value": total_rows / t_total, "unit": "actions/s", "cores": 1, "kind": "port",
-                "sample": "%d x %d-row C2-shaped checkpoint, decode (21 leaves) + key + probe, oracle/dk_ref.c"
-                          % (reps, rows)}
+                "sample": "%d x %d-row %s-shaped checkpoint, decode (%d leaves) + key + probe, oracle/dk_ref.c"
+                          % (reps, rows, cfg_name.upper(), len(leaves))}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -88,8 +127,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=10_000_000)
-    ap.add_argument("--compression", default="none")
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--rows", type=int, default=None, help="checkpoint adds (default: the config's)")
+    ap.add_argument("--compression", default=None, help="override the config's codec")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -108,13 +148,23 @@ def main():
 
     from delta_amd import kernel as K
 
-    work = args.workdir or tempfile.mkdtemp(prefix="dk_bench_r%d_" % rank)
+    cfg = CONFIGS[args.config]
+    rows = args.rows or cfg["rows"]
+    compression = args.compression or cfg["spec"].get("compression", "none")
+    if cfg["shared"]:
+        # one table for all ranks: rank 0 writes it, the others wait at the barrier
+        work = args.workdir or os.path.join(tempfile.gettempdir(), "dk_bench_%s_%d" % (args.config, rows))
+    else:
+        work = args.workdir or tempfile.mkdtemp(prefix="dk_bench_r%d_" % rank)
     t0 = time.time()
     if args.workdir and os.path.isdir(os.path.join(work, "_delta_log")):
         log("[rank %d] reusing table in %s" % (rank, work))
-    else:
-        info = make_table(work, args.rows, 20250218 + rank, args.compression)
+    elif rank == 0 or not cfg["shared"]:
+        shutil.rmtree(work, ignore_errors=True)
+        info = make_table(work, rows, 20250218 + (0 if cfg["shared"] else rank), compression, cfg)
         log("[rank %d] generated %d-row table in %.1fs" % (rank, info["checkpoint_rows"], time.time() - t0))
+    if dist is not None and cfg["shared"]:
+        dist.barrier()
 
     eng = K.GpuEngine(device=local if world > 1 else 0, timing=True)
     # snapshot load: the first (cold: code-object load, first allocations) and the median of 5 warm
@@ -128,7 +178,14 @@ def main():
         snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
         warm.append((time.perf_counter() - t0) * 1e3)
     snapshot_ms = sorted(warm)[len(warm) // 2]
-    scan = snap.getScanBuilder().build()
+    sb = snap.getScanBuilder().withStats(cfg["stats"])
+    if cfg["predicate"]:
+        from delta_amd.expressions import Column, Literal, Predicate
+        col, op, lit = cfg["predicate"]
+        sb = sb.withFilter(Predicate(op, Column(col), Literal.ofLong(lit)))
+    if cfg["shared"] and world > 1:
+        sb = sb.withShard(world, rank)
+    scan = sb.build()
     t0 = time.perf_counter()
     scan.prepare(eng)
     prepare_s = time.perf_counter() - t0
@@ -169,7 +226,17 @@ def main():
         if c1 > c0:
             kern[name] = (avg1 * c1 - avg0 * c0) / (c1 - c0)
     step_us = kern.pop("step_total", None)
-    units = (n_ckpt_rows + n_tail) * world
+    if cfg["shared"]:
+        # every rank replays the whole tail; the checkpoint rows are split among the ranks
+        tot = n_ckpt_rows
+        if dist is not None:
+            import torch
+            tt = torch.tensor([n_ckpt_rows], dtype=torch.int64, device="cuda")
+            dist.all_reduce(tt)
+            tot = int(tt.item())
+        units = tot + n_tail
+    else:
+        units = (n_ckpt_rows + n_tail) * world
     value = units * args.steps / elapsed
     ms_per_step = elapsed / args.steps * 1e3
     dom = max(kern.items(), key=lambda kv: kv[1]) if kern else ("none", 0.0)
@@ -182,7 +249,7 @@ def main():
     k_read, k_written = scan.ckpt.kernel_traffic(rk) if rk else (0, 0)
     k_bytes = k_read + k_written
     achieved = k_bytes / (kern[rk] * 1e-6) / 1e9 if rk else None
-    pmc = pmc_traffic(rk, n_ckpt_rows, args.compression) if rk else None
+    pmc = pmc_traffic(rk, n_ckpt_rows, compression) if rk else None
 
     result = {
         "metric": "checkpoint actions reconciled/sec (node) + snapshot load ms, 100M AddFile",
@@ -193,15 +260,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if cfg["shared"] else "weak",
         "vs_baseline": None,
         "dtype": "u8/int64",
         "data": "synthetic (seed 20250218; delta_amd/synth.py)",
-        "config": {"workload": "C2: %d-AddFile single-part checkpoint per GPU, 2-key partitionValues, "
-                               "stats_parsed present, 100-commit JSON tail; read schema add(no stats)+remove"
-                               % n_ckpt_rows,
-                   "compression": args.compression, "parallelism": "weak: one checkpoint part per GPU",
-                   "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail},
+        "config": {"workload": cfg["desc"] % rows, "name": args.config,
+                   "compression": compression,
+                   "parallelism": ("strong: checkpoint files round-robin over %d GPU(s), tail on every GPU" % world
+                                   if cfg["shared"] else "weak: one checkpoint per GPU"),
+                   "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail,
+                   "checkpoint_files_per_gpu": len(scan.ckpt_files)},
         "snapshot_load_ms": snapshot_ms,
         "snapshot_load_cold_ms": snapshot_cold_ms,
         "snapshot_load_phases_ms": {k: round(v, 3) for k, v in snap.load_ms.items()},
@@ -220,12 +288,14 @@ def main():
                               "frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None}},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        result["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.cpu_reps, 20250218, args.compression)
+        result["cpu_baseline"] = cpu_baseline(args.cpu_rows, args.cpu_reps, 20250218, compression, args.config)
     if rank == 0:
         print(json.dumps(result), flush=True)
     scan.close()
     eng.close()
-    if not args.workdir:
+    if dist is not None and cfg["shared"]:
+        dist.barrier()          # every rank is done with the shared table
+    if not args.workdir and (rank == 0 or not cfg["shared"]):
         shutil.rmtree(work, ignore_errors=True)
     if dist is not None:
         dist.destroy_process_group()

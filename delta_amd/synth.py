@@ -66,6 +66,7 @@ class TableSpec:
     max_rows_per_page: int = 20_000  # parquet-mr 1.12 page row-count limit
     write_page_index: bool = True
     hot_frac: float = 0.0            # C5 skew: fraction of paths under one hot partition
+    v2_sidecars: int = 0             # > 0: V2 checkpoint = parquet manifest + this many sidecars
     variable_paths: bool = False     # add random suffixes / escapes so lengths vary
     seed: int = SEED
     extra: dict = field(default_factory=dict)
@@ -410,6 +411,50 @@ def _json_remove(path, day, ts, dv=None):
     return {"remove": d}
 
 
+CKPT_META_TYPE = pa.struct([("version", pa.int64()), ("tags", pa.map_(pa.string(), pa.string()))])
+SIDECAR_TYPE = pa.struct([("path", pa.string()), ("sizeInBytes", pa.int64()), ("modificationTime", pa.int64()),
+                          ("tags", pa.map_(pa.string(), pa.string()))])
+
+
+def _uuid(rng):
+    h = "".join("%02x" % b for b in rng.integers(0, 256, 16))
+    return "%s-%s-%s-%s-%s" % (h[:8], h[8:12], h[12:16], h[16:20], h[20:])
+
+
+def _write_v2(log, v, parts, spec: TableSpec, rng):
+    """V2 checkpoint (PROTOCOL.md "V2 Spec"): sidecars under _delta_log/_sidecars/ hold the add /
+    remove rows (one per part, P&M rows dropped); the manifest ``<v>.checkpoint.<uuid>.parquet``
+    holds protocol, metaData, checkpointMetadata and one sidecar row per file."""
+    side = os.path.join(log, "_sidecars")
+    os.makedirs(side, exist_ok=True)
+    sc_rows, files = [], []
+    proto_row = meta_row = None
+    for i, t in enumerate(parts):
+        if i == 0:
+            proto_row = t.column("protocol")[0].as_py()
+            meta_row = t.column("metaData")[1].as_py()
+            t = t.slice(2)
+        t = t.select(["add", "remove"])
+        name = "%020d.checkpoint.%010d.%010d.%s.parquet" % (v, i + 1, len(parts), _uuid(rng))
+        fn = os.path.join(side, name)
+        _write_parquet(t, fn, spec)
+        sc_rows.append({"path": name, "sizeInBytes": os.path.getsize(fn), "modificationTime": 1_714_496_113_961,
+                        "tags": None})
+        files.append(fn)
+    n = 3 + len(sc_rows)
+    add_t, rm_t = parts[0].schema.field("add").type, parts[0].schema.field("remove").type
+    man = pa.table({
+        "add": pa.nulls(n, type=add_t), "remove": pa.nulls(n, type=rm_t),
+        "metaData": pa.array([None, meta_row, None] + [None] * len(sc_rows), type=METADATA_TYPE),
+        "protocol": pa.array([proto_row, None, None] + [None] * len(sc_rows), type=PROTOCOL_TYPE),
+        "checkpointMetadata": pa.array([None, None, {"version": v, "tags": None}] + [None] * len(sc_rows),
+                                       type=CKPT_META_TYPE),
+        "sidecar": pa.array([None, None, None] + sc_rows, type=SIDECAR_TYPE)})
+    mfn = os.path.join(log, "%020d.checkpoint.%s.parquet" % (v, _uuid(rng)))
+    _write_parquet(man, mfn, spec)
+    return [mfn] + files
+
+
 def write_table(root: str, spec: TableSpec):
     """Write the synthetic table under ``root``. Returns a dict describing what was written."""
     rng = np.random.Generator(np.random.PCG64(spec.seed))
@@ -418,7 +463,9 @@ def write_table(root: str, spec: TableSpec):
     parts, ck_paths = build_checkpoint_tables(spec, rng)
     v = spec.ckpt_version
     files = []
-    if spec.n_parts == 1:
+    if spec.v2_sidecars > 0:
+        files = _write_v2(log, v, parts, spec, rng)
+    elif spec.n_parts == 1:
         fn = os.path.join(log, "%020d.checkpoint.parquet" % v)
         _write_parquet(parts[0], fn, spec)
         files.append(fn)
@@ -428,7 +475,7 @@ def write_table(root: str, spec: TableSpec):
             _write_parquet(t, fn, spec)
             files.append(fn)
     lc = {"version": v, "size": int(sum(t.num_rows for t in parts))}
-    if spec.n_parts > 1:
+    if spec.n_parts > 1 and spec.v2_sidecars == 0:
         lc["parts"] = spec.n_parts
     with open(os.path.join(log, "_last_checkpoint"), "w") as f:
         f.write(json.dumps(lc))

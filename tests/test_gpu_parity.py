@@ -43,3 +43,19 @@ def test_with_stats_parity(tmp_path):
     spec = synth.TableSpec(n_adds=8_000, n_commits=5, with_stats=True)
     synth.write_table(str(tmp_path), spec)
     assert_same(product_scan(str(tmp_path), with_stats=True), oracle_scan(str(tmp_path), with_stats=True))
+
+
+V2_CASES = {
+    # C5 shape: V2 manifest + sidecars, snappy, v2 pages, DELTA_BINARY_PACKED, hot partition
+    "v2-sidecars-c5": dict(n_parts=6, v2_sidecars=6, compression="snappy", data_page_version="2.0",
+                           delta_binary_packed=True, hot_frac=0.6, ckpt_removes=200, dv_frac=0.1),
+    "v2-one-sidecar-dict": dict(n_parts=1, v2_sidecars=1, pv_keys=2),
+}
+
+
+@pytest.mark.parametrize("name", list(V2_CASES))
+@pytest.mark.parametrize("jbs", [1024, 5])
+def test_v2_sidecar_parity(tmp_path, name, jbs):
+    spec = synth.TableSpec(n_adds=30_000, n_commits=8, seed=synth.SEED + 7, **V2_CASES[name])
+    synth.write_table(str(tmp_path), spec)
+    assert_same(product_scan(str(tmp_path), jbs), oracle_scan(str(tmp_path), jbs))

@@ -106,13 +106,23 @@ def test_gloo_world2(tmp_path):
     assert res.startswith("ok"), res
 
 
+def test_oracle_shards_v2_sidecars(tmp_path):
+    from oracle import ref
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=6_000, n_parts=5, v2_sidecars=5, n_commits=6,
+                                                     ckpt_removes=50, hot_frac=0.6))
+    full = ref.replay(str(tmp_path))
+    counters, payloads = shard.merge([_oracle_shard_output(str(tmp_path), 3, r) for r in range(3)])
+    assert counters == full.counters.as_tuple()
+    assert _flatten(payloads) == full.scan_files()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_gpu_shards_merge_to_oracle(tmp_path, world):
+@pytest.mark.parametrize("world,v2", [(2, 0), (3, 0), (3, 5)])
+def test_gpu_shards_merge_to_oracle(tmp_path, world, v2):
     from delta_amd import kernel as K
     from oracle import ref
     synth.write_table(str(tmp_path), synth.TableSpec(n_adds=20_000, n_parts=5, n_commits=8, dv_frac=0.2,
-                                                     ckpt_removes=100))
+                                                     ckpt_removes=100, v2_sidecars=v2))
     eng = K.GpuEngine()
     outs, scans = [], []
     for r in range(world):
