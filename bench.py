@@ -66,7 +66,7 @@ def table_spec(cfg, rows, seed, compression=None):
     kw = dict(cfg["spec"])
     if compression is not None:
         kw["compression"] = compression
-    return synth.TableSpec(n_adds=rows, seed=seed, **kw)
+    return synth.TableSpec(n_adds=rows, seed=seed, extra={"progress": True}, **kw)
 
 
 def make_table(root, rows, seed, compression, cfg=None):

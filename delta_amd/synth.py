@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -344,6 +345,8 @@ def build_checkpoint_tables(spec: TableSpec, rng):
     all_paths = []
     proto, meta = _pm_rows(spec)
     for pi, cnt in enumerate(per):
+        if spec.extra.get("progress") and pi % 8 == 0:
+            print("[synth] building part %d/%d" % (pi + 1, spec.n_parts), file=sys.stderr, flush=True)
         adds = _add_struct(rng, cnt, start, spec, data_change=False)
         all_paths.append(adds.field("path"))
         n_pm = 2 if pi == 0 else 0
