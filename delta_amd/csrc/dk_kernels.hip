@@ -167,13 +167,21 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
 
 // --------------------------------------------------------------------------------------------
 // K1b: SNAPPY raw-block decompression, one wave64 per compressed page.
-// Every lane parses the same tag (uniform control flow; same-address loads coalesce into one
-// transaction), then the wave copies the literal / back-reference 64 bytes per step. Back
-// references read bytes other lanes stored earlier, so a workgroup-scope acq_rel fence orders
-// them whenever the source range reaches past the last fenced output position.
+// Tag parsing is a serial chain, so every byte the chain touches lives in LDS: the compressed
+// stream is staged through an 8 KiB window (refilled with coalesced dword loads), and the last
+// 64 KiB of output -- the reach of every offset the snappy compressor emits (it works on 64 KiB
+// fragments) -- sit in an LDS ring that back references read. Output goes to HBM with plain
+// stores that nothing in this kernel reads back, except a copy whose offset exceeds the ring
+// (legal in the format, never produced by snappy): that one reads HBM after a workgroup fence.
+// All lanes parse the same tag (uniform control flow); the wave copies 64 bytes per step.
 // --------------------------------------------------------------------------------------------
+constexpr int SNAP_RING = 65536;
+constexpr int SNAP_WIN = 8192;
+
 __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                uint8_t* __restrict__ arena) {
+  __shared__ uint8_t ring[SNAP_RING];
+  __shared__ uint32_t win[SNAP_WIN / 4];
   DPage& pgw = pages[blockIdx.x];
   const DPage pg = pgw;                            // by value: byte stores below may alias
   if (pg.unc_off < 0 || pg.status != PS_OK) return;
@@ -191,64 +199,101 @@ __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks
     for (int64_t i = lane; i < clen; i += 64) out[i] = in[i];
     return;
   }
+  const uint8_t* wbytes = (const uint8_t*)win;
+  // window: in-offsets [ws, ws + SNAP_WIN) (ws may sit up to 3 bytes before the stream start)
+  int64_t ws = 0;
+  auto refill = [&](int64_t at) {
+    const uintptr_t a4 = ((uintptr_t)(in + at)) & ~(uintptr_t)3;
+    ws = at - (int64_t)((uintptr_t)(in + at) - a4);
+    const uintptr_t lim = (uintptr_t)(in + clen);   // never load past the stream
+    __syncthreads();
+#pragma unroll 4
+    for (int q = lane; q < SNAP_WIN / 4; q += 64) {
+      const uintptr_t ad = a4 + (uintptr_t)q * 4;
+      if (ad < lim) win[q] = *(const uint32_t*)ad;
+    }
+    __syncthreads();
+  };
+  auto B = [&](int64_t at) -> uint32_t { return wbytes[at - ws]; };
+  refill(0);
   // preamble: varint uncompressed length
   int64_t p = 0;
   uint64_t n = 0;
-  for (int s = 0; s < 35; s += 7) {
+  for (int sh = 0; sh < 35; sh += 7) {
     if (p >= clen) break;
-    uint8_t b = in[p++];
-    n |= (uint64_t)(b & 0x7f) << s;
+    const uint32_t b = B(p++);
+    n |= (uint64_t)(b & 0x7f) << sh;
     if (!(b & 0x80)) break;
   }
   bool bad = (int64_t)n != ulen;
   int64_t o = 0, fenced = 0;
   while (!bad && p < clen) {
-    const uint8_t tag = in[p++];
+    if ((p + 5 < clen ? p + 5 : clen) > ws + SNAP_WIN) refill(p);
+    const uint32_t tag = B(p);
+    const uint32_t b1 = p + 1 < clen ? B(p + 1) : 0, b2 = p + 2 < clen ? B(p + 2) : 0;
+    const uint32_t b3 = p + 3 < clen ? B(p + 3) : 0, b4 = p + 4 < clen ? B(p + 4) : 0;
+    p++;
     const int kind = tag & 3;
     int64_t len, off = 0;
     if (kind == 0) {
       len = (tag >> 2) + 1;
       if (len > 60) {
-        int nb = (int)len - 60;
+        const int nb = (int)len - 60;
         if (p + nb > clen) { bad = true; break; }
-        len = 0;
-        for (int k = 0; k < nb; k++) len |= (int64_t)in[p + k] << (8 * k);
+        len = (int64_t)b1 | (nb > 1 ? (int64_t)b2 << 8 : 0) | (nb > 2 ? (int64_t)b3 << 16 : 0) |
+              (nb > 3 ? (int64_t)b4 << 24 : 0);
         len += 1;
         p += nb;
       }
       if (p + len > clen || o + len > ulen) { bad = true; break; }
-      for (int64_t i = lane; i < len; i += 64) out[o + i] = in[p + i];
+      if (p + len > ws + SNAP_WIN && len <= SNAP_WIN - 64) refill(p);
+      const bool from_win = p + len <= ws + SNAP_WIN;
+      for (int64_t i = lane; i < len; i += 64) {
+        const uint8_t v = from_win ? wbytes[p + i - ws] : in[p + i];
+        ring[(o + i) & (SNAP_RING - 1)] = v;
+        out[o + i] = v;
+      }
       p += len;
     } else {
       if (kind == 1) {
         if (p + 1 > clen) { bad = true; break; }
         len = ((tag >> 2) & 7) + 4;
-        off = ((int64_t)(tag >> 5) << 8) | in[p];
+        off = ((int64_t)(tag >> 5) << 8) | b1;
         p += 1;
       } else if (kind == 2) {
         if (p + 2 > clen) { bad = true; break; }
         len = (tag >> 2) + 1;
-        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8);
+        off = (int64_t)b1 | ((int64_t)b2 << 8);
         p += 2;
       } else {
         if (p + 4 > clen) { bad = true; break; }
         len = (tag >> 2) + 1;
-        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8) | ((int64_t)in[p + 2] << 16) | ((int64_t)in[p + 3] << 24);
+        off = (int64_t)b1 | ((int64_t)b2 << 8) | ((int64_t)b3 << 16) | ((int64_t)b4 << 24);
         p += 4;
       }
       if (off == 0 || off > o || o + len > ulen) { bad = true; break; }
       const int64_t src = o - off;
-      if (src + (off < len ? off : len) > fenced) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        fenced = o;
-      }
-      if (off >= len) {
-        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + i];
+      if (off <= SNAP_RING) {
+        // len <= 64: one step; every lane reads before any lane writes
+        const int64_t i = lane;
+        uint8_t v = 0;
+        if (i < len) v = ring[(src + (off < len ? i % off : i)) & (SNAP_RING - 1)];
+        __syncthreads();
+        if (i < len) { ring[(o + i) & (SNAP_RING - 1)] = v; out[o + i] = v; }
       } else {
-        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + (i % off)];
+        if (src + (off < len ? off : len) > fenced) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          fenced = o;
+        }
+        for (int64_t i = lane; i < len; i += 64) {
+          const uint8_t v = out[src + (off < len ? i % off : i)];
+          ring[(o + i) & (SNAP_RING - 1)] = v;
+          out[o + i] = v;
+        }
       }
     }
+    __syncthreads();
     o += len;
   }
   if (o != ulen) bad = true;
