@@ -19,7 +19,8 @@
 
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
-void launch_snappy(const DChunk*, DPage*, int, uint8_t*, hipStream_t);
+void launch_snappy(const DChunk*, DPage*, uint8_t*, int, const int32_t*, const int32_t*, int, const int2*, int64_t*,
+                   int32_t*, hipStream_t);
 void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
@@ -425,6 +426,9 @@ struct dk_parquet {
   std::vector<DColumn> h_cols;
   std::vector<int> col_file;
   DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp, d_tiles;
+  // snappy: compressed pages, their 64 KiB fragment bases / work items / starts, serial flags
+  DBuf d_cpage, d_fbase, d_fwork, d_fstart, d_serial;
+  int n_cpages = 0, n_frags = 0;
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
   int n_ltiles = 0;
   DBuf d_pchunks;            // string-position chunks (DPosChunk)
@@ -488,7 +492,11 @@ static int run_pipeline(dk_parquet* p, int mode) {
   int n = p->n_pages;
   { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
   if (mode == -1) return 0;
-  if (p->has_compressed) { KTimer::Scope sc(&T, 13, s); launch_snappy(C, P, n, p->d_arena.as<uint8_t>(), s); }
+  if (p->has_compressed) {
+    KTimer::Scope sc(&T, 13, s);
+    launch_snappy(C, P, p->d_arena.as<uint8_t>(), p->n_cpages, p->d_cpage.as<int32_t>(), p->d_fbase.as<int32_t>(),
+                  p->n_frags, p->d_fwork.as<int2>(), p->d_fstart.as<int64_t>(), p->d_serial.as<int32_t>(), s);
+  }
   { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P, n, arena, runs, s); }
   { KTimer::Scope sc(&T, 2, s); per_column_tiles(p, [&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols, p->n_cols, P, LT, st, s); }
@@ -552,6 +560,8 @@ static int prepare(dk_parquet* p) {
                   std::to_string(file_offset(f, pg.hdr_off)) + ")");
   }
   int64_t posn = 0, arena_n = 0, dbp_n = 0;
+  std::vector<int32_t> cpage, fbase(1, 0);
+  std::vector<int2> fwork;
   for (size_t i = 0; i < p->h_pages.size(); i++) {
     DPage& pg = p->h_pages[i];
     DChunk& ck = p->h_chunks[pg.chunk];
@@ -564,6 +574,12 @@ static int prepare(dk_parquet* p) {
         pg.unc_off = arena_n;
         arena_n += ((int64_t)pg.usize + 15) & ~(int64_t)15;
         p->has_compressed = true;
+        const int64_t lv = pg.ptype == PAGE_DATA_V2 ? (int64_t)pg.rl_len + pg.dl_len : 0;
+        const int64_t body = pg.usize > lv ? pg.usize - lv : 0;
+        const int nf = body > 0 ? (int)((body + 65535) / 65536) : 1;   // k_snappy_* fragments (64 KiB)
+        for (int k = 0; k < nf; k++) fwork.push_back(make_int2((int)cpage.size(), k));
+        cpage.push_back((int32_t)i);
+        fbase.push_back(fbase.back() + nf);
       }
       pg.status = PS_OK;
     }
@@ -624,6 +640,14 @@ static int prepare(dk_parquet* p) {
   }
   if (p->d_pos.alloc((size_t)(posn + 16) * 4)) return 1;
   if (p->d_arena.alloc((size_t)arena_n + 256)) return 1;
+  p->n_cpages = (int)cpage.size();
+  p->n_frags = (int)fwork.size();
+  if (p->n_cpages) {
+    if (upload(p->d_cpage, cpage.data(), cpage.size() * 4, s) || upload(p->d_fbase, fbase.data(), fbase.size() * 4, s) ||
+        upload(p->d_fwork, fwork.data(), fwork.size() * sizeof(int2), s) || p->d_fstart.alloc(fwork.size() * 8) ||
+        p->d_serial.alloc(cpage.size() * 4))
+      return 1;
+  }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
   p->bytes_arena = arena_n;
   if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;

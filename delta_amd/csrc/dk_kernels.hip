@@ -5,7 +5,7 @@
 // work bounded by HBM bandwidth; there is no dense contraction, so no MFMA.
 // Pipeline per replay step:
 //   k_page_headers      Thrift PageHeader parse, one lane per page
-//   k_snappy            raw snappy blocks, one wave per compressed page
+//   k_snappy_*          raw snappy blocks: split into 64 KiB fragments, one wave per fragment
 //   k_page_runs         run tables of the rep / def / dictionary-index hybrid streams
 //   k_pos_*             PLAIN BYTE_ARRAY entry positions, 16 KiB chunks: speculative zero-run
 //                       candidates + exact chain verification, sequential fallback
@@ -165,24 +165,204 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
   pages[i] = pg;
 }
 
-// --------------------------------------------------------------------------------------------
-// K1b: SNAPPY raw-block decompression, one wave64 per compressed page.
-// Tag parsing is a serial chain, so every byte the chain touches lives in LDS: the compressed
-// stream is staged through an 8 KiB window (refilled with coalesced dword loads), and the last
-// 64 KiB of output -- the reach of every offset the snappy compressor emits (it works on 64 KiB
-// fragments) -- sit in an LDS ring that back references read. Output goes to HBM with plain
-// stores that nothing in this kernel reads back, except a copy whose offset exceeds the ring
-// (legal in the format, never produced by snappy): that one reads HBM after a workgroup fence.
-// All lanes parse the same tag (uniform control flow); the wave copies 64 bytes per step.
-// --------------------------------------------------------------------------------------------
-constexpr int SNAP_RING = 65536;
-constexpr int SNAP_WIN = 8192;
+constexpr int SNAP_FRAG = 65536;
+constexpr int SNAP_WIN = 4096;
 
-__global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                               uint8_t* __restrict__ arena) {
-  __shared__ uint8_t ring[SNAP_RING];
+// compressed-stream window in LDS: in-offsets [ws, ws + SNAP_WIN) (ws may precede the stream start
+// by up to 3 bytes: the window is filled with aligned dword loads, never past the stream end)
+struct SnapWin {
+  const uint8_t* in;
+  int64_t clen, ws;
+  uint32_t* win;
+  __device__ __forceinline__ void refill(int64_t at) {
+    const uintptr_t a4 = ((uintptr_t)(in + at)) & ~(uintptr_t)3;
+    ws = at - (int64_t)((uintptr_t)(in + at) - a4);
+    const uintptr_t lim = (uintptr_t)(in + clen);
+    __syncthreads();
+#pragma unroll 4
+    for (int q = threadIdx.x; q < SNAP_WIN / 4; q += 64) {
+      const uintptr_t ad = a4 + (uintptr_t)q * 4;
+      if (ad < lim) win[q] = *(const uint32_t*)ad;
+    }
+    __syncthreads();
+  }
+  __device__ __forceinline__ uint32_t b(int64_t at) const { return ((const uint8_t*)win)[at - ws]; }
+  __device__ __forceinline__ const uint8_t* ptr(int64_t at) const { return (const uint8_t*)win + (at - ws); }
+  __device__ __forceinline__ bool has(int64_t at, int64_t n) const { return at >= ws && at + n <= ws + SNAP_WIN; }
+};
+
+// one tag at p (wave-uniform). Literal: off = -1, *p -> first payload byte. Copy: *p -> next tag.
+__device__ __forceinline__ bool snap_tag(SnapWin& w, int64_t* pp, int64_t* len, int64_t* off) {
+  int64_t p = *pp;
+  const int64_t c = w.clen;
+  if ((p + 5 < c ? p + 5 : c) > w.ws + SNAP_WIN) w.refill(p);
+  const uint32_t tag = w.b(p);
+  const uint32_t b1 = p + 1 < c ? w.b(p + 1) : 0, b2 = p + 2 < c ? w.b(p + 2) : 0;
+  const uint32_t b3 = p + 3 < c ? w.b(p + 3) : 0, b4 = p + 4 < c ? w.b(p + 4) : 0;
+  p++;
+  const int kind = tag & 3;
+  *off = -1;
+  if (kind == 0) {
+    int64_t l = (tag >> 2) + 1;
+    if (l > 60) {
+      const int nb = (int)l - 60;
+      if (p + nb > c) return false;
+      l = (int64_t)b1 | (nb > 1 ? (int64_t)b2 << 8 : 0) | (nb > 2 ? (int64_t)b3 << 16 : 0) | (nb > 3 ? (int64_t)b4 << 24 : 0);
+      l += 1;
+      p += nb;
+    }
+    *len = l;
+  } else if (kind == 1) {
+    if (p + 1 > c) return false;
+    *len = ((tag >> 2) & 7) + 4;
+    *off = ((int64_t)(tag >> 5) << 8) | b1;
+    p += 1;
+  } else if (kind == 2) {
+    if (p + 2 > c) return false;
+    *len = (tag >> 2) + 1;
+    *off = (int64_t)b1 | ((int64_t)b2 << 8);
+    p += 2;
+  } else {
+    if (p + 4 > c) return false;
+    *len = (tag >> 2) + 1;
+    *off = (int64_t)b1 | ((int64_t)b2 << 8) | ((int64_t)b3 << 16) | ((int64_t)b4 << 24);
+    p += 4;
+  }
+  *pp = p;
+  return true;
+}
+
+__device__ __forceinline__ bool snap_stream(const DChunk& ck, const DPage& pg, const uint8_t* arena,
+                                            const uint8_t** in, int64_t* clen, uint8_t** out, int64_t* ulen,
+                                            int64_t* lv) {
+  *in = ck.file + pg.data_off;
+  *clen = pg.csize;
+  *out = (uint8_t*)arena + pg.unc_off;
+  *ulen = pg.usize;
+  *lv = (pg.ptype == PAGE_DATA_V2) ? (int64_t)pg.rl_len + pg.dl_len : 0;
+  if (*lv > *clen || *lv > *ulen) return false;
+  *in += *lv; *clen -= *lv; *out += *lv; *ulen -= *lv;
+  return true;
+}
+
+__global__ __launch_bounds__(64) void k_snappy_split(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+                                                     uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
+                                                     const int32_t* __restrict__ fbase, int64_t* __restrict__ fstart,
+                                                     int32_t* __restrict__ serial) {
   __shared__ uint32_t win[SNAP_WIN / 4];
-  DPage& pgw = pages[blockIdx.x];
+  const int ci = blockIdx.x, lane = threadIdx.x;
+  const DPage pg = pages[cpage[ci]];
+  const DChunk ck = chunks[pg.chunk];
+  const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
+  if (pg.status != PS_OK || !snap_stream(ck, pg, arena, &in, &clen, &out, &ulen, &lv)) {
+    if (lane == 0) serial[ci] = 1;
+    return;
+  }
+  for (int64_t i = lane; i < lv; i += 64) out[i - lv] = in[i - lv];   // v2 levels: stored uncompressed
+  const int nfrag = fbase[ci + 1] - fbase[ci];
+  int64_t* fs = fstart + fbase[ci];
+  SnapWin w{in, clen, 0, win};
+  w.refill(0);
+  int64_t p = 0;
+  uint64_t n = 0;
+  for (int sh = 0; sh < 35; sh += 7) {
+    if (p >= clen) break;
+    const uint32_t b = w.b(p++);
+    n |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) break;
+  }
+  bool bad = (int64_t)n != ulen;
+  int64_t o = 0;
+  int k = 0;
+  if (lane == 0) fs[0] = p;
+  while (!bad && p < clen) {
+    int64_t len, off;
+    if (!snap_tag(w, &p, &len, &off)) { bad = true; break; }
+    if (off < 0) {
+      if (p + len > clen) { bad = true; break; }
+      p += len;
+    } else if (off == 0 || off > o - (int64_t)k * SNAP_FRAG) { bad = true; break; }   // reaches before its fragment
+    if (o + len > ulen) { bad = true; break; }
+    const int64_t fend = (int64_t)(k + 1) * SNAP_FRAG;
+    if (o + len > fend) { bad = true; break; }                             // straddles a boundary
+    o += len;
+    if (o == fend && o < ulen) {
+      if (++k >= nfrag) { bad = true; break; }
+      if (lane == 0) fs[k] = p;
+    }
+  }
+  if (o != ulen || k + 1 != nfrag) bad = true;
+  if (lane == 0) serial[ci] = bad ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void k_snappy_frag(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
+                                                    uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
+                                                    const int2* __restrict__ work, const int32_t* __restrict__ fbase,
+                                                    const int64_t* __restrict__ fstart, const int32_t* __restrict__ serial) {
+  __shared__ uint32_t win[SNAP_WIN / 4];
+  const int2 wk = work[blockIdx.x];            // (compressed-page index, fragment)
+  if (serial[wk.x]) return;
+  const int lane = threadIdx.x;
+  const DPage pg = pages[cpage[wk.x]];
+  const DChunk ck = chunks[pg.chunk];
+  const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
+  snap_stream(ck, pg, arena, &in, &clen, &out, &ulen, &lv);
+  int64_t p = fstart[fbase[wk.x] + wk.y];
+  const int64_t o0 = (int64_t)wk.y * SNAP_FRAG;
+  const int64_t o1 = o0 + SNAP_FRAG < ulen ? o0 + SNAP_FRAG : ulen;
+  SnapWin w{in, clen, 0, win};
+  w.refill(p);
+  int64_t o = o0, fenced = o0;
+  while (o < o1) {                              // the split pass validated every tag of the fragment
+    int64_t len, off;
+    snap_tag(w, &p, &len, &off);
+    if (off < 0) {
+      if (!w.has(p, len) && len <= SNAP_WIN - 64) w.refill(p);
+      if (w.has(p, len)) {
+        const uint8_t* src = w.ptr(p);
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = src[i];
+      } else {
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = in[p + i];
+      }
+      p += len;
+    } else {
+      const int64_t src = o - off;
+      if (src + (off < len ? off : len) > fenced) {   // reads bytes this wave stored
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        fenced = o;
+      }
+      if (off >= len) {
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + i];
+      } else {
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + (i % off)];
+      }
+    }
+    o += len;
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// K1b: SNAPPY raw-block decompression.
+//   k_snappy_split   one wave per compressed page walks the tags (no copies) through an LDS window
+//                    and records where each 64 KiB output fragment starts in the compressed stream.
+//                    Google's compressor encodes every 64 KiB input fragment on its own (fresh hash
+//                    table; no tag straddles, no copy reaches across, a fragment boundary), so the
+//                    fragments decode independently. A page that breaks this (legal in the format,
+//                    never produced by snappy) or is malformed is flagged for the serial path.
+//   k_snappy_frag    one wave per fragment decodes it into the arena.
+//   k_snappy_serial  flagged pages: one wave64 decodes the whole page (and reports errors).
+// Serial path:
+// Every lane parses the same tag (uniform control flow; same-address loads coalesce into one
+// transaction), then the wave copies the literal / back-reference 64 bytes per step. Back
+// references read bytes other lanes stored earlier, so a workgroup-scope acq_rel fence orders
+// them whenever the source range reaches past the last fenced output position.
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_snappy_serial(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
+                                                      uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
+                                                      const int32_t* __restrict__ serial) {
+  if (!serial[blockIdx.x]) return;
+  DPage& pgw = pages[cpage[blockIdx.x]];
   const DPage pg = pgw;                            // by value: byte stores below may alias
   if (pg.unc_off < 0 || pg.status != PS_OK) return;
   const DChunk ck = chunks[pg.chunk];
@@ -199,101 +379,64 @@ __global__ __launch_bounds__(64) void k_snappy(const DChunk* __restrict__ chunks
     for (int64_t i = lane; i < clen; i += 64) out[i] = in[i];
     return;
   }
-  const uint8_t* wbytes = (const uint8_t*)win;
-  // window: in-offsets [ws, ws + SNAP_WIN) (ws may sit up to 3 bytes before the stream start)
-  int64_t ws = 0;
-  auto refill = [&](int64_t at) {
-    const uintptr_t a4 = ((uintptr_t)(in + at)) & ~(uintptr_t)3;
-    ws = at - (int64_t)((uintptr_t)(in + at) - a4);
-    const uintptr_t lim = (uintptr_t)(in + clen);   // never load past the stream
-    __syncthreads();
-#pragma unroll 4
-    for (int q = lane; q < SNAP_WIN / 4; q += 64) {
-      const uintptr_t ad = a4 + (uintptr_t)q * 4;
-      if (ad < lim) win[q] = *(const uint32_t*)ad;
-    }
-    __syncthreads();
-  };
-  auto B = [&](int64_t at) -> uint32_t { return wbytes[at - ws]; };
-  refill(0);
   // preamble: varint uncompressed length
   int64_t p = 0;
   uint64_t n = 0;
-  for (int sh = 0; sh < 35; sh += 7) {
+  for (int s = 0; s < 35; s += 7) {
     if (p >= clen) break;
-    const uint32_t b = B(p++);
-    n |= (uint64_t)(b & 0x7f) << sh;
+    uint8_t b = in[p++];
+    n |= (uint64_t)(b & 0x7f) << s;
     if (!(b & 0x80)) break;
   }
   bool bad = (int64_t)n != ulen;
   int64_t o = 0, fenced = 0;
   while (!bad && p < clen) {
-    if ((p + 5 < clen ? p + 5 : clen) > ws + SNAP_WIN) refill(p);
-    const uint32_t tag = B(p);
-    const uint32_t b1 = p + 1 < clen ? B(p + 1) : 0, b2 = p + 2 < clen ? B(p + 2) : 0;
-    const uint32_t b3 = p + 3 < clen ? B(p + 3) : 0, b4 = p + 4 < clen ? B(p + 4) : 0;
-    p++;
+    const uint8_t tag = in[p++];
     const int kind = tag & 3;
     int64_t len, off = 0;
     if (kind == 0) {
       len = (tag >> 2) + 1;
       if (len > 60) {
-        const int nb = (int)len - 60;
+        int nb = (int)len - 60;
         if (p + nb > clen) { bad = true; break; }
-        len = (int64_t)b1 | (nb > 1 ? (int64_t)b2 << 8 : 0) | (nb > 2 ? (int64_t)b3 << 16 : 0) |
-              (nb > 3 ? (int64_t)b4 << 24 : 0);
+        len = 0;
+        for (int k = 0; k < nb; k++) len |= (int64_t)in[p + k] << (8 * k);
         len += 1;
         p += nb;
       }
       if (p + len > clen || o + len > ulen) { bad = true; break; }
-      if (p + len > ws + SNAP_WIN && len <= SNAP_WIN - 64) refill(p);
-      const bool from_win = p + len <= ws + SNAP_WIN;
-      for (int64_t i = lane; i < len; i += 64) {
-        const uint8_t v = from_win ? wbytes[p + i - ws] : in[p + i];
-        ring[(o + i) & (SNAP_RING - 1)] = v;
-        out[o + i] = v;
-      }
+      for (int64_t i = lane; i < len; i += 64) out[o + i] = in[p + i];
       p += len;
     } else {
       if (kind == 1) {
         if (p + 1 > clen) { bad = true; break; }
         len = ((tag >> 2) & 7) + 4;
-        off = ((int64_t)(tag >> 5) << 8) | b1;
+        off = ((int64_t)(tag >> 5) << 8) | in[p];
         p += 1;
       } else if (kind == 2) {
         if (p + 2 > clen) { bad = true; break; }
         len = (tag >> 2) + 1;
-        off = (int64_t)b1 | ((int64_t)b2 << 8);
+        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8);
         p += 2;
       } else {
         if (p + 4 > clen) { bad = true; break; }
         len = (tag >> 2) + 1;
-        off = (int64_t)b1 | ((int64_t)b2 << 8) | ((int64_t)b3 << 16) | ((int64_t)b4 << 24);
+        off = (int64_t)in[p] | ((int64_t)in[p + 1] << 8) | ((int64_t)in[p + 2] << 16) | ((int64_t)in[p + 3] << 24);
         p += 4;
       }
       if (off == 0 || off > o || o + len > ulen) { bad = true; break; }
       const int64_t src = o - off;
-      if (off <= SNAP_RING) {
-        // len <= 64: one step; every lane reads before any lane writes
-        const int64_t i = lane;
-        uint8_t v = 0;
-        if (i < len) v = ring[(src + (off < len ? i % off : i)) & (SNAP_RING - 1)];
-        __syncthreads();
-        if (i < len) { ring[(o + i) & (SNAP_RING - 1)] = v; out[o + i] = v; }
+      if (src + (off < len ? off : len) > fenced) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        fenced = o;
+      }
+      if (off >= len) {
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + i];
       } else {
-        if (src + (off < len ? off : len) > fenced) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-          fenced = o;
-        }
-        for (int64_t i = lane; i < len; i += 64) {
-          const uint8_t v = out[src + (off < len ? i % off : i)];
-          ring[(o + i) & (SNAP_RING - 1)] = v;
-          out[o + i] = v;
-        }
+        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + (i % off)];
       }
     }
-    __syncthreads();
     o += len;
   }
   if (o != ulen) bad = true;
@@ -2124,8 +2267,12 @@ namespace dk {
 void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
 }
-void launch_snappy(const DChunk* c, DPage* p, int n, uint8_t* arena, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_snappy, dim3(n), dim3(64), 0, s, c, p, arena);
+void launch_snappy(const DChunk* c, DPage* p, uint8_t* arena, int n_cp, const int32_t* cpage, const int32_t* fbase,
+                   int n_frag, const int2* work, int64_t* fstart, int32_t* serial, hipStream_t s) {
+  if (!n_cp) return;
+  hipLaunchKernelGGL(k_snappy_split, dim3(n_cp), dim3(64), 0, s, c, p, arena, cpage, fbase, fstart, serial);
+  if (n_frag) hipLaunchKernelGGL(k_snappy_frag, dim3(n_frag), dim3(64), 0, s, c, p, arena, cpage, work, fbase, fstart, serial);
+  hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, c, p, arena, cpage, serial);
 }
 void launch_positions(const DChunk* c, DPage* p, int n_pages, const uint8_t* arena, int32_t* pos, DPosChunk* pcs,
                       int npc, hipStream_t s) {
