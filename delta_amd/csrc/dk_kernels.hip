@@ -196,9 +196,14 @@ __device__ __forceinline__ bool snap_tag(SnapWin& w, int64_t* pp, int64_t* len, 
   int64_t p = *pp;
   const int64_t c = w.clen;
   if ((p + 5 < c ? p + 5 : c) > w.ws + SNAP_WIN) w.refill(p);
-  const uint32_t tag = w.b(p);
-  const uint32_t b1 = p + 1 < c ? w.b(p + 1) : 0, b2 = p + 2 < c ? w.b(p + 2) : 0;
-  const uint32_t b3 = p + 3 < c ? w.b(p + 3) : 0, b4 = p + 4 < c ? w.b(p + 4) : 0;
+  // the tag and its 4 argument bytes from two aligned LDS dwords (one round trip), made scalar;
+  // bytes past the stream end are never used (the length checks below come first)
+  const int64_t ix = p - w.ws;
+  const uint32_t d0 = __builtin_amdgcn_readfirstlane(w.win[ix >> 2]);
+  const uint32_t d1 = __builtin_amdgcn_readfirstlane(w.win[(ix >> 2) + 1]);
+  const uint64_t q = (((uint64_t)d1 << 32) | d0) >> (8 * (ix & 3));
+  const uint32_t tag = (uint32_t)q & 0xff, b1 = (uint32_t)(q >> 8) & 0xff, b2 = (uint32_t)(q >> 16) & 0xff;
+  const uint32_t b3 = (uint32_t)(q >> 24) & 0xff, b4 = (uint32_t)(q >> 32) & 0xff;
   p++;
   const int kind = tag & 3;
   *off = -1;
@@ -249,7 +254,7 @@ __global__ __launch_bounds__(64) void k_snappy_split(const DChunk* __restrict__ 
                                                      uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
                                                      const int32_t* __restrict__ fbase, int64_t* __restrict__ fstart,
                                                      int32_t* __restrict__ serial) {
-  __shared__ uint32_t win[SNAP_WIN / 4];
+  __shared__ uint32_t win[SNAP_WIN / 4 + 1];
   const int ci = blockIdx.x, lane = threadIdx.x;
   const DPage pg = pages[cpage[ci]];
   const DChunk ck = chunks[pg.chunk];
@@ -299,7 +304,7 @@ __global__ __launch_bounds__(64) void k_snappy_frag(const DChunk* __restrict__ c
                                                     uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
                                                     const int2* __restrict__ work, const int32_t* __restrict__ fbase,
                                                     const int64_t* __restrict__ fstart, const int32_t* __restrict__ serial) {
-  __shared__ uint32_t win[SNAP_WIN / 4];
+  __shared__ uint32_t win[SNAP_WIN / 4 + 1];
   const int2 wk = work[blockIdx.x];            // (compressed-page index, fragment)
   if (serial[wk.x]) return;
   const int lane = threadIdx.x;
