@@ -280,21 +280,64 @@ __global__ __launch_bounds__(64) void k_snappy_split(const DChunk* __restrict__ 
   int64_t o = 0;
   int k = 0;
   if (lane == 0) fs[0] = p;
+  // Window-parallel walk: every lane parses a tag speculatively at p + lane (header bytes from two
+  // aligned LDS dwords); the true chain then hops through the 64 candidates with readlane (a few
+  // scalar cycles per tag instead of an LDS round trip plus a full parse).
   while (!bad && p < clen) {
-    int64_t len, off;
-    if (!snap_tag(w, &p, &len, &off)) { bad = true; break; }
-    if (off < 0) {
-      if (p + len > clen) { bad = true; break; }
-      p += len;
-    } else if (off == 0 || off > o - (int64_t)k * SNAP_FRAG) { bad = true; break; }   // reaches before its fragment
-    if (o + len > ulen) { bad = true; break; }
-    const int64_t fend = (int64_t)(k + 1) * SNAP_FRAG;
-    if (o + len > fend) { bad = true; break; }                             // straddles a boundary
-    o += len;
-    if (o == fend && o < ulen) {
-      if (++k >= nfrag) { bad = true; break; }
-      if (lane == 0) fs[k] = p;
+    if ((p + 69 < clen ? p + 69 : clen) > w.ws + SNAP_WIN) w.refill(p);
+    const int64_t q = p + lane;
+    uint32_t adv = 0, olen = 0, ok = 0;
+    int32_t off = -1;
+    if (q < clen) {
+      const int64_t ix = q - w.ws;
+      const uint64_t d = ((((uint64_t)w.win[(ix >> 2) + 1]) << 32) | w.win[ix >> 2]) >> (8 * (ix & 3));
+      const uint32_t tag = (uint32_t)d & 0xff;
+      const int kind = tag & 3;
+      uint32_t hdr = 1;
+      int64_t l = 0;
+      if (kind == 0) {
+        l = (tag >> 2) + 1;
+        if (l > 60) {
+          const int nb = (int)l - 60;
+          hdr += nb;
+          l = (int64_t)((d >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
+        }
+        ok = (q + hdr + l <= clen) && l < (1ll << 30);
+        adv = hdr + (uint32_t)(ok ? l : 0);
+      } else if (kind == 1) {
+        hdr = 2; l = ((tag >> 2) & 7) + 4; off = (int32_t)((((tag >> 5) & 7u) << 8) | ((d >> 8) & 0xff));
+        ok = q + 2 <= clen; adv = hdr;
+      } else if (kind == 2) {
+        hdr = 3; l = (tag >> 2) + 1; off = (int32_t)((d >> 8) & 0xffff);
+        ok = q + 3 <= clen; adv = hdr;
+      } else {
+        hdr = 5; l = (tag >> 2) + 1;
+        const uint64_t o32 = (d >> 8) & 0xffffffffull;
+        off = o32 > 0x7fffffffull ? 0x7fffffff : (int32_t)o32;
+        ok = q + 5 <= clen; adv = hdr;
+      }
+      olen = (uint32_t)l;
     }
+    int64_t j = 0;
+    while (j < 64 && p + j < clen) {
+      const int jl = (int)j;
+      const uint32_t t_ok = __builtin_amdgcn_readlane(ok, jl);
+      const uint32_t t_adv = __builtin_amdgcn_readlane(adv, jl);
+      const int64_t t_len = (int64_t)__builtin_amdgcn_readlane(olen, jl);
+      const int32_t t_off = (int32_t)__builtin_amdgcn_readlane((uint32_t)off, jl);
+      if (!t_ok) { bad = true; break; }
+      if (t_off >= 0 && (t_off == 0 || t_off > o - (int64_t)k * SNAP_FRAG)) { bad = true; break; }   // reaches before its fragment
+      if (o + t_len > ulen) { bad = true; break; }
+      const int64_t fend = (int64_t)(k + 1) * SNAP_FRAG;
+      if (o + t_len > fend) { bad = true; break; }                           // straddles a boundary
+      o += t_len;
+      j += t_adv;
+      if (o == fend && o < ulen) {
+        if (++k >= nfrag) { bad = true; break; }
+        if (lane == 0) fs[k] = p + j;
+      }
+    }
+    p += j;
   }
   if (o != ulen || k + 1 != nfrag) bad = true;
   if (lane == 0) serial[ci] = bad ? 1 : 0;
