@@ -48,8 +48,9 @@ CONFIGS = {
                desc="C3: %d-AddFile 64-part snappy checkpoint sharded over the GPUs by part, 1k commits "
                     "(100 adds + 100 removes each); read schema add(no stats)+remove"),
     "c4": dict(rows=50_000_000, shared=False, stats=True, predicate=("id", ">", 25_000_000),
-               spec=dict(dv_frac=0.3, with_stats=True, n_commits=100, adds_per_commit=50, removes_per_commit=50),
-               desc="C4: %d-AddFile checkpoint per GPU, 30%% with deletion vectors, predicate id > 25000000 "
+               spec=dict(n_parts=8, dv_frac=0.3, with_stats=True, n_commits=100, adds_per_commit=50,
+                         removes_per_commit=50),
+               desc="C4: %d-AddFile 8-part checkpoint per GPU, 30%% with deletion vectors, predicate id > 25000000 "
                     "over stats; read schema add(with stats)+remove"),
     "c5": dict(rows=10_000_000, shared=True, stats=False, predicate=None,
                spec=dict(n_parts=16, v2_sidecars=16, compression="snappy", data_page_version="2.0",
