@@ -484,7 +484,8 @@ def write_table(root: str, spec: TableSpec):
         f.write(json.dumps(lc))
 
     # ---- JSON commit tail ----
-    ck_all = pa.concat_arrays(ck_paths) if len(ck_paths) > 1 else ck_paths[0]
+    # large_string: the concatenated paths of a 50M+ row checkpoint exceed 2 GiB of chars
+    ck_all = pa.concat_arrays([a.cast(pa.large_string()) for a in ck_paths]) if len(ck_paths) > 1 else ck_paths[0]
     n_ck = len(ck_all)
     new_serial = 0
     added_in_tail = []      # paths added by commits (candidates for duplicates / removal)
