@@ -1724,6 +1724,51 @@ __device__ bool js_small_exact(const uint8_t* s, int32_t i, int32_t e, long long
   return true;
 }
 
+// A date stats value: DefaultJsonRow.java:249-252 decodes it as
+// InternalUtils.daysSinceEpoch(java.sql.Date.valueOf(text)) (InternalUtils.java:85-89). valueOf takes
+// "yyyy-[m]m-[d]d" (a 4-char year, 1-2 char month and day, each an Integer.parseInt field that may
+// carry a '+'), month 1..12 and day 1..31, and the lenient calendar carries a day past the month's
+// end into the next month (2021-02-30 -> 2021-03-02). Years before 1583 go through the Julian part of
+// the hybrid calendar, which this build does not restate: they are a decode error here (as are
+// escaped or non-ASCII-digit strings), see DESIGN.md 4.1.
+__device__ bool js_date_field(const uint8_t* s, int32_t a, int32_t b, long long* v) {
+  if (b - a >= 2 && s[a] == '+') a++;               // Integer.parseInt: a lone sign is malformed
+  if (a >= b) return false;
+  long long x = 0;
+  for (int32_t k = a; k < b; k++) {
+    if (s[k] < '0' || s[k] > '9') return false;
+    x = x * 10 + (s[k] - '0');
+  }
+  *v = x;
+  return true;
+}
+
+__device__ long long civil_days(long long y, long long m, long long d) {   // proleptic Gregorian
+  y -= m <= 2;
+  const long long era = (y >= 0 ? y : y - 399) / 400;
+  const long long yoe = y - era * 400;
+  const long long doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const long long doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + doe - 719468;
+}
+
+__device__ bool js_date(const uint8_t* s, int32_t a, int32_t b, long long* v) {   // content s[a, b)
+  const int32_t len = b - a;
+  int32_t d1 = -1, d2 = -1;
+  for (int32_t k = a; k < b; k++)
+    if (s[k] == '-') { if (d1 < 0) d1 = k - a; else { d2 = k - a; break; } }
+  if (!(d1 > 0 && d2 > 0 && d2 < len - 1)) return false;
+  if (!(d1 == 4 && d2 - d1 > 1 && d2 - d1 <= 3 && len - d2 > 1 && len - d2 <= 3)) return false;
+  long long y, m, d;
+  if (!js_date_field(s, a, a + 4, &y) || !js_date_field(s, a + d1 + 1, a + d2, &m) ||
+      !js_date_field(s, a + d2 + 1, b, &d))
+    return false;
+  if (m < 1 || m > 12 || d < 1 || d > 31) return false;
+  if (y < 1583) return false;                         // Julian / cutover dates: not restated
+  *v = civil_days(y, m, 1) + d - 1;
+  return true;
+}
+
 // extract the program's stats fields from one JSON object; returns false on a decode error
 __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long long* val, uint32_t* set) {
   uint32_t mstack[JS_MAXD];
@@ -1785,10 +1830,20 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
         continue;
       }
       if (c == '"') {
-        if (leaf || pre) return false;                // a string where a number / struct is expected
+        if (pre) return false;                        // a string where a struct is expected
         bool esc;
         const int32_t e = js_skip_string(s, n, i, &esc);
         if (e < 0) return false;
+        if (leaf) {
+          for (int p = 0; p < P.n_paths; p++)
+            if ((leaf >> p) & 1) {
+              if (P.path_type[p] != SK_DATE || esc) return false;   // only dates are textual
+              long long v;
+              if (!js_date(s, i + 1, e - 1, &v)) return false;
+              val[p] = v;
+              *set |= 1u << p;
+            }
+        }
         i = e;
       } else if (c == '-' || (c >= '0' && c <= '9')) {
         if (pre) return false;
@@ -1800,6 +1855,7 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
           for (int p = 0; p < P.n_paths; p++)
             if ((leaf >> p) & 1) {
               const int t = P.path_type[p];
+              if (t == SK_DATE) return false;         // a date must be a JSON string
               if (t == SK_SHORT || t == SK_BYTE) {
                 if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
               } else if (!integral || !fits) {

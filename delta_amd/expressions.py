@@ -42,6 +42,10 @@ class Literal:
         return Literal(int(v), "byte")
 
     @staticmethod
+    def ofDate(days_since_epoch):                      # Literal.ofDate(int daysSinceEpochUTC)
+        return Literal(int(days_since_epoch), "date")
+
+    @staticmethod
     def ofString(v):
         return Literal(str(v), "string")
 

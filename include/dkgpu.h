@@ -107,7 +107,7 @@ void dk_json_tail_free(dk_json_tail* t);
  * COALESCE(program(stats), true); null / absent stats keep the row. */
 typedef struct dk_skip_program {
   int32_t n_paths;                 /* <= 8 stats fields                                        */
-  int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte                       */
+  int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte, 4 date (epoch days) */
   int32_t path_depth[8];           /* name components, 1..4 ("maxValues","id" -> 2)             */
   int32_t name_off[8][4];          /* component names: offsets / lengths into names (UTF-8)     */
   int32_t name_len[8][4];

@@ -10,7 +10,8 @@ does with a data-skipping predicate once the scan files are reconciled.
       must be an object
   DefaultJsonRow.decodeElement          kernel-defaults/.../internal/data/DefaultJsonRow.java:136-270
       long/integer: an integral token in range; short/byte: any number whose exact value is an
-      integer in range (canConvertToExactIntegral); struct: an object; JSON null = null
+      integer in range (canConvertToExactIntegral); date: a string through java.sql.Date.valueOf
+      (:249-252); struct: an object; JSON null = null
   DefaultExpressionEvaluator            kernel-defaults/.../internal/expressions/
       comparators are null when either side is null; AND/OR are Kleene (visitAnd/visitOr)
 
@@ -20,6 +21,7 @@ Nothing here is used by the product path.
 """
 from __future__ import annotations
 
+import datetime as _dt
 import json
 from decimal import Decimal
 
@@ -51,9 +53,37 @@ def parse_root(s: str):
     return obj
 
 
+def _date_field(t):
+    if len(t) >= 2 and t[0] == "+":                   # Integer.parseInt accepts a leading '+'
+        t = t[1:]
+    if not t or any(c not in "0123456789" for c in t):
+        raise StatsDecodeError("Couldn't decode %r, expected a date" % t)
+    return int(t)
+
+
+def _date(text):
+    """InternalUtils.daysSinceEpoch(java.sql.Date.valueOf(text)): DefaultJsonRow.java:249-252,
+    InternalUtils.java:85-89. valueOf: a 4-char year, 1-2 char month and day, month 1..12, day
+    1..31; the lenient calendar carries a day past the month end into the next month. Years before
+    1583 (Julian part of the hybrid calendar) and non-ASCII digits are refused by this build."""
+    n = len(text)
+    d1 = text.find("-")
+    d2 = text.find("-", d1 + 1)
+    if not (d1 > 0 and d2 > 0 and d2 < n - 1 and d1 == 4 and 1 < d2 - d1 <= 3 and 1 < n - d2 <= 3):
+        raise StatsDecodeError("Couldn't decode %r, expected a date" % text)
+    y, m, d = _date_field(text[:4]), _date_field(text[d1 + 1:d2]), _date_field(text[d2 + 1:])
+    if not (1 <= m <= 12 and 1 <= d <= 31) or y < 1583:
+        raise StatsDecodeError("Couldn't decode %r, expected a date" % text)
+    return (_dt.date(y, m, 1) - _dt.date(1970, 1, 1)).days + d - 1
+
+
 def _leaf(v, typ):
     if v is None:
         return None
+    if typ == "date":
+        if not isinstance(v, str):
+            raise StatsDecodeError("Couldn't decode %r, expected a date" % (v,))
+        return _date(v)
     lo, hi = RANGES[typ]
     if isinstance(v, bool) or not isinstance(v, (int, Decimal)):
         raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))

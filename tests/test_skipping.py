@@ -3,8 +3,8 @@
 Pinned to the reference's own expectations on its golden tables (KDT = kernel-defaults/src/test/scala/
 io/delta/kernel/defaults):
   ScanSuite.scala:1150-1196  basic data skipping for all types (+ column mapping name/id, checkpoint):
-                             hits / misses for int, long, byte, short (the integral types the GPU
-                             evaluator decodes; float/double/string/date/decimal filters are refused)
+                             hits / misses for int, long, byte, short and date (the types the GPU
+                             evaluator decodes; float/double/string/decimal filters are refused)
   ScanSuite.scala:1233-1239  filter on a non-existent column -> no skipping
   ScanSuite.scala:1243-1253  AND of two data columns -> 1 file
   ScanSuite.scala:1255-1267  stats collected changing across versions -> 1 / 2 / 1 files
@@ -37,11 +37,21 @@ def cmp(op, c, v):
     return Predicate(op, c, v)
 
 
+def _days(text):
+    import datetime
+    return (datetime.date.fromisoformat(text) - datetime.date(1970, 1, 1)).days
+
+
+# ScanSuite.scala:1158-1160: as_date value 2000-01-01, smaller 1999-01-01, bigger 2000-01-02
+DATES = tuple(Literal.ofDate(_days(t)) for t in ("2000-01-01", "1999-01-01", "2000-01-02"))
+
+
 def all_types_hits_misses():
-    """ScanSuite.scala:1150-1183: value in table 0, smaller -1, bigger 1."""
+    """ScanSuite.scala:1150-1183: value in table 0, smaller -1, bigger 1 (dates: DATES)."""
     hits, misses = [], []
-    for name, lit in INTEGRAL.items():
-        c, value, small, big = col(name), lit(0), lit(-1), lit(1)
+    cases = [(name, lit(0), lit(-1), lit(1)) for name, lit in INTEGRAL.items()] + [("as_date",) + DATES]
+    for name, value, small, big in cases:
+        c = col(name)
         misses += [cmp("=", c, small), cmp(">", c, value), cmp(">=", c, big), cmp("<", c, value),
                    cmp("<=", c, small)]
         hits += [cmp("=", c, value), cmp(">", c, small), cmp(">=", c, value), cmp("<", c, big),
@@ -157,6 +167,26 @@ def test_compile_refuses_unsupported():
     paths, types, ops = sk.compile_program(node, leaves)
     assert paths == [("minValues", "a"), ("maxValues", "a")] and types == [0, 0]
     assert [o[0] for o in ops] == [sk.OP_STAT, sk.OP_LIT, sk.OP_LE, sk.OP_STAT, sk.OP_LIT, sk.OP_GE, sk.OP_AND]
+
+
+def test_oracle_date_decoding_rules():
+    """java.sql.Date.valueOf + daysSinceEpoch (DefaultJsonRow.java:249-252): 1-2 char month/day, a
+    '+' sign on a field, lenient day carry; bad shapes and pre-1583 years raise."""
+    from oracle import skipping as osk
+    t = {("minValues", "d"): "date"}
+    for text, want in (("2000-01-01", "2000-01-01"), ("2000-1-2", "2000-01-02"), ("2021-02-30", "2021-03-02"),
+                       ("2020-02-30", "2020-03-01"), ("2000-+1-+9", "2000-01-09"), ("1970-01-01", "1970-01-01"),
+                       ("1583-01-01", "1583-01-01"), ("9999-12-31", "9999-12-31")):
+        got = osk.decode_stats('{"minValues":{"d":"%s"}}' % text, t)[("minValues", "d")]
+        assert got == _days(want), text
+    for bad in ("2000-13-01", "2000-00-10", "2000-01-32", "2000-01-0", "200-01-01", "2000-001-01",
+                "2000/01/01", "2000-01-", "-999-01-01", "1582-12-31", "+999-01-01", "2000-01-+",
+                "2000-01-01T00", ""):
+        with pytest.raises(osk.StatsDecodeError):
+            osk.decode_stats('{"minValues":{"d":"%s"}}' % bad, t)
+    for bad in ('{"minValues":{"d":10957}}', '{"minValues":{"d":true}}'):
+        with pytest.raises(osk.StatsDecodeError):
+            osk.decode_stats(bad, t)
 
 
 def test_pack_layout():
@@ -289,12 +319,12 @@ def test_gpu_synthetic_parity(tmp_path):
     eng.close()
 
 
-def _write_edge_table(root, stats_list):
+def _write_edge_table(root, stats_list, columns=(("x", "short"), ("id", "long"))):
     """A commit-only table whose adds carry the given raw stats strings (None = no stats)."""
     log = os.path.join(root, "_delta_log")
     os.makedirs(log)
-    schema = {"type": "struct", "fields": [{"name": "x", "type": "short", "nullable": True, "metadata": {}},
-                                           {"name": "id", "type": "long", "nullable": True, "metadata": {}}]}
+    schema = {"type": "struct", "fields": [{"name": n, "type": t, "nullable": True, "metadata": {}}
+                                           for n, t in columns]}
     with open(os.path.join(log, "%020d.json" % 0), "w") as f:
         f.write(json.dumps({"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}) + "\n")
         f.write(json.dumps({"metaData": {"id": "t", "format": {"provider": "parquet", "options": {}},
@@ -386,4 +416,61 @@ def test_gpu_stats_decode_errors_raise(tmp_path):
         _write_edge_table(root, [EDGE_STATS[0], bad])
         with pytest.raises(DkError, match="data skipping"):
             _gpu_files(root, BAD_PREDICATE, eng)
+    eng.close()
+
+
+DATE_COLUMNS = (("d", "date"), ("id", "long"))
+DATE_EDGE_STATS = [
+    '{"numRecords":2,"minValues":{"d":"2000-01-01","id":1},"maxValues":{"d":"2000-1-5","id":2}}',
+    '{"numRecords":2,"minValues":{"d":"2021-02-30"},"maxValues":{"d":"2021-3-+9"}}',
+    '{"numRecords":2,"minValues":{"d":null},"maxValues":{"d":"1999-12-31"},"nullCount":{"d":1}}',
+    '{"numRecords":2,"minValues":{"d":"2000-01-01","d":"2010-06-15"},"maxValues":{"d":"2020-01-01"}}',
+    '{"numRecords":2,"minValues":{"d":"1583-01-01"},"maxValues":{"d":"9999-12-31"},"nullCount":{"d":0}}',
+    None,
+]
+DATE_PREDICATES = [cmp("=", col("d"), Literal.ofDate(_days("2000-01-03"))),
+                   cmp(">", col("d"), Literal.ofDate(_days("2021-03-01"))),
+                   cmp("<", col("d"), Literal.ofDate(_days("2000-01-01"))),
+                   And(cmp(">=", col("d"), Literal.ofDate(_days("2010-06-15"))),
+                       cmp("<=", col("d"), Literal.ofDate(_days("2021-03-02")))),
+                   Predicate("IS_NULL", col("d")),
+                   Or(cmp("=", col("d"), Literal.ofDate(_days("1583-01-01"))), cmp("=", col("id"), Literal.ofLong(7)))]
+DATE_BAD_STATS = ['{"numRecords":2,"minValues":{"d":10957}}', '{"numRecords":2,"minValues":{"d":"1500-01-01"}}',
+                  '{"numRecords":2,"minValues":{"d":"2000-13-01"}}', '{"numRecords":2,"minValues":{"d":"2000-01"}}',
+                  '{"numRecords":2,"minValues":{"d":{"a":1}}}', '{"numRecords":2,"minValues":{"d":"2000-01-1x"}}']
+DATE_BAD_PREDICATE = cmp("<=", col("d"), Literal.ofDate(_days("2030-01-01")))
+
+
+def test_oracle_date_edge_cases_expected(tmp_path):
+    root = str(tmp_path / "t")
+    _write_edge_table(root, DATE_EDGE_STATS, DATE_COLUMNS)
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in DATE_PREDICATES]
+    assert got[0] == [0, 4, 5]                          # 2000-01-01 <= d <= 2000-01-05
+    assert got[1] == [1, 4, 5]                          # max > 2021-03-01 (row 1: 2021-3-+9)
+    assert got[2] == [2, 4, 5]                          # min < 2000-01-01 (row 2: null min -> kept)
+    assert got[3] == [1, 3, 4, 5]                       # row 1 min is 2021-03-02 (lenient carry)
+    assert got[4] == [0, 1, 2, 3, 5]                    # nullCount.d > 0 provably false only on row 4
+    assert got[5] == [1, 2, 3, 4, 5]                    # row 0: both sides provably false
+    for i, bad in enumerate(DATE_BAD_STATS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_edge_table(r, [DATE_EDGE_STATS[0], bad], DATE_COLUMNS)
+        from oracle import skipping as osk
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(r, DATE_BAD_PREDICATE)
+
+
+@pytest.mark.gpu
+def test_gpu_date_stats_parity(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_edge_table(root, DATE_EDGE_STATS, DATE_COLUMNS)
+    eng = K.GpuEngine()
+    for p in DATE_PREDICATES:
+        assert _gpu_files(root, p, eng) == oracle_files(root, p), p
+    for i, bad in enumerate(DATE_BAD_STATS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_edge_table(r, [DATE_EDGE_STATS[0], bad], DATE_COLUMNS)
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(r, DATE_BAD_PREDICATE, eng)
     eng.close()
