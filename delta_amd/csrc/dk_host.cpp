@@ -1700,7 +1700,7 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
   if (P.n_fields < 0 || P.n_fields > PP_MAX_FIELDS || P.n_ops <= 0 || P.n_ops > PP_MAX_OPS)
     return fail("dk_replay_set_partition_filter: bad program size");
   for (int f = 0; f < P.n_fields; f++)
-    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_STRING || P.name_off[f] < 0 || P.name_len[f] < 0 ||
+    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_DATE || P.name_off[f] < 0 || P.name_len[f] < 0 ||
         P.name_off[f] + P.name_len[f] > PP_POOL)
       return fail("dk_replay_set_partition_filter: bad field");
   int depth = 0;

@@ -2013,6 +2013,9 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
           const int ty = P.field_type[k];
           if (ty == PT_STRING) {
             f[k].kind = 2; f[k].p = vp; f[k].len = vl;
+          } else if (ty == PT_DATE) {                    // PartitionValueEvaluator.java:72-73
+            if (!js_date(vp, 0, vl, &f[k].v)) { *err = true; return -1; }
+            f[k].kind = 1;
           } else {
             const long long lo = ty == PT_LONG ? (-9223372036854775807ll - 1) : ty == PT_INT ? -2147483648ll
                                : ty == PT_SHORT ? -32768 : -128;

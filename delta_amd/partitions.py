@@ -6,8 +6,9 @@ element_at(add.partitionValues, <physical name>), deserialized to the column's t
 string) and compiled to the postfix program k_part_eval runs (ScanImpl.applyPartitionPruning,
 ScanImpl.java:247-294).
 
-Supported: partition columns of type string, long, integer, short, byte; literals of a matching
-kind (string with string, any integral with integral, or null); =, <, <=, >, >=, IS NOT DISTINCT
+Supported: partition columns of type string, long, integer, short, byte, date (values through
+java.sql.Date.valueOf, PartitionValueEvaluator.java:72-73); literals of a matching kind (string with
+string, any integral with integral, date with date, or null); =, <, <=, >, >=, IS NOT DISTINCT
 FROM, IS_NULL, IS_NOT_NULL, NOT, AND, OR. Anything else raises UnsupportedPartitionFilter, so an
 accepted filter is evaluated exactly as the reference evaluates it.
 """
@@ -17,7 +18,7 @@ import json
 
 from .expressions import Column, Literal, Predicate
 
-PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4}
+PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4, "date": 5}
 INTEGRAL = {"long", "integer", "short", "byte"}
 (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LT, PO_LE, PO_GT, PO_GE, PO_EQ, PO_NSEQ, PO_ISNULL,
  PO_ISNOTNULL, PO_NOT, PO_AND, PO_OR) = range(15)
@@ -63,7 +64,7 @@ def compile_program(pred: Predicate, fields: dict):
         if isinstance(node, Column):
             k, t = field(node)
             ops.append((PO_FIELD, k, 0))
-            return "string" if t == "string" else "integral"
+            return t if t in ("string", "date") else "integral"
         if isinstance(node, Literal):
             if node.value is None:
                 ops.append((PO_LIT_NULL, 0, 0))
@@ -73,9 +74,9 @@ def compile_program(pred: Predicate, fields: dict):
                 ops.append((PO_LIT_STR, len(b), len(pool)))
                 pool.extend(b)
                 return "string"
-            if node.type in INTEGRAL and isinstance(node.value, int) and not isinstance(node.value, bool):
-                ops.append((PO_LIT_INT, 0, int(node.value)))
-                return "integral"
+            if node.type in INTEGRAL | {"date"} and isinstance(node.value, int) and not isinstance(node.value, bool):
+                ops.append((PO_LIT_INT, 0, int(node.value)))   # a date literal is its epoch day
+                return "date" if node.type == "date" else "integral"
             raise UnsupportedPartitionFilter("partition pruning with a %s literal is not supported" % node.type)
         raise UnsupportedPartitionFilter("partition pruning on expression %r is not supported" % (node,))
 

@@ -124,7 +124,7 @@ typedef struct dk_skip_program {
  * A row stays selected iff the predicate is TRUE (null and false drop it). */
 typedef struct dk_part_program {
   int32_t n_fields;                /* <= 8 partition columns                                      */
-  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string                 */
+  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string, 5 date        */
   int32_t name_off[8];             /* physical column name (map key): offset / length in pool      */
   int32_t name_len[8];
   int32_t n_ops;                   /* <= 64                                                       */

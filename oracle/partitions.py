@@ -4,7 +4,8 @@
   PartitionUtils.rewritePartitionPredicateOnScanFileSchema (util/PartitionUtils.java:324-358):
       a partition column becomes element_at(add.partitionValues, physical name), deserialized by
       PartitionValueEvaluator (kernel-defaults/.../expressions/PartitionValueEvaluator.java:50-90:
-      Long/Integer/Short/Byte.parseX -- a malformed value fails the scan) unless it is a string
+      Long/Integer/Short/Byte.parseX, dates through java.sql.Date.valueOf (:72-73, restated in
+      oracle/skipping.py:_date) -- a malformed value fails the scan) unless it is a string
   DefaultExpressionEvaluator: comparators are null if a side is null (IS NOT DISTINCT FROM is
       null-safe), AND/OR/NOT are Kleene and are evaluated on every row of the batch; strings compare
       as unsigned UTF-8 bytes, then length (DefaultExpressionUtils.java:39-56)
@@ -41,6 +42,12 @@ def element_at(pv, key: bytes):
 def deserialize(v, typ):
     if v is None or typ == "string":
         return v
+    if typ == "date":                                  # PartitionValueEvaluator.java:72-73
+        from oracle.skipping import StatsDecodeError, _date
+        try:
+            return _date(v.decode("utf-8", "replace"))
+        except StatsDecodeError as e:
+            raise PartitionValueError(str(e)) from e
     if not _INT.match(v):
         raise PartitionValueError("For input string: %r" % v)
     x = int(v)

@@ -57,7 +57,10 @@ def test_partition_fields_and_compile():
     assert [pool[o:o + n] for o, n, _ in flist] == [b"col-p", b"s"] and [t for _, _, t in flist] == [1, 4]
     assert [o[0] for o in ops] == [pp.PO_FIELD, pp.PO_LIT_INT, pp.PO_GE, pp.PO_FIELD, pp.PO_LIT_STR, pp.PO_EQ,
                                    pp.PO_AND]
-    for bad in (cmp("=", col("d"), Literal(1, "date")), cmp("=", col("s"), Literal.ofInt(1)),
+    flist, ops, _ = pp.compile_program(cmp("<", col("d"), Literal.ofDate(10957)), f)
+    assert [t for _, _, t in flist] == [5] and ops[1] == (pp.PO_LIT_INT, 0, 10957)
+    for bad in (cmp("=", col("d"), Literal.ofInt(1)), cmp("=", col("s"), Literal.ofInt(1)),
+                cmp("=", col("d"), Literal.ofString("2000-01-01")),
                 Predicate("STARTS_WITH", col("s"), Literal.ofString("a"))):
         with pytest.raises(pp.UnsupportedPartitionFilter):
             pp.compile_program(bad, f)
@@ -219,4 +222,50 @@ def test_gpu_malformed_value_raises(tmp_path):
         _write_pv_table(root, [{"p": "1"}, {"p": bad}])
         with pytest.raises(DkError, match="partition"):
             _gpu_files(root, cmp("=", col("p"), Literal.ofInt(1)), eng)
+    eng.close()
+
+
+def _days(text):
+    import datetime
+    return (datetime.date.fromisoformat(text) - datetime.date(1970, 1, 1)).days
+
+
+# PartitionValueEvaluator.java:72-73: daysSinceEpoch(java.sql.Date.valueOf(value))
+DATE_PVS = [{"p": "2000-01-01"}, {"p": None}, {"p": "2000-1-2"}, {"p": "2021-02-30"}, {"p": "2021-+3-01"},
+            {}, {"p": "1999-12-31"}, {"p": "9999-12-31"}]
+DATE_PREDICATES = [cmp("=", col("p"), Literal.ofDate(_days("2000-01-02"))),
+                   cmp(">=", col("p"), Literal.ofDate(_days("2021-03-02"))),
+                   cmp("<", col("p"), Literal.ofDate(_days("2000-01-02"))),
+                   Or(Predicate("IS_NULL", col("p")), cmp("=", col("p"), Literal.ofDate(_days("2021-03-01")))),
+                   cmp("IS NOT DISTINCT FROM", col("p"), Literal.ofNull("date"))]
+DATE_BAD_PVS = ["2000-13-01", "1500-01-01", "2000-01", "x", "", "2000-01-01 "]
+
+
+def test_oracle_date_partition_values(tmp_path):
+    from oracle import partitions as opp
+    root = str(tmp_path / "t")
+    _write_pv_table(root, DATE_PVS, "date")
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in DATE_PREDICATES]
+    assert got == [[2], [3, 7], [0, 6], [1, 4, 5], [1, 5]]    # row 3 is 2021-03-02 (lenient carry)
+    for i, bad in enumerate(DATE_BAD_PVS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_pv_table(r, [{"p": "2000-01-01"}, {"p": bad}], "date")
+        with pytest.raises(opp.PartitionValueError):
+            oracle_files(r, DATE_PREDICATES[0])
+
+
+@pytest.mark.gpu
+def test_gpu_date_partition_values(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_pv_table(root, DATE_PVS, "date")
+    eng = K.GpuEngine()
+    for pred in DATE_PREDICATES:
+        assert _gpu_files(root, pred, eng) == oracle_files(root, pred), pred
+    for i, bad in enumerate(DATE_BAD_PVS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_pv_table(r, [{"p": "2000-01-01"}, {"p": bad}], "date")
+        with pytest.raises(DkError, match="partition"):
+            _gpu_files(r, DATE_PREDICATES[0], eng)
     eng.close()
