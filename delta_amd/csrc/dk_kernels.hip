@@ -1837,9 +1837,14 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
         if (leaf) {
           for (int p = 0; p < P.n_paths; p++)
             if ((leaf >> p) & 1) {
-              if (P.path_type[p] != SK_DATE || esc) return false;   // only dates are textual
+              const int t = P.path_type[p];
               long long v;
-              if (!js_date(s, i + 1, e - 1, &v)) return false;
+              if (t == SK_STRING) {                   // body span + escape flag, compared lazily
+                v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
+              } else {
+                if (t != SK_DATE || esc) return false;  // only dates and strings are textual
+                if (!js_date(s, i + 1, e - 1, &v)) return false;
+              }
               val[p] = v;
               *set |= 1u << p;
             }
@@ -1855,7 +1860,7 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
           for (int p = 0; p < P.n_paths; p++)
             if ((leaf >> p) & 1) {
               const int t = P.path_type[p];
-              if (t == SK_DATE) return false;         // a date must be a JSON string
+              if (t == SK_DATE || t == SK_STRING) return false;   // textual types need a JSON string
               if (t == SK_SHORT || t == SK_BYTE) {
                 if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
               } else if (!integral || !fits) {
@@ -1896,32 +1901,107 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
   }
 }
 
+// The UTF-8 bytes Java's String.getBytes(UTF_8) gives for a string value, one at a time: a stats
+// string is the JSON body s[a, b) with escapes decoded as Jackson decodes them (a \uXXXX surrogate
+// pair is one supplementary code point; a lone surrogate encodes as '?'); a literal is raw bytes.
+struct Utf8Cursor {
+  const uint8_t* s;
+  int32_t i, end;
+  bool esc;
+  uint8_t pend[4];
+  int np, pp;
+  __device__ static uint32_t hex4(const uint8_t* h) {
+    uint32_t v = 0;
+    for (int k = 0; k < 4; k++) {
+      const uint8_t c = h[k];
+      v = v * 16 + (c <= '9' ? c - '0' : (c | 0x20) - 'a' + 10);
+    }
+    return v;
+  }
+  __device__ bool next(uint8_t* out) {
+    if (pp < np) { *out = pend[pp++]; return true; }
+    if (i >= end) return false;
+    const uint8_t c = s[i];
+    if (!esc || c != '\\') { i++; *out = c; return true; }
+    const uint8_t e = s[i + 1];
+    if (e != 'u') {
+      i += 2;
+      *out = e == 'b' ? 8 : e == 'f' ? 12 : e == 'n' ? 10 : e == 'r' ? 13 : e == 't' ? 9 : e;
+      return true;
+    }
+    uint32_t cp = hex4(s + i + 2);
+    i += 6;
+    if (cp >= 0xD800 && cp <= 0xDBFF && i + 6 <= end && s[i] == '\\' && s[i + 1] == 'u') {
+      const uint32_t lo = hex4(s + i + 2);
+      if (lo >= 0xDC00 && lo <= 0xDFFF) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); i += 6; }
+    }
+    np = pp = 0;
+    if (cp >= 0xD800 && cp <= 0xDFFF) pend[np++] = '?';
+    else if (cp < 0x80) pend[np++] = (uint8_t)cp;
+    else if (cp < 0x800) { pend[np++] = 0xC0 | (cp >> 6); pend[np++] = 0x80 | (cp & 63); }
+    else if (cp < 0x10000) { pend[np++] = 0xE0 | (cp >> 12); pend[np++] = 0x80 | ((cp >> 6) & 63); pend[np++] = 0x80 | (cp & 63); }
+    else { pend[np++] = 0xF0 | (cp >> 18); pend[np++] = 0x80 | ((cp >> 12) & 63); pend[np++] = 0x80 | ((cp >> 6) & 63); pend[np++] = 0x80 | (cp & 63); }
+    *out = pend[pp++];
+    return true;
+  }
+};
+
+// stack slot kinds: 0 integral (or boolean), 1 stats string (packed span), 2 literal string
+__device__ Utf8Cursor sk_cursor(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len) {
+  Utf8Cursor c;
+  c.np = c.pp = 0;
+  if (kind == 1) {
+    c.s = s; c.i = (int32_t)(v & 0x7fffffff); c.end = c.i + (int32_t)((v >> 32) & 0x3fffffff); c.esc = (v >> 62) & 1;
+  } else {
+    c.s = (const uint8_t*)P.names; c.i = (int32_t)v; c.end = c.i + lit_len; c.esc = false;
+  }
+  return c;
+}
+
+// DefaultExpressionUtils.STRING_COMPARATOR (:49-54): unsigned UTF-8 bytes, then length
+__device__ int sk_strcmp(Utf8Cursor a, Utf8Cursor b) {
+  while (true) {
+    uint8_t x, y;
+    const bool ha = a.next(&x), hb = b.next(&y);
+    if (!ha || !hb) return ha ? 1 : hb ? -1 : 0;
+    if (x != y) return (int)x - (int)y;
+  }
+}
+
 // Kleene evaluation of the postfix program; returns 1 true, 0 false, -1 null
-__device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set) {
+__device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, const uint8_t* s) {
   long long sv[16];
   int8_t sn[16];      // -1 null, else 0/1 for booleans (values: 0 = non-null)
+  int8_t sk[16];      // slot kind (sk_cursor)
+  int32_t sl[16];     // literal string length
   int sp = 0;
   for (int k = 0; k < P.n_ops && k < SK_MAX_OPS; k++) {
     const int op = P.op[k];
     if (op == OP_STAT) {
       const int p = P.arg[k];
-      sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1; sp++;
+      sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1; sk[sp] = P.path_type[p] == SK_STRING; sp++;
     } else if (op == OP_LIT) {
-      sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sp++;
+      sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sp++;
+    } else if (op == OP_LIT_STR) {
+      sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = 2; sl[sp] = P.arg[k]; sp++;
     } else if (op >= OP_LT && op <= OP_EQ) {
-      const long long b = sv[--sp]; const int8_t bn = sn[sp];
-      const long long a = sv[--sp]; const int8_t an = sn[sp];
+      const long long b = sv[--sp]; const int8_t bn = sn[sp], bk = sk[sp]; const int32_t bl = sl[sp];
+      const long long a = sv[--sp]; const int8_t an = sn[sp], ak = sk[sp]; const int32_t al = sl[sp];
       int8_t r;
       if (an < 0 || bn < 0) r = -1;
+      else if (ak || bk) {
+        const int c = sk_strcmp(sk_cursor(ak, a, s, P, al), sk_cursor(bk, b, s, P, bl));
+        r = op == OP_LT ? c < 0 : op == OP_LE ? c <= 0 : op == OP_GT ? c > 0 : op == OP_GE ? c >= 0 : c == 0;
+      }
       else r = op == OP_LT ? a < b : op == OP_LE ? a <= b : op == OP_GT ? a > b : op == OP_GE ? a >= b : a == b;
-      sn[sp] = r; sv[sp] = 0; sp++;
+      sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sp++;
     } else {
       const int8_t b = sn[--sp];
       const int8_t a = sn[--sp];
       int8_t r;
       if (op == OP_AND) r = (a == 0 || b == 0) ? 0 : (a == 1 && b == 1) ? 1 : -1;
       else r = (a == 1 || b == 1) ? 1 : (a == 0 && b == 0) ? 0 : -1;
-      sn[sp] = r; sv[sp] = 0; sp++;
+      sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sp++;
     }
   }
   return sp == 1 ? sn[0] : -1;
@@ -1946,7 +2026,7 @@ __global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg 
     long long val[SK_MAX_PATHS];
     uint32_t set = 0;
     if (!js_extract(s, len, P, val, &set)) { set_err(st, E_STATS, R.row_tag + r, 0); continue; }
-    if (sk_eval(P, val, set) == 0) sel[r] = 0;                    // COALESCE(skip, true)
+    if (sk_eval(P, val, set, s) == 0) sel[r] = 0;                    // COALESCE(skip, true)
   }
 }
 

@@ -18,7 +18,7 @@ from .expressions import ALWAYS_TRUE, Column, Literal, Predicate
 MIN, MAX, NULL_COUNT, NUM_RECORDS = "minValues", "maxValues", "nullCount", "numRecords"
 SKIPPING_ELIGIBLE = {"byte", "short", "integer", "long", "float", "double", "date", "timestamp",
                      "timestamp_ntz", "string"}          # StatsSchemaHelper.java:209-222 (+ decimal)
-GPU_TYPES = {"byte", "short", "integer", "long", "date"}          # stats value types k_stats_eval decodes
+GPU_TYPES = {"byte", "short", "integer", "long", "date", "string"}          # stats value types k_stats_eval decodes
 REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
            "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}   # DataSkippingUtils.java:346-356
 NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
@@ -213,9 +213,9 @@ def referenced_stats(node, out=None):
 
 
 # ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
-OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR = range(9)
+OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR = range(10)
 _CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
-TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4}
+TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5}
 
 
 def stat_type(path, leaves):
@@ -254,6 +254,8 @@ def compile_program(node, leaves):
             v = n[1]
             if v is None:
                 ops.append((OP_LIT, 1, 0))                   # null literal: comparisons yield null
+            elif isinstance(v, str):                         # compared as UTF-8 bytes (String.getBytes)
+                ops.append((OP_LIT_STR, 0, v.encode("utf-8", "replace")))
             elif isinstance(v, bool) or not isinstance(v, int):
                 raise UnsupportedSkipping("data skipping with a %r literal is not supported" % (v,))
             elif not -(1 << 63) <= v < (1 << 63):
@@ -263,6 +265,9 @@ def compile_program(node, leaves):
         elif n[0] == "timeadd":
             raise UnsupportedSkipping("timestamp data skipping is not supported by this engine build")
         else:
+            kinds = {_operand_kind(c, leaves) for c in (n[1], n[2])} - {None}
+            if len(kinds) > 1:
+                raise UnsupportedSkipping("data skipping comparison of a string with a non-string")
             emit(n[1])
             emit(n[2])
             ops.append((_CMP[n[0]], 0, 0))
@@ -272,13 +277,21 @@ def compile_program(node, leaves):
     return paths, [TYPE_CODE[stat_type(p, leaves)] for p in paths], ops
 
 
+def _operand_kind(n, leaves):
+    if n[0] == "stat":
+        return "string" if stat_type(n[1], leaves) == "string" else "number"
+    if n[0] == "lit":
+        return None if n[1] is None else "string" if isinstance(n[1], str) else "number"
+    return "number"
+
+
 MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 512
 
 
 def _stack_depth(ops):
     d = hi = 0
     for op, _, _ in ops:
-        d += 1 if op in (OP_STAT, OP_LIT) else -1
+        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR) else -1
         hi = max(hi, d)
     return hi
 
@@ -301,8 +314,17 @@ def pack(program, struct_type):
             names += b
     if len(names) > NAMES_BYTES:
         raise UnsupportedSkipping("stats field names exceed %d bytes" % NAMES_BYTES)
+    packed = []
+    for op, arg, lit in ops:
+        if op == OP_LIT_STR:                                 # literal bytes follow the names
+            packed.append((op, len(lit), len(names)))
+            names += lit
+        else:
+            packed.append((op, arg, lit))
+    if len(names) > NAMES_BYTES:
+        raise UnsupportedSkipping("stats field names and string literals exceed %d bytes" % NAMES_BYTES)
     prog.names = bytes(names)
     prog.n_ops = len(ops)
-    for k, (op, arg, lit) in enumerate(ops):
+    for k, (op, arg, lit) in enumerate(packed):
         prog.op[k], prog.arg[k], prog.lit[k] = op, arg, lit
     return prog

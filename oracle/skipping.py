@@ -11,7 +11,8 @@ does with a data-skipping predicate once the scan files are reconciled.
   DefaultJsonRow.decodeElement          kernel-defaults/.../internal/data/DefaultJsonRow.java:136-270
       long/integer: an integral token in range; short/byte: any number whose exact value is an
       integer in range (canConvertToExactIntegral); date: a string through java.sql.Date.valueOf
-      (:249-252); struct: an object; JSON null = null
+      (:249-252); string: a JSON string, compared as unsigned UTF-8 bytes then length
+      (DefaultExpressionUtils.java:49-54); struct: an object; JSON null = null
   DefaultExpressionEvaluator            kernel-defaults/.../internal/expressions/
       comparators are null when either side is null; AND/OR are Kleene (visitAnd/visitOr)
 
@@ -80,6 +81,10 @@ def _date(text):
 def _leaf(v, typ):
     if v is None:
         return None
+    if typ == "string":                                # DefaultJsonRow.java:170-173 (isTextual),
+        if not isinstance(v, str):                     # compared as String.getBytes(UTF_8): a lone
+            raise StatsDecodeError("Couldn't decode %r, expected a string" % (v,))   # surrogate is '?'
+        return v.encode("utf-8", "replace")
     if typ == "date":
         if not isinstance(v, str):
             raise StatsDecodeError("Couldn't decode %r, expected a date" % (v,))
@@ -118,7 +123,7 @@ def evaluate(node, vals):
     if k == "stat":
         return vals[node[1]]
     if k == "lit":
-        return node[1]
+        return node[1].encode("utf-8", "replace") if isinstance(node[1], str) else node[1]
     if k == "AND":
         a, b = evaluate(node[1], vals), evaluate(node[2], vals)
         if a is False or b is False:

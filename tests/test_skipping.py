@@ -3,8 +3,8 @@
 Pinned to the reference's own expectations on its golden tables (KDT = kernel-defaults/src/test/scala/
 io/delta/kernel/defaults):
   ScanSuite.scala:1150-1196  basic data skipping for all types (+ column mapping name/id, checkpoint):
-                             hits / misses for int, long, byte, short and date (the types the GPU
-                             evaluator decodes; float/double/string/decimal filters are refused)
+                             hits / misses for int, long, byte, short, date and string (the types the
+                             GPU evaluator decodes; float/double/decimal filters are refused)
   ScanSuite.scala:1233-1239  filter on a non-existent column -> no skipping
   ScanSuite.scala:1243-1253  AND of two data columns -> 1 file
   ScanSuite.scala:1255-1267  stats collected changing across versions -> 1 / 2 / 1 files
@@ -50,6 +50,7 @@ def all_types_hits_misses():
     """ScanSuite.scala:1150-1183: value in table 0, smaller -1, bigger 1 (dates: DATES)."""
     hits, misses = [], []
     cases = [(name, lit(0), lit(-1), lit(1)) for name, lit in INTEGRAL.items()] + [("as_date",) + DATES]
+    cases.append(("as_string", Literal.ofString("0"), Literal.ofString("!"), Literal.ofString("1")))   # :1157
     for name, value, small, big in cases:
         c = col(name)
         misses += [cmp("=", c, small), cmp(">", c, value), cmp(">=", c, big), cmp("<", c, value),
@@ -157,8 +158,8 @@ def test_construct_rules():
 
 def test_compile_refuses_unsupported():
     leaves = {("f",): ("float", ("f",)), ("s",): ("string", ("s",)), ("a",): ("long", ("a",))}
-    for p in (cmp("=", col("f"), Literal(0.0, "float")), cmp("=", col("s"), Literal.ofString("x")),
-              cmp("=", col("a"), Literal(0.5, "double"))):
+    for p in (cmp("=", col("f"), Literal(0.0, "float")), cmp("=", col("s"), Literal.ofInt(1)),
+              cmp("=", col("a"), Literal.ofString("1")), cmp("=", col("a"), Literal(0.5, "double"))):
         node = sk.construct(p, leaves)
         assert node is not None
         with pytest.raises(sk.UnsupportedSkipping):
@@ -473,4 +474,65 @@ def test_gpu_date_stats_parity(tmp_path):
         _write_edge_table(r, [DATE_EDGE_STATS[0], bad], DATE_COLUMNS)
         with pytest.raises(DkError, match="data skipping"):
             _gpu_files(r, DATE_BAD_PREDICATE, eng)
+    eng.close()
+
+
+STRING_COLUMNS = (("s", "string"), ("id", "long"))
+STRING_EDGE_STATS = [
+    '{"numRecords":2,"minValues":{"s":"apple"},"maxValues":{"s":"banana"}}',
+    '{"numRecords":2,"minValues":{"s":"b"},"maxValues":{"s":"ba"}}',
+    '{"numRecords":2,"minValues":{"s":"\\u00e9t\\u00e9"},"maxValues":{"s":"\u00fcber"}}',
+    '{"numRecords":2,"minValues":{"s":"\\ud83d\\ude00"},"maxValues":{"s":"\\ud83d\\ude00z"}}',
+    '{"numRecords":2,"minValues":{"s":"\\ud800x"},"maxValues":{"s":"?y"}}',
+    '{"numRecords":2,"minValues":{"s":"a\\"b\\\\c\\n"},"maxValues":{"s":"a\\/z\\t"}}',
+    '{"numRecords":2,"minValues":{"s":""},"maxValues":{"s":null},"nullCount":{"s":1}}',
+    '{"numRecords":2,"minValues":{"s":"zz","s":"c"},"maxValues":{"s":"cz"}}',
+    None,
+]
+STRING_PREDICATES = [cmp("=", col("s"), Literal.ofString("b")),
+                     cmp(">", col("s"), Literal.ofString("\u00e9")),
+                     cmp("<", col("s"), Literal.ofString("a/")),
+                     cmp("=", col("s"), Literal.ofString("\U0001F600")),
+                     cmp(">=", col("s"), Literal.ofString("?x")),
+                     cmp("=", col("s"), Literal.ofString('a"b\\c\n')),
+                     Or(cmp("<", col("s"), Literal.ofString("")), cmp("=", col("s"), Literal.ofString("ca"))),
+                     Predicate("NOT", cmp("<=", col("s"), Literal.ofString("banana")))]
+STRING_BAD_STATS = ['{"numRecords":2,"minValues":{"s":1}}', '{"numRecords":2,"minValues":{"s":true}}',
+                    '{"numRecords":2,"minValues":{"s":{"x":"a"}}}', '{"numRecords":2,"minValues":{"s":["a"]}}']
+
+
+def test_oracle_string_edge_cases_expected(tmp_path):
+    root = str(tmp_path / "t")
+    _write_edge_table(root, STRING_EDGE_STATS, STRING_COLUMNS)
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in STRING_PREDICATES]
+    assert got[0] == [0, 1, 6, 8]                      # min <= "b" <= max; row 6: null max -> kept
+    assert got[1] == [2, 3, 6, 8]                      # max > "é" (UTF-8 bytes: é = c3 a9 < ü, emoji)
+    assert got[2] == [4, 5, 6, 8]                      # min < "a/" ("?" < "a", '"' < "/" < "p")
+    assert got[3] == [3, 6, 8]                         # escaped surrogate pair == the code point
+    assert got[4] == [0, 1, 2, 3, 4, 5, 6, 7, 8]       # lone surrogate -> "?x" (max "?y" >= "?x")
+    assert got[5] == [5, 6, 8]                         # escapes decoded: a"b\\c<LF> <= lit <= a/z<TAB>
+    assert got[6] == [6, 7, 8]                         # "" < "" false (null OR); row 7: last key wins
+    assert got[7] == [2, 3, 6, 7, 8]                   # NOT (max <= "banana") -> max > "banana"
+    from oracle import skipping as osk
+    for i, bad in enumerate(STRING_BAD_STATS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_edge_table(r, [STRING_EDGE_STATS[0], bad], STRING_COLUMNS)
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(r, STRING_PREDICATES[0])
+
+
+@pytest.mark.gpu
+def test_gpu_string_stats_parity(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_edge_table(root, STRING_EDGE_STATS, STRING_COLUMNS)
+    eng = K.GpuEngine()
+    for p in STRING_PREDICATES:
+        assert _gpu_files(root, p, eng) == oracle_files(root, p), p
+    for i, bad in enumerate(STRING_BAD_STATS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_edge_table(r, [STRING_EDGE_STATS[0], bad], STRING_COLUMNS)
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(r, STRING_PREDICATES[0], eng)
     eng.close()
