@@ -1769,6 +1769,70 @@ __device__ bool js_date(const uint8_t* s, int32_t a, int32_t b, long long* v) { 
   return true;
 }
 
+// A timestamp stats value: DefaultJsonRow.java:254-258 decodes it as
+// MICROS.between(EPOCH, OffsetDateTime.parse(text).toInstant()). ISO_OFFSET_DATE_TIME, strict:
+// yyyy-MM-dd, 'T' (either case), HH:mm, optional :ss and .fraction (1-9 digits), then 'Z' (either
+// case) or +/-HH:MM[:SS] (at most 18:00). Years outside 1678..2261 (where the nanosecond difference
+// Instant.until computes would overflow), signed or 5+ digit years, and the fraction-without-digits
+// form are a decode error in this build.
+__device__ bool ts_digits(const uint8_t* s, int32_t* k, int32_t b, int n, long long* out) {
+  if (*k + n > b) return false;
+  long long x = 0;
+  for (int j = 0; j < n; j++) {
+    const uint8_t c = s[*k + j];
+    if (c < '0' || c > '9') return false;
+    x = x * 10 + (c - '0');
+  }
+  *k += n;
+  *out = x;
+  return true;
+}
+
+__device__ bool js_timestamp(const uint8_t* s, int32_t a, int32_t b, long long* v) {
+  int32_t k = a;
+  long long y, mo, d, h, mi, sec = 0, nanos = 0;
+  if (!ts_digits(s, &k, b, 4, &y) || k >= b || s[k++] != '-' || !ts_digits(s, &k, b, 2, &mo) ||
+      k >= b || s[k++] != '-' || !ts_digits(s, &k, b, 2, &d) || k >= b || (s[k] | 0x20) != 't')
+    return false;
+  k++;
+  if (!ts_digits(s, &k, b, 2, &h) || k >= b || s[k++] != ':' || !ts_digits(s, &k, b, 2, &mi)) return false;
+  if (k < b && s[k] == ':') {
+    k++;
+    if (!ts_digits(s, &k, b, 2, &sec)) return false;
+    if (k < b && s[k] == '.') {
+      k++;
+      int nd = 0;
+      while (k < b && s[k] >= '0' && s[k] <= '9' && nd < 9) { nanos = nanos * 10 + (s[k] - '0'); k++; nd++; }
+      if (nd == 0 || (k < b && s[k] >= '0' && s[k] <= '9')) return false;
+      for (; nd < 9; nd++) nanos *= 10;
+    }
+  }
+  if (y < 1678 || y > 2261 || mo < 1 || mo > 12 || d < 1 || h > 23 || mi > 59 || sec > 59) return false;
+  const int dim = mo == 2 ? ((y % 4 == 0 && (y % 100 != 0 || y % 400 == 0)) ? 29 : 28)
+                : (mo == 4 || mo == 6 || mo == 9 || mo == 11) ? 30 : 31;
+  if (d > dim) return false;
+  if (k >= b) return false;
+  long long off = 0;
+  if ((s[k] | 0x20) == 'z') {
+    k++;
+  } else if (s[k] == '+' || s[k] == '-') {
+    const bool neg = s[k++] == '-';
+    long long oh, om, os = 0;
+    if (!ts_digits(s, &k, b, 2, &oh) || k >= b || s[k++] != ':' || !ts_digits(s, &k, b, 2, &om)) return false;
+    if (k < b && s[k] == ':') { k++; if (!ts_digits(s, &k, b, 2, &os)) return false; }
+    if (oh > 18 || om > 59 || os > 59) return false;
+    off = oh * 3600 + om * 60 + os;
+    if (off > 18 * 3600) return false;
+    if (neg) off = -off;
+  } else {
+    return false;
+  }
+  if (k != b) return false;
+  const long long secs = civil_days(y, mo, d) * 86400 + h * 3600 + mi * 60 + sec - off;
+  *v = (secs * 1000000000ll + nanos) / 1000;            // Java long division: toward zero
+  return true;
+}
+
 // extract the program's stats fields from one JSON object; returns false on a decode error
 __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long long* val, uint32_t* set) {
   uint32_t mstack[JS_MAXD];
@@ -1842,8 +1906,8 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
               if (t == SK_STRING) {                   // body span + escape flag, compared lazily
                 v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
               } else {
-                if (t != SK_DATE || esc) return false;  // only dates and strings are textual
-                if (!js_date(s, i + 1, e - 1, &v)) return false;
+                if ((t != SK_DATE && t != SK_TIMESTAMP) || esc) return false;   // textual types only
+                if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v) : js_timestamp(s, i + 1, e - 1, &v))) return false;
               }
               val[p] = v;
               *set |= 1u << p;
@@ -1860,7 +1924,7 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
           for (int p = 0; p < P.n_paths; p++)
             if ((leaf >> p) & 1) {
               const int t = P.path_type[p];
-              if (t == SK_DATE || t == SK_STRING) return false;   // textual types need a JSON string
+              if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP) return false;   // textual types need a JSON string
               if (t == SK_SHORT || t == SK_BYTE) {
                 if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
               } else if (!integral || !fits) {
@@ -1982,6 +2046,8 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1; sk[sp] = P.path_type[p] == SK_STRING; sp++;
     } else if (op == OP_LIT) {
       sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sp++;
+    } else if (op == OP_TIMEADD) {                     // DefaultExpressionEvaluator.visitTimeAdd :593-625
+      if (sp > 0 && sn[sp - 1] >= 0) sv[sp - 1] += P.lit[k];
     } else if (op == OP_LIT_STR) {
       sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = 2; sl[sp] = P.arg[k]; sp++;
     } else if (op >= OP_LT && op <= OP_EQ) {

@@ -46,6 +46,10 @@ class Literal:
         return Literal(int(days_since_epoch), "date")
 
     @staticmethod
+    def ofTimestamp(micros_since_epoch_utc):             # Literal.ofTimestamp(long)
+        return Literal(int(micros_since_epoch_utc), "timestamp")
+
+    @staticmethod
     def ofString(v):
         return Literal(str(v), "string")
 

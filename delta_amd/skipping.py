@@ -18,7 +18,7 @@ from .expressions import ALWAYS_TRUE, Column, Literal, Predicate
 MIN, MAX, NULL_COUNT, NUM_RECORDS = "minValues", "maxValues", "nullCount", "numRecords"
 SKIPPING_ELIGIBLE = {"byte", "short", "integer", "long", "float", "double", "date", "timestamp",
                      "timestamp_ntz", "string"}          # StatsSchemaHelper.java:209-222 (+ decimal)
-GPU_TYPES = {"byte", "short", "integer", "long", "date", "string"}          # stats value types k_stats_eval decodes
+GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp"}          # stats value types k_stats_eval decodes
 REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
            "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}   # DataSkippingUtils.java:346-356
 NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
@@ -213,9 +213,9 @@ def referenced_stats(node, out=None):
 
 
 # ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
-OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR = range(10)
+OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD = range(11)
 _CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
-TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5}
+TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6}
 
 
 def stat_type(path, leaves):
@@ -262,8 +262,9 @@ def compile_program(node, leaves):
                 raise UnsupportedSkipping("literal %d does not fit a long" % v)
             else:
                 ops.append((OP_LIT, 0, int(v)))
-        elif n[0] == "timeadd":
-            raise UnsupportedSkipping("timestamp data skipping is not supported by this engine build")
+        elif n[0] == "timeadd":                              # max + 1 ms (StatsSchemaHelper :154-159)
+            emit(n[1])
+            ops.append((OP_TIMEADD, 0, 1000))
         else:
             kinds = {_operand_kind(c, leaves) for c in (n[1], n[2])} - {None}
             if len(kinds) > 1:
@@ -291,7 +292,7 @@ MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 512
 def _stack_depth(ops):
     d = hi = 0
     for op, _, _ in ops:
-        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR) else -1
+        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR) else 0 if op == OP_TIMEADD else -1
         hi = max(hi, d)
     return hi
 

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import json
+import re
 from decimal import Decimal
 
 RANGES = {"long": (-(1 << 63), (1 << 63) - 1), "integer": (-(1 << 31), (1 << 31) - 1),
@@ -78,9 +79,45 @@ def _date(text):
     return (_dt.date(y, m, 1) - _dt.date(1970, 1, 1)).days + d - 1
 
 
+_TS = re.compile(r"(\d{4})-(\d{2})-(\d{2})[Tt](\d{2}):(\d{2})(?::(\d{2})(?:\.(\d{1,9}))?)?"
+                 r"(?:([Zz])|([+-])(\d{2}):(\d{2})(?::(\d{2}))?)")
+
+
+def _timestamp(text):
+    """MICROS.between(EPOCH, OffsetDateTime.parse(text).toInstant()): DefaultJsonRow.java:254-258.
+    ISO_OFFSET_DATE_TIME with the strict resolver; years outside 1678..2261 (where Instant.until's
+    nanosecond difference would overflow), signed years and '.' without digits are refused here."""
+    m = _TS.fullmatch(text) if text.isascii() else None
+    if not m:
+        raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % text)
+    y, mo, d, h, mi = (int(m.group(i)) for i in range(1, 6))
+    sec = int(m.group(6) or 0)
+    nanos = int((m.group(7) or "").ljust(9, "0") or 0)
+    try:
+        day = _dt.date(y, mo, d)
+    except ValueError:
+        raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % text) from None
+    if not 1678 <= y <= 2261 or h > 23 or mi > 59 or sec > 59:
+        raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % text)
+    off = 0
+    if m.group(9):
+        oh, om, os_ = int(m.group(10)), int(m.group(11)), int(m.group(12) or 0)
+        off = oh * 3600 + om * 60 + os_
+        if oh > 18 or om > 59 or os_ > 59 or off > 18 * 3600:
+            raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % text)
+        off = -off if m.group(9) == "-" else off
+    secs = (day - _dt.date(1970, 1, 1)).days * 86400 + h * 3600 + mi * 60 + sec - off
+    total = secs * 1_000_000_000 + nanos
+    return total // 1000 if total >= 0 else -((-total) // 1000)     # Java division: toward zero
+
+
 def _leaf(v, typ):
     if v is None:
         return None
+    if typ == "timestamp":
+        if not isinstance(v, str):
+            raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % (v,))
+        return _timestamp(v)
     if typ == "string":                                # DefaultJsonRow.java:170-173 (isTextual),
         if not isinstance(v, str):                     # compared as String.getBytes(UTF_8): a lone
             raise StatsDecodeError("Couldn't decode %r, expected a string" % (v,))   # surrogate is '?'
@@ -122,6 +159,9 @@ def evaluate(node, vals):
     k = node[0]
     if k == "stat":
         return vals[node[1]]
+    if k == "timeadd":                                 # DefaultExpressionEvaluator.visitTimeAdd
+        a = evaluate(node[1], vals)
+        return None if a is None else a + 1000
     if k == "lit":
         return node[1].encode("utf-8", "replace") if isinstance(node[1], str) else node[1]
     if k == "AND":

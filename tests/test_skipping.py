@@ -536,3 +536,89 @@ def test_gpu_string_stats_parity(tmp_path):
         with pytest.raises(DkError, match="data skipping"):
             _gpu_files(r, STRING_PREDICATES[0], eng)
     eng.close()
+
+
+# ScanSuite.scala:808-842 (TIMESTAMP): Spark writes ms-truncated stats in yyyy-MM-dd'T'HH:mm:ss.SSSXXX;
+# the max is widened by TIMEADD(+1 ms) before comparing.
+def _micros(text):
+    import datetime
+    t = datetime.datetime.fromisoformat(text.replace("Z", "+00:00"))
+    d = t - datetime.datetime(1970, 1, 1, tzinfo=datetime.timezone.utc)
+    return (d.days * 86400 + d.seconds) * 1_000_000 + d.microseconds
+
+
+def _ts(op, c, text):
+    return cmp(op, c, Literal.ofTimestamp(_micros(text)))
+
+
+TS_COLUMNS = (("ts", "timestamp"), ("nested", {"type": "struct", "fields": [
+    {"name": "ts", "type": "timestamp", "nullable": True, "metadata": {}}]}))
+TS_SPARK_STATS = ('{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03.456Z","nested":{"ts":"2019-09-09T01:02:03.456Z"}},'
+                  '"maxValues":{"ts":"2019-09-09T01:02:03.456Z","nested":{"ts":"2019-09-09T01:02:03.456Z"}},'
+                  '"nullCount":{"ts":0,"nested":{"ts":0}}}')
+NTS = Column("nested", "ts")
+TS_HITS = [_ts("=", col("ts"), "2019-09-09T01:02:03.456789Z"), _ts(">=", col("ts"), "2019-09-09T01:02:03.456789Z"),
+           _ts("<=", col("ts"), "2019-09-09T01:02:03.456789Z"), _ts(">=", NTS, "2019-09-09T01:02:03.456789Z"),
+           _ts("<=", NTS, "2019-09-09T01:02:03.456789Z")]
+TS_MISSES = [_ts("=", col("ts"), "2019-09-09T01:02:03.457001Z"), _ts(">=", col("ts"), "2019-09-09T01:02:03.457001Z"),
+             _ts("<=", col("ts"), "2019-09-09T01:02:03.455999Z"), _ts(">=", NTS, "2019-09-09T01:02:03.457001Z"),
+             _ts("<=", NTS, "2019-09-09T01:02:03.455999Z")]
+TS_EDGE_STATS = [
+    '{"numRecords":1,"minValues":{"ts":"2019-09-09t01:02:03+05:30"},"maxValues":{"ts":"2019-09-08T20:32:03.000001z"}}',
+    '{"numRecords":1,"minValues":{"ts":"1969-12-31T23:59:59.9999995Z"},"maxValues":{"ts":"1970-01-01T00:00-00:00"}}',
+    '{"numRecords":1,"minValues":{"ts":"2000-02-29T23:59:59.123456789-18:00"},"maxValues":{"ts":"2000-03-01T17:59:59.123456789Z"}}',
+    '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03.456Z","ts":"2020-01-01T00:00:00Z"},"maxValues":{"ts":null}}',
+    None,
+]
+TS_EDGE_PREDICATES = [_ts("=", col("ts"), "2019-09-08T20:32:03Z"), _ts("<", col("ts"), "1970-01-01T00:00:00Z"),
+                      _ts(">", col("ts"), "2000-03-01T17:59:59.124Z"), _ts(">=", col("ts"), "2020-01-01T00:00:00Z"),
+                      _ts("=", col("ts"), "1970-01-01T00:00:00.001Z")]
+TS_BAD_STATS = ['{"numRecords":1,"minValues":{"ts":"2019-02-29T00:00:00Z"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03"}}',
+                '{"numRecords":1,"minValues":{"ts":"2019-09-09 01:02:03Z"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T24:00:00Z"}}',
+                '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03+19:00"}}', '{"numRecords":1,"minValues":{"ts":12}}',
+                '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03.1234567891Z"}}', '{"numRecords":1,"minValues":{"ts":"1500-01-01T00:00:00Z"}}']
+
+
+def test_oracle_timestamp_reference_hits_and_misses(tmp_path):
+    root = str(tmp_path / "t")
+    _write_edge_table(root, [TS_SPARK_STATS], TS_COLUMNS)
+    for p in TS_HITS:
+        assert oracle_files(root, p)[0], p
+    for p in TS_MISSES:
+        assert not oracle_files(root, p)[0], p
+    r = str(tmp_path / "e")
+    _write_edge_table(r, TS_EDGE_STATS, TS_COLUMNS)
+    got = [sorted(int(x[0].decode()[1:-8]) for x in oracle_files(r, p)[0]) for p in TS_EDGE_PREDICATES]
+    assert got[0] == [0, 4]                         # row 0: +05:30 is 20:32:03Z (row 3: min 2020 wins)
+    assert got[1] == [4]                            # row 1 min: -500 ns truncates toward zero to 0
+    assert got[2] == [0, 2, 3, 4]                   # row 2 max .123456 + 1 ms = .124456 > .124
+    assert got[3] == [3, 4]                         # row 3: last min key wins (2020), null max -> kept
+    assert got[4] == [1, 4]                         # row 1: max 0 + 1 ms = 1 ms
+    from oracle import skipping as osk
+    for i, bad in enumerate(TS_BAD_STATS):
+        b = str(tmp_path / ("b%d" % i))
+        _write_edge_table(b, [TS_SPARK_STATS, bad], TS_COLUMNS)
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(b, TS_HITS[0])
+
+
+@pytest.mark.gpu
+def test_gpu_timestamp_stats_parity(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_edge_table(root, [TS_SPARK_STATS], TS_COLUMNS)
+    eng = K.GpuEngine()
+    for p in TS_HITS + TS_MISSES:
+        g = _gpu_files(root, p, eng)
+        assert g == oracle_files(root, p) and bool(g[0]) == (p in TS_HITS), p
+    r = str(tmp_path / "e")
+    _write_edge_table(r, TS_EDGE_STATS, TS_COLUMNS)
+    for p in TS_EDGE_PREDICATES:
+        assert _gpu_files(r, p, eng) == oracle_files(r, p), p
+    for i, bad in enumerate(TS_BAD_STATS):
+        b = str(tmp_path / ("b%d" % i))
+        _write_edge_table(b, [TS_SPARK_STATS, bad], TS_COLUMNS)
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(b, TS_HITS[0], eng)
+    eng.close()
