@@ -148,10 +148,10 @@ struct DSkipProg {
 // the partition columns it reads (physical names, looked up in each row's partitionValues map) and
 // a postfix program over their deserialized values.
 constexpr int PP_MAX_FIELDS = 8, PP_MAX_OPS = 64, PP_POOL = 1024;
-enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING = 4, PT_DATE = 5 };
+enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING = 4, PT_DATE = 5, PT_DECIMAL = 6 };
 enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, PO_LT = 4, PO_LE = 5, PO_GT = 6,
                  PO_GE = 7, PO_EQ = 8, PO_NSEQ = 9, PO_ISNULL = 10, PO_ISNOTNULL = 11, PO_NOT = 12, PO_AND = 13,
-                 PO_OR = 14 };
+                 PO_OR = 14, PO_LIT_DEC = 15 };
 struct DPartProg {
   int32_t n_fields;
   int32_t field_type[PP_MAX_FIELDS];

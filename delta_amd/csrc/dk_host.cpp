@@ -1705,7 +1705,7 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
   if (P.n_fields < 0 || P.n_fields > PP_MAX_FIELDS || P.n_ops <= 0 || P.n_ops > PP_MAX_OPS)
     return fail("dk_replay_set_partition_filter: bad program size");
   for (int f = 0; f < P.n_fields; f++)
-    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_DATE || P.name_off[f] < 0 || P.name_len[f] < 0 ||
+    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_DECIMAL || P.name_off[f] < 0 || P.name_len[f] < 0 ||
         P.name_off[f] + P.name_len[f] > PP_POOL)
       return fail("dk_replay_set_partition_filter: bad field");
   int depth = 0;
@@ -1713,7 +1713,7 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
     const int op = P.op[k];
     if (op == PO_FIELD) { if (P.arg[k] < 0 || P.arg[k] >= P.n_fields) return fail("dk_replay_set_partition_filter: bad field ref"); depth++; }
     else if (op == PO_LIT_INT || op == PO_LIT_NULL) depth++;
-    else if (op == PO_LIT_STR) {
+    else if (op == PO_LIT_STR || op == PO_LIT_DEC) {
       if (P.lit[k] < 0 || P.arg[k] < 0 || P.lit[k] + P.arg[k] > PP_POOL) return fail("dk_replay_set_partition_filter: bad literal");
       depth++;
     } else if ((op >= PO_LT && op <= PO_NSEQ) || op == PO_AND || op == PO_OR) {

@@ -2136,7 +2136,77 @@ __device__ __forceinline__ int bytes_cmp(const uint8_t* a, int32_t na, const uin
   return na < nb ? -1 : na > nb ? 1 : 0;
 }
 
-struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean
+// A decimal partition value: new BigDecimal(text) (PartitionValueEvaluator.java:112-113), compared
+// with BigDecimal.compareTo (numeric, scale-insensitive). Grammar: [+-] digits [. digits] | [+-] .
+// digits, then optional [eE][+-]digits; the scale (fraction digits - exponent) must fit an int.
+// Non-ASCII digits (which Character.isDigit accepts) are a malformed value in this build.
+struct DecNum {
+  const uint8_t* s;
+  int32_t first, end;   // first significant digit, end of the mantissa ('.' skipped when walking)
+  int sign;             // 0 for zero
+  long long adj;        // decimal exponent of the first significant digit
+};
+
+__device__ bool dec_parse(const uint8_t* s, int32_t n, DecNum* d) {
+  int32_t i = 0;
+  bool neg = false;
+  if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+  const int32_t m0 = i;
+  int32_t dot = -1, ndig = 0, int_digits = 0, first = -1, first_idx = 0;
+  for (; i < n && s[i] != 'e' && s[i] != 'E'; i++) {
+    if (s[i] == '.') { if (dot >= 0) return false; dot = i; continue; }
+    if (s[i] < '0' || s[i] > '9') return false;
+    if (first < 0 && s[i] != '0') { first = i; first_idx = ndig; }
+    if (dot < 0) int_digits++;
+    ndig++;
+  }
+  if (ndig == 0) return false;
+  const int32_t mend = i;
+  long long ex = 0;
+  if (i < n) {                                        // exponent
+    i++;
+    bool eneg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; i++; }
+    if (i >= n) return false;
+    for (; i < n; i++) {
+      if (s[i] < '0' || s[i] > '9') return false;
+      ex = ex * 10 + (s[i] - '0');
+      if (ex > 4000000000ll) return false;
+    }
+    if (eneg) ex = -ex;
+  }
+  const long long scale = (long long)(ndig - int_digits) - ex;
+  if (scale < -2147483648ll || scale > 2147483647ll) return false;
+  (void)m0;
+  d->s = s; d->end = mend;
+  if (first < 0) { d->sign = 0; d->first = mend; d->adj = 0; return true; }
+  d->sign = neg ? -1 : 1;
+  d->first = first;
+  d->adj = (long long)int_digits - 1 - first_idx + ex;
+  return true;
+}
+
+__device__ int dec_cmp(const DecNum& a, const DecNum& b) {
+  if (a.sign != b.sign) return a.sign < b.sign ? -1 : 1;
+  if (a.sign == 0) return 0;
+  int mag = 0;
+  if (a.adj != b.adj) {
+    mag = a.adj < b.adj ? -1 : 1;
+  } else {
+    int32_t i = a.first, j = b.first;
+    while (true) {
+      while (i < a.end && a.s[i] == '.') i++;
+      while (j < b.end && b.s[j] == '.') j++;
+      if (i >= a.end && j >= b.end) break;
+      const int x = i < a.end ? a.s[i++] - '0' : 0;
+      const int y = j < b.end ? b.s[j++] - '0' : 0;
+      if (x != y) { mag = x < y ? -1 : 1; break; }
+    }
+  }
+  return a.sign > 0 ? mag : -mag;
+}
+
+struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean, 4 decimal text
   int32_t kind, len;
   long long v;
   const uint8_t* p;
@@ -2162,6 +2232,10 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
           } else if (ty == PT_DATE) {                    // PartitionValueEvaluator.java:72-73
             if (!js_date(vp, 0, vl, &f[k].v)) { *err = true; return -1; }
             f[k].kind = 1;
+          } else if (ty == PT_DECIMAL) {
+            DecNum dn;
+            if (!dec_parse(vp, vl, &dn)) { *err = true; return -1; }
+            f[k].kind = 4; f[k].p = vp; f[k].len = vl;
           } else {
             const long long lo = ty == PT_LONG ? (-9223372036854775807ll - 1) : ty == PT_INT ? -2147483648ll
                                : ty == PT_SHORT ? -32768 : -128;
@@ -2185,6 +2259,8 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
       st[sp].kind = 1; st[sp].v = P.lit[i]; sp++;
     } else if (op == PO_LIT_STR) {
       st[sp].kind = 2; st[sp].p = (const uint8_t*)P.pool + P.lit[i]; st[sp].len = P.arg[i]; sp++;
+    } else if (op == PO_LIT_DEC) {
+      st[sp].kind = 4; st[sp].p = (const uint8_t*)P.pool + P.lit[i]; st[sp].len = P.arg[i]; sp++;
     } else if (op == PO_LIT_NULL) {
       st[sp++].kind = 0;
     } else if (op >= PO_LT && op <= PO_NSEQ) {
@@ -2197,7 +2273,17 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
       } else if (a.kind == 0 || b.kind == 0) {
         r.kind = 0;
       } else {
-        const int c = a.kind == 2 ? bytes_cmp(a.p, a.len, b.p, b.len) : (a.v < b.v ? -1 : a.v > b.v ? 1 : 0);
+        int c;
+        if (a.kind == 2) {
+          c = bytes_cmp(a.p, a.len, b.p, b.len);
+        } else if (a.kind == 4) {
+          DecNum x{}, y{};
+          dec_parse(a.p, a.len, &x);                     // both validated (field load / host planner)
+          dec_parse(b.p, b.len, &y);
+          c = dec_cmp(x, y);
+        } else {
+          c = a.v < b.v ? -1 : a.v > b.v ? 1 : 0;
+        }
         r.v = op == PO_LT ? c < 0 : op == PO_LE ? c <= 0 : op == PO_GT ? c > 0 : op == PO_GE ? c >= 0 : c == 0;
       }
       st[sp++] = r;

@@ -50,6 +50,11 @@ class Literal:
         return Literal(int(micros_since_epoch_utc), "timestamp")
 
     @staticmethod
+    def ofDecimal(value, precision, scale):              # Literal.ofDecimal(BigDecimal, int, int)
+        from decimal import Decimal
+        return Literal(Decimal(value), "decimal(%d,%d)" % (precision, scale))
+
+    @staticmethod
     def ofString(v):
         return Literal(str(v), "string")
 

@@ -7,8 +7,9 @@ string) and compiled to the postfix program k_part_eval runs (ScanImpl.applyPart
 ScanImpl.java:247-294).
 
 Supported: partition columns of type string, long, integer, short, byte, date (values through
-java.sql.Date.valueOf, PartitionValueEvaluator.java:72-73); literals of a matching kind (string with
-string, any integral with integral, date with date, or null); =, <, <=, >, >=, IS NOT DISTINCT
+java.sql.Date.valueOf, PartitionValueEvaluator.java:72-73), decimal (new BigDecimal(text), :112-113,
+compared with compareTo); literals of a matching kind (string with string, any integral with
+integral, date with date, decimal with decimal, or null); =, <, <=, >, >=, IS NOT DISTINCT
 FROM, IS_NULL, IS_NOT_NULL, NOT, AND, OR. Anything else raises UnsupportedPartitionFilter, so an
 accepted filter is evaluated exactly as the reference evaluates it.
 """
@@ -18,10 +19,10 @@ import json
 
 from .expressions import Column, Literal, Predicate
 
-PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4, "date": 5}
+PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4, "date": 5, "decimal": 6}
 INTEGRAL = {"long", "integer", "short", "byte"}
 (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LT, PO_LE, PO_GT, PO_GE, PO_EQ, PO_NSEQ, PO_ISNULL,
- PO_ISNOTNULL, PO_NOT, PO_AND, PO_OR) = range(15)
+ PO_ISNOTNULL, PO_NOT, PO_AND, PO_OR, PO_LIT_DEC) = range(16)
 CMP = {"<": PO_LT, "<=": PO_LE, ">": PO_GT, ">=": PO_GE, "=": PO_EQ, "IS NOT DISTINCT FROM": PO_NSEQ}
 MAX_FIELDS, MAX_OPS, MAX_STACK, POOL = 8, 64, 16, 1024
 
@@ -52,6 +53,8 @@ def compile_program(pred: Predicate, fields: dict):
         if len(col.names) != 1 or name not in fields:
             raise ValueError("%s is not present in metadata" % col.names[0])   # PartitionUtils.java:340-343
         t, phys = fields[name]
+        if t.startswith("decimal"):
+            t = "decimal"
         if t not in PT:
             raise UnsupportedPartitionFilter("partition pruning on %s column %s is not supported by this engine build"
                                              % (t, col.names[0]))
@@ -64,7 +67,7 @@ def compile_program(pred: Predicate, fields: dict):
         if isinstance(node, Column):
             k, t = field(node)
             ops.append((PO_FIELD, k, 0))
-            return t if t in ("string", "date") else "integral"
+            return t if t in ("string", "date", "decimal") else "integral"
         if isinstance(node, Literal):
             if node.value is None:
                 ops.append((PO_LIT_NULL, 0, 0))
@@ -74,6 +77,15 @@ def compile_program(pred: Predicate, fields: dict):
                 ops.append((PO_LIT_STR, len(b), len(pool)))
                 pool.extend(b)
                 return "string"
+            if node.type.startswith("decimal"):                # BigDecimal text, compareTo on the GPU
+                from decimal import Decimal
+                v = Decimal(node.value)
+                if not v.is_finite():
+                    raise UnsupportedPartitionFilter("decimal literal %s is not finite" % v)
+                b = str(v).encode("ascii")
+                ops.append((PO_LIT_DEC, len(b), len(pool)))
+                pool.extend(b)
+                return "decimal"
             if node.type in INTEGRAL | {"date"} and isinstance(node.value, int) and not isinstance(node.value, bool):
                 ops.append((PO_LIT_INT, 0, int(node.value)))   # a date literal is its epoch day
                 return "date" if node.type == "date" else "integral"
@@ -118,7 +130,7 @@ def compile_program(pred: Predicate, fields: dict):
 def _depth(ops):
     d = hi = 0
     for op, _, _ in ops:
-        if op in (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL):
+        if op in (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LIT_DEC):
             d += 1
         elif op not in (PO_ISNULL, PO_ISNOTNULL, PO_NOT):
             d -= 1

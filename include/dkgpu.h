@@ -126,13 +126,14 @@ typedef struct dk_skip_program {
  * A row stays selected iff the predicate is TRUE (null and false drop it). */
 typedef struct dk_part_program {
   int32_t n_fields;                /* <= 8 partition columns                                      */
-  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string, 5 date        */
+  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string, 5 date, 6 decimal */
   int32_t name_off[8];             /* physical column name (map key): offset / length in pool      */
   int32_t name_len[8];
   int32_t n_ops;                   /* <= 64                                                       */
   int32_t op[64];                  /* 0 FIELD(arg) 1 LIT_INT(lit) 2 LIT_STR(pool[lit], arg bytes) 3 LIT_NULL
                                       4 < 5 <= 6 > 7 >= 8 = 9 IS NOT DISTINCT FROM 10 IS_NULL
-                                      11 IS_NOT_NULL 12 NOT 13 AND 14 OR                          */
+                                      11 IS_NOT_NULL 12 NOT 13 AND 14 OR
+                                      15 LIT_DEC(BigDecimal text pool[lit], arg bytes)            */
   int32_t arg[64];
   int64_t lit[64];
   char pool[1024];

@@ -19,6 +19,7 @@ import re
 RANGES = {"long": (-(1 << 63), (1 << 63) - 1), "integer": (-(1 << 31), (1 << 31) - 1),
           "short": (-(1 << 15), (1 << 15) - 1), "byte": (-(1 << 7), (1 << 7) - 1)}
 _INT = re.compile(rb"^[+-]?[0-9]+$")
+_DEC = re.compile(rb"^[+-]?(?:[0-9]+\.?([0-9]*)|\.([0-9]+))(?:[eE]([+-]?[0-9]+))?\Z")
 
 
 class PartitionValueError(RuntimeError):
@@ -42,6 +43,15 @@ def element_at(pv, key: bytes):
 def deserialize(v, typ):
     if v is None or typ == "string":
         return v
+    if typ.startswith("decimal"):                      # new BigDecimal(text): PartitionValueEvaluator :112-113
+        from decimal import Decimal
+        m = _DEC.match(v)
+        if not m:
+            raise PartitionValueError("Character array is missing \"exponent\" mark 'e' or 'E': %r" % v)
+        frac = len(m.group(1) or m.group(2) or b"")
+        if not -(1 << 31) <= frac - int(m.group(3) or 0) < (1 << 31):
+            raise PartitionValueError("Scale out of range: %r" % v)
+        return Decimal(v.decode("ascii"))
     if typ == "date":                                  # PartitionValueEvaluator.java:72-73
         from oracle.skipping import StatsDecodeError, _date
         try:

@@ -269,3 +269,45 @@ def test_gpu_date_partition_values(tmp_path):
         with pytest.raises(DkError, match="partition"):
             _gpu_files(r, DATE_PREDICATES[0], eng)
     eng.close()
+
+
+# PartitionValueEvaluator.java:112-113: new BigDecimal(value), compared with compareTo
+DEC_PVS = [{"p": "1.50"}, {"p": "1.5"}, {"p": "-0.001"}, {"p": "1E+1"}, {"p": ".5"}, {"p": None}, {"p": "0.00"},
+           {"p": "+10"}, {"p": "-1e-3"}, {"p": "123456789012345678901234567890.5"}, {"p": "2."}]
+DEC_PREDICATES = [cmp("=", col("p"), Literal.ofDecimal("1.5", 10, 2)),
+                  cmp(">", col("p"), Literal.ofDecimal("1.499", 10, 3)),
+                  cmp("<", col("p"), Literal.ofDecimal("0", 10, 0)),
+                  cmp("=", col("p"), Literal.ofDecimal("10", 10, 0)),
+                  cmp("<=", col("p"), Literal.ofDecimal("0.5000", 10, 4)),
+                  Or(Predicate("IS_NULL", col("p")), cmp(">=", col("p"), Literal.ofDecimal("1E+29", 38, 0)))]
+DEC_BAD_PVS = ["x", "", "1.2.3", "1e", " 1", "e5", "1e99999999999", "\u0661"]
+
+
+def test_oracle_decimal_partition_values(tmp_path):
+    from oracle import partitions as opp
+    root = str(tmp_path / "t")
+    _write_pv_table(root, DEC_PVS, "decimal(38,3)")
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in DEC_PREDICATES]
+    assert got == [[0, 1], [0, 1, 3, 7, 9, 10], [2, 8], [3, 7], [2, 4, 6, 8], [5, 9]]
+    for i, bad in enumerate(DEC_BAD_PVS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(10,2)")
+        with pytest.raises(opp.PartitionValueError):
+            oracle_files(r, DEC_PREDICATES[0])
+
+
+@pytest.mark.gpu
+def test_gpu_decimal_partition_values(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_pv_table(root, DEC_PVS, "decimal(38,3)")
+    eng = K.GpuEngine()
+    for pred in DEC_PREDICATES:
+        assert _gpu_files(root, pred, eng) == oracle_files(root, pred), pred
+    for i, bad in enumerate(DEC_BAD_PVS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(10,2)")
+        with pytest.raises(DkError, match="partition"):
+            _gpu_files(r, DEC_PREDICATES[0], eng)
+    eng.close()
