@@ -1669,7 +1669,7 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   if (P.n_paths < 0 || P.n_paths > SK_MAX_PATHS || P.n_ops <= 0 || P.n_ops > SK_MAX_OPS)
     return fail("dk_replay_set_skipping: bad program size");
   for (int p = 0; p < P.n_paths; p++) {
-    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_TIMESTAMP)
+    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DECIMAL)
       return fail("dk_replay_set_skipping: bad stats path");
     for (int d = 0; d < P.path_depth[p]; d++)
       if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
@@ -1681,7 +1681,7 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
     if (op == OP_STAT) { if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail("dk_replay_set_skipping: bad stat"); depth++; }
     else if (op == OP_LIT) depth++;
     else if (op == OP_TIMEADD) { if (depth < 1) return fail("dk_replay_set_skipping: stack underflow"); }
-    else if (op == OP_LIT_STR) {
+    else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
       if (P.arg[k] < 0 || P.lit[k] < 0 || P.lit[k] + P.arg[k] > SK_NAMES) return fail("dk_replay_set_skipping: bad string literal");
       depth++;
     }

@@ -1925,6 +1925,11 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
             if ((leaf >> p) & 1) {
               const int t = P.path_type[p];
               if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP) return false;   // textual types need a JSON string
+              if (t == SK_DECIMAL) {                  // decimalValue() of the token: kept as its span
+                val[p] = (long long)i | ((long long)(e - i) << 32);
+                *set |= 1u << p;
+                continue;
+              }
               if (t == SK_SHORT || t == SK_BYTE) {
                 if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
               } else if (!integral || !fits) {
@@ -2010,7 +2015,85 @@ struct Utf8Cursor {
   }
 };
 
-// stack slot kinds: 0 integral (or boolean), 1 stats string (packed span), 2 literal string
+// A decimal partition value: new BigDecimal(text) (PartitionValueEvaluator.java:112-113), compared
+// with BigDecimal.compareTo (numeric, scale-insensitive). Grammar: [+-] digits [. digits] | [+-] .
+// digits, then optional [eE][+-]digits; the scale (fraction digits - exponent) must fit an int.
+// Non-ASCII digits (which Character.isDigit accepts) are a malformed value in this build.
+struct DecNum {
+  const uint8_t* s;
+  int32_t first, end;   // first significant digit, end of the mantissa ('.' skipped when walking)
+  int sign;             // 0 for zero
+  long long adj;        // decimal exponent of the first significant digit
+};
+
+__device__ bool dec_parse(const uint8_t* s, int32_t n, DecNum* d) {
+  int32_t i = 0;
+  bool neg = false;
+  if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
+  const int32_t m0 = i;
+  int32_t dot = -1, ndig = 0, int_digits = 0, first = -1, first_idx = 0;
+  for (; i < n && s[i] != 'e' && s[i] != 'E'; i++) {
+    if (s[i] == '.') { if (dot >= 0) return false; dot = i; continue; }
+    if (s[i] < '0' || s[i] > '9') return false;
+    if (first < 0 && s[i] != '0') { first = i; first_idx = ndig; }
+    if (dot < 0) int_digits++;
+    ndig++;
+  }
+  if (ndig == 0) return false;
+  const int32_t mend = i;
+  long long ex = 0;
+  if (i < n) {                                        // exponent
+    i++;
+    bool eneg = false;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; i++; }
+    if (i >= n) return false;
+    for (; i < n; i++) {
+      if (s[i] < '0' || s[i] > '9') return false;
+      ex = ex * 10 + (s[i] - '0');
+      if (ex > 4000000000ll) return false;
+    }
+    if (eneg) ex = -ex;
+  }
+  const long long scale = (long long)(ndig - int_digits) - ex;
+  if (scale < -2147483648ll || scale > 2147483647ll) return false;
+  (void)m0;
+  d->s = s; d->end = mend;
+  if (first < 0) { d->sign = 0; d->first = mend; d->adj = 0; return true; }
+  d->sign = neg ? -1 : 1;
+  d->first = first;
+  d->adj = (long long)int_digits - 1 - first_idx + ex;
+  return true;
+}
+
+__device__ int dec_cmp(const DecNum& a, const DecNum& b) {
+  if (a.sign != b.sign) return a.sign < b.sign ? -1 : 1;
+  if (a.sign == 0) return 0;
+  int mag = 0;
+  if (a.adj != b.adj) {
+    mag = a.adj < b.adj ? -1 : 1;
+  } else {
+    int32_t i = a.first, j = b.first;
+    while (true) {
+      while (i < a.end && a.s[i] == '.') i++;
+      while (j < b.end && b.s[j] == '.') j++;
+      if (i >= a.end && j >= b.end) break;
+      const int x = i < a.end ? a.s[i++] - '0' : 0;
+      const int y = j < b.end ? b.s[j++] - '0' : 0;
+      if (x != y) { mag = x < y ? -1 : 1; break; }
+    }
+  }
+  return a.sign > 0 ? mag : -mag;
+}
+
+__device__ void sk_decimal(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len, DecNum* d) {
+  *d = DecNum{};
+  if (kind == 3) dec_parse(s + (int32_t)(v & 0x7fffffff), (int32_t)(v >> 32), d);   // a validated JSON number
+  else dec_parse((const uint8_t*)P.names + v, lit_len, d);                          // host-checked literal
+}
+
+
+// stack slot kinds: 0 integral (or boolean), 1 stats string (packed span), 2 literal string,
+// 3 stats decimal (packed number-token span), 4 literal decimal (BigDecimal text in names)
 __device__ Utf8Cursor sk_cursor(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len) {
   Utf8Cursor c;
   c.np = c.pp = 0;
@@ -2043,18 +2126,26 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
     const int op = P.op[k];
     if (op == OP_STAT) {
       const int p = P.arg[k];
-      sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1; sk[sp] = P.path_type[p] == SK_STRING; sp++;
+      sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1;
+      sk[sp] = P.path_type[p] == SK_STRING ? 1 : P.path_type[p] == SK_DECIMAL ? 3 : 0; sp++;
     } else if (op == OP_LIT) {
       sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sp++;
     } else if (op == OP_TIMEADD) {                     // DefaultExpressionEvaluator.visitTimeAdd :593-625
       if (sp > 0 && sn[sp - 1] >= 0) sv[sp - 1] += P.lit[k];
-    } else if (op == OP_LIT_STR) {
-      sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = 2; sl[sp] = P.arg[k]; sp++;
+    } else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
+      sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = op == OP_LIT_STR ? 2 : 4; sl[sp] = P.arg[k]; sp++;
     } else if (op >= OP_LT && op <= OP_EQ) {
       const long long b = sv[--sp]; const int8_t bn = sn[sp], bk = sk[sp]; const int32_t bl = sl[sp];
       const long long a = sv[--sp]; const int8_t an = sn[sp], ak = sk[sp]; const int32_t al = sl[sp];
       int8_t r;
       if (an < 0 || bn < 0) r = -1;
+      else if (ak >= 3 || bk >= 3) {                    // BigDecimal.compareTo
+        DecNum x, y;
+        sk_decimal(ak, a, s, P, al, &x);
+        sk_decimal(bk, b, s, P, bl, &y);
+        const int c = dec_cmp(x, y);
+        r = op == OP_LT ? c < 0 : op == OP_LE ? c <= 0 : op == OP_GT ? c > 0 : op == OP_GE ? c >= 0 : c == 0;
+      }
       else if (ak || bk) {
         const int c = sk_strcmp(sk_cursor(ak, a, s, P, al), sk_cursor(bk, b, s, P, bl));
         r = op == OP_LT ? c < 0 : op == OP_LE ? c <= 0 : op == OP_GT ? c > 0 : op == OP_GE ? c >= 0 : c == 0;
@@ -2134,76 +2225,6 @@ __device__ __forceinline__ int bytes_cmp(const uint8_t* a, int32_t na, const uin
   for (int32_t i = 0; i < m; i++)
     if (a[i] != b[i]) return (int)a[i] - (int)b[i];
   return na < nb ? -1 : na > nb ? 1 : 0;
-}
-
-// A decimal partition value: new BigDecimal(text) (PartitionValueEvaluator.java:112-113), compared
-// with BigDecimal.compareTo (numeric, scale-insensitive). Grammar: [+-] digits [. digits] | [+-] .
-// digits, then optional [eE][+-]digits; the scale (fraction digits - exponent) must fit an int.
-// Non-ASCII digits (which Character.isDigit accepts) are a malformed value in this build.
-struct DecNum {
-  const uint8_t* s;
-  int32_t first, end;   // first significant digit, end of the mantissa ('.' skipped when walking)
-  int sign;             // 0 for zero
-  long long adj;        // decimal exponent of the first significant digit
-};
-
-__device__ bool dec_parse(const uint8_t* s, int32_t n, DecNum* d) {
-  int32_t i = 0;
-  bool neg = false;
-  if (i < n && (s[i] == '+' || s[i] == '-')) { neg = s[i] == '-'; i++; }
-  const int32_t m0 = i;
-  int32_t dot = -1, ndig = 0, int_digits = 0, first = -1, first_idx = 0;
-  for (; i < n && s[i] != 'e' && s[i] != 'E'; i++) {
-    if (s[i] == '.') { if (dot >= 0) return false; dot = i; continue; }
-    if (s[i] < '0' || s[i] > '9') return false;
-    if (first < 0 && s[i] != '0') { first = i; first_idx = ndig; }
-    if (dot < 0) int_digits++;
-    ndig++;
-  }
-  if (ndig == 0) return false;
-  const int32_t mend = i;
-  long long ex = 0;
-  if (i < n) {                                        // exponent
-    i++;
-    bool eneg = false;
-    if (i < n && (s[i] == '+' || s[i] == '-')) { eneg = s[i] == '-'; i++; }
-    if (i >= n) return false;
-    for (; i < n; i++) {
-      if (s[i] < '0' || s[i] > '9') return false;
-      ex = ex * 10 + (s[i] - '0');
-      if (ex > 4000000000ll) return false;
-    }
-    if (eneg) ex = -ex;
-  }
-  const long long scale = (long long)(ndig - int_digits) - ex;
-  if (scale < -2147483648ll || scale > 2147483647ll) return false;
-  (void)m0;
-  d->s = s; d->end = mend;
-  if (first < 0) { d->sign = 0; d->first = mend; d->adj = 0; return true; }
-  d->sign = neg ? -1 : 1;
-  d->first = first;
-  d->adj = (long long)int_digits - 1 - first_idx + ex;
-  return true;
-}
-
-__device__ int dec_cmp(const DecNum& a, const DecNum& b) {
-  if (a.sign != b.sign) return a.sign < b.sign ? -1 : 1;
-  if (a.sign == 0) return 0;
-  int mag = 0;
-  if (a.adj != b.adj) {
-    mag = a.adj < b.adj ? -1 : 1;
-  } else {
-    int32_t i = a.first, j = b.first;
-    while (true) {
-      while (i < a.end && a.s[i] == '.') i++;
-      while (j < b.end && b.s[j] == '.') j++;
-      if (i >= a.end && j >= b.end) break;
-      const int x = i < a.end ? a.s[i++] - '0' : 0;
-      const int y = j < b.end ? b.s[j++] - '0' : 0;
-      if (x != y) { mag = x < y ? -1 : 1; break; }
-    }
-  }
-  return a.sign > 0 ? mag : -mag;
 }
 
 struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean, 4 decimal text

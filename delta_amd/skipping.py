@@ -13,12 +13,14 @@ from __future__ import annotations
 
 import json
 
+from decimal import Decimal as _Decimal
+
 from .expressions import ALWAYS_TRUE, Column, Literal, Predicate
 
 MIN, MAX, NULL_COUNT, NUM_RECORDS = "minValues", "maxValues", "nullCount", "numRecords"
 SKIPPING_ELIGIBLE = {"byte", "short", "integer", "long", "float", "double", "date", "timestamp",
                      "timestamp_ntz", "string"}          # StatsSchemaHelper.java:209-222 (+ decimal)
-GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp"}          # stats value types k_stats_eval decodes
+GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp", "decimal"}          # stats value types k_stats_eval decodes
 REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
            "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}   # DataSkippingUtils.java:346-356
 NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
@@ -213,9 +215,9 @@ def referenced_stats(node, out=None):
 
 
 # ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
-OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD = range(11)
+OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD, OP_LIT_DEC = range(12)
 _CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
-TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6}
+TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6, "decimal": 7}
 
 
 def stat_type(path, leaves):
@@ -225,7 +227,7 @@ def stat_type(path, leaves):
         return "long"
     for t, phys in leaves.values():
         if phys == path[1:]:
-            return t
+            return "decimal" if t.startswith("decimal") else t
     raise KeyError(path)
 
 
@@ -254,6 +256,10 @@ def compile_program(node, leaves):
             v = n[1]
             if v is None:
                 ops.append((OP_LIT, 1, 0))                   # null literal: comparisons yield null
+            elif isinstance(v, _Decimal):                    # BigDecimal text, compareTo on the GPU
+                if not v.is_finite():
+                    raise UnsupportedSkipping("decimal literal %s is not finite" % v)
+                ops.append((OP_LIT_DEC, 0, str(v).encode("ascii")))
             elif isinstance(v, str):                         # compared as UTF-8 bytes (String.getBytes)
                 ops.append((OP_LIT_STR, 0, v.encode("utf-8", "replace")))
             elif isinstance(v, bool) or not isinstance(v, int):
@@ -280,9 +286,11 @@ def compile_program(node, leaves):
 
 def _operand_kind(n, leaves):
     if n[0] == "stat":
-        return "string" if stat_type(n[1], leaves) == "string" else "number"
+        t = stat_type(n[1], leaves)
+        return t if t in ("string", "decimal") else "number"
     if n[0] == "lit":
-        return None if n[1] is None else "string" if isinstance(n[1], str) else "number"
+        v = n[1]
+        return None if v is None else "string" if isinstance(v, str) else "decimal" if isinstance(v, _Decimal) else "number"
     return "number"
 
 
@@ -292,7 +300,7 @@ MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 512
 def _stack_depth(ops):
     d = hi = 0
     for op, _, _ in ops:
-        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR) else 0 if op == OP_TIMEADD else -1
+        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR, OP_LIT_DEC) else 0 if op == OP_TIMEADD else -1
         hi = max(hi, d)
     return hi
 
@@ -317,7 +325,7 @@ def pack(program, struct_type):
         raise UnsupportedSkipping("stats field names exceed %d bytes" % NAMES_BYTES)
     packed = []
     for op, arg, lit in ops:
-        if op == OP_LIT_STR:                                 # literal bytes follow the names
+        if op in (OP_LIT_STR, OP_LIT_DEC):                   # literal bytes follow the names
             packed.append((op, len(lit), len(names)))
             names += lit
         else:

@@ -108,14 +108,15 @@ void dk_json_tail_free(dk_json_tail* t);
 typedef struct dk_skip_program {
   int32_t n_paths;                 /* <= 8 stats fields                                        */
   int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte, 4 date (epoch days), 5 string,
-                                      6 timestamp (micros since epoch) */
+                                      6 timestamp (micros since epoch), 7 decimal */
   int32_t path_depth[8];           /* name components, 1..4 ("maxValues","id" -> 2)             */
   int32_t name_off[8][4];          /* component names: offsets / lengths into names (UTF-8)     */
   int32_t name_len[8][4];
   char names[512];
   int32_t n_ops;                   /* <= 64                                                     */
   int32_t op[64];                  /* 0 STAT(arg=path), 1 LIT(arg=1: null), 2 <, 3 <=, 4 >, 5 >=, 6 =, 7 AND, 8 OR,
-                                      9 LIT_STR(UTF-8 bytes names[lit, lit + arg)), 10 TIMEADD(top += lit micros) */
+                                      9 LIT_STR(UTF-8 bytes names[lit, lit + arg)), 10 TIMEADD(top += lit micros),
+                                      11 LIT_DEC(BigDecimal text names[lit, lit + arg)) */
   int32_t arg[64];
   int64_t lit[64];
 } dk_skip_program;

@@ -114,6 +114,10 @@ def _timestamp(text):
 def _leaf(v, typ):
     if v is None:
         return None
+    if typ == "decimal":                               # DefaultJsonRow: isNumber -> decimalValue()
+        if isinstance(v, bool) or not isinstance(v, (int, Decimal)):
+            raise StatsDecodeError("Couldn't decode %r, expected a decimal" % (v,))
+        return Decimal(v)
     if typ == "timestamp":
         if not isinstance(v, str):
             raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % (v,))

@@ -3,8 +3,8 @@
 Pinned to the reference's own expectations on its golden tables (KDT = kernel-defaults/src/test/scala/
 io/delta/kernel/defaults):
   ScanSuite.scala:1150-1196  basic data skipping for all types (+ column mapping name/id, checkpoint):
-                             hits / misses for int, long, byte, short, date and string (the types the
-                             GPU evaluator decodes; float/double/decimal filters are refused)
+                             hits / misses for int, long, byte, short, date, string and decimal (the
+                             types the GPU evaluator decodes; float/double filters are refused)
   ScanSuite.scala:1233-1239  filter on a non-existent column -> no skipping
   ScanSuite.scala:1243-1253  AND of two data columns -> 1 file
   ScanSuite.scala:1255-1267  stats collected changing across versions -> 1 / 2 / 1 files
@@ -51,6 +51,7 @@ def all_types_hits_misses():
     hits, misses = [], []
     cases = [(name, lit(0), lit(-1), lit(1)) for name, lit in INTEGRAL.items()] + [("as_date",) + DATES]
     cases.append(("as_string", Literal.ofString("0"), Literal.ofString("!"), Literal.ofString("1")))   # :1157
+    cases.append(("as_big_decimal",) + tuple(Literal.ofDecimal(v, 1, 0) for v in (0, -1, 1)))        # :1162-1164
     for name, value, small, big in cases:
         c = col(name)
         misses += [cmp("=", c, small), cmp(">", c, value), cmp(">=", c, big), cmp("<", c, value),
@@ -621,4 +622,52 @@ def test_gpu_timestamp_stats_parity(tmp_path):
         _write_edge_table(b, [TS_SPARK_STATS, bad], TS_COLUMNS)
         with pytest.raises(DkError, match="data skipping"):
             _gpu_files(b, TS_HITS[0], eng)
+    eng.close()
+
+
+DEC_COLUMNS = (("x", "decimal(38,4)"), ("id", "long"))
+DEC_EDGE_STATS = [
+    '{"numRecords":2,"minValues":{"x":1.50},"maxValues":{"x":2}}',
+    '{"numRecords":2,"minValues":{"x":-1E+2},"maxValues":{"x":-0.0001}}',
+    '{"numRecords":2,"minValues":{"x":123456789012345678901234567890.12},"maxValues":{"x":1.2345678901234567890123456789012E+31}}',
+    '{"numRecords":2,"minValues":{"x":0},"maxValues":{"x":0.00e5},"nullCount":{"x":0}}',
+    '{"numRecords":2,"minValues":{"x":null},"maxValues":{"x":1.5}}',
+    None,
+]
+DEC_PREDICATES = [cmp("=", col("x"), Literal.ofDecimal("1.5", 10, 2)),
+                  cmp("<", col("x"), Literal.ofDecimal("0", 1, 0)),
+                  cmp(">", col("x"), Literal.ofDecimal("1.2345678901234567890123456789011E+31", 38, 0)),
+                  cmp("=", col("x"), Literal.ofDecimal("0.000", 4, 3)),
+                  cmp(">=", col("x"), Literal.ofDecimal("1.5000000000000000001", 38, 19))]
+DEC_BAD_STATS = ['{"numRecords":2,"minValues":{"x":"1.5"}}', '{"numRecords":2,"minValues":{"x":true}}',
+                 '{"numRecords":2,"minValues":{"x":{"a":1}}}']
+
+
+def test_oracle_decimal_stats_expected(tmp_path):
+    root = str(tmp_path / "t")
+    _write_edge_table(root, DEC_EDGE_STATS, DEC_COLUMNS)
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in DEC_PREDICATES]
+    assert got == [[0, 4, 5], [1, 4, 5], [2, 5], [3, 4, 5], [0, 2, 5]]   # row 4: null min -> kept
+    from oracle import skipping as osk
+    for i, bad in enumerate(DEC_BAD_STATS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_edge_table(r, [DEC_EDGE_STATS[0], bad], DEC_COLUMNS)
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(r, DEC_PREDICATES[0])
+
+
+@pytest.mark.gpu
+def test_gpu_decimal_stats_parity(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_edge_table(root, DEC_EDGE_STATS, DEC_COLUMNS)
+    eng = K.GpuEngine()
+    for p in DEC_PREDICATES:
+        assert _gpu_files(root, p, eng) == oracle_files(root, p), p
+    for i, bad in enumerate(DEC_BAD_STATS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_edge_table(r, [DEC_EDGE_STATS[0], bad], DEC_COLUMNS)
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(r, DEC_PREDICATES[0], eng)
     eng.close()
