@@ -129,7 +129,7 @@ enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8, E_STATS = 1
 // Data-skipping program (layout of dk_skip_program in include/dkgpu.h): the stats fields to
 // extract from each row's add.stats JSON and a postfix program over them (delta_amd/skipping.py).
 constexpr int SK_MAX_PATHS = 8, SK_MAX_DEPTH = 4, SK_MAX_OPS = 64, SK_NAMES = 512;
-enum : int32_t { SK_LONG = 0, SK_INT = 1, SK_SHORT = 2, SK_BYTE = 3, SK_DATE = 4, SK_STRING = 5, SK_TIMESTAMP = 6, SK_DECIMAL = 7 };
+enum : int32_t { SK_LONG = 0, SK_INT = 1, SK_SHORT = 2, SK_BYTE = 3, SK_DATE = 4, SK_STRING = 5, SK_TIMESTAMP = 6, SK_DECIMAL = 7, SK_TIMESTAMP_NTZ = 8 };
 enum : int32_t { OP_STAT = 0, OP_LIT = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_EQ = 6, OP_AND = 7, OP_OR = 8, OP_LIT_STR = 9, OP_TIMEADD = 10, OP_LIT_DEC = 11 };
 struct DSkipProg {
   int32_t n_paths;

@@ -1669,7 +1669,7 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   if (P.n_paths < 0 || P.n_paths > SK_MAX_PATHS || P.n_ops <= 0 || P.n_ops > SK_MAX_OPS)
     return fail("dk_replay_set_skipping: bad program size");
   for (int p = 0; p < P.n_paths; p++) {
-    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DECIMAL)
+    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_TIMESTAMP_NTZ)
       return fail("dk_replay_set_skipping: bad stats path");
     for (int d = 0; d < P.path_depth[p]; d++)
       if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)

@@ -1788,21 +1788,27 @@ __device__ bool ts_digits(const uint8_t* s, int32_t* k, int32_t b, int n, long l
   return true;
 }
 
-__device__ bool js_timestamp(const uint8_t* s, int32_t a, int32_t b, long long* v) {
+// ntz: DefaultKernelUtils.parseTimestampNTZ (DefaultKernelUtils.java:34-40,91-95):
+// "yyyy-MM-dd'T'HH:mm:ss" + optional fraction of 1-6 digits, no offset, read as UTC, SMART resolver
+// (a day past the month end is clamped to its last day); an upper-case 'T' only.
+__device__ bool js_timestamp(const uint8_t* s, int32_t a, int32_t b, long long* v, bool ntz = false) {
   int32_t k = a;
   long long y, mo, d, h, mi, sec = 0, nanos = 0;
   if (!ts_digits(s, &k, b, 4, &y) || k >= b || s[k++] != '-' || !ts_digits(s, &k, b, 2, &mo) ||
-      k >= b || s[k++] != '-' || !ts_digits(s, &k, b, 2, &d) || k >= b || (s[k] | 0x20) != 't')
+      k >= b || s[k++] != '-' || !ts_digits(s, &k, b, 2, &d) || k >= b ||
+      (ntz ? s[k] != 'T' : (s[k] | 0x20) != 't'))
     return false;
   k++;
   if (!ts_digits(s, &k, b, 2, &h) || k >= b || s[k++] != ':' || !ts_digits(s, &k, b, 2, &mi)) return false;
+  if (ntz && (k >= b || s[k] != ':')) return false;     // seconds are required
   if (k < b && s[k] == ':') {
     k++;
     if (!ts_digits(s, &k, b, 2, &sec)) return false;
     if (k < b && s[k] == '.') {
       k++;
+      const int maxd = ntz ? 6 : 9;
       int nd = 0;
-      while (k < b && s[k] >= '0' && s[k] <= '9' && nd < 9) { nanos = nanos * 10 + (s[k] - '0'); k++; nd++; }
+      while (k < b && s[k] >= '0' && s[k] <= '9' && nd < maxd) { nanos = nanos * 10 + (s[k] - '0'); k++; nd++; }
       if (nd == 0 || (k < b && s[k] >= '0' && s[k] <= '9')) return false;
       for (; nd < 9; nd++) nanos *= 10;
     }
@@ -1810,10 +1816,14 @@ __device__ bool js_timestamp(const uint8_t* s, int32_t a, int32_t b, long long* 
   if (y < 1678 || y > 2261 || mo < 1 || mo > 12 || d < 1 || h > 23 || mi > 59 || sec > 59) return false;
   const int dim = mo == 2 ? ((y % 4 == 0 && (y % 100 != 0 || y % 400 == 0)) ? 29 : 28)
                 : (mo == 4 || mo == 6 || mo == 9 || mo == 11) ? 30 : 31;
-  if (d > dim) return false;
-  if (k >= b) return false;
+  if (d > 31) return false;
+  if (d > dim) { if (!ntz) return false; d = dim; }     // STRICT (offset form) vs SMART (ntz)
   long long off = 0;
-  if ((s[k] | 0x20) == 'z') {
+  if (ntz) {
+    if (k != b) return false;
+  } else if (k >= b) {
+    return false;
+  } else if ((s[k] | 0x20) == 'z') {
     k++;
   } else if (s[k] == '+' || s[k] == '-') {
     const bool neg = s[k++] == '-';
@@ -1906,8 +1916,9 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
               if (t == SK_STRING) {                   // body span + escape flag, compared lazily
                 v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
               } else {
-                if ((t != SK_DATE && t != SK_TIMESTAMP) || esc) return false;   // textual types only
-                if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v) : js_timestamp(s, i + 1, e - 1, &v))) return false;
+                if ((t != SK_DATE && t != SK_TIMESTAMP && t != SK_TIMESTAMP_NTZ) || esc) return false;
+                if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v)
+                                   : js_timestamp(s, i + 1, e - 1, &v, t == SK_TIMESTAMP_NTZ))) return false;
               }
               val[p] = v;
               *set |= 1u << p;
@@ -1924,7 +1935,7 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
           for (int p = 0; p < P.n_paths; p++)
             if ((leaf >> p) & 1) {
               const int t = P.path_type[p];
-              if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP) return false;   // textual types need a JSON string
+              if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP || t == SK_TIMESTAMP_NTZ) return false;
               if (t == SK_DECIMAL) {                  // decimalValue() of the token: kept as its span
                 val[p] = (long long)i | ((long long)(e - i) << 32);
                 *set |= 1u << p;

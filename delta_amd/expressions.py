@@ -55,6 +55,10 @@ class Literal:
         return Literal(Decimal(value), "decimal(%d,%d)" % (precision, scale))
 
     @staticmethod
+    def ofTimestampNtz(micros):                          # Literal.ofTimestampNtz(long)
+        return Literal(int(micros), "timestamp_ntz")
+
+    @staticmethod
     def ofString(v):
         return Literal(str(v), "string")
 

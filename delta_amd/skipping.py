@@ -20,7 +20,7 @@ from .expressions import ALWAYS_TRUE, Column, Literal, Predicate
 MIN, MAX, NULL_COUNT, NUM_RECORDS = "minValues", "maxValues", "nullCount", "numRecords"
 SKIPPING_ELIGIBLE = {"byte", "short", "integer", "long", "float", "double", "date", "timestamp",
                      "timestamp_ntz", "string"}          # StatsSchemaHelper.java:209-222 (+ decimal)
-GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp", "decimal"}          # stats value types k_stats_eval decodes
+GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp", "decimal", "timestamp_ntz"}          # stats value types k_stats_eval decodes
 REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
            "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}   # DataSkippingUtils.java:346-356
 NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
@@ -217,7 +217,7 @@ def referenced_stats(node, out=None):
 # ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
 OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD, OP_LIT_DEC = range(12)
 _CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
-TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6, "decimal": 7}
+TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6, "decimal": 7, "timestamp_ntz": 8}
 
 
 def stat_type(path, leaves):

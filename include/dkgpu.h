@@ -108,7 +108,8 @@ void dk_json_tail_free(dk_json_tail* t);
 typedef struct dk_skip_program {
   int32_t n_paths;                 /* <= 8 stats fields                                        */
   int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte, 4 date (epoch days), 5 string,
-                                      6 timestamp (micros since epoch), 7 decimal */
+                                      6 timestamp (micros since epoch), 7 decimal,
+                                      8 timestamp_ntz (micros, read as UTC) */
   int32_t path_depth[8];           /* name components, 1..4 ("maxValues","id" -> 2)             */
   int32_t name_off[8][4];          /* component names: offsets / lengths into names (UTF-8)     */
   int32_t name_len[8][4];

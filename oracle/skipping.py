@@ -111,6 +111,26 @@ def _timestamp(text):
     return total // 1000 if total >= 0 else -((-total) // 1000)     # Java division: toward zero
 
 
+_TS_NTZ = re.compile(r"(\d{4})-(\d{2})-(\d{2})T(\d{2}):(\d{2}):(\d{2})(?:\.(\d{1,6}))?")
+
+
+def _timestamp_ntz(text):
+    """DefaultKernelUtils.parseTimestampNTZ (DefaultKernelUtils.java:34-40,91-95): pattern
+    yyyy-MM-dd'T'HH:mm:ss + optional 1-6 digit fraction, SMART resolver (a day past the month end is
+    clamped to its last day), read as UTC. Same year window and refusals as _timestamp."""
+    m = _TS_NTZ.fullmatch(text) if text.isascii() else None
+    if not m:
+        raise StatsDecodeError("Couldn't decode %r, expected a timestamp_ntz" % text)
+    y, mo, d, h, mi, sec = (int(m.group(i)) for i in range(1, 7))
+    micros = int((m.group(7) or "").ljust(6, "0") or 0)
+    if not (1678 <= y <= 2261 and 1 <= mo <= 12 and 1 <= d <= 31 and h <= 23 and mi <= 59 and sec <= 59):
+        raise StatsDecodeError("Couldn't decode %r, expected a timestamp_ntz" % text)
+    import calendar
+    d = min(d, calendar.monthrange(y, mo)[1])
+    secs = (_dt.date(y, mo, d) - _dt.date(1970, 1, 1)).days * 86400 + h * 3600 + mi * 60 + sec
+    return secs * 1_000_000 + micros
+
+
 def _leaf(v, typ):
     if v is None:
         return None
@@ -118,6 +138,10 @@ def _leaf(v, typ):
         if isinstance(v, bool) or not isinstance(v, (int, Decimal)):
             raise StatsDecodeError("Couldn't decode %r, expected a decimal" % (v,))
         return Decimal(v)
+    if typ == "timestamp_ntz":
+        if not isinstance(v, str):
+            raise StatsDecodeError("Couldn't decode %r, expected a timestamp_ntz" % (v,))
+        return _timestamp_ntz(v)
     if typ == "timestamp":
         if not isinstance(v, str):
             raise StatsDecodeError("Couldn't decode %r, expected a timestamp" % (v,))

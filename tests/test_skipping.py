@@ -671,3 +671,68 @@ def test_gpu_decimal_stats_parity(tmp_path):
         with pytest.raises(DkError, match="data skipping"):
             _gpu_files(r, DEC_PREDICATES[0], eng)
     eng.close()
+
+
+# ScanSuite.scala:808-842 (TIMESTAMP_NTZ): stats written without an offset; max widened by +1 ms
+NTZ_COLUMNS = (("ts", "timestamp_ntz"), ("nested", {"type": "struct", "fields": [
+    {"name": "ts", "type": "timestamp_ntz", "nullable": True, "metadata": {}}]}))
+NTZ_SPARK_STATS = TS_SPARK_STATS.replace(".456Z", ".456")
+
+
+def _ntz(op, c, text):
+    return cmp(op, c, Literal.ofTimestampNtz(_micros(text)))
+
+
+NTZ_HITS = [_ntz(p.name, p.children[0], t) for p, t in zip(TS_HITS, ["2019-09-09T01:02:03.456789Z"] * 5)]
+NTZ_MISSES = [_ntz(p.name, p.children[0], t) for p, t in zip(TS_MISSES, ["2019-09-09T01:02:03.457001Z"] * 2 +
+                                                            ["2019-09-09T01:02:03.455999Z"] +
+                                                            ["2019-09-09T01:02:03.457001Z", "2019-09-09T01:02:03.455999Z"])]
+NTZ_EDGE_STATS = ['{"numRecords":1,"minValues":{"ts":"2019-02-30T00:00:00"},"maxValues":{"ts":"2019-02-28T00:00:00.5"}}',
+                  '{"numRecords":1,"minValues":{"ts":"2020-02-31T23:59:59.999999"},"maxValues":{"ts":"2020-03-01T00:00:00"}}',
+                  None]
+NTZ_EDGE_PREDICATES = [_ntz("=", col("ts"), "2019-02-28T00:00:00.200000Z"), _ntz("<", col("ts"), "2020-02-29T23:59:59.999999Z"),
+                       _ntz(">", col("ts"), "2020-03-01T00:00:00.000500Z")]
+NTZ_BAD_STATS = ['{"numRecords":1,"minValues":{"ts":"2019-09-09t01:02:03"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02"}}',
+                 '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03Z"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03.1234567"}}',
+                 '{"numRecords":1,"minValues":{"ts":"2019-09-32T01:02:03"}}']
+
+
+def test_oracle_timestamp_ntz(tmp_path):
+    root = str(tmp_path / "t")
+    _write_edge_table(root, [NTZ_SPARK_STATS], NTZ_COLUMNS)
+    for p in NTZ_HITS:
+        assert oracle_files(root, p)[0], p
+    for p in NTZ_MISSES:
+        assert not oracle_files(root, p)[0], p
+    r = str(tmp_path / "e")
+    _write_edge_table(r, NTZ_EDGE_STATS, NTZ_COLUMNS)
+    got = [sorted(int(x[0].decode()[1:-8]) for x in oracle_files(r, p)[0]) for p in NTZ_EDGE_PREDICATES]
+    assert got == [[0, 2], [0, 2], [1, 2]]        # Feb 30 -> Feb 28 and Feb 31 -> Feb 29 (SMART clamp)
+    from oracle import skipping as osk
+    for i, bad in enumerate(NTZ_BAD_STATS):
+        b = str(tmp_path / ("b%d" % i))
+        _write_edge_table(b, [NTZ_SPARK_STATS, bad], NTZ_COLUMNS)
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(b, NTZ_HITS[0])
+
+
+@pytest.mark.gpu
+def test_gpu_timestamp_ntz_parity(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    root = str(tmp_path / "t")
+    _write_edge_table(root, [NTZ_SPARK_STATS], NTZ_COLUMNS)
+    eng = K.GpuEngine()
+    for p in NTZ_HITS + NTZ_MISSES:
+        g = _gpu_files(root, p, eng)
+        assert g == oracle_files(root, p) and bool(g[0]) == (p in NTZ_HITS), p
+    r = str(tmp_path / "e")
+    _write_edge_table(r, NTZ_EDGE_STATS, NTZ_COLUMNS)
+    for p in NTZ_EDGE_PREDICATES:
+        assert _gpu_files(r, p, eng) == oracle_files(r, p), p
+    for i, bad in enumerate(NTZ_BAD_STATS):
+        b = str(tmp_path / ("b%d" % i))
+        _write_edge_table(b, [NTZ_SPARK_STATS, bad], NTZ_COLUMNS)
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(b, NTZ_HITS[0], eng)
+    eng.close()
