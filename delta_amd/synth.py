@@ -17,6 +17,7 @@ Paths follow ``<part>/part-<i%1000:05d>-<uuid4>.c000.snappy.parquet`` with ``<pa
 """
 from __future__ import annotations
 
+import dataclasses
 import json
 import os
 import sys
@@ -67,7 +68,8 @@ class TableSpec:
     max_rows_per_page: int = 20_000  # parquet-mr 1.12 page row-count limit
     write_page_index: bool = True
     hot_frac: float = 0.0            # C5 skew: fraction of paths under one hot partition
-    v2_sidecars: int = 0             # > 0: V2 checkpoint = parquet manifest + this many sidecars
+    v2_sidecars: int = 0             # > 0: V2 checkpoint = manifest + this many sidecars
+    v2_manifest: str = "parquet"     # V2 manifest format: "parquet" or "json"
     variable_paths: bool = False     # add random suffixes / escapes so lengths vary
     seed: int = SEED
     extra: dict = field(default_factory=dict)
@@ -336,49 +338,89 @@ def _pm_rows(spec: TableSpec):
     return proto, meta
 
 
-def build_checkpoint_tables(spec: TableSpec, rng):
-    """Returns (list of arrow tables, one per part, in part order; list of checkpoint add paths)."""
+def _part_sizes(spec: TableSpec):
     n = spec.n_adds
-    parts = []
-    per = [n // spec.n_parts + (1 if i < n % spec.n_parts else 0) for i in range(spec.n_parts)]
-    start = 0
-    all_paths = []
+    return [n // spec.n_parts + (1 if i < n % spec.n_parts else 0) for i in range(spec.n_parts)]
+
+
+def _part_rng(spec: TableSpec, pi):
+    """Each checkpoint part draws from its own stream, so parts can be generated in parallel and
+    the table is the same whatever the worker count."""
+    return np.random.Generator(np.random.PCG64([spec.seed, 1 + pi]))
+
+
+def build_part_table(spec: TableSpec, pi, cnt, start, rng):
+    """Arrow table of checkpoint part ``pi``: [protocol, metaData] rows (part 0 only) + ``cnt`` adds +
+    ``ckpt_removes`` tombstones (part 0 only). Returns (table, add path array)."""
     proto, meta = _pm_rows(spec)
-    for pi, cnt in enumerate(per):
-        if spec.extra.get("progress") and pi % 8 == 0:
-            print("[synth] building part %d/%d" % (pi + 1, spec.n_parts), file=sys.stderr, flush=True)
-        adds = _add_struct(rng, cnt, start, spec, data_change=False)
-        all_paths.append(adds.field("path"))
-        n_pm = 2 if pi == 0 else 0
-        n_rm = spec.ckpt_removes if pi == 0 else 0
-        total = n_pm + cnt + n_rm
-        # row layout: [protocol, metaData] + adds + removes
-        add_col = pa.concat_arrays([pa.nulls(n_pm, type=adds.type), adds,
-                                    pa.nulls(n_rm, type=adds.type)]) if (n_pm or n_rm) else adds
-        rm_type = _remove_type()
-        if n_rm:
-            rpaths, rday = gen_paths(rng, n_rm, 10_000_000 + start, spec)
-            rm = pa.StructArray.from_arrays([
-                rpaths, pa.array(np.full(n_rm, 1_699_000_000_000, np.int64)), pa.array(np.ones(n_rm, bool)),
-                pa.array(np.ones(n_rm, bool)), _pv_array(rday, spec, rng),
-                pa.array(rng.integers(1 << 20, 1 << 28, size=n_rm, dtype=np.int64)),
-                pa.nulls(n_rm, type=DV_TYPE), pa.nulls(n_rm, type=pa.int64()),
-                pa.nulls(n_rm, type=pa.int64())], fields=list(rm_type))
-            rm_col = pa.concat_arrays([pa.nulls(n_pm + cnt, type=rm_type), rm])
-        else:
-            rm_col = pa.nulls(total, type=rm_type)
-        if n_pm:
-            meta_col = pa.concat_arrays([pa.array([None, meta], type=METADATA_TYPE),
-                                         pa.nulls(total - 2, type=METADATA_TYPE)])
-            proto_col = pa.concat_arrays([pa.array([proto, None], type=PROTOCOL_TYPE),
-                                          pa.nulls(total - 2, type=PROTOCOL_TYPE)])
-        else:
-            meta_col = pa.nulls(total, type=METADATA_TYPE)
-            proto_col = pa.nulls(total, type=PROTOCOL_TYPE)
-        t = pa.table({"add": add_col, "remove": rm_col, "metaData": meta_col, "protocol": proto_col})
-        parts.append(t)
-        start += cnt
-    return parts, all_paths
+    adds = _add_struct(rng, cnt, start, spec, data_change=False)
+    n_pm = 2 if pi == 0 else 0
+    n_rm = spec.ckpt_removes if pi == 0 else 0
+    total = n_pm + cnt + n_rm
+    # row layout: [protocol, metaData] + adds + removes
+    add_col = pa.concat_arrays([pa.nulls(n_pm, type=adds.type), adds,
+                                pa.nulls(n_rm, type=adds.type)]) if (n_pm or n_rm) else adds
+    rm_type = _remove_type()
+    if n_rm:
+        rpaths, rday = gen_paths(rng, n_rm, 10_000_000 + start, spec)
+        rm = pa.StructArray.from_arrays([
+            rpaths, pa.array(np.full(n_rm, 1_699_000_000_000, np.int64)), pa.array(np.ones(n_rm, bool)),
+            pa.array(np.ones(n_rm, bool)), _pv_array(rday, spec, rng),
+            pa.array(rng.integers(1 << 20, 1 << 28, size=n_rm, dtype=np.int64)),
+            pa.nulls(n_rm, type=DV_TYPE), pa.nulls(n_rm, type=pa.int64()),
+            pa.nulls(n_rm, type=pa.int64())], fields=list(rm_type))
+        rm_col = pa.concat_arrays([pa.nulls(n_pm + cnt, type=rm_type), rm])
+    else:
+        rm_col = pa.nulls(total, type=rm_type)
+    if n_pm:
+        meta_col = pa.concat_arrays([pa.array([None, meta], type=METADATA_TYPE),
+                                     pa.nulls(total - 2, type=METADATA_TYPE)])
+        proto_col = pa.concat_arrays([pa.array([proto, None], type=PROTOCOL_TYPE),
+                                      pa.nulls(total - 2, type=PROTOCOL_TYPE)])
+    else:
+        meta_col = pa.nulls(total, type=METADATA_TYPE)
+        proto_col = pa.nulls(total, type=PROTOCOL_TYPE)
+    t = pa.table({"add": add_col, "remove": rm_col, "metaData": meta_col, "protocol": proto_col})
+    return t, adds.field("path")
+
+
+def _part_job(job):
+    """Build and write one checkpoint part (or V2 sidecar). Returns (part, {local add row: path} for
+    the rows the commit tail picks, file size, (protocol row, metaData row) for a V2 part 0)."""
+    spec, pi, cnt, start, path, picks, sidecar = job
+    t, paths = build_part_table(spec, pi, cnt, start, _part_rng(spec, pi))
+    pm = None
+    if sidecar:
+        if pi == 0:
+            pm = (t.column("protocol")[0].as_py(), t.column("metaData")[1].as_py())
+            t = t.slice(2)
+        t = t.select(["add", "remove"])
+    _write_parquet(t, path, spec)
+    picked = {int(i): paths[int(i)].as_py() for i in picks}
+    return pi, picked, os.path.getsize(path), pm
+
+
+def _run_part_jobs(spec: TableSpec, jobs):
+    """Parts of large tables are built in forked worker processes (call this before the process
+    touches the GPU); small ones in-process. DK_SYNTH_WORKERS caps the worker count."""
+    workers = min(len(jobs), int(os.environ.get("DK_SYNTH_WORKERS", "16")), os.cpu_count() or 1)
+    progress = spec.extra.get("progress")
+    if spec.n_adds < 2_000_000 or workers <= 1:
+        out = []
+        for j in jobs:
+            out.append(_part_job(j))
+            if progress:
+                print("[synth] part %d/%d written" % (len(out), len(jobs)), file=sys.stderr, flush=True)
+        return out
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    out = []
+    with cf.ProcessPoolExecutor(max_workers=workers, mp_context=mp.get_context("fork")) as ex:
+        for r in ex.map(_part_job, jobs):
+            out.append(r)
+            if progress and (len(out) % 8 == 0 or len(out) == len(jobs)):
+                print("[synth] part %d/%d written" % (len(out), len(jobs)), file=sys.stderr, flush=True)
+    return out
 
 
 def _write_parquet(table, path, spec: TableSpec):
@@ -424,28 +466,25 @@ def _uuid(rng):
     return "%s-%s-%s-%s-%s" % (h[:8], h[8:12], h[12:16], h[16:20], h[20:])
 
 
-def _write_v2(log, v, parts, spec: TableSpec, rng):
+def _write_v2_manifest(log, v, sidecars, pm, rng, spec: TableSpec):
     """V2 checkpoint (PROTOCOL.md "V2 Spec"): sidecars under _delta_log/_sidecars/ hold the add /
     remove rows (one per part, P&M rows dropped); the manifest ``<v>.checkpoint.<uuid>.parquet``
-    holds protocol, metaData, checkpointMetadata and one sidecar row per file."""
-    side = os.path.join(log, "_sidecars")
-    os.makedirs(side, exist_ok=True)
-    sc_rows, files = [], []
-    proto_row = meta_row = None
-    for i, t in enumerate(parts):
-        if i == 0:
-            proto_row = t.column("protocol")[0].as_py()
-            meta_row = t.column("metaData")[1].as_py()
-            t = t.slice(2)
-        t = t.select(["add", "remove"])
-        name = "%020d.checkpoint.%010d.%010d.%s.parquet" % (v, i + 1, len(parts), _uuid(rng))
-        fn = os.path.join(side, name)
-        _write_parquet(t, fn, spec)
-        sc_rows.append({"path": name, "sizeInBytes": os.path.getsize(fn), "modificationTime": 1_714_496_113_961,
-                        "tags": None})
-        files.append(fn)
+    (or ``.json``) holds protocol, metaData, checkpointMetadata and one sidecar row per file."""
+    proto_row, meta_row = pm
+    sc_rows = [{"path": name, "sizeInBytes": size, "modificationTime": 1_714_496_113_961, "tags": None}
+               for name, size in sidecars]
+    if spec.v2_manifest == "json":
+        mfn = os.path.join(log, "%020d.checkpoint.%s.json" % (v, _uuid(rng)))
+        # line order of the reference's GOLD/v2-checkpoint-json manifest
+        lines = [{"checkpointMetadata": {"version": v}}]
+        lines += [{"sidecar": {k: r[k] for k in ("path", "sizeInBytes", "modificationTime")}} for r in sc_rows]
+        lines += [{"protocol": proto_row}, {"metaData": _meta_json(meta_row)}]
+        with open(mfn, "w") as f:
+            f.write("\n".join(json.dumps(x) for x in lines) + "\n")
+        return mfn
     n = 3 + len(sc_rows)
-    add_t, rm_t = parts[0].schema.field("add").type, parts[0].schema.field("remove").type
+    t0, _ = build_part_table(dataclasses.replace(spec, ckpt_removes=0), 1, 0, 0, _part_rng(spec, 0))
+    add_t, rm_t = t0.schema.field("add").type, t0.schema.field("remove").type
     man = pa.table({
         "add": pa.nulls(n, type=add_t), "remove": pa.nulls(n, type=rm_t),
         "metaData": pa.array([None, meta_row, None] + [None] * len(sc_rows), type=METADATA_TYPE),
@@ -455,39 +494,65 @@ def _write_v2(log, v, parts, spec: TableSpec, rng):
         "sidecar": pa.array([None, None, None] + sc_rows, type=SIDECAR_TYPE)})
     mfn = os.path.join(log, "%020d.checkpoint.%s.parquet" % (v, _uuid(rng)))
     _write_parquet(man, mfn, spec)
-    return [mfn] + files
+    return mfn
+
+
+def _meta_json(meta_row):
+    """metaData row as a commit-JSON object (map columns come back from arrow as key/value pairs)."""
+    m = dict(meta_row)
+    fmt = dict(m.get("format") or {})
+    fmt["options"] = dict(fmt.get("options") or [])
+    m["format"] = fmt
+    m["configuration"] = dict(m.get("configuration") or [])
+    return {k: v for k, v in m.items() if v is not None}
 
 
 def write_table(root: str, spec: TableSpec):
     """Write the synthetic table under ``root``. Returns a dict describing what was written."""
-    rng = np.random.Generator(np.random.PCG64(spec.seed))
+    rng = np.random.Generator(np.random.PCG64([spec.seed, 0]))     # commit tail, file names
     log = os.path.join(root, "_delta_log")
     os.makedirs(log, exist_ok=True)
-    parts, ck_paths = build_checkpoint_tables(spec, rng)
     v = spec.ckpt_version
-    files = []
-    if spec.v2_sidecars > 0:
-        files = _write_v2(log, v, parts, spec, rng)
-    elif spec.n_parts == 1:
-        fn = os.path.join(log, "%020d.checkpoint.parquet" % v)
-        _write_parquet(parts[0], fn, spec)
-        files.append(fn)
-    else:
-        for i, t in enumerate(parts):
-            fn = os.path.join(log, "%020d.checkpoint.%010d.%010d.parquet" % (v, i + 1, spec.n_parts))
-            _write_parquet(t, fn, spec)
-            files.append(fn)
-    lc = {"version": v, "size": int(sum(t.num_rows for t in parts))}
-    if spec.n_parts > 1 and spec.v2_sidecars == 0:
+    per = _part_sizes(spec)
+    starts = np.concatenate([[0], np.cumsum(per)]).astype(np.int64)
+    n_ck = int(starts[-1])
+    # checkpoint rows the commit tail removes, drawn up front so each part hands back only those
+    n_pool = spec.n_commits * spec.removes_per_commit
+    pool = rng.integers(0, n_ck, size=n_pool) if n_ck else np.zeros(0, np.int64)
+    owner = np.searchsorted(starts, pool, side="right") - 1
+    sidecar = spec.v2_sidecars > 0
+    jobs = []
+    for pi, cnt in enumerate(per):
+        if sidecar:
+            side = os.path.join(log, "_sidecars")
+            os.makedirs(side, exist_ok=True)
+            path = os.path.join(side, "%020d.checkpoint.%010d.%010d.%s.parquet" % (v, pi + 1, spec.n_parts, _uuid(rng)))
+        elif spec.n_parts == 1:
+            path = os.path.join(log, "%020d.checkpoint.parquet" % v)
+        else:
+            path = os.path.join(log, "%020d.checkpoint.%010d.%010d.parquet" % (v, pi + 1, spec.n_parts))
+        picks = np.unique(pool[owner == pi] - starts[pi])
+        jobs.append((spec, pi, cnt, int(starts[pi]), path, picks, sidecar))
+    results = sorted(_run_part_jobs(spec, jobs), key=lambda r: r[0])
+    picked = {}
+    for pi, pk, _, _ in results:
+        for i, p in pk.items():
+            picked[int(starts[pi]) + i] = p
+    files = [j[4] for j in jobs]
+    n_rows_total = n_ck + 2 + spec.ckpt_removes
+    if sidecar:
+        pm = results[0][3]
+        man = _write_v2_manifest(log, v, [(os.path.basename(j[4]), r[2]) for j, r in zip(jobs, results)], pm, rng, spec)
+        files = [man] + files
+    lc = {"version": v, "size": int(n_rows_total)}
+    if spec.n_parts > 1 and not sidecar:
         lc["parts"] = spec.n_parts
     with open(os.path.join(log, "_last_checkpoint"), "w") as f:
         f.write(json.dumps(lc))
 
     # ---- JSON commit tail ----
-    # large_string: the concatenated paths of a 50M+ row checkpoint exceed 2 GiB of chars
-    ck_all = pa.concat_arrays([a.cast(pa.large_string()) for a in ck_paths]) if len(ck_paths) > 1 else ck_paths[0]
-    n_ck = len(ck_all)
     new_serial = 0
+    pool_i = 0
     added_in_tail = []      # paths added by commits (candidates for duplicates / removal)
     removed = []            # paths removed by commits (candidates for re-add)
     for c in range(spec.n_commits):
@@ -497,11 +562,13 @@ def write_table(root: str, spec: TableSpec):
         # removes
         for _ in range(spec.removes_per_commit):
             pick = rng.random()
-            if pick < 0.5 or not added_in_tail:
-                i = int(rng.integers(0, n_ck))
-                p = ck_all[i].as_py()
-            else:
+            if (pick < 0.5 or not added_in_tail) and pool_i < n_pool:
+                p = picked[int(pool[pool_i])]
+                pool_i += 1
+            elif added_in_tail:
                 p = added_in_tail[int(rng.integers(0, len(added_in_tail)))]
+            else:
+                continue
             removed.append(p)
             lines.append(json.dumps(_json_remove(p, "2024-01-01", 1_700_000_000_000 + ver)))
         # adds
@@ -539,4 +606,4 @@ def write_table(root: str, spec: TableSpec):
         with open(os.path.join(log, "%020d.json" % ver), "w") as f:
             f.write("\n".join(lines) + "\n")
     return {"checkpoint_files": files, "version": v + spec.n_commits,
-            "checkpoint_rows": lc["size"]}
+            "checkpoint_rows": n_ck}
