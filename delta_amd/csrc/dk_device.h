@@ -48,6 +48,32 @@ struct DPage {
   int32_t pad3;
 };
 
+// Speculative snappy decode (k_snap_*): compressed streams are cut into DK_SNAP_SEG-byte segments,
+// each walked by one lane; the walker records its first DK_SNAP_REC tag positions.
+constexpr int DK_SNAP_SEG = 2048;
+constexpr int DK_SNAP_REC = 16;
+struct SnapCtx {
+  const DChunk* chunks;
+  const DPage* pages;
+  uint8_t* arena;
+  const int32_t* cpage;      // compressed page -> page index
+  const int32_t* sbase;      // compressed page -> first segment (n_cpages + 1)
+  const int32_t* spage;      // segment -> compressed page
+  int32_t nseg;
+  int32_t* w_exit;           // walker: first tag start >= segment end (-1: the chain broke)
+  int32_t* w_out;            // walker: output bytes of its tags
+  int32_t* w_npos;           // walker: recorded positions
+  int32_t* w_pos;            // [DK_SNAP_REC][nseg] tag positions
+  int32_t* w_cum;            // [DK_SNAP_REC][nseg] walker output before that tag
+  int32_t* t_entry;          // true entry (link: speculative; fix: verified)
+  int32_t* t_out;            // true output bytes
+  int32_t* t_exit;           // true exit (-1: malformed)
+  const int32_t* fbase;      // compressed page -> first fragment (n_cpages + 1)
+  int64_t* fstart;           // fragment -> compressed offset of its first tag
+  int32_t* serial;           // compressed page -> 1: decode on the serial path
+};
+
+
 // One 16 KiB chunk of a string region for the chunk-parallel position scan.
 struct DPosChunk {
   int32_t page, blk0;    // (input) page, first aligned 16-byte block of the region

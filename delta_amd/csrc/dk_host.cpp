@@ -19,8 +19,7 @@
 
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
-void launch_snappy(const DChunk*, DPage*, uint8_t*, int, const int32_t*, const int32_t*, int, const int2*, int64_t*,
-                   int32_t*, hipStream_t);
+void launch_snappy(const SnapCtx&, int, int, const int2*, int, hipStream_t);
 void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
@@ -372,12 +371,12 @@ static int phys_width(int phys, int tl) {
 // kernel timing (HIP events on the engine stream)
 // ------------------------------------------------------------------------------------------------
 struct KTimer {
-  static constexpr int K = 20;
+  static constexpr int K = 24;
   const char* names[K] = {"k_page_headers", "unused", "k_tile_count", "k_tile_scan",
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
-                          "k_snappy", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", "k_part_eval",
-                          nullptr};
+                          "k_snap_walk_link", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", "k_part_eval",
+                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", nullptr, nullptr};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -428,7 +427,8 @@ struct dk_parquet {
   DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp, d_tiles;
   // snappy: compressed pages, their 64 KiB fragment bases / work items / starts, serial flags
   DBuf d_cpage, d_fbase, d_fwork, d_fstart, d_serial;
-  int n_cpages = 0, n_frags = 0;
+  DBuf d_sbase, d_spage, d_snapws;   // speculative-walk segments: page bases, owner page, workspace
+  int n_cpages = 0, n_frags = 0, n_segs = 0;
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
   int n_ltiles = 0;
   DBuf d_pchunks;            // string-position chunks (DPosChunk)
@@ -493,9 +493,19 @@ static int run_pipeline(dk_parquet* p, int mode) {
   { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
   if (mode == -1) return 0;
   if (p->has_compressed) {
-    KTimer::Scope sc(&T, 13, s);
-    launch_snappy(C, P, p->d_arena.as<uint8_t>(), p->n_cpages, p->d_cpage.as<int32_t>(), p->d_fbase.as<int32_t>(),
-                  p->n_frags, p->d_fwork.as<int2>(), p->d_fstart.as<int64_t>(), p->d_serial.as<int32_t>(), s);
+    SnapCtx X{};
+    X.chunks = C; X.pages = P; X.arena = p->d_arena.as<uint8_t>();
+    X.cpage = p->d_cpage.as<int32_t>(); X.sbase = p->d_sbase.as<int32_t>(); X.spage = p->d_spage.as<int32_t>();
+    X.nseg = p->n_segs;
+    int32_t* ws = p->d_snapws.as<int32_t>();
+    const int64_t ns = p->n_segs;
+    X.w_exit = ws; X.w_out = ws + ns; X.w_npos = ws + 2 * ns; X.t_entry = ws + 3 * ns; X.t_out = ws + 4 * ns;
+    X.t_exit = ws + 5 * ns; X.w_pos = ws + 6 * ns; X.w_cum = ws + (6 + DK_SNAP_REC) * ns;
+    X.fbase = p->d_fbase.as<int32_t>(); X.fstart = p->d_fstart.as<int64_t>(); X.serial = p->d_serial.as<int32_t>();
+    { KTimer::Scope s0(&T, 13, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 0, s); }
+    { KTimer::Scope s1(&T, 19, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 1, s); }
+    { KTimer::Scope s2(&T, 20, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 2, s); }
+    { KTimer::Scope s3(&T, 21, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 3, s); }
   }
   { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P, n, arena, runs, s); }
   { KTimer::Scope sc(&T, 2, s); per_column_tiles(p, [&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
@@ -560,7 +570,7 @@ static int prepare(dk_parquet* p) {
                   std::to_string(file_offset(f, pg.hdr_off)) + ")");
   }
   int64_t posn = 0, arena_n = 0, dbp_n = 0;
-  std::vector<int32_t> cpage, fbase(1, 0);
+  std::vector<int32_t> cpage, fbase(1, 0), sbase(1, 0), spage;
   std::vector<int2> fwork;
   for (size_t i = 0; i < p->h_pages.size(); i++) {
     DPage& pg = p->h_pages[i];
@@ -571,13 +581,19 @@ static int prepare(dk_parquet* p) {
         return fail("Error reading Parquet file: " + p->files[p->col_file[ck.col]].path +
                     " (unsupported compression codec " + std::to_string(ck.codec) + ")");
       if (!(pg.ptype == PAGE_DATA_V2 && !pg.is_comp)) {
-        pg.unc_off = arena_n;
-        arena_n += ((int64_t)pg.usize + 15) & ~(int64_t)15;
-        p->has_compressed = true;
         const int64_t lv = pg.ptype == PAGE_DATA_V2 ? (int64_t)pg.rl_len + pg.dl_len : 0;
+        // the decompressed body (after v2's uncompressed levels) starts 16-byte aligned, and the
+        // page's region is padded to 16 bytes (k_snap_frag stores whole dwordx4 granules)
+        pg.unc_off = ((arena_n + lv + 15) & ~(int64_t)15) - lv;
+        arena_n = (pg.unc_off + (int64_t)pg.usize + 15) & ~(int64_t)15;
+        p->has_compressed = true;
         const int64_t body = pg.usize > lv ? pg.usize - lv : 0;
-        const int nf = body > 0 ? (int)((body + 65535) / 65536) : 1;   // k_snappy_* fragments (64 KiB)
+        const int nf = body > 0 ? (int)((body + 65535) / 65536) : 1;   // k_snap_frag fragments (64 KiB)
         for (int k = 0; k < nf; k++) fwork.push_back(make_int2((int)cpage.size(), k));
+        const int64_t cbody = pg.csize > lv ? pg.csize - lv : 0;
+        const int ns = cbody > 0 ? (int)((cbody + DK_SNAP_SEG - 1) / DK_SNAP_SEG) : 1;
+        for (int k = 0; k < ns; k++) spage.push_back((int32_t)cpage.size());
+        sbase.push_back(sbase.back() + ns);
         cpage.push_back((int32_t)i);
         fbase.push_back(fbase.back() + nf);
       }
@@ -645,8 +661,11 @@ static int prepare(dk_parquet* p) {
   if (p->n_cpages) {
     if (upload(p->d_cpage, cpage.data(), cpage.size() * 4, s) || upload(p->d_fbase, fbase.data(), fbase.size() * 4, s) ||
         upload(p->d_fwork, fwork.data(), fwork.size() * sizeof(int2), s) || p->d_fstart.alloc(fwork.size() * 8) ||
-        p->d_serial.alloc(cpage.size() * 4))
+        p->d_serial.alloc(cpage.size() * 4) || upload(p->d_sbase, sbase.data(), sbase.size() * 4, s) ||
+        upload(p->d_spage, spage.data(), spage.size() * 4, s) ||
+        p->d_snapws.alloc(spage.size() * 4 * (6 + 2 * DK_SNAP_REC)))
       return 1;
+    p->n_segs = (int)spage.size();
   }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
   p->bytes_arena = arena_n;
@@ -888,6 +907,12 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
       const bool plain_str = c.phys == PT_BYTE_ARRAY && pg.enc == ENC_PLAIN;
       if (k == "k_string_copy") {
         if (plain_str) { rd += pg.vbytes; wr += pg.n_chars + (key ? 8ll * pg.n_values : 0); }
+      } else if (k == "k_snap_frag") {
+        // snappy pages: compressed body read, decompressed body written (v2 levels excluded)
+        if (pg.unc_off >= 0) {
+          const int64_t lv = pg.ptype == PAGE_DATA_V2 ? (int64_t)pg.rl_len + pg.dl_len : 0;
+          rd += pg.csize - lv; wr += pg.usize - lv;
+        }
       } else if (k == "k_tile_decode") {
         rd += body - pg.vbytes;                                   // level streams
         if (!plain_str) rd += pg.vbytes;                          // values / dictionary indices
@@ -904,6 +929,12 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
         return fail("dk_parquet_kernel_traffic: no byte model for " + k);
       }
     }
+    if (k == "k_snap_frag")                                       // snappy dictionary pages
+      for (const DChunk& ck : p->h_chunks)
+        if (ck.col == (int)ci && ck.dict_page >= 0) {
+          const DPage& d = p->h_pages[ck.dict_page];
+          if (d.unc_off >= 0) { rd += d.csize; wr += d.usize; }
+        }
     if (k == "k_tile_decode")                                     // dictionary pages (read once)
       for (const DChunk& ck : p->h_chunks)
         if (ck.col == (int)ci && ck.dict_page >= 0) {
@@ -1879,7 +1910,7 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
 extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {
   if (i < 0 || i >= KTimer::K) return 1;
   // decode kernels are timed by the parquet object's timer, the rest by the replay's
-  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16))) ? &r->ck->timer : &r->timer;
+  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16) || (i >= 19 && i <= 21))) ? &r->ck->timer : &r->timer;
   *name = t->names[i];
   if (!*name) return 1;
   *count = t->cnt[i];

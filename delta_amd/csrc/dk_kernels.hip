@@ -26,6 +26,13 @@ namespace dk {
 
 constexpr int NT = 256;          // threads per workgroup
 
+// Pointers loaded from memory (DChunk / DColumn fields) are generic to the compiler, which then
+// emits FLAT instructions (they wait on both the vector-memory and the LDS counters). Hot paths
+// re-type such pointers as global ones so they compile to global_load / global_store.
+#define GAS __attribute__((address_space(1)))
+template <class T> __device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 // --------------------------------------------------------------------------------------------
 // small helpers
 // --------------------------------------------------------------------------------------------
@@ -165,11 +172,16 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
   pages[i] = pg;
 }
 
-constexpr int SNAP_FRAG = 65536;
-constexpr int SNAP_WIN = 4096;
+constexpr int SNAP_FRAG = 65536;      // Google snappy compresses every 64 KiB of input on its own
+constexpr int SNAP_SEG = DK_SNAP_SEG; // compressed bytes per speculative walker
+constexpr int SNAP_REC = DK_SNAP_REC; // tag positions a walker records for the convergence test
+constexpr int SNAP_FWIN = 1024;       // k_snap_frag: compressed-stream window (LDS)
+constexpr int SNAP_RING = 4096;       // k_snap_frag: output ring (LDS)
+constexpr int SNAP_FLUSH = 1024;      // k_snap_frag: ring -> HBM flush granule
 
-// compressed-stream window in LDS: in-offsets [ws, ws + SNAP_WIN) (ws may precede the stream start
-// by up to 3 bytes: the window is filled with aligned dword loads, never past the stream end)
+// compressed-stream window in LDS: in-offsets [ws, ws + W) (ws may precede the stream start by up
+// to 3 bytes: the window is filled with aligned dword loads, never past the stream end)
+template <int W>
 struct SnapWin {
   const uint8_t* in;
   int64_t clen, ws;
@@ -177,64 +189,62 @@ struct SnapWin {
   __device__ __forceinline__ void refill(int64_t at) {
     const uintptr_t a4 = ((uintptr_t)(in + at)) & ~(uintptr_t)3;
     ws = at - (int64_t)((uintptr_t)(in + at) - a4);
-    const uintptr_t lim = (uintptr_t)(in + clen);
-    __syncthreads();
-#pragma unroll 4
-    for (int q = threadIdx.x; q < SNAP_WIN / 4; q += 64) {
-      const uintptr_t ad = a4 + (uintptr_t)q * 4;
-      if (ad < lim) win[q] = *(const uint32_t*)ad;
+    const uintptr_t lim = ((uintptr_t)(in + clen) - 1) & ~(uintptr_t)3;   // last dword with stream bytes
+    // all loads first (addresses clamped to the stream), then the LDS stores: one HBM round trip
+    uint32_t v[W / 256];
+#pragma unroll
+    for (int k = 0; k < W / 256; k++) {
+      const uintptr_t ad = a4 + (uintptr_t)(threadIdx.x + 64 * k) * 4;
+      v[k] = *(const GAS uint32_t*)(ad < lim ? ad : lim);
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < W / 256; k++) win[threadIdx.x + 64 * k] = v[k];
     __syncthreads();
   }
   __device__ __forceinline__ uint32_t b(int64_t at) const { return ((const uint8_t*)win)[at - ws]; }
-  __device__ __forceinline__ const uint8_t* ptr(int64_t at) const { return (const uint8_t*)win + (at - ws); }
-  __device__ __forceinline__ bool has(int64_t at, int64_t n) const { return at >= ws && at + n <= ws + SNAP_WIN; }
+  __device__ __forceinline__ bool has(int64_t at, int64_t n) const { return at >= ws && at + n <= ws + W; }
 };
 
-// one tag at p (wave-uniform). Literal: off = -1, *p -> first payload byte. Copy: *p -> next tag.
-__device__ __forceinline__ bool snap_tag(SnapWin& w, int64_t* pp, int64_t* len, int64_t* off) {
+// one tag at p (wave-uniform), header bytes from the LDS window. Literal: off = -1, *p -> first
+// payload byte. Copy: *p -> next tag. Bounds were validated by the walk.
+template <int W>
+__device__ __forceinline__ void snap_tag(SnapWin<W>& w, int64_t* pp, int32_t* len, int32_t* off) {
   int64_t p = *pp;
   const int64_t c = w.clen;
-  if ((p + 5 < c ? p + 5 : c) > w.ws + SNAP_WIN) w.refill(p);
-  // the tag and its 4 argument bytes from two aligned LDS dwords (one round trip), made scalar;
-  // bytes past the stream end are never used (the length checks below come first)
+  if ((p + 5 < c ? p + 5 : c) > w.ws + W) w.refill(p);
+  // the tag and its 4 argument bytes from two aligned LDS dwords (one round trip), made scalar
   const int64_t ix = p - w.ws;
   const uint32_t d0 = __builtin_amdgcn_readfirstlane(w.win[ix >> 2]);
   const uint32_t d1 = __builtin_amdgcn_readfirstlane(w.win[(ix >> 2) + 1]);
   const uint64_t q = (((uint64_t)d1 << 32) | d0) >> (8 * (ix & 3));
-  const uint32_t tag = (uint32_t)q & 0xff, b1 = (uint32_t)(q >> 8) & 0xff, b2 = (uint32_t)(q >> 16) & 0xff;
-  const uint32_t b3 = (uint32_t)(q >> 24) & 0xff, b4 = (uint32_t)(q >> 32) & 0xff;
-  p++;
+  const uint32_t tag = (uint32_t)q & 0xff;
   const int kind = tag & 3;
-  *off = -1;
+  p++;
   if (kind == 0) {
-    int64_t l = (tag >> 2) + 1;
+    uint32_t l = (tag >> 2) + 1;
     if (l > 60) {
       const int nb = (int)l - 60;
-      if (p + nb > c) return false;
-      l = (int64_t)b1 | (nb > 1 ? (int64_t)b2 << 8 : 0) | (nb > 2 ? (int64_t)b3 << 16 : 0) | (nb > 3 ? (int64_t)b4 << 24 : 0);
-      l += 1;
+      l = (uint32_t)((q >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
       p += nb;
     }
-    *len = l;
+    *len = (int32_t)l;
+    *off = -1;
   } else if (kind == 1) {
-    if (p + 1 > c) return false;
     *len = ((tag >> 2) & 7) + 4;
-    *off = ((int64_t)(tag >> 5) << 8) | b1;
+    *off = (int32_t)(((tag >> 5) << 8) | ((uint32_t)(q >> 8) & 0xff));
     p += 1;
   } else if (kind == 2) {
-    if (p + 2 > c) return false;
     *len = (tag >> 2) + 1;
-    *off = (int64_t)b1 | ((int64_t)b2 << 8);
+    *off = (int32_t)((q >> 8) & 0xffff);
     p += 2;
   } else {
-    if (p + 4 > c) return false;
     *len = (tag >> 2) + 1;
-    *off = (int64_t)b1 | ((int64_t)b2 << 8) | ((int64_t)b3 << 16) | ((int64_t)b4 << 24);
+    const uint64_t o32 = (q >> 8) & 0xffffffffull;
+    *off = o32 > 0x7fffffffull ? 0x7fffffff : (int32_t)o32;
     p += 4;
   }
   *pp = p;
-  return true;
 }
 
 __device__ __forceinline__ bool snap_stream(const DChunk& ck, const DPage& pg, const uint8_t* arena,
@@ -250,162 +260,294 @@ __device__ __forceinline__ bool snap_stream(const DChunk& ck, const DPage& pg, c
   return true;
 }
 
-__global__ __launch_bounds__(64) void k_snappy_split(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
-                                                     uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
-                                                     const int32_t* __restrict__ fbase, int64_t* __restrict__ fstart,
-                                                     int32_t* __restrict__ serial) {
-  __shared__ uint32_t win[SNAP_WIN / 4 + 1];
-  const int ci = blockIdx.x, lane = threadIdx.x;
-  const DPage pg = pages[cpage[ci]];
-  const DChunk ck = chunks[pg.chunk];
+// One tag at p parsed by a single lane straight from memory (two aligned dwords; buffers are padded
+// past the end). Returns false when the tag or its literal runs past the stream end.
+__device__ __forceinline__ bool snap_parse(const uint8_t* in, int64_t clen, int64_t p, int32_t* adv, int32_t* len) {
+  const uintptr_t a = (uintptr_t)(in + p);
+  const GAS uint32_t* w = (const GAS uint32_t*)(a & ~(uintptr_t)3);
+  const uint64_t d = ((((uint64_t)w[1]) << 32) | w[0]) >> (8 * (a & 3));
+  const uint32_t tag = (uint32_t)d & 0xff;
+  const int kind = tag & 3;
+  if (kind == 0) {
+    int64_t l = (tag >> 2) + 1, hdr = 1;
+    if (l > 60) {
+      const int nb = (int)l - 60;
+      hdr += nb;
+      l = (int64_t)((d >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
+    }
+    if (p + hdr + l > clen) return false;
+    *adv = (int32_t)(hdr + l);
+    *len = (int32_t)l;
+    return true;
+  }
+  const int hdr = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+  if (p + hdr > clen) return false;
+  *adv = hdr;
+  *len = kind == 1 ? (int32_t)(((tag >> 2) & 7) + 4) : (int32_t)((tag >> 2) + 1);
+  return true;
+}
+
+// varint preamble (uncompressed length); returns the first tag's offset, or -1
+__device__ __forceinline__ int64_t snap_preamble(const uint8_t* in, int64_t clen, uint64_t* n) {
+  int64_t p = 0;
+  *n = 0;
+  for (int sh = 0; sh < 35; sh += 7) {
+    if (p >= clen) return -1;
+    const uint32_t b = gp(in)[p++];
+    *n |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) return p;
+  }
+  return -1;
+}
+
+// --------------------------------------------------------------------------------------------
+// K1b: SNAPPY raw-block decompression, speculatively parallel.
+// A snappy stream is one serial chain of tags. It is cut into SNAP_SEG-byte segments:
+//   k_snap_walk   one lane per segment parses tags from the segment's first byte (a guess: it may
+//                 sit inside a literal or a tag) to the first tag at or past the segment end, and
+//                 records its exit, its output bytes and its first SNAP_REC tag positions.
+//   k_snap_link   one lane per segment re-walks from the previous walker's exit (the true entry
+//                 whenever the previous segment's walker joined the true chain) until it meets a
+//                 recorded position -- two chains that share a tag are identical from there on --
+//                 then takes the walker's exit and output; otherwise it walks the whole segment.
+//   k_snap_fix    one wave per page checks that every entry equals the previous segment's true exit
+//                 (re-walking, in order, any segment where it does not), scans the output bytes and
+//                 finds where each 64 KiB output fragment starts in the compressed stream. Google's
+//                 compressor encodes every 64 KiB of input on its own, so no tag straddles a
+//                 fragment boundary and no copy reaches back across one; a page that breaks this
+//                 (legal in the format, never written by snappy) or is malformed goes to the serial
+//                 path.
+//   k_snap_frag   one wave per fragment decodes it through a 4 KiB LDS output ring (back references
+//                 are served from LDS; farther ones from the flushed HBM output) and stores the
+//                 ring to HBM in 1 KiB dwordx4 granules.
+//   k_snappy_serial  flagged pages: one wave decodes the whole page and reports errors.
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool snap_page(const SnapCtx& X, int ci, const uint8_t** in, int64_t* clen, uint8_t** out,
+                                          int64_t* ulen, int64_t* lv) {
+  const DPage pg = X.pages[X.cpage[ci]];
+  if (pg.status != PS_OK) return false;
+  return snap_stream(X.chunks[pg.chunk], pg, X.arena, in, clen, out, ulen, lv);
+}
+
+__global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
+  const int k = blockIdx.x * NT + threadIdx.x;
+  if (k >= X.nseg) return;
+  const int ci = X.spage[k];
+  const int j = k - X.sbase[ci];
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
-  if (pg.status != PS_OK || !snap_stream(ck, pg, arena, &in, &clen, &out, &ulen, &lv)) {
-    if (lane == 0) serial[ci] = 1;
+  int32_t ex = -1, o = 0, n = 0;
+  if (snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
+    int64_t p = (int64_t)j * SNAP_SEG;
+    const int64_t end = p + SNAP_SEG < clen ? p + SNAP_SEG : clen;
+    if (j == 0) { uint64_t un; p = snap_preamble(in, clen, &un); }
+    bool dead = p < 0;
+    while (!dead && p < end) {
+      int32_t adv, len;
+      if (!snap_parse(in, clen, p, &adv, &len)) { dead = true; break; }
+      if (n < SNAP_REC) { X.w_pos[(int64_t)n * X.nseg + k] = (int32_t)p; X.w_cum[(int64_t)n * X.nseg + k] = o; n++; }
+      o += len;
+      p += adv;
+    }
+    ex = dead ? -1 : (int32_t)p;
+  }
+  X.w_exit[k] = ex;
+  X.w_out[k] = o;
+  X.w_npos[k] = n;
+}
+
+// true exit / output of segment j entered at e (serial walk, merging with the walker's recorded
+// positions when `merge`)
+__device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, const uint8_t* in, int64_t clen, int64_t e,
+                                              bool merge, int32_t* tout, int32_t* texit) {
+  const int64_t end = (int64_t)j * SNAP_SEG + SNAP_SEG < clen ? (int64_t)j * SNAP_SEG + SNAP_SEG : clen;
+  if (e < 0) { *tout = 0; *texit = -1; return; }
+  int64_t p = e;
+  int32_t o = 0;
+  const int n = merge ? X.w_npos[k] : 0;
+  int jj = 0;
+  int32_t pj = n > 0 ? X.w_pos[k] : 0;
+  while (true) {
+    while (jj < n && pj < p) { jj++; pj = jj < n ? X.w_pos[(int64_t)jj * X.nseg + k] : 0; }
+    if (jj < n && pj == p) {                 // joined the walker's chain
+      *tout = o + X.w_out[k] - X.w_cum[(int64_t)jj * X.nseg + k];
+      *texit = X.w_exit[k];
+      return;
+    }
+    if (p >= end) { *tout = o; *texit = (int32_t)p; return; }
+    int32_t adv, len;
+    if (!snap_parse(in, clen, p, &adv, &len)) { *tout = o; *texit = -1; return; }
+    o += len;
+    p += adv;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
+  const int k = blockIdx.x * NT + threadIdx.x;
+  if (k >= X.nseg) return;
+  const int ci = X.spage[k];
+  const int j = k - X.sbase[ci];
+  const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
+  int32_t e = -1, tout = 0, tex = -1;
+  if (snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
+    if (j == 0) {                            // walker 0 started on the true chain
+      uint64_t un;
+      e = (int32_t)snap_preamble(in, clen, &un);
+      tout = X.w_out[k];
+      tex = X.w_exit[k];
+    } else {
+      e = X.w_exit[k - 1];
+      snap_seg_from(X, k, j, in, clen, e, true, &tout, &tex);
+    }
+  }
+  X.t_entry[k] = e;
+  X.t_out[k] = tout;
+  X.t_exit[k] = tex;
+}
+
+__global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
+  const int ci = blockIdx.x, lane = threadIdx.x;
+  const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
+  if (!snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
+    if (lane == 0) X.serial[ci] = 1;
     return;
   }
-  for (int64_t i = lane; i < lv; i += 64) out[i - lv] = in[i - lv];   // v2 levels: stored uncompressed
-  const int nfrag = fbase[ci + 1] - fbase[ci];
-  int64_t* fs = fstart + fbase[ci];
-  SnapWin w{in, clen, 0, win};
-  w.refill(0);
-  int64_t p = 0;
-  uint64_t n = 0;
-  for (int sh = 0; sh < 35; sh += 7) {
-    if (p >= clen) break;
-    const uint32_t b = w.b(p++);
-    n |= (uint64_t)(b & 0x7f) << sh;
-    if (!(b & 0x80)) break;
-  }
-  bool bad = (int64_t)n != ulen;
-  int64_t o = 0;
-  int k = 0;
-  if (lane == 0) fs[0] = p;
-  // Window-parallel walk: every lane parses a tag speculatively at p + lane (header bytes from two
-  // aligned LDS dwords); the true chain then hops through the 64 candidates with readlane (a few
-  // scalar cycles per tag instead of an LDS round trip plus a full parse).
-  while (!bad && p < clen) {
-    if ((p + 69 < clen ? p + 69 : clen) > w.ws + SNAP_WIN) w.refill(p);
-    const int64_t q = p + lane;
-    uint32_t adv = 0, olen = 0, ok = 0;
-    int32_t off = -1;
-    if (q < clen) {
-      const int64_t ix = q - w.ws;
-      const uint64_t d = ((((uint64_t)w.win[(ix >> 2) + 1]) << 32) | w.win[ix >> 2]) >> (8 * (ix & 3));
-      const uint32_t tag = (uint32_t)d & 0xff;
-      const int kind = tag & 3;
-      uint32_t hdr = 1;
-      int64_t l = 0;
-      if (kind == 0) {
-        l = (tag >> 2) + 1;
-        if (l > 60) {
-          const int nb = (int)l - 60;
-          hdr += nb;
-          l = (int64_t)((d >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
+  for (int64_t i = lane; i < lv; i += 64) gp(out)[i - lv] = gp(in)[i - lv];   // v2 levels: stored uncompressed
+  uint64_t un;
+  const int64_t b0 = snap_preamble(in, clen, &un);
+  bool bad = b0 < 0 || (int64_t)un != ulen;
+  const int k0 = X.sbase[ci], k1 = X.sbase[ci + 1];
+  int32_t prev_exit = (int32_t)b0;
+  int64_t running = 0;
+  const int f0 = X.fbase[ci], nf = X.fbase[ci + 1] - f0;
+  for (int base = k0; base < k1 && !bad; base += 64) {
+    const int k = base + lane;
+    const bool valid = k < k1;
+    int32_t e = valid ? X.t_entry[k] : 0, tout = valid ? X.t_out[k] : 0, tex = valid ? X.t_exit[k] : 0;
+    // every entry must be the previous segment's true exit; re-walk (in order) where it is not
+    while (true) {
+      int32_t pv = __shfl_up(tex, 1, 64);
+      if (lane == 0) pv = prev_exit;
+      const unsigned long long m = __ballot(valid && (k == k0 ? e != (int32_t)b0 : e != pv));
+      if (!m) break;
+      const int L = __ffsll((long long)m) - 1;
+      const int32_t eL = __shfl(pv, L, 64);
+      int32_t to2, tx2;
+      snap_seg_from(X, base + L, base + L - k0, in, clen, eL, true, &to2, &tx2);
+      if (lane == L) { e = eL; tout = to2; tex = tx2; }
+    }
+    if (__ballot(valid && tex < 0)) { bad = true; break; }
+    // output offsets: exclusive scan of tout
+    int64_t x = tout;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { int64_t y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+    const int64_t ob = running + x - tout;
+    running += __shfl(x, 63, 64);
+    prev_exit = __shfl(tex, (k1 - base) >= 64 ? 63 : (k1 - base - 1), 64);
+    // fragment starts inside this segment: walk from its entry to each 64 KiB output boundary
+    if (valid && tout > 0) {
+      int64_t F = (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG;
+      int64_t p = e, o = ob;
+      while (F < ob + tout) {
+        while (o < F) {
+          int32_t adv, len;
+          if (!snap_parse(in, clen, p, &adv, &len)) { o = -1; break; }
+          o += len;
+          p += adv;
         }
-        ok = (q + hdr + l <= clen) && l < (1ll << 30);
-        adv = hdr + (uint32_t)(ok ? l : 0);
-      } else if (kind == 1) {
-        hdr = 2; l = ((tag >> 2) & 7) + 4; off = (int32_t)((((tag >> 5) & 7u) << 8) | ((d >> 8) & 0xff));
-        ok = q + 2 <= clen; adv = hdr;
-      } else if (kind == 2) {
-        hdr = 3; l = (tag >> 2) + 1; off = (int32_t)((d >> 8) & 0xffff);
-        ok = q + 3 <= clen; adv = hdr;
-      } else {
-        hdr = 5; l = (tag >> 2) + 1;
-        const uint64_t o32 = (d >> 8) & 0xffffffffull;
-        off = o32 > 0x7fffffffull ? 0x7fffffff : (int32_t)o32;
-        ok = q + 5 <= clen; adv = hdr;
-      }
-      olen = (uint32_t)l;
-    }
-    int64_t j = 0;
-    while (j < 64 && p + j < clen) {
-      const int jl = (int)j;
-      const uint32_t t_ok = __builtin_amdgcn_readlane(ok, jl);
-      const uint32_t t_adv = __builtin_amdgcn_readlane(adv, jl);
-      const int64_t t_len = (int64_t)__builtin_amdgcn_readlane(olen, jl);
-      const int32_t t_off = (int32_t)__builtin_amdgcn_readlane((uint32_t)off, jl);
-      if (!t_ok) { bad = true; break; }
-      if (t_off >= 0 && (t_off == 0 || t_off > o - (int64_t)k * SNAP_FRAG)) { bad = true; break; }   // reaches before its fragment
-      if (o + t_len > ulen) { bad = true; break; }
-      const int64_t fend = (int64_t)(k + 1) * SNAP_FRAG;
-      if (o + t_len > fend) { bad = true; break; }                           // straddles a boundary
-      o += t_len;
-      j += t_adv;
-      if (o == fend && o < ulen) {
-        if (++k >= nfrag) { bad = true; break; }
-        if (lane == 0) fs[k] = p + j;
+        if (o != F) { bad = true; break; }   // a tag straddles the boundary (or malformed)
+        const int f = (int)(F / SNAP_FRAG);
+        if (f < nf) X.fstart[f0 + f] = p; else bad = true;
+        F += SNAP_FRAG;
       }
     }
-    p += j;
+    bad = __ballot(bad) != 0;
   }
-  if (o != ulen || k + 1 != nfrag) bad = true;
-  if (lane == 0) serial[ci] = bad ? 1 : 0;
+  if (running != ulen || prev_exit != (int32_t)clen) bad = true;
+  if (lane == 0) X.serial[ci] = bad ? 1 : 0;
 }
 
-__global__ __launch_bounds__(64) void k_snappy_frag(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
-                                                    uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
-                                                    const int2* __restrict__ work, const int32_t* __restrict__ fbase,
-                                                    const int64_t* __restrict__ fstart, const int32_t* __restrict__ serial) {
-  __shared__ uint32_t win[SNAP_WIN / 4 + 1];
+// i mod d for 0 <= i < 64, 0 < d < 64 (d = copy offset): exact with a 16-bit reciprocal
+__device__ __forceinline__ int32_t small_mod(int32_t i, int32_t d, uint32_t rcp) {
+  return i - d * (int32_t)(((uint32_t)i * rcp) >> 16);
+}
+
+__global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restrict__ work) {
+  __shared__ u32x4 ring4[SNAP_RING / 16];
+  __shared__ uint32_t win[SNAP_FWIN / 4 + 2];
   const int2 wk = work[blockIdx.x];            // (compressed-page index, fragment)
-  if (serial[wk.x]) return;
+  if (X.serial[wk.x]) return;
   const int lane = threadIdx.x;
-  const DPage pg = pages[cpage[wk.x]];
-  const DChunk ck = chunks[pg.chunk];
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
-  snap_stream(ck, pg, arena, &in, &clen, &out, &ulen, &lv);
-  int64_t p = fstart[fbase[wk.x] + wk.y];
+  if (!snap_page(X, wk.x, &in, &clen, &out, &ulen, &lv)) return;
+  uint8_t* ring = (uint8_t*)ring4;
   const int64_t o0 = (int64_t)wk.y * SNAP_FRAG;
   const int64_t o1 = o0 + SNAP_FRAG < ulen ? o0 + SNAP_FRAG : ulen;
-  SnapWin w{in, clen, 0, win};
+  if (o1 <= o0) return;
+  int64_t p = X.fstart[X.fbase[wk.x] + wk.y];
+  SnapWin<SNAP_FWIN> w{in, clen, 0, win};
   w.refill(p);
-  int64_t o = o0, fenced = o0;
-  while (o < o1) {                              // the split pass validated every tag of the fragment
-    int64_t len, off;
+  int64_t o = o0, flushed = o0;
+  bool bad = false;
+  // ring -> HBM: [flushed, upto) in 16-byte granules (out + o0 is 16-byte aligned; the last
+  // fragment's final granule spills into the page's 16-byte padding)
+  GAS uint8_t* gout = gp(out);
+  const GAS uint8_t* gin = gp(in);
+  auto flush = [&](int64_t upto) {
+    for (int64_t u = flushed + 16 * lane; u < upto; u += 16 * 64)
+      *(GAS u32x4*)(gout + u) = ring4[(u & (SNAP_RING - 1)) >> 4];
+    flushed = upto;
+  };
+  while (o < o1) {
+    int32_t len, off;
     snap_tag(w, &p, &len, &off);
-    if (off < 0) {
-      if (!w.has(p, len) && len <= SNAP_WIN - 64) w.refill(p);
-      if (w.has(p, len)) {
-        const uint8_t* src = w.ptr(p);
-        for (int64_t i = lane; i < len; i += 64) out[o + i] = src[i];
-      } else {
-        for (int64_t i = lane; i < len; i += 64) out[o + i] = in[p + i];
+    if (off < 0) {                             // literal: 64 bytes per step, window or HBM
+      if (!w.has(p, len) && len <= SNAP_FWIN - 64) w.refill(p);
+      for (int32_t c = 0; c < len; c += 64) {
+        const int32_t q = c + lane;
+        if (q < len) {
+          const int64_t at = p + q;
+          ring[(o + q) & (SNAP_RING - 1)] = w.has(at, 1) ? (uint8_t)w.b(at) : gin[at];
+        }
+        const int64_t oc = o + (c + 64 < len ? c + 64 : len);
+        if (oc - flushed >= SNAP_FLUSH) flush(flushed + SNAP_FLUSH);
       }
       p += len;
+      if (!w.has(p, 5) && p < clen) w.refill(p);
+      o += len;
     } else {
-      const int64_t src = o - off;
-      if (src + (off < len ? off : len) > fenced) {   // reads bytes this wave stored
+      if (off == 0 || off > o - o0 || o + len > o1) { bad = true; break; }   // reaches before its fragment
+      if (off <= SNAP_RING - 64) {
+        if (lane < len) {
+          int32_t s;
+          if (off >= len) s = lane;
+          else s = small_mod(lane, off, (65536u + (uint32_t)off - 1) / (uint32_t)off);
+          ring[(o + lane) & (SNAP_RING - 1)] = ring[(o - off + s) & (SNAP_RING - 1)];
+        }
+      } else {                                 // far reference: from the flushed output in HBM
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        fenced = o;
+        if (lane < len) {
+          const int64_t at = o - off + lane;         // off > SNAP_RING - 64 > lane
+          const uintptr_t a = (uintptr_t)(out + at);
+          const uint32_t wv = __hip_atomic_load((const uint32_t*)(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+          ring[(o + lane) & (SNAP_RING - 1)] = (uint8_t)(wv >> (8 * (a & 3)));
+        }
       }
-      if (off >= len) {
-        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + i];
-      } else {
-        for (int64_t i = lane; i < len; i += 64) out[o + i] = out[src + (i % off)];
-      }
+      o += len;
+      if (o - flushed >= SNAP_FLUSH) flush(flushed + SNAP_FLUSH);
     }
-    o += len;
   }
+  if (bad) {
+    if (lane == 0) X.serial[wk.x] = 1;
+    return;
+  }
+  flush(o1);
 }
 
-// --------------------------------------------------------------------------------------------
-// K1b: SNAPPY raw-block decompression.
-//   k_snappy_split   one wave per compressed page walks the tags (no copies) through an LDS window
-//                    and records where each 64 KiB output fragment starts in the compressed stream.
-//                    Google's compressor encodes every 64 KiB input fragment on its own (fresh hash
-//                    table; no tag straddles, no copy reaches across, a fragment boundary), so the
-//                    fragments decode independently. A page that breaks this (legal in the format,
-//                    never produced by snappy) or is malformed is flagged for the serial path.
-//   k_snappy_frag    one wave per fragment decodes it into the arena.
-//   k_snappy_serial  flagged pages: one wave64 decodes the whole page (and reports errors).
-// Serial path:
-// Every lane parses the same tag (uniform control flow; same-address loads coalesce into one
-// transaction), then the wave copies the literal / back-reference 64 bytes per step. Back
+// Serial path (pages flagged by k_snap_fix / k_snap_frag): every lane parses the same tag (uniform
+// control flow), then the wave copies the literal / back-reference 64 bytes per step. Back
 // references read bytes other lanes stored earlier, so a workgroup-scope acq_rel fence orders
 // them whenever the source range reaches past the last fenced output position.
-// --------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_snappy_serial(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                       uint8_t* __restrict__ arena, const int32_t* __restrict__ cpage,
                                                       const int32_t* __restrict__ serial) {
@@ -2638,12 +2780,21 @@ namespace dk {
 void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
 }
-void launch_snappy(const DChunk* c, DPage* p, uint8_t* arena, int n_cp, const int32_t* cpage, const int32_t* fbase,
-                   int n_frag, const int2* work, int64_t* fstart, int32_t* serial, hipStream_t s) {
+// phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback
+void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int phase, hipStream_t s) {
   if (!n_cp) return;
-  hipLaunchKernelGGL(k_snappy_split, dim3(n_cp), dim3(64), 0, s, c, p, arena, cpage, fbase, fstart, serial);
-  if (n_frag) hipLaunchKernelGGL(k_snappy_frag, dim3(n_frag), dim3(64), 0, s, c, p, arena, cpage, work, fbase, fstart, serial);
-  hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, c, p, arena, cpage, serial);
+  const int g = (X.nseg + NT - 1) / NT;
+  if (phase == 0) {
+    hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
+    hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+  } else if (phase == 1) {
+    hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
+  } else if (phase == 2) {
+    if (n_frag) hipLaunchKernelGGL(k_snap_frag, dim3(n_frag), dim3(64), 0, s, X, work);
+  } else {
+    hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
+                       X.cpage, (const int32_t*)X.serial);
+  }
 }
 void launch_positions(const DChunk* c, DPage* p, int n_pages, const uint8_t* arena, int32_t* pos, DPosChunk* pcs,
                       int npc, hipStream_t s) {

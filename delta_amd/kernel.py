@@ -257,6 +257,39 @@ def build_log_segment(table_root: str) -> LogSegment:
 
 
 # ------------------------------------------------------------------------------------------------
+# tableRoot
+# ------------------------------------------------------------------------------------------------
+# ASCII characters java.net.URI's multi-argument constructors leave unquoted in a path component
+# (unreserved, punct, "/", "@"); '%' is always quoted.
+_PATH_CHARS = frozenset("abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_-!.~'()*,;:$&+=/@")
+
+
+def table_root_uri(path: str) -> str:
+    """The tableRoot string of a scan file for a local table.
+
+    Table.forPath resolves the path with DefaultFileSystemClient.resolvePath
+    (kernel-defaults/.../engine/DefaultFileSystemClient.java:82-86: the Hadoop Path qualified
+    against the local file system, i.e. "file:" + the absolute path with "//" collapsed and the
+    trailing "/" dropped, kernel-api/.../internal/fs/Path.java normalizePath); TableImpl keeps it as
+    a Path (TableImpl.java:81-85) and ActiveAddFilesIterator emits dataPath.toUri().toString()
+    (ActiveAddFilesIterator.java:251). Path builds its URI with the multi-argument java.net.URI
+    constructor, which percent-encodes (UTF-8, upper-case hex) every ASCII character that is not
+    legal in a path, '%' included, and every non-ASCII space or ISO control character."""
+    import unicodedata
+    p = os.path.abspath(path)
+    out = []
+    for ch in p:
+        o = ord(ch)
+        if o < 0x80:
+            out.append(ch if ch in _PATH_CHARS else "%%%02X" % o)
+        elif unicodedata.category(ch) in ("Zs", "Zl", "Zp") or o <= 0x9F:
+            out.append("".join("%%%02X" % b for b in ch.encode("utf-8", "surrogatepass")))
+        else:
+            out.append(ch)
+    return "file:" + "".join(out)
+
+
+# ------------------------------------------------------------------------------------------------
 # Table / Snapshot / Scan
 # ------------------------------------------------------------------------------------------------
 class Table:
@@ -296,6 +329,7 @@ class Snapshot:
         self.protocol = None
         self.metadata = None
         self.load_ms = {}   # snapshot-load phases (ms): log_segment, commits_pm, checkpoint_pm
+        self._manifest = None
 
     def getVersion(self):
         return self.log_segment.version
@@ -303,16 +337,42 @@ class Snapshot:
     def getScanBuilder(self):
         return ScanBuilder(self)
 
+    def _json_manifest(self):
+        """Actions of a V2 checkpoint's JSON manifest (ActionsIterator reads it with the JSON handler,
+        ActionsIterator.java:306-315, and extracts its sidecar rows, :256-283). Host-parsed: one
+        small file. Returns (sidecar paths in manifest order, protocol, metaData)."""
+        if self._manifest is None:
+            side, proto, meta = [], None, None
+            with open(self.log_segment.checkpoints[0].path, "rb") as f:
+                for ln, line in enumerate(f.read().decode("utf-8", "replace").splitlines()):
+                    if not line.strip():
+                        continue
+                    obj = json.loads(line)
+                    if obj.get("add") is not None or obj.get("remove") is not None:
+                        raise DkError("V2 checkpoint JSON manifest %s carries add/remove actions (line %d); "
+                                      "this engine build reconciles checkpoint rows from Parquet only"
+                                      % (self.log_segment.checkpoints[0].path, ln + 1))
+                    sc = obj.get("sidecar")
+                    if sc is not None:
+                        side.append(os.path.join(self.log_segment.log_path, "_sidecars", sc["path"]))
+                    if proto is None and obj.get("protocol") is not None:
+                        proto = obj["protocol"]
+                    if meta is None and obj.get("metaData") is not None:
+                        meta = obj["metaData"]
+            self._manifest = (side, proto, meta)
+        return self._manifest
+
     def _checkpoint_files(self, engine):
         """Checkpoint data files in replay order: multi-part parts descending (LogSegment
-        ordering); V2 parquet manifest first, then its sidecars in manifest order."""
+        ordering); V2 parquet manifest first, then its sidecars in manifest order; a V2 JSON
+        manifest contributes only its sidecars."""
         cks = self.log_segment.checkpoints
         if not cks:
             return []
         if cks[0].kind == "v2":
             man = cks[0].path
             if man.endswith(".json"):
-                raise DkError("V2 checkpoint with a JSON manifest is not supported by this engine build")
+                return list(self._json_manifest()[0])
             ps = ParquetSet(engine, [man], SIDECAR_LEAVES).decode()
             sp = ps.column(0, "sidecar.path")
             side = []
@@ -361,7 +421,16 @@ class Snapshot:
                 return
 
     def _pm_from_checkpoint(self, engine):
-        files = self._checkpoint_files(engine) if self.log_segment.checkpoints else []
+        cks = self.log_segment.checkpoints
+        if cks and cks[0].kind == "v2" and cks[0].path.endswith(".json"):
+            _, proto, meta = self._json_manifest()
+            if self.protocol is None:
+                self.protocol = proto
+            if self.metadata is None:
+                self.metadata = meta
+            files = self._checkpoint_files(engine) if (self.protocol is None or self.metadata is None) else []
+        else:
+            files = self._checkpoint_files(engine) if cks else []
         if files and (self.protocol is None or self.metadata is None):
             ps = ParquetSet(engine, files, PM_LEAVES).decode()
             for fi in range(len(files)):
@@ -422,6 +491,46 @@ class ScanBuilder:
         return GpuScan(self.snapshot, self.read_stats, self.shard, self.predicate)
 
 
+class LazyColumns(dict):
+    """leaf -> Column of one batch, copied from HBM on first access (the batch's vectors are
+    device-resident with a host mirror on demand); a leaf the file lacks reads as
+    None (all-null, NonExistentColumnReader)."""
+
+    def __init__(self, leaves, fetch):
+        super().__init__()
+        self._leaves = list(leaves)
+        self._fetch = fetch
+
+    def __missing__(self, leaf):
+        if leaf not in self._leaves:
+            raise KeyError(leaf)
+        c = self._fetch(leaf)
+        c = c if c.present else None
+        self[leaf] = c
+        return c
+
+    def get(self, leaf, default=None):
+        return self[leaf] if leaf in self._leaves else default
+
+    def __contains__(self, leaf):
+        return leaf in self._leaves
+
+    def keys(self):
+        return list(self._leaves)
+
+    def __iter__(self):
+        return iter(self._leaves)
+
+    def __len__(self):
+        return len(self._leaves)
+
+    def items(self):
+        return [(k, self[k]) for k in self._leaves]
+
+    def values(self):
+        return [self[k] for k in self._leaves]
+
+
 @dataclass
 class FilteredColumnarBatch:
     """data: leaf -> Column (add.* leaves) plus the constant tableRoot; selection: bool per row or
@@ -473,9 +582,8 @@ class GpuScan:
         self.replay = None
 
     def table_root(self):
-        # tableRoot = dataPath.toUri().toString() (ActiveAddFilesIterator.java:251)
-        p = self.snapshot.table.path
-        return "file:" + (p if p.endswith("/") else p + "/")
+        """tableRoot = dataPath.toUri().toString() (ActiveAddFilesIterator.java:251)."""
+        return table_root_uri(self.snapshot.table.path)
 
     def prepare(self, engine):
         """Host-side setup: parse the commit tail, open checkpoint files, upload to HBM."""
@@ -525,7 +633,7 @@ class GpuScan:
 
     def kernel_stats(self):
         out = {}
-        for i in range(20):
+        for i in range(24):
             name, avg, cnt = C.c_char_p(), C.c_double(), C.c_int64()
             if lib().dk_replay_kernel_stats(self._rh, i, C.byref(name), C.byref(avg), C.byref(cnt)) != 0:
                 continue
@@ -547,16 +655,14 @@ class GpuScan:
         if self.tail.rows:
             sel = np.zeros(self.tail.rows, dtype=np.uint8)
             check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
-            cols = {leaf: self.tail.column(leaf) for leaf in leaves}
-            cols = {k: (c if c.present else None) for k, c in cols.items()}
-            yield FilteredColumnarBatch(cols, root, int(self.tail.rows), sel.astype(bool), "json-tail")
+            cols = LazyColumns(leaves, self.tail.column)
+            yield FilteredColumnarBatch(cols, root, int(self.tail.rows), sel.view(bool), "json-tail")
         for fi, path in enumerate(self.ckpt_files or []):
             n = self.ckpt.num_rows(fi)
             sel = np.zeros(n, dtype=np.uint8)
             check(lib().dk_replay_ckpt_selection(self._rh, fi, sel.ctypes.data, n))
-            cols = {leaf: self.ckpt.column(fi, leaf) for leaf in leaves}
-            cols = {k: (c if c.present else None) for k, c in cols.items()}
-            yield FilteredColumnarBatch(cols, root, int(n), sel.astype(bool), path, self.ckpt_index[fi])
+            cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf))
+            yield FilteredColumnarBatch(cols, root, int(n), sel.view(bool), path, self.ckpt_index[fi])
 
     def close(self):
         if getattr(self, "_rh", None):

@@ -398,6 +398,38 @@ class Counters:
                 self.duplicateAddFiles, self.removeFilesSeenFromDeltaFiles)
 
 
+# java.net.URI (multi-argument constructors) path-component quoting: the ASCII characters left as
+# they are -- unreserved (alphanum "_-!.~'()*"), punct (",;:$&+="), "/" and "@" (URI.java L_PATH /
+# H_PATH); every other ASCII character, '%' included, is quoted.
+_URI_PATH_LEGAL = set(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_-!.~'()*,;:$&+=/@")
+
+
+def table_root_uri(table_root: str) -> str:
+    """dataPath.toUri().toString() for a local table (ActiveAddFilesIterator.java:251).
+
+    Table.forPath -> DefaultFileSystemClient.resolvePath (DefaultFileSystemClient.java:82-86):
+    fs.makeQualified(new Path(p)).toString() on the local file system is "file:" + the absolute,
+    normalized path (Path.normalizePath: no "//", no trailing "/"; relative paths against the
+    working directory), unquoted. TableImpl wraps it in a Path again (TableImpl.java:81-85), whose
+    URI comes from new URI(scheme, authority, path, null, fragment), and toUri().toString() prints
+    the quoted form: an ASCII byte outside _URI_PATH_LEGAL becomes %XX (upper-case); a non-ASCII
+    character is kept unless Character.isSpaceChar or isISOControl, in which case its UTF-8 bytes
+    are %XX-encoded (URI.quote)."""
+    import unicodedata
+    parts = [x for x in os.path.abspath(table_root).split("/") if x not in ("", ".")]
+    norm = "/" + "/".join(parts)
+    out = []
+    for ch in norm:
+        o = ord(ch)
+        if o < 0x80:
+            out.append(ch if o in _URI_PATH_LEGAL else "%" + format(o, "02X"))
+        elif 0x80 <= o <= 0x9F or unicodedata.category(ch) in ("Zs", "Zl", "Zp"):
+            out.append("".join("%" + format(b, "02X") for b in ch.encode("utf-8", "surrogatepass")))
+        else:
+            out.append(ch)
+    return "file:" + "".join(out)
+
+
 @dataclass
 class CheckpointBatch:
     """One decoded checkpoint / sidecar file (all rows) with its selection."""
@@ -419,11 +451,13 @@ class ReplayResult:
     ckpt_counters: Counters = field(default_factory=Counters)   # checkpoint part (this shard's)
 
     def scan_files(self):
-        """Ordered scan-file rows as canonical python tuples (App. B ordering)."""
-        out = [canon_add_from_json(r) for r in self.json_rows]
+        """Ordered scan-file rows (App. B ordering): the add struct as canonical python tuples plus
+        the tableRoot column (InternalScanFileUtils.SCAN_FILE_SCHEMA, ordinal 1)."""
+        root = (self.table_root,)
+        out = [canon_add_from_json(r) + root for r in self.json_rows]
         for b in self.checkpoint:
             idx = np.nonzero(b.selected)[0]
-            out.extend(canon_add_from_cols(b.cols, int(i)) for i in idx)
+            out.extend(canon_add_from_cols(b.cols, int(i)) + root for i in idx)
         return out
 
 
@@ -556,7 +590,7 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
         with_stats = True
     world, rank = shard if shard else (1, 0)
     seg = load_log_segment(table_root)
-    res = ReplayResult(version=seg.version, table_root=table_root)
+    res = ReplayResult(version=seg.version, table_root=table_root_uri(table_root))
     c = res.tail_counters
     cc = res.ckpt_counters
     ckpt_idx = 0
@@ -681,7 +715,7 @@ def load_protocol_metadata(table_root: str):
     seg = load_log_segment(table_root)
     prot = meta = None
     for f in seg.all_files_reversed():
-        if f.kind == "commit":
+        if f.kind == "commit" or f.path.endswith(".json"):      # commits and V2 JSON manifests
             with open(f.path, "rb") as fh:
                 lines = fh.read().decode("utf-8", "replace").splitlines()
             for line in lines:
@@ -693,8 +727,6 @@ def load_protocol_metadata(table_root: str):
                     m = obj["metaData"]
                     meta = (m.get("id"), m.get("schemaString"), m.get("partitionColumns"))
         else:
-            if f.path.endswith(".json"):
-                continue
             pf = ParquetFile.open(f.path)
             rv, wv = pf.read("protocol.minReaderVersion"), pf.read("protocol.minWriterVersion")
             if prot is None and rv is not None:

@@ -12,6 +12,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
 from oracle import ref  # noqa: E402
 
 GOLD = "/root/reference/connectors/golden-tables/src/main/resources/golden"
@@ -21,6 +22,7 @@ TABLES = {
     "log-replay-special-characters-a": GOLD, "log-replay-special-characters-b": GOLD,
     "delete-re-add-same-file-different-transactions": GOLD, "multi-part-checkpoint": GOLD,
     "basic-with-inserts-deletes-checkpoint": GOLD, "only-checkpoint-files": GOLD, "v2-checkpoint-parquet": GOLD,
+    "v2-checkpoint-json": GOLD,
     "dv-partitioned-with-checkpoint": GOLD, "data-skipping-basic-stats-all-types-checkpoint": GOLD,
     "data-skipping-basic-stats-all-types": GOLD, "data-skipping-basic-stats-all-types-columnmapping-name": GOLD,
     "data-skipping-basic-stats-all-types-columnmapping-id": GOLD,
@@ -30,13 +32,9 @@ TABLES = {
 
 
 def canon_json(rows):
-    def enc(x):
-        if isinstance(x, bytes):
-            return {"b": x.decode("utf-8", "surrogateescape")}
-        if isinstance(x, tuple):
-            return [enc(v) for v in x]
-        return x
-    return [enc(r) for r in rows]
+    """Rows as JSON; the machine-dependent tableRoot prefix becomes ${TABLES} (tests/golden_util.py)."""
+    from tests.golden_util import to_json_rows
+    return to_json_rows(rows)
 
 
 def main():

@@ -13,7 +13,7 @@ def product_scan(table_root, json_batch_size=1024, with_stats=False, engine=None
     rows = []
     for b in scan.getScanFiles(eng):
         for r in b.selected_rows():
-            rows.append(ref.canon_add_from_cols(b.data, int(r)))
+            rows.append(ref.canon_add_from_cols(b.data, int(r)) + (b.table_root,))
     out = (snap.getVersion(), rows, scan.metrics.as_tuple())
     scan.close()
     return out

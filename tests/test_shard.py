@@ -26,8 +26,9 @@ def _oracle_shard_output(table, world, rank, jbs=1024):
     r = ref.replay(table, json_batch_size=jbs, shard=(world, rank))
     files = {}
     for b in r.checkpoint:
-        files[b.file_index] = [ref.canon_add_from_cols(b.cols, int(i)) for i in np.nonzero(b.selected)[0]]
-    tail = [ref.canon_add_from_json(a) for a in r.json_rows]
+        files[b.file_index] = [ref.canon_add_from_cols(b.cols, int(i)) + (r.table_root,)
+                               for i in np.nonzero(b.selected)[0]]
+    tail = [ref.canon_add_from_json(a) + (r.table_root,) for a in r.json_rows]
     return shard.ShardOutput(rank, r.tail_counters.as_tuple(), r.ckpt_counters.as_tuple(), tail, files)
 
 
@@ -131,7 +132,7 @@ def test_gpu_shards_merge_to_oracle(tmp_path, world, v2):
         outs.append(o)
         scans.append(sc)
     counters, batches = shard.merge(outs)
-    rows = [ref.canon_add_from_cols(b.data, int(i)) for b in batches for i in b.selected_rows()]
+    rows = [ref.canon_add_from_cols(b.data, int(i)) + (b.table_root,) for b in batches for i in b.selected_rows()]
     full = ref.replay(str(tmp_path))
     assert counters == full.counters.as_tuple()
     assert rows == full.scan_files()

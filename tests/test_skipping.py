@@ -258,7 +258,8 @@ def _gpu_files(root, predicate, eng):
     snap = K.Table.forPath(eng, root).getLatestSnapshot(eng)
     scan = snap.getScanBuilder().withFilter(predicate).build()
     try:
-        rows = [ref.canon_add_from_cols(b.data, int(i)) for b in scan.getScanFiles(eng) for i in b.selected_rows()]
+        rows = [ref.canon_add_from_cols(b.data, int(i)) + (b.table_root,) for b in scan.getScanFiles(eng)
+                for i in b.selected_rows()]
         return rows, scan.metrics.as_tuple()
     finally:
         scan.close()
