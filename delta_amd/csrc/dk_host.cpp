@@ -20,6 +20,7 @@
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const SnapCtx&, int, int, const int2*, int, hipStream_t);
+void snap_stats(unsigned long long*);
 void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
@@ -54,7 +55,9 @@ static int fail(const std::string& m) { g_err = m; return 1; }
   } while (0)
 
 extern "C" const char* dk_last_error(void) { return g_err.c_str(); }
-extern "C" const char* dk_version(void) { return "libdkgpu 0.1 (gfx950)"; }
+extern "C" const char* dk_version(void) { return "libdkgpu 0.2 (gfx950)"; }
+// debug: k_snap_frag counters (non-zero only in DK_SNAP_STATS builds; tools/snap_stats.py)
+extern "C" int dk_debug_snap_stats(int64_t out[16]) { snap_stats((unsigned long long*)out); return 0; }
 
 // ------------------------------------------------------------------------------------------------
 // engine
@@ -139,7 +142,7 @@ struct FileM {
 
 static std::string read_string(TReader& t) {
   uint64_t n = t.varint();
-  if (t.bad || t.p + n > t.e) { t.bad = 1; return {}; }
+  if (t.bad || n > (uint64_t)(t.e - t.p)) { t.bad = 1; return {}; }
   std::string s((const char*)t.p, n);
   t.p += n;
   return s;
@@ -428,6 +431,7 @@ struct dk_parquet {
   // snappy: compressed pages, their 64 KiB fragment bases / work items / starts, serial flags
   DBuf d_cpage, d_fbase, d_fwork, d_fstart, d_serial;
   DBuf d_sbase, d_spage, d_snapws;   // speculative-walk segments: page bases, owner page, workspace
+  DBuf d_pwork;                      // page-mode work items (page, -1)
   int n_cpages = 0, n_frags = 0, n_segs = 0;
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
   int n_ltiles = 0;
@@ -475,6 +479,15 @@ static void per_column_tiles(const dk_parquet* p, F&& f) {
   for (const DColumn& c : p->h_cols) f(c.first_tile, c.n_tiles);
 }
 
+// Snappy page mode: DK_SNAPPY_MODE=page|frag forces it; by default page mode once the compressed
+// pages outnumber 8 waves per SIMD of the chip (k_snap_frag waves are LDS-limited to about that).
+static bool snap_page_mode(const dk_parquet* p) {
+  static const char* env = getenv("DK_SNAPPY_MODE");
+  if (env && !strcmp(env, "page")) return true;
+  if (env && !strcmp(env, "frag")) return false;
+  return p->n_cpages >= 8192;
+}
+
 // the decode pipeline (mode: -1 = headers only; 0 = prepare pass through the scans, which size the
 // outputs; 1 = full step)
 static int run_pipeline(dk_parquet* p, int mode) {
@@ -502,10 +515,15 @@ static int run_pipeline(dk_parquet* p, int mode) {
     X.w_exit = ws; X.w_out = ws + ns; X.w_npos = ws + 2 * ns; X.t_entry = ws + 3 * ns; X.t_out = ws + 4 * ns;
     X.t_exit = ws + 5 * ns; X.w_pos = ws + 6 * ns; X.w_cum = ws + (6 + DK_SNAP_REC) * ns;
     X.fbase = p->d_fbase.as<int32_t>(); X.fstart = p->d_fstart.as<int64_t>(); X.serial = p->d_serial.as<int32_t>();
-    { KTimer::Scope s0(&T, 13, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 0, s); }
-    { KTimer::Scope s1(&T, 19, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 1, s); }
-    { KTimer::Scope s2(&T, 20, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 2, s); }
-    { KTimer::Scope s3(&T, 21, s); launch_snappy(X, p->n_cpages, p->n_frags, p->d_fwork.as<int2>(), 3, s); }
+    // page mode (one wave decodes a whole page in order, no walk) once there are enough pages to
+    // fill the chip; otherwise the speculative walk splits pages into 64 KiB fragments
+    const bool page_mode = snap_page_mode(p);
+    const int nfr = page_mode ? -1 : p->n_frags;
+    const int2* wk = page_mode ? p->d_pwork.as<int2>() : p->d_fwork.as<int2>();
+    { KTimer::Scope s0(&T, 13, s); launch_snappy(X, p->n_cpages, nfr, wk, 0, s); }
+    { KTimer::Scope s1(&T, 19, s); launch_snappy(X, p->n_cpages, nfr, wk, 1, s); }
+    { KTimer::Scope s2(&T, 20, s); launch_snappy(X, p->n_cpages, nfr, wk, 2, s); }
+    { KTimer::Scope s3(&T, 21, s); launch_snappy(X, p->n_cpages, nfr, wk, 3, s); }
   }
   { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P, n, arena, runs, s); }
   { KTimer::Scope sc(&T, 2, s); per_column_tiles(p, [&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
@@ -665,6 +683,9 @@ static int prepare(dk_parquet* p) {
         upload(p->d_spage, spage.data(), spage.size() * 4, s) ||
         p->d_snapws.alloc(spage.size() * 4 * (6 + 2 * DK_SNAP_REC)))
       return 1;
+    std::vector<int2> pwork(cpage.size());
+    for (size_t i = 0; i < cpage.size(); i++) pwork[i] = make_int2((int)i, -1);
+    if (upload(p->d_pwork, pwork.data(), pwork.size() * sizeof(int2), s)) return 1;
     p->n_segs = (int)spage.size();
   }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;

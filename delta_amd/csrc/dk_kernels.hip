@@ -470,78 +470,329 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
 __device__ __forceinline__ int32_t small_mod(int32_t i, int32_t d, uint32_t rcp) {
   return i - d * (int32_t)(((uint32_t)i * rcp) >> 16);
 }
+__device__ __forceinline__ uint32_t small_rcp(int32_t d) { return d > 0 ? (65536u + (uint32_t)d - 1) / (uint32_t)d : 0; }
+
+__device__ unsigned long long dk_snap_stats[16];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
+
+// k_snap_frag: one wave per 64 KiB output fragment, in batches of up to 64 tags (one per lane).
+//  1. tag starts: every lane parses the candidate tag at cursor + lane (LDS window); the true chain
+//     hops through the candidates with readlane (a few scalar ops per tag), up to 4 windows per batch;
+//  2. each lane parses its tag; a wave scan gives output offsets;
+//  3. copies whose source lies inside this batch's output are resolved by pointer jumping over the
+//     batch's tags (a source inside a literal becomes a read of the compressed window, inside an
+//     earlier copy it follows that copy's source), so almost every byte reads a location no tag of
+//     the batch writes;
+//  4. those bytes are produced byte-parallel (each lane a contiguous run of output bytes, its tag
+//     from a prefix-max over a tag-start map); the rest (sources straddling tags, far references
+//     served from HBM) run one tag at a time in order.
+#ifdef DK_SNAP_STATS
+#define SSTAT(i, v) (st_[i] += (unsigned long long)(v))
+#else
+#define SSTAT(i, v) ((void)0)
+#endif
+constexpr int SF_FW = 2048;                // compressed window
+constexpr int SF_BOUT = 512;               // a batch stops collecting tags at this many output bytes
+constexpr int SF_BMAX = SF_BOUT + 64;      // max batch output (every batched tag has <= 64 bytes)
+constexpr int SF_RM = SNAP_RING - 1;
+enum : int32_t { SM_WIN = 0, SM_RING = 1, SM_FAR = 2, SM_DEP = 3, SM_FARQ = 4 };
 
 __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restrict__ work) {
-  __shared__ u32x4 ring4[SNAP_RING / 16];
-  __shared__ uint32_t win[SNAP_FWIN / 4 + 2];
+  // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map
+  __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX + 16) / 16];
+  __shared__ u32x4 prm[64];                // per-tag (ot, src, mode | per << 8, rcp)
+  uint8_t* L = (uint8_t*)lds4;
+  uint32_t* W32 = (uint32_t*)(L + SNAP_RING);
+  uint8_t* M = L + SNAP_RING + SF_FW + 16;
   const int2 wk = work[blockIdx.x];            // (compressed-page index, fragment)
   if (X.serial[wk.x]) return;
   const int lane = threadIdx.x;
-  const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
-  if (!snap_page(X, wk.x, &in, &clen, &out, &ulen, &lv)) return;
-  uint8_t* ring = (uint8_t*)ring4;
-  const int64_t o0 = (int64_t)wk.y * SNAP_FRAG;
-  const int64_t o1 = o0 + SNAP_FRAG < ulen ? o0 + SNAP_FRAG : ulen;
-  if (o1 <= o0) return;
-  int64_t p = X.fstart[X.fbase[wk.x] + wk.y];
-  SnapWin<SNAP_FWIN> w{in, clen, 0, win};
-  w.refill(p);
-  int64_t o = o0, flushed = o0;
-  bool bad = false;
-  // ring -> HBM: [flushed, upto) in 16-byte granules (out + o0 is 16-byte aligned; the last
-  // fragment's final granule spills into the page's 16-byte padding)
+  const uint8_t* in; uint8_t* out; int64_t clen64, ulen64, lv;
+  if (!snap_page(X, wk.x, &in, &clen64, &out, &ulen64, &lv)) return;
+  const int32_t clen = (int32_t)clen64, ulen = (int32_t)ulen64;
+  // wk.y >= 0: one 64 KiB fragment (starts found by k_snap_fix); wk.y < 0: the whole page, in order
+  // (page mode: no walk; any valid snappy stream, references may cross fragment boundaries)
+  int32_t o0, o1, p, ce;
+  if (wk.y >= 0) {
+    o0 = wk.y * SNAP_FRAG;
+    o1 = o0 + SNAP_FRAG < ulen ? o0 + SNAP_FRAG : ulen;
+    if (o1 <= o0) return;
+    const int f0 = X.fbase[wk.x], nf = X.fbase[wk.x + 1] - f0;
+    p = (int32_t)X.fstart[f0 + wk.y];
+    ce = wk.y + 1 < nf ? (int32_t)X.fstart[f0 + wk.y + 1] : clen;
+  } else {
+    for (int64_t i = lane; i < lv; i += 64) gp(out)[i - lv] = gp(in)[i - lv];   // v2 levels: stored uncompressed
+    uint64_t un;
+    p = (int32_t)snap_preamble(in, clen, &un);
+    if (p < 0 || (int64_t)un != ulen) { if (lane == 0) X.serial[wk.x] = 1; return; }
+    o0 = 0; o1 = ulen; ce = clen;
+    if (o1 == 0) { if (lane == 0 && p != clen) X.serial[wk.x] = 1; return; }
+  }
   GAS uint8_t* gout = gp(out);
   const GAS uint8_t* gin = gp(in);
-  auto flush = [&](int64_t upto) {
-    for (int64_t u = flushed + 16 * lane; u < upto; u += 16 * 64)
-      *(GAS u32x4*)(gout + u) = ring4[(u & (SNAP_RING - 1)) >> 4];
+  int32_t ws = 0;
+  // window = stream bytes [ws, ws + SF_FW), ws 4-byte aligned relative to the buffer
+  auto refill = [&](int32_t at) {
+    const uintptr_t a4 = ((uintptr_t)(in + at)) & ~(uintptr_t)3;
+    ws = at - (int32_t)((uintptr_t)(in + at) - a4);
+    const uintptr_t lim = ((uintptr_t)(in + clen) - 1) & ~(uintptr_t)3;
+    uint32_t v[SF_FW / 256];
+#pragma unroll
+    for (int k = 0; k < SF_FW / 256; k++) {
+      const uintptr_t ad = a4 + (uintptr_t)(lane + 64 * k) * 4;
+      v[k] = *(const GAS uint32_t*)(ad < lim ? ad : lim);
+    }
+#pragma unroll
+    for (int k = 0; k < SF_FW / 256; k++) W32[lane + 64 * k] = v[k];
+  };
+  int32_t o = o0, flushed = o0;
+  auto flush_to = [&](int32_t upto) {          // ring -> HBM, 16-byte granules
+    for (int32_t u = flushed + 16 * lane; u < upto; u += 16 * 64)
+      *(GAS u32x4*)(gout + u) = lds4[(u & SF_RM) >> 4];
     flushed = upto;
   };
-  while (o < o1) {
-    int32_t len, off;
-    snap_tag(w, &p, &len, &off);
-    if (off < 0) {                             // literal: 64 bytes per step, window or HBM
-      if (!w.has(p, len) && len <= SNAP_FWIN - 64) w.refill(p);
-      for (int32_t c = 0; c < len; c += 64) {
-        const int32_t q = c + lane;
-        if (q < len) {
-          const int64_t at = p + q;
-          ring[(o + q) & (SNAP_RING - 1)] = w.has(at, 1) ? (uint8_t)w.b(at) : gin[at];
-        }
-        const int64_t oc = o + (c + 64 < len ? c + 64 : len);
-        if (oc - flushed >= SNAP_FLUSH) flush(flushed + SNAP_FLUSH);
-      }
-      p += len;
-      if (!w.has(p, 5) && p < clen) w.refill(p);
-      o += len;
-    } else {
-      if (off == 0 || off > o - o0 || o + len > o1) { bad = true; break; }   // reaches before its fragment
-      if (off <= SNAP_RING - 64) {
-        if (lane < len) {
-          int32_t s;
-          if (off >= len) s = lane;
-          else s = small_mod(lane, off, (65536u + (uint32_t)off - 1) / (uint32_t)off);
-          ring[(o + lane) & (SNAP_RING - 1)] = ring[(o - off + s) & (SNAP_RING - 1)];
-        }
-      } else {                                 // far reference: from the flushed output in HBM
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane < len) {
-          const int64_t at = o - off + lane;         // off > SNAP_RING - 64 > lane
-          const uintptr_t a = (uintptr_t)(out + at);
-          const uint32_t wv = __hip_atomic_load((const uint32_t*)(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-          ring[(o + lane) & (SNAP_RING - 1)] = (uint8_t)(wv >> (8 * (a & 3)));
+#ifdef DK_SNAP_STATS
+  unsigned long long st_[16] = {0};
+#endif
+  SSTAT(9, 1);
+  refill(p);
+  bool bad = false;
+  while (o < o1 && !bad) {
+    if (p + 640 > ws + SF_FW && ws + SF_FW < clen) { refill(p); SSTAT(6, 1); }
+    // ---- 1. tag starts ----
+    int32_t n = 0, t = p, outsum = 0, vstart = 0, biglen = 0;
+    for (int r = 0; r < 4 && t < ce && n <= 32 && outsum < SF_BOUT && !biglen; r++) {
+      // candidate tag at t + lane: advance (bytes to the next tag) and output length
+      int32_t adv = 1, olen = 0;
+      {
+        const int32_t ix = t + lane - ws;
+        const uint64_t d = ((((uint64_t)W32[(ix >> 2) + 1]) << 32) | W32[ix >> 2]) >> (8 * (ix & 3));
+        const uint32_t tag = (uint32_t)d & 0xff, kind = tag & 3;
+        if (kind == 0) {
+          uint32_t l = (tag >> 2) + 1, hdr = 1;
+          if (l > 60) {
+            const uint32_t nb = l - 60;
+            hdr += nb;
+            l = (uint32_t)((d >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
+          }
+          olen = l > 0x40000000u ? 0x40000000 : (int32_t)l;
+          adv = (int32_t)hdr + olen;
+        } else {
+          adv = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+          olen = kind == 1 ? (int32_t)(((tag >> 2) & 7) + 4) : (int32_t)((tag >> 2) + 1);
         }
       }
-      o += len;
-      if (o - flushed >= SNAP_FLUSH) flush(flushed + SNAP_FLUSH);
+      int32_t j = 0;
+      SSTAT(12, 1);
+      while (j < 64 && t + j < ce && n < 64 && outsum < SF_BOUT) {
+        const int32_t l = __builtin_amdgcn_readlane(olen, j);
+        if (l > 64) { if (n == 0) { biglen = l; vstart = t + j; } break; }   // long literal: its own step
+        if (lane == n) vstart = t + j;
+        n++;
+        outsum += l;
+        j += __builtin_amdgcn_readlane(adv, j);
+      }
+      if (!biglen) t += j;
     }
+    if (biglen) {
+      // ---- long literal (> 64 bytes) at p: 64 bytes per step through the window ----
+      const int32_t ix = p - ws;
+      const uint32_t tag = ((const uint8_t*)W32)[ix];
+      const int32_t src = p + 1 + (int32_t)((tag >> 2) + 1 > 60 ? (tag >> 2) + 1 - 60 : 0);
+      if (o + biglen > o1) { bad = true; break; }
+      for (int32_t c = 0; c < biglen; c += 64) {
+        if (src + c + 64 > ws + SF_FW && ws + SF_FW < clen) refill(src + c);
+        if (c + lane < biglen) L[(o + c + lane) & SF_RM] = ((const uint8_t*)W32)[src + c + lane - ws];
+        const int32_t oc = o + (c + 64 < biglen ? c + 64 : biglen);
+        if (oc - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
+      }
+      p = src + biglen;
+      o += biglen;
+      SSTAT(5, 1);
+      continue;
+    }
+#ifdef SF_ONLY_DISCOVERY
+    o += outsum; p = t;
+    while (o - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
+    continue;
+#endif
+    // ---- 2. parse each tag (lane j = tag j) ----
+    const bool valid = lane < n;
+    int32_t len = 0, off = 0, src = 0, per = 0, mode = SM_WIN;
+    bool is_copy = false;
+    if (valid) {
+      const int32_t ix = vstart - ws;
+      const uint64_t d = ((((uint64_t)W32[(ix >> 2) + 1]) << 32) | W32[ix >> 2]) >> (8 * (ix & 3));
+      const uint32_t tag = (uint32_t)d & 0xff, kind = tag & 3;
+      if (kind == 0) {
+        const uint32_t l = (tag >> 2) + 1;
+        const int32_t hdr = l > 60 ? 1 + (int32_t)(l - 60) : 1;
+        len = l > 60 ? (int32_t)((d >> 8) & ((1ull << (8 * (l - 60))) - 1)) + 1 : (int32_t)l;
+        src = vstart + hdr;
+      } else if (kind == 1) {
+        len = ((tag >> 2) & 7) + 4;
+        off = (int32_t)(((tag >> 5) << 8) | ((uint32_t)(d >> 8) & 0xff));
+        is_copy = true;
+      } else if (kind == 2) {
+        len = (tag >> 2) + 1;
+        off = (int32_t)((d >> 8) & 0xffff);
+        is_copy = true;
+      } else {
+        len = (tag >> 2) + 1;
+        const uint64_t o32 = (d >> 8) & 0xffffffffull;
+        off = o32 > 0x7fffffffull ? 0x7fffffff : (int32_t)o32;
+        is_copy = true;
+      }
+    }
+    // ---- 3. output offsets ----
+    int32_t x = len;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) { const int32_t y = __shfl_up(x, k, 64); if (lane >= k) x += y; }
+    const int32_t total = __shfl(x, 63, 64);
+    const int32_t ot = o + x - len;
+    if (o + total > o1) { bad = true; break; }
+    // ---- 4. modes: WIN (compressed window), RING (resolved ring read), FAR (HBM), DEP (in-batch) ----
+    const int32_t ring_lo = o + total - SNAP_RING;    // lowest position no write of this batch overwrites
+    bool stuck = false;
+    if (valid && is_copy) {
+      src = ot - off;
+      per = off < len ? off : 0;
+      if (off == 0 || off > ot - o0) bad = true;     // offset 0, or reaches before its fragment
+      const int32_t ext = per ? per : len;
+      mode = src + ext <= o ? (src >= ring_lo ? SM_RING : SM_FAR) : SM_DEP;
+    }
+    if (__ballot(bad)) { bad = true; break; }
+    SSTAT(0, 1); SSTAT(1, n); SSTAT(11, __popcll(__ballot(valid && !is_copy)));
+#ifdef SF_NO_RESOLVE
+    for (int round = 0; round < 0; round++) {
+#else
+    for (int round = 0; round < 6; round++) {
+#endif
+      const bool act = valid && mode == SM_DEP && !stuck;
+      if (!__ballot(act)) break;
+      SSTAT(7, 1);
+      int32_t u = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1) {
+        const int32_t c = u + step;
+        const int32_t otc = __shfl(ot, c < n ? c : 0, 64);
+        if (c < n && otc <= src) u = c;
+      }
+      const int32_t ot_u = __shfl(ot, u, 64), len_u = __shfl(len, u, 64), mode_u = __shfl(mode, u, 64);
+      const int32_t src_u = __shfl(src, u, 64), per_u = __shfl(per, u, 64);
+      if (act) {
+        const int32_t ext = per ? per : len;
+        if (u >= lane || per_u != 0 || src < ot_u || src + ext > ot_u + len_u) {
+          stuck = true;                               // straddles tags: serial
+        } else {
+          src = src_u + (src - ot_u);
+          if (mode_u == SM_WIN) mode = SM_WIN;
+          else if (src + ext <= o) mode = src >= ring_lo ? SM_RING : SM_FAR;
+          // else u reads inside this batch too: follow its source next round
+        }
+      }
+    }
+    // far sources of <= 8 bytes (most: short matches far back): the owning lane loads them with
+    // three dwords from the output this wave flushed to HBM, now, and stores them after step 5
+    const int32_t ext_f = per ? per : len;
+    if (valid && mode == SM_FAR && ext_f <= 8 && len <= 8) mode = SM_FARQ;
+    const bool farq = valid && mode == SM_FARQ;
+    uint32_t fw0 = 0, fw1 = 0, fw2 = 0;
+#ifdef SF_NO_FAR
+    if (false) {
+#else
+    if (__ballot(farq)) {
+#endif
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (farq) {
+        const GAS uint32_t* a = (const GAS uint32_t*)(((uintptr_t)(out + src)) & ~(uintptr_t)3);
+        fw0 = a[0]; fw1 = a[1]; fw2 = a[2];
+      }
+    }
+    // ---- 5. byte-parallel production of every WIN / RING / FAR tag ----
+#ifdef SF_NO_BYTES
+    const int32_t CH = 0;
+#else
+    const int32_t CH = (total + 63) >> 6;             // output bytes per lane (<= 9)
+#endif
+    SSTAT(8, CH); SSTAT(2, __popcll(__ballot(valid && mode == SM_DEP))); SSTAT(3, __popcll(__ballot(valid && mode >= SM_FAR && mode != SM_DEP)));
+    SSTAT(4, __popcll(__ballot(valid && is_copy && mode == SM_WIN))); SSTAT(10, __popcll(__ballot(valid && mode == SM_RING)));
+    for (int32_t b = lane * 16; b < total; b += 64 * 16) *(uint4*)(M + b) = make_uint4(0, 0, 0, 0);
+    if (valid) {
+      prm[lane] = u32x4{(uint32_t)ot, (uint32_t)(mode == SM_WIN ? SNAP_RING + src - ws : src),
+                        (uint32_t)(mode | (per << 8)), small_rcp(per)};
+      if (len > 0) M[ot - o] = (uint8_t)(lane + 1);
+    }
+    {
+      const int32_t b0 = lane * CH;
+      int32_t mx = 0;
+      for (int32_t k = 0; k < CH; k++) if (b0 + k < total) mx = max(mx, (int32_t)M[b0 + k]);
+      int32_t ex = mx;                                 // inclusive prefix max over lanes
+#pragma unroll
+      for (int k = 1; k < 64; k <<= 1) { const int32_t y = __shfl_up(ex, k, 64); if (lane >= k) ex = max(ex, y); }
+      int32_t cur = __shfl_up(ex, 1, 64);
+      if (lane == 0) cur = 0;
+      u32x4 q = prm[cur > 0 ? cur - 1 : 0];
+      int32_t ga[9];                                   // FAR bytes: output offset of the source, -1 none
+      bool any_far = false;
+#pragma unroll
+      for (int32_t k = 0; k < 9; k++) {
+        ga[k] = -1;
+        const int32_t b = b0 + k;
+        if (k < CH && b < total) {
+          const int32_t mk = M[b];
+          if (mk) q = prm[mk - 1];
+          const int32_t md = (int32_t)(q.z & 0xff);
+          if (md <= SM_FAR) {
+            int32_t i = o + b - (int32_t)q.x;
+            const int32_t pr = (int32_t)(q.z >> 8);
+            if (pr) i = small_mod(i, pr, q.w);
+            if (md == SM_FAR) { ga[k] = (int32_t)q.y + i; any_far = true; }
+            else L[(o + b) & SF_RM] = L[md == SM_WIN ? (int32_t)q.y + i : (((int32_t)q.y + i) & SF_RM)];
+          }
+        }
+      }
+      if (__ballot(any_far)) {
+        // far sources: bytes this wave flushed to HBM earlier (its stores complete first)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        uint32_t gv[9];
+#pragma unroll
+        for (int32_t k = 0; k < 9; k++) gv[k] = ga[k] >= 0 ? gout[ga[k]] : 0;
+#pragma unroll
+        for (int32_t k = 0; k < 9; k++) if (ga[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)gv[k];
+      }
+    }
+    if (farq) {
+      const uint32_t sh = (uint32_t)(((uintptr_t)(out + src)) & 3);
+      for (int32_t i = 0; i < len; i++) {
+        const uint32_t k = sh + (uint32_t)(per ? i % per : i);
+        const uint32_t w = k < 4 ? fw0 : (k < 8 ? fw1 : fw2);
+        L[(ot + i) & SF_RM] = (uint8_t)(w >> (8 * (k & 3)));
+      }
+    }
+    // ---- 6. sources straddling tags of this batch: one tag at a time, in order ----
+    unsigned long long m = __ballot(valid && mode == SM_DEP);
+    while (m) {
+      const int j = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int32_t ot_j = __shfl(ot, j, 64), len_j = __shfl(len, j, 64), src_j = __shfl(src, j, 64);
+      const int32_t per_j = __shfl(per, j, 64);
+      if (lane < len_j) {
+        const int32_t i = per_j ? small_mod(lane, per_j, small_rcp(per_j)) : lane;
+        L[(ot_j + lane) & SF_RM] = L[(src_j + i) & SF_RM];
+      }
+    }
+    o += total;
+    p = t;
+    while (o - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
   }
-  if (bad) {
+#ifdef DK_SNAP_STATS
+  if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&dk_snap_stats[i], st_[i]);
+#endif
+  if (bad || o != o1 || p != ce) {
     if (lane == 0) X.serial[wk.x] = 1;
     return;
   }
-  flush(o1);
+  flush_to(o1);
 }
 
 // Serial path (pages flagged by k_snap_fix / k_snap_frag): every lane parses the same tag (uniform
@@ -1951,11 +2202,15 @@ __device__ bool js_timestamp(const uint8_t* s, int32_t a, int32_t b, long long* 
       const int maxd = ntz ? 6 : 9;
       int nd = 0;
       while (k < b && s[k] >= '0' && s[k] <= '9' && nd < maxd) { nanos = nanos * 10 + (s[k] - '0'); k++; nd++; }
-      if (nd == 0 || (k < b && s[k] >= '0' && s[k] <= '9')) return false;
+      // ntz: appendFraction(MICRO_OF_SECOND, 0, 6, true) has minimum width 0, so a bare '.' is a
+      // zero fraction; the offset form (ISO_LOCAL_TIME) needs a digit
+      if ((nd == 0 && !ntz) || (k < b && s[k] >= '0' && s[k] <= '9')) return false;
       for (; nd < 9; nd++) nanos *= 10;
     }
   }
-  if (y < 1678 || y > 2261 || mo < 1 || mo > 12 || d < 1 || h > 23 || mi > 59 || sec > 59) return false;
+  // ntz (SMART resolver, Parsed.resolveTime): 24:00:00 with a zero fraction is midnight of the next day
+  const bool eod = ntz && h == 24 && mi == 0 && sec == 0 && nanos == 0;
+  if (y < 1678 || y > 2261 || mo < 1 || mo > 12 || d < 1 || (h > 23 && !eod) || mi > 59 || sec > 59) return false;
   const int dim = mo == 2 ? ((y % 4 == 0 && (y % 100 != 0 || y % 400 == 0)) ? 29 : 28)
                 : (mo == 4 || mo == 6 || mo == 9 || mo == 11) ? 30 : 31;
   if (d > 31) return false;
@@ -2780,10 +3035,21 @@ namespace dk {
 void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
 }
-// phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback
+void snap_stats(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dk_snap_stats), 16 * 8); }
+
+// phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback; n_frag < 0: page mode
+// (phases 0 and 1 skipped; work holds one (page, -1) item per compressed page)
 void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int phase, hipStream_t s) {
   if (!n_cp) return;
   const int g = (X.nseg + NT - 1) / NT;
+  if (n_frag < 0) {
+    if (phase == 0) (void)hipMemsetAsync(X.serial, 0, (size_t)n_cp * 4, s);
+    else if (phase == 2) hipLaunchKernelGGL(k_snap_frag, dim3(n_cp), dim3(64), 0, s, X, work);
+    else if (phase == 3)
+      hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
+                         X.cpage, (const int32_t*)X.serial);
+    return;
+  }
   if (phase == 0) {
     hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
     hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);

@@ -67,8 +67,9 @@ struct TReader {
         case 1: case 2: break;
         case 3: byte(); break;
         case 4: case 5: case 6: varint(); break;
-        case 7: p += 8; if (p > e) bad = 1; break;
-        case 8: { uint64_t n = varint(); p += n; if (p > e) bad = 1; break; }
+        case 7: if (e - p < 8) bad = 1; else p += 8; break;
+        // bound-check before advancing: a huge length must not wrap the pointer past the check
+        case 8: { uint64_t n = varint(); if (bad || n > (uint64_t)(e - p)) bad = 1; else p += n; break; }
         case 9: case 10: {
           int etp; int n = list_header(&etp);
           if (sp + 1 >= 16) { bad = 1; return; }

@@ -50,9 +50,21 @@ class Literal:
         return Literal(int(micros_since_epoch_utc), "timestamp")
 
     @staticmethod
-    def ofDecimal(value, precision, scale):              # Literal.ofDecimal(BigDecimal, int, int)
-        from decimal import Decimal
-        return Literal(Decimal(value), "decimal(%d,%d)" % (precision, scale))
+    def ofDecimal(value, precision, scale):
+        """Literal.ofDecimal(BigDecimal, int, int) (Literal.java:173-183): the value is stored with
+        setScale(scale) (ArithmeticException when that needs rounding) and its precision must not
+        exceed `precision`."""
+        import decimal
+        with decimal.localcontext() as ctx:
+            ctx.prec = 200
+            d = decimal.Decimal(value)
+            q = d.quantize(decimal.Decimal(1).scaleb(-scale))
+            if q != d:
+                raise ArithmeticError("Rounding necessary")
+            digits = len(q.as_tuple().digits)
+            if digits > precision:
+                raise ValueError("Decimal precision=%d for decimal %s exceeds max precision %d" % (digits, q, precision))
+        return Literal(q, "decimal(%d,%d)" % (precision, scale))
 
     @staticmethod
     def ofTimestampNtz(micros):                          # Literal.ofTimestampNtz(long)

@@ -557,6 +557,7 @@ class GpuScan:
         self.shard = shard
         self.predicate = predicate
         self.skipping = None          # (planner node, paths, types) when a data-skipping filter applies
+        self._deferred_error = None
         self.partition = None
         self.partition_filter, self.data_filter = None, None
         if predicate is not None:
@@ -567,13 +568,21 @@ class GpuScan:
             self.partition = None     # compiled partition-pruning program (delta_amd/partitions.py)
             if self.partition_filter is not None:
                 from . import partitions as pp
-                self.partition = pp.compile_program(
-                    self.partition_filter, pp.partition_fields(md["schemaString"], parts))
+                try:
+                    self.partition = pp.compile_program(
+                        self.partition_filter, pp.partition_fields(md["schemaString"], parts))
+                except sk.UnsupportedExpression as e:
+                    self._deferred_error = e          # the reference fails when the scan files are read
             if self.data_filter is not None:
                 leaves = sk.data_schema_leaves(md["schemaString"], parts)
                 node = sk.construct(self.data_filter, leaves)
                 if node is not None:
-                    self.skipping = (node,) + sk.compile_program(node, leaves)
+                    try:
+                        sk.check_types(node, leaves)
+                    except sk.UnsupportedExpression as e:
+                        self._deferred_error = e      # the reference fails when the scan files are read
+                    else:
+                        self.skipping = (node,) + sk.compile_program(node, leaves)
         # ScanImpl.getScanFiles: shouldReadStats = hasDataSkippingFilter || includeStats (:128-130)
         self.read_stats = read_stats or self.skipping is not None
         self.metrics = ScanMetrics()
@@ -587,6 +596,8 @@ class GpuScan:
 
     def prepare(self, engine):
         """Host-side setup: parse the commit tail, open checkpoint files, upload to HBM."""
+        if self._deferred_error is not None:
+            raise self._deferred_error
         seg = self.snapshot.log_segment
         commits = list(reversed(seg.deltas))
         self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)

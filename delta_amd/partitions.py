@@ -63,11 +63,17 @@ def compile_program(pred: Predicate, fields: dict):
         return used.index((phys, t)), t
 
     def operand(node):
-        """emit an operand; returns its kind: 'string', 'integral' or None (null literal)."""
+        """emit an operand; returns (kind: 'string', 'integral', 'date', 'decimal' or None for a null
+        literal, Kernel type name)."""
         if isinstance(node, Column):
             k, t = field(node)
             ops.append((PO_FIELD, k, 0))
-            return t if t in ("string", "date", "decimal") else "integral"
+            return (t if t in ("string", "date", "decimal") else "integral"), fields[node.names[0].lower()][0]
+        if isinstance(node, Literal):
+            return operand_lit(node), node.type
+        raise UnsupportedPartitionFilter("partition pruning on expression %r is not supported" % (node,))
+
+    def operand_lit(node):
         if isinstance(node, Literal):
             if node.value is None:
                 ops.append((PO_LIT_NULL, 0, 0))
@@ -108,8 +114,14 @@ def compile_program(pred: Predicate, fields: dict):
             operand(c[0])
             ops.append((PO_ISNULL if n == "IS_NULL" else PO_ISNOTNULL, 0, 0))
         elif n in CMP:
-            ka = operand(c[0])
-            kb = operand(c[1])
+            (ka, ta), (kb, tb) = operand(c[0]), operand(c[1])
+            # DefaultExpressionEvaluator.transformBinaryComparator (:337-354): differently typed
+            # operands need an ImplicitCastExpression up-cast, otherwise the evaluator throws
+            from .skipping import UnsupportedExpression, comparable
+            if not comparable(ta, tb):
+                raise UnsupportedExpression(
+                    "Unsupported expression: %s: operands are of different types which are not comparable: "
+                    "left type=%s, right type=%s" % (n, ta, tb))
             if ka is not None and kb is not None and ka != kb:
                 raise UnsupportedPartitionFilter("comparison of %s with %s is not supported" % (ka, kb))
             ops.append((CMP[n], 0, 0))

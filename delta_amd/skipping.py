@@ -26,6 +26,11 @@ REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
 NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
 
 
+class UnsupportedExpression(RuntimeError):
+    """The reference's expression handler throws for this predicate (KernelException
+    "Unsupported expression"); the scan fails the same way."""
+
+
 class UnsupportedSkipping(RuntimeError):
     pass
 
@@ -122,7 +127,7 @@ def construct(pred: Predicate, leaves: dict):
         return None
     if n == "IS_NULL":                                                          # :240-252
         if isinstance(c[0], Column) and c[0].names in leaves:
-            return (">", ("stat", (NULL_COUNT,) + leaves[c[0].names][1]), ("lit", 0))
+            return (">", ("stat", (NULL_COUNT,) + leaves[c[0].names][1]), ("lit", 0, "long"))
         return None
     if n in ("=", "<", "<=", ">", ">=", "IS NOT DISTINCT FROM"):               # :254-274
         left, right = c
@@ -142,7 +147,7 @@ def _comparator(n, col, lit, leaves):
     """constructComparatorDataSkippingFilters (:286-331)."""
     mn = ("stat", (MIN,) + leaves[col.names][1])
     mx = _max(col, leaves)
-    v = ("lit", lit.value)
+    v = ("lit", lit.value, lit.type)
     if n == "=":
         return ("AND", ("<=", mn, v), (">=", mx, v))
     if n == "<":
@@ -292,6 +297,56 @@ def _operand_kind(n, leaves):
         v = n[1]
         return None if v is None else "string" if isinstance(v, str) else "decimal" if isinstance(v, _Decimal) else "number"
     return "number"
+
+
+# ImplicitCastExpression.UP_CASTABLE_TYPE_TABLE (kernel-defaults/.../internal/expressions/
+# ImplicitCastExpression.java:30-41, canCastTo :118-125)
+_UP_CAST = {"byte": {"short", "integer", "long", "float", "double"}, "short": {"integer", "long", "float", "double"},
+            "integer": {"long", "float", "double"}, "long": {"float", "double"}, "float": {"double"}}
+
+
+def operand_type(n, leaves):
+    """Kernel DataType name of a skipping-predicate operand (decimals keep precision and scale)."""
+    if n[0] == "stat":
+        if n[1][0] in (NUM_RECORDS, NULL_COUNT):
+            return "long"
+        for t, phys in leaves.values():
+            if phys == n[1][1:]:
+                return t
+        raise KeyError(n[1])
+    if n[0] == "lit":
+        return n[2]
+    if n[0] == "timeadd":
+        return operand_type(n[1], leaves)
+    return "boolean"
+
+
+def comparable(lt, rt):
+    """ImplicitCastExpression.canCastTo either way, or the same type."""
+    return lt == rt or rt in _UP_CAST.get(lt, ()) or lt in _UP_CAST.get(rt, ())
+
+
+def check_comparable(n, leaves):
+    """DefaultExpressionEvaluator.transformBinaryComparator (DefaultExpressionEvaluator.java:337-354):
+    operands of different types compare only after an implicit up-cast of one side; any other pair
+    makes the evaluator throw (unsupportedExpressionException)."""
+    lt, rt = operand_type(n[1], leaves), operand_type(n[2], leaves)
+    if comparable(lt, rt):
+        return
+    raise UnsupportedExpression(
+        "Unsupported expression: %s: operands are of different types which are not comparable: "
+        "left type=%s, right type=%s" % (n[0], lt, rt))
+
+
+def check_types(node, leaves):
+    """Walk a constructed skipping predicate and apply check_comparable to every comparator."""
+    if node is None:
+        return
+    if node[0] in ("AND", "OR"):
+        check_types(node[1], leaves)
+        check_types(node[2], leaves)
+    elif node[0] in _CMP:
+        check_comparable(node, leaves)
 
 
 MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 512

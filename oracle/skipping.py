@@ -111,7 +111,7 @@ def _timestamp(text):
     return total // 1000 if total >= 0 else -((-total) // 1000)     # Java division: toward zero
 
 
-_TS_NTZ = re.compile(r"(\d{4})-(\d{2})-(\d{2})T(\d{2}):(\d{2}):(\d{2})(?:\.(\d{1,6}))?")
+_TS_NTZ = re.compile(r"(\d{4})-(\d{2})-(\d{2})T(\d{2}):(\d{2}):(\d{2})(?:\.(\d{0,6}))?")
 
 
 def _timestamp_ntz(text):
@@ -122,8 +122,12 @@ def _timestamp_ntz(text):
     if not m:
         raise StatsDecodeError("Couldn't decode %r, expected a timestamp_ntz" % text)
     y, mo, d, h, mi, sec = (int(m.group(i)) for i in range(1, 7))
+    # appendFraction(MICRO_OF_SECOND, 0, 6, true): minimum width 0, so "." alone is a zero fraction
     micros = int((m.group(7) or "").ljust(6, "0") or 0)
-    if not (1678 <= y <= 2261 and 1 <= mo <= 12 and 1 <= d <= 31 and h <= 23 and mi <= 59 and sec <= 59):
+    # java.time.format.Parsed.resolveTime, SMART: 24:00:00(.0) is the end of the day = next midnight
+    end_of_day = h == 24 and mi == 0 and sec == 0 and micros == 0
+    if not (1678 <= y <= 2261 and 1 <= mo <= 12 and 1 <= d <= 31 and (h <= 23 or end_of_day) and mi <= 59
+            and sec <= 59):
         raise StatsDecodeError("Couldn't decode %r, expected a timestamp_ntz" % text)
     import calendar
     d = min(d, calendar.monthrange(y, mo)[1])

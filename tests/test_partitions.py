@@ -12,6 +12,7 @@ import os
 import pytest
 
 from delta_amd import partitions as pp
+from delta_amd import skipping as sk
 from delta_amd import synth
 from delta_amd.expressions import And, Column, Literal, Or, Predicate
 from tests.golden_util import TABLES, load_expected
@@ -59,11 +60,14 @@ def test_partition_fields_and_compile():
                                    pp.PO_AND]
     flist, ops, _ = pp.compile_program(cmp("<", col("d"), Literal.ofDate(10957)), f)
     assert [t for _, _, t in flist] == [5] and ops[1] == (pp.PO_LIT_INT, 0, 10957)
+    # differently typed operands without an up-cast throw, as transformBinaryComparator does
     for bad in (cmp("=", col("d"), Literal.ofInt(1)), cmp("=", col("s"), Literal.ofInt(1)),
-                cmp("=", col("d"), Literal.ofString("2000-01-01")),
-                Predicate("STARTS_WITH", col("s"), Literal.ofString("a"))):
-        with pytest.raises(pp.UnsupportedPartitionFilter):
+                cmp("=", col("d"), Literal.ofString("2000-01-01")), cmp("=", col("p"), Literal.ofNull("string"))):
+        with pytest.raises(sk.UnsupportedExpression, match="not comparable"):
             pp.compile_program(bad, f)
+    pp.compile_program(cmp("=", col("p"), Literal.ofLong(1)), f)          # integer -> long up-cast
+    with pytest.raises(pp.UnsupportedPartitionFilter):
+        pp.compile_program(Predicate("STARTS_WITH", col("s"), Literal.ofString("a")), f)
     with pytest.raises(ValueError):
         pp.compile_program(cmp("=", col("zz"), Literal.ofInt(1)), f)
 
@@ -274,12 +278,13 @@ def test_gpu_date_partition_values(tmp_path):
 # PartitionValueEvaluator.java:112-113: new BigDecimal(value), compared with compareTo
 DEC_PVS = [{"p": "1.50"}, {"p": "1.5"}, {"p": "-0.001"}, {"p": "1E+1"}, {"p": ".5"}, {"p": None}, {"p": "0.00"},
            {"p": "+10"}, {"p": "-1e-3"}, {"p": "123456789012345678901234567890.5"}, {"p": "2."}]
-DEC_PREDICATES = [cmp("=", col("p"), Literal.ofDecimal("1.5", 10, 2)),
-                  cmp(">", col("p"), Literal.ofDecimal("1.499", 10, 3)),
-                  cmp("<", col("p"), Literal.ofDecimal("0", 10, 0)),
-                  cmp("=", col("p"), Literal.ofDecimal("10", 10, 0)),
-                  cmp("<=", col("p"), Literal.ofDecimal("0.5000", 10, 4)),
-                  Or(Predicate("IS_NULL", col("p")), cmp(">=", col("p"), Literal.ofDecimal("1E+29", 38, 0)))]
+# literals of the column's type decimal(38,3) (differently typed decimals are not comparable)
+DEC_PREDICATES = [cmp("=", col("p"), Literal.ofDecimal("1.5", 38, 3)),
+                  cmp(">", col("p"), Literal.ofDecimal("1.499", 38, 3)),
+                  cmp("<", col("p"), Literal.ofDecimal("0", 38, 3)),
+                  cmp("=", col("p"), Literal.ofDecimal("10", 38, 3)),
+                  cmp("<=", col("p"), Literal.ofDecimal("0.5000", 38, 3)),
+                  Or(Predicate("IS_NULL", col("p")), cmp(">=", col("p"), Literal.ofDecimal("1E+29", 38, 3)))]
 DEC_BAD_PVS = ["x", "", "1.2.3", "1e", " 1", "e5", "1e99999999999", "\u0661"]
 
 
@@ -291,7 +296,7 @@ def test_oracle_decimal_partition_values(tmp_path):
     assert got == [[0, 1], [0, 1, 3, 7, 9, 10], [2, 8], [3, 7], [2, 4, 6, 8], [5, 9]]
     for i, bad in enumerate(DEC_BAD_PVS):
         r = str(tmp_path / ("b%d" % i))
-        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(10,2)")
+        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(38,3)")
         with pytest.raises(opp.PartitionValueError):
             oracle_files(r, DEC_PREDICATES[0])
 
@@ -307,7 +312,7 @@ def test_gpu_decimal_partition_values(tmp_path):
         assert _gpu_files(root, pred, eng) == oracle_files(root, pred), pred
     for i, bad in enumerate(DEC_BAD_PVS):
         r = str(tmp_path / ("b%d" % i))
-        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(10,2)")
+        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(38,3)")
         with pytest.raises(DkError, match="partition"):
             _gpu_files(r, DEC_PREDICATES[0], eng)
     eng.close()

@@ -92,6 +92,7 @@ def oracle_skipping(root, predicate):
     node = sk.construct(data, leaves)
     if node is None:
         return None
+    sk.check_types(node, leaves)
     paths, types, _ = sk.compile_program(node, leaves)
     names = {v: k for k, v in sk.TYPE_CODE.items()}
     return node, {p: names[t] for p, t in zip(paths, types)}
@@ -136,25 +137,52 @@ def test_construct_rules():
     leaves = {("a",): ("long", ("a",)), ("b",): ("integer", ("col-b",)), ("m",): ("map", ("m",))}
     v = Literal.ofLong(5)
     # literal on the left is reversed; OR needs both sides; AND keeps one side
-    assert sk.construct(cmp("<", v, col("a")), leaves) == (">", ("stat", ("maxValues", "a")), ("lit", 5))
+    assert sk.construct(cmp("<", v, col("a")), leaves) == (">", ("stat", ("maxValues", "a")), ("lit", 5, "long"))
     assert sk.construct(Or(cmp("<", col("a"), v), cmp("<", col("m"), v)), leaves) is None
     assert sk.construct(And(cmp("<", col("a"), v), cmp("<", col("m"), v)), leaves) == \
-        ("<", ("stat", ("minValues", "a")), ("lit", 5))
+        ("<", ("stat", ("minValues", "a")), ("lit", 5, "long"))
     # physical names; IS_NULL / IS_NOT_NULL use nullCount and numRecords
     assert sk.construct(Predicate("IS_NOT_NULL", col("b")), leaves) == \
         ("<", ("stat", ("nullCount", "col-b")), ("stat", ("numRecords",)))
     assert sk.construct(Predicate("NOT", Predicate("IS_NOT_NULL", col("b"))), leaves) == \
-        (">", ("stat", ("nullCount", "col-b")), ("lit", 0))
+        (">", ("stat", ("nullCount", "col-b")), ("lit", 0, "long"))
     # NOT(a = 5) -> min < 5 OR max > 5; NOT(a < 5) -> max >= 5
     assert sk.construct(Predicate("NOT", cmp("=", col("a"), v)), leaves) == \
-        ("OR", ("<", ("stat", ("minValues", "a")), ("lit", 5)), (">", ("stat", ("maxValues", "a")), ("lit", 5)))
+        ("OR", ("<", ("stat", ("minValues", "a")), ("lit", 5, "long")), (">", ("stat", ("maxValues", "a")), ("lit", 5, "long")))
     assert sk.construct(Predicate("NOT", cmp("<", col("a"), v)), leaves) == \
-        (">=", ("stat", ("maxValues", "a")), ("lit", 5))
+        (">=", ("stat", ("maxValues", "a")), ("lit", 5, "long"))
     # IS NOT DISTINCT FROM null -> IS_NULL
     assert sk.construct(cmp("IS NOT DISTINCT FROM", col("a"), Literal.ofNull("long")), leaves) == \
-        (">", ("stat", ("nullCount", "a")), ("lit", 0))
+        (">", ("stat", ("nullCount", "a")), ("lit", 0, "long"))
     # non-existent column: no skipping (ScanSuite.scala:1233-1239)
     assert sk.construct(cmp("=", col("foo"), Literal.ofInt(1)), leaves) is None
+
+
+@pytest.mark.parametrize("coltype,lit,ok", [
+    ("integer", Literal.ofLong(5), True),            # int -> long up-cast
+    ("long", Literal.ofInt(5), True),
+    ("byte", Literal.ofShort(5), True),
+    ("long", Literal.ofLong(5), True),
+    ("date", Literal.ofDate(5), True),
+    ("timestamp_ntz", Literal.ofTimestamp(5), False),
+    ("timestamp", Literal.ofTimestampNtz(5), False),
+    ("date", Literal.ofTimestamp(5), False),
+    ("date", Literal.ofLong(5), False),
+    ("timestamp_ntz", Literal.ofLong(5), False),
+    ("decimal(10,2)", Literal.ofDecimal("1.5", 10, 2), True),
+    ("decimal(10,2)", Literal.ofDecimal("1.5", 5, 1), False),    # DecimalType.equals: precision + scale
+    ("string", Literal.ofInt(5), False),
+])
+def test_comparator_types(coltype, lit, ok):
+    """DefaultExpressionEvaluator.transformBinaryComparator (:337-354): only ImplicitCastExpression
+    .canCastTo up-casts make differently typed operands comparable; other pairs throw."""
+    leaves = {("a",): (coltype, ("a",))}
+    node = sk.construct(cmp(">", col("a"), lit), leaves)
+    if ok:
+        sk.check_types(node, leaves)
+    else:
+        with pytest.raises(sk.UnsupportedExpression, match="operands are of different types"):
+            sk.check_types(node, leaves)
 
 
 def test_compile_refuses_unsupported():
@@ -635,11 +663,14 @@ DEC_EDGE_STATS = [
     '{"numRecords":2,"minValues":{"x":null},"maxValues":{"x":1.5}}',
     None,
 ]
-DEC_PREDICATES = [cmp("=", col("x"), Literal.ofDecimal("1.5", 10, 2)),
-                  cmp("<", col("x"), Literal.ofDecimal("0", 1, 0)),
-                  cmp(">", col("x"), Literal.ofDecimal("1.2345678901234567890123456789011E+31", 38, 0)),
-                  cmp("=", col("x"), Literal.ofDecimal("0.000", 4, 3)),
-                  cmp(">=", col("x"), Literal.ofDecimal("1.5000000000000000001", 38, 19))]
+# literals of the column's own type (decimal(38,4)): differently typed decimals are not comparable
+# (DecimalType.equals, DefaultExpressionEvaluator.transformBinaryComparator); the values keep their
+# own digits and scale, which compareTo ignores
+DEC_PREDICATES = [cmp("=", col("x"), Literal.ofDecimal("1.5", 38, 4)),
+                  cmp("<", col("x"), Literal.ofDecimal("0", 38, 4)),
+                  cmp(">", col("x"), Literal.ofDecimal("1.2345678901234567890123456789011E+31", 38, 4)),
+                  cmp("=", col("x"), Literal.ofDecimal("0.000", 38, 4)),
+                  cmp(">=", col("x"), Literal.ofDecimal("1.5001", 38, 4))]
 DEC_BAD_STATS = ['{"numRecords":2,"minValues":{"x":"1.5"}}', '{"numRecords":2,"minValues":{"x":true}}',
                  '{"numRecords":2,"minValues":{"x":{"a":1}}}']
 
@@ -690,12 +721,15 @@ NTZ_MISSES = [_ntz(p.name, p.children[0], t) for p, t in zip(TS_MISSES, ["2019-0
                                                             ["2019-09-09T01:02:03.457001Z", "2019-09-09T01:02:03.455999Z"])]
 NTZ_EDGE_STATS = ['{"numRecords":1,"minValues":{"ts":"2019-02-30T00:00:00"},"maxValues":{"ts":"2019-02-28T00:00:00.5"}}',
                   '{"numRecords":1,"minValues":{"ts":"2020-02-31T23:59:59.999999"},"maxValues":{"ts":"2020-03-01T00:00:00"}}',
+                  # SMART end of day: 24:00:00 is next midnight; a bare '.' is a zero fraction
+                  '{"numRecords":1,"minValues":{"ts":"2019-02-28T24:00:00"},"maxValues":{"ts":"2019-03-01T00:00:00."}}',
                   None]
 NTZ_EDGE_PREDICATES = [_ntz("=", col("ts"), "2019-02-28T00:00:00.200000Z"), _ntz("<", col("ts"), "2020-02-29T23:59:59.999999Z"),
-                       _ntz(">", col("ts"), "2020-03-01T00:00:00.000500Z")]
+                       _ntz(">", col("ts"), "2020-03-01T00:00:00.000500Z"), _ntz("=", col("ts"), "2019-03-01T00:00:00Z")]
 NTZ_BAD_STATS = ['{"numRecords":1,"minValues":{"ts":"2019-09-09t01:02:03"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02"}}',
                  '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03Z"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T01:02:03.1234567"}}',
-                 '{"numRecords":1,"minValues":{"ts":"2019-09-32T01:02:03"}}']
+                 '{"numRecords":1,"minValues":{"ts":"2019-09-32T01:02:03"}}',
+                 '{"numRecords":1,"minValues":{"ts":"2019-09-09T24:00:01"}}', '{"numRecords":1,"minValues":{"ts":"2019-09-09T24:00:00.1"}}']
 
 
 def test_oracle_timestamp_ntz(tmp_path):
@@ -708,7 +742,8 @@ def test_oracle_timestamp_ntz(tmp_path):
     r = str(tmp_path / "e")
     _write_edge_table(r, NTZ_EDGE_STATS, NTZ_COLUMNS)
     got = [sorted(int(x[0].decode()[1:-8]) for x in oracle_files(r, p)[0]) for p in NTZ_EDGE_PREDICATES]
-    assert got == [[0, 2], [0, 2], [1, 2]]        # Feb 30 -> Feb 28 and Feb 31 -> Feb 29 (SMART clamp)
+    # Feb 30 -> Feb 28 and Feb 31 -> Feb 29 (SMART clamp); row 2's 24:00:00 is Mar 1 00:00
+    assert got == [[0, 3], [0, 2, 3], [1, 3], [2, 3]]
     from oracle import skipping as osk
     for i, bad in enumerate(NTZ_BAD_STATS):
         b = str(tmp_path / ("b%d" % i))

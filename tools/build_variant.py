@@ -27,6 +27,7 @@ def main():
                 if f.endswith((".h", ".hip", ".cpp")):
                     shutil.copy(os.path.join(overlay, f), d)
         flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-w", "-I", os.path.join(ROOT, "include")]
+        flags += os.environ.get("DK_VARIANT_FLAGS", "").split()
         procs, objs = [], []
         for src in ("dk_host.cpp", "dk_kernels.hip"):
             obj = os.path.join(d, src + ".o")
