@@ -57,7 +57,7 @@ static int fail(const std::string& m) { g_err = m; return 1; }
 extern "C" const char* dk_last_error(void) { return g_err.c_str(); }
 extern "C" const char* dk_version(void) { return "libdkgpu 0.2 (gfx950)"; }
 // debug: k_snap_frag counters (non-zero only in DK_SNAP_STATS builds; tools/snap_stats.py)
-extern "C" int dk_debug_snap_stats(int64_t out[16]) { snap_stats((unsigned long long*)out); return 0; }
+extern "C" int dk_debug_snap_stats(int64_t out[24]) { snap_stats((unsigned long long*)out); return 0; }
 
 // ------------------------------------------------------------------------------------------------
 // engine
@@ -683,8 +683,13 @@ static int prepare(dk_parquet* p) {
         upload(p->d_spage, spage.data(), spage.size() * 4, s) ||
         p->d_snapws.alloc(spage.size() * 4 * (6 + 2 * DK_SNAP_REC)))
       return 1;
+    // page mode: largest pages first (workgroups are dispatched in order; the long serial decodes
+    // start early and the short ones fill in behind them)
     std::vector<int2> pwork(cpage.size());
     for (size_t i = 0; i < cpage.size(); i++) pwork[i] = make_int2((int)i, -1);
+    std::stable_sort(pwork.begin(), pwork.end(), [&](const int2& a, const int2& b) {
+      return p->h_pages[cpage[a.x]].usize > p->h_pages[cpage[b.x]].usize;
+    });
     if (upload(p->d_pwork, pwork.data(), pwork.size() * sizeof(int2), s)) return 1;
     p->n_segs = (int)spage.size();
   }

@@ -472,7 +472,31 @@ __device__ __forceinline__ int32_t small_mod(int32_t i, int32_t d, uint32_t rcp)
 }
 __device__ __forceinline__ uint32_t small_rcp(int32_t d) { return d > 0 ? (65536u + (uint32_t)d - 1) / (uint32_t)d : 0; }
 
-__device__ unsigned long long dk_snap_stats[16];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
+// wave64 inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31
+// across rows): VALU only, no LDS round trip
+__device__ __forceinline__ int32_t dpp_scan_add(int32_t v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+__device__ __forceinline__ int32_t dpp_scan_max(int32_t v) {     // v >= 0
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+__device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets v of lane i-1 (lane 0: 0)
+  return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
 
 // k_snap_frag: one wave per 64 KiB output fragment, in batches of up to 64 tags (one per lane).
 //  1. tag starts: every lane parses the candidate tag at cursor + lane (LDS window); the true chain
@@ -487,8 +511,10 @@ __device__ unsigned long long dk_snap_stats[16];   // DK_SNAP_STATS builds only 
 //     served from HBM) run one tag at a time in order.
 #ifdef DK_SNAP_STATS
 #define SSTAT(i, v) (st_[i] += (unsigned long long)(v))
+#define STIME(i) do { const unsigned long long c_ = clock64(); st_[i] += c_ - tc_; tc_ = c_; } while (0)
 #else
 #define SSTAT(i, v) ((void)0)
+#define STIME(i) ((void)0)
 #endif
 constexpr int SF_FW = 2048;                // compressed window
 constexpr int SF_BOUT = 512;               // a batch stops collecting tags at this many output bytes
@@ -496,7 +522,12 @@ constexpr int SF_BMAX = SF_BOUT + 64;      // max batch output (every batched ta
 constexpr int SF_RM = SNAP_RING - 1;
 enum : int32_t { SM_WIN = 0, SM_RING = 1, SM_FAR = 2, SM_DEP = 3, SM_FARQ = 4 };
 
-__global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restrict__ work) {
+// EXP instances take experiment flags (A/B timing, tools/snap_ab.py): SX_* skip parts of the work
+// and SX_NOWRITE keeps the output of a preceding correct launch.
+enum : int { SX_NO_FAR = 1, SX_NO_BYTES = 2, SX_NO_RESOLVE = 4, SX_ONLY_DISCOVERY = 8, SX_NOWRITE = 16 };
+template <bool EXP>
+__global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __restrict__ work, int xflags) {
+  const int xf = EXP ? xflags : 0;
   // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map
   __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX + 16) / 16];
   __shared__ u32x4 prm[64];                // per-tag (ot, src, mode | per << 8, rcp)
@@ -527,6 +558,12 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
     o0 = 0; o1 = ulen; ce = clen;
     if (o1 == 0) { if (lane == 0 && p != clen) X.serial[wk.x] = 1; return; }
   }
+  // every cursor below is wave-uniform; say so (values loaded by vector loads look divergent to the
+  // compiler, which would then run the tag chain as a divergent loop)
+  p = __builtin_amdgcn_readfirstlane(p);
+  ce = __builtin_amdgcn_readfirstlane(ce);
+  o0 = __builtin_amdgcn_readfirstlane(o0);
+  o1 = __builtin_amdgcn_readfirstlane(o1);
   GAS uint8_t* gout = gp(out);
   const GAS uint8_t* gin = gp(in);
   int32_t ws = 0;
@@ -546,21 +583,31 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
   };
   int32_t o = o0, flushed = o0;
   auto flush_to = [&](int32_t upto) {          // ring -> HBM, 16-byte granules
+    if (xf & SX_NOWRITE) { flushed = upto; return; }
     for (int32_t u = flushed + 16 * lane; u < upto; u += 16 * 64)
       *(GAS u32x4*)(gout + u) = lds4[(u & SF_RM) >> 4];
     flushed = upto;
   };
 #ifdef DK_SNAP_STATS
-  unsigned long long st_[16] = {0};
+  unsigned long long st_[24] = {0};
+  unsigned long long tc_ = clock64();
 #endif
   SSTAT(9, 1);
   refill(p);
   bool bad = false;
   while (o < o1 && !bad) {
+    p = __builtin_amdgcn_readfirstlane(p);
+    o = __builtin_amdgcn_readfirstlane(o);
+    ws = __builtin_amdgcn_readfirstlane(ws);
+    flushed = __builtin_amdgcn_readfirstlane(flushed);
     if (p + 640 > ws + SF_FW && ws + SF_FW < clen) { refill(p); SSTAT(6, 1); }
+    STIME(13);                                   // loop top + refill
     // ---- 1. tag starts ----
     int32_t n = 0, t = p, outsum = 0, vstart = 0, biglen = 0;
-    for (int r = 0; r < 4 && t < ce && n <= 32 && outsum < SF_BOUT && !biglen; r++) {
+    // windows of 64 candidate bytes until the batch is full; the window data (tags + literals of
+    // up to 64 bytes) must stay inside the LDS copy of the stream
+    for (int r = 0; r < 8 && t < ce && n < 64 && outsum < SF_BOUT && (t + 200 <= ws + SF_FW || ws + SF_FW >= clen);
+         r++) {
       // candidate tag at t + lane: advance (bytes to the next tag) and output length
       int32_t adv = 1, olen = 0;
       {
@@ -581,22 +628,53 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
           olen = kind == 1 ? (int32_t)(((tag >> 2) & 7) + 4) : (int32_t)((tag >> 2) + 1);
         }
       }
-      int32_t j = 0;
       SSTAT(12, 1);
-      while (j < 64 && t + j < ce && n < 64 && outsum < SF_BOUT) {
-        const int32_t l = __builtin_amdgcn_readlane(olen, j);
-        if (l > 64) { if (n == 0) { biglen = l; vstart = t + j; } break; }   // long literal: its own step
-        if (lane == n) vstart = t + j;
-        n++;
-        outsum += l;
-        j += __builtin_amdgcn_readlane(adv, j);
+      // the true chain through this window, by pointer doubling: J_k[c] = the tag 2^k hops after
+      // candidate c (positions >= 64, and the stream end, absorb); lane i then composes the J_k of
+      // the bits of i to find the i-th tag of the chain from offset 0 (a dependent depth of 11
+      // ds_bpermutes per window instead of a scalar step per tag)
+      const int32_t lim = ce - t;                       // the stream end within the window
+      int32_t J0 = lane < lim ? lane + adv : lane;      // a position past the end maps to itself
+      int32_t Jk[6];
+      Jk[0] = J0;
+#pragma unroll
+      for (int k = 1; k < 6; k++) {
+        const int32_t prev = Jk[k - 1];
+        const int32_t g = __shfl(prev, prev < 64 ? prev : 0, 64);
+        Jk[k] = prev < 64 ? g : prev;
       }
-      if (!biglen) t += j;
+      int32_t pos = 0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        const int32_t g = __shfl(Jk[k], pos < 64 ? pos : 0, 64);
+        if (((lane >> k) & 1) && pos < 64) pos = g;
+      }
+      const bool intag = pos < 64 && pos < lim;         // lane i holds the i-th tag of the window
+      const int32_t nw = __popcll(__ballot(intag));
+      const int32_t ol = __shfl(olen, intag ? pos : 0, 64);
+      // accept tags in order while the batch has room: < 64 tags, < SF_BOUT output bytes before
+      // the tag, and no literal longer than 64 bytes (that one runs alone, as the batch's only tag)
+      const int32_t pre = dpp_scan_add(intag ? ol : 0);   // inclusive prefix of output bytes
+      const bool big = intag && ol > 64;
+      const bool stop = intag && (big || n + lane >= 64 || outsum + pre - ol >= SF_BOUT);
+      const unsigned long long sm = __ballot(stop);
+      const int32_t acc = sm ? (int32_t)(__ffsll((long long)sm) - 1) : nw;
+      if (acc == 0 && n == 0 && (__ballot(big) & 1ull)) {
+        biglen = __builtin_amdgcn_readlane(ol, 0);
+        break;
+      }
+      const int32_t mv = __shfl(pos, lane - n >= 0 ? lane - n : 0, 64);
+      if (lane >= n && lane < n + acc) vstart = t + mv;
+      outsum += acc > 0 ? __builtin_amdgcn_readlane(pre, acc - 1) : 0;
+      n += acc;
+      const int32_t ex = __builtin_amdgcn_readlane(pos, acc);   // next tag after the accepted ones
+      t += ex;
+      if (acc < nw) break;                              // the batch is full
     }
     if (biglen) {
       // ---- long literal (> 64 bytes) at p: 64 bytes per step through the window ----
       const int32_t ix = p - ws;
-      const uint32_t tag = ((const uint8_t*)W32)[ix];
+      const uint32_t tag = __builtin_amdgcn_readfirstlane(((const uint8_t*)W32)[ix]);
       const int32_t src = p + 1 + (int32_t)((tag >> 2) + 1 > 60 ? (tag >> 2) + 1 - 60 : 0);
       if (o + biglen > o1) { bad = true; break; }
       for (int32_t c = 0; c < biglen; c += 64) {
@@ -610,11 +688,12 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
       SSTAT(5, 1);
       continue;
     }
-#ifdef SF_ONLY_DISCOVERY
-    o += outsum; p = t;
-    while (o - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
-    continue;
-#endif
+    if (xf & SX_ONLY_DISCOVERY) {
+      o += outsum; p = t;
+      while (o - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
+      continue;
+    }
+    STIME(14);                                   // discovery
     // ---- 2. parse each tag (lane j = tag j) ----
     const bool valid = lane < n;
     int32_t len = 0, off = 0, src = 0, per = 0, mode = SM_WIN;
@@ -644,12 +723,11 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
       }
     }
     // ---- 3. output offsets ----
-    int32_t x = len;
-#pragma unroll
-    for (int k = 1; k < 64; k <<= 1) { const int32_t y = __shfl_up(x, k, 64); if (lane >= k) x += y; }
-    const int32_t total = __shfl(x, 63, 64);
+    const int32_t x = dpp_scan_add(len);
+    const int32_t total = __builtin_amdgcn_readlane(x, 63);
     const int32_t ot = o + x - len;
     if (o + total > o1) { bad = true; break; }
+    STIME(15);                                   // parse + scan
     // ---- 4. modes: WIN (compressed window), RING (resolved ring read), FAR (HBM), DEP (in-batch) ----
     const int32_t ring_lo = o + total - SNAP_RING;    // lowest position no write of this batch overwrites
     bool stuck = false;
@@ -662,11 +740,7 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
     }
     if (__ballot(bad)) { bad = true; break; }
     SSTAT(0, 1); SSTAT(1, n); SSTAT(11, __popcll(__ballot(valid && !is_copy)));
-#ifdef SF_NO_RESOLVE
-    for (int round = 0; round < 0; round++) {
-#else
-    for (int round = 0; round < 6; round++) {
-#endif
+    for (int round = 0; round < ((xf & SX_NO_RESOLVE) ? 0 : 6); round++) {
       const bool act = valid && mode == SM_DEP && !stuck;
       if (!__ballot(act)) break;
       SSTAT(7, 1);
@@ -691,29 +765,23 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
         }
       }
     }
+    STIME(16);                                   // modes + resolution
     // far sources of <= 8 bytes (most: short matches far back): the owning lane loads them with
     // three dwords from the output this wave flushed to HBM, now, and stores them after step 5
     const int32_t ext_f = per ? per : len;
     if (valid && mode == SM_FAR && ext_f <= 8 && len <= 8) mode = SM_FARQ;
     const bool farq = valid && mode == SM_FARQ;
     uint32_t fw0 = 0, fw1 = 0, fw2 = 0;
-#ifdef SF_NO_FAR
-    if (false) {
-#else
-    if (__ballot(farq)) {
-#endif
+    if (!(xf & SX_NO_FAR) && __ballot(farq)) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (farq) {
         const GAS uint32_t* a = (const GAS uint32_t*)(((uintptr_t)(out + src)) & ~(uintptr_t)3);
         fw0 = a[0]; fw1 = a[1]; fw2 = a[2];
       }
     }
+    STIME(17);                                   // far-quick loads issued
     // ---- 5. byte-parallel production of every WIN / RING / FAR tag ----
-#ifdef SF_NO_BYTES
-    const int32_t CH = 0;
-#else
-    const int32_t CH = (total + 63) >> 6;             // output bytes per lane (<= 9)
-#endif
+    const int32_t CH = (xf & SX_NO_BYTES) ? 0 : (total + 63) >> 6;   // output bytes per lane (<= 9)
     SSTAT(8, CH); SSTAT(2, __popcll(__ballot(valid && mode == SM_DEP))); SSTAT(3, __popcll(__ballot(valid && mode >= SM_FAR && mode != SM_DEP)));
     SSTAT(4, __popcll(__ballot(valid && is_copy && mode == SM_WIN))); SSTAT(10, __popcll(__ballot(valid && mode == SM_RING)));
     for (int32_t b = lane * 16; b < total; b += 64 * 16) *(uint4*)(M + b) = make_uint4(0, 0, 0, 0);
@@ -723,35 +791,44 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
       if (len > 0) M[ot - o] = (uint8_t)(lane + 1);
     }
     {
+      // staged so the dependent LDS depth is fixed: tag-map bytes, the owning tags (running max,
+      // DPP prefix max across lanes), their parameters, the source bytes, the stores
       const int32_t b0 = lane * CH;
-      int32_t mx = 0;
-      for (int32_t k = 0; k < CH; k++) if (b0 + k < total) mx = max(mx, (int32_t)M[b0 + k]);
-      int32_t ex = mx;                                 // inclusive prefix max over lanes
+      int32_t mb[9];
 #pragma unroll
-      for (int k = 1; k < 64; k <<= 1) { const int32_t y = __shfl_up(ex, k, 64); if (lane >= k) ex = max(ex, y); }
-      int32_t cur = __shfl_up(ex, 1, 64);
-      if (lane == 0) cur = 0;
-      u32x4 q = prm[cur > 0 ? cur - 1 : 0];
-      int32_t ga[9];                                   // FAR bytes: output offset of the source, -1 none
+      for (int32_t k = 0; k < 9; k++) mb[k] = (k < CH && b0 + k < total) ? (int32_t)M[b0 + k] : 0;
+      int32_t mx = 0;
+#pragma unroll
+      for (int32_t k = 0; k < 9; k++) mx = max(mx, mb[k]);
+      int32_t cur = dpp_shr1(dpp_scan_max(mx));          // owner of this lane's first byte
+      u32x4 q[9];
+#pragma unroll
+      for (int32_t k = 0; k < 9; k++) {
+        if (mb[k]) cur = mb[k];
+        q[k] = prm[cur > 0 ? cur - 1 : 0];
+      }
+      int32_t sa[9];                                     // LDS source address, -1 none
+      int32_t ga[9];                                     // FAR: output offset of the source, -1 none
       bool any_far = false;
 #pragma unroll
       for (int32_t k = 0; k < 9; k++) {
-        ga[k] = -1;
+        sa[k] = -1; ga[k] = -1;
         const int32_t b = b0 + k;
-        if (k < CH && b < total) {
-          const int32_t mk = M[b];
-          if (mk) q = prm[mk - 1];
-          const int32_t md = (int32_t)(q.z & 0xff);
-          if (md <= SM_FAR) {
-            int32_t i = o + b - (int32_t)q.x;
-            const int32_t pr = (int32_t)(q.z >> 8);
-            if (pr) i = small_mod(i, pr, q.w);
-            if (md == SM_FAR) { ga[k] = (int32_t)q.y + i; any_far = true; }
-            else L[(o + b) & SF_RM] = L[md == SM_WIN ? (int32_t)q.y + i : (((int32_t)q.y + i) & SF_RM)];
-          }
+        const int32_t md = (int32_t)(q[k].z & 0xff);
+        if (k < CH && b < total && md <= SM_FAR) {
+          int32_t i = o + b - (int32_t)q[k].x;
+          const int32_t pr = (int32_t)(q[k].z >> 8);
+          if (pr) i = small_mod(i, pr, q[k].w);
+          if (md == SM_FAR) { ga[k] = (int32_t)q[k].y + i; any_far = true; }
+          else sa[k] = md == SM_WIN ? (int32_t)q[k].y + i : (((int32_t)q[k].y + i) & SF_RM);
         }
       }
-      if (__ballot(any_far)) {
+      uint32_t v[9];
+#pragma unroll
+      for (int32_t k = 0; k < 9; k++) v[k] = sa[k] >= 0 ? L[sa[k]] : 0;
+#pragma unroll
+      for (int32_t k = 0; k < 9; k++) if (sa[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)v[k];
+      if (!(xf & SX_NO_FAR) && __ballot(any_far)) {
         // far sources: bytes this wave flushed to HBM earlier (its stores complete first)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         uint32_t gv[9];
@@ -763,12 +840,14 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
     }
     if (farq) {
       const uint32_t sh = (uint32_t)(((uintptr_t)(out + src)) & 3);
+      const uint32_t rc = small_rcp(per);
       for (int32_t i = 0; i < len; i++) {
-        const uint32_t k = sh + (uint32_t)(per ? i % per : i);
+        const uint32_t k = sh + (uint32_t)(per ? small_mod(i, per, rc) : i);
         const uint32_t w = k < 4 ? fw0 : (k < 8 ? fw1 : fw2);
         L[(ot + i) & SF_RM] = (uint8_t)(w >> (8 * (k & 3)));
       }
     }
+    STIME(18);                                   // bytes + far
     // ---- 6. sources straddling tags of this batch: one tag at a time, in order ----
     unsigned long long m = __ballot(valid && mode == SM_DEP);
     while (m) {
@@ -781,19 +860,23 @@ __global__ __launch_bounds__(64) void k_snap_frag(SnapCtx X, const int2* __restr
         L[(ot_j + lane) & SF_RM] = L[(src_j + i) & SF_RM];
       }
     }
+    STIME(19);                                   // dep serial
     o += total;
     p = t;
     while (o - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
+    STIME(20);                                   // flush
   }
 #ifdef DK_SNAP_STATS
-  if (lane == 0) for (int i = 0; i < 16; i++) atomicAdd(&dk_snap_stats[i], st_[i]);
+  if (lane == 0) for (int i = 0; i < 24; i++) atomicAdd(&dk_snap_stats[i], st_[i]);
 #endif
   if (bad || o != o1 || p != ce) {
-    if (lane == 0) X.serial[wk.x] = 1;
+    if (lane == 0 && !(xf & SX_NOWRITE)) X.serial[wk.x] = 1;
     return;
   }
   flush_to(o1);
 }
+template __global__ void k_snap_frag_t<false>(SnapCtx, const int2*, int);
+template __global__ void k_snap_frag_t<true>(SnapCtx, const int2*, int);
 
 // Serial path (pages flagged by k_snap_fix / k_snap_frag): every lane parses the same tag (uniform
 // control flow), then the wave copies the literal / back-reference 64 bytes per step. Back
@@ -3035,7 +3118,16 @@ namespace dk {
 void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
 }
-void snap_stats(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dk_snap_stats), 16 * 8); }
+void snap_stats(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dk_snap_stats), 24 * 8); }
+
+// DK_SNAP_EXP=<flags> (A/B timing only): a correct decode, then the timed experiment instance with
+// SX_NOWRITE | flags over the same work
+static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s) {
+  static const int exp = getenv("DK_SNAP_EXP") ? atoi(getenv("DK_SNAP_EXP")) : -1;
+  if (exp < 0) { hipLaunchKernelGGL(k_snap_frag_t<false>, dim3(n), dim3(64), 0, s, X, work, 0); return; }
+  hipLaunchKernelGGL(k_snap_frag_t<false>, dim3(n), dim3(64), 0, s, X, work, 0);
+  hipLaunchKernelGGL(k_snap_frag_t<true>, dim3(n), dim3(64), 0, s, X, work, exp | SX_NOWRITE);
+}
 
 // phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback; n_frag < 0: page mode
 // (phases 0 and 1 skipped; work holds one (page, -1) item per compressed page)
@@ -3044,7 +3136,7 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
   const int g = (X.nseg + NT - 1) / NT;
   if (n_frag < 0) {
     if (phase == 0) (void)hipMemsetAsync(X.serial, 0, (size_t)n_cp * 4, s);
-    else if (phase == 2) hipLaunchKernelGGL(k_snap_frag, dim3(n_cp), dim3(64), 0, s, X, work);
+    else if (phase == 2) launch_frag(X, n_cp, work, s);
     else if (phase == 3)
       hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
                          X.cpage, (const int32_t*)X.serial);
@@ -3056,7 +3148,7 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
   } else if (phase == 2) {
-    if (n_frag) hipLaunchKernelGGL(k_snap_frag, dim3(n_frag), dim3(64), 0, s, X, work);
+    if (n_frag) launch_frag(X, n_frag, work, s);
   } else {
     hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
                        X.cpage, (const int32_t*)X.serial);

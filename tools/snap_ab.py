@@ -1,5 +1,7 @@
-"""Time k_snap_frag / k_snap_walk_link for several library builds on one table (A/B of snappy
-variants). Usage: python tools/snap_ab.py TABLE lib1.so [lib2.so ...] (each in a subprocess)."""
+"""Time k_snap_frag / k_snap_walk_link on one table for several configurations (A/B of snappy
+variants), each in a subprocess. Arguments after TABLE: a library path (DK_LIB_PATH) or
+"exp=<flags>" (DK_SNAP_EXP: a correct decode plus the experiment instance; compare with exp=16).
+Usage: python tools/snap_ab.py TABLE [lib.so | exp=N] ..."""
 import json
 import os
 import subprocess
@@ -23,7 +25,10 @@ print(json.dumps(out))
 '''
 table = sys.argv[1]
 for so in sys.argv[2:]:
-    env = dict(os.environ, DK_LIB_PATH=os.path.abspath(so))
+    if so.startswith("exp="):
+        env = dict(os.environ, DK_SNAP_EXP=so[4:])
+    else:
+        env = dict(os.environ, DK_LIB_PATH=os.path.abspath(so))
     r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, table)], env=env, capture_output=True, text=True, timeout=300)
     try:
         d = json.loads(r.stdout.strip().splitlines()[-1])
