@@ -37,9 +37,11 @@ REMOVE_LEAVES = ["remove.path", "remove.deletionVector.storageType", "remove.del
                  "remove.deletionVector.cardinality"]
 PM_LEAVES = ["protocol.minReaderVersion", "protocol.minWriterVersion",
              "protocol.readerFeatures.list.element", "protocol.writerFeatures.list.element",
-             "metaData.id", "metaData.schemaString", "metaData.partitionColumns.list.element",
+             "metaData.id", "metaData.name", "metaData.description", "metaData.format.provider",
+             "metaData.format.options.key_value.key", "metaData.format.options.key_value.value",
+             "metaData.schemaString", "metaData.partitionColumns.list.element",
              "metaData.configuration.key_value.key", "metaData.configuration.key_value.value",
-             "metaData.format.provider", "metaData.createdTime"]
+             "metaData.createdTime"]
 SIDECAR_LEAVES = ["sidecar.path", "sidecar.sizeInBytes", "sidecar.modificationTime"]
 
 TIMING = 1
@@ -386,25 +388,29 @@ class Snapshot:
 
     def _load_protocol_metadata(self, engine):
         """LogReplay.loadTableProtocolAndMetadata (internal/replay/LogReplay.java:220-314): newest
-        commit first, then the checkpoint (decoded on the GPU)."""
+        commit first, then the checkpoint (decoded on the GPU); once both are found the table must
+        be readable (TableFeatures.validateReadSupportedTable, delta_amd/actions.py)."""
+        from . import actions as A
         t0 = time.perf_counter()
         try:
             self._pm_from_commits()
         finally:
             self.load_ms["commits_pm"] = (time.perf_counter() - t0) * 1e3
-        if self.protocol is not None and self.metadata is not None:
-            return
-        t0 = time.perf_counter()
-        try:
-            self._pm_from_checkpoint(engine)
-        finally:
-            self.load_ms["checkpoint_pm"] = (time.perf_counter() - t0) * 1e3
+        if self.protocol is None or self.metadata is None:
+            t0 = time.perf_counter()
+            try:
+                self._pm_from_checkpoint(engine)
+            finally:
+                self.load_ms["checkpoint_pm"] = (time.perf_counter() - t0) * 1e3
         if self.protocol is None:
             raise DkError("No protocol found at version %d" % self.getVersion())
         if self.metadata is None:
             raise DkError("No metadata found at version %d" % self.getVersion())
+        # dataPath.toString(): the qualified path, unescaped (internal/fs/Path.java:328-350)
+        A.validate_read_supported(self.protocol, "file:" + self.table.path, self.metadata)
 
     def _pm_from_commits(self):
+        from . import actions as A
         for d in reversed(self.log_segment.deltas):
             with open(d.path, "rb") as f:
                 raw = f.read()
@@ -414,20 +420,21 @@ class Snapshot:
                 if '"protocol"' in line or '"metaData"' in line or "\\u" in line:
                     obj = json.loads(line)
                     if self.protocol is None and obj.get("protocol") is not None:
-                        self.protocol = obj["protocol"]
+                        self.protocol = A.protocol_from_json(obj["protocol"])
                     if self.metadata is None and obj.get("metaData") is not None:
-                        self.metadata = obj["metaData"]
+                        self.metadata = A.metadata_from_json(obj["metaData"])
             if self.protocol is not None and self.metadata is not None:
                 return
 
     def _pm_from_checkpoint(self, engine):
+        from . import actions as A
         cks = self.log_segment.checkpoints
         if cks and cks[0].kind == "v2" and cks[0].path.endswith(".json"):
             _, proto, meta = self._json_manifest()
-            if self.protocol is None:
-                self.protocol = proto
-            if self.metadata is None:
-                self.metadata = meta
+            if self.protocol is None and proto is not None:
+                self.protocol = A.protocol_from_json(proto)
+            if self.metadata is None and meta is not None:
+                self.metadata = A.metadata_from_json(meta)
             files = self._checkpoint_files(engine) if (self.protocol is None or self.metadata is None) else []
         else:
             files = self._checkpoint_files(engine) if cks else []
@@ -438,20 +445,77 @@ class Snapshot:
                 # only that row's values come back to the host
                 r = ps.first_row(fi, "protocol.minReaderVersion") if self.protocol is None else -1
                 if r >= 0:
-                    rv = ps.column_rows(fi, "protocol.minReaderVersion", r, 1)
-                    wv = ps.column_rows(fi, "protocol.minWriterVersion", r, 1)
-                    self.protocol = {"minReaderVersion": int(rv.fixed.view(np.int32)[0]),
-                                     "minWriterVersion": int(wv.fixed.view(np.int32)[0]) if wv.present else 0}
+                    self.protocol = _protocol_row(ps, fi, r)
                 r = ps.first_row(fi, "metaData.id") if self.metadata is None else -1
                 if r >= 0:
-                    mid = ps.column_rows(fi, "metaData.id", r, 1)
-                    ss = ps.column_rows(fi, "metaData.schemaString", r, 1)
-                    pc = ps.column_rows(fi, "metaData.partitionColumns.list.element", r, 1)
-                    self.metadata = {"id": mid.string(0).decode() if mid.row_def[0] >= 2 else None,
-                                     "schemaString": (ss.string(0).decode()
-                                                      if ss.present and ss.row_def[0] >= 2 else None),
-                                     "partitionColumns": _list_at(pc if pc.present else None, 0)}
+                    self.metadata = _metadata_row(ps, fi, r)
+                if self.protocol is not None and self.metadata is not None:
+                    break
             ps.close()
+
+
+def _row(ps, fi, leaf, r):
+    c = ps.column_rows(fi, leaf, r, 1)
+    return c if c.present else None
+
+
+def _str_row(ps, fi, leaf, r):
+    c = _row(ps, fi, leaf, r)
+    return None if c is None or c.row_def[0] < c.max_def else c.string(0).decode("utf-8", "replace")
+
+
+def _int_row(ps, fi, leaf, r, dtype):
+    c = _row(ps, fi, leaf, r)
+    return None if c is None or c.row_def[0] < c.max_def else int(c.fixed.view(dtype)[0])
+
+
+def _list_row(ps, fi, leaf, r):
+    c = _row(ps, fi, leaf, r)
+    return _list_at(c, 0)
+
+
+def _map_row(ps, fi, kleaf, vleaf, r):
+    kc, vc = _row(ps, fi, kleaf, r), _row(ps, fi, vleaf, r)
+    if kc is None or kc.row_def[0] < kc.rep_def - 1:
+        return None
+    a, b = int(kc.row_offs[0]), int(kc.row_offs[1])
+    out = {}
+    for i in range(a, b):
+        v = None if vc is None or vc.entry_def[i] < vc.max_def else vc.string(i).decode("utf-8", "replace")
+        out[kc.string(i).decode("utf-8", "replace")] = v
+    return out
+
+
+def _protocol_row(ps, fi, r):
+    """Protocol.fromColumnVector (actions/Protocol.java:33-47) on checkpoint row r."""
+    from .actions import KernelException
+    rv = _int_row(ps, fi, "protocol.minReaderVersion", r, np.int32)
+    wv = _int_row(ps, fi, "protocol.minWriterVersion", r, np.int32)
+    if rv is None or wv is None:
+        raise KernelException("protocol action with a null minReaderVersion / minWriterVersion")
+    return {"minReaderVersion": rv, "minWriterVersion": wv,
+            "readerFeatures": _list_row(ps, fi, "protocol.readerFeatures.list.element", r) or [],
+            "writerFeatures": _list_row(ps, fi, "protocol.writerFeatures.list.element", r) or []}
+
+
+def _metadata_row(ps, fi, r):
+    """Metadata.fromColumnVector (actions/Metadata.java:35-55) on checkpoint row r."""
+    from .actions import KernelException
+    md = {"id": _str_row(ps, fi, "metaData.id", r),
+          "name": _str_row(ps, fi, "metaData.name", r),
+          "description": _str_row(ps, fi, "metaData.description", r),
+          "format": {"provider": _str_row(ps, fi, "metaData.format.provider", r),
+                     "options": _map_row(ps, fi, "metaData.format.options.key_value.key",
+                                         "metaData.format.options.key_value.value", r) or {}},
+          "schemaString": _str_row(ps, fi, "metaData.schemaString", r),
+          "partitionColumns": _list_row(ps, fi, "metaData.partitionColumns.list.element", r),
+          "createdTime": _int_row(ps, fi, "metaData.createdTime", r, np.int64),
+          "configuration": _map_row(ps, fi, "metaData.configuration.key_value.key",
+                                    "metaData.configuration.key_value.value", r)}
+    for key in ("id", "schemaString", "partitionColumns", "configuration"):
+        if md[key] is None:
+            raise KernelException("Field `%s` in `metaData` is not nullable, but it is null" % key)
+    return md
 
 
 def _list_at(col, r):

@@ -707,11 +707,94 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
     return res
 
 
+def _pm_json_protocol(p):
+    """Protocol.fromColumnVector over a commit-JSON protocol (Protocol.java:33-47): null feature
+    lists read as empty; the versions are required ints."""
+    for k in ("minReaderVersion", "minWriterVersion"):
+        if not _is_int(p.get(k)):
+            raise OracleError("protocol.%s: expected an int, got %r" % (k, p.get(k)))
+    return {"minReaderVersion": p["minReaderVersion"], "minWriterVersion": p["minWriterVersion"],
+            "readerFeatures": list(p.get("readerFeatures") or []), "writerFeatures": list(p.get("writerFeatures") or [])}
+
+
+def _pm_json_metadata(m):
+    """Metadata.fromColumnVector over a commit-JSON metaData (Metadata.java:35-55)."""
+    for k in ("id", "format", "schemaString", "partitionColumns", "configuration"):
+        if m.get(k) is None:
+            raise OracleError("metaData.%s is required" % k)
+    if m.get("createdTime") is not None and not _is_long(m["createdTime"]):
+        raise OracleError("metaData.createdTime: expected a long")
+    fmt = m["format"]
+    return {"id": m["id"], "name": m.get("name"), "description": m.get("description"),
+            "format": {"provider": fmt.get("provider"), "options": dict(fmt.get("options") or {})},
+            "schemaString": m["schemaString"], "partitionColumns": list(m["partitionColumns"]),
+            "createdTime": m.get("createdTime"), "configuration": dict(m["configuration"])}
+
+
+def _first_defined(col, min_def=1):
+    idx = np.nonzero(col.row_def >= min_def)[0] if col is not None else []
+    return int(idx[0]) if len(idx) else -1
+
+
+def _list_value(col, r):
+    if col is None or col.row_def[r] < col.rep_def - 1:
+        return None
+    a, b = int(col.row_offs[r]), int(col.row_offs[r + 1])
+    return [bytes(col.chars[col.offs[i]:col.offs[i + 1]]).decode() if col.entry_def[i] >= col.max_def else None
+            for i in range(a, b)]
+
+
+def _map_value(kc, vc, r):
+    pairs = _map_at(kc, vc, r)
+    return None if pairs is None else {k.decode(): (None if v is None else v.decode()) for k, v in pairs}
+
+
+def _scalar(pf, leaf, r, dtype=None):
+    c = pf.read(leaf)
+    if c is None or c.row_def[r] < c.max_def:
+        return None
+    if dtype is None:
+        return bytes(c.chars[c.offs[r]:c.offs[r + 1]]).decode()
+    w = np.dtype(dtype).itemsize
+    return int(c.fixed[r * w:(r + 1) * w].view(dtype)[0])
+
+
+SUPPORTED_READER_FEATURES = {"columnMapping", "deletionVectors", "timestampNtz", "typeWidening-preview",
+                             "typeWidening", "vacuumProtocolCheck", "variantType", "variantType-preview",
+                             "v2Checkpoint"}                 # TableFeatures.java:47-61
+
+
+def validate_read_supported(prot, table_path, meta):
+    """TableFeatures.validateReadSupportedTable (TableFeatures.java:76-98) with
+    ColumnMapping.getColumnMappingMode (util/ColumnMapping.java:41-51,78-92)."""
+    def cm_mode():
+        v = (meta.get("configuration") or {}).get("delta.columnMapping.mode")
+        if v is not None and v.lower() not in ("none", "id", "name"):
+            raise OracleError("Invalid value for table property 'delta.columnMapping.mode': '%s'." % v)
+    rv = prot["minReaderVersion"]
+    if rv == 1:
+        return
+    if rv == 2:
+        cm_mode()
+        return
+    if rv == 3:
+        bad = set(prot["readerFeatures"]) - SUPPORTED_READER_FEATURES
+        if bad:
+            raise OracleError("Unsupported Delta reader features: table `%s` requires reader table features [%s]"
+                              % (table_path, ", ".join(sorted(bad))))
+        if "columnMapping" in prot["readerFeatures"]:
+            cm_mode()
+        return
+    raise OracleError("Unsupported Delta protocol reader version: table `%s` requires reader version %d"
+                      % (table_path, rv))
+
+
 def load_protocol_metadata(table_root: str):
     """``LogReplay.loadTableProtocolAndMetadata`` (internal/replay/LogReplay.java:220-314), no hint:
     files newest first (``LogSegment.allLogFilesReversed``); the first row whose ``protocol`` /
-    ``metaData`` struct is non-null wins. Returns ((minReaderVersion, minWriterVersion),
-    (id, schemaString, partitionColumns)) with the checkpoint decoded by the C oracle."""
+    ``metaData`` struct is non-null wins; then ``TableFeatures.validateReadSupportedTable``.
+    Returns (protocol dict, metadata dict) -- every field of Protocol / Metadata -- with the
+    checkpoint decoded by the C oracle."""
     seg = load_log_segment(table_root)
     prot = meta = None
     for f in seg.all_files_reversed():
@@ -719,37 +802,34 @@ def load_protocol_metadata(table_root: str):
             with open(f.path, "rb") as fh:
                 lines = fh.read().decode("utf-8", "replace").splitlines()
             for line in lines:
+                if not line.strip():
+                    continue
                 obj = json.loads(line)
                 if prot is None and obj.get("protocol") is not None:
-                    p = obj["protocol"]
-                    prot = (p.get("minReaderVersion"), p.get("minWriterVersion"))
+                    prot = _pm_json_protocol(obj["protocol"])
                 if meta is None and obj.get("metaData") is not None:
-                    m = obj["metaData"]
-                    meta = (m.get("id"), m.get("schemaString"), m.get("partitionColumns"))
+                    meta = _pm_json_metadata(obj["metaData"])
         else:
             pf = ParquetFile.open(f.path)
-            rv, wv = pf.read("protocol.minReaderVersion"), pf.read("protocol.minWriterVersion")
-            if prot is None and rv is not None:
-                idx = np.nonzero(rv.row_def >= 1)[0]
-                if len(idx):
-                    r = int(idx[0])
-                    prot = (int(rv.fixed.view(np.int32)[r]), int(wv.fixed.view(np.int32)[r]) if wv is not None else 0)
-            mid = pf.read("metaData.id")
-            if meta is None and mid is not None:
-                idx = np.nonzero(mid.row_def >= 1)[0]
-                if len(idx):
-                    r = int(idx[0])
-                    ss = pf.read("metaData.schemaString")
-                    pc = pf.read("metaData.partitionColumns.list.element")
-                    plist = None
-                    if pc is not None and pc.row_def[r] >= pc.rep_def - 1:
-                        a, b = int(pc.row_offs[r]), int(pc.row_offs[r + 1])
-                        plist = [bytes(pc.chars[pc.offs[i]:pc.offs[i + 1]]).decode() if pc.entry_def[i] >= pc.max_def
-                                 else None for i in range(a, b)]
-                    meta = (bytes(mid.chars[mid.offs[r]:mid.offs[r + 1]]).decode() if mid.row_def[r] >= 2 else None,
-                            bytes(ss.chars[ss.offs[r]:ss.offs[r + 1]]).decode()
-                            if ss is not None and ss.row_def[r] >= 2 else None,
-                            plist)
+            r = _first_defined(pf.read("protocol.minReaderVersion")) if prot is None else -1
+            if r >= 0:
+                prot = {"minReaderVersion": _scalar(pf, "protocol.minReaderVersion", r, np.int32),
+                        "minWriterVersion": _scalar(pf, "protocol.minWriterVersion", r, np.int32),
+                        "readerFeatures": _list_value(pf.read("protocol.readerFeatures.list.element"), r) or [],
+                        "writerFeatures": _list_value(pf.read("protocol.writerFeatures.list.element"), r) or []}
+            r = _first_defined(pf.read("metaData.id")) if meta is None else -1
+            if r >= 0:
+                meta = {"id": _scalar(pf, "metaData.id", r), "name": _scalar(pf, "metaData.name", r),
+                        "description": _scalar(pf, "metaData.description", r),
+                        "format": {"provider": _scalar(pf, "metaData.format.provider", r),
+                                   "options": _map_value(pf.read("metaData.format.options.key_value.key"),
+                                                         pf.read("metaData.format.options.key_value.value"), r) or {}},
+                        "schemaString": _scalar(pf, "metaData.schemaString", r),
+                        "partitionColumns": _list_value(pf.read("metaData.partitionColumns.list.element"), r),
+                        "createdTime": _scalar(pf, "metaData.createdTime", r, np.int64),
+                        "configuration": _map_value(pf.read("metaData.configuration.key_value.key"),
+                                                    pf.read("metaData.configuration.key_value.value"), r)}
         if prot is not None and meta is not None:
+            validate_read_supported(prot, "file:" + os.path.abspath(table_root), meta)
             return prot, meta
     raise OracleError("No %s found at version %d" % ("protocol" if prot is None else "metadata", seg.version))

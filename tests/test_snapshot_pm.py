@@ -2,6 +2,7 @@
 220-314): the product's protocol / metadata must equal the oracle's on every golden table, and on a
 synthetic checkpoint-only table where the first non-null rows sit deep inside the checkpoint."""
 import os
+import re
 
 import pytest
 
@@ -15,9 +16,7 @@ def _product_pm(root):
     eng = K.GpuEngine()
     try:
         snap = K.Table.forPath(eng, root).getLatestSnapshot(eng)
-        p, m = snap.protocol, snap.metadata
-        return ((p.get("minReaderVersion"), p.get("minWriterVersion")),
-                (m.get("id"), m.get("schemaString"), m.get("partitionColumns")))
+        return snap.protocol, snap.metadata
     finally:
         eng.close()
 
@@ -26,8 +25,9 @@ def _product_pm(root):
 def test_oracle_pm_golden(name):
     from oracle import ref
     prot, meta = ref.load_protocol_metadata(os.path.join(TABLES, name))
-    assert prot[0] >= 1 and prot[1] >= 1
-    assert meta[0] and meta[1].startswith("{")
+    assert prot["minReaderVersion"] >= 1 and prot["minWriterVersion"] >= 1
+    assert meta["id"] and meta["schemaString"].startswith("{") and meta["format"]["provider"] == "parquet"
+    assert isinstance(meta["configuration"], dict) and isinstance(meta["partitionColumns"], list)
 
 
 @pytest.mark.gpu
@@ -70,7 +70,9 @@ def test_gpu_pm_checkpoint_only(tmp_path, parts, move):
     _checkpoint_only(d, parts, move)
     got = _product_pm(d)
     assert got == ref.load_protocol_metadata(d)
-    assert got[1][2] is not None
+    assert got[1]["partitionColumns"] == ["date"]
+    assert got[0]["readerFeatures"] == ["deletionVectors", "v2Checkpoint"]
+    assert got[1]["configuration"] == {"delta.enableDeletionVectors": "true"}
 
 
 def test_oracle_pm_moved_rows(tmp_path):
@@ -78,4 +80,70 @@ def test_oracle_pm_moved_rows(tmp_path):
     d = str(tmp_path)
     _checkpoint_only(d, 1, (25_001, 13_007))
     prot, meta = ref.load_protocol_metadata(d)
-    assert prot == (3, 7) and meta[2] == ["date"]
+    assert (prot["minReaderVersion"], prot["minWriterVersion"]) == (3, 7) and meta["partitionColumns"] == ["date"]
+    assert prot["readerFeatures"] == ["deletionVectors", "v2Checkpoint"]
+    assert meta["format"] == {"provider": "parquet", "options": {}} and meta["createdTime"] == 1_700_000_000_000
+
+
+def _pm_table(d, protocol, configuration=None):
+    """A one-commit table with the given protocol / metaData configuration."""
+    import json
+    log = os.path.join(d, "_delta_log")
+    os.makedirs(log)
+    meta = {"id": "t", "format": {"provider": "parquet", "options": {}},
+            "schemaString": json.dumps({"type": "struct", "fields": [
+                {"name": "a", "type": "long", "nullable": True, "metadata": {}}]}),
+            "partitionColumns": [], "configuration": configuration or {}, "createdTime": 1}
+    with open(os.path.join(log, "%020d.json" % 0), "w") as f:
+        f.write(json.dumps({"protocol": protocol}) + "\n" + json.dumps({"metaData": meta}) + "\n")
+        f.write(json.dumps({"add": {"path": "a.parquet", "partitionValues": {}, "size": 1, "modificationTime": 1,
+                                    "dataChange": True}}) + "\n")
+    return d
+
+
+# TableFeatures.validateReadSupportedTable (TableFeatures.java:76-98): (protocol, configuration,
+# expected error fragment or None)
+VALIDATION_CASES = [
+    ({"minReaderVersion": 1, "minWriterVersion": 2}, None, None),
+    ({"minReaderVersion": 2, "minWriterVersion": 5}, {"delta.columnMapping.mode": "Name"}, None),
+    ({"minReaderVersion": 2, "minWriterVersion": 5}, {"delta.columnMapping.mode": "bogus"},
+     "Invalid value for table property 'delta.columnMapping.mode'"),
+    ({"minReaderVersion": 3, "minWriterVersion": 7, "readerFeatures": ["deletionVectors", "v2Checkpoint"],
+      "writerFeatures": ["deletionVectors"]}, None, None),
+    ({"minReaderVersion": 3, "minWriterVersion": 7, "readerFeatures": ["deletionVectors", "fancyFeature"],
+      "writerFeatures": []}, None, "requires reader table features [fancyFeature]"),
+    ({"minReaderVersion": 3, "minWriterVersion": 7, "readerFeatures": ["columnMapping"], "writerFeatures": []},
+     {"delta.columnMapping.mode": "oops"}, "Invalid value for table property"),
+    ({"minReaderVersion": 4, "minWriterVersion": 7}, None, "requires reader version 4"),
+]
+
+
+@pytest.mark.parametrize("case", range(len(VALIDATION_CASES)))
+def test_oracle_read_support(tmp_path, case):
+    from oracle import ref
+    prot, conf, err = VALIDATION_CASES[case]
+    d = _pm_table(str(tmp_path / "t"), prot, conf)
+    if err is None:
+        p, m = ref.load_protocol_metadata(d)
+        assert p["minReaderVersion"] == prot["minReaderVersion"]
+        assert p["readerFeatures"] == prot.get("readerFeatures", [])
+    else:
+        with pytest.raises(ref.OracleError, match=re.escape(err)):
+            ref.load_protocol_metadata(d)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", range(len(VALIDATION_CASES)))
+def test_gpu_read_support(tmp_path, case):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    from oracle import ref
+    prot, conf, err = VALIDATION_CASES[case]
+    d = _pm_table(str(tmp_path / "t"), prot, conf)
+    if err is None:
+        assert _product_pm(d) == ref.load_protocol_metadata(d)
+    else:
+        eng = K.GpuEngine()
+        with pytest.raises(DkError, match=re.escape(err)):
+            K.Table.forPath(eng, d).getLatestSnapshot(eng)
+        eng.close()
