@@ -15,9 +15,10 @@ Three timed regions:
      (BASELINE.md "Metric definitions"). `jmh_op_ms` adds the snapshot load, as the JMH op does.
   3. `snapshot_load_ms`: Table.forPath(...).getLatestSnapshot (cold and warm).
 
-Multi-GPU (one process per GPU; RCCL only for barriers / max-reductions of the elapsed time): C3 is
-one table sharded over the ranks by checkpoint part (strong scaling); the other configs give every
-rank its own table (weak scaling). No collective runs inside the timed region.
+Multi-GPU (one process per GPU): C3 is one table sharded over the ranks by checkpoint row groups
+(delta_amd/shard.py, strong scaling); each step ends with the exchange that assembles the result --
+ScanMetrics counters and the selection bitmaps of every shard, packed on the GPU and all-gathered over
+RCCL. The other configs give every rank its own table (weak scaling, no collective).
 """
 import argparse
 import json
@@ -37,8 +38,8 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-# BASELINE.json configs. "shared": one table sharded over the ranks by checkpoint
-# file (strong scaling); otherwise every rank reconciles its own table (weak scaling).
+# BASELINE.json configs. "shared": one table sharded over the ranks by checkpoint row
+# groups (strong scaling); otherwise every rank reconciles its own table (weak scaling).
 CONFIGS = {
     "c1": dict(rows=1_000_000, shared=False, stats=False, predicate=None,
                spec=dict(pv_keys=1, n_commits=100, adds_per_commit=50, removes_per_commit=50),
@@ -51,7 +52,7 @@ CONFIGS = {
     "c3": dict(rows=100_000_000, shared=True, stats=False, predicate=None,
                spec=dict(n_parts=64, compression="snappy", n_commits=1000, adds_per_commit=100,
                          removes_per_commit=100, readd_frac=0.1, dup_frac=0.05),
-               desc="C3: %d-AddFile 64-part snappy checkpoint (sharded over the GPUs by part) + 1k JSON commits "
+               desc="C3: %d-AddFile 64-part snappy checkpoint (row groups sharded over the GPUs) + 1k JSON commits "
                     "(100 adds + 100 removes each, 10%% re-adds, 5%% duplicates); read schema add(no stats)+remove"),
     "c4": dict(rows=50_000_000, shared=False, stats=True, predicate=("id", ">", 25_000_000),
                spec=dict(n_parts=8, dv_frac=0.3, with_stats=True, n_commits=100, adds_per_commit=50,
@@ -63,7 +64,7 @@ CONFIGS = {
                          delta_binary_packed=True, hot_frac=0.6, n_commits=100, adds_per_commit=50,
                          removes_per_commit=50),
                desc="C5: %d-AddFile V2 checkpoint (manifest + 16 sidecars, snappy, v2 pages, DELTA_BINARY_PACKED, "
-                    "60%% of paths under one hot partition) sharded over the GPUs by file; "
+                    "60%% of paths under one hot partition) row groups sharded over the GPUs; "
                     "read schema add(no stats)+remove+sidecar"),
 }
 
@@ -244,16 +245,27 @@ def main():
     n_ckpt_rows = sum(scan.ckpt.num_rows(i) for i in range(len(scan.ckpt_files))) if scan.ckpt else 0
     n_tail = int(scan.tail.rows)
     bytes_read, bytes_written = scan.ckpt.traffic() if scan.ckpt else (0, 0)
-    for _ in range(args.warmup):
+    merged = None
+
+    def step():
+        nonlocal merged
         scan.run()
         scan.sync()
-    counters = scan.metrics.as_tuple()
+        if dist is not None and cfg["shared"]:
+            # the exchange: ScanMetrics counters and every shard's selection bitmap (packed on the
+            # GPU) all-gathered over RCCL; row data stays on the GPU that decoded it
+            from delta_amd import shard
+            merged = shard.gather_selections(shard.scan_units(scan, device_bits=True), scan.tail_metrics.as_tuple(),
+                                             scan.ckpt_metrics.as_tuple(), device="cuda")
+
+    for _ in range(args.warmup):
+        step()
+    counters = merged[0] if merged else scan.metrics.as_tuple()
     barrier()
     stats0 = scan.kernel_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        scan.run()
-        scan.sync()
+        step()
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0)
     stats1 = scan.kernel_stats()
@@ -333,7 +345,8 @@ def main():
         "data": "synthetic (seed 20250218; delta_amd/synth.py)",
         "config": {"workload": cfg["desc"] % rows, "name": args.config,
                    "compression": compression,
-                   "parallelism": ("strong: checkpoint parts round-robin over %d GPU(s), tail on every GPU" % world
+                   "parallelism": ("strong: checkpoint row groups in %d contiguous runs (one per GPU), tail on every "
+                                   "GPU, counters + selection bitmaps all-gathered over RCCL each step" % world
                                    if cfg["shared"] else "weak: one table per GPU"),
                    "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail,
                    "checkpoint_files_per_gpu": len(ckpt_files)},

@@ -48,7 +48,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
-           "dk_replay_kernel_stats", "dk_replay_free"]
+           "dk_replay_kernel_stats", "dk_replay_free", "dk_parquet_open_rg", "dk_parquet_row_groups",
+           "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits"]
 
 
 def lib(build_if_missing=True):
@@ -67,6 +68,11 @@ def lib(build_if_missing=True):
         "dk_engine_create": (C.c_int, [C.POINTER(dk_config), C.POINTER(P)]),
         "dk_engine_destroy": (None, [P]),
         "dk_parquet_open": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, C.POINTER(P)]),
+        "dk_parquet_open_rg": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, P, P,
+                                         C.POINTER(P)]),
+        "dk_parquet_row_groups": (C.c_int, [C.c_char_p, C.POINTER(I64), I32, C.POINTER(I32)]),
+        "dk_parquet_row_offset": (I64, [P, I32]),
+        "dk_replay_ckpt_selection_bits": (C.c_int, [P, I32, P, I64, I32]),
         "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),
         "dk_parquet_num_rows": (I64, [P, I32]),
         "dk_parquet_column": (C.c_int, [P, I32, I32, C.POINTER(dk_column)]),

@@ -21,6 +21,7 @@ namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const SnapCtx&, int, int, const int2*, int, hipStream_t);
 void snap_stats(unsigned long long*);
+void launch_pack_bits(const uint8_t*, long long, uint8_t*, hipStream_t);
 void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
@@ -134,7 +135,9 @@ struct FileM {
   std::vector<uint8_t> footer;            // the FileMetaData bytes
   std::vector<uint8_t> bytes;             // packed column-chunk / offset-index bytes
   std::vector<Span> spans;
-  int64_t num_rows = 0;
+  int64_t num_rows = 0;                   // rows of the selected row groups
+  int32_t rg_lo = 0, rg_hi = -1;          // selected row groups [rg_lo, rg_hi) (-1: to the end)
+  int64_t row0 = 0;                       // file row index of the first selected row
   std::vector<SchemaEl> schema;
   std::vector<LeafM> leaves;
   std::vector<RowGroupM> rgs;
@@ -793,8 +796,37 @@ static int prepare(dk_parquet* p) {
   return 0;
 }
 
+// Select row groups [lo, hi) of a parsed file (hi < 0: to the end): the file then reads as just
+// those rows (num_rows, row0) -- a shard of a checkpoint part, or row-group pruning.
+static int select_row_groups(FileM& f, int32_t lo, int32_t hi) {
+  const int32_t n = (int32_t)f.rgs.size();
+  if (hi < 0) hi = n;
+  if (lo < 0 || lo > hi || hi > n) return fail("Error reading Parquet file: " + f.path + " (row groups out of range)");
+  f.rg_lo = lo; f.rg_hi = hi;
+  f.row0 = 0; f.num_rows = 0;
+  for (int32_t g = 0; g < n; g++) {
+    if (g < lo) f.row0 += f.rgs[g].num_rows;
+    else if (g < hi) f.num_rows += f.rgs[g].num_rows;
+  }
+  return 0;
+}
+
+extern "C" int dk_parquet_row_groups(const char* path, int64_t* rows, int32_t cap, int32_t* n) {
+  FileM f;
+  f.path = path ? path : "";
+  if (read_footer(f) || parse_footer(f)) return 1;
+  *n = (int32_t)f.rgs.size();
+  for (int32_t g = 0; g < *n && g < cap; g++) rows[g] = f.rgs[g].num_rows;
+  return 0;
+}
+
 extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                                int32_t n_leaves, dk_parquet** out) {
+  return dk_parquet_open_rg(e, paths, n_files, leaves, n_leaves, nullptr, nullptr, out);
+}
+
+extern "C" int dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                                  int32_t n_leaves, const int32_t* rg_lo, const int32_t* rg_hi, dk_parquet** out) {
   if (!e) return fail("null engine");
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_parquet> p(new dk_parquet());
@@ -810,13 +842,14 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
     FileM& f = p->files[fi];
     f.path = paths[fi];
     if (read_footer(f) || parse_footer(f)) return 1;
+    if (select_row_groups(f, rg_lo ? rg_lo[fi] : 0, rg_hi ? rg_hi[fi] : -1)) return 1;
     {   // projection: only the chunks (and offset indexes) of the requested leaves travel to HBM
       std::vector<Span> want;
       for (int li = 0; li < n_leaves; li++) {
         int idx = leaf_index(f, p->leaves[li]);
         if (idx < 0) continue;
-        for (const RowGroupM& rg : f.rgs) {
-          const ColMeta& m = rg.cols[idx];
+        for (int32_t g = f.rg_lo; g < f.rg_hi; g++) {
+          const ColMeta& m = f.rgs[g].cols[idx];
           want.push_back({chunk_start(m), m.total_compressed, 0});
           if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= f.size) want.push_back({m.oi_off, m.oi_len, 0});
         }
@@ -840,7 +873,7 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
       int colid = (int)p->h_cols.size();
       // chunks and pages in row-group order; data pages of a column stay contiguous
       std::vector<DPage> dicts;
-      for (size_t g = 0; g < f.rgs.size(); g++) {
+      for (int32_t g = f.rg_lo; g < f.rg_hi; g++) {
         const ColMeta& m = f.rgs[g].cols[idx];
         c.n_rows += f.rgs[g].num_rows;
         DChunk ck{};
@@ -912,6 +945,11 @@ extern "C" int dk_parquet_sync(dk_parquet* p) {
 extern "C" int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file) {
   if (!p || file < 0 || file >= (int)p->files.size()) return -1;
   return p->files[file].num_rows;
+}
+
+extern "C" int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file) {
+  if (!p || file < 0 || file >= (int)p->files.size()) return -1;
+  return p->files[file].row0;
 }
 
 extern "C" int dk_parquet_traffic(dk_parquet* p, int64_t* r, int64_t* w) {
@@ -1930,6 +1968,25 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
   if (n != r->ck->files[file].num_rows) return fail("bad selection size");
   if (r->probe[file].n_rows == 0) { memset(out, 0, n); return 0; }
   HIPOK(hipMemcpy(out, r->d_csel[file]->p, n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+extern "C" int dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* dst, int64_t n, int32_t dst_on_device) {
+  if (!r->have_result) return fail("dk_replay_ckpt_selection_bits: no result (run + sync first)");
+  if (!r->ck || file < 0 || file >= (int)r->d_csel.size()) return fail("bad checkpoint file index");
+  if (n != r->ck->files[file].num_rows) return fail("bad selection size");
+  const int64_t nb = (n + 7) / 8;
+  hipStream_t s = r->eng->stream;
+  if (dst_on_device) {
+    launch_pack_bits(r->d_csel[file]->as<uint8_t>(), n, (uint8_t*)dst, s);
+    HIPOK(hipStreamSynchronize(s));
+    return 0;
+  }
+  DBuf tmp;
+  if (tmp.alloc(nb + 16)) return 1;
+  launch_pack_bits(r->d_csel[file]->as<uint8_t>(), n, tmp.as<uint8_t>(), s);
+  HIPOK(hipMemcpyAsync(dst, tmp.p, nb, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
   return 0;
 }
 

@@ -3264,4 +3264,20 @@ void launch_first_row(const uint8_t* row_def, long long n, int min_def, unsigned
   hipLaunchKernelGGL(k_first_row, dim3(grid), dim3(256), 0, s, row_def, n, min_def, out);
 }
 
+// Selection bytes -> bits (LSB first within a byte, numpy.packbits(bitorder="little")): one lane per
+// output byte; the multi-GPU merge moves these bitmaps instead of rows (delta_amd/shard.py).
+__global__ void k_pack_bits(const uint8_t* __restrict__ sel, long long n, uint8_t* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i * 8 >= n) return;
+  uint32_t b = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (i * 8 + k < n && sel[i * 8 + k]) b |= 1u << k;
+  out[i] = (uint8_t)b;
+}
+void launch_pack_bits(const uint8_t* sel, long long n, uint8_t* out, hipStream_t s) {
+  const long long nb = (n + 7) / 8;
+  if (nb > 0) hipLaunchKernelGGL(k_pack_bits, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, sel, n, out);
+}
+
 }  // namespace dk

@@ -83,16 +83,34 @@ class GpuEngine:
         return ParquetSet(self, paths, leaves)
 
 
+def row_group_rows(path):
+    """Row counts of a Parquet file's row groups (footer only)."""
+    cap = 4096
+    rows = (C.c_int64 * cap)()
+    n = C.c_int32()
+    check(lib().dk_parquet_row_groups(path.encode(), rows, cap, C.byref(n)))
+    if n.value > cap:
+        raise DkError("%s has more than %d row groups" % (path, cap))
+    return [int(rows[i]) for i in range(n.value)]
+
+
 class ParquetSet:
     """A set of Parquet files decoded on the GPU (one batch per file; batches in input order)."""
 
-    def __init__(self, engine: GpuEngine, paths, leaves):
+    def __init__(self, engine: GpuEngine, paths, leaves, row_groups=None):
+        """row_groups: optional [(first, end)] row-group range per file (dk_parquet_open_rg)."""
         self.engine = engine
         self.paths = list(paths)
         self.leaves = list(leaves)
         self._h = C.c_void_p()
-        check(lib().dk_parquet_open(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
-                                    len(self.leaves), C.byref(self._h)))
+        if row_groups is None:
+            check(lib().dk_parquet_open(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
+                                        len(self.leaves), C.byref(self._h)))
+        else:
+            lo = (C.c_int32 * max(1, len(row_groups)))(*[a for a, _ in row_groups])
+            hi = (C.c_int32 * max(1, len(row_groups)))(*[b for _, b in row_groups])
+            check(lib().dk_parquet_open_rg(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
+                                           len(self.leaves), lo, hi, C.byref(self._h)))
 
     def decode(self):
         check(lib().dk_parquet_decode(self._h))
@@ -101,6 +119,10 @@ class ParquetSet:
 
     def num_rows(self, file_idx):
         return lib().dk_parquet_num_rows(self._h, file_idx)
+
+    def row_offset(self, file_idx):
+        """File row index of this set's first row of the file (non-zero for a row-group shard)."""
+        return lib().dk_parquet_row_offset(self._h, file_idx)
 
     def column(self, file_idx, leaf) -> Column:
         c = dk_column()
@@ -605,6 +627,7 @@ class FilteredColumnarBatch:
     selection: np.ndarray | None
     source: str = ""
     file_index: int = -1          # replay-order checkpoint file index; -1 = commit tail
+    row_offset: int = 0           # file row of this batch's first row (row-group shards)
 
     def selected_rows(self):
         if self.selection is None:
@@ -666,14 +689,18 @@ class GpuScan:
         commits = list(reversed(seg.deltas))
         self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
         all_files = self.snapshot._checkpoint_files(engine)
+        ranges = None
         if self.shard:
-            from .shard import owned_files
-            self.ckpt_index = owned_files(len(all_files), *self.shard)
+            # this rank's contiguous run of checkpoint row groups (delta_amd/shard.py)
+            from .shard import plan_units
+            units = plan_units([row_group_rows(f) for f in all_files], *self.shard)
+            self.ckpt_index = [f for f, _, _ in units]
+            ranges = [(a, b) for _, a, b in units]
         else:
             self.ckpt_index = list(range(len(all_files)))
         self.ckpt_files = [all_files[i] for i in self.ckpt_index]
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
-        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves) if self.ckpt_files else None
+        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, ranges) if self.ckpt_files else None
         self._rh = C.c_void_p()
         check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
                                      C.byref(self._rh)))
@@ -706,6 +733,20 @@ class GpuScan:
         self.tail_metrics = ScanMetrics(*[int(x) for x in tail])
         self.ckpt_metrics = ScanMetrics(*[int(x) for x in ck])
 
+    def selection_bits(self, fi, device=False):
+        """Packed selection of checkpoint file fi of this scan (LSB first): a numpy array, or a
+        torch uint8 tensor on this GPU filled by the device (for RCCL) when device=True."""
+        n = self.ckpt.num_rows(fi)
+        nb = (n + 7) // 8
+        if device:
+            import torch
+            t = torch.empty(max(1, nb), dtype=torch.uint8, device="cuda")
+            check(lib().dk_replay_ckpt_selection_bits(self._rh, fi, C.c_void_p(t.data_ptr()), n, 1))
+            return t[:nb]
+        out = np.zeros(max(1, nb), dtype=np.uint8)
+        check(lib().dk_replay_ckpt_selection_bits(self._rh, fi, out.ctypes.data, n, 0))
+        return out[:nb]
+
     def kernel_stats(self):
         out = {}
         for i in range(24):
@@ -737,7 +778,8 @@ class GpuScan:
             sel = np.zeros(n, dtype=np.uint8)
             check(lib().dk_replay_ckpt_selection(self._rh, fi, sel.ctypes.data, n))
             cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf))
-            yield FilteredColumnarBatch(cols, root, int(n), sel.view(bool), path, self.ckpt_index[fi])
+            yield FilteredColumnarBatch(cols, root, int(n), sel.view(bool), path, self.ckpt_index[fi],
+                                        int(self.ckpt.row_offset(fi)))
 
     def close(self):
         if getattr(self, "_rh", None):

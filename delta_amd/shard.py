@@ -6,12 +6,18 @@ inserted into the "already returned" set and checkpoint removes are ignored
 Checkpoint files (multi-part parts, V2 manifest + sidecars) therefore shard across ranks with no
 data-path exchange:
 
-* rank r owns the checkpoint files whose replay-order index i has i % world == r
-  (``owned_files``; replay order is LogSegment.allLogFilesReversed, LogSegment.java:166-178);
+* the checkpoint's row groups, in replay order (LogSegment.allLogFilesReversed,
+  LogSegment.java:166-178; rows in file order), are cut into ``world`` contiguous runs of about
+  equal row counts (``plan_units``), so single-part and uneven multi-part checkpoints spread over
+  every rank; a rank reads each of its files as the row-group range it owns
+  (dk_parquet_open_rg). ``owned_files`` (whole files round-robin) is the coarser alternative;
 * every rank parses the (small) commit tail and builds its key table on its own GPU;
-* results merge on one rank (``gather`` over torch.distributed, then ``merge``): the ScanMetrics
-  counters are the tail part (taken once, from rank 0) plus the sum of the checkpoint parts, and the
-  selected rows are emitted tail first, then checkpoint files in replay order.
+* results merge on one rank: ``gather_selections`` all-gathers each rank's ScanMetrics counters and
+  its selection bitmaps, packed on the GPU (dk_replay_ckpt_selection_bits), over RCCL (or gloo);
+  the row data stays on the GPU that decoded it. The counters are the tail part (taken once, from
+  rank 0) plus the sum of the checkpoint parts; selections come out tail first, then checkpoint
+  rows in replay order. ``gather`` / ``merge`` do the same for whole payloads
+  (host objects, used by tests).
 
 The same merge serves GPU ranks (payloads are ``FilteredColumnarBatch``es) and the CPU tests
 (payloads are oracle rows); it never looks inside a payload.
@@ -28,13 +34,34 @@ def owned_files(n_files: int, world: int, rank: int) -> list:
     return [i for i in range(n_files) if i % world == rank]
 
 
+def plan_units(rg_rows, world: int, rank: int) -> list:
+    """This rank's share of the checkpoint: [(file index, first row group, end row group)] over
+    `rg_rows` (row counts per row group, per file in replay order). The row groups form one
+    sequence cut into `world` contiguous runs at the multiples of total / world."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad shard (world=%r, rank=%r)" % (world, rank))
+    seq = [(f, g, n) for f, rows in enumerate(rg_rows) for g, n in enumerate(rows)]
+    total = sum(n for _, _, n in seq) or 1
+    mine, acc = [], 0
+    for f, g, n in seq:
+        # a row group belongs to the rank whose share of the row sequence holds its middle row
+        owner = min(world - 1, int((acc + n / 2.0) * world / total))
+        if owner == rank:
+            if mine and mine[-1][0] == f and mine[-1][2] == g:
+                mine[-1] = (f, mine[-1][1], g + 1)
+            else:
+                mine.append((f, g, g + 1))
+        acc += n
+    return mine
+
+
 @dataclass
 class ShardOutput:
     rank: int
     tail_counters: tuple                         # commit-tail part of the five ScanMetrics counters
     ckpt_counters: tuple                         # this rank's checkpoint part
     tail: object = None                          # commit-tail payload (used from rank 0 only)
-    files: dict = field(default_factory=dict)    # replay-order checkpoint file index -> payload
+    files: dict = field(default_factory=dict)    # (replay-order file index, first row) -> payload
 
 
 def merge(outputs) -> tuple:
@@ -48,11 +75,62 @@ def merge(outputs) -> tuple:
     files = {}
     for o in outs:
         for i, payload in o.files.items():
-            if i in files:
-                raise ValueError("checkpoint file %d produced by two ranks" % i)
-            files[i] = payload
+            key = i if isinstance(i, tuple) else (i, 0)
+            if key in files:
+                raise ValueError("checkpoint rows %r produced by two ranks" % (key,))
+            files[key] = payload
     payloads = ([outs[0].tail] if outs[0].tail is not None else []) + [files[i] for i in sorted(files)]
     return tuple(counters), payloads
+
+
+def gather_selections(units, tail_counters, ckpt_counters, group=None, device=None):
+    """All ranks' checkpoint selection bitmaps and counters on every rank, in two all-gathers
+    (sizes, then one padded int64 header + one padded byte tensor per rank) -- RCCL when the
+    tensors live on the GPU (backend "nccl"), gloo on the CPU.
+
+    units: [(replay-order file index, first row, rows, packed bits (uint8 array or tensor))].
+    Returns (counters, [(file index, first row, rows, bits numpy array)] in replay order)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    world = dist.get_world_size(group)
+    head = [len(units)] + list(tail_counters) + list(ckpt_counters)
+    for f, r0, n, _ in units:
+        head += [f, r0, n]
+    blobs = [b if isinstance(b, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(b, dtype=np.uint8))
+             for _, _, _, b in units]
+    bits = torch.cat([b.reshape(-1).to(dev) for b in blobs]) if blobs else torch.zeros(0, dtype=torch.uint8, device=dev)
+    sizes = torch.tensor([len(head), bits.numel()], dtype=torch.int64, device=dev)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    hmax = max(int(s[0]) for s in all_sizes)
+    bmax = max(1, max(int(s[1]) for s in all_sizes))
+    h = torch.zeros(hmax, dtype=torch.int64, device=dev)
+    h[:len(head)] = torch.tensor(head, dtype=torch.int64, device=dev)
+    b = torch.zeros(bmax, dtype=torch.uint8, device=dev)
+    b[:bits.numel()] = bits
+    hs = [torch.zeros_like(h) for _ in range(world)]
+    bs = [torch.zeros_like(b) for _ in range(world)]
+    dist.all_gather(hs, h, group=group)
+    dist.all_gather(bs, b, group=group)
+    counters = None
+    sels = []
+    for rk in range(world):
+        hv = hs[rk].cpu().numpy()
+        bv = bs[rk].cpu().numpy()
+        nu = int(hv[0])
+        tail, ck = hv[1:6], hv[6:11]
+        counters = [int(x) for x in tail] if counters is None else counters
+        counters = [a + int(c) for a, c in zip(counters, ck)]
+        pos = 0
+        for u in range(nu):
+            f, r0, n = (int(x) for x in hv[11 + 3 * u: 14 + 3 * u])
+            nb = (n + 7) // 8
+            sels.append((f, r0, n, bv[pos:pos + nb].copy()))
+            pos += nb
+    sels.sort(key=lambda x: (x[0], x[1]))
+    return tuple(counters), sels
 
 
 def gather(output: ShardOutput, group=None):
@@ -66,7 +144,7 @@ def gather(output: ShardOutput, group=None):
 
 def gpu_shard_scan(engine, snapshot, world: int, rank: int, with_stats: bool = False):
     """Run this rank's share of getScanFiles on its GPU. Returns (ShardOutput whose payloads are
-    FilteredColumnarBatches with host-resident columns, the scan to close() when done)."""
+    FilteredColumnarBatches with columns fetched on demand, the scan to close() when done)."""
     scan = snapshot.getScanBuilder().withStats(with_stats).withShard(world, rank).build()
     batches = list(scan.getScanFiles(engine))
     out = ShardOutput(rank, scan.tail_metrics.as_tuple(), scan.ckpt_metrics.as_tuple())
@@ -74,5 +152,16 @@ def gpu_shard_scan(engine, snapshot, world: int, rank: int, with_stats: bool = F
         if b.file_index < 0:
             out.tail = b
         else:
-            out.files[b.file_index] = b
+            out.files[(b.file_index, b.row_offset)] = b
     return out, scan
+
+
+def scan_units(scan, device_bits=False):
+    """This rank's (file index, first row, rows, packed selection bits) after scan.run() + sync():
+    bits packed on the GPU, into a torch device tensor when device_bits (for RCCL), else host."""
+    import numpy as np
+    units = []
+    for fi in range(len(scan.ckpt_files or [])):
+        n = scan.ckpt.num_rows(fi)
+        units.append((scan.ckpt_index[fi], scan.ckpt.row_offset(fi), n, scan.selection_bits(fi, device=device_bits)))
+    return units

@@ -73,6 +73,15 @@ void dk_engine_destroy(dk_engine* e);
  * projected column chunks (and their offset indexes) are read from the file and copied to HBM. */
 int  dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
                      const char* const* leaves, int32_t n_leaves, dk_parquet** out);
+/* The same over row groups [rg_lo[i], rg_hi[i]) of file i (rg_hi < 0: to the end; NULL arrays: all
+ * row groups): the file then reads as just those rows. Used to shard one checkpoint part over
+ * several GPUs and for row-group pruning (ParquetFileReader.java:118-134 filters row groups). */
+int  dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files,
+                        const char* const* leaves, int32_t n_leaves, const int32_t* rg_lo,
+                        const int32_t* rg_hi, dk_parquet** out);
+/* Row counts of a file's row groups from its footer (no device work); *n = number of groups. */
+int  dk_parquet_row_groups(const char* path, int64_t* rows, int32_t cap, int32_t* n);
+int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file);   /* file row of the first selected row */
 int  dk_parquet_decode(dk_parquet* p);                 /* async on the engine stream */
 int  dk_parquet_sync(dk_parquet* p);
 int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file);
@@ -161,6 +170,9 @@ int  dk_replay_counters(dk_replay* r, int64_t out[5]);
 int  dk_replay_counters_split(dk_replay* r, int64_t tail[5], int64_t ckpt[5]);
 int  dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n);
 int  dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out, int64_t n);
+/* the same selection packed into bits (LSB first) -- ceil(n / 8) bytes at dst, a device pointer
+ * (the multi-GPU merge hands it to RCCL) when dst_on_device, else host memory */
+int  dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* dst, int64_t n, int32_t dst_on_device);
 /* per-kernel average device time (us) over recorded runs (DK_FLAG_TIMING); names via index */
 int  dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count);
 void dk_replay_free(dk_replay* r);

@@ -1,0 +1,42 @@
+"""One rank of tests/test_shard.py::test_gpu_two_processes_gloo (not a test module): scan this
+rank's row-group shard on the GPU, gather counters + selection bitmaps over gloo, and have rank 0
+write them to a JSON file. Usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR/PORT=.. python shard_worker.py TABLE OUT"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch.distributed as dist
+    from delta_amd import kernel as K
+    from delta_amd import shard
+    table, out = sys.argv[1], sys.argv[2]
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    eng = K.GpuEngine()
+    snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
+    scan = snap.getScanBuilder().withShard(world, rank).build()
+    scan.prepare(eng)
+    scan.run()
+    scan.sync()
+    counters, sels = shard.gather_selections(shard.scan_units(scan), scan.tail_metrics.as_tuple(),
+                                             scan.ckpt_metrics.as_tuple())
+    if rank == 0:
+        files = {}
+        for f, r0, n, bits in sels:
+            files.setdefault(f, []).append(np.unpackbits(bits, bitorder="little")[:n])
+        with open(out, "w") as fh:
+            json.dump({"counters": list(counters),
+                       "selection": {str(f): np.concatenate(v).astype(int).tolist() for f, v in files.items()}}, fh)
+    scan.close()
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -139,3 +139,129 @@ def test_gpu_shards_merge_to_oracle(tmp_path, world, v2):
     for sc in scans:
         sc.close()
     eng.close()
+
+
+# ---- row-group sharding + bitmap gather (the product's plan_units / gather_selections) ----
+
+def test_plan_units_cover_every_row_group_once():
+    for rg in ([[100] * 10], [[1000, 1000], [1000], [500, 500, 500]], [[5]], [[1] * 3, [1] * 2], []):
+        for world in (1, 2, 3, 8):
+            units = [shard.plan_units(rg, world, r) for r in range(world)]
+            flat = sorted((f, g) for u in units for (f, a, b) in u for g in range(a, b))
+            assert flat == [(f, g) for f, rows in enumerate(rg) for g in range(len(rows))]
+            for u in units:                      # contiguous runs, in replay order
+                assert u == sorted(u)
+    # a single-part checkpoint with several row groups spreads over the ranks
+    assert all(shard.plan_units([[100] * 8], 4, r) for r in range(4))
+
+
+def _oracle_units(table, world, rank):
+    """This rank's units with selections from the oracle's full replay (bits packed LSB first)."""
+    from delta_amd import kernel as K
+    from oracle import ref
+    r = ref.replay(table)
+    files = [b.path for b in r.checkpoint]
+    units = shard.plan_units([K.row_group_rows(p) for p in files], world, rank)
+    rgs = [K.row_group_rows(p) for p in files]
+    out = []
+    for f, a, b in units:
+        r0 = sum(rgs[f][:a])
+        n = sum(rgs[f][a:b])
+        sel = r.checkpoint[f].selected[r0:r0 + n].astype(bool)
+        out.append((f, r0, n, np.packbits(sel, bitorder="little")))
+    # the checkpoint part of the counters travels from rank 0 (per-unit splits are the GPU test's)
+    ck = r.ckpt_counters.as_tuple() if rank == 0 else (0, 0, 0, 0, 0)
+    return r, out, r.tail_counters.as_tuple(), ck
+
+
+def _gloo_bits_worker(rank, world, port, table, out_path):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        full, units, tail, ck = _oracle_units(table, world, rank)
+        counters, sels = shard.gather_selections(units, tail, ck)
+        if rank == 0:
+            ok = counters == full.counters.as_tuple()
+            for b in full.checkpoint:                 # reassemble each file's selection from the units
+                parts = [s for s in sels if s[0] == b.file_index]
+                bits = np.concatenate([np.unpackbits(s[3], bitorder="little")[:s[2]] for s in parts])
+                ok = ok and np.array_equal(bits.astype(bool), b.selected.astype(bool))
+            with open(out_path, "w") as f:
+                f.write("ok %d" % len(sels) if ok else "MISMATCH")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_selection_bitmaps(tmp_path):
+    """gloo world 2: plan_units splits a single-part checkpoint by row groups and uneven parts by
+    rows; gather_selections reassembles the oracle's selection bits and counters on rank 0."""
+    import torch.multiprocessing as mp
+    for name, spec in (("single", dict(n_parts=1, row_group_size=1500)), ("uneven", dict(n_parts=3, row_group_size=2000))):
+        table = str(tmp_path / name)
+        synth.write_table(table, synth.TableSpec(n_adds=9_000, n_commits=6, dv_frac=0.1, **spec))
+        out = str(tmp_path / (name + ".txt"))
+        mp.spawn(_gloo_bits_worker, args=(2, _free_port(), table, out), nprocs=2, join=True)
+        with open(out) as f:
+            res = f.read()
+        assert res.startswith("ok"), (name, res)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,spec", [(3, dict(n_parts=1, row_group_size=2500)), (4, dict(n_parts=3, row_group_size=3000))])
+def test_gpu_row_group_shards(tmp_path, world, spec):
+    """Single-part and uneven multi-part checkpoints split by row groups over simulated ranks: the
+    merged rows equal the oracle's, and the bitmaps packed on the GPU equal the selections."""
+    from delta_amd import kernel as K
+    from oracle import ref
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=20_000, n_commits=8, dv_frac=0.2, **spec))
+    eng = K.GpuEngine()
+    outs, scans = [], []
+    for r in range(world):
+        snap = K.Table.forPath(eng, str(tmp_path)).getLatestSnapshot(eng)
+        o, sc = shard.gpu_shard_scan(eng, snap, world, r)
+        outs.append(o)
+        scans.append(sc)
+        for fi in range(len(sc.ckpt_files or [])):
+            bits = np.unpackbits(sc.selection_bits(fi), bitorder="little")[:sc.ckpt.num_rows(fi)]
+            sel = np.zeros(sc.ckpt.num_rows(fi), np.uint8)
+            from delta_amd._lib import lib
+            lib().dk_replay_ckpt_selection(sc._rh, fi, sel.ctypes.data, len(sel))
+            assert np.array_equal(bits.astype(bool), sel.astype(bool))
+    assert sum(1 for sc in scans if sc.ckpt_files) == world       # every rank got checkpoint rows
+    counters, batches = shard.merge(outs)
+    rows = [ref.canon_add_from_cols(b.data, int(i)) + (b.table_root,) for b in batches for i in b.selected_rows()]
+    full = ref.replay(str(tmp_path))
+    assert counters == full.counters.as_tuple()
+    assert rows == full.scan_files()
+    for sc in scans:
+        sc.close()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_two_processes_gloo(tmp_path):
+    """Two processes on the GPU, each scanning its row-group shard with the product, merge
+    counters and selection bitmaps with gather_selections over gloo; rank 0 checks the oracle."""
+    import json
+    import subprocess
+    import sys
+    from oracle import ref
+    table = str(tmp_path / "t")
+    synth.write_table(table, synth.TableSpec(n_adds=30_000, n_parts=3, row_group_size=4000, n_commits=8, dv_frac=0.1))
+    port = _free_port()
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "shard_worker.py")
+    out = str(tmp_path / "res.json")
+    procs = [subprocess.Popen([sys.executable, worker, table, out],
+                              env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                                       MASTER_PORT=str(port)))
+             for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    with open(out) as f:
+        res = json.load(f)
+    full = ref.replay(table)
+    assert tuple(res["counters"]) == full.counters.as_tuple()
+    for b in full.checkpoint:
+        bits = np.array(res["selection"][str(b.file_index)], dtype=bool)
+        assert np.array_equal(bits, b.selected.astype(bool))
