@@ -24,7 +24,7 @@ class dk_config(C.Structure):
 class dk_part_program(C.Structure):
     _fields_ = [("n_fields", C.c_int32), ("field_type", C.c_int32 * 8), ("name_off", C.c_int32 * 8),
                 ("name_len", C.c_int32 * 8), ("n_ops", C.c_int32), ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64),
-                ("lit", C.c_int64 * 64), ("pool", C.c_char * 1024)]
+                ("lit", C.c_int64 * 64), ("pool", C.c_char * 4096)]
 
 
 class dk_column(C.Structure):
@@ -37,7 +37,7 @@ class dk_column(C.Structure):
 
 class dk_skip_program(C.Structure):
     _fields_ = [("n_paths", C.c_int32), ("path_type", C.c_int32 * 8), ("path_depth", C.c_int32 * 8),
-                ("name_off", (C.c_int32 * 4) * 8), ("name_len", (C.c_int32 * 4) * 8), ("names", C.c_char * 512),
+                ("name_off", (C.c_int32 * 4) * 8), ("name_len", (C.c_int32 * 4) * 8), ("names", C.c_char * 4096),
                 ("n_ops", C.c_int32), ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64), ("lit", C.c_int64 * 64)]
 
 

@@ -154,9 +154,12 @@ enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8, E_STATS = 1
 
 // Data-skipping program (layout of dk_skip_program in include/dkgpu.h): the stats fields to
 // extract from each row's add.stats JSON and a postfix program over them (delta_amd/skipping.py).
-constexpr int SK_MAX_PATHS = 8, SK_MAX_DEPTH = 4, SK_MAX_OPS = 64, SK_NAMES = 512;
-enum : int32_t { SK_LONG = 0, SK_INT = 1, SK_SHORT = 2, SK_BYTE = 3, SK_DATE = 4, SK_STRING = 5, SK_TIMESTAMP = 6, SK_DECIMAL = 7, SK_TIMESTAMP_NTZ = 8 };
-enum : int32_t { OP_STAT = 0, OP_LIT = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_EQ = 6, OP_AND = 7, OP_OR = 8, OP_LIT_STR = 9, OP_TIMEADD = 10, OP_LIT_DEC = 11 };
+constexpr int SK_MAX_PATHS = 8, SK_MAX_DEPTH = 4, SK_MAX_OPS = 64, SK_NAMES = 4096;
+enum : int32_t { SK_LONG = 0, SK_INT = 1, SK_SHORT = 2, SK_BYTE = 3, SK_DATE = 4, SK_STRING = 5, SK_TIMESTAMP = 6, SK_DECIMAL = 7, SK_TIMESTAMP_NTZ = 8,
+                 SK_FLOAT = 9, SK_DOUBLE = 10 };
+enum : int32_t { OP_STAT = 0, OP_LIT = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_EQ = 6, OP_AND = 7, OP_OR = 8, OP_LIT_STR = 9, OP_TIMEADD = 10, OP_LIT_DEC = 11,
+                 OP_FCMP = 12 };
+enum : int32_t { FC_LT = 0, FC_LE = 1, FC_GT = 2, FC_GE = 3, FC_ALL = 4, FC_NONE = 5 };
 struct DSkipProg {
   int32_t n_paths;
   int32_t path_type[SK_MAX_PATHS];
@@ -173,11 +176,12 @@ struct DSkipProg {
 // Partition-pruning program (layout of dk_part_program in include/dkgpu.h; delta_amd/partitions.py):
 // the partition columns it reads (physical names, looked up in each row's partitionValues map) and
 // a postfix program over their deserialized values.
-constexpr int PP_MAX_FIELDS = 8, PP_MAX_OPS = 64, PP_POOL = 1024;
-enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING = 4, PT_DATE = 5, PT_DECIMAL = 6 };
+constexpr int PP_MAX_FIELDS = 8, PP_MAX_OPS = 64, PP_POOL = 4096;
+enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING = 4, PT_DATE = 5, PT_DECIMAL = 6,
+                 PT_BOOL = 7, PT_F32 = 8, PT_F64 = 9, PT_TIMESTAMP = 10 };
 enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, PO_LT = 4, PO_LE = 5, PO_GT = 6,
                  PO_GE = 7, PO_EQ = 8, PO_NSEQ = 9, PO_ISNULL = 10, PO_ISNOTNULL = 11, PO_NOT = 12, PO_AND = 13,
-                 PO_OR = 14, PO_LIT_DEC = 15 };
+                 PO_OR = 14, PO_LIT_DEC = 15, PO_FCMP = 16 };
 struct DPartProg {
   int32_t n_fields;
   int32_t field_type[PP_MAX_FIELDS];

@@ -38,8 +38,8 @@ void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
 void launch_first_row(const uint8_t*, long long, int, unsigned long long*, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
-void launch_stats_eval(const StatsRows&, const DSkipProg&, uint8_t*, DState*, hipStream_t);
-void launch_part_eval(const MapRows&, const DPartProg&, uint8_t*, DState*, hipStream_t);
+void launch_stats_eval(const StatsRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
+void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipStream_t);
 void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
@@ -1577,6 +1577,7 @@ struct dk_replay {
   // data skipping (dk_replay_set_skipping): program + the tail's stats strings per action
   bool has_skip = false;
   DSkipProg skip{};
+  DBuf d_skip, d_part;                  // device copies of the programs
   DBuf d_tstats_chars, d_tstats_off, d_tstats_len;
   std::vector<StatsRows> ck_stats;      // per checkpoint file (n = 0: no stats column)
   // partition pruning (dk_replay_set_partition_filter): program + partitionValues maps
@@ -1764,29 +1765,57 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   if (P.n_paths < 0 || P.n_paths > SK_MAX_PATHS || P.n_ops <= 0 || P.n_ops > SK_MAX_OPS)
     return fail("dk_replay_set_skipping: bad program size");
   for (int p = 0; p < P.n_paths; p++) {
-    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_TIMESTAMP_NTZ)
+    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DOUBLE)
       return fail("dk_replay_set_skipping: bad stats path");
     for (int d = 0; d < P.path_depth[p]; d++)
       if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
         return fail("dk_replay_set_skipping: bad stats path name");
   }
   int depth = 0;
+  bool fstat[SK_MAX_OPS + 1] = {false};       // stack slot holds a float / double stats value
+  bool nlit[SK_MAX_OPS + 1] = {false};        // stack slot holds a null literal
   for (int k = 0; k < P.n_ops; k++) {
     const int op = P.op[k];
-    if (op == OP_STAT) { if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail("dk_replay_set_skipping: bad stat"); depth++; }
-    else if (op == OP_LIT) depth++;
+    if (op == OP_STAT) {
+      if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail("dk_replay_set_skipping: bad stat");
+      const int t = P.path_type[P.arg[k]];
+      fstat[depth] = t == SK_FLOAT || t == SK_DOUBLE;
+      nlit[depth] = false;
+      depth++;
+    }
+    else if (op == OP_FCMP) {                   // only on a float / double stat, threshold in names
+      const long long off = P.lit[k] & 0xffffffffll, len = P.lit[k] >> 32;
+      if (depth < 1 || !fstat[depth - 1]) return fail("dk_replay_set_skipping: FCMP needs a float stat");
+      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len > SK_NAMES) return fail("dk_replay_set_skipping: bad FCMP");
+      fstat[depth - 1] = false;
+      nlit[depth - 1] = false;
+    }
+    else if (op == OP_LIT) { fstat[depth] = false; nlit[depth] = P.arg[k] != 0; depth++; }
     else if (op == OP_TIMEADD) { if (depth < 1) return fail("dk_replay_set_skipping: stack underflow"); }
     else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
       if (P.arg[k] < 0 || P.lit[k] < 0 || P.lit[k] + P.arg[k] > SK_NAMES) return fail("dk_replay_set_skipping: bad string literal");
+      fstat[depth] = false;
+      nlit[depth] = false;
       depth++;
     }
-    else if (op >= OP_LT && op <= OP_OR) { if (depth < 2) return fail("dk_replay_set_skipping: stack underflow"); depth--; }
+    else if (op >= OP_LT && op <= OP_OR) {
+      if (depth < 2) return fail("dk_replay_set_skipping: stack underflow");
+      // a float stat compares only through FCMP, or with a null literal (the result is null)
+      if ((fstat[depth - 1] && !nlit[depth - 2]) || (fstat[depth - 2] && !nlit[depth - 1]))
+        return fail("dk_replay_set_skipping: a float stat compares only through FCMP");
+      depth--;
+      fstat[depth - 1] = false;
+      nlit[depth - 1] = false;
+    }
     else return fail("dk_replay_set_skipping: bad opcode");
     if (depth > 16) return fail("dk_replay_set_skipping: program too deep");
   }
   if (depth != 1) return fail("dk_replay_set_skipping: program must leave one value");
   if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
   r->skip = P;
+  if (!r->d_skip.p && r->d_skip.alloc(sizeof(DSkipProg))) return -1;
+  if (hipMemcpy(r->d_skip.p, &r->skip, sizeof(DSkipProg), hipMemcpyHostToDevice) != hipSuccess)
+    return fail("dk_replay_set_skipping: copy failed");
   r->has_skip = true;
   return 0;
 }
@@ -1800,22 +1829,44 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
   if (P.n_fields < 0 || P.n_fields > PP_MAX_FIELDS || P.n_ops <= 0 || P.n_ops > PP_MAX_OPS)
     return fail("dk_replay_set_partition_filter: bad program size");
   for (int f = 0; f < P.n_fields; f++)
-    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_DECIMAL || P.name_off[f] < 0 || P.name_len[f] < 0 ||
+    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_TIMESTAMP || P.name_off[f] < 0 || P.name_len[f] < 0 ||
         P.name_off[f] + P.name_len[f] > PP_POOL)
       return fail("dk_replay_set_partition_filter: bad field");
   int depth = 0;
+  bool ffield[PP_MAX_OPS + 1] = {false};      // stack slot holds a float / double field
+  bool pnull[PP_MAX_OPS + 1] = {false};       // stack slot holds a null literal
   for (int k = 0; k < P.n_ops; k++) {
     const int op = P.op[k];
-    if (op == PO_FIELD) { if (P.arg[k] < 0 || P.arg[k] >= P.n_fields) return fail("dk_replay_set_partition_filter: bad field ref"); depth++; }
-    else if (op == PO_LIT_INT || op == PO_LIT_NULL) depth++;
+    if (op == PO_FIELD) {
+      if (P.arg[k] < 0 || P.arg[k] >= P.n_fields) return fail("dk_replay_set_partition_filter: bad field ref");
+      ffield[depth] = P.field_type[P.arg[k]] == PT_F32 || P.field_type[P.arg[k]] == PT_F64;
+      pnull[depth] = false;
+      depth++;
+    }
+    else if (op == PO_LIT_INT || op == PO_LIT_NULL) { ffield[depth] = false; pnull[depth] = op == PO_LIT_NULL; depth++; }
     else if (op == PO_LIT_STR || op == PO_LIT_DEC) {
       if (P.lit[k] < 0 || P.arg[k] < 0 || P.lit[k] + P.arg[k] > PP_POOL) return fail("dk_replay_set_partition_filter: bad literal");
+      ffield[depth] = false;
+      pnull[depth] = false;
       depth++;
+    } else if (op == PO_FCMP) {
+      const long long off = P.lit[k] & 0xffffffffll, len = P.lit[k] >> 32;
+      if (depth < 1 || !ffield[depth - 1]) return fail("dk_replay_set_partition_filter: FCMP needs a float field");
+      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len > PP_POOL) return fail("dk_replay_set_partition_filter: bad FCMP");
+      ffield[depth - 1] = false;
+      pnull[depth - 1] = false;
     } else if ((op >= PO_LT && op <= PO_NSEQ) || op == PO_AND || op == PO_OR) {
       if (depth < 2) return fail("dk_replay_set_partition_filter: stack underflow");
+      if ((op >= PO_LT && op <= PO_NSEQ) &&
+          ((ffield[depth - 1] && !pnull[depth - 2]) || (ffield[depth - 2] && !pnull[depth - 1])))
+        return fail("dk_replay_set_partition_filter: a float field compares only through FCMP");
       depth--;
+      ffield[depth - 1] = false;
+      pnull[depth - 1] = false;
     } else if (op == PO_ISNULL || op == PO_ISNOTNULL || op == PO_NOT) {
       if (depth < 1) return fail("dk_replay_set_partition_filter: stack underflow");
+      ffield[depth - 1] = false;
+      pnull[depth - 1] = false;
     } else {
       return fail("dk_replay_set_partition_filter: bad opcode");
     }
@@ -1823,6 +1874,9 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
   }
   if (depth != 1) return fail("dk_replay_set_partition_filter: program must leave one value");
   r->part = P;
+  if (!r->d_part.p && r->d_part.alloc(sizeof(DPartProg))) return -1;
+  if (hipMemcpy(r->d_part.p, &r->part, sizeof(DPartProg), hipMemcpyHostToDevice) != hipSuccess)
+    return fail("dk_replay_set_partition_filter: copy failed");
   r->has_part = true;
   return 0;
 }
@@ -1846,14 +1900,14 @@ static int replay_launch(dk_replay* r) {
   { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->d_jsel.as<uint8_t>(), st, s); }
   if (r->has_part && na) {                 // partition pruning on the tail's adds (before skipping)
     KTimer::Scope sc(&T, 18, s);
-    launch_part_eval(r->tail_maps, r->part, r->d_jsel.as<uint8_t>(), st, s);
+    launch_part_eval(r->tail_maps, r->d_part.as<DPartProg>(), r->d_jsel.as<uint8_t>(), st, s);
   }
   if (r->has_skip && na) {                 // data skipping on the tail's selected adds
     KTimer::Scope sc(&T, 17, s);
     StatsRows R{};
     R.n = na; R.soff = r->d_tstats_off.as<int64_t>(); R.slen = r->d_tstats_len.as<int32_t>();
     R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
-    launch_stats_eval(R, r->skip, r->d_jsel.as<uint8_t>(), st, s);
+    launch_stats_eval(R, r->d_skip.as<DSkipProg>(), r->d_jsel.as<uint8_t>(), st, s);
   }
   if (r->ck) {
     dk_parquet* p = r->ck;
@@ -1872,12 +1926,12 @@ static int replay_launch(dk_replay* r) {
     if (r->has_part)                        // partition pruning on the checkpoint files' rows
       for (size_t fi = 0; fi < r->ck_maps.size(); fi++) {
         KTimer::Scope sc(&T, 18, s);
-        launch_part_eval(r->ck_maps[fi], r->part, r->d_csel[fi]->as<uint8_t>(), st, s);
+        launch_part_eval(r->ck_maps[fi], r->d_part.as<DPartProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
       }
     if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
       for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
         KTimer::Scope sc(&T, 17, s);
-        launch_stats_eval(r->ck_stats[fi], r->skip, r->d_csel[fi]->as<uint8_t>(), st, s);
+        launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
     }
   }
   return 0;

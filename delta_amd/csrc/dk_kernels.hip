@@ -2323,144 +2323,6 @@ __device__ bool js_timestamp(const uint8_t* s, int32_t a, int32_t b, long long* 
   return true;
 }
 
-// extract the program's stats fields from one JSON object; returns false on a decode error
-__device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long long* val, uint32_t* set) {
-  uint32_t mstack[JS_MAXD];
-  uint8_t is_obj[JS_MAXD];
-  uint32_t leafmask[SK_MAX_DEPTH + 2];
-  for (int d = 0; d < SK_MAX_DEPTH + 2; d++) leafmask[d] = 0;
-  uint32_t all = 0;
-  for (int p = 0; p < P.n_paths; p++) { leafmask[P.path_depth[p]] |= 1u << p; all |= 1u << p; }
-  *set = 0;
-  int32_t i = 0;
-  while (i < n && js_ws(s[i])) i++;
-  if (i >= n || s[i] != '{') return false;          // the stats row must be an object (struct)
-  i++;
-  int depth = 1;
-  is_obj[1] = 1;
-  mstack[1] = all;
-  // states: 0 = key or '}' (after '{'), 1 = key (after ','), 2 = value, 3 = after value, 4 = value or ']'
-  int state = 0;
-  uint32_t m = 0;                                     // paths matching the current member's key chain
-  while (true) {
-    while (i < n && js_ws(s[i])) i++;
-    if (i >= n) return false;
-    const uint8_t c = s[i];
-    if (state == 0 || state == 1) {
-      if (c == '}' && state == 0) { state = 3; goto close; }
-      if (c != '"') return false;
-      bool esc;
-      const int32_t e = js_skip_string(s, n, i, &esc);
-      if (e < 0) return false;
-      m = 0;
-      const uint32_t cand = depth <= SK_MAX_DEPTH ? mstack[depth] : 0;
-      for (int p = 0; p < P.n_paths; p++)
-        if ((cand >> p) & 1) {
-          if (js_key_eq(s, i + 1, e - 1, esc, P.names + P.name_off[p][depth - 1], P.name_len[p][depth - 1]))
-            m |= 1u << p;
-        }
-      i = e;
-      while (i < n && js_ws(s[i])) i++;
-      if (i >= n || s[i] != ':') return false;
-      i++;
-      state = 2;
-      continue;
-    }
-    if (state == 2 || state == 4) {
-      if (state == 4 && c == ']') { state = 3; goto close; }
-      const uint32_t leaf = depth <= SK_MAX_DEPTH ? (m & leafmask[depth]) : 0;
-      const uint32_t pre = m & ~leaf;
-      if (c == '{' || c == '[') {
-        if (leaf) return false;                       // number expected
-        if (c == '[' && pre) return false;            // struct expected
-        if (pre) *set &= ~pre;                        // a (repeated) parent object: its fields restart
-        if (depth + 1 >= JS_MAXD) return false;       // deeper than supported
-        depth++;
-        is_obj[depth] = c == '{';
-        mstack[depth] = c == '{' ? pre : 0;
-        i++;
-        state = c == '{' ? 0 : 4;
-        m = 0;
-        continue;
-      }
-      if (c == '"') {
-        if (pre) return false;                        // a string where a struct is expected
-        bool esc;
-        const int32_t e = js_skip_string(s, n, i, &esc);
-        if (e < 0) return false;
-        if (leaf) {
-          for (int p = 0; p < P.n_paths; p++)
-            if ((leaf >> p) & 1) {
-              const int t = P.path_type[p];
-              long long v;
-              if (t == SK_STRING) {                   // body span + escape flag, compared lazily
-                v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
-              } else {
-                if ((t != SK_DATE && t != SK_TIMESTAMP && t != SK_TIMESTAMP_NTZ) || esc) return false;
-                if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v)
-                                   : js_timestamp(s, i + 1, e - 1, &v, t == SK_TIMESTAMP_NTZ))) return false;
-              }
-              val[p] = v;
-              *set |= 1u << p;
-            }
-        }
-        i = e;
-      } else if (c == '-' || (c >= '0' && c <= '9')) {
-        if (pre) return false;
-        bool integral, fits;
-        long long v;
-        const int32_t e = js_number(s, n, i, &integral, &fits, &v);
-        if (e < 0) return false;
-        if (leaf) {
-          for (int p = 0; p < P.n_paths; p++)
-            if ((leaf >> p) & 1) {
-              const int t = P.path_type[p];
-              if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP || t == SK_TIMESTAMP_NTZ) return false;
-              if (t == SK_DECIMAL) {                  // decimalValue() of the token: kept as its span
-                val[p] = (long long)i | ((long long)(e - i) << 32);
-                *set |= 1u << p;
-                continue;
-              }
-              if (t == SK_SHORT || t == SK_BYTE) {
-                if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
-              } else if (!integral || !fits) {
-                return false;                         // long/integer need an integral token
-              }
-              const bool in = t == SK_LONG ? true
-                            : t == SK_INT ? (v >= -2147483648ll && v <= 2147483647ll)
-                            : t == SK_SHORT ? (v >= -32768 && v <= 32767) : (v >= -128 && v <= 127);
-              if (!in) return false;
-              val[p] = v;
-              *set |= 1u << p;
-            }
-        }
-        i = e;
-      } else if (c == 't' || c == 'f' || c == 'n') {
-        const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
-        const int ll = c == 'f' ? 5 : 4;
-        if (i + ll > n) return false;
-        for (int k = 0; k < ll; k++) if (s[i + k] != (uint8_t)lit[k]) return false;
-        if (c != 'n' && (leaf || pre)) return false;  // boolean where a number / struct is expected
-        if (c == 'n') *set &= ~(leaf | pre);          // JSON null: the field (and its children) null
-        i += ll;
-      } else {
-        return false;
-      }
-      state = 3;
-      continue;
-    }
-    // state 3: after a value
-    if (c == ',') { state = is_obj[depth] ? 1 : 4; i++; continue; }
-    if ((c == '}' && is_obj[depth]) || (c == ']' && !is_obj[depth])) goto close;
-    return false;
-  close:
-    i++;
-    depth--;
-    if (depth == 0) return true;                      // trailing content is ignored (readTree)
-    state = 3;
-  }
-}
-
 // The UTF-8 bytes Java's String.getBytes(UTF_8) gives for a string value, one at a time: a stats
 // string is the JSON body s[a, b) with escapes decoded as Jackson decodes them (a \uXXXX surrogate
 // pair is one supplementary code point; a lone surrogate encodes as '?'); a literal is raw bytes.
@@ -2576,6 +2438,192 @@ __device__ int dec_cmp(const DecNum& a, const DecNum& b) {
   return a.sign > 0 ? mag : -mag;
 }
 
+// float / double stats (DefaultJsonRow.java:182-238): a JSON number is rounded from its exact decimal
+// value (DecimalNode.floatValue / doubleValue, USE_BIG_DECIMAL_FOR_FLOATS) and fails to decode when it
+// rounds to an infinity, i.e. when |x| >= the overflow threshold below (2^128 - 2^103, 2^1024 - 2^970);
+// the strings NaN, +INF, +Infinity, Infinity, -INF, -Infinity (after unescaping) are the special
+// values. The value is kept as its token span; comparisons run on the exact digits (OP_FCMP).
+__constant__ char FLT_OVF[] = "340282356779733661637539395458142568448";
+__constant__ char DBL_OVF[] = "179769313486231580793728971405303415079934132710037826936173778980444968292764750946649017977587207096330286416692887910946555547851940402630657488671505820681908902000708383676273854845817711531764475730270069855571366959622842914819860834936475292719074168444365510704342711559699508093042880177904174497792";
+
+__device__ bool fp_in_range(const uint8_t* s, int32_t i, int32_t e, bool dbl) {
+  DecNum x;
+  if (!dec_parse(s + i, e - i, &x)) return false;
+  if (x.sign == 0) return true;
+  x.sign = 1;
+  DecNum t;
+  dec_parse((const uint8_t*)(dbl ? DBL_OVF : FLT_OVF), dbl ? 309 : 39, &t);
+  return dec_cmp(x, t) < 0;
+}
+
+// 1 NaN, 2 +Infinity, 3 -Infinity, 0 another string (JSON string body s[a, b))
+__device__ int fp_special(const uint8_t* s, int32_t a, int32_t b, bool esc) {
+  const char* names[6] = {"NaN", "+INF", "+Infinity", "Infinity", "-INF", "-Infinity"};
+  const int codes[6] = {1, 2, 2, 2, 3, 3};
+  for (int k = 0; k < 6; k++) {
+    Utf8Cursor c;
+    c.s = s; c.i = a; c.end = b; c.esc = esc; c.np = c.pp = 0;
+    const char* w = names[k];
+    int j = 0;
+    uint8_t x;
+    bool same = true;
+    while (c.next(&x)) {
+      if (w[j] == 0 || (uint8_t)w[j] != x) { same = false; break; }
+      j++;
+    }
+    if (same && w[j] == 0) return codes[k];
+  }
+  return 0;
+}
+
+// extract the program's stats fields from one JSON object; returns false on a decode error
+__device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long long* val, uint32_t* set) {
+  uint32_t mstack[JS_MAXD];
+  uint8_t is_obj[JS_MAXD];
+  uint32_t leafmask[SK_MAX_DEPTH + 2];
+  for (int d = 0; d < SK_MAX_DEPTH + 2; d++) leafmask[d] = 0;
+  uint32_t all = 0;
+  for (int p = 0; p < P.n_paths; p++) { leafmask[P.path_depth[p]] |= 1u << p; all |= 1u << p; }
+  *set = 0;
+  int32_t i = 0;
+  while (i < n && js_ws(s[i])) i++;
+  if (i >= n || s[i] != '{') return false;          // the stats row must be an object (struct)
+  i++;
+  int depth = 1;
+  is_obj[1] = 1;
+  mstack[1] = all;
+  // states: 0 = key or '}' (after '{'), 1 = key (after ','), 2 = value, 3 = after value, 4 = value or ']'
+  int state = 0;
+  uint32_t m = 0;                                     // paths matching the current member's key chain
+  while (true) {
+    while (i < n && js_ws(s[i])) i++;
+    if (i >= n) return false;
+    const uint8_t c = s[i];
+    if (state == 0 || state == 1) {
+      if (c == '}' && state == 0) { state = 3; goto close; }
+      if (c != '"') return false;
+      bool esc;
+      const int32_t e = js_skip_string(s, n, i, &esc);
+      if (e < 0) return false;
+      m = 0;
+      const uint32_t cand = depth <= SK_MAX_DEPTH ? mstack[depth] : 0;
+      for (int p = 0; p < P.n_paths; p++)
+        if ((cand >> p) & 1) {
+          if (js_key_eq(s, i + 1, e - 1, esc, P.names + P.name_off[p][depth - 1], P.name_len[p][depth - 1]))
+            m |= 1u << p;
+        }
+      i = e;
+      while (i < n && js_ws(s[i])) i++;
+      if (i >= n || s[i] != ':') return false;
+      i++;
+      state = 2;
+      continue;
+    }
+    if (state == 2 || state == 4) {
+      if (state == 4 && c == ']') { state = 3; goto close; }
+      const uint32_t leaf = depth <= SK_MAX_DEPTH ? (m & leafmask[depth]) : 0;
+      const uint32_t pre = m & ~leaf;
+      if (c == '{' || c == '[') {
+        if (leaf) return false;                       // number expected
+        if (c == '[' && pre) return false;            // struct expected
+        if (pre) *set &= ~pre;                        // a (repeated) parent object: its fields restart
+        if (depth + 1 >= JS_MAXD) return false;       // deeper than supported
+        depth++;
+        is_obj[depth] = c == '{';
+        mstack[depth] = c == '{' ? pre : 0;
+        i++;
+        state = c == '{' ? 0 : 4;
+        m = 0;
+        continue;
+      }
+      if (c == '"') {
+        if (pre) return false;                        // a string where a struct is expected
+        bool esc;
+        const int32_t e = js_skip_string(s, n, i, &esc);
+        if (e < 0) return false;
+        if (leaf) {
+          for (int p = 0; p < P.n_paths; p++)
+            if ((leaf >> p) & 1) {
+              const int t = P.path_type[p];
+              long long v;
+              if (t == SK_STRING) {                   // body span + escape flag, compared lazily
+                v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
+              } else if (t == SK_FLOAT || t == SK_DOUBLE) {
+                const int code = fp_special(s, i + 1, e - 1, esc);
+                if (!code) return false;
+                v = (1ll << 62) | code;
+              } else {
+                if ((t != SK_DATE && t != SK_TIMESTAMP && t != SK_TIMESTAMP_NTZ) || esc) return false;
+                if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v)
+                                   : js_timestamp(s, i + 1, e - 1, &v, t == SK_TIMESTAMP_NTZ))) return false;
+              }
+              val[p] = v;
+              *set |= 1u << p;
+            }
+        }
+        i = e;
+      } else if (c == '-' || (c >= '0' && c <= '9')) {
+        if (pre) return false;
+        bool integral, fits;
+        long long v;
+        const int32_t e = js_number(s, n, i, &integral, &fits, &v);
+        if (e < 0) return false;
+        if (leaf) {
+          for (int p = 0; p < P.n_paths; p++)
+            if ((leaf >> p) & 1) {
+              const int t = P.path_type[p];
+              if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP || t == SK_TIMESTAMP_NTZ) return false;
+              if (t == SK_FLOAT || t == SK_DOUBLE) {   // exact token, range-checked
+                if (!fp_in_range(s, i, e, t == SK_DOUBLE)) return false;
+                val[p] = (long long)i | ((long long)(e - i) << 32);
+                *set |= 1u << p;
+                continue;
+              }
+              if (t == SK_DECIMAL) {                  // decimalValue() of the token: kept as its span
+                val[p] = (long long)i | ((long long)(e - i) << 32);
+                *set |= 1u << p;
+                continue;
+              }
+              if (t == SK_SHORT || t == SK_BYTE) {
+                if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
+              } else if (!integral || !fits) {
+                return false;                         // long/integer need an integral token
+              }
+              const bool in = t == SK_LONG ? true
+                            : t == SK_INT ? (v >= -2147483648ll && v <= 2147483647ll)
+                            : t == SK_SHORT ? (v >= -32768 && v <= 32767) : (v >= -128 && v <= 127);
+              if (!in) return false;
+              val[p] = v;
+              *set |= 1u << p;
+            }
+        }
+        i = e;
+      } else if (c == 't' || c == 'f' || c == 'n') {
+        const char* lit = c == 't' ? "true" : c == 'f' ? "false" : "null";
+        const int ll = c == 'f' ? 5 : 4;
+        if (i + ll > n) return false;
+        for (int k = 0; k < ll; k++) if (s[i + k] != (uint8_t)lit[k]) return false;
+        if (c != 'n' && (leaf || pre)) return false;  // boolean where a number / struct is expected
+        if (c == 'n') *set &= ~(leaf | pre);          // JSON null: the field (and its children) null
+        i += ll;
+      } else {
+        return false;
+      }
+      state = 3;
+      continue;
+    }
+    // state 3: after a value
+    if (c == ',') { state = is_obj[depth] ? 1 : 4; i++; continue; }
+    if ((c == '}' && is_obj[depth]) || (c == ']' && !is_obj[depth])) goto close;
+    return false;
+  close:
+    i++;
+    depth--;
+    if (depth == 0) return true;                      // trailing content is ignored (readTree)
+    state = 3;
+  }
+}
+
 __device__ void sk_decimal(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len, DecNum* d) {
   *d = DecNum{};
   if (kind == 3) dec_parse(s + (int32_t)(v & 0x7fffffff), (int32_t)(v >> 32), d);   // a validated JSON number
@@ -2618,7 +2666,24 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
     if (op == OP_STAT) {
       const int p = P.arg[k];
       sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1;
-      sk[sp] = P.path_type[p] == SK_STRING ? 1 : P.path_type[p] == SK_DECIMAL ? 3 : 0; sp++;
+      const int pt = P.path_type[p];
+      sk[sp] = pt == SK_STRING ? 1 : pt == SK_DECIMAL ? 3 : (pt == SK_FLOAT || pt == SK_DOUBLE) ? 5 : 0; sp++;
+    } else if (op == OP_FCMP) {                          // float / double stat vs a planned threshold
+      if (sp <= 0) return -1;
+      const long long a = sv[sp - 1];
+      const int fl = P.arg[k], mode = fl & 15;
+      int8_t r;
+      if (sn[sp - 1] < 0) r = -1;
+      else if ((a >> 62) & 1) r = (int8_t)((fl >> (3 + (int)(a & 3))) & 1);   // NaN / +Inf / -Inf
+      else if (mode == FC_ALL || mode == FC_NONE) r = mode == FC_ALL;
+      else {
+        DecNum x, y;
+        dec_parse(s + (int32_t)(a & 0x7fffffff), (int32_t)(a >> 32), &x);
+        dec_parse((const uint8_t*)P.names + (int32_t)(P.lit[k] & 0xffffffff), (int32_t)(P.lit[k] >> 32), &y);
+        const int c = dec_cmp(x, y);
+        r = mode == FC_LT ? c < 0 : mode == FC_LE ? c <= 0 : mode == FC_GT ? c > 0 : c >= 0;
+      }
+      sn[sp - 1] = r; sv[sp - 1] = 0; sk[sp - 1] = 0;
     } else if (op == OP_LIT) {
       sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sp++;
     } else if (op == OP_TIMEADD) {                     // DefaultExpressionEvaluator.visitTimeAdd :593-625
@@ -2655,8 +2720,11 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
   return sp == 1 ? sn[0] : -1;
 }
 
-__global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg P, uint8_t* __restrict__ sel,
-                                                   DState* __restrict__ st) {
+// the program lives in device memory (its literal pool holds exact float thresholds of up to ~760
+// digits, too large for a kernel argument)
+__global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg* __restrict__ Pp,
+                                                   uint8_t* __restrict__ sel, DState* __restrict__ st) {
+  const DSkipProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
        r += (long long)gridDim.x * blockDim.x) {
     if (!sel[r]) continue;
@@ -2718,8 +2786,124 @@ __device__ __forceinline__ int bytes_cmp(const uint8_t* a, int32_t na, const uin
   return na < nb ? -1 : na > nb ? 1 : 0;
 }
 
-struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean, 4 decimal text
-  int32_t kind, len;
+// Partition values of the remaining simple types (PartitionValueEvaluator.java:50-100):
+//  boolean   Boolean.parseBoolean: "true" in any case is true, anything else false (never fails)
+//  float /   Float.parseFloat / Double.parseDouble (FloatingDecimal.readJavaFormatString): trimmed,
+//  double    optional sign, NaN / Infinity, or decimal digits with an optional fraction and exponent
+//            and an optional f/F/d/D suffix; rounds to nearest even, overflows to +-Infinity and
+//            keeps the sign of a zero. Hexadecimal literals (0x1.8p1) are refused by this build.
+//            The value stays as its digit span; comparisons run on the exact digits (PO_FCMP).
+//  timestamp java.sql.Timestamp.valueOf ("yyyy-[m]m-[d]d hh:mm:ss[.f{1,9}]", Integer.parseInt
+//            fields, lenient rollover of day / hour / minute / second) then
+//            InternalUtils.microsSinceEpoch (InternalUtils.java:95-98): the local date-time fields,
+//            read here as UTC (the JVM zone cancels out unless it has DST gaps); years before 1583
+//            (Julian calendar) are refused.
+__device__ bool java_parse_int(const uint8_t* s, int32_t a, int32_t b, long long* v) {
+  return java_parse_long(s + a, b - a, -2147483648ll, 2147483647ll, v);
+}
+
+__device__ bool java_timestamp_valueof(const uint8_t* s, int32_t n, long long* out) {
+  int32_t a = 0, b = n;
+  while (a < b && s[a] <= ' ') a++;
+  while (b > a && s[b - 1] <= ' ') b--;
+  int32_t sp = -1;
+  for (int32_t k = a; k < b; k++) if (s[k] == ' ') { sp = k; break; }
+  if (sp <= a) return false;
+  // date: yyyy-m[m]-d[d]
+  int32_t d1 = -1, d2 = -1;
+  for (int32_t k = a; k < sp; k++) if (s[k] == '-') { d1 = k; break; }
+  if (d1 >= 0) for (int32_t k = d1 + 1; k < sp; k++) if (s[k] == '-') { d2 = k; break; }
+  if (!(d1 > a && d2 > a && d2 < sp - 1)) return false;
+  if (d1 - a != 4 || d2 - d1 - 1 < 1 || d2 - d1 - 1 > 2 || sp - d2 - 1 < 1 || sp - d2 - 1 > 2) return false;
+  long long y, mo, d;
+  if (!java_parse_int(s, a, d1, &y) || !java_parse_int(s, d1 + 1, d2, &mo) || !java_parse_int(s, d2 + 1, sp, &d))
+    return false;
+  if (mo < 1 || mo > 12 || d < 1 || d > 31 || y < 1583) return false;
+  // time: h:m:s[.f]
+  const int32_t t0 = sp + 1;
+  int32_t c1 = -1, c2 = -1, per = -1;
+  for (int32_t k = t0; k < b; k++) if (s[k] == ':') { c1 = k; break; }
+  if (c1 >= 0) for (int32_t k = c1 + 1; k < b; k++) if (s[k] == ':') { c2 = k; break; }
+  if (c2 >= 0) for (int32_t k = c2 + 1; k < b; k++) if (s[k] == '.') { per = k; break; }
+  if (!(c1 > t0 && c2 > t0 && c2 < b - 1)) return false;
+  long long h, mi, sec, nanos = 0;
+  if (!java_parse_int(s, t0, c1, &h) || !java_parse_int(s, c1 + 1, c2, &mi)) return false;
+  if (per > t0 && per < b - 1) {
+    if (!java_parse_int(s, c2 + 1, per, &sec)) return false;
+    const int32_t nd = b - per - 1;
+    if (nd > 9 || s[per + 1] < '0' || s[per + 1] > '9') return false;
+    if (!java_parse_int(s, per + 1, b, &nanos)) return false;
+    for (int k = nd; k < 9; k++) nanos *= 10;
+  } else if (per > t0) {
+    return false;
+  } else if (!java_parse_int(s, c2 + 1, b, &sec)) {
+    return false;
+  }
+  const long long secs = (civil_days(y, mo, 1) + d - 1) * 86400 + h * 3600 + mi * 60 + sec;
+  // MICROS.between(EPOCH, t): the nanosecond difference truncated toward zero
+  *out = secs * 1000000 + (secs < 0 ? (nanos + 999) / 1000 : nanos / 1000);
+  return true;
+}
+
+// Float.parseFloat / Double.parseDouble: *special 0 number (digit span [*a, *b) incl. sign), 1 NaN,
+// 2 +Infinity, 3 -Infinity; *negz: a zero (or underflowed) value with a minus sign
+__device__ bool java_parse_fp(const uint8_t* s, int32_t n, int32_t* a, int32_t* b, int* special, bool* negz) {
+  int32_t i = 0, e = n;
+  while (i < e && s[i] <= ' ') i++;
+  while (e > i && s[e - 1] <= ' ') e--;
+  if (i >= e) return false;
+  const int32_t start = i;
+  bool neg = false;
+  if (s[i] == '+' || s[i] == '-') { neg = s[i] == '-'; i++; }
+  *special = 0; *negz = false;
+  const char* nan = "NaN";
+  const char* inf = "Infinity";
+  if (i < e && s[i] == 'N') {
+    if (e - i != 3) return false;
+    for (int k = 0; k < 3; k++) if (s[i + k] != (uint8_t)nan[k]) return false;
+    *special = 1;
+    return true;
+  }
+  if (i < e && s[i] == 'I') {
+    if (e - i != 8) return false;
+    for (int k = 0; k < 8; k++) if (s[i + k] != (uint8_t)inf[k]) return false;
+    *special = neg ? 3 : 2;
+    return true;
+  }
+  if (e - i >= 2 && s[i] == '0' && (s[i + 1] | 0x20) == 'x') return false;   // hex: refused
+  if (e > i && ((s[e - 1] | 0x20) == 'f' || (s[e - 1] | 0x20) == 'd')) e--;  // type suffix
+  int32_t k = i, nd = 0;
+  bool nonzero = false;
+  while (k < e && s[k] >= '0' && s[k] <= '9') { nonzero |= s[k] != '0'; k++; nd++; }
+  if (k < e && s[k] == '.') {
+    k++;
+    while (k < e && s[k] >= '0' && s[k] <= '9') { nonzero |= s[k] != '0'; k++; nd++; }
+  }
+  if (nd == 0) return false;
+  long long ex = 0;
+  bool eneg = false, big = false;
+  if (k < e && (s[k] | 0x20) == 'e') {
+    k++;
+    if (k < e && (s[k] == '+' || s[k] == '-')) { eneg = s[k] == '-'; k++; }
+    if (k >= e) return false;
+    for (; k < e; k++) {
+      if (s[k] < '0' || s[k] > '9') return false;
+      if (ex < 100000000ll) ex = ex * 10 + (s[k] - '0'); else big = true;
+    }
+  }
+  if (k != e) return false;
+  if (!nonzero) { *negz = neg; *a = start; *b = e; return true; }
+  if (big) {                                        // |exponent| >= 1e8: overflow or underflow
+    if (eneg) { *negz = neg; *special = 4; return true; }                      // rounds to a zero
+    *special = neg ? 3 : 2;
+    return true;
+  }
+  *a = start; *b = e;
+  return true;
+}
+
+struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean, 4 decimal text,
+  int32_t kind, len;    // 5 float / double (p, len: digit span; v: special code | negative zero << 8)
   long long v;
   const uint8_t* p;
 };
@@ -2748,6 +2932,20 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
             DecNum dn;
             if (!dec_parse(vp, vl, &dn)) { *err = true; return -1; }
             f[k].kind = 4; f[k].p = vp; f[k].len = vl;
+          } else if (ty == PT_BOOL) {                 // Boolean.parseBoolean
+            const char* tr = "true";
+            bool t = vl == 4;
+            for (int q = 0; q < 4 && t; q++) t = (vp[q] | 0x20) == (uint8_t)tr[q];
+            f[k].kind = 1; f[k].v = t;
+          } else if (ty == PT_TIMESTAMP) {
+            if (!java_timestamp_valueof(vp, vl, &f[k].v)) { *err = true; return -1; }
+            f[k].kind = 1;
+          } else if (ty == PT_F32 || ty == PT_F64) {
+            int32_t fa = 0, fb = 0;
+            int sp_ = 0;
+            bool nz = false;
+            if (!java_parse_fp(vp, vl, &fa, &fb, &sp_, &nz)) { *err = true; return -1; }
+            f[k].kind = 5; f[k].p = vp + fa; f[k].len = fb - fa; f[k].v = sp_ | (nz ? 256 : 0);
           } else {
             const long long lo = ty == PT_LONG ? (-9223372036854775807ll - 1) : ty == PT_INT ? -2147483648ll
                                : ty == PT_SHORT ? -32768 : -128;
@@ -2775,6 +2973,23 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
       st[sp].kind = 4; st[sp].p = (const uint8_t*)P.pool + P.lit[i]; st[sp].len = P.arg[i]; sp++;
     } else if (op == PO_LIT_NULL) {
       st[sp++].kind = 0;
+    } else if (op == PO_FCMP) {                          // float / double field vs a planned threshold
+      PVal& a = st[sp - 1];
+      if (a.kind != 0) {
+        const int fl = P.arg[i], mode = fl & 15, code = (int)(a.v & 255);
+        int r;
+        if (code >= 1 && code <= 3) r = (fl >> (3 + code)) & 1;                 // NaN / +Inf / -Inf
+        else if (mode == FC_ALL || mode == FC_NONE) r = mode == FC_ALL;
+        else {
+          DecNum x{}, y{};
+          if (code == 4) { x.sign = 0; } else dec_parse(a.p, a.len, &x);        // code 4: underflow
+          dec_parse((const uint8_t*)P.pool + (int32_t)(P.lit[i] & 0xffffffff), (int32_t)(P.lit[i] >> 32), &y);
+          int c = dec_cmp(x, y);
+          if (c == 0 && (a.v & 256)) c = -1;                                     // -0.0 sits just below 0
+          r = mode == FC_LT ? c < 0 : mode == FC_LE ? c <= 0 : mode == FC_GT ? c > 0 : c >= 0;
+        }
+        a.kind = 3; a.v = r;
+      }
     } else if (op >= PO_LT && op <= PO_NSEQ) {
       const PVal b = st[--sp];
       const PVal a = st[--sp];
@@ -2822,8 +3037,9 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
   return st[0].v ? 1 : 0;
 }
 
-__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg P, uint8_t* __restrict__ sel,
-                                                  DState* __restrict__ st) {
+__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg* __restrict__ Pp,
+                                                  uint8_t* __restrict__ sel, DState* __restrict__ st) {
+  const DPartProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < M.n;
        r += (long long)gridDim.x * blockDim.x) {
     const long long row = M.act_row ? M.act_row[r] : r;
@@ -3230,7 +3446,7 @@ void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const D
 }  // namespace dk
 
 namespace dk {
-void launch_stats_eval(const StatsRows& R, const DSkipProg& P, uint8_t* sel, DState* st, hipStream_t s) {
+void launch_stats_eval(const StatsRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {
   if (R.n <= 0) return;
   const long long want = (R.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
@@ -3239,7 +3455,7 @@ void launch_stats_eval(const StatsRows& R, const DSkipProg& P, uint8_t* sel, DSt
 }  // namespace dk
 
 namespace dk {
-void launch_part_eval(const MapRows& M, const DPartProg& P, uint8_t* sel, DState* st, hipStream_t s) {
+void launch_part_eval(const MapRows& M, const DPartProg* P, uint8_t* sel, DState* st, hipStream_t s) {
   if (M.n <= 0) return;
   const long long want = (M.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);

@@ -71,6 +71,15 @@ class Literal:
         return Literal(int(micros), "timestamp_ntz")
 
     @staticmethod
+    def ofFloat(v):                                      # Literal.ofFloat(float): a binary32 value
+        import struct
+        return Literal(struct.unpack("<f", struct.pack("<f", float(v)))[0], "float")
+
+    @staticmethod
+    def ofDouble(v):
+        return Literal(float(v), "double")
+
+    @staticmethod
     def ofString(v):
         return Literal(str(v), "string")
 

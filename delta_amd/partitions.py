@@ -8,10 +8,13 @@ ScanImpl.java:247-294).
 
 Supported: partition columns of type string, long, integer, short, byte, date (values through
 java.sql.Date.valueOf, PartitionValueEvaluator.java:72-73), decimal (new BigDecimal(text), :112-113,
-compared with compareTo); literals of a matching kind (string with string, any integral with
-integral, date with date, decimal with decimal, or null); =, <, <=, >, >=, IS NOT DISTINCT
-FROM, IS_NULL, IS_NOT_NULL, NOT, AND, OR. Anything else raises UnsupportedPartitionFilter, so an
-accepted filter is evaluated exactly as the reference evaluates it.
+compared with compareTo), boolean (Boolean.parseBoolean), float / double (Float.parseFloat /
+Double.parseDouble, compared exactly through delta_amd/binfloat.py thresholds with Float.compare
+semantics and ImplicitCastExpression widening of integral operands), timestamp / timestamp_ntz
+(java.sql.Timestamp.valueOf -> InternalUtils.microsSinceEpoch, read as UTC); literals of a matching
+kind (or null); =, <, <=, >, >=, IS NOT DISTINCT FROM, IS_NULL, IS_NOT_NULL, NOT, AND, OR. A float
+comparison needs a column on one side and a literal on the other. Anything else raises
+UnsupportedPartitionFilter, so an accepted filter is evaluated exactly as the reference evaluates it.
 """
 from __future__ import annotations
 
@@ -19,12 +22,17 @@ import json
 
 from .expressions import Column, Literal, Predicate
 
-PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4, "date": 5, "decimal": 6}
+PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4, "date": 5, "decimal": 6, "boolean": 7,
+      "float": 8, "double": 9, "timestamp": 10, "timestamp_ntz": 10}
 INTEGRAL = {"long", "integer", "short", "byte"}
+FLOATS = ("float", "double")
 (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LT, PO_LE, PO_GT, PO_GE, PO_EQ, PO_NSEQ, PO_ISNULL,
- PO_ISNOTNULL, PO_NOT, PO_AND, PO_OR, PO_LIT_DEC) = range(16)
+ PO_ISNOTNULL, PO_NOT, PO_AND, PO_OR, PO_LIT_DEC, PO_FCMP) = range(17)
+REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=", "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}
+_KIND = {"string": "string", "date": "date", "decimal": "decimal", "boolean": "boolean", "timestamp": "timestamp",
+         "timestamp_ntz": "timestamp", "float": "float", "double": "float"}
 CMP = {"<": PO_LT, "<=": PO_LE, ">": PO_GT, ">=": PO_GE, "=": PO_EQ, "IS NOT DISTINCT FROM": PO_NSEQ}
-MAX_FIELDS, MAX_OPS, MAX_STACK, POOL = 8, 64, 16, 1024
+MAX_FIELDS, MAX_OPS, MAX_STACK, POOL = 8, 64, 16, 4096
 
 
 class UnsupportedPartitionFilter(RuntimeError):
@@ -58,6 +66,7 @@ def compile_program(pred: Predicate, fields: dict):
         if t not in PT:
             raise UnsupportedPartitionFilter("partition pruning on %s column %s is not supported by this engine build"
                                              % (t, col.names[0]))
+        t = "timestamp" if t == "timestamp_ntz" else t         # one parse for both (Timestamp.valueOf)
         if (phys, t) not in used:
             used.append((phys, t))
         return used.index((phys, t)), t
@@ -68,7 +77,7 @@ def compile_program(pred: Predicate, fields: dict):
         if isinstance(node, Column):
             k, t = field(node)
             ops.append((PO_FIELD, k, 0))
-            return (t if t in ("string", "date", "decimal") else "integral"), fields[node.names[0].lower()][0]
+            return _KIND.get(t, "integral"), fields[node.names[0].lower()][0]
         if isinstance(node, Literal):
             return operand_lit(node), node.type
         raise UnsupportedPartitionFilter("partition pruning on expression %r is not supported" % (node,))
@@ -92,9 +101,13 @@ def compile_program(pred: Predicate, fields: dict):
                 ops.append((PO_LIT_DEC, len(b), len(pool)))
                 pool.extend(b)
                 return "decimal"
-            if node.type in INTEGRAL | {"date"} and isinstance(node.value, int) and not isinstance(node.value, bool):
-                ops.append((PO_LIT_INT, 0, int(node.value)))   # a date literal is its epoch day
-                return "date" if node.type == "date" else "integral"
+            if node.type == "boolean":
+                ops.append((PO_LIT_INT, 0, int(bool(node.value))))
+                return "boolean"
+            if node.type in INTEGRAL | {"date", "timestamp", "timestamp_ntz"} and isinstance(node.value, int) \
+                    and not isinstance(node.value, bool):
+                ops.append((PO_LIT_INT, 0, int(node.value)))   # dates: epoch days, timestamps: micros
+                return _KIND.get(node.type, "integral")
             raise UnsupportedPartitionFilter("partition pruning with a %s literal is not supported" % node.type)
         raise UnsupportedPartitionFilter("partition pruning on expression %r is not supported" % (node,))
 
@@ -113,6 +126,8 @@ def compile_program(pred: Predicate, fields: dict):
         elif n in ("IS_NULL", "IS_NOT_NULL"):
             operand(c[0])
             ops.append((PO_ISNULL if n == "IS_NULL" else PO_ISNOTNULL, 0, 0))
+        elif n in CMP and any(_type(x) in FLOATS for x in c):
+            float_cmp(n, c[0], c[1])
         elif n in CMP:
             (ka, ta), (kb, tb) = operand(c[0]), operand(c[1])
             # DefaultExpressionEvaluator.transformBinaryComparator (:337-354): differently typed
@@ -128,7 +143,73 @@ def compile_program(pred: Predicate, fields: dict):
         else:
             raise UnsupportedPartitionFilter("partition predicate %s is not supported by this engine build" % n)
 
+    def _type(x):
+        if isinstance(x, Column) and len(x.names) == 1 and x.names[0].lower() in fields:
+            return fields[x.names[0].lower()][0]
+        return x.type if isinstance(x, Literal) else None
+
+    def float_cmp(n, left, right):
+        """column <op> literal in float / double (either side float-typed): planned exactly by
+        binfloat.plan; integral columns widened to float get integer bounds, float columns PO_FCMP."""
+        from . import binfloat
+        from .skipping import LONG_MAX, LONG_MIN, UnsupportedExpression, _UP_CAST, comparable
+        if isinstance(left, Literal) and isinstance(right, Column):
+            left, right, n = right, left, REVERSE[n]
+        if not (isinstance(left, Column) and isinstance(right, Literal)):
+            raise UnsupportedPartitionFilter("float partition comparison needs a column and a literal: %r, %r"
+                                             % (left, right))
+        ct, lt = _type(left), right.type
+        if not comparable(ct, lt):
+            raise UnsupportedExpression(
+                "Unsupported expression: %s: operands are of different types which are not comparable: "
+                "left type=%s, right type=%s" % (n, ct, lt))
+        if ct not in FLOATS and ct not in INTEGRAL:
+            raise UnsupportedPartitionFilter("comparison of %s with %s is not supported" % (ct, lt))
+        if right.value is None:                              # null literal: generic null semantics
+            operand(left)
+            ops.append((PO_LIT_NULL, 0, 0))
+            ops.append((CMP[n], 0, 0))
+            return
+        cmp_t = ct if ct == lt else (lt if lt in _UP_CAST.get(ct, ()) else ct)
+        value_fmt = ct if ct in FLOATS else cmp_t
+        op = "=" if n == "IS NOT DISTINCT FROM" else n
+        conds, (r_nan, r_pinf, r_ninf) = binfloat.plan(op, right.value, lt, value_fmt, cmp_t)
+        terms = 0
+        if n == "IS NOT DISTINCT FROM":                      # null-safe: a null column is false
+            operand(left)
+            ops.append((PO_ISNOTNULL, 0, 0))
+            terms += 1
+        if ct not in FLOATS:
+            b = binfloat.integral_bounds(conds)
+            if b is None:
+                parts = [(PO_LT, LONG_MIN)]
+            else:
+                parts = ([(PO_GE, b[0])] if b[0] > LONG_MIN else []) + ([(PO_LE, b[1])] if b[1] < LONG_MAX else [])
+                parts = parts or [(PO_GE, LONG_MIN)]
+            for cop, v in parts:
+                operand(left)
+                ops.append((PO_LIT_INT, 0, int(v)))
+                ops.append((cop, 0, 0))
+                terms += 1
+                if terms > 1:
+                    ops.append((PO_AND, 0, 0))
+            return
+        flags = (int(r_nan) << 4) | (int(r_pinf) << 5) | (int(r_ninf) << 6)
+        from .skipping import FC_ALL, FC_NONE, _FC_MODE
+        for cnd in conds:
+            operand(left)
+            if cnd in (binfloat.ALL, binfloat.NONE):
+                ops.append((PO_FCMP, flags | (FC_ALL if cnd == binfloat.ALL else FC_NONE), (0, 0)))
+            else:
+                text = binfloat.decimal_text(cnd[1], short=True).encode("ascii")
+                ops.append((PO_FCMP, flags | _FC_MODE[cnd[0]], (len(pool), len(text))))
+                pool.extend(text)
+            terms += 1
+            if terms > 1:
+                ops.append((PO_AND, 0, 0))
+
     pred_(pred)
+    ops[:] = [(o, a, (l[0] | (l[1] << 32)) if o == PO_FCMP else l) for o, a, l in ops]
     flist = []
     for phys, t in used:
         b = phys.encode("utf-8")
@@ -144,7 +225,7 @@ def _depth(ops):
     for op, _, _ in ops:
         if op in (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LIT_DEC):
             d += 1
-        elif op not in (PO_ISNULL, PO_ISNOTNULL, PO_NOT):
+        elif op not in (PO_ISNULL, PO_ISNOTNULL, PO_NOT, PO_FCMP):
             d -= 1
         hi = max(hi, d)
     return hi

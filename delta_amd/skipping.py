@@ -20,7 +20,8 @@ from .expressions import ALWAYS_TRUE, Column, Literal, Predicate
 MIN, MAX, NULL_COUNT, NUM_RECORDS = "minValues", "maxValues", "nullCount", "numRecords"
 SKIPPING_ELIGIBLE = {"byte", "short", "integer", "long", "float", "double", "date", "timestamp",
                      "timestamp_ntz", "string"}          # StatsSchemaHelper.java:209-222 (+ decimal)
-GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp", "decimal", "timestamp_ntz"}          # stats value types k_stats_eval decodes
+GPU_TYPES = {"byte", "short", "integer", "long", "date", "string", "timestamp", "decimal", "timestamp_ntz",
+             "float", "double"}                          # stats value types k_stats_eval decodes
 REVERSE = {"=": "=", "<": ">", "<=": ">=", ">": "<", ">=": "<=",
            "IS NOT DISTINCT FROM": "IS NOT DISTINCT FROM"}   # DataSkippingUtils.java:346-356
 NOT_CMP = {"<": ">=", "<=": ">", ">": "<=", ">=": "<"}        # :430-441
@@ -220,9 +221,16 @@ def referenced_stats(node, out=None):
 
 
 # ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
-OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD, OP_LIT_DEC = range(12)
+OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD, OP_LIT_DEC, OP_FCMP = range(13)
+# OP_FCMP: pops a float/double stats value, pushes `x <mode> threshold` for its exact decimal value x
+# (threshold = decimal text in names), or the planned constant for NaN / +Infinity / -Infinity
+FC_LT, FC_LE, FC_GT, FC_GE, FC_ALL, FC_NONE = range(6)
+_FC_MODE = {"<": FC_LT, "<=": FC_LE, ">": FC_GT, ">=": FC_GE}
+FLOATS = ("float", "double")
+LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
 _CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
-TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6, "decimal": 7, "timestamp_ntz": 8}
+TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6, "decimal": 7,
+             "timestamp_ntz": 8, "float": 9, "double": 10}
 
 
 def stat_type(path, leaves):
@@ -276,6 +284,8 @@ def compile_program(node, leaves):
         elif n[0] == "timeadd":                              # max + 1 ms (StatsSchemaHelper :154-159)
             emit(n[1])
             ops.append((OP_TIMEADD, 0, 1000))
+        elif _float_comparison(n, leaves):
+            emit_float(n)
         else:
             kinds = {_operand_kind(c, leaves) for c in (n[1], n[2])} - {None}
             if len(kinds) > 1:
@@ -283,10 +293,55 @@ def compile_program(node, leaves):
             emit(n[1])
             emit(n[2])
             ops.append((_CMP[n[0]], 0, 0))
+
+    def emit_float(n):
+        """A comparison in float / double (Float.compare / Double.compare after ImplicitCastExpression
+        widening), planned exactly by binfloat.plan: integral stats get integer bounds, float /
+        double stats an OP_FCMP per bound."""
+        from . import binfloat
+        op, stat, lit = n
+        if stat[0] != "stat" or lit[0] != "lit":
+            raise UnsupportedSkipping("float comparison of %r with %r" % (stat, lit))
+        st, lt = operand_type(stat, leaves), lit[2]
+        if lit[1] is None:                                    # null literal: the comparison is null
+            emit(stat)
+            ops.append((OP_LIT, 1, 0))
+            ops.append((_CMP[op], 0, 0))
+            return
+        cmp_t = st if st == lt else (lt if lt in _UP_CAST.get(st, ()) else st)
+        value_fmt = st if st in FLOATS else cmp_t
+        conds, (r_nan, r_pinf, r_ninf) = binfloat.plan(op, lit[1], lt, value_fmt, cmp_t)
+        if st not in FLOATS:                                   # integral stats widened to cmp_t
+            b = binfloat.integral_bounds(conds)
+            if b is None:
+                parts = [(OP_LT, LONG_MIN)]                    # never (null when the stat is null)
+            else:
+                parts = ([(OP_GE, b[0])] if b[0] > LONG_MIN else []) + ([(OP_LE, b[1])] if b[1] < LONG_MAX else [])
+                parts = parts or [(OP_GE, LONG_MIN)]           # always
+            for k, (cop, v) in enumerate(parts):
+                emit(stat)
+                ops.append((OP_LIT, 0, int(v)))
+                ops.append((cop, 0, 0))
+                if k:
+                    ops.append((OP_AND, 0, 0))
+            return
+        flags = (int(r_nan) << 4) | (int(r_pinf) << 5) | (int(r_ninf) << 6)
+        for k, c in enumerate(conds):
+            emit(stat)
+            if c in (binfloat.ALL, binfloat.NONE):
+                ops.append((OP_FCMP, flags | (FC_ALL if c == binfloat.ALL else FC_NONE), b""))
+            else:
+                ops.append((OP_FCMP, flags | _FC_MODE[c[0]], binfloat.decimal_text(c[1], short=True).encode("ascii")))
+            if k:
+                ops.append((OP_AND, 0, 0))
     emit(node)
     if len(ops) > MAX_OPS or _stack_depth(ops) > MAX_STACK:
         raise UnsupportedSkipping("data skipping filter is too large for the device evaluator")
     return paths, [TYPE_CODE[stat_type(p, leaves)] for p in paths], ops
+
+
+def _float_comparison(n, leaves):
+    return any(operand_type(c, leaves) in FLOATS for c in (n[1], n[2]) if c[0] in ("stat", "lit"))
 
 
 def _operand_kind(n, leaves):
@@ -349,13 +404,13 @@ def check_types(node, leaves):
         check_comparable(node, leaves)
 
 
-MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 512
+MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 4096
 
 
 def _stack_depth(ops):
     d = hi = 0
     for op, _, _ in ops:
-        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR, OP_LIT_DEC) else 0 if op == OP_TIMEADD else -1
+        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR, OP_LIT_DEC) else 0 if op in (OP_TIMEADD, OP_FCMP) else -1
         hi = max(hi, d)
     return hi
 
@@ -382,6 +437,9 @@ def pack(program, struct_type):
     for op, arg, lit in ops:
         if op in (OP_LIT_STR, OP_LIT_DEC):                   # literal bytes follow the names
             packed.append((op, len(lit), len(names)))
+            names += lit
+        elif op == OP_FCMP:                                  # flags; threshold text offset | length << 32
+            packed.append((op, arg, len(names) | (len(lit) << 32)))
             names += lit
         else:
             packed.append((op, arg, lit))

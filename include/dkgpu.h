@@ -118,15 +118,19 @@ typedef struct dk_skip_program {
   int32_t n_paths;                 /* <= 8 stats fields                                        */
   int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte, 4 date (epoch days), 5 string,
                                       6 timestamp (micros since epoch), 7 decimal,
-                                      8 timestamp_ntz (micros, read as UTC) */
+                                      8 timestamp_ntz (micros, read as UTC), 9 float, 10 double */
   int32_t path_depth[8];           /* name components, 1..4 ("maxValues","id" -> 2)             */
   int32_t name_off[8][4];          /* component names: offsets / lengths into names (UTF-8)     */
   int32_t name_len[8][4];
-  char names[512];
+  char names[4096];
   int32_t n_ops;                   /* <= 64                                                     */
   int32_t op[64];                  /* 0 STAT(arg=path), 1 LIT(arg=1: null), 2 <, 3 <=, 4 >, 5 >=, 6 =, 7 AND, 8 OR,
                                       9 LIT_STR(UTF-8 bytes names[lit, lit + arg)), 10 TIMEADD(top += lit micros),
-                                      11 LIT_DEC(BigDecimal text names[lit, lit + arg)) */
+                                      11 LIT_DEC(BigDecimal text names[lit, lit + arg)),
+                                      12 FCMP(pop a float/double stat x; push x <mode> threshold over its
+                                         exact decimal value: arg & 15 = 0 <, 1 <=, 2 >, 3 >=, 4 always,
+                                         5 never; arg bits 4/5/6 = the result for NaN / +Inf / -Inf;
+                                         threshold = names[lit & 0xffffffff, + (lit >> 32))) */
   int32_t arg[64];
   int64_t lit[64];
 } dk_skip_program;
@@ -137,17 +141,21 @@ typedef struct dk_skip_program {
  * A row stays selected iff the predicate is TRUE (null and false drop it). */
 typedef struct dk_part_program {
   int32_t n_fields;                /* <= 8 partition columns                                      */
-  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string, 5 date, 6 decimal */
+  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string, 5 date, 6 decimal,
+                                      7 boolean, 8 float, 9 double, 10 timestamp / timestamp_ntz
+                                      (java.sql.Timestamp.valueOf, fields read as UTC) */
   int32_t name_off[8];             /* physical column name (map key): offset / length in pool      */
   int32_t name_len[8];
   int32_t n_ops;                   /* <= 64                                                       */
   int32_t op[64];                  /* 0 FIELD(arg) 1 LIT_INT(lit) 2 LIT_STR(pool[lit], arg bytes) 3 LIT_NULL
                                       4 < 5 <= 6 > 7 >= 8 = 9 IS NOT DISTINCT FROM 10 IS_NULL
                                       11 IS_NOT_NULL 12 NOT 13 AND 14 OR
-                                      15 LIT_DEC(BigDecimal text pool[lit], arg bytes)            */
+                                      15 LIT_DEC(BigDecimal text pool[lit], arg bytes)
+                                      16 FCMP(pop a float/double field; as dk_skip_program's FCMP,
+                                         threshold pool[lit & 0xffffffff, + (lit >> 32)))          */
   int32_t arg[64];
   int64_t lit[64];
-  char pool[1024];
+  char pool[4096];
 } dk_part_program;
 
 /* ---- Replay: reconcile the tail and the checkpoint files on the GPU ----

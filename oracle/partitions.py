@@ -5,7 +5,10 @@
       a partition column becomes element_at(add.partitionValues, physical name), deserialized by
       PartitionValueEvaluator (kernel-defaults/.../expressions/PartitionValueEvaluator.java:50-90:
       Long/Integer/Short/Byte.parseX, dates through java.sql.Date.valueOf (:72-73, restated in
-      oracle/skipping.py:_date) -- a malformed value fails the scan) unless it is a string
+      oracle/skipping.py:_date), Boolean.parseBoolean, Float.parseFloat / Double.parseDouble
+      (:93-100), timestamps through java.sql.Timestamp.valueOf + InternalUtils.microsSinceEpoch
+      (:80-87; InternalUtils.java:95-98) -- a malformed value fails the scan) unless it is a string;
+      float comparisons use Float.compare / Double.compare after ImplicitCastExpression widening
   DefaultExpressionEvaluator: comparators are null if a side is null (IS NOT DISTINCT FROM is
       null-safe), AND/OR/NOT are Kleene and are evaluated on every row of the batch; strings compare
       as unsigned UTF-8 bytes, then length (DefaultExpressionUtils.java:39-56)
@@ -40,9 +43,115 @@ def element_at(pv, key: bytes):
     return None
 
 
+_JFLOAT = re.compile(rb"^([+-]?)(?:(NaN)|(Infinity)|(0[xX][0-9a-fA-F]*\.?[0-9a-fA-F]*[pP][+-]?[0-9]+)|"
+                     rb"((?:[0-9]+\.?[0-9]*|\.[0-9]+)(?:[eE][+-]?[0-9]+)?))[fFdD]?$")
+
+
+def _java_trim(b: bytes) -> bytes:
+    i, j = 0, len(b)
+    while i < j and b[i] <= 0x20:
+        i += 1
+    while j > i and b[j - 1] <= 0x20:
+        j -= 1
+    return b[i:j]
+
+
+def _parse_floating(v: bytes, typ: str):
+    """Float.parseFloat / Double.parseDouble (FloatingDecimal.readJavaFormatString): trimmed; sign;
+    NaN / Infinity; decimal or hexadecimal digits with an optional f/F/d/D suffix (none after NaN /
+    Infinity); correctly rounded, overflow to +-Infinity, the sign kept on zero."""
+    import math
+    from decimal import Decimal
+    from fractions import Fraction
+    from oracle.skipping import _to_float32
+    t = _java_trim(v)
+    m = _JFLOAT.match(t)
+    if not m or (m.group(2) or m.group(3)) and t[-1:] in b"fFdD" and not t.endswith((b"NaN", b"Infinity")):
+        raise PartitionValueError("For input string: %r" % v)
+    neg = m.group(1) == b"-"
+    if m.group(2):
+        return math.nan
+    if m.group(3):
+        return -math.inf if neg else math.inf
+    if m.group(4):
+        hx = m.group(4).decode().lower()
+        mant, ex = hx[2:].split("p")
+        ip, _, fp = mant.partition(".")
+        x = Fraction(int((ip + fp) or "0", 16), 16 ** len(fp)) * Fraction(2) ** int(ex)
+    else:
+        x = Fraction(Decimal(m.group(5).decode()))
+    if typ == "float":
+        r = _to_float32(x) if x else 0.0
+    else:
+        try:
+            r = x.numerator / x.denominator if x else 0.0
+        except OverflowError:
+            r = math.inf
+    return -r if neg else r
+
+
+def _timestamp_valueof(v: bytes) -> int:
+    """java.sql.Timestamp.valueOf(s) then InternalUtils.microsSinceEpoch (InternalUtils.java:95-98):
+    "yyyy-[m]m-[d]d hh:mm:ss[.f{1,9}]" split on the first space / dashes / colons / period, each
+    field Integer.parseInt, month 1..12 and day 1..31, then the lenient calendar rolls the fields
+    over; the local date-time is read back in the same zone, so the fields count as UTC here.
+    Years before 1583 (Julian calendar) are refused, as for dates."""
+    import datetime as _dt
+    bad = PartitionValueError("Timestamp format must be yyyy-mm-dd hh:mm:ss[.fffffffff]: %r" % v)
+    s = _java_trim(v).decode("utf-8", "replace")
+
+    def pint(x):
+        if not re.fullmatch(r"[+-]?[0-9]+", x):
+            raise bad
+        i = int(x)
+        if not -(1 << 31) <= i < (1 << 31):
+            raise bad
+        return i
+    sp = s.find(" ")
+    if sp <= 0:
+        raise bad
+    date_s, time_s = s[:sp], s[sp + 1:]
+    d1 = date_s.find("-")
+    d2 = date_s.find("-", d1 + 1)
+    if not (d1 > 0 and d2 > 0 and d2 < len(date_s) - 1):
+        raise bad
+    yyyy, mm, dd = date_s[:d1], date_s[d1 + 1:d2], date_s[d2 + 1:]
+    if not (len(yyyy) == 4 and 1 <= len(mm) <= 2 and 1 <= len(dd) <= 2):
+        raise bad
+    y, mo, d = pint(yyyy), pint(mm), pint(dd)
+    if not (1 <= mo <= 12 and 1 <= d <= 31) or y < 1583:
+        raise bad
+    c1 = time_s.find(":")
+    c2 = time_s.find(":", c1 + 1)
+    per = time_s.find(".", c2 + 1)
+    if not (c1 > 0 and c2 > 0 and c2 < len(time_s) - 1):
+        raise bad
+    h, mi = pint(time_s[:c1]), pint(time_s[c1 + 1:c2])
+    nanos = 0
+    if 0 < per < len(time_s) - 1:
+        sec = pint(time_s[c2 + 1:per])
+        frac = time_s[per + 1:]
+        if len(frac) > 9 or not frac[0].isdigit():
+            raise bad
+        nanos = pint(frac) * 10 ** (9 - len(frac))
+    elif per > 0:
+        raise bad
+    else:
+        sec = pint(time_s[c2 + 1:])
+    days = (_dt.date(y, mo, 1) - _dt.date(1970, 1, 1)).days + d - 1
+    total = (days * 86400 + h * 3600 + mi * 60 + sec) * 1_000_000_000 + nanos
+    return total // 1000 if total >= 0 else -((-total) // 1000)
+
+
 def deserialize(v, typ):
     if v is None or typ == "string":
         return v
+    if typ == "boolean":                               # Boolean.parseBoolean: never fails
+        return v.lower() == b"true"
+    if typ in ("float", "double"):
+        return _parse_floating(v, typ)
+    if typ in ("timestamp", "timestamp_ntz"):
+        return _timestamp_valueof(v)
     if typ.startswith("decimal"):                      # new BigDecimal(text): PartitionValueEvaluator :112-113
         from decimal import Decimal
         m = _DEC.match(v)
@@ -89,13 +198,29 @@ def evaluate(node, pv, fields):
         a = evaluate(c[0], pv, fields)
         return (a is None) if n == "IS_NULL" else (a is not None)
     a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
+    ta, tb = _type(c[0], fields), _type(c[1], fields)
+    if ta in ("float", "double") or tb in ("float", "double"):
+        from oracle.skipping import _float_compare
+        cmp = (lambda x, y: _float_compare(x, ta, y, tb))
+    else:
+        cmp = (lambda x, y: (x > y) - (x < y))
     if n == "IS NOT DISTINCT FROM":
         if a is None or b is None:
             return a is None and b is None
-        return a == b
+        return cmp(a, b) == 0
     if a is None or b is None:
         return None
-    return {"<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b, "=": a == b}[n]
+    r = cmp(a, b)
+    return {"<": r < 0, "<=": r <= 0, ">": r > 0, ">=": r >= 0, "=": r == 0}[n]
+
+
+def _type(node, fields):
+    kind = type(node).__name__
+    if kind == "Column":
+        return fields[node.names[0].lower()][0]
+    if kind == "Literal":
+        return node.type
+    return "boolean"
 
 
 def json_map(add: dict):

@@ -12,7 +12,10 @@ does with a data-skipping predicate once the scan files are reconciled.
       long/integer: an integral token in range; short/byte: any number whose exact value is an
       integer in range (canConvertToExactIntegral); date: a string through java.sql.Date.valueOf
       (:249-252); string: a JSON string, compared as unsigned UTF-8 bytes then length
-      (DefaultExpressionUtils.java:49-54); struct: an object; JSON null = null
+      (DefaultExpressionUtils.java:49-54); float/double: the exact number rounded to the format
+      (an infinite result is an error) or one of the NaN / Infinity strings (:182-238), compared
+      with Float.compare / Double.compare (DefaultExpressionUtils.java:146-153) after
+      ImplicitCastExpression widening; struct: an object; JSON null = null
   DefaultExpressionEvaluator            kernel-defaults/.../internal/expressions/
       comparators are null when either side is null; AND/OR are Kleene (visitAnd/visitOr)
 
@@ -24,8 +27,12 @@ from __future__ import annotations
 
 import datetime as _dt
 import json
+import math
 import re
 from decimal import Decimal
+from fractions import Fraction
+
+import numpy as np
 
 RANGES = {"long": (-(1 << 63), (1 << 63) - 1), "integer": (-(1 << 31), (1 << 31) - 1),
           "short": (-(1 << 15), (1 << 15) - 1), "byte": (-(1 << 7), (1 << 7) - 1)}
@@ -135,9 +142,70 @@ def _timestamp_ntz(text):
     return secs * 1_000_000 + micros
 
 
+_F32_MAX = float.fromhex("0x1.fffffep127")
+
+
+def _nearest_even(x: Fraction, lo: float, hi: float, lo_even: bool) -> float:
+    """Whichever of lo < hi (adjacent binary values around x) is nearer to x; ties to the even one."""
+    dl, dh = x - Fraction(lo), Fraction(hi) - x
+    return lo if dl < dh or (dl == dh and lo_even) else hi
+
+
+def _to_float32(x: Fraction):
+    """Correctly rounded binary32 value of an exact x (as a Python float), +-inf on overflow.
+    The double nearest x is found first (correctly rounded by Python), then the two binary32
+    neighbours around x are compared exactly, so double rounding cannot creep in."""
+    if x == 0:
+        return 0.0
+    a = abs(x)
+    d = float(a) if a < Fraction(2) ** 1030 else math.inf
+    f = float(np.float32(d)) if d <= _F32_MAX else math.inf
+    # neighbours of x in binary32 (inf stands for the first value past the largest)
+    if f != math.inf and Fraction(f) > a:
+        hi, lo = f, float(np.nextafter(np.float32(f), np.float32(0)))
+    elif f != math.inf:
+        lo = f
+        hi = float(np.nextafter(np.float32(f), np.float32(np.inf))) if f < _F32_MAX else 2.0 ** 128
+    else:
+        lo, hi = _F32_MAX, 2.0 ** 128
+    if Fraction(lo) == a:
+        r = lo
+    else:
+        lo_even = lo == 0 or (int(np.float32(lo).view(np.uint32)) & 1) == 0
+        r = _nearest_even(a, lo, hi, lo_even)
+    r = math.inf if r >= 2.0 ** 128 else r
+    return r if x > 0 else -r
+
+
+_SPECIAL = {"NaN": math.nan, "+INF": math.inf, "+Infinity": math.inf, "Infinity": math.inf,
+            "-INF": -math.inf, "-Infinity": -math.inf}
+
+
+def _floating(v, typ):
+    """DefaultJsonRow.java:182-238: a number is rounded from its exact value (DecimalNode
+    floatValue / doubleValue; IntNode / LongNode / BigIntegerNode widen), an infinite result is a
+    decode error; the strings NaN / +INF / +Infinity / Infinity / -INF / -Infinity are accepted.
+    Zero is +0.0 whatever its sign (BigDecimal has no negative zero)."""
+    if isinstance(v, str):
+        if v in _SPECIAL:
+            return _SPECIAL[v]
+        raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))
+    if isinstance(v, bool) or not isinstance(v, (int, Decimal)):
+        raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))
+    x = Fraction(v)
+    if x == 0:
+        return 0.0
+    r = _to_float32(x) if typ == "float" else float(Decimal(v))
+    if math.isinf(r):
+        raise StatsDecodeError("Couldn't decode %r, expected a %s" % (v, typ))
+    return r
+
+
 def _leaf(v, typ):
     if v is None:
         return None
+    if typ in ("float", "double"):
+        return _floating(v, typ)
     if typ == "decimal":                               # DefaultJsonRow: isNumber -> decimalValue()
         if isinstance(v, bool) or not isinstance(v, (int, Decimal)):
             raise StatsDecodeError("Couldn't decode %r, expected a decimal" % (v,))
@@ -186,7 +254,45 @@ def decode_stats(s: str, types: dict) -> dict:
     return out
 
 
-def evaluate(node, vals):
+_WIDEN = {"byte": 0, "short": 1, "integer": 2, "long": 3, "float": 4, "double": 5}
+
+
+def _java_compare(a, b) -> int:
+    """Float.compare / Double.compare: -0.0 < 0.0, NaN above everything and equal to itself."""
+    an, bn = a != a, b != b
+    if an or bn:
+        return (an > bn) - (an < bn)
+    if a == b == 0:
+        sa, sb = math.copysign(1.0, a), math.copysign(1.0, b)
+        return (sa > sb) - (sa < sb)
+    return (a > b) - (a < b)
+
+
+def _cast(v, frm, to):
+    """ImplicitCastExpression (ImplicitCastExpression.java:30-41, 118-125): integral -> float /
+    double rounds to nearest even, float -> double is exact."""
+    if frm == to or frm in ("float", "double"):
+        return float(v)
+    return _to_float32(Fraction(v)) if to == "float" else float(v)
+
+
+def _float_compare(a, ta, b, tb):
+    """The comparator over two operands of which one is float / double typed."""
+    w = ta if _WIDEN.get(ta, -1) >= _WIDEN.get(tb, -1) else tb
+    return _java_compare(_cast(a, ta, w), _cast(b, tb, w))
+
+
+def _type_of(node, types):
+    if node[0] == "stat":
+        return types.get(node[1]) if types else None
+    if node[0] == "lit":
+        return node[2] if len(node) > 2 else None
+    if node[0] == "timeadd":
+        return _type_of(node[1], types)
+    return "boolean"
+
+
+def evaluate(node, vals, types=None):
     """True / False / None (null) for a planner node over decoded stats."""
     k = node[0]
     if k == "stat":
@@ -197,18 +303,22 @@ def evaluate(node, vals):
     if k == "lit":
         return node[1].encode("utf-8", "replace") if isinstance(node[1], str) else node[1]
     if k == "AND":
-        a, b = evaluate(node[1], vals), evaluate(node[2], vals)
+        a, b = evaluate(node[1], vals, types), evaluate(node[2], vals, types)
         if a is False or b is False:
             return False
         return True if (a is True and b is True) else None
     if k == "OR":
-        a, b = evaluate(node[1], vals), evaluate(node[2], vals)
+        a, b = evaluate(node[1], vals, types), evaluate(node[2], vals, types)
         if a is True or b is True:
             return True
         return False if (a is False and b is False) else None
-    a, b = evaluate(node[1], vals), evaluate(node[2], vals)
+    a, b = evaluate(node[1], vals, types), evaluate(node[2], vals, types)
     if a is None or b is None:
         return None
+    ta, tb = _type_of(node[1], types), _type_of(node[2], types)
+    if ta in ("float", "double") or tb in ("float", "double"):
+        c = _float_compare(a, ta, b, tb)
+        return {"<": c < 0, "<=": c <= 0, ">": c > 0, ">=": c >= 0, "=": c == 0}[k]
     return {"<": a < b, "<=": a <= b, ">": a > b, ">=": a >= b, "=": a == b}[k]
 
 
@@ -216,4 +326,4 @@ def keep(stats: str | None, node, types) -> bool:
     """COALESCE(skippingPredicate, true) for one selected row (null stats -> kept)."""
     if stats is None:
         return True
-    return evaluate(node, decode_stats(stats, types)) is not False
+    return evaluate(node, decode_stats(stats, types), types) is not False

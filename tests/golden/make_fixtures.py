@@ -28,6 +28,8 @@ TABLES = {
     "data-skipping-basic-stats-all-types-columnmapping-id": GOLD,
     "data-skipping-change-stats-collected-across-versions": GOLD, "data-skipping-partition-and-data-column": GOLD,
     "basic-dv-with-checkpoint": KDRES, "basic-with-checkpoint": KDRES,
+    "data-reader-partition-values": GOLD, "data-reader-timestamp_ntz": GOLD,
+    "data-reader-timestamp_ntz-name-mode": GOLD, "data-reader-timestamp_ntz-id-mode": GOLD,
 }
 
 

@@ -75,7 +75,7 @@ def test_partition_fields_and_compile():
 def test_pack_layout():
     import ctypes
     from delta_amd._lib import dk_part_program
-    assert ctypes.sizeof(dk_part_program) == 4 + 32 * 3 + 4 + 256 + 256 + 512 + 1024
+    assert ctypes.sizeof(dk_part_program) == 4 + 32 * 3 + 4 + 256 + 256 + 512 + 4096
     f = {"p": ("integer", "p")}
     prog = pp.pack(pp.compile_program(Predicate("IS_NULL", col("p")), f), dk_part_program)
     assert prog.n_fields == 1 and prog.n_ops == 2 and bytes(prog.pool)[:1] == b"p"
@@ -315,4 +315,169 @@ def test_gpu_decimal_partition_values(tmp_path):
         _write_pv_table(r, [{"p": "1"}, {"p": bad}], "decimal(38,3)")
         with pytest.raises(DkError, match="partition"):
             _gpu_files(r, DEC_PREDICATES[0], eng)
+    eng.close()
+
+
+# ---------------------------------------------------------------- boolean / float / double / timestamp
+# PartitionPruningSuite.scala:37-97 on golden data-reader-partition-values: `col = value` keeps the one
+# partition holding the value (two for date and timestamp), `col = null` keeps nothing
+PV_TABLE = os.path.join(TABLES, "data-reader-partition-values")
+PV_CASES = [(col("as_boolean"), Literal.ofBoolean(False), Literal.ofNull("boolean"), 1),
+            (col("as_byte"), Literal.ofByte(1), Literal.ofNull("byte"), 1),
+            (col("as_short"), Literal.ofShort(1), Literal.ofNull("short"), 1),
+            (col("as_int"), Literal.ofInt(1), Literal.ofNull("integer"), 1),
+            (col("as_long"), Literal.ofLong(1), Literal.ofNull("long"), 1),
+            (col("as_float"), Literal.ofFloat(1), Literal.ofNull("float"), 1),
+            (col("as_double"), Literal.ofDouble(1), Literal.ofNull("double"), 1),
+            (col("as_date"), Literal.ofDate(18878), Literal.ofNull("date"), 2),
+            (col("as_string"), Literal.ofString("1"), Literal.ofNull("string"), 1),
+            (col("as_timestamp"), Literal.ofTimestamp(1631099471000000), Literal.ofNull("timestamp"), 2),
+            (col("as_big_decimal"), Literal.ofDecimal(1, 1, 0), Literal.ofNull("decimal(1,0)"), 1)]
+# :99-160 (combinations; the data-column halves only add a data filter, so the partition side decides)
+PV_COMBOS = [(And(cmp(">=", col("as_float"), Literal.ofFloat(-200)), cmp("=", col("as_date"), Literal.ofDate(18878))), 2),
+             (Or(cmp("=", col("as_float"), Literal.ofFloat(0)), cmp("=", col("as_int"), Literal.ofInt(1))), 2),
+             (cmp("=", col("as_float"), Literal.ofFloat(0)), 1),
+             (cmp("=", col("as_float"), Literal.ofFloat(234)), 0)]
+# :197-255 on data-reader-timestamp_ntz[-name-mode|-id-mode]: files (not rows) per predicate
+NTZ_TABLES = ["data-reader-timestamp_ntz", "data-reader-timestamp_ntz-name-mode", "data-reader-timestamp_ntz-id-mode"]
+NTZ_CASES = [(cmp("=", col("tsNtzPartition"), Literal.ofTimestampNtz(1637202600123456)), 1),
+             (cmp("=", col("tsNtzPartition"), Literal.ofNull("timestamp_ntz")), 0),
+             (cmp(">=", col("tsNtzPartition"), Literal.ofTimestampNtz(1373043660123456)), 3),
+             (Predicate("IS_NULL", col("tsNtzPartition")), 1)]
+
+
+def test_oracle_partition_values_golden():
+    for c, value, null, n in PV_CASES:
+        assert len(oracle_files(PV_TABLE, cmp("=", c, value))[0]) == n, c
+        assert oracle_files(PV_TABLE, cmp("=", c, null))[0] == [], c
+    for pred, n in PV_COMBOS:
+        assert len(oracle_files(PV_TABLE, pred)[0]) == n, pred
+    for name in NTZ_TABLES:
+        for pred, n in NTZ_CASES:
+            assert len(oracle_files(os.path.join(TABLES, name), pred)[0]) == n, (name, pred)
+
+
+@pytest.mark.gpu
+def test_gpu_partition_values_golden():
+    from delta_amd import kernel as K
+    eng = K.GpuEngine()
+    preds = [cmp("=", c, v) for c, value, null, _ in PV_CASES for v in (value, null)] + [p for p, _ in PV_COMBOS]
+    for pred in preds:
+        assert _gpu_files(PV_TABLE, pred, eng) == oracle_files(PV_TABLE, pred), pred
+    for name in NTZ_TABLES:
+        root = os.path.join(TABLES, name)
+        for pred, _ in NTZ_CASES:
+            assert _gpu_files(root, pred, eng) == oracle_files(root, pred), (name, pred)
+    eng.close()
+
+
+# Float.parseFloat / Double.parseDouble values (PartitionValueEvaluator.java:93-100)
+FLOAT_PVS = [{"p": "1.0"}, {"p": "-0.0"}, {"p": "0"}, {"p": "NaN"}, {"p": "Infinity"}, {"p": "-Infinity"},
+             {"p": "1e50"}, {"p": "-1e-50"}, {"p": " 1.5f "}, {"p": "16777217"}, {"p": "0.1"}, {"p": None},
+             {"p": "+.5e1D"}, {"p": "3.4028235677973366E38"}]
+FLOAT_PREDICATES = [cmp("=", col("p"), Literal.ofFloat(1.0)), cmp("<", col("p"), Literal.ofFloat(0.0)),
+                    cmp(">=", col("p"), Literal.ofFloat(-0.0)), cmp("=", col("p"), Literal.ofFloat(float("nan"))),
+                    cmp(">", col("p"), Literal.ofFloat(3e38)), cmp("=", col("p"), Literal.ofFloat(16777216)),
+                    cmp("=", col("p"), Literal.ofDouble(0.1)), cmp("<", Literal.ofFloat(1.25), col("p")),
+                    cmp("IS NOT DISTINCT FROM", col("p"), Literal.ofFloat(float("inf"))),
+                    cmp("IS NOT DISTINCT FROM", col("p"), Literal.ofNull("float")),
+                    cmp("=", col("p"), Literal.ofInt(5)), Predicate("NOT", cmp("<=", col("p"), Literal.ofFloat(1.5)))]
+FLOAT_BAD_PVS = ["x", "", "1e", "NaNf", ".", "1.0.0", "Inf", "--1"]
+
+
+def test_oracle_float_partition_values(tmp_path):
+    from oracle import partitions as opp
+    root = str(tmp_path / "t")
+    _write_pv_table(root, FLOAT_PVS, "float")
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in FLOAT_PREDICATES]
+    # worked by hand: "-0.0" and "-1e-50" are -0.0f (below 0.0f); "1e50" overflows to Infinity while
+    # 3.4028235677973366E38 stays Float.MAX_VALUE (below the overflow tie); NaN is above everything;
+    # 16777217 rounds to 2^24; 0.1f widened to double is not 0.1d; the int literal 5 widens to 5.0f
+    assert got == [[0], [1, 5, 7], [0, 1, 2, 3, 4, 6, 7, 8, 9, 10, 12, 13], [3], [3, 4, 6, 13], [9], [],
+                   [3, 4, 6, 8, 9, 12, 13],
+                   [4, 6], [11], [12], [3, 4, 6, 9, 12, 13]]
+    for i, bad in enumerate(FLOAT_BAD_PVS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "float")
+        with pytest.raises(opp.PartitionValueError):
+            oracle_files(r, FLOAT_PREDICATES[0])
+
+
+@pytest.mark.gpu
+def test_gpu_float_partition_values(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    eng = K.GpuEngine()
+    for typ in ("float", "double"):
+        root = str(tmp_path / typ)
+        _write_pv_table(root, FLOAT_PVS, typ)
+        for pred in FLOAT_PREDICATES:
+            assert _gpu_files(root, pred, eng) == oracle_files(root, pred), (typ, pred)
+    root = str(tmp_path / "int")
+    _write_pv_table(root, [{"p": "16777217"}, {"p": "16777218"}, {"p": "-3"}, {"p": None}], "integer")
+    for pred in (cmp("=", col("p"), Literal.ofFloat(16777216)), cmp(">", col("p"), Literal.ofDouble(-2.5)),
+                 cmp("<", col("p"), Literal.ofFloat(float("nan")))):
+        assert _gpu_files(root, pred, eng) == oracle_files(root, pred), pred
+    for i, bad in enumerate(FLOAT_BAD_PVS):
+        r = str(tmp_path / ("b%d" % i))
+        _write_pv_table(r, [{"p": "1"}, {"p": bad}], "float")
+        with pytest.raises(DkError, match="partition"):
+            _gpu_files(r, FLOAT_PREDICATES[0], eng)
+    eng.close()
+
+
+BOOL_PVS = [{"p": "true"}, {"p": "TRUE"}, {"p": "false"}, {"p": "yes"}, {"p": ""}, {"p": None}, {"p": "True "}]
+BOOL_PREDICATES = [cmp("=", col("p"), Literal.ofBoolean(True)), cmp("<", col("p"), Literal.ofBoolean(True)),
+                   Predicate("NOT", cmp("=", col("p"), Literal.ofBoolean(False)))]
+# java.sql.Timestamp.valueOf: lenient field rollover, 1-2 digit month/day, optional 1-9 digit fraction
+TS_PVS = [{"p": "2021-09-08 11:11:11"}, {"p": "2021-9-8 11:11:11.5"}, {"p": "2021-09-07 35:11:11"},
+          {"p": "2021-09-08 11:11:10.999999999"}, {"p": None}, {"p": " 2021-09-08 11:11:11.000001 "},
+          {"p": "1969-12-31 23:59:59.9999995"}, {"p": "2021-02-30 00:00:00"}]
+TS_PREDICATES = [cmp("=", col("p"), Literal.ofTimestamp(1631099471000000)),
+                 cmp(">", col("p"), Literal.ofTimestamp(1631099471000000)),
+                 cmp("<", col("p"), Literal.ofTimestamp(0)),
+                 cmp("=", col("p"), Literal.ofTimestamp(1614643200000000))]
+TS_BAD_PVS = ["2021-09-08T11:11:11", "2021-09-08 11:11", "2021-09-08", "x", "2021-09-08 11:11:11.", "1500-01-01 00:00:00",
+              "2021-13-01 00:00:00", "2021-09-08 11:11:11.1234567890"]
+
+
+def test_oracle_bool_timestamp_partition_values(tmp_path):
+    from oracle import partitions as opp
+    root = str(tmp_path / "b")
+    _write_pv_table(root, BOOL_PVS, "boolean")
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in BOOL_PREDICATES]
+    assert got == [[0, 1], [2, 3, 4, 6], [0, 1]]          # "True " is not "true": parseBoolean does not trim
+    root = str(tmp_path / "t")
+    _write_pv_table(root, TS_PVS, "timestamp")
+    got = [sorted(int(r[0].decode()[1:-8]) for r in oracle_files(root, p)[0]) for p in TS_PREDICATES]
+    # row 2: 35:11:11 on the 7th rolls over to the 8th 11:11:11; row 6 truncates toward zero to 0
+    assert got == [[0, 2], [1, 5], [], [7]]
+    for i, bad in enumerate(TS_BAD_PVS):
+        r = str(tmp_path / ("x%d" % i))
+        _write_pv_table(r, [{"p": "2021-09-08 11:11:11"}, {"p": bad}], "timestamp")
+        with pytest.raises(opp.PartitionValueError):
+            oracle_files(r, TS_PREDICATES[0])
+
+
+@pytest.mark.gpu
+def test_gpu_bool_timestamp_partition_values(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    eng = K.GpuEngine()
+    root = str(tmp_path / "b")
+    _write_pv_table(root, BOOL_PVS, "boolean")
+    for pred in BOOL_PREDICATES:
+        assert _gpu_files(root, pred, eng) == oracle_files(root, pred), pred
+    for typ in ("timestamp", "timestamp_ntz"):
+        root = str(tmp_path / typ)
+        _write_pv_table(root, TS_PVS, typ)
+        lit = Literal.ofTimestamp if typ == "timestamp" else Literal.ofTimestampNtz
+        for p in TS_PREDICATES:
+            pred = cmp(p.name, p.children[0], lit(p.children[1].value))
+            assert _gpu_files(root, pred, eng) == oracle_files(root, pred), (typ, pred)
+    for i, bad in enumerate(TS_BAD_PVS):
+        r = str(tmp_path / ("x%d" % i))
+        _write_pv_table(r, [{"p": "2021-09-08 11:11:11"}, {"p": bad}], "timestamp")
+        with pytest.raises(DkError, match="partition"):
+            _gpu_files(r, TS_PREDICATES[0], eng)
     eng.close()

@@ -3,8 +3,10 @@
 Pinned to the reference's own expectations on its golden tables (KDT = kernel-defaults/src/test/scala/
 io/delta/kernel/defaults):
   ScanSuite.scala:1150-1196  basic data skipping for all types (+ column mapping name/id, checkpoint):
-                             hits / misses for int, long, byte, short, date, string and decimal (the
-                             types the GPU evaluator decodes; float/double filters are refused)
+                             hits / misses for int, long, byte, short, float, double, date, string
+                             and decimal
+  ScanSuite.scala:1198-1212  implicit casting (short column vs float literal, float column vs short)
+  ScanSuite.scala:846-887    float / double columns with float literals (Spark-style stats)
   ScanSuite.scala:1233-1239  filter on a non-existent column -> no skipping
   ScanSuite.scala:1243-1253  AND of two data columns -> 1 file
   ScanSuite.scala:1255-1267  stats collected changing across versions -> 1 / 2 / 1 files
@@ -52,6 +54,8 @@ def all_types_hits_misses():
     cases = [(name, lit(0), lit(-1), lit(1)) for name, lit in INTEGRAL.items()] + [("as_date",) + DATES]
     cases.append(("as_string", Literal.ofString("0"), Literal.ofString("!"), Literal.ofString("1")))   # :1157
     cases.append(("as_big_decimal",) + tuple(Literal.ofDecimal(v, 1, 0) for v in (0, -1, 1)))        # :1162-1164
+    cases.append(("as_float",) + tuple(Literal.ofFloat(v) for v in (0, -1, 1)))                      # :1155
+    cases.append(("as_double",) + tuple(Literal.ofDouble(v) for v in (0, -1, 1)))                    # :1156
     for name, value, small, big in cases:
         c = col(name)
         misses += [cmp("=", c, small), cmp(">", c, value), cmp(">=", c, big), cmp("<", c, value),
@@ -187,8 +191,7 @@ def test_comparator_types(coltype, lit, ok):
 
 def test_compile_refuses_unsupported():
     leaves = {("f",): ("float", ("f",)), ("s",): ("string", ("s",)), ("a",): ("long", ("a",))}
-    for p in (cmp("=", col("f"), Literal(0.0, "float")), cmp("=", col("s"), Literal.ofInt(1)),
-              cmp("=", col("a"), Literal.ofString("1")), cmp("=", col("a"), Literal(0.5, "double"))):
+    for p in (cmp("=", col("s"), Literal.ofInt(1)), cmp("=", col("a"), Literal.ofString("1"))):
         node = sk.construct(p, leaves)
         assert node is not None
         with pytest.raises(sk.UnsupportedSkipping):
@@ -197,6 +200,25 @@ def test_compile_refuses_unsupported():
     paths, types, ops = sk.compile_program(node, leaves)
     assert paths == [("minValues", "a"), ("maxValues", "a")] and types == [0, 0]
     assert [o[0] for o in ops] == [sk.OP_STAT, sk.OP_LIT, sk.OP_LE, sk.OP_STAT, sk.OP_LIT, sk.OP_GE, sk.OP_AND]
+
+
+def test_compile_float_comparisons():
+    """Float / double comparisons compile to exact thresholds (delta_amd/binfloat.py): a float stat
+    gets OP_FCMP against the rounding-cell edge, an integral stat widened to float integer bounds."""
+    leaves = {("f",): ("float", ("f",)), ("a",): ("long", ("a",)), ("d",): ("double", ("d",))}
+    paths, types, ops = sk.compile_program(sk.construct(cmp("<", col("f"), Literal.ofFloat(1.5)), leaves), leaves)
+    assert types == [9] and [o[0] for o in ops] == [sk.OP_STAT, sk.OP_FCMP]
+    # round_float(x) < 1.5f  <=>  x < 1.5 - 2^-24 (the tie goes to the even neighbour 1.5)
+    assert ops[1][1] & 15 == sk.FC_LT and ops[1][2] == b"1.499999940395355224609375"
+    assert ops[1][1] >> 4 == 0b100                       # NaN: false, +Inf: false, -Inf: true
+    # long column = float literal 2^24 + 1 (stored as 16777216f): min <= V holds for the longs that
+    # round to at most 16777216f (x <= 16777217, the tie rounds to even), max >= V for x >= 16777216
+    _, _, ops = sk.compile_program(sk.construct(cmp("=", col("a"), Literal.ofFloat(16777217)), leaves), leaves)
+    assert [(o[0], o[2]) for o in ops if o[0] in (sk.OP_LIT, sk.OP_LE, sk.OP_GE)] == \
+        [(sk.OP_LIT, 16777217), (sk.OP_LE, 0), (sk.OP_LIT, 16777216), (sk.OP_GE, 0)]
+    # double column vs NaN literal: < holds for every non-NaN value
+    _, _, ops = sk.compile_program(sk.construct(cmp("<", col("d"), Literal.ofDouble(float("nan"))), leaves), leaves)
+    assert ops[1][0] == sk.OP_FCMP and ops[1][1] & 15 == sk.FC_ALL and ops[1][1] >> 4 == 0b110
 
 
 def test_oracle_date_decoding_rules():
@@ -222,7 +244,7 @@ def test_oracle_date_decoding_rules():
 def test_pack_layout():
     from delta_amd._lib import dk_skip_program
     import ctypes
-    assert ctypes.sizeof(dk_skip_program) == 4 + 32 + 32 + 128 + 128 + 512 + 4 + 256 + 256 + 512
+    assert ctypes.sizeof(dk_skip_program) == 4 + 32 + 32 + 128 + 128 + 4096 + 4 + 256 + 256 + 512
     leaves = {("s", "x"): ("short", ("col-s", "col-x"))}
     prog = sk.pack(sk.compile_program(sk.construct(cmp(">", col("s", "x") if False else Column("s", "x"),
                                                        Literal.ofShort(3)), leaves), leaves), dk_skip_program)
@@ -771,4 +793,114 @@ def test_gpu_timestamp_ntz_parity(tmp_path):
         _write_edge_table(b, [NTZ_SPARK_STATS, bad], NTZ_COLUMNS)
         with pytest.raises(DkError, match="data skipping"):
             _gpu_files(b, NTZ_HITS[0], eng)
+    eng.close()
+
+
+# ---------------------------------------------------------------- float / double
+def test_oracle_implicit_casting(tmp_path):
+    """ScanSuite.scala:1198-1212 on the golden table (short column vs float literal and back)."""
+    root = os.path.join(TABLES, "data-skipping-basic-stats-all-types")
+    for p in (cmp("=", col("as_short"), Literal.ofFloat(0)), cmp("=", col("as_float"), Literal.ofShort(0))):
+        assert oracle_files(root, p)[0], p
+    for p in (cmp("=", col("as_short"), Literal.ofFloat(1)), cmp("=", col("as_float"), Literal.ofShort(1))):
+        assert not oracle_files(root, p)[0], p
+
+
+SPARK_FP_COLUMNS = (("c1", "long"), ("c3", "float"), ("c4", "double"))
+SPARK_FP_STATS = ['{"numRecords":2,"minValues":{"c1":1,"c3":1.0,"c4":1.0},"maxValues":{"c1":2,"c3":2.0,"c4":2.0},'
+                  '"nullCount":{"c1":0,"c3":0,"c4":0}}']
+SPARK_FP_HITS = [cmp("<", col("c3"), Literal.ofFloat(1.5)), cmp(">", col("c4"), Literal.ofFloat(1.0))]
+SPARK_FP_MISSES = [cmp("<", col("c3"), Literal.ofFloat(0.5)), cmp(">", col("c4"), Literal.ofFloat(5.0))]
+
+FP_COLUMNS = (("f", "float"), ("d", "double"), ("i", "long"))
+FP_EDGE_STATS = [
+    '{"numRecords":1,"minValues":{"f":0.1,"d":0.1,"i":16777217},"maxValues":{"f":0.1,"d":0.1,"i":16777217}}',
+    '{"numRecords":1,"minValues":{"f":"NaN","d":"-Infinity","i":-1},"maxValues":{"f":"NaN","d":"+INF","i":1}}',
+    '{"numRecords":1,"minValues":{"f":-0.0,"d":-1E-400,"i":0},"maxValues":{"f":1E-50,"d":-0,"i":0}}',
+    '{"numRecords":1,"minValues":{"f":16777217,"d":9007199254740993,"i":9007199254740993},'
+    '"maxValues":{"f":16777217.000000001,"d":9007199254740993.5,"i":9007199254740993}}',
+    '{"numRecords":1,"minValues":{"f":"\\u004eaN","d":"Infinity"},"maxValues":{"f":"-INF","d":"NaN"}}',
+    '{"numRecords":1,"minValues":{"f":3.4028235677973366E38,"d":1.7976931348623157E308},'
+    '"maxValues":{"f":-3.4028235677973366E38,"d":4.9E-324}}',
+    '{"numRecords":1,"minValues":{"f":1.4999999403953552,"d":1.5},"maxValues":{"f":1.49999994039535522,"d":2}}',
+    None,
+]
+FP_EDGE_PREDICATES = [
+    cmp("=", col("f"), Literal.ofFloat(0.1)),                      # 0.1 rounds to 0.1f
+    cmp("=", col("d"), Literal.ofDouble(0.1)),
+    cmp("=", col("f"), Literal.ofDouble(0.1)),                      # float(0.1) widened != 0.1d
+    cmp("<", col("f"), Literal.ofFloat(float("nan"))),              # everything but NaN is < NaN
+    cmp("=", col("f"), Literal.ofFloat(float("nan"))),
+    cmp(">", col("d"), Literal.ofDouble(float("inf"))),             # only NaN is > +Inf
+    cmp("<", col("d"), Literal.ofDouble(float("-inf"))),
+    cmp("<", col("f"), Literal.ofFloat(0.0)),                       # -0.0 < 0.0 (Float.compare)
+    cmp(">=", col("f"), Literal.ofFloat(-0.0)),
+    cmp("=", col("d"), Literal.ofDouble(-0.0)),                     # -1E-400 rounds to -0.0
+    cmp("=", col("f"), Literal.ofFloat(16777216)),                  # 16777217 rounds (tie) to 2^24
+    cmp(">", col("f"), Literal.ofFloat(16777216)),                  # 16777217.000000001 -> 16777218
+    cmp("=", col("d"), Literal.ofDouble(9007199254740992)),
+    cmp("=", col("i"), Literal.ofFloat(16777216)),                  # long widened to float
+    cmp(">", col("i"), Literal.ofDouble(9007199254740992)),         # long widened to double: tie -> even
+    cmp("<", col("f"), Literal.ofFloat(1.5)),                       # 1.4999999403953552 is the tie
+    cmp(">=", col("d"), Literal.ofDouble(1.7976931348623157e308)),
+    cmp(">", col("d"), Literal.ofDouble(0.0)),                      # 4.9E-324: the smallest subnormal
+    Or(cmp("<", col("f"), Literal.ofFloat(-3e38)), cmp(">", col("f"), Literal.ofFloat(3e38))),
+    Predicate("NOT", cmp("=", col("d"), Literal.ofDouble(1.5))),
+]
+FP_BAD_STATS = ['{"numRecords":1,"minValues":{"f":3.4028235677973367E38}}',     # rounds to +Infinity
+                '{"numRecords":1,"minValues":{"d":1E309}}', '{"numRecords":1,"minValues":{"f":"nan"}}',
+                '{"numRecords":1,"minValues":{"d":"1.5"}}', '{"numRecords":1,"minValues":{"f":true}}',
+                '{"numRecords":1,"minValues":{"d":{"a":1}}}', '{"numRecords":1,"minValues":{"f":"-Inf"}}']
+FP_BAD_PREDICATE = And(cmp("<=", col("f"), Literal.ofFloat(100)), cmp("<=", col("d"), Literal.ofDouble(100)))
+
+
+def test_oracle_float_stats_expected(tmp_path):
+    root = str(tmp_path / "s")
+    _write_edge_table(root, SPARK_FP_STATS, SPARK_FP_COLUMNS)
+    for p in SPARK_FP_HITS:
+        assert oracle_files(root, p)[0], p
+    for p in SPARK_FP_MISSES:
+        assert not oracle_files(root, p)[0], p
+    r = str(tmp_path / "t")
+    _write_edge_table(r, FP_EDGE_STATS, FP_COLUMNS)
+    got = [sorted(int(x[0].decode()[1:-8]) for x in oracle_files(r, p)[0]) for p in FP_EDGE_PREDICATES]
+    # worked by hand from the decoding rules: row 2's "-0.0" is +0.0 (BigDecimal) while -1E-400 rounds
+    # to -0.0; row 3's 16777217 ties to 2^24 and 9007199254740993 to 2^53; row 6's float minimum sits
+    # just below the 1.5f tie; row 5's float extremes stay finite; NaN compares above +Infinity
+    want = [[0, 7], [0, 1, 7], [7], [0, 2, 3, 5, 6, 7], [1, 7], [4, 7], [7], [7], [0, 1, 2, 3, 6, 7],
+            [1, 2, 7], [3, 7], [1, 3, 7], [1, 3, 7], [0, 4, 5, 6, 7], [4, 5, 6, 7], [0, 2, 6, 7], [1, 4, 7],
+            [0, 1, 3, 4, 5, 6, 7], [1, 7], [0, 1, 2, 3, 4, 6, 7]]
+    assert got == want
+    from oracle import skipping as osk
+    for i, bad in enumerate(FP_BAD_STATS):
+        b = str(tmp_path / ("b%d" % i))
+        _write_edge_table(b, [FP_EDGE_STATS[0], bad], FP_COLUMNS)
+        with pytest.raises(osk.StatsDecodeError):
+            oracle_files(b, FP_BAD_PREDICATE)
+
+
+@pytest.mark.gpu
+def test_gpu_float_stats_parity(tmp_path):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    eng = K.GpuEngine()
+    for name in ALL_TYPES[:1]:
+        root = os.path.join(TABLES, name)
+        for p in (cmp("=", col("as_short"), Literal.ofFloat(0)), cmp("=", col("as_float"), Literal.ofShort(0)),
+                  cmp("=", col("as_short"), Literal.ofFloat(1)), cmp("=", col("as_float"), Literal.ofShort(1))):
+            assert _gpu_files(root, p, eng) == oracle_files(root, p), p
+    s = str(tmp_path / "s")
+    _write_edge_table(s, SPARK_FP_STATS, SPARK_FP_COLUMNS)
+    for p in SPARK_FP_HITS + SPARK_FP_MISSES:
+        g = _gpu_files(s, p, eng)
+        assert g == oracle_files(s, p) and bool(g[0]) == (p in SPARK_FP_HITS), p
+    r = str(tmp_path / "t")
+    _write_edge_table(r, FP_EDGE_STATS, FP_COLUMNS)
+    for p in FP_EDGE_PREDICATES:
+        assert _gpu_files(r, p, eng) == oracle_files(r, p), p
+    for i, bad in enumerate(FP_BAD_STATS):
+        b = str(tmp_path / ("b%d" % i))
+        _write_edge_table(b, [FP_EDGE_STATS[0], bad], FP_COLUMNS)
+        with pytest.raises(DkError, match="data skipping"):
+            _gpu_files(b, FP_BAD_PREDICATE, eng)
     eng.close()
