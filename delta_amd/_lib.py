@@ -27,6 +27,11 @@ class dk_part_program(C.Structure):
                 ("lit", C.c_int64 * 64), ("pool", C.c_char * 4096)]
 
 
+class dk_rg_filter(C.Structure):
+    _fields_ = [("n_cols", C.c_int32), ("col_off", C.c_int32 * 8), ("col_len", C.c_int32 * 8), ("n_ops", C.c_int32),
+                ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64), ("lit", C.c_int64 * 64), ("pool", C.c_char * 2048)]
+
+
 class dk_column(C.Structure):
     _fields_ = [("n_rows", C.c_int64), ("n_entries", C.c_int64), ("n_chars", C.c_int64),
                 ("phys", C.c_int32), ("width", C.c_int32), ("max_def", C.c_int32), ("max_rep", C.c_int32),
@@ -49,7 +54,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free", "dk_parquet_open_rg", "dk_parquet_row_groups",
-           "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits"]
+           "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits", "dk_parquet_open_sel",
+           "dk_parquet_prune_row_groups"]
 
 
 def lib(build_if_missing=True):
@@ -71,6 +77,9 @@ def lib(build_if_missing=True):
         "dk_parquet_open_rg": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, P, P,
                                          C.POINTER(P)]),
         "dk_parquet_row_groups": (C.c_int, [C.c_char_p, C.POINTER(I64), I32, C.POINTER(I32)]),
+        "dk_parquet_open_sel": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, P, P,
+                                          C.POINTER(P)]),
+        "dk_parquet_prune_row_groups": (C.c_int, [C.c_char_p, P, P, I32, C.POINTER(I32)]),
         "dk_parquet_row_offset": (I64, [P, I32]),
         "dk_replay_ckpt_selection_bits": (C.c_int, [P, I32, P, I64, I32]),
         "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),

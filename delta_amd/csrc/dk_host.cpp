@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <cmath>
 #include <memory>
 #include <string>
 #include <vector>
@@ -116,14 +117,31 @@ struct DBuf {
 // ------------------------------------------------------------------------------------------------
 // Parquet footer (FileMetaData) + offset index
 // ------------------------------------------------------------------------------------------------
-struct SchemaEl { std::string name; int type = -1, type_length = 0, repetition = 0, num_children = 0; };
+// logical annotation of a leaf as parquet-mr derives it (LogicalType union, else ConvertedType)
+enum : int { LT_NONE = 0, LT_STRING = 1, LT_INT = 2, LT_DATE = 3, LT_OTHER = 4 };
+struct SchemaEl {
+  std::string name;
+  int type = -1, type_length = 0, repetition = 0, num_children = 0;
+  int conv = -1, logical = -1, int_bits = 0, int_signed = 1;
+};
+// Statistics (parquet.thrift): deprecated max(1) / min(2), null_count(3), max_value(5) / min_value(6)
+struct StatsM {
+  bool has_min = false, has_max = false, has_min_value = false, has_max_value = false, has_nulls = false;
+  std::string min, max, min_value, max_value;
+  int64_t null_count = 0;
+};
 struct ColMeta {
   int type = -1, codec = 0;
   int64_t num_values = 0, total_compressed = 0, data_page_offset = 0, dict_page_offset = -1;
   int64_t oi_off = -1; int32_t oi_len = 0;
+  bool has_stats = false;
+  StatsM st;
 };
 struct RowGroupM { int64_t num_rows = 0; std::vector<ColMeta> cols; };
-struct LeafM { std::string path; int phys, type_length, max_def, max_rep, rep_def; };
+struct LeafM {
+  std::string path; int phys, type_length, max_def, max_rep, rep_def;
+  int leaf_rep = 0, lt = LT_NONE, int_bits = 0, int_signed = 1;   // own repetition, logical type
+};
 // A checkpoint file as the decoder sees it: the footer, plus only the byte ranges of the
 // projected column chunks (and their offset indexes), read with pread -- parquet-mr's column
 // projection (ParquetFileReader reads the chunks of the requested schema only). `bytes` holds the
@@ -136,8 +154,10 @@ struct FileM {
   std::vector<uint8_t> bytes;             // packed column-chunk / offset-index bytes
   std::vector<Span> spans;
   int64_t num_rows = 0;                   // rows of the selected row groups
-  int32_t rg_lo = 0, rg_hi = -1;          // selected row groups [rg_lo, rg_hi) (-1: to the end)
+  std::vector<int32_t> sel;               // selected row groups, ascending
   int64_t row0 = 0;                       // file row index of the first selected row
+  std::string created_by;
+  std::vector<int> col_order;             // per leaf: 1 TYPE_DEFINED_ORDER, 0 unset
   std::vector<SchemaEl> schema;
   std::vector<LeafM> leaves;
   std::vector<RowGroupM> rgs;
@@ -151,6 +171,19 @@ static std::string read_string(TReader& t) {
   return s;
 }
 
+static void parse_stats(TReader& t, StatsM& st) {
+  int last = 0, ty, id;
+  while ((id = t.field(&last, &ty))) {
+    if (id == 1 && ty == 8) { st.max = read_string(t); st.has_max = true; }
+    else if (id == 2 && ty == 8) { st.min = read_string(t); st.has_min = true; }
+    else if (id == 3) { st.null_count = t.zigzag(); st.has_nulls = true; }
+    else if (id == 5 && ty == 8) { st.max_value = read_string(t); st.has_max_value = true; }
+    else if (id == 6 && ty == 8) { st.min_value = read_string(t); st.has_min_value = true; }
+    else t.skip(ty);
+    if (t.bad) return;
+  }
+}
+
 static void parse_col_meta(TReader& t, ColMeta& m) {
   int last = 0, ty, id;
   while ((id = t.field(&last, &ty))) {
@@ -161,6 +194,7 @@ static void parse_col_meta(TReader& t, ColMeta& m) {
       case 7: m.total_compressed = t.zigzag(); break;
       case 9: m.data_page_offset = t.zigzag(); break;
       case 11: m.dict_page_offset = t.zigzag(); break;
+      case 12: if (ty == 12) { m.has_stats = true; parse_stats(t, m.st); } else t.skip(ty); break;
       default: t.skip(ty);
     }
     if (t.bad) return;
@@ -245,12 +279,39 @@ static int parse_footer(FileM& f) {
           else if (i2 == 3) s.repetition = (int)t.zigzag();
           else if (i2 == 4) s.name = read_string(t);
           else if (i2 == 5) s.num_children = (int)t.zigzag();
+          else if (i2 == 6) s.conv = (int)t.zigzag();
+          else if (i2 == 10 && t2 == 12) {        // LogicalType union: the set member's field id
+            int l3 = 0, t3, i3;
+            while ((i3 = t.field(&l3, &t3))) {
+              s.logical = i3;
+              if (i3 == 10 && t3 == 12) {         // IntType {bitWidth: byte, isSigned: bool}
+                int l4 = 0, t4, i4;
+                while ((i4 = t.field(&l4, &t4))) {
+                  if (i4 == 1 && t4 == 3) s.int_bits = (int8_t)t.byte();
+                  else if (i4 == 2 && (t4 == 1 || t4 == 2)) s.int_signed = t4 == 1;
+                  else t.skip(t4);
+                  if (t.bad) break;
+                }
+              } else t.skip(t3);
+              if (t.bad) break;
+            }
+          }
           else t.skip(t2);
           if (t.bad) break;
         }
       }
     } else if (id == 3) {
       f.num_rows = t.zigzag();
+    } else if (id == 6 && ty == 8) {
+      f.created_by = read_string(t);
+    } else if (id == 7 && ty == 9) {              // column_orders: list<ColumnOrder union>
+      int et;
+      int n = t.list_header(&et);
+      for (int i = 0; i < n && !t.bad; i++) {
+        int l2 = 0, t2, i2, kind = 0;
+        while ((i2 = t.field(&l2, &t2))) { kind = i2 == 1 ? 1 : 0; t.skip(t2); if (t.bad) break; }
+        f.col_order.push_back(kind);
+      }
     } else if (id == 4 && ty == 9) {
       int et;
       int n = t.list_header(&et);
@@ -300,7 +361,22 @@ static int parse_footer(FileM& f) {
     int rep_def = e.repetition == 2 ? def : top.rep_def;
     std::string path = top.path.empty() ? e.name : top.path + "." + e.name;
     if (e.num_children > 0) st.push_back({e.num_children, def, rep, rep_def, path});
-    else f.leaves.push_back({path, e.type, e.type_length, def, rep, rep_def});
+    else {
+      LeafM L{path, e.type, e.type_length, def, rep, rep_def};
+      L.leaf_rep = e.repetition;
+      // parquet-mr: the LogicalType when set, else the ConvertedType (UTF8 0, DATE 6, INT_8..INT_64
+      // 15..18, UINT_8..UINT_64 11..14)
+      if (e.logical == 1) L.lt = LT_STRING;
+      else if (e.logical == 6) L.lt = LT_DATE;
+      else if (e.logical == 10) { L.lt = LT_INT; L.int_bits = e.int_bits; L.int_signed = e.int_signed; }
+      else if (e.logical > 0) L.lt = LT_OTHER;
+      else if (e.conv == 0) L.lt = LT_STRING;
+      else if (e.conv == 6) L.lt = LT_DATE;
+      else if (e.conv >= 15 && e.conv <= 18) { L.lt = LT_INT; L.int_bits = 8 << (e.conv - 15); }
+      else if (e.conv >= 11 && e.conv <= 14) { L.lt = LT_INT; L.int_bits = 8 << (e.conv - 11); L.int_signed = 0; }
+      else if (e.conv >= 0) L.lt = LT_OTHER;
+      f.leaves.push_back(L);
+    }
   }
   for (auto& rg : f.rgs)
     if (rg.cols.size() != f.leaves.size()) return fail("Error reading Parquet file: " + f.path + " (column count)");
@@ -798,16 +874,306 @@ static int prepare(dk_parquet* p) {
 
 // Select row groups [lo, hi) of a parsed file (hi < 0: to the end): the file then reads as just
 // those rows (num_rows, row0) -- a shard of a checkpoint part, or row-group pruning.
+static int select_row_groups(FileM& f, const std::vector<int32_t>& groups) {
+  const int32_t n = (int32_t)f.rgs.size();
+  for (size_t i = 0; i < groups.size(); i++)
+    if (groups[i] < 0 || groups[i] >= n || (i && groups[i] <= groups[i - 1]))
+      return fail("Error reading Parquet file: " + f.path + " (row groups out of range)");
+  f.sel = groups;
+  f.row0 = 0; f.num_rows = 0;
+  for (int32_t g = 0; g < (groups.empty() ? n : groups[0]); g++) f.row0 += f.rgs[g].num_rows;
+  for (int32_t g : groups) f.num_rows += f.rgs[g].num_rows;
+  return 0;
+}
+
 static int select_row_groups(FileM& f, int32_t lo, int32_t hi) {
   const int32_t n = (int32_t)f.rgs.size();
   if (hi < 0) hi = n;
   if (lo < 0 || lo > hi || hi > n) return fail("Error reading Parquet file: " + f.path + " (row groups out of range)");
-  f.rg_lo = lo; f.rg_hi = hi;
-  f.row0 = 0; f.num_rows = 0;
-  for (int32_t g = 0; g < n; g++) {
-    if (g < lo) f.row0 += f.rgs[g].num_rows;
-    else if (g < hi) f.num_rows += f.rgs[g].num_rows;
+  std::vector<int32_t> g;
+  for (int32_t i = lo; i < hi; i++) g.push_back(i);
+  return select_row_groups(f, g);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Row-group pruning of checkpoint parts and sidecars (the checkpoint predicate, ActionsIterator.java:
+// 336-351, handed to DefaultParquetHandler -> ParquetFileReader.java:111-132). The Kernel predicate
+// is converted as ParquetFilterUtils.toParquetFilter does (KD/internal/parquet/ParquetFilterUtils.java:
+// 63-440: comparators need a column and a non-null literal of a compatible type -- a literal on the
+// left is swapped without flipping the operator --, AND keeps a convertible side, OR needs both,
+// NOT wraps, IS_NULL / IS_NOT_NULL become eq / notEq(null); predicates on missing or repeated
+// columns and anything else are dropped), then evaluated per row group by parquet-mr 1.12.3's
+// StatisticsFilter (after LogicalInverseRewriter pushes NOT down) over the footer statistics as
+// ParquetMetadataConverter.fromParquetStatisticsInternal reads them (min_value / max_value when the
+// column has TYPE_DEFINED_ORDER or they are equal; the deprecated min / max only for signed sort
+// orders and uncorrupted writers; float / double stats with a NaN carry no min / max, a +0.0 min
+// reads as -0.0 and a -0.0 max as +0.0).
+// ------------------------------------------------------------------------------------------------
+namespace {
+enum : int { RF_COL = 0, RF_LIT = 1, RF_NULL = 2, RF_EQ = 3, RF_LT = 4, RF_LE = 5, RF_GT = 6, RF_GE = 7, RF_AND = 8,
+             RF_OR = 9, RF_NOT = 10, RF_ISNULL = 11, RF_ISNOTNULL = 12, RF_UNSUPPORTED = 13 };
+// literal types (Kernel DataType of the literal)
+enum : int { RL_LONG = 0, RL_INT = 1, RL_SHORT = 2, RL_BYTE = 3, RL_DATE = 4, RL_FLOAT = 5, RL_DOUBLE = 6, RL_BOOL = 7,
+             RL_STRING = 8, RL_OTHER = 9 };
+// parquet-mr filter node (after conversion); op: RF_EQ..RF_GE, RF_AND/OR/NOT, 20 = notEq
+constexpr int PF_NOTEQ = 20;
+struct PNode {
+  int op = 0, leaf = -1, a = -1, b = -1;
+  bool null_value = false;
+  int64_t iv = 0; double dv = 0; std::string bv;   // the value in the column's primitive type
+};
+struct PItem { int kind = 0; int col = -1; int lt = 0; int64_t lit = 0; std::string str; int node = -1; };  // kind 0 col, 1 lit, 2 null lit, 3 filter (node -1: none)
+
+int cmp_signed(int64_t a, int64_t b) { return a < b ? -1 : a > b ? 1 : 0; }
+int cmp_unsigned(uint64_t a, uint64_t b) { return a < b ? -1 : a > b ? 1 : 0; }
+int cmp_float(double a, double b) {                 // Float.compare / Double.compare
+  const bool an = a != a, bn = b != b;
+  if (an || bn) return an && bn ? 0 : an ? 1 : -1;
+  if (a < b) return -1;
+  if (a > b) return 1;
+  if (a == 0 && b == 0) { const bool sa = std::signbit(a), sb = std::signbit(b); return sa == sb ? 0 : sa ? -1 : 1; }
+  return 0;
+}
+int cmp_binary(const std::string& a, const std::string& b) {   // unsigned lexicographic, then length
+  const size_t n = a.size() < b.size() ? a.size() : b.size();
+  for (size_t i = 0; i < n; i++)
+    if ((uint8_t)a[i] != (uint8_t)b[i]) return (uint8_t)a[i] < (uint8_t)b[i] ? -1 : 1;
+  return a.size() < b.size() ? -1 : a.size() > b.size() ? 1 : 0;
+}
+
+// VersionParser + SemanticVersion for CorruptStatistics.shouldIgnoreStatistics (binary columns):
+// ignore stats written by parquet-mr before 1.8.0 (except CDH 5.5-5.x backports), or when created_by
+// is missing / unparseable
+bool ignore_binary_stats(const std::string& created_by) {
+  if (created_by.empty()) return true;
+  // "<application> version <semver> (build <hash>)"
+  const size_t sp = created_by.find(" version ");
+  if (sp == std::string::npos) return true;
+  const std::string app = created_by.substr(0, sp);
+  if (app != "parquet-mr") return false;
+  std::string ver = created_by.substr(sp + 9);
+  const size_t end = ver.find(' ');
+  if (end != std::string::npos) ver = ver.substr(0, end);
+  int v[3] = {0, 0, 0};
+  size_t i = 0;
+  for (int k = 0; k < 3; k++) {
+    if (i >= ver.size() || !isdigit((unsigned char)ver[i])) return true;
+    while (i < ver.size() && isdigit((unsigned char)ver[i])) v[k] = v[k] * 10 + (ver[i++] - '0');
+    if (k < 2) { if (i >= ver.size() || ver[i] != '.') return true; i++; }
   }
+  const long sem = v[0] * 1000000L + v[1] * 1000L + v[2];
+  return sem < 1008000L;
+}
+
+struct RGStats {          // parquet-mr Statistics of one column chunk
+  bool has_minmax = false, nulls_set = false;
+  int64_t nulls = 0, value_count = 0;
+  int64_t imin = 0, imax = 0; double dmin = 0, dmax = 0; std::string bmin, bmax;
+  bool empty() const { return !has_minmax && !nulls_set; }
+};
+
+bool decode_stat(const std::string& raw, int phys, int64_t* iv, double* dv, std::string* bv) {
+  if (phys == PT_INT32) { if (raw.size() != 4) return false; int32_t x; memcpy(&x, raw.data(), 4); *iv = x; return true; }
+  if (phys == PT_INT64) { if (raw.size() != 8) return false; int64_t x; memcpy(&x, raw.data(), 8); *iv = x; return true; }
+  if (phys == PT_BOOLEAN) { if (raw.size() != 1) return false; *iv = raw[0] != 0; return true; }
+  if (phys == PT_FLOAT) { if (raw.size() != 4) return false; float x; memcpy(&x, raw.data(), 4); *dv = x; return true; }
+  if (phys == PT_DOUBLE) { if (raw.size() != 8) return false; double x; memcpy(&x, raw.data(), 8); *dv = x; return true; }
+  *bv = raw;
+  return true;
+}
+
+RGStats chunk_stats(const FileM& f, int leaf, const ColMeta& m) {
+  RGStats r;
+  r.value_count = m.num_values;
+  if (!m.has_stats) return r;
+  const LeafM& L = f.leaves[leaf];
+  const StatsM& st = m.st;
+  const bool typed_order = leaf < (int)f.col_order.size() && f.col_order[leaf] == 1;
+  const bool is_bin = L.phys == PT_BYTE_ARRAY || L.phys == PT_FIXED;
+  const bool signed_order = !(is_bin || (L.lt == LT_INT && !L.int_signed));
+  const std::string *mn = nullptr, *mx = nullptr;
+  if (st.has_min_value && st.has_max_value) {
+    if (typed_order || st.min_value == st.max_value) { mn = &st.min_value; mx = &st.max_value; }
+  } else if (st.has_min && st.has_max) {
+    const bool ignore = is_bin && ignore_binary_stats(f.created_by);
+    if (!ignore && (signed_order || st.min == st.max)) { mn = &st.min; mx = &st.max; }
+  }
+  if (mn && mx) {
+    r.has_minmax = decode_stat(*mn, L.phys, &r.imin, &r.dmin, &r.bmin) && decode_stat(*mx, L.phys, &r.imax, &r.dmax, &r.bmax);
+    if (r.has_minmax && (L.phys == PT_FLOAT || L.phys == PT_DOUBLE)) {
+      if (r.dmin != r.dmin || r.dmax != r.dmax) r.has_minmax = false;   // NaN: no usable min / max
+      else {
+        if (cmp_float(r.dmin, 0.0) == 0) r.dmin = -0.0;
+        if (cmp_float(r.dmax, -0.0) == 0) r.dmax = 0.0;
+      }
+    }
+  }
+  if (st.has_nulls) { r.nulls_set = true; r.nulls = st.null_count; }
+  return r;
+}
+
+struct RGFilter {
+  const FileM& f;
+  std::vector<PNode> nodes;
+  int cmp_min(const PNode& n, const RGStats& s) const {   // comparator().compare(min, value)
+    const LeafM& L = f.leaves[n.leaf];
+    if (L.phys == PT_FLOAT || L.phys == PT_DOUBLE) return cmp_float(s.dmin, n.dv);
+    if (L.phys == PT_BYTE_ARRAY) return cmp_binary(s.bmin, n.bv);
+    if (L.lt == LT_INT && !L.int_signed) return L.phys == PT_INT32 ? cmp_unsigned((uint32_t)s.imin, (uint32_t)n.iv) : cmp_unsigned((uint64_t)s.imin, (uint64_t)n.iv);
+    return cmp_signed(s.imin, n.iv);
+  }
+  int cmp_max(const PNode& n, const RGStats& s) const {
+    const LeafM& L = f.leaves[n.leaf];
+    if (L.phys == PT_FLOAT || L.phys == PT_DOUBLE) return cmp_float(s.dmax, n.dv);
+    if (L.phys == PT_BYTE_ARRAY) return cmp_binary(s.bmax, n.bv);
+    if (L.lt == LT_INT && !L.int_signed) return L.phys == PT_INT32 ? cmp_unsigned((uint32_t)s.imax, (uint32_t)n.iv) : cmp_unsigned((uint64_t)s.imax, (uint64_t)n.iv);
+    return cmp_signed(s.imax, n.iv);
+  }
+  // StatisticsFilter.canDrop with LogicalInverseRewriter's NOT push-down (neg)
+  bool can_drop(int id, int g, bool neg) const {
+    const PNode& n = nodes[id];
+    if (n.op == RF_NOT) return can_drop(n.a, g, !neg);
+    if (n.op == RF_AND || n.op == RF_OR) {
+      const bool is_and = (n.op == RF_AND) != neg;            // not(and) = or(not, not)
+      const bool l = can_drop(n.a, g, neg), r = can_drop(n.b, g, neg);
+      return is_and ? (l || r) : (l && r);
+    }
+    int op = n.op;
+    if (neg) op = op == RF_EQ ? PF_NOTEQ : op == PF_NOTEQ ? RF_EQ : op == RF_LT ? RF_GE : op == RF_LE ? RF_GT
+                : op == RF_GT ? RF_LE : RF_LT;
+    const RGStats s = chunk_stats(f, n.leaf, f.rgs[g].cols[n.leaf]);
+    if (s.empty()) return false;
+    const bool all_nulls = s.nulls_set && s.nulls == s.value_count;
+    if (op == RF_EQ) {
+      if (n.null_value) return s.nulls_set ? s.nulls == 0 : false;
+      if (all_nulls) return true;
+      if (!s.has_minmax) return false;
+      return cmp_min(n, s) > 0 || cmp_max(n, s) < 0;
+    }
+    if (op == PF_NOTEQ) {
+      if (n.null_value) return all_nulls;
+      if (s.nulls_set && s.nulls > 0) return false;
+      if (!s.has_minmax) return false;
+      return cmp_min(n, s) == 0 && cmp_max(n, s) == 0;
+    }
+    if (all_nulls) return true;
+    if (!s.has_minmax) return false;
+    if (op == RF_LT) return cmp_min(n, s) >= 0;
+    if (op == RF_LE) return cmp_min(n, s) > 0;
+    if (op == RF_GT) return cmp_max(n, s) <= 0;
+    return cmp_max(n, s) < 0;                                  // RF_GE
+  }
+};
+
+// ParquetFilterUtils.canUseLiteral
+bool can_use_literal(int lt, int64_t v, const LeafM& L) {
+  const bool integer = lt == RL_BYTE || lt == RL_SHORT || lt == RL_INT || lt == RL_DATE ||
+                       (lt == RL_LONG && (int64_t)(int32_t)v == v);
+  const bool lng = lt == RL_LONG || lt == RL_BYTE || lt == RL_SHORT || lt == RL_INT || lt == RL_DATE;
+  switch (L.phys) {
+    case PT_BOOLEAN: return lt == RL_BOOL;
+    case PT_INT32: return integer && (L.lt == LT_NONE || (L.lt == LT_INT && L.int_bits <= 32) || L.lt == LT_DATE);
+    case PT_INT64: return lng && (L.lt == LT_NONE || (L.lt == LT_INT && L.int_bits <= 64));
+    case PT_FLOAT: return lt == RL_FLOAT;
+    case PT_DOUBLE: return lt == RL_DOUBLE;
+    case PT_BYTE_ARRAY: return lt == RL_STRING && (L.lt == LT_NONE || L.lt == LT_STRING);
+    default: return false;
+  }
+}
+}  // namespace
+
+extern "C" int dk_parquet_prune_row_groups(const char* path, const dk_rg_filter* flt, uint8_t* keep, int32_t cap,
+                                           int32_t* n) {
+  FileM f;
+  f.path = path ? path : "";
+  if (read_footer(f) || parse_footer(f)) return 1;
+  *n = (int32_t)f.rgs.size();
+  for (int32_t g = 0; g < *n && g < cap; g++) keep[g] = 1;
+  if (!flt) return 0;
+  if (flt->n_cols < 0 || flt->n_cols > 8 || flt->n_ops < 0 || flt->n_ops > 64) return fail("dk_parquet_prune_row_groups: bad filter");
+  std::vector<int> col_leaf(flt->n_cols, -1);       // filter column -> non-repeated leaf of this file
+  for (int c = 0; c < flt->n_cols; c++) {
+    if (flt->col_off[c] < 0 || flt->col_len[c] < 0 || flt->col_off[c] + flt->col_len[c] > (int)sizeof(flt->pool))
+      return fail("dk_parquet_prune_row_groups: bad column");
+    const std::string name(flt->pool + flt->col_off[c], flt->col_len[c]);
+    for (size_t li = 0; li < f.leaves.size(); li++)
+      if (f.leaves[li].path == name && f.leaves[li].leaf_rep != 2) col_leaf[c] = (int)li;
+  }
+  RGFilter F{f, {}};
+  std::vector<PItem> st;
+  auto filt = [&](int node) { PItem it; it.kind = 3; it.node = node; return it; };
+  for (int k = 0; k < flt->n_ops; k++) {
+    const int op = flt->op[k];
+    if (op == RF_COL) {
+      if (flt->arg[k] < 0 || flt->arg[k] >= flt->n_cols) return fail("dk_parquet_prune_row_groups: bad column ref");
+      PItem it; it.kind = 0; it.col = col_leaf[flt->arg[k]]; st.push_back(it);
+    } else if (op == RF_LIT) {
+      PItem it; it.kind = 1; it.lt = flt->arg[k]; it.lit = flt->lit[k];
+      if (it.lt == RL_STRING) {
+        const int64_t off = flt->lit[k] & 0xffffffffll, len = flt->lit[k] >> 32;
+        if (off < 0 || len < 0 || off + len > (int64_t)sizeof(flt->pool)) return fail("dk_parquet_prune_row_groups: bad literal");
+        it.str.assign(flt->pool + off, (size_t)len);
+      }
+      st.push_back(it);
+    } else if (op == RF_NULL) {
+      PItem it; it.kind = 2; st.push_back(it);
+    } else if (op == RF_UNSUPPORTED) {
+      st.push_back(filt(-1));
+    } else if (op >= RF_EQ && op <= RF_GE) {
+      if (st.size() < 2) return fail("dk_parquet_prune_row_groups: stack underflow");
+      PItem b = st.back(); st.pop_back();
+      PItem a = st.back(); st.pop_back();
+      if (a.kind != 0 && b.kind == 0) std::swap(a, b);            // literal first: swapped, operator kept
+      int node = -1;
+      if (a.kind == 0 && b.kind == 1 && a.col >= 0) {
+        const LeafM& L = f.leaves[a.col];
+        if (can_use_literal(b.lt, b.lit, L) && (L.phys != PT_BOOLEAN || op == RF_EQ)) {
+          PNode pn; pn.op = op; pn.leaf = a.col;
+          if (L.phys == PT_FLOAT) { double d; memcpy(&d, &b.lit, 8); pn.dv = (float)d; }
+          else if (L.phys == PT_DOUBLE) memcpy(&pn.dv, &b.lit, 8);
+          else if (L.phys == PT_BYTE_ARRAY) pn.bv = b.str;
+          else pn.iv = L.phys == PT_INT32 ? (int64_t)(int32_t)b.lit : b.lit;
+          F.nodes.push_back(pn);
+          node = (int)F.nodes.size() - 1;
+        }
+      }
+      st.push_back(filt(node));
+    } else if (op == RF_ISNULL || op == RF_ISNOTNULL) {
+      if (st.empty()) return fail("dk_parquet_prune_row_groups: stack underflow");
+      PItem a = st.back(); st.pop_back();
+      int node = -1;
+      if (a.kind == 0 && a.col >= 0) {
+        const int ph = f.leaves[a.col].phys;
+        if (ph == PT_BOOLEAN || ph == PT_INT32 || ph == PT_INT64 || ph == PT_FLOAT || ph == PT_DOUBLE || ph == PT_BYTE_ARRAY) {
+          PNode pn; pn.op = op == RF_ISNULL ? RF_EQ : PF_NOTEQ; pn.leaf = a.col; pn.null_value = true;
+          F.nodes.push_back(pn);
+          node = (int)F.nodes.size() - 1;
+        }
+      }
+      st.push_back(filt(node));
+    } else if (op == RF_AND || op == RF_OR) {
+      if (st.size() < 2) return fail("dk_parquet_prune_row_groups: stack underflow");
+      const PItem b = st.back(); st.pop_back();
+      const PItem a = st.back(); st.pop_back();
+      const int l = a.kind == 3 ? a.node : -1, r = b.kind == 3 ? b.node : -1;
+      int node = -1;
+      if (l >= 0 && r >= 0) { PNode pn; pn.op = op; pn.a = l; pn.b = r; F.nodes.push_back(pn); node = (int)F.nodes.size() - 1; }
+      else if (op == RF_AND) node = l >= 0 ? l : r;
+      st.push_back(filt(node));
+    } else if (op == RF_NOT) {
+      if (st.empty()) return fail("dk_parquet_prune_row_groups: stack underflow");
+      const PItem a = st.back(); st.pop_back();
+      int node = -1;
+      if (a.kind == 3 && a.node >= 0) { PNode pn; pn.op = RF_NOT; pn.a = a.node; F.nodes.push_back(pn); node = (int)F.nodes.size() - 1; }
+      st.push_back(filt(node));
+    } else {
+      return fail("dk_parquet_prune_row_groups: bad opcode");
+    }
+  }
+  if (st.size() != 1) return fail("dk_parquet_prune_row_groups: program must leave one value");
+  const int root = st[0].kind == 3 ? st[0].node : -1;
+  if (root < 0) return 0;                                      // nothing convertible: read everything
+  for (int32_t g = 0; g < *n && g < cap; g++) keep[g] = F.can_drop(root, g, false) ? 0 : 1;
   return 0;
 }
 
@@ -825,8 +1191,47 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
   return dk_parquet_open_rg(e, paths, n_files, leaves, n_leaves, nullptr, nullptr, out);
 }
 
+static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                        int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out);
+
 extern "C" int dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                                   int32_t n_leaves, const int32_t* rg_lo, const int32_t* rg_hi, dk_parquet** out) {
+  if (!rg_lo && !rg_hi) return parquet_open(e, paths, n_files, leaves, n_leaves, nullptr, out);
+  std::vector<std::vector<int32_t>> groups(n_files > 0 ? n_files : 0);
+  for (int32_t fi = 0; fi < n_files; fi++) {
+    FileM f;
+    f.path = paths[fi];
+    if (read_footer(f) || parse_footer(f)) return 1;
+    const int32_t n = (int32_t)f.rgs.size();
+    const int32_t lo = rg_lo ? rg_lo[fi] : 0, hi = rg_hi && rg_hi[fi] >= 0 ? rg_hi[fi] : n;
+    if (lo < 0 || lo > hi || hi > n) return fail("Error reading Parquet file: " + f.path + " (row groups out of range)");
+    for (int32_t g = lo; g < hi; g++) groups[fi].push_back(g);
+  }
+  return parquet_open(e, paths, n_files, leaves, n_leaves, &groups, out);
+}
+
+extern "C" int dk_parquet_open_sel(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                                   int32_t n_leaves, const int32_t* rg_count, const int32_t* rg_list, dk_parquet** out) {
+  if (!rg_count) return parquet_open(e, paths, n_files, leaves, n_leaves, nullptr, out);
+  std::vector<std::vector<int32_t>> groups(n_files > 0 ? n_files : 0);
+  bool all = true;
+  for (int32_t fi = 0, at = 0; fi < n_files; fi++) {
+    if (rg_count[fi] < 0) {                       // every row group of this file
+      FileM f;
+      f.path = paths[fi];
+      if (read_footer(f) || parse_footer(f)) return 1;
+      for (int32_t g = 0; g < (int32_t)f.rgs.size(); g++) groups[fi].push_back(g);
+      continue;
+    }
+    all = false;
+    for (int32_t k = 0; k < rg_count[fi]; k++) groups[fi].push_back(rg_list[at + k]);
+    at += rg_count[fi];
+  }
+  return parquet_open(e, paths, n_files, leaves, n_leaves, all ? nullptr : &groups, out);
+}
+
+static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                        int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out) {
   if (!e) return fail("null engine");
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_parquet> p(new dk_parquet());
@@ -842,13 +1247,13 @@ extern "C" int dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_
     FileM& f = p->files[fi];
     f.path = paths[fi];
     if (read_footer(f) || parse_footer(f)) return 1;
-    if (select_row_groups(f, rg_lo ? rg_lo[fi] : 0, rg_hi ? rg_hi[fi] : -1)) return 1;
+    if (groups ? select_row_groups(f, (*groups)[fi]) : select_row_groups(f, 0, -1)) return 1;
     {   // projection: only the chunks (and offset indexes) of the requested leaves travel to HBM
       std::vector<Span> want;
       for (int li = 0; li < n_leaves; li++) {
         int idx = leaf_index(f, p->leaves[li]);
         if (idx < 0) continue;
-        for (int32_t g = f.rg_lo; g < f.rg_hi; g++) {
+        for (int32_t g : f.sel) {
           const ColMeta& m = f.rgs[g].cols[idx];
           want.push_back({chunk_start(m), m.total_compressed, 0});
           if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= f.size) want.push_back({m.oi_off, m.oi_len, 0});
@@ -873,7 +1278,7 @@ extern "C" int dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_
       int colid = (int)p->h_cols.size();
       // chunks and pages in row-group order; data pages of a column stay contiguous
       std::vector<DPage> dicts;
-      for (int32_t g = f.rg_lo; g < f.rg_hi; g++) {
+      for (int32_t g : f.sel) {
         const ColMeta& m = f.rgs[g].cols[idx];
         c.n_rows += f.rgs[g].num_rows;
         DChunk ck{};

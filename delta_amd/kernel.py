@@ -23,7 +23,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import Column, DkError, check, dk_column, dk_config, dk_part_program, dk_skip_program, lib
+from ._lib import Column, DkError, check, dk_column, dk_config, dk_part_program, dk_rg_filter, dk_skip_program, lib
 
 ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
               "add.size", "add.modificationTime", "add.dataChange",
@@ -83,6 +83,17 @@ class GpuEngine:
         return ParquetSet(self, paths, leaves)
 
 
+def prune_row_groups(path, packed_filter):
+    """Row groups of `path` that survive the checkpoint predicate (dk_parquet_prune_row_groups)."""
+    cap = 4096
+    keep = (C.c_uint8 * cap)()
+    n = C.c_int32()
+    check(lib().dk_parquet_prune_row_groups(path.encode(), C.byref(packed_filter), keep, cap, C.byref(n)))
+    if n.value > cap:
+        raise DkError("%s has more than %d row groups" % (path, cap))
+    return [g for g in range(n.value) if keep[g]]
+
+
 def row_group_rows(path):
     """Row counts of a Parquet file's row groups (footer only)."""
     cap = 4096
@@ -97,13 +108,20 @@ def row_group_rows(path):
 class ParquetSet:
     """A set of Parquet files decoded on the GPU (one batch per file; batches in input order)."""
 
-    def __init__(self, engine: GpuEngine, paths, leaves, row_groups=None):
-        """row_groups: optional [(first, end)] row-group range per file (dk_parquet_open_rg)."""
+    def __init__(self, engine: GpuEngine, paths, leaves, row_groups=None, groups=None):
+        """row_groups: optional [(first, end)] row-group range per file (dk_parquet_open_rg);
+        groups: optional list of row-group indices per file (dk_parquet_open_sel)."""
         self.engine = engine
         self.paths = list(paths)
         self.leaves = list(leaves)
         self._h = C.c_void_p()
-        if row_groups is None:
+        if groups is not None:
+            cnt = (C.c_int32 * max(1, len(groups)))(*[len(g) for g in groups])
+            flat = [g for gs in groups for g in gs]
+            lst = (C.c_int32 * max(1, len(flat)))(*flat)
+            check(lib().dk_parquet_open_sel(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
+                                            len(self.leaves), cnt, lst, C.byref(self._h)))
+        elif row_groups is None:
             check(lib().dk_parquet_open(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
                                         len(self.leaves), C.byref(self._h)))
         else:
@@ -386,10 +404,25 @@ class Snapshot:
             self._manifest = (side, proto, meta)
         return self._manifest
 
-    def _checkpoint_files(self, engine):
+    def _checkpoint_files(self, engine, with_pruning=False):
         """Checkpoint data files in replay order: multi-part parts descending (LogSegment
         ordering); V2 parquet manifest first, then its sidecars in manifest order; a V2 JSON
-        manifest contributes only its sidecars."""
+        manifest contributes only its sidecars. with_pruning: also whether the checkpoint predicate
+        can prune each file's row groups -- multi-part parts and sidecars get it as is; a classic
+        or V2 top-level file gets OR(predicate, sidecar IS NOT NULL), which never converts to a
+        parquet-mr filter (ActionsIterator.java:175-226, 336-351)."""
+        files = self._checkpoint_file_list(engine)
+        if not with_pruning:
+            return files
+        cks = self.log_segment.checkpoints
+        if not cks:
+            return files, []
+        if cks[0].kind == "v2":
+            top = 0 if cks[0].path.endswith(".json") else 1
+            return files, [i >= top for i in range(len(files))]
+        return files, [cks[0].kind == "multipart"] * len(files)
+
+    def _checkpoint_file_list(self, engine):
         cks = self.log_segment.checkpoints
         if not cks:
             return []
@@ -688,19 +721,37 @@ class GpuScan:
         seg = self.snapshot.log_segment
         commits = list(reversed(seg.deltas))
         self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
-        all_files = self.snapshot._checkpoint_files(engine)
-        ranges = None
-        if self.shard:
-            # this rank's contiguous run of checkpoint row groups (delta_amd/shard.py)
-            from .shard import plan_units
-            units = plan_units([row_group_rows(f) for f in all_files], *self.shard)
-            self.ckpt_index = [f for f, _, _ in units]
-            ranges = [(a, b) for _, a, b in units]
+        all_files, prunable = self.snapshot._checkpoint_files(engine, with_pruning=True)
+        # row groups read per file: all, minus those the checkpoint predicate (the partition filter
+        # on add.partitionValues_parsed) proves empty in multi-part parts and sidecars
+        groups = [None] * len(all_files)
+        if self.partition_filter is not None and any(prunable):
+            from . import partitions as pp
+            md = self.snapshot.metadata or {}
+            prog = pp.row_group_filter(self.partition_filter,
+                                       pp.partition_fields(md["schemaString"], md.get("partitionColumns") or []))
+            packed = pp.pack_row_group_filter(prog, dk_rg_filter)
+            for i, f in enumerate(all_files):
+                if prunable[i]:
+                    groups[i] = prune_row_groups(f, packed)
+        if self.shard or any(g is not None for g in groups):
+            # shards: this rank's contiguous run of the surviving row groups (delta_amd/shard.py)
+            rows = [row_group_rows(f) for f in all_files]
+            groups = [list(range(len(r))) if g is None else g for g, r in zip(groups, rows)]
+            if self.shard:
+                from .shard import plan_units
+                units = plan_units([[rows[fi][g] for g in gs] for fi, gs in enumerate(groups)], *self.shard)
+                self.ckpt_index = [f for f, _, _ in units]
+                sel = [groups[f][a:b] for f, a, b in units]
+            else:                                   # a fully pruned file yields no batch at all
+                self.ckpt_index = [i for i, g in enumerate(groups) if g]
+                sel = [groups[i] for i in self.ckpt_index]
         else:
             self.ckpt_index = list(range(len(all_files)))
+            sel = None
         self.ckpt_files = [all_files[i] for i in self.ckpt_index]
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
-        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, ranges) if self.ckpt_files else None
+        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel) if self.ckpt_files else None
         self._rh = C.c_void_p()
         check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
                                      C.byref(self._rh)))

@@ -243,3 +243,101 @@ def pack(program, struct_type):
         p.op[k], p.arg[k], p.lit[k] = op, arg, lit
     p.pool = pool
     return p
+
+
+# ---- checkpoint row-group pruning (ActionsIterator.java:336-351 -> ParquetFileReader.java:111-132) ----
+RF_COL, RF_LIT, RF_NULL, RF_EQ, RF_LT, RF_LE, RF_GT, RF_GE, RF_AND, RF_OR, RF_NOT, RF_ISNULL, RF_ISNOTNULL, \
+    RF_UNSUPPORTED = range(14)
+RL = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "float": 5, "double": 6, "boolean": 7, "string": 8}
+_RF_CMP = {"=": RF_EQ, "<": RF_LT, "<=": RF_LE, ">": RF_GT, ">=": RF_GE}
+
+
+def row_group_filter(pred: Predicate, fields: dict):
+    """The partition filter rewritten onto add.partitionValues_parsed.<physical name>
+    (PartitionUtils.rewritePartitionPredicateOnCheckpointFileSchema, PartitionUtils.java:275-303) as a
+    dk_rg_filter program: (column paths, ops, pool). Conversion to parquet-mr filters and the
+    row-group statistics test happen per file in libdkgpu (dk_parquet_prune_row_groups)."""
+    import struct
+    cols, ops = [], []
+    pool = bytearray()
+
+    def col(c: Column):
+        name = c.names[0].lower()
+        if name not in fields:
+            raise ValueError("%s is not present in metadata" % c.names[0])
+        path = "add.partitionValues_parsed." + fields[name][1]
+        if path not in cols:
+            cols.append(path)
+        ops.append((RF_COL, cols.index(path), 0))
+
+    def lit(x: Literal):
+        if x.value is None:
+            ops.append((RF_NULL, 0, 0))
+        elif x.type == "string":
+            b = x.value.encode("utf-8")
+            ops.append((RF_LIT, RL["string"], len(pool) | (len(b) << 32)))
+            pool.extend(b)
+        elif x.type in ("float", "double"):
+            ops.append((RF_LIT, RL[x.type], struct.unpack("<q", struct.pack("<d", float(x.value)))[0]))
+        elif x.type == "boolean":
+            ops.append((RF_LIT, RL["boolean"], int(bool(x.value))))
+        elif x.type in RL:
+            ops.append((RF_LIT, RL[x.type], int(x.value)))
+        else:
+            ops.append((RF_LIT, 9, 0))                     # timestamp / decimal / ...: not convertible
+
+    def expr(e):
+        if isinstance(e, Column):
+            col(e)
+        elif isinstance(e, Literal):
+            lit(e)
+        else:
+            node(e)
+
+    def node(p: Predicate):
+        n = p.name.lower()
+        c = p.children
+        if n in _RF_CMP and len(c) == 2:
+            expr(c[0])
+            expr(c[1])
+            ops.append((_RF_CMP[n], 0, 0))
+        elif n in ("and", "or") and len(c) == 2:
+            node(c[0])
+            node(c[1])
+            ops.append((RF_AND if n == "and" else RF_OR, 0, 0))
+        elif n == "not" and len(c) == 1:
+            node(c[0])
+            ops.append((RF_NOT, 0, 0))
+        elif n in ("is_null", "is_not_null") and len(c) == 1:
+            expr(c[0])
+            ops.append((RF_ISNULL if n == "is_null" else RF_ISNOTNULL, 0, 0))
+        else:
+            for ch in c:                                    # columns must still exist in metadata
+                if isinstance(ch, Column):
+                    name = ch.names[0].lower()
+                    if name not in fields:
+                        raise ValueError("%s is not present in metadata" % ch.names[0])
+            ops.append((RF_UNSUPPORTED, 0, 0))
+
+    node(pred)
+    if len(cols) > 8 or len(ops) > 64:
+        raise UnsupportedPartitionFilter("partition filter is too large for checkpoint row-group pruning")
+    return cols, ops, bytes(pool)
+
+
+def pack_row_group_filter(program, struct_type):
+    cols, ops, pool = program
+    f = struct_type()
+    pool = bytearray(pool)
+    f.n_cols = len(cols)
+    for i, c in enumerate(cols):
+        b = c.encode("utf-8")
+        f.col_off[i], f.col_len[i] = len(pool), len(b)
+        pool.extend(b)
+    if len(pool) > 2048:
+        raise UnsupportedPartitionFilter("partition filter literals exceed 2 KiB for row-group pruning")
+    f.n_ops = len(ops)
+    for k, (op, arg, lit) in enumerate(ops):
+        f.op[k], f.arg[k], f.lit[k] = op, arg, lit
+    f.pool = bytes(pool)
+    return f

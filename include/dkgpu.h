@@ -81,6 +81,34 @@ int  dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files,
                         const int32_t* rg_hi, dk_parquet** out);
 /* Row counts of a file's row groups from its footer (no device work); *n = number of groups. */
 int  dk_parquet_row_groups(const char* path, int64_t* rows, int32_t cap, int32_t* n);
+/* The same over an explicit ascending list of row groups per file: rg_count[i] groups taken from
+ * rg_list (concatenated over the files), rg_count[i] < 0 = all groups of file i. */
+int  dk_parquet_open_sel(dk_engine* e, const char* const* paths, int32_t n_files,
+                         const char* const* leaves, int32_t n_leaves, const int32_t* rg_count,
+                         const int32_t* rg_list, dk_parquet** out);
+
+/* Row-group pruning predicate: the checkpoint predicate ActionsIterator hands the ParquetHandler for
+ * checkpoint parts and sidecars (KA/internal/replay/ActionsIterator.java:336-351; the partition filter
+ * rewritten onto add.partitionValues_parsed, PartitionUtils.java:275-303), in postfix over leaf
+ * columns. Converted per file as ParquetFilterUtils.toParquetFilter does and evaluated per row group
+ * with parquet-mr's StatisticsFilter over the footer statistics (ParquetFileReader.java:111-132). */
+typedef struct dk_rg_filter {
+  int32_t n_cols;                  /* <= 8 leaf columns, dotted paths in pool                     */
+  int32_t col_off[8];
+  int32_t col_len[8];
+  int32_t n_ops;                   /* <= 64                                                       */
+  int32_t op[64];                  /* 0 COL(arg) 1 LIT(arg = type: 0 long 1 integer 2 short 3 byte
+                                      4 date 5 float 6 double 7 boolean 8 string 9 other; lit = value,
+                                      float / double as the bits of a double, string: pool offset |
+                                      length << 32) 2 NULL 3 = 4 < 5 <= 6 > 7 >= 8 AND 9 OR 10 NOT
+                                      11 IS_NULL 12 IS_NOT_NULL 13 UNSUPPORTED (an unconvertible node) */
+  int32_t arg[64];
+  int64_t lit[64];
+  char pool[2048];
+} dk_rg_filter;
+/* keep[g] = 0 for the row groups of `path` the filter proves empty (filter NULL: keep all). */
+int  dk_parquet_prune_row_groups(const char* path, const dk_rg_filter* filter, uint8_t* keep, int32_t cap,
+                                 int32_t* n);
 int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file);   /* file row of the first selected row */
 int  dk_parquet_decode(dk_parquet* p);                 /* async on the engine stream */
 int  dk_parquet_sync(dk_parquet* p);

@@ -135,6 +135,7 @@ typedef struct {
   int n_rg; int64_t* rg_rows;
   int n_leaves; Leaf* leaves;
   ChunkMeta* chunks; /* n_rg * n_leaves */
+  uint8_t* keep;     /* row groups to read (NULL: all) -- the ParquetHandler's row-group filter */
 } PFile;
 
 static void parse_schema_el(TR* t, SchemaEl* s) {
@@ -212,7 +213,7 @@ static int build_leaves(PFile* f) {
 EXPORT void dkr_close(void* h) {
   PFile* f = (PFile*)h;
   if (!f) return;
-  free(f->schema); free(f->rg_rows); free(f->leaves); free(f->chunks); free(f);
+  free(f->schema); free(f->rg_rows); free(f->leaves); free(f->chunks); free(f->keep); free(f);
 }
 
 EXPORT void* dkr_open(const uint8_t* buf, int64_t len) {
@@ -271,6 +272,14 @@ EXPORT void* dkr_open(const uint8_t* buf, int64_t len) {
 }
 
 EXPORT int64_t dkr_num_rows(void* h) { return ((PFile*)h)->num_rows; }
+/* Read only the row groups with keep[g] != 0 from here on (num_rows becomes their row count). */
+EXPORT void dkr_select_row_groups(void* h, const uint8_t* keep) {
+  PFile* f = (PFile*)h;
+  free(f->keep);
+  f->keep = malloc(f->n_rg ? f->n_rg : 1);
+  f->num_rows = 0;
+  for (int g = 0; g < f->n_rg; g++) { f->keep[g] = keep[g] != 0; if (f->keep[g]) f->num_rows += f->rg_rows[g]; }
+}
 EXPORT int dkr_num_leaves(void* h) { return ((PFile*)h)->n_leaves; }
 EXPORT int dkr_num_row_groups(void* h) { return ((PFile*)h)->n_rg; }
 EXPORT const char* dkr_leaf_path(void* h, int i) { return ((PFile*)h)->leaves[i].path; }
@@ -599,7 +608,7 @@ EXPORT int dkr_read_leaf(void* h, int leaf, dkr_col* out) {
   if (leaf < 0 || leaf >= f->n_leaves) { seterr("bad leaf"); return -1; }
   Leaf* L = &f->leaves[leaf];
   Raw r; memset(&r, 0, sizeof r);
-  for (int g = 0; g < f->n_rg; g++) if (decode_chunk(f, leaf, g, &r)) return -1;
+  for (int g = 0; g < f->n_rg; g++) if ((!f->keep || f->keep[g]) && decode_chunk(f, leaf, g, &r)) return -1;
   int w = phys_width(L->phys, L->type_length);
   if (L->phys == 0) w = 1;
   out->phys = L->phys; out->width = L->phys == 6 ? 0 : w; out->max_def = L->max_def; out->max_rep = L->max_rep; out->rep_def = L->rep_def;

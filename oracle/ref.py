@@ -59,6 +59,7 @@ def lib():
         L.dkr_num_rows.argtypes = [C.c_void_p]
         L.dkr_num_leaves.argtypes = [C.c_void_p]
         L.dkr_num_row_groups.argtypes = [C.c_void_p]
+        L.dkr_select_row_groups.argtypes = [C.c_void_p, C.c_char_p]
         L.dkr_leaf_path.restype = C.c_char_p
         L.dkr_leaf_path.argtypes = [C.c_void_p, C.c_int]
         L.dkr_leaf_info.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_int)]
@@ -143,6 +144,11 @@ class ParquetFile:
         if getattr(self, "_h", None):
             lib().dkr_close(self._h)
             self._h = None
+
+    def select_row_groups(self, keep):
+        """Read only the row groups with keep[g] true (the reader's row-group filter)."""
+        lib().dkr_select_row_groups(self._h, bytes(1 if k else 0 for k in keep))
+        self.num_rows = lib().dkr_num_rows(self._h)
 
     def leaf_index(self, path):
         """Field matching by exact name, then case-insensitive (ParquetSchemaUtils.java:92-119)."""
@@ -533,8 +539,10 @@ def canon_add_from_cols(cols, r):
     return row
 
 
-def decode_checkpoint_file(path, with_stats=False, extra_leaves=()):
+def decode_checkpoint_file(path, with_stats=False, extra_leaves=(), keep=None):
     pf = ParquetFile.open(path)
+    if keep is not None:
+        pf.select_row_groups(keep)
     cols = {}
     for leaf in ADD_LEAVES + ([STATS_LEAF] if with_stats else []) + list(extra_leaves):
         cols[leaf] = pf.read(leaf)
@@ -665,7 +673,12 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
             if not mine and g.kind != "v2":
                 continue
             extra = SIDECAR_LEAVES if g.kind == "v2" else ()
-            pf, cols = decode_checkpoint_file(g.path, with_stats, extra)
+            keep = None
+            if partition is not None and g.kind in ("multipart", "sidecar"):
+                # the checkpoint predicate prunes row groups of parts and sidecars (oracle/rowgroups.py)
+                from .rowgroups import surviving_row_groups
+                keep = surviving_row_groups(g.path, *partition)
+            pf, cols = decode_checkpoint_file(g.path, with_stats, extra, keep)
             if g.kind == "v2":
                 sp = cols.get("sidecar.path")
                 if sp is not None:

@@ -481,3 +481,136 @@ def test_gpu_bool_timestamp_partition_values(tmp_path):
         with pytest.raises(DkError, match="partition"):
             _gpu_files(r, TS_PREDICATES[0], eng)
     eng.close()
+
+
+# ---------------------------------------------------------------- checkpoint row-group pruning
+# ActionsIterator.java:336-351: the partition filter, rewritten onto add.partitionValues_parsed,
+# prunes row groups of multi-part parts and sidecars by their footer statistics
+# (ParquetFileReader.java:111-132, ParquetFilterUtils.toParquetFilter, parquet-mr StatisticsFilter);
+# pruned rows are never read, so the ScanMetrics counters shrink too.
+def _rewrite_with_parsed(root, rg_rows=700):
+    """Give every checkpoint part of a synth table an integer partition column `part` (0..9 by date)
+    and add.partitionValues_parsed {date, part}, sorted by part, in small row groups."""
+    import glob
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    for path in sorted(glob.glob(os.path.join(root, "_delta_log", "*.checkpoint.*.parquet"))):
+        t = pq.read_table(path)
+        add = t.column("add").combine_chunks()
+        pvs = add.field("partitionValues").to_pylist()
+        valid = add.is_valid().to_pylist()
+        dates = [dict(pv).get("date") if (ok and pv is not None) else None for ok, pv in zip(valid, pvs)]
+        parts = [None if d is None else int(d.replace("-", "")) % 10 for d in dates]
+        new_pv = [None if not ok else (list(pv or []) + [("part", str(p))]) for ok, pv, p in zip(valid, pvs, parts)]
+        parsed = pa.StructArray.from_arrays([pa.array(dates, pa.string()), pa.array(parts, pa.int32())],
+                                            names=["date", "part"], mask=pa.array([not v for v in valid]))
+        fields = [add.field(i) for i in range(add.type.num_fields)]
+        names = [add.type[i].name for i in range(add.type.num_fields)]
+        fields[names.index("partitionValues")] = pa.array(new_pv, add.type.field("partitionValues").type)
+        new_add = pa.StructArray.from_arrays(fields + [parsed], names=names + ["partitionValues_parsed"],
+                                             mask=pa.array([not v for v in valid]))
+        t = t.set_column(t.schema.get_field_index("add"), "add", new_add)
+        if "metaData" in t.schema.names:
+            md = t.column("metaData").combine_chunks()
+            rows = md.to_pylist()
+            for r in rows:
+                if r is not None:
+                    sch = json.loads(r["schemaString"])
+                    if not any(f["name"] == "part" for f in sch["fields"]):
+                        sch["fields"].append({"name": "part", "type": "integer", "nullable": True, "metadata": {}})
+                    r["schemaString"] = json.dumps(sch)
+                    r["partitionColumns"] = ["date", "part"]
+            t = t.set_column(t.schema.get_field_index("metaData"), "metaData", pa.array(rows, md.type))
+        order = sorted(range(t.num_rows), key=lambda i: (-1 if parts[i] is None else parts[i], i))
+        t = t.take(pa.array(order))
+        pq.write_table(t, path, row_group_size=rg_rows, compression="snappy")
+
+
+RG_PREDICATES = [cmp(">", col("part"), Literal.ofInt(6)), cmp("=", col("part"), Literal.ofInt(3)),
+                 Predicate("NOT", cmp("<", col("part"), Literal.ofInt(7))),
+                 Or(cmp("<", col("part"), Literal.ofInt(2)), cmp(">", col("part"), Literal.ofLong(8))),
+                 Predicate("IS_NULL", col("part")), Predicate("IS_NOT_NULL", col("part")),
+                 cmp("<", Literal.ofInt(5), col("part")),              # swapped without flipping: lt(part, 5)
+                 And(cmp(">=", col("part"), Literal.ofInt(4)), cmp("<", col("date"), Literal.ofString("2024-07-01"))),
+                 cmp("=", col("date"), Literal.ofString("2024-03-15")),
+                 cmp("IS NOT DISTINCT FROM", col("part"), Literal.ofInt(2)),   # not convertible: no pruning
+                 cmp(">", col("part"), Literal.ofLong(1 << 40))]           # long literal beyond int: none
+
+
+@pytest.fixture(scope="module")
+def rg_table(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("rgprune"))
+    synth.write_table(d, synth.TableSpec(n_adds=12_000, n_parts=3, n_commits=4, compression="snappy"))
+    _rewrite_with_parsed(d)
+    return d
+
+
+def test_oracle_row_group_pruning(rg_table):
+    from oracle import ref
+    full = ref.replay(rg_table).counters.as_tuple()
+    seen = {}
+    for p in RG_PREDICATES:
+        files, counters = oracle_files(rg_table, p)
+        seen[repr(p)] = counters[0]
+        assert counters[0] <= full[0]
+    # row groups hold one `part` value each (sorted, 700 rows): range predicates prune
+    assert seen[repr(RG_PREDICATES[0])] < full[0] and seen[repr(RG_PREDICATES[1])] < seen[repr(RG_PREDICATES[0])]
+    assert seen[repr(RG_PREDICATES[9])] == full[0]         # IS NOT DISTINCT FROM does not convert
+
+
+@pytest.mark.gpu
+def test_gpu_row_group_pruning(rg_table):
+    from delta_amd import kernel as K
+    eng = K.GpuEngine()
+    for p in RG_PREDICATES:
+        assert _gpu_files(rg_table, p, eng) == oracle_files(rg_table, p), p
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_row_group_pruning_sharded(rg_table):
+    """Pruned row groups are left out before the shard plan; the merged shards equal the oracle."""
+    from delta_amd import kernel as K
+    from delta_amd import shard as S
+    from oracle import ref
+    eng = K.GpuEngine()
+    p = RG_PREDICATES[0]
+    want = oracle_files(rg_table, p)
+    outs, scans = [], []
+    for r in range(3):
+        snap = K.Table.forPath(eng, rg_table).getLatestSnapshot(eng)
+        scan = snap.getScanBuilder().withFilter(p).withShard(3, r).build()
+        batches = list(scan.getScanFiles(eng))
+        o = S.ShardOutput(r, scan.tail_metrics.as_tuple(), scan.ckpt_metrics.as_tuple())
+        for b in batches:
+            if b.file_index < 0:
+                o.tail = b
+            else:
+                o.files[(b.file_index, b.row_offset)] = b
+        outs.append(o)
+        scans.append(scan)
+    counters, batches = S.merge(outs)
+    rows = [ref.canon_add_from_cols(b.data, int(i)) + (b.table_root,) for b in batches for i in b.selected_rows()]
+    assert counters == want[1] and rows == want[0]
+    for s in scans:
+        s.close()
+    eng.close()
+
+
+def test_row_group_pruning_decisions_match_oracle(rg_table):
+    """The product's per-file pruning (dk_parquet_prune_row_groups, host C++) against the oracle's
+    independent restatement (oracle/rowgroups.py) for every predicate and part file (no GPU)."""
+    import glob
+    from delta_amd import kernel as K
+    from delta_amd._lib import dk_rg_filter
+    from oracle.rowgroups import surviving_row_groups
+    schema, parts = table_metadata(rg_table)
+    fields = pp.partition_fields(schema, parts)
+    files = sorted(glob.glob(os.path.join(rg_table, "_delta_log", "*.checkpoint.*.parquet")))
+    extra = [cmp(">=", col("date"), Literal.ofString("2024-10-01")), Predicate("NOT", cmp("=", col("part"), Literal.ofInt(0))),
+             cmp("<=", col("part"), Literal.ofDate(3)), cmp("=", col("part"), Literal.ofString("3"))]
+    for p in RG_PREDICATES + extra:
+        packed = pp.pack_row_group_filter(pp.row_group_filter(p, fields), dk_rg_filter)
+        for f in files:
+            want = [g for g, k in enumerate(surviving_row_groups(f, p, fields)) if k]
+            assert K.prune_row_groups(f, packed) == want, (p, f)
