@@ -308,16 +308,27 @@ def main():
             t_b = time.perf_counter()
             sc2 = build_scan(s2)
             size_sum, n_sel = 0, 0
-            for b in sc2.getScanFiles(eng):
-                rows_sel = b.selected_rows()
+            t_p = t_r = None
+            it = sc2.getScanFiles(eng)      # prepare (host read + H2D) + device step + counters
+            t_r = time.perf_counter()
+            import numpy as np
+            for b in it:
+                # the JMH consumer (BenchmarkParallelCheckpointReading.java:124-135): sum add.size
+                # over the selected rows
                 col = b.data["add.size"]
-                size_sum += int(col.fixed.view("<i8")[rows_sel].sum())
-                n_sel += len(rows_sel)
+                v = col.fixed.view("<i8")
+                if b.selection is None:
+                    size_sum += int(v.sum())
+                    n_sel += b.size
+                else:
+                    size_sum += int(np.add.reduce(v, where=b.selection))
+                    n_sel += int(np.count_nonzero(b.selection))
             t_c = time.perf_counter()
             seen = sc2.metrics.addFilesSeen
+            prep_ms = {k: round(v, 2) for k, v in sc2.prepare_ms.items()}
             sc2.close()
-            runs.append((t_c - t_b, t_b - t_a, seen, n_sel, size_sum))
-        gsf_s, snap_s, seen, n_sel, size_sum = min(runs)
+            runs.append((t_c - t_b, t_b - t_a, seen, n_sel, size_sum, t_r - t_b, t_c - t_r))
+        gsf_s, snap_s, seen, n_sel, size_sum, open_run_s, consume_s = min(runs)
         gsf_s = max_over_ranks(gsf_s)
         snap_s = max_over_ranks(snap_s)
         seen_all = sum_over_ranks(seen) - (world - 1) * (n_tail and scan.tail_metrics.addFilesSeen) \
@@ -326,6 +337,8 @@ def main():
                "jmh_op_ms": (gsf_s + snap_s) * 1e3,
                "actions_per_s": seen_all / gsf_s, "jmh_op_actions_per_s": seen_all / (gsf_s + snap_s),
                "addFilesSeen": seen_all, "selected_rows_rank0": n_sel, "size_sum_rank0": size_sum,
+               "phases_ms": {"prepare_and_device_step": open_run_s * 1e3, "consume": consume_s * 1e3,
+                             "prepare": dict(prep_ms)},
                "reps": args.e2e_reps,
                "includes": "host read of the projected column chunks + H2D + device decode/reconcile + "
                            "D2H of selection and add.size + host sum over selected rows"}

@@ -55,7 +55,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free", "dk_parquet_open_rg", "dk_parquet_row_groups",
            "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits", "dk_parquet_open_sel",
-           "dk_parquet_prune_row_groups"]
+           "dk_parquet_prune_row_groups", "dk_parquet_nonnull_row_groups"]
 
 
 def lib(build_if_missing=True):
@@ -80,6 +80,7 @@ def lib(build_if_missing=True):
         "dk_parquet_open_sel": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, P, P,
                                           C.POINTER(P)]),
         "dk_parquet_prune_row_groups": (C.c_int, [C.c_char_p, P, P, I32, C.POINTER(I32)]),
+        "dk_parquet_nonnull_row_groups": (C.c_int, [C.c_char_p, C.c_char_p, P, I32, C.POINTER(I32)]),
         "dk_parquet_row_offset": (I64, [P, I32]),
         "dk_replay_ckpt_selection_bits": (C.c_int, [P, I32, P, I64, I32]),
         "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),

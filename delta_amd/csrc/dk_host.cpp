@@ -9,7 +9,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <cmath>
+#include <atomic>
+#include <chrono>
 #include <memory>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -1177,6 +1180,24 @@ extern "C" int dk_parquet_prune_row_groups(const char* path, const dk_rg_filter*
   return 0;
 }
 
+// Row groups of `path` whose leaf may hold a non-null value: those without statistics, or whose
+// null_count is below the chunk's value count. The snapshot-load P&M pass only decodes these (the
+// first non-null protocol / metaData row cannot lie in an all-null row group).
+extern "C" int dk_parquet_nonnull_row_groups(const char* path, const char* leaf, uint8_t* keep, int32_t cap,
+                                             int32_t* n) {
+  FileM f;
+  f.path = path ? path : "";
+  if (read_footer(f) || parse_footer(f)) return 1;
+  *n = (int32_t)f.rgs.size();
+  const int idx = leaf ? leaf_index(f, leaf) : -1;
+  for (int32_t g = 0; g < *n && g < cap; g++) {
+    if (idx < 0) { keep[g] = 0; continue; }                 // a missing leaf is null everywhere
+    const ColMeta& m = f.rgs[g].cols[idx];
+    keep[g] = !(m.has_stats && m.st.has_nulls && m.st.null_count >= m.num_values);
+  }
+  return 0;
+}
+
 extern "C" int dk_parquet_row_groups(const char* path, int64_t* rows, int32_t cap, int32_t* n) {
   FileM f;
   f.path = path ? path : "";
@@ -1193,6 +1214,20 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
 
 static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out);
+
+// fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads
+template <class F>
+static void parallel_for(int n, F fn) {
+  int nt = 16;
+  if (const char* v = getenv("DK_IO_THREADS")) nt = atoi(v) > 0 ? atoi(v) : 1;
+  if (nt > n) nt = n;
+  if (nt <= 1) { for (int i = 0; i < n; i++) fn(i); return; }
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++)
+    th.emplace_back([&] { for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
+  for (auto& x : th) x.join();
+}
 
 extern "C" int dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                                   int32_t n_leaves, const int32_t* rg_lo, const int32_t* rg_hi, dk_parquet** out) {
@@ -1243,26 +1278,39 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->leafidx.assign(n_files, std::vector<int>(n_leaves, -1));
   p->dfile.resize(n_files);
   hipStream_t s = e->stream;
-  for (int fi = 0; fi < n_files; fi++) {
+  // host I/O in parallel over files (footer, row-group selection, projected column chunks):
+  // DefaultParquetHandler reads files one after another; here every file of the call is in flight
+  std::vector<std::string> errs(n_files > 0 ? n_files : 0);
+  const auto t_io0 = std::chrono::steady_clock::now();
+  parallel_for(n_files, [&](int fi) {
     FileM& f = p->files[fi];
     f.path = paths[fi];
-    if (read_footer(f) || parse_footer(f)) return 1;
-    if (groups ? select_row_groups(f, (*groups)[fi]) : select_row_groups(f, 0, -1)) return 1;
-    {   // projection: only the chunks (and offset indexes) of the requested leaves travel to HBM
-      std::vector<Span> want;
-      for (int li = 0; li < n_leaves; li++) {
-        int idx = leaf_index(f, p->leaves[li]);
-        if (idx < 0) continue;
-        for (int32_t g : f.sel) {
-          const ColMeta& m = f.rgs[g].cols[idx];
-          want.push_back({chunk_start(m), m.total_compressed, 0});
-          if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= f.size) want.push_back({m.oi_off, m.oi_len, 0});
-        }
+    if (read_footer(f) || parse_footer(f) ||
+        (groups ? select_row_groups(f, (*groups)[fi]) : select_row_groups(f, 0, -1))) { errs[fi] = g_err; return; }
+    // projection: only the chunks (and offset indexes) of the requested leaves travel to HBM
+    std::vector<Span> want;
+    for (int li = 0; li < n_leaves; li++) {
+      int idx = leaf_index(f, p->leaves[li]);
+      if (idx < 0) continue;
+      for (int32_t g : f.sel) {
+        const ColMeta& m = f.rgs[g].cols[idx];
+        want.push_back({chunk_start(m), m.total_compressed, 0});
+        if (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= f.size) want.push_back({m.oi_off, m.oi_len, 0});
       }
-      if (read_spans(f, want)) return 1;
     }
-    if (p->dfile[fi].alloc(f.bytes.size() + 256)) return 1;
-    if (!f.bytes.empty()) HIPOK(hipMemcpyAsync(p->dfile[fi].p, f.bytes.data(), f.bytes.size(), hipMemcpyHostToDevice, s));
+    if (read_spans(f, want)) { errs[fi] = g_err; return; }
+    // the file's image goes to HBM from this thread, overlapping the other files' reads
+    hipSetDevice(e->cfg.device);
+    if (p->dfile[fi].alloc(f.bytes.size() + 256)) { errs[fi] = g_err; return; }
+    if (!f.bytes.empty() &&
+        hipMemcpy(p->dfile[fi].p, f.bytes.data(), f.bytes.size(), hipMemcpyHostToDevice) != hipSuccess)
+      errs[fi] = "hipMemcpy failed for " + f.path;
+  });
+  for (int fi = 0; fi < n_files; fi++)
+    if (!errs[fi].empty()) return fail(errs[fi]);
+  const auto t_io1 = std::chrono::steady_clock::now();
+  for (int fi = 0; fi < n_files; fi++) {
+    FileM& f = p->files[fi];
     for (int li = 0; li < n_leaves; li++) {
       int idx = leaf_index(f, p->leaves[li]);
       p->leafidx[fi][li] = idx;
@@ -1314,7 +1362,17 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   }
   p->n_pages = (int)p->h_pages.size();
   p->n_cols = (int)p->h_cols.size();
+  const auto t_h2d = std::chrono::steady_clock::now();
   if (prepare(p.get())) return 1;
+  if (getenv("DK_VERBOSE")) {
+    const auto t_end = std::chrono::steady_clock::now();
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count(); };
+    int64_t nb = 0;
+    for (const FileM& f : p->files) nb += (int64_t)f.bytes.size();
+    fprintf(stderr, "[dk] parquet_open %d files %.1f MB: io+h2d %.1f ms, metadata %.1f ms, prepare %.1f ms\n",
+            n_files, nb / 1e6, ms(t_io0, t_io1), ms(t_io1, t_h2d), ms(t_h2d, t_end));
+  }
   *out = p.release();
   return 0;
 }
@@ -1839,13 +1897,15 @@ void put_dv(CB* c, const std::vector<JNode>& N, const JNode* dv, int add_def) {
 }
 }  // namespace
 
-extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
-                                  int32_t with_stats, dk_json_tail** out) {
-  (void)versions;
-  if (!e) return fail("null engine");
-  std::unique_ptr<dk_json_tail> t(new dk_json_tail());
-  t->with_stats = with_stats != 0;
-  CB* c = t->col;
+// One commit file's rows in the tail layout (the files parse in parallel, then concatenate).
+struct TailPart {
+  int64_t rows = 0;
+  CB col[JL_N];
+  std::vector<int32_t> step, rowin;     // step local to the file
+  int32_t n_steps = 0;
+};
+
+static void init_tail_cols(CB* c) {
   c[JL_PATH].init(PT_BYTE_ARRAY, 0, 2, 0, 0);
   c[JL_PVK].init(PT_BYTE_ARRAY, 0, 3, 1, 3);
   c[JL_PVV].init(PT_BYTE_ARRAY, 0, 4, 1, 3);
@@ -1868,77 +1928,118 @@ extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const 
   c[JL_RDVOFF].init(PT_INT32, 4, 3, 0, 0);
   c[JL_RDVSIZE].init(PT_INT32, 4, 3, 0, 0);
   c[JL_RDVCARD].init(PT_INT64, 8, 3, 0, 0);
-  const int J = e->cfg.json_batch_size;
+}
+
+// DefaultJsonHandler.readJsonFiles over one commit: lines (BufferedReader.readLine: \n, \r or \r\n),
+// each a JSON object decoded with DefaultJsonRow's rules for the add / remove read schema, in
+// batches of J lines. Returns an error message or "".
+static std::string parse_commit_file(const char* path, int J, bool with_stats, TailPart& P) {
+  CB* c = P.col;
+  init_tail_cols(c);
+  std::vector<uint8_t> raw;
+  FILE* fp = fopen(path, "rb");
+  if (!fp) return std::string("Error reading JSON file: ") + path;
+  fseek(fp, 0, SEEK_END); long n = ftell(fp); fseek(fp, 0, SEEK_SET);
+  raw.resize(n > 0 ? n : 0);
+  size_t got = n > 0 ? fread(raw.data(), 1, n, fp) : 0;
+  fclose(fp);
+  if ((long)got != n) return std::string("Error reading JSON file: ") + path;
+  std::string text = java_utf8(raw.data(), raw.size());
   std::vector<JNode> N;
-  for (int fi = 0; fi < n_files; fi++) {
-    std::vector<uint8_t> raw;
-    FILE* fp = fopen(paths[fi], "rb");
-    if (!fp) return fail(std::string("Error reading JSON file: ") + paths[fi]);
-    fseek(fp, 0, SEEK_END); long n = ftell(fp); fseek(fp, 0, SEEK_SET);
-    raw.resize(n > 0 ? n : 0);
-    size_t got = n > 0 ? fread(raw.data(), 1, n, fp) : 0;
-    fclose(fp);
-    if ((long)got != n) return fail(std::string("Error reading JSON file: ") + paths[fi]);
-    std::string text = java_utf8(raw.data(), raw.size());
-    // BufferedReader.readLine: lines end at \n, \r or \r\n
-    size_t i = 0;
-    int in_batch = 0;
-    bool any = false;
-    while (i < text.size()) {
-      size_t j = i;
-      while (j < text.size() && text[j] != '\n' && text[j] != '\r') j++;
-      std::string line = text.substr(i, j - i);
-      if (j < text.size() && text[j] == '\r' && j + 1 < text.size() && text[j + 1] == '\n') j++;
-      i = j + 1;
-      N.clear();
-      JParser jp(line.data(), line.data() + line.size(), N);
-      int root = jp.value(0);
-      if (root >= 0) { jp.ws(); if (jp.p != jp.e) { root = -1; jp.err = "trailing characters"; } }
-      if (root < 0) return fail(std::string("Error reading JSON file: ") + paths[fi] + " (" + jp.err + ")");
-      if (in_batch == J) { t->n_steps++; in_batch = 0; }
-      t->step.push_back(t->n_steps);
-      t->rowin.push_back(in_batch++);
-      any = true;
-      try {
-        const JNode& R = N[root];
-        if (R.t != J_OBJ) mismatch(N, R, "object");
-        const JNode* add = field(N, R, "add", true);
-        const JNode* rm = field(N, R, "remove", true);
-        if (add) {
-          if (add->t != J_OBJ) mismatch(N, *add, "object");
-          const JNode& A = *add;
-          c[JL_PATH].str_row(as_str(N, *field(N, A, "path", false)));
-          put_map(c[JL_PVK], c[JL_PVV], N, field(N, A, "partitionValues", false), 1);
-          int64_t v = as_long(N, *field(N, A, "size", false)); c[JL_SIZE].fix_row(&v);
-          v = as_long(N, *field(N, A, "modificationTime", false)); c[JL_MTIME].fix_row(&v);
-          uint8_t b = as_bool(N, *field(N, A, "dataChange", false)); c[JL_DC].fix_row(&b);
-          put_dv(&c[JL_DVST], N, field(N, A, "deletionVector", true), 1);
-          put_map(c[JL_TGK], c[JL_TGV], N, field(N, A, "tags", true), 1);
-          const JNode* x = field(N, A, "baseRowId", true);
-          if (x) { v = as_long(N, *x); c[JL_BRID].fix_row(&v); } else c[JL_BRID].null_row(1);
-          x = field(N, A, "defaultRowCommitVersion", true);
-          if (x) { v = as_long(N, *x); c[JL_DRCV].fix_row(&v); } else c[JL_DRCV].null_row(1);
-          if (t->with_stats) { x = field(N, A, "stats", true); if (x) c[JL_STATS].str_row(as_str(N, *x)); else c[JL_STATS].null_row(1); }
-          else c[JL_STATS].null_row(1);
-        } else {
-          for (int k : {JL_PATH, JL_SIZE, JL_MTIME, JL_DC, JL_DVST, JL_DVPID, JL_DVOFF, JL_DVSIZE, JL_DVCARD, JL_BRID, JL_DRCV, JL_STATS})
-            c[k].null_row(0);
-          put_map(c[JL_PVK], c[JL_PVV], N, nullptr, 0);
-          put_map(c[JL_TGK], c[JL_TGV], N, nullptr, 0);
-        }
-        if (rm) {
-          if (rm->t != J_OBJ) mismatch(N, *rm, "object");
-          c[JL_RPATH].str_row(as_str(N, *field(N, *rm, "path", false)));
-          put_dv(&c[JL_RDVST], N, field(N, *rm, "deletionVector", true), 1);
-        } else {
-          for (int k : {JL_RPATH, JL_RDVST, JL_RDVPID, JL_RDVOFF, JL_RDVSIZE, JL_RDVCARD}) c[k].null_row(0);
-        }
-      } catch (const JErr& je) {
-        return fail(je.msg);
+  size_t i = 0;
+  int in_batch = 0;
+  bool any = false;
+  while (i < text.size()) {
+    size_t j = i;
+    while (j < text.size() && text[j] != '\n' && text[j] != '\r') j++;
+    std::string line = text.substr(i, j - i);
+    if (j < text.size() && text[j] == '\r' && j + 1 < text.size() && text[j + 1] == '\n') j++;
+    i = j + 1;
+    N.clear();
+    JParser jp(line.data(), line.data() + line.size(), N);
+    int root = jp.value(0);
+    if (root >= 0) { jp.ws(); if (jp.p != jp.e) { root = -1; jp.err = "trailing characters"; } }
+    if (root < 0) return std::string("Error reading JSON file: ") + path + " (" + jp.err + ")";
+    if (in_batch == J) { P.n_steps++; in_batch = 0; }
+    P.step.push_back(P.n_steps);
+    P.rowin.push_back(in_batch++);
+    any = true;
+    try {
+      const JNode& R = N[root];
+      if (R.t != J_OBJ) mismatch(N, R, "object");
+      const JNode* add = field(N, R, "add", true);
+      const JNode* rm = field(N, R, "remove", true);
+      if (add) {
+        if (add->t != J_OBJ) mismatch(N, *add, "object");
+        const JNode& A = *add;
+        c[JL_PATH].str_row(as_str(N, *field(N, A, "path", false)));
+        put_map(c[JL_PVK], c[JL_PVV], N, field(N, A, "partitionValues", false), 1);
+        int64_t v = as_long(N, *field(N, A, "size", false)); c[JL_SIZE].fix_row(&v);
+        v = as_long(N, *field(N, A, "modificationTime", false)); c[JL_MTIME].fix_row(&v);
+        uint8_t b = as_bool(N, *field(N, A, "dataChange", false)); c[JL_DC].fix_row(&b);
+        put_dv(&c[JL_DVST], N, field(N, A, "deletionVector", true), 1);
+        put_map(c[JL_TGK], c[JL_TGV], N, field(N, A, "tags", true), 1);
+        const JNode* x = field(N, A, "baseRowId", true);
+        if (x) { v = as_long(N, *x); c[JL_BRID].fix_row(&v); } else c[JL_BRID].null_row(1);
+        x = field(N, A, "defaultRowCommitVersion", true);
+        if (x) { v = as_long(N, *x); c[JL_DRCV].fix_row(&v); } else c[JL_DRCV].null_row(1);
+        if (with_stats) { x = field(N, A, "stats", true); if (x) c[JL_STATS].str_row(as_str(N, *x)); else c[JL_STATS].null_row(1); }
+        else c[JL_STATS].null_row(1);
+      } else {
+        for (int k : {JL_PATH, JL_SIZE, JL_MTIME, JL_DC, JL_DVST, JL_DVPID, JL_DVOFF, JL_DVSIZE, JL_DVCARD, JL_BRID, JL_DRCV, JL_STATS})
+          c[k].null_row(0);
+        put_map(c[JL_PVK], c[JL_PVV], N, nullptr, 0);
+        put_map(c[JL_TGK], c[JL_TGV], N, nullptr, 0);
       }
-      t->rows++;
+      if (rm) {
+        if (rm->t != J_OBJ) mismatch(N, *rm, "object");
+        c[JL_RPATH].str_row(as_str(N, *field(N, *rm, "path", false)));
+        put_dv(&c[JL_RDVST], N, field(N, *rm, "deletionVector", true), 1);
+      } else {
+        for (int k : {JL_RPATH, JL_RDVST, JL_RDVPID, JL_RDVOFF, JL_RDVSIZE, JL_RDVCARD}) c[k].null_row(0);
+      }
+    } catch (const JErr& je) {
+      return je.msg;
     }
-    if (any) { t->n_steps++; in_batch = 0; }
+    P.rows++;
+  }
+  if (any) P.n_steps++;
+  return "";
+}
+
+static void append_cb(CB& d, const CB& s) {
+  const int64_t ebase = d.max_rep ? (int64_t)d.entry_def.size() : 0, cbase = (int64_t)d.chars.size();
+  d.row_def.insert(d.row_def.end(), s.row_def.begin(), s.row_def.end());
+  d.entry_def.insert(d.entry_def.end(), s.entry_def.begin(), s.entry_def.end());
+  d.fixed.insert(d.fixed.end(), s.fixed.begin(), s.fixed.end());
+  d.chars.insert(d.chars.end(), s.chars.begin(), s.chars.end());
+  for (size_t k = 1; k < s.row_offs.size(); k++) d.row_offs.push_back(s.row_offs[k] + ebase);
+  for (size_t k = 1; k < s.offs.size(); k++) d.offs.push_back(s.offs[k] + cbase);
+}
+
+extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
+                                  int32_t with_stats, dk_json_tail** out) {
+  (void)versions;
+  if (!e) return fail("null engine");
+  std::unique_ptr<dk_json_tail> t(new dk_json_tail());
+  t->with_stats = with_stats != 0;
+  init_tail_cols(t->col);
+  const int J = e->cfg.json_batch_size;
+  // commits parse in parallel (each starts its own batches); the first failing file in replay
+  // order reports, as the sequential reader would
+  std::vector<TailPart> parts(n_files > 0 ? n_files : 0);
+  std::vector<std::string> errs(parts.size());
+  parallel_for(n_files, [&](int fi) { errs[fi] = parse_commit_file(paths[fi], J, t->with_stats, parts[fi]); });
+  for (int fi = 0; fi < n_files; fi++)
+    if (!errs[fi].empty()) return fail(errs[fi]);
+  for (int fi = 0; fi < n_files; fi++) {
+    TailPart& P = parts[fi];
+    for (int k = 0; k < JL_N; k++) append_cb(t->col[k], P.col[k]);
+    for (int32_t st : P.step) t->step.push_back(t->n_steps + st);
+    t->rowin.insert(t->rowin.end(), P.rowin.begin(), P.rowin.end());
+    t->n_steps += P.n_steps;
+    t->rows += P.rows;
+    P = TailPart();
   }
   *out = t.release();
   return 0;

@@ -94,6 +94,17 @@ def prune_row_groups(path, packed_filter):
     return [g for g in range(n.value) if keep[g]]
 
 
+def nonnull_row_groups(path, leaf):
+    """keep flag per row group: False where footer statistics show `leaf` null in every row."""
+    cap = 4096
+    keep = (C.c_uint8 * cap)()
+    n = C.c_int32()
+    check(lib().dk_parquet_nonnull_row_groups(path.encode(), leaf.encode(), keep, cap, C.byref(n)))
+    if n.value > cap:
+        raise DkError("%s has more than %d row groups" % (path, cap))
+    return [bool(keep[g]) for g in range(n.value)]
+
+
 def row_group_rows(path):
     """Row counts of a Parquet file's row groups (footer only)."""
     cap = 4096
@@ -469,6 +480,8 @@ class Snapshot:
         for d in reversed(self.log_segment.deltas):
             with open(d.path, "rb") as f:
                 raw = f.read()
+            if b'"protocol"' not in raw and b'"metaData"' not in raw and b"\\u" not in raw:
+                continue                          # no line of this commit can hold either action
             for line in raw.decode("utf-8", "replace").splitlines():
                 # only a line naming one of the two actions can hold it (a "\u"-escaped key
                 # is the one way to spell it otherwise)
@@ -494,7 +507,22 @@ class Snapshot:
         else:
             files = self._checkpoint_files(engine) if cks else []
         if files and (self.protocol is None or self.metadata is None):
-            ps = ParquetSet(engine, files, PM_LEAVES).decode()
+            # only row groups whose footer statistics allow a non-null protocol / metaData row
+            # (an all-null row group cannot hold the first one); files with none are not read
+            want = [lf for lf, need in (("protocol.minReaderVersion", self.protocol is None),
+                                        ("metaData.id", self.metadata is None)) if need]
+            groups = []
+            for f in files:
+                keep = None
+                for lf in want:
+                    k = nonnull_row_groups(f, lf)
+                    keep = k if keep is None else [a or b for a, b in zip(keep, k)]
+                groups.append([g for g, k in enumerate(keep) if k])
+            files = [f for f, g in zip(files, groups) if g]
+            groups = [g for g in groups if g]
+            if not files:
+                return
+            ps = ParquetSet(engine, files, PM_LEAVES, groups=groups).decode()
             for fi in range(len(files)):
                 # the first non-null protocol / metaData row of the batch, found on the device;
                 # only that row's values come back to the host
@@ -709,6 +737,7 @@ class GpuScan:
         self.tail_metrics = ScanMetrics()
         self.ckpt_metrics = ScanMetrics()
         self.replay = None
+        self.prepare_ms = {}
 
     def table_root(self):
         """tableRoot = dataPath.toUri().toString() (ActiveAddFilesIterator.java:251)."""
@@ -718,9 +747,12 @@ class GpuScan:
         """Host-side setup: parse the commit tail, open checkpoint files, upload to HBM."""
         if self._deferred_error is not None:
             raise self._deferred_error
+        t0 = time.perf_counter()
         seg = self.snapshot.log_segment
         commits = list(reversed(seg.deltas))
         self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
+        t1 = time.perf_counter()
+        self.prepare_ms = {"commit_tail": (t1 - t0) * 1e3}
         all_files, prunable = self.snapshot._checkpoint_files(engine, with_pruning=True)
         # row groups read per file: all, minus those the checkpoint predicate (the partition filter
         # on add.partitionValues_parsed) proves empty in multi-part parts and sidecars
@@ -751,10 +783,14 @@ class GpuScan:
             sel = None
         self.ckpt_files = [all_files[i] for i in self.ckpt_index]
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
+        t2 = time.perf_counter()
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel) if self.ckpt_files else None
+        t3 = time.perf_counter()
         self._rh = C.c_void_p()
         check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
                                      C.byref(self._rh)))
+        self.prepare_ms.update({"plan_files": (t2 - t1) * 1e3, "checkpoint_open": (t3 - t2) * 1e3,
+                                "replay_create": (time.perf_counter() - t3) * 1e3})
         if self.partition is not None:
             from . import partitions as pp
             pprog = pp.pack(self.partition, dk_part_program)

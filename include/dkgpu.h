@@ -81,6 +81,9 @@ int  dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files,
                         const int32_t* rg_hi, dk_parquet** out);
 /* Row counts of a file's row groups from its footer (no device work); *n = number of groups. */
 int  dk_parquet_row_groups(const char* path, int64_t* rows, int32_t cap, int32_t* n);
+/* keep[g] = 0 for the row groups whose footer statistics show `leaf` null in every row (used by the
+ * snapshot-load P&M pass to decode only row groups that can hold a protocol / metaData row). */
+int  dk_parquet_nonnull_row_groups(const char* path, const char* leaf, uint8_t* keep, int32_t cap, int32_t* n);
 /* The same over an explicit ascending list of row groups per file: rg_count[i] groups taken from
  * rg_list (concatenated over the files), rg_count[i] < 0 = all groups of file i. */
 int  dk_parquet_open_sel(dk_engine* e, const char* const* paths, int32_t n_files,
