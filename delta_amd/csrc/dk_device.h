@@ -71,6 +71,8 @@ struct SnapCtx {
   const int32_t* fbase;      // compressed page -> first fragment (n_cpages + 1)
   int64_t* fstart;           // fragment -> compressed offset of its first tag
   int32_t* serial;           // compressed page -> 1: decode on the serial path
+  uint64_t* tbits;           // page mode: tag-start bitmap, DK_SNAP_SEG / 64 words per segment (or null)
+  int32_t page_mode;         // 1: whole pages decode in order (no 64 KiB fragment starts needed)
 };
 
 

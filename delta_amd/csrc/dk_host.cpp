@@ -513,6 +513,7 @@ struct dk_parquet {
   // snappy: compressed pages, their 64 KiB fragment bases / work items / starts, serial flags
   DBuf d_cpage, d_fbase, d_fwork, d_fstart, d_serial;
   DBuf d_sbase, d_spage, d_snapws;   // speculative-walk segments: page bases, owner page, workspace
+  DBuf d_tbits;                      // page mode: tag-start bitmap (DK_SNAP_SEG / 64 words per segment)
   DBuf d_pwork;                      // page-mode work items (page, -1)
   int n_cpages = 0, n_frags = 0, n_segs = 0;
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
@@ -601,6 +602,8 @@ static int run_pipeline(dk_parquet* p, int mode) {
     // fill the chip; otherwise the speculative walk splits pages into 64 KiB fragments
     const bool page_mode = snap_page_mode(p);
     const int nfr = page_mode ? -1 : p->n_frags;
+    X.page_mode = page_mode ? 1 : 0;
+    X.tbits = page_mode ? p->d_tbits.as<uint64_t>() : nullptr;
     const int2* wk = page_mode ? p->d_pwork.as<int2>() : p->d_fwork.as<int2>();
     { KTimer::Scope s0(&T, 13, s); launch_snappy(X, p->n_cpages, nfr, wk, 0, s); }
     { KTimer::Scope s1(&T, 19, s); launch_snappy(X, p->n_cpages, nfr, wk, 1, s); }
@@ -774,6 +777,10 @@ static int prepare(dk_parquet* p) {
     });
     if (upload(p->d_pwork, pwork.data(), pwork.size() * sizeof(int2), s)) return 1;
     p->n_segs = (int)spage.size();
+    // page mode finds tags through a bitmap built by the speculative walk (DK_SNAP_BITS=0: the
+    // in-kernel pointer-doubling discovery instead)
+    static const bool bits = !getenv("DK_SNAP_BITS") || atoi(getenv("DK_SNAP_BITS")) != 0;
+    if (bits && snap_page_mode(p) && p->d_tbits.alloc(((size_t)p->n_segs * (DK_SNAP_SEG / 64) + 4) * 8)) return 1;
   }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
   p->bytes_arena = arena_n;

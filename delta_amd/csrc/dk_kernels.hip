@@ -329,6 +329,87 @@ __device__ __forceinline__ bool snap_page(const SnapCtx& X, int ci, const uint8_
   return snap_stream(X.chunks[pg.chunk], pg, X.arena, in, clen, out, ulen, lv);
 }
 
+// Tag-start bitmap of one segment (page mode): bit i of word w = a tag starts at segment offset
+// 64 w + i. A walker stores the words of its chain in order; words it never reaches are zero.
+struct SnapBits {
+  GAS uint64_t* w;       // the segment's SNAP_SEG / 64 words (null: not recording)
+  int64_t s0;            // stream offset of the segment's first byte
+  int wi = 0;            // word being filled
+  uint64_t cur = 0;
+  __device__ __forceinline__ void mark(int64_t p) {
+    if (!w) return;
+    const int t = (int)((p - s0) >> 6);
+    while (wi < t) { w[wi++] = cur; cur = 0; }
+    cur |= 1ull << ((p - s0) & 63);
+  }
+  // flush words up to (not including) the one holding offset `upto` (upto < 0: all words; the
+  // word holding `upto` keeps its bits at and past `upto` from the existing contents)
+  __device__ __forceinline__ void finish(int64_t upto) {
+    if (!w) return;
+    const int last = upto < 0 ? SNAP_SEG / 64 : (int)((upto - s0) >> 6);
+    while (wi < last && wi < SNAP_SEG / 64) { w[wi++] = cur; cur = 0; }
+    if (upto >= 0 && wi < SNAP_SEG / 64) {
+      const uint64_t keep = ~0ull << ((upto - s0) & 63);
+      w[wi] = (w[wi] & keep) | (cur & ~keep);
+    }
+  }
+};
+
+__device__ __forceinline__ GAS uint64_t* snap_seg_bits(const SnapCtx& X, int k) {
+  return X.tbits ? (GAS uint64_t*)(X.tbits + (int64_t)k * (SNAP_SEG / 64)) : nullptr;
+}
+
+// A lane's 32-byte register window over the stream (two dwordx4 loads from a 16-byte aligned
+// address): tags parse from registers, so a walker issues one load pair per ~8 tags instead of two
+// loads per tag (its lanes walk different segments: every load is a separate cache line).
+struct SnapRegWin {
+  const uint8_t* in;
+  int64_t base = 1ll << 62;      // stream offset of w[0]
+  uint32_t w[8];
+  __device__ __forceinline__ void load(int64_t p) {
+    const uintptr_t a = ((uintptr_t)(in + p)) & ~(uintptr_t)15;
+    base = p - (int64_t)((uintptr_t)(in + p) - a);
+    const u32x4 x = *(const GAS u32x4*)a, y = *(const GAS u32x4*)(a + 16);
+    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+  }
+  __device__ __forceinline__ uint32_t sel(int i) const {
+    uint32_t v = w[0];
+#pragma unroll
+    for (int q = 1; q < 8; q++) v = i == q ? w[q] : v;
+    return v;
+  }
+  // 8 bytes from stream offset p (p - base <= 24 after refill)
+  __device__ __forceinline__ uint64_t at(int64_t p) {
+    if (p < base || p + 5 > base + 32) load(p);
+    const int rel = (int)(p - base), i = rel >> 2;
+    return ((((uint64_t)sel(i + 1)) << 32) | sel(i)) >> (8 * (rel & 3));
+  }
+};
+
+// snap_parse over a register window
+__device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_t p, int32_t* adv, int32_t* len) {
+  const uint64_t d = W.at(p);
+  const uint32_t tag = (uint32_t)d & 0xff;
+  const int kind = tag & 3;
+  if (kind == 0) {
+    int64_t l = (tag >> 2) + 1, hdr = 1;
+    if (l > 60) {
+      const int nb = (int)l - 60;
+      hdr += nb;
+      l = (int64_t)((d >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
+    }
+    if (p + hdr + l > clen) return false;
+    *adv = (int32_t)(hdr + l);
+    *len = (int32_t)l;
+    return true;
+  }
+  const int hdr = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+  if (p + hdr > clen) return false;
+  *adv = hdr;
+  *len = kind == 1 ? (int32_t)(((tag >> 2) & 7) + 4) : (int32_t)((tag >> 2) + 1);
+  return true;
+}
+
 __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
   const int k = blockIdx.x * NT + threadIdx.x;
   if (k >= X.nseg) return;
@@ -336,20 +417,24 @@ __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
   const int j = k - X.sbase[ci];
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
   int32_t ex = -1, o = 0, n = 0;
+  SnapBits B{snap_seg_bits(X, k), (int64_t)j * SNAP_SEG};
   if (snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
     int64_t p = (int64_t)j * SNAP_SEG;
     const int64_t end = p + SNAP_SEG < clen ? p + SNAP_SEG : clen;
     if (j == 0) { uint64_t un; p = snap_preamble(in, clen, &un); }
     bool dead = p < 0;
+    SnapRegWin W{in};
     while (!dead && p < end) {
       int32_t adv, len;
-      if (!snap_parse(in, clen, p, &adv, &len)) { dead = true; break; }
+      if (!snap_parse_w(W, clen, p, &adv, &len)) { dead = true; break; }
       if (n < SNAP_REC) { X.w_pos[(int64_t)n * X.nseg + k] = (int32_t)p; X.w_cum[(int64_t)n * X.nseg + k] = o; n++; }
+      B.mark(p);
       o += len;
       p += adv;
     }
     ex = dead ? -1 : (int32_t)p;
   }
+  B.finish(-1);
   X.w_exit[k] = ex;
   X.w_out[k] = o;
   X.w_npos[k] = n;
@@ -358,9 +443,12 @@ __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
 // true exit / output of segment j entered at e (serial walk, merging with the walker's recorded
 // positions when `merge`)
 __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, const uint8_t* in, int64_t clen, int64_t e,
-                                              bool merge, int32_t* tout, int32_t* texit) {
+                                              bool merge, int32_t* tout, int32_t* texit, bool bits = false) {
   const int64_t end = (int64_t)j * SNAP_SEG + SNAP_SEG < clen ? (int64_t)j * SNAP_SEG + SNAP_SEG : clen;
-  if (e < 0) { *tout = 0; *texit = -1; return; }
+  // bits (e verified): the bitmap words up to the join point are rewritten from the true chain (the
+  // walker's words from there on are already right; without a join every word is rewritten)
+  SnapBits B{bits ? snap_seg_bits(X, k) : nullptr, (int64_t)j * SNAP_SEG};
+  if (e < 0) { *tout = 0; *texit = -1; B.finish(-1); return; }
   int64_t p = e;
   int32_t o = 0;
   const int n = merge ? X.w_npos[k] : 0;
@@ -371,11 +459,13 @@ __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, co
     if (jj < n && pj == p) {                 // joined the walker's chain
       *tout = o + X.w_out[k] - X.w_cum[(int64_t)jj * X.nseg + k];
       *texit = X.w_exit[k];
+      B.finish(p);
       return;
     }
-    if (p >= end) { *tout = o; *texit = (int32_t)p; return; }
+    if (p >= end) { *tout = o; *texit = (int32_t)p; B.finish(-1); return; }
     int32_t adv, len;
-    if (!snap_parse(in, clen, p, &adv, &len)) { *tout = o; *texit = -1; return; }
+    if (!snap_parse(in, clen, p, &adv, &len)) { *tout = o; *texit = -1; B.finish(-1); return; }
+    B.mark(p);
     o += len;
     p += adv;
   }
@@ -432,10 +522,18 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
       const int L = __ffsll((long long)m) - 1;
       const int32_t eL = __shfl(pv, L, 64);
       int32_t to2, tx2;
-      snap_seg_from(X, base + L, base + L - k0, in, clen, eL, true, &to2, &tx2);
+      if (lane == L) snap_seg_from(X, base + L, base + L - k0, in, clen, eL, true, &to2, &tx2);
+      to2 = __shfl(to2, L, 64);
+      tx2 = __shfl(tx2, L, 64);
       if (lane == L) { e = eL; tout = to2; tex = tx2; }
     }
     if (__ballot(valid && tex < 0)) { bad = true; break; }
+    // entries verified: each segment's tag-start bits up to where the walker joined the true chain
+    // are rewritten from its true entry (every lane its own segment)
+    if (X.tbits && valid) {
+      int32_t to3, tx3;
+      snap_seg_from(X, k, k - k0, in, clen, e, true, &to3, &tx3, true);
+    }
     // output offsets: exclusive scan of tout
     int64_t x = tout;
 #pragma unroll
@@ -444,7 +542,8 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
     running += __shfl(x, 63, 64);
     prev_exit = __shfl(tex, (k1 - base) >= 64 ? 63 : (k1 - base - 1), 64);
     // fragment starts inside this segment: walk from its entry to each 64 KiB output boundary
-    if (valid && tout > 0) {
+    // (page mode decodes whole pages in order and needs none)
+    if (valid && tout > 0 && !X.page_mode) {
       int64_t F = (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG;
       int64_t p = e, o = ob;
       while (F < ob + tout) {
@@ -531,6 +630,8 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
   // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map
   __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX + 16) / 16];
   __shared__ u32x4 prm[64];                // per-tag (ot, src, mode | per << 8, rcp)
+  __shared__ uint32_t BW[SF_FW / 32 + 4];  // tag-start bits of the window's 64-byte blocks (bitmap mode)
+  __shared__ int16_t TP[64];               // bitmap discovery: offsets of the batch's tags
   uint8_t* L = (uint8_t*)lds4;
   uint32_t* W32 = (uint32_t*)(L + SNAP_RING);
   uint8_t* M = L + SNAP_RING + SF_FW + 16;
@@ -566,8 +667,12 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
   o1 = __builtin_amdgcn_readfirstlane(o1);
   GAS uint8_t* gout = gp(out);
   const GAS uint8_t* gin = gp(in);
-  int32_t ws = 0;
-  // window = stream bytes [ws, ws + SF_FW), ws 4-byte aligned relative to the buffer
+  int32_t ws = 0, wb0 = 0;
+  // page mode with a tag-start bitmap (k_snap_walk / link / fix): tags are found by bit counting
+  const bool use_bits = X.tbits != nullptr && wk.y < 0;
+  const GAS uint32_t* pbits = use_bits ? (const GAS uint32_t*)(X.tbits + (int64_t)X.sbase[wk.x] * (SNAP_SEG / 64)) : nullptr;
+  // window = stream bytes [ws, ws + SF_FW), ws 4-byte aligned relative to the buffer; in bitmap mode
+  // also the bits of the 64-byte blocks from wb0 = ws rounded down to 64 (dwords of 32 positions)
   auto refill = [&](int32_t at) {
     const uintptr_t a4 = ((uintptr_t)(in + at)) & ~(uintptr_t)3;
     ws = at - (int32_t)((uintptr_t)(in + at) - a4);
@@ -578,8 +683,19 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
       const uintptr_t ad = a4 + (uintptr_t)(lane + 64 * k) * 4;
       v[k] = *(const GAS uint32_t*)(ad < lim ? ad : lim);
     }
+    uint32_t bw = 0, bw2 = 0;
+    if (use_bits) {                                  // SF_FW / 32 + 4 = 68 dwords: lanes 0-3 take two
+      wb0 = (ws < 0 ? 0 : ws) & ~63;
+      const int32_t nbw = (((clen + 63) >> 6) << 1) - (wb0 >> 5);    // bitmap dwords left in the page
+      if (lane < nbw) bw = pbits[(wb0 >> 5) + lane];
+      if (lane < SF_FW / 32 + 4 - 64 && 64 + lane < nbw) bw2 = pbits[(wb0 >> 5) + 64 + lane];
+    }
 #pragma unroll
     for (int k = 0; k < SF_FW / 256; k++) W32[lane + 64 * k] = v[k];
+    if (use_bits) {
+      BW[lane] = bw;
+      if (lane < SF_FW / 32 + 4 - 64) BW[64 + lane] = bw2;
+    }
   };
   int32_t o = o0, flushed = o0;
   auto flush_to = [&](int32_t upto) {          // ring -> HBM, 16-byte granules
@@ -604,9 +720,66 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
     STIME(13);                                   // loop top + refill
     // ---- 1. tag starts ----
     int32_t n = 0, t = p, outsum = 0, vstart = 0, biglen = 0;
+    if (use_bits) {
+      // 256 candidate bytes, 4 per lane: the set bits are the tag starts; a wave scan ranks them
+      // and each tag's offset lands in TP[rank]; lane i then parses tag i from the LDS window
+      const int32_t q = t + 4 * lane, rel = q - wb0;
+      uint32_t b4 = 0;
+      if (q < ce) {
+        const uint64_t d = ((uint64_t)BW[(rel >> 5) + 1] << 32) | BW[rel >> 5];
+        b4 = (uint32_t)(d >> (rel & 31)) & 15u;
+      }
+      const int32_t cnt = __popc(b4);
+      const int32_t incl = dpp_scan_add(cnt);
+      const int32_t nt = __builtin_amdgcn_readlane(incl, 63);
+      int32_t r0 = incl - cnt;
+      for (int bb = 0; bb < 4; bb++)
+        if ((b4 >> bb) & 1) { if (r0 < 64) TP[r0] = (int16_t)(4 * lane + bb); r0++; }
+      const int32_t nw = nt < 64 ? nt : 64;
+      const bool intag = lane < nw;
+      const int32_t pos = intag ? (int32_t)TP[lane] : 0;
+      int32_t ol = 0, adv = 1;
+      if (intag) {
+        const int32_t ix = t + pos - ws;
+        const uint64_t d = ((((uint64_t)W32[(ix >> 2) + 1]) << 32) | W32[ix >> 2]) >> (8 * (ix & 3));
+        const uint32_t tag = (uint32_t)d & 0xff, kind = tag & 3;
+        if (kind == 0) {
+          uint32_t l = (tag >> 2) + 1, hdr = 1;
+          if (l > 60) {
+            const uint32_t nb = l - 60;
+            hdr += nb;
+            l = (uint32_t)((d >> 8) & (nb == 4 ? 0xffffffffull : ((1ull << (8 * nb)) - 1))) + 1;
+          }
+          ol = l > 0x40000000u ? 0x40000000 : (int32_t)l;
+          adv = (int32_t)hdr + ol;
+        } else {
+          adv = kind == 1 ? 2 : (kind == 2 ? 3 : 5);
+          ol = kind == 1 ? (int32_t)(((tag >> 2) & 7) + 4) : (int32_t)((tag >> 2) + 1);
+        }
+      }
+      SSTAT(12, 1);
+      const int32_t pre = dpp_scan_add(intag ? ol : 0);
+      const bool big = intag && ol > 64;
+      const bool stop = intag && (big || pre - ol >= SF_BOUT);
+      const unsigned long long sm = __ballot(stop);
+      const int32_t acc = sm ? (int32_t)(__ffsll((long long)sm) - 1) : nw;
+      if (nw == 0 || __builtin_amdgcn_readlane(pos, 0) != 0) {
+        bad = true;                                     // the bitmap lost the chain: serial path
+      } else if (acc == 0) {
+        biglen = __builtin_amdgcn_readlane(ol, 0);      // a literal over 64 bytes runs alone
+      } else {
+        if (lane < acc) vstart = t + pos;
+        outsum = __builtin_amdgcn_readlane(pre, acc - 1);
+        n = acc;
+        t = acc < nw ? t + __builtin_amdgcn_readlane(pos, acc)
+                     : t + __builtin_amdgcn_readlane(pos, acc - 1) + __builtin_amdgcn_readlane(adv, acc - 1);
+      }
+      if (bad) break;
+    }
     // windows of 64 candidate bytes until the batch is full; the window data (tags + literals of
     // up to 64 bytes) must stay inside the LDS copy of the stream
-    for (int r = 0; r < 8 && t < ce && n < 64 && outsum < SF_BOUT && (t + 200 <= ws + SF_FW || ws + SF_FW >= clen);
+    for (int r = 0; !use_bits && r < 8 && t < ce && n < 64 && outsum < SF_BOUT &&
+                    (t + 200 <= ws + SF_FW || ws + SF_FW >= clen);
          r++) {
       // candidate tag at t + lane: advance (bytes to the next tag) and output length
       int32_t adv = 1, olen = 0;
@@ -3346,13 +3519,21 @@ static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s
 }
 
 // phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback; n_frag < 0: page mode
-// (phases 0 and 1 skipped; work holds one (page, -1) item per compressed page)
+// (work holds one (page, -1) item per compressed page; phases 0 and 1 only build the tag-start
+// bitmap, when X.tbits is set)
 void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int phase, hipStream_t s) {
   if (!n_cp) return;
   const int g = (X.nseg + NT - 1) / NT;
   if (n_frag < 0) {
-    if (phase == 0) (void)hipMemsetAsync(X.serial, 0, (size_t)n_cp * 4, s);
-    else if (phase == 2) launch_frag(X, n_cp, work, s);
+    if (phase == 0) {
+      (void)hipMemsetAsync(X.serial, 0, (size_t)n_cp * 4, s);
+      if (X.tbits) {                      // tag-start bitmap: speculative walk + link
+        hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
+        hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+      }
+    } else if (phase == 1) {
+      if (X.tbits) hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
+    } else if (phase == 2) launch_frag(X, n_cp, work, s);
     else if (phase == 3)
       hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
                          X.cpage, (const int32_t*)X.serial);
