@@ -46,6 +46,25 @@ class dk_skip_program(C.Structure):
                 ("n_ops", C.c_int32), ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64), ("lit", C.c_int64 * 64)]
 
 
+class dk_read_options(C.Structure):
+    _fields_ = [("field_ids", C.c_void_p), ("predicate", C.c_void_p), ("row_index", C.c_int32),
+                ("window_rows", C.c_int32)]
+
+
+class dk_batch_column(C.Structure):
+    _fields_ = [("present", C.c_int32), ("phys", C.c_int32), ("width", C.c_int32), ("max_def", C.c_int32),
+                ("max_rep", C.c_int32), ("rep_def", C.c_int32), ("n_values", C.c_int64), ("value_offset", C.c_int64),
+                ("row_def", C.c_void_p), ("row_offs", C.c_void_p), ("validity", C.c_void_p),
+                ("entry_def", C.c_void_p), ("fixed", C.c_void_p), ("offs", C.c_void_p), ("chars", C.c_void_p)]
+
+
+class dk_batch(C.Structure):
+    _fields_ = [("file", C.c_int32), ("n_cols", C.c_int32), ("n_rows", C.c_int64),
+                ("cols", C.POINTER(dk_batch_column)), ("row_index", C.c_void_p)]
+
+
+MAX_LEAF_DEPTH = 8
+
 EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
            "dk_parquet_first_row", "dk_parquet_column_rows",
@@ -55,7 +74,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free", "dk_parquet_open_rg", "dk_parquet_row_groups",
            "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits", "dk_parquet_open_sel",
-           "dk_parquet_prune_row_groups", "dk_parquet_nonnull_row_groups"]
+           "dk_parquet_prune_row_groups", "dk_parquet_nonnull_row_groups",
+           "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close"]
 
 
 def lib(build_if_missing=True):
@@ -105,6 +125,12 @@ def lib(build_if_missing=True):
         "dk_replay_ckpt_selection": (C.c_int, [P, I32, P, I64]),
         "dk_replay_kernel_stats": (C.c_int, [P, I32, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(I64)]),
         "dk_replay_free": (None, [P]),
+        "dk_reader_open": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32,
+                                     C.POINTER(dk_read_options), C.POINTER(P)]),
+        "dk_reader_next": (C.c_int, [P, C.POINTER(C.POINTER(dk_batch))]),
+        "dk_reader_num_rows": (I64, [P, I32]),
+        "dk_batch_release": (None, [C.POINTER(dk_batch)]),
+        "dk_reader_close": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -125,6 +125,19 @@ struct DColumn {
   uint64_t* dhash;       // key columns: path hash of every dictionary entry (k_string_copy)
 };
 
+// streaming reader: one leaf's window of batches -> validity bits + int32 offsets (dk_arrow.hip)
+struct ArrowWin {
+  const uint8_t* def;          // per value definition levels (row_def or entry_def), window-based
+  const int64_t* offs;         // byte-array offsets (nv + 1), window-based, or null
+  const int64_t* row_offs;     // repeated leaf: entry offsets per row (nr + 1), window-based, or null
+  int64_t nv, nr;              // values / rows in the window
+  int32_t max_def;
+  uint64_t* bits;              // out: ceil(nv / 64) words
+  int32_t* offs32;             // out: nv + 1
+  int32_t* row_offs32;         // out: nr + 1
+  int32_t* overflow;           // out: set when a rebased offset does not fit int32
+};
+
 constexpr uint32_t kDecodeSeed = 0;   // seed of the path hashes computed during decode
 constexpr int DK_COPY_TILE = 128;     // values per k_string_copy workgroup (host tile table step)
 

@@ -12,6 +12,7 @@
 #include <atomic>
 #include <chrono>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <vector>
@@ -26,6 +27,7 @@ void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const SnapCtx&, int, int, const int2*, int, hipStream_t);
 void snap_stats(unsigned long long*);
 void launch_pack_bits(const uint8_t*, long long, uint8_t*, hipStream_t);
+void launch_arrow_window(const ArrowWin&, hipStream_t);
 void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
@@ -67,9 +69,10 @@ extern "C" int dk_debug_snap_stats(int64_t out[24]) { snap_stats((unsigned long 
 // ------------------------------------------------------------------------------------------------
 // engine
 // ------------------------------------------------------------------------------------------------
+// The engine holds configuration only; every call object owns its stream, so one engine can be used
+// from several threads at once (each reader / replay stays single-threaded, like Kernel iterators).
 struct dk_engine {
   dk_config cfg;
-  hipStream_t stream = nullptr;
 };
 
 extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
@@ -88,7 +91,6 @@ extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
   HIPOK(hipSetDevice(c.device));
   auto* e = new dk_engine();
   e->cfg = c;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return fail("stream"); }
   *out = e;
   return 0;
 }
@@ -96,7 +98,6 @@ extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
 extern "C" void dk_engine_destroy(dk_engine* e) {
   if (!e) return;
   hipSetDevice(e->cfg.device);
-  if (e->stream) hipStreamDestroy(e->stream);
   delete e;
 }
 
@@ -117,6 +118,15 @@ struct DBuf {
   template <class T> T* as() const { return (T*)p; }
 };
 
+// A HIP stream owned by one call object (dk_parquet, dk_replay, dk_reader): Kernel calls
+// readParquetFiles from several connector threads at once (MultiThreadedTableReader.java:244), so
+// nothing of a call runs on a stream shared through the engine.
+struct StreamH {
+  hipStream_t s = nullptr;
+  ~StreamH() { if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); } }
+  int create() { return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? 0 : fail("hipStreamCreate failed"); }
+};
+
 // ------------------------------------------------------------------------------------------------
 // Parquet footer (FileMetaData) + offset index
 // ------------------------------------------------------------------------------------------------
@@ -126,6 +136,9 @@ struct SchemaEl {
   std::string name;
   int type = -1, type_length = 0, repetition = 0, num_children = 0;
   int conv = -1, logical = -1, int_bits = 0, int_signed = 1;
+  int field_id = -1;                    // SchemaElement.field_id (9), -1 when absent
+  std::vector<int> kids;                // children (schema element indices), in file order
+  int leaf = -1;                        // leaf index of a primitive element
 };
 // Statistics (parquet.thrift): deprecated max(1) / min(2), null_count(3), max_value(5) / min_value(6)
 struct StatsM {
@@ -283,6 +296,7 @@ static int parse_footer(FileM& f) {
           else if (i2 == 4) s.name = read_string(t);
           else if (i2 == 5) s.num_children = (int)t.zigzag();
           else if (i2 == 6) s.conv = (int)t.zigzag();
+          else if (i2 == 9) s.field_id = (int)t.zigzag();
           else if (i2 == 10 && t2 == 12) {        // LogicalType union: the set member's field id
             int l3 = 0, t3, i3;
             while ((i3 = t.field(&l3, &t3))) {
@@ -349,21 +363,23 @@ static int parse_footer(FileM& f) {
   }
   if (t.bad || f.schema.empty()) return fail("Error reading Parquet file: " + f.path + " (corrupt footer)");
   // leaves (DFS over the flattened schema)
-  struct Fr { int remaining, def, rep, rep_def; std::string path; };
+  struct Fr { int remaining, def, rep, rep_def; std::string path; int el; };
   std::vector<Fr> st;
-  st.push_back({f.schema[0].num_children, 0, 0, 0, ""});
+  st.push_back({f.schema[0].num_children, 0, 0, 0, "", 0});
   size_t pos = 1;
   while (!st.empty()) {
     if (st.back().remaining == 0) { st.pop_back(); continue; }
     st.back().remaining--;
     if (pos >= f.schema.size()) return fail("Error reading Parquet file: " + f.path + " (bad schema)");
-    const SchemaEl& e = f.schema[pos++];
+    f.schema[st.back().el].kids.push_back((int)pos);
+    SchemaEl& e = f.schema[pos++];
+    if (e.num_children <= 0) e.leaf = (int)f.leaves.size();
     Fr& top = st.back();
     int def = top.def + (e.repetition != 0 ? 1 : 0);
     int rep = top.rep + (e.repetition == 2 ? 1 : 0);
     int rep_def = e.repetition == 2 ? def : top.rep_def;
     std::string path = top.path.empty() ? e.name : top.path + "." + e.name;
-    if (e.num_children > 0) st.push_back({e.num_children, def, rep, rep_def, path});
+    if (e.num_children > 0) st.push_back({e.num_children, def, rep, rep_def, path, (int)pos - 1});
     else {
       LeafM L{path, e.type, e.type_length, def, rep, rep_def};
       L.leaf_rep = e.repetition;
@@ -439,12 +455,65 @@ static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef
   return 0;
 }
 
-static int leaf_index(const FileM& f, const std::string& want) {
-  for (size_t i = 0; i < f.leaves.size(); i++) if (f.leaves[i].path == want) return (int)i;
-  auto low = [](std::string s) { for (auto& c : s) c = (char)tolower((unsigned char)c); return s; };
-  std::string w = low(want);
-  for (size_t i = 0; i < f.leaves.size(); i++) if (low(f.leaves[i].path) == w) return (int)i;
-  return -1;
+// The file leaf of a projected column, resolved one schema level at a time as
+// ParquetSchemaUtils.findSubFieldType does (ParquetSchemaUtils.java:92-119): by the Kernel field's
+// parquet.field.id when it has one and a child carries that id, then by exact name, then by the first
+// case-insensitive name. Every struct group descended into builds its id -> child map first, so a
+// group with two children of the same id fails (getParquetFieldToTypeMap, :122-138). Inside a map the
+// key_value / key / value levels are structural (the repeated child, its first and second field).
+// ids: one entry per dotted component (-1 = no id), or null. Returns the leaf index, -1 when the
+// column is absent (read as all-null), -2 on error (g_err set).
+static constexpr int kMaxLeafDepth = 8;
+static int leaf_index(const FileM& f, const std::string& want, const int32_t* ids = nullptr) {
+  std::vector<std::string> comps;
+  for (size_t a = 0;;) {
+    const size_t b = want.find('.', a);
+    comps.push_back(want.substr(a, b == std::string::npos ? std::string::npos : b - a));
+    if (b == std::string::npos) break;
+    a = b + 1;
+  }
+  auto low = [](std::string x) { for (auto& c : x) c = (char)tolower((unsigned char)c); return x; };
+  int g = 0;
+  int map_level = 0;                        // 1: g is a MAP group, 2: g is a map's key_value group
+  for (size_t ci = 0; ci < comps.size(); ci++) {
+    const SchemaEl& G = f.schema[g];
+    if (G.kids.empty()) return -1;          // a primitive where the projection expects a group
+    const std::string& name = comps[ci];
+    int hit = -1;
+    if (map_level == 0 && (G.conv == 1 || G.logical == 2)) map_level = 1;   // MAP annotation
+    if (map_level == 1) {
+      if (G.kids.size() == 1 && f.schema[G.kids[0]].repetition == 2) hit = G.kids[0];
+      map_level = hit >= 0 ? 2 : 0;
+    } else if (map_level == 2) {
+      if (G.kids.size() == 2 && (name == "key" || name == "value")) hit = G.kids[name == "key" ? 0 : 1];
+      map_level = 0;
+    }
+    if (hit < 0) {
+      // a struct group: id map first (duplicate ids fail even when the read schema has none)
+      std::vector<std::pair<int, int>> by_id;
+      for (int k : G.kids)
+        if (f.schema[k].field_id >= 0) {
+          for (auto& q : by_id)
+            if (q.first == f.schema[k].field_id) {
+              fail("java.lang.IllegalStateException: Parquet file contains multiple columns (" +
+                   f.schema[q.second].name + ", " + f.schema[k].name + ") with the same field id");
+              return -2;
+            }
+          by_id.push_back({f.schema[k].field_id, k});
+        }
+      const int id = ids && ci < (size_t)kMaxLeafDepth ? ids[ci] : -1;
+      if (id >= 0)
+        for (auto& q : by_id) if (q.first == id) { hit = q.second; break; }
+      if (hit < 0) for (int k : G.kids) if (f.schema[k].name == name) { hit = k; break; }
+      if (hit < 0) {
+        const std::string w = low(name);
+        for (int k : G.kids) if (low(f.schema[k].name) == w) { hit = k; break; }
+      }
+    }
+    if (hit < 0) return -1;
+    g = hit;
+  }
+  return f.schema[g].leaf;                  // -1 when the path ends on a group
 }
 
 static int phys_width(int phys, int tl) {
@@ -498,6 +567,8 @@ struct HostCol {           // host mirror of one decoded column (filled on deman
 };
 
 struct dk_parquet {
+  StreamH own;                      // first member: destroyed after every buffer below
+  hipStream_t stream = nullptr;
   dk_engine* eng = nullptr;
   std::vector<FileM> files;
   std::vector<std::string> leaves;
@@ -573,8 +644,8 @@ static bool snap_page_mode(const dk_parquet* p) {
 
 // the decode pipeline (mode: -1 = headers only; 0 = prepare pass through the scans, which size the
 // outputs; 1 = full step)
-static int run_pipeline(dk_parquet* p, int mode) {
-  hipStream_t s = p->eng->stream;
+static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
+  if (!s) s = p->stream;
   KTimer& T = p->timer;
   const DChunk* C = p->d_chunks.as<DChunk>();
   DPage* P = p->d_pages.as<DPage>();
@@ -652,7 +723,7 @@ static std::string page_status_msg(const dk_parquet* p, const std::vector<DPage>
 }
 
 static int prepare(dk_parquet* p) {
-  hipStream_t s = p->eng->stream;
+  hipStream_t s = p->stream;
   // 1. parse headers once to size the scratch areas
   if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;
   if (upload(p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), s)) return 1;
@@ -1197,6 +1268,7 @@ extern "C" int dk_parquet_nonnull_row_groups(const char* path, const char* leaf,
   if (read_footer(f) || parse_footer(f)) return 1;
   *n = (int32_t)f.rgs.size();
   const int idx = leaf ? leaf_index(f, leaf) : -1;
+  if (idx == -2) return 1;
   for (int32_t g = 0; g < *n && g < cap; g++) {
     if (idx < 0) { keep[g] = 0; continue; }                 // a missing leaf is null everywhere
     const ColMeta& m = f.rgs[g].cols[idx];
@@ -1220,7 +1292,8 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
 }
 
 static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
-                        int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out);
+                        int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
+                        const int32_t* field_ids = nullptr);
 
 // fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads
 template <class F>
@@ -1273,18 +1346,21 @@ extern "C" int dk_parquet_open_sel(dk_engine* e, const char* const* paths, int32
 }
 
 static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
-                        int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out) {
+                        int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
+                        const int32_t* field_ids) {
   if (!e) return fail("null engine");
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_parquet> p(new dk_parquet());
   p->eng = e;
+  if (p->own.create()) return 1;
+  p->stream = p->own.s;
   p->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
   for (int i = 0; i < n_leaves; i++) p->leaves.push_back(leaves[i]);
   p->files.resize(n_files);
   p->colmap.assign(n_files, std::vector<int>(n_leaves, -1));
   p->leafidx.assign(n_files, std::vector<int>(n_leaves, -1));
   p->dfile.resize(n_files);
-  hipStream_t s = e->stream;
+  hipStream_t s = p->stream;
   // host I/O in parallel over files (footer, row-group selection, projected column chunks):
   // DefaultParquetHandler reads files one after another; here every file of the call is in flight
   std::vector<std::string> errs(n_files > 0 ? n_files : 0);
@@ -1297,7 +1373,9 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
     // projection: only the chunks (and offset indexes) of the requested leaves travel to HBM
     std::vector<Span> want;
     for (int li = 0; li < n_leaves; li++) {
-      int idx = leaf_index(f, p->leaves[li]);
+      const int idx = leaf_index(f, p->leaves[li], field_ids ? field_ids + (size_t)li * kMaxLeafDepth : nullptr);
+      if (idx == -2) { errs[fi] = g_err; return; }
+      p->leafidx[fi][li] = idx;
       if (idx < 0) continue;
       for (int32_t g : f.sel) {
         const ColMeta& m = f.rgs[g].cols[idx];
@@ -1319,8 +1397,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   for (int fi = 0; fi < n_files; fi++) {
     FileM& f = p->files[fi];
     for (int li = 0; li < n_leaves; li++) {
-      int idx = leaf_index(f, p->leaves[li]);
-      p->leafidx[fi][li] = idx;
+      const int idx = p->leafidx[fi][li];
       if (idx < 0) continue;
       const LeafM& L = f.leaves[idx];
       if (L.max_rep > 1) return fail("Error reading Parquet file: " + f.path + " (nested repetition not supported: " + L.path + ")");
@@ -1388,8 +1465,8 @@ extern "C" int dk_parquet_decode(dk_parquet* p) {
   hipSetDevice(p->eng->cfg.device);
   DState st0{};
   st0.err_row = LLONG_MAX;
-  HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, p->eng->stream));
-  KTimer::Scope sc(&p->timer, 12, p->eng->stream);
+  HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, p->stream));
+  KTimer::Scope sc(&p->timer, 12, p->stream);
   for (auto& h : p->host) h.ready = false;
   return run_pipeline(p, 1);
 }
@@ -1407,7 +1484,8 @@ static int check_state(dk_parquet* p) {
 }
 
 extern "C" int dk_parquet_sync(dk_parquet* p) {
-  HIPOK(hipStreamSynchronize(p->eng->stream));
+  hipSetDevice(p->eng->cfg.device);   // this thread may not have used the device yet
+  HIPOK(hipStreamSynchronize(p->stream));
   p->timer.collect();
   return check_state(p);
 }
@@ -1481,8 +1559,9 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
 }
 
 extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out) {
+  hipSetDevice(p->eng->cfg.device);   // this thread may not have used the device yet
   memset(out, 0, sizeof *out);
-  HIPOK(hipStreamSynchronize(p->eng->stream));
+  HIPOK(hipStreamSynchronize(p->stream));
   if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
   int ci = p->colmap[file][leaf];
   out->n_rows = p->files[file].num_rows;
@@ -1540,7 +1619,7 @@ extern "C" int dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, i
   const DColumn& c = p->h_cols[ci];
   if (!c.n_rows) return 0;
   hipSetDevice(p->eng->cfg.device);
-  hipStream_t s = p->eng->stream;
+  hipStream_t s = p->stream;
   if (!p->d_first.p && p->d_first.alloc(8)) return 1;
   const unsigned long long none = ~0ull;
   HIPOK(hipMemcpyAsync(p->d_first.p, &none, 8, hipMemcpyHostToDevice, s));
@@ -1555,8 +1634,9 @@ extern "C" int dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, i
 
 extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf, int64_t row0, int64_t n,
                                       dk_column* out) {
+  hipSetDevice(p->eng->cfg.device);   // this thread may not have used the device yet
   memset(out, 0, sizeof *out);
-  HIPOK(hipStreamSynchronize(p->eng->stream));
+  HIPOK(hipStreamSynchronize(p->stream));
   if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
   if (row0 < 0 || n < 0 || row0 + n > p->files[file].num_rows) return fail("bad row range");
   int ci = p->colmap[file][leaf];
@@ -1604,7 +1684,7 @@ extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf,
 extern "C" void dk_parquet_close(dk_parquet* p) {
   if (!p) return;
   hipSetDevice(p->eng->cfg.device);
-  hipStreamSynchronize(p->eng->stream);
+  hipStreamSynchronize(p->stream);
   delete p;
 }
 
@@ -2080,6 +2160,9 @@ extern "C" void dk_json_tail_free(dk_json_tail* t) { delete t; }
 // replay
 // ------------------------------------------------------------------------------------------------
 struct dk_replay {
+  StreamH own;                          // the replay's stream (the checkpoint decode runs on it too)
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;   // ordering against the checkpoint's own stream
   dk_engine* eng = nullptr;
   dk_json_tail* tail = nullptr;
   dk_parquet* ck = nullptr;
@@ -2120,8 +2203,13 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_replay> r(new dk_replay());
   r->eng = e; r->tail = tail; r->ck = ckpt;
+  if (r->own.create()) return 1;
+  r->stream = r->own.s;
+  if (ckpt && (hipEventCreateWithFlags(&r->ev_in, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreateWithFlags(&r->ev_out, hipEventDisableTiming) != hipSuccess))
+    return fail("hipEventCreate failed");
   r->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
-  hipStream_t s = e->stream;
+  hipStream_t s = r->stream;
   // actions: removes and adds of each tail row (a row may carry both)
   std::vector<uint8_t> jchars;
   int64_t canon_n = 0;
@@ -2395,7 +2483,7 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
 }
 
 static int replay_launch(dk_replay* r) {
-  hipStream_t s = r->eng->stream;
+  hipStream_t s = r->stream;
   KTimer& T = r->timer;
   KTimer::Scope total(&T, 12, s);
   DState st0{};
@@ -2424,9 +2512,12 @@ static int replay_launch(dk_replay* r) {
   }
   if (r->ck) {
     dk_parquet* p = r->ck;
+    // the decode runs on the replay's stream, after anything queued on the checkpoint's own
+    HIPOK(hipEventRecord(r->ev_in, p->stream));
+    HIPOK(hipStreamWaitEvent(s, r->ev_in, 0));
     // decode errors are collected into the replay state too
     HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
-    if (run_pipeline(p, 1)) return 1;
+    if (run_pipeline(p, 1, s)) return 1;
     for (size_t fi = 0; fi < r->probe.size(); fi++) {
       KTimer::Scope sc(&T, 11, s);
       ProbeCols pc = r->probe[fi];
@@ -2446,6 +2537,9 @@ static int replay_launch(dk_replay* r) {
         KTimer::Scope sc(&T, 17, s);
         launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
     }
+    // later work on the checkpoint's stream (column reads) sees the decoded columns
+    HIPOK(hipEventRecord(r->ev_out, s));
+    HIPOK(hipStreamWaitEvent(p->stream, r->ev_out, 0));
   }
   return 0;
 }
@@ -2458,7 +2552,8 @@ extern "C" int dk_replay_run(dk_replay* r) {
 }
 
 extern "C" int dk_replay_sync(dk_replay* r) {
-  hipStream_t s = r->eng->stream;
+  hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
+  hipStream_t s = r->stream;
   for (int attempt = 0; attempt < 8; attempt++) {
     HIPOK(hipStreamSynchronize(s));
     r->timer.collect();
@@ -2520,6 +2615,7 @@ extern "C" int dk_replay_counters_split(dk_replay* r, int64_t tail[5], int64_t c
 }
 
 extern "C" int dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n) {
+  hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   if (!r->have_result) return fail("replay has no result");
   if (!r->tail || n != r->tail->rows) return fail("bad selection size");
   memset(out, 0, n);
@@ -2530,6 +2626,7 @@ extern "C" int dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n) {
 }
 
 extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out, int64_t n) {
+  hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   if (!r->have_result) return fail("replay has no result");
   if (!r->ck || file < 0 || file >= (int)r->d_csel.size()) return fail("bad checkpoint file index");
   if (n != r->ck->files[file].num_rows) return fail("bad selection size");
@@ -2539,11 +2636,12 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
 }
 
 extern "C" int dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* dst, int64_t n, int32_t dst_on_device) {
+  hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   if (!r->have_result) return fail("dk_replay_ckpt_selection_bits: no result (run + sync first)");
   if (!r->ck || file < 0 || file >= (int)r->d_csel.size()) return fail("bad checkpoint file index");
   if (n != r->ck->files[file].num_rows) return fail("bad selection size");
   const int64_t nb = (n + 7) / 8;
-  hipStream_t s = r->eng->stream;
+  hipStream_t s = r->stream;
   if (dst_on_device) {
     launch_pack_bits(r->d_csel[file]->as<uint8_t>(), n, (uint8_t*)dst, s);
     HIPOK(hipStreamSynchronize(s));
@@ -2571,6 +2669,335 @@ extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name
 extern "C" void dk_replay_free(dk_replay* r) {
   if (!r) return;
   hipSetDevice(r->eng->cfg.device);
-  hipStreamSynchronize(r->eng->stream);
+  hipStreamSynchronize(r->stream);
+  if (r->ev_in) hipEventDestroy(r->ev_in);
+  if (r->ev_out) hipEventDestroy(r->ev_out);
   delete r;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Streaming ParquetHandler reader (dk_reader_*): ParquetHandler.readParquetFiles as Kernel consumes
+// it -- a CloseableIterator<ColumnarBatch> of at most parquet.reader.batch-size rows per batch, in
+// input-file order then row order (ParquetHandler.java:59-68, ParquetFileReader.java:54-147), safe to
+// close early (ScanImpl.java:376-392). The files are decoded on the GPU when the reader opens; batches
+// are then shipped to pinned host memory one window (about 1M rows) at a time: validity bits and
+// int32 offsets are built on the device (k_arrow_window), the other buffers are slices of the
+// decoded columns.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct PinnedBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  ~PinnedBuf() { if (p) hipHostFree(p); }
+  int reserve(size_t n) {
+    if (n <= cap) return 0;
+    if (p) { hipHostFree(p); p = nullptr; cap = 0; }
+    if (hipHostMalloc((void**)&p, n, hipHostMallocDefault) != hipSuccess) { p = nullptr; return fail("hipHostMalloc failed"); }
+    cap = n;
+    return 0;
+  }
+};
+
+struct WinLeaf {                 // one leaf's buffers inside a window (offsets into the host buffer)
+  int present = 0, null_only = 0;
+  int64_t nv = 0, nchars = 0;
+  size_t o_rowdef = 0, o_entdef = 0, o_fixed = 0, o_chars = 0, o_bits = 0, o_offs = 0, o_rowoffs = 0;
+};
+
+struct RWin {                    // rows [r0, r0 + nr) of one file in pinned host memory
+  int file = -1;
+  int64_t r0 = 0, nr = 0;
+  PinnedBuf buf;
+  std::vector<WinLeaf> leaf;
+  size_t o_rowidx = 0;
+  int refs = 0;                  // outstanding batches (+1 while it is the reader's current window)
+};
+
+}  // namespace
+
+struct dk_reader {
+  StreamH own;
+  dk_engine* eng = nullptr;
+  dk_parquet* p = nullptr;
+  std::vector<std::string> leaves;
+  int B = 1024;
+  int64_t W = 1 << 20;
+  bool row_index = false;
+  int file = 0;
+  int64_t next = 0;              // next row of `file`
+  RWin* cur = nullptr;
+  std::vector<RWin*> pool;       // windows no batch refers to any more
+  std::mutex mu;                 // batches may be released from other threads
+  int outstanding = 0;           // live batches
+  bool closed = false;
+  DBuf d_stage, d_ovf;
+  // row-index map per file: (first selected row, file row) of every selected row group
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> rgmap;
+  ~dk_reader() {
+    delete cur;
+    for (RWin* w : pool) delete w;
+    if (p) dk_parquet_close(p);
+  }
+};
+
+struct dk_batch_impl {
+  dk_batch pub;
+  std::vector<dk_batch_column> cols;
+  dk_reader* rd;
+  RWin* win;
+};
+
+static void reader_maybe_free(dk_reader* r, std::unique_lock<std::mutex>& lk) {
+  if (r->closed && r->outstanding == 0) { lk.unlock(); delete r; }
+}
+
+extern "C" int dk_reader_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                              int32_t n_leaves, const dk_read_options* opt, dk_reader** out) {
+  *out = nullptr;
+  if (!e) return fail("null engine");
+  hipSetDevice(e->cfg.device);
+  std::unique_ptr<dk_reader> r(new dk_reader());
+  r->eng = e;
+  r->B = e->cfg.parquet_batch_size > 0 ? e->cfg.parquet_batch_size : 1024;
+  if (opt && opt->window_rows > 0) r->W = opt->window_rows;
+  r->W = std::max<int64_t>(r->B, r->W / r->B * r->B);
+  r->row_index = opt && opt->row_index;
+  for (int i = 0; i < n_leaves; i++) r->leaves.push_back(leaves[i]);
+  if (r->own.create()) return 1;
+  // the predicate prunes row groups (best effort, like parquet-mr's StatisticsFilter: never rows)
+  std::vector<std::vector<int32_t>> groups(n_files > 0 ? n_files : 0);
+  for (int32_t fi = 0; fi < n_files; fi++) {
+    FileM f;
+    f.path = paths[fi];
+    if (read_footer(f) || parse_footer(f)) return 1;
+    std::vector<uint8_t> keep(f.rgs.size() + 1, 1);
+    int32_t ng = 0;
+    if (opt && opt->predicate &&
+        dk_parquet_prune_row_groups(paths[fi], opt->predicate, keep.data(), (int32_t)keep.size(), &ng)) return 1;
+    int64_t at = 0, sel = 0;
+    std::vector<std::pair<int64_t, int64_t>> m;
+    for (int32_t g = 0; g < (int32_t)f.rgs.size(); g++) {
+      if (keep[g]) { groups[fi].push_back(g); m.push_back({sel, at}); sel += f.rgs[g].num_rows; }
+      at += f.rgs[g].num_rows;
+    }
+    r->rgmap.push_back(m);
+  }
+  if (parquet_open(e, paths, n_files, leaves, n_leaves, &groups, &r->p, opt ? opt->field_ids : nullptr)) return 1;
+  if (dk_parquet_decode(r->p) || dk_parquet_sync(r->p)) return 1;
+  if (r->d_ovf.alloc(16)) return 1;
+  *out = r.release();
+  return 0;
+}
+
+// file rows [r0, r0 + nr) of the reader's current file into a window
+static int load_window(dk_reader* r, RWin* w, int64_t r0, int64_t nr) {
+  dk_parquet* p = r->p;
+  const int fi = r->file;
+  const hipStream_t s = r->own.s;
+  const size_t nl = r->leaves.size();
+  w->file = fi; w->r0 = r0; w->leaf.assign(nl, WinLeaf());
+  // value / char ranges of the window (two int64 per leaf and level from HBM)
+  struct Rng { int64_t v0 = 0, v1 = 0, c0 = 0, c1 = 0; };
+  std::vector<Rng> rg(nl);
+  for (;;) {
+    bool fits = true;
+    for (size_t li = 0; li < nl; li++) {
+      const int ci = p->colmap[fi][li];
+      if (ci < 0) continue;
+      const DColumn& c = p->h_cols[ci];
+      Rng& q = rg[li];
+      q = Rng();
+      if (c.null_only) { q.v0 = c.max_rep > 0 ? 0 : r0; q.v1 = c.max_rep > 0 ? 0 : r0 + nr; continue; }
+      if (c.max_rep > 0) {
+        HIPOK(hipMemcpy(&q.v0, c.row_offs + r0, 8, hipMemcpyDeviceToHost));
+        HIPOK(hipMemcpy(&q.v1, c.row_offs + r0 + nr, 8, hipMemcpyDeviceToHost));
+      } else { q.v0 = r0; q.v1 = r0 + nr; }
+      if (c.phys == PT_BYTE_ARRAY) {
+        HIPOK(hipMemcpy(&q.c0, c.offs + q.v0, 8, hipMemcpyDeviceToHost));
+        HIPOK(hipMemcpy(&q.c1, c.offs + q.v1, 8, hipMemcpyDeviceToHost));
+      }
+      if (q.c1 - q.c0 >= (1ll << 31) - 1 || q.v1 - q.v0 >= (1ll << 31) - 1) fits = false;
+    }
+    if (fits) break;
+    if (nr <= r->B) return fail("Error reading Parquet file: " + p->files[fi].path + " (a batch exceeds 2 GiB)");
+    nr = std::max<int64_t>(r->B, nr / 2 / r->B * r->B);           // int32 offsets: a smaller window
+  }
+  w->nr = nr;
+  // host layout, 64-byte aligned pieces; device staging for bits + int32 offsets
+  size_t hsz = 0, dsz = 0;
+  auto take = [](size_t& at, size_t n) { at = (at + 63) & ~(size_t)63; const size_t o = at; at += n; return o; };
+  std::vector<size_t> d_bits(nl), d_offs(nl), d_roffs(nl);
+  for (size_t li = 0; li < nl; li++) {
+    const int ci = p->colmap[fi][li];
+    WinLeaf& L = w->leaf[li];
+    L.o_rowdef = take(hsz, nr);
+    if (ci < 0) continue;
+    const DColumn& c = p->h_cols[ci];
+    L.present = 1; L.null_only = c.null_only;
+    L.nv = rg[li].v1 - rg[li].v0;
+    L.nchars = rg[li].c1 - rg[li].c0;
+    if (c.max_rep > 0) { L.o_entdef = take(hsz, L.nv); L.o_rowoffs = take(hsz, 4 * (nr + 1)); d_roffs[li] = take(dsz, 4 * (nr + 1)); }
+    L.o_bits = take(hsz, 8 * ((L.nv + 63) / 64)); d_bits[li] = take(dsz, 8 * ((L.nv + 63) / 64));
+    if (c.phys == PT_BYTE_ARRAY) {
+      L.o_offs = take(hsz, 4 * (L.nv + 1)); d_offs[li] = take(dsz, 4 * (L.nv + 1));
+      L.o_chars = take(hsz, L.nchars);
+    } else {
+      L.o_fixed = take(hsz, (size_t)L.nv * c.width);
+    }
+  }
+  if (r->row_index) w->o_rowidx = take(hsz, 8 * nr);
+  if (w->buf.reserve(hsz + 64)) return 1;
+  if (dsz > r->d_stage.n && r->d_stage.alloc(dsz + 64)) return 1;
+  uint8_t* H = w->buf.p;
+  uint8_t* D = r->d_stage.as<uint8_t>();
+  HIPOK(hipMemsetAsync(r->d_ovf.p, 0, 4, s));
+  for (size_t li = 0; li < nl; li++) {
+    const int ci = p->colmap[fi][li];
+    WinLeaf& L = w->leaf[li];
+    if (ci < 0) { memset(H + L.o_rowdef, 0, nr); continue; }
+    const DColumn& c = p->h_cols[ci];
+    HIPOK(hipMemcpyAsync(H + L.o_rowdef, c.row_def + r0, nr, hipMemcpyDeviceToHost, s));
+    if (c.null_only) {          // no value anywhere: all-null values, empty maps
+      memset(H + L.o_bits, 0, 8 * ((L.nv + 63) / 64));
+      if (c.max_rep > 0) { memset(H + L.o_rowoffs, 0, 4 * (nr + 1)); }
+      if (c.phys == PT_BYTE_ARRAY) memset(H + L.o_offs, 0, 4 * (L.nv + 1));
+      else memset(H + L.o_fixed, 0, (size_t)L.nv * c.width);
+      continue;
+    }
+    const int64_t v0 = rg[li].v0;
+    ArrowWin A{};
+    A.def = c.max_rep > 0 ? c.entry_def + v0 : c.row_def + r0;
+    A.offs = c.phys == PT_BYTE_ARRAY ? c.offs + v0 : nullptr;
+    A.row_offs = c.max_rep > 0 ? c.row_offs + r0 : nullptr;
+    A.nv = L.nv; A.nr = c.max_rep > 0 ? nr : 0; A.max_def = c.max_def;
+    A.bits = (uint64_t*)(D + d_bits[li]);
+    A.offs32 = (int32_t*)(D + d_offs[li]);
+    A.row_offs32 = (int32_t*)(D + d_roffs[li]);
+    A.overflow = r->d_ovf.as<int32_t>();
+    launch_arrow_window(A, s);
+    HIPOK(hipMemcpyAsync(H + L.o_bits, D + d_bits[li], 8 * ((L.nv + 63) / 64), hipMemcpyDeviceToHost, s));
+    if (c.max_rep > 0) {
+      HIPOK(hipMemcpyAsync(H + L.o_rowoffs, D + d_roffs[li], 4 * (nr + 1), hipMemcpyDeviceToHost, s));
+      if (L.nv) HIPOK(hipMemcpyAsync(H + L.o_entdef, c.entry_def + v0, L.nv, hipMemcpyDeviceToHost, s));
+    }
+    if (c.phys == PT_BYTE_ARRAY) {
+      HIPOK(hipMemcpyAsync(H + L.o_offs, D + d_offs[li], 4 * (L.nv + 1), hipMemcpyDeviceToHost, s));
+      if (L.nchars) HIPOK(hipMemcpyAsync(H + L.o_chars, c.chars + rg[li].c0, L.nchars, hipMemcpyDeviceToHost, s));
+    } else if (L.nv) {
+      HIPOK(hipMemcpyAsync(H + L.o_fixed, c.fixed + v0 * c.width, (size_t)L.nv * c.width, hipMemcpyDeviceToHost, s));
+    }
+  }
+  // row index: the file row of each selected row (row groups pruned by the predicate are skipped,
+  // as parquet-mr's getCurrentRowIndex counts them)
+  if (r->row_index) {
+    int64_t* ri = (int64_t*)(H + w->o_rowidx);
+    const auto& m = r->rgmap[fi];
+    size_t k = 0;
+    for (int64_t i = 0; i < nr; i++) {
+      const int64_t row = r0 + i;
+      while (k + 1 < m.size() && m[k + 1].first <= row) k++;
+      ri[i] = m.empty() ? row : m[k].second + (row - m[k].first);
+    }
+  }
+  int32_t ovf = 0;
+  HIPOK(hipMemcpyAsync(&ovf, r->d_ovf.p, 4, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  if (ovf) return fail("Error reading Parquet file: " + p->files[fi].path + " (int32 offset overflow)");
+  return 0;
+}
+
+extern "C" int dk_reader_next(dk_reader* r, dk_batch** out) {
+  *out = nullptr;
+  if (!r) return fail("null reader");
+  hipSetDevice(r->eng->cfg.device);
+  dk_parquet* p = r->p;
+  for (;;) {
+    if (r->file >= (int)p->files.size()) return 0;
+    const int64_t n = p->files[r->file].num_rows;
+    if (r->next >= n) { r->file++; r->next = 0; continue; }
+    if (!r->cur || r->cur->file != r->file || r->next >= r->cur->r0 + r->cur->nr) {
+      RWin* w = nullptr;
+      {
+        std::lock_guard<std::mutex> g(r->mu);
+        if (r->cur) { if (--r->cur->refs == 0) r->pool.push_back(r->cur); r->cur = nullptr; }
+        if (!r->pool.empty()) { w = r->pool.back(); r->pool.pop_back(); }
+      }
+      if (!w) w = new RWin();
+      if (load_window(r, w, r->next, std::min<int64_t>(r->W, n - r->next))) {
+        std::lock_guard<std::mutex> g(r->mu);
+        r->pool.push_back(w);
+        return 1;
+      }
+      w->refs = 1;
+      r->cur = w;
+    }
+    break;
+  }
+  RWin* w = r->cur;
+  const int64_t b0 = r->next, b1 = std::min<int64_t>(b0 + r->B, w->r0 + w->nr);
+  const int64_t rb = b0 - w->r0, nb = b1 - b0;
+  auto* b = new dk_batch_impl();
+  b->rd = r; b->win = w;
+  b->cols.resize(r->leaves.size());
+  uint8_t* H = w->buf.p;
+  for (size_t li = 0; li < r->leaves.size(); li++) {
+    const WinLeaf& L = w->leaf[li];
+    dk_batch_column& c = b->cols[li];
+    memset(&c, 0, sizeof c);
+    c.row_def = H + L.o_rowdef + rb;
+    if (!L.present) { c.present = 0; c.n_values = nb; continue; }
+    const DColumn& d = p->h_cols[p->colmap[w->file][li]];
+    c.present = 1; c.phys = d.phys; c.width = d.width; c.max_def = d.max_def; c.max_rep = d.max_rep; c.rep_def = d.rep_def;
+    c.validity = H + L.o_bits;
+    if (d.max_rep > 0) {
+      c.row_offs = (const int32_t*)(H + L.o_rowoffs) + rb;
+      c.entry_def = H + L.o_entdef;
+      c.value_offset = c.row_offs[0];
+      c.n_values = c.row_offs[nb] - c.row_offs[0];
+    } else {
+      c.value_offset = rb;
+      c.n_values = nb;
+    }
+    if (d.phys == PT_BYTE_ARRAY) { c.offs = (const int32_t*)(H + L.o_offs); c.chars = H + L.o_chars; }
+    else c.fixed = H + L.o_fixed;
+  }
+  b->pub.file = w->file;
+  b->pub.n_rows = nb;
+  b->pub.n_cols = (int32_t)b->cols.size();
+  b->pub.cols = b->cols.data();
+  b->pub.row_index = r->row_index ? (const int64_t*)(H + w->o_rowidx) + rb : nullptr;
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    w->refs++;
+    r->outstanding++;
+  }
+  r->next = b1;
+  *out = &b->pub;
+  return 0;
+}
+
+extern "C" void dk_batch_release(dk_batch* pub) {
+  if (!pub) return;
+  dk_batch_impl* b = reinterpret_cast<dk_batch_impl*>(pub);   // pub is the first member
+  dk_reader* r = b->rd;
+  std::unique_lock<std::mutex> lk(r->mu);
+  if (--b->win->refs == 0) r->pool.push_back(b->win);
+  r->outstanding--;
+  delete b;
+  reader_maybe_free(r, lk);
+}
+
+extern "C" void dk_reader_close(dk_reader* r) {
+  if (!r) return;
+  hipSetDevice(r->eng->cfg.device);
+  std::unique_lock<std::mutex> lk(r->mu);
+  if (r->closed) return;
+  r->closed = true;
+  if (r->cur) { if (--r->cur->refs == 0) r->pool.push_back(r->cur); r->cur = nullptr; }
+  reader_maybe_free(r, lk);
+}
+
+extern "C" int64_t dk_reader_num_rows(dk_reader* r, int32_t file) {
+  return r ? dk_parquet_num_rows(r->p, file) : -1;
 }

@@ -23,7 +23,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import Column, DkError, check, dk_column, dk_config, dk_part_program, dk_rg_filter, dk_skip_program, lib
+from ._lib import (MAX_LEAF_DEPTH, Column, DkError, check, dk_batch, dk_column, dk_config, dk_part_program,
+                   dk_read_options, dk_rg_filter, dk_skip_program, lib)
 
 ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
               "add.size", "add.modificationTime", "add.dataChange",
@@ -81,6 +82,14 @@ class GpuEngine:
     # ParquetHandler.readParquetFiles (engine/ParquetHandler.java:64-68)
     def read_parquet_files(self, paths, leaves):
         return ParquetSet(self, paths, leaves)
+
+    def readParquetFiles(self, paths, leaves, predicate=None, field_ids=None, window_rows=0):
+        """ParquetHandler.readParquetFiles as a Kernel caller consumes it: an iterator of ColumnarBatch
+        (<= parquet_batch_size rows, file by file, never spanning files), closable before exhaustion.
+        leaves: projected leaf paths; ROW_INDEX_COLUMN among them requests the row-index metadata
+        column. predicate: optional dk_rg_filter (row-group pruning, best effort). field_ids: optional
+        {leaf: [id or -1 per dotted component]} (parquet.field.id of the Kernel fields)."""
+        return ParquetReader(self, paths, leaves, predicate, field_ids, window_rows)
 
 
 def prune_row_groups(path, packed_filter):
@@ -193,6 +202,124 @@ class ParquetSet:
         if self._h:
             lib().dk_parquet_close(self._h)
             self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+ROW_INDEX_COLUMN = "_metadata.row_index"     # StructField.METADATA_ROW_INDEX_COLUMN_NAME
+
+
+def _np_view(ptr, n, dtype):
+    if not ptr or n <= 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,))
+
+
+class BatchColumn:
+    """One leaf of a ColumnarBatch, copied out of the batch's pinned buffers. Offsets are rebased to the
+    batch (row_offs / offs start at 0), so the layout equals a dk_column slice of the same rows."""
+
+    def __init__(self, c, n_rows, path):
+        self.path = path
+        self.present = bool(c.present)
+        self.n_rows = n_rows
+        self.phys, self.width, self.max_def, self.max_rep, self.rep_def = c.phys, c.width, c.max_def, c.max_rep, c.rep_def
+        self.row_def = _np_view(c.row_def, n_rows, np.uint8).copy()
+        self.row_offs = self.entry_def = self.fixed = self.offs = self.chars = self.validity = None
+        if not self.present:
+            return
+        v0, nv = c.value_offset, c.n_values
+        if c.max_rep > 0:
+            ro = _np_view(c.row_offs, n_rows + 1, np.int32).astype(np.int64)
+            self.row_offs = ro - ro[0]
+            self.entry_def = _np_view(c.entry_def, v0 + nv, np.uint8)[v0:].copy()
+        bits = _np_view(c.validity, (v0 + nv + 7) // 8, np.uint8)
+        self.validity = np.unpackbits(bits, bitorder="little")[v0:v0 + nv].astype(bool)
+        if c.phys == 6:
+            o = _np_view(c.offs, v0 + nv + 1, np.int32)[v0:].astype(np.int64)
+            self.chars = _np_view(c.chars, int(o[-1]) if nv >= 0 else 0, np.uint8)[o[0]:o[-1]].copy() \
+                if o[-1] > o[0] else np.zeros(0, np.uint8)
+            self.offs = o - o[0]
+        else:
+            self.fixed = _np_view(c.fixed, (v0 + nv) * c.width, np.uint8)[v0 * c.width:].copy()
+
+    def string(self, i):
+        return bytes(self.chars[self.offs[i]:self.offs[i + 1]])
+
+
+class ColumnarBatch:
+    """A batch from ParquetReader: columns by leaf path (requested order), plus the row index."""
+
+    def __init__(self, b: dk_batch, leaves, want_row_index):
+        self.file = b.file
+        self.n_rows = b.n_rows
+        self.columns = {leaf: BatchColumn(b.cols[i], b.n_rows, leaf) for i, leaf in enumerate(leaves)}
+        self.row_index = _np_view(b.row_index, b.n_rows, np.int64).copy() if want_row_index else None
+
+
+class ParquetReader:
+    """Iterator over dk_reader batches; close() early is safe (ScanImpl.java:376-392)."""
+
+    def __init__(self, engine, paths, leaves, predicate=None, field_ids=None, window_rows=0):
+        self.paths = list(paths)
+        self.want_row_index = ROW_INDEX_COLUMN in leaves
+        self.leaves = [x for x in leaves if x != ROW_INDEX_COLUMN]
+        opt = dk_read_options()
+        self._ids = None
+        if field_ids:
+            ids = np.full(len(self.leaves) * MAX_LEAF_DEPTH, -1, np.int32)
+            for i, leaf in enumerate(self.leaves):
+                for d, v in enumerate((field_ids.get(leaf) or [])[:MAX_LEAF_DEPTH]):
+                    ids[i * MAX_LEAF_DEPTH + d] = -1 if v is None else v
+            self._ids = ids
+            opt.field_ids = ids.ctypes.data
+        self._pred = predicate
+        opt.predicate = C.cast(C.byref(predicate), C.c_void_p) if predicate is not None else None
+        opt.row_index = 1 if self.want_row_index else 0
+        opt.window_rows = window_rows
+        self._h = C.c_void_p()
+        check(lib().dk_reader_open(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
+                                   len(self.leaves), C.byref(opt), C.byref(self._h)))
+
+    def num_rows(self, file_idx):
+        return lib().dk_reader_num_rows(self._h, file_idx)
+
+    def next_raw(self):
+        """The next dk_batch pointer (caller releases it with release()), or None at the end."""
+        out = C.POINTER(dk_batch)()
+        check(lib().dk_reader_next(self._h, C.byref(out)))
+        return out if out else None
+
+    @staticmethod
+    def release(raw):
+        lib().dk_batch_release(raw)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        raw = self.next_raw()
+        if raw is None:
+            raise StopIteration
+        try:
+            return ColumnarBatch(raw.contents, self.leaves, self.want_row_index)
+        finally:
+            lib().dk_batch_release(raw)
+
+    def close(self):
+        if self._h:
+            lib().dk_reader_close(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
     def __del__(self):
         try:

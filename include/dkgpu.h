@@ -16,6 +16,10 @@
  *   dk_json_tail_*       JsonHandler.readJsonFiles over the commit tail
  *                        (kernel-api/.../engine/JsonHandler.java:87-91;
  *                         kernel-defaults/.../engine/DefaultJsonHandler.java:79-157)
+ *   dk_reader_*, dk_batch_*  the streaming form of ParquetHandler.readParquetFiles: a
+ *                        CloseableIterator<ColumnarBatch> of <= parquet.reader.batch-size rows
+ *                        (engine/ParquetHandler.java:59-68; defaults/internal/parquet/
+ *                         ParquetFileReader.java:54-147, ParquetSchemaUtils.java:92-138)
  *   dk_replay_*          the active-AddFile log replay behind Scan.getScanFiles
  *                        (kernel-api/.../Scan.java:101; internal/replay/LogReplay.java:194-206,
  *                         internal/replay/ActiveAddFilesIterator.java:146-275) and its
@@ -33,6 +37,7 @@ typedef struct dk_engine dk_engine;
 typedef struct dk_parquet dk_parquet;
 typedef struct dk_json_tail dk_json_tail;
 typedef struct dk_replay dk_replay;
+typedef struct dk_reader dk_reader;
 
 typedef struct dk_config {
   int32_t parquet_batch_size;  /* delta.kernel.default.parquet.reader.batch-size (default 1024) */
@@ -130,6 +135,62 @@ int  dk_parquet_traffic(dk_parquet* p, int64_t* bytes_read, int64_t* bytes_writt
 /* algorithmic bytes one launch of a decode kernel must move ("k_string_copy", "k_tile_decode") */
 int  dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int64_t* bytes_read, int64_t* bytes_written);
 void dk_parquet_close(dk_parquet* p);
+
+/* ---- Streaming ParquetHandler.readParquetFiles (ParquetHandler.java:64-68) ----
+ * The files are decoded on the GPU when the reader opens (on the reader's own HIP stream: one engine
+ * may serve several threads, each reader is single-threaded like a Kernel iterator). dk_reader_next
+ * then yields batches of at most dk_config.parquet_batch_size rows, file by file in input order and
+ * rows in file order, never spanning two files (ParquetFileReader.java:54-147); *out = NULL once
+ * exhausted. A batch stays valid until dk_batch_release, also after dk_reader_close, and closing a
+ * reader before it is exhausted is safe (ScanImpl.java:376-392).
+ *
+ * Batch layout (pinned host memory, Arrow-like). Row-indexed arrays -- row_def, row_offs, row_index --
+ * start at the batch's first row. Value-indexed arrays -- validity, entry_def, fixed, offs -- are
+ * shared by the batches of one transfer window: value i of the batch is at index value_offset + i,
+ * and a repeated leaf's row r holds values [row_offs[r], row_offs[r + 1]) (absolute indices, as the
+ * Arrow C data interface's offset). Byte array value v = chars[offs[v], offs[v + 1]). */
+#define DK_MAX_LEAF_DEPTH 8
+typedef struct dk_read_options {
+  /* parquet.field.id of each dotted component of each leaf (n_leaves x DK_MAX_LEAF_DEPTH, -1 = none),
+   * or NULL: a component resolves by field id, then exact name, then case-insensitive name
+   * (ParquetSchemaUtils.findSubFieldType, :92-119); duplicate ids in a struct group fail (:122-138) */
+  const int32_t* field_ids;
+  /* optional row-group predicate (best effort, as parquet-mr's StatisticsFilter, ParquetFileReader.java:
+   * 111-132): row groups it proves empty are not read; NULL = read everything */
+  const dk_rg_filter* predicate;
+  int32_t row_index;             /* 1: batches carry the file row index of every row (the
+                                    _metadata.row_index metadata column, ParquetFileReader.java:57-59,96) */
+  int32_t window_rows;           /* rows per host transfer window (0: about 1M, rounded to batches) */
+} dk_read_options;
+
+typedef struct dk_batch_column {
+  int32_t present;               /* 0: the file lacks the leaf -> every value null (NonExistentColumnReader) */
+  int32_t phys, width, max_def, max_rep, rep_def;
+  int64_t n_values;              /* values of the batch: rows, or entries of a repeated leaf */
+  int64_t value_offset;          /* index of the batch's first value in the value-indexed arrays */
+  const uint8_t* row_def;        /* definition level per row (null ancestors: def below their level) */
+  const int32_t* row_offs;       /* repeated leaf: n_rows + 1 entry offsets (absolute value indices) */
+  const uint8_t* validity;       /* bit v (LSB first) = value v is non-null (def == max_def) */
+  const uint8_t* entry_def;      /* repeated leaf: definition level per entry */
+  const uint8_t* fixed;          /* fixed-width values, value v at fixed + v * width (0 where null) */
+  const int32_t* offs;           /* byte arrays: value offsets into chars */
+  const uint8_t* chars;
+} dk_batch_column;
+
+typedef struct dk_batch {
+  int32_t file;                  /* index of the input file the rows come from */
+  int32_t n_cols;                /* == n_leaves, in the requested order */
+  int64_t n_rows;
+  const dk_batch_column* cols;
+  const int64_t* row_index;      /* per row, when dk_read_options.row_index; else NULL */
+} dk_batch;
+
+int  dk_reader_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                    int32_t n_leaves, const dk_read_options* opt, dk_reader** out);
+int  dk_reader_next(dk_reader* r, dk_batch** out);
+int64_t dk_reader_num_rows(dk_reader* r, int32_t file);   /* rows the reader yields for a file */
+void dk_batch_release(dk_batch* b);
+void dk_reader_close(dk_reader* r);
 
 /* ---- Commit tail (host JSON parse, newest commit first, batches of json_batch_size lines) ----
  * One row per JSON line, in replay order, with the add/remove read schema. Columns are addressed
