@@ -63,6 +63,11 @@ class dk_batch(C.Structure):
                 ("cols", C.POINTER(dk_batch_column)), ("row_index", C.c_void_p)]
 
 
+class dk_dv_descriptor(C.Structure):
+    _fields_ = [("storage_type", C.c_char_p), ("path_or_inline", C.c_char_p), ("has_offset", C.c_int32),
+                ("offset", C.c_int32), ("size_in_bytes", C.c_int32), ("cardinality", C.c_int64)]
+
+
 MAX_LEAF_DEPTH = 8
 
 EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
@@ -75,7 +80,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_kernel_stats", "dk_replay_free", "dk_parquet_open_rg", "dk_parquet_row_groups",
            "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits", "dk_parquet_open_sel",
            "dk_parquet_prune_row_groups", "dk_parquet_nonnull_row_groups",
-           "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close"]
+           "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close",
+           "dk_dv_load", "dk_dv_num_bits", "dk_dv_bitmap", "dk_dv_selection", "dk_dv_free"]
 
 
 def lib(build_if_missing=True):
@@ -131,6 +137,11 @@ def lib(build_if_missing=True):
         "dk_reader_num_rows": (I64, [P, I32]),
         "dk_batch_release": (None, [C.POINTER(dk_batch)]),
         "dk_reader_close": (None, [P]),
+        "dk_dv_load": (C.c_int, [P, C.c_char_p, C.POINTER(dk_dv_descriptor), I32, C.POINTER(P)]),
+        "dk_dv_num_bits": (I64, [P, I32]),
+        "dk_dv_bitmap": (C.c_int, [P, I32, P, I64, I32]),
+        "dk_dv_selection": (C.c_int, [P, I32, P, I64, P]),
+        "dk_dv_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -138,6 +138,16 @@ struct ArrowWin {
   int32_t* overflow;           // out: set when a rebased offset does not fit int32
 };
 
+// deletion vectors: one roaring container of one DV (dk_dv.hip)
+enum : int32_t { DV_ARRAY = 0, DV_BITMAP = 1, DV_RUN = 2 };
+struct DvCont {
+  int64_t src;        // byte offset of the container payload in the uploaded blob
+  int64_t out_word;   // first u64 word of the DV's bitmap
+  int64_t word0;      // first word of the container's 64K-value range, relative to out_word
+  int64_t nwords;     // words of the DV's bitmap (bound for bitmap containers)
+  int32_t type, n;    // DV_*; values (array) or runs (run)
+};
+
 constexpr uint32_t kDecodeSeed = 0;   // seed of the path hashes computed during decode
 constexpr int DK_COPY_TILE = 128;     // values per k_string_copy workgroup (host tile table step)
 

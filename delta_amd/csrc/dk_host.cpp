@@ -28,6 +28,8 @@ void launch_snappy(const SnapCtx&, int, int, const int2*, int, hipStream_t);
 void snap_stats(unsigned long long*);
 void launch_pack_bits(const uint8_t*, long long, uint8_t*, hipStream_t);
 void launch_arrow_window(const ArrowWin&, hipStream_t);
+void launch_dv_expand(const DvCont*, int, const uint8_t*, unsigned long long*, hipStream_t);
+void launch_dv_select(const unsigned long long*, long long, const long long*, long long, uint8_t*, hipStream_t);
 void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
@@ -3000,4 +3002,287 @@ extern "C" void dk_reader_close(dk_reader* r) {
 
 extern "C" int64_t dk_reader_num_rows(dk_reader* r, int32_t file) {
   return r ? dk_parquet_num_rows(r->p, file) : -1;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Deletion vectors (dk_dv_*): DeletionVectorUtils.loadNewDvAndBitmap for every DV of a scan
+// (internal/deletionvectors/DeletionVectorUtils.java:27-37, DeletionVectorStoredBitmap.java:50-129,
+// RoaringBitmapArray.java:100-229, Base85Codec.java, DeletionVectorDescriptor.java:176-231).
+// Host: descriptor -> bytes (Z85 inline payload or the file range), size and CRC-32 checks, the
+// RoaringBitmapArray / portable-roaring headers; device: container expansion (dk_dv.hip).
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+// Base85Codec.decodeBlocks (Z85 alphabet); false when the text is not 5-aligned or not valid Z85
+bool z85_decode(const std::string& in, std::vector<uint8_t>& out) {
+  static const char* enc = "0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ.-:+=^!/*?&<>()[]{}@%$#";
+  int8_t dec[128];
+  memset(dec, -1, sizeof dec);
+  for (int i = 0; i < 85; i++) dec[(uint8_t)enc[i]] = (int8_t)i;
+  if (in.size() % 5) return false;
+  out.clear();
+  for (size_t i = 0; i < in.size(); i += 5) {
+    uint64_t sum = 0;
+    for (int k = 0; k < 5; k++) {
+      const uint8_t c = (uint8_t)in[i + k];
+      if (c >= 128 || dec[c] < 0) return false;
+      sum = sum * 85 + (uint64_t)dec[c];
+    }
+    const uint32_t v = (uint32_t)sum;                   // (int) sum: the low 32 bits, big-endian
+    out.push_back(v >> 24); out.push_back(v >> 16); out.push_back(v >> 8); out.push_back(v);
+  }
+  return true;
+}
+
+uint32_t crc32_ieee(const uint8_t* p, size_t n) {       // java.util.zip.CRC32
+  static uint32_t tab[256];
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = c & 1 ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      tab[i] = c;
+    }
+  });
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; i++) c = tab[(c ^ p[i]) & 0xff] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+// Hadoop Path.toString of a local path: "file:/x/y" -> "/x/y" for reading
+std::string local_path(const std::string& p) {
+  if (p.compare(0, 7, "file://") == 0 && p.size() > 7 && p[7] == '/') return p.substr(7);
+  if (p.compare(0, 5, "file:") == 0) return p.substr(5);
+  return p;
+}
+
+std::string join_path(const std::string& a, const std::string& b) {
+  if (a.empty()) return b;
+  return a.back() == '/' ? a + b : a + "/" + b;
+}
+
+// LE reader over one serialized RoaringBitmapArray (BufferUnderflowException past the end)
+struct LeBuf {
+  const uint8_t* p; size_t n, at = 0; bool bad = false;
+  bool need(size_t k) { if (bad || at + k > n) { bad = true; return false; } return true; }
+  uint32_t u16() { if (!need(2)) return 0; uint32_t v = p[at] | (p[at + 1] << 8); at += 2; return v; }
+  uint32_t u32() { if (!need(4)) return 0; uint32_t v; memcpy(&v, p + at, 4); at += 4; return v; }
+  uint64_t u64() { if (!need(8)) return 0; uint64_t v; memcpy(&v, p + at, 8); at += 8; return v; }
+};
+
+// org.roaringbitmap 0.9.25 RoaringArray.deserialize (portable format) of one 32-bit bitmap at b.at:
+// appends its containers (values high << 32 | key << 16 | low) and returns its serialized size
+bool roaring32(LeBuf& b, size_t base_off, uint64_t high, std::vector<DvCont>& out, uint64_t* maxv, std::string* err) {
+  const size_t start = b.at;
+  const uint32_t cookie = b.u32();
+  const bool hasrun = (cookie & 0xFFFF) == 12347;
+  if (!hasrun && cookie != 12346) { *err = "org.roaringbitmap.InvalidRoaringFormat: I failed to find one of the right cookies."; return false; }
+  const uint32_t size = hasrun ? (cookie >> 16) + 1 : b.u32();
+  if (size > (1u << 16)) { *err = "org.roaringbitmap.InvalidRoaringFormat: Size too large"; return false; }
+  std::vector<uint8_t> runbits;
+  if (hasrun) { const size_t nb = (size + 7) / 8; if (!b.need(nb)) return false; runbits.assign(b.p + b.at, b.p + b.at + nb); b.at += nb; }
+  std::vector<uint32_t> key(size), card(size);
+  for (uint32_t k = 0; k < size; k++) { key[k] = b.u16(); card[k] = b.u16() + 1; }
+  if (!hasrun || size >= 4) { if (!b.need(4ull * size)) return false; b.at += 4ull * size; }   // offset header
+  for (uint32_t k = 0; k < size; k++) {
+    const bool run = hasrun && (runbits[k / 8] >> (k % 8) & 1);
+    DvCont c{};
+    c.word0 = (int64_t)((high << 32 | (uint64_t)key[k] << 16) >> 6);
+    if (run) {
+      c.type = DV_RUN;
+      c.src = (int64_t)(base_off + b.at);
+      const uint32_t nr = b.u16();
+      c.n = (int32_t)nr;
+      if (!b.need(4ull * nr)) return false;
+      uint32_t last = 0;
+      for (uint32_t r = 0; r < nr; r++) {
+        const uint32_t st = b.p[b.at + 4 * r] | (b.p[b.at + 4 * r + 1] << 8);
+        const uint32_t ln = b.p[b.at + 4 * r + 2] | (b.p[b.at + 4 * r + 3] << 8);
+        if (st + ln > 0xFFFF) { *err = "org.roaringbitmap.InvalidRoaringFormat: run past the container"; return false; }
+        last = std::max(last, st + ln);
+      }
+      b.at += 4ull * nr;
+      if (nr) *maxv = std::max<uint64_t>(*maxv, high << 32 | (uint64_t)key[k] << 16 | last);
+    } else if (card[k] > 4096) {
+      c.type = DV_BITMAP;
+      c.src = (int64_t)(base_off + b.at);
+      if (!b.need(8192)) return false;
+      for (int w = 1023; w >= 0; w--) {
+        uint64_t v; memcpy(&v, b.p + b.at + 8 * w, 8);
+        if (v) { *maxv = std::max<uint64_t>(*maxv, high << 32 | (uint64_t)key[k] << 16 | (uint64_t)(64 * w + 63 - __builtin_clzll(v))); break; }
+      }
+      b.at += 8192;
+    } else {
+      c.type = DV_ARRAY;
+      c.src = (int64_t)(base_off + b.at);
+      c.n = (int32_t)card[k];
+      if (!b.need(2ull * card[k])) return false;
+      const uint32_t lastv = b.p[b.at + 2 * (card[k] - 1)] | (b.p[b.at + 2 * (card[k] - 1) + 1] << 8);
+      *maxv = std::max<uint64_t>(*maxv, high << 32 | (uint64_t)key[k] << 16 | lastv);
+      b.at += 2ull * card[k];
+    }
+    out.push_back(c);
+  }
+  (void)start;
+  return true;
+}
+
+}  // namespace
+
+struct dk_dv_set {
+  StreamH own;
+  dk_engine* eng = nullptr;
+  DBuf d_bits;
+  std::vector<int64_t> word0, nbits;    // per DV: first word, bits (max deleted row + 1; 0 = empty)
+};
+
+extern "C" int dk_dv_load(dk_engine* e, const char* table_root, const dk_dv_descriptor* dvs, int32_t n,
+                          dk_dv_set** out) {
+  *out = nullptr;
+  if (!e) return fail("null engine");
+  hipSetDevice(e->cfg.device);
+  std::unique_ptr<dk_dv_set> S(new dk_dv_set());
+  S->eng = e;
+  if (S->own.create()) return 1;
+  const std::string root = table_root ? table_root : "";
+  std::vector<uint8_t> blob;
+  std::vector<DvCont> conts;
+  std::vector<std::vector<DvCont>> per(n);
+  S->nbits.assign(n, 0);
+  S->word0.assign(n, 0);
+  for (int32_t i = 0; i < n; i++) {
+    const dk_dv_descriptor& d = dvs[i];
+    const std::string st = d.storage_type ? d.storage_type : "", pd = d.path_or_inline ? d.path_or_inline : "";
+    if (d.cardinality == 0) continue;                          // isEmpty: no read
+    // isInline() compares the storage type by reference (`storageType == INLINE_DV_MARKER`,
+    // DeletionVectorDescriptor.java:176-178): a descriptor read from the log never is, so every DV
+    // takes the on-disk branch, and an "i" DV fails in getAbsolutePath (:190-216)
+    std::string path;
+    if (st == "u") {
+      if (pd.size() < 20) return fail("java.lang.StringIndexOutOfBoundsException: deletion vector path " + pd);
+      std::vector<uint8_t> u;
+      if (!z85_decode(pd.substr(pd.size() - 20), u) || u.size() < 16)
+        return fail("java.lang.IllegalArgumentException: Input is not valid Z85: " + pd.substr(pd.size() - 20));
+      char id[40];
+      snprintf(id, sizeof id, "%02x%02x%02x%02x-%02x%02x-%02x%02x-%02x%02x-%02x%02x%02x%02x%02x%02x", u[0], u[1], u[2],
+               u[3], u[4], u[5], u[6], u[7], u[8], u[9], u[10], u[11], u[12], u[13], u[14], u[15]);
+      const std::string prefix = pd.substr(0, pd.size() - 20);
+      path = join_path(prefix.empty() ? root : join_path(root, prefix), std::string("deletion_vector_") + id + ".bin");
+    } else if (st == "p") {
+      if (pd.find(':') == std::string::npos) return fail("java.lang.IllegalArgumentException: Relative URIs are not supported for DVs");
+      path = pd;
+    } else {
+      return fail("A uri " + pd + " which cannot be turned into a relative path as found in the transaction log");
+    }
+    // FileReadRequest(offset, sizeInBytes + 8): 4-byte big-endian size, the bitmap, 4-byte CRC-32
+    const std::string lp = local_path(path);
+    FILE* fp = fopen(lp.c_str(), "rb");
+    if (!fp) return fail("Couldn't load dv: java.io.FileNotFoundException: " + path);
+    const int64_t off = d.has_offset ? d.offset : 0;
+    std::vector<uint8_t> raw((size_t)std::max(0, d.size_in_bytes) + 8);
+    const bool ok = fseek(fp, off, SEEK_SET) == 0 && fread(raw.data(), 1, raw.size(), fp) == raw.size();
+    fclose(fp);
+    if (!ok) return fail("Couldn't load dv: java.io.EOFException: " + path);
+    const uint32_t size_file = (uint32_t)raw[0] << 24 | raw[1] << 16 | raw[2] << 8 | raw[3];
+    if ((int32_t)size_file != d.size_in_bytes) return fail("DV size mismatch");
+    const uint8_t* body = raw.data() + 4;
+    const size_t nb = (size_t)d.size_in_bytes;
+    const uint32_t want = (uint32_t)body[nb] << 24 | body[nb + 1] << 16 | body[nb + 2] << 8 | body[nb + 3];
+    if (crc32_ieee(body, nb) != want) return fail("DV checksum mismatch");
+    // RoaringBitmapArray.readFrom: magic, then the native or portable array of 32-bit bitmaps
+    const size_t base = blob.size();
+    blob.insert(blob.end(), body, body + nb);
+    LeBuf b{blob.data() + base, nb};
+    std::string err;
+    uint64_t maxv = 0;
+    bool any = false;
+    const uint32_t magic = b.u32();
+    if (magic == 1681511377u) {                                 // portable
+      const uint64_t nbm = b.u64();
+      if ((int64_t)nbm < 0) return fail("Couldn't load dv: java.io.IOException: Invalid RoaringBitmapArray length (" + std::to_string((int64_t)nbm) + " < 0)");
+      if (nbm > 0x7fffffffull) return fail("Couldn't load dv: java.io.IOException: Invalid RoaringBitmapArray length (" + std::to_string(nbm) + " > 2147483647)");
+      for (uint64_t k = 0; k < nbm && !b.bad; k++) {
+        const int32_t key = (int32_t)b.u32();
+        if (key < 0) return fail("Couldn't load dv: java.io.IOException: Invalid unsigned entry in RoaringBitmapArray (" + std::to_string(key) + ")");
+        const size_t before = per[i].size();
+        if (!roaring32(b, base, (uint64_t)key, per[i], &maxv, &err)) break;
+        any = any || per[i].size() > before;
+      }
+    } else if (magic == 1681511376u) {                          // native
+      const int32_t nbm = (int32_t)b.u32();
+      if (nbm < 0) return fail("Couldn't load dv: java.io.IOException: Invalid RoaringBitmapArray length (" + std::to_string(nbm) + " < 0)");
+      for (int32_t k = 0; k < nbm && !b.bad; k++) {
+        const uint32_t bsize = b.u32();
+        const size_t at0 = b.at;
+        const size_t before = per[i].size();
+        if (!roaring32(b, base, (uint64_t)k, per[i], &maxv, &err)) break;
+        any = any || per[i].size() > before;
+        b.at = at0 + bsize;
+      }
+    } else {
+      return fail("Couldn't load dv: java.io.IOException: Unexpected RoaringBitmapArray magic number " + std::to_string((int32_t)magic));
+    }
+    if (!err.empty()) return fail("Couldn't load dv: " + err);
+    if (b.bad || b.at > nb) return fail("Couldn't load dv: java.nio.BufferUnderflowException");
+    if (any) {
+      if (maxv >= (1ull << 36)) return fail("deletion vector row index too large for a dense bitmap");
+      S->nbits[i] = (int64_t)maxv + 1;
+    }
+  }
+  // one zeroed word array for all DVs; containers carry their DV's word base
+  int64_t words = 0;
+  for (int32_t i = 0; i < n; i++) {
+    S->word0[i] = words;
+    const int64_t nw = (S->nbits[i] + 63) / 64;
+    for (DvCont c : per[i]) { c.out_word = words; c.nwords = nw; conts.push_back(c); }
+    words += nw;
+  }
+  const hipStream_t s = S->own.s;
+  if (S->d_bits.alloc((size_t)std::max<int64_t>(words, 1) * 8)) return 1;
+  HIPOK(hipMemsetAsync(S->d_bits.p, 0, (size_t)std::max<int64_t>(words, 1) * 8, s));
+  if (!conts.empty()) {
+    DBuf d_blob, d_conts;
+    if (upload(d_blob, blob.data(), blob.size(), s) || upload(d_conts, conts.data(), conts.size() * sizeof(DvCont), s)) return 1;
+    launch_dv_expand(d_conts.as<DvCont>(), (int)conts.size(), d_blob.as<uint8_t>(), S->d_bits.as<unsigned long long>(), s);
+    HIPOK(hipStreamSynchronize(s));
+  }
+  HIPOK(hipStreamSynchronize(s));
+  *out = S.release();
+  return 0;
+}
+
+extern "C" int64_t dk_dv_num_bits(dk_dv_set* S, int32_t i) {
+  return S && i >= 0 && i < (int32_t)S->nbits.size() ? S->nbits[i] : -1;
+}
+
+extern "C" int dk_dv_bitmap(dk_dv_set* S, int32_t i, void* dst, int64_t nbytes, int32_t dst_on_device) {
+  if (!S || i < 0 || i >= (int32_t)S->nbits.size()) return fail("bad deletion vector index");
+  hipSetDevice(S->eng->cfg.device);
+  const int64_t need = (S->nbits[i] + 7) / 8;
+  if (nbytes < need) return fail("dk_dv_bitmap: destination too small");
+  if (need) HIPOK(hipMemcpyAsync(dst, S->d_bits.as<uint8_t>() + S->word0[i] * 8, need,
+                                 dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, S->own.s));
+  HIPOK(hipStreamSynchronize(S->own.s));
+  return 0;
+}
+
+extern "C" int dk_dv_selection(dk_dv_set* S, int32_t i, const int64_t* row_index, int64_t n, uint8_t* sel) {
+  if (!S || i < 0 || i >= (int32_t)S->nbits.size()) return fail("bad deletion vector index");
+  hipSetDevice(S->eng->cfg.device);
+  for (int64_t k = 0; k < n; k++)       // RoaringBitmapArray.contains: checkArgument(value >= 0 && <= max)
+    if (row_index[k] < 0) return fail("java.lang.IllegalArgumentException: row index " + std::to_string(row_index[k]));
+  DBuf d_rows, d_sel;
+  const hipStream_t s = S->own.s;
+  if (upload(d_rows, row_index, (size_t)n * 8, s) || d_sel.alloc((size_t)n + 1)) return 1;
+  launch_dv_select(S->d_bits.as<unsigned long long>() + S->word0[i], S->nbits[i], d_rows.as<long long>(), n,
+                   d_sel.as<uint8_t>(), s);
+  if (n) HIPOK(hipMemcpyAsync(sel, d_sel.p, n, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" void dk_dv_free(dk_dv_set* S) {
+  if (!S) return;
+  hipSetDevice(S->eng->cfg.device);
+  delete S;
 }

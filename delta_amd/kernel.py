@@ -23,8 +23,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._lib import (MAX_LEAF_DEPTH, Column, DkError, check, dk_batch, dk_column, dk_config, dk_part_program,
-                   dk_read_options, dk_rg_filter, dk_skip_program, lib)
+from ._lib import (MAX_LEAF_DEPTH, Column, DkError, check, dk_batch, dk_column, dk_config, dk_dv_descriptor,
+                   dk_part_program, dk_read_options, dk_rg_filter, dk_skip_program, lib)
 
 ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
               "add.size", "add.modificationTime", "add.dataChange",
@@ -326,6 +326,94 @@ class ParquetReader:
             self.close()
         except Exception:
             pass
+
+
+class DeletionVectors:
+    """The DVs of a set of scan files, loaded into dense deleted-row bitmaps on the GPU
+    (DeletionVectorUtils.loadNewDvAndBitmap, DeletionVectorUtils.java:27-37). descriptors: tuples
+    (storageType, pathOrInlineDv, offset or None, sizeInBytes, cardinality)."""
+
+    def __init__(self, engine, table_root, descriptors):
+        self.n = len(descriptors)
+        arr = (dk_dv_descriptor * max(1, self.n))()
+        self._keep = []
+        for i, (st, pd, off, size, card) in enumerate(descriptors):
+            a, b = st.encode(), pd.encode()
+            self._keep += [a, b]
+            arr[i].storage_type, arr[i].path_or_inline = a, b
+            arr[i].has_offset = 0 if off is None else 1
+            arr[i].offset = off or 0
+            arr[i].size_in_bytes, arr[i].cardinality = size, card
+        self._h = C.c_void_p()
+        check(lib().dk_dv_load(engine._h, table_root.encode(), arr, self.n, C.byref(self._h)))
+
+    def num_bits(self, i):
+        return lib().dk_dv_num_bits(self._h, i)
+
+    def deleted(self, i):
+        """Bool per row index (up to the largest deleted row): True = deleted."""
+        nb = self.num_bits(i)
+        buf = np.zeros(max(1, (nb + 7) // 8), np.uint8)
+        check(lib().dk_dv_bitmap(self._h, i, buf.ctypes.data, buf.size, 0))
+        return np.unpackbits(buf, bitorder="little")[:nb].astype(bool)
+
+    def selection(self, i, row_index):
+        """SelectionColumnVector: True where the row survives DV i."""
+        ri = np.ascontiguousarray(row_index, dtype=np.int64)
+        sel = np.zeros(max(1, ri.size), np.uint8)
+        check(lib().dk_dv_selection(self._h, i, ri.ctypes.data, ri.size, sel.ctypes.data))
+        return sel[:ri.size].astype(bool)
+
+    def close(self):
+        if self._h:
+            lib().dk_dv_free(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _dv_of(data, r):
+    """(storageType, pathOrInlineDv, offset, sizeInBytes, cardinality) of scan-file row r, or None."""
+    st = data["add.deletionVector.storageType"]
+    if st is None or not st.present or st.row_def[r] < st.max_def:
+        return None
+    off = data["add.deletionVector.offset"]
+    has_off = off is not None and off.present and off.row_def[r] == off.max_def
+    size = data["add.deletionVector.sizeInBytes"].fixed.view("<i4")[r]
+    card = data["add.deletionVector.cardinality"].fixed.view("<i8")[r]
+    return (st.string(r).decode(), data["add.deletionVector.pathOrInlineDv"].string(r).decode(),
+            int(off.fixed.view("<i4")[r]) if has_off else None, int(size), int(card))
+
+
+def read_scan_data(engine, scan, leaves):
+    """Scan.transformPhysicalData over every selected scan file (Scan.java:147-230): each data file
+    is read with the row-index metadata column (readParquetFiles) and, when the scan file carries a
+    deletion vector, filtered by it (SelectionColumnVector). Yields (add.path, ColumnarBatch,
+    selection or None)."""
+    from urllib.parse import unquote
+    root = scan.table_root()
+    files = []
+    for b in scan.getScanFiles(engine):
+        for r in b.selected_rows():
+            files.append((b.data["add.path"].string(int(r)).decode(), _dv_of(b.data, int(r))))
+    with_dv = [dv for _, dv in files if dv is not None]
+    dvs = DeletionVectors(engine, root, with_dv) if with_dv else None
+    k = 0
+    for path, dv in files:
+        full = path if re.match(r"^[A-Za-z][A-Za-z0-9+.-]*:", path) else root.rstrip("/") + "/" + unquote(path)
+        local = full[5:] if full.startswith("file:") else full
+        with engine.readParquetFiles([local], list(leaves) + [ROW_INDEX_COLUMN]) as rd:
+            for batch in rd:
+                sel = dvs.selection(k, batch.row_index) if dv is not None else None
+                yield path, batch, sel
+        if dv is not None:
+            k += 1
+    if dvs is not None:
+        dvs.close()
 
 
 class JsonTail:

@@ -20,6 +20,10 @@
  *                        CloseableIterator<ColumnarBatch> of <= parquet.reader.batch-size rows
  *                        (engine/ParquetHandler.java:59-68; defaults/internal/parquet/
  *                         ParquetFileReader.java:54-147, ParquetSchemaUtils.java:92-138)
+ *   dk_dv_*              deletion-vector bitmaps for data reads: DeletionVectorUtils.loadNewDvAndBitmap
+ *                        and SelectionColumnVector (kernel-api/.../Scan.java:176-199;
+ *                         internal/deletionvectors/DeletionVectorStoredBitmap.java:50-129,
+ *                         RoaringBitmapArray.java:100-229)
  *   dk_replay_*          the active-AddFile log replay behind Scan.getScanFiles
  *                        (kernel-api/.../Scan.java:101; internal/replay/LogReplay.java:194-206,
  *                         internal/replay/ActiveAddFilesIterator.java:146-275) and its
@@ -38,6 +42,7 @@ typedef struct dk_parquet dk_parquet;
 typedef struct dk_json_tail dk_json_tail;
 typedef struct dk_replay dk_replay;
 typedef struct dk_reader dk_reader;
+typedef struct dk_dv_set dk_dv_set;
 
 typedef struct dk_config {
   int32_t parquet_batch_size;  /* delta.kernel.default.parquet.reader.batch-size (default 1024) */
@@ -191,6 +196,31 @@ int  dk_reader_next(dk_reader* r, dk_batch** out);
 int64_t dk_reader_num_rows(dk_reader* r, int32_t file);   /* rows the reader yields for a file */
 void dk_batch_release(dk_batch* b);
 void dk_reader_close(dk_reader* r);
+
+/* ---- Deletion vectors (Scan.transformPhysicalData's DV load, Scan.java:176-199) ----
+ * Each descriptor is a scan file's add.deletionVector. A DV with cardinality 0 is empty and not read;
+ * "u" DVs live at <table root>/<random prefix>/deletion_vector_<uuid>.bin, "p" DVs at their absolute
+ * URI. The stored bytes are checked as DeletionVectorStoredBitmap.loadFromStream does (4-byte size,
+ * CRC-32) and decoded as RoaringBitmapArray.readFrom (native or portable magic, portable roaring
+ * containers: org.roaringbitmap 0.9.25) into a dense deleted-row bitmap per DV on the GPU.
+ * Error messages follow the reference ("DV size mismatch", "DV checksum mismatch", "Couldn't load dv:
+ * ..."); an inline ("i") DV fails as it does in the reference, whose isInline() compares the storage
+ * type by reference (DeletionVectorDescriptor.java:176-178, :210-215). */
+typedef struct dk_dv_descriptor {
+  const char* storage_type;      /* "u", "p" or "i" */
+  const char* path_or_inline;
+  int32_t has_offset, offset;
+  int32_t size_in_bytes;
+  int64_t cardinality;
+} dk_dv_descriptor;
+/* table_root: the scan state's table root (a Hadoop path URI such as file:/data/t) */
+int  dk_dv_load(dk_engine* e, const char* table_root, const dk_dv_descriptor* dvs, int32_t n, dk_dv_set** out);
+int64_t dk_dv_num_bits(dk_dv_set* s, int32_t i);     /* largest deleted row + 1 (0: empty DV) */
+/* the packed bitmap (LSB first; bit r = row r deleted), ceil(num_bits / 8) bytes */
+int  dk_dv_bitmap(dk_dv_set* s, int32_t i, void* dst, int64_t nbytes, int32_t dst_on_device);
+/* SelectionColumnVector: sel[k] = 1 iff row_index[k] is not deleted by DV i */
+int  dk_dv_selection(dk_dv_set* s, int32_t i, const int64_t* row_index, int64_t n, uint8_t* sel);
+void dk_dv_free(dk_dv_set* s);
 
 /* ---- Commit tail (host JSON parse, newest commit first, batches of json_batch_size lines) ----
  * One row per JSON line, in replay order, with the add/remove read schema. Columns are addressed
