@@ -15,6 +15,7 @@
 #include <mutex>
 #include <thread>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "../../include/dkgpu.h"
@@ -2157,6 +2158,63 @@ extern "C" int dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column*
 }
 
 extern "C" void dk_json_tail_free(dk_json_tail* t) { delete t; }
+
+// Snapshot-load P&M scan over the commit files (LogReplay.loadTableProtocolAndMetadata,
+// internal/replay/LogReplay.java:220-314, reading PROTOCOL_METADATA_READ_SCHEMA through
+// DefaultJsonHandler): files newest first, read 16 at a time on host threads, stopping after the
+// block in which both actions have been seen. Per file: the first line whose top-level object has a
+// non-null "protocol" / "metaData" (its line index and byte range), or -1. Only lines that contain
+// one of the two key names (or a \u escape, the one other way to spell a key) are parsed.
+extern "C" int dk_log_pm_scan(const char* const* paths, int32_t n, int64_t* p_line, int64_t* p_off, int64_t* p_len,
+                              int64_t* m_line, int64_t* m_off, int64_t* m_len, int32_t* n_scanned) {
+  for (int32_t i = 0; i < n; i++) { p_line[i] = m_line[i] = -1; p_off[i] = p_len[i] = m_off[i] = m_len[i] = 0; }
+  *n_scanned = 0;
+  std::vector<std::string> errs(n > 0 ? n : 0);
+  auto scan = [&](int i) {
+    FILE* fp = fopen(paths[i], "rb");
+    if (!fp) { errs[i] = std::string("Error reading JSON file: ") + paths[i]; return; }
+    fseek(fp, 0, SEEK_END); long sz = ftell(fp); fseek(fp, 0, SEEK_SET);
+    std::vector<char> raw(sz > 0 ? sz : 0);
+    const size_t got = sz > 0 ? fread(raw.data(), 1, sz, fp) : 0;
+    fclose(fp);
+    if ((long)got != sz) { errs[i] = std::string("Error reading JSON file: ") + paths[i]; return; }
+    const char* b = raw.data();
+    const size_t N = raw.size();
+    std::vector<JNode> nodes;
+    size_t at = 0;
+    for (int64_t line = 0; at < N && (p_line[i] < 0 || m_line[i] < 0); line++) {
+      size_t j = at;
+      while (j < N && b[j] != '\n' && b[j] != '\r') j++;
+      const std::string_view v(b + at, j - at);
+      const size_t next = (j < N && b[j] == '\r' && j + 1 < N && b[j + 1] == '\n') ? j + 2 : j + 1;
+      if (v.find("\"protocol\"") != std::string_view::npos || v.find("\"metaData\"") != std::string_view::npos ||
+          v.find("\\u") != std::string_view::npos) {
+        const std::string text = java_utf8((const uint8_t*)v.data(), v.size());
+        nodes.clear();
+        JParser jp(text.data(), text.data() + text.size(), nodes);
+        const int root = jp.value(0);
+        if (root < 0) { errs[i] = std::string("Error reading JSON file: ") + paths[i] + " (" + jp.err + ")"; return; }
+        if (nodes[root].t == J_OBJ)
+          for (auto& kv : nodes[root].kv) {
+            if (nodes[kv.second].t == J_NULL) continue;
+            if (kv.first == "protocol" && p_line[i] < 0) { p_line[i] = line; p_off[i] = (int64_t)at; p_len[i] = (int64_t)v.size(); }
+            if (kv.first == "metaData" && m_line[i] < 0) { m_line[i] = line; m_off[i] = (int64_t)at; m_len[i] = (int64_t)v.size(); }
+          }
+      }
+      at = next;
+    }
+  };
+  for (int32_t b0 = 0; b0 < n; b0 += 16) {
+    const int32_t b1 = std::min<int32_t>(n, b0 + 16);
+    parallel_for(b1 - b0, [&](int k) { scan(b0 + k); });
+    for (int32_t i = b0; i < b1; i++) if (!errs[i].empty()) return fail(errs[i]);
+    *n_scanned = b1;
+    bool hp = false, hm = false;
+    for (int32_t i = 0; i < b1; i++) { hp = hp || p_line[i] >= 0; hm = hm || m_line[i] >= 0; }
+    if (hp && hm) break;
+  }
+  return 0;
+}
 
 // ------------------------------------------------------------------------------------------------
 // replay

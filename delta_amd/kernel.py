@@ -558,6 +558,54 @@ def table_root_uri(path: str) -> str:
 
 
 # ------------------------------------------------------------------------------------------------
+# Checksum (.crc) files (ChecksumReader / CRCInfo)
+# ------------------------------------------------------------------------------------------------
+_CRC = re.compile(r"^(\d+)\.crc$")
+
+
+def _read_checksum_file(path):
+    """ChecksumReader.readChecksumFile (replay/ChecksumReader.java:98-127): exactly one JSON row
+    with non-null protocol and metadata (CRCInfo.FULL_SCHEMA: "protocol", "metadata"), decoded with
+    the P&M rules; anything else -- missing, empty, several rows, undecodable -- is no CRC."""
+    from . import actions as A
+    try:
+        with open(path, "rb") as f:
+            lines = f.read().decode("utf-8", "replace").splitlines()
+        if len(lines) != 1:
+            return None
+        obj = json.loads(lines[0])
+        p, m = obj.get("protocol"), obj.get("metadata")
+        if p is None or m is None:
+            return None
+        return (int(os.path.basename(path).split(".")[0]), A.protocol_from_json(p), A.metadata_from_json(m))
+    except Exception:
+        return None
+
+
+def read_crc_info(log_path, version, lower):
+    """ChecksumReader.getCRCInfo (ChecksumReader.java:40-96): the checksum file at `version`, else the
+    newest one in [lower, version] (listing from <lower>.crc)."""
+    lower = min(lower, version)
+    got = _read_checksum_file(os.path.join(log_path, "%020d.crc" % version))
+    if got is not None or version == 0 or version == lower:
+        return got
+    start = "%020d.crc" % lower
+    try:
+        names = sorted(n for n in os.listdir(log_path) if n >= start)
+    except OSError:
+        return None
+    crcs = []
+    for n in names:
+        m = _CRC.match(n)
+        if not m:
+            continue
+        if int(m.group(1)) > version:
+            break                                       # takeWhile(version <= target)
+        crcs.append(n)
+    return _read_checksum_file(os.path.join(log_path, crcs[-1])) if crcs else None
+
+
+# ------------------------------------------------------------------------------------------------
 # Table / Snapshot / Scan
 # ------------------------------------------------------------------------------------------------
 class Table:
@@ -573,6 +621,8 @@ class Table:
         seg = build_log_segment(self.path)
         snap = Snapshot(self, seg)
         snap.load_ms["log_segment"] = (time.perf_counter() - t0) * 1e3
+        snap._json_batch_size = engine.json_batch_size
+        snap._parquet_batch_size = engine.cfg.parquet_batch_size
         snap._load_protocol_metadata(engine)
         return snap
 
@@ -596,7 +646,9 @@ class Snapshot:
         self.log_segment = seg
         self.protocol = None
         self.metadata = None
-        self.load_ms = {}   # snapshot-load phases (ms): log_segment, commits_pm, checkpoint_pm
+        self.load_ms = {}   # snapshot-load phases (ms): log_segment, crc, commits_pm, checkpoint_pm
+        self.crc_info = None
+        self._validated = False   # TableFeatures.validateReadSupportedTable ran in the P&M pass
         self._manifest = None
 
     def getVersion(self):
@@ -668,16 +720,36 @@ class Snapshot:
         return [f.path for f in sorted(cks, key=lambda f: os.path.basename(f.path), reverse=True)]
 
     def _load_protocol_metadata(self, engine):
-        """LogReplay.loadTableProtocolAndMetadata (internal/replay/LogReplay.java:220-314): newest
-        commit first, then the checkpoint (decoded on the GPU); once both are found the table must
-        be readable (TableFeatures.validateReadSupportedTable, delta_amd/actions.py)."""
+        """LogReplay's snapshot-load pass (internal/replay/LogReplay.java:130-150, 220-314, 384-426).
+
+        1. maybeGetNewerSnapshotHintAndCurrentCrcInfo: a fresh Table has no snapshot hint, so the
+           newest checksum file in [max(checkpoint version, version - 100, 0), version] becomes the
+           hint (ChecksumReader.getCRCInfo, replay/ChecksumReader.java:40-96). A hint at the
+           snapshot version ends the pass with its Protocol and Metadata (nothing else is read and,
+           as in the reference, nothing is validated).
+        2. Otherwise files newest first: commits (scanned on host threads, dk_log_pm_scan), then the
+           checkpoint (decoded on the GPU). Per batch the protocol is looked for first, then the
+           metadata; the table is validated (TableFeatures.validateReadSupportedTable) only when the
+           metadata turns up while the protocol is already known (:270-283). After the commit at
+           hint version + 1 the hint fills whatever is still missing (:292-302)."""
         from . import actions as A
+        seg = self.log_segment
+        v = seg.version
+        t0 = time.perf_counter()
+        ck_v = seg.checkpoints[0].version if seg.checkpoints else 0
+        crc = read_crc_info(seg.log_path, v, max(ck_v, v - 100, 0))
+        self.load_ms["crc"] = (time.perf_counter() - t0) * 1e3
+        self.crc_info = crc
+        if crc is not None and crc[0] == v:
+            self.protocol, self.metadata = crc[1], crc[2]
+            return
+        self._validated = False
         t0 = time.perf_counter()
         try:
-            self._pm_from_commits()
+            done = self._pm_from_commits(hint=crc)
         finally:
             self.load_ms["commits_pm"] = (time.perf_counter() - t0) * 1e3
-        if self.protocol is None or self.metadata is None:
+        if not done and (self.protocol is None or self.metadata is None):
             t0 = time.perf_counter()
             try:
                 self._pm_from_checkpoint(engine)
@@ -687,37 +759,78 @@ class Snapshot:
             raise DkError("No protocol found at version %d" % self.getVersion())
         if self.metadata is None:
             raise DkError("No metadata found at version %d" % self.getVersion())
-        # dataPath.toString(): the qualified path, unescaped (internal/fs/Path.java:328-350)
-        A.validate_read_supported(self.protocol, "file:" + self.table.path, self.metadata)
 
-    def _pm_from_commits(self):
+    def _found(self, protocol=None, metadata=None):
+        """One batch's finds, in the reference's order: protocol first, then metadata; validate when
+        the metadata arrives with the protocol already known. Returns True once both are known."""
         from . import actions as A
-        for d in reversed(self.log_segment.deltas):
-            with open(d.path, "rb") as f:
-                raw = f.read()
-            if b'"protocol"' not in raw and b'"metaData"' not in raw and b"\\u" not in raw:
-                continue                          # no line of this commit can hold either action
-            for line in raw.decode("utf-8", "replace").splitlines():
-                # only a line naming one of the two actions can hold it (a "\u"-escaped key
-                # is the one way to spell it otherwise)
-                if '"protocol"' in line or '"metaData"' in line or "\\u" in line:
-                    obj = json.loads(line)
-                    if self.protocol is None and obj.get("protocol") is not None:
-                        self.protocol = A.protocol_from_json(obj["protocol"])
-                    if self.metadata is None and obj.get("metaData") is not None:
-                        self.metadata = A.metadata_from_json(obj["metaData"])
-            if self.protocol is not None and self.metadata is not None:
-                return
+        if self.protocol is None and protocol is not None:
+            self.protocol = protocol
+            if self.metadata is not None:
+                return True
+        if self.metadata is None and metadata is not None:
+            self.metadata = metadata
+            if self.protocol is not None:
+                # dataPath.toString(): the qualified path, unescaped (internal/fs/Path.java:328-350)
+                A.validate_read_supported(self.protocol, "file:" + self.table.path, self.metadata)
+                self._validated = True
+                return True
+        return False
+
+    def _pm_from_commits(self, hint=None):
+        """Commit files newest first; returns True when the pass is complete (both found, or the
+        hint filled the rest)."""
+        from . import actions as A
+        deltas = list(reversed(self.log_segment.deltas))
+        if hint is not None:                 # only commits newer than the hint are read
+            deltas = [d for d in deltas if d.version > hint[0]]
+        n = len(deltas)
+        if n:
+            arr = lambda t: (t * n)()
+            pl, po, pn, ml, mo, mn = (arr(C.c_int64) for _ in range(6))
+            scanned = C.c_int32()
+            check(lib().dk_log_pm_scan(_cstrs([d.path for d in deltas]), n, pl, po, pn, ml, mo, mn, C.byref(scanned)))
+            J = self._json_batch_size
+            for i in range(scanned.value):
+                def action(off, ln, key):
+                    with open(deltas[i].path, "rb") as f:
+                        f.seek(off)
+                        return json.loads(f.read(ln).decode("utf-8", "replace"))[key]
+                # batches of J lines per commit file (DefaultJsonHandler): in line order
+                events = sorted([(pl[i] // J, 0, "p")] * (pl[i] >= 0) + [(ml[i] // J, 1, "m")] * (ml[i] >= 0))
+                b = 0
+                while b < len(events):
+                    batch = [e for e in events if e[0] == events[b][0]]
+                    prot = meta = None
+                    for _, _, k in batch:
+                        if k == "p" and self.protocol is None:
+                            prot = A.protocol_from_json(action(po[i], pn[i], "protocol"))
+                        if k == "m" and self.metadata is None:
+                            meta = A.metadata_from_json(action(mo[i], mn[i], "metaData"))
+                    if self._found(prot, meta):
+                        return True
+                    b += len(batch)
+                if hint is not None and deltas[i].version == hint[0] + 1:
+                    return self._from_hint(hint)
+        if hint is not None:
+            return self._from_hint(hint)
+        return False
+
+    def _from_hint(self, hint):
+        if self.protocol is None:
+            self.protocol = hint[1]
+        if self.metadata is None:
+            self.metadata = hint[2]
+        return True
 
     def _pm_from_checkpoint(self, engine):
         from . import actions as A
         cks = self.log_segment.checkpoints
         if cks and cks[0].kind == "v2" and cks[0].path.endswith(".json"):
             _, proto, meta = self._json_manifest()
-            if self.protocol is None and proto is not None:
-                self.protocol = A.protocol_from_json(proto)
-            if self.metadata is None and meta is not None:
-                self.metadata = A.metadata_from_json(meta)
+            if self._found(A.protocol_from_json(proto) if self.protocol is None and proto is not None else None,
+                           A.metadata_from_json(meta) if self.metadata is None and meta is not None else None):
+                return
             files = self._checkpoint_files(engine) if (self.protocol is None or self.metadata is None) else []
         else:
             files = self._checkpoint_files(engine) if cks else []
@@ -738,16 +851,21 @@ class Snapshot:
             if not files:
                 return
             ps = ParquetSet(engine, files, PM_LEAVES, groups=groups).decode()
+            B = self._parquet_batch_size
             for fi in range(len(files)):
-                # the first non-null protocol / metaData row of the batch, found on the device;
-                # only that row's values come back to the host
-                r = ps.first_row(fi, "protocol.minReaderVersion") if self.protocol is None else -1
-                if r >= 0:
-                    self.protocol = _protocol_row(ps, fi, r)
-                r = ps.first_row(fi, "metaData.id") if self.metadata is None else -1
-                if r >= 0:
-                    self.metadata = _metadata_row(ps, fi, r)
-                if self.protocol is not None and self.metadata is not None:
+                # the first non-null protocol / metaData row of the file, found on the device; only
+                # that row's values come back to the host; batches of B rows in row order (counted
+                # over the row groups decoded here).
+                rp = ps.first_row(fi, "protocol.minReaderVersion") if self.protocol is None else -1
+                rm = ps.first_row(fi, "metaData.id") if self.metadata is None else -1
+                prot = _protocol_row(ps, fi, rp) if rp >= 0 else None
+                meta = _metadata_row(ps, fi, rm) if rm >= 0 else None
+                if prot is not None and meta is not None and rp // B != rm // B:
+                    first, second = ((prot, None), (None, meta)) if rp < rm else ((None, meta), (prot, None))
+                    done = self._found(*first) or self._found(*second)
+                else:
+                    done = self._found(prot, meta)
+                if done:
                     break
             ps.close()
 

@@ -507,6 +507,20 @@ def _meta_json(meta_row):
     return {k: v for k, v in m.items() if v is not None}
 
 
+def write_crc(root: str, version: int, spec: TableSpec = None, protocol=None, metadata=None, extra=None):
+    """A Spark-style checksum file <version>.crc (one JSON object: table size, file counts, the
+    protocol and the metadata -- the fields ChecksumReader / CRCInfo read) in root/_delta_log."""
+    proto, meta = _pm_rows(spec or TableSpec())
+    obj = {"tableSizeBytes": 0, "numFiles": 0, "numMetadata": 1, "numProtocol": 1,
+           "protocol": protocol if protocol is not None else proto,
+           "metadata": metadata if metadata is not None else _meta_json(meta)}
+    obj.update(extra or {})
+    path = os.path.join(root, "_delta_log", "%020d.crc" % version)
+    with open(path, "w") as f:
+        f.write(json.dumps(obj) + "\n")
+    return path
+
+
 def write_table(root: str, spec: TableSpec):
     """Write the synthetic table under ``root``. Returns a dict describing what was written."""
     rng = np.random.Generator(np.random.PCG64([spec.seed, 0]))     # commit tail, file names

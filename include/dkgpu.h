@@ -228,6 +228,12 @@ void dk_dv_free(dk_dv_set* s);
 int  dk_json_tail_parse(dk_engine* e, const char* const* commit_paths, const int64_t* versions,
                         int32_t n_files, int32_t with_stats, dk_json_tail** out);
 int64_t dk_json_tail_rows(dk_json_tail* t);
+/* Snapshot-load P&M scan of commit files given newest first (LogReplay.loadTableProtocolAndMetadata,
+ * internal/replay/LogReplay.java:220-314): per file, the line index and byte range of the first line
+ * with a non-null top-level "protocol" / "metaData" (-1: none). Files are read 16 at a time on host
+ * threads; the scan stops after the block in which both were seen (*n_scanned = files scanned). */
+int  dk_log_pm_scan(const char* const* paths, int32_t n, int64_t* p_line, int64_t* p_off, int64_t* p_len,
+                    int64_t* m_line, int64_t* m_off, int64_t* m_len, int32_t* n_scanned);
 int  dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out);
 void dk_json_tail_free(dk_json_tail* t);
 

@@ -802,37 +802,96 @@ def validate_read_supported(prot, table_path, meta):
                       % (table_path, rv))
 
 
-def load_protocol_metadata(table_root: str):
-    """``LogReplay.loadTableProtocolAndMetadata`` (internal/replay/LogReplay.java:220-314), no hint:
-    files newest first (``LogSegment.allLogFilesReversed``); the first row whose ``protocol`` /
-    ``metaData`` struct is non-null wins; then ``TableFeatures.validateReadSupportedTable``.
-    Returns (protocol dict, metadata dict) -- every field of Protocol / Metadata -- with the
-    checkpoint decoded by the C oracle."""
+def _crc_file(path):
+    """ChecksumReader.readChecksumFile (ChecksumReader.java:98-127): one row, non-null protocol and
+    metadata, decodable -- else None."""
+    try:
+        with open(path, "rb") as fh:
+            lines = fh.read().decode("utf-8", "replace").splitlines()
+        if len(lines) != 1:
+            return None
+        obj = json.loads(lines[0])
+        if obj.get("protocol") is None or obj.get("metadata") is None:
+            return None
+        return (int(os.path.basename(path).split(".")[0]), _pm_json_protocol(obj["protocol"]),
+                _pm_json_metadata(obj["metadata"]))
+    except Exception:
+        return None
+
+
+def crc_info(log_path, version, lower):
+    """ChecksumReader.getCRCInfo (ChecksumReader.java:40-96)."""
+    lower = min(lower, version)
+    got = _crc_file(os.path.join(log_path, "%020d.crc" % version))
+    if got is not None or version in (0, lower):
+        return got
+    cands = []
+    for n in sorted(os.listdir(log_path)):
+        if n < "%020d.crc" % lower or not re.fullmatch(r"\d+\.crc", n):
+            continue
+        if int(n.split(".")[0]) > version:
+            break
+        cands.append(n)
+    return _crc_file(os.path.join(log_path, cands[-1])) if cands else None
+
+
+def load_protocol_metadata(table_root: str, json_batch_size=1024, parquet_batch_size=1024):
+    """``LogReplay.loadTableProtocolAndMetadata`` (internal/replay/LogReplay.java:220-314) behind
+    ``maybeGetNewerSnapshotHintAndCurrentCrcInfo`` (:384-426) for a fresh table (no snapshot hint):
+    the newest checksum file in [max(checkpoint version, version - 100, 0), version] is the hint; a
+    hint at the snapshot version answers directly. Otherwise files newest first
+    (``LogSegment.allLogFilesReversed``), batch by batch: the first non-null ``protocol`` row, then
+    the first non-null ``metaData`` row; ``TableFeatures.validateReadSupportedTable`` runs only when
+    the metadata is found with the protocol already known; after the commit at hint version + 1 the
+    hint fills the rest. Returns (protocol dict, metadata dict, validated) -- every field of Protocol /
+    Metadata -- with the checkpoint decoded by the C oracle."""
     seg = load_log_segment(table_root)
-    prot = meta = None
+    ckv = max([f.version for f in seg.all_files_reversed() if f.kind != "commit"], default=0)
+    hint = crc_info(os.path.join(table_root, "_delta_log"), seg.version, max(ckv, seg.version - 100, 0))
+    if hint is not None and hint[0] == seg.version:
+        return hint[1], hint[2], False
+    st = {"p": None, "m": None}
+    path = "file:" + os.path.abspath(table_root)
+
+    def batch(prot, meta):
+        if st["p"] is None and prot is not None:
+            st["p"] = prot()
+            if st["m"] is not None:
+                return "done"
+        if st["m"] is None and meta is not None:
+            st["m"] = meta()
+            if st["p"] is not None:
+                validate_read_supported(st["p"], path, st["m"])
+                return "validated"
+        return None
+
     for f in seg.all_files_reversed():
+        if hint is not None and f.version <= hint[0]:
+            break
         if f.kind == "commit" or f.path.endswith(".json"):      # commits and V2 JSON manifests
             with open(f.path, "rb") as fh:
                 lines = fh.read().decode("utf-8", "replace").splitlines()
-            for line in lines:
-                if not line.strip():
-                    continue
-                obj = json.loads(line)
-                if prot is None and obj.get("protocol") is not None:
-                    prot = _pm_json_protocol(obj["protocol"])
-                if meta is None and obj.get("metaData") is not None:
-                    meta = _pm_json_metadata(obj["metaData"])
+            for b0 in range(0, len(lines), json_batch_size):
+                objs = [json.loads(x) for x in lines[b0:b0 + json_batch_size] if x.strip()]
+                po = next((o["protocol"] for o in objs if o.get("protocol") is not None), None)
+                mo = next((o["metaData"] for o in objs if o.get("metaData") is not None), None)
+                r = batch(None if po is None else (lambda po=po: _pm_json_protocol(po)),
+                          None if mo is None else (lambda mo=mo: _pm_json_metadata(mo)))
+                if r:
+                    return st["p"], st["m"], r == "validated"
         else:
             pf = ParquetFile.open(f.path)
-            r = _first_defined(pf.read("protocol.minReaderVersion")) if prot is None else -1
-            if r >= 0:
-                prot = {"minReaderVersion": _scalar(pf, "protocol.minReaderVersion", r, np.int32),
+            rp = _first_defined(pf.read("protocol.minReaderVersion")) if st["p"] is None else -1
+            rm = _first_defined(pf.read("metaData.id")) if st["m"] is None else -1
+
+            def prot(r=rp):
+                return {"minReaderVersion": _scalar(pf, "protocol.minReaderVersion", r, np.int32),
                         "minWriterVersion": _scalar(pf, "protocol.minWriterVersion", r, np.int32),
                         "readerFeatures": _list_value(pf.read("protocol.readerFeatures.list.element"), r) or [],
                         "writerFeatures": _list_value(pf.read("protocol.writerFeatures.list.element"), r) or []}
-            r = _first_defined(pf.read("metaData.id")) if meta is None else -1
-            if r >= 0:
-                meta = {"id": _scalar(pf, "metaData.id", r), "name": _scalar(pf, "metaData.name", r),
+
+            def meta(r=rm):
+                return {"id": _scalar(pf, "metaData.id", r), "name": _scalar(pf, "metaData.name", r),
                         "description": _scalar(pf, "metaData.description", r),
                         "format": {"provider": _scalar(pf, "metaData.format.provider", r),
                                    "options": _map_value(pf.read("metaData.format.options.key_value.key"),
@@ -842,7 +901,15 @@ def load_protocol_metadata(table_root: str):
                         "createdTime": _scalar(pf, "metaData.createdTime", r, np.int64),
                         "configuration": _map_value(pf.read("metaData.configuration.key_value.key"),
                                                     pf.read("metaData.configuration.key_value.value"), r)}
-        if prot is not None and meta is not None:
-            validate_read_supported(prot, "file:" + os.path.abspath(table_root), meta)
-            return prot, meta
-    raise OracleError("No %s found at version %d" % ("protocol" if prot is None else "metadata", seg.version))
+            bp = rp // parquet_batch_size if rp >= 0 else None
+            bm = rm // parquet_batch_size if rm >= 0 else None
+            order = sorted({b for b in (bp, bm) if b is not None})
+            for b in order:
+                r = batch(prot if bp == b else None, meta if bm == b else None)
+                if r:
+                    return st["p"], st["m"], r == "validated"
+        if hint is not None and f.kind == "commit" and f.version == hint[0] + 1:
+            break
+    if hint is not None:
+        return st["p"] or hint[1], st["m"] or hint[2], False
+    raise OracleError("No %s found at version %d" % ("protocol" if st["p"] is None else "metadata", seg.version))

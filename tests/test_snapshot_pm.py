@@ -16,7 +16,7 @@ def _product_pm(root):
     eng = K.GpuEngine()
     try:
         snap = K.Table.forPath(eng, root).getLatestSnapshot(eng)
-        return snap.protocol, snap.metadata
+        return snap.protocol, snap.metadata, snap._validated
     finally:
         eng.close()
 
@@ -24,7 +24,7 @@ def _product_pm(root):
 @pytest.mark.parametrize("name", NAMES)
 def test_oracle_pm_golden(name):
     from oracle import ref
-    prot, meta = ref.load_protocol_metadata(os.path.join(TABLES, name))
+    prot, meta, _ = ref.load_protocol_metadata(os.path.join(TABLES, name))
     assert prot["minReaderVersion"] >= 1 and prot["minWriterVersion"] >= 1
     assert meta["id"] and meta["schemaString"].startswith("{") and meta["format"]["provider"] == "parquet"
     assert isinstance(meta["configuration"], dict) and isinstance(meta["partitionColumns"], list)
@@ -79,7 +79,7 @@ def test_oracle_pm_moved_rows(tmp_path):
     from oracle import ref
     d = str(tmp_path)
     _checkpoint_only(d, 1, (25_001, 13_007))
-    prot, meta = ref.load_protocol_metadata(d)
+    prot, meta, _ = ref.load_protocol_metadata(d)
     assert (prot["minReaderVersion"], prot["minWriterVersion"]) == (3, 7) and meta["partitionColumns"] == ["date"]
     assert prot["readerFeatures"] == ["deletionVectors", "v2Checkpoint"]
     assert meta["format"] == {"provider": "parquet", "options": {}} and meta["createdTime"] == 1_700_000_000_000
@@ -124,7 +124,7 @@ def test_oracle_read_support(tmp_path, case):
     prot, conf, err = VALIDATION_CASES[case]
     d = _pm_table(str(tmp_path / "t"), prot, conf)
     if err is None:
-        p, m = ref.load_protocol_metadata(d)
+        p, m, _ = ref.load_protocol_metadata(d)
         assert p["minReaderVersion"] == prot["minReaderVersion"]
         assert p["readerFeatures"] == prot.get("readerFeatures", [])
     else:
@@ -147,3 +147,96 @@ def test_gpu_read_support(tmp_path, case):
         with pytest.raises(DkError, match=re.escape(err)):
             K.Table.forPath(eng, d).getLatestSnapshot(eng)
         eng.close()
+
+
+# ---- checksum files and the order of the P&M finds (LogReplay.java:130-150, 260-302, 384-426) ----
+BAD = {"minReaderVersion": 3, "minWriterVersion": 7, "readerFeatures": ["fancyFeature"], "writerFeatures": []}
+GOOD = {"minReaderVersion": 1, "minWriterVersion": 2}
+
+
+def _meta(i):
+    import json
+    return {"id": "t%d" % i, "format": {"provider": "parquet", "options": {}},
+            "schemaString": json.dumps({"type": "struct", "fields": []}), "partitionColumns": [],
+            "configuration": {}, "createdTime": i}
+
+
+def _commits(d, actions_per_commit, crcs=()):
+    """Commits 0..n-1 with the given actions; crcs: (version, protocol, metadata, n_lines)."""
+    import json
+    log = os.path.join(d, "_delta_log")
+    os.makedirs(log)
+    for v, acts in enumerate(actions_per_commit):
+        with open(os.path.join(log, "%020d.json" % v), "w") as f:
+            f.write("".join(json.dumps(a) + "\n" for a in acts) or json.dumps({"commitInfo": {}}) + "\n")
+    for v, p, m, lines in crcs:
+        with open(os.path.join(log, "%020d.crc" % v), "w") as f:
+            f.write("\n".join([json.dumps({"protocol": p, "metadata": m, "numFiles": 0})] * lines) + "\n")
+    return d
+
+
+# (commits, crcs, expected error fragment or None)
+CRC_CASES = {
+    # a checksum file at the snapshot version answers alone: no log read, no validation
+    "crc-at-version": ([[{"protocol": GOOD}, {"metaData": _meta(0)}], [{"protocol": BAD}]],
+                       [(1, BAD, _meta(9), 1)], None),
+    # an older checksum file is the hint: the newer commit's metadata wins, the hint's protocol fills in
+    "crc-hint": ([[{"protocol": GOOD}, {"metaData": _meta(0)}], [{"protocol": GOOD}], [{"metaData": _meta(2)}]],
+                 [(1, BAD, _meta(1), 1)], None),
+    # a checksum file with two rows is not a checksum file: the log decides (and validates)
+    "crc-two-rows": ([[{"protocol": BAD}, {"metaData": _meta(0)}], []], [(1, GOOD, _meta(9), 2)],
+                     "requires reader table features [fancyFeature]"),
+    # metadata in a newer commit than the protocol: found first, so the reference never validates
+    "meta-newer-than-protocol": ([[{"protocol": BAD}], [{"metaData": _meta(1)}]], [], None),
+    # protocol newer than the metadata: validated when the metadata arrives
+    "protocol-newer": ([[{"metaData": _meta(0)}], [{"protocol": BAD}]], [], "fancyFeature"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CRC_CASES))
+def test_oracle_crc_and_order(tmp_path, name):
+    from oracle import ref
+    commits, crcs, err = CRC_CASES[name]
+    d = _commits(str(tmp_path / "t"), commits, crcs)
+    if err:
+        with pytest.raises(ref.OracleError, match=re.escape(err)):
+            ref.load_protocol_metadata(d)
+        return
+    p, m, validated = ref.load_protocol_metadata(d)
+    if name == "crc-at-version":
+        assert p == ref._pm_json_protocol(BAD) and m["id"] == "t9" and not validated
+    if name == "crc-hint":
+        assert p == ref._pm_json_protocol(BAD) and m["id"] == "t2" and not validated
+    if name == "meta-newer-than-protocol":
+        assert p["readerFeatures"] == ["fancyFeature"] and m["id"] == "t1" and not validated
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CRC_CASES))
+def test_gpu_crc_and_order(tmp_path, name):
+    from delta_amd import kernel as K
+    from delta_amd._lib import DkError
+    from oracle import ref
+    commits, crcs, err = CRC_CASES[name]
+    d = _commits(str(tmp_path / "t"), commits, crcs)
+    if err:
+        eng = K.GpuEngine()
+        with pytest.raises(DkError, match=re.escape(err)):
+            K.Table.forPath(eng, d).getLatestSnapshot(eng)
+        eng.close()
+    else:
+        assert _product_pm(d) == ref.load_protocol_metadata(d)
+
+
+@pytest.mark.gpu
+def test_gpu_crc_on_synthetic_checkpoint(tmp_path):
+    """A Spark-style checksum at the snapshot version: the snapshot loads from it, the scan is
+    unchanged."""
+    from delta_amd import kernel as K
+    from delta_amd import synth
+    from oracle import ref
+    d = str(tmp_path)
+    info = synth.write_table(d, synth.TableSpec(n_adds=5_000, n_commits=3))
+    synth.write_crc(d, info["version"])
+    got = _product_pm(d)
+    assert got == ref.load_protocol_metadata(d) and got[2] is False
