@@ -81,7 +81,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_parquet_row_offset", "dk_replay_ckpt_selection_bits", "dk_parquet_open_sel",
            "dk_parquet_prune_row_groups", "dk_parquet_nonnull_row_groups",
            "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close",
-           "dk_dv_load", "dk_dv_num_bits", "dk_dv_bitmap", "dk_dv_selection", "dk_dv_free", "dk_log_pm_scan"]
+           "dk_dv_load", "dk_dv_num_bits", "dk_dv_bitmap", "dk_dv_selection", "dk_dv_free", "dk_log_pm_scan",
+           "dk_replay_stats_parsed_files"]
 
 
 def lib(build_if_missing=True):
@@ -142,6 +143,7 @@ def lib(build_if_missing=True):
         "dk_dv_bitmap": (C.c_int, [P, I32, P, I64, I32]),
         "dk_dv_selection": (C.c_int, [P, I32, P, I64, P]),
         "dk_dv_free": (None, [P]),
+        "dk_replay_stats_parsed_files": (C.c_int, [P]),
         "dk_log_pm_scan": (C.c_int, [C.POINTER(C.c_char_p), I32] + [C.POINTER(I64)] * 6 + [C.POINTER(I32)]),
     }
     for name, (res, args) in sig.items():

@@ -243,6 +243,18 @@ struct StatsRows {
   int64_t row_tag;
 };
 
+// Data skipping over add.stats_parsed (typed Parquet columns of the same stats, one per program
+// path; integral and date paths only): per path its definition levels and fixed-width values.
+struct StatsParsedRows {
+  int64_t n;
+  int32_t n_paths;
+  int32_t struct_def;                 // row_def >= this: add.stats_parsed is non-null
+  const uint8_t* def[8];
+  const uint8_t* vals[8];
+  int32_t max_def[8];
+  int32_t width[8];                   // 4 (INT32, sign-extended) or 8 (INT64)
+};
+
 // Device-side counters and error state of one replay.
 struct DState {
   unsigned long long counters[5];        // commit-tail part (k_json_select)
@@ -262,6 +274,15 @@ struct ProbeCols {
   int32_t has_dv;
   int64_t n_rows;
   int64_t row_tag;   // added to the row index in error reports
+};
+
+// All checkpoint files of a replay for the one-launch probe: rows numbered across the files.
+struct ProbeSet {
+  const ProbeCols* cols;       // per file (device memory)
+  const int64_t* row0;         // n_files + 1 prefix of the files' rows
+  uint8_t* const* sel;         // per file selection bytes
+  int32_t n_files;
+  int64_t total;
 };
 
 }  // namespace dk

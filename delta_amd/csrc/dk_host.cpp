@@ -48,7 +48,10 @@ void launch_first_row(const uint8_t*, long long, int, unsigned long long*, hipSt
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
 void launch_stats_eval(const StatsRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
+void launch_stats_parsed(const StatsParsedRows&, const DSkipProg*, uint8_t*, hipStream_t);
 void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipStream_t);
+void launch_probe_all(const ProbeSet&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
+                      int32_t*, unsigned int*, DState*, hipStream_t);
 void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
@@ -2236,6 +2239,7 @@ struct dk_replay {
   DBuf d_skip, d_part;                  // device copies of the programs
   DBuf d_tstats_chars, d_tstats_off, d_tstats_len;
   std::vector<StatsRows> ck_stats;      // per checkpoint file (n = 0: no stats column)
+  std::vector<StatsParsedRows> ck_parsed;   // per checkpoint file: stats_parsed columns (n = 0: JSON)
   // partition pruning (dk_replay_set_partition_filter): program + partitionValues maps
   bool has_part = false;
   DPartProg part{};
@@ -2244,6 +2248,12 @@ struct dk_replay {
   std::vector<std::unique_ptr<DBuf>> map_bufs;
   std::vector<std::unique_ptr<DBuf>> d_csel;   // per checkpoint file
   std::vector<ProbeCols> probe;
+  // one-launch probe over every checkpoint file (ProbeSet): per-file columns / row prefix / selection
+  std::vector<ProbeCols> probe_run;      // the columns as launched (path hashes dropped on a reseed)
+  std::vector<int64_t> probe_row0;
+  std::vector<uint8_t*> probe_sel;
+  DBuf d_probe_cols, d_probe_row0, d_probe_sel;
+  bool probe_all = false;
   uint64_t mask = 0;
   uint32_t seed = 0;
   KTimer timer;
@@ -2315,9 +2325,15 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   if (r->d_state.alloc(sizeof(DState))) return 1;
   if (r->d_jsel.alloc(na + 16)) return 1;
   if (ckpt) {
-    int64_t max_rows = 1;
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) max_rows = std::max<int64_t>(max_rows, ckpt->files[fi].num_rows);
-    if (r->d_cand.alloc((size_t)max_rows * 4 + 64)) return 1;
+    int64_t max_rows = 1, total = 0;
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      max_rows = std::max<int64_t>(max_rows, ckpt->files[fi].num_rows);
+      total += ckpt->files[fi].num_rows;
+    }
+    // every file in one probe launch while global row numbers fit the int32 candidate list
+    static const bool per_file = getenv("DK_PROBE_PER_FILE") && atoi(getenv("DK_PROBE_PER_FILE"));
+    r->probe_all = !per_file && ckpt->files.size() > 1 && total < (1ll << 31) - 1;
+    if (r->d_cand.alloc((size_t)(r->probe_all ? total : max_rows) * 4 + 64)) return 1;
     if (r->d_cand_n.alloc(64)) return 1;
     for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
       ProbeCols pc{};
@@ -2474,6 +2490,30 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   if (depth != 1) return fail("dk_replay_set_skipping: program must leave one value");
   if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
   r->skip = P;
+  // add.stats_parsed fast path, per checkpoint file: every program path must be an integral / date
+  // stat whose typed leaf add.stats_parsed.<path> was projected and decoded with the matching width
+  r->ck_parsed.assign(r->ck ? r->ck->files.size() : 0, StatsParsedRows{});
+  static const bool no_parsed = getenv("DK_NO_STATS_PARSED") && atoi(getenv("DK_NO_STATS_PARSED"));
+  for (size_t fi = 0; fi < r->ck_parsed.size() && !no_parsed; fi++) {
+    StatsParsedRows R{};
+    R.n_paths = P.n_paths;
+    R.struct_def = 2;                     // add (1) . stats_parsed (2)
+    bool ok = P.n_paths > 0;
+    for (int q = 0; q < P.n_paths && ok; q++) {
+      const int t = P.path_type[q];
+      std::string leaf = "add.stats_parsed";
+      for (int d = 0; d < P.path_depth[q]; d++) leaf += "." + std::string(P.names + P.name_off[q][d], P.name_len[q][d]);
+      const DColumn* c = find_col(r->ck, (int)fi, leaf.c_str());
+      const int want = t == SK_LONG ? PT_INT64 : PT_INT32;
+      ok = (t == SK_LONG || t == SK_INT || t == SK_SHORT || t == SK_BYTE || t == SK_DATE) && c && c->present &&
+           !c->max_rep && c->phys == want && c->max_def >= 3;
+      if (!ok) break;
+      R.def[q] = c->row_def; R.max_def[q] = c->max_def;
+      R.vals[q] = c->null_only ? nullptr : c->fixed; R.width[q] = c->width;
+      if (c->null_only) R.max_def[q] = 1 << 30;          // no value anywhere: always null
+    }
+    if (ok) { R.n = r->ck->files[fi].num_rows; r->ck_parsed[fi] = R; }
+  }
   if (!r->d_skip.p && r->d_skip.alloc(sizeof(DSkipProg))) return -1;
   if (hipMemcpy(r->d_skip.p, &r->skip, sizeof(DSkipProg), hipMemcpyHostToDevice) != hipSuccess)
     return fail("dk_replay_set_skipping: copy failed");
@@ -2578,14 +2618,35 @@ static int replay_launch(dk_replay* r) {
     // decode errors are collected into the replay state too
     HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
     if (run_pipeline(p, 1, s)) return 1;
-    for (size_t fi = 0; fi < r->probe.size(); fi++) {
+    HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;       // dvUniqueId stream of "no DV"
+    dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
+    const uint64_t h_nodv = kd.hs.final_(kd.n);
+    if (r->probe_all) {
       KTimer::Scope sc(&T, 11, s);
-      ProbeCols pc = r->probe[fi];
-      if (r->seed != kDecodeSeed) pc.path_hash = nullptr;   // collision retry: rehash from the chars
-      HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;     // dvUniqueId stream of "no DV"
-      dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
-      launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, kd.hs.final_(kd.n),
-                   r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
+      const size_t nf = r->probe.size();
+      r->probe_run = r->probe;
+      r->probe_row0.assign(nf + 1, 0);
+      r->probe_sel.resize(nf);
+      for (size_t fi = 0; fi < nf; fi++) {
+        if (r->seed != kDecodeSeed) r->probe_run[fi].path_hash = nullptr;   // collision retry
+        r->probe_row0[fi + 1] = r->probe_row0[fi] + r->probe_run[fi].n_rows;
+        r->probe_sel[fi] = r->d_csel[fi]->as<uint8_t>();
+      }
+      if (upload(r->d_probe_cols, r->probe_run.data(), nf * sizeof(ProbeCols), s) ||
+          upload(r->d_probe_row0, r->probe_row0.data(), (nf + 1) * 8, s) ||
+          upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
+      ProbeSet PS{r->d_probe_cols.as<ProbeCols>(), r->d_probe_row0.as<int64_t>(), r->d_probe_sel.as<uint8_t* const>(),
+                  (int32_t)nf, r->probe_row0[nf]};
+      launch_probe_all(PS, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv, r->d_cand.as<int32_t>(),
+                       r->d_cand_n.as<unsigned int>(), st, s);
+    } else {
+      for (size_t fi = 0; fi < r->probe.size(); fi++) {
+        KTimer::Scope sc(&T, 11, s);
+        ProbeCols pc = r->probe[fi];
+        if (r->seed != kDecodeSeed) pc.path_hash = nullptr;   // collision retry: rehash from the chars
+        launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv,
+                     r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
+      }
     }
     if (r->has_part)                        // partition pruning on the checkpoint files' rows
       for (size_t fi = 0; fi < r->ck_maps.size(); fi++) {
@@ -2595,7 +2656,10 @@ static int replay_launch(dk_replay* r) {
     if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
       for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
         KTimer::Scope sc(&T, 17, s);
-        launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+        if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
+          launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), s);
+        else
+          launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
     }
     // later work on the checkpoint's stream (column reads) sees the decoded columns
     HIPOK(hipEventRecord(r->ev_out, s));
@@ -2713,6 +2777,13 @@ extern "C" int dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* d
   HIPOK(hipMemcpyAsync(dst, tmp.p, nb, hipMemcpyDeviceToHost, s));
   HIPOK(hipStreamSynchronize(s));
   return 0;
+}
+
+// checkpoint files whose data skipping reads add.stats_parsed (after dk_replay_set_skipping)
+extern "C" int dk_replay_stats_parsed_files(dk_replay* r) {
+  int n = 0;
+  if (r && r->has_skip) for (const auto& R : r->ck_parsed) n += R.n > 0;
+  return n;
 }
 
 extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {

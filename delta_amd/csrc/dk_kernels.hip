@@ -3381,6 +3381,24 @@ __device__ __forceinline__ void block_count3(DState* st, unsigned long long a, u
 //                 candidate list (wave-aggregated atomic).
 //   k_probe_cand  the full key path for the candidates: canonical URI hash (java.net.URI rules),
 //                 dvUniqueId stream, byte-exact verification against the tail key, counters.
+// one row of k_probe_fast: seen (add non-null), chosen (decided selected), defer (candidate)
+__device__ __forceinline__ void probe_fast_row(const ProbeCols& pc, long long r, const Slot* __restrict__ slots,
+                                               uint64_t mask, uint64_t h_nodv, bool* seen, bool* chosen, bool* defer) {
+  *seen = *chosen = *defer = false;
+  if (r >= pc.n_rows || pc.path_def[r] < 1) return;
+  *seen = true;
+  const uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
+  if (hp == 0 || (pc.has_dv && pc.st_def[r] >= 2)) { *defer = true; return; }
+  const uint64_t h = hash_combine(hp, h_nodv);
+  uint64_t q = h & mask;
+  unsigned long long k;
+  while ((k = slots[q].h) != 0ull) {
+    if (k == h) { *defer = true; return; }
+    q = (q + 1) & mask;
+  }
+  *chosen = true;
+}
+
 __global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
                                                    uint64_t h_nodv, uint8_t* __restrict__ sel,
                                                    int32_t* __restrict__ cand, unsigned int* __restrict__ cand_n,
@@ -3389,23 +3407,8 @@ __global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const Slot* __r
   const int lane = threadIdx.x & 63;
   for (long long r0 = (long long)blockIdx.x * blockDim.x; r0 < pc.n_rows; r0 += (long long)gridDim.x * blockDim.x) {
     const long long r = r0 + threadIdx.x;
-    bool seen = false, chosen = false, defer = false;
-    if (r < pc.n_rows && pc.path_def[r] >= 1) {
-      seen = true;
-      const uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
-      if (hp == 0 || (pc.has_dv && pc.st_def[r] >= 2)) {
-        defer = true;
-      } else {
-        const uint64_t h = hash_combine(hp, h_nodv);
-        uint64_t q = h & mask;
-        unsigned long long k;
-        while ((k = slots[q].h) != 0ull) {
-          if (k == h) { defer = true; break; }
-          q = (q + 1) & mask;
-        }
-        chosen = !defer;
-      }
-    }
+    bool seen, chosen, defer;
+    probe_fast_row(pc, r, slots, mask, h_nodv, &seen, &chosen, &defer);
     if (r < pc.n_rows && !defer) sel[r] = chosen;
     const uint64_t m = __ballot(defer);
     if (m) {
@@ -3419,15 +3422,53 @@ __global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const Slot* __r
   block_count3(st, n_seen, n_chosen, 0);
 }
 
-__global__ __launch_bounds__(NT) void k_probe_cand(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
-                                                   const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
-                                                   uint32_t seed, uint8_t* __restrict__ sel,
-                                                   const int32_t* __restrict__ cand, const unsigned int* __restrict__ cand_n,
-                                                   DState* __restrict__ st) {
-  unsigned long long n_chosen = 0, n_dup = 0;
-  const long long nc = *cand_n;
-  for (long long ci = (long long)blockIdx.x * blockDim.x + threadIdx.x; ci < nc; ci += (long long)gridDim.x * blockDim.x) {
-    const long long r = cand[ci];
+// file of global row g: the last f with row0[f] <= g (row0 ascending, n + 1 entries)
+__device__ __forceinline__ int probe_file(const int64_t* __restrict__ row0, int n, long long g) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (row0[mid] <= g) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Every checkpoint file of the replay in one launch (rows numbered across files; candidates keep
+// the global row), instead of a launch pair per file: a 64-part checkpoint's 1.56M-row files each
+// fill the chip for only a few microseconds.
+__global__ __launch_bounds__(NT) void k_probe_fast_all(ProbeSet PS, const Slot* __restrict__ slots, uint64_t mask,
+                                                       uint64_t h_nodv, int32_t* __restrict__ cand,
+                                                       unsigned int* __restrict__ cand_n, DState* __restrict__ st) {
+  unsigned long long n_seen = 0, n_chosen = 0;
+  const int lane = threadIdx.x & 63;
+  for (long long g0 = (long long)blockIdx.x * blockDim.x; g0 < PS.total; g0 += (long long)gridDim.x * blockDim.x) {
+    const long long g = g0 + threadIdx.x;
+    bool seen = false, chosen = false, defer = false;
+    int f = 0;
+    long long r = 0;
+    if (g < PS.total) {
+      f = probe_file(PS.row0, PS.n_files, g);
+      r = g - PS.row0[f];
+      probe_fast_row(PS.cols[f], r, slots, mask, h_nodv, &seen, &chosen, &defer);
+      if (!defer) PS.sel[f][r] = chosen;
+    }
+    const uint64_t m = __ballot(defer);
+    if (m) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(cand_n, (unsigned int)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (defer) cand[base + lane_rank(m)] = (int32_t)g;
+    }
+    n_seen += seen; n_chosen += chosen;
+  }
+  block_count3(st, n_seen, n_chosen, 0);
+}
+
+// the full key path for one candidate row r of file pc (selection written, counters returned)
+__device__ __forceinline__ void probe_cand_row(const ProbeCols& pc, long long r, const Slot* __restrict__ slots,
+                                               uint64_t mask, const DJsonAction* __restrict__ acts,
+                                               const uint8_t* __restrict__ canon, uint32_t seed,
+                                               uint8_t* __restrict__ sel, DState* __restrict__ st,
+                                               unsigned long long* n_chosen, unsigned long long* n_dup) {
     bool chosen = false, dup = false;
     uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
     const int64_t o0 = pc.path_offs[r];
@@ -3492,7 +3533,32 @@ __global__ __launch_bounds__(NT) void k_probe_cand(ProbeCols pc, const Slot* __r
       else chosen = true;
     }
     sel[r] = chosen;
-    n_chosen += chosen; n_dup += dup;
+    *n_chosen += chosen; *n_dup += dup;
+}
+
+__global__ __launch_bounds__(NT) void k_probe_cand(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
+                                                   const DJsonAction* __restrict__ acts, const uint8_t* __restrict__ canon,
+                                                   uint32_t seed, uint8_t* __restrict__ sel,
+                                                   const int32_t* __restrict__ cand, const unsigned int* __restrict__ cand_n,
+                                                   DState* __restrict__ st) {
+  unsigned long long n_chosen = 0, n_dup = 0;
+  const long long nc = *cand_n;
+  for (long long ci = (long long)blockIdx.x * blockDim.x + threadIdx.x; ci < nc; ci += (long long)gridDim.x * blockDim.x)
+    probe_cand_row(pc, cand[ci], slots, mask, acts, canon, seed, sel, st, &n_chosen, &n_dup);
+  block_count3(st, 0, n_chosen, n_dup);
+}
+
+__global__ __launch_bounds__(NT) void k_probe_cand_all(ProbeSet PS, const Slot* __restrict__ slots, uint64_t mask,
+                                                       const DJsonAction* __restrict__ acts,
+                                                       const uint8_t* __restrict__ canon, uint32_t seed,
+                                                       const int32_t* __restrict__ cand,
+                                                       const unsigned int* __restrict__ cand_n, DState* __restrict__ st) {
+  unsigned long long n_chosen = 0, n_dup = 0;
+  const long long nc = *cand_n;
+  for (long long ci = (long long)blockIdx.x * blockDim.x + threadIdx.x; ci < nc; ci += (long long)gridDim.x * blockDim.x) {
+    const long long g = cand[ci];
+    const int f = probe_file(PS.row0, PS.n_files, g);
+    probe_cand_row(PS.cols[f], g - PS.row0[f], slots, mask, acts, canon, seed, PS.sel[f], st, &n_chosen, &n_dup);
   }
   block_count3(st, 0, n_chosen, n_dup);
 }
@@ -3613,6 +3679,17 @@ void launch_table_update(DJsonAction* a, int n, Slot* slots, uint64_t mask, cons
 void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint8_t* sel, DState* st, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, sel, st);
 }
+void launch_probe_all(const ProbeSet& PS, const Slot* slots, uint64_t mask, const DJsonAction* acts,
+                      const uint8_t* canon, uint32_t seed, uint64_t h_nodv, int32_t* cand, unsigned int* cand_n,
+                      DState* st, hipStream_t s) {
+  if (!PS.total) return;
+  const long long want = (PS.total + NT - 1) / NT;
+  const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
+  hipMemsetAsync(cand_n, 0, sizeof(unsigned int), s);
+  hipLaunchKernelGGL(k_probe_fast_all, dim3(grid), dim3(NT), 0, s, PS, slots, mask, h_nodv, cand, cand_n, st);
+  hipLaunchKernelGGL(k_probe_cand_all, dim3(grid), dim3(NT), 0, s, PS, slots, mask, acts, canon, seed, cand, cand_n, st);
+}
+
 void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const DJsonAction* acts,
                   const uint8_t* canon, uint32_t seed, uint64_t h_nodv, uint8_t* sel, int32_t* cand,
                   unsigned int* cand_n, DState* st, hipStream_t s) {
@@ -3627,6 +3704,33 @@ void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const D
 }  // namespace dk
 
 namespace dk {
+// The same predicate over add.stats_parsed: the typed columns replace the JSON scan; a row whose
+// stats_parsed struct is null keeps its selection, as a null stats string does.
+__global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DSkipProg* __restrict__ Pp,
+                                                     uint8_t* __restrict__ sel) {
+  const DSkipProg& P = *Pp;
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
+       r += (long long)gridDim.x * blockDim.x) {
+    if (!sel[r] || R.def[0][r] < R.struct_def) continue;
+    long long val[SK_MAX_PATHS];
+    uint32_t set = 0;
+    for (int p = 0; p < R.n_paths; p++) {
+      if (R.def[p][r] < R.max_def[p]) { val[p] = 0; continue; }
+      val[p] = R.width[p] == 8 ? ((const long long*)R.vals[p])[r] : (long long)((const int32_t*)R.vals[p])[r];
+      set |= 1u << p;
+    }
+    // (no string / decimal / float stat here: the stats base pointer is never read)
+    if (sk_eval(P, val, set, (const uint8_t*)P.names) == 0) sel[r] = 0;   // COALESCE(skip, true)
+  }
+}
+
+void launch_stats_parsed(const StatsParsedRows& R, const DSkipProg* P, uint8_t* sel, hipStream_t s) {
+  if (R.n <= 0) return;
+  const long long want = (R.n + NT - 1) / NT;
+  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
+  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, sel);
+}
+
 void launch_stats_eval(const StatsRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {
   if (R.n <= 0) return;
   const long long want = (R.n + NT - 1) / NT;

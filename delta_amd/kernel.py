@@ -1116,6 +1116,12 @@ class GpuScan:
             sel = None
         self.ckpt_files = [all_files[i] for i in self.ckpt_index]
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
+        if self.skipping is not None:
+            # the typed add.stats_parsed leaves of the program's stats paths (integral / date): the
+            # engine evaluates skipping over them where a checkpoint file carries them
+            _, paths, types, _ = self.skipping
+            if all(t in (0, 1, 2, 3, 4) for t in types):
+                leaves = leaves + ["add.stats_parsed." + ".".join(p) for p in paths]
         t2 = time.perf_counter()
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel) if self.ckpt_files else None
         t3 = time.perf_counter()

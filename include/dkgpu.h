@@ -293,6 +293,12 @@ int  dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_rep
 /* install (prog != NULL) or clear the data-skipping program applied after reconciliation; the
  * tail must have been parsed with stats and the checkpoint projection must include add.stats */
 int  dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog);
+/* Checkpoint files whose skipping reads the typed add.stats_parsed columns instead of the add.stats
+ * JSON: those where every program path is an integral / date stat whose leaf
+ * add.stats_parsed.<path> was projected (INT64 for long, INT32 otherwise). The predicate is the same;
+ * the columns are Spark's from_json(stats) (JsonHandler.parseJson hook), so the
+ * selection equals the JSON path's. DK_NO_STATS_PARSED=1 turns it off. */
+int  dk_replay_stats_parsed_files(dk_replay* r);
 /* install (prog != NULL) or clear the partition-pruning program, applied before data skipping; the
  * checkpoint projection must include add.partitionValues */
 int  dk_replay_set_partition_filter(dk_replay* r, const dk_part_program* prog);

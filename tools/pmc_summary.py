@@ -26,7 +26,9 @@ args = ap.parse_args()
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(args.root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
-        acc[r["Kernel_Name"].split("(")[0].replace("dk::", "")][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        name = r["Kernel_Name"].split("(")[0].replace("dk::", "").replace("void ", "")
+        name = name.split("<")[0].replace("k_snap_frag_t", "k_snap_frag")      # template instances
+        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 
 def big_mean(v):
     # the bench's full-size launches: the snapshot-load P&M pass launches the same kernels over a few
