@@ -50,9 +50,10 @@ void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*,
 void launch_stats_eval(const StatsRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
 void launch_stats_parsed(const StatsParsedRows&, const DSkipProg*, uint8_t*, hipStream_t);
 void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipStream_t);
-void launch_probe_all(const ProbeSet&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
+void launch_table_fp(const Slot*, uint32_t*, uint64_t, hipStream_t);
+void launch_probe_all(const ProbeSet&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                       int32_t*, unsigned int*, DState*, hipStream_t);
-void launch_probe(const ProbeCols&, const Slot*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
+void launch_probe(const ProbeCols&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
 
@@ -2232,6 +2233,7 @@ struct dk_replay {
   std::vector<DJsonAction> acts;
   std::vector<int64_t> act_row;        // tail row of each action
   DBuf d_acts, d_jchars, d_canon, d_slots, d_state, d_jsel;
+  DBuf d_fp;                  // slot fingerprints for k_probe_fast (k_table_fp)
   DBuf d_cand, d_cand_n;      // probe candidates (rows needing the full key path)
   // data skipping (dk_replay_set_skipping): program + the tail's stats strings per action
   bool has_skip = false;
@@ -2322,6 +2324,7 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   if (upload(r->d_jchars, jchars.data(), jchars.size(), s)) return 1;
   if (r->d_canon.alloc(canon_n + 64)) return 1;
   if (r->d_slots.alloc(cap * sizeof(Slot))) return 1;
+  if (r->d_fp.alloc(cap * sizeof(uint32_t))) return 1;
   if (r->d_state.alloc(sizeof(DState))) return 1;
   if (r->d_jsel.alloc(na + 16)) return 1;
   if (ckpt) {
@@ -2618,6 +2621,7 @@ static int replay_launch(dk_replay* r) {
     // decode errors are collected into the replay state too
     HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
     if (run_pipeline(p, 1, s)) return 1;
+    launch_table_fp(S, r->d_fp.as<uint32_t>(), r->mask + 1, s);
     HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;       // dvUniqueId stream of "no DV"
     dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
     const uint64_t h_nodv = kd.hs.final_(kd.n);
@@ -2637,14 +2641,14 @@ static int replay_launch(dk_replay* r) {
           upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
       ProbeSet PS{r->d_probe_cols.as<ProbeCols>(), r->d_probe_row0.as<int64_t>(), r->d_probe_sel.as<uint8_t* const>(),
                   (int32_t)nf, r->probe_row0[nf]};
-      launch_probe_all(PS, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv, r->d_cand.as<int32_t>(),
+      launch_probe_all(PS, S, r->d_fp.as<uint32_t>(), r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv, r->d_cand.as<int32_t>(),
                        r->d_cand_n.as<unsigned int>(), st, s);
     } else {
       for (size_t fi = 0; fi < r->probe.size(); fi++) {
         KTimer::Scope sc(&T, 11, s);
         ProbeCols pc = r->probe[fi];
         if (r->seed != kDecodeSeed) pc.path_hash = nullptr;   // collision retry: rehash from the chars
-        launch_probe(pc, S, r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv,
+        launch_probe(pc, S, r->d_fp.as<uint32_t>(), r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv,
                      r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
       }
     }

@@ -176,7 +176,16 @@ constexpr int SNAP_FRAG = 65536;      // Google snappy compresses every 64 KiB o
 constexpr int SNAP_SEG = DK_SNAP_SEG; // compressed bytes per speculative walker
 constexpr int SNAP_REC = DK_SNAP_REC; // tag positions a walker records for the convergence test
 constexpr int SNAP_FWIN = 1024;       // k_snap_frag: compressed-stream window (LDS)
-constexpr int SNAP_RING = 4096;       // k_snap_frag: output ring (LDS)
+#ifndef DK_SF_RING
+#define DK_SF_RING 4096
+#endif
+#ifndef DK_SF_FW
+#define DK_SF_FW 2048
+#endif
+#ifndef DK_SF_MARGIN
+#define DK_SF_MARGIN 640
+#endif
+constexpr int SNAP_RING = DK_SF_RING; // k_snap_frag: output ring (LDS)
 constexpr int SNAP_FLUSH = 1024;      // k_snap_frag: ring -> HBM flush granule
 
 // compressed-stream window in LDS: in-offsets [ws, ws + W) (ws may precede the stream start by up
@@ -615,9 +624,18 @@ __device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS builds only 
 #define SSTAT(i, v) ((void)0)
 #define STIME(i) ((void)0)
 #endif
-constexpr int SF_FW = 2048;                // compressed window
-constexpr int SF_BOUT = 512;               // a batch stops collecting tags at this many output bytes
+constexpr int SF_FW = DK_SF_FW;            // compressed window
+#ifndef DK_SF_BOUT
+#define DK_SF_BOUT 512
+#endif
+constexpr int SF_BOUT = DK_SF_BOUT;        // a batch stops collecting tags at this many output bytes
 constexpr int SF_BMAX = SF_BOUT + 64;      // max batch output (every batched tag has <= 64 bytes)
+constexpr int SF_CH = (SF_BMAX + 63) / 64; // output bytes per lane in the byte-parallel stage
+#ifndef DK_SF_CPL
+#define DK_SF_CPL 4
+#endif
+constexpr int SF_CPL = DK_SF_CPL;          // bitmap discovery: candidate stream bytes per lane (4 or 8)
+static_assert(SF_CPL * 64 + 69 <= DK_SF_MARGIN, "the discovery window must stay inside the LDS copy");
 constexpr int SF_RM = SNAP_RING - 1;
 enum : int32_t { SM_WIN = 0, SM_RING = 1, SM_FAR = 2, SM_DEP = 3, SM_FARQ = 4 };
 
@@ -693,7 +711,7 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
 #pragma unroll
     for (int k = 0; k < SF_FW / 256; k++) W32[lane + 64 * k] = v[k];
     if (use_bits) {
-      BW[lane] = bw;
+      if (lane < SF_FW / 32 + 4) BW[lane] = bw;
       if (lane < SF_FW / 32 + 4 - 64) BW[64 + lane] = bw2;
     }
   };
@@ -716,25 +734,25 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
     o = __builtin_amdgcn_readfirstlane(o);
     ws = __builtin_amdgcn_readfirstlane(ws);
     flushed = __builtin_amdgcn_readfirstlane(flushed);
-    if (p + 640 > ws + SF_FW && ws + SF_FW < clen) { refill(p); SSTAT(6, 1); }
+    if (p + DK_SF_MARGIN > ws + SF_FW && ws + SF_FW < clen) { refill(p); SSTAT(6, 1); }
     STIME(13);                                   // loop top + refill
     // ---- 1. tag starts ----
     int32_t n = 0, t = p, outsum = 0, vstart = 0, biglen = 0;
     if (use_bits) {
-      // 256 candidate bytes, 4 per lane: the set bits are the tag starts; a wave scan ranks them
-      // and each tag's offset lands in TP[rank]; lane i then parses tag i from the LDS window
-      const int32_t q = t + 4 * lane, rel = q - wb0;
+      // 64 * SF_CPL candidate bytes, SF_CPL per lane: the set bits are the tag starts; a wave scan
+      // ranks them and each tag's offset lands in TP[rank]; lane i then parses tag i from the window
+      const int32_t q = t + SF_CPL * lane, rel = q - wb0;
       uint32_t b4 = 0;
       if (q < ce) {
         const uint64_t d = ((uint64_t)BW[(rel >> 5) + 1] << 32) | BW[rel >> 5];
-        b4 = (uint32_t)(d >> (rel & 31)) & 15u;
+        b4 = (uint32_t)(d >> (rel & 31)) & ((1u << SF_CPL) - 1);
       }
       const int32_t cnt = __popc(b4);
       const int32_t incl = dpp_scan_add(cnt);
       const int32_t nt = __builtin_amdgcn_readlane(incl, 63);
       int32_t r0 = incl - cnt;
-      for (int bb = 0; bb < 4; bb++)
-        if ((b4 >> bb) & 1) { if (r0 < 64) TP[r0] = (int16_t)(4 * lane + bb); r0++; }
+      for (int bb = 0; bb < SF_CPL; bb++)
+        if ((b4 >> bb) & 1) { if (r0 < 64) TP[r0] = (int16_t)(SF_CPL * lane + bb); r0++; }
       const int32_t nw = nt < 64 ? nt : 64;
       const bool intag = lane < nw;
       const int32_t pos = intag ? (int32_t)TP[lane] : 0;
@@ -954,7 +972,7 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
     }
     STIME(17);                                   // far-quick loads issued
     // ---- 5. byte-parallel production of every WIN / RING / FAR tag ----
-    const int32_t CH = (xf & SX_NO_BYTES) ? 0 : (total + 63) >> 6;   // output bytes per lane (<= 9)
+    const int32_t CH = (xf & SX_NO_BYTES) ? 0 : (total + 63) >> 6;   // output bytes per lane (<= SF_CH)
     SSTAT(8, CH); SSTAT(2, __popcll(__ballot(valid && mode == SM_DEP))); SSTAT(3, __popcll(__ballot(valid && mode >= SM_FAR && mode != SM_DEP)));
     SSTAT(4, __popcll(__ballot(valid && is_copy && mode == SM_WIN))); SSTAT(10, __popcll(__ballot(valid && mode == SM_RING)));
     for (int32_t b = lane * 16; b < total; b += 64 * 16) *(uint4*)(M + b) = make_uint4(0, 0, 0, 0);
@@ -967,24 +985,24 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
       // staged so the dependent LDS depth is fixed: tag-map bytes, the owning tags (running max,
       // DPP prefix max across lanes), their parameters, the source bytes, the stores
       const int32_t b0 = lane * CH;
-      int32_t mb[9];
+      int32_t mb[SF_CH];
 #pragma unroll
-      for (int32_t k = 0; k < 9; k++) mb[k] = (k < CH && b0 + k < total) ? (int32_t)M[b0 + k] : 0;
+      for (int32_t k = 0; k < SF_CH; k++) mb[k] = (k < CH && b0 + k < total) ? (int32_t)M[b0 + k] : 0;
       int32_t mx = 0;
 #pragma unroll
-      for (int32_t k = 0; k < 9; k++) mx = max(mx, mb[k]);
+      for (int32_t k = 0; k < SF_CH; k++) mx = max(mx, mb[k]);
       int32_t cur = dpp_shr1(dpp_scan_max(mx));          // owner of this lane's first byte
-      u32x4 q[9];
+      u32x4 q[SF_CH];
 #pragma unroll
-      for (int32_t k = 0; k < 9; k++) {
+      for (int32_t k = 0; k < SF_CH; k++) {
         if (mb[k]) cur = mb[k];
         q[k] = prm[cur > 0 ? cur - 1 : 0];
       }
-      int32_t sa[9];                                     // LDS source address, -1 none
-      int32_t ga[9];                                     // FAR: output offset of the source, -1 none
+      int32_t sa[SF_CH];                                     // LDS source address, -1 none
+      int32_t ga[SF_CH];                                     // FAR: output offset of the source, -1 none
       bool any_far = false;
 #pragma unroll
-      for (int32_t k = 0; k < 9; k++) {
+      for (int32_t k = 0; k < SF_CH; k++) {
         sa[k] = -1; ga[k] = -1;
         const int32_t b = b0 + k;
         const int32_t md = (int32_t)(q[k].z & 0xff);
@@ -996,19 +1014,19 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
           else sa[k] = md == SM_WIN ? (int32_t)q[k].y + i : (((int32_t)q[k].y + i) & SF_RM);
         }
       }
-      uint32_t v[9];
+      uint32_t v[SF_CH];
 #pragma unroll
-      for (int32_t k = 0; k < 9; k++) v[k] = sa[k] >= 0 ? L[sa[k]] : 0;
+      for (int32_t k = 0; k < SF_CH; k++) v[k] = sa[k] >= 0 ? L[sa[k]] : 0;
 #pragma unroll
-      for (int32_t k = 0; k < 9; k++) if (sa[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)v[k];
+      for (int32_t k = 0; k < SF_CH; k++) if (sa[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)v[k];
       if (!(xf & SX_NO_FAR) && __ballot(any_far)) {
         // far sources: bytes this wave flushed to HBM earlier (its stores complete first)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        uint32_t gv[9];
+        uint32_t gv[SF_CH];
 #pragma unroll
-        for (int32_t k = 0; k < 9; k++) gv[k] = ga[k] >= 0 ? gout[ga[k]] : 0;
+        for (int32_t k = 0; k < SF_CH; k++) gv[k] = ga[k] >= 0 ? gout[ga[k]] : 0;
 #pragma unroll
-        for (int32_t k = 0; k < 9; k++) if (ga[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)gv[k];
+        for (int32_t k = 0; k < SF_CH; k++) if (ga[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)gv[k];
       }
     }
     if (farq) {
@@ -3382,7 +3400,13 @@ __device__ __forceinline__ void block_count3(DState* st, unsigned long long a, u
 //   k_probe_cand  the full key path for the candidates: canonical URI hash (java.net.URI rules),
 //                 dvUniqueId stream, byte-exact verification against the tail key, counters.
 // one row of k_probe_fast: seen (add non-null), chosen (decided selected), defer (candidate)
-__device__ __forceinline__ void probe_fast_row(const ProbeCols& pc, long long r, const Slot* __restrict__ slots,
+// The fast probe walks a 32-bit fingerprint per slot (fp[q] = high word of slots[q].h | 1, 0 = empty;
+// built by k_table_fp) instead of the 32-byte slots: the walk visits the same slots, the array is an
+// eighth of the size (L2-resident at C3's 400k tail actions), and an equal fingerprint only defers
+// the row to k_probe_cand, which compares the full hash and the key bytes.
+__device__ __forceinline__ uint32_t slot_fp(uint64_t h) { return (uint32_t)(h >> 32) | 1u; }
+
+__device__ __forceinline__ void probe_fast_row(const ProbeCols& pc, long long r, const uint32_t* __restrict__ fp,
                                                uint64_t mask, uint64_t h_nodv, bool* seen, bool* chosen, bool* defer) {
   *seen = *chosen = *defer = false;
   if (r >= pc.n_rows || pc.path_def[r] < 1) return;
@@ -3390,16 +3414,25 @@ __device__ __forceinline__ void probe_fast_row(const ProbeCols& pc, long long r,
   const uint64_t hp = pc.path_hash ? pc.path_hash[r] : 0ull;
   if (hp == 0 || (pc.has_dv && pc.st_def[r] >= 2)) { *defer = true; return; }
   const uint64_t h = hash_combine(hp, h_nodv);
+  const uint32_t f = slot_fp(h);
   uint64_t q = h & mask;
-  unsigned long long k;
-  while ((k = slots[q].h) != 0ull) {
-    if (k == h) { *defer = true; return; }
+  uint32_t k;
+  while ((k = fp[q]) != 0u) {
+    if (k == f) { *defer = true; return; }
     q = (q + 1) & mask;
   }
   *chosen = true;
 }
 
-__global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const Slot* __restrict__ slots, uint64_t mask,
+__global__ void k_table_fp(const Slot* __restrict__ slots, uint32_t* __restrict__ fp, uint64_t n) {
+  const uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) { const uint64_t h = slots[q].h; fp[q] = h ? slot_fp(h) : 0u; }
+}
+void launch_table_fp(const Slot* slots, uint32_t* fp, uint64_t n, hipStream_t s) {
+  hipLaunchKernelGGL(k_table_fp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, fp, n);
+}
+
+__global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const uint32_t* __restrict__ fp, uint64_t mask,
                                                    uint64_t h_nodv, uint8_t* __restrict__ sel,
                                                    int32_t* __restrict__ cand, unsigned int* __restrict__ cand_n,
                                                    DState* __restrict__ st) {
@@ -3408,7 +3441,7 @@ __global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const Slot* __r
   for (long long r0 = (long long)blockIdx.x * blockDim.x; r0 < pc.n_rows; r0 += (long long)gridDim.x * blockDim.x) {
     const long long r = r0 + threadIdx.x;
     bool seen, chosen, defer;
-    probe_fast_row(pc, r, slots, mask, h_nodv, &seen, &chosen, &defer);
+    probe_fast_row(pc, r, fp, mask, h_nodv, &seen, &chosen, &defer);
     if (r < pc.n_rows && !defer) sel[r] = chosen;
     const uint64_t m = __ballot(defer);
     if (m) {
@@ -3435,7 +3468,7 @@ __device__ __forceinline__ int probe_file(const int64_t* __restrict__ row0, int 
 // Every checkpoint file of the replay in one launch (rows numbered across files; candidates keep
 // the global row), instead of a launch pair per file: a 64-part checkpoint's 1.56M-row files each
 // fill the chip for only a few microseconds.
-__global__ __launch_bounds__(NT) void k_probe_fast_all(ProbeSet PS, const Slot* __restrict__ slots, uint64_t mask,
+__global__ __launch_bounds__(NT) void k_probe_fast_all(ProbeSet PS, const uint32_t* __restrict__ fp, uint64_t mask,
                                                        uint64_t h_nodv, int32_t* __restrict__ cand,
                                                        unsigned int* __restrict__ cand_n, DState* __restrict__ st) {
   unsigned long long n_seen = 0, n_chosen = 0;
@@ -3448,7 +3481,7 @@ __global__ __launch_bounds__(NT) void k_probe_fast_all(ProbeSet PS, const Slot* 
     if (g < PS.total) {
       f = probe_file(PS.row0, PS.n_files, g);
       r = g - PS.row0[f];
-      probe_fast_row(PS.cols[f], r, slots, mask, h_nodv, &seen, &chosen, &defer);
+      probe_fast_row(PS.cols[f], r, fp, mask, h_nodv, &seen, &chosen, &defer);
       if (!defer) PS.sel[f][r] = chosen;
     }
     const uint64_t m = __ballot(defer);
@@ -3679,25 +3712,25 @@ void launch_table_update(DJsonAction* a, int n, Slot* slots, uint64_t mask, cons
 void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint8_t* sel, DState* st, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, sel, st);
 }
-void launch_probe_all(const ProbeSet& PS, const Slot* slots, uint64_t mask, const DJsonAction* acts,
+void launch_probe_all(const ProbeSet& PS, const Slot* slots, const uint32_t* fp, uint64_t mask, const DJsonAction* acts,
                       const uint8_t* canon, uint32_t seed, uint64_t h_nodv, int32_t* cand, unsigned int* cand_n,
                       DState* st, hipStream_t s) {
   if (!PS.total) return;
   const long long want = (PS.total + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 4096 ? want : 4096);
   hipMemsetAsync(cand_n, 0, sizeof(unsigned int), s);
-  hipLaunchKernelGGL(k_probe_fast_all, dim3(grid), dim3(NT), 0, s, PS, slots, mask, h_nodv, cand, cand_n, st);
+  hipLaunchKernelGGL(k_probe_fast_all, dim3(grid), dim3(NT), 0, s, PS, fp, mask, h_nodv, cand, cand_n, st);
   hipLaunchKernelGGL(k_probe_cand_all, dim3(grid), dim3(NT), 0, s, PS, slots, mask, acts, canon, seed, cand, cand_n, st);
 }
 
-void launch_probe(const ProbeCols& pc, const Slot* slots, uint64_t mask, const DJsonAction* acts,
+void launch_probe(const ProbeCols& pc, const Slot* slots, const uint32_t* fp, uint64_t mask, const DJsonAction* acts,
                   const uint8_t* canon, uint32_t seed, uint64_t h_nodv, uint8_t* sel, int32_t* cand,
                   unsigned int* cand_n, DState* st, hipStream_t s) {
   if (!pc.n_rows) return;
   const long long want = (pc.n_rows + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);   // 256 CUs x 8 workgroups
   hipMemsetAsync(cand_n, 0, sizeof(unsigned int), s);
-  hipLaunchKernelGGL(k_probe_fast, dim3(grid), dim3(NT), 0, s, pc, slots, mask, h_nodv, sel, cand, cand_n, st);
+  hipLaunchKernelGGL(k_probe_fast, dim3(grid), dim3(NT), 0, s, pc, fp, mask, h_nodv, sel, cand, cand_n, st);
   hipLaunchKernelGGL(k_probe_cand, dim3(grid), dim3(NT), 0, s, pc, slots, mask, acts, canon, seed, sel, cand, cand_n, st);
 }
 

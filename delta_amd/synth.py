@@ -330,6 +330,7 @@ def _pm_rows(spec: TableSpec):
     proto = {"minReaderVersion": 3, "minWriterVersion": 7,
              "readerFeatures": ["deletionVectors", "v2Checkpoint"],
              "writerFeatures": ["deletionVectors", "v2Checkpoint"]}
+    proto.update(spec.extra.get("protocol") or {})
     meta = {"id": "6f7a3d1e-2b0c-4c1e-9c4a-5a8e7d9b0c11", "name": None, "description": None,
             "format": {"provider": "parquet", "options": []},
             "schemaString": SCHEMA_STRING, "partitionColumns": ["date"],

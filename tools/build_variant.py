@@ -29,7 +29,9 @@ def main():
         flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-w", "-I", os.path.join(ROOT, "include")]
         flags += os.environ.get("DK_VARIANT_FLAGS", "").split()
         procs, objs = [], []
-        for src in ("dk_host.cpp", "dk_kernels.hip"):
+        sys.path.insert(0, ROOT)
+        from delta_amd.build import SOURCES
+        for src in SOURCES:
             obj = os.path.join(d, src + ".o")
             procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc"] + flags + ["-c", os.path.join(d, src), "-o", obj]))
             objs.append(obj)
