@@ -3455,6 +3455,8 @@ __global__ __launch_bounds__(NT) void k_probe_fast(ProbeCols pc, const uint32_t*
   block_count3(st, n_seen, n_chosen, 0);
 }
 
+constexpr int PROBE_LDS_FILES = 1024;     // k_probe_fast_all keeps the row prefix of this many files in LDS
+
 // file of global row g: the last f with row0[f] <= g (row0 ascending, n + 1 entries)
 __device__ __forceinline__ int probe_file(const int64_t* __restrict__ row0, int n, long long g) {
   int lo = 0, hi = n - 1;
@@ -3471,16 +3473,29 @@ __device__ __forceinline__ int probe_file(const int64_t* __restrict__ row0, int 
 __global__ __launch_bounds__(NT) void k_probe_fast_all(ProbeSet PS, const uint32_t* __restrict__ fp, uint64_t mask,
                                                        uint64_t h_nodv, int32_t* __restrict__ cand,
                                                        unsigned int* __restrict__ cand_n, DState* __restrict__ st) {
+  // the files' row prefix in LDS (the per-row file lookup is a short LDS binary search); a wave
+  // whose 64 rows share one file reads that file's columns through scalar loads
+  __shared__ int64_t srow0[PROBE_LDS_FILES + 1];
+  const bool lds_row0 = PS.n_files <= PROBE_LDS_FILES;
+  if (lds_row0)
+    for (int i = threadIdx.x; i <= PS.n_files; i += blockDim.x) srow0[i] = PS.row0[i];
+  __syncthreads();
+  const int64_t* row0 = lds_row0 ? srow0 : PS.row0;
   unsigned long long n_seen = 0, n_chosen = 0;
   const int lane = threadIdx.x & 63;
   for (long long g0 = (long long)blockIdx.x * blockDim.x; g0 < PS.total; g0 += (long long)gridDim.x * blockDim.x) {
     const long long g = g0 + threadIdx.x;
     bool seen = false, chosen = false, defer = false;
-    int f = 0;
-    long long r = 0;
-    if (g < PS.total) {
-      f = probe_file(PS.row0, PS.n_files, g);
-      r = g - PS.row0[f];
+    const int f = g < PS.total ? probe_file(row0, PS.n_files, g) : 0;
+    const int f0 = __builtin_amdgcn_readfirstlane(f);
+    if (__ballot(g < PS.total && f != f0) == 0) {           // one file for the whole wave
+      const long long r = g - row0[f0];
+      if (g < PS.total) {
+        probe_fast_row(PS.cols[f0], r, fp, mask, h_nodv, &seen, &chosen, &defer);
+        if (!defer) PS.sel[f0][r] = chosen;
+      }
+    } else if (g < PS.total) {
+      const long long r = g - row0[f];
       probe_fast_row(PS.cols[f], r, fp, mask, h_nodv, &seen, &chosen, &defer);
       if (!defer) PS.sel[f][r] = chosen;
     }
