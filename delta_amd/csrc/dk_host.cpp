@@ -648,9 +648,17 @@ static void per_column_tiles(const dk_parquet* p, F&& f) {
 // pages outnumber 8 waves per SIMD of the chip (k_snap_frag waves are LDS-limited to about that).
 static bool snap_page_mode(const dk_parquet* p) {
   static const char* env = getenv("DK_SNAPPY_MODE");
-  if (env && !strcmp(env, "page")) return true;
-  if (env && !strcmp(env, "frag")) return false;
-  return p->n_cpages >= 8192;
+  (void)p;
+  return env && !strcmp(env, "page");
+}
+// Default (hybrid): 64 KiB fragments (k_snap_fix finds their starts from the verified segment
+// entries) decoded with page mode's tag-start bitmap: page mode's discovery with frag mode's load
+// balance -- one wave per 1 MB page left the largest pages as two serial rounds of ~20 ms each on
+// C3. DK_SNAPPY_MODE=page | frag forces the other two.
+static bool snap_hybrid(const dk_parquet* p) {
+  static const char* env = getenv("DK_SNAPPY_MODE");
+  (void)p;
+  return !env || !strcmp(env, "hybrid");
 }
 
 // the decode pipeline (mode: -1 = headers only; 0 = prepare pass through the scans, which size the
@@ -691,7 +699,7 @@ static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
     const bool page_mode = snap_page_mode(p);
     const int nfr = page_mode ? -1 : p->n_frags;
     X.page_mode = page_mode ? 1 : 0;
-    X.tbits = page_mode ? p->d_tbits.as<uint64_t>() : nullptr;
+    X.tbits = (page_mode || snap_hybrid(p)) ? p->d_tbits.as<uint64_t>() : nullptr;
     const int2* wk = page_mode ? p->d_pwork.as<int2>() : p->d_fwork.as<int2>();
     { KTimer::Scope s0(&T, 13, s); launch_snappy(X, p->n_cpages, nfr, wk, 0, s); }
     { KTimer::Scope s1(&T, 19, s); launch_snappy(X, p->n_cpages, nfr, wk, 1, s); }
@@ -869,7 +877,7 @@ static int prepare(dk_parquet* p) {
     // page mode finds tags through a bitmap built by the speculative walk (DK_SNAP_BITS=0: the
     // in-kernel pointer-doubling discovery instead)
     static const bool bits = !getenv("DK_SNAP_BITS") || atoi(getenv("DK_SNAP_BITS")) != 0;
-    if (bits && snap_page_mode(p) && p->d_tbits.alloc(((size_t)p->n_segs * (DK_SNAP_SEG / 64) + 4) * 8)) return 1;
+    if (bits && (snap_page_mode(p) || snap_hybrid(p)) && p->d_tbits.alloc(((size_t)p->n_segs * (DK_SNAP_SEG / 64) + 4) * 8)) return 1;
   }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
   p->bytes_arena = arena_n;

@@ -687,7 +687,7 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
   const GAS uint8_t* gin = gp(in);
   int32_t ws = 0, wb0 = 0;
   // page mode with a tag-start bitmap (k_snap_walk / link / fix): tags are found by bit counting
-  const bool use_bits = X.tbits != nullptr && wk.y < 0;
+  const bool use_bits = X.tbits != nullptr;       // page mode, or fragments of hybrid mode
   const GAS uint32_t* pbits = use_bits ? (const GAS uint32_t*)(X.tbits + (int64_t)X.sbase[wk.x] * (SNAP_SEG / 64)) : nullptr;
   // window = stream bytes [ws, ws + SF_FW), ws 4-byte aligned relative to the buffer; in bitmap mode
   // also the bits of the 64-byte blocks from wb0 = ws rounded down to 64 (dwords of 32 positions)
@@ -746,6 +746,7 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
       if (q < ce) {
         const uint64_t d = ((uint64_t)BW[(rel >> 5) + 1] << 32) | BW[rel >> 5];
         b4 = (uint32_t)(d >> (rel & 31)) & ((1u << SF_CPL) - 1);
+        if (ce - q < SF_CPL) b4 &= (1u << (ce - q)) - 1;   // tags of the next fragment (hybrid mode)
       }
       const int32_t cnt = __popc(b4);
       const int32_t incl = dpp_scan_add(cnt);
