@@ -50,7 +50,10 @@ struct DPage {
 
 // Speculative snappy decode (k_snap_*): compressed streams are cut into DK_SNAP_SEG-byte segments,
 // each walked by one lane; the walker records its first DK_SNAP_REC tag positions.
-constexpr int DK_SNAP_SEG = 2048;
+#ifndef DK_SNAP_SEG_BYTES
+#define DK_SNAP_SEG_BYTES 2048
+#endif
+constexpr int DK_SNAP_SEG = DK_SNAP_SEG_BYTES;
 constexpr int DK_SNAP_REC = 16;
 struct SnapCtx {
   const DChunk* chunks;
