@@ -103,7 +103,10 @@ struct DTile {
   int64_t n_chars;
   int64_t row_base, entry_base, value_base, char_base;
 };
-constexpr int DK_LEVEL_TILE = 2048;
+#ifndef DK_LEVEL_TILE_LEVELS
+#define DK_LEVEL_TILE_LEVELS 2048
+#endif
+constexpr int DK_LEVEL_TILE = DK_LEVEL_TILE_LEVELS;
 
 struct DColumn {
   int32_t first_page, n_pages;   // data pages, contiguous in the page table, in file order

@@ -1518,7 +1518,10 @@ __global__ __launch_bounds__(NT) void k_delta_decode(const DChunk* __restrict__ 
 // --------------------------------------------------------------------------------------------
 constexpr int TL = DK_LEVEL_TILE;
 constexpr int LPT = TL / NT;           // levels per thread
-constexpr int DSTAGE = 8192;          // dictionary bytes staged in LDS by k_tile_decode
+#ifndef DK_DSTAGE_BYTES
+#define DK_DSTAGE_BYTES 8192
+#endif
+constexpr int DSTAGE = DK_DSTAGE_BYTES; // dictionary bytes staged in LDS by k_tile_decode
 
 // lane-serial walk of one hybrid stream's run headers; returns the number of runs, *cover = values
 // covered. strict: the stream must cover `limit` values (levels), else PS_BAD_LEVELS.

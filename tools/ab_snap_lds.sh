@@ -10,6 +10,6 @@ for v in ${VARIANTS:-vA vB vC vD}; do
   python3 -c "import json; d=json.load(open('$OUT/$v.json')); k=d['kernels_us']; print('$v', round(d['ms_per_step'],2), {x: round(k[x]) for x in list(k)[:5]})"
 done
 for v in ${VARIANTS:-vA vB vC vD}; do
-  DK_LIB_PATH=$GRAFT_REPO_ROOT/variants/$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "snappy or v2 or c5 or C3 or c3 or reader" > $OUT/pt_$v.log 2>&1 || { echo "tests $v failed"; tail -20 $OUT/pt_$v.log; exit 1; }
+  DK_LIB_PATH=$GRAFT_REPO_ROOT/variants/$v.so timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "${KEXPR:-snappy or v2 or c5 or C3 or c3 or reader}" > $OUT/pt_$v.log 2>&1 || { echo "tests $v failed"; tail -20 $OUT/pt_$v.log; exit 1; }
   echo "$v tests: $(tail -n 1 $OUT/pt_$v.log)"
 done
