@@ -32,6 +32,7 @@ constexpr int NT = 256;          // threads per workgroup
 #define GAS __attribute__((address_space(1)))
 template <class T> __device__ __forceinline__ GAS T* gp(T* p) { return (GAS T*)p; }
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // --------------------------------------------------------------------------------------------
 // small helpers
@@ -579,6 +580,13 @@ __device__ __forceinline__ int32_t small_mod(int32_t i, int32_t d, uint32_t rcp)
   return i - d * (int32_t)(((uint32_t)i * rcp) >> 16);
 }
 __device__ __forceinline__ uint32_t small_rcp(int32_t d) { return d > 0 ? (65536u + (uint32_t)d - 1) / (uint32_t)d : 0; }
+// the same without a reciprocal operand: float quotient (off by at most one for i, d < 64), fixed up
+__device__ __forceinline__ int32_t small_mod_f(int32_t i, int32_t d) {
+  const int32_t q = (int32_t)((float)i * __builtin_amdgcn_rcpf((float)d));
+  int32_t r = i - q * d;
+  r = r < 0 ? r + d : r;
+  return r >= d ? r - d : r;
+}
 
 // wave64 inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31
 // across rows): VALU only, no LDS round trip
@@ -642,12 +650,22 @@ enum : int32_t { SM_WIN = 0, SM_RING = 1, SM_FAR = 2, SM_DEP = 3, SM_FARQ = 4 };
 // EXP instances take experiment flags (A/B timing, tools/snap_ab.py): SX_* skip parts of the work
 // and SX_NOWRITE keeps the output of a preceding correct launch.
 enum : int { SX_NO_FAR = 1, SX_NO_BYTES = 2, SX_NO_RESOLVE = 4, SX_ONLY_DISCOVERY = 8, SX_NOWRITE = 16 };
+// 5 waves per SIMD (96 VGPRs, a few spilled bytes; the LDS allows 20 waves per CU): the kernel is
+// latency bound per wave, and 4 -> 5 waves took it from 34.0 to 29.5 ms at C3 (profiles/r02/occupancy_ab)
+#ifndef DK_SF_WPE
+#define DK_SF_WPE 5
+#endif
+#if DK_SF_WPE > 0
+#define SF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DK_SF_WPE)))
+#else
+#define SF_WPE_ATTR
+#endif
 template <bool EXP>
-__global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __restrict__ work, int xflags) {
+__global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const int2* __restrict__ work, int xflags) {
   const int xf = EXP ? xflags : 0;
   // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map
   __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX + 16) / 16];
-  __shared__ u32x4 prm[64];                // per-tag (ot, src, mode | per << 8, rcp)
+  __shared__ u32x2 prm[64];                // per-tag (src, (ot - o) | mode << 10 | per << 13)
   __shared__ uint32_t BW[SF_FW / 32 + 4];  // tag-start bits of the window's 64-byte blocks (bitmap mode)
   __shared__ int16_t TP[64];               // bitmap discovery: offsets of the batch's tags
   uint8_t* L = (uint8_t*)lds4;
@@ -978,8 +996,8 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
     SSTAT(4, __popcll(__ballot(valid && is_copy && mode == SM_WIN))); SSTAT(10, __popcll(__ballot(valid && mode == SM_RING)));
     for (int32_t b = lane * 16; b < total; b += 64 * 16) *(uint4*)(M + b) = make_uint4(0, 0, 0, 0);
     if (valid) {
-      prm[lane] = u32x4{(uint32_t)ot, (uint32_t)(mode == SM_WIN ? SNAP_RING + src - ws : src),
-                        (uint32_t)(mode | (per << 8)), small_rcp(per)};
+      prm[lane] = u32x2{(uint32_t)(mode == SM_WIN ? SNAP_RING + src - ws : src),
+                        (uint32_t)((ot - o) | (mode << 10) | (per << 13))};
       if (len > 0) M[ot - o] = (uint8_t)(lane + 1);
     }
     {
@@ -993,26 +1011,25 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
 #pragma unroll
       for (int32_t k = 0; k < SF_CH; k++) mx = max(mx, mb[k]);
       int32_t cur = dpp_shr1(dpp_scan_max(mx));          // owner of this lane's first byte
-      u32x4 q[SF_CH];
+      u32x2 q[SF_CH];
 #pragma unroll
       for (int32_t k = 0; k < SF_CH; k++) {
         if (mb[k]) cur = mb[k];
         q[k] = prm[cur > 0 ? cur - 1 : 0];
       }
-      int32_t sa[SF_CH];                                     // LDS source address, -1 none
-      int32_t ga[SF_CH];                                     // FAR: output offset of the source, -1 none
+      int32_t sa[SF_CH];          // LDS source address (>= 0), FAR: -2 - output offset of the source, -1 none
       bool any_far = false;
 #pragma unroll
       for (int32_t k = 0; k < SF_CH; k++) {
-        sa[k] = -1; ga[k] = -1;
+        sa[k] = -1;
         const int32_t b = b0 + k;
-        const int32_t md = (int32_t)(q[k].z & 0xff);
+        const int32_t md = (int32_t)((q[k].y >> 10) & 7);
         if (k < CH && b < total && md <= SM_FAR) {
-          int32_t i = o + b - (int32_t)q[k].x;
-          const int32_t pr = (int32_t)(q[k].z >> 8);
-          if (pr) i = small_mod(i, pr, q[k].w);
-          if (md == SM_FAR) { ga[k] = (int32_t)q[k].y + i; any_far = true; }
-          else sa[k] = md == SM_WIN ? (int32_t)q[k].y + i : (((int32_t)q[k].y + i) & SF_RM);
+          int32_t i = b - (int32_t)(q[k].y & 1023);
+          const int32_t pr = (int32_t)(q[k].y >> 13);
+          if (pr) i = small_mod_f(i, pr);
+          if (md == SM_FAR) { sa[k] = -2 - ((int32_t)q[k].x + i); any_far = true; }
+          else sa[k] = md == SM_WIN ? (int32_t)q[k].x + i : (((int32_t)q[k].x + i) & SF_RM);
         }
       }
       uint32_t v[SF_CH];
@@ -1025,9 +1042,9 @@ __global__ __launch_bounds__(64) void k_snap_frag_t(SnapCtx X, const int2* __res
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         uint32_t gv[SF_CH];
 #pragma unroll
-        for (int32_t k = 0; k < SF_CH; k++) gv[k] = ga[k] >= 0 ? gout[ga[k]] : 0;
+        for (int32_t k = 0; k < SF_CH; k++) gv[k] = sa[k] <= -2 ? gout[-2 - sa[k]] : 0;
 #pragma unroll
-        for (int32_t k = 0; k < SF_CH; k++) if (ga[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)gv[k];
+        for (int32_t k = 0; k < SF_CH; k++) if (sa[k] <= -2) L[(o + b0 + k) & SF_RM] = (uint8_t)gv[k];
       }
     }
     if (farq) {
