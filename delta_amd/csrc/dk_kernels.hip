@@ -504,8 +504,33 @@ __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
   X.t_exit[k] = tex;
 }
 
+// wave64 inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31
+// across rows): VALU only, no LDS round trip
+__device__ __forceinline__ int32_t dpp_scan_add(int32_t v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+__device__ __forceinline__ int32_t dpp_scan_max(int32_t v) {     // v >= 0
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+__device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets v of lane i-1 (lane 0: 0)
+  return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+}
+
 __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
   const int ci = blockIdx.x, lane = threadIdx.x;
+  __shared__ int16_t TPF[64];               // bitmap boundary walk: offsets of a step's tags
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
   if (!snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
     if (lane == 0) X.serial[ci] = 1;
@@ -552,8 +577,60 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
     running += __shfl(x, 63, 64);
     prev_exit = __shfl(tex, (k1 - base) >= 64 ? 63 : (k1 - base - 1), 64);
     // fragment starts inside this segment: walk from its entry to each 64 KiB output boundary
-    // (page mode decodes whole pages in order and needs none)
-    if (valid && tout > 0 && !X.page_mode) {
+    // (page mode decodes whole pages in order and needs none). With the tag-start bitmap (just
+    // rewritten to the true chain above) the wave walks one boundary at a time, 256 stream bytes per
+    // step: lanes rank the set bits of 4 bytes each, parse up to 64 tags in parallel and scan their
+    // output lengths (a dependent chain per 256 bytes instead of per tag)
+    if (!X.page_mode && X.tbits && !bad) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");     // the bitmap words this wave wrote
+      unsigned long long mb = __ballot(valid && tout > 0 && (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG < ob + tout);
+      while (mb && !bad) {
+        const int L = __ffsll((long long)mb) - 1;
+        mb &= mb - 1;
+        const int64_t obL = __shfl(ob, L, 64);
+        const int32_t toutL = __shfl(tout, L, 64), eL = __shfl(e, L, 64);
+        const int64_t s0 = (int64_t)(base + L - k0) * SNAP_SEG;
+        const int64_t send = s0 + SNAP_SEG < clen ? s0 + SNAP_SEG : clen;
+        const GAS uint64_t* wb = snap_seg_bits(X, base + L);
+        int64_t F = (obL + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG, p = eL, o = obL;
+        while (F < obL + toutL) {
+          const int64_t q = p + 4 * lane;
+          uint32_t b4 = 0;
+          if (q < send) {
+            const int rel = (int)(q - s0), wi = rel >> 6, sh = rel & 63;
+            uint64_t w = wb[wi] >> sh;
+            if (sh > 60 && wi + 1 < SNAP_SEG / 64) w |= wb[wi + 1] << (64 - sh);
+            b4 = (uint32_t)w & 0xfu;
+            if (send - q < 4) b4 &= (1u << (send - q)) - 1u;
+          }
+          const int32_t cnt = __popc(b4), incl = dpp_scan_add(cnt);
+          const int32_t nt = __builtin_amdgcn_readlane(incl, 63);
+          int32_t r0 = incl - cnt;
+          for (int bb = 0; bb < 4; bb++)
+            if ((b4 >> bb) & 1) { if (r0 < 64) TPF[r0] = (int16_t)(4 * lane + bb); r0++; }
+          const int32_t nw = nt < 64 ? nt : 64;
+          const bool intag = lane < nw;
+          const int32_t pos = intag ? (int32_t)TPF[lane] : 0;
+          int32_t adv = 0, len = 0;
+          bool perr = false;
+          if (intag) perr = !snap_parse(in, clen, p + pos, &adv, &len);
+          if (nw == 0 || __builtin_amdgcn_readlane(pos, 0) != 0 || __ballot(perr)) { bad = true; break; }
+          const int32_t oi = dpp_scan_add(len);
+          const int32_t tot = __builtin_amdgcn_readlane(oi, nw - 1);
+          const int64_t pnext = p + __builtin_amdgcn_readlane(pos, nw - 1) + __builtin_amdgcn_readlane(adv, nw - 1);
+          if (o + tot < F) { p = pnext; o += tot; continue; }
+          const unsigned long long hit = __ballot(intag && o + oi - len == F);
+          int64_t pb;
+          if (hit) pb = p + __builtin_amdgcn_readlane(pos, __ffsll((long long)hit) - 1);
+          else if (o + tot == F) pb = pnext;
+          else { bad = true; break; }                  // a tag straddles the boundary
+          const int f = (int)(F / SNAP_FRAG);
+          if (f >= nf) { bad = true; break; }
+          if (lane == 0) X.fstart[f0 + f] = pb;
+          p = pb; o = F; F += SNAP_FRAG;
+        }
+      }
+    } else if (valid && tout > 0 && !X.page_mode) {
       int64_t F = (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG;
       int64_t p = e, o = ob;
       while (F < ob + tout) {
@@ -588,29 +665,6 @@ __device__ __forceinline__ int32_t small_mod_f(int32_t i, int32_t d) {
   return r >= d ? r - d : r;
 }
 
-// wave64 inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31
-// across rows): VALU only, no LDS round trip
-__device__ __forceinline__ int32_t dpp_scan_add(int32_t v) {
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
-  return v;
-}
-__device__ __forceinline__ int32_t dpp_scan_max(int32_t v) {     // v >= 0
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
-  return v;
-}
-__device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets v of lane i-1 (lane 0: 0)
-  return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
-}
 
 __device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
 
