@@ -96,25 +96,42 @@ def interval_ms(text):
 
 
 # ---- CHECKPOINT_SCHEMA as Arrow types -----------------------------------------------------------
+# Field order and nullability follow the reference definitions (paths under kernel-api/.../internal/
+# actions/): SingleAction.CHECKPOINT_SCHEMA (SingleAction.java:30-37), AddFile.FULL_SCHEMA =
+# SCHEMA_WITHOUT_STATS + stats (AddFile.java:42-70), RemoveFile.FULL_SCHEMA (RemoveFile.java:23-38),
+# DeletionVectorDescriptor.READ_SCHEMA (:84-90), Metadata.FULL_SCHEMA (Metadata.java:57-72) with
+# Format.FULL_SCHEMA (Format.java:42-48), Protocol.FULL_SCHEMA (Protocol.java:49-54),
+# SetTransaction.FULL_SCHEMA (SetTransaction.java:28-32), DomainMetadata.FULL_SCHEMA
+# (DomainMetadata.java:34-38). `nullable=False` becomes a REQUIRED Parquet field.
 def checkpoint_schema():
     import pyarrow as pa
-    S, L, B = pa.string(), pa.int64(), pa.bool_()
-    M = pa.map_(S, S)
-    dv = pa.struct([("storageType", S), ("pathOrInlineDv", S), ("offset", pa.int32()), ("sizeInBytes", pa.int32()),
-                    ("cardinality", L)])
-    add = pa.struct([("path", S), ("partitionValues", M), ("size", L), ("modificationTime", L), ("dataChange", B),
-                     ("stats", S), ("tags", M), ("deletionVector", dv), ("baseRowId", L),
-                     ("defaultRowCommitVersion", L)])
-    rm = pa.struct([("path", S), ("deletionTimestamp", L), ("dataChange", B), ("extendedFileMetadata", B),
-                    ("partitionValues", M), ("size", L), ("stats", S), ("tags", M), ("deletionVector", dv),
-                    ("baseRowId", L), ("defaultRowCommitVersion", L)])
-    meta = pa.struct([("id", S), ("name", S), ("description", S),
-                      ("format", pa.struct([("provider", S), ("options", M)])), ("schemaString", S),
-                      ("partitionColumns", pa.list_(S)), ("createdTime", L), ("configuration", M)])
-    proto = pa.struct([("minReaderVersion", pa.int32()), ("minWriterVersion", pa.int32()),
-                       ("readerFeatures", pa.list_(S)), ("writerFeatures", pa.list_(S))])
-    txn = pa.struct([("appId", S), ("version", L), ("lastUpdated", L)])
-    dm = pa.struct([("domain", S), ("configuration", S), ("removed", B)])
+    S, L, B, I = pa.string(), pa.int64(), pa.bool_(), pa.int32()
+
+    def F(name, t, nullable=True):
+        return pa.field(name, t, nullable=nullable)
+
+    def M(value_nullable=True):                 # MapType(string, string, valueContainsNull)
+        return pa.map_(F("key", S, False), F("value", S, value_nullable))
+
+    def A(contains_null):                       # ArrayType(string, containsNull)
+        return pa.list_(F("element", S, contains_null))
+
+    dv = pa.struct([F("storageType", S, False), F("pathOrInlineDv", S, False), F("offset", I),
+                    F("sizeInBytes", I, False), F("cardinality", L, False)])
+    add = pa.struct([F("path", S, False), F("partitionValues", M(), False), F("size", L, False),
+                     F("modificationTime", L, False), F("dataChange", B, False), F("deletionVector", dv),
+                     F("tags", M()), F("baseRowId", L), F("defaultRowCommitVersion", L), F("stats", S)])
+    rm = pa.struct([F("path", S, False), F("deletionTimestamp", L), F("dataChange", B, False),
+                    F("extendedFileMetadata", B), F("partitionValues", M()), F("size", L), F("stats", S),
+                    F("tags", M()), F("deletionVector", dv), F("baseRowId", L), F("defaultRowCommitVersion", L)])
+    fmt = pa.struct([F("provider", S, False), F("options", M(False))])
+    meta = pa.struct([F("id", S, False), F("name", S), F("description", S), F("format", fmt, False),
+                      F("schemaString", S, False), F("partitionColumns", A(False), False), F("createdTime", L),
+                      F("configuration", M(False), False)])
+    proto = pa.struct([F("minReaderVersion", I, False), F("minWriterVersion", I, False),
+                       F("readerFeatures", A(False)), F("writerFeatures", A(False))])
+    txn = pa.struct([F("appId", S, False), F("version", L, False), F("lastUpdated", L)])
+    dm = pa.struct([F("domain", S, False), F("configuration", S, False), F("removed", B, False)])
     return pa.schema([("txn", txn), ("add", add), ("remove", rm), ("metaData", meta), ("protocol", proto),
                       ("domainMetadata", dm)])
 
@@ -169,7 +186,11 @@ def _add_from_cols(d, r):
     g = d.get
     dv = None
     st = g("add.deletionVector.storageType")
-    if st is not None and st.present and st.row_def[r] >= 3:
+    # the deletionVector struct is defined iff the level reaches the struct's own (optional add = 1,
+    # optional deletionVector = 2), whether storageType itself is optional (max_def 3) or required
+    # (max_def 2, DeletionVectorDescriptor.READ_SCHEMA marks it non-nullable); RowColumnReader
+    # starts the struct exactly then (RowColumnReader.java:65-173)
+    if st is not None and st.present and st.row_def[r] >= 2:
         dv = {"storageType": _s(st, r), "pathOrInlineDv": _s(g("add.deletionVector.pathOrInlineDv"), r),
               "offset": _f(g("add.deletionVector.offset"), r, np.int32),
               "sizeInBytes": _f(g("add.deletionVector.sizeInBytes"), r, np.int32),
@@ -248,7 +269,15 @@ def checkpoint_actions(engine, snapshot, now_ms=None):
         row = 0
         for d in reversed(snapshot.log_segment.deltas):
             with open(d.path, "rb") as f:
-                lines = f.read().decode("utf-8", "replace").splitlines()
+                raw = f.read()
+            # one row per line as the tail parser splits them (BufferedReader.readLine: '\n', '\r'
+            # or '\r\n' ends a line), so row indices line up with the tail selection; other
+            # separators str.splitlines() would honour (U+2028, U+0085, ...) may sit inside JSON
+            # strings
+            text = raw.decode("utf-8", "replace")
+            lines = re.split(r"\r\n|\r|\n", text)
+            if lines and lines[-1] == "":
+                lines.pop()
             for line in lines:
                 obj = json.loads(line)
                 r, row = row, row + 1

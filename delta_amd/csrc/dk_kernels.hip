@@ -700,6 +700,10 @@ constexpr int SF_CPL = DK_SF_CPL;          // bitmap discovery: candidate stream
 static_assert(SF_CPL * 64 + 69 <= DK_SF_MARGIN, "the discovery window must stay inside the LDS copy");
 constexpr int SF_RM = SNAP_RING - 1;
 enum : int32_t { SM_WIN = 0, SM_RING = 1, SM_FAR = 2, SM_DEP = 3, SM_FARQ = 4 };
+// k_snap_frag packs a tag's output offset inside the batch (< SF_BMAX) into 10 bits and its mode
+// into the next 3 (prm[].y): both must fit
+static_assert(SF_BMAX <= 1024, "DK_SF_BOUT too large: batch offsets are packed in 10 bits");
+static_assert(SM_FARQ < 8, "snappy tag modes are packed in 3 bits");
 
 // EXP instances take experiment flags (A/B timing, tools/snap_ab.py): SX_* skip parts of the work
 // and SX_NOWRITE keeps the output of a preceding correct launch.
