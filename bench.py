@@ -2,28 +2,38 @@
 
 BASELINE.json's metric is quoted at 100M AddFile: configs[2] (C3) = a 100M-AddFile
 64-part snappy checkpoint + 1k JSON commits (100 adds + 100 removes each, re-adds and duplicates),
-read schema add(without stats) + remove. It fits one MI355X (≈40 GB of HBM), so N=1 runs all of it.
+read schema add(without stats) + remove. It fits one MI355X, so N=1 runs all of it.
 
-Three timed regions:
-  1. `value`: one "step" = the device half of Scan.getScanFiles over inputs already resident in HBM
-     (commit-tail key build + probe table, page-header parse, snappy, level/value decode of every
-     projected add/remove leaf, URI-canonical key hashing, probe, selection, ScanMetrics counters).
-     value = (checkpoint rows + tail rows) x steps / wall time between barriers.
-  2. `end_to_end`: getScanFiles until fully consumed, as BenchmarkParallelCheckpointReading.java:
-     110-139 consumes it (iterate the selected rows, sum add.size): host file read + H2D + decode +
-     reconcile + D2H of the selection and add.size; actions/s = addFilesSeen / that wall time
-     (BASELINE.md "Metric definitions"). `jmh_op_ms` adds the snapshot load, as the JMH op does.
-  3. `snapshot_load_ms`: Table.forPath(...).getLatestSnapshot (cold and warm).
+`value` is BASELINE.md's metric ("Metric definitions"): actions/s = ScanMetrics.numAddFilesSeen ÷
+getScanFiles wall time until fully consumed. One timed "step" = one getScanFiles over the table, as
+BenchmarkParallelCheckpointReading.java:110-139 runs it: a fresh scan on the loaded snapshot, host
+read of the projected column chunks, H2D, device decode + reconcile, D2H of the selection and of
+add.size, and the consumer summing add.size over the selected rows. The other regions are reported
+beside it:
+  device_step       the device half of getScanFiles over inputs already resident in HBM (commit-tail
+                    keys + table, page headers, snappy, level/value decode of every projected leaf,
+                    URI-canonical key hashes, probe, selection, counters); the roofline is measured
+                    here, per kernel, with HIP events on the replay stream;
+  snapshot_load_ms  Table.forPath(...).getLatestSnapshot (cold, warm, and with a .crc).
 
-Multi-GPU (one process per GPU): C3 is one table sharded over the ranks by checkpoint row groups
-(delta_amd/shard.py, strong scaling); each step ends with the exchange that assembles the result --
-ScanMetrics counters and the selection bitmaps of every shard, packed on the GPU and all-gathered over
-RCCL. The other configs give every rank its own table (weak scaling, no collective).
+Multi-GPU, one process per GPU over RCCL: `python bench.py --gpus N` starts N ranks itself (a
+parent that never touches the GPU spawns N children with RANK / LOCAL_RANK / WORLD_SIZE), or the
+driver's `torch.distributed.run --nproc-per-node N bench.py --gpus N` does. C3 is ONE table whose
+checkpoint row groups are cut into N contiguous runs (delta_amd/shard.py): each rank reads, decodes
+and reconciles its run against the whole (replicated) commit tail and consumes its own scan files;
+counters and consumer sums are all-reduced. The device-step region ends with the exchange that puts
+every rank's counters and packed selection bitmaps on rank 0 in one RCCL all-gather into one device
+buffer (shard.SelectionExchange), timed separately as `exchange_ms`.
+
+`--dry-run`: no GPU; the launcher, the row-group planning and the exchange run over gloo on the CPU
+with placeholder selections (tests/test_bench_launcher.py).
 """
 import argparse
 import json
 import os
 import shutil
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -32,6 +42,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
+METRIC = "checkpoint actions reconciled/sec (node) + snapshot load ms, 100M AddFile"
+REMOVE_LEAVES = ["remove.path", "remove.deletionVector.storageType", "remove.deletionVector.pathOrInlineDv",
+                 "remove.deletionVector.offset", "remove.deletionVector.sizeInBytes",
+                 "remove.deletionVector.cardinality"]
 
 
 def log(*a):
@@ -54,11 +68,11 @@ CONFIGS = {
                          removes_per_commit=100, readd_frac=0.1, dup_frac=0.05),
                desc="C3: %d-AddFile 64-part snappy checkpoint (row groups sharded over the GPUs) + 1k JSON commits "
                     "(100 adds + 100 removes each, 10%% re-adds, 5%% duplicates); read schema add(no stats)+remove"),
-    "c4": dict(rows=50_000_000, shared=False, stats=True, predicate=("id", ">", 25_000_000),
-               spec=dict(n_parts=8, dv_frac=0.3, with_stats=True, n_commits=100, adds_per_commit=50,
-                         removes_per_commit=50),
-               desc="C4: %d-AddFile 8-part checkpoint per GPU, 30%% with deletion vectors, predicate id > 25000000 "
-                    "over stats; read schema add(with stats)+remove"),
+    "c4": dict(rows=50_000_000, shared=True, stats=True, predicate=("id", ">", 25_000_000),
+               spec=dict(n_parts=8, dv_frac=0.3, with_stats=True, with_stats_parsed=True, n_commits=100,
+                         adds_per_commit=50, removes_per_commit=50),
+               desc="C4: %d-AddFile 8-part checkpoint (row groups sharded over the GPUs), 30%% with deletion "
+                    "vectors, predicate id > 25000000 over stats_parsed; read schema add(with stats)+remove"),
     "c5": dict(rows=10_000_000, shared=True, stats=False, predicate=None,
                spec=dict(n_parts=16, v2_sidecars=16, compression="snappy", data_page_version="2.0",
                          delta_binary_packed=True, hot_frac=0.6, n_commits=100, adds_per_commit=50,
@@ -84,8 +98,8 @@ def make_table(root, rows, seed, compression, cfg):
 
 def pmc_traffic(kernel, rows, compression):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of the same workload
-    (tools/pmc.sh + tools/pmc_summary.py --json: separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE
-    doubled for gfx950's half-count of wide loads, KB -> bytes), or None when no profile matches."""
+    (tools/pmc.sh + tools/pmc_summary.py --json: separate FETCH_SIZE / WRITE_SIZE passes, KB -> bytes,
+    FETCH_SIZE doubled only for kernels calibrated as 16 B/lane streaming readers), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
@@ -98,16 +112,68 @@ def pmc_traffic(kernel, rows, compression):
     return None
 
 
-def cpu_baseline(files, with_stats, threads, reps_single=2):
-    """The oracle (plain C restatement of parquet-mr decode + URI keys + probe, oracle/dk_ref.c) on a
-    bounded sample of the same workload: whole checkpoint parts of the bench table, decoded (every
-    projected leaf), keyed and probed. Single thread over `reps_single` parts, then `threads` threads
-    with one part each (ctypes releases the GIL inside the C decoder)."""
-    import concurrent.futures as cf
+# ------------------------------------------------------------------------------------------------
+# launcher: N ranks from one command, before anything touches the GPU
+# ------------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv):
+    """Parent of an N-rank run: starts N fresh child processes of this script (one per GPU) with
+    the torch.distributed environment and returns the worst exit code. It imports nothing that
+    initialises HIP; children are started, never exec'd into."""
+    n = args.gpus
+    env0 = dict(os.environ)
+    env0.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), DK_BENCH_CHILD="1")
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                c = p.poll()
+                if c is None:
+                    continue
+                procs.remove(p)
+                if c != 0:
+                    rc = rc or c
+                    for q in procs:            # one rank failed: the others would wait forever
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline + full-size parity (the oracle: test infrastructure, used here only as the checker
+# and the reported CPU baseline)
+# ------------------------------------------------------------------------------------------------
+def cpu_baseline(work, files, with_stats, threads, reps_single=2, got=None):
+    """The oracle (oracle/dk_ref.c: parquet-mr decode of every projected leaf + java.net.URI keys +
+    probe; oracle/ref.py: commit-tail replay) on the bench table.
+
+    1 thread: `reps_single` whole checkpoint parts probed against the real tail key set.
+    `threads` threads: the WHOLE table (tail + every part, one part per task) -- this run is also
+    the full-size parity check: its five counters and every checkpoint row's selection bit are
+    compared with the GPU's (`got`)."""
+    import concurrent.futures as cf  # noqa: F401
+    import numpy as np
     from oracle import ref
-    leaves = ref.ADD_LEAVES + (["add.stats"] if with_stats else []) + [
-        "remove.path", "remove.deletionVector.storageType", "remove.deletionVector.pathOrInlineDv",
-        "remove.deletionVector.offset", "remove.deletionVector.sizeInBytes", "remove.deletionVector.cardinality"]
+    ref.lib()
+    out = {"unit": "actions/s", "kind": "port"}
+    # single thread over a sample: decode + key + probe against an empty key set of the same shape
+    # (the probe cost is dominated by the key build, not the table)
+    leaves = ref.ADD_LEAVES + (["add.stats"] if with_stats else []) + REMOVE_LEAVES
 
     def one(path):
         pf = ref.ParquetFile.open(path)
@@ -117,22 +183,36 @@ def cpu_baseline(files, with_stats, threads, reps_single=2):
         ref.lib().dkr_keyset_free(ks)
         return pf.num_rows
 
-    ref.lib()
     sample = files[:max(1, reps_single)]
     t0 = time.perf_counter()
     n1 = sum(one(p) for p in sample)
     v1 = n1 / (time.perf_counter() - t0)
-    out = {"value": v1, "unit": "actions/s", "cores": 1, "kind": "port",
-           "sample": "%d checkpoint part(s) of the bench table (%d rows): decode of %d leaves + URI key + probe, "
-                     "oracle/dk_ref.c (CPU restatement, not DefaultEngine)" % (len(sample), n1, len(leaves))}
-    if threads > 1 and len(files) > 1:
-        par = [files[i % len(files)] for i in range(threads)]
+    out.update(value=v1, cores=1,
+               sample="%d checkpoint part(s) of the bench table (%d rows): decode of %d leaves + URI key + probe, "
+                      "oracle/dk_ref.c (CPU restatement, not DefaultEngine)" % (len(sample), n1, len(leaves)))
+    if threads > 1:
         t0 = time.perf_counter()
-        with cf.ThreadPoolExecutor(threads) as ex:
-            nT = sum(ex.map(one, par))
-        vT = nT / (time.perf_counter() - t0)
-        out["threads"] = {"value": vT, "unit": "actions/s", "cores": threads,
-                          "sample": "%d parts on %d threads (%d rows)" % (len(par), threads, nT)}
+        res = ref.replay(work, with_stats=with_stats, threads=threads, keep_cols=False,
+                         extra_leaves=REMOVE_LEAVES)
+        dt = time.perf_counter() - t0
+        seen = res.counters.addFilesSeen
+        full = {"value": seen / dt, "unit": "actions/s", "cores": threads, "seconds": dt,
+                "sample": "the whole table: commit-tail replay (Python) + %d parts decoded and probed on %d threads"
+                          % (len(res.checkpoint), threads)}
+        out["threads"] = full
+        if got is not None:
+            counters, tail_paths, bits = got
+            oc = res.counters.as_tuple()
+            bad = [i for i, b in enumerate(res.checkpoint)
+                   if not np.array_equal(np.packbits(b.selected.astype(bool), bitorder="little"), bits[i])]
+            otail = [a["path"] for a in res.json_rows]
+            out["parity"] = {"counters_gpu": list(counters), "counters_oracle": list(oc),
+                             "counters_match": tuple(counters) == tuple(oc),
+                             "tail_selected_match": tail_paths == otail, "tail_selected": len(otail),
+                             "checkpoint_files": len(res.checkpoint),
+                             "checkpoint_rows": int(sum(b.n_rows for b in res.checkpoint)),
+                             "checkpoint_bits_match": not bad and len(bits) == len(res.checkpoint),
+                             "mismatched_files": bad[:8]}
     return out
 
 
@@ -144,9 +224,59 @@ def wait_for(marker, timeout_s):
         time.sleep(0.5)
 
 
-def main():
+def dry_run(args, cfg, work, world, rank):
+    """CPU rehearsal of the multi-rank path over gloo: launcher, planning (shard.plan_units over the
+    checkpoint footers, read by the product's host footer parser) and the one-collective exchange with
+    placeholder selections (bit = row parity). Rank 0 checks every checkpoint row came back exactly
+    once, in replay order."""
+    import numpy as np
+    import torch.distributed as dist
+    from delta_amd import kernel as K
+    from delta_amd import shard
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+    seg = K.build_log_segment(work)
+    files = [f.path for f in sorted(seg.checkpoints, key=lambda f: os.path.basename(f.path), reverse=True)]
+    rg = [K.row_group_rows(f) for f in files]
+    units = shard.plan_units(rg, world, rank)
+    meta = shard.unit_layout(rg, units)
+    ex = shard.SelectionExchange(meta)
+
+    def write_bits(i, dst):
+        f, r0, n = meta[i]
+        rows = np.arange(r0, r0 + n)
+        dst.copy_(__import__("torch").from_numpy(np.packbits((rows % 2 == 0), bitorder="little")))
+
+    t0 = time.perf_counter()
+    res = ex.exchange([0] * 5, [sum(n for _, _, n in meta)] + [0] * 4, write_bits)
+    dt = time.perf_counter() - t0
+    ok = None
+    if rank == 0:
+        counters, sels = res
+        total = sum(sum(r) for r in rg)
+        cover = {}
+        for f, r0, n, bits in sels:
+            want = np.packbits(np.arange(r0, r0 + n) % 2 == 0, bitorder="little")
+            assert np.array_equal(bits, want), (f, r0)
+            cover.setdefault(f, []).append((r0, n))
+        for f, rs in cover.items():
+            rs.sort()
+            assert rs[0][0] == 0 and all(a[0] + a[1] == b[0] for a, b in zip(rs, rs[1:])), f
+            assert rs[-1][0] + rs[-1][1] == sum(rg[f])
+        ok = counters[0] == total and len(cover) == len(files)
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "actions/s", "n_gpus": world,
+                          "dry_run": True, "backend": dist.get_backend(), "ranks": dist.get_world_size(),
+                          "checkpoint_files": len(files), "checkpoint_rows": total, "units": len(sels),
+                          "exchange_ms": dt * 1e3, "ok": bool(ok)}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    return 0 if (rank != 0 or ok) else 1
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
@@ -154,12 +284,19 @@ def main():
     ap.add_argument("--compression", default=None, help="override the config's codec")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--e2e-reps", type=int, default=2)
+    ap.add_argument("--device-steps", type=int, default=None, help="timed device-only steps (default: --steps)")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of launcher + planning + exchange")
     ap.add_argument("--workdir", default=None)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if args.gpus is None:
+        args.gpus = env_world or 1
+    if args.gpus > 1 and env_world == 0:
+        return launch(args, argv)               # the parent: spawn one child per GPU, touch nothing
+    world = env_world or 1
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     cfg = CONFIGS[args.config]
@@ -183,12 +320,23 @@ def main():
     else:
         wait_for(marker, 1800)
 
+    if args.dry_run:
+        rc = dry_run(args, cfg, work, world, rank)
+        if not args.workdir and rank == 0:
+            shutil.rmtree(work, ignore_errors=True)
+        return rc
+
+    import numpy as np
     dist = None
+    backend = None
     if world > 1:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        backend = dist.get_backend()
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: RCCL world is %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
 
     from delta_amd import kernel as K
 
@@ -198,38 +346,37 @@ def main():
             dist.barrier()
             torch.cuda.synchronize()
 
-    def max_over_ranks(x):
+    def reduce_over_ranks(xs, op):
         if dist is None:
-            return x
+            return list(xs)
         import torch
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
+        t = torch.tensor(list(xs), dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=op)
+        return [float(v) for v in t.cpu().tolist()]
 
-    def sum_over_ranks(x):
-        if dist is None:
-            return x
-        import torch
-        t = torch.tensor([x], dtype=torch.int64, device="cuda")
-        dist.all_reduce(t)
-        return int(t.item())
+    def max_over_ranks(x):
+        return reduce_over_ranks([x], dist.ReduceOp.MAX if dist else None)[0]
+
+    def sum_over_ranks(xs):
+        return [int(round(v)) for v in reduce_over_ranks(xs, dist.ReduceOp.SUM if dist else None)]
 
     eng = K.GpuEngine(device=local if world > 1 else 0, timing=True)
-    # 3. snapshot load: the first (cold: code-object load, first allocations) and the median of 5
-    # warm loads, as the reference's JMH harness measures after warm-up iterations
+
+    # ---- region 3: snapshot load (cold: code-object load + first allocations; warm: median of 5) ----
     t0 = time.perf_counter()
     snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
     snapshot_cold_ms = (time.perf_counter() - t0) * 1e3
+    cold_phases = {k: round(v, 3) for k, v in snap.load_ms.items()}
     warm = []
     for _ in range(5):
         t0 = time.perf_counter()
         snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
         warm.append((time.perf_counter() - t0) * 1e3)
     snapshot_ms = sorted(warm)[len(warm) // 2]
-    # the same snapshot load with a Spark-style checksum file at the snapshot version (Spark writes
-    # one per commit; ChecksumReader.getCRCInfo then answers the P&M pass alone)
     snapshot_crc_ms = None
-    if world == 1 or not cfg["shared"]:
+    if rank == 0 and (world == 1 or not cfg["shared"]):
+        # with a Spark-style checksum file at the snapshot version (ChecksumReader.getCRCInfo then
+        # answers the P&M pass alone)
         from delta_amd import synth
         crc = synth.write_crc(work, snap.getVersion())
         try:
@@ -252,7 +399,7 @@ def main():
             sb = sb.withShard(world, rank)
         return sb.build()
 
-    # 1. device steps
+    # ---- region 1: the device step over inputs resident in HBM (roofline) ----
     scan = build_scan(snap)
     t0 = time.perf_counter()
     scan.prepare(eng)
@@ -260,49 +407,57 @@ def main():
     n_ckpt_rows = sum(scan.ckpt.num_rows(i) for i in range(len(scan.ckpt_files))) if scan.ckpt else 0
     n_tail = int(scan.tail.rows)
     bytes_read, bytes_written = scan.ckpt.traffic() if scan.ckpt else (0, 0)
+    exchange = None
+    if dist is not None and cfg["shared"]:
+        from delta_amd import shard
+        meta = [(scan.ckpt_index[fi], scan.ckpt.row_offset(fi), scan.ckpt.num_rows(fi))
+                for fi in range(len(scan.ckpt_files or []))]
+        exchange = shard.SelectionExchange(meta, device="cuda")
+    ex_ms = []
     merged = None
 
-    def step():
+    def device_step():
         nonlocal merged
         scan.run()
         scan.sync()
-        if dist is not None and cfg["shared"]:
-            # the exchange: ScanMetrics counters and every shard's selection bitmap (packed on the
-            # GPU) all-gathered over RCCL; row data stays on the GPU that decoded it
-            from delta_amd import shard
-            merged = shard.gather_selections(shard.scan_units(scan, device_bits=True), scan.tail_metrics.as_tuple(),
-                                             scan.ckpt_metrics.as_tuple(), device="cuda")
+        if exchange is not None:
+            import ctypes as C
+            import torch
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            offs = (C.c_int64 * max(1, len(exchange.slots)))(*[off for off, _ in exchange.slots])
 
+            def write_all(i, dst):
+                if i == 0:   # every file of this rank in one call, straight into the collective buffer
+                    base = exchange.buf.data_ptr()
+                    K.check(K.lib().dk_replay_ckpt_selection_bits_all(scan._rh, C.c_void_p(base), offs, 1))
+            merged = exchange.exchange(scan.tail_metrics.as_tuple(), scan.ckpt_metrics.as_tuple(), write_all)
+            torch.cuda.synchronize()
+            ex_ms.append((time.perf_counter() - te) * 1e3)
+
+    dsteps = args.device_steps if args.device_steps is not None else args.steps
     for _ in range(args.warmup):
-        step()
-    counters = merged[0] if merged else scan.metrics.as_tuple()
+        device_step()
+    device_counters = merged[0] if merged else scan.metrics.as_tuple()
     barrier()
     stats0 = scan.kernel_stats()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for _ in range(dsteps):
+        device_step()
     barrier()
-    elapsed = max_over_ranks(time.perf_counter() - t0)
+    dev_elapsed = max_over_ranks(time.perf_counter() - t0)
     stats1 = scan.kernel_stats()
-
-    # per-kernel averages over the timed steps only
     kern = {}
     for name, (avg1, c1) in stats1.items():
         avg0, c0 = stats0.get(name, (0.0, 0))
         if c1 > c0:
             kern[name] = (avg1 * c1 - avg0 * c0) / (c1 - c0)
     step_us = kern.pop("step_total", None)
-    if cfg["shared"]:
-        units = sum_over_ranks(n_ckpt_rows) + n_tail      # every rank replays the whole tail
-    else:
-        units = (n_ckpt_rows + n_tail) * world
-    value = units * args.steps / elapsed
-    ms_per_step = elapsed / args.steps * 1e3
     dom = max(kern.items(), key=lambda kv: kv[1]) if kern else ("none", 0.0)
     step_bytes = bytes_read + bytes_written
     step_gbs = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
-    # roofline of the dominant kernel that has a byte model (dk_parquet_kernel_traffic):
-    # algorithmic bytes of one launch / its average launch time (HIP events, engine stream)
+    # roofline of the dominant kernel with a byte model (dk_parquet_kernel_traffic):
+    # algorithmic bytes of one launch / its average launch time (HIP events on the replay stream)
     modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy") if k in kern]
     rk = max(modelled, key=lambda k: kern[k]) if modelled else None
     k_read, k_written = scan.ckpt.kernel_traffic(rk) if rk else (0, 0)
@@ -310,56 +465,71 @@ def main():
     achieved = k_bytes / (kern[rk] * 1e-6) / 1e9 if rk else None
     pmc = pmc_traffic(rk, n_ckpt_rows, compression) if rk else None
     ckpt_files = list(scan.ckpt_files)
+    if cfg["shared"]:
+        dev_units = sum_over_ranks([n_ckpt_rows])[0] + n_tail      # the tail is replicated, counted once
+    else:
+        dev_units = sum_over_ranks([n_ckpt_rows + n_tail])[0]
     scan.close()
 
-    # 2. end to end: getScanFiles until consumed (the JMH consumer sums add.size of selected rows)
-    e2e = None
-    if not args.no_e2e:
-        runs = []
-        for _ in range(args.e2e_reps):
-            barrier()
-            t_a = time.perf_counter()
-            s2 = K.Table.forPath(eng, work).getLatestSnapshot(eng)
-            t_b = time.perf_counter()
-            sc2 = build_scan(s2)
-            size_sum, n_sel = 0, 0
-            t_p = t_r = None
-            it = sc2.getScanFiles(eng)      # prepare (host read + H2D) + device step + counters
-            t_r = time.perf_counter()
-            import numpy as np
-            for b in it:
-                # the JMH consumer (BenchmarkParallelCheckpointReading.java:124-135): sum add.size
-                # over the selected rows
-                col = b.data["add.size"]
-                v = col.fixed.view("<i8")
-                if b.selection is None:
-                    size_sum += int(v.sum())
-                    n_sel += b.size
+    # ---- the headline: getScanFiles until fully consumed ----
+    capture = {}
+
+    def e2e_step(capture_result=False):
+        """One getScanFiles on the loaded snapshot, consumed as the JMH benchmark consumes it
+        (BenchmarkParallelCheckpointReading.java:124-135: sum add.size over the selected rows)."""
+        sc = build_scan(snap)
+        size_sum, n_sel = 0, 0
+        tail_paths, bits = [], []
+        it = sc.getScanFiles(eng)
+        t_c = time.perf_counter()
+        for b in it:
+            v = b.data["add.size"].fixed.view("<i8")
+            if b.selection is None:
+                size_sum += int(v.sum())
+                n_sel += b.size
+            else:
+                # sum over the selected rows = all rows minus the (few) unselected ones
+                uns = np.flatnonzero(~b.selection)
+                size_sum += int(v.sum()) - int(v[uns].sum())
+                n_sel += b.size - len(uns)
+            if capture_result:
+                if b.file_index < 0:
+                    pc = b.data["add.path"]
+                    tail_paths = [pc.string(int(r)).decode("utf-8", "replace") for r in b.selected_rows()]
                 else:
-                    size_sum += int(np.add.reduce(v, where=b.selection))
-                    n_sel += int(np.count_nonzero(b.selection))
-            t_c = time.perf_counter()
-            seen = sc2.metrics.addFilesSeen
-            prep_ms = {k: round(v, 2) for k, v in sc2.prepare_ms.items()}
-            sc2.close()
-            runs.append((t_c - t_b, t_b - t_a, seen, n_sel, size_sum, t_r - t_b, t_c - t_r))
-        gsf_s, snap_s, seen, n_sel, size_sum, open_run_s, consume_s = min(runs)
-        gsf_s = max_over_ranks(gsf_s)
-        snap_s = max_over_ranks(snap_s)
-        seen_all = sum_over_ranks(seen) - (world - 1) * (n_tail and scan.tail_metrics.addFilesSeen) \
-            if cfg["shared"] else sum_over_ranks(seen)
-        e2e = {"getScanFiles_ms": gsf_s * 1e3, "snapshot_load_ms": snap_s * 1e3,
-               "jmh_op_ms": (gsf_s + snap_s) * 1e3,
-               "actions_per_s": seen_all / gsf_s, "jmh_op_actions_per_s": seen_all / (gsf_s + snap_s),
-               "addFilesSeen": seen_all, "selected_rows_rank0": n_sel, "size_sum_rank0": size_sum,
-               "phases_ms": {"prepare_and_device_step": open_run_s * 1e3, "consume": consume_s * 1e3,
-                             "prepare": dict(prep_ms)},
-               "reps": args.e2e_reps,
-               "includes": "host read of the projected column chunks + H2D + device decode/reconcile + "
-                           "D2H of selection and add.size + host sum over selected rows"}
+                    sel = np.ones(b.size, bool) if b.selection is None else b.selection
+                    bits.append(np.packbits(sel, bitorder="little"))
+        consume_ms = (time.perf_counter() - t_c) * 1e3
+        seen = sc.metrics.addFilesSeen if not (cfg["shared"] and world > 1 and rank > 0) \
+            else sc.ckpt_metrics.addFilesSeen                  # the replicated tail counts once
+        if capture_result:
+            capture.update(counters=sc.metrics.as_tuple(), tail_paths=tail_paths, bits=bits)
+        phases = dict(sc.prepare_ms)
+        phases["consume"] = consume_ms
+        sc.close()
+        return seen, n_sel, size_sum, phases
+
+    for i in range(args.warmup):
+        e2e_step(capture_result=(i == 0 and world == 1))
+    barrier()
+    t0 = time.perf_counter()
+    seen_tot = sel_tot = size_tot = 0
+    phase_sum = {}
+    for _ in range(args.steps):
+        seen, n_sel, size_sum, phases = e2e_step()
+        seen_tot += seen
+        sel_tot += n_sel
+        size_tot += size_sum
+        for k, v in phases.items():
+            phase_sum[k] = phase_sum.get(k, 0.0) + v
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0)
+    seen_all, sel_all, size_all = sum_over_ranks([seen_tot, sel_tot, size_tot])
+    value = seen_all / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
 
     result = {
-        "metric": "checkpoint actions reconciled/sec (node) + snapshot load ms, 100M AddFile",
+        "metric": METRIC,
         "value": value,
         "unit": "actions/s",
         "n_gpus": world,
@@ -371,20 +541,29 @@ def main():
         "vs_baseline": None,
         "dtype": "u8/int64",
         "data": "synthetic (seed 20250218; delta_amd/synth.py)",
-        "config": {"workload": cfg["desc"] % rows, "name": args.config,
-                   "compression": compression,
-                   "parallelism": ("strong: checkpoint row groups in %d contiguous runs (one per GPU), tail on every "
-                                   "GPU, counters + selection bitmaps all-gathered over RCCL each step" % world
-                                   if cfg["shared"] else "weak: one table per GPU"),
+        "config": {"workload": cfg["desc"] % rows, "name": args.config, "compression": compression,
+                   "parallelism": ("strong: checkpoint row groups in %d contiguous runs (one per GPU), commit tail "
+                                   "on every GPU; device step ends with one RCCL all-gather of counters + "
+                                   "selection bitmaps" % world if cfg["shared"] else "weak: one table per GPU"),
                    "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail,
                    "checkpoint_files_per_gpu": len(ckpt_files)},
+        "value_definition": "ScanMetrics.numAddFilesSeen / getScanFiles wall time until fully consumed "
+                            "(BASELINE.md), summed over ranks / max-over-ranks time of the K timed steps",
+        "ranks": world, "backend": backend or "none (1 process)",
+        "rccl_ranks": (dist.get_world_size() if dist is not None else None),
+        "addFilesSeen_per_step": seen_all // args.steps, "selected_per_step": sel_all // args.steps,
+        "size_sum_per_step": size_all // args.steps,
+        "getScanFiles_phases_ms": {k: round(v / args.steps, 2) for k, v in phase_sum.items()},
+        "device_step": {"ms": dev_elapsed / max(1, dsteps) * 1e3, "steps": dsteps,
+                        "actions_per_s": dev_units * dsteps / dev_elapsed if dev_elapsed else None,
+                        "counters": list(device_counters),
+                        "exchange_ms": (sorted(ex_ms)[len(ex_ms) // 2] if ex_ms else None),
+                        "prepare_s": prepare_s},
         "snapshot_load_ms": snapshot_ms,
         "snapshot_load_cold_ms": snapshot_cold_ms,
+        "snapshot_load_cold_phases_ms": cold_phases,
         "snapshot_load_with_crc_ms": snapshot_crc_ms,
         "snapshot_load_phases_ms": {k: round(v, 3) for k, v in snap.load_ms.items()},
-        "end_to_end": e2e,
-        "prepare_s": prepare_s,
-        "counters": counters,
         "kernels_us": {k: round(v, 2) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])},
         "roofline": {"bound": "hbm", "kernel": rk, "kernel_us": kern.get(rk),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -398,7 +577,10 @@ def main():
                               "frac": (step_gbs / HBM_PEAK_GBS) if step_gbs else None}},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        result["cpu_baseline"] = cpu_baseline(ckpt_files, cfg["stats"], args.cpu_threads)
+        got = (capture["counters"], capture["tail_paths"], capture["bits"]) if capture else None
+        result["cpu_baseline"] = cpu_baseline(work, ckpt_files, cfg["stats"], args.cpu_threads, got=got) \
+            if not cfg["predicate"] else None
+        result["cpu_baseline_host"] = {"nproc": os.cpu_count(), "cpu": _cpu_model()}
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
@@ -408,7 +590,19 @@ def main():
         shutil.rmtree(work, ignore_errors=True)
     if dist is not None:
         dist.destroy_process_group()
+    return 0
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

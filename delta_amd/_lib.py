@@ -82,7 +82,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_parquet_prune_row_groups", "dk_parquet_nonnull_row_groups",
            "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close",
            "dk_dv_load", "dk_dv_num_bits", "dk_dv_bitmap", "dk_dv_selection", "dk_dv_free", "dk_log_pm_scan",
-           "dk_replay_stats_parsed_files"]
+           "dk_replay_stats_parsed_files", "dk_replay_ckpt_selection_bits_all",
+           "dk_replay_ckpt_selection_host", "dk_parquet_open_ms"]
 
 
 def lib(build_if_missing=True):
@@ -110,6 +111,9 @@ def lib(build_if_missing=True):
         "dk_parquet_nonnull_row_groups": (C.c_int, [C.c_char_p, C.c_char_p, P, I32, C.POINTER(I32)]),
         "dk_parquet_row_offset": (I64, [P, I32]),
         "dk_replay_ckpt_selection_bits": (C.c_int, [P, I32, P, I64, I32]),
+        "dk_replay_ckpt_selection_bits_all": (C.c_int, [P, P, P, I32]),
+        "dk_replay_ckpt_selection_host": (C.c_int, [P, I32, C.POINTER(P)]),
+        "dk_parquet_open_ms": (C.c_int, [P, C.POINTER(C.c_double)]),
         "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),
         "dk_parquet_num_rows": (I64, [P, I32]),
         "dk_parquet_column": (C.c_int, [P, I32, I32, C.POINTER(dk_column)]),
@@ -165,10 +169,19 @@ def _arr(ptr, n, dtype):
     return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,)).copy()
 
 
-class Column:
-    """Host copy of a dk_column (same field names as the oracle's Column, by design)."""
+def _view(ptr, n, dtype):
+    if not ptr or n <= 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,))
 
-    def __init__(self, c: dk_column, path: str):
+
+class Column:
+    """A dk_column on the host (same field names as the oracle's Column, by design). copy=False
+    wraps the library's pinned mirror without copying: valid until the owning set decodes again or
+    closes (scan-file batches, consumed before their scan closes)."""
+
+    def __init__(self, c: dk_column, path: str, copy: bool = True):
+        _arr = globals()["_arr"] if copy else _view
         self.path = path
         self.present = bool(c.present)
         self.n_rows = c.n_rows

@@ -18,6 +18,9 @@
 #include <string_view>
 #include <vector>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include "../../include/dkgpu.h"
 #include "dk_device.h"
 #include "dk_thrift.h"
@@ -111,18 +114,141 @@ extern "C" void dk_engine_destroy(dk_engine* e) {
 // ------------------------------------------------------------------------------------------------
 // device buffer helper
 // ------------------------------------------------------------------------------------------------
+// Process-wide block caches for device memory (hipMalloc) and pinned host memory (hipHostMalloc),
+// per device. A getScanFiles allocates tens of GB (decoded-column arena, snappy arena, file images,
+// pinned host staging); the next scan on the same table asks for the same sizes, so released blocks
+// are kept and handed out again instead of being unmapped and re-mapped (hipFree also synchronises
+// the whole device). A released block may still be in use by work queued on some stream, so it is
+// parked until the cache has synchronised the device once (which it does only when it would reuse a
+// parked block); the cache trims itself above `cap` bytes, and on an allocation failure.
+struct MemCache {
+  struct Blk { void* p; size_t n; int dev; };
+  std::mutex mu;
+  std::vector<Blk> idle, parked;   // reusable / released but maybe still in use
+  size_t held = 0;                 // bytes in idle + parked
+  const bool pinned;
+  const size_t cap;
+  MemCache(bool pinned_, size_t cap_) : pinned(pinned_), cap(cap_) {}
+  static size_t round(size_t n) {  // big blocks on 2 MiB granules so near sizes share blocks
+    return n >= (1u << 20) ? (n + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1) : (n + 255) & ~(size_t)255;
+  }
+  int raw_alloc(void** p, size_t n) {
+    return pinned ? (hipHostMalloc(p, n, hipHostMallocDefault) == hipSuccess ? 0 : 1)
+                  : (hipMalloc(p, n) == hipSuccess ? 0 : 1);
+  }
+  void raw_free(void* p) { if (pinned) hipHostFree(p); else hipFree(p); }
+  static bool fits(const Blk& b, size_t n, int dev) { return b.dev == dev && b.n >= n && b.n <= n + n / 4 + (4u << 20); }
+  void* get(size_t want, size_t* got) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    const size_t n = round(want);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      int best = -1;
+      for (size_t i = 0; i < idle.size(); i++)
+        if (fits(idle[i], n, dev) && (best < 0 || idle[i].n < idle[best].n)) best = (int)i;
+      if (best < 0) {
+        bool any = false;
+        for (const Blk& b : parked) any |= fits(b, n, dev);
+        if (any) {                 // the parked blocks are idle once everything queued so far is done
+          hipDeviceSynchronize();
+          idle.insert(idle.end(), parked.begin(), parked.end());
+          parked.clear();
+          for (size_t i = 0; i < idle.size(); i++)
+            if (fits(idle[i], n, dev) && (best < 0 || idle[i].n < idle[best].n)) best = (int)i;
+        }
+      }
+      if (best >= 0) {
+        Blk b = idle[best];
+        idle.erase(idle.begin() + best);
+        held -= b.n;
+        *got = b.n;
+        return b.p;
+      }
+    }
+    void* p = nullptr;
+    if (raw_alloc(&p, n)) {        // out of memory: give back every cached block of this device, retry
+      trim(dev, 0);
+      if (raw_alloc(&p, n)) return nullptr;
+    }
+    *got = n;
+    return p;
+  }
+  void put(void* p, size_t n) {
+    if (!p) return;
+    int dev = 0;
+    hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    parked.push_back({p, n, dev});
+    held += n;
+    if (held > cap) trim_locked(-1, cap / 2);
+  }
+  void trim(int dev, size_t keep) { std::lock_guard<std::mutex> lk(mu); trim_locked(dev, keep); }
+  void trim_locked(int dev, size_t keep) {
+    hipDeviceSynchronize();
+    idle.insert(idle.end(), parked.begin(), parked.end());
+    parked.clear();
+    // free the largest blocks first until at most `keep` bytes stay cached
+    std::sort(idle.begin(), idle.end(), [](const Blk& a, const Blk& b) { return a.n > b.n; });
+    for (size_t i = 0; i < idle.size() && held > keep;) {
+      if (dev >= 0 && idle[i].dev != dev) { i++; continue; }
+      int cur = 0;
+      hipGetDevice(&cur);
+      hipSetDevice(idle[i].dev);
+      raw_free(idle[i].p);
+      hipSetDevice(cur);
+      held -= idle[i].n;
+      idle.erase(idle.begin() + i);
+    }
+  }
+};
+static MemCache& dev_cache() { static MemCache* c = new MemCache(false, (size_t)96 << 30); return *c; }
+static MemCache& pinned_cache() { static MemCache* c = new MemCache(true, (size_t)24 << 30); return *c; }
+
 struct DBuf {
   void* p = nullptr;
-  size_t n = 0;
-  ~DBuf() { if (p) hipFree(p); }
+  size_t n = 0;       // bytes asked for
+  size_t cap = 0;     // bytes of the cached block
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  DBuf(DBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+  ~DBuf() { release(); }
+  void release() { if (p) dev_cache().put(p, cap); p = nullptr; n = cap = 0; }
   int alloc(size_t bytes) {
-    if (p) { hipFree(p); p = nullptr; }
+    release();
     n = bytes;
     if (bytes == 0) return 0;
-    if (hipMalloc(&p, bytes) != hipSuccess) { p = nullptr; return fail("hipMalloc failed for " + std::to_string(bytes) + " bytes"); }
+    p = dev_cache().get(bytes, &cap);
+    if (!p) { n = 0; return fail("hipMalloc failed for " + std::to_string(bytes) + " bytes"); }
     return 0;
   }
   template <class T> T* as() const { return (T*)p; }
+};
+
+// Pinned host memory from the process-wide cache (file images on their way to HBM, selections and
+// column mirrors on their way back): DMA at full PCIe rate, no page faults on reuse.
+struct HBuf {
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  HBuf() = default;
+  HBuf(const HBuf&) = delete;
+  HBuf& operator=(const HBuf&) = delete;
+  HBuf(HBuf&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+  HBuf& operator=(HBuf&& o) noexcept { if (this != &o) { release(); p = o.p; n = o.n; cap = o.cap; o.p = nullptr; o.n = o.cap = 0; } return *this; }
+  ~HBuf() { release(); }
+  void release() { if (p) pinned_cache().put(p, cap); p = nullptr; n = cap = 0; }
+  int alloc(size_t bytes) {
+    release();
+    n = bytes;
+    if (!bytes) return 0;
+    p = (uint8_t*)pinned_cache().get(bytes, &cap);
+    if (!p) { n = 0; return fail("hipHostMalloc failed for " + std::to_string(bytes) + " bytes"); }
+    return 0;
+  }
+  uint8_t* data() const { return p; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
 };
 
 // A HIP stream owned by one call object (dk_parquet, dk_replay, dk_reader): Kernel calls
@@ -174,7 +300,7 @@ struct FileM {
   std::string path;
   int64_t size = 0;
   std::vector<uint8_t> footer;            // the FileMetaData bytes
-  std::vector<uint8_t> bytes;             // packed column-chunk / offset-index bytes
+  HBuf bytes;                             // packed column-chunk / offset-index bytes (pinned)
   std::vector<Span> spans;
   int64_t num_rows = 0;                   // rows of the selected row groups
   std::vector<int32_t> sel;               // selected row groups, ascending
@@ -272,15 +398,29 @@ static int read_spans(FileM& f, std::vector<Span> want) {
     sp.packed_off = cur;
     cur += sp.len;
   }
-  f.bytes.resize(cur);
-  FILE* fp = fopen(f.path.c_str(), "rb");
-  if (!fp) return fail("Error reading Parquet file: " + f.path + " (cannot open)");
-  for (const Span& sp : f.spans)
-    if (fseek(fp, sp.file_off, SEEK_SET) || fread(f.bytes.data() + sp.packed_off, 1, sp.len, fp) != (size_t)sp.len) {
-      fclose(fp);
-      return fail("Error reading Parquet file: " + f.path + " (short read)");
+  if (f.bytes.alloc(cur)) return 1;
+  return 0;
+}
+
+// pread the file's spans into its pinned image; after each `chunk` bytes, sink(offset, length) may
+// start moving that part on (the H2D copy of an image overlaps the rest of its read)
+template <class Sink>
+static int read_spans_into(FileM& f, size_t chunk, Sink&& sink) {
+  const int fd = open(f.path.c_str(), O_RDONLY);
+  if (fd < 0) return fail("Error reading Parquet file: " + f.path + " (cannot open)");
+  size_t flushed = 0;
+  for (const Span& sp : f.spans) {
+    int64_t done = 0;
+    while (done < sp.len) {
+      const ssize_t k = pread(fd, f.bytes.data() + sp.packed_off + done, (size_t)(sp.len - done), sp.file_off + done);
+      if (k <= 0) { close(fd); return fail("Error reading Parquet file: " + f.path + " (short read)"); }
+      done += k;
+      const size_t at = (size_t)(sp.packed_off + done);
+      if (at - flushed >= chunk) { if (sink(flushed, at - flushed)) { close(fd); return 1; } flushed = at; }
     }
-  fclose(fp);
+  }
+  close(fd);
+  if (f.bytes.size() > flushed && sink(flushed, f.bytes.size() - flushed)) return 1;
   return 0;
 }
 
@@ -567,14 +707,35 @@ struct KTimer {
 // ------------------------------------------------------------------------------------------------
 // dk_parquet: a set of files x projected leaves, decoded on the GPU
 // ------------------------------------------------------------------------------------------------
-struct HostCol {           // host mirror of one decoded column (filled on demand)
+struct HostCol {           // host copy of a row range of one decoded column (dk_parquet_column_rows)
   bool ready = false;
   std::vector<uint8_t> row_def, entry_def, fixed, chars;
   std::vector<int64_t> row_offs, offs;
 };
+// Host mirror of one decoded column in pinned memory (dk_parquet_column). The first request for a
+// leaf queues the D2H copies of that leaf for EVERY file of the set at once (a scan consumer reads
+// the same leaves of every batch), each with its own event; a request waits only for its file.
+struct HostMirror {
+  int state = 0;            // 0 empty, 1 copy queued (wait on ev), 2 ready
+  hipEvent_t ev = nullptr;
+  HBuf row_def, row_offs, entry_def, fixed, offs, chars;
+  HostMirror() = default;
+  HostMirror(const HostMirror&) = delete;
+  HostMirror(HostMirror&& o) noexcept : state(o.state), ev(o.ev), row_def(std::move(o.row_def)), row_offs(std::move(o.row_offs)),
+      entry_def(std::move(o.entry_def)), fixed(std::move(o.fixed)), offs(std::move(o.offs)), chars(std::move(o.chars)) { o.ev = nullptr; }
+  ~HostMirror() { if (ev) hipEventDestroy(ev); }
+};
 
+static constexpr int kCopyStreams = 4;   // H2D streams of a file open (the SDMA engines work in parallel)
+struct EventH {
+  hipEvent_t e = nullptr;
+  ~EventH() { if (e) hipEventDestroy(e); }
+  operator hipEvent_t() const { return e; }
+};
 struct dk_parquet {
-  StreamH own;                      // first member: destroyed after every buffer below
+  StreamH own;                      // first members: destroyed after every buffer below
+  StreamH copy[kCopyStreams];
+  EventH copy_done[kCopyStreams];
   hipStream_t stream = nullptr;
   dk_engine* eng = nullptr;
   std::vector<FileM> files;
@@ -603,13 +764,14 @@ struct dk_parquet {
   std::vector<int> col_tile0;
   int copy_cb = 16384;       // k_string_copy staging buffer bytes (sized to the data in prepare)
   std::vector<std::unique_ptr<DBuf>> outbufs;
-  std::vector<HostCol> host;
+  std::vector<HostMirror> host;
   std::vector<HostCol> slice;   // dk_parquet_column_rows: one row range per column, offsets rebased
   DBuf d_first;                 // dk_parquet_first_row result
   int n_pages = 0, n_cols = 0;
   bool has_compressed = false, has_dbp = false;
   int64_t bytes_read = 0, bytes_written = 0, bytes_arena = 0;
   KTimer timer;
+  double open_ms[3] = {0, 0, 0};   // host read + H2D issue, page metadata, prepare passes
   bool prepared = false;
   // the prepare pass ran every stage up to the tile scans on the current inputs: the next full
   // pipeline run only re-runs the scans (sentinels into the freshly allocated outputs), the string
@@ -985,7 +1147,8 @@ static int prepare(dk_parquet* p) {
   if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
   if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;   // dict_hash_off
   HIPOK(hipStreamSynchronize(s));
-  p->host.assign(p->h_cols.size(), HostCol());
+  p->host.clear();
+  p->host.resize(p->h_cols.size());
   p->slice.assign(p->h_cols.size(), HostCol());
   p->prepared = true;
   static const bool no_reuse = getenv("DK_NO_PREPARE_REUSE") && atoi(getenv("DK_NO_PREPARE_REUSE"));
@@ -1394,6 +1557,10 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->eng = e;
   if (p->own.create()) return 1;
   p->stream = p->own.s;
+  for (int k = 0; k < kCopyStreams; k++) {
+    if (p->copy[k].create()) return 1;
+    HIPOK(hipEventCreateWithFlags(&p->copy_done[k].e, hipEventDisableTiming));
+  }
   p->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
   for (int i = 0; i < n_leaves; i++) p->leaves.push_back(leaves[i]);
   p->files.resize(n_files);
@@ -1424,13 +1591,23 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
       }
     }
     if (read_spans(f, want)) { errs[fi] = g_err; return; }
-    // the file's image goes to HBM from this thread, overlapping the other files' reads
+    // the file's image is read into pinned memory and goes to HBM in 8 MiB pieces on a copy stream
+    // while the rest of it (and the other files) are still being read
     hipSetDevice(e->cfg.device);
     if (p->dfile[fi].alloc(f.bytes.size() + 256)) { errs[fi] = g_err; return; }
-    if (!f.bytes.empty() &&
-        hipMemcpy(p->dfile[fi].p, f.bytes.data(), f.bytes.size(), hipMemcpyHostToDevice) != hipSuccess)
-      errs[fi] = "hipMemcpy failed for " + f.path;
+    hipStream_t cs = p->copy[fi % kCopyStreams].s;
+    uint8_t* dst = p->dfile[fi].as<uint8_t>();
+    if (read_spans_into(f, (size_t)8 << 20, [&](size_t off, size_t len) {
+          return hipMemcpyAsync(dst + off, f.bytes.data() + off, len, hipMemcpyHostToDevice, cs) == hipSuccess
+                     ? 0 : fail("hipMemcpyAsync failed for " + f.path);
+        }))
+      errs[fi] = g_err;
   });
+  // the decode stream starts after every copy
+  for (int k = 0; k < kCopyStreams; k++) {
+    HIPOK(hipEventRecord(p->copy_done[k], p->copy[k].s));
+    HIPOK(hipStreamWaitEvent(p->stream, p->copy_done[k], 0));
+  }
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
   const auto t_io1 = std::chrono::steady_clock::now();
@@ -1488,26 +1665,30 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->n_cols = (int)p->h_cols.size();
   const auto t_h2d = std::chrono::steady_clock::now();
   if (prepare(p.get())) return 1;
-  if (getenv("DK_VERBOSE")) {
+  {
     const auto t_end = std::chrono::steady_clock::now();
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count(); };
-    int64_t nb = 0;
-    for (const FileM& f : p->files) nb += (int64_t)f.bytes.size();
-    fprintf(stderr, "[dk] parquet_open %d files %.1f MB: io+h2d %.1f ms, metadata %.1f ms, prepare %.1f ms\n",
-            n_files, nb / 1e6, ms(t_io0, t_io1), ms(t_io1, t_h2d), ms(t_h2d, t_end));
+    p->open_ms[0] = ms(t_io0, t_io1); p->open_ms[1] = ms(t_io1, t_h2d); p->open_ms[2] = ms(t_h2d, t_end);
+    if (getenv("DK_VERBOSE")) {
+      int64_t nb = 0;
+      for (const FileM& f : p->files) nb += (int64_t)f.bytes.size();
+      fprintf(stderr, "[dk] parquet_open %d files %.1f MB: io+h2d %.1f ms, metadata %.1f ms, prepare %.1f ms\n",
+              n_files, nb / 1e6, p->open_ms[0], p->open_ms[1], p->open_ms[2]);
+    }
   }
   *out = p.release();
   return 0;
 }
 
+static int invalidate_mirrors(dk_parquet* p);
 extern "C" int dk_parquet_decode(dk_parquet* p) {
   hipSetDevice(p->eng->cfg.device);
   DState st0{};
   st0.err_row = LLONG_MAX;
   HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, p->stream));
   KTimer::Scope sc(&p->timer, 12, p->stream);
-  for (auto& h : p->host) h.ready = false;
+  if (invalidate_mirrors(p)) return 1;
   return run_pipeline(p, 1);
 }
 
@@ -1538,6 +1719,11 @@ extern "C" int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file) {
 extern "C" int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file) {
   if (!p || file < 0 || file >= (int)p->files.size()) return -1;
   return p->files[file].row0;
+}
+
+extern "C" int dk_parquet_open_ms(dk_parquet* p, double out[3]) {
+  for (int i = 0; i < 3; i++) out[i] = p->open_ms[i];
+  return 0;
 }
 
 extern "C" int dk_parquet_traffic(dk_parquet* p, int64_t* r, int64_t* w) {
@@ -1598,55 +1784,73 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
   return 0;
 }
 
+// queue the D2H copy of decoded column ci into its pinned mirror (on the parquet stream, so it
+// follows the decode that produced the column)
+static int queue_mirror(dk_parquet* p, int ci) {
+  const DColumn& c = p->h_cols[ci];
+  HostMirror& h = p->host[ci];
+  if (h.state) return 0;
+  hipStream_t s = p->stream;
+  const int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
+  if (h.row_def.alloc(c.n_rows + 1)) return 1;
+  if (c.n_rows) HIPOK(hipMemcpyAsync(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost, s));
+  if (c.max_rep > 0) {
+    if (h.row_offs.alloc((c.n_rows + 1) * 8) || h.entry_def.alloc(nv + 1)) return 1;
+    if (c.null_only) { memset(h.row_offs.data(), 0, (c.n_rows + 1) * 8); memset(h.entry_def.data(), 0, nv + 1); }
+    else {
+      HIPOK(hipMemcpyAsync(h.row_offs.data(), c.row_offs, (c.n_rows + 1) * 8, hipMemcpyDeviceToHost, s));
+      if (nv) HIPOK(hipMemcpyAsync(h.entry_def.data(), c.entry_def, nv, hipMemcpyDeviceToHost, s));
+    }
+  }
+  if (c.phys == PT_BYTE_ARRAY) {
+    if (h.offs.alloc((nv + 1) * 8) || h.chars.alloc(c.n_chars + 1)) return 1;
+    if (c.null_only) memset(h.offs.data(), 0, (nv + 1) * 8);
+    else {
+      HIPOK(hipMemcpyAsync(h.offs.data(), c.offs, (nv + 1) * 8, hipMemcpyDeviceToHost, s));
+      if (c.n_chars) HIPOK(hipMemcpyAsync(h.chars.data(), c.chars, c.n_chars, hipMemcpyDeviceToHost, s));
+    }
+  } else {
+    if (h.fixed.alloc(nv * c.width + 1)) return 1;
+    if (c.null_only) memset(h.fixed.data(), 0, nv * c.width + 1);
+    else if (nv) HIPOK(hipMemcpyAsync(h.fixed.data(), c.fixed, nv * c.width, hipMemcpyDeviceToHost, s));
+  }
+  if (!h.ev) HIPOK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
+  HIPOK(hipEventRecord(h.ev, s));
+  h.state = 1;
+  return 0;
+}
+
+// a new decode overwrites the device columns: wait for copies in flight, then forget the mirrors
+static int invalidate_mirrors(dk_parquet* p) {
+  for (auto& h : p->host) {
+    if (h.state == 1) HIPOK(hipEventSynchronize(h.ev));
+    h.state = 0;
+  }
+  return 0;
+}
+
 extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out) {
   hipSetDevice(p->eng->cfg.device);   // this thread may not have used the device yet
   memset(out, 0, sizeof *out);
-  HIPOK(hipStreamSynchronize(p->stream));
   if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
   int ci = p->colmap[file][leaf];
   out->n_rows = p->files[file].num_rows;
   if (ci < 0) { out->present = 0; return 0; }
   const DColumn& c = p->h_cols[ci];
-  HostCol& h = p->host[ci];
+  HostMirror& h = p->host[ci];
+  if (h.state == 0)                    // first touch of this leaf: queue it for this and every later file
+    for (int f = file; f < (int)p->files.size(); f++)
+      if (p->colmap[f][leaf] >= 0 && queue_mirror(p, p->colmap[f][leaf])) return 1;
+  if (h.state == 1) { HIPOK(hipEventSynchronize(h.ev)); h.state = 2; }
   int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
-  if (!h.ready && c.null_only) {
-    h.row_def.resize(c.n_rows);
-    HIPOK(hipMemcpy(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost));
-    h.row_offs.assign(c.max_rep > 0 ? c.n_rows + 1 : 0, 0);
-    h.entry_def.assign(nv, 0);
-    h.offs.assign(c.phys == PT_BYTE_ARRAY ? nv + 1 : 0, 0);
-    h.chars.clear();
-    h.fixed.assign(c.phys == PT_BYTE_ARRAY ? 0 : nv * c.width, 0);
-    h.ready = true;
-  }
-  if (!h.ready) {
-    h.row_def.resize(c.n_rows);
-    HIPOK(hipMemcpy(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost));
-    if (c.max_rep > 0) {
-      h.row_offs.resize(c.n_rows + 1);
-      h.entry_def.resize(nv);
-      HIPOK(hipMemcpy(h.row_offs.data(), c.row_offs, (c.n_rows + 1) * 8, hipMemcpyDeviceToHost));
-      HIPOK(hipMemcpy(h.entry_def.data(), c.entry_def, nv, hipMemcpyDeviceToHost));
-    }
-    if (c.phys == PT_BYTE_ARRAY) {
-      h.offs.resize(nv + 1);
-      h.chars.resize(c.n_chars);
-      HIPOK(hipMemcpy(h.offs.data(), c.offs, (nv + 1) * 8, hipMemcpyDeviceToHost));
-      if (c.n_chars) HIPOK(hipMemcpy(h.chars.data(), c.chars, c.n_chars, hipMemcpyDeviceToHost));
-    } else {
-      h.fixed.resize(nv * c.width);
-      if (nv) HIPOK(hipMemcpy(h.fixed.data(), c.fixed, nv * c.width, hipMemcpyDeviceToHost));
-    }
-    h.ready = true;
-  }
   out->n_entries = nv; out->n_chars = c.n_chars;
   out->phys = c.phys; out->width = c.width; out->max_def = c.max_def; out->max_rep = c.max_rep;
   out->rep_def = c.rep_def; out->present = 1;
   out->row_def = h.row_def.data();
-  out->row_offs = c.max_rep > 0 ? h.row_offs.data() : nullptr;
+  out->row_offs = c.max_rep > 0 ? (const int64_t*)h.row_offs.data() : nullptr;
   out->entry_def = c.max_rep > 0 ? h.entry_def.data() : nullptr;
   out->fixed = c.phys == PT_BYTE_ARRAY ? nullptr : h.fixed.data();
-  out->offs = c.phys == PT_BYTE_ARRAY ? h.offs.data() : nullptr;
+  out->offs = c.phys == PT_BYTE_ARRAY ? (const int64_t*)h.offs.data() : nullptr;
   out->chars = c.phys == PT_BYTE_ARRAY ? h.chars.data() : nullptr;
   return 0;
 }
@@ -2295,6 +2499,10 @@ struct dk_replay {
   std::vector<uint8_t> h_jsel;
   DState h_state{};
   bool have_result = false;
+  // every checkpoint file's selection bytes in one pinned block (dk_replay_ckpt_selection_host)
+  HBuf h_csel;
+  std::vector<int64_t> h_csel_off;
+  bool h_csel_ready = false;
 };
 
 static const DColumn* find_col(dk_parquet* p, int fi, const char* leaf) {
@@ -2708,7 +2916,8 @@ static int replay_launch(dk_replay* r) {
 extern "C" int dk_replay_run(dk_replay* r) {
   hipSetDevice(r->eng->cfg.device);
   r->have_result = false;
-  if (r->ck) for (auto& h : r->ck->host) h.ready = false;
+  r->h_csel_ready = false;
+  if (r->ck && invalidate_mirrors(r->ck)) return 1;
   return replay_launch(r);
 }
 
@@ -2796,6 +3005,31 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
   return 0;
 }
 
+// Zero-copy view of checkpoint file `file`'s selection (one byte per row, valid until the next run
+// or free). The first call after a sync moves every file's selection to one pinned block in one
+// round of async copies and one synchronisation.
+extern "C" int dk_replay_ckpt_selection_host(dk_replay* r, int32_t file, const uint8_t** out) {
+  hipSetDevice(r->eng->cfg.device);
+  *out = nullptr;
+  if (!r->have_result) return fail("replay has no result");
+  if (!r->ck || file < 0 || file >= (int)r->d_csel.size()) return fail("bad checkpoint file index");
+  if (!r->h_csel_ready) {
+    const int nf = (int)r->d_csel.size();
+    r->h_csel_off.assign(nf + 1, 0);
+    for (int f = 0; f < nf; f++) r->h_csel_off[f + 1] = r->h_csel_off[f] + ((r->ck->files[f].num_rows + 63) & ~(int64_t)63);
+    if (r->h_csel.alloc(r->h_csel_off[nf] + 64)) return 1;
+    for (int f = 0; f < nf; f++) {
+      const int64_t n = r->ck->files[f].num_rows;
+      if (r->probe[f].n_rows == 0) memset(r->h_csel.data() + r->h_csel_off[f], 0, n);
+      else if (n) HIPOK(hipMemcpyAsync(r->h_csel.data() + r->h_csel_off[f], r->d_csel[f]->p, n, hipMemcpyDeviceToHost, r->stream));
+    }
+    HIPOK(hipStreamSynchronize(r->stream));
+    r->h_csel_ready = true;
+  }
+  *out = r->h_csel.data() + r->h_csel_off[file];
+  return 0;
+}
+
 extern "C" int dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* dst, int64_t n, int32_t dst_on_device) {
   hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   if (!r->have_result) return fail("dk_replay_ckpt_selection_bits: no result (run + sync first)");
@@ -2812,6 +3046,26 @@ extern "C" int dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* d
   if (tmp.alloc(nb + 16)) return 1;
   launch_pack_bits(r->d_csel[file]->as<uint8_t>(), n, tmp.as<uint8_t>(), s);
   HIPOK(hipMemcpyAsync(dst, tmp.p, nb, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// every checkpoint file's packed selection at dst + offsets[file] (one pack launch per file, one
+// synchronisation for all): the multi-GPU exchange fills its collective buffer with this
+extern "C" int dk_replay_ckpt_selection_bits_all(dk_replay* r, void* dst, const int64_t* offsets, int32_t dst_on_device) {
+  hipSetDevice(r->eng->cfg.device);
+  if (!r->have_result) return fail("dk_replay_ckpt_selection_bits_all: no result (run + sync first)");
+  if (!r->ck) return 0;
+  hipStream_t s = r->stream;
+  const int nf = (int)r->d_csel.size();
+  int64_t total = 0;
+  for (int f = 0; f < nf; f++) total = std::max(total, offsets[f] + (r->ck->files[f].num_rows + 7) / 8);
+  DBuf tmp;
+  uint8_t* base = (uint8_t*)dst;
+  if (!dst_on_device) { if (tmp.alloc(total + 16)) return 1; base = tmp.as<uint8_t>(); }
+  for (int f = 0; f < nf; f++)
+    launch_pack_bits(r->d_csel[f]->as<uint8_t>(), r->ck->files[f].num_rows, base + offsets[f], s);
+  if (!dst_on_device && total) HIPOK(hipMemcpyAsync(dst, tmp.p, total, hipMemcpyDeviceToHost, s));
   HIPOK(hipStreamSynchronize(s));
   return 0;
 }

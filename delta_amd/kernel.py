@@ -162,10 +162,11 @@ class ParquetSet:
         """File row index of this set's first row of the file (non-zero for a row-group shard)."""
         return lib().dk_parquet_row_offset(self._h, file_idx)
 
-    def column(self, file_idx, leaf) -> Column:
+    def column(self, file_idx, leaf, copy=True) -> Column:
+        """copy=False: a view of the library's pinned mirror, valid until the next decode / close."""
         c = dk_column()
         check(lib().dk_parquet_column(self._h, file_idx, self.leaves.index(leaf), C.byref(c)))
-        return Column(c, leaf)
+        return Column(c, leaf, copy)
 
     def first_row(self, file_idx, leaf, min_def=1):
         """Index of the first row whose definition level is >= min_def, or -1 (device scan)."""
@@ -1141,6 +1142,10 @@ class GpuScan:
                                      C.byref(self._rh)))
         self.prepare_ms.update({"plan_files": (t2 - t1) * 1e3, "checkpoint_open": (t3 - t2) * 1e3,
                                 "replay_create": (time.perf_counter() - t3) * 1e3})
+        if self.ckpt is not None:
+            om = (C.c_double * 3)()
+            check(lib().dk_parquet_open_ms(self.ckpt._h, om))
+            self.prepare_ms.update({"open_read_h2d": om[0], "open_metadata": om[1], "open_prepare": om[2]})
         if self.partition is not None:
             from . import partitions as pp
             pprog = pp.pack(self.partition, dk_part_program)
@@ -1198,8 +1203,10 @@ class GpuScan:
         if self.replay is None:
             self.prepare(engine)
             self.replay = True
+        t0 = time.perf_counter()
         self.run()
         self.sync()
+        self.prepare_ms["device_run"] = (time.perf_counter() - t0) * 1e3
         return self._batches()
 
     def _batches(self):
@@ -1210,12 +1217,16 @@ class GpuScan:
             check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
             cols = LazyColumns(leaves, self.tail.column)
             yield FilteredColumnarBatch(cols, root, int(self.tail.rows), sel.view(bool), "json-tail")
+        # checkpoint batches: zero-copy views of the library's pinned selection bytes and column
+        # mirrors (every file's selection comes to the host in one round of copies; a leaf's first
+        # access queues its copy for every later file), valid until the scan is closed
         for fi, path in enumerate(self.ckpt_files or []):
             n = self.ckpt.num_rows(fi)
-            sel = np.zeros(n, dtype=np.uint8)
-            check(lib().dk_replay_ckpt_selection(self._rh, fi, sel.ctypes.data, n))
-            cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf))
-            yield FilteredColumnarBatch(cols, root, int(n), sel.view(bool), path, self.ckpt_index[fi],
+            ptr = C.c_void_p()
+            check(lib().dk_replay_ckpt_selection_host(self._rh, fi, C.byref(ptr)))
+            sel = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_bool)), shape=(n,)) if n else np.zeros(0, bool)
+            cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf, copy=False))
+            yield FilteredColumnarBatch(cols, root, int(n), sel, path, self.ckpt_index[fi],
                                         int(self.ckpt.row_offset(fi)))
 
     def close(self):

@@ -133,6 +133,77 @@ def gather_selections(units, tail_counters, ckpt_counters, group=None, device=No
     return tuple(counters), sels
 
 
+class SelectionExchange:
+    """The device-step exchange: every rank's five tail + five checkpoint ScanMetrics counters and
+    its packed selection bitmaps land on the root rank in ONE collective.
+
+    The unit layout (file, first row, rows) of every rank is exchanged once, when the exchange is
+    built (``all_gather_object``, outside any timed region), so every rank knows every buffer's
+    size. Each step then writes its counters (80 bytes) and its bitmaps straight into one
+    fixed-size buffer on its own device (``write_bits(i, dst)`` fills unit i, e.g. with
+    ``dk_replay_ckpt_selection_bits(..., dst_on_device=1)``), ``all_gather_into_tensor`` moves the
+    world's buffers into one tensor (RCCL over xGMI when the tensors live on the GPU, gloo on the
+    CPU), and only the root copies that tensor to the host, once."""
+
+    HEAD = 80                               # 10 x int64 counters
+
+    def __init__(self, units_meta, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.dev = torch.device(device) if device is not None else torch.device("cpu")
+        metas = [None] * self.world
+        dist.all_gather_object(metas, [tuple(int(x) for x in u) for u in units_meta], group=group)
+        self.metas = metas
+        sizes = [self.HEAD + sum((n + 7) // 8 for _, _, n in m) for m in metas]
+        self.size = max(sizes)
+        self.buf = torch.zeros(self.size, dtype=torch.uint8, device=self.dev)
+        self.out = torch.empty(self.size * self.world, dtype=torch.uint8, device=self.dev)
+        self.slots = []                     # (offset, bytes) of this rank's units inside buf
+        at = self.HEAD
+        for _, _, n in metas[self.rank]:
+            self.slots.append((at, (n + 7) // 8))
+            at += (n + 7) // 8
+
+    def exchange(self, tail_counters, ckpt_counters, write_bits, root=0):
+        """(counters, [(file, first row, rows, bits)] in replay order) on the root, None elsewhere."""
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        head = torch.tensor(list(tail_counters) + list(ckpt_counters), dtype=torch.int64)
+        self.buf[:self.HEAD].copy_(head.view(torch.uint8), non_blocking=False)
+        for i, (off, nb) in enumerate(self.slots):
+            write_bits(i, self.buf[off:off + nb])
+        dist.all_gather_into_tensor(self.out, self.buf, group=self.group)
+        if self.rank != root:
+            return None
+        host = self.out.cpu().numpy()                          # the one D2H
+        counters, sels = None, []
+        for rk in range(self.world):
+            blk = host[rk * self.size:(rk + 1) * self.size]
+            hv = blk[:self.HEAD].view(np.int64)
+            counters = [int(x) for x in hv[:5]] if counters is None else counters
+            counters = [a + int(c) for a, c in zip(counters, hv[5:10])]
+            at = self.HEAD
+            for f, r0, n in self.metas[rk]:
+                nb = (n + 7) // 8
+                sels.append((f, r0, n, blk[at:at + nb].copy()))
+                at += nb
+        sels.sort(key=lambda x: (x[0], x[1]))
+        return tuple(counters), sels
+
+
+def unit_layout(rg_rows, units):
+    """(file, first row, rows) per planned unit [(file, first rg, end rg)] of plan_units, over the
+    row counts per row group of every file (no pruning)."""
+    out = []
+    for f, a, b in units:
+        out.append((f, sum(rg_rows[f][:a]), sum(rg_rows[f][a:b])))
+    return out
+
+
 def gather(output: ShardOutput, group=None):
     """All ranks' outputs on rank 0 (None elsewhere), over torch.distributed (gloo or RCCL)."""
     import torch.distributed as dist

@@ -126,7 +126,9 @@ int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file);   /* file row of the
 int  dk_parquet_decode(dk_parquet* p);                 /* async on the engine stream */
 int  dk_parquet_sync(dk_parquet* p);
 int64_t dk_parquet_num_rows(dk_parquet* p, int32_t file);
-/* D2H copy of one decoded column into library-owned host memory (valid until close). */
+/* One decoded column in library-owned pinned host memory (valid until the next decode or close).
+ * The first request for a leaf queues that leaf's D2H copy for this file and every later file of
+ * the set (a scan consumer reads the same leaves of every batch); each request waits for its file. */
 int  dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_column* out);
 /* Snapshot-load P&M pass (LogReplay.loadTableProtocolAndMetadata, internal/replay/LogReplay.java:
  * 220-314, which takes the first row whose protocol / metaData is non-null): index of the first row
@@ -135,6 +137,8 @@ int  dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, int32_t min
 /* D2H copy of rows [row0, row0+n) of one decoded column; row_offs / offs rebased to the slice
  * (valid until the next call for the same column or close). */
 int  dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf, int64_t row0, int64_t n, dk_column* out);
+/* wall ms of the open's phases: host read (+ H2D issue), page metadata, prepare passes (sizing) */
+int  dk_parquet_open_ms(dk_parquet* p, double out[3]);
 /* bytes read (projected column chunks) and written (decoded buffers) per decode, for roofline */
 int  dk_parquet_traffic(dk_parquet* p, int64_t* bytes_read, int64_t* bytes_written);
 /* algorithmic bytes one launch of a decode kernel must move ("k_string_copy", "k_tile_decode") */
@@ -312,9 +316,16 @@ int  dk_replay_counters(dk_replay* r, int64_t out[5]);
 int  dk_replay_counters_split(dk_replay* r, int64_t tail[5], int64_t ckpt[5]);
 int  dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n);
 int  dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out, int64_t n);
+/* zero-copy: *out = checkpoint file `file`'s selection, one byte per row, in library-owned pinned
+ * memory valid until the next dk_replay_run or dk_replay_free (the first call after a sync moves
+ * every file's selection to the host at once) */
+int  dk_replay_ckpt_selection_host(dk_replay* r, int32_t file, const uint8_t** out);
 /* the same selection packed into bits (LSB first) -- ceil(n / 8) bytes at dst, a device pointer
  * (the multi-GPU merge hands it to RCCL) when dst_on_device, else host memory */
 int  dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* dst, int64_t n, int32_t dst_on_device);
+/* every checkpoint file's packed selection at dst + offsets[file] (one synchronisation for all);
+ * the multi-GPU exchange writes its collective buffer with it */
+int  dk_replay_ckpt_selection_bits_all(dk_replay* r, void* dst, const int64_t* offsets, int32_t dst_on_device);
 /* per-kernel average device time (us) over recorded runs (DK_FLAG_TIMING); names via index */
 int  dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count);
 void dk_replay_free(dk_replay* r);

@@ -522,20 +522,25 @@ def canon_add_from_cols(cols, r):
     dvst = g("add.deletionVector.storageType")
     dv = None
     if dvst is not None and dvst.row_def[r] >= 2:
-        dv = (_str_at(dvst, r, 3), _str_at(g("add.deletionVector.pathOrInlineDv"), r, 3),
+        pid = g("add.deletionVector.pathOrInlineDv")
+        dv = (_str_at(dvst, r, dvst.max_def), _str_at(pid, r, pid.max_def if pid is not None else 0),
               _fixed_at(g("add.deletionVector.offset"), r, np.int32),
               _fixed_at(g("add.deletionVector.sizeInBytes"), r, np.int32),
               _fixed_at(g("add.deletionVector.cardinality"), r, np.int64))
     dc = g("add.dataChange")
-    row = (_str_at(g("add.path"), r, 2),
+    pc = g("add.path")
+    # levels from the file: Spark writes every checkpoint field optional (add.path max_def 2), Kernel's
+    # writer marks path / size / ... required (max_def 1, AddFile.FULL_SCHEMA)
+    row = (_str_at(pc, r, pc.max_def if pc is not None else 0),
            _map_at(g("add.partitionValues.key_value.key"), g("add.partitionValues.key_value.value"), r),
            _fixed_at(g("add.size"), r, np.int64), _fixed_at(g("add.modificationTime"), r, np.int64),
-           None if dc is None or dc.row_def[r] < 2 else bool(dc.fixed[r]),
+           None if dc is None or dc.row_def[r] < dc.max_def else bool(dc.fixed[r]),
            dv,
            _map_at(g("add.tags.key_value.key"), g("add.tags.key_value.value"), r),
            _fixed_at(g("add.baseRowId"), r, np.int64), _fixed_at(g("add.defaultRowCommitVersion"), r, np.int64))
     if STATS_LEAF in cols:
-        row = row + (_str_at(cols[STATS_LEAF], r, 2),)
+        sc = cols[STATS_LEAF]
+        row = row + (_str_at(sc, r, sc.max_def if sc is not None else 0),)
     return row
 
 
@@ -569,7 +574,7 @@ def probe_checkpoint(cols, n_rows, keyset, counters: Counters):
         offv = off.fixed.view(np.int32) if off is not None else np.zeros(n_rows, np.int32)
         offd = off.row_def if off is not None else np.zeros(n_rows, np.uint8)
         args = (ptr(st.row_def), ptr(st.offs), ptr(st.chars), ptr(pid.offs), ptr(pid.chars),
-                ptr(offd), ptr(offv), 3)
+                ptr(offd), ptr(offv), off.max_def if off is not None else 3)
     else:
         args = (None, None, None, None, None, None, None, 3)
     rc = L.dkr_probe_checkpoint(keyset, n_rows, ptr(path.row_def), ptr(path.offs), ptr(path.chars),
@@ -583,7 +588,7 @@ def probe_checkpoint(cols, n_rows, keyset, counters: Counters):
 
 
 def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, skipping=None,
-           partition=None) -> ReplayResult:
+           partition=None, threads=1, keep_cols=True, extra_leaves=()) -> ReplayResult:
     """getLatestSnapshot + getScanFiles restated; returns the ordered active scan files + counters.
 
     shard=(world, rank): reconcile only the checkpoint files whose replay-order index i has
@@ -593,7 +598,13 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
     skipping=(predicate node, {stats path: type}): ScanImpl.applyDataSkipping on the reconciled
     rows (oracle/skipping.py); implies with_stats, leaves the counters unchanged.
     partition=(predicate, {lower name: (type, physical name)}): ScanImpl.applyPartitionPruning
-    (oracle/partitions.py), applied before data skipping, on every add row of every batch."""
+    (oracle/partitions.py), applied before data skipping, on every add row of every batch.
+
+    threads > 1: multi-part / classic checkpoint files are decoded and probed on a thread pool
+    (the C decoder releases the GIL); a checkpoint file's selection depends only on the commit-tail
+    key sets, which are final before any checkpoint file is read (App. A, R4), so the result is
+    the sequential one. keep_cols=False drops each file's decoded columns after its probe (full-size
+    runs); extra_leaves are decoded too (timing the whole projected read schema)."""
     if skipping is not None:
         with_stats = True
     world, rank = shard if shard else (1, 0)
@@ -609,6 +620,7 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
     queue = list(files)
     L = lib()
     keyset = None
+    pool_items = []         # (file, replay-order index) decoded on the thread pool (threads > 1)
     while queue:
         f = queue.pop(0)
         if f.kind == "commit":
@@ -672,7 +684,10 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                 continue
             if not mine and g.kind != "v2":
                 continue
-            extra = SIDECAR_LEAVES if g.kind == "v2" else ()
+            if threads > 1 and g.kind in ("classic", "multipart") and partition is None:
+                pool_items.append((g, idx))
+                continue
+            extra = tuple(SIDECAR_LEAVES if g.kind == "v2" else ()) + tuple(extra_leaves)
             keep = None
             if partition is not None and g.kind in ("multipart", "sidecar"):
                 # the checkpoint predicate prunes row groups of parts and sidecars (oracle/rowgroups.py)
@@ -690,7 +705,28 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                 continue
             b = CheckpointBatch(g.path, cols, pf.num_rows, file_index=idx)
             b.selected = probe_checkpoint(cols, pf.num_rows, keyset, cc)
+            if not keep_cols:
+                b.cols = {}
             res.checkpoint.append(b)
+    if pool_items:
+        import concurrent.futures as cf
+
+        def work(item):
+            g, idx = item
+            pf, cols = decode_checkpoint_file(g.path, with_stats, extra_leaves)
+            part = Counters()
+            b = CheckpointBatch(g.path, cols, pf.num_rows, file_index=idx)
+            b.selected = probe_checkpoint(cols, pf.num_rows, keyset, part)
+            if not keep_cols:
+                b.cols = {}
+            return b, part
+
+        with cf.ThreadPoolExecutor(threads) as ex:
+            for b, part in ex.map(work, pool_items):
+                res.checkpoint.append(b)
+                cc.addFilesSeen += part.addFilesSeen
+                cc.activeAddFiles += part.activeAddFiles
+                cc.duplicateAddFiles += part.duplicateAddFiles
     if keyset is not None:
         L.dkr_keyset_free(keyset)
     res.counters = Counters(*[a + b for a, b in zip(c.as_tuple(), cc.as_tuple())])
