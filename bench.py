@@ -506,7 +506,9 @@ def main(argv=None):
             capture.update(counters=sc.metrics.as_tuple(), tail_paths=tail_paths, bits=bits)
         phases = dict(sc.prepare_ms)
         phases["consume"] = consume_ms
+        t_x = time.perf_counter()
         sc.close()
+        phases["close"] = (time.perf_counter() - t_x) * 1e3
         return seen, n_sel, size_sum, phases
 
     for i in range(args.warmup):

@@ -83,7 +83,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close",
            "dk_dv_load", "dk_dv_num_bits", "dk_dv_bitmap", "dk_dv_selection", "dk_dv_free", "dk_log_pm_scan",
            "dk_replay_stats_parsed_files", "dk_replay_ckpt_selection_bits_all",
-           "dk_replay_ckpt_selection_host", "dk_parquet_open_ms"]
+           "dk_replay_ckpt_selection_host", "dk_parquet_open_ms", "dk_replay_attach_checkpoint"]
 
 
 def lib(build_if_missing=True):
@@ -114,6 +114,7 @@ def lib(build_if_missing=True):
         "dk_replay_ckpt_selection_bits_all": (C.c_int, [P, P, P, I32]),
         "dk_replay_ckpt_selection_host": (C.c_int, [P, I32, C.POINTER(P)]),
         "dk_parquet_open_ms": (C.c_int, [P, C.POINTER(C.c_double)]),
+        "dk_replay_attach_checkpoint": (C.c_int, [P, P]),
         "dk_parquet_decode": (C.c_int, [P]), "dk_parquet_sync": (C.c_int, [P]),
         "dk_parquet_num_rows": (I64, [P, I32]),
         "dk_parquet_column": (C.c_int, [P, I32, I32, C.POINTER(dk_column)]),

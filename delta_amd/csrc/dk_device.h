@@ -76,6 +76,8 @@ struct SnapCtx {
   int32_t* serial;           // compressed page -> 1: decode on the serial path
   uint64_t* tbits;           // page mode: tag-start bitmap, DK_SNAP_SEG / 64 words per segment (or null)
   int32_t page_mode;         // 1: whole pages decode in order (no 64 KiB fragment starts needed)
+  int32_t k0, k1;            // launch range: segments [k0, k1) (k_snap_walk / k_snap_link)
+  int32_t c0;                // launch range: first compressed page (k_snap_fix)
 };
 
 
@@ -85,6 +87,8 @@ struct DPosChunk {
   int32_t cnt, base;     // candidates in the chunk, their first index
 };
 constexpr int DK_POS_CHUNK = 16384;
+// k_expand record kinds (per-page work lists built on the device from per-group counts)
+enum : int { EX_TILE = 0, EX_POSCHUNK = 1, EX_FRAG = 2, EX_SEG = 3 };
 
 // One run of an RLE/bit-packed hybrid stream: values [start, next.start) are `val` (RLE,
 // bp_idx < 0) or bit-packed from byte bp_off (relative to the page data start) on.

@@ -31,10 +31,12 @@ void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
 void launch_snappy(const SnapCtx&, int, int, const int2*, int, hipStream_t);
 void snap_stats(unsigned long long*);
 void launch_pack_bits(const uint8_t*, long long, uint8_t*, hipStream_t);
+void launch_expand(const int64_t*, const int32_t*, int, int, void*, hipStream_t);
+void launch_copy_zc(void*, const void*, long long, hipStream_t);
 void launch_arrow_window(const ArrowWin&, hipStream_t);
 void launch_dv_expand(const DvCont*, int, const uint8_t*, unsigned long long*, hipStream_t);
 void launch_dv_select(const unsigned long long*, long long, const long long*, long long, uint8_t*, hipStream_t);
-void launch_positions(const DChunk*, DPage*, int, const uint8_t*, int32_t*, DPosChunk*, int, hipStream_t);
+void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
 void launch_tile_scan1(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
@@ -117,27 +119,38 @@ extern "C" void dk_engine_destroy(dk_engine* e) {
 // Process-wide block caches for device memory (hipMalloc) and pinned host memory (hipHostMalloc),
 // per device. A getScanFiles allocates tens of GB (decoded-column arena, snappy arena, file images,
 // pinned host staging); the next scan on the same table asks for the same sizes, so released blocks
-// are kept and handed out again instead of being unmapped and re-mapped (hipFree also synchronises
-// the whole device). A released block may still be in use by work queued on some stream, so it is
-// parked until the cache has synchronised the device once (which it does only when it would reuse a
-// parked block); the cache trims itself above `cap` bytes, and on an allocation failure.
+// are kept and handed out again instead of being unmapped and re-mapped (hipHostMalloc pins page by
+// page: ~90 ms for a 90 MB file image; hipFree synchronises the device). Sizes are rounded to a
+// geometric grid (8 classes per doubling, <= 12.5 % slack) so near sizes share blocks.
+//
+// A released block may still be read or written by work queued on its owner's stream. Owners
+// release inside a SyncedRelease scope once their stream is drained (object close / free), and
+// those blocks are reusable at once; any other release parks the block, and parked blocks are only
+// reused after the cache itself drains the device (when trimming).
+static thread_local int t_synced = 0;
+struct SyncedRelease {
+  SyncedRelease() { t_synced++; }
+  ~SyncedRelease() { t_synced--; }
+};
 struct MemCache {
   struct Blk { void* p; size_t n; int dev; };
   std::mutex mu;
-  std::vector<Blk> idle, parked;   // reusable / released but maybe still in use
+  std::vector<Blk> idle, parked;
   size_t held = 0;                 // bytes in idle + parked
   const bool pinned;
   const size_t cap;
   MemCache(bool pinned_, size_t cap_) : pinned(pinned_), cap(cap_) {}
-  static size_t round(size_t n) {  // big blocks on 2 MiB granules so near sizes share blocks
-    return n >= (1u << 20) ? (n + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1) : (n + 255) & ~(size_t)255;
+  static size_t round(size_t n) {
+    if (n < ((size_t)1 << 20)) return (n + 4095) & ~(size_t)4095;
+    int e = 63 - __builtin_clzll((unsigned long long)n);       // 2^e <= n < 2^(e+1)
+    const size_t step = (size_t)1 << (e - 3);                   // 8 classes per doubling
+    return (n + step - 1) & ~(step - 1);
   }
   int raw_alloc(void** p, size_t n) {
     return pinned ? (hipHostMalloc(p, n, hipHostMallocDefault) == hipSuccess ? 0 : 1)
                   : (hipMalloc(p, n) == hipSuccess ? 0 : 1);
   }
   void raw_free(void* p) { if (pinned) hipHostFree(p); else hipFree(p); }
-  static bool fits(const Blk& b, size_t n, int dev) { return b.dev == dev && b.n >= n && b.n <= n + n / 4 + (4u << 20); }
   void* get(size_t want, size_t* got) {
     int dev = 0;
     hipGetDevice(&dev);
@@ -145,22 +158,14 @@ struct MemCache {
     {
       std::lock_guard<std::mutex> lk(mu);
       int best = -1;
-      for (size_t i = 0; i < idle.size(); i++)
-        if (fits(idle[i], n, dev) && (best < 0 || idle[i].n < idle[best].n)) best = (int)i;
-      if (best < 0) {
-        bool any = false;
-        for (const Blk& b : parked) any |= fits(b, n, dev);
-        if (any) {                 // the parked blocks are idle once everything queued so far is done
-          hipDeviceSynchronize();
-          idle.insert(idle.end(), parked.begin(), parked.end());
-          parked.clear();
-          for (size_t i = 0; i < idle.size(); i++)
-            if (fits(idle[i], n, dev) && (best < 0 || idle[i].n < idle[best].n)) best = (int)i;
-        }
+      for (size_t i = 0; i < idle.size(); i++) {   // the smallest idle block of this class or up to 2 above
+        const Blk& b = idle[i];
+        if (b.dev == dev && b.n >= n && b.n <= n + n / 4 && (best < 0 || b.n < idle[best].n)) best = (int)i;
       }
       if (best >= 0) {
         Blk b = idle[best];
-        idle.erase(idle.begin() + best);
+        idle[best] = idle.back();
+        idle.pop_back();
         held -= b.n;
         *got = b.n;
         return b.p;
@@ -179,7 +184,7 @@ struct MemCache {
     int dev = 0;
     hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    parked.push_back({p, n, dev});
+    (t_synced ? idle : parked).push_back({p, n, dev});
     held += n;
     if (held > cap) trim_locked(-1, cap / 2);
   }
@@ -204,6 +209,31 @@ struct MemCache {
 };
 static MemCache& dev_cache() { static MemCache* c = new MemCache(false, (size_t)96 << 30); return *c; }
 static MemCache& pinned_cache() { static MemCache* c = new MemCache(true, (size_t)24 << 30); return *c; }
+
+// Non-blocking streams are pooled per device (creating one costs milliseconds): a call object takes
+// one when it is created and gives it back, drained, when it is freed.
+struct StreamPool {
+  std::mutex mu;
+  std::vector<std::pair<int, hipStream_t>> free_;
+  hipStream_t get() {
+    int dev = 0;
+    hipGetDevice(&dev);
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (size_t i = 0; i < free_.size(); i++)
+        if (free_[i].first == dev) { hipStream_t s = free_[i].second; free_.erase(free_.begin() + i); return s; }
+    }
+    hipStream_t s = nullptr;
+    return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? s : nullptr;
+  }
+  void put(hipStream_t s) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    std::lock_guard<std::mutex> lk(mu);
+    free_.push_back({dev, s});
+  }
+};
+static StreamPool& stream_pool() { static StreamPool* p = new StreamPool(); return *p; }
 
 struct DBuf {
   void* p = nullptr;
@@ -256,8 +286,8 @@ struct HBuf {
 // nothing of a call runs on a stream shared through the engine.
 struct StreamH {
   hipStream_t s = nullptr;
-  ~StreamH() { if (s) { hipStreamSynchronize(s); hipStreamDestroy(s); } }
-  int create() { return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? 0 : fail("hipStreamCreate failed"); }
+  ~StreamH() { if (s) { hipStreamSynchronize(s); stream_pool().put(s); } }
+  int create() { s = stream_pool().get(); return s ? 0 : fail("hipStreamCreate failed"); }
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -726,15 +756,24 @@ struct HostMirror {
   ~HostMirror() { if (ev) hipEventDestroy(ev); }
 };
 
-static constexpr int kCopyStreams = 4;   // H2D streams of a file open (the SDMA engines work in parallel)
+static constexpr int kCopyStreams = 8;   // H2D streams of a file open (the SDMA engines work in parallel)
+static int copy_streams() {
+  static const int n = getenv("DK_COPY_STREAMS") ? std::max(1, std::min(kCopyStreams, atoi(getenv("DK_COPY_STREAMS")))) : 4;
+  return n;
+}
 struct EventH {
   hipEvent_t e = nullptr;
+  EventH() = default;
+  EventH(const EventH&) = delete;
+  EventH& operator=(const EventH&) = delete;
+  EventH(EventH&& o) noexcept : e(o.e) { o.e = nullptr; }
   ~EventH() { if (e) hipEventDestroy(e); }
   operator hipEvent_t() const { return e; }
 };
 struct dk_parquet {
   StreamH own;                      // first members: destroyed after every buffer below
   StreamH copy[kCopyStreams];
+  StreamH aux;                      // table uploads while `stream` waits for the H2D copies
   EventH copy_done[kCopyStreams];
   hipStream_t stream = nullptr;
   dk_engine* eng = nullptr;
@@ -767,11 +806,20 @@ struct dk_parquet {
   std::vector<HostMirror> host;
   std::vector<HostCol> slice;   // dk_parquet_column_rows: one row range per column, offsets rebased
   DBuf d_first;                 // dk_parquet_first_row result
+  DBuf d_expand;                // k_expand inputs (group prefix + ids)
+  // slices for the pipelined prepare: per file its first page / column (n_files + 1 entries), the
+  // compressed-page list and its segment / fragment prefixes, and an event after each file's copies
+  std::vector<int> file_page0, file_col0;
+  std::vector<int32_t> h_cpage, h_sbase, h_fbase;
+  std::vector<EventH> file_ev;
+  std::vector<HBuf> staging;        // pinned sources of zero-copy uploads, released when prepare ends
   int n_pages = 0, n_cols = 0;
   bool has_compressed = false, has_dbp = false;
   int64_t bytes_read = 0, bytes_written = 0, bytes_arena = 0;
   KTimer timer;
-  double open_ms[3] = {0, 0, 0};   // host read + H2D issue, page metadata, prepare passes
+  // host read + H2D issue, page metadata, prepare passes; inside prepare: H2D wait + headers,
+  // host page tables, device sizing passes, host tiles + output arena
+  double open_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   bool prepared = false;
   // the prepare pass ran every stage up to the tile scans on the current inputs: the next full
   // pipeline run only re-runs the scans (sentinels into the freshly allocated outputs), the string
@@ -823,7 +871,76 @@ static bool snap_hybrid(const dk_parquet* p) {
   return !env || !strcmp(env, "hybrid");
 }
 
-// the decode pipeline (mode: -1 = headers only; 0 = prepare pass through the scans, which size the
+// A contiguous slice of the decode work: files [f0, f1) own pages [pa, pb), compressed pages
+// [ca, cb) with their segments [s0, s1) and fragments [fr0, fr1), columns [col0, col1), level tiles
+// [t0, t1) and string-position chunks [pc0, pc1). The prepare pass runs one slice per group of files
+// as soon as those files' H2D copies have landed.
+struct PRange { int pa = 0, pb = 0, ca = 0, cb = 0, s0 = 0, s1 = 0, fr0 = 0, fr1 = 0, col0 = 0, col1 = 0, t0 = 0, t1 = 0, pc0 = 0, pc1 = 0; };
+
+static PRange file_range(const dk_parquet* p, int f0, int f1) {
+  PRange R;
+  R.pa = p->file_page0[f0]; R.pb = p->file_page0[f1];
+  R.col0 = p->file_col0[f0]; R.col1 = p->file_col0[f1];
+  R.ca = (int)(std::lower_bound(p->h_cpage.begin(), p->h_cpage.end(), R.pa) - p->h_cpage.begin());
+  R.cb = (int)(std::lower_bound(p->h_cpage.begin(), p->h_cpage.end(), R.pb) - p->h_cpage.begin());
+  if (!p->h_sbase.empty()) { R.s0 = p->h_sbase[R.ca]; R.s1 = p->h_sbase[R.cb]; R.fr0 = p->h_fbase[R.ca]; R.fr1 = p->h_fbase[R.cb]; }
+  R.t0 = R.col0 < p->n_cols ? p->h_cols[R.col0].first_tile : p->n_ltiles;
+  R.t1 = R.col1 < p->n_cols ? p->h_cols[R.col1].first_tile : p->n_ltiles;
+  R.pc0 = R.pa < p->n_pages ? p->h_pages[R.pa].pchunk0 : p->n_pchunks;
+  R.pc1 = R.pb < p->n_pages ? p->h_pages[R.pb].pchunk0 : p->n_pchunks;
+  return R;
+}
+
+// headers, snappy, runs, counts, positions, chars and the scans over one slice
+static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
+  KTimer& T = p->timer;
+  const DChunk* C = p->d_chunks.as<DChunk>();
+  DPage* P = p->d_pages.as<DPage>();
+  int32_t* pos = p->d_pos.as<int32_t>();
+  const uint8_t* arena = p->d_arena.as<uint8_t>();
+  DState* st = p->d_state.as<DState>();
+  DColumn* cols = p->d_cols.as<DColumn>();
+  DTile* LT = p->d_ltiles.as<DTile>();
+  Seg* runs = p->d_runs.as<Seg>();
+  const int np = R.pb - R.pa;
+  if (p->has_compressed && R.cb > R.ca) {
+    SnapCtx X{};
+    X.chunks = C; X.pages = P; X.arena = p->d_arena.as<uint8_t>();
+    X.cpage = p->d_cpage.as<int32_t>(); X.sbase = p->d_sbase.as<int32_t>(); X.spage = p->d_spage.as<int32_t>();
+    X.nseg = p->n_segs;
+    int32_t* ws = p->d_snapws.as<int32_t>();
+    const int64_t ns = p->n_segs;
+    X.w_exit = ws; X.w_out = ws + ns; X.w_npos = ws + 2 * ns; X.t_entry = ws + 3 * ns; X.t_out = ws + 4 * ns;
+    X.t_exit = ws + 5 * ns; X.w_pos = ws + 6 * ns; X.w_cum = ws + (6 + DK_SNAP_REC) * ns;
+    X.fbase = p->d_fbase.as<int32_t>(); X.fstart = p->d_fstart.as<int64_t>(); X.serial = p->d_serial.as<int32_t>();
+    X.k0 = R.s0; X.k1 = R.s1; X.c0 = R.ca;
+    // page mode (one wave decodes a whole page in order, no walk; never sliced) or the speculative
+    // walk that splits pages into 64 KiB fragments
+    const bool page_mode = snap_page_mode(p);
+    const int ncp = R.cb - R.ca;
+    const int nfr = page_mode ? -1 : R.fr1 - R.fr0;
+    X.page_mode = page_mode ? 1 : 0;
+    X.tbits = (page_mode || snap_hybrid(p)) ? p->d_tbits.as<uint64_t>() : nullptr;
+    const int2* wk = page_mode ? p->d_pwork.as<int2>() : p->d_fwork.as<int2>() + R.fr0;
+    { KTimer::Scope s0(&T, 13, s); launch_snappy(X, ncp, nfr, wk, 0, s); }
+    { KTimer::Scope s1(&T, 19, s); launch_snappy(X, ncp, nfr, wk, 1, s); }
+    { KTimer::Scope s2(&T, 20, s); launch_snappy(X, ncp, nfr, wk, 2, s); }
+    { KTimer::Scope s3(&T, 21, s); launch_snappy(X, ncp, nfr, wk, 3, s); }
+  }
+  { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P + R.pa, np, arena, runs, s); }
+  auto tiles = [&](auto&& f) {
+    if (!split_launch()) { f(R.t0, R.t1 - R.t0); return; }
+    for (int c = R.col0; c < R.col1; c++) f(p->h_cols[c].first_tile, p->h_cols[c].n_tiles);
+  };
+  { KTimer::Scope sc(&T, 2, s); tiles([&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
+  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0, s); }
+  if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P + R.pa, np, arena, p->d_dbp.as<long long>(), s); }
+  { KTimer::Scope sc(&T, 16, s); tiles([&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
+}
+
+// the decode pipeline over every file (mode: -1 = headers only; 0 = through the scans, which size the
 // outputs; 1 = full step)
 static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
   if (!s) s = p->stream;
@@ -837,45 +954,16 @@ static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
   const long long* dbp = p->d_dbp.as<long long>();
   DTile* LT = p->d_ltiles.as<DTile>();
   Seg* runs = p->d_runs.as<Seg>();
-  int n = p->n_pages;
   const bool reuse = mode == 1 && p->fresh;
   p->fresh = false;
   if (reuse) {                         // headers, snappy, runs, counts, positions, chars: done by prepare
     { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols, p->n_cols, P, LT, st, s); }
     { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols, p->n_cols, P, LT, st, s); }
   } else {
-  { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, n, s); }
-  if (mode == -1) return 0;
-  if (p->has_compressed) {
-    SnapCtx X{};
-    X.chunks = C; X.pages = P; X.arena = p->d_arena.as<uint8_t>();
-    X.cpage = p->d_cpage.as<int32_t>(); X.sbase = p->d_sbase.as<int32_t>(); X.spage = p->d_spage.as<int32_t>();
-    X.nseg = p->n_segs;
-    int32_t* ws = p->d_snapws.as<int32_t>();
-    const int64_t ns = p->n_segs;
-    X.w_exit = ws; X.w_out = ws + ns; X.w_npos = ws + 2 * ns; X.t_entry = ws + 3 * ns; X.t_out = ws + 4 * ns;
-    X.t_exit = ws + 5 * ns; X.w_pos = ws + 6 * ns; X.w_cum = ws + (6 + DK_SNAP_REC) * ns;
-    X.fbase = p->d_fbase.as<int32_t>(); X.fstart = p->d_fstart.as<int64_t>(); X.serial = p->d_serial.as<int32_t>();
-    // page mode (one wave decodes a whole page in order, no walk) once there are enough pages to
-    // fill the chip; otherwise the speculative walk splits pages into 64 KiB fragments
-    const bool page_mode = snap_page_mode(p);
-    const int nfr = page_mode ? -1 : p->n_frags;
-    X.page_mode = page_mode ? 1 : 0;
-    X.tbits = (page_mode || snap_hybrid(p)) ? p->d_tbits.as<uint64_t>() : nullptr;
-    const int2* wk = page_mode ? p->d_pwork.as<int2>() : p->d_fwork.as<int2>();
-    { KTimer::Scope s0(&T, 13, s); launch_snappy(X, p->n_cpages, nfr, wk, 0, s); }
-    { KTimer::Scope s1(&T, 19, s); launch_snappy(X, p->n_cpages, nfr, wk, 1, s); }
-    { KTimer::Scope s2(&T, 20, s); launch_snappy(X, p->n_cpages, nfr, wk, 2, s); }
-    { KTimer::Scope s3(&T, 21, s); launch_snappy(X, p->n_cpages, nfr, wk, 3, s); }
-  }
-  { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P, n, arena, runs, s); }
-  { KTimer::Scope sc(&T, 2, s); per_column_tiles(p, [&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
-  { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols, p->n_cols, P, LT, st, s); }
-  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, n, arena, pos, p->d_pchunks.as<DPosChunk>(), p->n_pchunks, s); }
-  if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P, n, arena, p->d_dbp.as<long long>(), s); }
-  { KTimer::Scope sc(&T, 16, s); per_column_tiles(p, [&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
-  { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols, p->n_cols, P, LT, st, s); }
-  if (mode == 0) return 0;
+    { KTimer::Scope sc(&T, 0, s); launch_page_headers(C, P, p->n_pages, s); }
+    if (mode == -1) return 0;
+    sizing_stages(p, s, file_range(p, 0, (int)p->files.size()));
+    if (mode == 0) return 0;
   }
   // string copy first: it fills the key column's per-value hashes that k_tile_decode forwards
   {
@@ -910,19 +998,54 @@ static std::string page_status_msg(const dk_parquet* p, const std::vector<DPage>
   return "";
 }
 
+// dst = the work items of `groups` (item i of group g: k_expand's record kind over gid[g] or g and
+// the item's index within its group), base = the groups' item prefix (n + 1 entries)
+static int expand(dk_parquet* p, hipStream_t us, DBuf& dst, const std::vector<int32_t>& gid,
+                  const std::vector<int64_t>& base, int kind, size_t item_bytes) {
+  const int n = (int)base.size() - 1;
+  const int64_t total = base.back();
+  if (dst.alloc((size_t)std::max<int64_t>(total, 1) * item_bytes)) return 1;
+  if (!total) return 0;
+  // the kernel reads the prefix / ids straight from pinned host memory (kept until prepare ends):
+  // no DMA behind the file images, no synchronisation
+  HBuf hb;
+  if (hb.alloc((size_t)(n + 1) * 8 + (size_t)n * 4 + 64)) return 1;
+  memcpy(hb.data(), base.data(), (size_t)(n + 1) * 8);
+  if (!gid.empty()) memcpy(hb.data() + (size_t)(n + 1) * 8, gid.data(), (size_t)n * 4);
+  launch_expand((const int64_t*)hb.data(), gid.empty() ? nullptr : (const int32_t*)(hb.data() + (size_t)(n + 1) * 8),
+                n, kind, dst.p, us);
+  p->staging.push_back(std::move(hb));
+  return 0;
+}
+
+// upload through pinned staging copied by a kernel (launch_copy_zc): never queues behind, nor
+// blocks on, the H2D copies of the file images
+static int upload_zc(dk_parquet* p, DBuf& d, const void* src, size_t n, hipStream_t s) {
+  if (d.n < n || !d.p) if (d.alloc(n ? n : 16)) return 1;
+  if (!n) return 0;
+  HBuf hb;
+  if (hb.alloc(n)) return 1;
+  memcpy(hb.data(), src, n);
+  launch_copy_zc(d.p, hb.data(), (long long)n, s);
+  p->staging.push_back(std::move(hb));
+  return 0;
+}
+
 static int prepare(dk_parquet* p) {
   hipStream_t s = p->stream;
-  // 1. parse headers once to size the scratch areas
-  if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;
-  if (upload(p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), s)) return 1;
+  // the decode stream waits for the file images' H2D copies: table uploads and work-list expansion
+  // go on the aux stream meanwhile (a pageable upload on a waiting stream would block the host)
+  hipStream_t us = p->aux.s;
+  using clk = std::chrono::steady_clock;
+  auto since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  const auto t0 = clk::now();
+  // 1. page headers were parsed on the host while the images were read (build_file_meta): size the
+  // scratch areas from them right away, while the H2D copies still run
   DState st0{};
   st0.err_row = LLONG_MAX;
-  if (upload(p->d_state, &st0, sizeof st0, s)) return 1;
-  if (p->d_pos.alloc(64)) return 1;
-  if (p->d_arena.alloc(64)) return 1;
-  run_pipeline(p, -1);
-  HIPOK(hipMemcpyAsync(p->h_pages.data(), p->d_pages.p, p->h_pages.size() * sizeof(DPage), hipMemcpyDeviceToHost, s));
-  HIPOK(hipStreamSynchronize(s));
+  if (upload_zc(p, p->d_state, &st0, sizeof st0, us)) return 1;
+  p->open_ms[3] = since(t0);
+  const auto t1 = clk::now();
   // header errors
   for (DPage& pg : p->h_pages) if (pg.status != PS_OK && pg.status != PS_UNSUPPORTED) return fail(page_status_msg(p, p->h_pages));
   for (const DPage& pg : p->h_pages) {   // every page body must lie inside the bytes that were read
@@ -932,8 +1055,9 @@ static int prepare(dk_parquet* p) {
                   std::to_string(file_offset(f, pg.hdr_off)) + ")");
   }
   int64_t posn = 0, arena_n = 0, dbp_n = 0;
-  std::vector<int32_t> cpage, fbase(1, 0), sbase(1, 0), spage;
-  std::vector<int2> fwork;
+  // per-page work lists (fragments, segments, level tiles, position chunks) are expanded on the device
+  // from per-group counts (k_expand): the host only builds the prefix arrays (one entry per page)
+  std::vector<int32_t> cpage, fbase(1, 0), sbase(1, 0);
   for (size_t i = 0; i < p->h_pages.size(); i++) {
     DPage& pg = p->h_pages[i];
     DChunk& ck = p->h_chunks[pg.chunk];
@@ -951,10 +1075,8 @@ static int prepare(dk_parquet* p) {
         p->has_compressed = true;
         const int64_t body = pg.usize > lv ? pg.usize - lv : 0;
         const int nf = body > 0 ? (int)((body + 65535) / 65536) : 1;   // k_snap_frag fragments (64 KiB)
-        for (int k = 0; k < nf; k++) fwork.push_back(make_int2((int)cpage.size(), k));
         const int64_t cbody = pg.csize > lv ? pg.csize - lv : 0;
         const int ns = cbody > 0 ? (int)((cbody + DK_SNAP_SEG - 1) / DK_SNAP_SEG) : 1;
-        for (int k = 0; k < ns; k++) spage.push_back((int32_t)cpage.size());
         sbase.push_back(sbase.back() + ns);
         cpage.push_back((int32_t)i);
         fbase.push_back(fbase.back() + nf);
@@ -975,10 +1097,11 @@ static int prepare(dk_parquet* p) {
   // level tiles and run-table scratch (standard writers emit >= 8 values per hybrid run; a stream
   // with more than num_values / 4 + 64 runs is reported as unsupported)
   {
-    std::vector<DTile> tiles;
+    std::vector<int32_t> tpage;              // tile groups: data pages with levels, in column order
+    std::vector<int64_t> tbase(1, 0);
     int64_t runs_n = 0;
     for (DColumn& c : p->h_cols) {
-      c.first_tile = (int)tiles.size();
+      c.first_tile = (int)tbase.back();
       for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
         DPage& pg = p->h_pages[pi];
         const DChunk& ck = p->h_chunks[pg.chunk];
@@ -990,52 +1113,60 @@ static int prepare(dk_parquet* p) {
         if (ck.max_rep > 0) { pg.run_r = runs_n; runs_n += cap; }
         if (ck.max_def > 0) { pg.run_d = runs_n; runs_n += cap; }
         if (idx) { pg.run_i = runs_n; runs_n += cap; }
-        pg.first_tile = (int)tiles.size();
-        for (int l0 = 0; l0 < nv; l0 += DK_LEVEL_TILE) { DTile tl{}; tl.page = pi; tl.lvl0 = l0; tiles.push_back(tl); }
-        pg.n_tiles = (int)tiles.size() - pg.first_tile;
+        pg.first_tile = (int)tbase.back();
+        pg.n_tiles = (nv + DK_LEVEL_TILE - 1) / DK_LEVEL_TILE;
+        if (pg.n_tiles) { tpage.push_back(pi); tbase.push_back(tbase.back() + pg.n_tiles); }
       }
-      c.n_tiles = (int)tiles.size() - c.first_tile;
+      c.n_tiles = (int)tbase.back() - c.first_tile;
     }
-    p->n_ltiles = (int)tiles.size();
+    p->n_ltiles = (int)tbase.back();
     // string-position chunks of every BYTE_ARRAY PLAIN data page and dictionary page (the region
     // is at most the page body; chunks past the region's end find nothing)
-    std::vector<DPosChunk> pcs;
+    std::vector<int32_t> ppage;
+    std::vector<int64_t> pbase(1, 0);
     for (size_t pi = 0; pi < p->h_pages.size(); pi++) {
       DPage& pg = p->h_pages[pi];
       const DChunk& ck = p->h_chunks[pg.chunk];
-      pg.pchunk0 = (int)pcs.size();
+      pg.pchunk0 = (int)pbase.back();
       pg.npchunk = 0;
       pg.pos_fail = 0;
       if (ck.phys != PT_BYTE_ARRAY || (!(pg.flags & PF_DICT) && pg.enc != ENC_PLAIN)) continue;
       const int64_t body = (pg.unc_off >= 0 ? pg.usize : pg.csize) + 16;
-      for (int64_t b0 = 0; b0 * 16 < body; b0 += DK_POS_CHUNK / 16) { DPosChunk c{}; c.page = (int)pi; c.blk0 = (int32_t)b0; pcs.push_back(c); }
-      pg.npchunk = (int)pcs.size() - pg.pchunk0;
+      pg.npchunk = (int)((body + DK_POS_CHUNK - 1) / DK_POS_CHUNK);
+      ppage.push_back((int32_t)pi);
+      pbase.push_back(pbase.back() + pg.npchunk);
     }
-    p->n_pchunks = (int)pcs.size();
-    if (upload(p->d_pchunks, pcs.data(), pcs.size() * sizeof(DPosChunk), s)) return 1;
-    if (upload(p->d_ltiles, tiles.data(), tiles.size() * sizeof(DTile), s)) return 1;
+    p->n_pchunks = (int)pbase.back();
+    if (expand(p, us, p->d_pchunks, ppage, pbase, EX_POSCHUNK, sizeof(DPosChunk)) ||
+        expand(p, us, p->d_ltiles, tpage, tbase, EX_TILE, sizeof(DTile)))
+      return 1;
     if (p->d_runs.alloc((size_t)(runs_n + 1) * sizeof(Seg))) return 1;
   }
   if (p->d_pos.alloc((size_t)(posn + 16) * 4)) return 1;
   if (p->d_arena.alloc((size_t)arena_n + 256)) return 1;
   p->n_cpages = (int)cpage.size();
-  p->n_frags = (int)fwork.size();
+  p->n_frags = fbase.back();
+  p->h_cpage = cpage; p->h_sbase = sbase; p->h_fbase = fbase;
   if (p->n_cpages) {
-    if (upload(p->d_cpage, cpage.data(), cpage.size() * 4, s) || upload(p->d_fbase, fbase.data(), fbase.size() * 4, s) ||
-        upload(p->d_fwork, fwork.data(), fwork.size() * sizeof(int2), s) || p->d_fstart.alloc(fwork.size() * 8) ||
-        p->d_serial.alloc(cpage.size() * 4) || upload(p->d_sbase, sbase.data(), sbase.size() * 4, s) ||
-        upload(p->d_spage, spage.data(), spage.size() * 4, s) ||
-        p->d_snapws.alloc(spage.size() * 4 * (6 + 2 * DK_SNAP_REC)))
+    std::vector<int64_t> fb(fbase.begin(), fbase.end()), sb(sbase.begin(), sbase.end());
+    std::vector<int32_t> none;
+    if (upload_zc(p, p->d_cpage, cpage.data(), cpage.size() * 4, us) || upload_zc(p, p->d_fbase, fbase.data(), fbase.size() * 4, us) ||
+        expand(p, us, p->d_fwork, none, fb, EX_FRAG, sizeof(int2)) || p->d_fstart.alloc((size_t)p->n_frags * 8) ||
+        p->d_serial.alloc(cpage.size() * 4) || upload_zc(p, p->d_sbase, sbase.data(), sbase.size() * 4, us) ||
+        expand(p, us, p->d_spage, none, sb, EX_SEG, 4) ||
+        p->d_snapws.alloc((size_t)sbase.back() * 4 * (6 + 2 * DK_SNAP_REC)))
       return 1;
-    // page mode: largest pages first (workgroups are dispatched in order; the long serial decodes
-    // start early and the short ones fill in behind them)
-    std::vector<int2> pwork(cpage.size());
-    for (size_t i = 0; i < cpage.size(); i++) pwork[i] = make_int2((int)i, -1);
-    std::stable_sort(pwork.begin(), pwork.end(), [&](const int2& a, const int2& b) {
-      return p->h_pages[cpage[a.x]].usize > p->h_pages[cpage[b.x]].usize;
-    });
-    if (upload(p->d_pwork, pwork.data(), pwork.size() * sizeof(int2), s)) return 1;
-    p->n_segs = (int)spage.size();
+    p->n_segs = sbase.back();
+    if (snap_page_mode(p)) {
+      // page mode: largest pages first (workgroups are dispatched in order; the long serial decodes
+      // start early and the short ones fill in behind them)
+      std::vector<int2> pwork(cpage.size());
+      for (size_t i = 0; i < cpage.size(); i++) pwork[i] = make_int2((int)i, -1);
+      std::stable_sort(pwork.begin(), pwork.end(), [&](const int2& a, const int2& b) {
+        return p->h_pages[cpage[a.x]].usize > p->h_pages[cpage[b.x]].usize;
+      });
+      if (upload_zc(p, p->d_pwork, pwork.data(), pwork.size() * sizeof(int2), us)) return 1;
+    }
     // page mode finds tags through a bitmap built by the speculative walk (DK_SNAP_BITS=0: the
     // in-kernel pointer-doubling discovery instead)
     static const bool bits = !getenv("DK_SNAP_BITS") || atoi(getenv("DK_SNAP_BITS")) != 0;
@@ -1043,18 +1174,50 @@ static int prepare(dk_parquet* p) {
   }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
   p->bytes_arena = arena_n;
-  if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;
-  if (upload(p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), s)) return 1;
+  if (upload_zc(p, p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), us)) return 1;
+  if (upload_zc(p, p->d_pages, p->h_pages.data(), p->h_pages.size() * sizeof(DPage), us)) return 1;
   // 2. count + scan to size the outputs (entries / chars are data dependent)
   for (DColumn& c : p->h_cols) { c.cap_entries = LLONG_MAX; c.cap_chars = LLONG_MAX; c.offs = nullptr; c.row_offs = nullptr; }
-  if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
-  run_pipeline(p, 0);
+  if (upload_zc(p, p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), us)) return 1;
+  {
+    hipEvent_t ev = nullptr;
+    HIPOK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    HIPOK(hipEventRecord(ev, us));
+    HIPOK(hipStreamWaitEvent(s, ev, 0));
+    hipEventDestroy(ev);
+  }
+  p->open_ms[4] = since(t1);            // host: page tables, scratch sizing and allocation
+  const auto t2 = clk::now();
+  // the sizing passes, one slice of files at a time, each as soon as its files' images have landed
+  // (the later files' H2D copies overlap the earlier slices' snappy / level passes); about 1/8 of
+  // the bytes per slice; page mode is never sliced
+  {
+    const int nf = (int)p->files.size();
+    int64_t total = 0;
+    for (const FileM& f : p->files) total += (int64_t)f.bytes.size();
+    static const int want = getenv("DK_OPEN_SLICES") ? std::max(1, atoi(getenv("DK_OPEN_SLICES"))) : 8;
+    const int slices = snap_page_mode(p) ? 1 : want;
+    const int64_t target = std::max<int64_t>(1, total / slices);
+    int f0 = 0;
+    int64_t acc = 0;
+    for (int f = 0; f < nf; f++) {
+      acc += (int64_t)p->files[f].bytes.size();
+      HIPOK(hipStreamWaitEvent(s, p->file_ev[f], 0));
+      if (f + 1 == nf || acc >= target) {
+        sizing_stages(p, s, file_range(p, f0, f + 1));
+        f0 = f + 1;
+        acc = 0;
+      }
+    }
+  }
   std::vector<DColumn> got(p->h_cols.size());
   HIPOK(hipMemcpyAsync(got.data(), p->d_cols.p, got.size() * sizeof(DColumn), hipMemcpyDeviceToHost, s));
   HIPOK(hipMemcpyAsync(p->h_pages.data(), p->d_pages.p, p->h_pages.size() * sizeof(DPage), hipMemcpyDeviceToHost, s));
   HIPOK(hipStreamSynchronize(s));
   std::string m = page_status_msg(p, p->h_pages);
   if (!m.empty()) return fail(m);
+  p->open_ms[5] = since(t2);            // sizing passes on the device (snappy, runs, counts, positions)
+  const auto t3 = clk::now();
   // 3. string-copy tile table (page counts are final after the count pass)
   {
     std::vector<int2> tiles;
@@ -1147,6 +1310,11 @@ static int prepare(dk_parquet* p) {
   if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
   if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;   // dict_hash_off
   HIPOK(hipStreamSynchronize(s));
+  {
+    SyncedRelease drained;              // the zero-copy sources have been read
+    p->staging.clear();
+  }
+  p->open_ms[6] = since(t3);            // host: tile tables + output arena
   p->host.clear();
   p->host.resize(p->h_cols.size());
   p->slice.assign(p->h_cols.size(), HostCol());
@@ -1548,6 +1716,73 @@ extern "C" int dk_parquet_open_sel(dk_engine* e, const char* const* paths, int32
   return parquet_open(e, paths, n_files, leaves, n_leaves, all ? nullptr : &groups, out);
 }
 
+// One file's share of the page / chunk / column tables, built (and its page headers parsed) on the
+// host thread that read the file, with file-local indices; parquet_open concatenates them in file
+// order. Page headers are parsed from the pinned image with the same code the device uses
+// (apply_page_header, dk_thrift.h), so the sizing pass needs no device round trip first.
+struct FileMeta {
+  std::vector<DColumn> cols;
+  std::vector<int> col_leaf;        // projected leaf of each local column
+  std::vector<DChunk> chunks;       // .col: local column; .dict_page: local page
+  std::vector<DPage> pages;         // .chunk: local chunk
+  int64_t bytes_read = 0;
+};
+
+static int build_file_meta(const dk_parquet* p, int fi, const FileM& f, const std::vector<int>& leafidx, FileMeta& M) {
+  const int n_leaves = (int)p->leaves.size();
+  const uint8_t* img = f.bytes.data();
+  const uint8_t* img_end = img + f.bytes.size();
+  for (int li = 0; li < n_leaves; li++) {
+    const int idx = leafidx[li];
+    if (idx < 0) continue;
+    const LeafM& L = f.leaves[idx];
+    if (L.max_rep > 1) return fail("Error reading Parquet file: " + f.path + " (nested repetition not supported: " + L.path + ")");
+    DColumn c{};
+    c.phys = L.phys; c.width = L.phys == PT_BYTE_ARRAY ? 0 : phys_width(L.phys, L.type_length);
+    c.max_def = L.max_def; c.max_rep = L.max_rep; c.rep_def = L.rep_def; c.present = 1;
+    c.key_hash = p->leaves[li] == "add.path";   // the reconciliation key (ActiveAddFilesIterator)
+    c.n_rows = 0;
+    c.first_page = (int)M.pages.size();
+    const int colid = (int)M.cols.size();
+    const int chunk0 = (int)M.chunks.size();
+    // chunks and pages in row-group order; data pages of a column stay contiguous
+    std::vector<DPage> dicts;
+    for (int32_t g : f.sel) {
+      const ColMeta& m = f.rgs[g].cols[idx];
+      c.n_rows += f.rgs[g].num_rows;
+      DChunk ck{};
+      ck.file = p->dfile[fi].as<uint8_t>();
+      ck.col = colid;
+      ck.phys = L.phys; ck.width = c.width; ck.max_def = L.max_def; ck.max_rep = L.max_rep; ck.rep_def = L.rep_def;
+      ck.codec = m.codec; ck.dict_page = -1; ck.dict_pos = 0;
+      const int chunk_id = (int)M.chunks.size();
+      std::vector<PageRef> refs;
+      if (enumerate_pages(f, m, refs)) return 1;
+      M.bytes_read += m.total_compressed;
+      for (const PageRef& r : refs) {
+        DPage pg{};
+        const uint8_t* hp = span_ptr(f, r.hdr_off, 1);
+        if (!hp) return fail("Error reading Parquet file: " + f.path + " (page outside its column chunk)");
+        pg.hdr_off = hp - img; pg.chunk = chunk_id; pg.flags = r.dict ? PF_DICT : 0; pg.unc_off = -1;
+        apply_page_header(pg, ck, img, img_end);
+        if (r.dict) { ck.dict_page = -2 - (int)dicts.size(); dicts.push_back(pg); }
+        else M.pages.push_back(pg);
+      }
+      M.chunks.push_back(ck);
+    }
+    c.n_pages = (int)M.pages.size() - c.first_page;
+    // dictionary pages go after the data pages (they are not part of the column's page range)
+    for (size_t d = 0; d < dicts.size(); d++) {
+      const int at = (int)M.pages.size();
+      for (size_t k = chunk0; k < M.chunks.size(); k++) if (M.chunks[k].dict_page == -2 - (int)d) M.chunks[k].dict_page = at;
+      M.pages.push_back(dicts[d]);
+    }
+    M.cols.push_back(c);
+    M.col_leaf.push_back(li);
+  }
+  return 0;
+}
+
 static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
                         const int32_t* field_ids) {
@@ -1557,7 +1792,8 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->eng = e;
   if (p->own.create()) return 1;
   p->stream = p->own.s;
-  for (int k = 0; k < kCopyStreams; k++) {
+  if (p->aux.create()) return 1;
+  for (int k = 0; k < copy_streams(); k++) {
     if (p->copy[k].create()) return 1;
     HIPOK(hipEventCreateWithFlags(&p->copy_done[k].e, hipEventDisableTiming));
   }
@@ -1571,6 +1807,9 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   // host I/O in parallel over files (footer, row-group selection, projected column chunks):
   // DefaultParquetHandler reads files one after another; here every file of the call is in flight
   std::vector<std::string> errs(n_files > 0 ? n_files : 0);
+  std::vector<FileMeta> metas(n_files > 0 ? n_files : 0);
+  p->file_ev.resize(n_files > 0 ? n_files : 0);
+  for (auto& ev : p->file_ev) HIPOK(hipEventCreateWithFlags(&ev.e, hipEventDisableTiming));
   const auto t_io0 = std::chrono::steady_clock::now();
   parallel_for(n_files, [&](int fi) {
     FileM& f = p->files[fi];
@@ -1595,72 +1834,46 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
     // while the rest of it (and the other files) are still being read
     hipSetDevice(e->cfg.device);
     if (p->dfile[fi].alloc(f.bytes.size() + 256)) { errs[fi] = g_err; return; }
-    hipStream_t cs = p->copy[fi % kCopyStreams].s;
+    hipStream_t cs = p->copy[fi % copy_streams()].s;
     uint8_t* dst = p->dfile[fi].as<uint8_t>();
     if (read_spans_into(f, (size_t)8 << 20, [&](size_t off, size_t len) {
           return hipMemcpyAsync(dst + off, f.bytes.data() + off, len, hipMemcpyHostToDevice, cs) == hipSuccess
                      ? 0 : fail("hipMemcpyAsync failed for " + f.path);
-        }))
-      errs[fi] = g_err;
+        })) { errs[fi] = g_err; return; }
+    if (hipEventRecord(p->file_ev[fi], cs) != hipSuccess) { errs[fi] = "hipEventRecord failed"; return; }
+    // its pages and headers while the copies run
+    if (build_file_meta(p.get(), fi, f, p->leafidx[fi], metas[fi])) errs[fi] = g_err;
   });
-  // the decode stream starts after every copy
-  for (int k = 0; k < kCopyStreams; k++) {
-    HIPOK(hipEventRecord(p->copy_done[k], p->copy[k].s));
-    HIPOK(hipStreamWaitEvent(p->stream, p->copy_done[k], 0));
-  }
+  // (the decode stream waits for each file's copies in prepare, slice by slice)
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
   const auto t_io1 = std::chrono::steady_clock::now();
-  for (int fi = 0; fi < n_files; fi++) {
-    FileM& f = p->files[fi];
-    for (int li = 0; li < n_leaves; li++) {
-      const int idx = p->leafidx[fi][li];
-      if (idx < 0) continue;
-      const LeafM& L = f.leaves[idx];
-      if (L.max_rep > 1) return fail("Error reading Parquet file: " + f.path + " (nested repetition not supported: " + L.path + ")");
-      DColumn c{};
-      c.phys = L.phys; c.width = L.phys == PT_BYTE_ARRAY ? 0 : phys_width(L.phys, L.type_length);
-      c.max_def = L.max_def; c.max_rep = L.max_rep; c.rep_def = L.rep_def; c.present = 1;
-      c.key_hash = p->leaves[li] == "add.path";   // the reconciliation key (ActiveAddFilesIterator)
-      c.n_rows = 0;
-      c.first_page = (int)p->h_pages.size();
-      int colid = (int)p->h_cols.size();
-      // chunks and pages in row-group order; data pages of a column stay contiguous
-      std::vector<DPage> dicts;
-      for (int32_t g : f.sel) {
-        const ColMeta& m = f.rgs[g].cols[idx];
-        c.n_rows += f.rgs[g].num_rows;
-        DChunk ck{};
-        ck.file = p->dfile[fi].as<uint8_t>();
-        ck.col = colid;
-        ck.phys = L.phys; ck.width = c.width; ck.max_def = L.max_def; ck.max_rep = L.max_rep; ck.rep_def = L.rep_def;
-        ck.codec = m.codec; ck.dict_page = -1; ck.dict_pos = 0;
-        int chunk_id = (int)p->h_chunks.size();
-        std::vector<PageRef> refs;
-        if (enumerate_pages(f, m, refs)) return 1;
-        p->bytes_read += m.total_compressed;
-        for (const PageRef& r : refs) {
-          DPage pg{};
-          const uint8_t* hp = span_ptr(f, r.hdr_off, 1);
-          if (!hp) return fail("Error reading Parquet file: " + f.path + " (page outside its column chunk)");
-          pg.hdr_off = hp - f.bytes.data(); pg.chunk = chunk_id; pg.flags = r.dict ? PF_DICT : 0; pg.unc_off = -1;
-          if (r.dict) { ck.dict_page = -2 - (int)dicts.size(); dicts.push_back(pg); }
-          else p->h_pages.push_back(pg);
-        }
-        p->h_chunks.push_back(ck);
-      }
-      c.n_pages = (int)p->h_pages.size() - c.first_page;
-      // dictionary pages go after the data pages (they are not part of the column's page range)
-      for (size_t d = 0; d < dicts.size(); d++) {
-        int at = (int)p->h_pages.size();
-        for (DChunk& ck : p->h_chunks) if (ck.col == colid && ck.dict_page == -2 - (int)d) ck.dict_page = at;
-        p->h_pages.push_back(dicts[d]);
-      }
-      p->colmap[fi][li] = colid;
+  for (int fi = 0; fi < n_files; fi++) {             // concatenate the files' tables in file order
+    FileMeta& M = metas[fi];
+    const int col0 = (int)p->h_cols.size(), chunk0 = (int)p->h_chunks.size(), page0 = (int)p->h_pages.size();
+    p->file_page0.push_back(page0);
+    p->file_col0.push_back(col0);
+    for (size_t k = 0; k < M.cols.size(); k++) {
+      DColumn c = M.cols[k];
+      c.first_page += page0;
+      p->colmap[fi][M.col_leaf[k]] = col0 + (int)k;
       p->h_cols.push_back(c);
       p->col_file.push_back(fi);
     }
+    for (DChunk ck : M.chunks) {
+      ck.col += col0;
+      if (ck.dict_page >= 0) ck.dict_page += page0;
+      p->h_chunks.push_back(ck);
+    }
+    for (DPage pg : M.pages) {
+      pg.chunk += chunk0;
+      p->h_pages.push_back(pg);
+    }
+    p->bytes_read += M.bytes_read;
+    M = FileMeta();
   }
+  p->file_page0.push_back((int)p->h_pages.size());
+  p->file_col0.push_back((int)p->h_cols.size());
   p->n_pages = (int)p->h_pages.size();
   p->n_cols = (int)p->h_cols.size();
   const auto t_h2d = std::chrono::steady_clock::now();
@@ -1721,8 +1934,8 @@ extern "C" int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file) {
   return p->files[file].row0;
 }
 
-extern "C" int dk_parquet_open_ms(dk_parquet* p, double out[3]) {
-  for (int i = 0; i < 3; i++) out[i] = p->open_ms[i];
+extern "C" int dk_parquet_open_ms(dk_parquet* p, double out[7]) {
+  for (int i = 0; i < 7; i++) out[i] = p->open_ms[i];
   return 0;
 }
 
@@ -1929,6 +2142,8 @@ extern "C" void dk_parquet_close(dk_parquet* p) {
   if (!p) return;
   hipSetDevice(p->eng->cfg.device);
   hipStreamSynchronize(p->stream);
+  for (int k = 0; k < kCopyStreams; k++) if (p->copy[k].s) hipStreamSynchronize(p->copy[k].s);
+  SyncedRelease drained;                 // every buffer below is idle: back to the caches for reuse
   delete p;
 }
 
@@ -2511,16 +2726,85 @@ static const DColumn* find_col(dk_parquet* p, int fi, const char* leaf) {
   return nullptr;
 }
 
+// The checkpoint half of a replay: selection buffers, probe columns, partition maps and stats rows
+// of every checkpoint file. Separate from the commit-tail half so that the tail's action table and
+// key table are built while the checkpoint files are still being read (dk_replay_attach_checkpoint).
+static int replay_attach(dk_replay* r, dk_parquet* ckpt) {
+  r->ck = ckpt;
+  if (hipEventCreateWithFlags(&r->ev_in, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&r->ev_out, hipEventDisableTiming) != hipSuccess)
+    return fail("hipEventCreate failed");
+  if (ckpt) {
+    int64_t max_rows = 1, total = 0;
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      max_rows = std::max<int64_t>(max_rows, ckpt->files[fi].num_rows);
+      total += ckpt->files[fi].num_rows;
+    }
+    // every file in one probe launch while global row numbers fit the int32 candidate list
+    static const bool per_file = getenv("DK_PROBE_PER_FILE") && atoi(getenv("DK_PROBE_PER_FILE"));
+    r->probe_all = !per_file && ckpt->files.size() > 1 && total < (1ll << 31) - 1;
+    if (r->d_cand.alloc((size_t)(r->probe_all ? total : max_rows) * 4 + 64)) return 1;
+    if (r->d_cand_n.alloc(64)) return 1;
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      ProbeCols pc{};
+      const DColumn* path = find_col(ckpt, (int)fi, "add.path");
+      pc.n_rows = ckpt->files[fi].num_rows;
+      r->d_csel.emplace_back(new DBuf());
+      if (r->d_csel.back()->alloc(pc.n_rows + 16)) return 1;
+      if (!path) { pc.n_rows = 0; r->probe.push_back(pc); continue; }
+      if (path->phys != PT_BYTE_ARRAY || path->max_rep) return fail("add.path has an unexpected type");
+      pc.path_def = path->row_def; pc.path_offs = path->offs; pc.path_chars = path->chars;
+      pc.path_hash = path->hash;
+      const DColumn* st = find_col(ckpt, (int)fi, "add.deletionVector.storageType");
+      const DColumn* pid = find_col(ckpt, (int)fi, "add.deletionVector.pathOrInlineDv");
+      const DColumn* off = find_col(ckpt, (int)fi, "add.deletionVector.offset");
+      if (st && pid) {
+        pc.has_dv = 1;
+        pc.st_def = st->row_def; pc.st_offs = st->offs; pc.st_chars = st->chars;
+        pc.pid_offs = pid->offs; pc.pid_chars = pid->chars;
+        if (off) { pc.off_def = off->row_def; pc.off_vals = (const int32_t*)off->fixed; pc.off_maxdef = off->max_def; }
+      }
+      r->probe.push_back(pc);
+    }
+  }
+  if (ckpt) {
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      MapRows M{};
+      const DColumn* kc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.key");
+      const DColumn* vc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.value");
+      if (kc && vc && kc->row_offs && kc->offs && vc->entry_def && vc->offs) {
+        M.n = ckpt->files[fi].num_rows;
+        M.row_def = kc->row_def; M.rep_def = kc->rep_def; M.v_max_def = vc->max_def;
+        M.row_offs = kc->row_offs; M.k_offs = kc->offs; M.k_chars = kc->chars;
+        M.v_def = vc->entry_def; M.v_offs = vc->offs; M.v_chars = vc->chars;
+      } else {                  // no map entry anywhere (or no map leaf): every field is null
+        M.n = ckpt->files[fi].num_rows;
+      }
+      r->ck_maps.push_back(M);
+    }
+  }
+  if (ckpt) {
+    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+      StatsRows R{};
+      const DColumn* sc = find_col(ckpt, (int)fi, "add.stats");
+      if (sc && !sc->null_only && sc->offs) {
+        R.n = ckpt->files[fi].num_rows;
+        R.row_def = sc->row_def; R.max_def = sc->max_def;
+        R.offs = sc->offs; R.chars = sc->chars;
+      }
+      r->ck_stats.push_back(R);
+    }
+  }
+  return 0;
+}
+
 extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_replay** out) {
   if (!e) return fail("null engine");
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_replay> r(new dk_replay());
-  r->eng = e; r->tail = tail; r->ck = ckpt;
+  r->eng = e; r->tail = tail;
   if (r->own.create()) return 1;
   r->stream = r->own.s;
-  if (ckpt && (hipEventCreateWithFlags(&r->ev_in, hipEventDisableTiming) != hipSuccess ||
-               hipEventCreateWithFlags(&r->ev_out, hipEventDisableTiming) != hipSuccess))
-    return fail("hipEventCreate failed");
   r->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
   hipStream_t s = r->stream;
   // actions: removes and adds of each tail row (a row may carry both)
@@ -2568,39 +2852,6 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   if (r->d_fp.alloc(cap * sizeof(uint32_t))) return 1;
   if (r->d_state.alloc(sizeof(DState))) return 1;
   if (r->d_jsel.alloc(na + 16)) return 1;
-  if (ckpt) {
-    int64_t max_rows = 1, total = 0;
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      max_rows = std::max<int64_t>(max_rows, ckpt->files[fi].num_rows);
-      total += ckpt->files[fi].num_rows;
-    }
-    // every file in one probe launch while global row numbers fit the int32 candidate list
-    static const bool per_file = getenv("DK_PROBE_PER_FILE") && atoi(getenv("DK_PROBE_PER_FILE"));
-    r->probe_all = !per_file && ckpt->files.size() > 1 && total < (1ll << 31) - 1;
-    if (r->d_cand.alloc((size_t)(r->probe_all ? total : max_rows) * 4 + 64)) return 1;
-    if (r->d_cand_n.alloc(64)) return 1;
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      ProbeCols pc{};
-      const DColumn* path = find_col(ckpt, (int)fi, "add.path");
-      pc.n_rows = ckpt->files[fi].num_rows;
-      r->d_csel.emplace_back(new DBuf());
-      if (r->d_csel.back()->alloc(pc.n_rows + 16)) return 1;
-      if (!path) { pc.n_rows = 0; r->probe.push_back(pc); continue; }
-      if (path->phys != PT_BYTE_ARRAY || path->max_rep) return fail("add.path has an unexpected type");
-      pc.path_def = path->row_def; pc.path_offs = path->offs; pc.path_chars = path->chars;
-      pc.path_hash = path->hash;
-      const DColumn* st = find_col(ckpt, (int)fi, "add.deletionVector.storageType");
-      const DColumn* pid = find_col(ckpt, (int)fi, "add.deletionVector.pathOrInlineDv");
-      const DColumn* off = find_col(ckpt, (int)fi, "add.deletionVector.offset");
-      if (st && pid) {
-        pc.has_dv = 1;
-        pc.st_def = st->row_def; pc.st_offs = st->offs; pc.st_chars = st->chars;
-        pc.pid_offs = pid->offs; pc.pid_chars = pid->chars;
-        if (off) { pc.off_def = off->row_def; pc.off_vals = (const int32_t*)off->fixed; pc.off_maxdef = off->max_def; }
-      }
-      r->probe.push_back(pc);
-    }
-  }
   // partitionValues maps for partition pruning: the tail's (rows mapped from add actions) and the
   // checkpoint's decoded key / value leaves
   auto up = [&](const void* src, size_t n) -> void* {
@@ -2629,22 +2880,6 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
       return 1;
     r->tail_maps = M;
   }
-  if (ckpt) {
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      MapRows M{};
-      const DColumn* kc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.key");
-      const DColumn* vc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.value");
-      if (kc && vc && kc->row_offs && kc->offs && vc->entry_def && vc->offs) {
-        M.n = ckpt->files[fi].num_rows;
-        M.row_def = kc->row_def; M.rep_def = kc->rep_def; M.v_max_def = vc->max_def;
-        M.row_offs = kc->row_offs; M.k_offs = kc->offs; M.k_chars = kc->chars;
-        M.v_def = vc->entry_def; M.v_offs = vc->offs; M.v_chars = vc->chars;
-      } else {                  // no map entry anywhere (or no map leaf): every field is null
-        M.n = ckpt->files[fi].num_rows;
-      }
-      r->ck_maps.push_back(M);
-    }
-  }
   // stats strings for data skipping: the tail's per action (adds only), the checkpoint's column
   if (tail && tail->with_stats) {
     const CB& sc = tail->col[JL_STATS];
@@ -2660,22 +2895,19 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
     if (upload(r->d_tstats_off, soff.data(), soff.size() * 8, s)) return 1;
     if (upload(r->d_tstats_len, slen.data(), slen.size() * 4, s)) return 1;
   }
-  if (ckpt) {
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      StatsRows R{};
-      const DColumn* sc = find_col(ckpt, (int)fi, "add.stats");
-      if (sc && !sc->null_only && sc->offs) {
-        R.n = ckpt->files[fi].num_rows;
-        R.row_def = sc->row_def; R.max_def = sc->max_def;
-        R.offs = sc->offs; R.chars = sc->chars;
-      }
-      r->ck_stats.push_back(R);
-    }
-  }
   HIPOK(hipStreamSynchronize(s));
+  if (ckpt && replay_attach(r.get(), ckpt)) return 1;
   *out = r.release();
   return 0;
 }
+
+extern "C" int dk_replay_attach_checkpoint(dk_replay* r, dk_parquet* ckpt) {
+  if (!r || !ckpt) return fail("dk_replay_attach_checkpoint: null argument");
+  if (r->ck) return fail("dk_replay_attach_checkpoint: a checkpoint is already attached");
+  hipSetDevice(r->eng->cfg.device);
+  return replay_attach(r, ckpt);
+}
+
 
 extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog) {
   static_assert(sizeof(dk_skip_program) == sizeof(DSkipProg), "dk_skip_program layout");
@@ -3094,6 +3326,7 @@ extern "C" void dk_replay_free(dk_replay* r) {
   hipStreamSynchronize(r->stream);
   if (r->ev_in) hipEventDestroy(r->ev_in);
   if (r->ev_out) hipEventDestroy(r->ev_out);
+  SyncedRelease drained;
   delete r;
 }
 

@@ -154,22 +154,7 @@ __global__ void k_page_headers(const DChunk* __restrict__ chunks, DPage* __restr
   if (i >= n_pages) return;
   DPage pg = pages[i];
   const DChunk& ck = chunks[pg.chunk];
-  const uint8_t* p = ck.file + pg.hdr_off;
-  // headers are small; bound the parse to 64 KiB (large min/max statistics are skipped)
-  PageHeader h = parse_page_header(p, p + 65536);
-  pg.status = PS_OK;
-  if (!h.ok) pg.status = PS_BAD_HEADER;
-  pg.ptype = h.type; pg.enc = h.enc; pg.num_values = h.num_values; pg.dl_len = h.dl_len; pg.rl_len = h.rl_len;
-  pg.csize = h.csize; pg.usize = h.usize; pg.hdr_len = h.hdr_len; pg.is_comp = h.is_comp;
-  pg.data_off = pg.hdr_off + h.hdr_len;
-  if (h.ok) {
-    bool dict = (pg.flags & PF_DICT) != 0;
-    if (dict != (h.type == PAGE_DICT)) pg.status = PS_BAD_HEADER;
-    if (!dict && h.type != PAGE_DATA && h.type != PAGE_DATA_V2) pg.status = PS_UNSUPPORTED;
-    if (h.type == PAGE_DATA && ((ck.max_def > 0 && h.dl_enc != ENC_RLE) || (ck.max_rep > 0 && h.rl_enc != ENC_RLE)))
-      pg.status = PS_UNSUPPORTED;
-    if (ck.codec != CODEC_NONE && pg.unc_off < 0 && !(h.type == PAGE_DATA_V2 && !h.is_comp)) pg.status = PS_UNSUPPORTED;
-  }
+  apply_page_header(pg, ck, ck.file, nullptr);
   pages[i] = pg;
 }
 
@@ -421,8 +406,8 @@ __device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_
 }
 
 __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
-  const int k = blockIdx.x * NT + threadIdx.x;
-  if (k >= X.nseg) return;
+  const int k = X.k0 + blockIdx.x * NT + threadIdx.x;
+  if (k >= X.k1) return;
   const int ci = X.spage[k];
   const int j = k - X.sbase[ci];
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
@@ -482,8 +467,8 @@ __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, co
 }
 
 __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
-  const int k = blockIdx.x * NT + threadIdx.x;
-  if (k >= X.nseg) return;
+  const int k = X.k0 + blockIdx.x * NT + threadIdx.x;
+  if (k >= X.k1) return;
   const int ci = X.spage[k];
   const int j = k - X.sbase[ci];
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
@@ -529,7 +514,7 @@ __device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets 
 }
 
 __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
-  const int ci = blockIdx.x, lane = threadIdx.x;
+  const int ci = X.c0 + blockIdx.x, lane = threadIdx.x;
   __shared__ int16_t TPF[64];               // bitmap boundary walk: offsets of a step's tags
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
   if (!snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
@@ -3697,6 +3682,54 @@ __global__ __launch_bounds__(NT) void k_probe_cand_all(ProbeSet PS, const Slot* 
 // ------------------------------------------------------------------------------------------------
 namespace dk {
 
+// Work-list expansion: group g owns items [base[g], base[g + 1]); item k of the group becomes a
+// level tile (page gid[g], levels from k * DK_LEVEL_TILE), a string-position chunk (page gid[g], from
+// block k * DK_POS_CHUNK / 16), a snappy fragment (compressed page g, fragment k) or a segment's
+// owner (compressed page g). One workgroup per group; the host keeps only the prefix arrays.
+__global__ void k_expand(const int64_t* __restrict__ base, const int32_t* __restrict__ gid, int n, int kind,
+                         void* __restrict__ out) {
+  const int g = blockIdx.x;
+  if (g >= n) return;
+  const int64_t b = base[g], e = base[g + 1];
+  const int32_t id = gid ? gid[g] : g;
+  for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) {
+    const int32_t k = (int32_t)(i - b);
+    if (kind == EX_TILE) {
+      DTile t{};
+      t.page = id; t.lvl0 = k * DK_LEVEL_TILE;
+      ((DTile*)out)[i] = t;
+    } else if (kind == EX_POSCHUNK) {
+      DPosChunk c{};
+      c.page = id; c.blk0 = k * (DK_POS_CHUNK / 16);
+      ((DPosChunk*)out)[i] = c;
+    } else if (kind == EX_FRAG) {
+      ((int2*)out)[i] = make_int2(id, k);
+    } else {
+      ((int32_t*)out)[i] = id;
+    }
+  }
+}
+void launch_expand(const int64_t* base, const int32_t* gid, int n, int kind, void* out, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_expand, dim3(n), dim3(64), 0, s, base, gid, n, kind, out);
+}
+
+// Host-to-device copy by a kernel reading pinned host memory over PCIe: table uploads that must not
+// queue behind the file images on the DMA engines (prepare runs while those copies are in flight)
+__global__ void k_copy_zc(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, long long n) {
+  const long long n16 = n >> 4;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += step)
+    ((uint4*)dst)[i] = ((const uint4*)src)[i];
+  for (long long i = (n16 << 4) + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) dst[i] = src[i];
+}
+void launch_copy_zc(void* dst, const void* src, long long n, hipStream_t s) {
+  if (n <= 0) return;
+  long long blocks = ((n >> 4) + 255) / 256;
+  if (blocks < 1) blocks = 1;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_copy_zc, dim3((unsigned)blocks), dim3(256), 0, s, (uint8_t*)dst, (const uint8_t*)src, n);
+}
+
 void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_headers, dim3((n + 255) / 256), dim3(256), 0, s, c, p, n, nullptr);
 }
@@ -3714,13 +3747,15 @@ static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s
 // phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback; n_frag < 0: page mode
 // (work holds one (page, -1) item per compressed page; phases 0 and 1 only build the tag-start
 // bitmap, when X.tbits is set)
+// The compressed pages [X.c0, X.c0 + n_cp) with their segments [X.k0, X.k1) and fragment work items
+// work[0, n_frag) (n_frag < 0: page mode, work = one item per page)
 void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int phase, hipStream_t s) {
   if (!n_cp) return;
-  const int g = (X.nseg + NT - 1) / NT;
+  const int g = (X.k1 - X.k0 + NT - 1) / NT;
   if (n_frag < 0) {
     if (phase == 0) {
-      (void)hipMemsetAsync(X.serial, 0, (size_t)n_cp * 4, s);
-      if (X.tbits) {                      // tag-start bitmap: speculative walk + link
+      (void)hipMemsetAsync(X.serial + X.c0, 0, (size_t)n_cp * 4, s);
+      if (X.tbits && g > 0) {             // tag-start bitmap: speculative walk + link
         hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
         hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
       }
@@ -3729,29 +3764,32 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
     } else if (phase == 2) launch_frag(X, n_cp, work, s);
     else if (phase == 3)
       hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
-                         X.cpage, (const int32_t*)X.serial);
+                         X.cpage + X.c0, (const int32_t*)X.serial + X.c0);
     return;
   }
   if (phase == 0) {
-    hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
-    hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+    if (g > 0) {
+      hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
+      hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+    }
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
   } else if (phase == 2) {
     if (n_frag) launch_frag(X, n_frag, work, s);
   } else {
     hipLaunchKernelGGL(k_snappy_serial, dim3(n_cp), dim3(64), 0, s, X.chunks, const_cast<DPage*>(X.pages), X.arena,
-                       X.cpage, (const int32_t*)X.serial);
+                       X.cpage + X.c0, (const int32_t*)X.serial + X.c0);
   }
 }
-void launch_positions(const DChunk* c, DPage* p, int n_pages, const uint8_t* arena, int32_t* pos, DPosChunk* pcs,
-                      int npc, hipStream_t s) {
+// string positions of pages [page0, page0 + n_pages) whose chunks are pcs[pc0, pc0 + npc)
+void launch_positions(const DChunk* c, DPage* p, int page0, int n_pages, const uint8_t* arena, int32_t* pos,
+                      DPosChunk* pcs, int pc0, int npc, hipStream_t s) {
   if (!npc) return;
-  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs);
-  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p, arena, pos, pcs);
-  hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs);
-  hipLaunchKernelGGL(k_pos_verify, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs);
-  hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p, n_pages, arena, pos);
+  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
+  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
+  hipLaunchKernelGGL(k_pos_verify, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
+  hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos);
 }
 void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_runs, dim3((n + 63) / 64), dim3(64), 0, s, c, p, n, arena, runs);

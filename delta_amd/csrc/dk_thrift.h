@@ -173,4 +173,25 @@ DK_HD PageHeader parse_page_header(const uint8_t* p, const uint8_t* e) {
   return h;
 }
 
+// A page header into its DPage, with the checks k_page_headers and the host open share: the parse
+// is bounded by 64 KiB and by `end` (large min / max statistics are skipped).
+DK_HD inline void apply_page_header(DPage& pg, const DChunk& ck, const uint8_t* base, const uint8_t* end) {
+  const uint8_t* p = base + pg.hdr_off;
+  const uint8_t* e = (end && end - p < 65536) ? end : p + 65536;
+  PageHeader h = parse_page_header(p, e);
+  pg.status = PS_OK;
+  if (!h.ok) pg.status = PS_BAD_HEADER;
+  pg.ptype = h.type; pg.enc = h.enc; pg.num_values = h.num_values; pg.dl_len = h.dl_len; pg.rl_len = h.rl_len;
+  pg.csize = h.csize; pg.usize = h.usize; pg.hdr_len = h.hdr_len; pg.is_comp = h.is_comp;
+  pg.data_off = pg.hdr_off + h.hdr_len;
+  if (h.ok) {
+    bool dict = (pg.flags & PF_DICT) != 0;
+    if (dict != (h.type == PAGE_DICT)) pg.status = PS_BAD_HEADER;
+    if (!dict && h.type != PAGE_DATA && h.type != PAGE_DATA_V2) pg.status = PS_UNSUPPORTED;
+    if (h.type == PAGE_DATA && ((ck.max_def > 0 && h.dl_enc != ENC_RLE) || (ck.max_rep > 0 && h.rl_enc != ENC_RLE)))
+      pg.status = PS_UNSUPPORTED;
+    if (ck.codec != CODEC_NONE && pg.unc_off < 0 && !(h.type == PAGE_DATA_V2 && !h.is_comp)) pg.status = PS_UNSUPPORTED;
+  }
+}
+
 }  // namespace dk

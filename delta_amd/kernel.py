@@ -1095,9 +1095,64 @@ class GpuScan:
         t0 = time.perf_counter()
         seg = self.snapshot.log_segment
         commits = list(reversed(seg.deltas))
-        self.tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
-        t1 = time.perf_counter()
-        self.prepare_ms = {"commit_tail": (t1 - t0) * 1e3}
+        # the commit tail is parsed (host threads, GIL released in the library) while the checkpoint
+        # files are opened below; its errors still surface first, as in the reference's replay order
+        import threading
+        tail_box = {}
+
+        def parse_tail():
+            # the tail, then the replay's commit-tail half (action table + key-table inputs)
+            t = time.perf_counter()
+            try:
+                tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
+                tail_box["tail"] = tail
+                tail_box["ms"] = (time.perf_counter() - t) * 1e3
+                t = time.perf_counter()
+                rh = C.c_void_p()
+                check(lib().dk_replay_create(engine._h, tail._h, None, C.byref(rh)))
+                tail_box["rh"] = rh
+                tail_box["create_ms"] = (time.perf_counter() - t) * 1e3
+            except BaseException as e:          # re-raised on the calling thread
+                tail_box["error"] = e
+
+        tail_thread = threading.Thread(target=parse_tail, daemon=True)
+        tail_thread.start()
+        try:
+            self._prepare_checkpoint(engine, t0)
+        except BaseException as e:
+            tail_thread.join()
+            self.tail = tail_box.get("tail")        # freed by close()
+            self._rh = tail_box.get("rh")
+            if "error" in tail_box:
+                raise tail_box["error"]
+            raise e
+        tail_thread.join()
+        if "tail" in tail_box:
+            self.tail = tail_box["tail"]
+        if "rh" in tail_box:
+            self._rh = tail_box["rh"]
+        if "error" in tail_box:
+            raise tail_box["error"]
+        self.prepare_ms["commit_tail"] = tail_box["ms"]
+        self.prepare_ms["replay_create_tail"] = tail_box["create_ms"]
+        t3 = time.perf_counter()
+        if self.ckpt is not None:
+            check(lib().dk_replay_attach_checkpoint(self._rh, self.ckpt._h))
+        self.prepare_ms["replay_attach"] = (time.perf_counter() - t3) * 1e3
+        if self.partition is not None:
+            from . import partitions as pp
+            pprog = pp.pack(self.partition, dk_part_program)
+            check(lib().dk_replay_set_partition_filter(self._rh, C.byref(pprog)))
+        if self.skipping is not None:
+            from . import skipping as sk
+            prog = sk.pack(self.skipping[1:], dk_skip_program)
+            check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
+        return self
+
+    def _prepare_checkpoint(self, engine, t1):
+        """Plan the checkpoint files (row-group pruning, shards) and open them (host read + H2D +
+        the device sizing passes)."""
+        self.prepare_ms = {}
         all_files, prunable = self.snapshot._checkpoint_files(engine, with_pruning=True)
         # row groups read per file: all, minus those the checkpoint predicate (the partition filter
         # on add.partitionValues_parsed) proves empty in multi-part parts and sidecars
@@ -1137,24 +1192,13 @@ class GpuScan:
         t2 = time.perf_counter()
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel) if self.ckpt_files else None
         t3 = time.perf_counter()
-        self._rh = C.c_void_p()
-        check(lib().dk_replay_create(engine._h, self.tail._h, self.ckpt._h if self.ckpt else None,
-                                     C.byref(self._rh)))
-        self.prepare_ms.update({"plan_files": (t2 - t1) * 1e3, "checkpoint_open": (t3 - t2) * 1e3,
-                                "replay_create": (time.perf_counter() - t3) * 1e3})
+        self.prepare_ms.update({"plan_files": (t2 - t1) * 1e3, "checkpoint_open": (t3 - t2) * 1e3})
         if self.ckpt is not None:
-            om = (C.c_double * 3)()
+            om = (C.c_double * 7)()
             check(lib().dk_parquet_open_ms(self.ckpt._h, om))
-            self.prepare_ms.update({"open_read_h2d": om[0], "open_metadata": om[1], "open_prepare": om[2]})
-        if self.partition is not None:
-            from . import partitions as pp
-            pprog = pp.pack(self.partition, dk_part_program)
-            check(lib().dk_replay_set_partition_filter(self._rh, C.byref(pprog)))
-        if self.skipping is not None:
-            from . import skipping as sk
-            prog = sk.pack(self.skipping[1:], dk_skip_program)
-            check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
-        return self
+            self.prepare_ms.update({"open_read_h2d": om[0], "open_metadata": om[1], "open_prepare": om[2],
+                                    "prep_h2d_headers": om[3], "prep_host_pages": om[4], "prep_device_sizing": om[5],
+                                    "prep_host_tiles_alloc": om[6]})
 
     def getRemainingFilter(self):
         """ScanImpl.getRemainingFilter (:221-223): the data filter, which skipping never fully

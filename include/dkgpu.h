@@ -137,8 +137,10 @@ int  dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, int32_t min
 /* D2H copy of rows [row0, row0+n) of one decoded column; row_offs / offs rebased to the slice
  * (valid until the next call for the same column or close). */
 int  dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf, int64_t row0, int64_t n, dk_column* out);
-/* wall ms of the open's phases: host read (+ H2D issue), page metadata, prepare passes (sizing) */
-int  dk_parquet_open_ms(dk_parquet* p, double out[3]);
+/* wall ms of the open's phases: host read (+ H2D issue), page metadata, prepare passes (sizing);
+ * then inside prepare: H2D completion + page headers, host page tables, device sizing passes, host
+ * tile tables + output arena */
+int  dk_parquet_open_ms(dk_parquet* p, double out[7]);
 /* bytes read (projected column chunks) and written (decoded buffers) per decode, for roofline */
 int  dk_parquet_traffic(dk_parquet* p, int64_t* bytes_read, int64_t* bytes_written);
 /* algorithmic bytes one launch of a decode kernel must move ("k_string_copy", "k_tile_decode") */
@@ -294,6 +296,10 @@ typedef struct dk_part_program {
  * ckpt may be NULL (no checkpoint). Checkpoint files are given in replay order (multi-part:
  * descending part number, LogSegment.java:171-177). */
 int  dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_replay** out);
+/* The same in two halves: dk_replay_create(e, tail, NULL, &r) builds the commit-tail half (action
+ * table, key table inputs) -- e.g. while the checkpoint files are still being opened -- and this
+ * attaches the checkpoint afterwards (once per replay). */
+int  dk_replay_attach_checkpoint(dk_replay* r, dk_parquet* ckpt);
 /* install (prog != NULL) or clear the data-skipping program applied after reconciliation; the
  * tail must have been parsed with stats and the checkpoint projection must include add.stats */
 int  dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog);
