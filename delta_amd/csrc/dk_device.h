@@ -1,5 +1,6 @@
 // Device-side data model shared by the host orchestration (dk_host.cpp) and the kernels.
 #pragma once
+#define DK_DEVICE_TYPES 1   // dk_thrift.h's apply_page_header needs DPage / DChunk
 #include <stdint.h>
 
 namespace dk {

@@ -173,9 +173,10 @@ DK_HD PageHeader parse_page_header(const uint8_t* p, const uint8_t* e) {
   return h;
 }
 
+#ifdef DK_DEVICE_TYPES
 // A page header into its DPage, with the checks k_page_headers and the host open share: the parse
 // is bounded by 64 KiB and by `end` (large min / max statistics are skipped).
-DK_HD inline void apply_page_header(DPage& pg, const DChunk& ck, const uint8_t* base, const uint8_t* end) {
+DK_HD void apply_page_header(DPage& pg, const DChunk& ck, const uint8_t* base, const uint8_t* end) {
   const uint8_t* p = base + pg.hdr_off;
   const uint8_t* e = (end && end - p < 65536) ? end : p + 65536;
   PageHeader h = parse_page_header(p, e);
@@ -193,5 +194,6 @@ DK_HD inline void apply_page_header(DPage& pg, const DChunk& ck, const uint8_t* 
     if (ck.codec != CODEC_NONE && pg.unc_off < 0 && !(h.type == PAGE_DATA_V2 && !h.is_comp)) pg.status = PS_UNSUPPORTED;
   }
 }
+#endif
 
 }  // namespace dk
