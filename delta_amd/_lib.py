@@ -74,6 +74,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
            "dk_parquet_first_row", "dk_parquet_column_rows",
            "dk_parquet_traffic", "dk_parquet_kernel_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
+           "dk_json_tail_parse_parts", "dk_json_tail_checkpoint_row0",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
@@ -125,6 +126,8 @@ def lib(build_if_missing=True):
         "dk_parquet_close": (None, [P]),
         "dk_json_tail_parse": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(I64), I32, I32, C.POINTER(P)]),
         "dk_json_tail_rows": (I64, [P]),
+        "dk_json_tail_parse_parts": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(I64), I32, I32, I32, C.POINTER(P)]),
+        "dk_json_tail_checkpoint_row0": (I64, [P]),
         "dk_json_tail_column": (C.c_int, [P, C.c_char_p, C.POINTER(dk_column)]),
         "dk_json_tail_free": (None, [P]),
         "dk_replay_create": (C.c_int, [P, P, P, C.POINTER(P)]),
@@ -203,3 +206,18 @@ class Column:
 
     def string(self, i):
         return bytes(self.chars[self.offs[i]:self.offs[i + 1]])
+
+    def slice_rows(self, a, b):
+        """Rows [a, b) as a column of their own (views; entry- and char-level arrays are shared:
+        the row-level offsets keep pointing into them)."""
+        import copy
+        c = copy.copy(self)
+        c.n_rows = b - a
+        c.row_def = self.row_def[a:b]
+        if self.max_rep > 0:
+            c.row_offs = self.row_offs[a:b + 1]
+        elif self.offs is not None:
+            c.offs = self.offs[a:b + 1]
+        elif self.fixed is not None:
+            c.fixed = self.fixed[a * self.width:b * self.width]
+        return c

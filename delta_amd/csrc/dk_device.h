@@ -162,8 +162,10 @@ struct DvCont {
 constexpr uint32_t kDecodeSeed = 0;   // seed of the path hashes computed during decode
 constexpr int DK_COPY_TILE = 128;     // values per k_string_copy workgroup (host tile table step)
 
-// Commit-tail actions, one per JSON line, in replay order.
-enum : int32_t { JA_NONE = 0, JA_ADD = 1, JA_REMOVE = 2 };
+// Commit-tail actions, one per JSON line, in replay order. JA_CKADD: an add row of a JSON-format
+// checkpoint part (a V2 checkpoint's JSON manifest, ActionsIterator.java:213-248): probed like a
+// Parquet checkpoint row, never entered into the key table.
+enum : int32_t { JA_NONE = 0, JA_ADD = 1, JA_REMOVE = 2, JA_CKADD = 3 };
 struct DJsonAction {
   int32_t kind;          // JA_*
   int32_t step;          // global batch index in replay order

@@ -51,7 +51,7 @@ void launch_slots_init(Slot*, uint64_t, hipStream_t);
 void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
 void launch_first_row(const uint8_t*, long long, int, unsigned long long*, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
-void launch_json_select(const DJsonAction*, int, const Slot*, uint8_t*, DState*, hipStream_t);
+void launch_json_select(const DJsonAction*, int, const Slot*, uint64_t, const uint8_t*, uint8_t*, DState*, hipStream_t);
 void launch_stats_eval(const StatsRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
 void launch_stats_parsed(const StatsParsedRows&, const DSkipProg*, uint8_t*, hipStream_t);
 void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipStream_t);
@@ -2363,6 +2363,7 @@ enum { JL_PATH, JL_PVK, JL_PVV, JL_SIZE, JL_MTIME, JL_DC, JL_DVST, JL_DVPID, JL_
 
 struct dk_json_tail {
   int64_t rows = 0;
+  int64_t ckpt_row0 = -1;             // rows from here on come from JSON checkpoint parts (-1: none)
   bool with_stats = false;
   CB col[JL_N];
   std::vector<int32_t> step, rowin;   // per row: batch step and row within batch
@@ -2565,8 +2566,14 @@ static void append_cb(CB& d, const CB& s) {
 
 extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
                                   int32_t with_stats, dk_json_tail** out) {
+  return dk_json_tail_parse_parts(e, paths, versions, n_files, 0, with_stats, out);
+}
+
+extern "C" int dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
+                                        int32_t n_checkpoint_files, int32_t with_stats, dk_json_tail** out) {
   (void)versions;
   if (!e) return fail("null engine");
+  if (n_checkpoint_files < 0 || n_checkpoint_files > n_files) return fail("dk_json_tail_parse_parts: bad file counts");
   std::unique_ptr<dk_json_tail> t(new dk_json_tail());
   t->with_stats = with_stats != 0;
   init_tail_cols(t->col);
@@ -2580,6 +2587,7 @@ extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const 
     if (!errs[fi].empty()) return fail(errs[fi]);
   for (int fi = 0; fi < n_files; fi++) {
     TailPart& P = parts[fi];
+    if (fi == n_files - n_checkpoint_files) t->ckpt_row0 = t->rows;
     for (int k = 0; k < JL_N; k++) append_cb(t->col[k], P.col[k]);
     for (int32_t st : P.step) t->step.push_back(t->n_steps + st);
     t->rowin.insert(t->rowin.end(), P.rowin.begin(), P.rowin.end());
@@ -2592,6 +2600,9 @@ extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const 
 }
 
 extern "C" int64_t dk_json_tail_rows(dk_json_tail* t) { return t ? t->rows : -1; }
+extern "C" int64_t dk_json_tail_checkpoint_row0(dk_json_tail* t) {
+  return t ? (t->ckpt_row0 >= 0 ? t->ckpt_row0 : t->rows) : -1;
+}
 
 extern "C" int dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out) {
   memset(out, 0, sizeof *out);
@@ -2818,11 +2829,15 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
       jchars.insert(jchars.end(), col.chars.begin() + b, col.chars.begin() + en);
     };
     for (int64_t row = 0; row < tail->rows; row++) {
+      // rows of a JSON checkpoint part: adds are checkpoint adds, removes are ignored
+      // (ActiveAddFilesIterator.java:163-183 reads tombstones only from commit files)
+      const bool ck = tail->ckpt_row0 >= 0 && row >= tail->ckpt_row0;
       for (int kind : {JA_REMOVE, JA_ADD}) {
+        if (ck && kind == JA_REMOVE) continue;
         const CB& pc = c[kind == JA_ADD ? JL_PATH : JL_RPATH];
         if (pc.row_def[row] < 1) continue;
         DJsonAction a{};
-        a.kind = kind; a.step = tail->step[row]; a.row = tail->rowin[row];
+        a.kind = ck ? JA_CKADD : kind; a.step = tail->step[row]; a.row = tail->rowin[row];
         add_str(pc, row, &a.path_off, &a.path_len);
         const CB& st = c[kind == JA_ADD ? JL_DVST : JL_RDVST];
         const CB& pid = c[kind == JA_ADD ? JL_DVPID : JL_RDVPID];
@@ -2863,7 +2878,7 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
     const CB& kc = tail->col[JL_PVK];
     const CB& vc = tail->col[JL_PVV];
     std::vector<int64_t> arow(na);
-    for (size_t i = 0; i < na; i++) arow[i] = r->acts[i].kind == JA_ADD ? r->act_row[i] : -1;
+    for (size_t i = 0; i < na; i++) arow[i] = r->acts[i].kind != JA_REMOVE ? r->act_row[i] : -1;
     MapRows M{};
     M.n = (int64_t)na;
     M.act_row = (const int64_t*)up(arow.data(), arow.size() * 8);
@@ -2887,7 +2902,7 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
     std::vector<int32_t> slen(na + 1, -1);
     for (size_t i = 0; i < na; i++) {
       const int64_t row = r->act_row[i];
-      if (r->acts[i].kind != JA_ADD || sc.row_def[row] < 2) continue;
+      if (r->acts[i].kind == JA_REMOVE || sc.row_def[row] < 2) continue;
       soff[i] = sc.offs[row];
       slen[i] = (int32_t)(sc.offs[row + 1] - sc.offs[row]);
     }
@@ -3074,7 +3089,7 @@ static int replay_launch(dk_replay* r) {
   { KTimer::Scope sc(&T, 7, s); launch_json_canon(A, na, r->d_jchars.as<uint8_t>(), r->d_canon.as<uint8_t>(), r->seed, st, s); }
   { KTimer::Scope sc(&T, 8, s); launch_table_insert(A, na, S, r->mask, s); }
   { KTimer::Scope sc(&T, 9, s); launch_table_update(A, na, S, r->mask, r->d_canon.as<uint8_t>(), st, s); }
-  { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->d_jsel.as<uint8_t>(), st, s); }
+  { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->mask, r->d_canon.as<uint8_t>(), r->d_jsel.as<uint8_t>(), st, s); }
   if (r->has_part && na) {                 // partition pruning on the tail's adds (before skipping)
     KTimer::Scope sc(&T, 18, s);
     launch_part_eval(r->tail_maps, r->d_part.as<DPartProg>(), r->d_jsel.as<uint8_t>(), st, s);
@@ -3184,7 +3199,7 @@ extern "C" int dk_replay_sync(dk_replay* r) {
       if (!acts.empty()) HIPOK(hipMemcpy(acts.data(), r->d_acts.p, acts.size() * sizeof(DJsonAction), hipMemcpyDeviceToHost));
       for (size_t i = 0; i < acts.size(); i++)
         if (acts[i].status) {
-          const CB& pc = r->tail->col[acts[i].kind == JA_ADD ? JL_PATH : JL_RPATH];
+          const CB& pc = r->tail->col[acts[i].kind != JA_REMOVE ? JL_PATH : JL_RPATH];
           int64_t row = r->act_row[i];
           std::string path(pc.chars.begin() + pc.offs[row], pc.chars.begin() + pc.offs[row + 1]);
           return fail((acts[i].status == -1 ? "java.net.URISyntaxException: Illegal character in path: "
@@ -3223,7 +3238,7 @@ extern "C" int dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n) {
   memset(out, 0, n);
   std::vector<uint8_t> sel(r->acts.size());
   if (!sel.empty()) HIPOK(hipMemcpy(sel.data(), r->d_jsel.p, sel.size(), hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < sel.size(); i++) if (r->acts[i].kind == JA_ADD && sel[i]) out[r->act_row[i]] = 1;
+  for (size_t i = 0; i < sel.size(); i++) if (r->acts[i].kind != JA_REMOVE && sel[i]) out[r->act_row[i]] = 1;
   return 0;
 }
 

@@ -3369,7 +3369,7 @@ __global__ void k_table_insert(const DJsonAction* __restrict__ acts, int n, Slot
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const DJsonAction& a = acts[i];
-  if (a.kind == JA_NONE || a.status) return;
+  if (a.kind == JA_NONE || a.kind == JA_CKADD || a.status) return;
   unsigned long long h = a.h;
   uint64_t s = h & mask;
   for (;;) {
@@ -3394,7 +3394,7 @@ __global__ void k_table_update(DJsonAction* __restrict__ acts, int n, Slot* __re
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   DJsonAction a = acts[i];
-  if (a.kind == JA_NONE || a.status) return;
+  if (a.kind == JA_NONE || a.kind == JA_CKADD || a.status) return;
   uint64_t s = a.h & mask;
   while (slots[s].h != a.h) s = (s + 1) & mask;
   const DJsonAction& rp = acts[slots[s].rep];
@@ -3410,22 +3410,37 @@ __device__ __forceinline__ void wave_count(unsigned long long* ctr, bool pred) {
 }
 
 __global__ void k_json_select(const DJsonAction* __restrict__ acts, int n, const Slot* __restrict__ slots,
-                              uint8_t* __restrict__ sel, DState* __restrict__ st) {
+                              uint64_t mask, const uint8_t* __restrict__ canon, uint8_t* __restrict__ sel,
+                              DState* __restrict__ st) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool is_add = false, is_rm = false, chosen = false, dup = false;
+  bool is_add = false, is_ck = false, is_rm = false, chosen = false, dup = false;
   if (i < n) {
     const DJsonAction a = acts[i];
     is_add = a.kind == JA_ADD;
+    is_ck = a.kind == JA_CKADD;
     is_rm = a.kind == JA_REMOVE;
     if (is_add && a.status == 0) {
       const Slot s = slots[a.slot];
       unsigned long long mypos = ((unsigned long long)a.step << 32) | (unsigned)a.row;
       dup = s.first_add != mypos;                 // alreadyReturned (ActiveAddFilesIterator :210,227)
       chosen = !dup && s.min_rm_step > a.step;    // not tombstoned by this or a newer batch (R2/R5)
+    } else if (is_ck && a.status == 0) {
+      // a checkpoint row (JSON manifest): the commit tail's sets are final; the key is in the table
+      // iff some slot holds its hash and the representative's canonical bytes are equal
+      bool hit = false;
+      Slot s{};
+      for (uint64_t k = a.h & mask;; k = (k + 1) & mask) {
+        s = slots[k];
+        if (s.h == 0ull) break;
+        if (s.h == a.h) { hit = canon_equal(a, acts[s.rep], canon); break; }
+      }
+      dup = hit && s.first_add != ~0ull;          // alreadyReturned
+      chosen = !dup && !(hit && s.min_rm_step != 0x7fffffff);   // and not alreadyDeleted
     }
     sel[i] = chosen;
   }
-  wave_count(&st->counters[0], is_add);
+  // counters: a JSON-manifest add counts as a checkpoint add (not addFilesSeenFromDeltaFiles)
+  wave_count(&st->counters[0], is_add || is_ck);
   wave_count(&st->counters[1], is_add);
   wave_count(&st->counters[2], chosen);
   wave_count(&st->counters[3], dup);
@@ -3841,8 +3856,9 @@ void launch_table_update(DJsonAction* a, int n, Slot* slots, uint64_t mask, cons
                          hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_table_update, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, mask, canon, st);
 }
-void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint8_t* sel, DState* st, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, sel, st);
+void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint64_t mask, const uint8_t* canon, uint8_t* sel,
+                        DState* st, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, mask, canon, sel, st);
 }
 void launch_probe_all(const ProbeSet& PS, const Slot* slots, const uint32_t* fp, uint64_t mask, const DJsonAction* acts,
                       const uint8_t* canon, uint32_t seed, uint64_t h_nodv, int32_t* cand, unsigned int* cand_n,

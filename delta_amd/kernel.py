@@ -418,14 +418,19 @@ def read_scan_data(engine, scan, leaves):
 
 
 class JsonTail:
-    """Commit files parsed on the host (DefaultJsonHandler.readJsonFiles semantics)."""
+    """Commit files parsed on the host (DefaultJsonHandler.readJsonFiles semantics), optionally
+    followed by JSON-format checkpoint parts (a V2 checkpoint's JSON manifest): rows
+    [ckpt_row0, rows) are those parts' rows, whose adds reconcile as checkpoint adds."""
 
-    def __init__(self, engine: GpuEngine, commit_paths, versions, with_stats=False):
+    def __init__(self, engine: GpuEngine, commit_paths, versions, with_stats=False, checkpoint_paths=()):
         self._h = C.c_void_p()
+        paths = list(commit_paths) + list(checkpoint_paths)
+        versions = list(versions) + [0] * len(checkpoint_paths)
         vers = (C.c_int64 * max(1, len(versions)))(*versions)
-        check(lib().dk_json_tail_parse(engine._h, _cstrs(commit_paths), vers, len(commit_paths),
-                                       1 if with_stats else 0, C.byref(self._h)))
+        check(lib().dk_json_tail_parse_parts(engine._h, _cstrs(paths), vers, len(paths), len(checkpoint_paths),
+                                             1 if with_stats else 0, C.byref(self._h)))
         self.rows = lib().dk_json_tail_rows(self._h)
+        self.ckpt_row0 = lib().dk_json_tail_checkpoint_row0(self._h)
 
     def column(self, leaf) -> Column:
         c = dk_column()
@@ -672,18 +677,16 @@ class Snapshot:
     def _json_manifest(self):
         """Actions of a V2 checkpoint's JSON manifest (ActionsIterator reads it with the JSON handler,
         ActionsIterator.java:306-315, and extracts its sidecar rows, :256-283). Host-parsed: one
-        small file. Returns (sidecar paths in manifest order, protocol, metaData)."""
+        small file. Returns (sidecar paths in manifest order, protocol, metaData). Its add rows
+        are checkpoint rows too: GpuScan parses the manifest after the commit tail
+        (dk_json_tail_parse_parts) and reconciles them as checkpoint adds."""
         if self._manifest is None:
             side, proto, meta = [], None, None
             with open(self.log_segment.checkpoints[0].path, "rb") as f:
-                for ln, line in enumerate(f.read().decode("utf-8", "replace").splitlines()):
+                for line in f.read().decode("utf-8", "replace").splitlines():
                     if not line.strip():
                         continue
                     obj = json.loads(line)
-                    if obj.get("add") is not None or obj.get("remove") is not None:
-                        raise DkError("V2 checkpoint JSON manifest %s carries add/remove actions (line %d); "
-                                      "this engine build reconciles checkpoint rows from Parquet only"
-                                      % (self.log_segment.checkpoints[0].path, ln + 1))
                     sc = obj.get("sidecar")
                     if sc is not None:
                         side.append(os.path.join(self.log_segment.log_path, "_sidecars", sc["path"]))
@@ -693,6 +696,11 @@ class Snapshot:
                         meta = obj["metaData"]
             self._manifest = (side, proto, meta)
         return self._manifest
+
+    def _json_checkpoint_parts(self):
+        """The checkpoint parts read with the JSON handler: a V2 checkpoint's JSON manifest."""
+        cks = self.log_segment.checkpoints
+        return [cks[0].path] if cks and cks[0].kind == "v2" and cks[0].path.endswith(".json") else []
 
     def _checkpoint_files(self, engine, with_pruning=False):
         """Checkpoint data files in replay order: multi-part parts descending (LogSegment
@@ -1104,7 +1112,8 @@ class GpuScan:
             # the tail, then the replay's commit-tail half (action table + key-table inputs)
             t = time.perf_counter()
             try:
-                tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats)
+                tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats,
+                                checkpoint_paths=self.snapshot._json_checkpoint_parts())
                 tail_box["tail"] = tail
                 tail_box["ms"] = (time.perf_counter() - t) * 1e3
                 t = time.perf_counter()
@@ -1259,8 +1268,16 @@ class GpuScan:
         if self.tail.rows:
             sel = np.zeros(self.tail.rows, dtype=np.uint8)
             check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
-            cols = LazyColumns(leaves, self.tail.column)
-            yield FilteredColumnarBatch(cols, root, int(self.tail.rows), sel.view(bool), "json-tail")
+            r0 = int(self.tail.ckpt_row0)
+            if r0 > 0:
+                cols = LazyColumns(leaves, self.tail.column)
+                yield FilteredColumnarBatch(cols, root, r0, sel[:r0].view(bool), "json-tail")
+            if r0 < self.tail.rows:
+                # a V2 JSON manifest's rows: the first checkpoint batch (ActionsIterator reads the
+                # manifest before its sidecars)
+                cols = LazyColumns(leaves, lambda leaf: self.tail.column(leaf).slice_rows(r0, self.tail.rows))
+                yield FilteredColumnarBatch(cols, root, int(self.tail.rows - r0), sel[r0:].view(bool),
+                                            self.snapshot._json_checkpoint_parts()[0], -1, 0)
         # checkpoint batches: zero-copy views of the library's pinned selection bytes and column
         # mirrors (every file's selection comes to the host in one round of copies; a leaf's first
         # access queues its copy for every later file), valid until the scan is closed

@@ -70,6 +70,9 @@ class TableSpec:
     hot_frac: float = 0.0            # C5 skew: fraction of paths under one hot partition
     v2_sidecars: int = 0             # > 0: V2 checkpoint = manifest + this many sidecars
     v2_manifest: str = "parquet"     # V2 manifest format: "parquet" or "json"
+    v2_json_adds: int = 0            # JSON manifest: this many add rows inline (+ a few removes, which
+                                     # the reader ignores); the first commit removes a quarter of them
+                                     # and re-adds another quarter
     variable_paths: bool = False     # add random suffixes / escapes so lengths vary
     seed: int = SEED
     extra: dict = field(default_factory=dict)
@@ -480,6 +483,14 @@ def _write_v2_manifest(log, v, sidecars, pm, rng, spec: TableSpec):
         lines = [{"checkpointMetadata": {"version": v}}]
         lines += [{"sidecar": {k: r[k] for k in ("path", "sizeInBytes", "modificationTime")}} for r in sc_rows]
         lines += [{"protocol": proto_row}, {"metaData": _meta_json(meta_row)}]
+        if spec.v2_json_adds > 0:
+            arr, day = gen_paths(rng, spec.v2_json_adds, 9_000_000, spec)
+            spec.extra["manifest_adds"] = paths = arr.to_pylist()
+            for i, pth in enumerate(paths):
+                lines.append(_json_add(pth, "2024-01-01", 1000 + i, 1_700_000_000_000 + i, pv_keys=spec.pv_keys,
+                                       stats='{"numRecords":1}' if i % 3 else None))
+                if i % 7 == 3:      # a checkpoint remove: never a tombstone
+                    lines.append(_json_remove(pth + ".old", "2024-01-01", 1_700_000_000_000))
         with open(mfn, "w") as f:
             f.write("\n".join(json.dumps(x) for x in lines) + "\n")
         return mfn
@@ -574,6 +585,12 @@ def write_table(root: str, spec: TableSpec):
         ver = v + 1 + c
         lines = [json.dumps({"commitInfo": {"timestamp": 1_700_000_000_000 + ver,
                                             "operation": "WRITE"}})]
+        if c == 0 and spec.extra.get("manifest_adds"):
+            ma = spec.extra["manifest_adds"]
+            q = max(1, len(ma) // 4)
+            lines += [json.dumps(_json_remove(pth, "2024-01-01", 1_700_000_000_000 + ver)) for pth in ma[:q]]
+            lines += [json.dumps(_json_add(pth, "2024-01-01", 77, 1_700_000_000_000 + ver, pv_keys=spec.pv_keys))
+                      for pth in ma[q:2 * q]]
         # removes
         for _ in range(spec.removes_per_commit):
             pick = rng.random()

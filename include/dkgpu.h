@@ -234,6 +234,14 @@ void dk_dv_free(dk_dv_set* s);
 int  dk_json_tail_parse(dk_engine* e, const char* const* commit_paths, const int64_t* versions,
                         int32_t n_files, int32_t with_stats, dk_json_tail** out);
 int64_t dk_json_tail_rows(dk_json_tail* t);
+/* The same over the commit tail followed by n_checkpoint_files JSON-format checkpoint parts (a V2
+ * checkpoint's JSON manifest, read by ActionsIterator.getActionsIterFromSinglePartOrV2Checkpoint
+ * through JsonHandler.readJsonFiles, ActionsIterator.java:175-248): their add rows are checkpoint
+ * adds (isFromCheckpoint), their removes are ignored. Rows [dk_json_tail_checkpoint_row0(t), rows)
+ * are those parts' rows. */
+int  dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
+                              int32_t n_checkpoint_files, int32_t with_stats, dk_json_tail** out);
+int64_t dk_json_tail_checkpoint_row0(dk_json_tail* t);
 /* Snapshot-load P&M scan of commit files given newest first (LogReplay.loadTableProtocolAndMetadata,
  * internal/replay/LogReplay.java:220-314): per file, the line index and byte range of the first line
  * with a non-null top-level "protocol" / "metaData" (-1: none). Files are read 16 at a time on host

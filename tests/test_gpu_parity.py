@@ -50,6 +50,9 @@ V2_CASES = {
     "v2-sidecars-c5": dict(n_parts=6, v2_sidecars=6, compression="snappy", data_page_version="2.0",
                            delta_binary_packed=True, hot_frac=0.6, ckpt_removes=200, dv_frac=0.1),
     "v2-one-sidecar-dict": dict(n_parts=1, v2_sidecars=1, pv_keys=2),
+    # V2 JSON manifest carrying add rows (checkpoint adds read by the JSON handler before the
+    # sidecars, ActionsIterator.java:213-248) and remove rows (ignored); the tail removes / re-adds some
+    "v2-json-manifest-adds": dict(n_parts=3, v2_sidecars=3, v2_manifest="json", v2_json_adds=400, with_stats=True),
 }
 
 

@@ -614,3 +614,20 @@ def test_row_group_pruning_decisions_match_oracle(rg_table):
         for f in files:
             want = [g for g, k in enumerate(surviving_row_groups(f, p, fields)) if k]
             assert K.prune_row_groups(f, packed) == want, (p, f)
+
+
+@pytest.mark.gpu
+def test_gpu_filters_over_json_manifest_adds(tmp_path):
+    """Partition pruning and data skipping over the add rows of a V2 JSON manifest (checkpoint rows
+    read by the JSON handler, ActionsIterator.java:213-248) equal the oracle's."""
+    from delta_amd import kernel as K
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=9_000, n_parts=2, v2_sidecars=2, v2_manifest="json",
+                                                     v2_json_adds=300, n_commits=4, with_stats=True))
+    eng = K.GpuEngine()
+    for pred in (cmp("=", col("date"), Literal.ofString("2024-01-01")), cmp(">", col("date"), Literal.ofString("2024-01-01")),
+                 cmp(">", col("id"), Literal.ofLong(30_000_000)),
+                 And(cmp(">=", col("date"), Literal.ofString("2023-01-01")), cmp("<", col("id"), Literal.ofLong(1_000_000)))):
+        g = _gpu_files(str(tmp_path), pred, eng)
+        o = oracle_files(str(tmp_path), pred)
+        assert g[1] == o[1] and g[0] == o[0], pred
+    eng.close()
