@@ -286,6 +286,11 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--device-steps", type=int, default=None, help="timed device-only steps (default: --steps)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of launcher + planning + exchange")
+    ap.add_argument("--exchange", default="allgather", choices=["allgather", "alltoall"],
+                    help="multi-GPU C3: allgather = every rank probes against its own copy of the commit-tail key "
+                         "table and the selection bitmaps are all-gathered; alltoall = checkpoint rows are routed "
+                         "to the owner of their path hash over RCCL all-to-all and the answers come back by the "
+                         "reverse all-to-all (DESIGN.md §6)")
     ap.add_argument("--workdir", default=None)
     args = ap.parse_args(argv)
 
@@ -389,6 +394,17 @@ def main(argv=None):
         finally:
             os.remove(crc)
 
+    a2a = args.exchange == "alltoall" and cfg["shared"] and world > 1
+    a2a_ms = []
+
+    def hash_exchange(side):
+        from delta_amd import shard
+        import torch
+        te = time.perf_counter()
+        shard.exchange_hash_owner(side, device="cuda")
+        torch.cuda.synchronize()
+        a2a_ms.append((time.perf_counter() - te) * 1e3)
+
     def build_scan(s):
         sb = s.getScanBuilder().withStats(cfg["stats"])
         if cfg["predicate"]:
@@ -396,7 +412,7 @@ def main(argv=None):
             col, op, lit = cfg["predicate"]
             sb = sb.withFilter(Predicate(op, Column(col), Literal.ofLong(lit)))
         if cfg["shared"] and world > 1:
-            sb = sb.withShard(world, rank)
+            sb = sb.withShard(world, rank, exchange=hash_exchange if a2a else None)
         return sb.build()
 
     # ---- region 1: the device step over inputs resident in HBM (roofline) ----
@@ -408,7 +424,7 @@ def main(argv=None):
     n_tail = int(scan.tail.rows)
     bytes_read, bytes_written = scan.ckpt.traffic() if scan.ckpt else (0, 0)
     exchange = None
-    if dist is not None and cfg["shared"]:
+    if dist is not None and cfg["shared"] and not a2a:
         from delta_amd import shard
         meta = [(scan.ckpt_index[fi], scan.ckpt.row_offset(fi), scan.ckpt.num_rows(fi))
                 for fi in range(len(scan.ckpt_files or []))]
@@ -438,7 +454,11 @@ def main(argv=None):
     dsteps = args.device_steps if args.device_steps is not None else args.steps
     for _ in range(args.warmup):
         device_step()
+    del a2a_ms[:]
     device_counters = merged[0] if merged else scan.metrics.as_tuple()
+    if a2a:      # the result stays where it was decoded; the counters of the world, for the report
+        device_counters = tuple(scan.tail_metrics.as_tuple()[i] + v
+                                for i, v in enumerate(sum_over_ranks(scan.ckpt_metrics.as_tuple())))
     barrier()
     stats0 = scan.kernel_stats()
     t0 = time.perf_counter()
@@ -446,6 +466,7 @@ def main(argv=None):
         device_step()
     barrier()
     dev_elapsed = max_over_ranks(time.perf_counter() - t0)
+    a2a_dev = sorted(a2a_ms)[len(a2a_ms) // 2] if a2a_ms else None
     stats1 = scan.kernel_stats()
     kern = {}
     for name, (avg1, c1) in stats1.items():
@@ -544,9 +565,13 @@ def main(argv=None):
         "dtype": "u8/int64",
         "data": "synthetic (seed 20250218; delta_amd/synth.py)",
         "config": {"workload": cfg["desc"] % rows, "name": args.config, "compression": compression,
-                   "parallelism": ("strong: checkpoint row groups in %d contiguous runs (one per GPU), commit tail "
-                                   "on every GPU; device step ends with one RCCL all-gather of counters + "
-                                   "selection bitmaps" % world if cfg["shared"] else "weak: one table per GPU"),
+                   "parallelism": (("strong: checkpoint row groups in %d contiguous runs (one per GPU), commit tail "
+                                    "on every GPU; " % world +
+                                    ("checkpoint rows routed to the owner of their path hash and answered over RCCL "
+                                     "all-to-all (exchange=alltoall)" if a2a else
+                                     "device step ends with one RCCL all-gather of counters + selection bitmaps"))
+                                   if cfg["shared"] else "weak: one table per GPU"),
+                   "exchange": args.exchange if (cfg["shared"] and world > 1) else None,
                    "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail,
                    "checkpoint_files_per_gpu": len(ckpt_files)},
         "value_definition": "ScanMetrics.numAddFilesSeen / getScanFiles wall time until fully consumed "
@@ -559,7 +584,7 @@ def main(argv=None):
         "device_step": {"ms": dev_elapsed / max(1, dsteps) * 1e3, "steps": dsteps,
                         "actions_per_s": dev_units * dsteps / dev_elapsed if dev_elapsed else None,
                         "counters": list(device_counters),
-                        "exchange_ms": (sorted(ex_ms)[len(ex_ms) // 2] if ex_ms else None),
+                        "exchange_ms": (sorted(ex_ms)[len(ex_ms) // 2] if ex_ms else a2a_dev),
                         "prepare_s": prepare_s},
         "snapshot_load_ms": snapshot_ms,
         "snapshot_load_cold_ms": snapshot_cold_ms,

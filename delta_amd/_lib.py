@@ -75,6 +75,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_parquet_first_row", "dk_parquet_column_rows",
            "dk_parquet_traffic", "dk_parquet_kernel_traffic", "dk_parquet_close", "dk_json_tail_parse", "dk_json_tail_rows",
            "dk_json_tail_parse_parts", "dk_json_tail_checkpoint_row0",
+           "dk_replay_set_exchange", "dk_replay_exchange_counts", "dk_replay_exchange_pack", "dk_replay_exchange_filter",
+           "dk_replay_exchange_finish", "dk_json_pm_decode",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
@@ -128,6 +130,12 @@ def lib(build_if_missing=True):
         "dk_json_tail_rows": (I64, [P]),
         "dk_json_tail_parse_parts": (C.c_int, [P, C.POINTER(C.c_char_p), C.POINTER(I64), I32, I32, I32, C.POINTER(P)]),
         "dk_json_tail_checkpoint_row0": (I64, [P]),
+        "dk_replay_set_exchange": (C.c_int, [P, I32, I32]),
+        "dk_json_pm_decode": (C.c_int, [C.c_char_p, I64, I64, I32, C.c_char_p, I64, C.POINTER(I64)]),
+        "dk_replay_exchange_counts": (C.c_int, [P, C.POINTER(I64)]),
+        "dk_replay_exchange_pack": (C.c_int, [P, P]),
+        "dk_replay_exchange_filter": (C.c_int, [P, P, I64, P]),
+        "dk_replay_exchange_finish": (C.c_int, [P, P]),
         "dk_json_tail_column": (C.c_int, [P, C.c_char_p, C.POINTER(dk_column)]),
         "dk_json_tail_free": (None, [P]),
         "dk_replay_create": (C.c_int, [P, P, P, C.POINTER(P)]),

@@ -58,6 +58,13 @@ void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipSt
 void launch_table_fp(const Slot*, uint32_t*, uint64_t, hipStream_t);
 void launch_probe_all(const ProbeSet&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                       int32_t*, unsigned int*, DState*, hipStream_t);
+int a2a_blocks(long long, long long*);
+void launch_a2a_count(const ProbeSet&, int, unsigned long long*, unsigned long long*, hipStream_t);
+void launch_a2a_pack(const ProbeSet&, int, const unsigned long long*, uint64_t*, int32_t*, int32_t*, unsigned int*, DState*,
+                     hipStream_t);
+void launch_a2a_filter(const uint64_t*, long long, const uint64_t*, long long, uint8_t*, hipStream_t);
+void launch_a2a_apply(const ProbeSet&, const int32_t*, const uint8_t*, long long, const Slot*, uint64_t, const DJsonAction*,
+                      const uint8_t*, uint32_t, int32_t*, unsigned int*, DState*, hipStream_t);
 void launch_probe(const ProbeCols&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
 }  // namespace dk
@@ -2626,6 +2633,110 @@ extern "C" int dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column*
 
 extern "C" void dk_json_tail_free(dk_json_tail* t) { delete t; }
 
+// One commit line's protocol / metaData action decoded with DefaultJsonRow's rules for
+// Protocol.FULL_SCHEMA / Metadata.FULL_SCHEMA (kernel-defaults/.../internal/data/DefaultJsonRow.java:
+// 136-357; actions/Protocol.java:49-54, Metadata.java:57-72, Format.java:42-48): required fields
+// missing or null fail ("Root node at key .. is null but field isn't nullable"), ints need an
+// integral JSON number in int range, longs an integral number in long range, strings JSON strings,
+// arrays JSON arrays without null elements, maps JSON objects without null values. The result is
+// the action re-serialised with exactly the schema's fields (null where absent), for the host.
+namespace {
+void json_esc(std::string& o, const std::string& s) {
+  o += '"';
+  for (unsigned char c : s) {
+    if (c == '"') o += "\\\"";
+    else if (c == '\\') o += "\\\\";
+    else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); o += b; }
+    else o += (char)c;
+  }
+  o += '"';
+}
+void pm_str(std::string& o, const std::vector<JNode>& N, const JNode& obj, const char* k, bool nullable) {
+  const JNode* v = field(N, obj, k, nullable);
+  if (!v) { o += "null"; return; }
+  json_esc(o, as_str(N, *v));
+}
+void pm_str_array(std::string& o, const std::vector<JNode>& N, const JNode& obj, const char* k, bool nullable) {
+  const JNode* v = field(N, obj, k, nullable);
+  if (!v) { o += "null"; return; }
+  if (v->t != J_ARR) mismatch(N, *v, "array");
+  o += '[';
+  for (size_t i = 0; i < v->arr.size(); i++) {
+    const JNode& e = N[v->arr[i]];
+    if (e.t == J_NULL) throw JErr{"Array type expects no nulls as elements, but received `null` as array element"};
+    if (i) o += ',';
+    json_esc(o, as_str(N, e));
+  }
+  o += ']';
+}
+void pm_str_map(std::string& o, const std::vector<JNode>& N, const JNode& obj, const char* k, bool nullable) {
+  const JNode* v = field(N, obj, k, nullable);
+  if (!v) { o += "null"; return; }
+  if (v->t != J_OBJ) mismatch(N, *v, "map");
+  o += '{';
+  for (size_t i = 0; i < v->kv.size(); i++) {
+    const JNode& e = N[v->kv[i].second];
+    if (e.t == J_NULL) throw JErr{"Map type expects no nulls in values, but received `null` as value"};
+    if (i) o += ',';
+    json_esc(o, v->kv[i].first);
+    o += ':';
+    json_esc(o, as_str(N, e));
+  }
+  o += '}';
+}
+}  // namespace
+
+extern "C" int dk_json_pm_decode(const char* path, int64_t off, int64_t len, int32_t which, char* out, int64_t cap,
+                                 int64_t* out_len) {
+  FILE* fp = fopen(path, "rb");
+  if (!fp) return fail(std::string("Error reading JSON file: ") + path);
+  std::vector<uint8_t> raw(len > 0 ? len : 0);
+  const bool ok = fseek(fp, (long)off, SEEK_SET) == 0 && (len <= 0 || fread(raw.data(), 1, len, fp) == (size_t)len);
+  fclose(fp);
+  if (!ok) return fail(std::string("Error reading JSON file: ") + path);
+  const std::string text = java_utf8(raw.data(), raw.size());
+  std::vector<JNode> N;
+  JParser jp(text.data(), text.data() + text.size(), N);
+  int root = jp.value(0);
+  if (root >= 0) { jp.ws(); if (jp.p != jp.e) { root = -1; jp.err = "trailing characters"; } }
+  if (root < 0) return fail(std::string("Error reading JSON file: ") + path + " (" + jp.err + ")");
+  std::string o;
+  try {
+    const JNode& R = N[root];
+    if (R.t != J_OBJ) mismatch(N, R, "object");
+    const JNode* a = field(N, R, which == 0 ? "protocol" : "metaData", false);
+    if (a->t != J_OBJ) mismatch(N, *a, "object");
+    const JNode& A = *a;
+    if (which == 0) {
+      o += "{\"minReaderVersion\":" + std::to_string(as_int(N, *field(N, A, "minReaderVersion", false)));
+      o += ",\"minWriterVersion\":" + std::to_string(as_int(N, *field(N, A, "minWriterVersion", false)));
+      o += ",\"readerFeatures\":"; pm_str_array(o, N, A, "readerFeatures", true);
+      o += ",\"writerFeatures\":"; pm_str_array(o, N, A, "writerFeatures", true);
+      o += '}';
+    } else {
+      o += "{\"id\":"; pm_str(o, N, A, "id", false);
+      o += ",\"name\":"; pm_str(o, N, A, "name", true);
+      o += ",\"description\":"; pm_str(o, N, A, "description", true);
+      const JNode* f = field(N, A, "format", false);
+      if (f->t != J_OBJ) mismatch(N, *f, "object");
+      o += ",\"format\":{\"provider\":"; pm_str(o, N, *f, "provider", false);
+      o += ",\"options\":"; pm_str_map(o, N, *f, "options", true);
+      o += "},\"schemaString\":"; pm_str(o, N, A, "schemaString", false);
+      o += ",\"partitionColumns\":"; pm_str_array(o, N, A, "partitionColumns", false);
+      const JNode* ct = field(N, A, "createdTime", true);
+      o += ",\"createdTime\":" + (ct ? std::to_string(as_long(N, *ct)) : std::string("null"));
+      o += ",\"configuration\":"; pm_str_map(o, N, A, "configuration", false);
+      o += '}';
+    }
+  } catch (const JErr& je) {
+    return fail(je.msg);
+  }
+  *out_len = (int64_t)o.size();
+  if ((int64_t)o.size() > cap) return 2;                   // caller retries with *out_len bytes
+  memcpy(out, o.data(), o.size());
+  return 0;
+}
+
 // Snapshot-load P&M scan over the commit files (LogReplay.loadTableProtocolAndMetadata,
 // internal/replay/LogReplay.java:220-314, reading PROTOCOL_METADATA_READ_SCHEMA through
 // DefaultJsonHandler): files newest first, read 16 at a time on host threads, stopping after the
@@ -2719,6 +2830,13 @@ struct dk_replay {
   std::vector<uint8_t*> probe_sel;
   DBuf d_probe_cols, d_probe_row0, d_probe_sel;
   bool probe_all = false;
+  // hash(path)-owner exchange (dk_replay_set_exchange): this rank's share of the commit-tail path
+  // hashes (sorted), per-chunk owner offsets, the send rows, and where the run stopped
+  int32_t xw = 0, xr = 0;                 // world, rank (xw = 0: the local probe)
+  DBuf d_owned, d_xbc, d_xtot, d_xg;
+  int64_t n_owned = 0, n_send = 0;
+  std::vector<unsigned long long> xtot;
+  int32_t xphase = 0;                     // 1: counted (run), 2: packed, 3: finished
   uint64_t mask = 0;
   uint32_t seed = 0;
   KTimer timer;
@@ -3073,10 +3191,13 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
   return 0;
 }
 
+static int replay_ckpt_filters(dk_replay* r);
 static int replay_launch(dk_replay* r) {
   hipStream_t s = r->stream;
   KTimer& T = r->timer;
   KTimer::Scope total(&T, 12, s);
+  r->xphase = 0;
+  if (r->xw > 0) HIPOK(hipMemsetAsync(r->d_xtot.p, 0, (size_t)r->xw * 8, s));
   DState st0{};
   st0.err_row = LLONG_MAX;
   HIPOK(hipMemcpyAsync(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
@@ -3113,7 +3234,7 @@ static int replay_launch(dk_replay* r) {
     HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;       // dvUniqueId stream of "no DV"
     dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
     const uint64_t h_nodv = kd.hs.final_(kd.n);
-    if (r->probe_all) {
+    if (r->probe_all || r->xw > 0) {
       KTimer::Scope sc(&T, 11, s);
       const size_t nf = r->probe.size();
       r->probe_run = r->probe;
@@ -3129,6 +3250,15 @@ static int replay_launch(dk_replay* r) {
           upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
       ProbeSet PS{r->d_probe_cols.as<ProbeCols>(), r->d_probe_row0.as<int64_t>(), r->d_probe_sel.as<uint8_t* const>(),
                   (int32_t)nf, r->probe_row0[nf]};
+      if (r->xw > 0) {
+        // exchange mode: route counts only; dk_replay_exchange_pack / _filter / _finish do the rest
+        long long chunk;
+        const int nb = a2a_blocks(PS.total, &chunk);
+        if (r->d_xbc.alloc((size_t)nb * r->xw * 8 + 64)) return 1;
+        launch_a2a_count(PS, r->xw, r->d_xbc.as<unsigned long long>(), r->d_xtot.as<unsigned long long>(), s);
+        r->xphase = 1;
+        return 0;
+      }
       launch_probe_all(PS, S, r->d_fp.as<uint32_t>(), r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv, r->d_cand.as<int32_t>(),
                        r->d_cand_n.as<unsigned int>(), st, s);
     } else {
@@ -3140,23 +3270,33 @@ static int replay_launch(dk_replay* r) {
                      r->d_csel[fi]->as<uint8_t>(), r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
       }
     }
-    if (r->has_part)                        // partition pruning on the checkpoint files' rows
-      for (size_t fi = 0; fi < r->ck_maps.size(); fi++) {
-        KTimer::Scope sc(&T, 18, s);
-        launch_part_eval(r->ck_maps[fi], r->d_part.as<DPartProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
-      }
-    if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
-      for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
-        KTimer::Scope sc(&T, 17, s);
-        if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
-          launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), s);
-        else
-          launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
-    }
-    // later work on the checkpoint's stream (column reads) sees the decoded columns
-    HIPOK(hipEventRecord(r->ev_out, s));
-    HIPOK(hipStreamWaitEvent(p->stream, r->ev_out, 0));
+    if (replay_ckpt_filters(r)) return 1;
   }
+  return 0;
+}
+
+// the checkpoint rows' partition pruning and data skipping after the probe, then the hand-back to
+// the checkpoint's own stream
+static int replay_ckpt_filters(dk_replay* r) {
+  hipStream_t s = r->stream;
+  KTimer& T = r->timer;
+  DState* st = r->d_state.as<DState>();
+  if (r->has_part)                        // partition pruning on the checkpoint files' rows
+    for (size_t fi = 0; fi < r->ck_maps.size(); fi++) {
+      KTimer::Scope sc(&T, 18, s);
+      launch_part_eval(r->ck_maps[fi], r->d_part.as<DPartProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+    }
+  if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
+    for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
+      KTimer::Scope sc(&T, 17, s);
+      if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
+        launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), s);
+      else
+        launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+    }
+  // later work on the checkpoint's stream (column reads) sees the decoded columns
+  HIPOK(hipEventRecord(r->ev_out, s));
+  HIPOK(hipStreamWaitEvent(r->ck->stream, r->ev_out, 0));
   return 0;
 }
 
@@ -3168,9 +3308,105 @@ extern "C" int dk_replay_run(dk_replay* r) {
   return replay_launch(r);
 }
 
+// ---- hash(path)-owner exchange ("alltoall" mode) ----
+extern "C" int dk_replay_set_exchange(dk_replay* r, int32_t world, int32_t rank) {
+  if (!r) return fail("null replay");
+  hipSetDevice(r->eng->cfg.device);
+  if (world <= 1) { r->xw = 0; return 0; }
+  if (world > 64 || rank < 0 || rank >= world) return fail("dk_replay_set_exchange: bad world / rank");
+  if (!r->tail) return fail("dk_replay_set_exchange: no commit tail");
+  // this rank's share of the commit tail's keys, by path hash (seed kDecodeSeed, the checkpoint
+  // columns' decode-time hash): simple paths only -- a simple checkpoint path never equals a
+  // non-simple tail path, and non-simple checkpoint paths stay local candidates
+  std::vector<uint64_t> own;
+  for (size_t i = 0; i < r->acts.size(); i++) {
+    const DJsonAction& a = r->acts[i];
+    if (a.kind != JA_ADD && a.kind != JA_REMOVE) continue;
+    const CB& pc = r->tail->col[a.kind == JA_ADD ? JL_PATH : JL_RPATH];
+    const int64_t row = r->act_row[i];
+    const uint8_t* p = pc.chars.data() + pc.offs[row];
+    const int32_t n = (int32_t)(pc.offs[row + 1] - pc.offs[row]);
+    auto load8 = [&](int32_t j) -> uint64_t {
+      uint64_t w = 0;
+      for (int b = 0; b < 8 && 8 * j + b < n; b++) w |= (uint64_t)p[8 * j + b] << (8 * b);
+      return w;
+    };
+    uint64_t hp = 0;
+    if (simple_path_hash(n, load8, kDecodeSeed, &hp) && hp % (uint64_t)world == (uint64_t)rank) own.push_back(hp);
+  }
+  std::sort(own.begin(), own.end());
+  own.erase(std::unique(own.begin(), own.end()), own.end());
+  r->n_owned = (int64_t)own.size();
+  if (upload(r->d_owned, own.data(), own.size() * 8, r->stream)) return 1;
+  if (r->d_xtot.alloc((size_t)world * 8 + 64)) return 1;
+  int64_t total = 0;
+  if (r->ck) for (auto& f : r->ck->files) total += f.num_rows;
+  if (r->d_cand.n < (size_t)total * 4 + 64 && r->d_cand.alloc((size_t)total * 4 + 64)) return 1;
+  if (r->d_xg.alloc((size_t)total * 4 + 64)) return 1;
+  HIPOK(hipStreamSynchronize(r->stream));
+  r->xw = world; r->xr = rank;
+  r->xtot.assign(world, 0);
+  return 0;
+}
+
+extern "C" int dk_replay_exchange_counts(dk_replay* r, int64_t* counts) {
+  hipSetDevice(r->eng->cfg.device);
+  if (r->xw <= 0 || r->xphase != 1) return fail("dk_replay_exchange_counts: no exchange-mode run");
+  HIPOK(hipStreamSynchronize(r->stream));
+  HIPOK(hipMemcpy(r->xtot.data(), r->d_xtot.p, (size_t)r->xw * 8, hipMemcpyDeviceToHost));
+  r->n_send = 0;
+  for (int o = 0; o < r->xw; o++) { counts[o] = (int64_t)r->xtot[o]; r->n_send += counts[o]; }
+  return 0;
+}
+
+extern "C" int dk_replay_exchange_pack(dk_replay* r, uint64_t* send) {
+  hipSetDevice(r->eng->cfg.device);
+  if (r->xw <= 0 || r->xphase != 1) return fail("dk_replay_exchange_pack: counts first");
+  hipStream_t s = r->stream;
+  if (r->ck && !r->probe_row0.empty() && r->probe_row0.back() > 0) {
+    ProbeSet PS{r->d_probe_cols.as<ProbeCols>(), r->d_probe_row0.as<int64_t>(), r->d_probe_sel.as<uint8_t* const>(),
+                (int32_t)r->probe.size(), r->probe_row0.back()};
+    KTimer::Scope sc(&r->timer, 11, s);
+    launch_a2a_pack(PS, r->xw, r->d_xbc.as<unsigned long long>(), send, r->d_xg.as<int32_t>(), r->d_cand.as<int32_t>(),
+                    r->d_cand_n.as<unsigned int>(), r->d_state.as<DState>(), s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  r->xphase = 2;
+  return 0;
+}
+
+extern "C" int dk_replay_exchange_filter(dk_replay* r, const uint64_t* recv, int64_t n, uint8_t* flags) {
+  hipSetDevice(r->eng->cfg.device);
+  if (r->xw <= 0) return fail("dk_replay_exchange_filter: not in exchange mode");
+  KTimer::Scope sc(&r->timer, 11, r->stream);
+  launch_a2a_filter(recv, n, r->d_owned.as<uint64_t>(), r->n_owned, flags, r->stream);
+  HIPOK(hipStreamSynchronize(r->stream));
+  return 0;
+}
+
+extern "C" int dk_replay_exchange_finish(dk_replay* r, const uint8_t* back) {
+  hipSetDevice(r->eng->cfg.device);
+  if (r->xw <= 0 || r->xphase != 2) return fail("dk_replay_exchange_finish: pack first");
+  hipStream_t s = r->stream;
+  if (r->ck) {
+    if (!r->probe_row0.empty() && r->probe_row0.back() > 0) {
+      ProbeSet PS{r->d_probe_cols.as<ProbeCols>(), r->d_probe_row0.as<int64_t>(), r->d_probe_sel.as<uint8_t* const>(),
+                  (int32_t)r->probe.size(), r->probe_row0.back()};
+      KTimer::Scope sc(&r->timer, 11, s);
+      launch_a2a_apply(PS, r->d_xg.as<int32_t>(), back, r->n_send, r->d_slots.as<Slot>(), r->mask, r->d_acts.as<DJsonAction>(),
+                       r->d_canon.as<uint8_t>(), r->seed, r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(),
+                       r->d_state.as<DState>(), s);
+    }
+    if (replay_ckpt_filters(r)) return 1;
+  }
+  r->xphase = 3;
+  return 0;
+}
+
 extern "C" int dk_replay_sync(dk_replay* r) {
   hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   hipStream_t s = r->stream;
+  if (r->xw > 0 && r->xphase != 3) return fail("dk_replay_sync: the exchange-mode run has not finished its exchange");
   for (int attempt = 0; attempt < 8; attempt++) {
     HIPOK(hipStreamSynchronize(s));
     r->timer.collect();
@@ -3178,7 +3414,11 @@ extern "C" int dk_replay_sync(dk_replay* r) {
     HIPOK(hipMemcpy(&r->h_state, r->d_state.p, sizeof(DState), hipMemcpyDeviceToHost));
     if (r->h_state.err_flags & E_COLLISION) {     // 64-bit key-hash collision: rebuild with a new seed
       r->seed++;
-      if (replay_launch(r)) return 1;
+      const int32_t xw = r->xw;                   // (exchange mode: the rebuilt run probes locally)
+      r->xw = 0;
+      const int rc = replay_launch(r);
+      r->xw = xw;
+      if (rc) return 1;
       continue;
     }
     if (r->h_state.err_flags & E_PART) {

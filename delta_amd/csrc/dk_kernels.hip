@@ -3860,6 +3860,184 @@ void launch_json_select(const DJsonAction* a, int n, const Slot* slots, uint64_t
                         DState* st, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_json_select, dim3((n + 255) / 256), dim3(256), 0, s, a, n, slots, mask, canon, sel, st);
 }
+// --------------------------------------------------------------------------------------------
+// hash(path)-owner exchange (multi-GPU "alltoall" mode; the repartition-by-path of
+// delta-spark's Snapshot.scala:478-483). Every rank routes its checkpoint add rows to the rank that
+// owns their path hash (owner = hp mod world), as 8-byte records {hp}; the owner answers one byte
+// per record -- 0: no commit-tail key of its share has this path hash, so the row's key is not in
+// the tail and the row is selected; 1: maybe -- and the origin runs the exact key probe
+// (k_probe_cand_all) on the maybes. Rows with no fast-path hash (dictionary / non-simple paths) or
+// with a deletion vector stay local candidates. A2A_ROWS rows per workgroup chunk; the send buffer
+// is owner-major, chunks in order inside each owner (a radix partition: count, scan, pack).
+// --------------------------------------------------------------------------------------------
+constexpr int A2A_MAXW = 64;          // ranks
+__device__ __forceinline__ int a2a_class(const ProbeCols& pc, long long r, uint64_t* hp) {
+  if (r >= pc.n_rows || pc.path_def[r] < 1) return 0;                     // no add in this row
+  *hp = pc.path_hash ? pc.path_hash[r] : 0ull;
+  if (*hp == 0ull || (pc.has_dv && pc.st_def[r] >= 2)) return 2;           // local candidate
+  return 1;                                                                // routed
+}
+__device__ __forceinline__ int a2a_owner(uint64_t hp, int world) { return (int)(hp % (uint64_t)world); }
+
+__global__ __launch_bounds__(NT) void k_a2a_count(ProbeSet PS, int world, long long chunk,
+                                                  unsigned long long* __restrict__ bc) {
+  __shared__ unsigned int cnt[A2A_MAXW];
+  for (int o = threadIdx.x; o < world; o += NT) cnt[o] = 0;
+  __syncthreads();
+  const long long g0 = (long long)blockIdx.x * chunk, g1 = g0 + chunk < PS.total ? g0 + chunk : PS.total;
+  for (long long g = g0 + threadIdx.x; g < g1; g += NT) {
+    const int f = probe_file(PS.row0, PS.n_files, g);
+    uint64_t hp = 0;
+    if (a2a_class(PS.cols[f], g - PS.row0[f], &hp) == 1) atomicAdd(&cnt[a2a_owner(hp, world)], 1u);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < world; o += NT) bc[(long long)blockIdx.x * world + o] = cnt[o];
+}
+
+// bc[b][o] -> exclusive offsets in owner-major order; totals[o] = records for owner o
+__global__ void k_a2a_scan(unsigned long long* __restrict__ bc, int nb, int world,
+                           unsigned long long* __restrict__ totals) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  unsigned long long run = 0;
+  for (int o = 0; o < world; o++) {
+    unsigned long long t = 0;
+    for (int b = 0; b < nb; b++) {
+      const unsigned long long c = bc[(long long)b * world + o];
+      bc[(long long)b * world + o] = run + t;
+      t += c;
+    }
+    totals[o] = t;
+    run += t;
+  }
+}
+
+__global__ __launch_bounds__(NT) void k_a2a_pack(ProbeSet PS, int world, long long chunk,
+                                                 const unsigned long long* __restrict__ boff, uint64_t* __restrict__ send_h,
+                                                 int32_t* __restrict__ send_g, int32_t* __restrict__ cand,
+                                                 unsigned int* __restrict__ cand_n, DState* __restrict__ st) {
+  __shared__ unsigned long long cur[A2A_MAXW];
+  __shared__ unsigned int tcnt[A2A_MAXW];
+  for (int o = threadIdx.x; o < world; o += NT) { cur[o] = boff[(long long)blockIdx.x * world + o]; tcnt[o] = 0; }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  unsigned long long n_seen = 0;
+  const long long g0 = (long long)blockIdx.x * chunk, g1 = g0 + chunk < PS.total ? g0 + chunk : PS.total;
+  for (long long t0 = g0; t0 < g1; t0 += NT) {
+    const long long g = t0 + threadIdx.x;
+    int cls = 0, own = 0;
+    uint64_t hp = 0;
+    unsigned int rank = 0;
+    if (g < g1) {
+      const int f = probe_file(PS.row0, PS.n_files, g);
+      const long long r = g - PS.row0[f];
+      cls = a2a_class(PS.cols[f], r, &hp);
+      if (cls == 0) PS.sel[f][r] = 0;
+      if (cls == 1) { own = a2a_owner(hp, world); rank = atomicAdd(&tcnt[own], 1u); }
+    }
+    const uint64_t m = __ballot(cls == 2);
+    if (m) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(cand_n, (unsigned int)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (cls == 2) cand[base + lane_rank(m)] = (int32_t)g;
+    }
+    __syncthreads();
+    if (cls == 1) {
+      const unsigned long long pos = cur[own] + rank;
+      send_h[pos] = hp;
+      send_g[pos] = (int32_t)g;
+    }
+    n_seen += cls != 0;
+    __syncthreads();
+    for (int o = threadIdx.x; o < world; o += NT) { cur[o] += tcnt[o]; tcnt[o] = 0; }
+    __syncthreads();
+  }
+  block_count3(st, n_seen, 0, 0);
+}
+
+// owner side: flag = 1 iff hp is among this rank's commit-tail path hashes (sorted)
+__global__ __launch_bounds__(NT) void k_a2a_filter(const uint64_t* __restrict__ recv, long long n,
+                                                   const uint64_t* __restrict__ owned, long long n_owned,
+                                                   uint8_t* __restrict__ flags) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const uint64_t h = recv[i];
+    long long lo = 0, hi = n_owned;
+    while (lo < hi) { const long long mid = (lo + hi) >> 1; if (owned[mid] < h) lo = mid + 1; else hi = mid; }
+    flags[i] = lo < n_owned && owned[lo] == h;
+  }
+}
+
+// origin side: answers back in send order; 0 decides the row (selected), 1 makes it a candidate
+__global__ __launch_bounds__(NT) void k_a2a_apply(ProbeSet PS, const int32_t* __restrict__ send_g,
+                                                  const uint8_t* __restrict__ back, long long n,
+                                                  int32_t* __restrict__ cand, unsigned int* __restrict__ cand_n,
+                                                  DState* __restrict__ st) {
+  unsigned long long n_chosen = 0;
+  const int lane = threadIdx.x & 63;
+  for (long long i0 = (long long)blockIdx.x * NT; i0 < n; i0 += (long long)gridDim.x * NT) {
+    const long long i = i0 + threadIdx.x;
+    bool maybe = false;
+    if (i < n) {
+      const long long g = send_g[i];
+      maybe = back[i] != 0;
+      if (!maybe) {
+        const int f = probe_file(PS.row0, PS.n_files, g);
+        PS.sel[f][g - PS.row0[f]] = 1;
+        n_chosen++;
+      }
+    }
+    const uint64_t m = __ballot(maybe);
+    if (m) {
+      unsigned int base = 0;
+      if (lane == 0) base = atomicAdd(cand_n, (unsigned int)__popcll(m));
+      base = __shfl(base, 0, 64);
+      if (maybe) cand[base + lane_rank(m)] = send_g[i];
+    }
+  }
+  block_count3(st, 0, n_chosen, 0);
+}
+
+int a2a_blocks(long long total, long long* chunk) {
+  long long nb = (total + 16383) / 16384;               // >= 16 Ki rows per workgroup
+  if (nb > 2048) nb = 2048;
+  if (nb < 1) nb = 1;
+  *chunk = (total + nb - 1) / nb;
+  if (*chunk < 1) *chunk = 1;
+  return (int)nb;
+}
+void launch_a2a_count(const ProbeSet& PS, int world, unsigned long long* bc, unsigned long long* totals, hipStream_t s) {
+  long long chunk;
+  const int nb = a2a_blocks(PS.total, &chunk);
+  hipLaunchKernelGGL(k_a2a_count, dim3(nb), dim3(NT), 0, s, PS, world, chunk, bc);
+  hipLaunchKernelGGL(k_a2a_scan, dim3(1), dim3(64), 0, s, bc, nb, world, totals);
+}
+void launch_a2a_pack(const ProbeSet& PS, int world, const unsigned long long* boff, uint64_t* send_h, int32_t* send_g,
+                     int32_t* cand, unsigned int* cand_n, DState* st, hipStream_t s) {
+  long long chunk;
+  const int nb = a2a_blocks(PS.total, &chunk);
+  hipMemsetAsync(cand_n, 0, sizeof(unsigned int), s);
+  hipLaunchKernelGGL(k_a2a_pack, dim3(nb), dim3(NT), 0, s, PS, world, chunk, boff, send_h, send_g, cand, cand_n, st);
+}
+void launch_a2a_filter(const uint64_t* recv, long long n, const uint64_t* owned, long long n_owned, uint8_t* flags,
+                       hipStream_t s) {
+  if (n <= 0) return;
+  const long long want = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_a2a_filter, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(NT), 0, s, recv, n, owned, n_owned, flags);
+}
+void launch_a2a_apply(const ProbeSet& PS, const int32_t* send_g, const uint8_t* back, long long n, const Slot* slots,
+                      uint64_t mask, const DJsonAction* acts, const uint8_t* canon, uint32_t seed, int32_t* cand,
+                      unsigned int* cand_n, DState* st, hipStream_t s) {
+  if (n > 0) {
+    const long long want = (n + NT - 1) / NT;
+    hipLaunchKernelGGL(k_a2a_apply, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(NT), 0, s, PS, send_g, back, n,
+                       cand, cand_n, st);
+  }
+  if (PS.total > 0) {
+    const long long want = (PS.total + NT - 1) / NT;
+    hipLaunchKernelGGL(k_probe_cand_all, dim3((unsigned)(want < 4096 ? want : 4096)), dim3(NT), 0, s, PS, slots, mask,
+                       acts, canon, seed, cand, cand_n, st);
+  }
+}
 void launch_probe_all(const ProbeSet& PS, const Slot* slots, const uint32_t* fp, uint64_t mask, const DJsonAction* acts,
                       const uint8_t* canon, uint32_t seed, uint64_t h_nodv, int32_t* cand, unsigned int* cand_n,
                       DState* st, hipStream_t s) {

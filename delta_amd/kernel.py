@@ -813,9 +813,18 @@ class Snapshot:
             J = self._json_batch_size
             for i in range(scanned.value):
                 def action(off, ln, key):
-                    with open(deltas[i].path, "rb") as f:
-                        f.seek(off)
-                        return json.loads(f.read(ln).decode("utf-8", "replace"))[key]
+                    # decoded in libdkgpu with DefaultJsonRow's rules (dk_json_pm_decode), handed
+                    # back re-serialised with exactly the schema's fields
+                    path = deltas[i].path.encode()
+                    which = 0 if key == "protocol" else 1
+                    n = C.c_int64()
+                    buf = C.create_string_buffer(2 * int(ln) + 256)
+                    rc = lib().dk_json_pm_decode(path, off, ln, which, buf, len(buf), C.byref(n))
+                    if rc == 2:
+                        buf = C.create_string_buffer(int(n.value) + 16)
+                        rc = lib().dk_json_pm_decode(path, off, ln, which, buf, len(buf), C.byref(n))
+                    check(rc)
+                    return json.loads(buf.raw[:n.value].decode("utf-8"))
                 # batches of J lines per commit file (DefaultJsonHandler): in line order
                 events = sorted([(pl[i] // J, 0, "p")] * (pl[i] >= 0) + [(ml[i] // J, 1, "m")] * (ml[i] >= 0))
                 b = 0
@@ -982,13 +991,20 @@ class ScanBuilder:
         self.read_stats = flag
         return self
 
-    def withShard(self, world, rank):
-        """Reconcile only this rank's checkpoint files (delta_amd/shard.py)."""
+    def withShard(self, world, rank, exchange=None):
+        """Reconcile only this rank's checkpoint row groups (delta_amd/shard.py). exchange: None (the
+        probe runs against this rank's own copy of the commit-tail key table), or a callable that
+        drives the hash(path)-owner exchange for this rank (shard.exchange_hash_owner over
+        torch.distributed, or an in-process loopback), called with the scan's ExchangeSide after
+        every run."""
         self.shard = (int(world), int(rank))
+        self.exchange = exchange
         return self
 
     def build(self):
-        return GpuScan(self.snapshot, self.read_stats, self.shard, self.predicate)
+        sc = GpuScan(self.snapshot, self.read_stats, self.shard, self.predicate)
+        sc.exchange = getattr(self, "exchange", None)
+        return sc
 
 
 class LazyColumns(dict):
@@ -1148,6 +1164,8 @@ class GpuScan:
         if self.ckpt is not None:
             check(lib().dk_replay_attach_checkpoint(self._rh, self.ckpt._h))
         self.prepare_ms["replay_attach"] = (time.perf_counter() - t3) * 1e3
+        if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
+            check(lib().dk_replay_set_exchange(self._rh, self.shard[0], self.shard[1]))
         if self.partition is not None:
             from . import partitions as pp
             pprog = pp.pack(self.partition, dk_part_program)
@@ -1215,8 +1233,12 @@ class GpuScan:
         return self.data_filter
 
     def run(self):
-        """The device step: commit-tail keys + table, checkpoint decode, probe, selection."""
+        """The device step: commit-tail keys + table, checkpoint decode, probe, selection (with an
+        exchange: decode + routing, the exchange, then the probe of the rows the owners flagged)."""
         check(lib().dk_replay_run(self._rh))
+        if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
+            from .shard import ExchangeSide
+            self.exchange(ExchangeSide(self))
 
     def sync(self):
         check(lib().dk_replay_sync(self._rh))

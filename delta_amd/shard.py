@@ -236,3 +236,112 @@ def scan_units(scan, device_bits=False):
         n = scan.ckpt.num_rows(fi)
         units.append((scan.ckpt_index[fi], scan.ckpt.row_offset(fi), n, scan.selection_bits(fi, device=device_bits)))
     return units
+
+
+# ------------------------------------------------------------------------------------------------
+# hash(path)-owner exchange ("alltoall" mode)
+#
+# delta-spark reconciles a snapshot by repartitioning every action by its path
+# (spark/.../Snapshot.scala:478-483, repartition(coalesce(add.path, remove.path))). Here each rank
+# decodes its row-group shard of the checkpoint; every add row with a fast-path key hash is routed
+# as an 8-byte record {path hash} to its owner rank, path_owner(hash, world); the owner holds the
+# commit-tail path hashes of its share and answers one byte per record (1: a tail key with that path
+# hash exists); answers return in send order by the reverse all-to-all, and the origin selects the
+# rows answered 0 and runs the exact key probe on the rest (dk_replay_exchange_*).
+# ------------------------------------------------------------------------------------------------
+def path_owner(path_hash: int, world: int) -> int:
+    """The rank that owns a key: its canonical-path hash (seed 0, dk_uri.h) modulo the world size
+    (a2a_owner in dk_kernels.hip)."""
+    return int(path_hash % world)
+
+
+class ExchangeSide:
+    """One rank's side of the exchange over a GpuScan's replay (device buffers: torch tensors on the
+    scan's GPU, filled and read by libdkgpu)."""
+
+    def __init__(self, scan):
+        import torch
+        self.scan = scan
+        self.world, self.rank = scan.shard
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def counts(self):
+        import ctypes as C
+        import numpy as np
+        from ._lib import check, lib
+        c = np.zeros(self.world, np.int64)
+        check(lib().dk_replay_exchange_counts(self.scan._rh, c.ctypes.data_as(C.POINTER(C.c_int64))))
+        return c
+
+    def pack(self, n):
+        import ctypes as C
+        import torch
+        from ._lib import check, lib
+        send = torch.empty(max(1, n), dtype=torch.int64, device=self.device)
+        check(lib().dk_replay_exchange_pack(self.scan._rh, C.c_void_p(send.data_ptr())))
+        return send[:n]
+
+    def filter(self, recv):
+        import ctypes as C
+        import torch
+        from ._lib import check, lib
+        recv = recv.to(self.device).contiguous()
+        flags = torch.empty(max(1, recv.numel()), dtype=torch.uint8, device=self.device)
+        torch.cuda.current_stream().synchronize()           # the received records have landed
+        check(lib().dk_replay_exchange_filter(self.scan._rh, C.c_void_p(recv.data_ptr()), recv.numel(),
+                                              C.c_void_p(flags.data_ptr())))
+        return flags[:recv.numel()]
+
+    def finish(self, back):
+        import ctypes as C
+        import torch
+        from ._lib import check, lib
+        back = back.to(self.device).contiguous()
+        torch.cuda.current_stream().synchronize()
+        check(lib().dk_replay_exchange_finish(self.scan._rh, C.c_void_p(back.data_ptr())))
+        self._keep = back                                    # alive until the replay has read it
+
+
+def exchange_hash_owner(side, group=None, device=None):
+    """Drive one exchange for this rank over torch.distributed: sizes, records (all_to_all_single),
+    the owners' answers back (the reverse all_to_all_single). device: where the collective's tensors
+    live -- "cuda" for RCCL over xGMI, None / "cpu" for gloo. Returns the bytes this rank sent."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    counts = side.counts()
+    n_send = int(counts.sum())
+    send = side.pack(n_send).to(dev)
+    c = torch.tensor(counts, dtype=torch.int64, device=dev)
+    rc = torch.empty_like(c)
+    dist.all_to_all_single(rc, c, group=group)
+    rcl = [int(x) for x in rc.cpu().tolist()]
+    recv = torch.empty(max(1, sum(rcl)), dtype=torch.int64, device=dev)[:sum(rcl)]
+    dist.all_to_all_single(recv, send, output_split_sizes=rcl, input_split_sizes=[int(x) for x in counts], group=group)
+    flags = side.filter(recv).to(dev)
+    back = torch.empty(max(1, n_send), dtype=torch.uint8, device=dev)[:n_send]
+    dist.all_to_all_single(back, flags, output_split_sizes=[int(x) for x in counts], input_split_sizes=rcl, group=group)
+    side.finish(back)
+    return 9 * n_send
+
+
+def exchange_local(sides):
+    """The same exchange between ranks simulated in one process (every side's counts / pack first,
+    then every owner's filter, then every origin's finish): tests and single-GPU rehearsals."""
+    import torch
+    world = len(sides)
+    counts = [s.counts() for s in sides]
+    sends = [s.pack(int(c.sum())) for s, c in zip(sides, counts)]
+    offs = [[0] + list(torch.cumsum(torch.tensor(c), 0).tolist()) for c in counts]
+    flags = []
+    for o in range(world):
+        recv = torch.cat([sends[s][offs[s][o]:offs[s][o + 1]].to(sends[o].device if sends[o].numel() else sends[s].device)
+                          for s in range(world)]) if world else None
+        flags.append((sides[o].filter(recv), [int(counts[s][o]) for s in range(world)]))
+    for s in range(world):
+        parts = []
+        for o in range(world):
+            f, seg = flags[o]
+            a = sum(seg[:s])
+            parts.append(f[a:a + seg[s]].to(sends[s].device))
+        sides[s].finish(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8))

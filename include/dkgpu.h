@@ -246,6 +246,11 @@ int64_t dk_json_tail_checkpoint_row0(dk_json_tail* t);
  * internal/replay/LogReplay.java:220-314): per file, the line index and byte range of the first line
  * with a non-null top-level "protocol" / "metaData" (-1: none). Files are read 16 at a time on host
  * threads; the scan stops after the block in which both were seen (*n_scanned = files scanned). */
+/* One commit line's protocol (which = 0) or metaData (which = 1) action, bytes [off, off + len) of
+ * `path`, decoded with DefaultJsonRow's rules for Protocol / Metadata FULL_SCHEMA and re-serialised
+ * as JSON with exactly the schema's fields. Returns 2 (with *out_len set) when cap is too small. */
+int  dk_json_pm_decode(const char* path, int64_t off, int64_t len, int32_t which, char* out, int64_t cap,
+                       int64_t* out_len);
 int  dk_log_pm_scan(const char* const* paths, int32_t n, int64_t* p_line, int64_t* p_off, int64_t* p_len,
                     int64_t* m_line, int64_t* m_off, int64_t* m_len, int32_t* n_scanned);
 int  dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out);
@@ -341,6 +346,23 @@ int  dk_replay_ckpt_selection_bits(dk_replay* r, int32_t file, void* dst, int64_
  * the multi-GPU exchange writes its collective buffer with it */
 int  dk_replay_ckpt_selection_bits_all(dk_replay* r, void* dst, const int64_t* offsets, int32_t dst_on_device);
 /* per-kernel average device time (us) over recorded runs (DK_FLAG_TIMING); names via index */
+/* hash(path)-owner exchange (multi-GPU "alltoall" mode; the repartition of actions by path that
+ * delta-spark's Snapshot.scala:478-483 performs). After dk_replay_set_exchange(r, world, rank),
+ * dk_replay_run stops after the decode and routing counts; the caller then drives one exchange:
+ *   dk_replay_exchange_counts   records this rank sends to each rank (int64[world])
+ *   dk_replay_exchange_pack     the 8-byte records {path hash} into `send` (device, owner-major)
+ *   (all-to-all of the records)
+ *   dk_replay_exchange_filter   owner side: one byte per received record (1: some commit-tail key
+ *                               of this rank's share has that path hash), into `flags` (device)
+ *   (reverse all-to-all of the flags, in the order the records were sent)
+ *   dk_replay_exchange_finish   rows answered 0 are selected; the rest take the exact key probe
+ * then dk_replay_sync as usual. Every call orders itself on the replay's stream and returns with
+ * the stream drained, so the caller's collectives may touch the buffers. world <= 64. */
+int  dk_replay_set_exchange(dk_replay* r, int32_t world, int32_t rank);
+int  dk_replay_exchange_counts(dk_replay* r, int64_t* counts);
+int  dk_replay_exchange_pack(dk_replay* r, uint64_t* send);
+int  dk_replay_exchange_filter(dk_replay* r, const uint64_t* recv, int64_t n, uint8_t* flags);
+int  dk_replay_exchange_finish(dk_replay* r, const uint8_t* back);
 int  dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count);
 void dk_replay_free(dk_replay* r);
 

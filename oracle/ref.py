@@ -762,17 +762,58 @@ def _pm_json_protocol(p):
     for k in ("minReaderVersion", "minWriterVersion"):
         if not _is_int(p.get(k)):
             raise OracleError("protocol.%s: expected an int, got %r" % (k, p.get(k)))
+    for k in ("readerFeatures", "writerFeatures"):
+        if p.get(k) is not None:
+            _json_str_array(p[k], "protocol." + k)
     return {"minReaderVersion": p["minReaderVersion"], "minWriterVersion": p["minWriterVersion"],
             "readerFeatures": list(p.get("readerFeatures") or []), "writerFeatures": list(p.get("writerFeatures") or [])}
 
 
+def _json_str(v, what):
+    """DefaultJsonRow StringType: a JSON string (isTextual)."""
+    if not isinstance(v, str):
+        raise OracleError("%s: expected a string, got %r" % (what, v))
+    return v
+
+
+def _json_str_array(v, what):
+    """ArrayType(string, containsNull = false) (DefaultJsonRow.java:265-290)."""
+    if not isinstance(v, list):
+        raise OracleError("%s: expected an array" % what)
+    if any(x is None for x in v):
+        raise OracleError("%s: Array type expects no nulls as elements" % what)
+    return [_json_str(x, what) for x in v]
+
+
+def _json_str_map(v, what):
+    """MapType(string, string, valueContainsNull = false) (DefaultJsonRow.java:298-320)."""
+    if not isinstance(v, dict):
+        raise OracleError("%s: expected a map" % what)
+    if any(x is None for x in v.values()):
+        raise OracleError("%s: Map type expects no nulls in values" % what)
+    return {k: _json_str(x, what) for k, x in v.items()}
+
+
 def _pm_json_metadata(m):
-    """Metadata.fromColumnVector over a commit-JSON metaData (Metadata.java:35-55)."""
+    """Metadata.fromColumnVector over a commit-JSON metaData (Metadata.java:35-72, Format.java:42-48)
+    decoded with DefaultJsonRow's rules (DefaultJsonRow.java:136-357)."""
     for k in ("id", "format", "schemaString", "partitionColumns", "configuration"):
         if m.get(k) is None:
             raise OracleError("metaData.%s is required" % k)
     if m.get("createdTime") is not None and not _is_long(m["createdTime"]):
         raise OracleError("metaData.createdTime: expected a long")
+    for k in ("id", "schemaString"):
+        _json_str(m[k], "metaData." + k)
+    for k in ("name", "description"):
+        if m.get(k) is not None:
+            _json_str(m[k], "metaData." + k)
+    if not isinstance(m["format"], dict) or m["format"].get("provider") is None:
+        raise OracleError("metaData.format.provider is required")
+    _json_str(m["format"]["provider"], "format.provider")
+    if m["format"].get("options") is not None:
+        _json_str_map(m["format"]["options"], "format.options")
+    _json_str_array(m["partitionColumns"], "metaData.partitionColumns")
+    _json_str_map(m["configuration"], "metaData.configuration")
     fmt = m["format"]
     return {"id": m["id"], "name": m.get("name"), "description": m.get("description"),
             "format": {"provider": fmt.get("provider"), "options": dict(fmt.get("options") or {})},

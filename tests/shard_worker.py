@@ -1,6 +1,7 @@
 """One rank of tests/test_shard.py::test_gpu_two_processes_gloo (not a test module): scan this
 rank's row-group shard on the GPU, gather counters + selection bitmaps over gloo, and have rank 0
-write them to a JSON file. Usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR/PORT=.. python shard_worker.py TABLE OUT"""
+write them to a JSON file. Usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR/PORT=.. python shard_worker.py TABLE OUT [alltoall]
+(alltoall: the probe goes through the hash(path)-owner exchange, its collectives over gloo)"""
 import json
 import os
 import sys
@@ -19,7 +20,8 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     eng = K.GpuEngine()
     snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
-    scan = snap.getScanBuilder().withShard(world, rank).build()
+    a2a = len(sys.argv) > 3 and sys.argv[3] == "alltoall"
+    scan = snap.getScanBuilder().withShard(world, rank, exchange=shard.exchange_hash_owner if a2a else None).build()
     scan.prepare(eng)
     scan.run()
     scan.sync()

@@ -240,9 +240,11 @@ def test_gpu_row_group_shards(tmp_path, world, spec):
 
 
 @pytest.mark.gpu
-def test_gpu_two_processes_gloo(tmp_path):
-    """Two processes on the GPU, each scanning its row-group shard with the product, merge
-    counters and selection bitmaps with gather_selections over gloo; rank 0 checks the oracle."""
+@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+def test_gpu_two_processes_gloo(tmp_path, mode):
+    """Two processes on the GPU, each scanning its row-group shard with the product (alltoall: its
+    rows routed to their path-hash owners and answered back), merge counters and selection bitmaps
+    with gather_selections over gloo; rank 0 checks the oracle."""
     import json
     import subprocess
     import sys
@@ -252,7 +254,7 @@ def test_gpu_two_processes_gloo(tmp_path):
     port = _free_port()
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "shard_worker.py")
     out = str(tmp_path / "res.json")
-    procs = [subprocess.Popen([sys.executable, worker, table, out],
+    procs = [subprocess.Popen([sys.executable, worker, table, out, mode],
                               env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
                                        MASTER_PORT=str(port)))
              for r in range(2)]
