@@ -509,10 +509,9 @@ def main(argv=None):
                 size_sum += int(v.sum())
                 n_sel += b.size
             else:
-                # sum over the selected rows = all rows minus the (few) unselected ones
-                uns = np.flatnonzero(~b.selection)
-                size_sum += int(v.sum()) - int(v[uns].sum())
-                n_sel += b.size - len(uns)
+                # a masked reduction over the selected rows (no gather, no temporaries)
+                size_sum += int(v.sum(where=b.selection))
+                n_sel += int(np.count_nonzero(b.selection))
             if capture_result:
                 if b.file_index < 0:
                     pc = b.data["add.path"]
