@@ -77,6 +77,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_json_tail_parse_parts", "dk_json_tail_checkpoint_row0",
            "dk_replay_set_exchange", "dk_replay_exchange_counts", "dk_replay_exchange_pack", "dk_replay_exchange_filter",
            "dk_replay_exchange_finish", "dk_json_pm_decode",
+           "dk_ckpt_writer_open", "dk_ckpt_writer_add_json", "dk_ckpt_writer_add_checkpoint_adds", "dk_ckpt_writer_close",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
@@ -132,6 +133,10 @@ def lib(build_if_missing=True):
         "dk_json_tail_checkpoint_row0": (I64, [P]),
         "dk_replay_set_exchange": (C.c_int, [P, I32, I32]),
         "dk_json_pm_decode": (C.c_int, [C.c_char_p, I64, I64, I32, C.c_char_p, I64, C.POINTER(I64)]),
+        "dk_ckpt_writer_open": (C.c_int, [P, C.c_char_p, I32, C.POINTER(P)]),
+        "dk_ckpt_writer_add_json": (C.c_int, [P, C.c_char_p, I64]),
+        "dk_ckpt_writer_add_checkpoint_adds": (C.c_int, [P, P, I32, I64, I64, C.POINTER(I64)]),
+        "dk_ckpt_writer_close": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
         "dk_replay_exchange_counts": (C.c_int, [P, C.POINTER(I64)]),
         "dk_replay_exchange_pack": (C.c_int, [P, P]),
         "dk_replay_exchange_filter": (C.c_int, [P, P, I64, P]),

@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdkgpu.so")
-SOURCES = ["dk_host.cpp", "dk_kernels.hip", "dk_arrow.hip", "dk_dv.hip"]
+SOURCES = ["dk_host.cpp", "dk_kernels.hip", "dk_arrow.hip", "dk_dv.hip", "dk_encode.hip"]
 HEADERS = ["dk_device.h", "dk_thrift.h", "dk_uri.h"]
 
 

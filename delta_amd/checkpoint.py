@@ -241,10 +241,15 @@ def _checkpoint_other_rows(engine, files):
     return out
 
 
-def checkpoint_actions(engine, snapshot, now_ms=None):
+def checkpoint_actions(engine, snapshot, now_ms=None, sink=None):
     """CreateCheckpointIterator's output: the selected rows of every batch, batches in reverse log
     order and rows in batch order, as (action name, value dict) pairs; plus the number of add
-    actions kept (getNumberOfAddActions)."""
+    actions kept (getNumberOfAddActions).
+
+    sink (the GPU encoder): instead of materialising the old checkpoint's surviving adds, every
+    maximal run of checkpoint rows between two other actions is handed over as
+    sink(("ckpt", scan, file, row0, row1)) -- the device gathers those rows by the replay's
+    selection -- with the rows before it flushed first as sink(("rows", [(action, value)...]))."""
     md = snapshot.metadata
     retention = interval_ms((md.get("configuration") or {}).get("delta.deletedFileRetentionDuration",
                                                                  "interval 1 week"))
@@ -263,7 +268,8 @@ def checkpoint_actions(engine, snapshot, now_ms=None):
 
     try:
         batches = scan.getScanFiles(engine)
-        tail = next(batches) if scan.tail.rows else None
+        n_commit_rows = int(scan.tail.ckpt_row0)          # (a V2 JSON manifest's rows follow them)
+        tail = next(batches) if n_commit_rows else None
         # commit rows: the JSON lines in tail order (newest commit first); the add selection is the
         # GPU replay's, the rest follows processRemoves / processProtocol / ... row by row
         row = 0
@@ -304,14 +310,31 @@ def checkpoint_actions(engine, snapshot, now_ms=None):
                     dm = obj["domainMetadata"]
                     if first("domainMetadata", dm.get("domain")):
                         out.append(("domainMetadata", {k: dm.get(k) for k in ("domain", "configuration", "removed")}))
-        if tail is not None and row != scan.tail.rows:
+        if tail is not None and row != n_commit_rows:
             raise DkError("commit tail rows do not match the commit lines")
         # checkpoint rows in file order: adds the GPU replay kept; the first protocol / metaData /
         # txn per appId / domainMetadata per domain
         others = _checkpoint_other_rows(engine, list(scan.ckpt_files or []))
         for fi, b in enumerate(batches):
-            sel = set(int(r) for r in b.selected_rows())
             oth = others[fi] if fi < len(others) else {}
+            if sink is not None and b.file_index >= 0:
+                # runs of rows between the other actions go to the device encoder whole
+                r0 = 0
+                for r in sorted(oth) + [b.size]:
+                    if r > r0:
+                        sink(("rows", out))
+                        out = []
+                        sink(("ckpt", scan, fi, r0, r))
+                    if r < b.size:
+                        kind, v = oth[r]
+                        key = 0 if kind in ("protocol", "metaData") else (v["appId"] if kind == "txn" else v["domain"])
+                        if first(kind, key):
+                            out.append((kind, snapshot.protocol if kind == "protocol" else
+                                        snapshot.metadata if kind == "metaData" else v))
+                    r0 = r + 1
+                n_adds += int(b.size if b.selection is None else np.count_nonzero(b.selection))
+                continue
+            sel = set(int(r) for r in b.selected_rows())
             for r in sorted(sel | set(oth)):
                 if r in sel:
                     out.append(("add", _add_from_cols(b.data, r)))
@@ -322,9 +345,55 @@ def checkpoint_actions(engine, snapshot, now_ms=None):
                 if first(kind, key):
                     out.append((kind, snapshot.protocol if kind == "protocol" else
                                 snapshot.metadata if kind == "metaData" else v))
+        if sink is not None:
+            sink(("rows", out))
+            out = []
     finally:
         scan.close()
     return out, n_adds
+
+
+def _json_value(kind, v):
+    """A checkpoint row's value as the JSON object the device encoder shreds (maps as objects)."""
+    if v is None:
+        return None
+    if kind == "metaData":
+        return {"id": v["id"], "name": v.get("name"), "description": v.get("description"),
+                "format": {"provider": v["format"]["provider"], "options": dict(v["format"].get("options") or {})},
+                "schemaString": v["schemaString"], "partitionColumns": v["partitionColumns"],
+                "createdTime": v.get("createdTime"), "configuration": dict(v.get("configuration") or {})}
+    if kind in ("add", "remove"):
+        v = dict(v)
+        for m in ("partitionValues", "tags"):
+            if isinstance(v.get(m), list):
+                v[m] = dict(v[m])
+    return v
+
+
+def _write_gpu(engine, snap, path, now_ms, codec=1):
+    """The checkpoint file encoded on the device (dk_ckpt_writer_*): action rows built here go over
+    as JSON lines, the old checkpoint's surviving adds never leave the GPU."""
+    import ctypes as C
+    from ._lib import check, lib
+    w = C.c_void_p()
+    check(lib().dk_ckpt_writer_open(engine._h, path.encode(), codec, C.byref(w)))
+    try:
+        def sink(item):
+            if item[0] == "rows":
+                if item[1]:
+                    text = "\n".join(json.dumps({k: _json_value(k, v)}) for k, v in item[1]).encode()
+                    check(lib().dk_ckpt_writer_add_json(w, text, len(text)))
+            else:
+                _, scan, fi, r0, r1 = item
+                n = C.c_int64()
+                check(lib().dk_ckpt_writer_add_checkpoint_adds(w, scan._rh, fi, r0, r1, C.byref(n)))
+        _, n_adds = checkpoint_actions(engine, snap, now_ms, sink=sink)
+    except BaseException:
+        lib().dk_ckpt_writer_close(w, None, None)
+        raise
+    nr, size = C.c_int64(), C.c_int64()
+    check(lib().dk_ckpt_writer_close(w, C.byref(nr), C.byref(size)))
+    return n_adds
 
 
 def _arrow_value(kind, v):
@@ -338,11 +407,10 @@ def _arrow_value(kind, v):
     return v
 
 
-def write_checkpoint(engine, table_path, now_ms=None):
+def write_checkpoint(engine, table_path, now_ms=None, encoder="gpu"):
     """SnapshotManager.checkpoint at the latest version: <v>.checkpoint.parquet + _last_checkpoint.
+    encoder "gpu": the file is encoded on the device (dk_ckpt_writer_*); "host": pyarrow.
     Returns (version, number of add actions)."""
-    import pyarrow as pa
-    import pyarrow.parquet as pq
     from .kernel import Table
     snap = Table.forPath(engine, table_path).getLatestSnapshot(engine)
     v = snap.getVersion()
@@ -351,16 +419,26 @@ def write_checkpoint(engine, table_path, now_ms=None):
     final = os.path.join(log, "%020d.checkpoint.parquet" % v)
     if os.path.exists(final):
         raise CheckpointAlreadyExistsException("Checkpoint for given version %d already exists in the table" % v)
-    actions, n_adds = checkpoint_actions(engine, snap, now_ms)
-    schema = checkpoint_schema()
-    cols = {name: [] for name in schema.names}
-    for kind, val in actions:
-        for name in schema.names:
-            cols[name].append(_arrow_value(kind, val) if name == kind else None)
-    table = pa.table({name: pa.array(cols[name], type=schema.field(name).type) for name in schema.names},
-                     schema=schema)
     tmp = os.path.join(log, ".%020d.checkpoint.parquet.%d.tmp" % (v, os.getpid()))
-    pq.write_table(table, tmp, compression="snappy")
+    if encoder == "gpu":
+        try:
+            n_adds = _write_gpu(engine, snap, tmp, now_ms)
+        except BaseException:
+            if os.path.exists(tmp):
+                os.remove(tmp)
+            raise
+    else:
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+        actions, n_adds = checkpoint_actions(engine, snap, now_ms)
+        schema = checkpoint_schema()
+        cols = {name: [] for name in schema.names}
+        for kind, val in actions:
+            for name in schema.names:
+                cols[name].append(_arrow_value(kind, val) if name == kind else None)
+        table = pa.table({name: pa.array(cols[name], type=schema.field(name).type) for name in schema.names},
+                         schema=schema)
+        pq.write_table(table, tmp, compression="snappy")
     try:
         os.link(tmp, final)                     # atomic, and fails when the checkpoint exists
     except FileExistsError:

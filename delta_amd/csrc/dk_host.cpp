@@ -4194,3 +4194,667 @@ extern "C" void dk_dv_free(dk_dv_set* S) {
   hipSetDevice(S->eng->cfg.device);
   delete S;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Checkpoint Parquet writer (Table.checkpoint -> ParquetHandler.writeParquetFileAtomically,
+// kernel-defaults/.../engine/DefaultParquetHandler.java:110-163 over parquet-mr's writer): the
+// CHECKPOINT_SCHEMA file (SingleAction.java:30-37 with each action's FULL_SCHEMA), encoded on the
+// device (dk_encode.hip). Row group 0 holds the rows built on the host (JSON action lines shredded
+// here with DefaultJsonRow's type rules); each later row group holds the surviving add rows of one
+// old checkpoint file, gathered on the device from its decoded columns by the replay's selection.
+// v1 data pages of <= 262144 rows: levels as RLE/bit-packed hybrid (one bit-packed run), PLAIN
+// values, snappy (or uncompressed); Thrift compact page headers and footer written here.
+// ------------------------------------------------------------------------------------------------
+namespace dk {
+struct EncSrc {
+  const uint8_t* row_def; const int64_t* row_offs; const uint8_t* entry_def;
+  const uint8_t* fixed; const int64_t* offs; const uint8_t* chars;
+  int32_t width, is_str, repeated, max_def_new;
+  int32_t entry_def_old;
+  uint8_t defmap[16], emap[16];
+};
+struct SzBlock { long long src; int32_t n; int32_t pad; };
+void enc_exscan(const long long*, long long, long long*, long long*, long long*, hipStream_t);
+long long enc_scan_blocks(long long);
+void enc_sel_rows(const uint8_t*, long long, long long*, long long*, long long*, long long*, int32_t*, hipStream_t);
+void enc_count(const EncSrc&, const int32_t*, long long, long long*, long long*, long long*, int*, hipStream_t);
+void enc_fill(const EncSrc&, const int32_t*, long long, const long long*, const long long*, const long long*, uint8_t*,
+              uint8_t*, uint8_t*, int32_t*, uint8_t*, long long*, hipStream_t);
+void enc_bitpack(const uint8_t*, long long, int, uint8_t*, hipStream_t);
+void enc_plain_str(const int32_t*, const long long*, const uint8_t*, long long, long long, long long, uint8_t*, hipStream_t);
+void enc_snappy(const uint8_t*, const SzBlock*, int, long long, uint8_t*, int32_t*, hipStream_t);
+}  // namespace dk
+
+namespace {
+enum { W_REQ = 0, W_OPT = 1, W_REP = 2 };
+enum { WC_NONE = -1, WC_UTF8 = 0, WC_MAP = 1, WC_LIST = 3 };
+struct WNode {
+  std::string name; int rep; int phys; int conv;
+  std::vector<int> kids; int leaf = -1; int def = 0, replv = 0;   // levels at this node (inclusive)
+};
+struct WLeaf {
+  std::string path; int node; int phys, width, max_def, max_rep;
+  std::vector<std::string> comps;
+  std::vector<int> chain;                 // node indices root-child .. leaf
+  // host-built rows (row group 0)
+  std::vector<uint8_t> def, rep, fixed, chars;
+  std::vector<int32_t> lens;
+};
+struct WSchema {
+  std::vector<WNode> nodes;               // preorder, nodes[0] = root
+  std::vector<WLeaf> leaves;
+  int add(int parent, const char* name, int rep, int phys = -1, int conv = WC_NONE) {
+    WNode n; n.name = name; n.rep = rep; n.phys = phys; n.conv = conv;
+    nodes.push_back(n);
+    const int id = (int)nodes.size() - 1;
+    if (parent >= 0) nodes[parent].kids.push_back(id);
+    return id;
+  }
+  int str(int p, const char* n, int rep) { return add(p, n, rep, PT_BYTE_ARRAY, WC_UTF8); }
+  int map(int p, const char* n, int rep, int value_rep) {
+    const int m = add(p, n, rep, -1, WC_MAP);
+    const int kv = add(m, "key_value", W_REP);
+    str(kv, "key", W_REQ); str(kv, "value", value_rep);
+    return m;
+  }
+  int list(int p, const char* n, int rep) {
+    const int l = add(p, n, rep, -1, WC_LIST);
+    const int g = add(l, "list", W_REP);
+    str(g, "element", W_REQ);
+    return l;
+  }
+  void dv(int p) {
+    const int d = add(p, "deletionVector", W_OPT);
+    str(d, "storageType", W_REQ); str(d, "pathOrInlineDv", W_REQ); add(d, "offset", W_OPT, PT_INT32);
+    add(d, "sizeInBytes", W_REQ, PT_INT32); add(d, "cardinality", W_REQ, PT_INT64);
+  }
+  void build() {
+    const int root = add(-1, "schema", W_REQ);
+    int t = add(root, "txn", W_OPT);
+    str(t, "appId", W_REQ); add(t, "version", W_REQ, PT_INT64); add(t, "lastUpdated", W_OPT, PT_INT64);
+    int a = add(root, "add", W_OPT);
+    str(a, "path", W_REQ); map(a, "partitionValues", W_REQ, W_OPT); add(a, "size", W_REQ, PT_INT64);
+    add(a, "modificationTime", W_REQ, PT_INT64); add(a, "dataChange", W_REQ, PT_BOOLEAN); dv(a);
+    map(a, "tags", W_OPT, W_OPT); add(a, "baseRowId", W_OPT, PT_INT64); add(a, "defaultRowCommitVersion", W_OPT, PT_INT64);
+    str(a, "stats", W_OPT);
+    int r = add(root, "remove", W_OPT);
+    str(r, "path", W_REQ); add(r, "deletionTimestamp", W_OPT, PT_INT64); add(r, "dataChange", W_REQ, PT_BOOLEAN);
+    add(r, "extendedFileMetadata", W_OPT, PT_BOOLEAN); map(r, "partitionValues", W_OPT, W_OPT); add(r, "size", W_OPT, PT_INT64);
+    str(r, "stats", W_OPT); map(r, "tags", W_OPT, W_OPT); dv(r); add(r, "baseRowId", W_OPT, PT_INT64);
+    add(r, "defaultRowCommitVersion", W_OPT, PT_INT64);
+    int m = add(root, "metaData", W_OPT);
+    str(m, "id", W_REQ); str(m, "name", W_OPT); str(m, "description", W_OPT);
+    int f = add(m, "format", W_REQ); str(f, "provider", W_REQ); map(f, "options", W_OPT, W_REQ);
+    str(m, "schemaString", W_REQ); list(m, "partitionColumns", W_REQ); add(m, "createdTime", W_OPT, PT_INT64);
+    map(m, "configuration", W_REQ, W_REQ);
+    int pr = add(root, "protocol", W_OPT);
+    add(pr, "minReaderVersion", W_REQ, PT_INT32); add(pr, "minWriterVersion", W_REQ, PT_INT32);
+    list(pr, "readerFeatures", W_OPT); list(pr, "writerFeatures", W_OPT);
+    int dm = add(root, "domainMetadata", W_OPT);
+    str(dm, "domain", W_REQ); str(dm, "configuration", W_REQ); add(dm, "removed", W_REQ, PT_BOOLEAN);
+    // levels and leaves (preorder = the footer's schema list order = column order)
+    std::vector<int> stack;
+    walk(0, 0, 0, stack);
+  }
+  void walk(int id, int def, int rep, std::vector<int>& chain) {
+    WNode& n = nodes[id];
+    if (id != 0) {
+      if (n.rep != W_REQ) def++;
+      if (n.rep == W_REP) rep++;
+      chain.push_back(id);
+    }
+    n.def = def; n.replv = rep;
+    if (n.phys >= 0) {
+      WLeaf L;
+      L.node = id; L.phys = n.phys; L.max_def = def; L.max_rep = rep; L.chain = chain;
+      L.width = n.phys == PT_INT64 ? 8 : n.phys == PT_INT32 ? 4 : n.phys == PT_BOOLEAN ? 1 : 0;
+      for (int c : chain) { L.comps.push_back(nodes[c].name); L.path += (L.path.empty() ? "" : ".") + nodes[c].name; }
+      n.leaf = (int)leaves.size();
+      leaves.push_back(std::move(L));
+    }
+    for (int k : std::vector<int>(n.kids)) walk(k, def, rep, chain);
+    if (id != 0) chain.pop_back();
+  }
+};
+
+// Dremel shredding of one JSON value (DefaultJsonRow's type rules: strings must be JSON strings,
+// ints / longs integral in range, booleans JSON booleans; a required field missing or null and a
+// null array element or required map value are errors)
+struct Shredder {
+  WSchema& S;
+  const std::vector<JNode>& N;
+  void push(WLeaf& L, int r, int d, const JNode* v) {
+    L.def.push_back((uint8_t)d);
+    if (L.max_rep) L.rep.push_back((uint8_t)r);
+    if (d < L.max_def) return;
+    if (L.phys == PT_BYTE_ARRAY) {
+      const std::string& s = as_str(N, *v);
+      L.lens.push_back((int32_t)s.size());
+      L.chars.insert(L.chars.end(), s.begin(), s.end());
+    } else if (L.phys == PT_INT64) {
+      const int64_t x = as_long(N, *v);
+      L.fixed.insert(L.fixed.end(), (const uint8_t*)&x, (const uint8_t*)&x + 8);
+    } else if (L.phys == PT_INT32) {
+      const int32_t x = as_int(N, *v);
+      L.fixed.insert(L.fixed.end(), (const uint8_t*)&x, (const uint8_t*)&x + 4);
+    } else {
+      L.fixed.push_back(as_bool(N, *v) ? 1 : 0);
+    }
+  }
+  void nulls(int id, int r, int d) {
+    const WNode& n = S.nodes[id];
+    if (n.leaf >= 0) { push(S.leaves[n.leaf], r, d, nullptr); return; }
+    for (int k : n.kids) nulls(k, r, d);
+  }
+  void value(int id, const JNode* v, int r, int d) {       // d: def of the parent
+    const WNode& n = S.nodes[id];
+    if (!v || v->t == J_NULL) {
+      if (n.rep == W_REQ) throw JErr{"Field `" + n.name + "` is not nullable, but it is missing or null"};
+      nulls(id, r, d);
+      return;
+    }
+    const int dd = n.rep == W_OPT ? d + 1 : d;
+    if (n.leaf >= 0) { push(S.leaves[n.leaf], r, dd, v); return; }
+    if (n.conv == WC_MAP) {
+      if (v->t != J_OBJ) mismatch(N, *v, "map");
+      const WNode& kv = S.nodes[n.kids[0]];
+      const int key = kv.kids[0], val = kv.kids[1];
+      if (v->kv.empty()) { nulls(n.kids[0], r, dd); return; }
+      for (size_t i = 0; i < v->kv.size(); i++) {
+        const int ri = i ? kv.replv : r;
+        WLeaf& KL = S.leaves[S.nodes[key].leaf];
+        KL.def.push_back((uint8_t)(dd + 1)); KL.rep.push_back((uint8_t)ri);
+        KL.lens.push_back((int32_t)v->kv[i].first.size());
+        KL.chars.insert(KL.chars.end(), v->kv[i].first.begin(), v->kv[i].first.end());
+        const JNode& x = N[v->kv[i].second];
+        if (x.t == J_NULL && S.nodes[val].rep == W_REQ)
+          throw JErr{"Map type expects no nulls in values, but received `null` as value"};
+        value(val, &x, ri, dd + 1);
+      }
+      return;
+    }
+    if (n.conv == WC_LIST) {
+      if (v->t != J_ARR) mismatch(N, *v, "array");
+      const WNode& g = S.nodes[n.kids[0]];
+      if (v->arr.empty()) { nulls(n.kids[0], r, dd); return; }
+      for (size_t i = 0; i < v->arr.size(); i++) {
+        const JNode& x = N[v->arr[i]];
+        if (x.t == J_NULL) throw JErr{"Array type expects no nulls as elements, but received `null` as array element"};
+        value(g.kids[0], &x, i ? g.replv : r, dd + 1);
+      }
+      return;
+    }
+    if (v->t != J_OBJ) mismatch(N, *v, "object");
+    for (int k : n.kids) value(k, member(N, *v, S.nodes[k].name.c_str()), r, dd);
+  }
+};
+
+// Thrift compact protocol writer (the footer and page headers)
+struct TWriter {
+  std::vector<uint8_t> b;
+  std::vector<int> last{0};
+  void varint(uint64_t v) { while (v >= 0x80) { b.push_back((uint8_t)(v | 0x80)); v >>= 7; } b.push_back((uint8_t)v); }
+  void zz(int64_t v) { varint(((uint64_t)v << 1) ^ (uint64_t)(v >> 63)); }
+  void field(int id, int type) {
+    const int d = id - last.back();
+    if (d > 0 && d <= 15) b.push_back((uint8_t)((d << 4) | type));
+    else { b.push_back((uint8_t)type); zz(id); }
+    last.back() = id;
+  }
+  void i32(int id, int64_t v) { field(id, 5); zz(v); }
+  void i64(int id, int64_t v) { field(id, 6); zz(v); }
+  void str(int id, const std::string& s) { field(id, 8); varint(s.size()); b.insert(b.end(), s.begin(), s.end()); }
+  void begin(int id) { field(id, 12); last.push_back(0); }
+  void end() { b.push_back(0); last.pop_back(); }
+  void list(int id, int etype, size_t n) {
+    field(id, 9);
+    if (n < 15) b.push_back((uint8_t)((n << 4) | etype)); else { b.push_back((uint8_t)(0xf0 | etype)); varint(n); }
+  }
+  void lbegin() { last.push_back(0); }             // a struct element of a list
+  void lend() { b.push_back(0); last.pop_back(); }
+};
+
+struct WChunk { int64_t offset = 0, comp = 0, unc = 0, nlev = 0; };
+}  // namespace
+
+struct dk_ckpt_writer {
+  dk_engine* eng = nullptr;
+  StreamH own;
+  hipStream_t s = nullptr;
+  std::string path;
+  FILE* fp = nullptr;
+  int codec = 1;                          // 1 SNAPPY, 0 UNCOMPRESSED
+  WSchema S;
+  int64_t host_rows = 0, off = 4, total_rows = 0;
+  std::vector<std::vector<WChunk>> rgs;   // per row group, per leaf
+  std::vector<int64_t> rg_rows;
+  DBuf d_def, d_rep, d_vals, d_lens, d_chars, d_coff, d_tmp, d_sums, d_total, d_ubuf, d_cbuf, d_clens, d_blocks;
+  DBuf d_rows, d_rowpos, d_lv, d_vv, d_cc, d_lb, d_vb, d_cb, d_err;
+};
+
+namespace {
+// one leaf's level / value arrays, already in device memory (d_def, d_rep, d_vals | d_lens + d_chars
+// + d_coff), over `nrows` rows whose level / value / char boundaries at page starts are in pb
+// (3 x (np + 1): level, value, char): encode, compress, append to the file
+int write_chunk(dk_ckpt_writer* w, WLeaf& L, int64_t nlev, const std::vector<int64_t>& lb, const std::vector<int64_t>& vb,
+                const std::vector<int64_t>& cb, WChunk& out) {
+  hipStream_t s = w->s;
+  const int np = (int)lb.size() - 1;
+  auto bw_of = [](int m) { int b = 0; while ((1 << b) <= m) b++; return m == 0 ? 0 : b; };
+  const int bwd = bw_of(L.max_def), bwr = bw_of(L.max_rep);
+  auto hyb = [](int64_t n, int bw) -> int64_t {           // 4-byte length + varint header + groups
+    const int64_t g = (n + 7) / 8;
+    uint64_t h = ((uint64_t)g << 1) | 1; int hb = 1; while (h >= 0x80) { h >>= 7; hb++; }
+    return 4 + hb + g * bw;
+  };
+  std::vector<int64_t> poff(np + 1, 0), psz(np);
+  for (int p = 0; p < np; p++) {
+    const int64_t nl = lb[p + 1] - lb[p], nv = vb[p + 1] - vb[p];
+    int64_t z = (L.max_rep ? hyb(nl, bwr) : 0) + (L.max_def ? hyb(nl, bwd) : 0);
+    z += L.phys == PT_BYTE_ARRAY ? 4 * nv + (cb[p + 1] - cb[p]) : L.phys == PT_BOOLEAN ? (nv + 7) / 8 : nv * L.width;
+    psz[p] = z; poff[p + 1] = poff[p] + z;
+  }
+  if (poff[np] > (int64_t)w->d_ubuf.n && w->d_ubuf.alloc((size_t)poff[np] + 64)) return 1;
+  uint8_t* U = w->d_ubuf.as<uint8_t>();
+  // page bodies: [rep levels][def levels][values]; the 4-byte lengths and varint headers from the host
+  std::vector<uint8_t> head(16);
+  for (int p = 0; p < np; p++) {
+    int64_t at = poff[p];
+    const int64_t nl = lb[p + 1] - lb[p], nv = vb[p + 1] - vb[p];
+    auto levels = [&](const DBuf& lv, int bw) -> int {
+      const int64_t g = (nl + 7) / 8, tot = hyb(nl, bw);
+      int n = 0;
+      uint32_t len = (uint32_t)(tot - 4);
+      for (int k = 0; k < 4; k++) head[n++] = (uint8_t)(len >> (8 * k));
+      uint64_t h = ((uint64_t)g << 1) | 1;
+      while (h >= 0x80) { head[n++] = (uint8_t)(h | 0x80); h >>= 7; }
+      head[n++] = (uint8_t)h;
+      HIPOK(hipMemcpyAsync(U + at, head.data(), n, hipMemcpyHostToDevice, s));
+      HIPOK(hipStreamSynchronize(s));
+      enc_bitpack(lv.as<uint8_t>() + lb[p], nl, bw, U + at + n, s);
+      at += tot;
+      return 0;
+    };
+    if (L.max_rep && levels(w->d_rep, bwr)) return 1;
+    if (L.max_def && levels(w->d_def, bwd)) return 1;
+    if (L.phys == PT_BYTE_ARRAY) {
+      enc_plain_str(w->d_lens.as<int32_t>(), w->d_coff.as<long long>(), w->d_chars.as<uint8_t>(), vb[p], nv, cb[p], U + at, s);
+    } else if (L.phys == PT_BOOLEAN) {
+      enc_bitpack(w->d_vals.as<uint8_t>() + vb[p], nv, 1, U + at, s);
+    } else if (nv > 0) {
+      HIPOK(hipMemcpyAsync(U + at, w->d_vals.as<uint8_t>() + vb[p] * L.width, (size_t)(nv * L.width), hipMemcpyDeviceToDevice, s));
+    }
+  }
+  // compression: snappy in 64 KiB blocks per page (one stream per page: varint length + blocks)
+  std::vector<std::vector<uint8_t>> pages(np);
+  if (w->codec == 1) {
+    std::vector<SzBlock> blk;
+    std::vector<int> bpage;
+    for (int p = 0; p < np; p++)
+      for (int64_t a = 0; a < psz[p]; a += 65536) {
+        SzBlock b{}; b.src = poff[p] + a; b.n = (int32_t)std::min<int64_t>(65536, psz[p] - a);
+        blk.push_back(b); bpage.push_back(p);
+      }
+    const long long cap = 65536 + 65536 / 6 + 64;
+    if (!blk.empty()) {
+      if (upload(w->d_blocks, blk.data(), blk.size() * sizeof(SzBlock), s)) return 1;
+      if ((size_t)(blk.size() * cap) > w->d_cbuf.n && w->d_cbuf.alloc(blk.size() * cap)) return 1;
+      if (blk.size() * 4 > w->d_clens.n && w->d_clens.alloc(blk.size() * 4 + 16)) return 1;
+      enc_snappy(U, w->d_blocks.as<SzBlock>(), (int)blk.size(), cap, w->d_cbuf.as<uint8_t>(), w->d_clens.as<int32_t>(), s);
+      std::vector<int32_t> cl(blk.size());
+      HIPOK(hipMemcpyAsync(cl.data(), w->d_clens.p, cl.size() * 4, hipMemcpyDeviceToHost, s));
+      HIPOK(hipStreamSynchronize(s));
+      std::vector<uint8_t> tmp;
+      for (size_t i = 0; i < blk.size(); i++) {
+        std::vector<uint8_t>& pg = pages[bpage[i]];
+        if (pg.empty()) {                                  // preamble: varint of the page's bytes
+          uint64_t v = (uint64_t)psz[bpage[i]];
+          while (v >= 0x80) { pg.push_back((uint8_t)(v | 0x80)); v >>= 7; }
+          pg.push_back((uint8_t)v);
+        }
+        const size_t at = pg.size();
+        pg.resize(at + cl[i]);
+        HIPOK(hipMemcpyAsync(pg.data() + at, w->d_cbuf.as<uint8_t>() + i * cap, cl[i], hipMemcpyDeviceToHost, s));
+      }
+      HIPOK(hipStreamSynchronize(s));
+    }
+    for (int p = 0; p < np; p++)
+      if (pages[p].empty()) pages[p].push_back(0);       // an empty page: varint 0, no tags
+  } else {
+    for (int p = 0; p < np; p++) {
+      pages[p].resize(psz[p]);
+      if (psz[p]) HIPOK(hipMemcpyAsync(pages[p].data(), U + poff[p], psz[p], hipMemcpyDeviceToHost, s));
+    }
+    HIPOK(hipStreamSynchronize(s));
+  }
+  out.offset = w->off; out.nlev = nlev; out.unc = 0; out.comp = 0;
+  for (int p = 0; p < np; p++) {
+    TWriter t;
+    t.i32(1, 0);                                  // DATA_PAGE
+    t.i32(2, psz[p]);
+    t.i32(3, (int64_t)pages[p].size());
+    t.begin(5);                                   // DataPageHeader
+    t.i32(1, lb[p + 1] - lb[p]); t.i32(2, 0); t.i32(3, 3); t.i32(4, 3);
+    t.end();
+    t.b.push_back(0);
+    if (fwrite(t.b.data(), 1, t.b.size(), w->fp) != t.b.size() ||
+        (!pages[p].empty() && fwrite(pages[p].data(), 1, pages[p].size(), w->fp) != pages[p].size()))
+      return fail("checkpoint write failed: " + w->path);
+    w->off += (int64_t)(t.b.size() + pages[p].size());
+    out.unc += (int64_t)t.b.size() + psz[p];
+    out.comp += (int64_t)(t.b.size() + pages[p].size());
+  }
+  return 0;
+}
+
+std::vector<int64_t> page_rows(int64_t nrows) {
+  const int64_t PR = 262144;
+  std::vector<int64_t> b;
+  for (int64_t r = 0; r < nrows; r += PR) b.push_back(r);
+  b.push_back(nrows);
+  if (nrows == 0) b = {0, 0};
+  return b;
+}
+}  // namespace
+
+extern "C" int dk_ckpt_writer_open(dk_engine* e, const char* path, int32_t codec, dk_ckpt_writer** out) {
+  if (!e) return fail("null engine");
+  hipSetDevice(e->cfg.device);
+  std::unique_ptr<dk_ckpt_writer> w(new dk_ckpt_writer());
+  w->eng = e; w->path = path; w->codec = codec ? 1 : 0;
+  if (w->own.create()) return 1;
+  w->s = w->own.s;
+  w->S.build();
+  w->fp = fopen(path, "wb");
+  if (!w->fp) return fail(std::string("cannot create ") + path);
+  if (fwrite("PAR1", 1, 4, w->fp) != 4) return fail("checkpoint write failed");
+  *out = w.release();
+  return 0;
+}
+
+// row group 0: action rows as JSON lines ({"add": {...}} / {"remove": ...} / {"metaData": ...} /
+// {"protocol": ...} / {"txn": ...} / {"domainMetadata": ...}, one action per line), in order
+extern "C" int dk_ckpt_writer_add_json(dk_ckpt_writer* w, const char* text, int64_t len) {
+  hipSetDevice(w->eng->cfg.device);
+  std::vector<JNode> N;
+  int64_t i = 0, nrows = 0;
+  try {
+    while (i < len) {
+      int64_t j = i;
+      while (j < len && text[j] != '\n') j++;
+      if (j > i) {
+        N.clear();
+        JParser jp(text + i, text + j, N);
+        int root = jp.value(0);
+        if (root >= 0) { jp.ws(); if (jp.p != jp.e) root = -1; }
+        if (root < 0 || N[root].t != J_OBJ) return fail("dk_ckpt_writer_add_json: bad action line");
+        Shredder sh{w->S, N};
+        for (int k : w->S.nodes[0].kids) sh.value(k, member(N, N[root], w->S.nodes[k].name.c_str()), 0, 0);
+        nrows++;
+      }
+      i = j + 1;
+    }
+  } catch (const JErr& je) {
+    return fail("checkpoint row: " + je.msg);
+  }
+  w->host_rows += nrows;
+  return 0;
+}
+
+// flush row group 0 (the host rows)
+static int flush_host_rows(dk_ckpt_writer* w) {
+  hipStream_t s = w->s;
+  const int64_t nrows = w->host_rows;
+  std::vector<WChunk> chunks(w->S.leaves.size());
+  const std::vector<int64_t> prow = page_rows(nrows);
+  for (size_t li = 0; li < w->S.leaves.size(); li++) {
+    WLeaf& L = w->S.leaves[li];
+    const int64_t nlev = (int64_t)L.def.size(), nv = L.phys == PT_BYTE_ARRAY ? (int64_t)L.lens.size() : (int64_t)(L.width ? L.fixed.size() / L.width : 0);
+    // page boundaries at row starts: level / value / char indices
+    std::vector<int64_t> lb, vb, cb;
+    int64_t row = -1, v = 0, c = 0;
+    size_t pi = 0;
+    for (int64_t l = 0; l < nlev; l++) {
+      const bool start = !L.max_rep || L.rep[l] == 0;
+      if (start) {
+        row++;
+        if (pi < prow.size() - 1 && row == prow[pi]) { lb.push_back(l); vb.push_back(v); cb.push_back(c); pi++; }
+      }
+      if (L.def[l] == L.max_def) { if (L.phys == PT_BYTE_ARRAY) c += L.lens[v]; v++; }
+    }
+    while (lb.size() < prow.size()) { lb.push_back(nlev); vb.push_back(v); cb.push_back(c); }
+    if (nv != v) return fail("checkpoint writer: value count mismatch in " + L.path);
+    if (upload(w->d_def, L.def.data(), L.def.size(), s) || upload(w->d_rep, L.rep.data(), L.rep.size(), s)) return 1;
+    if (L.phys == PT_BYTE_ARRAY) {
+      std::vector<long long> coff(L.lens.size() + 1, 0);
+      for (size_t k = 0; k < L.lens.size(); k++) coff[k + 1] = coff[k] + L.lens[k];
+      if (upload(w->d_lens, L.lens.data(), L.lens.size() * 4, s) || upload(w->d_chars, L.chars.data(), L.chars.size(), s) ||
+          upload(w->d_coff, coff.data(), coff.size() * 8, s)) return 1;
+    } else if (upload(w->d_vals, L.fixed.data(), L.fixed.size(), s)) return 1;
+    HIPOK(hipStreamSynchronize(s));
+    if (write_chunk(w, L, nlev, lb, vb, cb, chunks[li])) return 1;
+    L.def.clear(); L.rep.clear(); L.fixed.clear(); L.chars.clear(); L.lens.clear();
+  }
+  w->rgs.push_back(chunks);
+  w->rg_rows.push_back(nrows);
+  w->total_rows += nrows;
+  w->host_rows = 0;
+  return 0;
+}
+
+// The old checkpoint's column for a new-schema leaf path (add.* only), with the repetition of every
+// node along the path in the old file's schema
+static const DColumn* old_leaf(dk_parquet* p, int fi, const WLeaf& L, std::vector<int>* reps) {
+  const DColumn* c = find_col(p, fi, L.path.c_str());
+  if (!c) return nullptr;
+  const FileM& f = p->files[fi];
+  // walk the old schema along the components as leaf_index resolves them (a MAP group's repeated
+  // child and its key / value by position, struct fields by name)
+  int g = 0, map_level = 0;
+  for (size_t ci = 0; ci < L.comps.size(); ci++) {
+    const SchemaEl& G = f.schema[g];
+    if (G.kids.empty()) return nullptr;
+    int hit = -1;
+    if (map_level == 0 && (G.conv == 1 || G.logical == 2)) map_level = 1;
+    if (map_level == 1) {
+      if (G.kids.size() == 1 && f.schema[G.kids[0]].repetition == 2) hit = G.kids[0];
+      map_level = hit >= 0 ? 2 : 0;
+    } else if (map_level == 2) {
+      if (G.kids.size() == 2 && (L.comps[ci] == "key" || L.comps[ci] == "value")) hit = G.kids[L.comps[ci] == "key" ? 0 : 1];
+      map_level = 0;
+    }
+    if (hit < 0) for (int k : G.kids) if (f.schema[k].name == L.comps[ci]) { hit = k; break; }
+    if (hit < 0) return nullptr;
+    reps->push_back(f.schema[hit].repetition);
+    g = hit;
+  }
+  return c;
+}
+
+// row group: the surviving add rows among rows [row0, row1) of checkpoint file `file` of the replay
+// (selection on the device); host rows added before it are flushed as their own row group first
+extern "C" int dk_ckpt_writer_add_checkpoint_adds(dk_ckpt_writer* w, dk_replay* r, int32_t file, int64_t row0,
+                                                  int64_t row1, int64_t* n_rows) {
+  hipSetDevice(w->eng->cfg.device);
+  if (w->host_rows > 0 && flush_host_rows(w)) return 1;
+  if (!r || !r->ck || file < 0 || file >= (int32_t)r->ck->files.size()) return fail("dk_ckpt_writer_add_checkpoint_adds: bad file");
+  if (!r->have_result) return fail("dk_ckpt_writer_add_checkpoint_adds: the replay has no result");
+  if (row0 < 0 || row1 < row0 || row1 > r->ck->files[file].num_rows) return fail("dk_ckpt_writer_add_checkpoint_adds: bad rows");
+  hipStream_t s = w->s;
+  HIPOK(hipStreamSynchronize(r->stream));
+  dk_parquet* p = r->ck;
+  const int64_t n = row1 - row0;
+  const uint8_t* sel = r->d_csel[file]->as<uint8_t>() + row0;
+  const long long nsb = enc_scan_blocks(n + 1);
+  if (w->d_tmp.alloc((size_t)(n + 1) * 8 + 64) || w->d_rowpos.alloc((size_t)(n + 1) * 8 + 64) ||
+      w->d_sums.alloc((size_t)nsb * 8 + 64) || w->d_total.alloc(64) || w->d_rows.alloc((size_t)(n + 1) * 4 + 64) ||
+      w->d_err.alloc(64)) return 1;
+  enc_sel_rows(sel, n, w->d_tmp.as<long long>(), w->d_rowpos.as<long long>(), w->d_sums.as<long long>(),
+               w->d_total.as<long long>(), w->d_rows.as<int32_t>(), s);
+  long long ns = 0;
+  HIPOK(hipMemcpyAsync(&ns, w->d_total.p, 8, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  std::vector<WChunk> chunks(w->S.leaves.size());
+  const std::vector<int64_t> prow = page_rows(ns);
+  if (w->d_lv.alloc((size_t)(ns + 1) * 8 + 64) || w->d_vv.alloc((size_t)(ns + 1) * 8 + 64) ||
+      w->d_cc.alloc((size_t)(ns + 1) * 8 + 64) || w->d_lb.alloc((size_t)(ns + 2) * 8 + 64) ||
+      w->d_vb.alloc((size_t)(ns + 2) * 8 + 64) || w->d_cb.alloc((size_t)(ns + 2) * 8 + 64)) return 1;
+  for (size_t li = 0; li < w->S.leaves.size(); li++) {
+    WLeaf& L = w->S.leaves[li];
+    std::vector<int> reps;
+    const DColumn* c = L.comps[0] == "add" ? old_leaf(p, file, L, &reps) : nullptr;
+    int64_t nlev = ns, nv = 0, nc = 0;
+    std::vector<int64_t> lb, vb(prow.size(), 0), cb(prow.size(), 0);
+    if (!c || !c->present) {
+      // every row of this group is an add: a leaf of another action, or an add leaf with no value
+      // in the old file, is null at the deepest level its ancestors reach
+      int d = 0;
+      if (L.comps[0] == "add") {
+        d = w->S.nodes[L.chain[0]].def;      // add defined
+        for (size_t k = 1; k < L.chain.size(); k++) {
+          const WNode& nd = w->S.nodes[L.chain[k]];
+          if (nd.rep != W_REQ) break;
+          return fail("checkpoint writer: required field " + L.path + " is missing in " + p->files[file].path);
+        }
+      }
+      std::vector<uint8_t> lv(ns, (uint8_t)d);
+      if (upload(w->d_def, lv.data(), lv.size(), s)) return 1;
+      if (L.max_rep) { std::vector<uint8_t> rp(ns, 0); if (upload(w->d_rep, rp.data(), rp.size(), s)) return 1; }
+      HIPOK(hipStreamSynchronize(s));
+      for (int64_t rr : prow) lb.push_back(rr);
+    } else {
+      // definition levels: old -> new through the nodes each old level defines
+      if (reps.size() != L.chain.size()) return fail("checkpoint writer: schema mismatch for " + L.path);
+      EncSrc E{};
+      // row-indexed arrays start at row0 (entry-indexed ones are reached through row_offs)
+      const bool rep_old = c->max_rep > 0;
+      E.row_def = c->row_def + row0; E.row_offs = c->row_offs ? c->row_offs + row0 : nullptr; E.entry_def = c->entry_def;
+      E.fixed = c->fixed ? (rep_old ? c->fixed : c->fixed + row0 * c->width) : nullptr;
+      E.offs = c->offs ? (rep_old ? c->offs : c->offs + row0) : nullptr;
+      E.chars = c->chars;
+      E.width = c->width; E.is_str = L.phys == PT_BYTE_ARRAY; E.repeated = L.max_rep > 0 && c->max_rep > 0 && c->row_offs;
+      E.max_def_new = L.max_def; E.entry_def_old = c->rep_def;
+      if ((L.max_rep > 0) != (c->max_rep > 0) || c->phys != L.phys || (L.phys != PT_BYTE_ARRAY && !c->null_only && c->width != L.width))
+        return fail("checkpoint writer: type mismatch for " + L.path);
+      for (int dold = 0; dold < 16; dold++) {
+        int cnt = 0, J = -1;
+        for (size_t k = 0; k < reps.size(); k++) {
+          cnt += reps[k] != W_REQ;
+          if (cnt > dold) break;
+          J = (int)k;
+        }
+        int dnew = 0;
+        for (int k = 0; k <= J; k++) dnew += w->S.nodes[L.chain[k]].rep != W_REQ;
+        const bool bad = J + 1 < (int)L.chain.size() && w->S.nodes[L.chain[J + 1]].rep == W_REQ;
+        E.defmap[dold] = bad ? 0xff : (uint8_t)dnew;
+        E.emap[dold] = E.defmap[dold];
+      }
+      HIPOK(hipMemsetAsync(w->d_err.p, 0, 4, s));
+      enc_count(E, w->d_rows.as<int32_t>(), ns, w->d_lv.as<long long>(), w->d_vv.as<long long>(),
+                E.is_str ? w->d_cc.as<long long>() : nullptr, w->d_err.as<int>(), s);
+      auto scan = [&](DBuf& in, DBuf& outb, long long* tot) -> int {
+        if (ns > 0) {
+          enc_exscan(in.as<long long>(), ns, outb.as<long long>(), w->d_sums.as<long long>(), w->d_total.as<long long>(), s);
+          HIPOK(hipMemcpyAsync(tot, w->d_total.p, 8, hipMemcpyDeviceToHost, s));
+        } else *tot = 0;
+        return 0;
+      };
+      long long tl = 0, tv = 0, tc = 0;
+      if (scan(w->d_lv, w->d_lb, &tl) || scan(w->d_vv, w->d_vb, &tv) || (E.is_str && scan(w->d_cc, w->d_cb, &tc))) return 1;
+      int err = 0;
+      HIPOK(hipMemcpyAsync(&err, w->d_err.p, 4, hipMemcpyDeviceToHost, s));
+      HIPOK(hipStreamSynchronize(s));
+      if (err) return fail("checkpoint writer: a required field of " + L.path + " is null in " + p->files[file].path);
+      nlev = tl; nv = tv; nc = tc;
+      if (w->d_def.alloc((size_t)nlev + 64) || w->d_rep.alloc((size_t)nlev + 64)) return 1;
+      if (E.is_str) {
+        if (w->d_lens.alloc((size_t)nv * 4 + 64) || w->d_chars.alloc((size_t)nc + 64) || w->d_coff.alloc((size_t)(nv + 1) * 8 + 64)) return 1;
+      } else if (w->d_vals.alloc((size_t)nv * std::max(1, L.width) + 64)) return 1;
+      enc_fill(E, w->d_rows.as<int32_t>(), ns, w->d_lb.as<long long>(), w->d_vb.as<long long>(),
+               E.is_str ? w->d_cb.as<long long>() : nullptr, w->d_def.as<uint8_t>(), L.max_rep ? w->d_rep.as<uint8_t>() : nullptr,
+               w->d_vals.as<uint8_t>(), w->d_lens.as<int32_t>(), w->d_chars.as<uint8_t>(),
+               E.is_str ? w->d_coff.as<long long>() : nullptr, s);
+      if (E.is_str) HIPOK(hipMemcpyAsync(w->d_coff.as<long long>() + nv, &tc, 8, hipMemcpyHostToDevice, s));
+      // page boundaries (rows prow) -> level / value / char indices
+      std::vector<long long> hb(3 * prow.size());
+      for (size_t k = 0; k < prow.size(); k++) {
+        const int64_t rr = prow[k];
+        if (rr >= ns) { hb[3 * k] = tl; hb[3 * k + 1] = tv; hb[3 * k + 2] = tc; continue; }
+        HIPOK(hipMemcpyAsync(&hb[3 * k], w->d_lb.as<long long>() + rr, 8, hipMemcpyDeviceToHost, s));
+        HIPOK(hipMemcpyAsync(&hb[3 * k + 1], w->d_vb.as<long long>() + rr, 8, hipMemcpyDeviceToHost, s));
+        if (E.is_str) HIPOK(hipMemcpyAsync(&hb[3 * k + 2], w->d_cb.as<long long>() + rr, 8, hipMemcpyDeviceToHost, s));
+      }
+      HIPOK(hipStreamSynchronize(s));
+      for (size_t k = 0; k < prow.size(); k++) { lb.push_back(hb[3 * k]); vb[k] = hb[3 * k + 1]; cb[k] = E.is_str ? hb[3 * k + 2] : 0; }
+    }
+    if (write_chunk(w, L, nlev, lb, vb, cb, chunks[li])) return 1;
+  }
+  w->rgs.push_back(chunks);
+  w->rg_rows.push_back(ns);
+  w->total_rows += ns;
+  if (n_rows) *n_rows = ns;
+  return 0;
+}
+
+extern "C" int dk_ckpt_writer_close(dk_ckpt_writer* w, int64_t* n_rows, int64_t* file_size) {
+  if (!w) return fail("null writer");
+  hipSetDevice(w->eng->cfg.device);
+  int rc = 0;
+  if (w->host_rows > 0) rc = flush_host_rows(w);
+  if (!rc) {
+    TWriter t;
+    t.i32(1, 1);
+    t.list(2, 12, w->S.nodes.size());
+    for (const WNode& n : w->S.nodes) {
+      t.lbegin();
+      if (n.phys >= 0) t.i32(1, n.phys);
+      if (&n != &w->S.nodes[0]) t.i32(3, n.rep);
+      t.str(4, n.name);
+      if (n.phys < 0) t.i32(5, (int64_t)n.kids.size());
+      if (n.conv >= 0) t.i32(6, n.conv);
+      t.lend();
+    }
+    t.i64(3, w->total_rows);
+    t.list(4, 12, w->rgs.size());
+    for (size_t g = 0; g < w->rgs.size(); g++) {
+      t.lbegin();
+      t.list(1, 12, w->S.leaves.size());
+      int64_t tot = 0;
+      for (size_t li = 0; li < w->S.leaves.size(); li++) {
+        const WLeaf& L = w->S.leaves[li];
+        const WChunk& c = w->rgs[g][li];
+        tot += c.unc;
+        t.lbegin();
+        t.i64(2, c.offset);
+        t.begin(3);
+        t.i32(1, L.phys);
+        t.list(2, 5, 2); t.zz(0); t.zz(3);              // PLAIN, RLE
+        t.list(3, 8, L.comps.size());
+        for (const std::string& x : L.comps) { t.varint(x.size()); t.b.insert(t.b.end(), x.begin(), x.end()); }
+        t.i32(4, w->codec);
+        t.i64(5, c.nlev);
+        t.i64(6, c.unc);
+        t.i64(7, c.comp);
+        t.i64(9, c.offset);
+        t.end();
+        t.lend();
+      }
+      t.i64(2, tot);
+      t.i64(3, w->rg_rows[g]);
+      t.lend();
+    }
+    t.str(6, "delta_amd dk_ckpt_writer (gfx950 encoder)");
+    t.b.push_back(0);
+    const uint32_t fl = (uint32_t)t.b.size();
+    if (fwrite(t.b.data(), 1, t.b.size(), w->fp) != t.b.size() || fwrite(&fl, 1, 4, w->fp) != 4 ||
+        fwrite("PAR1", 1, 4, w->fp) != 4)
+      rc = fail("checkpoint write failed: " + w->path);
+    w->off += (int64_t)t.b.size() + 8;
+  }
+  if (fclose(w->fp) != 0 && !rc) rc = fail("checkpoint write failed: " + w->path);
+  if (n_rows) *n_rows = w->total_rows;
+  if (file_size) *file_size = w->off;
+  HIPOK(hipStreamSynchronize(w->s));
+  delete w;
+  return rc;
+}

@@ -622,7 +622,7 @@ class Table:
     def forPath(engine, path):
         return Table(path)
 
-    def checkpoint(self, engine, version=None, now_ms=None):
+    def checkpoint(self, engine, version=None, now_ms=None, encoder="gpu"):
         """Table.checkpoint (TableImpl.java:132-140 -> SnapshotManager.checkpoint): writes the classic
         checkpoint of the latest version and _last_checkpoint (delta_amd/checkpoint.py). Returns
         (version, number of add actions written)."""
@@ -631,7 +631,7 @@ class Table:
         if version is not None and version != latest:
             raise DkError("checkpoint: this engine writes checkpoints of the latest version (%d), not %d"
                           % (latest, version))
-        return write_checkpoint(engine, self.path, now_ms)
+        return write_checkpoint(engine, self.path, now_ms, encoder=encoder)
 
     def getLatestSnapshot(self, engine):
         t0 = time.perf_counter()

@@ -363,6 +363,19 @@ int  dk_replay_exchange_counts(dk_replay* r, int64_t* counts);
 int  dk_replay_exchange_pack(dk_replay* r, uint64_t* send);
 int  dk_replay_exchange_filter(dk_replay* r, const uint64_t* recv, int64_t n, uint8_t* flags);
 int  dk_replay_exchange_finish(dk_replay* r, const uint8_t* back);
+/* Checkpoint Parquet writer (Table.checkpoint's ParquetHandler.writeParquetFileAtomically,
+ * DefaultParquetHandler.java:110-163): CHECKPOINT_SCHEMA (SingleAction.java:30-37), encoded on the
+ * device. Rows come in iterator order as row groups: action rows built by the caller as JSON lines
+ * (one {"<action>": {...}} object per line, decoded with DefaultJsonRow's rules), and runs of rows
+ * of the replay's checkpoint file whose surviving adds are gathered on the device from the decoded
+ * columns by the replay's selection. codec: 1 SNAPPY (the reference's default), 0 UNCOMPRESSED.
+ * close writes the footer and frees the writer. */
+typedef struct dk_ckpt_writer dk_ckpt_writer;
+int  dk_ckpt_writer_open(dk_engine* e, const char* path, int32_t codec, dk_ckpt_writer** out);
+int  dk_ckpt_writer_add_json(dk_ckpt_writer* w, const char* lines, int64_t len);
+int  dk_ckpt_writer_add_checkpoint_adds(dk_ckpt_writer* w, dk_replay* r, int32_t file, int64_t row0, int64_t row1,
+                                        int64_t* n_rows);
+int  dk_ckpt_writer_close(dk_ckpt_writer* w, int64_t* n_rows, int64_t* file_size);
 int  dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count);
 void dk_replay_free(dk_replay* r);
 

@@ -71,8 +71,9 @@ CASES = {
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("encoder", ["gpu", "host"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_gpu_checkpoint_write(tmp_path, name):
+def test_gpu_checkpoint_write(tmp_path, name, encoder):
     from delta_amd import kernel as K
     from delta_amd import synth
     from tests.parity_util import assert_same, oracle_scan, product_scan
@@ -92,9 +93,21 @@ def test_gpu_checkpoint_write(tmp_path, name):
     before = oracle_scan(d)
     want, want_adds = ock.checkpoint_actions(d, now)
     eng = K.GpuEngine()
-    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=now)
+    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=now, encoder=encoder)
     assert v == info["version"] and n_adds == want_adds
+    # read back with pyarrow (an independent Parquet reader): rows in order, and the schema's
+    # repetition / nesting as the reference declares it
     got = ock.read_checkpoint(os.path.join(log, "%020d.checkpoint.parquet" % v))
+    if encoder == "gpu":
+        import pyarrow.parquet as pq
+        from tests.test_checkpoint_schema import EXPECTED
+        pf = pq.ParquetFile(os.path.join(log, "%020d.checkpoint.parquet" % v))
+        sch = pf.schema_arrow
+        assert sch.names == ["txn", "add", "remove", "metaData", "protocol", "domainMetadata"]
+        for top in ("add", "remove", "metaData", "protocol", "txn", "domainMetadata"):
+            t = sch.field(top).type
+            assert [(t.field(i).name, t.field(i).nullable) for i in range(t.num_fields)] == EXPECTED[top], top
+        assert pf.metadata.row_group(pf.metadata.num_row_groups - 1).column(0).compression == "SNAPPY"
     assert len(got) == len(want)
     for i, (a, b) in enumerate(zip(got, want)):
         assert a == b, (i, a, b)

@@ -15,10 +15,10 @@ NAMES = ["batches", "batch_tags", "dep_tags", "far_tags", "win_copies", "big_lit
 eng = K.GpuEngine()
 snap = K.Table.forPath(eng, sys.argv[1]).getLatestSnapshot(eng)
 scan = snap.getScanBuilder().build()
-scan.prepare(eng)
 z = (C.c_int64 * 24)()
 lib().dk_debug_snap_stats(z)
 base = list(z)
+scan.prepare(eng)          # the prepare pass decodes the snappy pages (the first run reuses them)
 scan.run(); scan.sync()
 lib().dk_debug_snap_stats(z)
 d = {n: z[i] - base[i] for i, n in enumerate(NAMES)}
