@@ -306,6 +306,8 @@ struct SchemaEl {
   std::string name;
   int type = -1, type_length = 0, repetition = 0, num_children = 0;
   int conv = -1, logical = -1, int_bits = 0, int_signed = 1;
+  int ts_unit = 0;                      // TIMESTAMP logical type unit: 1 millis, 2 micros, 3 nanos
+  int scale = -1, precision = -1;       // DECIMAL (SchemaElement 7 / 8, or the logical type's)
   int field_id = -1;                    // SchemaElement.field_id (9), -1 when absent
   std::vector<int> kids;                // children (schema element indices), in file order
   int leaf = -1;                        // leaf index of a primitive element
@@ -327,6 +329,7 @@ struct RowGroupM { int64_t num_rows = 0; std::vector<ColMeta> cols; };
 struct LeafM {
   std::string path; int phys, type_length, max_def, max_rep, rep_def;
   int leaf_rep = 0, lt = LT_NONE, int_bits = 0, int_signed = 1;   // own repetition, logical type
+  int ts_unit = 0, dec_scale = -1;      // timestamp unit (1 ms, 2 us, 3 ns; INT96 = 4), decimal scale
 };
 // A checkpoint file as the decoder sees it: the footer, plus only the byte ranges of the
 // projected column chunks (and their offset indexes), read with pread -- parquet-mr's column
@@ -480,6 +483,8 @@ static int parse_footer(FileM& f) {
           else if (i2 == 4) s.name = read_string(t);
           else if (i2 == 5) s.num_children = (int)t.zigzag();
           else if (i2 == 6) s.conv = (int)t.zigzag();
+          else if (i2 == 7) s.scale = (int)t.zigzag();
+          else if (i2 == 8) s.precision = (int)t.zigzag();
           else if (i2 == 9) s.field_id = (int)t.zigzag();
           else if (i2 == 10 && t2 == 12) {        // LogicalType union: the set member's field id
             int l3 = 0, t3, i3;
@@ -490,6 +495,23 @@ static int parse_footer(FileM& f) {
                 while ((i4 = t.field(&l4, &t4))) {
                   if (i4 == 1 && t4 == 3) s.int_bits = (int8_t)t.byte();
                   else if (i4 == 2 && (t4 == 1 || t4 == 2)) s.int_signed = t4 == 1;
+                  else t.skip(t4);
+                  if (t.bad) break;
+                }
+              } else if (i3 == 8 && t3 == 12) {   // TimestampType {isAdjustedToUTC, unit: TimeUnit union}
+                int l4 = 0, t4, i4;
+                while ((i4 = t.field(&l4, &t4))) {
+                  if (i4 == 2 && t4 == 12) {
+                    int l5 = 0, t5, i5;
+                    while ((i5 = t.field(&l5, &t5))) { s.ts_unit = i5; t.skip(t5); if (t.bad) break; }
+                  } else t.skip(t4);
+                  if (t.bad) break;
+                }
+              } else if (i3 == 5 && t3 == 12) {   // DecimalType {scale, precision}
+                int l4 = 0, t4, i4;
+                while ((i4 = t.field(&l4, &t4))) {
+                  if (i4 == 1) s.scale = (int)t.zigzag();
+                  else if (i4 == 2) s.precision = (int)t.zigzag();
                   else t.skip(t4);
                   if (t.bad) break;
                 }
@@ -578,6 +600,13 @@ static int parse_footer(FileM& f) {
       else if (e.conv >= 15 && e.conv <= 18) { L.lt = LT_INT; L.int_bits = 8 << (e.conv - 15); }
       else if (e.conv >= 11 && e.conv <= 14) { L.lt = LT_INT; L.int_bits = 8 << (e.conv - 11); L.int_signed = 0; }
       else if (e.conv >= 0) L.lt = LT_OTHER;
+      // timestamp unit (typed add.stats_parsed): the logical type's, else TIMESTAMP_MILLIS (9) /
+      // TIMESTAMP_MICROS (10), else an INT96 leaf (Spark's default timestamp encoding)
+      if (e.logical == 8) L.ts_unit = e.ts_unit;
+      else if (e.logical <= 0 && e.conv == 9) L.ts_unit = 1;
+      else if (e.logical <= 0 && e.conv == 10) L.ts_unit = 2;
+      else if (e.type == PT_INT96) L.ts_unit = 4;
+      if (e.logical == 5 || (e.logical <= 0 && e.conv == 5)) L.dec_scale = e.scale >= 0 ? e.scale : 0;
       f.leaves.push_back(L);
     }
   }

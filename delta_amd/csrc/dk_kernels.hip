@@ -699,7 +699,7 @@ enum : int { SX_NO_FAR = 1, SX_NO_BYTES = 2, SX_NO_RESOLVE = 4, SX_ONLY_DISCOVER
 #define DK_SF_WPE 5
 #endif
 #ifndef DK_SF_FARQ16
-#define DK_SF_FARQ16 0
+#define DK_SF_FARQ16 1
 #endif
 #ifndef DK_SF_FARQ_MAX
 #define DK_SF_FARQ_MAX 8
