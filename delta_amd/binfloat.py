@@ -190,6 +190,35 @@ def plan(op: str, lit, lit_type: str, value_fmt: str, cmp_fmt: str):
     conditions is a list of ("<"|"<="|">"|">=", Fraction) whose AND holds exactly for the exact
     values x (finite or overflowing) that satisfy it, or [ALL] / [NONE]; the results are those of
     the NaN / +Infinity / -Infinity values."""
+    (a, b), specials = rank_run(op, lit, lit_type, value_fmt, cmp_fmt)
+    mx = _max_index(value_fmt)
+    lo_r, hi_r = -mx - 2, mx + 1
+    if a > b:
+        return [NONE], specials
+    conds = []
+    if a > lo_r:
+        lo, lo_inc, _, _ = cell(a, value_fmt)
+        conds.append((">=" if lo_inc else ">", lo))
+    if b < hi_r:
+        _, _, hi, hi_inc = cell(b, value_fmt)
+        conds.append(("<=" if hi_inc else "<", hi))
+    return (conds or [ALL]), specials
+
+
+def rank(bits: int, name) -> int:
+    """Rank of a non-NaN value of the format from its IEEE bits: the bit pattern for +0.0 and up
+    (+Infinity is max_index + 1), -1 - |bits| below (-0.0 is -1, -Infinity -max_index - 2) -- the
+    Float.compare / Double.compare order."""
+    p = FORMATS[name][0]
+    sign_bit = 1 << (31 if p == 24 else 63)
+    mag = bits & (sign_bit - 1)
+    return -mag - 1 if bits & sign_bit else mag
+
+
+def rank_run(op: str, lit, lit_type: str, value_fmt: str, cmp_fmt: str):
+    """The values of value_fmt (as ranks, see rank) whose comparison `value <op> literal` in
+    cmp_fmt holds: one contiguous run ((a, b); a > b when empty), plus the NaN / +Infinity /
+    -Infinity results."""
     V = literal_value(lit, lit_type, cmp_fmt)
     test = _TEST[op]
     specials = tuple(test(java_compare(s, V)) for s in (NAN, PINF, NINF))
@@ -231,17 +260,9 @@ def plan(op: str, lit, lit_type: str, value_fmt: str, cmp_fmt: str):
     else:
         ok = (f, f) if exact else (1, 0)
     ok = (max(ok[0], lo_r), min(ok[1], hi_r))
-    a, b = ok
-    if a > b:
-        return [NONE], specials
-    conds = []
-    if a > lo_r:
-        lo, lo_inc, _, _ = cell(a, value_fmt)
-        conds.append((">=" if lo_inc else ">", lo))
-    if b < hi_r:
-        _, _, hi, hi_inc = cell(b, value_fmt)
-        conds.append(("<=" if hi_inc else "<", hi))
-    return (conds or [ALL]), specials
+    if ok[0] > ok[1]:
+        ok = (1, 0)
+    return ok, specials
 
 
 def decimal_text(q: Fraction, short=False) -> str:

@@ -257,15 +257,28 @@ struct StatsRows {
 };
 
 // Data skipping over add.stats_parsed (typed Parquet columns of the same stats, one per program
-// path; integral and date paths only): per path its definition levels and fixed-width values.
+// path): per path its definition levels and values, and how to read them.
+// value kinds: TP_INT integral / date / timestamp micros (INT32 sign-extended or INT64), TP_MILLIS
+// timestamp millis, TP_INT96 timestamp (nanos of day + Julian day), TP_STR UTF-8 bytes, TP_DEC
+// unscaled INT32 / INT64 with a scale, TP_F32 / TP_F64 IEEE float / double
+enum : int32_t { TP_INT = 0, TP_MILLIS = 1, TP_INT96 = 2, TP_STR = 3, TP_DEC = 4, TP_F32 = 5, TP_F64 = 6 };
 struct StatsParsedRows {
   int64_t n;
   int32_t n_paths;
   int32_t struct_def;                 // row_def >= this: add.stats_parsed is non-null
   const uint8_t* def[8];
-  const uint8_t* vals[8];
+  const uint8_t* vals[8];             // fixed-width values, one per row (TP_STR: null)
   int32_t max_def[8];
-  int32_t width[8];                   // 4 (INT32, sign-extended) or 8 (INT64)
+  int32_t width[8];                   // 4, 8 or 12 (INT96)
+  int32_t kind[8];                    // TP_*
+  int32_t scale[8];                   // TP_DEC: the decimal's scale
+  const int64_t* offs[8];             // TP_STR: n + 1 offsets into chars
+  const uint8_t* chars[8];
+  // the add.stats JSON of the same rows (column mode): the reference reads only it, so a row with a
+  // null add.stats keeps its selection, and a row whose typed values cannot stand for the JSON (a
+  // null stats_parsed struct, a float -0.0 -- Kernel reads "-0.0" as +0.0 but "-1e-400" as -0.0 --,
+  // sub-microsecond INT96 nanos) is evaluated from its JSON like k_stats_eval does
+  StatsRows js;
 };
 
 // Device-side counters and error state of one replay.

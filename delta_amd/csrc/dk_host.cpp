@@ -53,7 +53,7 @@ void launch_first_row(const uint8_t*, long long, int, unsigned long long*, hipSt
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint64_t, const uint8_t*, uint8_t*, DState*, hipStream_t);
 void launch_stats_eval(const StatsRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
-void launch_stats_parsed(const StatsParsedRows&, const DSkipProg*, uint8_t*, hipStream_t);
+void launch_stats_parsed(const StatsParsedRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
 void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipStream_t);
 void launch_table_fp(const Slot*, uint32_t*, uint64_t, hipStream_t);
 void launch_probe_all(const ProbeSet&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
@@ -2883,6 +2883,12 @@ static const DColumn* find_col(dk_parquet* p, int fi, const char* leaf) {
     if (p->leaves[li] == leaf) { int ci = p->colmap[fi][li]; return ci >= 0 ? &p->h_cols[ci] : nullptr; }
   return nullptr;
 }
+// the file's schema leaf behind a projected leaf (logical type, timestamp unit, decimal scale)
+static const LeafM* find_leafm(dk_parquet* p, int fi, const char* leaf) {
+  for (size_t li = 0; li < p->leaves.size(); li++)
+    if (p->leaves[li] == leaf) { int x = p->leafidx[fi][li]; return x >= 0 ? &p->files[fi].leaves[x] : nullptr; }
+  return nullptr;
+}
 
 // The checkpoint half of a replay: selection buffers, probe columns, partition maps and stats rows
 // of every checkpoint file. Separate from the commit-tail half so that the tail's action table and
@@ -3101,7 +3107,8 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
     else if (op == OP_FCMP) {                   // only on a float / double stat, threshold in names
       const long long off = P.lit[k] & 0xffffffffll, len = P.lit[k] >> 32;
       if (depth < 1 || !fstat[depth - 1]) return fail("dk_replay_set_skipping: FCMP needs a float stat");
-      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len > SK_NAMES) return fail("dk_replay_set_skipping: bad FCMP");
+      // (the threshold text is followed by the comparison's rank run, two int64s)
+      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len + 16 > SK_NAMES) return fail("dk_replay_set_skipping: bad FCMP");
       fstat[depth - 1] = false;
       nlit[depth - 1] = false;
     }
@@ -3128,26 +3135,51 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   if (depth != 1) return fail("dk_replay_set_skipping: program must leave one value");
   if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
   r->skip = P;
-  // add.stats_parsed fast path, per checkpoint file: every program path must be an integral / date
-  // stat whose typed leaf add.stats_parsed.<path> was projected and decoded with the matching width
+  // add.stats_parsed fast path, per checkpoint file: every program path's typed leaf
+  // add.stats_parsed.<path> was projected and decoded with a physical / logical type that holds the
+  // stat's Kernel type (long: INT64; int / short / byte / date: INT32; timestamp(_ntz): INT64 micros /
+  // millis or INT96; string: BYTE_ARRAY; decimal: INT32 / INT64 with a scale; float: FLOAT; double:
+  // DOUBLE), and the file's add.stats JSON column is there for the rows the typed values cannot
+  // stand for (k_stats_parsed)
   r->ck_parsed.assign(r->ck ? r->ck->files.size() : 0, StatsParsedRows{});
   static const bool no_parsed = getenv("DK_NO_STATS_PARSED") && atoi(getenv("DK_NO_STATS_PARSED"));
   for (size_t fi = 0; fi < r->ck_parsed.size() && !no_parsed; fi++) {
     StatsParsedRows R{};
     R.n_paths = P.n_paths;
     R.struct_def = 2;                     // add (1) . stats_parsed (2)
-    bool ok = P.n_paths > 0;
+    R.js = fi < r->ck_stats.size() ? r->ck_stats[fi] : StatsRows{};
+    bool ok = P.n_paths > 0 && R.js.n > 0 && R.js.offs;
     for (int q = 0; q < P.n_paths && ok; q++) {
       const int t = P.path_type[q];
       std::string leaf = "add.stats_parsed";
       for (int d = 0; d < P.path_depth[q]; d++) leaf += "." + std::string(P.names + P.name_off[q][d], P.name_len[q][d]);
       const DColumn* c = find_col(r->ck, (int)fi, leaf.c_str());
-      const int want = t == SK_LONG ? PT_INT64 : PT_INT32;
-      ok = (t == SK_LONG || t == SK_INT || t == SK_SHORT || t == SK_BYTE || t == SK_DATE) && c && c->present &&
-           !c->max_rep && c->phys == want && c->max_def >= 3;
+      const LeafM* L = find_leafm(r->ck, (int)fi, leaf.c_str());
+      ok = c && L && c->present && !c->max_rep && c->max_def >= 3;
       if (!ok) break;
+      int kind = -1;
+      switch (t) {
+        case SK_LONG: if (c->phys == PT_INT64 && L->dec_scale < 0 && !L->ts_unit) kind = TP_INT; break;
+        case SK_INT: case SK_SHORT: case SK_BYTE: case SK_DATE:
+          if (c->phys == PT_INT32 && L->dec_scale < 0) kind = TP_INT; break;
+        case SK_TIMESTAMP: case SK_TIMESTAMP_NTZ:
+          if (c->phys == PT_INT64 && L->ts_unit == 2) kind = TP_INT;
+          else if (c->phys == PT_INT64 && L->ts_unit == 1) kind = TP_MILLIS;
+          else if (c->phys == PT_INT96) kind = TP_INT96;
+          break;
+        case SK_STRING: if (c->phys == PT_BYTE_ARRAY) kind = TP_STR; break;
+        case SK_DECIMAL:
+          if ((c->phys == PT_INT32 || c->phys == PT_INT64) && L->dec_scale >= 0 && L->dec_scale <= 38) kind = TP_DEC; break;
+        case SK_FLOAT: if (c->phys == PT_FLOAT) kind = TP_F32; break;
+        case SK_DOUBLE: if (c->phys == PT_DOUBLE) kind = TP_F64; break;
+      }
+      ok = kind >= 0 && (kind == TP_STR ? (c->null_only || c->offs) : (c->null_only || c->fixed));
+      if (!ok) break;
+      R.kind[q] = kind; R.scale[q] = kind == TP_DEC ? L->dec_scale : 0;
       R.def[q] = c->row_def; R.max_def[q] = c->max_def;
-      R.vals[q] = c->null_only ? nullptr : c->fixed; R.width[q] = c->width;
+      R.vals[q] = c->null_only || kind == TP_STR ? nullptr : c->fixed; R.width[q] = c->width;
+      R.offs[q] = kind == TP_STR && !c->null_only ? c->offs : nullptr;
+      R.chars[q] = kind == TP_STR && !c->null_only ? c->chars : nullptr;
       if (c->null_only) R.max_def[q] = 1 << 30;          // no value anywhere: always null
     }
     if (ok) { R.n = r->ck->files[fi].num_rows; r->ck_parsed[fi] = R; }
@@ -3319,7 +3351,7 @@ static int replay_ckpt_filters(dk_replay* r) {
     for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
       KTimer::Scope sc(&T, 17, s);
       if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
-        launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), s);
+        launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
       else
         launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
     }

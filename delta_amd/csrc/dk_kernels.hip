@@ -2915,19 +2915,41 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
   }
 }
 
-__device__ void sk_decimal(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len, DecNum* d) {
+// a typed decimal (unscaled value, scale) as the text "<unscaled>E-<scale>" (buffer >= 26 bytes)
+__device__ int32_t dec_text(long long v, int32_t scale, uint8_t* b) {
+  int32_t n = 0;
+  unsigned long long m = v < 0 ? 0ull - (unsigned long long)v : (unsigned long long)v;
+  if (v < 0) b[n++] = '-';
+  uint8_t t[20];
+  int k = 0;
+  do { t[k++] = (uint8_t)('0' + m % 10); m /= 10; } while (m);
+  while (k) b[n++] = t[--k];
+  if (scale > 0) {
+    b[n++] = 'E'; b[n++] = '-';
+    if (scale >= 10) b[n++] = (uint8_t)('0' + scale / 10);
+    b[n++] = (uint8_t)('0' + scale % 10);
+  }
+  return n;
+}
+
+__device__ void sk_decimal(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len, DecNum* d,
+                           uint8_t* tbuf = nullptr) {
   *d = DecNum{};
-  if (kind == 3) dec_parse(s + (int32_t)(v & 0x7fffffff), (int32_t)(v >> 32), d);   // a validated JSON number
+  if (kind == 7) dec_parse(tbuf, dec_text(v, lit_len, tbuf), d);                    // typed decimal (lit_len: scale)
+  else if (kind == 3) dec_parse(s + (int32_t)(v & 0x7fffffff), (int32_t)(v >> 32), d);   // a validated JSON number
   else dec_parse((const uint8_t*)P.names + v, lit_len, d);                          // host-checked literal
 }
 
 
 // stack slot kinds: 0 integral (or boolean), 1 stats string (packed span), 2 literal string,
 // 3 stats decimal (packed number-token span), 4 literal decimal (BigDecimal text in names)
-__device__ Utf8Cursor sk_cursor(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len) {
+__device__ Utf8Cursor sk_cursor(int kind, long long v, const uint8_t* s, const DSkipProg& P, int32_t lit_len,
+                                const uint8_t* tp = nullptr) {
   Utf8Cursor c;
   c.np = c.pp = 0;
-  if (kind == 1) {
+  if (kind == 6) {                                   // typed string: the column's UTF-8 bytes
+    c.s = tp; c.i = 0; c.end = (int32_t)v; c.esc = false;
+  } else if (kind == 1) {
     c.s = s; c.i = (int32_t)(v & 0x7fffffff); c.end = c.i + (int32_t)((v >> 32) & 0x3fffffff); c.esc = (v >> 62) & 1;
   } else {
     c.s = (const uint8_t*)P.names; c.i = (int32_t)v; c.end = c.i + lit_len; c.esc = false;
@@ -2945,12 +2967,21 @@ __device__ int sk_strcmp(Utf8Cursor a, Utf8Cursor b) {
   }
 }
 
-// Kleene evaluation of the postfix program; returns 1 true, 0 false, -1 null
-__device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, const uint8_t* s) {
+// typed stats values (k_stats_parsed), per path: kind TP_*, decimal scale, string bytes (the value
+// slot then holds the string's length; a decimal's slot its unscaled value; a float's its rank in
+// the stat's format, FK_NAN for NaN)
+struct SkTyped { int32_t kind[SK_MAX_PATHS]; int32_t scale[SK_MAX_PATHS]; const uint8_t* ptr[SK_MAX_PATHS]; };
+constexpr long long FK_NAN = 0x7fffffffffffffffll;
+
+// Kleene evaluation of the postfix program; returns 1 true, 0 false, -1 null. typed: the values are
+// add.stats_parsed's (null: the JSON stats path's packed spans).
+__device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, const uint8_t* s,
+                       const SkTyped* typed = nullptr) {
   long long sv[16];
   int8_t sn[16];      // -1 null, else 0/1 for booleans (values: 0 = non-null)
-  int8_t sk[16];      // slot kind (sk_cursor)
+  int8_t sk[16];      // slot kind (sk_cursor; 6 typed string, 7 typed decimal text, 8 typed float as double bits)
   int32_t sl[16];     // literal string length
+  const uint8_t* sq[16];   // typed strings / decimal texts
   int sp = 0;
   for (int k = 0; k < P.n_ops && k < SK_MAX_OPS; k++) {
     const int op = P.op[k];
@@ -2958,7 +2989,28 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       const int p = P.arg[k];
       sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1;
       const int pt = P.path_type[p];
-      sk[sp] = pt == SK_STRING ? 1 : pt == SK_DECIMAL ? 3 : (pt == SK_FLOAT || pt == SK_DOUBLE) ? 5 : 0; sp++;
+      sk[sp] = pt == SK_STRING ? 1 : pt == SK_DECIMAL ? 3 : (pt == SK_FLOAT || pt == SK_DOUBLE) ? 5 : 0;
+      if (typed) {
+        const int tk = typed->kind[p];
+        sk[sp] = tk == TP_STR ? 6 : tk == TP_DEC ? 7 : (tk == TP_F32 || tk == TP_F64) ? 8 : 0;
+        sq[sp] = typed->ptr[p];
+        sl[sp] = typed->scale[p];
+      }
+      sp++;
+    } else if (op == OP_FCMP && sp > 0 && sk[sp - 1] == 8) {
+      // a typed float / double stat, as its rank: the comparison holds for the ranks [lo, hi] the
+      // planner put after the threshold text (binfloat.rank_run; lo > hi: never), NaN per flag bit 4
+      const int fl = P.arg[k];
+      int8_t r;
+      if (sn[sp - 1] < 0) r = -1;
+      else if (sv[sp - 1] == FK_NAN) r = (int8_t)((fl >> 4) & 1);
+      else {
+        const uint8_t* t = (const uint8_t*)P.names + (int32_t)(P.lit[k] & 0xffffffff) + (int32_t)(P.lit[k] >> 32);
+        unsigned long long lo = 0, hi = 0;
+        for (int b = 0; b < 8; b++) { lo |= (unsigned long long)t[b] << (8 * b); hi |= (unsigned long long)t[8 + b] << (8 * b); }
+        r = (int8_t)((long long)lo <= sv[sp - 1] && sv[sp - 1] <= (long long)hi);
+      }
+      sn[sp - 1] = r; sv[sp - 1] = 0; sk[sp - 1] = 0;
     } else if (op == OP_FCMP) {                          // float / double stat vs a planned threshold
       if (sp <= 0) return -1;
       const long long a = sv[sp - 1];
@@ -2985,16 +3037,18 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       const long long b = sv[--sp]; const int8_t bn = sn[sp], bk = sk[sp]; const int32_t bl = sl[sp];
       const long long a = sv[--sp]; const int8_t an = sn[sp], ak = sk[sp]; const int32_t al = sl[sp];
       int8_t r;
+      const uint8_t* aq = sq[sp]; const uint8_t* bq = sq[sp + 1];
       if (an < 0 || bn < 0) r = -1;
-      else if (ak >= 3 || bk >= 3) {                    // BigDecimal.compareTo
+      else if ((ak >= 3 && ak <= 5) || ak == 7 || (bk >= 3 && bk <= 5) || bk == 7) {   // BigDecimal.compareTo
         DecNum x, y;
-        sk_decimal(ak, a, s, P, al, &x);
-        sk_decimal(bk, b, s, P, bl, &y);
+        uint8_t xb[32], yb[32];
+        sk_decimal(ak, a, s, P, al, &x, xb);
+        sk_decimal(bk, b, s, P, bl, &y, yb);
         const int c = dec_cmp(x, y);
         r = op == OP_LT ? c < 0 : op == OP_LE ? c <= 0 : op == OP_GT ? c > 0 : op == OP_GE ? c >= 0 : c == 0;
       }
       else if (ak || bk) {
-        const int c = sk_strcmp(sk_cursor(ak, a, s, P, al), sk_cursor(bk, b, s, P, bl));
+        const int c = sk_strcmp(sk_cursor(ak, a, s, P, al, aq), sk_cursor(bk, b, s, P, bl, bq));
         r = op == OP_LT ? c < 0 : op == OP_LE ? c <= 0 : op == OP_GT ? c > 0 : op == OP_GE ? c >= 0 : c == 0;
       }
       else r = op == OP_LT ? a < b : op == OP_LE ? a <= b : op == OP_GT ? a > b : op == OP_GE ? a >= b : a == b;
@@ -4099,31 +4153,76 @@ void launch_probe(const ProbeCols& pc, const Slot* slots, const uint32_t* fp, ui
 }  // namespace dk
 
 namespace dk {
-// The same predicate over add.stats_parsed: the typed columns replace the JSON scan; a row whose
-// stats_parsed struct is null keeps its selection, as a null stats string does.
+// The same predicate over add.stats_parsed: the typed columns replace the JSON scan. The reference
+// reads add.stats only (ScanImpl's JsonHandler.parseJson of the stats string), and Spark writes
+// stats_parsed as from_json(stats), so a typed value stands for the JSON's where both are present;
+// rows the typed values cannot stand for are evaluated from their JSON (StatsParsedRows.js).
+__device__ __forceinline__ long long ld_i64(const uint8_t* p) {
+  return (long long)((unsigned long long)ld_u32(p) | ((unsigned long long)ld_u32(p + 4) << 32));
+}
 __global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DSkipProg* __restrict__ Pp,
-                                                     uint8_t* __restrict__ sel) {
+                                                     uint8_t* __restrict__ sel, DState* __restrict__ st) {
   const DSkipProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
        r += (long long)gridDim.x * blockDim.x) {
-    if (!sel[r] || R.def[0][r] < R.struct_def) continue;
+    if (!sel[r] || R.js.row_def[r] < R.js.max_def) continue;         // null add.stats: kept
     long long val[SK_MAX_PATHS];
     uint32_t set = 0;
-    for (int p = 0; p < R.n_paths; p++) {
-      if (R.def[p][r] < R.max_def[p]) { val[p] = 0; continue; }
-      val[p] = R.width[p] == 8 ? ((const long long*)R.vals[p])[r] : (long long)((const int32_t*)R.vals[p])[r];
+    SkTyped T;
+    bool typed = R.def[0][r] >= R.struct_def;
+    for (int p = 0; p < R.n_paths && typed; p++) {
+      const int kd = R.kind[p];
+      T.kind[p] = kd; T.scale[p] = R.scale[p]; T.ptr[p] = nullptr;
+      val[p] = 0;
+      if (R.def[p][r] < R.max_def[p]) continue;
+      const uint8_t* v = R.vals[p] + r * R.width[p];
+      long long x;
+      if (kd == TP_STR) {
+        const long long o0 = R.offs[p][r];
+        T.ptr[p] = R.chars[p] + o0;
+        x = R.offs[p][r + 1] - o0;
+      } else if (kd == TP_INT || kd == TP_DEC) {
+        x = R.width[p] == 8 ? ld_i64(v) : (long long)(int32_t)ld_u32(v);
+      } else if (kd == TP_MILLIS) {
+        x = ld_i64(v);
+        if (x > 9223372036854775ll || x < -9223372036854775ll) { typed = false; break; }
+        x *= 1000;
+      } else if (kd == TP_INT96) {                                     // nanos of day, Julian day
+        const unsigned long long ns = (unsigned long long)ld_i64(v);
+        const long long day = (long long)(int32_t)ld_u32(v + 8);
+        if (ns % 1000 || ns >= 86400000000000ull) { typed = false; break; }
+        x = (day - 2440588ll) * 86400000000ll + (long long)(ns / 1000);
+      } else {                                                          // TP_F32 / TP_F64: rank
+        const bool f32 = kd == TP_F32;
+        const unsigned long long b = f32 ? (unsigned long long)ld_u32(v) : (unsigned long long)ld_i64(v);
+        const unsigned long long mag = f32 ? (b & 0x7fffffffull) : (b & 0x7fffffffffffffffull);
+        const bool neg = f32 ? (b >> 31) & 1 : (b >> 63) & 1;
+        if (mag > (f32 ? 0x7f800000ull : 0x7ff0000000000000ull)) x = FK_NAN;
+        else if (mag == 0 && neg) { typed = false; break; }             // -0.0: ambiguous
+        else x = neg ? -(long long)mag - 1 : (long long)mag;
+      }
+      val[p] = x;
       set |= 1u << p;
     }
-    // (no string / decimal / float stat here: the stats base pointer is never read)
-    if (sk_eval(P, val, set, (const uint8_t*)P.names) == 0) sel[r] = 0;   // COALESCE(skip, true)
+    if (typed) {
+      if (sk_eval(P, val, set, (const uint8_t*)P.names, &T) == 0) sel[r] = 0;   // COALESCE(skip, true)
+      continue;
+    }
+    const uint8_t* s = R.js.chars + R.js.offs[r];
+    set = 0;
+    if (!js_extract(s, (int32_t)(R.js.offs[r + 1] - R.js.offs[r]), P, val, &set)) {
+      set_err(st, E_STATS, R.js.row_tag + r, 0);
+      continue;
+    }
+    if (sk_eval(P, val, set, s) == 0) sel[r] = 0;
   }
 }
 
-void launch_stats_parsed(const StatsParsedRows& R, const DSkipProg* P, uint8_t* sel, hipStream_t s) {
+void launch_stats_parsed(const StatsParsedRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {
   if (R.n <= 0) return;
   const long long want = (R.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
-  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, sel);
+  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, sel, st);
 }
 
 void launch_stats_eval(const StatsRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {

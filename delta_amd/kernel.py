@@ -1211,11 +1211,11 @@ class GpuScan:
         self.ckpt_files = [all_files[i] for i in self.ckpt_index]
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
         if self.skipping is not None:
-            # the typed add.stats_parsed leaves of the program's stats paths (integral / date): the
-            # engine evaluates skipping over them where a checkpoint file carries them
+            # the typed add.stats_parsed leaves of the program's stats paths: the engine evaluates
+            # skipping over them where a checkpoint file carries them with a type that holds the stat
+            # (dk_replay_set_skipping), the add.stats JSON standing in for the rows they cannot
             _, paths, types, _ = self.skipping
-            if all(t in (0, 1, 2, 3, 4) for t in types):
-                leaves = leaves + ["add.stats_parsed." + ".".join(p) for p in paths]
+            leaves = leaves + ["add.stats_parsed." + ".".join(p) for p in paths]
         t2 = time.perf_counter()
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel) if self.ckpt_files else None
         t3 = time.perf_counter()

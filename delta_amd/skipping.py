@@ -12,6 +12,7 @@ as in the reference (rewriteEqualNullSafe, :528-534).
 from __future__ import annotations
 
 import json
+import struct
 
 from decimal import Decimal as _Decimal
 
@@ -311,6 +312,7 @@ def compile_program(node, leaves):
         cmp_t = st if st == lt else (lt if lt in _UP_CAST.get(st, ()) else st)
         value_fmt = st if st in FLOATS else cmp_t
         conds, (r_nan, r_pinf, r_ninf) = binfloat.plan(op, lit[1], lt, value_fmt, cmp_t)
+        ranks = binfloat.rank_run(op, lit[1], lt, value_fmt, cmp_t)[0]
         if st not in FLOATS:                                   # integral stats widened to cmp_t
             b = binfloat.integral_bounds(conds)
             if b is None:
@@ -329,9 +331,10 @@ def compile_program(node, leaves):
         for k, c in enumerate(conds):
             emit(stat)
             if c in (binfloat.ALL, binfloat.NONE):
-                ops.append((OP_FCMP, flags | (FC_ALL if c == binfloat.ALL else FC_NONE), b""))
+                ops.append((OP_FCMP, flags | (FC_ALL if c == binfloat.ALL else FC_NONE), FcmpText(b"", ranks)))
             else:
-                ops.append((OP_FCMP, flags | _FC_MODE[c[0]], binfloat.decimal_text(c[1], short=True).encode("ascii")))
+                ops.append((OP_FCMP, flags | _FC_MODE[c[0]],
+                            FcmpText(binfloat.decimal_text(c[1], short=True).encode("ascii"), ranks)))
             if k:
                 ops.append((OP_AND, 0, 0))
     emit(node)
@@ -407,6 +410,17 @@ def check_types(node, leaves):
 MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 4096
 
 
+class FcmpText(bytes):
+    """An OP_FCMP threshold (exact decimal text, for a stat read from the JSON) carrying the same
+    comparison as a run of value ranks (binfloat.rank_run, for a typed add.stats_parsed float):
+    pack writes the two ranks as int64s right after the text."""
+
+    def __new__(cls, text, ranks):
+        o = super().__new__(cls, text)
+        o.ranks = tuple(int(x) for x in ranks)
+        return o
+
+
 def _stack_depth(ops):
     d = hi = 0
     for op, _, _ in ops:
@@ -440,7 +454,7 @@ def pack(program, struct_type):
             names += lit
         elif op == OP_FCMP:                                  # flags; threshold text offset | length << 32
             packed.append((op, arg, len(names) | (len(lit) << 32)))
-            names += lit
+            names += lit + struct.pack("<qq", *getattr(lit, "ranks", (1, 0)))
         else:
             packed.append((op, arg, lit))
     if len(names) > NAMES_BYTES:

@@ -639,3 +639,155 @@ def write_table(root: str, spec: TableSpec):
             f.write("\n".join(lines) + "\n")
     return {"checkpoint_files": files, "version": v + spec.n_commits,
             "checkpoint_rows": n_ck}
+
+
+# ---------------------------------------------------------------- typed add.stats_parsed tables
+TYPED_STATS_COLUMNS = (("l", "long"), ("i", "integer"), ("d", "date"), ("ts", "timestamp"), ("tz", "timestamp_ntz"),
+                       ("s", "string"), ("dc", "decimal(12,2)"), ("dd", "decimal(6,1)"), ("f", "float"),
+                       ("g", "double"))
+_TS_ALPHABET = ["a", "b", "c", "x", "y", "z", "é", "中", "\"", "\\", "\U0001f600"]
+
+
+def _typed_value(rng, name, n_ts):
+    """One stats value of column ``name``: (JSON text fragment, typed Python value), or None (no stat)."""
+    import datetime
+    import decimal
+    if rng.random() < 0.05:
+        return None
+    if name == "l":
+        v = int(rng.integers(-10 ** 6, 10 ** 6)) * 1_000_003
+        return str(v), v
+    if name == "i":
+        v = int(rng.integers(-(1 << 31), 1 << 31))
+        return str(v), v
+    if name == "d":
+        v = int(rng.integers(-3000, 20000))
+        return '"%s"' % (datetime.date(1970, 1, 1) + datetime.timedelta(days=v)).isoformat(), v
+    if name in ("ts", "tz"):
+        ms = int(rng.integers(-10 ** 11, 2 * 10 ** 12))
+        t = datetime.datetime(1970, 1, 1) + datetime.timedelta(milliseconds=ms)
+        text = t.strftime("%Y-%m-%dT%H:%M:%S.") + "%03d" % (t.microsecond // 1000) + ("Z" if name == "ts" else "")
+        return '"%s"' % text, ms * (1 if n_ts == "ms" else 1000)
+    if name == "s":
+        k = int(rng.integers(0, 7))
+        v = "".join(_TS_ALPHABET[int(j)] for j in rng.integers(0, len(_TS_ALPHABET), size=k))
+        return json.dumps(v, ensure_ascii=bool(rng.integers(0, 2))), v
+    if name in ("dc", "dd"):
+        scale, lim = (2, 10 ** 11) if name == "dc" else (1, 99_999)
+        u = int(rng.integers(-lim, lim + 1))
+        d = decimal.Decimal(u).scaleb(-scale)
+        return str(d), d
+    # float / double: specials (NaN / Infinity as JSON strings, -0.0 as a number) and plain values
+    c = rng.random()
+    if c < 0.04:
+        v = float("nan")
+    elif c < 0.07:
+        v = float("inf")
+    elif c < 0.10:
+        v = float("-inf")
+    elif c < 0.15:
+        v = -0.0
+    elif c < 0.20:
+        v = 0.0
+    else:
+        v = float(rng.normal() * 1000.0)
+        if name == "f":
+            v = float(np.float32(v))
+    if v != v:
+        return '"NaN"', v
+    if v in (float("inf"), float("-inf")):
+        return '"%s"' % ("Infinity" if v > 0 else "-Infinity"), v
+    return repr(v), v
+
+
+def write_typed_stats_table(root, n=3000, seed=7, ts_unit="us", n_tail=40):
+    """A table whose checkpoint adds carry add.stats (Delta's JSON) and add.stats_parsed (Spark's
+    from_json(stats): the same values, typed) for every stats type of TYPED_STATS_COLUMNS: long, int,
+    date, timestamp / timestamp_ntz (INT64 ``ts_unit`` "us" or "ms", or INT96 for "int96"), string
+    (with escapes and multi-byte UTF-8), decimal as INT64 / INT32, float, double (NaN, +-Infinity,
+    -0.0, which Kernel reads from "-0.0" as +0.0). Some rows have JSON stats and a null stats_parsed,
+    some a null JSON and typed stats (the reference reads only the JSON: kept), some neither. A
+    commit after the checkpoint adds ``n_tail`` files with JSON stats and removes a few. Returns
+    {column: [typed min values]} for building predicates."""
+    import decimal
+    rng = np.random.default_rng(seed)
+    log = os.path.join(root, "_delta_log")
+    os.makedirs(log, exist_ok=True)
+    names = [c for c, _ in TYPED_STATS_COLUMNS]
+    unit = "us" if ts_unit == "int96" else ts_unit
+    typ = {"l": pa.int64(), "i": pa.int32(), "d": pa.date32(), "ts": pa.timestamp(unit, tz="UTC"),
+           "tz": pa.timestamp(unit), "s": STR, "dc": pa.decimal128(12, 2), "dd": pa.decimal128(6, 1),
+           "f": pa.float32(), "g": pa.float64()}
+    vals_t = pa.struct([(c, typ[c]) for c in names])
+    nc_t = pa.struct([(c, pa.int64()) for c in names])
+    sp_t = pa.struct([("numRecords", pa.int64()), ("minValues", vals_t), ("maxValues", vals_t), ("nullCount", nc_t)])
+    schema = {"type": "struct", "fields": [{"name": c, "type": t, "nullable": True, "metadata": {}}
+                                           for c, t in TYPED_STATS_COLUMNS]}
+    proto = {"minReaderVersion": 1, "minWriterVersion": 2}
+    meta = {"id": "typed-stats", "format": {"provider": "parquet", "options": {}},
+            "schemaString": json.dumps(schema), "partitionColumns": [], "configuration": {}, "createdTime": 0}
+    mins = {c: [] for c in names}
+
+    def stats_row():
+        nrec = int(rng.integers(1, 1000))
+        js, parsed = {}, {"numRecords": nrec, "minValues": {}, "maxValues": {}, "nullCount": {}}
+        for side in ("minValues", "maxValues"):
+            parts = []
+            for c in names:
+                tv = _typed_value(rng, c, unit)
+                parsed[side][c] = None if tv is None else tv[1]
+                if tv is not None:
+                    parts.append('"%s":%s' % (c, tv[0]))
+                    if side == "minValues":
+                        mins[c].append(tv[1])
+            js[side] = "{" + ",".join(parts) + "}"
+        ncs = {c: int(rng.integers(0, 3)) for c in names}
+        parsed["nullCount"] = ncs
+        text = '{"numRecords":%d,"minValues":%s,"maxValues":%s,"nullCount":{%s}}' % (
+            nrec, js["minValues"], js["maxValues"], ",".join('"%s":%d' % (c, ncs[c]) for c in names))
+        return text, parsed
+
+    adds, stats, sps = [], [], []
+    for k in range(n):
+        text, parsed = stats_row()
+        if k % 53 == 5:
+            text = None
+        if k % 59 == 7:
+            parsed = None
+        if k % 61 == 9:
+            text = parsed = None
+        adds.append("f%05d.parquet" % k)
+        stats.append(text)
+        sps.append(parsed)
+    add_t = pa.struct([("path", STR), ("partitionValues", MAP_SS), ("size", pa.int64()),
+                       ("modificationTime", pa.int64()), ("dataChange", pa.bool_()), ("stats", STR),
+                       ("stats_parsed", sp_t)])
+    rows = [{"path": p, "partitionValues": [], "size": 1000 + i, "modificationTime": 1_700_000_000_000,
+             "dataChange": False, "stats": st, "stats_parsed": sp} for i, (p, st, sp) in enumerate(zip(adds, stats, sps))]
+    total = n + 2
+    add_col = pa.concat_arrays([pa.nulls(2, type=add_t), pa.array(rows, type=add_t)])
+    t = pa.table({"protocol": pa.array([proto, None] + [None] * n, type=PROTOCOL_TYPE),
+                  "metaData": pa.array([None, dict(meta, format={"provider": "parquet", "options": []},
+                                                   configuration=[])] + [None] * n, type=METADATA_TYPE),
+                  "add": add_col, "remove": pa.nulls(total, type=_remove_type())})
+    pq.write_table(t, os.path.join(log, "%020d.checkpoint.parquet" % 0), compression="snappy",
+                   row_group_size=1024, store_decimal_as_integer=True,
+                   use_deprecated_int96_timestamps=ts_unit == "int96")
+    with open(os.path.join(log, "%020d.json" % 0), "w") as f:
+        f.write(json.dumps({"protocol": proto}) + "\n" + json.dumps({"metaData": meta}) + "\n")
+        for p, st in zip(adds, stats):
+            a = {"path": p, "partitionValues": {}, "size": 1, "modificationTime": 0, "dataChange": True}
+            if st is not None:
+                a["stats"] = st
+            f.write(json.dumps({"add": a}) + "\n")
+    with open(os.path.join(log, "_last_checkpoint"), "w") as f:
+        f.write(json.dumps({"version": 0, "size": total}) + "\n")
+    with open(os.path.join(log, "%020d.json" % 1), "w") as f:
+        for k in range(n_tail):
+            a = {"path": "t%05d.parquet" % k, "partitionValues": {}, "size": 1, "modificationTime": 0,
+                 "dataChange": True, "stats": stats_row()[0]}
+            f.write(json.dumps({"add": a}) + "\n")
+        for k in range(0, n, max(1, n // 20)):
+            f.write(json.dumps({"remove": {"path": adds[k], "deletionTimestamp": 1, "dataChange": True}}) + "\n")
+    del decimal
+    return mins

@@ -277,7 +277,10 @@ typedef struct dk_skip_program {
                                       12 FCMP(pop a float/double stat x; push x <mode> threshold over its
                                          exact decimal value: arg & 15 = 0 <, 1 <=, 2 >, 3 >=, 4 always,
                                          5 never; arg bits 4/5/6 = the result for NaN / +Inf / -Inf;
-                                         threshold = names[lit & 0xffffffff, + (lit >> 32))) */
+                                         threshold = names[lit & 0xffffffff, + (lit >> 32)), followed by
+                                         two little-endian int64 (lo, hi): the same comparison as the
+                                         run of the value format's ranks (Float/Double.compare order,
+                                         -0.0 = -1, lo > hi: never) for add.stats_parsed floats) */
   int32_t arg[64];
   int64_t lit[64];
 } dk_skip_program;

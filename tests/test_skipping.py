@@ -938,8 +938,109 @@ def test_gpu_stats_parsed_equals_json(tmp_path):
         assert g[1] == o[1], p
         assert g[0] == o[0], p
         assert g[2] == 3, p                       # every checkpoint part used stats_parsed
-    # a string stat has no typed fast path here: the JSON stats decide, still equal to the oracle
+    # a string stat reads the typed BYTE_ARRAY leaf too
     p = cmp(">", col("name"), Literal.ofString("n25"))
     g = _gpu_files_parsed(str(tmp_path), p, eng)
-    assert g[2] == 0 and g[0] == oracle_files(str(tmp_path), p)[0]
+    assert g[2] == 3 and g[0] == oracle_files(str(tmp_path), p)[0]
     eng.close()
+
+
+def typed_predicates(mins, ts_unit):
+    """Predicates over every column of synth.TYPED_STATS_COLUMNS; '=' literals taken from the table."""
+    def pick(c, k):
+        vs = [v for v in mins[c] if v == v]
+        return vs[k % len(vs)]
+    us = (lambda v: v * 1000) if ts_unit == "ms" else (lambda v: v)
+    nan, inf = float("nan"), float("inf")
+    return [
+        cmp("=", col("l"), Literal.ofLong(pick("l", 3))), cmp(">", col("l"), Literal.ofLong(0)),
+        cmp("<=", col("i"), Literal.ofInt(pick("i", 5))), cmp(">", col("i"), Literal.ofLong(1 << 40)),
+        cmp("=", col("d"), Literal.ofDate(pick("d", 2))), cmp(">", col("d"), Literal.ofDate(10000)),
+        cmp("=", col("ts"), Literal.ofTimestamp(us(pick("ts", 4)))),
+        cmp("<", col("ts"), Literal.ofTimestamp(us(pick("ts", 9)))),
+        cmp(">=", col("tz"), Literal.ofTimestampNtz(us(pick("tz", 1)))),
+        cmp(">=", col("s"), Literal.ofString("b")), cmp("=", col("s"), Literal.ofString(pick("s", 4))),
+        cmp("<", col("s"), Literal.ofString("\u4e2d")), cmp(">", col("s"), Literal.ofString("z\U0001f600")),
+        cmp("=", col("dc"), Literal.ofDecimal(str(pick("dc", 1)), 12, 2)),
+        cmp(">", col("dc"), Literal.ofDecimal("0.00", 12, 2)),
+        cmp("<", col("dd"), Literal.ofDecimal("-0.5", 6, 1)),
+        cmp("<", col("f"), Literal.ofFloat(0.0)), cmp(">=", col("f"), Literal.ofFloat(-0.0)),
+        cmp("=", col("f"), Literal.ofFloat(pick("f", 3))), cmp("<", col("f"), Literal.ofFloat(nan)),
+        cmp(">", col("f"), Literal.ofDouble(10.5)), cmp("=", col("f"), Literal.ofFloat(inf)),
+        cmp("=", col("g"), Literal.ofDouble(pick("g", 2))), cmp(">", col("g"), Literal.ofDouble(inf)),
+        cmp("<=", col("g"), Literal.ofDouble(-0.0)), cmp(">", col("g"), Literal.ofFloat(-3.25)),
+        Predicate("IS_NULL", col("s")), Predicate("IS_NOT_NULL", col("g")),
+        And(cmp(">", col("l"), Literal.ofLong(0)), cmp("<", col("f"), Literal.ofFloat(100.0))),
+        Or(cmp("=", col("d"), Literal.ofDate(pick("d", 7))), cmp(">", col("dc"), Literal.ofDecimal("5.00", 12, 2))),
+        And(cmp(">=", col("s"), Literal.ofString("x")), cmp("<", col("ts"), Literal.ofTimestamp(0))),
+    ]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ts_unit", ["us", "ms", "int96"])
+def test_gpu_typed_stats_parsed_equals_json(tmp_path, ts_unit):
+    """Typed add.stats_parsed for every stats type (synth.write_typed_stats_table): timestamps as
+    INT64 micros / millis or INT96, strings, INT32 / INT64 decimals, floats and doubles with NaN,
+    +-Infinity and -0.0 (evaluated from the row's JSON: Kernel reads "-0.0" as +0.0), rows with only
+    one of add.stats / stats_parsed. Every predicate selects what the oracle (add.stats only)
+    selects, and the checkpoint's skipping ran over stats_parsed."""
+    from delta_amd import kernel as K
+    root = str(tmp_path / "t")
+    mins = synth.write_typed_stats_table(root, n=3000, seed=11, ts_unit=ts_unit)
+    eng = K.GpuEngine()
+    try:
+        for p in typed_predicates(mins, ts_unit):
+            g = _gpu_files_parsed(root, p, eng)
+            o = oracle_files(root, p)
+            assert g[2] == 1, p
+            assert g[1] == o[1], p
+            assert g[0] == o[0], p
+    finally:
+        eng.close()
+
+
+def test_oracle_typed_stats_table(tmp_path):
+    """The typed-stats fixture is a valid table for the oracle, and the predicates discriminate (each
+    keeps some files and drops some)."""
+    root = str(tmp_path / "t")
+    mins = synth.write_typed_stats_table(root, n=400, seed=11, ts_unit="ms")
+    live = 400 + 40 - 20                       # checkpoint adds + tail adds - tail removes
+    kept = [len(oracle_files(root, p)[0]) for p in typed_predicates(mins, "ms")]
+    assert all(k > 0 for k in kept), kept
+    assert sum(k < live for k in kept) >= len(kept) - 3, kept
+
+
+def test_rank_run_matches_java_compare():
+    """binfloat.rank_run (the typed stats_parsed float comparison) agrees with Float.compare /
+    Double.compare over random and special float / double values."""
+    import math
+    import random
+    import struct
+    from fractions import Fraction
+    from delta_amd import binfloat as bf
+    rnd = random.Random(5)
+    for fmt, pk, bits_n in (("float", "<f", 32), ("double", "<d", 64)):
+        specials = [0.0, -0.0, 1.5, -1.5, float("inf"), float("-inf"), float("nan"), 16777216.0, 0.1, 1e-45, 5e-324]
+        for lit_type in ("float", "double", "long"):
+            if fmt == "float" and lit_type == "double":
+                continue
+            for _ in range(40):
+                lit = rnd.choice(specials) if rnd.random() < 0.5 else rnd.uniform(-100, 100)
+                if lit_type == "long":
+                    if lit != lit or math.isinf(lit):
+                        continue
+                    lit = int(lit)
+                op = rnd.choice(["<", "<=", ">", ">=", "="])
+                (a, b), (r_nan, _, _) = bf.rank_run(op, lit, lit_type, fmt, fmt)
+                V = bf.literal_value(lit, lit_type, fmt)
+                for _ in range(60):
+                    x = rnd.choice(specials) if rnd.random() < 0.3 else rnd.uniform(-120, 120)
+                    bits = struct.unpack("<I" if bits_n == 32 else "<Q", struct.pack(pk, x))[0]
+                    x = struct.unpack(pk, struct.pack(pk, x))[0]
+                    if x != x:
+                        assert r_nan == bf._TEST[op](bf.java_compare(bf.NAN, V))
+                        continue
+                    xv = bf.PINF if x == float("inf") else bf.NINF if x == float("-inf") else \
+                        (Fraction(x), math.copysign(1.0, x) < 0 and x == 0)
+                    want = bf._TEST[op](bf.java_compare(xv, V))
+                    assert (a <= bf.rank(bits, fmt) <= b) == want, (fmt, lit_type, lit, op, x)
