@@ -6,6 +6,16 @@ import os
 
 import numpy as np
 
+
+def put_bytes(obj, field, data: bytes):
+    """Copy ``data`` into the char-array field of a ctypes structure byte for byte (an assignment
+    ``obj.field = data`` stops at the first NUL byte)."""
+    f = getattr(type(obj), field)
+    if len(data) > f.size:
+        raise ValueError("%s: %d bytes do not fit %d" % (field, len(data), f.size))
+    C.memset(C.addressof(obj) + f.offset, 0, f.size)
+    C.memmove(C.addressof(obj) + f.offset, data, len(data))
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # DK_LIB_PATH: load another build of the same ABI (A/B of kernel variants; tools/build_variant.py)
 LIB_PATH = os.environ.get("DK_LIB_PATH") or os.path.join(_HERE, "libdkgpu.so")

@@ -248,7 +248,8 @@ struct MapRows {
 // or, for the commit tail, explicit (offset, length) pairs per action (length < 0 = null).
 struct StatsRows {
   int64_t n;
-  const uint8_t* row_def; int32_t max_def; int32_t pad;
+  const uint8_t* row_def; int32_t max_def;
+  int32_t marked;               // 1: only rows whose selection byte is 2 (k_stats_parsed's hand-offs)
   const int64_t* offs;          // column mode: n + 1 offsets
   const int64_t* soff;          // action mode: offset per row
   const int32_t* slen;          // action mode: length per row (< 0: null)
@@ -277,7 +278,7 @@ struct StatsParsedRows {
   // the add.stats JSON of the same rows (column mode): the reference reads only it, so a row with a
   // null add.stats keeps its selection, and a row whose typed values cannot stand for the JSON (a
   // null stats_parsed struct, a float -0.0 -- Kernel reads "-0.0" as +0.0 but "-1e-400" as -0.0 --,
-  // sub-microsecond INT96 nanos) is evaluated from its JSON like k_stats_eval does
+  // sub-microsecond INT96 nanos) is marked (selection byte 2) for k_stats_eval over its JSON
   StatsRows js;
 };
 

@@ -1225,24 +1225,45 @@ static int prepare(dk_parquet* p) {
   p->open_ms[4] = since(t1);            // host: page tables, scratch sizing and allocation
   const auto t2 = clk::now();
   // the sizing passes, one slice of files at a time, each as soon as its files' images have landed
-  // (the later files' H2D copies overlap the earlier slices' snappy / level passes); about 1/8 of
-  // the bytes per slice; page mode is never sliced
+  // (the later files' H2D copies overlap the earlier slices' snappy / level passes); page mode is
+  // never sliced. Adaptive (default): a slice is every file whose image has landed by the time the
+  // previous slice is queued, at least 1/DK_OPEN_SLICES of the bytes (the host waits for more
+  // files until it has that much, or the rest) -- each slice's passes have a fixed latency cost
+  // (k_snap_fix's per-page chains), so fewer, larger slices once the reads have run ahead.
+  // DK_OPEN_ADAPTIVE=0: fixed slices of 1/DK_OPEN_SLICES of the bytes.
   {
     const int nf = (int)p->files.size();
     int64_t total = 0;
     for (const FileM& f : p->files) total += (int64_t)f.bytes.size();
     static const int want = getenv("DK_OPEN_SLICES") ? std::max(1, atoi(getenv("DK_OPEN_SLICES"))) : 8;
+    static const bool adaptive = !getenv("DK_OPEN_ADAPTIVE") || atoi(getenv("DK_OPEN_ADAPTIVE")) != 0;
     const int slices = snap_page_mode(p) ? 1 : want;
     const int64_t target = std::max<int64_t>(1, total / slices);
     int f0 = 0;
     int64_t acc = 0;
-    for (int f = 0; f < nf; f++) {
-      acc += (int64_t)p->files[f].bytes.size();
-      HIPOK(hipStreamWaitEvent(s, p->file_ev[f], 0));
-      if (f + 1 == nf || acc >= target) {
-        sizing_stages(p, s, file_range(p, f0, f + 1));
-        f0 = f + 1;
+    if (adaptive && slices > 1) {
+      while (f0 < nf) {
+        int f1 = f0;
         acc = 0;
+        // at least `target` bytes (or the rest), then every file already landed
+        while (f1 < nf && (acc < target || hipEventQuery(p->file_ev[f1]) == hipSuccess)) {
+          HIPOK(hipEventSynchronize(p->file_ev[f1]));
+          acc += (int64_t)p->files[f1].bytes.size();
+          f1++;
+        }
+        for (int f = f0; f < f1; f++) HIPOK(hipStreamWaitEvent(s, p->file_ev[f], 0));
+        sizing_stages(p, s, file_range(p, f0, f1));
+        f0 = f1;
+      }
+    } else {
+      for (int f = 0; f < nf; f++) {
+        acc += (int64_t)p->files[f].bytes.size();
+        HIPOK(hipStreamWaitEvent(s, p->file_ev[f], 0));
+        if (f + 1 == nf || acc >= target) {
+          sizing_stages(p, s, file_range(p, f0, f + 1));
+          f0 = f + 1;
+          acc = 0;
+        }
       }
     }
   }

@@ -3072,7 +3072,9 @@ __global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg*
   const DSkipProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
        r += (long long)gridDim.x * blockDim.x) {
-    if (!sel[r]) continue;
+    const uint8_t cur = sel[r];
+    if (R.marked ? cur != 2 : !cur) continue;
+    if (R.marked) sel[r] = 1;                                       // decided below, or kept
     const uint8_t* s;
     int32_t len;
     if (R.offs) {
@@ -4161,7 +4163,7 @@ __device__ __forceinline__ long long ld_i64(const uint8_t* p) {
   return (long long)((unsigned long long)ld_u32(p) | ((unsigned long long)ld_u32(p + 4) << 32));
 }
 __global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DSkipProg* __restrict__ Pp,
-                                                     uint8_t* __restrict__ sel, DState* __restrict__ st) {
+                                                     uint8_t* __restrict__ sel) {
   const DSkipProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
        r += (long long)gridDim.x * blockDim.x) {
@@ -4204,17 +4206,8 @@ __global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DS
       val[p] = x;
       set |= 1u << p;
     }
-    if (typed) {
-      if (sk_eval(P, val, set, (const uint8_t*)P.names, &T) == 0) sel[r] = 0;   // COALESCE(skip, true)
-      continue;
-    }
-    const uint8_t* s = R.js.chars + R.js.offs[r];
-    set = 0;
-    if (!js_extract(s, (int32_t)(R.js.offs[r + 1] - R.js.offs[r]), P, val, &set)) {
-      set_err(st, E_STATS, R.js.row_tag + r, 0);
-      continue;
-    }
-    if (sk_eval(P, val, set, s) == 0) sel[r] = 0;
+    if (!typed) { sel[r] = 2; continue; }                                // k_stats_eval decides
+    if (sk_eval(P, val, set, (const uint8_t*)P.names, &T) == 0) sel[r] = 0;   // COALESCE(skip, true)
   }
 }
 
@@ -4222,7 +4215,10 @@ void launch_stats_parsed(const StatsParsedRows& R, const DSkipProg* P, uint8_t* 
   if (R.n <= 0) return;
   const long long want = (R.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
-  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, sel, st);
+  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, sel);
+  StatsRows J = R.js;                  // the marked rows, from their JSON
+  J.marked = 1;
+  hipLaunchKernelGGL(k_stats_eval, dim3(grid), dim3(NT), 0, s, J, P, sel, st);
 }
 
 void launch_stats_eval(const StatsRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import json
 
+from ._lib import put_bytes
 from .expressions import Column, Literal, Predicate
 
 PT = {"long": 0, "integer": 1, "short": 2, "byte": 3, "string": 4, "date": 5, "decimal": 6, "boolean": 7,
@@ -241,7 +242,7 @@ def pack(program, struct_type):
     p.n_ops = len(ops)
     for k, (op, arg, lit) in enumerate(ops):
         p.op[k], p.arg[k], p.lit[k] = op, arg, lit
-    p.pool = pool
+    put_bytes(p, "pool", bytes(pool))
     return p
 
 
@@ -339,5 +340,5 @@ def pack_row_group_filter(program, struct_type):
     f.n_ops = len(ops)
     for k, (op, arg, lit) in enumerate(ops):
         f.op[k], f.arg[k], f.lit[k] = op, arg, lit
-    f.pool = bytes(pool)
+    put_bytes(f, "pool", bytes(pool))
     return f

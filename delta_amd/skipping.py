@@ -185,21 +185,25 @@ def _construct_not(child: Predicate, leaves):
         return construct(Predicate("IS_NULL", c[0]), leaves)
     if n == "IS_NULL":
         return construct(Predicate("IS_NOT_NULL", c[0]), leaves)
-    if n == "=":
-        # NOT(a = x) -> OR(min < x, max > x)   (constructDataSkippingFiltersForNotEqual :537-560)
-        return construct(Predicate("OR", Predicate("<", c[0], c[1]), Predicate(">", c[0], c[1])), leaves)
+    if n in ("=", "IS NOT DISTINCT FROM"):
+        # constructDataSkippingFiltersForNotEqual (:537-560): a literal on the left swaps sides; the
+        # column must be min/max eligible and the literal eligible
+        left, right = c
+        if isinstance(right, Column) and isinstance(left, Literal):
+            return _construct_not(Predicate(child.name, right, left), leaves)
+        if not (isinstance(left, Column) and isinstance(right, Literal)
+                and _eligible_minmax(leaves, left) and _eligible_literal(right)):
+            return None
+        if n == "=":                         # NOT(a = x) -> OR(min < x, max > x)
+            v = ("lit", right.value, right.type)
+            return ("OR", ("<", ("stat", (MIN,) + leaves[left.names][1]), v), (">", _max(left, leaves), v))
+        # NOT(a <=> x) -> NOT(rewriteEqualNullSafe(a, x)) (:528-534)
+        if right.value is None:
+            return construct(Predicate("NOT", Predicate("IS_NULL", left)), leaves)
+        return construct(Predicate("NOT", Predicate("AND", Predicate("IS_NOT_NULL", left),
+                                                    Predicate("=", left, right))), leaves)
     if n in NOT_CMP:
         return construct(Predicate(NOT_CMP[n], c[0], c[1]), leaves)
-    if n == "IS NOT DISTINCT FROM":
-        left, right = c
-        if isinstance(left, Column) and isinstance(right, Literal):
-            if right.value is None:
-                return construct(Predicate("IS_NOT_NULL", left), leaves)
-            return construct(Predicate("OR", Predicate("IS_NULL", left),
-                                       Predicate("NOT", Predicate("=", left, right))), leaves)
-        if isinstance(right, Column) and isinstance(left, Literal):
-            return _construct_not(Predicate(n, right, left), leaves)
-        return None
     if n == "NOT":
         return construct(c[0], leaves)
     return None
@@ -459,7 +463,8 @@ def pack(program, struct_type):
             packed.append((op, arg, lit))
     if len(names) > NAMES_BYTES:
         raise UnsupportedSkipping("stats field names and string literals exceed %d bytes" % NAMES_BYTES)
-    prog.names = bytes(names)
+    from ._lib import put_bytes
+    put_bytes(prog, "names", bytes(names))       # (the rank runs hold NUL bytes)
     prog.n_ops = len(ops)
     for k, (op, arg, lit) in enumerate(packed):
         prog.op[k], prog.arg[k], prog.lit[k] = op, arg, lit

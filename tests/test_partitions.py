@@ -38,7 +38,8 @@ def oracle_files(root, predicate, bs=1024):
     from delta_amd import skipping as sk
     from oracle import ref
     schema, parts = table_metadata(root)
-    pf, df = sk.split_filters(predicate, parts)
+    from oracle import skipping_filter as osf
+    pf, df = osf.split(predicate, parts)
     part = (pf, pp.partition_fields(schema, parts)) if pf is not None else None
     skip = oracle_skipping(root, df) if df is not None else None
     r = ref.replay(root, json_batch_size=bs, with_stats=skip is not None, skipping=skip, partition=part)

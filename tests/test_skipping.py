@@ -87,19 +87,20 @@ def table_metadata(root):
 
 
 def oracle_skipping(root, predicate):
+    """The oracle's own skipping predicate (oracle/skipping_filter.py restates
+    constructDataSkippingFilter; the product planner is not used) and its stats types."""
+    from oracle import skipping_filter as osf
     schema, parts = table_metadata(root)
-    pf, data = sk.split_filters(predicate, parts)
+    pf, data = osf.split(predicate, parts)
     assert pf is None
     if data is None:
         return None
-    leaves = sk.data_schema_leaves(schema, parts)
-    node = sk.construct(data, leaves)
+    S = osf.StatsSchema(schema, parts)
+    node = osf.build(data, S)
     if node is None:
         return None
-    sk.check_types(node, leaves)
-    paths, types, _ = sk.compile_program(node, leaves)
-    names = {v: k for k, v in sk.TYPE_CODE.items()}
-    return node, {p: names[t] for p, t in zip(paths, types)}
+    osf.check(node, S)
+    return node, osf.stat_types(node, S)
 
 
 def oracle_files(root, predicate, bs=1024):
@@ -1044,3 +1045,97 @@ def test_rank_run_matches_java_compare():
                         (Fraction(x), math.copysign(1.0, x) < 0 and x == 0)
                     want = bf._TEST[op](bf.java_compare(xv, V))
                     assert (a <= bf.rank(bits, fmt) <= b) == want, (fmt, lit_type, lit, op, x)
+
+
+def test_pack_keeps_rank_bytes():
+    """The FCMP threshold text is followed by its rank run (two int64s, NUL bytes included) in the
+    packed names (a ctypes char-array assignment would stop at the first NUL)."""
+    import ctypes as C
+    import struct
+    from delta_amd import _lib
+    leaves = {("f",): ("float", ("f",))}
+    prog = sk.compile_program(sk.construct(cmp("=", col("f"), Literal.ofFloat(0.0)), leaves), leaves)
+    p = sk.pack(prog, _lib.dk_skip_program)
+    names = C.string_at(C.addressof(p) + type(p).names.offset, 4096)
+    for k in range(p.n_ops):
+        if p.op[k] == sk.OP_FCMP:
+            off, ln = p.lit[k] & 0xffffffff, p.lit[k] >> 32
+            assert struct.unpack("<qq", names[off + ln:off + ln + 16]) == prog[2][k][2].ranks
+    # min <= 0.0f: every rank up to +0.0 (-0.0 included); max >= 0.0f: from +0.0 (Float.compare: -0.0 < 0.0)
+    assert [prog[2][k][2].ranks for k in range(p.n_ops) if p.op[k] == sk.OP_FCMP] == \
+        [(-0x7f800001, 0), (0, 0x7f800000)]
+
+
+# ---------------------------------------------------------------- planner vs the oracle's own restatement
+_PLAN_SCHEMA = json.dumps({"type": "struct", "fields": [
+    {"name": n, "type": t, "nullable": True, "metadata": m} for n, t, m in (
+        ("l", "long", {}), ("i", "integer", {}), ("sh", "short", {}), ("b", "byte", {}), ("f", "float", {}),
+        ("d", "double", {}), ("dt", "date", {}), ("ts", "timestamp", {}), ("tz", "timestamp_ntz", {}),
+        ("s", "string", {"delta.columnMapping.physicalName": "col-s"}), ("dc", "decimal(10,2)", {}),
+        ("bo", "boolean", {}), ("bi", "binary", {}), ("p", "integer", {}),
+        ("st", {"type": "struct", "fields": [{"name": "x", "type": "long", "nullable": True, "metadata": {}},
+                                             {"name": "y", "type": "boolean", "nullable": True, "metadata": {}}]},
+         {}),
+        ("ar", {"type": "array", "elementType": "long", "containsNull": True}, {}))]})
+
+
+def _random_predicate(rnd, depth):
+    cols = [col(n) for n in ("l", "i", "sh", "b", "f", "d", "dt", "ts", "tz", "s", "dc", "bo", "bi", "p", "ar",
+                             "nope")] + [Column("st", "x"), Column("st", "y"), Column("st")]
+    lits = [Literal.ofLong(5), Literal.ofInt(-3), Literal.ofShort(2), Literal.ofByte(1), Literal.ofFloat(1.5),
+            Literal.ofDouble(-2.25), Literal.ofDate(100), Literal.ofTimestamp(10 ** 12), Literal.ofTimestampNtz(7),
+            Literal.ofString("k"), Literal.ofDecimal("1.25", 10, 2), Literal.ofDecimal("1.5", 5, 1),
+            Literal.ofBoolean(True), Literal.ofNull("long"), Literal.ofNull("string")]
+    r = rnd.random()
+    if depth > 0 and r < 0.35:
+        return Predicate(rnd.choice(["AND", "OR"]), _random_predicate(rnd, depth - 1), _random_predicate(rnd, depth - 1))
+    if depth > 0 and r < 0.5:
+        return Predicate("NOT", _random_predicate(rnd, depth - 1))
+    if r < 0.6:
+        return Predicate(rnd.choice(["IS_NULL", "IS_NOT_NULL"]), rnd.choice(cols))
+    if r < 0.63:
+        return Predicate("STARTS_WITH", rnd.choice(cols), rnd.choice(lits))
+    op = rnd.choice(["=", "<", "<=", ">", ">=", "IS NOT DISTINCT FROM"])
+    a, b = rnd.choice(cols), rnd.choice(lits)
+    if rnd.random() < 0.3:
+        a, b = b, a
+    if rnd.random() < 0.05:
+        b = rnd.choice(cols)
+    return Predicate(op, a, b)
+
+
+def test_planner_matches_oracle_restatement():
+    """delta_amd/skipping.py (construct, split_filters, check_types) against oracle/skipping_filter.py,
+    an independent restatement of DataSkippingUtils.constructDataSkippingFilter / StatsSchemaHelper /
+    PartitionUtils.splitMetadataAndDataPredicates / transformBinaryComparator, on 3,000 random
+    predicates over every column kind (eligible, ineligible, nested, array, partition, missing)."""
+    import random
+    from oracle import skipping_filter as osf
+    rnd = random.Random(12)
+    parts = ["p"]
+    leaves = sk.data_schema_leaves(_PLAN_SCHEMA, parts)
+    S = osf.StatsSchema(_PLAN_SCHEMA, parts)
+    n_nodes = 0
+    for _ in range(3000):
+        p = _random_predicate(rnd, 4)
+        pf, df = sk.split_filters(p, parts)
+        opf, odf = osf.split(p, parts)
+        assert (pf, df) == (opf, odf), p
+        if df is None:
+            continue
+        got, want = sk.construct(df, leaves), osf.build(df, S)
+        assert got == want, (p, got, want)
+        if want is None:
+            continue
+        n_nodes += 1
+        try:
+            osf.check(want, S)
+            bad = None
+        except osf.Incomparable as e:
+            bad = e
+        if bad is None:
+            sk.check_types(got, leaves)
+        else:
+            with pytest.raises(sk.UnsupportedExpression):
+                sk.check_types(got, leaves)
+    assert n_nodes > 1000
