@@ -86,6 +86,10 @@ struct SnapCtx {
 struct DPosChunk {
   int32_t page, blk0;    // (input) page, first aligned 16-byte block of the region
   int32_t cnt, base;     // candidates in the chunk, their first index
+  int32_t first;         // region offset of the chunk's first candidate
+  int32_t last_next;     // its last candidate's successor (offset + 4 + length)
+  int32_t ok;            // every other candidate's successor is the next candidate of the chunk
+  int32_t pad;
 };
 constexpr int DK_POS_CHUNK = 16384;
 // k_expand record kinds (per-page work lists built on the device from per-group counts)

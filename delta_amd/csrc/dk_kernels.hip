@@ -1261,10 +1261,13 @@ __global__ __launch_bounds__(64) void k_snappy_serial(const DChunk* __restrict__
 // Speculation: with non-empty, NUL-free string content and lengths < 2^16 whose low byte is
 // non-zero, every maximal run of zero bytes ends exactly at byte 3 of a length prefix. Regions are
 // cut into 16 KiB chunks (one workgroup each, one dwordx4 per lane per step):
-//   k_pos_count    candidates per chunk
-//   k_pos_scan     per page: exclusive scan over its chunks; count != n -> fallback
+//   k_pos_count    candidates per chunk, gathered in order in LDS, and the exact length chain
+//                  inside the chunk: every candidate's successor (q + 4 + len(q)) is the next one;
+//                  the chunk's first candidate and its last one's successor are kept
+//   k_pos_scan     per page: exclusive scan over its chunks; the chain across chunks (first
+//                  candidate 0, each chunk's first = the previous non-empty chunk's last
+//                  successor, the last successor = R) and count == n, else the fallback
 //   k_pos_write    candidates -> P in order
-//   k_pos_verify   the exact length chain: P[0] = 0, P[k] + 4 + len(P[k]) = P[k+1], P[n] = R
 //   k_pos_fallback pages that failed: one lane walks the chain (always exact)
 // --------------------------------------------------------------------------------------------
 constexpr int POS_CHB = DK_POS_CHUNK / 16;   // aligned 16-byte blocks per chunk
@@ -1335,14 +1338,50 @@ __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chu
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   __shared__ int lds[12];
-  int cnt = 0;
-  if (str_region(pg, ck, arena, pos, S) && (int64_t)C.blk0 < S.nblk) {
+  // a value takes >= 5 region bytes (4-byte prefix + content), so a chunk holds <= 3277 prefixes
+  __shared__ int16_t cpos[DK_POS_CHUNK / 5 + 8];
+  __shared__ int s_bad, s_last;
+  const bool on = str_region(pg, ck, arena, pos, S) && (int64_t)C.blk0 < S.nblk;
+  const int64_t cstart = 16 * (int64_t)C.blk0 - (on ? S.mis : 0);   // region offset of the chunk start
+  if (threadIdx.x == 0) { s_bad = 0; s_last = -1; }
+  int run = 0;
 #pragma unroll
-    for (int j = 0; j < POS_BPT; j++) cnt += __popc(pos_cand_mask(S, (int64_t)C.blk0 + j * NT + threadIdx.x));
+  for (int j = 0; j < POS_BPT; j++) {
+    const int64_t i = (int64_t)C.blk0 + j * NT + threadIdx.x;
+    uint32_t m = on ? pos_cand_mask(S, i) : 0u;
+    int ex, e1, e2, tot, t1, t2;
+    block_scan3(__popc(m), 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
+    int k = run + ex;
+    const int64_t rb = 16 * i - (on ? S.mis : 0);
+    while (m) {
+      const int b = __ffs(m) - 1;
+      m &= m - 1;
+      if (k < DK_POS_CHUNK / 5 + 8) cpos[k] = (int16_t)(rb + b - 3 - cstart);
+      k++;
+    }
+    run += tot;
   }
-  int e0, e1, e2, tot, t1, t2;
-  block_scan3(cnt, 0, 0, &e0, &e1, &e2, &tot, &t1, &t2, lds);
-  if (threadIdx.x == 0) C.cnt = tot;
+  __syncthreads();
+  const int cnt = run;
+  if (cnt > DK_POS_CHUNK / 5 + 8) {                 // impossible for a real chain: fallback
+    if (threadIdx.x == 0) { C.cnt = cnt; C.first = -1; C.last_next = -1; C.ok = 0; }
+    return;
+  }
+  bool bad = false;
+  for (int k = threadIdx.x; k < cnt; k += NT) {
+    const int64_t q = cstart + cpos[k];
+    const int64_t nx = q + 4 + (int64_t)ld_u32(S.r + q);
+    if (k + 1 < cnt) { if (nx != cstart + cpos[k + 1]) bad = true; }
+    else s_last = nx > 0x7fffffffll ? -2 : (int)nx;
+  }
+  if (bad) s_bad = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    C.cnt = cnt;
+    C.first = cnt ? (int32_t)(cstart + cpos[0]) : -1;
+    C.last_next = s_last;
+    C.ok = !s_bad;
+  }
 }
 
 __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
@@ -1365,7 +1404,19 @@ __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chun
     run += tot;
   }
   if (threadIdx.x == 0) {
-    pgw.pos_fail = run != S.n;
+    // the length chain across the page's chunks (inside each chunk: k_pos_count)
+    bool ok = run == S.n;
+    int64_t expect = 0;
+    for (int c = 0; c < pg.npchunk && ok; c++) {
+      const DPosChunk& C = pcs[pg.pchunk0 + c];
+      if (!C.ok) ok = false;
+      else if (C.cnt) {
+        if ((int64_t)C.first != expect || C.last_next < 0) ok = false;
+        expect = C.last_next;
+      }
+    }
+    if (expect != S.R) ok = false;
+    pgw.pos_fail = !ok;
     S.P[S.n] = (int32_t)S.R;
   }
 }
@@ -1397,26 +1448,6 @@ __global__ __launch_bounds__(NT) void k_pos_write(const DChunk* __restrict__ chu
     }
     run += tot;
   }
-}
-
-__global__ __launch_bounds__(NT) void k_pos_verify(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                   const DPosChunk* __restrict__ pcs) {
-  const DPosChunk C = pcs[blockIdx.x];
-  const DPage pg = pages[C.page];
-  if (pg.pos_fail || C.cnt == 0) return;
-  const DChunk ck = chunks[pg.chunk];
-  StrRegion S;
-  if (!str_region(pg, ck, arena, pos, S)) return;
-  bool bad = false;
-  const int kend = min(C.base + C.cnt, S.n);
-  for (int k = C.base + threadIdx.x; k < kend; k += NT) {
-    const int64_t pk = S.P[k];
-    const int64_t nx = k + 1 < S.n ? (int64_t)S.P[k + 1] : S.R;
-    if (k == 0 && pk != 0) bad = true;
-    if (pk + 4 > S.R || pk + 4 + (int64_t)ld_u32(S.r + pk) != nx) bad = true;
-  }
-  if (__syncthreads_or(bad) && threadIdx.x == 0) pages[C.page].pos_fail = 1;
 }
 
 __global__ void k_pos_fallback(const DChunk* __restrict__ chunks, DPage* __restrict__ pages, int n_pages,
@@ -2990,6 +3021,7 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1;
       const int pt = P.path_type[p];
       sk[sp] = pt == SK_STRING ? 1 : pt == SK_DECIMAL ? 3 : (pt == SK_FLOAT || pt == SK_DOUBLE) ? 5 : 0;
+      sl[sp] = 0; sq[sp] = nullptr;
       if (typed) {
         const int tk = typed->kind[p];
         sk[sp] = tk == TP_STR ? 6 : tk == TP_DEC ? 7 : (tk == TP_F32 || tk == TP_F64) ? 8 : 0;
@@ -3028,11 +3060,11 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       }
       sn[sp - 1] = r; sv[sp - 1] = 0; sk[sp - 1] = 0;
     } else if (op == OP_LIT) {
-      sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sp++;
+      sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sl[sp] = 0; sq[sp] = nullptr; sp++;
     } else if (op == OP_TIMEADD) {                     // DefaultExpressionEvaluator.visitTimeAdd :593-625
       if (sp > 0 && sn[sp - 1] >= 0) sv[sp - 1] += P.lit[k];
     } else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
-      sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = op == OP_LIT_STR ? 2 : 4; sl[sp] = P.arg[k]; sp++;
+      sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = op == OP_LIT_STR ? 2 : 4; sl[sp] = P.arg[k]; sq[sp] = nullptr; sp++;
     } else if (op >= OP_LT && op <= OP_EQ) {
       const long long b = sv[--sp]; const int8_t bn = sn[sp], bk = sk[sp]; const int32_t bl = sl[sp];
       const long long a = sv[--sp]; const int8_t an = sn[sp], ak = sk[sp]; const int32_t al = sl[sp];
@@ -3052,14 +3084,14 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
         r = op == OP_LT ? c < 0 : op == OP_LE ? c <= 0 : op == OP_GT ? c > 0 : op == OP_GE ? c >= 0 : c == 0;
       }
       else r = op == OP_LT ? a < b : op == OP_LE ? a <= b : op == OP_GT ? a > b : op == OP_GE ? a >= b : a == b;
-      sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sp++;
+      sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sl[sp] = 0; sq[sp] = nullptr; sp++;
     } else {
       const int8_t b = sn[--sp];
       const int8_t a = sn[--sp];
       int8_t r;
       if (op == OP_AND) r = (a == 0 || b == 0) ? 0 : (a == 1 && b == 1) ? 1 : -1;
       else r = (a == 1 || b == 1) ? 1 : (a == 0 && b == 0) ? 0 : -1;
-      sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sp++;
+      sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sl[sp] = 0; sq[sp] = nullptr; sp++;
     }
   }
   return sp == 1 ? sn[0] : -1;
@@ -3895,7 +3927,6 @@ void launch_positions(const DChunk* c, DPage* p, int page0, int n_pages, const u
   hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
   hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs);
   hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
-  hipLaunchKernelGGL(k_pos_verify, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
   hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos);
 }
 void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {

@@ -13,3 +13,5 @@ DK_OPEN_ADAPTIVE=$m timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 > 
 python -c "import json; d=json.load(open('$OUT/b_${m}_$i.json')); p=d['getScanFiles_phases_ms']; print('adaptive=$m', round(d['ms_per_step'],1), p['open_read_h2d'], p['prep_device_sizing'], p['consume'], p['close'])"
 done
 done
+timeout -k 10 500 rocprofv3 --runtime-trace --memory-copy-trace --kernel-trace --output-format csv -d $OUT/rt -o run -- python -u bench.py --steps 2 --warmup 1 > $OUT/brt.json 2> $OUT/brt.err || { echo "runtime trace failed"; tail -20 $OUT/brt.err; exit 1; }
+ls $OUT/rt
