@@ -846,6 +846,9 @@ struct dk_parquet {
   // slices for the pipelined prepare: per file its first page / column (n_files + 1 entries), the
   // compressed-page list and its segment / fragment prefixes, and an event after each file's copies
   std::vector<int> file_page0, file_col0;
+  // grouped replay runs (dk_replay_run_grouped): per file, the event after which its decoded columns
+  // are final (set and cleared by the replay; empty: the stream order is enough)
+  std::vector<hipEvent_t> file_done;
   std::vector<int32_t> h_cpage, h_sbase, h_fbase;
   std::vector<EventH> file_ev;
   std::vector<HBuf> staging;        // pinned sources of zero-copy uploads, released when prepare ends
@@ -976,10 +979,10 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
 }
 
-// the decode pipeline over every file (mode: -1 = headers only; 0 = through the scans, which size the
-// outputs; 1 = full step)
-static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
-  if (!s) s = p->stream;
+// the value decode of columns [c0, c1) (every column of a run of files): string copies first -- they
+// fill the key column's per-value hashes that k_tile_decode forwards -- then the level / value tiles
+static void decode_cols(dk_parquet* p, hipStream_t s, int c0, int c1) {
+  if (c1 <= c0) return;
   KTimer& T = p->timer;
   const DChunk* C = p->d_chunks.as<DChunk>();
   DPage* P = p->d_pages.as<DPage>();
@@ -990,6 +993,42 @@ static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
   const long long* dbp = p->d_dbp.as<long long>();
   DTile* LT = p->d_ltiles.as<DTile>();
   Seg* runs = p->d_runs.as<Seg>();
+  {
+    KTimer::Scope sc(&T, 6, s);
+    const int2* tiles = p->d_tiles.as<int2>();
+    if (!split_launch()) {
+      const int t0 = p->col_tile0[c0], t1 = p->col_tile0[c1];
+      if (t1 > t0) launch_string_copy(C, P, t1 - t0, cols, arena, pos, tiles, s, t0, p->copy_cb);
+    } else {
+      for (int c = c0; c < c1; c++)
+        launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c],
+                           p->copy_cb);
+    }
+  }
+  {
+    KTimer::Scope sc(&T, 5, s);
+    if (!split_launch()) {
+      const int a = p->h_cols[c0].first_tile;
+      const int b = c1 < p->n_cols ? p->h_cols[c1].first_tile : p->n_ltiles;
+      if (b > a) launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, b - a, a, st, s);
+    } else {
+      for (int c = c0; c < c1; c++)
+        launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, p->h_cols[c].n_tiles, p->h_cols[c].first_tile, st, s);
+    }
+  }
+}
+
+// the decode pipeline over every file (mode: -1 = headers only; 0 = through the scans, which size the
+// outputs; 1 = full step; front_only: mode 1 without the value decode, which the caller runs per file
+// group with decode_cols)
+static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr, bool front_only = false) {
+  if (!s) s = p->stream;
+  KTimer& T = p->timer;
+  const DChunk* C = p->d_chunks.as<DChunk>();
+  DPage* P = p->d_pages.as<DPage>();
+  DState* st = p->d_state.as<DState>();
+  DColumn* cols = p->d_cols.as<DColumn>();
+  DTile* LT = p->d_ltiles.as<DTile>();
   const bool reuse = mode == 1 && p->fresh;
   p->fresh = false;
   if (reuse) {                         // headers, snappy, runs, counts, positions, chars: done by prepare
@@ -1001,17 +1040,7 @@ static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr) {
     sizing_stages(p, s, file_range(p, 0, (int)p->files.size()));
     if (mode == 0) return 0;
   }
-  // string copy first: it fills the key column's per-value hashes that k_tile_decode forwards
-  {
-    KTimer::Scope sc(&T, 6, s);
-    const int2* tiles = p->d_tiles.as<int2>();
-    if (!split_launch()) launch_string_copy(C, P, p->col_tile0.back(), cols, arena, pos, tiles, s, 0, p->copy_cb);
-    else
-      for (int c = 0; c < p->n_cols; c++)
-        launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c],
-                           p->copy_cb);
-  }
-  { KTimer::Scope sc(&T, 5, s); per_column_tiles(p, [&](int a, int k) { launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, k, a, st, s); }); }
+  if (!front_only) decode_cols(p, s, 0, p->n_cols);
   return 0;
 }
 
@@ -2061,6 +2090,8 @@ static int queue_mirror(dk_parquet* p, int ci) {
   HostMirror& h = p->host[ci];
   if (h.state) return 0;
   hipStream_t s = p->stream;
+  const int cf = p->col_file[ci];
+  if (cf < (int)p->file_done.size() && p->file_done[cf]) HIPOK(hipStreamWaitEvent(s, p->file_done[cf], 0));
   const int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
   if (h.row_def.alloc(c.n_rows + 1)) return 1;
   if (c.n_rows) HIPOK(hipMemcpyAsync(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost, s));
@@ -2897,6 +2928,17 @@ struct dk_replay {
   HBuf h_csel;
   std::vector<int64_t> h_csel_off;
   bool h_csel_ready = false;
+  // grouped run (dk_replay_run_grouped): the checkpoint files in n_groups runs, each decoded, probed,
+  // filtered and its selections copied to h_csel before the next; grp_ev[g] after group g's copies
+  int32_t n_groups = 0;
+  std::vector<int32_t> grp_f0;            // first file of each group (n_groups + 1 entries)
+  std::vector<hipEvent_t> grp_ev;
+  hipEvent_t ev_tail = nullptr;           // after the commit-tail half (its selection is final)
+  std::vector<int64_t> grp_row0;          // per group: its files' row prefix, rebased (probe_all)
+  DBuf d_grp_row0;
+  std::vector<uint8_t> file_ready;        // dk_replay_wait_file passed for the file
+  bool tail_ready = false;
+  StreamH aux;                            // error-state reads while a grouped run is in flight
 };
 
 static const DColumn* find_col(dk_parquet* p, int fi, const char* leaf) {
@@ -3274,6 +3316,7 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
 }
 
 static int replay_ckpt_filters(dk_replay* r);
+static int replay_grouped(dk_replay* r, uint64_t h_nodv);
 static int replay_launch(dk_replay* r) {
   hipStream_t s = r->stream;
   KTimer& T = r->timer;
@@ -3304,18 +3347,23 @@ static int replay_launch(dk_replay* r) {
     R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
     launch_stats_eval(R, r->d_skip.as<DSkipProg>(), r->d_jsel.as<uint8_t>(), st, s);
   }
+  if (!r->ev_tail) HIPOK(hipEventCreateWithFlags(&r->ev_tail, hipEventDisableTiming));
+  HIPOK(hipEventRecord(r->ev_tail, s));
+  if (r->ck) r->ck->file_done.clear();
   if (r->ck) {
     dk_parquet* p = r->ck;
+    const bool grouped = r->n_groups > 0 && r->xw == 0;
     // the decode runs on the replay's stream, after anything queued on the checkpoint's own
     HIPOK(hipEventRecord(r->ev_in, p->stream));
     HIPOK(hipStreamWaitEvent(s, r->ev_in, 0));
     // decode errors are collected into the replay state too
     HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
-    if (run_pipeline(p, 1, s)) return 1;
+    if (run_pipeline(p, 1, s, grouped)) return 1;
     launch_table_fp(S, r->d_fp.as<uint32_t>(), r->mask + 1, s);
     HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;       // dvUniqueId stream of "no DV"
     dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
     const uint64_t h_nodv = kd.hs.final_(kd.n);
+    if (grouped) return replay_grouped(r, h_nodv);
     if (r->probe_all || r->xw > 0) {
       KTimer::Scope sc(&T, 11, s);
       const size_t nf = r->probe.size();
@@ -3357,25 +3405,96 @@ static int replay_launch(dk_replay* r) {
   return 0;
 }
 
+// partition pruning and data skipping on checkpoint file fi's rows (after its probe)
+static void replay_file_filters(dk_replay* r, size_t fi) {
+  hipStream_t s = r->stream;
+  KTimer& T = r->timer;
+  DState* st = r->d_state.as<DState>();
+  if (r->has_part && fi < r->ck_maps.size()) {
+    KTimer::Scope sc(&T, 18, s);
+    launch_part_eval(r->ck_maps[fi], r->d_part.as<DPartProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+  }
+  if (r->has_skip && fi < r->ck_stats.size()) {
+    KTimer::Scope sc(&T, 17, s);
+    if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
+      launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+    else
+      launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+  }
+}
+
+// the grouped form of the checkpoint half (after the front of the decode pipeline and the table
+// fingerprints): per group of files, value decode, probe, filters and the D2H of the selections,
+// then an event the host waits on before handing out those files' batches
+static int replay_grouped(dk_replay* r, uint64_t h_nodv) {
+  hipStream_t s = r->stream;
+  KTimer& T = r->timer;
+  dk_parquet* p = r->ck;
+  DState* st = r->d_state.as<DState>();
+  DJsonAction* A = r->d_acts.as<DJsonAction>();
+  Slot* S = r->d_slots.as<Slot>();
+  const int nf = (int)p->files.size();
+  const int ng = std::max(1, std::min(r->n_groups, nf));
+  r->grp_f0.assign(ng + 1, 0);
+  for (int g = 0; g <= ng; g++) r->grp_f0[g] = (int)((int64_t)nf * g / ng);
+  while ((int)r->grp_ev.size() < ng) {
+    hipEvent_t e = nullptr;
+    HIPOK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    r->grp_ev.push_back(e);
+  }
+  p->file_done.assign(nf, nullptr);
+  r->file_ready.assign(nf, 0);
+  // the host block every selection lands in
+  r->h_csel_off.assign(nf + 1, 0);
+  for (int f = 0; f < nf; f++) r->h_csel_off[f + 1] = r->h_csel_off[f] + ((p->files[f].num_rows + 63) & ~(int64_t)63);
+  // (kept across reruns of the same scan: batches already handed out point into it)
+  if (r->h_csel.size() != (size_t)(r->h_csel_off[nf] + 64) && r->h_csel.alloc(r->h_csel_off[nf] + 64)) return 1;
+  // probe sets: per-file columns and selections as in the one-launch probe, row prefixes per group
+  r->probe_run = r->probe;
+  r->probe_sel.resize(nf);
+  r->grp_row0.assign(nf + ng, 0);
+  for (int f = 0; f < nf; f++) {
+    if (r->seed != kDecodeSeed) r->probe_run[f].path_hash = nullptr;   // collision retry
+    r->probe_sel[f] = r->d_csel[f]->as<uint8_t>();
+  }
+  for (int g = 0; g < ng; g++) {
+    int64_t* row0 = r->grp_row0.data() + r->grp_f0[g] + g;
+    for (int f = r->grp_f0[g]; f < r->grp_f0[g + 1]; f++) row0[f - r->grp_f0[g] + 1] = row0[f - r->grp_f0[g]] + r->probe_run[f].n_rows;
+  }
+  if (upload(r->d_probe_cols, r->probe_run.data(), nf * sizeof(ProbeCols), s) ||
+      upload(r->d_grp_row0, r->grp_row0.data(), r->grp_row0.size() * 8, s) ||
+      upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
+  for (int g = 0; g < ng; g++) {
+    const int f0 = r->grp_f0[g], f1 = r->grp_f0[g + 1];
+    decode_cols(p, s, p->file_col0[f0], p->file_col0[f1]);
+    {
+      KTimer::Scope sc(&T, 11, s);
+      const int64_t* row0 = r->grp_row0.data() + f0 + g;
+      ProbeSet PS{r->d_probe_cols.as<ProbeCols>() + f0, r->d_grp_row0.as<int64_t>() + f0 + g,
+                  r->d_probe_sel.as<uint8_t* const>() + f0, (int32_t)(f1 - f0), row0[f1 - f0]};
+      launch_probe_all(PS, S, r->d_fp.as<uint32_t>(), r->mask, A, r->d_canon.as<uint8_t>(), r->seed, h_nodv,
+                       r->d_cand.as<int32_t>(), r->d_cand_n.as<unsigned int>(), st, s);
+    }
+    for (int f = f0; f < f1; f++) replay_file_filters(r, (size_t)f);
+    for (int f = f0; f < f1; f++) {
+      const int64_t n = p->files[f].num_rows;
+      if (r->probe[f].n_rows == 0) memset(r->h_csel.data() + r->h_csel_off[f], 0, n);
+      else if (n) HIPOK(hipMemcpyAsync(r->h_csel.data() + r->h_csel_off[f], r->d_csel[f]->p, n, hipMemcpyDeviceToHost, s));
+    }
+    HIPOK(hipEventRecord(r->grp_ev[g], s));
+    for (int f = f0; f < f1; f++) p->file_done[f] = r->grp_ev[g];
+  }
+  r->h_csel_ready = true;
+  HIPOK(hipEventRecord(r->ev_out, s));   // the checkpoint stream waits for it at dk_replay_sync
+  return 0;
+}
+
 // the checkpoint rows' partition pruning and data skipping after the probe, then the hand-back to
 // the checkpoint's own stream
 static int replay_ckpt_filters(dk_replay* r) {
   hipStream_t s = r->stream;
-  KTimer& T = r->timer;
-  DState* st = r->d_state.as<DState>();
-  if (r->has_part)                        // partition pruning on the checkpoint files' rows
-    for (size_t fi = 0; fi < r->ck_maps.size(); fi++) {
-      KTimer::Scope sc(&T, 18, s);
-      launch_part_eval(r->ck_maps[fi], r->d_part.as<DPartProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
-    }
-  if (r->has_skip)                        // data skipping on the checkpoint files' selected adds
-    for (size_t fi = 0; fi < r->ck_stats.size(); fi++) {
-      KTimer::Scope sc(&T, 17, s);
-      if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
-        launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
-      else
-        launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
-    }
+  if (r->has_part || r->has_skip)         // partition pruning, then data skipping, per file
+    for (size_t fi = 0; fi < r->d_csel.size(); fi++) replay_file_filters(r, fi);
   // later work on the checkpoint's stream (column reads) sees the decoded columns
   HIPOK(hipEventRecord(r->ev_out, s));
   HIPOK(hipStreamWaitEvent(r->ck->stream, r->ev_out, 0));
@@ -3387,7 +3506,59 @@ extern "C" int dk_replay_run(dk_replay* r) {
   r->have_result = false;
   r->h_csel_ready = false;
   if (r->ck && invalidate_mirrors(r->ck)) return 1;
+  r->n_groups = 0;
   return replay_launch(r);
+}
+
+// The run with the checkpoint files in n_groups groups (1 <= n_groups; at most one group per file),
+// so that a consumer can take the first files' batches while the later groups are still decoding:
+// dk_replay_wait_file(r, -1) before the commit-tail selection, dk_replay_wait_file(r, f) before
+// file f's selection / columns, dk_replay_sync at the end (counters). Exchange mode runs ungrouped.
+extern "C" int dk_replay_run_grouped(dk_replay* r, int32_t n_groups) {
+  if (!r) return fail("null replay");
+  if (n_groups < 1) return fail("dk_replay_run_grouped: n_groups must be >= 1");
+  hipSetDevice(r->eng->cfg.device);
+  r->have_result = false;
+  r->h_csel_ready = false;
+  r->tail_ready = false;
+  r->file_ready.clear();
+  if (r->ck && invalidate_mirrors(r->ck)) return 1;
+  r->n_groups = n_groups;
+  if (!r->aux.s && r->aux.create()) return 1;
+  return replay_launch(r);
+}
+
+// Wait until file f's selection (f = -1: the commit tail's) of a grouped run is on the host; a device
+// error seen by then (flags only grow) is reported the way dk_replay_sync reports it, after the whole
+// run (a key-hash collision reruns it). After dk_replay_sync, or for an ungrouped run: the sync.
+extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
+  if (!r) return fail("null replay");
+  hipSetDevice(r->eng->cfg.device);
+  if (r->have_result) return 0;
+  const bool grouped = r->n_groups > 0 && r->xw == 0 && r->ck && !r->grp_f0.empty() && r->ev_tail;
+  if (!grouped) return dk_replay_sync(r);      // no checkpoint, an ungrouped run, or exchange mode
+  if (file >= (int)r->file_ready.size()) return fail("dk_replay_wait_file: bad checkpoint file index");
+  if (file >= 0 && r->file_ready[file]) return 0;
+  if (file < 0 && r->tail_ready) return 0;
+  hipEvent_t ev = r->ev_tail;
+  if (file >= 0) {
+    int g = 0;
+    while (r->grp_f0[g + 1] <= file) g++;
+    ev = r->grp_ev[g];
+  }
+  HIPOK(hipEventSynchronize(ev));
+  DState st{}, ps{};
+  HIPOK(hipMemcpyAsync(&st, r->d_state.p, sizeof st, hipMemcpyDeviceToHost, r->aux.s));
+  if (r->ck) HIPOK(hipMemcpyAsync(&ps, r->ck->d_state.p, sizeof ps, hipMemcpyDeviceToHost, r->aux.s));
+  HIPOK(hipStreamSynchronize(r->aux.s));
+  if (st.err_flags || ps.err_flags) return dk_replay_sync(r);
+  if (file < 0) r->tail_ready = true;
+  else {
+    int g = 0;
+    while (r->grp_f0[g + 1] <= file) g++;
+    for (int f = r->grp_f0[g]; f < r->grp_f0[g + 1]; f++) r->file_ready[f] = 1;
+  }
+  return 0;
 }
 
 // ---- hash(path)-owner exchange ("alltoall" mode) ----
@@ -3491,6 +3662,7 @@ extern "C" int dk_replay_sync(dk_replay* r) {
   if (r->xw > 0 && r->xphase != 3) return fail("dk_replay_sync: the exchange-mode run has not finished its exchange");
   for (int attempt = 0; attempt < 8; attempt++) {
     HIPOK(hipStreamSynchronize(s));
+    if (r->ck && r->n_groups > 0) HIPOK(hipStreamWaitEvent(r->ck->stream, r->ev_out, 0));
     r->timer.collect();
     if (r->ck) { r->ck->timer.collect(); if (check_state(r->ck)) return 1; }
     HIPOK(hipMemcpy(&r->h_state, r->d_state.p, sizeof(DState), hipMemcpyDeviceToHost));
@@ -3555,7 +3727,7 @@ extern "C" int dk_replay_counters_split(dk_replay* r, int64_t tail[5], int64_t c
 
 extern "C" int dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n) {
   hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
-  if (!r->have_result) return fail("replay has no result");
+  if (!r->have_result && !r->tail_ready) return fail("replay has no result");
   if (!r->tail || n != r->tail->rows) return fail("bad selection size");
   memset(out, 0, n);
   std::vector<uint8_t> sel(r->acts.size());
@@ -3580,8 +3752,9 @@ extern "C" int dk_replay_ckpt_selection(dk_replay* r, int32_t file, uint8_t* out
 extern "C" int dk_replay_ckpt_selection_host(dk_replay* r, int32_t file, const uint8_t** out) {
   hipSetDevice(r->eng->cfg.device);
   *out = nullptr;
-  if (!r->have_result) return fail("replay has no result");
   if (!r->ck || file < 0 || file >= (int)r->d_csel.size()) return fail("bad checkpoint file index");
+  if (!r->have_result && !(file < (int)r->file_ready.size() && r->file_ready[file]))
+    return fail("replay has no result");
   if (!r->h_csel_ready) {
     const int nf = (int)r->d_csel.size();
     r->h_csel_off.assign(nf + 1, 0);
@@ -3661,8 +3834,11 @@ extern "C" void dk_replay_free(dk_replay* r) {
   if (!r) return;
   hipSetDevice(r->eng->cfg.device);
   hipStreamSynchronize(r->stream);
+  if (r->ck) { hipStreamSynchronize(r->ck->stream); r->ck->file_done.clear(); }
   if (r->ev_in) hipEventDestroy(r->ev_in);
   if (r->ev_out) hipEventDestroy(r->ev_out);
+  if (r->ev_tail) hipEventDestroy(r->ev_tail);
+  for (hipEvent_t e : r->grp_ev) hipEventDestroy(e);
   SyncedRelease drained;
   delete r;
 }
@@ -4760,7 +4936,8 @@ extern "C" int dk_ckpt_writer_add_checkpoint_adds(dk_ckpt_writer* w, dk_replay* 
   hipSetDevice(w->eng->cfg.device);
   if (w->host_rows > 0 && flush_host_rows(w)) return 1;
   if (!r || !r->ck || file < 0 || file >= (int32_t)r->ck->files.size()) return fail("dk_ckpt_writer_add_checkpoint_adds: bad file");
-  if (!r->have_result) return fail("dk_ckpt_writer_add_checkpoint_adds: the replay has no result");
+  if (!r->have_result && !(file < (int32_t)r->file_ready.size() && r->file_ready[file]))
+    return fail("dk_ckpt_writer_add_checkpoint_adds: the replay has no result");
   if (row0 < 0 || row1 < row0 || row1 > r->ck->files[file].num_rows) return fail("dk_ckpt_writer_add_checkpoint_adds: bad rows");
   hipStream_t s = w->s;
   HIPOK(hipStreamSynchronize(r->stream));

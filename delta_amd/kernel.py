@@ -48,6 +48,15 @@ SIDECAR_LEAVES = ["sidecar.path", "sidecar.sizeInBytes", "sidecar.modificationTi
 TIMING = 1
 
 
+def scan_groups(n_files):
+    """Groups of checkpoint files for a grouped getScanFiles run (dk_replay_run_grouped): about 8
+    files per group, at most 8 groups; DK_SCAN_GROUPS overrides (0: one ungrouped run)."""
+    env = os.environ.get("DK_SCAN_GROUPS")
+    if env is not None:
+        return max(0, min(int(env), n_files))
+    return 0 if n_files <= 1 else min(8, max(2, n_files // 8))
+
+
 def _cstrs(items):
     arr = (C.c_char_p * len(items))()
     arr[:] = [s.encode() if isinstance(s, str) else s for s in items]
@@ -1279,12 +1288,21 @@ class GpuScan:
             self.prepare(engine)
             self.replay = True
         t0 = time.perf_counter()
+        groups = scan_groups(len(self.ckpt_files or []))
+        exchanging = getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1
+        if groups and not exchanging:
+            # grouped: batches go out as their group of files is decoded and probed; the counters are
+            # final once the iterator is exhausted (ScanImpl's metrics are read after it, too)
+            check(lib().dk_replay_run_grouped(self._rh, groups))
+            check(lib().dk_replay_wait_file(self._rh, -1))
+            self.prepare_ms["device_run"] = (time.perf_counter() - t0) * 1e3
+            return self._batches(grouped=True)
         self.run()
         self.sync()
         self.prepare_ms["device_run"] = (time.perf_counter() - t0) * 1e3
         return self._batches()
 
-    def _batches(self):
+    def _batches(self, grouped=False):
         root = self.table_root()
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else [])
         if self.tail.rows:
@@ -1304,6 +1322,8 @@ class GpuScan:
         # mirrors (every file's selection comes to the host in one round of copies; a leaf's first
         # access queues its copy for every later file), valid until the scan is closed
         for fi, path in enumerate(self.ckpt_files or []):
+            if grouped:
+                check(lib().dk_replay_wait_file(self._rh, fi))
             n = self.ckpt.num_rows(fi)
             ptr = C.c_void_p()
             check(lib().dk_replay_ckpt_selection_host(self._rh, fi, C.byref(ptr)))
@@ -1311,6 +1331,8 @@ class GpuScan:
             cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf, copy=False))
             yield FilteredColumnarBatch(cols, root, int(n), sel, path, self.ckpt_index[fi],
                                         int(self.ckpt.row_offset(fi)))
+        if grouped:
+            self.sync()                     # the counters (and any error the waits did not see)
 
     def close(self):
         if getattr(self, "_rh", None):

@@ -329,6 +329,15 @@ int  dk_replay_stats_parsed_files(dk_replay* r);
  * checkpoint projection must include add.partitionValues */
 int  dk_replay_set_partition_filter(dk_replay* r, const dk_part_program* prog);
 int  dk_replay_run(dk_replay* r);                      /* async: key build, probe, decode */
+/* The same run with the checkpoint files in n_groups groups, each decoded, probed, filtered and its
+ * selections copied to host memory in turn, so that ScanImpl.getScanFiles' batches can be handed
+ * out while later groups still decode (CloseableIterator<FilteredColumnarBatch>.next,
+ * ScanImpl.java:120-186 / ActiveAddFilesIterator.java:146-275): dk_replay_wait_file(r, -1) before
+ * the commit-tail selection, dk_replay_wait_file(r, f) before file f's selection and columns
+ * (dk_replay_ckpt_selection_host, dk_parquet_column), dk_replay_sync at the end for the counters. A
+ * device error seen by a wait is reported after the whole run, as dk_replay_sync reports it. */
+int  dk_replay_run_grouped(dk_replay* r, int32_t n_groups);
+int  dk_replay_wait_file(dk_replay* r, int32_t file);
 int  dk_replay_sync(dk_replay* r);
 /* counters: addFilesSeen, addFilesSeenFromDeltaFiles, activeAddFiles, duplicateAddFiles,
  * removeFilesSeenFromDeltaFiles */
