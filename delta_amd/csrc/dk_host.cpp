@@ -623,9 +623,51 @@ static int64_t chunk_start(const ColMeta& m) {
   return start;
 }
 
-static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef>& out) {
+static int pread_full(int fd, uint8_t* dst, int64_t len, int64_t off) {
+  for (int64_t done = 0; done < len;) {
+    const ssize_t k = pread(fd, dst + done, (size_t)(len - done), off + done);
+    if (k <= 0) return 1;
+    done += k;
+  }
+  return 0;
+}
+
+// Header pre-read (parquet_open's first phase): the file bytes [lo, hi) are valid in the image; more
+// are pread on demand, in blocks of at least 16 KiB (many small pages' headers per read), so the page
+// tables can be built before the column chunks themselves are read.
+struct HdrWin {
+  int fd = -1;
+  const FileM* f = nullptr;
+  int64_t lo = 0, hi = 0;
+  // make the file bytes [off, min(off + want, lim)) valid; returns the end of the valid range, -1 on error
+  int64_t ensure(int64_t off, int64_t want, int64_t lim) {
+    const int64_t e = std::min(off + want, lim);
+    if (off >= lo && e <= hi) return hi;
+    const int64_t n = std::max(e - off, std::min<int64_t>(16384, lim - off));
+    uint8_t* dst = n > 0 ? (uint8_t*)span_ptr(*f, off, n) : nullptr;
+    if (!dst || pread_full(fd, dst, n, off)) return -1;
+    lo = off;
+    hi = off + n;
+    return hi;
+  }
+  // a complete page header at file offset p (chunk end `end`) in the image
+  int header(int64_t p, int64_t end) {
+    for (int64_t want = 256;; want *= 8) {
+      const int64_t h = ensure(p, want, end);
+      if (h < 0) return fail("Error reading Parquet file: " + f->path + " (short read)");
+      const uint8_t* b = span_ptr(*f, p, h - p);
+      if (b && parse_page_header(b, b + (h - p)).ok) return 0;
+      if (h >= end || want > (int64_t)1 << 26) return 0;   // malformed: the table build reports it
+    }
+  }
+};
+
+static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef>& out, HdrWin* w = nullptr) {
   const int64_t N = f.size;
   int64_t start = chunk_start(m);
+  const int64_t cend = start + m.total_compressed;
+  if (w && m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= N && w->ensure(m.oi_off, m.oi_len, m.oi_off + m.oi_len) < 0)
+    return fail("Error reading Parquet file: " + f.path + " (short read)");
   const uint8_t* oi = (m.oi_off > 0 && m.oi_len > 0 && m.oi_off + m.oi_len <= N) ? span_ptr(f, m.oi_off, m.oi_len) : nullptr;
   if (oi) {
     TReader t{oi, oi + m.oi_len, 0};
@@ -650,17 +692,21 @@ static int enumerate_pages(const FileM& f, const ColMeta& m, std::vector<PageRef
     if (!t.bad && !offs.empty()) {
       if (offs[0] > start) out.push_back({start, true});   // dictionary page precedes the first data page
       for (int64_t o : offs) out.push_back({o, false});
+      if (w)
+        for (const PageRef& r : out)
+          if (r.hdr_off >= start && r.hdr_off < cend && w->header(r.hdr_off, cend)) return 1;
       return 0;
     }
     out.clear();
   }
   // host walk (no offset index)
-  int64_t p = start, end = start + m.total_compressed;
+  int64_t p = start, end = cend;
   const uint8_t* cb = end <= N ? span_ptr(f, start, m.total_compressed) : nullptr;
   if (!cb) return fail("Error reading Parquet file: " + f.path + " (chunk out of range)");
   const uint8_t* b = cb - start;   // file-offset view of the chunk
   while (p < end) {
-    PageHeader h = parse_page_header(b + p, b + end);
+    if (w && w->header(p, end)) return 1;
+    PageHeader h = parse_page_header(b + p, b + (w ? std::min(w->hi, end) : end));
     if (!h.ok || h.csize < 0) return fail("Error reading Parquet file: " + f.path + " (bad page header)");
     if (h.type != PAGE_INDEX) out.push_back({p, h.type == PAGE_DICT});
     p += h.hdr_len + h.csize;
@@ -810,6 +856,7 @@ struct dk_parquet {
   StreamH own;                      // first members: destroyed after every buffer below
   StreamH copy[kCopyStreams];
   StreamH aux;                      // table uploads while `stream` waits for the H2D copies
+  StreamH side[2];                  // sizing slices rotate over stream, side[0], side[1] (created on demand)
   EventH copy_done[kCopyStreams];
   hipStream_t stream = nullptr;
   dk_engine* eng = nullptr;
@@ -851,6 +898,9 @@ struct dk_parquet {
   std::vector<hipEvent_t> file_done;
   std::vector<int32_t> h_cpage, h_sbase, h_fbase;
   std::vector<EventH> file_ev;
+  // the images are read while prepare runs: per file 0 = its H2D copies not queued yet, 1 = queued
+  // (file_ev recorded), 2 = its read failed (null: every image was queued before prepare)
+  std::unique_ptr<std::atomic<int>[]> queued;
   std::vector<HBuf> staging;        // pinned sources of zero-copy uploads, released when prepare ends
   int n_pages = 0, n_cols = 0;
   bool has_compressed = false, has_dbp = false;
@@ -1096,6 +1146,16 @@ static int upload_zc(dk_parquet* p, DBuf& d, const void* src, size_t n, hipStrea
   return 0;
 }
 
+// Wait until file f's image copies are queued (file_ev recorded: a stream may wait for it; an event
+// that was never recorded would let it through at once). False: the file's read failed.
+static bool wait_queued(const dk_parquet* p, int f) {
+  if (!p->queued) return true;
+  int v;
+  while ((v = p->queued[f].load(std::memory_order_acquire)) == 0) std::this_thread::yield();
+  return v == 1;
+}
+static bool is_queued(const dk_parquet* p, int f) { return !p->queued || p->queued[f].load(std::memory_order_acquire) == 1; }
+
 static int prepare(dk_parquet* p) {
   hipStream_t s = p->stream;
   // the decode stream waits for the file images' H2D copies: table uploads and work-list expansion
@@ -1271,22 +1331,46 @@ static int prepare(dk_parquet* p) {
     int f0 = 0;
     int64_t acc = 0;
     if (adaptive && slices > 1) {
+      // slices touch disjoint pages / segments / tiles / columns: they rotate over up to three
+      // streams (DK_OPEN_STREAMS), so one slice's latency tail (k_snap_fix / k_snap_frag's longest
+      // pages) overlaps the next slice's passes; `s` joins them all at the end
+      static const int nss = getenv("DK_OPEN_STREAMS") ? std::max(1, std::min(3, atoi(getenv("DK_OPEN_STREAMS")))) : 3;
+      hipStream_t ss[3] = {s, nullptr, nullptr};
+      hipEvent_t tables = nullptr;
+      if (nss > 1) {
+        HIPOK(hipEventCreateWithFlags(&tables, hipEventDisableTiming));
+        HIPOK(hipEventRecord(tables, s));          // the table uploads (s already waits for them)
+        for (int k = 1; k < nss; k++) {
+          if (!p->side[k - 1].s && p->side[k - 1].create()) return 1;
+          ss[k] = p->side[k - 1].s;
+          HIPOK(hipStreamWaitEvent(ss[k], tables, 0));
+        }
+      }
+      int slice = 0;
       while (f0 < nf) {
         int f1 = f0;
         acc = 0;
         // at least `target` bytes (or the rest), then every file already landed
-        while (f1 < nf && (acc < target || hipEventQuery(p->file_ev[f1]) == hipSuccess)) {
+        while (f1 < nf && (acc < target || (is_queued(p, f1) && hipEventQuery(p->file_ev[f1]) == hipSuccess))) {
+          if (!wait_queued(p, f1)) { if (tables) hipEventDestroy(tables); return 1; }   // parquet_open reports the read error
           HIPOK(hipEventSynchronize(p->file_ev[f1]));
           acc += (int64_t)p->files[f1].bytes.size();
           f1++;
         }
-        for (int f = f0; f < f1; f++) HIPOK(hipStreamWaitEvent(s, p->file_ev[f], 0));
-        sizing_stages(p, s, file_range(p, f0, f1));
+        hipStream_t cs = ss[slice++ % nss];
+        for (int f = f0; f < f1; f++) HIPOK(hipStreamWaitEvent(cs, p->file_ev[f], 0));
+        sizing_stages(p, cs, file_range(p, f0, f1));
         f0 = f1;
       }
+      for (int k = 1; k < nss; k++) {               // `s` waits for the side streams' slices
+        HIPOK(hipEventRecord(tables, ss[k]));
+        HIPOK(hipStreamWaitEvent(s, tables, 0));
+      }
+      if (tables) hipEventDestroy(tables);
     } else {
       for (int f = 0; f < nf; f++) {
         acc += (int64_t)p->files[f].bytes.size();
+        if (!wait_queued(p, f)) return 1;
         HIPOK(hipStreamWaitEvent(s, p->file_ev[f], 0));
         if (f + 1 == nf || acc >= target) {
           sizing_stages(p, s, file_range(p, f0, f + 1));
@@ -1916,23 +2000,64 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
       }
     }
     if (read_spans(f, want)) { errs[fi] = g_err; return; }
-    // the file's image is read into pinned memory and goes to HBM in 8 MiB pieces on a copy stream
-    // while the rest of it (and the other files) are still being read
+    // first only the offset indexes and page headers (pread in blocks): the page tables, and with them
+    // the whole host half of prepare, are built before the column chunks are read
+    {
+      HdrWin w;
+      w.f = &f;
+      w.fd = open(f.path.c_str(), O_RDONLY);
+      if (w.fd < 0) { errs[fi] = "Error reading Parquet file: " + f.path + " (cannot open)"; return; }
+      std::vector<PageRef> refs;
+      for (int li = 0; li < n_leaves && errs[fi].empty(); li++) {
+        const int idx = p->leafidx[fi][li];
+        if (idx < 0) continue;
+        for (int32_t g : f.sel) {
+          refs.clear();
+          if (enumerate_pages(f, f.rgs[g].cols[idx], refs, &w)) { errs[fi] = g_err; break; }
+        }
+      }
+      close(w.fd);
+      if (!errs[fi].empty()) return;
+    }
     hipSetDevice(e->cfg.device);
     if (p->dfile[fi].alloc(f.bytes.size() + 256)) { errs[fi] = g_err; return; }
-    hipStream_t cs = p->copy[fi % copy_streams()].s;
-    uint8_t* dst = p->dfile[fi].as<uint8_t>();
-    if (read_spans_into(f, (size_t)8 << 20, [&](size_t off, size_t len) {
-          return hipMemcpyAsync(dst + off, f.bytes.data() + off, len, hipMemcpyHostToDevice, cs) == hipSuccess
-                     ? 0 : fail("hipMemcpyAsync failed for " + f.path);
-        })) { errs[fi] = g_err; return; }
-    if (hipEventRecord(p->file_ev[fi], cs) != hipSuccess) { errs[fi] = "hipEventRecord failed"; return; }
-    // its pages and headers while the copies run
     if (build_file_meta(p.get(), fi, f, p->leafidx[fi], metas[fi])) errs[fi] = g_err;
   });
-  // (the decode stream waits for each file's copies in prepare, slice by slice)
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
+  // then the images: read into pinned memory, each going to HBM in 8 MiB pieces on a copy stream while
+  // the rest of it (and the other files) are still being read -- on background threads, while prepare
+  // runs the sizing passes over the files whose copies have landed (DK_OPEN_OVERLAP=0: every image is
+  // read before prepare)
+  p->queued.reset(new std::atomic<int>[n_files > 0 ? n_files : 1]);
+  for (int fi = 0; fi < n_files; fi++) p->queued[fi].store(0);
+  std::thread reader([&] {
+    parallel_for(n_files, [&](int fi) {
+      FileM& f = p->files[fi];
+      hipSetDevice(e->cfg.device);
+      hipStream_t cs = p->copy[fi % copy_streams()].s;
+      uint8_t* dst = p->dfile[fi].as<uint8_t>();
+      if (read_spans_into(f, (size_t)8 << 20, [&](size_t off, size_t len) {
+            return hipMemcpyAsync(dst + off, f.bytes.data() + off, len, hipMemcpyHostToDevice, cs) == hipSuccess
+                       ? 0 : fail("hipMemcpyAsync failed for " + f.path);
+          })) { errs[fi] = g_err; p->queued[fi].store(2, std::memory_order_release); return; }
+      if (hipEventRecord(p->file_ev[fi], cs) != hipSuccess) {
+        errs[fi] = "hipEventRecord failed";
+        p->queued[fi].store(2, std::memory_order_release);
+        return;
+      }
+      p->queued[fi].store(1, std::memory_order_release);
+    });
+  });
+  struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } joiner{reader};
+  static const bool overlap = !getenv("DK_OPEN_OVERLAP") || atoi(getenv("DK_OPEN_OVERLAP")) != 0;
+  auto read_errors = [&]() -> int {
+    if (reader.joinable()) reader.join();
+    for (int fi = 0; fi < n_files; fi++)
+      if (!errs[fi].empty()) return fail(errs[fi]);
+    return 0;
+  };
+  if (!overlap && read_errors()) return 1;
   const auto t_io1 = std::chrono::steady_clock::now();
   for (int fi = 0; fi < n_files; fi++) {             // concatenate the files' tables in file order
     FileMeta& M = metas[fi];
@@ -1963,7 +2088,13 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->n_pages = (int)p->h_pages.size();
   p->n_cols = (int)p->h_cols.size();
   const auto t_h2d = std::chrono::steady_clock::now();
-  if (prepare(p.get())) return 1;
+  if (prepare(p.get())) {
+    const std::string perr = g_err;
+    if (read_errors()) return 1;                 // a failed read is the error to report
+    return fail(perr);
+  }
+  if (reader.joinable() && read_errors()) return 1;
+  p->queued.reset();
   {
     const auto t_end = std::chrono::steady_clock::now();
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
