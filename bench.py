@@ -41,6 +41,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+CONSUME_PROFILE = os.environ.get("DK_CONSUME_PROFILE", "0") not in ("", "0")   # consume-phase split
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
 METRIC = "checkpoint actions reconciled/sec (node) + snapshot load ms, 100M AddFile"
 REMOVE_LEAVES = ["remove.path", "remove.deletionVector.storageType", "remove.deletionVector.pathOrInlineDv",
@@ -503,8 +504,16 @@ def main(argv=None):
         tail_paths, bits = [], []
         it = sc.getScanFiles(eng)
         t_c = time.perf_counter()
+        cprof = CONSUME_PROFILE and not capture_result
+        t_w = t_v = t_s = 0.0
+        waits = []
+        t_a = time.perf_counter()
         for b in it:
+            if cprof:
+                t_b = time.perf_counter(); t_w += t_b - t_a; waits.append(round((t_b - t_a) * 1e3, 2))
             v = b.data["add.size"].fixed.view("<i8")
+            if cprof:
+                t_d = time.perf_counter(); t_v += t_d - t_b
             if b.selection is None:
                 size_sum += int(v.sum())
                 n_sel += b.size
@@ -512,6 +521,8 @@ def main(argv=None):
                 # a masked reduction over the selected rows (no gather, no temporaries)
                 size_sum += int(v.sum(where=b.selection))
                 n_sel += int(np.count_nonzero(b.selection))
+            if cprof:
+                t_a = time.perf_counter(); t_s += t_a - t_d
             if capture_result:
                 if b.file_index < 0:
                     pc = b.data["add.path"]
@@ -526,6 +537,11 @@ def main(argv=None):
             capture.update(counters=sc.metrics.as_tuple(), tail_paths=tail_paths, bits=bits)
         phases = dict(sc.prepare_ms)
         phases["consume"] = consume_ms
+        if cprof:   # DK_CONSUME_PROFILE=1: where the consumer's time goes
+            t_e = time.perf_counter()
+            waits.append(round((t_e - t_a) * 1e3, 2))     # the last next(): StopIteration (final sync)
+            phases.update(consume_wait=t_w * 1e3 + waits[-1], consume_column=t_v * 1e3, consume_sum=t_s * 1e3)
+            log("consume waits (ms, per next()):", waits)
         t_x = time.perf_counter()
         sc.close()
         phases["close"] = (time.perf_counter() - t_x) * 1e3

@@ -901,6 +901,7 @@ struct dk_parquet {
   // the images are read while prepare runs: per file 0 = its H2D copies not queued yet, 1 = queued
   // (file_ev recorded), 2 = its read failed (null: every image was queued before prepare)
   std::unique_ptr<std::atomic<int>[]> queued;
+  std::chrono::steady_clock::time_point t_open0;   // DK_VERBOSE timeline origin
   std::vector<HBuf> staging;        // pinned sources of zero-copy uploads, released when prepare ends
   int n_pages = 0, n_cols = 0;
   bool has_compressed = false, has_dbp = false;
@@ -1358,6 +1359,9 @@ static int prepare(dk_parquet* p) {
           f1++;
         }
         hipStream_t cs = ss[slice++ % nss];
+        static const bool verbose = getenv("DK_VERBOSE") != nullptr;
+        if (verbose) fprintf(stderr, "[dk] sizing slice %d: files [%d, %d) %.1f MB queued at %.1f ms\n", slice - 1, f0, f1,
+                             acc / 1e6, since(p->t_open0));
         for (int f = f0; f < f1; f++) HIPOK(hipStreamWaitEvent(cs, p->file_ev[f], 0));
         sizing_stages(p, cs, file_range(p, f0, f1));
         f0 = f1;
@@ -1387,6 +1391,7 @@ static int prepare(dk_parquet* p) {
   std::string m = page_status_msg(p, p->h_pages);
   if (!m.empty()) return fail(m);
   p->open_ms[5] = since(t2);            // sizing passes on the device (snappy, runs, counts, positions)
+  if (getenv("DK_VERBOSE")) fprintf(stderr, "[dk] sizing done at %.1f ms\n", since(p->t_open0));
   const auto t3 = clk::now();
   // 3. string-copy tile table (page counts are final after the count pass)
   {
@@ -1981,6 +1986,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->file_ev.resize(n_files > 0 ? n_files : 0);
   for (auto& ev : p->file_ev) HIPOK(hipEventCreateWithFlags(&ev.e, hipEventDisableTiming));
   const auto t_io0 = std::chrono::steady_clock::now();
+  p->t_open0 = t_io0;
   parallel_for(n_files, [&](int fi) {
     FileM& f = p->files[fi];
     f.path = paths[fi];
@@ -2000,38 +2006,105 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
       }
     }
     if (read_spans(f, want)) { errs[fi] = g_err; return; }
-    // first only the offset indexes and page headers (pread in blocks): the page tables, and with them
-    // the whole host half of prepare, are built before the column chunks are read
-    {
-      HdrWin w;
-      w.f = &f;
-      w.fd = open(f.path.c_str(), O_RDONLY);
-      if (w.fd < 0) { errs[fi] = "Error reading Parquet file: " + f.path + " (cannot open)"; return; }
-      std::vector<PageRef> refs;
-      for (int li = 0; li < n_leaves && errs[fi].empty(); li++) {
-        const int idx = p->leafidx[fi][li];
-        if (idx < 0) continue;
-        for (int32_t g : f.sel) {
-          refs.clear();
-          if (enumerate_pages(f, f.rgs[g].cols[idx], refs, &w)) { errs[fi] = g_err; break; }
-        }
-      }
-      close(w.fd);
-      if (!errs[fi].empty()) return;
-    }
     hipSetDevice(e->cfg.device);
     if (p->dfile[fi].alloc(f.bytes.size() + 256)) { errs[fi] = g_err; return; }
+  });
+  for (int fi = 0; fi < n_files; fi++)
+    if (!errs[fi].empty()) return fail(errs[fi]);
+  // then only the offset indexes and page headers (pread in blocks): the page tables, and with them
+  // the whole host half of prepare, are built before the column chunks are read (reading the headers
+  // beside the image reads was no faster: both are CPU-bound on the box's share of cores)
+  parallel_for(n_files, [&](int fi) {
+    FileM& f = p->files[fi];
+    HdrWin w;
+    w.f = &f;
+    w.fd = open(f.path.c_str(), O_RDONLY);
+    if (w.fd < 0) { errs[fi] = "Error reading Parquet file: " + f.path + " (cannot open)"; return; }
+    std::vector<PageRef> refs;
+    for (int li = 0; li < n_leaves && errs[fi].empty(); li++) {
+      const int idx = p->leafidx[fi][li];
+      if (idx < 0) continue;
+      for (int32_t g : f.sel) {
+        refs.clear();
+        if (enumerate_pages(f, f.rgs[g].cols[idx], refs, &w)) { errs[fi] = g_err; break; }
+      }
+    }
+    close(w.fd);
+    if (!errs[fi].empty()) return;
     if (build_file_meta(p.get(), fi, f, p->leafidx[fi], metas[fi])) errs[fi] = g_err;
   });
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
+  std::vector<std::string> rerrs(n_files > 0 ? n_files : 0);   // the reader's errors
   // then the images: read into pinned memory, each going to HBM in 8 MiB pieces on a copy stream while
   // the rest of it (and the other files) are still being read -- on background threads, while prepare
   // runs the sizing passes over the files whose copies have landed (DK_OPEN_OVERLAP=0: every image is
   // read before prepare)
   p->queued.reset(new std::atomic<int>[n_files > 0 ? n_files : 1]);
   for (int fi = 0; fi < n_files; fi++) p->queued[fi].store(0);
+  // Pieces (default): every span cut into 8 MiB pieces, all threads working through them in file
+  // order, so files land one after another from the first milliseconds on (one file per thread
+  // would land the first file only after a sixteenth of the whole read); the thread that finishes a
+  // file's last piece records its event. DK_OPEN_PIECES=0: one file per thread.
+  struct Piece { int fi; int64_t file_off, packed_off, len; };
+  std::vector<Piece> pieces;
+  static const bool by_piece = !getenv("DK_OPEN_PIECES") || atoi(getenv("DK_OPEN_PIECES")) != 0;
+  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[n_files > 0 ? n_files : 1]);
+  std::unique_ptr<int[]> fds(new int[n_files > 0 ? n_files : 1]);
+  for (int fi = 0; fi < n_files; fi++) {
+    int n = 0;
+    fds[fi] = -1;
+    if (by_piece)
+      for (const Span& sp : p->files[fi].spans)
+        for (int64_t o = 0; o < sp.len; o += (int64_t)8 << 20, n++)
+          pieces.push_back({fi, sp.file_off + o, sp.packed_off + o, std::min<int64_t>((int64_t)8 << 20, sp.len - o)});
+    left[fi].store(n);
+  }
   std::thread reader([&] {
+    if (by_piece) {
+      for (int fi = 0; fi < n_files; fi++) {
+        fds[fi] = open(p->files[fi].path.c_str(), O_RDONLY);
+        if (fds[fi] < 0) { rerrs[fi] = "Error reading Parquet file: " + p->files[fi].path + " (cannot open)"; p->queued[fi].store(2); }
+        else if (left[fi].load() == 0) {              // nothing projected to read
+          const bool rec = hipEventRecord(p->file_ev[fi], p->copy[fi % copy_streams()].s) == hipSuccess;
+          if (!rec) rerrs[fi] = "hipEventRecord failed";
+          p->queued[fi].store(rec ? 1 : 2, std::memory_order_release);
+        }
+      }
+      parallel_for((int)pieces.size(), [&](int k) {
+        const Piece& pc = pieces[k];
+        FileM& f = p->files[pc.fi];
+        if (p->queued[pc.fi].load(std::memory_order_acquire) == 2) return;
+        hipSetDevice(e->cfg.device);
+        hipStream_t cs = p->copy[pc.fi % copy_streams()].s;
+        const bool ok = pread_full(fds[pc.fi], f.bytes.data() + pc.packed_off, pc.len, pc.file_off) == 0 &&
+                        hipMemcpyAsync(p->dfile[pc.fi].as<uint8_t>() + pc.packed_off, f.bytes.data() + pc.packed_off,
+                                       (size_t)pc.len, hipMemcpyHostToDevice, cs) == hipSuccess;
+        if (!ok) {
+          static std::mutex mu;
+          std::lock_guard<std::mutex> g(mu);
+          if (rerrs[pc.fi].empty()) rerrs[pc.fi] = "Error reading Parquet file: " + f.path + " (short read)";
+          p->queued[pc.fi].store(2, std::memory_order_release);
+          return;
+        }
+        if (left[pc.fi].fetch_sub(1) == 1) {          // the file's last piece: its copies are all queued
+          const bool rec = hipEventRecord(p->file_ev[pc.fi], cs) == hipSuccess;
+          if (!rec) rerrs[pc.fi] = "hipEventRecord failed";
+          int expect = 0;
+          p->queued[pc.fi].compare_exchange_strong(expect, rec ? 1 : 2, std::memory_order_acq_rel);
+        }
+      });
+      if (getenv("DK_VERBOSE"))
+        fprintf(stderr, "[dk] images read and queued at %.1f ms\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p->t_open0).count());
+      for (int fi = 0; fi < n_files; fi++) {
+        if (fds[fi] >= 0) close(fds[fi]);
+        int expect = 0;                               // (every file is settled by now)
+        p->queued[fi].compare_exchange_strong(expect, 2);
+        if (expect == 0 && rerrs[fi].empty()) rerrs[fi] = "Error reading Parquet file: " + p->files[fi].path + " (short read)";
+      }
+      return;
+    }
     parallel_for(n_files, [&](int fi) {
       FileM& f = p->files[fi];
       hipSetDevice(e->cfg.device);
@@ -2040,9 +2113,9 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
       if (read_spans_into(f, (size_t)8 << 20, [&](size_t off, size_t len) {
             return hipMemcpyAsync(dst + off, f.bytes.data() + off, len, hipMemcpyHostToDevice, cs) == hipSuccess
                        ? 0 : fail("hipMemcpyAsync failed for " + f.path);
-          })) { errs[fi] = g_err; p->queued[fi].store(2, std::memory_order_release); return; }
+          })) { rerrs[fi] = g_err; p->queued[fi].store(2, std::memory_order_release); return; }
       if (hipEventRecord(p->file_ev[fi], cs) != hipSuccess) {
-        errs[fi] = "hipEventRecord failed";
+        rerrs[fi] = "hipEventRecord failed";
         p->queued[fi].store(2, std::memory_order_release);
         return;
       }
@@ -2054,7 +2127,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   auto read_errors = [&]() -> int {
     if (reader.joinable()) reader.join();
     for (int fi = 0; fi < n_files; fi++)
-      if (!errs[fi].empty()) return fail(errs[fi]);
+      if (!rerrs[fi].empty()) return fail(rerrs[fi]);
     return 0;
   };
   if (!overlap && read_errors()) return 1;

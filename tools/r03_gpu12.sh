@@ -1,15 +1,16 @@
 #!/bin/bash
-# open overlap with rotating sizing streams: GPU tests touching parquet open, then interleaved A/B
+# open overlap variants: GPU tests touching parquet open, then interleaved A/B (env sets per config)
 set -o pipefail
 TAG=$1; TESTS=${2:-tests}
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT; cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "gpu tests failed"; grep -E "^E |FAILED|Error" $OUT/pytest_gpu.log | head -20; tail -5 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
+CFGS=${CFGS:-"DK_OPEN_PIECES=1 DK_OPEN_PIECES=0,DK_OPEN_STREAMS=1 DK_OPEN_OVERLAP=0"}
 for i in 1 2; do
-for cfg in "1 3" "1 1" "0 1"; do
-set -- $cfg
-DK_OPEN_OVERLAP=$1 DK_OPEN_STREAMS=$2 timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline > $OUT/b_$1_$2_$i.json 2> $OUT/b_$1_$2_$i.err || { echo "bench failed"; tail -20 $OUT/b_$1_$2_$i.err; exit 1; }
-python -c "import json; d=json.load(open('$OUT/b_$1_$2_$i.json')); p=d['getScanFiles_phases_ms']; print('overlap=$1 streams=$2', round(d['ms_per_step'],1), 'open', p['checkpoint_open'], 'io', p['open_read_h2d'], 'prep', p['open_prepare'], 'sizing', p['prep_device_sizing'], 'run', p['device_run'], 'consume', p['consume'], 'close', p['close'], 'dev', round(d['device_step']['ms'],1))"
+for cfg in $CFGS; do
+name=$(echo $cfg | tr ',=' '__')
+env $(echo $cfg | tr ',' ' ') timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline > $OUT/b_${name}_$i.json 2> $OUT/b_${name}_$i.err || { echo "bench failed"; tail -20 $OUT/b_${name}_$i.err; exit 1; }
+python -c "import json; d=json.load(open('$OUT/b_${name}_$i.json')); p=d['getScanFiles_phases_ms']; print('$cfg', round(d['ms_per_step'],1), 'open', p['checkpoint_open'], 'io', p['open_read_h2d'], 'prep', p['open_prepare'], 'sizing', p['prep_device_sizing'], 'run', p['device_run'], 'consume', p['consume'], 'close', p['close'], 'dev', round(d['device_step']['ms'],1))"
 done
 done
