@@ -3130,12 +3130,17 @@ struct dk_replay {
   bool have_result = false;
   // every checkpoint file's selection bytes in one pinned block (dk_replay_ckpt_selection_host)
   HBuf h_csel;
+  // grouped runs: the error states (replay, checkpoint) after the tail and after each group, and the
+  // tail's selection bytes, written into pinned memory by a copy kernel before the event (a small
+  // hipMemcpy would queue on the DMA engines behind the groups' selection / mirror copies)
+  HBuf h_zstate, h_zjsel;
   std::vector<int64_t> h_csel_off;
   bool h_csel_ready = false;
   // grouped run (dk_replay_run_grouped): the checkpoint files in n_groups runs, each decoded, probed,
   // filtered and its selections copied to h_csel before the next; grp_ev[g] after group g's copies
   int32_t n_groups = 0;
   std::vector<int32_t> grp_f0;            // first file of each group (n_groups + 1 entries)
+  std::vector<int> prefetch;              // leaves mirrored to the host per group (dk_replay_prefetch_leaf)
   std::vector<hipEvent_t> grp_ev;
   hipEvent_t ev_tail = nullptr;           // after the commit-tail half (its selection is final)
   std::vector<int64_t> grp_row0;          // per group: its files' row prefix, rebased (probe_all)
@@ -3551,6 +3556,14 @@ static int replay_launch(dk_replay* r) {
     R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
     launch_stats_eval(R, r->d_skip.as<DSkipProg>(), r->d_jsel.as<uint8_t>(), st, s);
   }
+  if (r->n_groups > 0 && r->xw == 0 && r->ck) {
+    const int ng = std::max(1, std::min(r->n_groups, (int)r->ck->files.size()));
+    if (r->h_zstate.size() < (size_t)(ng + 1) * 2 * sizeof(DState) && r->h_zstate.alloc((size_t)(ng + 1) * 2 * sizeof(DState))) return 1;
+    if (r->h_zjsel.size() < (size_t)na + 16 && r->h_zjsel.alloc((size_t)na + 16)) return 1;
+    memset(r->h_zstate.data(), 0, 2 * sizeof(DState));
+    launch_copy_zc(r->h_zstate.data(), r->d_state.p, sizeof(DState), s);
+    launch_copy_zc(r->h_zjsel.data(), r->d_jsel.p, na, s);
+  }
   if (!r->ev_tail) HIPOK(hipEventCreateWithFlags(&r->ev_tail, hipEventDisableTiming));
   HIPOK(hipEventRecord(r->ev_tail, s));
   if (r->ck) r->ck->file_done.clear();
@@ -3685,8 +3698,16 @@ static int replay_grouped(dk_replay* r, uint64_t h_nodv) {
       if (r->probe[f].n_rows == 0) memset(r->h_csel.data() + r->h_csel_off[f], 0, n);
       else if (n) HIPOK(hipMemcpyAsync(r->h_csel.data() + r->h_csel_off[f], r->d_csel[f]->p, n, hipMemcpyDeviceToHost, s));
     }
+    {
+      uint8_t* z = r->h_zstate.data() + (size_t)(g + 1) * 2 * sizeof(DState);
+      launch_copy_zc(z, r->d_state.p, sizeof(DState), s);
+      launch_copy_zc(z + sizeof(DState), p->d_state.p, sizeof(DState), s);
+    }
     HIPOK(hipEventRecord(r->grp_ev[g], s));
     for (int f = f0; f < f1; f++) p->file_done[f] = r->grp_ev[g];
+    for (int leaf : r->prefetch)
+      for (int f = f0; f < f1; f++)
+        if (p->colmap[f][leaf] >= 0 && queue_mirror(p, p->colmap[f][leaf])) return 1;
   }
   r->h_csel_ready = true;
   HIPOK(hipEventRecord(r->ev_out, s));   // the checkpoint stream waits for it at dk_replay_sync
@@ -3735,6 +3756,17 @@ extern "C" int dk_replay_run_grouped(dk_replay* r, int32_t n_groups) {
 // Wait until file f's selection (f = -1: the commit tail's) of a grouped run is on the host; a device
 // error seen by then (flags only grow) is reported the way dk_replay_sync reports it, after the whole
 // run (a key-hash collision reruns it). After dk_replay_sync, or for an ungrouped run: the sync.
+extern "C" int dk_replay_prefetch_leaf(dk_replay* r, const char* leaf) {
+  if (!r || !leaf) return fail("dk_replay_prefetch_leaf: null argument");
+  if (!r->ck) return fail("dk_replay_prefetch_leaf: no checkpoint attached");
+  for (size_t li = 0; li < r->ck->leaves.size(); li++)
+    if (r->ck->leaves[li] == leaf) {
+      if (std::find(r->prefetch.begin(), r->prefetch.end(), (int)li) == r->prefetch.end()) r->prefetch.push_back((int)li);
+      return 0;
+    }
+  return fail(std::string("dk_replay_prefetch_leaf: leaf not projected: ") + leaf);
+}
+
 extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
   if (!r) return fail("null replay");
   hipSetDevice(r->eng->cfg.device);
@@ -3750,11 +3782,16 @@ extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
     while (r->grp_f0[g + 1] <= file) g++;
     ev = r->grp_ev[g];
   }
+  int slot = 0;
+  if (file >= 0) {
+    int g = 0;
+    while (r->grp_f0[g + 1] <= file) g++;
+    slot = g + 1;
+  }
   HIPOK(hipEventSynchronize(ev));
   DState st{}, ps{};
-  HIPOK(hipMemcpyAsync(&st, r->d_state.p, sizeof st, hipMemcpyDeviceToHost, r->aux.s));
-  if (r->ck) HIPOK(hipMemcpyAsync(&ps, r->ck->d_state.p, sizeof ps, hipMemcpyDeviceToHost, r->aux.s));
-  HIPOK(hipStreamSynchronize(r->aux.s));
+  memcpy(&st, r->h_zstate.data() + (size_t)slot * 2 * sizeof(DState), sizeof st);
+  memcpy(&ps, r->h_zstate.data() + (size_t)slot * 2 * sizeof(DState) + sizeof(DState), sizeof ps);
   if (st.err_flags || ps.err_flags) return dk_replay_sync(r);
   if (file < 0) r->tail_ready = true;
   else {
@@ -3935,7 +3972,9 @@ extern "C" int dk_replay_json_selection(dk_replay* r, uint8_t* out, int64_t n) {
   if (!r->tail || n != r->tail->rows) return fail("bad selection size");
   memset(out, 0, n);
   std::vector<uint8_t> sel(r->acts.size());
-  if (!sel.empty()) HIPOK(hipMemcpy(sel.data(), r->d_jsel.p, sel.size(), hipMemcpyDeviceToHost));
+  if (!r->have_result && r->tail_ready && r->h_zjsel.size() >= sel.size()) {
+    if (!sel.empty()) memcpy(sel.data(), r->h_zjsel.data(), sel.size());   // grouped run: copied before ev_tail
+  } else if (!sel.empty()) HIPOK(hipMemcpy(sel.data(), r->d_jsel.p, sel.size(), hipMemcpyDeviceToHost));
   for (size_t i = 0; i < sel.size(); i++) if (r->acts[i].kind != JA_REMOVE && sel[i]) out[r->act_row[i]] = 1;
   return 0;
 }

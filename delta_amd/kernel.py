@@ -1078,6 +1078,9 @@ class GpuScan:
     """Scan whose getScanFiles runs decode + reconciliation in libdkgpu (SURVEY.md §8(b) plugin
     point 2)."""
 
+    # leaves mirrored to host memory per decoded group (dk_replay_prefetch_leaf)
+    PREFETCH_LEAVES = ("add.size",)
+
     def __init__(self, snapshot, read_stats=False, shard=None, predicate=None):
         self.snapshot = snapshot
         self.shard = shard
@@ -1293,6 +1296,11 @@ class GpuScan:
         if groups and not exchanging:
             # grouped: batches go out as their group of files is decoded and probed; the counters are
             # final once the iterator is exhausted (ScanImpl's metrics are read after it, too)
+            # add.size (split planning reads it from every scan file) goes to host memory as each
+            # group finishes decoding, not at the consumer's first touch
+            for leaf in self.PREFETCH_LEAVES:
+                if leaf in self.ckpt.leaves:
+                    check(lib().dk_replay_prefetch_leaf(self._rh, leaf.encode()))
             check(lib().dk_replay_run_grouped(self._rh, groups))
             check(lib().dk_replay_wait_file(self._rh, -1))
             self.prepare_ms["device_run"] = (time.perf_counter() - t0) * 1e3

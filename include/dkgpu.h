@@ -338,6 +338,12 @@ int  dk_replay_run(dk_replay* r);                      /* async: key build, prob
  * device error seen by a wait is reported after the whole run, as dk_replay_sync reports it. */
 int  dk_replay_run_grouped(dk_replay* r, int32_t n_groups);
 int  dk_replay_wait_file(dk_replay* r, int32_t file);
+/* Grouped runs: also copy projected leaf `leaf` of each group's files to host memory as soon as the
+ * group is decoded (the pinned mirror dk_parquet_column hands out), instead of at the consumer's
+ * first touch -- for the columns every consumer of the scan files reads (Scan.getScanFiles' callers
+ * read add.size for split planning: BenchmarkParallelCheckpointReading.java:124-135). Call after the
+ * checkpoint is attached, before dk_replay_run_grouped. */
+int  dk_replay_prefetch_leaf(dk_replay* r, const char* leaf);
 int  dk_replay_sync(dk_replay* r);
 /* counters: addFilesSeen, addFilesSeenFromDeltaFiles, activeAddFiles, duplicateAddFiles,
  * removeFilesSeenFromDeltaFiles */
