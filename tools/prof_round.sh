@@ -14,7 +14,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-
 i=0
 for pass in "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -s KILL 200 rocprofv3 --pmc $pass --output-format csv -d $OUT/p$i -o k -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --workdir $WORK "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i ($pass) failed"; tail -5 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 200 rocprofv3 --pmc $pass --output-format csv -d $OUT/p$i -o k -- python3 $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --device-steps 2 --no-cpu-baseline --workdir $WORK "$@" > $OUT/p$i.log 2>&1 || { echo "pass $i ($pass) failed"; tail -5 $OUT/p$i.log; exit 1; }
 done
 find $OUT -name "*.csv" -size +30M -delete
 echo done
