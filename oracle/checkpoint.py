@@ -9,6 +9,11 @@
 Independent of the product: commit lines are read here, keys come from the oracle's own
 java.net.URI restatement (ref.json_key) and checkpoint rows from the C decoder. Output: the selected
 rows in iterator order as canonical (action, tuple) pairs (see canon()), and the add count.
+
+Parity unpinned: /root/reference holds no checkpoint written by Kernel's CreateCheckpointIterator (no
+golden output to compare with), so this restatement is checked on hand-made logs and through round
+trips (the written file read back by pyarrow, the table re-read through the new checkpoint), not
+against a reference-produced vector.
 """
 import json
 import os
