@@ -89,7 +89,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_exchange_finish", "dk_json_pm_decode",
            "dk_ckpt_writer_open", "dk_ckpt_writer_add_json", "dk_ckpt_writer_add_checkpoint_adds", "dk_ckpt_writer_close",
            "dk_json_tail_column", "dk_json_tail_free", "dk_replay_create", "dk_replay_set_skipping", "dk_replay_set_partition_filter", "dk_replay_run",
-           "dk_replay_run_grouped", "dk_replay_wait_file", "dk_replay_prefetch_leaf",
+           "dk_replay_run_grouped", "dk_replay_wait_file", "dk_replay_prefetch_leaf", "dk_parquet_open_async",
            "dk_replay_sync",
            "dk_replay_counters", "dk_replay_counters_split", "dk_replay_json_selection", "dk_replay_ckpt_selection",
            "dk_replay_kernel_stats", "dk_replay_free", "dk_parquet_open_rg", "dk_parquet_row_groups",
@@ -160,6 +160,7 @@ def lib(build_if_missing=True):
         "dk_replay_run": (C.c_int, [P]), "dk_replay_sync": (C.c_int, [P]),
         "dk_replay_run_grouped": (C.c_int, [P, C.c_int32]), "dk_replay_wait_file": (C.c_int, [P, C.c_int32]),
         "dk_replay_prefetch_leaf": (C.c_int, [P, C.c_char_p]),
+        "dk_parquet_open_async": (C.c_int, [P, C.POINTER(C.c_char_p), I32, C.POINTER(C.c_char_p), I32, P, P, C.POINTER(P)]),
         "dk_replay_counters": (C.c_int, [P, C.POINTER(I64)]),
         "dk_replay_counters_split": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
         "dk_replay_json_selection": (C.c_int, [P, P, I64]),

@@ -14,6 +14,9 @@
 #include <memory>
 #include <mutex>
 #include <thread>
+#include <condition_variable>
+#include <functional>
+#include <future>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -915,6 +918,29 @@ struct dk_parquet {
   // pipeline run only re-runs the scans (sentinels into the freshly allocated outputs), the string
   // copy and the value decode (a getScanFiles that runs once decodes each page once)
   bool fresh = false;
+  // the prepare pass also decoded every column, slice by slice as the files landed: the next full
+  // run skips the decode pipeline (value decode included) once; skip_decode: that run is under way
+  // (a grouped replay's per-group decode_cols calls are no-ops)
+  bool decoded_fresh = false, skip_decode = false;
+  // asynchronous open (dk_parquet_open_async): the opening thread keeps reading, sizing and decoding
+  // after the handle is returned; files [0, files_ready) have final columns and a decode event
+  // (file_dec) by then. open_state: 0 running, 1 done, 2 failed (open_err).
+  std::thread opener;
+  std::atomic<int> open_state{1};
+  std::string open_err;
+  std::mutex rmu;
+  std::condition_variable rcv;
+  int files_ready = INT_MAX;
+  std::vector<hipEvent_t> file_dec;  // per file (events owned by dec_events)
+  std::vector<hipEvent_t> dec_events;
+  StreamH mir;                       // host-mirror copies (not behind the open's passes on `stream`)
+  hipEvent_t mir_ev = nullptr;
+  bool async_open = false;
+  ~dk_parquet() {
+    if (opener.joinable()) opener.join();
+    for (hipEvent_t e : dec_events) hipEventDestroy(e);
+    if (mir_ev) hipEventDestroy(mir_ev);
+  }
 };
 
 static int upload(DBuf& d, const void* src, size_t n, hipStream_t s) {
@@ -1033,7 +1059,7 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
 // the value decode of columns [c0, c1) (every column of a run of files): string copies first -- they
 // fill the key column's per-value hashes that k_tile_decode forwards -- then the level / value tiles
 static void decode_cols(dk_parquet* p, hipStream_t s, int c0, int c1) {
-  if (c1 <= c0) return;
+  if (c1 <= c0 || p->skip_decode) return;
   KTimer& T = p->timer;
   const DChunk* C = p->d_chunks.as<DChunk>();
   DPage* P = p->d_pages.as<DPage>();
@@ -1080,6 +1106,13 @@ static int run_pipeline(dk_parquet* p, int mode, hipStream_t s = nullptr, bool f
   DState* st = p->d_state.as<DState>();
   DColumn* cols = p->d_cols.as<DColumn>();
   DTile* LT = p->d_ltiles.as<DTile>();
+  p->skip_decode = false;
+  if (mode == 1 && p->decoded_fresh) {   // prepare decoded everything already (per slice)
+    p->decoded_fresh = false;
+    p->fresh = false;
+    p->skip_decode = true;
+    return 0;
+  }
   const bool reuse = mode == 1 && p->fresh;
   p->fresh = false;
   if (reuse) {                         // headers, snappy, runs, counts, positions, chars: done by prepare
@@ -1147,6 +1180,109 @@ static int upload_zc(dk_parquet* p, DBuf& d, const void* src, size_t n, hipStrea
   return 0;
 }
 
+// String-copy tiles of columns [c0, c1) (appended; col_tile0 gets one entry per column) and the
+// staging size they need (p->copy_cb: the running max over calls; page counts must be final)
+static void build_tiles(dk_parquet* p, int c0, int c1, std::vector<int2>& tiles) {
+  const int base = p->col_tile0.back() - (int)tiles.size();   // tiles of earlier calls already counted
+  // staging buffer: the busiest PLAIN page's mean span of DK_COPY_TILE values (+5%), so a typical
+  // tile is one pass while the two buffers stay small enough for high occupancy
+  double span = 0;
+  for (int ci = c0; ci < c1; ci++) {
+    const DColumn& c = p->h_cols[ci];
+    if (c.phys != PT_BYTE_ARRAY) continue;
+    for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
+      const DPage& pg = p->h_pages[pi];
+      if ((pg.flags & PF_DICT) || pg.enc != ENC_PLAIN || pg.n_values <= 0) continue;
+      span = std::max(span, (double)pg.vbytes / pg.n_values * DK_COPY_TILE * 1.05 + 64);
+    }
+  }
+  p->copy_cb = std::max(p->copy_cb, span > 0 ? (int)span : 16384);
+  for (int ci = c0; ci < c1; ci++) {
+    const DColumn& c = p->h_cols[ci];
+    for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
+      const DPage& pg = p->h_pages[pi];
+      if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN) continue;
+      for (int v0 = 0; v0 < pg.n_values; v0 += DK_COPY_TILE) tiles.push_back(make_int2(pi, v0));
+    }
+    // key column: its dictionary pages are hashed entry by entry (hash-only tiles)
+    if (c.key_hash && c.phys == PT_BYTE_ARRAY && c.max_rep == 0)
+      for (const DChunk& ck : p->h_chunks)
+        if (ck.col == ci && ck.dict_page >= 0)
+          for (int v0 = 0; v0 < p->h_pages[ck.dict_page].num_values; v0 += DK_COPY_TILE)
+            tiles.push_back(make_int2(ck.dict_page, v0));
+    p->col_tile0.push_back(base + (int)tiles.size());
+  }
+}
+
+// Output buffers of columns [c0, c1) carved from one new device arena (one hipMalloc instead of ~3
+// per (file, leaf) -- thousands at C3's 64 files x 21 leaves); pass 0 sizes the arena, pass 1 hands
+// out the pointers. got[ci]: the device column after the sizing scans (entry / char totals).
+static int alloc_outputs(dk_parquet* p, int c0, int c1, const std::vector<DColumn>& got) {
+  size_t arena_bytes = 0;
+  for (int pass = 0; pass < 2; pass++) {
+  if (pass == 1) {
+    p->outbufs.emplace_back(new DBuf());
+    if (p->outbufs.back()->alloc(arena_bytes + 256)) return 1;
+  }
+  uint8_t* const arena_base = pass == 1 ? p->outbufs.back()->as<uint8_t>() : nullptr;
+  size_t arena_at = 0;
+  for (int i = c0; i < c1; i++) {
+    DColumn& c = p->h_cols[i];
+    c.n_entries = got[i].n_entries;
+    c.n_chars = got[i].n_chars;
+    c.cap_entries = c.n_entries;
+    c.cap_chars = c.n_chars;
+    int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
+    auto mk = [&](size_t bytes) -> void* {
+      const size_t at = arena_at;
+      arena_at += (bytes + 16 + 255) & ~(size_t)255;     // 256-byte aligned, 16 bytes of slack each
+      if (pass == 1) p->bytes_written += bytes;
+      return pass == 1 ? (void*)(arena_base + at) : (void*)(uintptr_t)(at + 256);   // pass 0: non-null
+    };
+    int64_t n_values = 0;
+    for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) n_values += p->h_pages[pi].n_values;
+    c.null_only = (n_values == 0 && (c.max_rep == 0 || c.n_entries == 0)) ? 1 : 0;
+    c.row_def = (uint8_t*)mk(c.n_rows);
+    c.vhash = c.hash = c.dhash = nullptr;
+    if (c.key_hash && !c.null_only && c.phys == PT_BYTE_ARRAY && c.max_rep == 0) {
+      int64_t dn = 0;        // dictionary entries of the column's chunks
+      for (DChunk& ck : p->h_chunks)
+        if (ck.col == i && ck.dict_page >= 0) { ck.dict_hash_off = dn; dn += p->h_pages[ck.dict_page].num_values; }
+      if (dn) {
+        c.dhash = (uint64_t*)mk(dn * 8);
+        if (pass == 1) p->bytes_written -= dn * 8;               // scratch
+        if (!c.dhash) return 1;
+      }
+      c.vhash = (uint64_t*)mk((n_values + 1) * 8);
+      if (pass == 1) p->bytes_written -= (n_values + 1) * 8;     // scratch, not an output (written + re-read once)
+      c.hash = (uint64_t*)mk(c.n_rows * 8);
+      if (!c.vhash || !c.hash) return 1;
+    }
+    c.row_offs = (c.max_rep > 0 && !c.null_only) ? (int64_t*)mk((c.n_rows + 1) * 8) : nullptr;
+    c.entry_def = (c.max_rep > 0 && !c.null_only) ? (uint8_t*)mk(nv) : nullptr;
+    c.fixed = nullptr; c.offs = nullptr; c.chars = nullptr;
+    if (!c.null_only) {
+      if (c.phys == PT_BYTE_ARRAY) {
+        c.offs = (int64_t*)mk((nv + 1) * 8);
+        c.chars = (uint8_t*)mk(c.n_chars);
+      } else {
+        c.fixed = (uint8_t*)mk(nv * c.width);
+      }
+    }
+    if (!c.row_def) return 1;
+  }
+  arena_bytes = arena_at;
+  }
+  return 0;
+}
+
+// Per-slice output allocation + value decode inside the open (DK_SLICE_DECODE=1; off by default
+// until measured on the GPU): the prerequisite of dk_parquet_open_async's overlap
+static bool slice_decode_on() {
+  static const bool on = getenv("DK_SLICE_DECODE") && atoi(getenv("DK_SLICE_DECODE")) != 0;
+  return on;
+}
+
 // Wait until file f's image copies are queued (file_ev recorded: a stream may wait for it; an event
 // that was never recorded would let it through at once). False: the file's read failed.
 static bool wait_queued(const dk_parquet* p, int f) {
@@ -1156,6 +1292,89 @@ static bool wait_queued(const dk_parquet* p, int f) {
   return v == 1;
 }
 static bool is_queued(const dk_parquet* p, int f) { return !p->queued || p->queued[f].load(std::memory_order_acquire) == 1; }
+
+static int check_state(dk_parquet* p);
+
+// upload_zc to dst (device memory of any buffer, any offset)
+static int upload_zc_to(dk_parquet* p, void* dst, const void* src, size_t n, hipStream_t s) {
+  if (!n) return 0;
+  HBuf hb;
+  if (hb.alloc(n)) return 1;
+  memcpy(hb.data(), src, n);
+  launch_copy_zc(dst, hb.data(), (long long)n, s);
+  p->staging.push_back(std::move(hb));
+  return 0;
+}
+
+// A sized slice whose outputs are still to be allocated: its columns and pages come back to pinned
+// memory through a copy kernel (a D2H copy would wait behind the H2D copies of the later files).
+struct SizedSlice {
+  PRange R;
+  int f0 = 0, f1 = 0;
+  hipStream_t cs = nullptr;
+  hipEvent_t ev = nullptr;
+  HBuf cols, pages;
+};
+
+// After a slice's sizing passes: page status, string-copy tiles, output arena, the scans again (the
+// sentinels into the new outputs) and the value decode of its columns, on its stream.
+static int finish_slice(dk_parquet* p, SizedSlice& S, std::vector<DColumn>& got) {
+  const PRange& R = S.R;
+  HIPOK(hipEventSynchronize(S.ev));
+  hipEventDestroy(S.ev);
+  S.ev = nullptr;
+  memcpy(got.data() + R.col0, S.cols.data(), (size_t)(R.col1 - R.col0) * sizeof(DColumn));
+  memcpy(p->h_pages.data() + R.pa, S.pages.data(), (size_t)(R.pb - R.pa) * sizeof(DPage));
+  for (int pi = R.pa; pi < R.pb; pi++)
+    if (p->h_pages[pi].status != PS_OK) {
+      std::vector<DPage> one(1, p->h_pages[pi]);
+      return fail(page_status_msg(p, one));
+    }
+  std::vector<int2> tiles;
+  const int t0 = p->col_tile0.back();
+  build_tiles(p, R.col0, R.col1, tiles);
+  if ((size_t)(t0 + tiles.size()) * sizeof(int2) > p->d_tiles.n) return fail("internal: string-copy tile bound exceeded");
+  if (upload_zc_to(p, p->d_tiles.as<int2>() + t0, tiles.data(), tiles.size() * sizeof(int2), S.cs)) return 1;
+  if (alloc_outputs(p, R.col0, R.col1, got)) return 1;
+  if (upload_zc_to(p, p->d_cols.as<DColumn>() + R.col0, p->h_cols.data() + R.col0, (size_t)(R.col1 - R.col0) * sizeof(DColumn), S.cs))
+    return 1;
+  int k0 = (int)p->h_chunks.size(), k1 = 0;        // the slice's chunks (dict_hash_off)
+  for (int k = 0; k < (int)p->h_chunks.size(); k++)
+    if (p->h_chunks[k].col >= R.col0 && p->h_chunks[k].col < R.col1) { k0 = std::min(k0, k); k1 = k + 1; }
+  if (k1 > k0 && upload_zc_to(p, p->d_chunks.as<DChunk>() + k0, p->h_chunks.data() + k0, (size_t)(k1 - k0) * sizeof(DChunk), S.cs))
+    return 1;
+  KTimer& T = p->timer;
+  DColumn* cols = p->d_cols.as<DColumn>();
+  { KTimer::Scope sc(&T, 3, S.cs); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, p->d_pages.as<DPage>(), p->d_ltiles.as<DTile>(), p->d_state.as<DState>(), S.cs); }
+  { KTimer::Scope sc(&T, 3, S.cs); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, p->d_pages.as<DPage>(), p->d_ltiles.as<DTile>(), p->d_state.as<DState>(), S.cs); }
+  decode_cols(p, S.cs, R.col0, R.col1);
+  hipEvent_t dev = nullptr;                       // the slice's files are decoded after this
+  HIPOK(hipEventCreateWithFlags(&dev, hipEventDisableTiming));
+  HIPOK(hipEventRecord(dev, S.cs));
+  p->dec_events.push_back(dev);
+  {
+    std::lock_guard<std::mutex> g(p->rmu);
+    if (p->file_dec.size() < p->files.size()) p->file_dec.resize(p->files.size(), nullptr);
+    for (int f = S.f0; f < S.f1; f++) p->file_dec[f] = dev;
+    if (p->files_ready != INT_MAX) p->files_ready = S.f1;
+  }
+  p->rcv.notify_all();
+  return 0;
+}
+
+// Asynchronous opens: wait until files [0, f1) are decoded (their columns final, file_dec recorded)
+static int wait_files(dk_parquet* p, int f1) {
+  std::unique_lock<std::mutex> lk(p->rmu);
+  p->rcv.wait(lk, [&] { return p->files_ready >= f1 || p->open_state.load() != 0; });
+  if (p->files_ready >= f1 || p->open_state.load() == 1) return 0;
+  return fail(p->open_err);
+}
+// ... until the whole open has finished (joined); its error, if any
+static int ensure_open(dk_parquet* p) {
+  if (p->opener.joinable() && p->opener.get_id() != std::this_thread::get_id()) p->opener.join();
+  if (p->open_state.load() == 2) return fail(p->open_err);
+  return 0;
+}
 
 static int prepare(dk_parquet* p) {
   hipStream_t s = p->stream;
@@ -1314,6 +1533,8 @@ static int prepare(dk_parquet* p) {
   }
   p->open_ms[4] = since(t1);            // host: page tables, scratch sizing and allocation
   const auto t2 = clk::now();
+  bool per_slice = false;                // outputs allocated and values decoded slice by slice
+  std::vector<DColumn> got(p->h_cols.size());
   // the sizing passes, one slice of files at a time, each as soon as its files' images have landed
   // (the later files' H2D copies overlap the earlier slices' snappy / level passes); page mode is
   // never sliced. Adaptive (default): a slice is every file whose image has landed by the time the
@@ -1331,6 +1552,27 @@ static int prepare(dk_parquet* p) {
     const int64_t target = std::max<int64_t>(1, total / slices);
     int f0 = 0;
     int64_t acc = 0;
+    per_slice = adaptive && slices > 1 && slice_decode_on();
+    std::vector<SizedSlice> sized;
+    if (per_slice) {
+      // string-copy tiles: a bound from the headers (PLAIN byte-array data pages and key-column
+      // dictionary pages, num_values >= the values the count pass finds)
+      int64_t nt = 0;
+      for (const DColumn& c : p->h_cols) {
+        if (c.phys != PT_BYTE_ARRAY) continue;
+        for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
+          const DPage& pg = p->h_pages[pi];
+          if (!(pg.flags & PF_DICT) && pg.enc == ENC_PLAIN) nt += (std::max(pg.num_values, 0) + DK_COPY_TILE - 1) / DK_COPY_TILE;
+        }
+      }
+      for (const DChunk& ck : p->h_chunks)
+        if (ck.dict_page >= 0 && p->h_cols[ck.col].key_hash && p->h_cols[ck.col].phys == PT_BYTE_ARRAY && p->h_cols[ck.col].max_rep == 0)
+          nt += (std::max(p->h_pages[ck.dict_page].num_values, 0) + DK_COPY_TILE - 1) / DK_COPY_TILE;
+      if (p->d_tiles.alloc((size_t)(nt + 1) * sizeof(int2))) return 1;
+      p->col_tile0.assign(1, 0);
+      p->copy_cb = 0;
+      p->bytes_written = 0;
+    }
     if (adaptive && slices > 1) {
       // slices touch disjoint pages / segments / tiles / columns: they rotate over up to three
       // streams (DK_OPEN_STREAMS), so one slice's latency tail (k_snap_fix / k_snap_frag's longest
@@ -1363,8 +1605,30 @@ static int prepare(dk_parquet* p) {
         if (verbose) fprintf(stderr, "[dk] sizing slice %d: files [%d, %d) %.1f MB queued at %.1f ms\n", slice - 1, f0, f1,
                              acc / 1e6, since(p->t_open0));
         for (int f = f0; f < f1; f++) HIPOK(hipStreamWaitEvent(cs, p->file_ev[f], 0));
-        sizing_stages(p, cs, file_range(p, f0, f1));
+        const PRange R = file_range(p, f0, f1);
+        sizing_stages(p, cs, R);
+        if (per_slice) {
+          // the slice's columns / pages back to pinned memory, then (one slice later, when its passes
+          // have had the next files' landing time to run) its outputs and value decode
+          SizedSlice S;
+          S.R = R; S.cs = cs; S.f0 = f0; S.f1 = f1;
+          if (S.cols.alloc((size_t)(R.col1 - R.col0) * sizeof(DColumn) + 16) || S.pages.alloc((size_t)(R.pb - R.pa) * sizeof(DPage) + 16))
+            return 1;
+          launch_copy_zc(S.cols.data(), p->d_cols.as<DColumn>() + R.col0, (long long)(R.col1 - R.col0) * sizeof(DColumn), cs);
+          launch_copy_zc(S.pages.data(), p->d_pages.as<DPage>() + R.pa, (long long)(R.pb - R.pa) * sizeof(DPage), cs);
+          HIPOK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
+          HIPOK(hipEventRecord(S.ev, cs));
+          sized.push_back(std::move(S));
+          while (sized.size() > 1) {
+            if (finish_slice(p, sized.front(), got)) return 1;
+            sized.erase(sized.begin());
+          }
+        }
         f0 = f1;
+      }
+      while (!sized.empty()) {
+        if (finish_slice(p, sized.front(), got)) return 1;
+        sized.erase(sized.begin());
       }
       for (int k = 1; k < nss; k++) {               // `s` waits for the side streams' slices
         HIPOK(hipEventRecord(tables, ss[k]));
@@ -1384,118 +1648,46 @@ static int prepare(dk_parquet* p) {
       }
     }
   }
-  std::vector<DColumn> got(p->h_cols.size());
-  HIPOK(hipMemcpyAsync(got.data(), p->d_cols.p, got.size() * sizeof(DColumn), hipMemcpyDeviceToHost, s));
-  HIPOK(hipMemcpyAsync(p->h_pages.data(), p->d_pages.p, p->h_pages.size() * sizeof(DPage), hipMemcpyDeviceToHost, s));
+  if (!per_slice) {
+    HIPOK(hipMemcpyAsync(got.data(), p->d_cols.p, got.size() * sizeof(DColumn), hipMemcpyDeviceToHost, s));
+    HIPOK(hipMemcpyAsync(p->h_pages.data(), p->d_pages.p, p->h_pages.size() * sizeof(DPage), hipMemcpyDeviceToHost, s));
+  }
   HIPOK(hipStreamSynchronize(s));
   std::string m = page_status_msg(p, p->h_pages);
   if (!m.empty()) return fail(m);
   p->open_ms[5] = since(t2);            // sizing passes on the device (snappy, runs, counts, positions)
   if (getenv("DK_VERBOSE")) fprintf(stderr, "[dk] sizing done at %.1f ms\n", since(p->t_open0));
   const auto t3 = clk::now();
-  // 3. string-copy tile table (page counts are final after the count pass)
-  {
+  // 3. string-copy tile table (page counts are final after the count pass), 4. output arena
+  if (!per_slice) {
     std::vector<int2> tiles;
     p->col_tile0.assign(1, 0);
-    // staging buffer: the busiest PLAIN page's mean span of DK_COPY_TILE values (+5%), so a typical
-    // tile is one pass while the two buffers stay small enough for high occupancy
-    double span = 0;
-    for (const DPage& pg : p->h_pages) {
-      const DChunk& ck = p->h_chunks[pg.chunk];
-      if (ck.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN || pg.n_values <= 0) continue;
-      span = std::max(span, (double)pg.vbytes / pg.n_values * DK_COPY_TILE * 1.05 + 64);
-    }
-    p->copy_cb = span > 0 ? (int)span : 16384;
-    for (size_t ci = 0; ci < p->h_cols.size(); ci++) {
-      const DColumn& c = p->h_cols[ci];
-      for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
-        const DPage& pg = p->h_pages[pi];
-        if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN) continue;
-        for (int v0 = 0; v0 < pg.n_values; v0 += DK_COPY_TILE) tiles.push_back(make_int2(pi, v0));
-      }
-      // key column: its dictionary pages are hashed entry by entry (hash-only tiles)
-      if (c.key_hash && c.phys == PT_BYTE_ARRAY && c.max_rep == 0)
-        for (const DChunk& ck : p->h_chunks)
-          if (ck.col == (int)ci && ck.dict_page >= 0)
-            for (int v0 = 0; v0 < p->h_pages[ck.dict_page].num_values; v0 += DK_COPY_TILE)
-              tiles.push_back(make_int2(ck.dict_page, v0));
-      p->col_tile0.push_back((int)tiles.size());
-    }
+    p->copy_cb = 0;
+    p->bytes_written = 0;
+    build_tiles(p, 0, (int)p->h_cols.size(), tiles);
     if (upload(p->d_tiles, tiles.data(), tiles.size() * sizeof(int2), s)) return 1;
+    if (alloc_outputs(p, 0, (int)p->h_cols.size(), got)) return 1;
   }
-  // 4. allocate outputs: every output buffer of every column is carved from one device arena (one
-  // hipMalloc instead of ~3 per (file, leaf) -- thousands at C3's 64 files x 21 leaves); pass 0
-  // sizes the arena, pass 1 hands out the pointers
-  size_t arena_bytes = 0;
-  for (int pass = 0; pass < 2; pass++) {
-  if (pass == 1) {
-    p->outbufs.emplace_back(new DBuf());
-    if (p->outbufs.back()->alloc(arena_bytes + 256)) return 1;
+  if (!per_slice) {
+    if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
+    if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;   // dict_hash_off
   }
-  uint8_t* const arena_base = pass == 1 ? p->outbufs.back()->as<uint8_t>() : nullptr;
-  size_t arena_at = 0;
-  p->bytes_written = 0;
-  for (size_t i = 0; i < p->h_cols.size(); i++) {
-    DColumn& c = p->h_cols[i];
-    c.n_entries = got[i].n_entries;
-    c.n_chars = got[i].n_chars;
-    c.cap_entries = c.n_entries;
-    c.cap_chars = c.n_chars;
-    int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
-    auto mk = [&](size_t bytes) -> void* {
-      const size_t at = arena_at;
-      arena_at += (bytes + 16 + 255) & ~(size_t)255;     // 256-byte aligned, 16 bytes of slack each
-      p->bytes_written += bytes;
-      return pass == 1 ? (void*)(arena_base + at) : (void*)(uintptr_t)(at + 256);   // pass 0: non-null
-    };
-    int64_t n_values = 0;
-    for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) n_values += p->h_pages[pi].n_values;
-    c.null_only = (n_values == 0 && (c.max_rep == 0 || c.n_entries == 0)) ? 1 : 0;
-    c.row_def = (uint8_t*)mk(c.n_rows);
-    c.vhash = c.hash = c.dhash = nullptr;
-    if (c.key_hash && !c.null_only && c.phys == PT_BYTE_ARRAY && c.max_rep == 0) {
-      int64_t dn = 0;        // dictionary entries of the column's chunks
-      for (DChunk& ck : p->h_chunks)
-        if (ck.col == (int)i && ck.dict_page >= 0) { ck.dict_hash_off = dn; dn += p->h_pages[ck.dict_page].num_values; }
-      if (dn) {
-        c.dhash = (uint64_t*)mk(dn * 8);
-        p->bytes_written -= dn * 8;               // scratch
-        if (!c.dhash) return 1;
-      }
-      c.vhash = (uint64_t*)mk((n_values + 1) * 8);
-      p->bytes_written -= (n_values + 1) * 8;     // scratch, not an output (written + re-read once)
-      c.hash = (uint64_t*)mk(c.n_rows * 8);
-      if (!c.vhash || !c.hash) return 1;
-    }
-    c.row_offs = (c.max_rep > 0 && !c.null_only) ? (int64_t*)mk((c.n_rows + 1) * 8) : nullptr;
-    c.entry_def = (c.max_rep > 0 && !c.null_only) ? (uint8_t*)mk(nv) : nullptr;
-    c.fixed = nullptr; c.offs = nullptr; c.chars = nullptr;
-    if (!c.null_only) {
-      if (c.phys == PT_BYTE_ARRAY) {
-        c.offs = (int64_t*)mk((nv + 1) * 8);
-        c.chars = (uint8_t*)mk(c.n_chars);
-      } else {
-        c.fixed = (uint8_t*)mk(nv * c.width);
-      }
-    }
-    if (!c.row_def) return 1;
-  }
-  arena_bytes = arena_at;
-  }
-  if (upload(p->d_cols, p->h_cols.data(), p->h_cols.size() * sizeof(DColumn), s)) return 1;
-  if (upload(p->d_chunks, p->h_chunks.data(), p->h_chunks.size() * sizeof(DChunk), s)) return 1;   // dict_hash_off
   HIPOK(hipStreamSynchronize(s));
+  if (per_slice && check_state(p)) return 1;   // decode errors of the per-slice value decode
   {
     SyncedRelease drained;              // the zero-copy sources have been read
     p->staging.clear();
   }
   p->open_ms[6] = since(t3);            // host: tile tables + output arena
-  p->host.clear();
-  p->host.resize(p->h_cols.size());
+  if (!p->async_open) {                 // (an asynchronous open's mirrors are in use already)
+    p->host.clear();
+    p->host.resize(p->h_cols.size());
+  }
   p->slice.assign(p->h_cols.size(), HostCol());
   p->prepared = true;
   static const bool no_reuse = getenv("DK_NO_PREPARE_REUSE") && atoi(getenv("DK_NO_PREPARE_REUSE"));
   p->fresh = !no_reuse;
+  p->decoded_fresh = per_slice && !no_reuse;
   return 0;
 }
 
@@ -1839,7 +2031,7 @@ extern "C" int dk_parquet_open(dk_engine* e, const char* const* paths, int32_t n
 
 static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
-                        const int32_t* field_ids = nullptr);
+                        const int32_t* field_ids = nullptr, const std::function<void(dk_parquet*)>* publish = nullptr);
 
 // fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads
 template <class F>
@@ -1960,7 +2152,7 @@ static int build_file_meta(const dk_parquet* p, int fi, const FileM& f, const st
 
 static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
-                        const int32_t* field_ids) {
+                        const int32_t* field_ids, const std::function<void(dk_parquet*)>* publish) {
   if (!e) return fail("null engine");
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_parquet> p(new dk_parquet());
@@ -2161,12 +2353,34 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->n_pages = (int)p->h_pages.size();
   p->n_cols = (int)p->h_cols.size();
   const auto t_h2d = std::chrono::steady_clock::now();
+  // asynchronous open: the caller gets the handle now (the tables are final); reads, sizing and the
+  // per-slice decode go on here, files becoming ready slice by slice (wait_files)
+  bool published = false;
+  auto failed = [&](int rc) -> int {
+    if (!published) return rc;
+    {
+      std::lock_guard<std::mutex> g(p->rmu);
+      p->open_err = g_err;
+      p->open_state.store(2);
+    }
+    p->rcv.notify_all();
+    p.release();                                  // the caller owns it
+    return rc;
+  };
+  if (publish) {
+    p->async_open = true;
+    p->host.resize(p->h_cols.size());            // column mirrors (queued per file as files get ready)
+    p->files_ready = 0;
+    p->open_state.store(0);
+    (*publish)(p.get());
+    published = true;
+  }
   if (prepare(p.get())) {
     const std::string perr = g_err;
-    if (read_errors()) return 1;                 // a failed read is the error to report
-    return fail(perr);
+    if (read_errors()) return failed(1);         // a failed read is the error to report
+    return failed(fail(perr));
   }
-  if (reader.joinable() && read_errors()) return 1;
+  if (reader.joinable() && read_errors()) return failed(1);
   p->queued.reset();
   {
     const auto t_end = std::chrono::steady_clock::now();
@@ -2180,12 +2394,76 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
               n_files, nb / 1e6, p->open_ms[0], p->open_ms[1], p->open_ms[2]);
     }
   }
+  if (published) {
+    {
+      std::lock_guard<std::mutex> g(p->rmu);
+      p->files_ready = INT_MAX;
+      p->open_state.store(1);
+    }
+    p->rcv.notify_all();
+    p.release();
+    return 0;
+  }
   *out = p.release();
+  return 0;
+}
+
+// The asynchronous form of dk_parquet_open_sel: returns once the footers, page headers and tables
+// are read (num_rows / row_offset answer at once); the chunk reads, sizing passes and value decode
+// continue on a thread of the handle, files becoming ready slice by slice. Every other call on the
+// handle waits for what it needs (dk_parquet_column: its file; the rest: the whole open).
+extern "C" int dk_parquet_open_async(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
+                                     int32_t n_leaves, const int32_t* rg_count, const int32_t* rg_list, dk_parquet** out) {
+  *out = nullptr;
+  const bool slice_decode = slice_decode_on() &&
+                            !(getenv("DK_OPEN_ADAPTIVE") && atoi(getenv("DK_OPEN_ADAPTIVE")) == 0) &&
+                            !(getenv("DK_SNAPPY_MODE") && !strcmp(getenv("DK_SNAPPY_MODE"), "page")) &&
+                            !(getenv("DK_ASYNC_OPEN") && atoi(getenv("DK_ASYNC_OPEN")) == 0) &&
+                            !(getenv("DK_OPEN_SLICES") && atoi(getenv("DK_OPEN_SLICES")) <= 1);
+  if (!slice_decode) return dk_parquet_open_sel(e, paths, n_files, leaves, n_leaves, rg_count, rg_list, out);
+  std::vector<std::vector<int32_t>> groups(n_files > 0 ? n_files : 0);
+  bool all = true;
+  if (rg_count) {
+    for (int32_t fi = 0, at = 0; fi < n_files; fi++) {
+      if (rg_count[fi] < 0) {
+        FileM f;
+        f.path = paths[fi];
+        if (read_footer(f) || parse_footer(f)) return 1;
+        for (int32_t g = 0; g < (int32_t)f.rgs.size(); g++) groups[fi].push_back(g);
+        continue;
+      }
+      all = false;
+      for (int32_t k = 0; k < rg_count[fi]; k++) groups[fi].push_back(rg_list[at + k]);
+      at += rg_count[fi];
+    }
+  }
+  std::promise<dk_parquet*> handed;
+  std::future<dk_parquet*> got = handed.get_future();
+  std::string early_err;
+  std::function<void(dk_parquet*)> publish = [&](dk_parquet* q) { handed.set_value(q); };
+  const std::vector<std::vector<int32_t>>* gp = (rg_count && !all) ? &groups : nullptr;
+  std::thread t([&, gp] {
+    dk_parquet* q = nullptr;
+    bool pub = false;
+    std::function<void(dk_parquet*)> pub_fn = [&](dk_parquet* x) { pub = true; publish(x); };
+    if (parquet_open(e, paths, n_files, leaves, n_leaves, gp, &q, nullptr, &pub_fn) && !pub) {
+      early_err = g_err;
+      handed.set_value(nullptr);
+    }
+  });
+  dk_parquet* p = got.get();
+  if (!p) {
+    t.join();
+    return fail(early_err);
+  }
+  p->opener = std::move(t);
+  *out = p;
   return 0;
 }
 
 static int invalidate_mirrors(dk_parquet* p);
 extern "C" int dk_parquet_decode(dk_parquet* p) {
+  if (ensure_open(p)) return 1;
   hipSetDevice(p->eng->cfg.device);
   DState st0{};
   st0.err_row = LLONG_MAX;
@@ -2208,6 +2486,7 @@ static int check_state(dk_parquet* p) {
 }
 
 extern "C" int dk_parquet_sync(dk_parquet* p) {
+  if (ensure_open(p)) return 1;
   hipSetDevice(p->eng->cfg.device);   // this thread may not have used the device yet
   HIPOK(hipStreamSynchronize(p->stream));
   p->timer.collect();
@@ -2225,17 +2504,20 @@ extern "C" int64_t dk_parquet_row_offset(dk_parquet* p, int32_t file) {
 }
 
 extern "C" int dk_parquet_open_ms(dk_parquet* p, double out[7]) {
+  if (ensure_open(p)) return 1;
   for (int i = 0; i < 7; i++) out[i] = p->open_ms[i];
   return 0;
 }
 
 extern "C" int dk_parquet_traffic(dk_parquet* p, int64_t* r, int64_t* w) {
+  if (ensure_open(p)) return 1;
   *r = p->bytes_read; *w = p->bytes_written; return 0;
 }
 
 // Algorithmic bytes of one launch of a decode kernel ("Roofline"): what the kernel must
 // read and write at minimum, from the page / column metadata of the last prepare.
 extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int64_t* r, int64_t* w) {
+  if (ensure_open(p)) return 1;
   if (!p || !kernel || !p->prepared) return fail("dk_parquet_kernel_traffic: not prepared");
   const std::string k = kernel;
   int64_t rd = 0, wr = 0;
@@ -2293,31 +2575,47 @@ static int queue_mirror(dk_parquet* p, int ci) {
   const DColumn& c = p->h_cols[ci];
   HostMirror& h = p->host[ci];
   if (h.state) return 0;
-  hipStream_t s = p->stream;
+  // own stream (an asynchronous open keeps queueing its passes on `stream`); while the open's H2D
+  // copies are in flight the copies are made by a kernel into the pinned mirror (a DMA copy would
+  // queue behind them)
+  if (!p->mir.s && p->mir.create()) return 1;
+  hipStream_t s = p->mir.s;
+  if (p->open_state.load() != 0) {                // after the decode queued on `stream`
+    if (!p->mir_ev) HIPOK(hipEventCreateWithFlags(&p->mir_ev, hipEventDisableTiming));
+    HIPOK(hipEventRecord(p->mir_ev, p->stream));
+    HIPOK(hipStreamWaitEvent(s, p->mir_ev, 0));
+  }
   const int cf = p->col_file[ci];
   if (cf < (int)p->file_done.size() && p->file_done[cf]) HIPOK(hipStreamWaitEvent(s, p->file_done[cf], 0));
+  if (cf < (int)p->file_dec.size() && p->file_dec[cf]) HIPOK(hipStreamWaitEvent(s, p->file_dec[cf], 0));
+  const bool zc = p->async_open;
+  auto d2h = [&](void* dst, const void* src, size_t n) -> int {
+    if (!n) return 0;
+    if (zc) { launch_copy_zc(dst, src, (long long)n, s); return 0; }
+    return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s) == hipSuccess ? 0 : fail("hipMemcpyAsync failed");
+  };
   const int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
   if (h.row_def.alloc(c.n_rows + 1)) return 1;
-  if (c.n_rows) HIPOK(hipMemcpyAsync(h.row_def.data(), c.row_def, c.n_rows, hipMemcpyDeviceToHost, s));
+  if (c.n_rows && d2h(h.row_def.data(), c.row_def, c.n_rows)) return 1;
   if (c.max_rep > 0) {
     if (h.row_offs.alloc((c.n_rows + 1) * 8) || h.entry_def.alloc(nv + 1)) return 1;
     if (c.null_only) { memset(h.row_offs.data(), 0, (c.n_rows + 1) * 8); memset(h.entry_def.data(), 0, nv + 1); }
     else {
-      HIPOK(hipMemcpyAsync(h.row_offs.data(), c.row_offs, (c.n_rows + 1) * 8, hipMemcpyDeviceToHost, s));
-      if (nv) HIPOK(hipMemcpyAsync(h.entry_def.data(), c.entry_def, nv, hipMemcpyDeviceToHost, s));
+      if (d2h(h.row_offs.data(), c.row_offs, (c.n_rows + 1) * 8)) return 1;
+      if (nv && d2h(h.entry_def.data(), c.entry_def, nv)) return 1;
     }
   }
   if (c.phys == PT_BYTE_ARRAY) {
     if (h.offs.alloc((nv + 1) * 8) || h.chars.alloc(c.n_chars + 1)) return 1;
     if (c.null_only) memset(h.offs.data(), 0, (nv + 1) * 8);
     else {
-      HIPOK(hipMemcpyAsync(h.offs.data(), c.offs, (nv + 1) * 8, hipMemcpyDeviceToHost, s));
-      if (c.n_chars) HIPOK(hipMemcpyAsync(h.chars.data(), c.chars, c.n_chars, hipMemcpyDeviceToHost, s));
+      if (d2h(h.offs.data(), c.offs, (nv + 1) * 8)) return 1;
+      if (c.n_chars && d2h(h.chars.data(), c.chars, c.n_chars)) return 1;
     }
   } else {
     if (h.fixed.alloc(nv * c.width + 1)) return 1;
     if (c.null_only) memset(h.fixed.data(), 0, nv * c.width + 1);
-    else if (nv) HIPOK(hipMemcpyAsync(h.fixed.data(), c.fixed, nv * c.width, hipMemcpyDeviceToHost, s));
+    else if (nv && d2h(h.fixed.data(), c.fixed, nv * c.width)) return 1;
   }
   if (!h.ev) HIPOK(hipEventCreateWithFlags(&h.ev, hipEventDisableTiming));
   HIPOK(hipEventRecord(h.ev, s));
@@ -2343,8 +2641,14 @@ extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_c
   if (ci < 0) { out->present = 0; return 0; }
   const DColumn& c = p->h_cols[ci];
   HostMirror& h = p->host[ci];
-  if (h.state == 0)                    // first touch of this leaf: queue it for this and every later file
-    for (int f = file; f < (int)p->files.size(); f++)
+  if (wait_files(p, file + 1)) return 1;   // asynchronous open: this file's columns are final
+  int ready;
+  {
+    std::lock_guard<std::mutex> g(p->rmu);
+    ready = std::min(p->files_ready, (int)p->files.size());
+  }
+  if (h.state == 0)                    // first touch of this leaf: queue it for this and every later (ready) file
+    for (int f = file; f < ready; f++)
       if (p->colmap[f][leaf] >= 0 && queue_mirror(p, p->colmap[f][leaf])) return 1;
   if (h.state == 1) { HIPOK(hipEventSynchronize(h.ev)); h.state = 2; }
   int64_t nv = c.max_rep > 0 ? c.n_entries : c.n_rows;
@@ -2361,6 +2665,7 @@ extern "C" int dk_parquet_column(dk_parquet* p, int32_t file, int32_t leaf, dk_c
 }
 
 extern "C" int dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, int32_t min_def, int64_t* row) {
+  if (ensure_open(p)) return 1;
   *row = -1;
   if (file < 0 || file >= (int)p->files.size() || leaf < 0 || leaf >= (int)p->leaves.size()) return fail("bad column index");
   int ci = p->colmap[file][leaf];
@@ -2383,6 +2688,7 @@ extern "C" int dk_parquet_first_row(dk_parquet* p, int32_t file, int32_t leaf, i
 
 extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf, int64_t row0, int64_t n,
                                       dk_column* out) {
+  if (ensure_open(p)) return 1;
   hipSetDevice(p->eng->cfg.device);   // this thread may not have used the device yet
   memset(out, 0, sizeof *out);
   HIPOK(hipStreamSynchronize(p->stream));
@@ -2431,6 +2737,7 @@ extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf,
 }
 
 extern "C" void dk_parquet_close(dk_parquet* p) {
+  if (p) ensure_open(p);
   if (!p) return;
   hipSetDevice(p->eng->cfg.device);
   hipStreamSynchronize(p->stream);
@@ -3141,6 +3448,15 @@ struct dk_replay {
   int32_t n_groups = 0;
   std::vector<int32_t> grp_f0;            // first file of each group (n_groups + 1 entries)
   std::vector<int> prefetch;              // leaves mirrored to the host per group (dk_replay_prefetch_leaf)
+  // attached to a checkpoint whose open is still running (dk_parquet_open_async): per-file probe
+  // columns, maps and stats rows are filled as the files get ready (attach_upto), and a grouped run
+  // issues each group when the consumer first waits on one of its files (issue_group)
+  bool lazy = false;
+  bool run_lazy = false;                  // this run overlaps the open (the open decodes the values)
+  std::vector<uint8_t> attached;
+  int grp_issued = 0;
+  uint64_t h_nodv = 0;
+  HBuf h_probe_cols, h_st0;
   std::vector<hipEvent_t> grp_ev;
   hipEvent_t ev_tail = nullptr;           // after the commit-tail half (its selection is final)
   std::vector<int64_t> grp_row0;          // per group: its files' row prefix, rebased (probe_all)
@@ -3165,71 +3481,87 @@ static const LeafM* find_leafm(dk_parquet* p, int fi, const char* leaf) {
 // The checkpoint half of a replay: selection buffers, probe columns, partition maps and stats rows
 // of every checkpoint file. Separate from the commit-tail half so that the tail's action table and
 // key table are built while the checkpoint files are still being read (dk_replay_attach_checkpoint).
+// one checkpoint file's probe columns, partition map and stats rows (its columns are final)
+static void attach_file(dk_replay* r, dk_parquet* ckpt, size_t fi) {
+  ProbeCols pc{};
+  const DColumn* path = find_col(ckpt, (int)fi, "add.path");
+  pc.n_rows = ckpt->files[fi].num_rows;
+  if (!path) pc.n_rows = 0;
+  else {
+    pc.path_def = path->row_def; pc.path_offs = path->offs; pc.path_chars = path->chars;
+    pc.path_hash = path->hash;
+    const DColumn* st = find_col(ckpt, (int)fi, "add.deletionVector.storageType");
+    const DColumn* pid = find_col(ckpt, (int)fi, "add.deletionVector.pathOrInlineDv");
+    const DColumn* off = find_col(ckpt, (int)fi, "add.deletionVector.offset");
+    if (st && pid) {
+      pc.has_dv = 1;
+      pc.st_def = st->row_def; pc.st_offs = st->offs; pc.st_chars = st->chars;
+      pc.pid_offs = pid->offs; pc.pid_chars = pid->chars;
+      if (off) { pc.off_def = off->row_def; pc.off_vals = (const int32_t*)off->fixed; pc.off_maxdef = off->max_def; }
+    }
+  }
+  r->probe[fi] = pc;
+  MapRows M{};
+  const DColumn* kc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.key");
+  const DColumn* vc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.value");
+  M.n = ckpt->files[fi].num_rows;
+  if (kc && vc && kc->row_offs && kc->offs && vc->entry_def && vc->offs) {
+    M.row_def = kc->row_def; M.rep_def = kc->rep_def; M.v_max_def = vc->max_def;
+    M.row_offs = kc->row_offs; M.k_offs = kc->offs; M.k_chars = kc->chars;
+    M.v_def = vc->entry_def; M.v_offs = vc->offs; M.v_chars = vc->chars;
+  }                            // else no map entry anywhere (or no map leaf): every field is null
+  r->ck_maps[fi] = M;
+  StatsRows R{};
+  const DColumn* sc = find_col(ckpt, (int)fi, "add.stats");
+  if (sc && !sc->null_only && sc->offs) {
+    R.n = ckpt->files[fi].num_rows;
+    R.row_def = sc->row_def; R.max_def = sc->max_def;
+    R.offs = sc->offs; R.chars = sc->chars;
+  }
+  r->ck_stats[fi] = R;
+  r->attached[fi] = 1;
+}
+
+// attach files [0, f1) (waiting for an asynchronous open to make them ready)
+static int attach_upto(dk_replay* r, int f1) {
+  if (!r->ck) return 0;
+  f1 = std::min(f1, (int)r->ck->files.size());
+  if (wait_files(r->ck, f1)) return 1;
+  for (int f = 0; f < f1; f++) if (!r->attached[f]) attach_file(r, r->ck, (size_t)f);
+  return 0;
+}
+
+// The checkpoint half of a replay: selection buffers, probe columns, partition maps and stats rows
+// of every checkpoint file. Separate from the commit-tail half so that the tail's action table and
+// key table are built while the checkpoint files are still being read (dk_replay_attach_checkpoint).
+// With the checkpoint's open still running, the per-file parts wait for their files (attach_upto).
 static int replay_attach(dk_replay* r, dk_parquet* ckpt) {
   r->ck = ckpt;
   if (hipEventCreateWithFlags(&r->ev_in, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&r->ev_out, hipEventDisableTiming) != hipSuccess)
     return fail("hipEventCreate failed");
   if (ckpt) {
+    const size_t nf = ckpt->files.size();
     int64_t max_rows = 1, total = 0;
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
+    for (size_t fi = 0; fi < nf; fi++) {
       max_rows = std::max<int64_t>(max_rows, ckpt->files[fi].num_rows);
       total += ckpt->files[fi].num_rows;
     }
     // every file in one probe launch while global row numbers fit the int32 candidate list
     static const bool per_file = getenv("DK_PROBE_PER_FILE") && atoi(getenv("DK_PROBE_PER_FILE"));
-    r->probe_all = !per_file && ckpt->files.size() > 1 && total < (1ll << 31) - 1;
+    r->probe_all = !per_file && nf > 1 && total < (1ll << 31) - 1;
     if (r->d_cand.alloc((size_t)(r->probe_all ? total : max_rows) * 4 + 64)) return 1;
     if (r->d_cand_n.alloc(64)) return 1;
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      ProbeCols pc{};
-      const DColumn* path = find_col(ckpt, (int)fi, "add.path");
-      pc.n_rows = ckpt->files[fi].num_rows;
+    for (size_t fi = 0; fi < nf; fi++) {
       r->d_csel.emplace_back(new DBuf());
-      if (r->d_csel.back()->alloc(pc.n_rows + 16)) return 1;
-      if (!path) { pc.n_rows = 0; r->probe.push_back(pc); continue; }
-      if (path->phys != PT_BYTE_ARRAY || path->max_rep) return fail("add.path has an unexpected type");
-      pc.path_def = path->row_def; pc.path_offs = path->offs; pc.path_chars = path->chars;
-      pc.path_hash = path->hash;
-      const DColumn* st = find_col(ckpt, (int)fi, "add.deletionVector.storageType");
-      const DColumn* pid = find_col(ckpt, (int)fi, "add.deletionVector.pathOrInlineDv");
-      const DColumn* off = find_col(ckpt, (int)fi, "add.deletionVector.offset");
-      if (st && pid) {
-        pc.has_dv = 1;
-        pc.st_def = st->row_def; pc.st_offs = st->offs; pc.st_chars = st->chars;
-        pc.pid_offs = pid->offs; pc.pid_chars = pid->chars;
-        if (off) { pc.off_def = off->row_def; pc.off_vals = (const int32_t*)off->fixed; pc.off_maxdef = off->max_def; }
-      }
-      r->probe.push_back(pc);
+      if (r->d_csel.back()->alloc(ckpt->files[fi].num_rows + 16)) return 1;
     }
-  }
-  if (ckpt) {
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      MapRows M{};
-      const DColumn* kc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.key");
-      const DColumn* vc = find_col(ckpt, (int)fi, "add.partitionValues.key_value.value");
-      if (kc && vc && kc->row_offs && kc->offs && vc->entry_def && vc->offs) {
-        M.n = ckpt->files[fi].num_rows;
-        M.row_def = kc->row_def; M.rep_def = kc->rep_def; M.v_max_def = vc->max_def;
-        M.row_offs = kc->row_offs; M.k_offs = kc->offs; M.k_chars = kc->chars;
-        M.v_def = vc->entry_def; M.v_offs = vc->offs; M.v_chars = vc->chars;
-      } else {                  // no map entry anywhere (or no map leaf): every field is null
-        M.n = ckpt->files[fi].num_rows;
-      }
-      r->ck_maps.push_back(M);
-    }
-  }
-  if (ckpt) {
-    for (size_t fi = 0; fi < ckpt->files.size(); fi++) {
-      StatsRows R{};
-      const DColumn* sc = find_col(ckpt, (int)fi, "add.stats");
-      if (sc && !sc->null_only && sc->offs) {
-        R.n = ckpt->files[fi].num_rows;
-        R.row_def = sc->row_def; R.max_def = sc->max_def;
-        R.offs = sc->offs; R.chars = sc->chars;
-      }
-      r->ck_stats.push_back(R);
-    }
+    r->probe.assign(nf, ProbeCols{});
+    r->ck_maps.assign(nf, MapRows{});
+    r->ck_stats.assign(nf, StatsRows{});
+    r->attached.assign(nf, 0);
+    r->lazy = ckpt->open_state.load() == 0;
+    if (!r->lazy) for (size_t fi = 0; fi < nf; fi++) attach_file(r, ckpt, fi);
   }
   return 0;
 }
@@ -3406,6 +3738,7 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   }
   if (depth != 1) return fail("dk_replay_set_skipping: program must leave one value");
   if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
+  if (r->lazy && attach_upto(r, INT_MAX)) return 1;   // the typed stats columns of every file
   r->skip = P;
   // add.stats_parsed fast path, per checkpoint file: every program path's typed leaf
   // add.stats_parsed.<path> was projected and decoded with a physical / logical type that holds the
@@ -3526,6 +3859,7 @@ extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_progra
 
 static int replay_ckpt_filters(dk_replay* r);
 static int replay_grouped(dk_replay* r, uint64_t h_nodv);
+static int issue_group(dk_replay* r);
 static int replay_launch(dk_replay* r) {
   hipStream_t s = r->stream;
   KTimer& T = r->timer;
@@ -3534,7 +3868,12 @@ static int replay_launch(dk_replay* r) {
   if (r->xw > 0) HIPOK(hipMemsetAsync(r->d_xtot.p, 0, (size_t)r->xw * 8, s));
   DState st0{};
   st0.err_row = LLONG_MAX;
-  HIPOK(hipMemcpyAsync(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
+  if (r->lazy && r->ck && r->ck->open_state.load() == 0) {
+    // the checkpoint's H2D copies are in flight: a small DMA copy would queue behind them
+    if (r->h_st0.size() < sizeof st0 && r->h_st0.alloc(sizeof st0 + 16)) return 1;
+    memcpy(r->h_st0.data(), &st0, sizeof st0);
+    launch_copy_zc(r->d_state.p, r->h_st0.data(), sizeof st0, s);
+  } else HIPOK(hipMemcpyAsync(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
   // probe table: h = 0 (empty), first_add = ~0, min_rm_step = INT32_MAX
   launch_slots_init(r->d_slots.as<Slot>(), r->mask + 1, s);
   int na = (int)r->acts.size();
@@ -3570,12 +3909,21 @@ static int replay_launch(dk_replay* r) {
   if (r->ck) {
     dk_parquet* p = r->ck;
     const bool grouped = r->n_groups > 0 && r->xw == 0;
-    // the decode runs on the replay's stream, after anything queued on the checkpoint's own
-    HIPOK(hipEventRecord(r->ev_in, p->stream));
-    HIPOK(hipStreamWaitEvent(s, r->ev_in, 0));
-    // decode errors are collected into the replay state too
-    HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
-    if (run_pipeline(p, 1, s, grouped)) return 1;
+    // a checkpoint still being opened (and decoded, slice by slice): only a grouped run overlaps
+    // it; anything else waits for the whole open first
+    const bool lazy_run = r->lazy && grouped && p->open_state.load() == 0;
+    r->run_lazy = lazy_run;
+    if (r->lazy && !lazy_run) {
+      if (ensure_open(p) || attach_upto(r, INT_MAX)) return 1;
+    }
+    if (!lazy_run) {
+      // the decode runs on the replay's stream, after anything queued on the checkpoint's own
+      HIPOK(hipEventRecord(r->ev_in, p->stream));
+      HIPOK(hipStreamWaitEvent(s, r->ev_in, 0));
+      // decode errors are collected into the replay state too
+      HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
+      if (run_pipeline(p, 1, s, grouped)) return 1;
+    }
     launch_table_fp(S, r->d_fp.as<uint32_t>(), r->mask + 1, s);
     HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;       // dvUniqueId stream of "no DV"
     dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
@@ -3678,12 +4026,66 @@ static int replay_grouped(dk_replay* r, uint64_t h_nodv) {
     int64_t* row0 = r->grp_row0.data() + r->grp_f0[g] + g;
     for (int f = r->grp_f0[g]; f < r->grp_f0[g + 1]; f++) row0[f - r->grp_f0[g] + 1] = row0[f - r->grp_f0[g]] + r->probe_run[f].n_rows;
   }
-  if (upload(r->d_probe_cols, r->probe_run.data(), nf * sizeof(ProbeCols), s) ||
-      upload(r->d_grp_row0, r->grp_row0.data(), r->grp_row0.size() * 8, s) ||
-      upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
+  // (row counts come from the footers: the prefixes are final before any file is attached)
   for (int g = 0; g < ng; g++) {
+    int64_t* row0 = r->grp_row0.data() + r->grp_f0[g] + g;
+    for (int f = r->grp_f0[g]; f < r->grp_f0[g + 1]; f++) row0[f - r->grp_f0[g] + 1] = row0[f - r->grp_f0[g]] + (find_col(p, f, "add.path") ? p->files[f].num_rows : 0);
+  }
+  if (r->lazy) {
+    // tables through pinned memory and a copy kernel: the open's H2D copies are still in flight
+    if (r->d_probe_cols.alloc(nf * sizeof(ProbeCols) + 16) || r->d_grp_row0.alloc(r->grp_row0.size() * 8 + 16) ||
+        r->d_probe_sel.alloc(nf * sizeof(uint8_t*) + 16) || r->h_probe_cols.alloc(nf * sizeof(ProbeCols) + 16))
+      return 1;
+    HBuf a, b;
+    if (a.alloc(r->grp_row0.size() * 8 + 16) || b.alloc(nf * sizeof(uint8_t*) + 16)) return 1;
+    memcpy(a.data(), r->grp_row0.data(), r->grp_row0.size() * 8);
+    memcpy(b.data(), r->probe_sel.data(), nf * sizeof(uint8_t*));
+    launch_copy_zc(r->d_grp_row0.p, a.data(), (long long)(r->grp_row0.size() * 8), s);
+    launch_copy_zc(r->d_probe_sel.p, b.data(), (long long)(nf * sizeof(uint8_t*)), s);
+    HIPOK(hipStreamSynchronize(s));                // (the staging goes back to the cache)
+  } else if (upload(r->d_probe_cols, r->probe_run.data(), nf * sizeof(ProbeCols), s) ||
+             upload(r->d_grp_row0, r->grp_row0.data(), r->grp_row0.size() * 8, s) ||
+             upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
+  r->h_nodv = h_nodv;
+  r->grp_issued = 0;
+  r->h_csel_ready = true;   // the block every group's selections land in (file f's after wait_file(f))
+  if (!r->run_lazy)
+    while (r->grp_issued < ng) if (issue_group(r)) return 1;
+  return 0;
+}
+
+// The next group of a grouped run: value decode (unless the open decoded it), probe, filters, the
+// selections and error states to pinned memory, its event, the prefetched mirrors. Lazy runs (the
+// checkpoint's open still running) attach the group's files first, waiting for them to be ready.
+static int issue_group(dk_replay* r) {
+  hipStream_t s = r->stream;
+  KTimer& T = r->timer;
+  dk_parquet* p = r->ck;
+  DState* st = r->d_state.as<DState>();
+  DJsonAction* A = r->d_acts.as<DJsonAction>();
+  Slot* S = r->d_slots.as<Slot>();
+  const int ng = (int)r->grp_f0.size() - 1;
+  const int g = r->grp_issued;
+  if (g >= ng) return 0;
+  const uint64_t h_nodv = r->h_nodv;
+  {
     const int f0 = r->grp_f0[g], f1 = r->grp_f0[g + 1];
-    decode_cols(p, s, p->file_col0[f0], p->file_col0[f1]);
+    if (r->lazy) {
+      if (attach_upto(r, f1)) return 1;
+      for (int f = f0; f < f1; f++) {
+        r->probe_run[f] = r->probe[f];
+        if (r->seed != kDecodeSeed) r->probe_run[f].path_hash = nullptr;   // collision retry
+      }
+      memcpy(r->h_probe_cols.data() + (size_t)f0 * sizeof(ProbeCols), r->probe_run.data() + f0, (size_t)(f1 - f0) * sizeof(ProbeCols));
+      launch_copy_zc(r->d_probe_cols.as<ProbeCols>() + f0, r->h_probe_cols.data() + (size_t)f0 * sizeof(ProbeCols),
+                     (long long)((f1 - f0) * sizeof(ProbeCols)), s);
+    }
+    if (r->run_lazy) {
+      for (int f = f0; f < f1; f++)                // the files' value decode (the open's slice streams)
+        if (f < (int)p->file_dec.size() && p->file_dec[f]) HIPOK(hipStreamWaitEvent(s, p->file_dec[f], 0));
+    } else {
+      decode_cols(p, s, p->file_col0[f0], p->file_col0[f1]);
+    }
     {
       KTimer::Scope sc(&T, 11, s);
       const int64_t* row0 = r->grp_row0.data() + f0 + g;
@@ -3696,6 +4098,7 @@ static int replay_grouped(dk_replay* r, uint64_t h_nodv) {
     for (int f = f0; f < f1; f++) {
       const int64_t n = p->files[f].num_rows;
       if (r->probe[f].n_rows == 0) memset(r->h_csel.data() + r->h_csel_off[f], 0, n);
+      else if (n && r->lazy) launch_copy_zc(r->h_csel.data() + r->h_csel_off[f], r->d_csel[f]->p, n, s);
       else if (n) HIPOK(hipMemcpyAsync(r->h_csel.data() + r->h_csel_off[f], r->d_csel[f]->p, n, hipMemcpyDeviceToHost, s));
     }
     {
@@ -3709,8 +4112,8 @@ static int replay_grouped(dk_replay* r, uint64_t h_nodv) {
       for (int f = f0; f < f1; f++)
         if (p->colmap[f][leaf] >= 0 && queue_mirror(p, p->colmap[f][leaf])) return 1;
   }
-  r->h_csel_ready = true;
-  HIPOK(hipEventRecord(r->ev_out, s));   // the checkpoint stream waits for it at dk_replay_sync
+  r->grp_issued = g + 1;
+  if (r->grp_issued == ng) HIPOK(hipEventRecord(r->ev_out, s));   // the checkpoint stream waits for it at dk_replay_sync
   return 0;
 }
 
@@ -3780,6 +4183,7 @@ extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
   if (file >= 0) {
     int g = 0;
     while (r->grp_f0[g + 1] <= file) g++;
+    while (r->grp_issued <= g) if (issue_group(r)) return 1;   // lazy runs issue groups on demand
     ev = r->grp_ev[g];
   }
   int slot = 0;
@@ -3901,6 +4305,9 @@ extern "C" int dk_replay_sync(dk_replay* r) {
   hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   hipStream_t s = r->stream;
   if (r->xw > 0 && r->xphase != 3) return fail("dk_replay_sync: the exchange-mode run has not finished its exchange");
+  if (r->ck && r->n_groups > 0 && r->xw == 0)      // a lazy grouped run: the groups not issued yet
+    while (r->grp_issued + 1 < (int)r->grp_f0.size()) if (issue_group(r)) return 1;
+  if (r->ck && ensure_open(r->ck)) return 1;        // (an asynchronous open has finished by now)
   for (int attempt = 0; attempt < 8; attempt++) {
     HIPOK(hipStreamSynchronize(s));
     if (r->ck && r->n_groups > 0) HIPOK(hipStreamWaitEvent(r->ck->stream, r->ev_out, 0));

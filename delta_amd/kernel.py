@@ -137,14 +137,25 @@ def row_group_rows(path):
 class ParquetSet:
     """A set of Parquet files decoded on the GPU (one batch per file; batches in input order)."""
 
-    def __init__(self, engine: GpuEngine, paths, leaves, row_groups=None, groups=None):
+    def __init__(self, engine: GpuEngine, paths, leaves, row_groups=None, groups=None, async_open=False):
         """row_groups: optional [(first, end)] row-group range per file (dk_parquet_open_rg);
-        groups: optional list of row-group indices per file (dk_parquet_open_sel)."""
+        groups: optional list of row-group indices per file (dk_parquet_open_sel);
+        async_open: return once the tables are read, the files being read, sized and decoded on a
+        library thread meanwhile (dk_parquet_open_async; every call waits for what it needs)."""
         self.engine = engine
         self.paths = list(paths)
         self.leaves = list(leaves)
         self._h = C.c_void_p()
-        if groups is not None:
+        self.async_open = bool(async_open and row_groups is None)
+        if async_open and row_groups is None:
+            cnt = lst = None
+            if groups is not None:
+                cnt = (C.c_int32 * max(1, len(groups)))(*[len(g) for g in groups])
+                flat = [g for gs in groups for g in gs]
+                lst = (C.c_int32 * max(1, len(flat)))(*flat)
+            check(lib().dk_parquet_open_async(engine._h, _cstrs(self.paths), len(self.paths), _cstrs(self.leaves),
+                                              len(self.leaves), cnt, lst, C.byref(self._h)))
+        elif groups is not None:
             cnt = (C.c_int32 * max(1, len(groups)))(*[len(g) for g in groups])
             flat = [g for gs in groups for g in gs]
             lst = (C.c_int32 * max(1, len(flat)))(*flat)
@@ -1229,15 +1240,24 @@ class GpuScan:
             _, paths, types, _ = self.skipping
             leaves = leaves + ["add.stats_parsed." + ".".join(p) for p in paths]
         t2 = time.perf_counter()
-        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel) if self.ckpt_files else None
+        # a plain scan (no shard, skipping or partition filter) opens the checkpoint asynchronously: the
+        # grouped getScanFiles hands out the first files' batches while the later files still land
+        plain = not self.shard and self.skipping is None and self.partition is None and self.predicate is None and \
+            scan_groups(len(self.ckpt_files or [])) and os.environ.get("DK_ASYNC_OPEN", "0") != "0"
+        self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel, async_open=bool(plain)) \
+            if self.ckpt_files else None
         t3 = time.perf_counter()
         self.prepare_ms.update({"plan_files": (t2 - t1) * 1e3, "checkpoint_open": (t3 - t2) * 1e3})
-        if self.ckpt is not None:
-            om = (C.c_double * 7)()
-            check(lib().dk_parquet_open_ms(self.ckpt._h, om))
-            self.prepare_ms.update({"open_read_h2d": om[0], "open_metadata": om[1], "open_prepare": om[2],
-                                    "prep_h2d_headers": om[3], "prep_host_pages": om[4], "prep_device_sizing": om[5],
-                                    "prep_host_tiles_alloc": om[6]})
+        if self.ckpt is not None and not self.ckpt.async_open:
+            self._open_phases()
+
+    def _open_phases(self):
+        """The checkpoint open's phases (an asynchronous open's once it has finished)."""
+        om = (C.c_double * 7)()
+        check(lib().dk_parquet_open_ms(self.ckpt._h, om))
+        self.prepare_ms.update({"open_read_h2d": om[0], "open_metadata": om[1], "open_prepare": om[2],
+                                "prep_h2d_headers": om[3], "prep_host_pages": om[4], "prep_device_sizing": om[5],
+                                "prep_host_tiles_alloc": om[6]})
 
     def getRemainingFilter(self):
         """ScanImpl.getRemainingFilter (:221-223): the data filter, which skipping never fully
@@ -1341,6 +1361,8 @@ class GpuScan:
                                         int(self.ckpt.row_offset(fi)))
         if grouped:
             self.sync()                     # the counters (and any error the waits did not see)
+            if self.ckpt is not None and self.ckpt.async_open:
+                self._open_phases()
 
     def close(self):
         if getattr(self, "_rh", None):

@@ -99,6 +99,16 @@ int  dk_parquet_nonnull_row_groups(const char* path, const char* leaf, uint8_t* 
 int  dk_parquet_open_sel(dk_engine* e, const char* const* paths, int32_t n_files,
                          const char* const* leaves, int32_t n_leaves, const int32_t* rg_count,
                          const int32_t* rg_list, dk_parquet** out);
+/* The same, asynchronous: returns once the footers, page headers and tables are read (num_rows /
+ * row_offset answer at once); the chunk reads, sizing passes and value decode go on on a library
+ * thread, files becoming ready slice by slice. dk_parquet_column waits for its file, every other
+ * call for the whole open (its error, if any, is reported there). A replay attached meanwhile
+ * attaches each file as it gets ready, and a grouped run issues each group when a wait first needs
+ * it. Falls back to the synchronous open where the per-slice decode is off (DK_SLICE_DECODE=0,
+ * DK_OPEN_ADAPTIVE=0, DK_SNAPPY_MODE=page, DK_ASYNC_OPEN=0). */
+int  dk_parquet_open_async(dk_engine* e, const char* const* paths, int32_t n_files,
+                           const char* const* leaves, int32_t n_leaves, const int32_t* rg_count,
+                           const int32_t* rg_list, dk_parquet** out);
 
 /* Row-group pruning predicate: the checkpoint predicate ActionsIterator hands the ParquetHandler for
  * checkpoint parts and sidecars (KA/internal/replay/ActionsIterator.java:336-351; the partition filter
