@@ -2578,9 +2578,9 @@ static int queue_mirror(dk_parquet* p, int ci) {
   // own stream (an asynchronous open keeps queueing its passes on `stream`); while the open's H2D
   // copies are in flight the copies are made by a kernel into the pinned mirror (a DMA copy would
   // queue behind them)
-  if (!p->mir.s && p->mir.create()) return 1;
-  hipStream_t s = p->mir.s;
-  if (p->open_state.load() != 0) {                // after the decode queued on `stream`
+  if (p->async_open && !p->mir.s && p->mir.create()) return 1;
+  hipStream_t s = p->async_open ? p->mir.s : p->stream;
+  if (p->async_open && p->open_state.load() != 0) {   // after the decode queued on `stream`
     if (!p->mir_ev) HIPOK(hipEventCreateWithFlags(&p->mir_ev, hipEventDisableTiming));
     HIPOK(hipEventRecord(p->mir_ev, p->stream));
     HIPOK(hipStreamWaitEvent(s, p->mir_ev, 0));
