@@ -1595,6 +1595,18 @@ static int prepare(dk_parquet* p) {
         acc = 0;
         // at least `target` bytes (or the rest), then every file already landed
         while (f1 < nf && (acc < target || (is_queued(p, f1) && hipEventQuery(p->file_ev[f1]) == hipSuccess))) {
+          // while the next file lands, finish the sized slices whose passes are done (never block
+          // the loop on them: the next slice is queued as soon as its files are in)
+          while (per_slice && !(is_queued(p, f1) && hipEventQuery(p->file_ev[f1]) == hipSuccess)) {
+            if (!sized.empty() && hipEventQuery(sized.front().ev) == hipSuccess) {
+              if (finish_slice(p, sized.front(), got)) return 1;
+              sized.erase(sized.begin());
+            } else if (p->queued && p->queued[f1].load() == 2) {
+              break;
+            } else {
+              std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+          }
           if (!wait_queued(p, f1)) { if (tables) hipEventDestroy(tables); return 1; }   // parquet_open reports the read error
           HIPOK(hipEventSynchronize(p->file_ev[f1]));
           acc += (int64_t)p->files[f1].bytes.size();
@@ -1619,7 +1631,7 @@ static int prepare(dk_parquet* p) {
           HIPOK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
           HIPOK(hipEventRecord(S.ev, cs));
           sized.push_back(std::move(S));
-          while (sized.size() > 1) {
+          while (!sized.empty() && hipEventQuery(sized.front().ev) == hipSuccess) {
             if (finish_slice(p, sized.front(), got)) return 1;
             sized.erase(sized.begin());
           }
