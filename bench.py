@@ -159,47 +159,101 @@ def launch(args, argv):
 # CPU baseline + full-size parity (the oracle: test infrastructure, used here only as the checker
 # and the reported CPU baseline)
 # ------------------------------------------------------------------------------------------------
-def cpu_baseline(work, files, with_stats, threads, reps_single=2, got=None):
-    """The oracle (oracle/dk_ref.c: parquet-mr decode of every projected leaf + java.net.URI keys +
-    probe; oracle/ref.py: commit-tail replay) on the bench table.
+def oracle_skipping(work, cfg):
+    """The oracle's own data-skipping predicate for the config's filter (oracle/skipping_filter.py
+    restates constructDataSkippingFilter; the product planner is not used) and its stats types."""
+    if not cfg["predicate"]:
+        return None
+    from delta_amd.expressions import Column, Literal, Predicate
+    from oracle import ref
+    from oracle import skipping_filter as osf
+    _, meta, _ = ref.load_protocol_metadata(work)
+    col, op, lit = cfg["predicate"]
+    pf, data = osf.split(Predicate(op, Column(col), Literal.ofLong(lit)), meta["partitionColumns"])
+    if pf is not None:
+        raise SystemExit("bench.py: the CPU baseline restates data-skipping filters only")
+    schema = osf.StatsSchema(meta["schemaString"], meta["partitionColumns"])
+    node = osf.build(data, schema) if data is not None else None
+    if node is None:
+        return None
+    osf.check(node, schema)
+    return node, osf.stat_types(node, schema)
 
-    1 thread: `reps_single` whole checkpoint parts probed against the real tail key set.
-    `threads` threads: the WHOLE table (tail + every part, one part per task) -- this run is also
-    the full-size parity check: its five counters and every checkpoint row's selection bit are
-    compared with the GPU's (`got`)."""
-    import concurrent.futures as cf  # noqa: F401
+
+def cpu_share():
+    """CPUs this process may run on (sched_getaffinity, i.e. `nproc`) and the cgroup CPU quota, if
+    any (cpu.max): the GPU box shows the whole machine's cores but grants one GPU's share."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return aff, quota
+
+
+def cpu_baseline(work, files, cfg, threads, got=None, single_rows=12_500_000):
+    """The oracle (oracle/dk_ref.c: parquet-mr decode of every projected leaf + java.net.URI keys +
+    probe + data skipping over add.stats; oracle/ref.py: commit-tail replay) on the bench table.
+
+    1 thread: whole checkpoint parts (up to 8, at most ~`single_rows` rows) decoded, probed against
+    the real tail key set and, with a filter, skipped.
+    `threads` threads: the WHOLE table (tail + every part, runs of row groups per task) -- this run
+    is also the full-size parity check: its five counters and every checkpoint row's selection bit
+    (after data skipping) are compared with the GPU's (`got`)."""
     import numpy as np
     from oracle import ref
     ref.lib()
+    with_stats = cfg["stats"]
+    skipping = oracle_skipping(work, cfg)
     out = {"unit": "actions/s", "kind": "port"}
-    # single thread over a sample: decode + key + probe against an empty key set of the same shape
-    # (the probe cost is dominated by the key build, not the table)
-    leaves = ref.ADD_LEAVES + (["add.stats"] if with_stats else []) + REMOVE_LEAVES
+    leaves = ref.ADD_LEAVES + (["add.stats"] if with_stats or skipping else []) + REMOVE_LEAVES
+    seg = ref.load_log_segment(work)
+    t0 = time.perf_counter()
+    keyset_res = ref.replay_tail_keyset(work, with_stats=with_stats or skipping is not None)
+    tail_s = time.perf_counter() - t0
 
     def one(path):
         pf = ref.ParquetFile.open(path)
         cols = {leaf: pf.read(leaf) for leaf in leaves}
-        ks = ref.lib().dkr_keyset_new()
-        ref.probe_checkpoint(cols, pf.num_rows, ks, ref.Counters())
-        ref.lib().dkr_keyset_free(ks)
+        sel = ref.probe_checkpoint(cols, pf.num_rows, keyset_res, ref.Counters())
+        if skipping is not None:
+            from oracle import skipping as sk
+            sk.apply_to_column(cols.get(ref.STATS_LEAF), sel, *skipping)
         return pf.num_rows
 
-    sample = files[:max(1, reps_single)]
+    sample, n_rows = [], 0
+    for p in files:
+        if len(sample) >= 8 or (sample and n_rows >= single_rows):
+            break
+        sample.append(p)
+        n_rows += ref.ParquetFile.open(p).num_rows
     t0 = time.perf_counter()
     n1 = sum(one(p) for p in sample)
     v1 = n1 / (time.perf_counter() - t0)
+    ref.lib().dkr_keyset_free(keyset_res)
     out.update(value=v1, cores=1,
-               sample="%d checkpoint part(s) of the bench table (%d rows): decode of %d leaves + URI key + probe, "
-                      "oracle/dk_ref.c (CPU restatement, not DefaultEngine)" % (len(sample), n1, len(leaves)))
+               sample="%d of %d checkpoint part(s) of the bench table (%d rows): decode of %d leaves + URI key + "
+                      "probe against the commit-tail key sets%s, oracle/dk_ref.c (CPU restatement, not "
+                      "DefaultEngine); the commit-tail replay (Python, %d commits) took %.2f s more"
+                      % (len(sample), len(files), n1, len(leaves),
+                         " + data skipping over add.stats (oracle/dk_skip.c)" if skipping else "",
+                         len(seg.deltas), tail_s))
     if threads > 1:
         t0 = time.perf_counter()
         res = ref.replay(work, with_stats=with_stats, threads=threads, keep_cols=False,
-                         extra_leaves=REMOVE_LEAVES)
+                         extra_leaves=REMOVE_LEAVES, skipping=skipping)
         dt = time.perf_counter() - t0
         seen = res.counters.addFilesSeen
-        full = {"value": seen / dt, "unit": "actions/s", "cores": threads, "seconds": dt,
-                "sample": "the whole table: commit-tail replay (Python) + %d parts decoded and probed on %d threads"
-                          % (len(res.checkpoint), threads)}
+        used = min(threads, getattr(res, "pool_tasks", threads))
+        full = {"value": seen / dt, "unit": "actions/s", "cores": used, "seconds": dt,
+                "sample": "the whole table: commit-tail replay (Python, serial) + %d checkpoint files decoded, probed"
+                          "%s in %d tasks (runs of row groups) on %d threads"
+                          % (len(res.checkpoint), " and skipped" if skipping else "",
+                             getattr(res, "pool_tasks", 0), used)}
         out["threads"] = full
         if got is not None:
             counters, tail_paths, bits = got
@@ -283,7 +337,8 @@ def main(argv=None):
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=None, help="checkpoint adds (default: the config's)")
     ap.add_argument("--compression", default=None, help="override the config's codec")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the whole-table CPU baseline (default: nproc, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--device-steps", type=int, default=None, help="timed device-only steps (default: --steps)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of launcher + planning + exchange")
@@ -620,9 +675,12 @@ def main(argv=None):
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         got = (capture["counters"], capture["tail_paths"], capture["bits"]) if capture else None
-        result["cpu_baseline"] = cpu_baseline(work, ckpt_files, cfg["stats"], args.cpu_threads, got=got) \
-            if not cfg["predicate"] else None
-        result["cpu_baseline_host"] = {"nproc": os.cpu_count(), "cpu": _cpu_model()}
+        aff, quota = cpu_share()
+        # the pool's rule: one GPU's share of the box is 16 CPUs although nproc shows the machine
+        threads = args.cpu_threads or min(aff, quota or 16)
+        result["cpu_baseline"] = cpu_baseline(work, ckpt_files, cfg, threads, got=got)
+        result["cpu_baseline_host"] = {"cpu_count": os.cpu_count(), "nproc": aff, "cgroup_cpus": quota,
+                                       "threads_used": threads, "cpu": _cpu_model()}
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

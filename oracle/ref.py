@@ -80,6 +80,8 @@ def lib():
         L.dkr_keyset_get.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
         P = C.c_void_p
         L.dkr_probe_checkpoint.argtypes = [P, C.c_int64, P, P, P, P, P, P, P, P, P, P, C.c_int, P, P, P]
+        L.dkr_skip_eval.restype = C.c_int64
+        L.dkr_skip_eval.argtypes = [P, P, P, C.c_int, P, P, C.c_int64, C.c_char_p, C.c_int64, C.c_int, P, C.c_int]
         _lib = L
     return _lib
 
@@ -127,8 +129,14 @@ class ParquetFile:
     PHYS = {0: "BOOLEAN", 1: "INT32", 2: "INT64", 3: "INT96", 4: "FLOAT", 5: "DOUBLE",
             6: "BYTE_ARRAY", 7: "FIXED_LEN_BYTE_ARRAY"}
 
-    def __init__(self, data: bytes):
-        self._buf = C.create_string_buffer(data, len(data))
+    def __init__(self, data):
+        import mmap
+        if isinstance(data, mmap.mmap):
+            # a private mapping of the file: the page cache is shared, nothing is copied
+            self._mm = data
+            self._buf = (C.c_char * len(data)).from_buffer(data)
+        else:
+            self._buf = C.create_string_buffer(data, len(data))
         self._h = lib().dkr_open(self._buf, len(data))
         if not self._h:
             raise OracleError(lib().dkr_errmsg().decode())
@@ -137,8 +145,11 @@ class ParquetFile:
 
     @classmethod
     def open(cls, path):
+        import mmap
         with open(path, "rb") as f:
-            return cls(f.read())
+            if os.fstat(f.fileno()).st_size == 0:
+                return cls(b"")
+            return cls(mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_COPY))
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -444,6 +455,7 @@ class CheckpointBatch:
     n_rows: int
     selected: np.ndarray = None
     file_index: int = 0          # position among the checkpoint files in replay order
+    skipped: bool = False        # data skipping already applied to `selected`
 
 
 @dataclass
@@ -684,7 +696,7 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                 continue
             if not mine and g.kind != "v2":
                 continue
-            if threads > 1 and g.kind in ("classic", "multipart") and partition is None:
+            if threads > 1 and g.kind in ("classic", "multipart", "sidecar") and partition is None:
                 pool_items.append((g, idx))
                 continue
             extra = tuple(SIDECAR_LEAVES if g.kind == "v2" else ()) + tuple(extra_leaves)
@@ -705,28 +717,45 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
                 continue
             b = CheckpointBatch(g.path, cols, pf.num_rows, file_index=idx)
             b.selected = probe_checkpoint(cols, pf.num_rows, keyset, cc)
+            if skipping is not None and partition is None:
+                _skip_file(b, cols, skipping)
             if not keep_cols:
                 b.cols = {}
             res.checkpoint.append(b)
     if pool_items:
         import concurrent.futures as cf
+        # tasks: whole files, or (keep_cols=False) runs of row groups so that a wide pool has work
+        tasks = []
+        n_rgs = [1 if keep_cols else lib().dkr_num_row_groups(ParquetFile.open(g.path)._h) for g, _ in pool_items]
+        per = max(1, sum(n_rgs) // max(1, threads))          # row groups per task
+        for (g, idx), n_rg in zip(pool_items, n_rgs):
+            for r0 in range(0, n_rg, per):
+                tasks.append((g, idx, None if per >= n_rg else [r0 <= r < r0 + per for r in range(n_rg)]))
 
         def work(item):
-            g, idx = item
-            pf, cols = decode_checkpoint_file(g.path, with_stats, extra_leaves)
+            g, idx, keep = item
+            pf, cols = decode_checkpoint_file(g.path, with_stats, extra_leaves, keep)
             part = Counters()
             b = CheckpointBatch(g.path, cols, pf.num_rows, file_index=idx)
             b.selected = probe_checkpoint(cols, pf.num_rows, keyset, part)
+            if skipping is not None:
+                _skip_file(b, cols, skipping)
             if not keep_cols:
                 b.cols = {}
             return b, part
 
-        with cf.ThreadPoolExecutor(threads) as ex:
-            for b, part in ex.map(work, pool_items):
-                res.checkpoint.append(b)
+        with cf.ThreadPoolExecutor(min(threads, len(tasks))) as ex:
+            for b, part in ex.map(work, tasks):
+                last = res.checkpoint[-1] if res.checkpoint else None
+                if last is not None and last.file_index == b.file_index:     # the next run of row groups
+                    last.selected = np.concatenate([last.selected, b.selected])
+                    last.n_rows += b.n_rows
+                else:
+                    res.checkpoint.append(b)
                 cc.addFilesSeen += part.addFilesSeen
                 cc.activeAddFiles += part.activeAddFiles
                 cc.duplicateAddFiles += part.duplicateAddFiles
+        res.pool_tasks = len(tasks)
     if keyset is not None:
         L.dkr_keyset_free(keyset)
     res.counters = Counters(*[a + b for a, b in zip(c.as_tuple(), cc.as_tuple())])
@@ -748,12 +777,43 @@ def replay(table_root: str, json_batch_size=1024, with_stats=False, shard=None, 
         node, types = skipping
         res.json_rows = [a for a in res.json_rows if sk.keep(a.get("stats"), node, types)]
         for b in res.checkpoint:
-            sc = b.cols.get(STATS_LEAF)
-            for i in np.nonzero(b.selected)[0]:
-                st = _str_at(sc, int(i), 2)
-                if not sk.keep(None if st is None else st.decode("utf-8", "replace"), node, types):
-                    b.selected[i] = False
+            if not b.skipped:
+                _skip_file(b, b.cols, skipping)
     return res
+
+
+def replay_tail_keyset(table_root: str, json_batch_size=1024, with_stats=False):
+    """The commit-tail half of replay(): the JSON add (A) and tombstone (T) key sets that every
+    checkpoint row is probed against (ActiveAddFilesIterator.java:164-234, App. A R2-R4), as a C
+    keyset (flag 1 = in A, 2 = in T). The caller frees it with dkr_keyset_free."""
+    seg = load_log_segment(table_root)
+    tomb, added = set(), set()
+    for f in seg.all_files_reversed():
+        if f.kind != "commit":
+            continue
+        for batch in read_json_batches(f.path, json_batch_size, with_stats):
+            for row in batch:
+                if row["remove"] is not None:
+                    tomb.add(json_key(row["remove"]))
+            for row in batch:
+                if row["add"] is not None:
+                    added.add(json_key(row["add"]))
+    L = lib()
+    ks = L.dkr_keyset_new()
+    for k in added:
+        L.dkr_keyset_or(ks, k, len(k), 1)
+    for k in tomb:
+        L.dkr_keyset_or(ks, k, len(k), 2)
+    return ks
+
+
+def _skip_file(b, cols, skipping):
+    """ScanImpl.applyDataSkipping over one checkpoint file's selected rows (oracle/skipping.py; the
+    integral fast path in oracle/dk_skip.c)."""
+    from . import skipping as sk
+    node, types = skipping
+    sk.apply_to_column(cols.get(STATS_LEAF), b.selected, node, types)
+    b.skipped = True
 
 
 def _pm_json_protocol(p):

@@ -327,3 +327,79 @@ def keep(stats: str | None, node, types) -> bool:
     if stats is None:
         return True
     return evaluate(node, decode_stats(stats, types), types) is not False
+
+
+# ---- the C fast path (oracle/dk_skip.c) for predicates over integral stats only ----------------
+_INTEGRAL = {"long": 0, "integer": 1, "short": 2, "byte": 3}
+_CMP_OPS = {"<": 3, "<=": 4, ">": 5, ">=": 6, "=": 7}
+
+
+def compile_integral(node, types):
+    """(paths blob, number of paths, int64 program) for dk_skip.c when every referenced stat is
+    long / integer / short / byte and every literal an integer in the long range; else None (the
+    caller evaluates every row with `keep`)."""
+    import struct
+    if not types or len(types) > 16 or any(t not in _INTEGRAL for t in types.values()):
+        return None
+    order = list(types)
+    ops = []
+
+    def emit(n):
+        k = n[0]
+        if k == "stat":
+            ops.append((1, order.index(n[1])))
+        elif k == "lit":
+            v = n[1]
+            if isinstance(v, bool) or not isinstance(v, int) or not -(1 << 63) <= v < (1 << 63):
+                raise ValueError
+            ops.append((2, v))
+        elif k in ("AND", "OR"):
+            emit(n[1]); emit(n[2]); ops.append((8 if k == "AND" else 9, 0))
+        elif k in _CMP_OPS:
+            emit(n[1]); emit(n[2]); ops.append((_CMP_OPS[k], 0))
+        else:
+            raise ValueError
+    try:
+        emit(node)
+    except (ValueError, IndexError):
+        return None
+    if len(ops) > 60:
+        return None
+    blob = bytearray()
+    for p in order:
+        if len(p) > 8:
+            return None
+        blob += bytes([_INTEGRAL[types[p]], len(p)])
+        for comp in p:
+            b = comp.encode("utf-8")
+            blob += struct.pack("<H", len(b)) + b
+    return bytes(blob), len(order), np.array([x for op in ops for x in op], dtype=np.int64)
+
+
+def apply_to_column(col, sel, node, types, max_def=2):
+    """Data skipping over one decoded add.stats column: sel (uint8, one per row) is cleared where
+    COALESCE(predicate, true) is FALSE. Integral predicates go through dk_skip.c (rows it is unsure
+    about, and every row of other predicates, through `keep`); other selected rows through `keep`."""
+    import ctypes as C
+    rows = np.nonzero(sel)[0]
+    if col is None or not len(rows):
+        return sel
+    prog = compile_integral(node, types)
+    if prog is not None:
+        from .ref import lib
+        blob, n_paths, ops = prog
+        defer = np.zeros(len(sel), dtype=np.uint8)
+        chars = col.chars if col.chars is not None and len(col.chars) else np.zeros(1, np.uint8)
+        P = C.c_void_p
+        nd = lib().dkr_skip_eval(P(chars.ctypes.data), P(col.offs.ctypes.data), P(col.row_def.ctypes.data),
+                                 max_def, P(sel.ctypes.data), P(defer.ctypes.data), len(sel), blob, len(blob),
+                                 n_paths, P(ops.ctypes.data), len(ops) // 2)
+        if nd < 0:
+            raise RuntimeError("dkr_skip_eval: malformed program")
+        rows = np.nonzero(defer)[0]
+    for i in rows:
+        i = int(i)
+        st = None if col.row_def[i] < max_def else col.string(i).decode("utf-8", "replace")
+        if not keep(st, node, types):
+            sel[i] = 0
+    return sel
