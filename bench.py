@@ -19,11 +19,13 @@ beside it:
 Multi-GPU, one process per GPU over RCCL: `python bench.py --gpus N` starts N ranks itself (a
 parent that never touches the GPU spawns N children with RANK / LOCAL_RANK / WORLD_SIZE), or the
 driver's `torch.distributed.run --nproc-per-node N bench.py --gpus N` does. C3 is ONE table whose
-checkpoint row groups are cut into N contiguous runs (delta_amd/shard.py): each rank reads, decodes
-and reconciles its run against the whole (replicated) commit tail and consumes its own scan files;
-counters and consumer sums are all-reduced. The device-step region ends with the exchange that puts
-every rank's counters and packed selection bitmaps on rank 0 in one RCCL all-gather into one device
-buffer (shard.SelectionExchange), timed separately as `exchange_ms`.
+checkpoint row groups are cut into N contiguous runs (delta_amd/shard.py). With the default
+`--exchange owner`, each rank parses only the commit files j = rank (mod N), the keys are owned by
+hash, and three RCCL all-to-alls resolve every commit-tail action and every checkpoint row at its
+key's owner (shard.OwnerExchange; `owner_exchange_ms`); each rank consumes its own scan files and
+counters and consumer sums are all-reduced. `--exchange allgather` keeps the whole commit tail on
+every rank and ends the device step with one RCCL all-gather of counters and selection bitmaps
+(shard.SelectionExchange, `exchange_ms`).
 
 `--dry-run`: no GPU; the launcher, the row-group planning and the exchange run over gloo on the CPU
 with placeholder selections (tests/test_bench_launcher.py).
@@ -340,13 +342,18 @@ def main(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the whole-table CPU baseline (default: nproc, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--full-row-steps", type=int, default=2,
+                    help="timed steps of the full-row consumer reported beside the headline (0: skip)")
     ap.add_argument("--device-steps", type=int, default=None, help="timed device-only steps (default: --steps)")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo rehearsal of launcher + planning + exchange")
-    ap.add_argument("--exchange", default="allgather", choices=["allgather", "alltoall"],
-                    help="multi-GPU C3: allgather = every rank probes against its own copy of the commit-tail key "
-                         "table and the selection bitmaps are all-gathered; alltoall = checkpoint rows are routed "
-                         "to the owner of their path hash over RCCL all-to-all and the answers come back by the "
-                         "reverse all-to-all (DESIGN.md §6)")
+    ap.add_argument("--exchange", default="owner", choices=["owner", "allgather", "alltoall"],
+                    help="multi-GPU: owner (default) = each rank parses 1/N of the commit files and the key table "
+                         "is partitioned by key hash: commit-tail actions, then every checkpoint row's key hash, "
+                         "then the hash hits' keys go to their owner over RCCL all-to-all and are answered exactly "
+                         "(delta-spark's repartition by path); allgather = every rank parses the whole commit tail "
+                         "and probes its rows against its own copy of the key table, selection bitmaps all-gathered; "
+                         "alltoall = allgather's tail, checkpoint rows pre-filtered by their path-hash owner "
+                         "(DESIGN.md §6)")
     ap.add_argument("--workdir", default=None)
     args = ap.parse_args(argv)
 
@@ -421,7 +428,9 @@ def main(argv=None):
     def sum_over_ranks(xs):
         return [int(round(v)) for v in reduce_over_ranks(xs, dist.ReduceOp.SUM if dist else None)]
 
+    t0 = time.perf_counter()
     eng = K.GpuEngine(device=local if world > 1 else 0, timing=True)
+    engine_create_ms = (time.perf_counter() - t0) * 1e3     # includes the code-object / allocator warm-up
 
     # ---- region 3: snapshot load (cold: code-object load + first allocations; warm: median of 5) ----
     t0 = time.perf_counter()
@@ -451,6 +460,11 @@ def main(argv=None):
             os.remove(crc)
 
     a2a = args.exchange == "alltoall" and cfg["shared"] and world > 1
+    owner = None
+    if args.exchange == "owner" and cfg["shared"] and world > 1:
+        from delta_amd import shard
+        owner = shard.OwnerExchange(device="cuda")
+    owner_ms = []
     a2a_ms = []
 
     def hash_exchange(side):
@@ -468,7 +482,7 @@ def main(argv=None):
             col, op, lit = cfg["predicate"]
             sb = sb.withFilter(Predicate(op, Column(col), Literal.ofLong(lit)))
         if cfg["shared"] and world > 1:
-            sb = sb.withShard(world, rank, exchange=hash_exchange if a2a else None)
+            sb = sb.withShard(world, rank, exchange=hash_exchange if a2a else None, owner=owner)
         return sb.build()
 
     # ---- region 1: the device step over inputs resident in HBM (roofline) ----
@@ -480,7 +494,7 @@ def main(argv=None):
     n_tail = int(scan.tail.rows)
     bytes_read, bytes_written = scan.ckpt.traffic() if scan.ckpt else (0, 0)
     exchange = None
-    if dist is not None and cfg["shared"] and not a2a:
+    if dist is not None and cfg["shared"] and not a2a and owner is None:
         from delta_amd import shard
         meta = [(scan.ckpt_index[fi], scan.ckpt.row_offset(fi), scan.ckpt.num_rows(fi))
                 for fi in range(len(scan.ckpt_files or []))]
@@ -492,6 +506,8 @@ def main(argv=None):
         nonlocal merged
         scan.run()
         scan.sync()
+        if owner is not None:
+            owner_ms.append(dict(owner.ms))
         if exchange is not None:
             import ctypes as C
             import torch
@@ -515,6 +531,9 @@ def main(argv=None):
     if a2a:      # the result stays where it was decoded; the counters of the world, for the report
         device_counters = tuple(scan.tail_metrics.as_tuple()[i] + v
                                 for i, v in enumerate(sum_over_ranks(scan.ckpt_metrics.as_tuple())))
+    if owner is not None:     # every rank's counters are its share: tail actions it owns + its rows
+        device_counters = tuple(sum_over_ranks(scan.metrics.as_tuple()))
+    del owner_ms[:]
     barrier()
     stats0 = scan.kernel_stats()
     t0 = time.perf_counter()
@@ -535,14 +554,16 @@ def main(argv=None):
     step_gbs = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
     # roofline of the dominant kernel with a byte model (dk_parquet_kernel_traffic):
     # algorithmic bytes of one launch / its average launch time (HIP events on the replay stream)
-    modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy") if k in kern]
+    modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy", "k_probe") if k in kern]
     rk = max(modelled, key=lambda k: kern[k]) if modelled else None
     k_read, k_written = scan.ckpt.kernel_traffic(rk) if rk else (0, 0)
     k_bytes = k_read + k_written
     achieved = k_bytes / (kern[rk] * 1e-6) / 1e9 if rk else None
     pmc = pmc_traffic(rk, n_ckpt_rows, compression) if rk else None
     ckpt_files = list(scan.ckpt_files)
-    if cfg["shared"]:
+    if cfg["shared"] and owner is not None:
+        dev_units = sum_over_ranks([n_ckpt_rows + n_tail])[0]       # each rank parsed its share of the tail
+    elif cfg["shared"]:
         dev_units = sum_over_ranks([n_ckpt_rows])[0] + n_tail      # the tail is replicated, counted once
     else:
         dev_units = sum_over_ranks([n_ckpt_rows + n_tail])[0]
@@ -585,9 +606,10 @@ def main(argv=None):
                 else:
                     sel = np.ones(b.size, bool) if b.selection is None else b.selection
                     bits.append(np.packbits(sel, bitorder="little"))
+        b = v = None            # the consumer keeps no batch (a kept batch is copied out at close)
         consume_ms = (time.perf_counter() - t_c) * 1e3
-        seen = sc.metrics.addFilesSeen if not (cfg["shared"] and world > 1 and rank > 0) \
-            else sc.ckpt_metrics.addFilesSeen                  # the replicated tail counts once
+        seen = sc.metrics.addFilesSeen if not (cfg["shared"] and world > 1 and rank > 0 and owner is None) \
+            else sc.ckpt_metrics.addFilesSeen                  # a replicated tail counts once
         if capture_result:
             capture.update(counters=sc.metrics.as_tuple(), tail_paths=tail_paths, bits=bits)
         phases = dict(sc.prepare_ms)
@@ -621,6 +643,57 @@ def main(argv=None):
     value = seen_all / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
+    # ---- beside the headline: a consumer that reads every selected scan file's path, partition
+    # values and size (a connector's split planner, MultiThreadedTableReader.java:204-251), not only
+    # add.size (the JMH shape above) ----
+    FULL_LEAVES = ("add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
+                   "add.size")
+
+    def full_row_step():
+        sc = build_scan(snap)
+        n_sel = path_bytes = pv_entries = size_sum = d2h = 0
+        t_a = time.perf_counter()
+        for b in sc.getScanFiles(eng):
+            cols = [b.data[leaf] for leaf in FULL_LEAVES]
+            pc, kc, vc, sz = cols
+            sel = np.ones(b.size, bool) if b.selection is None else b.selection
+            lens = np.diff(pc.offs[:b.size + 1])                  # path bytes per row
+            nent = np.diff(kc.row_offs[:b.size + 1])              # partitionValues entries per row
+            path_bytes += int(lens.sum(where=sel))
+            pv_entries += int(nent.sum(where=sel))
+            size_sum += int(sz.fixed.view("<i8").sum(where=sel))
+            n_sel += int(np.count_nonzero(sel))
+            if b.file_index >= 0:                                 # device-decoded: the D2H of its leaves
+                d2h += sum(int(a.nbytes) for c in cols if c is not None
+                           for a in (c.row_def, c.row_offs, c.entry_def, c.fixed, c.offs, c.chars) if a is not None)
+        b = cols = pc = kc = vc = sz = sel = None
+        ms = (time.perf_counter() - t_a) * 1e3
+        phases = dict(sc.prepare_ms)
+        seen = sc.metrics.addFilesSeen if not (cfg["shared"] and world > 1 and rank > 0 and owner is None) \
+            else sc.ckpt_metrics.addFilesSeen
+        sc.close()
+        return seen, n_sel, path_bytes, pv_entries, size_sum, d2h, ms + phases.get("plan_files", 0) + \
+            phases.get("checkpoint_open", 0) + phases.get("device_run", 0)
+
+    full_row = None
+    if args.full_row_steps > 0:
+        full_row_step()                                          # warm-up
+        barrier()
+        t_f = time.perf_counter()
+        fr = [full_row_step() for _ in range(args.full_row_steps)]
+        barrier()
+        f_el = max_over_ranks(time.perf_counter() - t_f)
+        f_seen, f_sel, f_pb, f_pv, f_d2h = sum_over_ranks([sum(x[0] for x in fr), sum(x[1] for x in fr),
+                                                          sum(x[2] for x in fr), sum(x[3] for x in fr),
+                                                          sum(x[5] for x in fr)])
+        k = args.full_row_steps
+        full_row = {"consumer": "reads add.path, add.partitionValues and add.size of every selected scan file "
+                                "(path length, partition entries, size sum)",
+                    "ms_per_step": f_el / k * 1e3, "actions_per_s": f_seen / f_el, "steps": k,
+                    "selected_per_step": f_sel // k, "path_bytes_per_step": f_pb // k,
+                    "partition_entries_per_step": f_pv // k,
+                    "d2h_bytes_per_step": f_d2h // k, "leaves": list(FULL_LEAVES)}
+
     result = {
         "metric": METRIC,
         "value": value,
@@ -635,11 +708,14 @@ def main(argv=None):
         "dtype": "u8/int64",
         "data": "synthetic (seed 20250218; delta_amd/synth.py)",
         "config": {"workload": cfg["desc"] % rows, "name": args.config, "compression": compression,
-                   "parallelism": (("strong: checkpoint row groups in %d contiguous runs (one per GPU), commit tail "
-                                    "on every GPU; " % world +
-                                    ("checkpoint rows routed to the owner of their path hash and answered over RCCL "
-                                     "all-to-all (exchange=alltoall)" if a2a else
-                                     "device step ends with one RCCL all-gather of counters + selection bitmaps"))
+                   "parallelism": (("strong: checkpoint row groups in %d contiguous runs (one per GPU); " % world +
+                                    ("commit files round-robin over the GPUs; keys owned by hash: commit-tail actions, "
+                                     "checkpoint row hashes and hash hits' keys resolved by their owner over RCCL "
+                                     "all-to-all (exchange=owner)" if owner is not None else
+                                     "commit tail on every GPU; checkpoint rows routed to the owner of their path hash "
+                                     "and answered over RCCL all-to-all (exchange=alltoall)" if a2a else
+                                     "commit tail on every GPU; device step ends with one RCCL all-gather of counters "
+                                     "+ selection bitmaps"))
                                    if cfg["shared"] else "weak: one table per GPU"),
                    "exchange": args.exchange if (cfg["shared"] and world > 1) else None,
                    "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail,
@@ -655,9 +731,13 @@ def main(argv=None):
                         "actions_per_s": dev_units * dsteps / dev_elapsed if dev_elapsed else None,
                         "counters": list(device_counters),
                         "exchange_ms": (sorted(ex_ms)[len(ex_ms) // 2] if ex_ms else a2a_dev),
+                        "owner_exchange_ms": ({k: round(sorted(m[k] for m in owner_ms)[len(owner_ms) // 2], 3)
+                                               for k in owner_ms[0]} if owner_ms else None),
                         "prepare_s": prepare_s},
+        "full_row_consume": full_row,
         "snapshot_load_ms": snapshot_ms,
         "snapshot_load_cold_ms": snapshot_cold_ms,
+        "engine_create_ms": engine_create_ms,
         "snapshot_load_cold_phases_ms": cold_phases,
         "snapshot_load_with_crc_ms": snapshot_crc_ms,
         "snapshot_load_phases_ms": {k: round(v, 3) for k, v in snap.load_ms.items()},

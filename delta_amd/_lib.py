@@ -98,7 +98,13 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_reader_open", "dk_reader_next", "dk_reader_num_rows", "dk_batch_release", "dk_reader_close",
            "dk_dv_load", "dk_dv_num_bits", "dk_dv_bitmap", "dk_dv_selection", "dk_dv_free", "dk_log_pm_scan",
            "dk_replay_stats_parsed_files", "dk_replay_ckpt_selection_bits_all",
-           "dk_replay_ckpt_selection_host", "dk_parquet_open_ms", "dk_replay_attach_checkpoint"]
+           "dk_replay_ckpt_selection_host", "dk_parquet_open_ms", "dk_replay_attach_checkpoint",
+           "dk_json_tail_file_steps", "dk_json_tail_file_row0", "dk_json_tail_rebase_steps", "dk_replay_set_owner", "dk_replay_owner_begin",
+           "dk_replay_owner_tail_counts", "dk_replay_owner_tail_pack", "dk_replay_owner_tail_resolve",
+           "dk_replay_owner_reseed", "dk_replay_owner_tail_finish", "dk_replay_owner_ckpt_counts",
+           "dk_replay_owner_ckpt_pack", "dk_replay_owner_ckpt_lookup", "dk_replay_owner_ckpt_apply",
+           "dk_replay_owner_cand_counts", "dk_replay_owner_cand_pack", "dk_replay_owner_cand_verify",
+           "dk_replay_owner_cand_finish"]
 
 
 def lib(build_if_missing=True):
@@ -180,6 +186,24 @@ def lib(build_if_missing=True):
         "dk_dv_free": (None, [P]),
         "dk_replay_stats_parsed_files": (C.c_int, [P]),
         "dk_log_pm_scan": (C.c_int, [C.POINTER(C.c_char_p), I32] + [C.POINTER(I64)] * 6 + [C.POINTER(I32)]),
+        "dk_json_tail_file_steps": (C.c_int, [P, C.POINTER(I32)]),
+        "dk_json_tail_file_row0": (C.c_int, [P, C.POINTER(I64)]),
+        "dk_json_tail_rebase_steps": (C.c_int, [P, C.POINTER(I32)]),
+        "dk_replay_set_owner": (C.c_int, [P, I32, I32]),
+        "dk_replay_owner_begin": (C.c_int, [P]),
+        "dk_replay_owner_tail_counts": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
+        "dk_replay_owner_tail_pack": (C.c_int, [P, P, P]),
+        "dk_replay_owner_tail_resolve": (C.c_int, [P, P, I64, P, I64, P, C.POINTER(I32)]),
+        "dk_replay_owner_reseed": (C.c_int, [P]),
+        "dk_replay_owner_tail_finish": (C.c_int, [P, P]),
+        "dk_replay_owner_ckpt_counts": (C.c_int, [P, C.POINTER(I64)]),
+        "dk_replay_owner_ckpt_pack": (C.c_int, [P, P]),
+        "dk_replay_owner_ckpt_lookup": (C.c_int, [P, P, I64, P]),
+        "dk_replay_owner_ckpt_apply": (C.c_int, [P, P]),
+        "dk_replay_owner_cand_counts": (C.c_int, [P, C.POINTER(I64), C.POINTER(I64)]),
+        "dk_replay_owner_cand_pack": (C.c_int, [P, P, P]),
+        "dk_replay_owner_cand_verify": (C.c_int, [P, P, I64, P, I64, P]),
+        "dk_replay_owner_cand_finish": (C.c_int, [P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -307,6 +307,19 @@ struct ProbeCols {
   int64_t row_tag;   // added to the row index in error reports
 };
 
+// Owner-partitioned reconciliation (multi-GPU "owner" mode): one key record routed to the rank that
+// owns its hash (h mod world), with the key's canonical bytes (canonical path stream, then the
+// dvUniqueId stream) travelling in a byte buffer alongside, in the same order. Commit-tail actions
+// carry their replay position (global batch step, row in batch); checkpoint candidates carry
+// kind JA_CKADD. src: the sender's index of the record's action / candidate.
+struct OwnerKeyRec {
+  uint64_t h;
+  int32_t kind, step, row;
+  int32_t key_len, canon_len;       // key bytes; the first canon_len are the path stream
+  int32_t src;
+};
+static_assert(sizeof(OwnerKeyRec) == 32, "OwnerKeyRec layout (dkgpu.h owner entry points)");
+
 // All checkpoint files of a replay for the one-launch probe: rows numbered across the files.
 struct ProbeSet {
   const ProbeCols* cols;       // per file (device memory)

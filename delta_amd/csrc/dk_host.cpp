@@ -70,6 +70,19 @@ void launch_a2a_apply(const ProbeSet&, const int32_t*, const uint8_t*, long long
                       const uint8_t*, uint32_t, int32_t*, unsigned int*, DState*, hipStream_t);
 void launch_probe(const ProbeCols&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                   uint8_t*, int32_t*, unsigned int*, DState*, hipStream_t);
+void launch_own_rowhash(const ProbeSet&, uint64_t*, uint32_t, uint64_t, DState*, hipStream_t);
+void launch_own_count(const ProbeSet&, const uint64_t*, int, unsigned long long*, unsigned long long*, hipStream_t);
+void launch_own_pack(const ProbeSet&, const uint64_t*, int, const unsigned long long*, uint64_t*, int32_t*, hipStream_t);
+void launch_own_lookup(const uint64_t*, long long, const Slot*, const uint32_t*, uint64_t, uint8_t*, hipStream_t);
+void launch_own_apply(const ProbeSet&, const int32_t*, const uint8_t*, long long, int32_t*, unsigned int*, DState*, hipStream_t);
+void launch_own_cand_len(const ProbeSet&, const int32_t*, long long, const uint64_t*, int, int32_t*, int32_t*, int32_t*,
+                         hipStream_t);
+void launch_own_cand_keys(const ProbeSet&, const int32_t*, long long, const uint64_t*, const int64_t*, const int64_t*,
+                          const int32_t*, const int32_t*, OwnerKeyRec*, uint8_t*, hipStream_t);
+void launch_own_verify(const OwnerKeyRec*, long long, const int64_t*, const uint8_t*, const Slot*, uint64_t,
+                       const DJsonAction*, const uint8_t*, uint8_t*, hipStream_t);
+void launch_own_cand_finish(const ProbeSet&, const int32_t*, const uint8_t*, long long, DState*, hipStream_t);
+int warm_kernels();
 }  // namespace dk
 
 using namespace dk;
@@ -97,6 +110,7 @@ struct dk_engine {
   dk_config cfg;
 };
 
+static int engine_warm(int device);
 extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
   dk_config c = cfg ? *cfg : dk_config{1024, 1024, 0, 0};
   if (c.parquet_batch_size <= 0) c.parquet_batch_size = 1024;
@@ -111,6 +125,7 @@ extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
     return fail("libdkgpu: no HIP device available (the GPU engine has no CPU fallback)");
   if (c.device < 0 || c.device >= ndev) return fail("libdkgpu: bad device ordinal");
   HIPOK(hipSetDevice(c.device));
+  if (engine_warm(c.device)) return 1;
   auto* e = new dk_engine();
   e->cfg = c;
   *out = e;
@@ -299,6 +314,27 @@ struct StreamH {
   ~StreamH() { if (s) { hipStreamSynchronize(s); stream_pool().put(s); } }
   int create() { s = stream_pool().get(); return s ? 0 : fail("hipStreamCreate failed"); }
 };
+
+// Warm-up at engine creation (once per device and process): the code objects' lazy load, a pooled
+// stream, a first launch on it, the first device / pinned blocks -- costs the first
+// getLatestSnapshot would otherwise pay.
+static int engine_warm(int device) {
+  static std::mutex warm_mu;
+  static std::vector<int> warmed;
+  std::lock_guard<std::mutex> lk(warm_mu);
+  if (std::find(warmed.begin(), warmed.end(), device) != warmed.end()) return 0;
+  warmed.push_back(device);
+  warm_kernels();
+  StreamH sh;
+  if (sh.create()) return 1;
+  DBuf d;
+  HBuf h;
+  if (d.alloc(1 << 20) || h.alloc(1 << 20)) return 1;
+  memset(h.data(), 0, 256);
+  launch_copy_zc(d.p, h.data(), 256, sh.s);
+  HIPOK(hipStreamSynchronize(sh.s));
+  return 0;
+}
 
 // ------------------------------------------------------------------------------------------------
 // Parquet footer (FileMetaData) + offset index
@@ -792,7 +828,7 @@ struct KTimer {
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
                           "k_snap_walk_link", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", "k_part_eval",
-                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", nullptr, nullptr};
+                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", "k_owner_route", "k_owner_resolve"};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -2533,6 +2569,30 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
   if (!p || !kernel || !p->prepared) return fail("dk_parquet_kernel_traffic: not prepared");
   const std::string k = kernel;
   int64_t rd = 0, wr = 0;
+  if (k == "k_probe") {
+    // k_probe_fast_all (+ k_probe_cand_all): per add row the path definition level and decode-time
+    // hash, a 4-byte fingerprint slot (at least), the selection byte; DV rows also read the DV leaves
+    // (storageType / offset definition levels, the two string offsets and chars, the offset value)
+    auto col = [&](size_t fi, const char* leaf) -> const DColumn* {
+      for (size_t li = 0; li < p->leaves.size(); li++)
+        if (p->leaves[li] == leaf) { const int ci = p->colmap[fi][li]; return ci >= 0 ? &p->h_cols[ci] : nullptr; }
+      return nullptr;
+    };
+    for (size_t fi = 0; fi < p->files.size(); fi++) {
+      const DColumn* path = col(fi, "add.path");
+      if (!path) continue;
+      const int64_t n = path->n_rows;
+      rd += n * (1 + 8 + 4);
+      wr += n;
+      const DColumn* st = col(fi, "add.deletionVector.storageType");
+      const DColumn* pid = col(fi, "add.deletionVector.pathOrInlineDv");
+      if (st && pid && !st->null_only) {
+        rd += n * (1 + 8 + 8 + 1 + 4) + st->n_chars + pid->n_chars;
+      }
+    }
+    *r = rd; *w = wr;
+    return 0;
+  }
   for (size_t ci = 0; ci < p->h_cols.size(); ci++) {
     const DColumn& c = p->h_cols[ci];
     const bool key = c.hash != nullptr;
@@ -2979,6 +3039,9 @@ struct dk_json_tail {
   CB col[JL_N];
   std::vector<int32_t> step, rowin;   // per row: batch step and row within batch
   int32_t n_steps = 0;
+  // per parsed file: first row, first step and batches (dk_json_tail_file_steps / _rebase_steps)
+  std::vector<int64_t> file_row0;
+  std::vector<int32_t> file_step0, file_nsteps;
 };
 
 namespace {
@@ -3199,6 +3262,9 @@ extern "C" int dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, 
   for (int fi = 0; fi < n_files; fi++) {
     TailPart& P = parts[fi];
     if (fi == n_files - n_checkpoint_files) t->ckpt_row0 = t->rows;
+    t->file_row0.push_back(t->rows);
+    t->file_step0.push_back(t->n_steps);
+    t->file_nsteps.push_back(P.n_steps);
     for (int k = 0; k < JL_N; k++) append_cb(t->col[k], P.col[k]);
     for (int32_t st : P.step) t->step.push_back(t->n_steps + st);
     t->rowin.insert(t->rowin.end(), P.rowin.begin(), P.rowin.end());
@@ -3206,7 +3272,43 @@ extern "C" int dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, 
     t->rows += P.rows;
     P = TailPart();
   }
+  t->file_row0.push_back(t->rows);
   *out = t.release();
+  return 0;
+}
+
+// batches of each parsed file (a file's lines in batches of json_batch_size; an empty file has none)
+extern "C" int dk_json_tail_file_steps(dk_json_tail* t, int32_t* steps) {
+  if (!t || !steps) return fail("dk_json_tail_file_steps: null argument");
+  for (size_t f = 0; f < t->file_nsteps.size(); f++) steps[f] = t->file_nsteps[f];
+  return 0;
+}
+
+// first row of each parsed file, and the row count at the end (n_files + 1 entries)
+extern "C" int dk_json_tail_file_row0(dk_json_tail* t, int64_t* row0) {
+  if (!t || !row0) return fail("dk_json_tail_file_row0: null argument");
+  for (size_t f = 0; f < t->file_row0.size(); f++) row0[f] = t->file_row0[f];
+  return 0;
+}
+
+// Renumber the batch steps so that file f's first batch is step0[f]: a rank that parsed only its
+// share of the commit files places its batches in the global replay order (ActionsIterator visits
+// the commit files newest first, LogSegment.java:166-178), which the owner-partitioned
+// reconciliation compares across ranks (R2 / R5: a remove tombstones adds of its own and later
+// batches).
+extern "C" int dk_json_tail_rebase_steps(dk_json_tail* t, const int32_t* step0) {
+  if (!t || !step0) return fail("dk_json_tail_rebase_steps: null argument");
+  const size_t nf = t->file_nsteps.size();
+  for (size_t f = 0; f < nf; f++) {
+    if (step0[f] < 0 || (int64_t)step0[f] + t->file_nsteps[f] > INT32_MAX - 1)
+      return fail("dk_json_tail_rebase_steps: step out of range");
+    const int32_t delta = step0[f] - t->file_step0[f];
+    for (int64_t row = t->file_row0[f]; row < t->file_row0[f + 1]; row++) t->step[row] += delta;
+    t->file_step0[f] = step0[f];
+  }
+  int32_t mx = 0;
+  for (size_t f = 0; f < nf; f++) mx = std::max(mx, t->file_step0[f] + t->file_nsteps[f]);
+  t->n_steps = mx;
   return 0;
 }
 
@@ -3441,6 +3543,22 @@ struct dk_replay {
   int64_t n_owned = 0, n_send = 0;
   std::vector<unsigned long long> xtot;
   int32_t xphase = 0;                     // 1: counted (run), 2: packed, 3: finished
+  // owner-partitioned reconciliation (dk_replay_set_owner, "owner" mode): this rank's commit-tail
+  // actions are routed to the owners of their keys; this rank owns the keys with h mod ow == orank,
+  // builds their table from the records routed to it (oacts / ocanon / oslots) and answers every
+  // rank's checkpoint rows for them
+  int32_t ow = 0, orank = 0;              // ow = 0: off
+  int32_t ophase = 0;                     // OP_* below
+  std::vector<DJsonAction> h_acts;        // own actions after k_json_canon (host copy)
+  std::vector<uint8_t> h_canon;
+  std::vector<int32_t> o_send_src;        // own action of each tail record, in send order
+  std::vector<int64_t> o_send_koff;       // its key bytes in the send buffer
+  DBuf d_oacts, d_ocanon, d_oslots, d_ofp, d_osel;
+  int64_t n_oacts = 0;
+  uint64_t omask = 0;
+  DBuf d_rowh;                            // key hash per checkpoint row (global row order)
+  int64_t n_ocand = 0;                    // checkpoint candidates (found by hash at their owner)
+  DBuf d_oc_plen, d_oc_dlen, d_oc_own, d_oc_rpos, d_oc_koff, d_oc_sendg, d_ov_koff;
   uint64_t mask = 0;
   uint32_t seed = 0;
   KTimer timer;
@@ -4141,12 +4259,14 @@ static int replay_ckpt_filters(dk_replay* r) {
   return 0;
 }
 
+static int owner_launch(dk_replay* r);
 extern "C" int dk_replay_run(dk_replay* r) {
   hipSetDevice(r->eng->cfg.device);
   r->have_result = false;
   r->h_csel_ready = false;
   if (r->ck && invalidate_mirrors(r->ck)) return 1;
   r->n_groups = 0;
+  if (r->ow > 0) return owner_launch(r);
   return replay_launch(r);
 }
 
@@ -4157,6 +4277,7 @@ extern "C" int dk_replay_run(dk_replay* r) {
 extern "C" int dk_replay_run_grouped(dk_replay* r, int32_t n_groups) {
   if (!r) return fail("null replay");
   if (n_groups < 1) return fail("dk_replay_run_grouped: n_groups must be >= 1");
+  if (r->ow > 0) return fail("dk_replay_run_grouped: owner mode runs ungrouped (dk_replay_run)");
   hipSetDevice(r->eng->cfg.device);
   r->have_result = false;
   r->h_csel_ready = false;
@@ -4313,10 +4434,411 @@ extern "C" int dk_replay_exchange_finish(dk_replay* r, const uint8_t* back) {
   return 0;
 }
 
+// ---- owner-partitioned reconciliation ("owner" mode) ----
+// Every rank parses only its share of the commit files (their batch steps rebased to the global
+// replay order, dk_json_tail_rebase_steps) and decodes only its share of the checkpoint. Each key
+// (URI(path), dvUniqueId) is owned by rank h mod world. One run, driven by the caller's collectives:
+//   begin; tail_counts / tail_pack -> (all-to-all) -> tail_resolve on the owner (the table of its
+//   keys, R2-R5 selection of the actions routed to it, counters) -> (reverse all-to-all) ->
+//   tail_finish (the origin's tail selection, then its partition / skipping filters);
+//   dk_replay_run (decode + key hash of every checkpoint row + routing counts); ckpt_counts /
+//   ckpt_pack -> (all-to-all of 8-byte hashes) -> ckpt_lookup -> (reverse) -> ckpt_apply (rows
+//   whose hash no tail key has are selected; the rest are candidates); cand_counts / cand_pack ->
+//   (all-to-all of candidate keys) -> cand_verify (byte-exact) -> (reverse) -> cand_finish;
+//   then dk_replay_sync.
+// A key-hash collision among an owner's tail keys is reported by tail_resolve; the caller reduces
+// the flag over the ranks and, if any is set, every rank calls dk_replay_owner_reseed and repeats the
+// tail exchange with the next seed.
+enum : int32_t { OP_IDLE = 0, OP_BEGUN, OP_TAIL_COUNTED, OP_TAIL_PACKED, OP_TAIL_RESOLVED, OP_TAIL_DONE, OP_DECODED,
+                 OP_CK_COUNTED, OP_CK_PACKED, OP_CK_APPLIED, OP_CAND_COUNTED, OP_CAND_PACKED, OP_DONE };
+
+static int owner_phase(dk_replay* r, int want, const char* who) {
+  if (!r) return fail(std::string(who) + ": null replay");
+  hipSetDevice(r->eng->cfg.device);
+  if (r->ow <= 0) return fail(std::string(who) + ": not in owner mode (dk_replay_set_owner)");
+  if (want >= 0 && r->ophase != want) return fail(std::string(who) + ": called out of order");
+  return 0;
+}
+
+extern "C" int dk_replay_set_owner(dk_replay* r, int32_t world, int32_t rank) {
+  if (!r) return fail("null replay");
+  if (world <= 1) { r->ow = 0; return 0; }
+  if (world > 64 || rank < 0 || rank >= world) return fail("dk_replay_set_owner: bad world / rank");
+  if (r->xw > 0) return fail("dk_replay_set_owner: the replay is in hash-exchange mode");
+  r->ow = world; r->orank = rank;
+  r->ophase = OP_IDLE;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_begin(dk_replay* r) {
+  if (owner_phase(r, -1, "dk_replay_owner_begin")) return 1;
+  r->have_result = false;
+  r->h_csel_ready = false;
+  r->n_groups = 0;
+  DState st0{};
+  st0.err_row = LLONG_MAX;
+  HIPOK(hipMemcpy(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice));
+  r->ophase = OP_BEGUN;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_tail_counts(dk_replay* r, int64_t* recs, int64_t* bytes) {
+  if (owner_phase(r, OP_BEGUN, "dk_replay_owner_tail_counts")) return 1;
+  hipStream_t s = r->stream;
+  const int na = (int)r->acts.size();
+  {
+    KTimer::Scope sc(&r->timer, 7, s);
+    launch_json_canon(r->d_acts.as<DJsonAction>(), na, r->d_jchars.as<uint8_t>(), r->d_canon.as<uint8_t>(), r->seed,
+                      r->d_state.as<DState>(), s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  r->h_acts.resize(na);
+  if (na) HIPOK(hipMemcpy(r->h_acts.data(), r->d_acts.p, na * sizeof(DJsonAction), hipMemcpyDeviceToHost));
+  r->h_canon.resize(r->d_canon.n);
+  if (r->d_canon.n) HIPOK(hipMemcpy(r->h_canon.data(), r->d_canon.p, r->d_canon.n, hipMemcpyDeviceToHost));
+  std::vector<std::vector<int32_t>> by(r->ow);
+  for (int i = 0; i < na; i++) {
+    const DJsonAction& a = r->h_acts[i];
+    if (a.kind == JA_NONE || a.status) continue;       // a key error: reported by dk_replay_sync
+    by[a.h % (uint64_t)r->ow].push_back(i);
+  }
+  r->o_send_src.clear();
+  r->o_send_koff.clear();
+  int64_t koff = 0;
+  for (int o = 0; o < r->ow; o++) {
+    recs[o] = (int64_t)by[o].size();
+    bytes[o] = 0;
+    for (int32_t i : by[o]) {
+      const int64_t kl = (int64_t)r->h_acts[i].canon_len + r->h_acts[i].dv_len;
+      r->o_send_src.push_back(i);
+      r->o_send_koff.push_back(koff);
+      koff += kl;
+      bytes[o] += kl;
+    }
+  }
+  r->ophase = OP_TAIL_COUNTED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_tail_pack(dk_replay* r, void* recs, void* keys) {
+  if (owner_phase(r, OP_TAIL_COUNTED, "dk_replay_owner_tail_pack")) return 1;
+  const size_t n = r->o_send_src.size();
+  std::vector<OwnerKeyRec> R(n);
+  std::vector<uint8_t> K;
+  for (size_t pos = 0; pos < n; pos++) {
+    const int32_t i = r->o_send_src[pos];
+    const DJsonAction& a = r->h_acts[i];
+    OwnerKeyRec& k = R[pos];
+    k.h = a.h; k.kind = a.kind; k.step = a.step; k.row = a.row;
+    k.key_len = a.canon_len + a.dv_len; k.canon_len = a.canon_len; k.src = i;
+    K.insert(K.end(), r->h_canon.begin() + a.canon_off, r->h_canon.begin() + a.canon_off + k.key_len);
+  }
+  if (n) HIPOK(hipMemcpy(recs, R.data(), n * sizeof(OwnerKeyRec), hipMemcpyHostToDevice));
+  if (!K.empty()) HIPOK(hipMemcpy(keys, K.data(), K.size(), hipMemcpyHostToDevice));
+  r->ophase = OP_TAIL_PACKED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_tail_resolve(dk_replay* r, const void* recs, int64_t n, const void* keys, int64_t nbytes,
+                                            uint8_t* answers, int32_t* flags) {
+  if (owner_phase(r, OP_TAIL_PACKED, "dk_replay_owner_tail_resolve")) return 1;
+  if (n < 0 || nbytes < 0 || n > INT32_MAX / 2) return fail("dk_replay_owner_tail_resolve: bad sizes");
+  hipStream_t s = r->stream;
+  std::vector<OwnerKeyRec> R(n);
+  if (n) HIPOK(hipMemcpy(R.data(), recs, n * sizeof(OwnerKeyRec), hipMemcpyDeviceToHost));
+  std::vector<DJsonAction> A(n);
+  int64_t koff = 0;
+  for (int64_t i = 0; i < n; i++) {
+    const OwnerKeyRec& k = R[i];
+    if (k.key_len < 0 || k.canon_len < 0 || k.canon_len > k.key_len || koff + k.key_len > nbytes ||
+        (k.kind != JA_ADD && k.kind != JA_REMOVE && k.kind != JA_CKADD))
+      return fail("dk_replay_owner_tail_resolve: malformed key record");
+    DJsonAction a{};
+    a.kind = k.kind; a.step = k.step; a.row = k.row;
+    a.canon_off = koff; a.canon_len = k.canon_len; a.dv_len = k.key_len - k.canon_len;
+    a.h = k.h;
+    A[i] = a;
+    koff += k.key_len;
+  }
+  if (koff != nbytes) return fail("dk_replay_owner_tail_resolve: key bytes do not match the records");
+  uint64_t cap = 1024;
+  while (cap < 2 * (uint64_t)n + 16) cap <<= 1;
+  r->omask = cap - 1;
+  r->n_oacts = n;
+  if (upload(r->d_oacts, A.data(), n * sizeof(DJsonAction), s)) return 1;
+  if (r->d_ocanon.alloc(nbytes + 64)) return 1;
+  if (nbytes) HIPOK(hipMemcpyAsync(r->d_ocanon.p, keys, nbytes, hipMemcpyDeviceToDevice, s));
+  if (r->d_oslots.alloc(cap * sizeof(Slot)) || r->d_ofp.alloc(cap * sizeof(uint32_t)) || r->d_osel.alloc(n + 16)) return 1;
+  DJsonAction* OA = r->d_oacts.as<DJsonAction>();
+  Slot* S = r->d_oslots.as<Slot>();
+  DState* st = r->d_state.as<DState>();
+  launch_slots_init(S, cap, s);
+  { KTimer::Scope sc(&r->timer, 8, s); launch_table_insert(OA, (int)n, S, r->omask, s); }
+  { KTimer::Scope sc(&r->timer, 9, s); launch_table_update(OA, (int)n, S, r->omask, r->d_ocanon.as<uint8_t>(), st, s); }
+  { KTimer::Scope sc(&r->timer, 10, s);
+    launch_json_select(OA, (int)n, S, r->omask, r->d_ocanon.as<uint8_t>(), r->d_osel.as<uint8_t>(), st, s); }
+  launch_table_fp(S, r->d_ofp.as<uint32_t>(), cap, s);
+  if (n) HIPOK(hipMemcpyAsync(answers, r->d_osel.p, n, hipMemcpyDeviceToDevice, s));
+  HIPOK(hipStreamSynchronize(s));
+  DState h{};
+  HIPOK(hipMemcpy(&h, r->d_state.p, sizeof h, hipMemcpyDeviceToHost));
+  *flags = h.err_flags & E_COLLISION;
+  r->ophase = OP_TAIL_RESOLVED;
+  return 0;
+}
+
+// after a collision anywhere: the next seed, the commit-tail counters cleared, the tail exchange again
+extern "C" int dk_replay_owner_reseed(dk_replay* r) {
+  if (owner_phase(r, -1, "dk_replay_owner_reseed")) return 1;
+  if (r->ophase != OP_TAIL_RESOLVED) return fail("dk_replay_owner_reseed: called out of order");
+  DState h{};
+  HIPOK(hipStreamSynchronize(r->stream));
+  HIPOK(hipMemcpy(&h, r->d_state.p, sizeof h, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 5; i++) h.counters[i] = 0;
+  h.err_flags &= ~E_COLLISION;
+  HIPOK(hipMemcpy(r->d_state.p, &h, sizeof h, hipMemcpyHostToDevice));
+  if (++r->seed > 64) return fail("replay: repeated key-hash collisions");
+  r->ophase = OP_BEGUN;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_tail_finish(dk_replay* r, const uint8_t* back) {
+  if (owner_phase(r, OP_TAIL_RESOLVED, "dk_replay_owner_tail_finish")) return 1;
+  hipStream_t s = r->stream;
+  const size_t n = r->o_send_src.size(), na = r->acts.size();
+  std::vector<uint8_t> hb(n), sel(na + 16, 0);
+  if (n) HIPOK(hipMemcpy(hb.data(), back, n, hipMemcpyDeviceToHost));
+  for (size_t pos = 0; pos < n; pos++) sel[r->o_send_src[pos]] = hb[pos] != 0;
+  if (upload(r->d_jsel, sel.data(), sel.size(), s)) return 1;
+  DState* st = r->d_state.as<DState>();
+  if (r->has_part && na) {                 // partition pruning on this rank's tail adds (before skipping)
+    KTimer::Scope sc(&r->timer, 18, s);
+    launch_part_eval(r->tail_maps, r->d_part.as<DPartProg>(), r->d_jsel.as<uint8_t>(), st, s);
+  }
+  if (r->has_skip && na) {                 // data skipping on this rank's selected tail adds
+    KTimer::Scope sc(&r->timer, 17, s);
+    StatsRows R{};
+    R.n = (int64_t)na; R.soff = r->d_tstats_off.as<int64_t>(); R.slen = r->d_tstats_len.as<int32_t>();
+    R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
+    launch_stats_eval(R, r->d_skip.as<DSkipProg>(), r->d_jsel.as<uint8_t>(), st, s);
+  }
+  r->ophase = OP_TAIL_DONE;
+  return 0;
+}
+
+static ProbeSet owner_probe_set(dk_replay* r) {
+  return ProbeSet{r->d_probe_cols.as<ProbeCols>(), r->d_probe_row0.as<int64_t>(), r->d_probe_sel.as<uint8_t* const>(),
+                  (int32_t)r->probe.size(), r->probe_row0.empty() ? 0 : r->probe_row0.back()};
+}
+
+// dk_replay_run in owner mode: the checkpoint decode, every row's key hash, the routing counts
+static int owner_launch(dk_replay* r) {
+  if (r->ophase != OP_TAIL_DONE) return fail("dk_replay_run (owner mode): finish the commit-tail exchange first");
+  hipStream_t s = r->stream;
+  r->probe_row0.assign(1, 0);
+  if (r->ck) {
+    dk_parquet* p = r->ck;
+    if (r->lazy && (ensure_open(p) || attach_upto(r, INT_MAX))) return 1;
+    HIPOK(hipEventRecord(r->ev_in, p->stream));
+    HIPOK(hipStreamWaitEvent(s, r->ev_in, 0));
+    DState st0{};
+    st0.err_row = LLONG_MAX;
+    HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
+    if (run_pipeline(p, 1, s, false)) return 1;
+    const size_t nf = r->probe.size();
+    r->probe_run = r->probe;
+    r->probe_row0.assign(nf + 1, 0);
+    r->probe_sel.resize(nf);
+    for (size_t fi = 0; fi < nf; fi++) {
+      if (r->seed != kDecodeSeed) r->probe_run[fi].path_hash = nullptr;   // the decode-time hashes use seed 0
+      r->probe_row0[fi + 1] = r->probe_row0[fi] + r->probe_run[fi].n_rows;
+      r->probe_sel[fi] = r->d_csel[fi]->as<uint8_t>();
+    }
+    const int64_t total = r->probe_row0[nf];
+    if (total >= (1ll << 31) - 1) return fail("owner mode: more than 2^31 checkpoint rows on one rank");
+    if (upload(r->d_probe_cols, r->probe_run.data(), nf * sizeof(ProbeCols), s) ||
+        upload(r->d_probe_row0, r->probe_row0.data(), (nf + 1) * 8, s) ||
+        upload(r->d_probe_sel, r->probe_sel.data(), nf * sizeof(uint8_t*), s)) return 1;
+    if (r->d_rowh.n < (size_t)total * 8 + 64 && r->d_rowh.alloc((size_t)total * 8 + 64)) return 1;
+    if (r->d_cand.n < (size_t)total * 4 + 64 && r->d_cand.alloc((size_t)total * 4 + 64)) return 1;
+    if (r->d_xg.n < (size_t)total * 4 + 64 && r->d_xg.alloc((size_t)total * 4 + 64)) return 1;
+    long long chunk;
+    const int nb = a2a_blocks(total, &chunk);
+    if (r->d_xbc.n < (size_t)nb * r->ow * 8 + 64 && r->d_xbc.alloc((size_t)nb * r->ow * 8 + 64)) return 1;
+    if (r->d_xtot.n < (size_t)r->ow * 8 + 64 && r->d_xtot.alloc((size_t)r->ow * 8 + 64)) return 1;
+    HIPOK(hipMemsetAsync(r->d_xtot.p, 0, (size_t)r->ow * 8, s));
+    HashSink kd; kd.hs.init(kHashSeed(r->seed)); kd.n = 0;       // dvUniqueId stream of "no DV"
+    dv_emit(false, nullptr, 0, nullptr, 0, false, 0, kd);
+    const uint64_t h_nodv = kd.hs.final_(kd.n);
+    const ProbeSet PS = owner_probe_set(r);
+    KTimer::Scope sc(&r->timer, 22, s);
+    launch_own_rowhash(PS, r->d_rowh.as<uint64_t>(), r->seed, h_nodv, r->d_state.as<DState>(), s);
+    if (total > 0)
+      launch_own_count(PS, r->d_rowh.as<uint64_t>(), r->ow, r->d_xbc.as<unsigned long long>(),
+                       r->d_xtot.as<unsigned long long>(), s);
+  }
+  r->ophase = OP_DECODED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_ckpt_counts(dk_replay* r, int64_t* counts) {
+  if (owner_phase(r, OP_DECODED, "dk_replay_owner_ckpt_counts")) return 1;
+  HIPOK(hipStreamSynchronize(r->stream));
+  r->n_send = 0;
+  for (int o = 0; o < r->ow; o++) counts[o] = 0;
+  if (r->ck && r->probe_row0.back() > 0) {
+    r->xtot.assign(r->ow, 0);
+    HIPOK(hipMemcpy(r->xtot.data(), r->d_xtot.p, (size_t)r->ow * 8, hipMemcpyDeviceToHost));
+    for (int o = 0; o < r->ow; o++) { counts[o] = (int64_t)r->xtot[o]; r->n_send += counts[o]; }
+  }
+  r->ophase = OP_CK_COUNTED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_ckpt_pack(dk_replay* r, uint64_t* send) {
+  if (owner_phase(r, OP_CK_COUNTED, "dk_replay_owner_ckpt_pack")) return 1;
+  hipStream_t s = r->stream;
+  if (r->n_send > 0) {
+    KTimer::Scope sc(&r->timer, 22, s);
+    launch_own_pack(owner_probe_set(r), r->d_rowh.as<uint64_t>(), r->ow, r->d_xbc.as<unsigned long long>(), send,
+                    r->d_xg.as<int32_t>(), s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  r->ophase = OP_CK_PACKED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_ckpt_lookup(dk_replay* r, const uint64_t* recv, int64_t n, uint8_t* flags) {
+  if (owner_phase(r, -1, "dk_replay_owner_ckpt_lookup")) return 1;
+  if (r->ophase < OP_TAIL_RESOLVED) return fail("dk_replay_owner_ckpt_lookup: the owner's key table is not built");
+  hipStream_t s = r->stream;
+  {
+    KTimer::Scope sc(&r->timer, 23, s);
+    launch_own_lookup(recv, n, r->d_oslots.as<Slot>(), r->d_ofp.as<uint32_t>(), r->omask, flags, s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int dk_replay_owner_ckpt_apply(dk_replay* r, const uint8_t* back) {
+  if (owner_phase(r, OP_CK_PACKED, "dk_replay_owner_ckpt_apply")) return 1;
+  hipStream_t s = r->stream;
+  if (r->ck) {
+    KTimer::Scope sc(&r->timer, 22, s);
+    launch_own_apply(owner_probe_set(r), r->d_xg.as<int32_t>(), back, r->n_send, r->d_cand.as<int32_t>(),
+                     r->d_cand_n.as<unsigned int>(), r->d_state.as<DState>(), s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  r->ophase = OP_CK_APPLIED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_cand_counts(dk_replay* r, int64_t* recs, int64_t* bytes) {
+  if (owner_phase(r, OP_CK_APPLIED, "dk_replay_owner_cand_counts")) return 1;
+  hipStream_t s = r->stream;
+  for (int o = 0; o < r->ow; o++) recs[o] = bytes[o] = 0;
+  unsigned int nc = 0;
+  if (r->ck) HIPOK(hipMemcpy(&nc, r->d_cand_n.p, sizeof nc, hipMemcpyDeviceToHost));
+  r->n_ocand = nc;
+  if (nc) {
+    if (r->d_oc_plen.alloc(nc * 4 + 16) || r->d_oc_dlen.alloc(nc * 4 + 16) || r->d_oc_own.alloc(nc * 4 + 16)) return 1;
+    const ProbeSet PS = owner_probe_set(r);
+    {
+      KTimer::Scope sc(&r->timer, 22, s);
+      launch_own_cand_len(PS, r->d_cand.as<int32_t>(), nc, r->d_rowh.as<uint64_t>(), r->ow, r->d_oc_plen.as<int32_t>(),
+                          r->d_oc_dlen.as<int32_t>(), r->d_oc_own.as<int32_t>(), s);
+    }
+    HIPOK(hipStreamSynchronize(s));
+    std::vector<int32_t> plen(nc), dlen(nc), own(nc), cand(nc);
+    HIPOK(hipMemcpy(plen.data(), r->d_oc_plen.p, nc * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(dlen.data(), r->d_oc_dlen.p, nc * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(own.data(), r->d_oc_own.p, nc * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(cand.data(), r->d_cand.p, nc * 4, hipMemcpyDeviceToHost));
+    // owner-major send order (stable): record position and key offset of each candidate
+    std::vector<int64_t> start(r->ow + 1, 0), kstart(r->ow + 1, 0);
+    for (unsigned i = 0; i < nc; i++) {
+      if (own[i] < 0 || own[i] >= r->ow) return fail("owner mode: bad candidate owner");
+      recs[own[i]]++;
+      bytes[own[i]] += plen[i] + dlen[i];
+    }
+    for (int o = 0; o < r->ow; o++) { start[o + 1] = start[o] + recs[o]; kstart[o + 1] = kstart[o] + bytes[o]; }
+    std::vector<int64_t> rpos(nc), koff(nc);
+    std::vector<int32_t> sendg(nc);
+    for (unsigned i = 0; i < nc; i++) {
+      const int o = own[i];
+      rpos[i] = start[o]++;
+      koff[i] = kstart[o];
+      kstart[o] += plen[i] + dlen[i];
+      sendg[rpos[i]] = cand[i];
+    }
+    if (upload(r->d_oc_rpos, rpos.data(), nc * 8, s) || upload(r->d_oc_koff, koff.data(), nc * 8, s) ||
+        upload(r->d_oc_sendg, sendg.data(), nc * 4, s)) return 1;
+    HIPOK(hipStreamSynchronize(s));
+  }
+  r->ophase = OP_CAND_COUNTED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_cand_pack(dk_replay* r, void* recs, void* keys) {
+  if (owner_phase(r, OP_CAND_COUNTED, "dk_replay_owner_cand_pack")) return 1;
+  hipStream_t s = r->stream;
+  if (r->n_ocand) {
+    KTimer::Scope sc(&r->timer, 22, s);
+    launch_own_cand_keys(owner_probe_set(r), r->d_cand.as<int32_t>(), r->n_ocand, r->d_rowh.as<uint64_t>(),
+                         r->d_oc_rpos.as<int64_t>(), r->d_oc_koff.as<int64_t>(), r->d_oc_plen.as<int32_t>(),
+                         r->d_oc_dlen.as<int32_t>(), (OwnerKeyRec*)recs, (uint8_t*)keys, s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  r->ophase = OP_CAND_PACKED;
+  return 0;
+}
+
+extern "C" int dk_replay_owner_cand_verify(dk_replay* r, const void* recs, int64_t n, const void* keys, int64_t nbytes,
+                                           uint8_t* answers) {
+  if (owner_phase(r, -1, "dk_replay_owner_cand_verify")) return 1;
+  if (r->ophase < OP_TAIL_RESOLVED) return fail("dk_replay_owner_cand_verify: the owner's key table is not built");
+  if (n < 0 || nbytes < 0) return fail("dk_replay_owner_cand_verify: bad sizes");
+  hipStream_t s = r->stream;
+  if (n) {
+    std::vector<OwnerKeyRec> R(n);
+    HIPOK(hipMemcpy(R.data(), recs, n * sizeof(OwnerKeyRec), hipMemcpyDeviceToHost));
+    std::vector<int64_t> koff(n);
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; i++) {
+      if (R[i].key_len < 0 || R[i].canon_len < 0 || R[i].canon_len > R[i].key_len)
+        return fail("dk_replay_owner_cand_verify: malformed key record");
+      koff[i] = k;
+      k += R[i].key_len;
+    }
+    if (k != nbytes) return fail("dk_replay_owner_cand_verify: key bytes do not match the records");
+    if (upload(r->d_ov_koff, koff.data(), n * 8, s)) return 1;
+    KTimer::Scope sc(&r->timer, 23, s);
+    launch_own_verify((const OwnerKeyRec*)recs, n, r->d_ov_koff.as<int64_t>(), (const uint8_t*)keys, r->d_oslots.as<Slot>(),
+                      r->omask, r->d_oacts.as<DJsonAction>(), r->d_ocanon.as<uint8_t>(), answers, s);
+  }
+  HIPOK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" int dk_replay_owner_cand_finish(dk_replay* r, const uint8_t* back) {
+  if (owner_phase(r, OP_CAND_PACKED, "dk_replay_owner_cand_finish")) return 1;
+  hipStream_t s = r->stream;
+  if (r->ck) {
+    if (r->n_ocand) {
+      KTimer::Scope sc(&r->timer, 22, s);
+      launch_own_cand_finish(owner_probe_set(r), r->d_oc_sendg.as<int32_t>(), back, r->n_ocand, r->d_state.as<DState>(), s);
+    }
+    if (replay_ckpt_filters(r)) return 1;
+  }
+  r->ophase = OP_DONE;
+  return 0;
+}
+
 extern "C" int dk_replay_sync(dk_replay* r) {
   hipSetDevice(r->eng->cfg.device);   // this thread may not have used the device yet
   hipStream_t s = r->stream;
   if (r->xw > 0 && r->xphase != 3) return fail("dk_replay_sync: the exchange-mode run has not finished its exchange");
+  if (r->ow > 0 && r->ophase != OP_DONE) return fail("dk_replay_sync: the owner-mode run has not finished its exchanges");
   if (r->ck && r->n_groups > 0 && r->xw == 0)      // a lazy grouped run: the groups not issued yet
     while (r->grp_issued + 1 < (int)r->grp_f0.size()) if (issue_group(r)) return 1;
   if (r->ck && ensure_open(r->ck)) return 1;        // (an asynchronous open has finished by now)
@@ -4327,6 +4849,7 @@ extern "C" int dk_replay_sync(dk_replay* r) {
     if (r->ck) { r->ck->timer.collect(); if (check_state(r->ck)) return 1; }
     HIPOK(hipMemcpy(&r->h_state, r->d_state.p, sizeof(DState), hipMemcpyDeviceToHost));
     if (r->h_state.err_flags & E_COLLISION) {     // 64-bit key-hash collision: rebuild with a new seed
+      if (r->ow > 0) return fail("replay (owner mode): a key-hash collision was not resolved by the tail exchange");
       r->seed++;
       const int32_t xw = r->xw;                   // (exchange mode: the rebuilt run probes locally)
       r->xw = 0;

@@ -19,6 +19,7 @@ import json
 import os
 import re
 import time
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -1011,20 +1012,37 @@ class ScanBuilder:
         self.read_stats = flag
         return self
 
-    def withShard(self, world, rank, exchange=None):
+    def withShard(self, world, rank, exchange=None, owner=None):
         """Reconcile only this rank's checkpoint row groups (delta_amd/shard.py). exchange: None (the
         probe runs against this rank's own copy of the commit-tail key table), or a callable that
         drives the hash(path)-owner exchange for this rank (shard.exchange_hash_owner over
         torch.distributed, or an in-process loopback), called with the scan's ExchangeSide after
-        every run."""
+        every run. owner: the owner-partitioned reconciliation (shard.OwnerExchange or a loopback):
+        this rank parses only its share of the commit files, and the key table of the keys it owns
+        answers every rank's rows for them."""
         self.shard = (int(world), int(rank))
         self.exchange = exchange
+        self.owner = owner
+        if exchange is not None and owner is not None:
+            raise ValueError("withShard: one exchange mode at a time")
         return self
 
     def build(self):
         sc = GpuScan(self.snapshot, self.read_stats, self.shard, self.predicate)
         sc.exchange = getattr(self, "exchange", None)
+        sc.owner = getattr(self, "owner", None) if self.shard and self.shard[0] > 1 else None
         return sc
+
+
+def _own_column(c):
+    """A Column whose arrays are its own (copies of a zero-copy view's)."""
+    import copy
+    o = copy.copy(c)
+    for a in ("row_def", "row_offs", "entry_def", "fixed", "offs", "chars"):
+        v = getattr(c, a, None)
+        if isinstance(v, np.ndarray):
+            setattr(o, a, v.copy())
+    return o
 
 
 class LazyColumns(dict):
@@ -1078,6 +1096,7 @@ class FilteredColumnarBatch:
     source: str = ""
     file_index: int = -1          # replay-order checkpoint file index; -1 = commit tail
     row_offset: int = 0           # file row of this batch's first row (row-group shards)
+    commit_index: int = -1        # owner mode: the commit file's replay-order index (tail batches)
 
     def selected_rows(self):
         if self.selection is None:
@@ -1130,6 +1149,7 @@ class GpuScan:
         self.ckpt_metrics = ScanMetrics()
         self.replay = None
         self.prepare_ms = {}
+        self._handed = weakref.WeakValueDictionary()   # zero-copy checkpoint batches handed out (_detach_batches)
 
     def table_root(self):
         """tableRoot = dataPath.toUri().toString() (ActiveAddFilesIterator.java:251)."""
@@ -1147,13 +1167,43 @@ class GpuScan:
         import threading
         tail_box = {}
 
+        owner = getattr(self, "owner", None)
+        parts = self.snapshot._json_checkpoint_parts()
+        if owner is not None:
+            # owner mode: this rank parses the commit files j = rank (mod world) of the replay order
+            # (newest first) and, on rank 0, the JSON manifest; their batch steps are renumbered in
+            # the global replay order once the ranks' batch counts are known (owner.global_steps)
+            world, rank = self.shard
+            self.tail_commits = [j for j in range(len(commits)) if j % world == rank]
+            self.tail_parts = list(range(len(commits), len(commits) + len(parts))) if rank == 0 else []
+            mine = [commits[j] for j in self.tail_commits]
+            parts = parts if rank == 0 else []
+        else:
+            mine = commits
+
         def parse_tail():
             # the tail, then the replay's commit-tail half (action table + key-table inputs)
             t = time.perf_counter()
             try:
-                tail = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], self.read_stats,
-                                checkpoint_paths=self.snapshot._json_checkpoint_parts())
+                tail = JsonTail(engine, [d.path for d in mine], [d.version for d in mine], self.read_stats,
+                                checkpoint_paths=parts)
                 tail_box["tail"] = tail
+                if owner is not None:
+                    files = self.tail_commits + self.tail_parts
+                    steps = (C.c_int32 * max(1, len(files)))()
+                    check(lib().dk_json_tail_file_steps(tail._h, steps))
+                    local = np.zeros(len(commits) + len(self.snapshot._json_checkpoint_parts()), np.int64)
+                    for k, j in enumerate(files):
+                        local[j] = steps[k]
+                    total = np.asarray(owner.global_steps(local), dtype=np.int64)
+                    step0 = np.concatenate([[0], np.cumsum(total)])
+                    if step0[-1] >= (1 << 31) - 1:
+                        raise DkError("owner mode: more than 2^31 commit-tail batches")
+                    base = (C.c_int32 * max(1, len(files)))(*[int(step0[j]) for j in files])
+                    check(lib().dk_json_tail_rebase_steps(tail._h, base))
+                    row0 = (C.c_int64 * (len(files) + 1))()
+                    check(lib().dk_json_tail_file_row0(tail._h, row0))
+                    self.tail_file_rows = [(files[k], int(row0[k]), int(row0[k + 1])) for k in range(len(files))]
                 tail_box["ms"] = (time.perf_counter() - t) * 1e3
                 t = time.perf_counter()
                 rh = C.c_void_p()
@@ -1189,6 +1239,8 @@ class GpuScan:
         self.prepare_ms["replay_attach"] = (time.perf_counter() - t3) * 1e3
         if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
             check(lib().dk_replay_set_exchange(self._rh, self.shard[0], self.shard[1]))
+        if getattr(self, "owner", None) is not None:
+            check(lib().dk_replay_set_owner(self._rh, self.shard[0], self.shard[1]))
         if self.partition is not None:
             from . import partitions as pp
             pprog = pp.pack(self.partition, dk_part_program)
@@ -1267,6 +1319,10 @@ class GpuScan:
     def run(self):
         """The device step: commit-tail keys + table, checkpoint decode, probe, selection (with an
         exchange: decode + routing, the exchange, then the probe of the rows the owners flagged)."""
+        if getattr(self, "owner", None) is not None:
+            from .shard import OwnerSide
+            self.owner(OwnerSide(self))            # the commit-tail exchange, dk_replay_run, the row exchanges
+            return
         check(lib().dk_replay_run(self._rh))
         if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
             from .shard import ExchangeSide
@@ -1310,9 +1366,12 @@ class GpuScan:
         if self.replay is None:
             self.prepare(engine)
             self.replay = True
+        else:
+            self._detach_batches()          # the rerun reuses the pinned blocks earlier batches view
         t0 = time.perf_counter()
         groups = scan_groups(len(self.ckpt_files or []))
-        exchanging = getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1
+        exchanging = (getattr(self, "exchange", None) is not None or getattr(self, "owner", None) is not None) \
+            and self.shard and self.shard[0] > 1
         if groups and not exchanging:
             # grouped: batches go out as their group of files is decoded and probed; the counters are
             # final once the iterator is exhausted (ScanImpl's metrics are read after it, too)
@@ -1333,7 +1392,24 @@ class GpuScan:
     def _batches(self, grouped=False):
         root = self.table_root()
         leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else [])
-        if self.tail.rows:
+        if self.tail.rows and getattr(self, "owner", None) is not None:
+            # owner mode: this rank's commit files, one batch each, tagged with their replay-order
+            # index (commit_index) so that the ranks' batches merge in the reference's order
+            sel = np.zeros(self.tail.rows, dtype=np.uint8)
+            check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
+            n_commits = len(self.snapshot.log_segment.deltas)
+            for j, a, b in self.tail_file_rows:
+                if b <= a:
+                    continue
+                cols = LazyColumns(leaves, lambda leaf, a=a, b=b: self.tail.column(leaf).slice_rows(a, b))
+                if j < n_commits:
+                    fb = FilteredColumnarBatch(cols, root, b - a, sel[a:b].view(bool), "json-tail")
+                else:                       # the V2 JSON manifest's rows (rank 0): first checkpoint batch
+                    fb = FilteredColumnarBatch(cols, root, b - a, sel[a:b].view(bool),
+                                               self.snapshot._json_checkpoint_parts()[0], -1, 0)
+                fb.commit_index = j
+                yield fb
+        elif self.tail.rows:
             sel = np.zeros(self.tail.rows, dtype=np.uint8)
             check(lib().dk_replay_json_selection(self._rh, sel.ctypes.data, self.tail.rows))
             r0 = int(self.tail.ckpt_row0)
@@ -1357,14 +1433,41 @@ class GpuScan:
             check(lib().dk_replay_ckpt_selection_host(self._rh, fi, C.byref(ptr)))
             sel = np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_bool)), shape=(n,)) if n else np.zeros(0, bool)
             cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf, copy=False))
-            yield FilteredColumnarBatch(cols, root, int(n), sel, path, self.ckpt_index[fi],
-                                        int(self.ckpt.row_offset(fi)))
+            fb = FilteredColumnarBatch(cols, root, int(n), sel, path, self.ckpt_index[fi],
+                                       int(self.ckpt.row_offset(fi)))
+            fb._file = fi
+            self._handed[id(fb)] = fb
+            yield fb
         if grouped:
             self.sync()                     # the counters (and any error the waits did not see)
             if self.ckpt is not None and self.ckpt.async_open:
                 self._open_phases()
 
+    def _detach_batches(self):
+        """Checkpoint batches handed out by getScanFiles view the library's pinned selection and
+        column mirrors (zero-copy). Before a rerun or close recycles those blocks, every batch still
+        referenced gets its own copies of its selection and of every leaf, so that it stays valid
+        after the iterator and the scan are closed, as the reference's batches do."""
+        live = list(getattr(self, "_handed", {}).values())
+        self._handed = weakref.WeakValueDictionary()
+        for b in live:
+            if b.selection is not None:
+                b.selection = np.array(b.selection, copy=True)
+            fi = b._file
+            for leaf in b.data.keys():
+                got = dict.get(b.data, leaf)
+                if got is None and dict.__contains__(b.data, leaf):
+                    continue                                  # fetched: absent from the file
+                if got is not None:
+                    dict.__setitem__(b.data, leaf, _own_column(got))
+                else:
+                    c = self.ckpt.column(fi, leaf, copy=True)
+                    dict.__setitem__(b.data, leaf, c if c.present else None)
+            b.data._fetch = None
+
     def close(self):
+        if getattr(self, "_handed", None):
+            self._detach_batches()
         if getattr(self, "_rh", None):
             lib().dk_replay_free(self._rh)
             self._rh = None

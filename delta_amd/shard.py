@@ -345,3 +345,341 @@ def exchange_local(sides):
             a = sum(seg[:s])
             parts.append(f[a:a + seg[s]].to(sends[s].device))
         sides[s].finish(torch.cat(parts) if parts else torch.zeros(0, dtype=torch.uint8))
+
+
+# ------------------------------------------------------------------------------------------------
+# owner-partitioned reconciliation ("owner" mode)
+#
+# delta-spark repartitions ALL actions by path and resolves each partition with one owner
+# (spark/src/main/scala/org/apache/spark/sql/delta/Snapshot.scala:476-485). Here the key
+# (URI(path), dvUniqueId) with hash h belongs to rank h mod world. Every rank parses only the commit
+# files j = rank (mod world) (their batches renumbered in the global replay order) and decodes only
+# its row groups of the checkpoint; three exchanges resolve everything exactly:
+#   1. commit-tail key records (32 B + the canonical key bytes) to their owners; each owner builds
+#      the table of its keys and selects the actions routed to it (R2-R5); the answers come back;
+#   2. every checkpoint row's 8-byte key hash to its owner; a hash no owned tail key has decides the
+#      row (selected); the rest come back as candidates;
+#   3. the candidates' canonical keys to their owners, answered byte-exactly (selected / duplicate /
+#      tombstoned).
+# No rank holds the whole commit tail; the ScanMetrics counters are summed over the ranks.
+# ------------------------------------------------------------------------------------------------
+REC_BYTES = 32                      # dk OwnerKeyRec
+
+
+class OwnerSide:
+    """One rank's side of the owner-partitioned reconciliation over a GpuScan's replay. Buffers are
+    torch uint8 / int64 tensors on the scan's GPU; every library call returns with its stream
+    drained."""
+
+    def __init__(self, scan):
+        import torch
+        self.scan = scan
+        self.world, self.rank = scan.shard
+        self.rh = scan._rh
+        self.device = torch.device("cuda", torch.cuda.current_device())
+
+    def _lib(self):
+        from ._lib import check, lib
+        return check, lib()
+
+    def _buf(self, n, dtype=None):
+        import torch
+        return torch.empty(max(1, n), dtype=dtype or torch.uint8, device=self.device)[:n]
+
+    def _in(self, t):
+        import torch
+        t = t.to(self.device).contiguous()
+        torch.cuda.current_stream().synchronize()          # the collective's data has landed
+        return t
+
+    def begin(self):
+        check, L = self._lib()
+        check(L.dk_replay_owner_begin(self.rh))
+
+    def tail_counts(self):
+        import ctypes as C
+        import numpy as np
+        check, L = self._lib()
+        recs, nbytes = np.zeros(self.world, np.int64), np.zeros(self.world, np.int64)
+        check(L.dk_replay_owner_tail_counts(self.rh, recs.ctypes.data_as(C.POINTER(C.c_int64)),
+                                            nbytes.ctypes.data_as(C.POINTER(C.c_int64))))
+        return recs, nbytes
+
+    def tail_pack(self, n, nbytes):
+        import ctypes as C
+        check, L = self._lib()
+        recs, keys = self._buf(n * REC_BYTES), self._buf(nbytes)
+        check(L.dk_replay_owner_tail_pack(self.rh, C.c_void_p(recs.data_ptr()), C.c_void_p(keys.data_ptr())))
+        return recs, keys
+
+    def tail_resolve(self, recs, keys):
+        import ctypes as C
+        check, L = self._lib()
+        recs, keys = self._in(recs), self._in(keys)
+        n = recs.numel() // REC_BYTES
+        ans, flags = self._buf(n), C.c_int32(0)
+        check(L.dk_replay_owner_tail_resolve(self.rh, C.c_void_p(recs.data_ptr()), n, C.c_void_p(keys.data_ptr()),
+                                             keys.numel(), C.c_void_p(ans.data_ptr()), C.byref(flags)))
+        return ans, int(flags.value)
+
+    def reseed(self):
+        check, L = self._lib()
+        check(L.dk_replay_owner_reseed(self.rh))
+
+    def tail_finish(self, back):
+        import ctypes as C
+        check, L = self._lib()
+        back = self._in(back)
+        check(L.dk_replay_owner_tail_finish(self.rh, C.c_void_p(back.data_ptr())))
+
+    def run(self):
+        check, L = self._lib()
+        check(L.dk_replay_run(self.rh))
+
+    def ckpt_counts(self):
+        import ctypes as C
+        import numpy as np
+        check, L = self._lib()
+        c = np.zeros(self.world, np.int64)
+        check(L.dk_replay_owner_ckpt_counts(self.rh, c.ctypes.data_as(C.POINTER(C.c_int64))))
+        return c
+
+    def ckpt_pack(self, n):
+        import ctypes as C
+        import torch
+        check, L = self._lib()
+        send = self._buf(n, torch.int64)
+        check(L.dk_replay_owner_ckpt_pack(self.rh, C.c_void_p(send.data_ptr())))
+        return send
+
+    def ckpt_lookup(self, recv):
+        import ctypes as C
+        check, L = self._lib()
+        recv = self._in(recv)
+        flags = self._buf(recv.numel())
+        check(L.dk_replay_owner_ckpt_lookup(self.rh, C.c_void_p(recv.data_ptr()), recv.numel(),
+                                            C.c_void_p(flags.data_ptr())))
+        return flags
+
+    def ckpt_apply(self, back):
+        import ctypes as C
+        check, L = self._lib()
+        back = self._in(back)
+        check(L.dk_replay_owner_ckpt_apply(self.rh, C.c_void_p(back.data_ptr())))
+
+    def cand_counts(self):
+        import ctypes as C
+        import numpy as np
+        check, L = self._lib()
+        recs, nbytes = np.zeros(self.world, np.int64), np.zeros(self.world, np.int64)
+        check(L.dk_replay_owner_cand_counts(self.rh, recs.ctypes.data_as(C.POINTER(C.c_int64)),
+                                            nbytes.ctypes.data_as(C.POINTER(C.c_int64))))
+        return recs, nbytes
+
+    def cand_pack(self, n, nbytes):
+        import ctypes as C
+        check, L = self._lib()
+        recs, keys = self._buf(n * REC_BYTES), self._buf(nbytes)
+        check(L.dk_replay_owner_cand_pack(self.rh, C.c_void_p(recs.data_ptr()), C.c_void_p(keys.data_ptr())))
+        return recs, keys
+
+    def cand_verify(self, recs, keys):
+        import ctypes as C
+        check, L = self._lib()
+        recs, keys = self._in(recs), self._in(keys)
+        n = recs.numel() // REC_BYTES
+        ans = self._buf(n)
+        check(L.dk_replay_owner_cand_verify(self.rh, C.c_void_p(recs.data_ptr()), n, C.c_void_p(keys.data_ptr()),
+                                            keys.numel(), C.c_void_p(ans.data_ptr())))
+        return ans
+
+    def cand_finish(self, back):
+        import ctypes as C
+        check, L = self._lib()
+        back = self._in(back)
+        check(L.dk_replay_owner_cand_finish(self.rh, C.c_void_p(back.data_ptr())))
+
+
+class OwnerExchange:
+    """The owner-partitioned reconciliation over torch.distributed (RCCL over xGMI when `device` is
+    "cuda", gloo on the CPU): ScanBuilder.withShard(world, rank, owner=OwnerExchange(...)). Each
+    step is timed into `ms` (phase -> milliseconds of the last run)."""
+
+    def __init__(self, group=None, device=None):
+        import torch
+        self.group = group
+        # "cuda" is pinned to this thread's current GPU now: global_steps runs on the scan's tail thread
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device == "cuda" else device
+        self.ms = {}
+        self.bytes_sent = 0
+
+    def global_steps(self, local):
+        """Batches of every commit file (replay order): this rank's counts summed over the ranks.
+        Called from the scan's commit-tail thread."""
+        import contextlib
+        import torch
+        import torch.distributed as dist
+        dev = self._dev()
+        with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
+            t = torch.as_tensor(local, dtype=torch.int64).to(dev)
+            dist.all_reduce(t, group=self.group)
+            return t.cpu().numpy()
+
+    def _dev(self):
+        import torch
+        return torch.device(self.device) if self.device is not None else torch.device("cpu")
+
+    def _a2a(self, send, send_counts, recv_counts=None):
+        """all_to_all_single of a 1-D tensor cut into per-destination runs; recv_counts exchanged
+        first unless given. Returns (received tensor on the transport device, recv_counts)."""
+        import torch
+        import torch.distributed as dist
+        dev = self._dev()
+        send = send.to(dev)
+        sc = [int(x) for x in send_counts]
+        if recv_counts is None:
+            c = torch.tensor(sc, dtype=torch.int64, device=dev)
+            rc = torch.empty_like(c)
+            dist.all_to_all_single(rc, c, group=self.group)
+            recv_counts = [int(x) for x in rc.cpu().tolist()]
+        rcl = [int(x) for x in recv_counts]
+        recv = torch.empty(max(1, sum(rcl)), dtype=send.dtype, device=dev)[:sum(rcl)]
+        dist.all_to_all_single(recv, send, output_split_sizes=rcl, input_split_sizes=sc, group=self.group)
+        self.bytes_sent += send.numel() * send.element_size()
+        return recv, rcl
+
+    def _any(self, flag):
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([int(flag)], dtype=torch.int64, device=self._dev())
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def __call__(self, side):
+        import time
+        t0 = time.perf_counter()
+        self.bytes_sent = 0
+        side.begin()
+        while True:
+            recs_c, bytes_c = side.tail_counts()
+            recs, keys = side.tail_pack(int(recs_c.sum()), int(bytes_c.sum()))
+            rrecs, rrc = self._a2a(recs, recs_c * REC_BYTES)
+            rkeys, _ = self._a2a(keys, bytes_c)
+            ans, flag = side.tail_resolve(rrecs, rkeys)
+            if self._any(flag):                  # a hash collision at some owner: all ranks reseed
+                side.reseed()
+                continue
+            back, _ = self._a2a(ans, [c // REC_BYTES for c in rrc], recs_c)
+            side.tail_finish(back)
+            break
+        t1 = time.perf_counter()
+        side.run()
+        c = side.ckpt_counts()
+        t2 = time.perf_counter()
+        send = side.ckpt_pack(int(c.sum()))
+        recv, rc = self._a2a(send, c)
+        flags = side.ckpt_lookup(recv)
+        back, _ = self._a2a(flags, rc, c)
+        side.ckpt_apply(back)
+        cr, cb = side.cand_counts()
+        recs, keys = side.cand_pack(int(cr.sum()), int(cb.sum()))
+        rrecs, rrc = self._a2a(recs, cr * REC_BYTES)
+        rkeys, _ = self._a2a(keys, cb)
+        ans = side.cand_verify(rrecs, rkeys)
+        back, _ = self._a2a(ans, [x // REC_BYTES for x in rrc], cr)
+        side.cand_finish(back)
+        t3 = time.perf_counter()
+        self.ms = {"tail_exchange": (t1 - t0) * 1e3, "decode_hash": (t2 - t1) * 1e3, "row_exchange": (t3 - t2) * 1e3}
+
+
+class OwnerLoopback:
+    """The owner exchange between `world` scans in ONE process (tests and single-GPU rehearsals):
+    the scans are prepared one after another (global_steps answers from the whole commit tail,
+    counted once up front), then run() drives every side's exchanges in lockstep."""
+
+    def __init__(self, global_steps):
+        import numpy as np
+        self._steps = np.asarray(global_steps, dtype=np.int64)
+        self.sides = {}
+
+    @classmethod
+    def for_table(cls, engine, snapshot):
+        """Batches of every commit file (and JSON manifest part) from one parse of the whole tail."""
+        import ctypes as C
+        from ._lib import check, lib
+        from .kernel import JsonTail
+        commits = list(reversed(snapshot.log_segment.deltas))
+        parts = snapshot._json_checkpoint_parts()
+        t = JsonTail(engine, [d.path for d in commits], [d.version for d in commits], False, checkpoint_paths=parts)
+        n = len(commits) + len(parts)
+        steps = (C.c_int32 * max(1, n))()
+        check(lib().dk_json_tail_file_steps(t._h, steps))
+        t.close()
+        return cls([steps[i] for i in range(n)])
+
+    def global_steps(self, local):
+        return self._steps
+
+    def __call__(self, side):
+        self.sides[side.rank] = side       # run() drives them once every rank's side has arrived
+
+    @staticmethod
+    def _route(sends):
+        """sends[s] = (1-D tensor, per-destination counts) -> per destination (concatenation over
+        sources, per-source counts)."""
+        import torch
+        world = len(sends)
+        out = []
+        for d in range(world):
+            parts, counts = [], []
+            for s in range(world):
+                t, cnt = sends[s]
+                a = int(sum(cnt[:d]))
+                parts.append(t[a:a + int(cnt[d])])
+                counts.append(int(cnt[d]))
+            dev = next((p.device for p in parts if p.numel()), sends[d][0].device)
+            out.append((torch.cat([p.to(dev) for p in parts]) if parts else sends[d][0][:0], counts))
+        return out
+
+    def run(self, scans):
+        """Every scan's run() with this loopback as its owner, then the exchanges in lockstep."""
+        self.sides = {}
+        for sc in scans:
+            sc.run()                            # registers the side
+        sides = [self.sides[r] for r in range(len(scans))]
+        world = len(sides)
+        for s in sides:
+            s.begin()
+        while True:
+            cnts = [s.tail_counts() for s in sides]
+            packed = [s.tail_pack(int(r.sum()), int(b.sum())) for s, (r, b) in zip(sides, cnts)]
+            rrecs = self._route([(p[0], r * REC_BYTES) for p, (r, _) in zip(packed, cnts)])
+            rkeys = self._route([(p[1], b) for p, (_, b) in zip(packed, cnts)])
+            res = [sides[d].tail_resolve(rrecs[d][0], rkeys[d][0]) for d in range(world)]
+            if any(f for _, f in res):
+                for s in sides:
+                    s.reseed()
+                continue
+            back = self._route([(res[d][0], [c // REC_BYTES for c in rrecs[d][1]]) for d in range(world)])
+            for s in range(world):
+                sides[s].tail_finish(back[s][0])
+            break
+        for s in sides:
+            s.run()
+        cs = [s.ckpt_counts() for s in sides]
+        sends = [s.ckpt_pack(int(c.sum())) for s, c in zip(sides, cs)]
+        recv = self._route([(t, c) for t, c in zip(sends, cs)])
+        flags = [sides[d].ckpt_lookup(recv[d][0]) for d in range(world)]
+        back = self._route([(flags[d], recv[d][1]) for d in range(world)])
+        for s in range(world):
+            sides[s].ckpt_apply(back[s][0])
+        cc = [s.cand_counts() for s in sides]
+        packed = [s.cand_pack(int(r.sum()), int(b.sum())) for s, (r, b) in zip(sides, cc)]
+        rrecs = self._route([(p[0], r * REC_BYTES) for p, (r, _) in zip(packed, cc)])
+        rkeys = self._route([(p[1], b) for p, (_, b) in zip(packed, cc)])
+        ans = [sides[d].cand_verify(rrecs[d][0], rkeys[d][0]) for d in range(world)]
+        back = self._route([(ans[d], [c // REC_BYTES for c in rrecs[d][1]]) for d in range(world)])
+        for s in range(world):
+            sides[s].cand_finish(back[s][0])
+        for sc in scans:
+            sc.sync()

@@ -391,6 +391,57 @@ int  dk_replay_exchange_counts(dk_replay* r, int64_t* counts);
 int  dk_replay_exchange_pack(dk_replay* r, uint64_t* send);
 int  dk_replay_exchange_filter(dk_replay* r, const uint64_t* recv, int64_t n, uint8_t* flags);
 int  dk_replay_exchange_finish(dk_replay* r, const uint8_t* back);
+
+/* Owner-partitioned reconciliation (multi-GPU "owner" mode): delta-spark's
+ * repartition of ALL actions by path with one resolver per key (spark/src/main/scala/org/apache/
+ * spark/sql/delta/Snapshot.scala:476-485) over ActiveAddFilesIterator's rules
+ * (KA/internal/replay/ActiveAddFilesIterator.java:164-234). Each rank parses only its share of the
+ * commit files and decodes only its share of the checkpoint; the key (URI(path), dvUniqueId) with
+ * hash h is owned by rank h mod world. Key records are dk OwnerKeyRec (32 bytes: u64 h; i32 kind,
+ * step, row, key_len, canon_len, src) with their canonical key bytes in a byte buffer alongside, in
+ * the same order; every buffer below is device memory (the caller's RCCL all-to-alls move them).
+ *   dk_json_tail_file_steps     batches per parsed commit file (the caller all-reduces them)
+ *   dk_json_tail_rebase_steps   the files' first batch in the GLOBAL replay order (before replay_create)
+ *   dk_replay_set_owner         owner mode for this replay (world <= 64)
+ *   dk_replay_owner_begin       a new run: counters and error state cleared
+ *   dk_replay_owner_tail_counts records / key bytes this rank sends to each rank (int64[world] each)
+ *   dk_replay_owner_tail_pack   the records and key bytes, owner-major
+ *   dk_replay_owner_tail_resolve owner: the key table of the records received (R2-R5 selection of
+ *                               each, commit-tail counters), one answer byte per record (1: the add
+ *                               is selected), *flags = E_COLLISION (4) on a 64-bit hash collision
+ *   dk_replay_owner_reseed      after a collision on any rank: next seed, repeat from tail_counts
+ *   dk_replay_owner_tail_finish origin: the answers (in send order) -> this rank's tail selection
+ *   dk_replay_run               decode + key hash of every checkpoint row + routing counts
+ *   dk_replay_owner_ckpt_counts / _pack   8-byte records {h} per rank, owner-major
+ *   dk_replay_owner_ckpt_lookup owner: 1 = a tail key has exactly this hash, 0 = none
+ *   dk_replay_owner_ckpt_apply  origin: rows answered 0 are selected, the rest are candidates
+ *   dk_replay_owner_cand_counts / _pack   the candidates' key records + canonical key bytes
+ *   dk_replay_owner_cand_verify owner, byte-exact: 0 = no tail key equals it (selected),
+ *                               1 = a JSON add (duplicate), 2 = a tombstone only
+ *   dk_replay_owner_cand_finish origin: the final selection, counters, then partition / skipping
+ * then dk_replay_sync. The five counters are split: commit-tail counters of the actions this rank
+ * owns, checkpoint counters of the rows this rank decoded; their sums over the ranks are the
+ * reference's. */
+int  dk_json_tail_file_steps(dk_json_tail* t, int32_t* steps);
+int  dk_json_tail_file_row0(dk_json_tail* t, int64_t* row0);     /* first row per file + total (n_files + 1) */
+int  dk_json_tail_rebase_steps(dk_json_tail* t, const int32_t* step0);
+int  dk_replay_set_owner(dk_replay* r, int32_t world, int32_t rank);
+int  dk_replay_owner_begin(dk_replay* r);
+int  dk_replay_owner_tail_counts(dk_replay* r, int64_t* recs, int64_t* bytes);
+int  dk_replay_owner_tail_pack(dk_replay* r, void* recs, void* keys);
+int  dk_replay_owner_tail_resolve(dk_replay* r, const void* recs, int64_t n, const void* keys, int64_t nbytes,
+                                  uint8_t* answers, int32_t* flags);
+int  dk_replay_owner_reseed(dk_replay* r);
+int  dk_replay_owner_tail_finish(dk_replay* r, const uint8_t* back);
+int  dk_replay_owner_ckpt_counts(dk_replay* r, int64_t* counts);
+int  dk_replay_owner_ckpt_pack(dk_replay* r, uint64_t* send);
+int  dk_replay_owner_ckpt_lookup(dk_replay* r, const uint64_t* recv, int64_t n, uint8_t* flags);
+int  dk_replay_owner_ckpt_apply(dk_replay* r, const uint8_t* back);
+int  dk_replay_owner_cand_counts(dk_replay* r, int64_t* recs, int64_t* bytes);
+int  dk_replay_owner_cand_pack(dk_replay* r, void* recs, void* keys);
+int  dk_replay_owner_cand_verify(dk_replay* r, const void* recs, int64_t n, const void* keys, int64_t nbytes,
+                                 uint8_t* answers);
+int  dk_replay_owner_cand_finish(dk_replay* r, const uint8_t* back);
 /* Checkpoint Parquet writer (Table.checkpoint's ParquetHandler.writeParquetFileAtomically,
  * DefaultParquetHandler.java:110-163): CHECKPOINT_SCHEMA (SingleAction.java:30-37), encoded on the
  * device. Rows come in iterator order as row groups: action rows built by the caller as JSON lines

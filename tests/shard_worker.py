@@ -1,7 +1,8 @@
 """One rank of tests/test_shard.py::test_gpu_two_processes_gloo (not a test module): scan this
 rank's row-group shard on the GPU, gather counters + selection bitmaps over gloo, and have rank 0
-write them to a JSON file. Usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR/PORT=.. python shard_worker.py TABLE OUT [alltoall]
-(alltoall: the probe goes through the hash(path)-owner exchange, its collectives over gloo)"""
+write them to a JSON file. Usage: RANK=.. WORLD_SIZE=.. MASTER_ADDR/PORT=.. python shard_worker.py TABLE OUT [allgather|alltoall|owner]
+(alltoall: the probe goes through the hash(path)-owner exchange; owner: the owner-partitioned
+reconciliation; their collectives over gloo)"""
 import json
 import os
 import sys
@@ -20,13 +21,20 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     eng = K.GpuEngine()
     snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
-    a2a = len(sys.argv) > 3 and sys.argv[3] == "alltoall"
-    scan = snap.getScanBuilder().withShard(world, rank, exchange=shard.exchange_hash_owner if a2a else None).build()
+    mode = sys.argv[3] if len(sys.argv) > 3 else "allgather"
+    if mode == "owner":      # owner-partitioned: every rank's counters are its share of the world's
+        scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerExchange()).build()
+    else:
+        scan = snap.getScanBuilder().withShard(world, rank, exchange=shard.exchange_hash_owner if mode == "alltoall"
+                                               else None).build()
     scan.prepare(eng)
     scan.run()
     scan.sync()
-    counters, sels = shard.gather_selections(shard.scan_units(scan), scan.tail_metrics.as_tuple(),
-                                             scan.ckpt_metrics.as_tuple())
+    if mode == "owner":
+        counters, sels = shard.gather_selections(shard.scan_units(scan), (0,) * 5, scan.metrics.as_tuple())
+    else:
+        counters, sels = shard.gather_selections(shard.scan_units(scan), scan.tail_metrics.as_tuple(),
+                                                 scan.ckpt_metrics.as_tuple())
     if rank == 0:
         files = {}
         for f, r0, n, bits in sels:

@@ -240,7 +240,7 @@ def test_gpu_row_group_shards(tmp_path, world, spec):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["allgather", "alltoall"])
+@pytest.mark.parametrize("mode", ["allgather", "alltoall", "owner"])
 def test_gpu_two_processes_gloo(tmp_path, mode):
     """Two processes on the GPU, each scanning its row-group shard with the product (alltoall: its
     rows routed to their path-hash owners and answered back), merge counters and selection bitmaps
