@@ -104,7 +104,8 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_owner_reseed", "dk_replay_owner_tail_finish", "dk_replay_owner_ckpt_counts",
            "dk_replay_owner_ckpt_pack", "dk_replay_owner_ckpt_lookup", "dk_replay_owner_ckpt_apply",
            "dk_replay_owner_cand_counts", "dk_replay_owner_cand_pack", "dk_replay_owner_cand_verify",
-           "dk_replay_owner_cand_finish"]
+           "dk_replay_owner_cand_finish", "dk_json_parse_stats", "dk_parsed_stats_column", "dk_parsed_stats_eval",
+           "dk_parsed_stats_free"]
 
 
 def lib(build_if_missing=True):
@@ -204,6 +205,10 @@ def lib(build_if_missing=True):
         "dk_replay_owner_cand_pack": (C.c_int, [P, P, P]),
         "dk_replay_owner_cand_verify": (C.c_int, [P, P, I64, P, I64, P]),
         "dk_replay_owner_cand_finish": (C.c_int, [P, P]),
+        "dk_json_parse_stats": (C.c_int, [P, P, I64, P, P, P, P, I32, C.POINTER(P)]),
+        "dk_parsed_stats_column": (C.c_int, [P, I32, P, P]),
+        "dk_parsed_stats_eval": (C.c_int, [P, P, P]),
+        "dk_parsed_stats_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

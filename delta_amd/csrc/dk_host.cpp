@@ -83,6 +83,10 @@ void launch_own_verify(const OwnerKeyRec*, long long, const int64_t*, const uint
                        const DJsonAction*, const uint8_t*, uint8_t*, hipStream_t);
 void launch_own_cand_finish(const ProbeSet&, const int32_t*, const uint8_t*, long long, DState*, hipStream_t);
 int warm_kernels();
+void launch_json_parse_stats(const uint8_t*, const int64_t*, const uint8_t*, const uint8_t*, long long, const DSkipProg*,
+                             long long*, uint32_t*, DState*, hipStream_t);
+void launch_parsed_eval(const uint8_t*, const int64_t*, long long, const DSkipProg*, const long long*, const uint32_t*,
+                        uint8_t*, hipStream_t);
 }  // namespace dk
 
 using namespace dk;
@@ -3811,20 +3815,17 @@ extern "C" int dk_replay_attach_checkpoint(dk_replay* r, dk_parquet* ckpt) {
 }
 
 
-extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog) {
-  static_assert(sizeof(dk_skip_program) == sizeof(DSkipProg), "dk_skip_program layout");
-  if (!r) return fail("null replay");
-  if (!prog) { r->has_skip = false; return 0; }
-  DSkipProg P;
-  memcpy(&P, prog, sizeof P);
+// validate a data-skipping program (layout dk_skip_program); `who` prefixes the error
+static int check_skip_program(const DSkipProg& P, const char* who) {
+  const std::string W = who;
   if (P.n_paths < 0 || P.n_paths > SK_MAX_PATHS || P.n_ops <= 0 || P.n_ops > SK_MAX_OPS)
-    return fail("dk_replay_set_skipping: bad program size");
+    return fail(W + ": bad program size");
   for (int p = 0; p < P.n_paths; p++) {
     if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DOUBLE)
-      return fail("dk_replay_set_skipping: bad stats path");
+      return fail(W + ": bad stats path");
     for (int d = 0; d < P.path_depth[p]; d++)
       if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
-        return fail("dk_replay_set_skipping: bad stats path name");
+        return fail(W + ": bad stats path name");
   }
   int depth = 0;
   bool fstat[SK_MAX_OPS + 1] = {false};       // stack slot holds a float / double stats value
@@ -3832,7 +3833,7 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   for (int k = 0; k < P.n_ops; k++) {
     const int op = P.op[k];
     if (op == OP_STAT) {
-      if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail("dk_replay_set_skipping: bad stat");
+      if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail(W + ": bad stat");
       const int t = P.path_type[P.arg[k]];
       fstat[depth] = t == SK_FLOAT || t == SK_DOUBLE;
       nlit[depth] = false;
@@ -3840,33 +3841,167 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
     }
     else if (op == OP_FCMP) {                   // only on a float / double stat, threshold in names
       const long long off = P.lit[k] & 0xffffffffll, len = P.lit[k] >> 32;
-      if (depth < 1 || !fstat[depth - 1]) return fail("dk_replay_set_skipping: FCMP needs a float stat");
+      if (depth < 1 || !fstat[depth - 1]) return fail(W + ": FCMP needs a float stat");
       // (the threshold text is followed by the comparison's rank run, two int64s)
-      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len + 16 > SK_NAMES) return fail("dk_replay_set_skipping: bad FCMP");
+      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len + 16 > SK_NAMES) return fail(W + ": bad FCMP");
       fstat[depth - 1] = false;
       nlit[depth - 1] = false;
     }
     else if (op == OP_LIT) { fstat[depth] = false; nlit[depth] = P.arg[k] != 0; depth++; }
-    else if (op == OP_TIMEADD) { if (depth < 1) return fail("dk_replay_set_skipping: stack underflow"); }
+    else if (op == OP_TIMEADD) { if (depth < 1) return fail(W + ": stack underflow"); }
     else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
-      if (P.arg[k] < 0 || P.lit[k] < 0 || P.lit[k] + P.arg[k] > SK_NAMES) return fail("dk_replay_set_skipping: bad string literal");
+      if (P.arg[k] < 0 || P.lit[k] < 0 || P.lit[k] + P.arg[k] > SK_NAMES) return fail(W + ": bad string literal");
       fstat[depth] = false;
       nlit[depth] = false;
       depth++;
     }
     else if (op >= OP_LT && op <= OP_OR) {
-      if (depth < 2) return fail("dk_replay_set_skipping: stack underflow");
+      if (depth < 2) return fail(W + ": stack underflow");
       // a float stat compares only through FCMP, or with a null literal (the result is null)
       if ((fstat[depth - 1] && !nlit[depth - 2]) || (fstat[depth - 2] && !nlit[depth - 1]))
-        return fail("dk_replay_set_skipping: a float stat compares only through FCMP");
+        return fail(W + ": a float stat compares only through FCMP");
       depth--;
       fstat[depth - 1] = false;
       nlit[depth - 1] = false;
     }
-    else return fail("dk_replay_set_skipping: bad opcode");
-    if (depth > 16) return fail("dk_replay_set_skipping: program too deep");
+    else return fail(W + ": bad opcode");
+    if (depth > 16) return fail(W + ": program too deep");
   }
-  if (depth != 1) return fail("dk_replay_set_skipping: program must leave one value");
+  if (depth != 1) return fail(W + ": program must leave one value");
+  return 0;
+}
+
+// ---- Engine plugin point 1: JsonHandler.parseJson over stats strings, and the data-skipping
+// PredicateEvaluator over the parsed result (KA/engine/JsonHandler.java:68-71,
+// KA/engine/ExpressionHandler.java:58, as ScanImpl.applyDataSkipping drives them,
+// KA/internal/ScanImpl.java:304-352) ----
+struct dk_parsed_stats {
+  StreamH own;
+  int device = 0;
+  int64_t n = 0;
+  DSkipProg schema{};
+  DBuf d_chars, d_offs, d_isnull, d_sel, d_prog, d_vals, d_set, d_state, d_out;
+  bool dev_input = false;
+  const uint8_t* chars = nullptr;          // device views of the input
+  const int64_t* offs = nullptr;
+};
+
+extern "C" int dk_json_parse_stats(dk_engine* e, const dk_skip_program* schema, int64_t n, const int64_t* offs,
+                                   const uint8_t* chars, const uint8_t* isnull, const uint8_t* selection,
+                                   int32_t on_device, dk_parsed_stats** out) {
+  if (!e || !schema || !out || n < 0 || (n && (!offs || !chars))) return fail("dk_json_parse_stats: bad arguments");
+  hipSetDevice(e->cfg.device);
+  std::unique_ptr<dk_parsed_stats> ps(new dk_parsed_stats());
+  ps->device = e->cfg.device;
+  memcpy(&ps->schema, schema, sizeof ps->schema);
+  // the schema is a program's path table (its ops are not used here): names and types only
+  DSkipProg P = ps->schema;
+  if (P.n_paths < 1 || P.n_paths > SK_MAX_PATHS) return fail("dk_json_parse_stats: 1..8 stats paths");
+  for (int p = 0; p < P.n_paths; p++) {
+    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DOUBLE)
+      return fail("dk_json_parse_stats: bad stats path");
+    for (int d = 0; d < P.path_depth[p]; d++)
+      if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
+        return fail("dk_json_parse_stats: bad stats path name");
+  }
+  if (ps->own.create()) return 1;
+  hipStream_t s = ps->own.s;
+  ps->n = n;
+  ps->dev_input = on_device != 0;
+  if (ps->dev_input) {
+    ps->chars = chars; ps->offs = offs;
+  } else {
+    const int64_t nchars = n ? offs[n] : 0;
+    if (upload(ps->d_chars, chars, (size_t)nchars + 16, s) || upload(ps->d_offs, offs, (size_t)(n + 1) * 8, s)) return 1;
+    ps->chars = ps->d_chars.as<uint8_t>(); ps->offs = ps->d_offs.as<int64_t>();
+  }
+  const uint8_t* dnull = isnull;
+  const uint8_t* dsel = selection;
+  if (!ps->dev_input) {
+    if (isnull) { if (upload(ps->d_isnull, isnull, (size_t)n + 16, s)) return 1; dnull = ps->d_isnull.as<uint8_t>(); }
+    if (selection) { if (upload(ps->d_sel, selection, (size_t)n + 16, s)) return 1; dsel = ps->d_sel.as<uint8_t>(); }
+  }
+  if (upload(ps->d_prog, &ps->schema, sizeof(DSkipProg), s)) return 1;
+  if (ps->d_vals.alloc((size_t)P.n_paths * n * 8 + 64) || ps->d_set.alloc((size_t)n * 4 + 64) ||
+      ps->d_state.alloc(sizeof(DState)))
+    return 1;
+  DState st0{};
+  st0.err_row = LLONG_MAX;
+  HIPOK(hipMemcpyAsync(ps->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
+  launch_json_parse_stats(ps->chars, ps->offs, dnull, dsel, n, ps->d_prog.as<DSkipProg>(), ps->d_vals.as<long long>(),
+                          ps->d_set.as<uint32_t>(), ps->d_state.as<DState>(), s);
+  HIPOK(hipStreamSynchronize(s));
+  DState h{};
+  HIPOK(hipMemcpy(&h, ps->d_state.p, sizeof h, hipMemcpyDeviceToHost));
+  if (h.err_flags & E_STATS)
+    return fail("Parsing the JSON statistics: couldn't decode the stats of row " + std::to_string(h.err_row));
+  *out = ps.release();
+  return 0;
+}
+
+// path p of the parsed stats on the host: present[r] (0 = null) and values[r] -- long / integer /
+// short / byte / date (epoch days) / timestamp(_ntz) (micros): the value; string / decimal / float /
+// double: the token's span in row r's string (offset | length << 32, bit 62 = JSON escapes or, for a
+// float / double, a special-value code NaN 1 / +Inf 2 / -Inf 3 in the low bits)
+extern "C" int dk_parsed_stats_column(dk_parsed_stats* ps, int32_t path, int64_t* values, uint8_t* present) {
+  if (!ps || path < 0 || path >= ps->schema.n_paths) return fail("dk_parsed_stats_column: bad path");
+  hipSetDevice(ps->device);
+  const int64_t n = ps->n;
+  if (!n) return 0;
+  std::vector<uint32_t> set(n);
+  HIPOK(hipMemcpy(set.data(), ps->d_set.p, n * 4, hipMemcpyDeviceToHost));
+  if (values) HIPOK(hipMemcpy(values, ps->d_vals.as<int64_t>() + (int64_t)path * n, n * 8, hipMemcpyDeviceToHost));
+  if (present) for (int64_t r = 0; r < n; r++) present[r] = (set[r] >> path) & 1;
+  return 0;
+}
+
+// PredicateEvaluator.eval(parsed stats, selection) for COALESCE(prog, true): prog's stats paths must
+// be the parsed schema's (same order, names and types); selection is updated in place (host memory,
+// or device memory when the stats were parsed from device input)
+extern "C" int dk_parsed_stats_eval(dk_parsed_stats* ps, const dk_skip_program* prog, uint8_t* selection) {
+  if (!ps || !prog || (ps->n && !selection)) return fail("dk_parsed_stats_eval: bad arguments");
+  DSkipProg P;
+  memcpy(&P, prog, sizeof P);
+  if (check_skip_program(P, "dk_parsed_stats_eval")) return 1;
+  const DSkipProg& S = ps->schema;
+  bool same = P.n_paths == S.n_paths;
+  for (int p = 0; same && p < P.n_paths; p++) {
+    same = P.path_type[p] == S.path_type[p] && P.path_depth[p] == S.path_depth[p];
+    for (int d = 0; same && d < P.path_depth[p]; d++)
+      same = P.name_len[p][d] == S.name_len[p][d] &&
+             !memcmp(P.names + P.name_off[p][d], S.names + S.name_off[p][d], P.name_len[p][d]);
+  }
+  if (!same) return fail("dk_parsed_stats_eval: the predicate's stats paths are not the parsed schema's");
+  hipSetDevice(ps->device);
+  hipStream_t s = ps->own.s;
+  if (!ps->n) return 0;
+  if (upload(ps->d_prog, &P, sizeof P, s)) return 1;
+  uint8_t* dsel = selection;
+  if (!ps->dev_input) {
+    if (upload(ps->d_out, selection, (size_t)ps->n, s)) return 1;
+    dsel = ps->d_out.as<uint8_t>();
+  }
+  launch_parsed_eval(ps->chars, ps->offs, ps->n, ps->d_prog.as<DSkipProg>(), ps->d_vals.as<long long>(),
+                     ps->d_set.as<uint32_t>(), dsel, s);
+  if (!ps->dev_input) HIPOK(hipMemcpyAsync(selection, dsel, (size_t)ps->n, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  return 0;
+}
+
+extern "C" void dk_parsed_stats_free(dk_parsed_stats* ps) {
+  if (!ps) return;
+  hipSetDevice(ps->device);
+  hipStreamSynchronize(ps->own.s);
+  delete ps;
+}
+
+extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog) {
+  static_assert(sizeof(dk_skip_program) == sizeof(DSkipProg), "dk_skip_program layout");
+  if (!r) return fail("null replay");
+  if (!prog) { r->has_skip = false; return 0; }
+  DSkipProg P;
+  memcpy(&P, prog, sizeof P);
+  if (check_skip_program(P, "dk_replay_set_skipping")) return 1;
   if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
   if (r->lazy && attach_upto(r, INT_MAX)) return 1;   // the typed stats columns of every file
   r->skip = P;

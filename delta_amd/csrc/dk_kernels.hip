@@ -4629,3 +4629,62 @@ int warm_kernels() {
   return n;
 }
 }  // namespace dk
+
+namespace dk {
+// ---- Engine plugin point 1: JsonHandler.parseJson over a stats string vector and
+// the data-skipping PredicateEvaluator over its result (ScanImpl.applyDataSkipping,
+// KA/internal/ScanImpl.java:304-352: parseJsonStats, then getPredicateEvaluator(prunedStatsSchema,
+// COALESCE(skip, true)).eval(batch, selection)). One lane per row.
+
+// DefaultJsonHandler.parseJson (KD/engine/DefaultJsonHandler.java:60-76): unselected and null rows are
+// all-null rows; a selected row's stats are decoded with DefaultJsonRow's rules (js_extract). vals is
+// path-major [n_paths][n]; set[r] has bit p when path p is non-null.
+__global__ __launch_bounds__(NT) void k_json_parse_stats(const uint8_t* __restrict__ chars, const int64_t* __restrict__ offs,
+                                                         const uint8_t* __restrict__ isnull, const uint8_t* __restrict__ sel,
+                                                         long long n, const DSkipProg* __restrict__ Pp,
+                                                         long long* __restrict__ vals, uint32_t* __restrict__ set,
+                                                         DState* __restrict__ st) {
+  const DSkipProg& P = *Pp;
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
+    uint32_t m = 0;
+    long long v[SK_MAX_PATHS];
+    if (!((sel && !sel[r]) || (isnull && isnull[r]))) {
+      const uint8_t* s = chars + offs[r];
+      if (!js_extract(s, (int32_t)(offs[r + 1] - offs[r]), P, v, &m)) { set_err(st, E_STATS, r, 0); m = 0; }
+    }
+    set[r] = m;
+    for (int p = 0; p < P.n_paths; p++) vals[(long long)p * n + r] = ((m >> p) & 1) ? v[p] : 0;
+  }
+}
+
+// PredicateEvaluator.eval(parsed, selection) for COALESCE(program, true): a selected row stays
+// selected unless the program is FALSE (DefaultPredicateEvaluator.java:42-72 ANDs the existing
+// selection in)
+__global__ __launch_bounds__(NT) void k_parsed_eval(const uint8_t* __restrict__ chars, const int64_t* __restrict__ offs,
+                                                    long long n, const DSkipProg* __restrict__ Pp,
+                                                    const long long* __restrict__ vals, const uint32_t* __restrict__ set,
+                                                    uint8_t* __restrict__ sel) {
+  const DSkipProg& P = *Pp;
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
+    if (!sel[r]) continue;
+    long long v[SK_MAX_PATHS];
+    for (int p = 0; p < P.n_paths; p++) v[p] = vals[(long long)p * n + r];
+    if (sk_eval(P, v, set[r], chars + offs[r]) == 0) sel[r] = 0;
+  }
+}
+
+void launch_json_parse_stats(const uint8_t* chars, const int64_t* offs, const uint8_t* isnull, const uint8_t* sel,
+                             long long n, const DSkipProg* P, long long* vals, uint32_t* set, DState* st, hipStream_t s) {
+  if (n <= 0) return;
+  const long long want = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_json_parse_stats, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(NT), 0, s, chars, offs, isnull,
+                     sel, n, P, vals, set, st);
+}
+void launch_parsed_eval(const uint8_t* chars, const int64_t* offs, long long n, const DSkipProg* P, const long long* vals,
+                        const uint32_t* set, uint8_t* sel, hipStream_t s) {
+  if (n <= 0) return;
+  const long long want = (n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_parsed_eval, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(NT), 0, s, chars, offs, n, P, vals,
+                     set, sel);
+}
+}  // namespace dk

@@ -295,6 +295,29 @@ typedef struct dk_skip_program {
   int64_t lit[64];
 } dk_skip_program;
 
+/* ---- Engine plugin point 1 beyond the ParquetHandler: the data-skipping hooks a
+ * stock ScanImpl calls through the Engine (KA/internal/ScanImpl.java:304-352):
+ *   JsonHandler.parseJson(statsVector, prunedStatsSchema, selection)   (KA/engine/JsonHandler.java:68-71)
+ *     -> dk_json_parse_stats: the stats strings (n rows: offs[n + 1] into chars, isnull / selection one
+ *        byte per row or NULL; host memory, or device memory when on_device -- a GPU-decoded
+ *        add.stats column) parsed on the GPU with DefaultJsonRow's rules for the schema's stats paths
+ *        (a dk_skip_program's path table; its ops are ignored). Unselected and null rows are all-null
+ *        rows (DefaultJsonHandler.java:60-76); a row that does not decode fails the call.
+ *   ExpressionHandler.getPredicateEvaluator(prunedStatsSchema, COALESCE(skip, true)).eval(parsed, sel)
+ *                                                                       (KA/engine/ExpressionHandler.java:58)
+ *     -> dk_parsed_stats_eval: the program over the parsed rows, ANDed into the selection in place
+ *        (DefaultPredicateEvaluator.java:42-72); its stats paths must be the parsed schema's.
+ * dk_parsed_stats_column hands one path back as (present, value) per row: integral / date (epoch
+ * days) / timestamp (micros) values, or for string / decimal / float / double the token's span in the
+ * row's string (offset | length << 32; bit 62: escaped string, or a float special value code). */
+typedef struct dk_parsed_stats dk_parsed_stats;
+int  dk_json_parse_stats(dk_engine* e, const dk_skip_program* schema, int64_t n, const int64_t* offs,
+                         const uint8_t* chars, const uint8_t* isnull, const uint8_t* selection, int32_t on_device,
+                         dk_parsed_stats** out);
+int  dk_parsed_stats_column(dk_parsed_stats* ps, int32_t path, int64_t* values, uint8_t* present);
+int  dk_parsed_stats_eval(dk_parsed_stats* ps, const dk_skip_program* prog, uint8_t* selection);
+void dk_parsed_stats_free(dk_parsed_stats* ps);
+
 /* Partition-pruning program (ScanImpl.applyPartitionPruning, ScanImpl.java:247-294): the predicate on
  * partition columns, rewritten over the scan file's partitionValues map
  * (PartitionUtils.rewritePartitionPredicateOnScanFileSchema, PartitionUtils.java:324-358), in postfix.

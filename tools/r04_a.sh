@@ -4,7 +4,7 @@ set -o pipefail
 TAG=$1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT; cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_owner.py tests/test_exchange.py tests/test_batch_lifetime.py tests/test_shard.py tests/test_gpu_parity.py tests/test_skipping.py tests/test_dv.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_owner.log 2>&1 || { echo "owner gpu tests failed"; grep -E "^E |FAILED|Error" $OUT/pytest_owner.log | head -30; tail -5 $OUT/pytest_owner.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_owner.py tests/test_exchange.py tests/test_batch_lifetime.py tests/test_shard.py tests/test_gpu_parity.py tests/test_skipping.py tests/test_dv.py tests/test_handlers.py -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_owner.log 2>&1 || { echo "owner gpu tests failed"; grep -E "^E |FAILED|Error" $OUT/pytest_owner.log | head -30; tail -5 $OUT/pytest_owner.log; exit 1; }
 tail -1 $OUT/pytest_owner.log
 for i in 1 2; do
 for cfg in "DK_SLICE_DECODE=0" "DK_SLICE_DECODE=1,DK_ASYNC_OPEN=1"; do
