@@ -1408,6 +1408,7 @@ class GpuScan:
                     fb = FilteredColumnarBatch(cols, root, b - a, sel[a:b].view(bool),
                                                self.snapshot._json_checkpoint_parts()[0], -1, 0)
                 fb.commit_index = j
+                self._handed[id(fb)] = fb
                 yield fb
         elif self.tail.rows:
             sel = np.zeros(self.tail.rows, dtype=np.uint8)
@@ -1415,13 +1416,17 @@ class GpuScan:
             r0 = int(self.tail.ckpt_row0)
             if r0 > 0:
                 cols = LazyColumns(leaves, self.tail.column)
-                yield FilteredColumnarBatch(cols, root, r0, sel[:r0].view(bool), "json-tail")
+                fb = FilteredColumnarBatch(cols, root, r0, sel[:r0].view(bool), "json-tail")
+                self._handed[id(fb)] = fb
+                yield fb
             if r0 < self.tail.rows:
                 # a V2 JSON manifest's rows: the first checkpoint batch (ActionsIterator reads the
                 # manifest before its sidecars)
                 cols = LazyColumns(leaves, lambda leaf: self.tail.column(leaf).slice_rows(r0, self.tail.rows))
-                yield FilteredColumnarBatch(cols, root, int(self.tail.rows - r0), sel[r0:].view(bool),
-                                            self.snapshot._json_checkpoint_parts()[0], -1, 0)
+                fb = FilteredColumnarBatch(cols, root, int(self.tail.rows - r0), sel[r0:].view(bool),
+                                           self.snapshot._json_checkpoint_parts()[0], -1, 0)
+                self._handed[id(fb)] = fb
+                yield fb
         # checkpoint batches: zero-copy views of the library's pinned selection bytes and column
         # mirrors (every file's selection comes to the host in one round of copies; a leaf's first
         # access queues its copy for every later file), valid until the scan is closed
@@ -1435,7 +1440,6 @@ class GpuScan:
             cols = LazyColumns(leaves, lambda leaf, fi=fi: self.ckpt.column(fi, leaf, copy=False))
             fb = FilteredColumnarBatch(cols, root, int(n), sel, path, self.ckpt_index[fi],
                                        int(self.ckpt.row_offset(fi)))
-            fb._file = fi
             self._handed[id(fb)] = fb
             yield fb
         if grouped:
@@ -1453,16 +1457,14 @@ class GpuScan:
         for b in live:
             if b.selection is not None:
                 b.selection = np.array(b.selection, copy=True)
-            fi = b._file
             for leaf in b.data.keys():
                 got = dict.get(b.data, leaf)
                 if got is None and dict.__contains__(b.data, leaf):
                     continue                                  # fetched: absent from the file
-                if got is not None:
-                    dict.__setitem__(b.data, leaf, _own_column(got))
-                else:
-                    c = self.ckpt.column(fi, leaf, copy=True)
-                    dict.__setitem__(b.data, leaf, c if c.present else None)
+                if got is None:
+                    c = b.data._fetch(leaf)                   # not read yet: read it now
+                    got = c if c.present else None
+                dict.__setitem__(b.data, leaf, None if got is None else _own_column(got))
             b.data._fetch = None
 
     def close(self):
