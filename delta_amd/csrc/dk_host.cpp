@@ -2830,13 +2830,24 @@ namespace {
 // Java UTF-8 decoding with replacement (InputStreamReader(UTF_8)): each maximal ill-formed
 // subsequence becomes U+FFFD.
 std::string java_utf8(const uint8_t* s, size_t n) {
+  // valid runs are copied in bulk (ASCII eight bytes at a time); each maximal ill-formed subpart
+  // becomes U+FFFD, as StandardCharsets.UTF_8.decode does
   std::string o;
   o.reserve(n);
-  size_t i = 0;
+  size_t i = 0, run = 0;                       // [run, i): valid, not yet appended
   while (i < n) {
+    while (i + 8 <= n) {
+      uint64_t w;
+      memcpy(&w, s + i, 8);
+      if (w & 0x8080808080808080ull) break;
+      i += 8;
+    }
+    if (i >= n) break;
+    if (s[i] < 0x80) { i++; continue; }
     uint32_t cp;
     int l = utf8_len_valid(s, (int64_t)i, (int64_t)n, &cp);
-    if (l) { o.append((const char*)s + i, l); i += l; continue; }
+    if (l) { i += l; continue; }
+    o.append((const char*)s + run, i - run);
     // maximal subpart length
     uint8_t b = s[i];
     int need = 0; uint8_t lo = 0x80, hi = 0xBF;
@@ -2851,7 +2862,9 @@ std::string java_utf8(const uint8_t* s, size_t n) {
     }
     o.append("\xEF\xBF\xBD");
     i = j;
+    run = j;
   }
+  o.append((const char*)s + run, n - run);
   return o;
 }
 
@@ -2865,20 +2878,38 @@ struct JNode {
   std::vector<int> arr;
 };
 
+// A parser over one JSON text whose nodes live in `nodes` from index 0. The nodes of an earlier
+// parse are reused in place (their strings and vectors keep their capacity), so parsing one commit
+// line after another allocates almost nothing once warm.
 struct JParser {
   const char* p; const char* e;
   std::vector<JNode>& nodes;
   std::string err;
-  JParser(const char* b, const char* en, std::vector<JNode>& n) : p(b), e(en), nodes(n) {}
+  size_t used = 0;
+  std::vector<std::string>& keys;        // per nesting depth: the key being parsed (thread's buffers)
+  static std::vector<std::string>& key_bufs() { static thread_local std::vector<std::string> k; return k; }
+  JParser(const char* b, const char* en, std::vector<JNode>& n) : p(b), e(en), nodes(n), keys(key_bufs()) {}
+  int alloc() {
+    if (used < nodes.size()) {
+      JNode& n = nodes[used];
+      n.t = J_NULL; n.b = false; n.integral = false;
+      n.s.clear(); n.kv.clear(); n.arr.clear();
+    } else {
+      nodes.emplace_back();
+    }
+    return (int)used++;
+  }
   void ws() { while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) p++; }
   bool str(std::string& out) {
     if (p >= e || *p != '"') return false;
     p++;
     out.clear();
     while (p < e && *p != '"') {
+      const char* q = p;                         // a run without escapes / control characters
+      while (q < e && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) q++;
+      if (q > p) { out.append(p, q - p); p = q; continue; }
       unsigned char c = (unsigned char)*p;
       if (c < 0x20) return false;
-      if (c != '\\') { out.push_back((char)c); p++; continue; }
       p++;
       if (p >= e) return false;
       char x = *p++;
@@ -2924,26 +2955,28 @@ struct JParser {
     if (depth > 200) { err = "nesting too deep"; return -1; }
     ws();
     if (p >= e) { err = "unexpected end"; return -1; }
-    int id = (int)nodes.size();
-    nodes.emplace_back();
+    int id = alloc();
     char c = *p;
     if (c == '{') {
       p++;
       nodes[id].t = J_OBJ;
       ws();
       if (p < e && *p == '}') { p++; return id; }
+      if ((int)keys.size() <= depth) keys.resize(depth + 1);
       for (;;) {
         ws();
-        std::string k;
+        std::string& k = keys[depth];
         if (!str(k)) { err = "bad object key"; return -1; }
         ws();
         if (p >= e || *p != ':') { err = "expected ':'"; return -1; }
         p++;
+        int dup = -1;                             // ObjectNode.set: last wins, first position
+        for (size_t m = 0; m < nodes[id].kv.size(); m++) if (nodes[id].kv[m].first == k) { dup = (int)m; break; }
+        if (dup < 0) nodes[id].kv.push_back({k, -1});
+        const int slot = dup < 0 ? (int)nodes[id].kv.size() - 1 : dup;
         int v = value(depth + 1);
         if (v < 0) return -1;
-        bool dup = false;
-        for (auto& m : nodes[id].kv) if (m.first == k) { m.second = v; dup = true; break; }   // ObjectNode.set: last wins, first position
-        if (!dup) nodes[id].kv.push_back({k, v});
+        nodes[id].kv[slot].second = v;
         ws();
         if (p < e && *p == ',') { p++; continue; }
         if (p < e && *p == '}') { p++; return id; }
@@ -2966,9 +2999,8 @@ struct JParser {
       }
     }
     if (c == '"') {
-      std::string s;
-      if (!str(s)) { err = "bad string"; return -1; }
-      nodes[id].t = J_STR; nodes[id].s = std::move(s);
+      if (!str(nodes[id].s)) { err = "bad string"; return -1; }
+      nodes[id].t = J_STR;
       return id;
     }
     if (e - p >= 4 && !memcmp(p, "null", 4)) { p += 4; nodes[id].t = J_NULL; return id; }
@@ -3177,11 +3209,11 @@ static std::string parse_commit_file(const char* path, int J, bool with_stats, T
   while (i < text.size()) {
     size_t j = i;
     while (j < text.size() && text[j] != '\n' && text[j] != '\r') j++;
-    std::string line = text.substr(i, j - i);
+    const char* lb = text.data() + i;
+    const char* le = text.data() + j;
     if (j < text.size() && text[j] == '\r' && j + 1 < text.size() && text[j + 1] == '\n') j++;
     i = j + 1;
-    N.clear();
-    JParser jp(line.data(), line.data() + line.size(), N);
+    JParser jp(lb, le, N);                      // N's nodes are reused line after line
     int root = jp.value(0);
     if (root >= 0) { jp.ws(); if (jp.p != jp.e) { root = -1; jp.err = "trailing characters"; } }
     if (root < 0) return std::string("Error reading JSON file: ") + path + " (" + jp.err + ")";
@@ -3260,7 +3292,10 @@ extern "C" int dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, 
   // order reports, as the sequential reader would
   std::vector<TailPart> parts(n_files > 0 ? n_files : 0);
   std::vector<std::string> errs(parts.size());
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   parallel_for(n_files, [&](int fi) { errs[fi] = parse_commit_file(paths[fi], J, t->with_stats, parts[fi]); });
+  const auto t1 = clk::now();
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
   for (int fi = 0; fi < n_files; fi++) {
@@ -3277,6 +3312,10 @@ extern "C" int dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, 
     P = TailPart();
   }
   t->file_row0.push_back(t->rows);
+  if (getenv("DK_VERBOSE"))
+    fprintf(stderr, "[dk] commit tail: %d files, %lld rows: parse %.1f ms, concatenate %.1f ms\n", n_files,
+            (long long)t->rows, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(clk::now() - t1).count());
   *out = t.release();
   return 0;
 }
@@ -3702,6 +3741,7 @@ static int replay_attach(dk_replay* r, dk_parquet* ckpt) {
 
 extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_replay** out) {
   if (!e) return fail("null engine");
+  const auto t_create0 = std::chrono::steady_clock::now();
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_replay> r(new dk_replay());
   r->eng = e; r->tail = tail;
@@ -3748,6 +3788,7 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
     }
   }
   size_t na = r->acts.size();
+  const auto t_built = std::chrono::steady_clock::now();
   uint64_t cap = 1024;
   while (cap < 2 * na + 16) cap <<= 1;
   r->mask = cap - 1;
@@ -3801,7 +3842,14 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
     if (upload(r->d_tstats_off, soff.data(), soff.size() * 8, s)) return 1;
     if (upload(r->d_tstats_len, slen.data(), slen.size() * 4, s)) return 1;
   }
+  const auto t_queued = std::chrono::steady_clock::now();
   HIPOK(hipStreamSynchronize(s));
+  if (getenv("DK_VERBOSE")) {
+    using ms = std::chrono::duration<double, std::milli>;
+    const auto t_end = std::chrono::steady_clock::now();
+    fprintf(stderr, "[dk] replay create: %zu actions: build %.1f ms, uploads queued %.1f ms, waited %.1f ms\n", na,
+            ms(t_built - t_create0).count(), ms(t_queued - t_built).count(), ms(t_end - t_queued).count());
+  }
   if (ckpt && replay_attach(r.get(), ckpt)) return 1;
   *out = r.release();
   return 0;
