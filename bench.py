@@ -554,8 +554,15 @@ def main(argv=None):
     step_gbs = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
     # roofline of the dominant kernel with a byte model (dk_parquet_kernel_traffic):
     # algorithmic bytes of one launch / its average launch time (HIP events on the replay stream)
-    modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy", "k_probe") if k in kern]
+    modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy", "k_plain_copy", "k_probe") if k in kern]
     rk = max(modelled, key=lambda k: kern[k]) if modelled else None
+    # every modelled kernel's own roofline fraction (same byte models, same HIP-event averages)
+    kern_roof = {}
+    for k in modelled:
+        r_, w_ = scan.ckpt.kernel_traffic(k)
+        gbs = (r_ + w_) / (kern[k] * 1e-6) / 1e9
+        kern_roof[k] = dict(us=round(kern[k], 1), algorithmic_bytes=r_ + w_, gbs=round(gbs, 1),
+                            frac=round(gbs / HBM_PEAK_GBS, 4))
     k_read, k_written = scan.ckpt.kernel_traffic(rk) if rk else (0, 0)
     k_bytes = k_read + k_written
     achieved = k_bytes / (kern[rk] * 1e-6) / 1e9 if rk else None
@@ -622,6 +629,8 @@ def main(argv=None):
         t_x = time.perf_counter()
         sc.close()
         phases["close"] = (time.perf_counter() - t_x) * 1e3
+        if cprof:
+            phases.update(getattr(sc, "close_ms", {}))
         return seen, n_sel, size_sum, phases
 
     for i in range(args.warmup):
@@ -742,6 +751,7 @@ def main(argv=None):
         "snapshot_load_with_crc_ms": snapshot_crc_ms,
         "snapshot_load_phases_ms": {k: round(v, 3) for k, v in snap.load_ms.items()},
         "kernels_us": {k: round(v, 2) for k, v in sorted(kern.items(), key=lambda kv: -kv[1])},
+        "kernels_roofline": kern_roof,
         "roofline": {"bound": "hbm", "kernel": rk, "kernel_us": kern.get(rk),
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,

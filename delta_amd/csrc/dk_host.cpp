@@ -15,6 +15,7 @@
 #include <mutex>
 #include <thread>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <future>
 #include <string>
@@ -39,11 +40,13 @@ void launch_copy_zc(void*, const void*, long long, hipStream_t);
 void launch_arrow_window(const ArrowWin&, hipStream_t);
 void launch_dv_expand(const DvCont*, int, const uint8_t*, unsigned long long*, hipStream_t);
 void launch_dv_select(const unsigned long long*, long long, const long long*, long long, uint8_t*, hipStream_t);
-void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, hipStream_t);
+void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, int, hipStream_t);
+void launch_plain_copy(const DChunk*, DPage*, const DColumn*, const uint8_t*, int32_t*, const DPosChunk*, int, int, int, int,
+                       unsigned long long*, unsigned int*, int32_t*, DState*, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
 void launch_tile_scan1(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
-void launch_tile_chars(const DChunk*, DPage*, const uint8_t*, const int32_t*, const Seg*, DTile*, int, int, hipStream_t);
+void launch_tile_chars(const DChunk*, DPage*, const uint8_t*, const int32_t*, const Seg*, DTile*, int, int, int, hipStream_t);
 void launch_tile_scan2(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
 void launch_tile_decode(const DChunk*, DPage*, const DColumn*, const uint8_t*, const int32_t*, const long long*, const Seg*, const DTile*, int, int, DState*, hipStream_t);
 void launch_delta_decode(const DChunk*, DPage*, int, const uint8_t*, long long*, hipStream_t);
@@ -241,25 +244,34 @@ static MemCache& pinned_cache() { static MemCache* c = new MemCache(true, (size_
 
 // Non-blocking streams are pooled per device (creating one costs milliseconds): a call object takes
 // one when it is created and gives it back, drained, when it is freed.
+// High-priority streams (the replay's: the commit tail's uploads and kernels, the probes) come from
+// their own pool: HIP maps stream priorities to separate hardware queues, so their work does not
+// queue behind the decode passes an asynchronous open keeps feeding to the normal queues.
 struct StreamPool {
   std::mutex mu;
-  std::vector<std::pair<int, hipStream_t>> free_;
-  hipStream_t get() {
+  std::vector<std::pair<int, hipStream_t>> free_[2];
+  hipStream_t get(bool high = false) {
     int dev = 0;
     hipGetDevice(&dev);
     {
       std::lock_guard<std::mutex> lk(mu);
-      for (size_t i = 0; i < free_.size(); i++)
-        if (free_[i].first == dev) { hipStream_t s = free_[i].second; free_.erase(free_.begin() + i); return s; }
+      auto& F = free_[high];
+      for (size_t i = 0; i < F.size(); i++)
+        if (F[i].first == dev) { hipStream_t s = F[i].second; F.erase(F.begin() + i); return s; }
     }
     hipStream_t s = nullptr;
+    if (high) {
+      int least = 0, greatest = 0;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
+      return hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) == hipSuccess ? s : nullptr;
+    }
     return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? s : nullptr;
   }
-  void put(hipStream_t s) {
+  void put(hipStream_t s, bool high = false) {
     int dev = 0;
     hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    free_.push_back({dev, s});
+    free_[high].push_back({dev, s});
   }
 };
 static StreamPool& stream_pool() { static StreamPool* p = new StreamPool(); return *p; }
@@ -315,9 +327,20 @@ struct HBuf {
 // nothing of a call runs on a stream shared through the engine.
 struct StreamH {
   hipStream_t s = nullptr;
-  ~StreamH() { if (s) { hipStreamSynchronize(s); stream_pool().put(s); } }
-  int create() { s = stream_pool().get(); return s ? 0 : fail("hipStreamCreate failed"); }
+  bool high = false;
+  ~StreamH() { if (s) { hipStreamSynchronize(s); stream_pool().put(s, high); } }
+  int create(bool high_priority = false) {
+    high = high_priority;
+    s = stream_pool().get(high);
+    return s ? 0 : fail("hipStreamCreate failed");
+  }
 };
+
+// the replay's stream is high-priority unless DK_REPLAY_PRIORITY=0 (A/B)
+static bool replay_high_priority() {
+  static const bool on = !(getenv("DK_REPLAY_PRIORITY") && atoi(getenv("DK_REPLAY_PRIORITY")) == 0);
+  return on;
+}
 
 // Warm-up at engine creation (once per device and process): the code objects' lazy load, a pooled
 // stream, a first launch on it, the first device / pinned blocks -- costs the first
@@ -329,8 +352,8 @@ static int engine_warm(int device) {
   if (std::find(warmed.begin(), warmed.end(), device) != warmed.end()) return 0;
   warmed.push_back(device);
   warm_kernels();
-  StreamH sh;
-  if (sh.create()) return 1;
+  StreamH sh, sh_hi;
+  if (sh.create() || sh_hi.create(replay_high_priority())) return 1;
   DBuf d;
   HBuf h;
   if (d.alloc(1 << 20) || h.alloc(1 << 20)) return 1;
@@ -827,12 +850,13 @@ static int phys_width(int phys, int tl) {
 // kernel timing (HIP events on the engine stream)
 // ------------------------------------------------------------------------------------------------
 struct KTimer {
-  static constexpr int K = 24;
+  static constexpr int K = 25;
   const char* names[K] = {"k_page_headers", "unused", "k_tile_count", "k_tile_scan",
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
                           "k_snap_walk_link", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", "k_part_eval",
-                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", "k_owner_route", "k_owner_resolve"};
+                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", "k_owner_route", "k_owner_resolve",
+                          "k_plain_copy"};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -900,6 +924,8 @@ struct dk_parquet {
   StreamH copy[kCopyStreams];
   StreamH aux;                      // table uploads while `stream` waits for the H2D copies
   StreamH side[2];                  // sizing slices rotate over stream, side[0], side[1] (created on demand)
+  StreamH dec;                      // per-slice value decode (high priority): never queued behind a later
+                                    // slice's sizing passes and their waits on its files' H2D copies
   EventH copy_done[kCopyStreams];
   hipStream_t stream = nullptr;
   dk_engine* eng = nullptr;
@@ -924,6 +950,7 @@ struct dk_parquet {
   int n_ltiles = 0;
   DBuf d_pchunks;            // string-position chunks (DPosChunk)
   int n_pchunks = 0;
+  DBuf d_pstat, d_pfail, d_ptick;   // k_plain_copy: chunk look-back words, page redo flags, tickets
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
   std::vector<int> col_tile0;
@@ -990,6 +1017,7 @@ static int upload(DBuf& d, const void* src, size_t n, hipStream_t s) {
 }
 
 
+
 // Per-page and per-tile kernels are launched once over every page / tile, or -- with
 // DK_SPLIT_LAUNCH=1, a profiling aid -- once per column so that rocprofv3's kernel trace
 // attributes time to columns.
@@ -1047,6 +1075,13 @@ static PRange file_range(const dk_parquet* p, int f0, int f1) {
   return R;
 }
 
+// PLAIN string pages in one pass at decode time (k_plain_copy); DK_PLAIN_FUSED=0: positions in the
+// sizing passes and k_string_copy tiles (A/B)
+static bool plain_fused() {
+  static const bool on = !(getenv("DK_PLAIN_FUSED") && atoi(getenv("DK_PLAIN_FUSED")) == 0);
+  return on;
+}
+
 // headers, snappy, runs, counts, positions, chars and the scans over one slice
 static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
   KTimer& T = p->timer;
@@ -1090,9 +1125,9 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
   };
   { KTimer::Scope sc(&T, 2, s); tiles([&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
-  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0, s); }
+  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0, plain_fused(), s); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P + R.pa, np, arena, p->d_dbp.as<long long>(), s); }
-  { KTimer::Scope sc(&T, 16, s); tiles([&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 16, s); tiles([&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, plain_fused(), s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
 }
 
@@ -1110,6 +1145,17 @@ static void decode_cols(dk_parquet* p, hipStream_t s, int c0, int c1) {
   const long long* dbp = p->d_dbp.as<long long>();
   DTile* LT = p->d_ltiles.as<DTile>();
   Seg* runs = p->d_runs.as<Seg>();
+  if (plain_fused()) {
+    // the columns' pages (decode ranges are whole files) and their position chunks
+    const int f0 = (int)(std::lower_bound(p->file_col0.begin(), p->file_col0.end(), c0) - p->file_col0.begin());
+    const int f1 = (int)(std::lower_bound(p->file_col0.begin(), p->file_col0.end(), c1) - p->file_col0.begin());
+    const int pa = p->file_page0[f0], pb = p->file_page0[f1];
+    const int pc0 = pa < p->n_pages ? p->h_pages[pa].pchunk0 : p->n_pchunks;
+    const int pc1 = pb < p->n_pages ? p->h_pages[pb].pchunk0 : p->n_pchunks;
+    KTimer::Scope sc(&T, 24, s);
+    launch_plain_copy(C, P, cols, arena, pos, p->d_pchunks.as<DPosChunk>(), pc0, pc1 - pc0, pa, pb - pa,
+                      p->d_pstat.as<unsigned long long>(), p->d_ptick.as<unsigned int>() + c0, p->d_pfail.as<int32_t>(), st, s);
+  }
   {
     KTimer::Scope sc(&T, 6, s);
     const int2* tiles = p->d_tiles.as<int2>();
@@ -1241,7 +1287,7 @@ static void build_tiles(dk_parquet* p, int c0, int c1, std::vector<int2>& tiles)
     const DColumn& c = p->h_cols[ci];
     for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
       const DPage& pg = p->h_pages[pi];
-      if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN) continue;
+      if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN || plain_fused()) continue;
       for (int v0 = 0; v0 < pg.n_values; v0 += DK_COPY_TILE) tiles.push_back(make_int2(pi, v0));
     }
     // key column: its dictionary pages are hashed entry by entry (hash-only tiles)
@@ -1360,7 +1406,8 @@ struct SizedSlice {
 // sentinels into the new outputs) and the value decode of its columns, on its stream.
 static int finish_slice(dk_parquet* p, SizedSlice& S, std::vector<DColumn>& got) {
   const PRange& R = S.R;
-  HIPOK(hipEventSynchronize(S.ev));
+  HIPOK(hipEventSynchronize(S.ev));                // the sizing passes are complete
+  const hipStream_t ds = p->dec.s ? p->dec.s : S.cs;
   hipEventDestroy(S.ev);
   S.ev = nullptr;
   memcpy(got.data() + R.col0, S.cols.data(), (size_t)(R.col1 - R.col0) * sizeof(DColumn));
@@ -1374,23 +1421,23 @@ static int finish_slice(dk_parquet* p, SizedSlice& S, std::vector<DColumn>& got)
   const int t0 = p->col_tile0.back();
   build_tiles(p, R.col0, R.col1, tiles);
   if ((size_t)(t0 + tiles.size()) * sizeof(int2) > p->d_tiles.n) return fail("internal: string-copy tile bound exceeded");
-  if (upload_zc_to(p, p->d_tiles.as<int2>() + t0, tiles.data(), tiles.size() * sizeof(int2), S.cs)) return 1;
+  if (upload_zc_to(p, p->d_tiles.as<int2>() + t0, tiles.data(), tiles.size() * sizeof(int2), ds)) return 1;
   if (alloc_outputs(p, R.col0, R.col1, got)) return 1;
-  if (upload_zc_to(p, p->d_cols.as<DColumn>() + R.col0, p->h_cols.data() + R.col0, (size_t)(R.col1 - R.col0) * sizeof(DColumn), S.cs))
+  if (upload_zc_to(p, p->d_cols.as<DColumn>() + R.col0, p->h_cols.data() + R.col0, (size_t)(R.col1 - R.col0) * sizeof(DColumn), ds))
     return 1;
   int k0 = (int)p->h_chunks.size(), k1 = 0;        // the slice's chunks (dict_hash_off)
   for (int k = 0; k < (int)p->h_chunks.size(); k++)
     if (p->h_chunks[k].col >= R.col0 && p->h_chunks[k].col < R.col1) { k0 = std::min(k0, k); k1 = k + 1; }
-  if (k1 > k0 && upload_zc_to(p, p->d_chunks.as<DChunk>() + k0, p->h_chunks.data() + k0, (size_t)(k1 - k0) * sizeof(DChunk), S.cs))
+  if (k1 > k0 && upload_zc_to(p, p->d_chunks.as<DChunk>() + k0, p->h_chunks.data() + k0, (size_t)(k1 - k0) * sizeof(DChunk), ds))
     return 1;
   KTimer& T = p->timer;
   DColumn* cols = p->d_cols.as<DColumn>();
-  { KTimer::Scope sc(&T, 3, S.cs); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, p->d_pages.as<DPage>(), p->d_ltiles.as<DTile>(), p->d_state.as<DState>(), S.cs); }
-  { KTimer::Scope sc(&T, 3, S.cs); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, p->d_pages.as<DPage>(), p->d_ltiles.as<DTile>(), p->d_state.as<DState>(), S.cs); }
-  decode_cols(p, S.cs, R.col0, R.col1);
+  { KTimer::Scope sc(&T, 3, ds); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, p->d_pages.as<DPage>(), p->d_ltiles.as<DTile>(), p->d_state.as<DState>(), ds); }
+  { KTimer::Scope sc(&T, 3, ds); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, p->d_pages.as<DPage>(), p->d_ltiles.as<DTile>(), p->d_state.as<DState>(), ds); }
+  decode_cols(p, ds, R.col0, R.col1);
   hipEvent_t dev = nullptr;                       // the slice's files are decoded after this
   HIPOK(hipEventCreateWithFlags(&dev, hipEventDisableTiming));
-  HIPOK(hipEventRecord(dev, S.cs));
+  HIPOK(hipEventRecord(dev, ds));
   p->dec_events.push_back(dev);
   {
     std::lock_guard<std::mutex> g(p->rmu);
@@ -1398,6 +1445,9 @@ static int finish_slice(dk_parquet* p, SizedSlice& S, std::vector<DColumn>& got)
     for (int f = S.f0; f < S.f1; f++) p->file_dec[f] = dev;
     if (p->files_ready != INT_MAX) p->files_ready = S.f1;
   }
+  if (getenv("DK_VERBOSE"))
+    fprintf(stderr, "[dk] decode of files [%d, %d) queued at %.1f ms\n", S.f0, S.f1,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p->t_open0).count());
   p->rcv.notify_all();
   return 0;
 }
@@ -1408,6 +1458,11 @@ static int wait_files(dk_parquet* p, int f1) {
   p->rcv.wait(lk, [&] { return p->files_ready >= f1 || p->open_state.load() != 0; });
   if (p->files_ready >= f1 || p->open_state.load() == 1) return 0;
   return fail(p->open_err);
+}
+// ... without waiting: are files [0, f1) decoded already?
+static bool files_ready_now(dk_parquet* p, int f1) {
+  std::lock_guard<std::mutex> lk(p->rmu);
+  return p->files_ready >= f1 || p->open_state.load() != 0;
 }
 // ... until the whole open has finished (joined); its error, if any
 static int ensure_open(dk_parquet* p) {
@@ -1522,6 +1577,10 @@ static int prepare(dk_parquet* p) {
       pbase.push_back(pbase.back() + pg.npchunk);
     }
     p->n_pchunks = (int)pbase.back();
+    // (k_plain_copy: up to 4 status words per chunk)
+    if (p->d_pstat.alloc((size_t)p->n_pchunks * 8 * 4 + 64) || p->d_pfail.alloc(p->h_pages.size() * 4 + 64) ||
+        p->d_ptick.alloc((p->h_cols.size() + 1) * 4 + 64))
+      return 1;
     if (expand(p, us, p->d_pchunks, ppage, pbase, EX_POSCHUNK, sizeof(DPosChunk)) ||
         expand(p, us, p->d_ltiles, tpage, tbase, EX_TILE, sizeof(DTile)))
       return 1;
@@ -1629,6 +1688,7 @@ static int prepare(dk_parquet* p) {
           HIPOK(hipStreamWaitEvent(ss[k], tables, 0));
         }
       }
+      if (per_slice && !p->dec.s && p->dec.create(true)) return 1;
       int slice = 0;
       while (f0 < nf) {
         int f1 = f0;
@@ -1684,6 +1744,11 @@ static int prepare(dk_parquet* p) {
       }
       for (int k = 1; k < nss; k++) {               // `s` waits for the side streams' slices
         HIPOK(hipEventRecord(tables, ss[k]));
+        HIPOK(hipStreamWaitEvent(s, tables, 0));
+      }
+      if (per_slice && p->dec.s) {                  // ... and for the slices' decode
+        if (!tables) HIPOK(hipEventCreateWithFlags(&tables, hipEventDisableTiming));
+        HIPOK(hipEventRecord(tables, p->dec.s));
         HIPOK(hipStreamWaitEvent(s, tables, 0));
       }
       if (tables) hipEventDestroy(tables);
@@ -2085,19 +2150,116 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
                         const int32_t* field_ids = nullptr, const std::function<void(dk_parquet*)>* publish = nullptr);
 
-// fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads
+// A process-wide pool of host worker threads behind parallel_for: a call no longer launches (and
+// joins) its own threads -- the commit P&M scan alone makes several calls, the open and the tail
+// parse one each. The caller works on its own job as well, so a parallel_for issued from inside a
+// pool task (nested) always completes, even with every worker busy; and so does one issued in a
+// forked child, which has no workers.
+struct HostPool {
+  struct Job {
+    std::function<void(int)> fn;
+    int n = 0;
+    std::atomic<int> next{0}, done{0};
+    std::mutex m;
+    std::condition_variable cv;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::shared_ptr<Job>> q;
+  explicit HostPool(int n) { for (int i = 0; i < n; i++) std::thread([this] { work(); }).detach(); }
+  size_t rr = 0;
+  static bool run_one(Job& j) {
+    const int i = j.next.fetch_add(1);
+    if (i >= j.n) return false;
+    j.fn(i);
+    if (j.done.fetch_add(1) + 1 == j.n) { std::lock_guard<std::mutex> g(j.m); j.cv.notify_all(); }
+    return true;
+  }
+  static void run(Job& j) { while (run_one(j)) {} }
+  // workers take one index at a time from the jobs in turn (concurrent callers -- the open's file
+  // reads and the commit-tail parse -- share the workers instead of queueing behind each other)
+  void work() {
+    for (;;) {
+      std::shared_ptr<Job> j;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        for (;;) {
+          while (!q.empty() && q.front()->next.load() >= q.front()->n) q.pop_front();   // exhausted
+          if (!q.empty()) break;
+          cv.wait(lk);
+        }
+        j = q[rr++ % q.size()];
+      }
+      run_one(*j);
+    }
+  }
+  void parallel(int n, int width, std::function<void(int)> fn) {
+    auto j = std::make_shared<Job>();
+    j->fn = std::move(fn);
+    j->n = n;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      q.push_back(j);
+    }
+    for (int k = 1; k < width; k++) cv.notify_one();
+    run(*j);
+    std::unique_lock<std::mutex> lk(j->m);
+    j->cv.wait(lk, [&] { return j->done.load() == j->n; });
+  }
+};
+static int io_threads() {
+  static const int nt = getenv("DK_IO_THREADS") && atoi(getenv("DK_IO_THREADS")) > 0 ? atoi(getenv("DK_IO_THREADS")) : 16;
+  return nt;
+}
+static HostPool& host_pool() { static HostPool* p = new HostPool(io_threads() - 1); return *p; }
+
+// fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads (the caller and the pool's)
 template <class F>
 static void parallel_for(int n, F fn) {
-  int nt = 16;
-  if (const char* v = getenv("DK_IO_THREADS")) nt = atoi(v) > 0 ? atoi(v) : 1;
-  if (nt > n) nt = n;
+  const int nt = std::min(io_threads(), n);
   if (nt <= 1) { for (int i = 0; i < n; i++) fn(i); return; }
-  std::atomic<int> next{0};
-  std::vector<std::thread> th;
-  for (int t = 0; t < nt; t++)
-    th.emplace_back([&] { for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
-  for (auto& x : th) x.join();
+  host_pool().parallel(n, nt, std::function<void(int)>(fn));
 }
+
+// Many small host -> device uploads gathered into one pinned block and copied by kernels
+// (launch_copy_zc): nothing waits on the DMA engines, which a concurrent checkpoint open keeps
+// busy with file images. add() allocates the destination at once; flush() stages and launches.
+struct ZcStage {
+  struct Item { void* dst; const void* src; size_t n; };
+  std::vector<Item> items;
+  size_t total = 0;
+  HBuf hb;
+  int add(DBuf& d, const void* src, size_t n) {
+    if (d.n < n || !d.p) if (d.alloc(n ? n : 16)) return 1;
+    add_raw(d.p, src, n);
+    return 0;
+  }
+  void add_raw(void* dst, const void* src, size_t n) {
+    if (n) { items.push_back({dst, src, n}); total += (n + 15) & ~size_t(15); }
+  }
+  // the staging block must outlive the copies: the caller synchronizes the stream before `this` dies
+  int flush(hipStream_t s) {
+    if (!total) return 0;
+    if (hb.alloc(total)) return 1;
+    // staging copies in 1 MiB pieces over the host threads, then one copy kernel per item
+    struct Piece { uint8_t* d; const uint8_t* s; size_t n; };
+    std::vector<Piece> pieces;
+    std::vector<size_t> at(items.size());
+    size_t o = 0;
+    for (size_t i = 0; i < items.size(); i++) {
+      at[i] = o;
+      for (size_t q = 0; q < items[i].n; q += (1 << 20))
+        pieces.push_back({hb.data() + o + q, (const uint8_t*)items[i].src + q, std::min<size_t>(1 << 20, items[i].n - q)});
+      o += (items[i].n + 15) & ~size_t(15);
+    }
+    parallel_for((int)pieces.size(), [&](int k) { memcpy(pieces[k].d, pieces[k].s, pieces[k].n); });
+    for (size_t i = 0; i < items.size(); i++) launch_copy_zc(items[i].dst, hb.data() + at[i], (long long)items[i].n, s);
+    items.clear();
+    total = 0;
+    return 0;
+  }
+};
+
 
 extern "C" int dk_parquet_open_rg(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                                   int32_t n_leaves, const int32_t* rg_lo, const int32_t* rg_hi, dk_parquet** out) {
@@ -2222,7 +2384,6 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->colmap.assign(n_files, std::vector<int>(n_leaves, -1));
   p->leafidx.assign(n_files, std::vector<int>(n_leaves, -1));
   p->dfile.resize(n_files);
-  hipStream_t s = p->stream;
   // host I/O in parallel over files (footer, row-group selection, projected column chunks):
   // DefaultParquetHandler reads files one after another; here every file of the call is in flight
   std::vector<std::string> errs(n_files > 0 ? n_files : 0);
@@ -2604,8 +2765,9 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
       const DPage& pg = p->h_pages[pi];
       const int64_t body = pg.unc_off >= 0 ? pg.usize : pg.csize;
       const bool plain_str = c.phys == PT_BYTE_ARRAY && pg.enc == ENC_PLAIN;
-      if (k == "k_string_copy") {
-        if (plain_str) { rd += pg.vbytes; wr += pg.n_chars + (key ? 8ll * pg.n_values : 0); }
+      if (k == "k_string_copy" || k == "k_plain_copy") {
+        // the value section read once; chars, the key column's hashes (+ positions, fused)
+        if (plain_str) rd += pg.vbytes, wr += pg.n_chars + (key ? 8ll * pg.n_values : 0) + (k == "k_plain_copy" ? 4ll * pg.n_values : 0);
       } else if (k == "k_snap_frag") {
         // snappy pages: compressed body read, decompressed body written (v2 levels excluded)
         if (pg.unc_off >= 0) {
@@ -3035,11 +3197,24 @@ bool parse_i64(const std::string& s, int64_t lo, int64_t hi, int64_t* out) {
   return true;
 }
 
+// vectors whose resize leaves new elements uninitialized: the tail concatenation sizes its columns
+// once and fills them from many threads, so the first touch of each page is spread over them too
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  using value_type = T;
+  NoInitAlloc() = default;
+  template <class U> NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U> struct rebind { using other = NoInitAlloc<U>; };
+  template <class U> void construct(U* p) noexcept { ::new ((void*)p) U; }
+  template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+template <class T> using RawVec = std::vector<T, NoInitAlloc<T>>;
+
 // column builder in the dk_column layout
 struct CB {
   int phys, width, max_def, max_rep, rep_def;
-  std::vector<uint8_t> row_def, entry_def, fixed, chars;
-  std::vector<int64_t> row_offs, offs;
+  RawVec<uint8_t> row_def, entry_def, fixed, chars;
+  RawVec<int64_t> row_offs, offs;
   void init(int ph, int w, int md, int mr, int rd) { phys = ph; width = w; max_def = md; max_rep = mr; rep_def = rd; if (mr) row_offs.push_back(0); if (ph == PT_BYTE_ARRAY) offs.push_back(0); }
   // non-repeated
   void null_row(int def) { row_def.push_back((uint8_t)def); if (phys == PT_BYTE_ARRAY) offs.push_back((int64_t)chars.size()); else fixed.insert(fixed.end(), width, 0); }
@@ -3264,14 +3439,62 @@ static std::string parse_commit_file(const char* path, int J, bool with_stats, T
   return "";
 }
 
-static void append_cb(CB& d, const CB& s) {
-  const int64_t ebase = d.max_rep ? (int64_t)d.entry_def.size() : 0, cbase = (int64_t)d.chars.size();
-  d.row_def.insert(d.row_def.end(), s.row_def.begin(), s.row_def.end());
-  d.entry_def.insert(d.entry_def.end(), s.entry_def.begin(), s.entry_def.end());
-  d.fixed.insert(d.fixed.end(), s.fixed.begin(), s.fixed.end());
-  d.chars.insert(d.chars.end(), s.chars.begin(), s.chars.end());
-  for (size_t k = 1; k < s.row_offs.size(); k++) d.row_offs.push_back(s.row_offs[k] + ebase);
-  for (size_t k = 1; k < s.offs.size(); k++) d.offs.push_back(s.offs[k] + cbase);
+// Concatenates the files' parts in file order: every destination is sized once, then the files
+// copy (offsets rebased) into their slices in parallel and free their parts.
+static void concat_tail(dk_json_tail* t, std::vector<TailPart>& parts, int n_checkpoint_files) {
+  const int nf = (int)parts.size();
+  struct Base { int64_t row_def, entry_def, fixed, chars, row_offs, offs; };
+  std::vector<Base> base((size_t)(nf + 1) * JL_N);
+  std::vector<int64_t> row0(nf + 1, 0);
+  std::vector<int32_t> step0(nf + 1, 0);
+  for (int k = 0; k < JL_N; k++) base[k] = Base{0, 0, 0, 0, 1, 1};
+  for (int fi = 0; fi < nf; fi++) {
+    const TailPart& P = parts[fi];
+    for (int k = 0; k < JL_N; k++) {
+      const CB& c = P.col[k];
+      const Base& b = base[(size_t)fi * JL_N + k];
+      base[(size_t)(fi + 1) * JL_N + k] = Base{b.row_def + (int64_t)c.row_def.size(), b.entry_def + (int64_t)c.entry_def.size(),
+                                               b.fixed + (int64_t)c.fixed.size(), b.chars + (int64_t)c.chars.size(),
+                                               b.row_offs + (int64_t)c.row_offs.size() - 1, b.offs + (int64_t)c.offs.size() - 1};
+    }
+    row0[fi + 1] = row0[fi] + P.rows;
+    step0[fi + 1] = step0[fi] + P.n_steps;
+  }
+  for (int k = 0; k < JL_N; k++) {
+    CB& d = t->col[k];
+    const Base& e = base[(size_t)nf * JL_N + k];
+    d.row_def.resize(e.row_def); d.entry_def.resize(e.entry_def); d.fixed.resize(e.fixed); d.chars.resize(e.chars);
+    d.row_offs.resize(d.max_rep ? e.row_offs : 0); d.offs.resize(d.phys == PT_BYTE_ARRAY ? e.offs : 0);
+  }
+  t->rows = row0[nf];
+  t->n_steps = step0[nf];
+  t->step.resize(t->rows);
+  t->rowin.resize(t->rows);
+  t->file_row0.assign(row0.begin(), row0.end());
+  t->file_step0.assign(step0.begin(), step0.begin() + nf);
+  t->file_nsteps.resize(nf);
+  if (n_checkpoint_files > 0) t->ckpt_row0 = row0[nf - n_checkpoint_files];
+  parallel_for(nf, [&](int fi) {
+    TailPart& P = parts[fi];
+    for (int k = 0; k < JL_N; k++) {
+      CB& d = t->col[k];
+      const CB& c = P.col[k];
+      const Base& b = base[(size_t)fi * JL_N + k];
+      if (!c.row_def.empty()) memcpy(d.row_def.data() + b.row_def, c.row_def.data(), c.row_def.size());
+      if (!c.entry_def.empty()) memcpy(d.entry_def.data() + b.entry_def, c.entry_def.data(), c.entry_def.size());
+      if (!c.fixed.empty()) memcpy(d.fixed.data() + b.fixed, c.fixed.data(), c.fixed.size());
+      if (!c.chars.empty()) memcpy(d.chars.data() + b.chars, c.chars.data(), c.chars.size());
+      const int64_t ebase = d.max_rep ? b.entry_def : 0;
+      for (size_t i = 1; i < c.row_offs.size(); i++) d.row_offs[b.row_offs + i - 1] = c.row_offs[i] + ebase;
+      for (size_t i = 1; i < c.offs.size(); i++) d.offs[b.offs + i - 1] = c.offs[i] + b.chars;
+    }
+    for (int64_t i = 0; i < P.rows; i++) {
+      t->step[row0[fi] + i] = step0[fi] + P.step[i];
+      t->rowin[row0[fi] + i] = P.rowin[i];
+    }
+    t->file_nsteps[fi] = P.n_steps;
+    P = TailPart();
+  });
 }
 
 extern "C" int dk_json_tail_parse(dk_engine* e, const char* const* paths, const int64_t* versions, int32_t n_files,
@@ -3298,20 +3521,7 @@ extern "C" int dk_json_tail_parse_parts(dk_engine* e, const char* const* paths, 
   const auto t1 = clk::now();
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
-  for (int fi = 0; fi < n_files; fi++) {
-    TailPart& P = parts[fi];
-    if (fi == n_files - n_checkpoint_files) t->ckpt_row0 = t->rows;
-    t->file_row0.push_back(t->rows);
-    t->file_step0.push_back(t->n_steps);
-    t->file_nsteps.push_back(P.n_steps);
-    for (int k = 0; k < JL_N; k++) append_cb(t->col[k], P.col[k]);
-    for (int32_t st : P.step) t->step.push_back(t->n_steps + st);
-    t->rowin.insert(t->rowin.end(), P.rowin.begin(), P.rowin.end());
-    t->n_steps += P.n_steps;
-    t->rows += P.rows;
-    P = TailPart();
-  }
-  t->file_row0.push_back(t->rows);
+  concat_tail(t.get(), parts, n_checkpoint_files);
   if (getenv("DK_VERBOSE"))
     fprintf(stderr, "[dk] commit tail: %d files, %lld rows: parse %.1f ms, concatenate %.1f ms\n", n_files,
             (long long)t->rows, std::chrono::duration<double, std::milli>(t1 - t0).count(),
@@ -3531,14 +3741,19 @@ extern "C" int dk_log_pm_scan(const char* const* paths, int32_t n, int64_t* p_li
       at = next;
     }
   };
-  for (int32_t b0 = 0; b0 < n; b0 += 16) {
-    const int32_t b1 = std::min<int32_t>(n, b0 + 16);
+  // newest first, in batches of 16, 32, 64, ... files (a few thread launches for a long log; files
+  // past the batch where both turn up are never looked at, as the sequential reader would not)
+  bool hp = false, hm = false;
+  for (int32_t b0 = 0, bs = 16; b0 < n; b0 += bs, bs = std::min(bs * 2, 512)) {
+    const int32_t b1 = std::min<int32_t>(n, b0 + bs);
     parallel_for(b1 - b0, [&](int k) { scan(b0 + k); });
-    for (int32_t i = b0; i < b1; i++) if (!errs[i].empty()) return fail(errs[i]);
-    *n_scanned = b1;
-    bool hp = false, hm = false;
-    for (int32_t i = 0; i < b1; i++) { hp = hp || p_line[i] >= 0; hm = hm || m_line[i] >= 0; }
-    if (hp && hm) break;
+    for (int32_t i = b0; i < b1; i++) {             // in replay order: an error counts only before both are found
+      if (!errs[i].empty()) return fail(errs[i]);
+      hp = hp || p_line[i] >= 0;
+      hm = hm || m_line[i] >= 0;
+      *n_scanned = i + 1;
+      if (hp && hm) return 0;
+    }
   }
   return 0;
 }
@@ -3743,57 +3958,84 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   if (!e) return fail("null engine");
   const auto t_create0 = std::chrono::steady_clock::now();
   hipSetDevice(e->cfg.device);
+  ZcStage zs;   // declared before r: r's stream is synchronized before the staging block is freed
   std::unique_ptr<dk_replay> r(new dk_replay());
   r->eng = e; r->tail = tail;
-  if (r->own.create()) return 1;
+  if (r->own.create(replay_high_priority())) return 1;
   r->stream = r->own.s;
   r->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
   hipStream_t s = r->stream;
-  // actions: removes and adds of each tail row (a row may carry both)
-  std::vector<uint8_t> jchars;
+  // actions: removes and adds of each tail row (a row may carry both), built in parallel over row
+  // blocks. Their strings stay in the tail's columns: d_jchars holds the character buffers of the
+  // six key columns back to back and each action points into it.
+  static const int kKeyCols[6] = {JL_PATH, JL_RPATH, JL_DVST, JL_DVPID, JL_RDVST, JL_RDVPID};
+  int64_t jbase[JL_N] = {};
+  int64_t jchars_n = 0;
+  if (tail) for (int k : kKeyCols) { jbase[k] = jchars_n; jchars_n += (int64_t)tail->col[k].chars.size(); }
   int64_t canon_n = 0;
+  std::vector<int64_t> arow, soff;
+  std::vector<int32_t> slen;
   if (tail) {
     const CB* c = tail->col;
-    auto add_str = [&](const CB& col, int64_t row, int64_t* off, int32_t* len) {
-      int64_t b = col.offs[row], en = col.offs[row + 1];
-      *off = (int64_t)jchars.size(); *len = (int32_t)(en - b);
-      jchars.insert(jchars.end(), col.chars.begin() + b, col.chars.begin() + en);
-    };
-    for (int64_t row = 0; row < tail->rows; row++) {
-      // rows of a JSON checkpoint part: adds are checkpoint adds, removes are ignored
-      // (ActiveAddFilesIterator.java:163-183 reads tombstones only from commit files)
-      const bool ck = tail->ckpt_row0 >= 0 && row >= tail->ckpt_row0;
-      for (int kind : {JA_REMOVE, JA_ADD}) {
-        if (ck && kind == JA_REMOVE) continue;
-        const CB& pc = c[kind == JA_ADD ? JL_PATH : JL_RPATH];
-        if (pc.row_def[row] < 1) continue;
-        DJsonAction a{};
-        a.kind = ck ? JA_CKADD : kind; a.step = tail->step[row]; a.row = tail->rowin[row];
-        add_str(pc, row, &a.path_off, &a.path_len);
-        const CB& st = c[kind == JA_ADD ? JL_DVST : JL_RDVST];
-        const CB& pid = c[kind == JA_ADD ? JL_DVPID : JL_RDVPID];
-        const CB& off = c[kind == JA_ADD ? JL_DVOFF : JL_RDVOFF];
-        a.has_dv = st.row_def[row] >= 2;
-        if (a.has_dv) {
-          add_str(st, row, &a.st_off, &a.st_len);
-          add_str(pid, row, &a.pid_off, &a.pid_len);
-          a.has_off = off.row_def[row] == 3;
-          if (a.has_off) memcpy(&a.dv_off, off.fixed.data() + row * 4, 4);
+    const int64_t R = tail->rows;
+    const int nb = (int)std::min<int64_t>(64, std::max<int64_t>(1, R / 2048));
+    std::vector<int64_t> b_na(nb + 1, 0), b_canon(nb + 1, 0);
+    // rows of a JSON checkpoint part: adds are checkpoint adds, removes are ignored
+    // (ActiveAddFilesIterator.java:163-183 reads tombstones only from commit files)
+    auto each = [&](int bi, bool fill) {
+      const int64_t r0 = R * bi / nb, r1 = R * (bi + 1) / nb;
+      int64_t ai = fill ? b_na[bi] : 0, co = fill ? b_canon[bi] : 0;   // (counting: this block's own)
+      for (int64_t row = r0; row < r1; row++) {
+        const bool ck = tail->ckpt_row0 >= 0 && row >= tail->ckpt_row0;
+        for (int kind : {JA_REMOVE, JA_ADD}) {
+          if (ck && kind == JA_REMOVE) continue;
+          const int pk = kind == JA_ADD ? JL_PATH : JL_RPATH;
+          const CB& pc = c[pk];
+          if (pc.row_def[row] < 1) continue;
+          const int sk = kind == JA_ADD ? JL_DVST : JL_RDVST, ik = kind == JA_ADD ? JL_DVPID : JL_RDVPID;
+          const CB& st = c[sk];
+          const bool has_dv = st.row_def[row] >= 2;
+          const int32_t path_len = (int32_t)(pc.offs[row + 1] - pc.offs[row]);
+          const int32_t st_len = has_dv ? (int32_t)(st.offs[row + 1] - st.offs[row]) : 0;
+          const int32_t pid_len = has_dv ? (int32_t)(c[ik].offs[row + 1] - c[ik].offs[row]) : 0;
+          if (fill) {
+            DJsonAction a{};
+            a.kind = ck ? JA_CKADD : kind; a.step = tail->step[row]; a.row = tail->rowin[row];
+            a.path_off = jbase[pk] + pc.offs[row]; a.path_len = path_len;
+            a.has_dv = has_dv;
+            if (has_dv) {
+              const CB& off = c[kind == JA_ADD ? JL_DVOFF : JL_RDVOFF];
+              a.st_off = jbase[sk] + st.offs[row]; a.st_len = st_len;
+              a.pid_off = jbase[ik] + c[ik].offs[row]; a.pid_len = pid_len;
+              a.has_off = off.row_def[row] == 3;
+              if (a.has_off) memcpy(&a.dv_off, off.fixed.data() + row * 4, 4);
+            }
+            a.canon_off = co;
+            r->acts[ai] = a;
+            r->act_row[ai] = row;
+          }
+          ai++;
+          co += path_len + 64 + st_len + pid_len + 32;
         }
-        a.canon_off = canon_n;
-        canon_n += a.path_len + 64 + a.st_len + a.pid_len + 32;
-        r->acts.push_back(a);
-        r->act_row.push_back(row);
       }
-    }
+      if (!fill) { b_na[bi + 1] = ai; b_canon[bi + 1] = co; }
+    };
+    parallel_for(nb, [&](int bi) { each(bi, false); });        // per block: actions, canonical bytes
+    for (int bi = 0; bi < nb; bi++) { b_na[bi + 1] += b_na[bi]; b_canon[bi + 1] += b_canon[bi]; }
+    r->acts.resize(b_na[nb]);
+    r->act_row.resize(b_na[nb]);
+    parallel_for(nb, [&](int bi) { each(bi, true); });
+    canon_n = b_canon[nb];
   }
   size_t na = r->acts.size();
   const auto t_built = std::chrono::steady_clock::now();
   uint64_t cap = 1024;
   while (cap < 2 * na + 16) cap <<= 1;
   r->mask = cap - 1;
-  if (upload(r->d_acts, r->acts.data(), na * sizeof(DJsonAction), s)) return 1;
-  if (upload(r->d_jchars, jchars.data(), jchars.size(), s)) return 1;
+  if (zs.add(r->d_acts, r->acts.data(), na * sizeof(DJsonAction))) return 1;
+  if (r->d_jchars.alloc(jchars_n + 16)) return 1;
+  if (tail)
+    for (int k : kKeyCols) zs.add_raw(r->d_jchars.as<uint8_t>() + jbase[k], tail->col[k].chars.data(), tail->col[k].chars.size());
   if (r->d_canon.alloc(canon_n + 64)) return 1;
   if (r->d_slots.alloc(cap * sizeof(Slot))) return 1;
   if (r->d_fp.alloc(cap * sizeof(uint32_t))) return 1;
@@ -3803,13 +4045,13 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   // checkpoint's decoded key / value leaves
   auto up = [&](const void* src, size_t n) -> void* {
     r->map_bufs.emplace_back(new DBuf());
-    if (upload(*r->map_bufs.back(), src, n, s)) return nullptr;
+    if (zs.add(*r->map_bufs.back(), src, n)) return nullptr;
     return r->map_bufs.back()->p;
   };
   if (tail) {
     const CB& kc = tail->col[JL_PVK];
     const CB& vc = tail->col[JL_PVV];
-    std::vector<int64_t> arow(na);
+    arow.assign(na, 0);
     for (size_t i = 0; i < na; i++) arow[i] = r->acts[i].kind != JA_REMOVE ? r->act_row[i] : -1;
     MapRows M{};
     M.n = (int64_t)na;
@@ -3830,18 +4072,19 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
   // stats strings for data skipping: the tail's per action (adds only), the checkpoint's column
   if (tail && tail->with_stats) {
     const CB& sc = tail->col[JL_STATS];
-    std::vector<int64_t> soff(na + 1, 0);
-    std::vector<int32_t> slen(na + 1, -1);
+    soff.assign(na + 1, 0);
+    slen.assign(na + 1, -1);
     for (size_t i = 0; i < na; i++) {
       const int64_t row = r->act_row[i];
       if (r->acts[i].kind == JA_REMOVE || sc.row_def[row] < 2) continue;
       soff[i] = sc.offs[row];
       slen[i] = (int32_t)(sc.offs[row + 1] - sc.offs[row]);
     }
-    if (upload(r->d_tstats_chars, sc.chars.data(), sc.chars.size(), s)) return 1;
-    if (upload(r->d_tstats_off, soff.data(), soff.size() * 8, s)) return 1;
-    if (upload(r->d_tstats_len, slen.data(), slen.size() * 4, s)) return 1;
+    if (zs.add(r->d_tstats_chars, sc.chars.data(), sc.chars.size())) return 1;
+    if (zs.add(r->d_tstats_off, soff.data(), soff.size() * 8)) return 1;
+    if (zs.add(r->d_tstats_len, slen.data(), slen.size() * 4)) return 1;
   }
+  if (zs.flush(s)) return 1;
   const auto t_queued = std::chrono::steady_clock::now();
   HIPOK(hipStreamSynchronize(s));
   if (getenv("DK_VERBOSE")) {
@@ -4306,11 +4549,7 @@ static void replay_file_filters(dk_replay* r, size_t fi) {
 // then an event the host waits on before handing out those files' batches
 static int replay_grouped(dk_replay* r, uint64_t h_nodv) {
   hipStream_t s = r->stream;
-  KTimer& T = r->timer;
   dk_parquet* p = r->ck;
-  DState* st = r->d_state.as<DState>();
-  DJsonAction* A = r->d_acts.as<DJsonAction>();
-  Slot* S = r->d_slots.as<Slot>();
   const int nf = (int)p->files.size();
   const int ng = std::max(1, std::min(r->n_groups, nf));
   r->grp_f0.assign(ng + 1, 0);
@@ -4426,6 +4665,9 @@ static int issue_group(dk_replay* r) {
         if (p->colmap[f][leaf] >= 0 && queue_mirror(p, p->colmap[f][leaf])) return 1;
   }
   r->grp_issued = g + 1;
+  if (getenv("DK_VERBOSE"))
+    fprintf(stderr, "[dk] group %d (files [%d, %d)) issued at %.1f ms\n", g, r->grp_f0[g], r->grp_f0[g + 1],
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - p->t_open0).count());
   if (r->grp_issued == ng) HIPOK(hipEventRecord(r->ev_out, s));   // the checkpoint stream waits for it at dk_replay_sync
   return 0;
 }
@@ -4468,7 +4710,7 @@ extern "C" int dk_replay_run_grouped(dk_replay* r, int32_t n_groups) {
   r->file_ready.clear();
   if (r->ck && invalidate_mirrors(r->ck)) return 1;
   r->n_groups = n_groups;
-  if (!r->aux.s && r->aux.create()) return 1;
+  if (!r->aux.s && r->aux.create(replay_high_priority())) return 1;
   return replay_launch(r);
 }
 
@@ -4502,6 +4744,13 @@ extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
     while (r->grp_issued <= g) if (issue_group(r)) return 1;   // lazy runs issue groups on demand
     ev = r->grp_ev[g];
   }
+  // ... and every later group whose files the open has decoded already, so that their probes and
+  // selection copies run while the consumer works on this one
+  if (r->run_lazy) {
+    const int ng = (int)r->grp_f0.size() - 1;
+    while (r->grp_issued < ng && files_ready_now(r->ck, r->grp_f0[r->grp_issued + 1]))
+      if (issue_group(r)) return 1;
+  }
   int slot = 0;
   if (file >= 0) {
     int g = 0;
@@ -4509,6 +4758,9 @@ extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
     slot = g + 1;
   }
   HIPOK(hipEventSynchronize(ev));
+  if (getenv("DK_VERBOSE") && file >= 0 && r->ck)
+    fprintf(stderr, "[dk] file %d ready at %.1f ms\n", file,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - r->ck->t_open0).count());
   DState st{}, ps{};
   memcpy(&st, r->h_zstate.data() + (size_t)slot * 2 * sizeof(DState), sizeof st);
   memcpy(&ps, r->h_zstate.data() + (size_t)slot * 2 * sizeof(DState) + sizeof(DState), sizeof ps);
@@ -5190,7 +5442,7 @@ extern "C" int dk_replay_stats_parsed_files(dk_replay* r) {
 extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {
   if (i < 0 || i >= KTimer::K) return 1;
   // decode kernels are timed by the parquet object's timer, the rest by the replay's
-  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16) || (i >= 19 && i <= 21))) ? &r->ck->timer : &r->timer;
+  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16) || (i >= 19 && i <= 21) || i == 24)) ? &r->ck->timer : &r->timer;
   *name = t->names[i];
   if (!*name) return 1;
   *count = t->cnt[i];

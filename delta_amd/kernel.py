@@ -1354,7 +1354,7 @@ class GpuScan:
 
     def kernel_stats(self):
         out = {}
-        for i in range(24):
+        for i in range(32):
             name, avg, cnt = C.c_char_p(), C.c_double(), C.c_int64()
             if lib().dk_replay_kernel_stats(self._rh, i, C.byref(name), C.byref(avg), C.byref(cnt)) != 0:
                 continue
@@ -1468,12 +1468,18 @@ class GpuScan:
             b.data._fetch = None
 
     def close(self):
+        t0 = time.perf_counter()
         if getattr(self, "_handed", None):
             self._detach_batches()
+        t1 = time.perf_counter()
         if getattr(self, "_rh", None):
             lib().dk_replay_free(self._rh)
             self._rh = None
+        t2 = time.perf_counter()
         for o in ("ckpt", "tail"):
             x = getattr(self, o, None)
             if x is not None:
                 x.close()
+        t3 = time.perf_counter()
+        # where close() spends its time (bench.py's DK_CONSUME_PROFILE block)
+        self.close_ms = dict(close_detach=(t1 - t0) * 1e3, close_replay=(t2 - t1) * 1e3, close_inputs=(t3 - t2) * 1e3)

@@ -33,6 +33,25 @@ def test_scan_parity(tmp_path, name, jbs):
     assert_same(product_scan(str(tmp_path), jbs), oracle_scan(str(tmp_path), jbs))
 
 
+@pytest.mark.parametrize("jbs", [1024, 7])
+def test_large_tail_parity(tmp_path, jbs):
+    """A commit tail of ~28k rows: the replay's action table is built in parallel over row blocks
+    (dk_replay_create), and the tail's columns are concatenated from the per-commit parses."""
+    spec = synth.TableSpec(n_adds=20_000, n_commits=40, adds_per_commit=400, removes_per_commit=300,
+                           pv_keys=2, dv_frac=0.2, seed=synth.SEED + 31)
+    synth.write_table(str(tmp_path), spec)
+    assert_same(product_scan(str(tmp_path), jbs), oracle_scan(str(tmp_path), jbs))
+
+
+def test_large_json_manifest_parity(tmp_path):
+    """V2 JSON manifest with 9000 add rows after the commits: checkpoint adds inside the tail, across
+    several of the replay's build blocks."""
+    spec = synth.TableSpec(n_adds=30_000, n_commits=10, n_parts=2, v2_sidecars=2, v2_manifest="json",
+                           v2_json_adds=9000, seed=synth.SEED + 32)
+    synth.write_table(str(tmp_path), spec)
+    assert_same(product_scan(str(tmp_path), 1024), oracle_scan(str(tmp_path), 1024))
+
+
 def test_multipart_parity(tmp_path):
     spec = synth.TableSpec(n_adds=30_000, n_parts=4, n_commits=8, dv_frac=0.1)
     synth.write_table(str(tmp_path), spec)
