@@ -1362,11 +1362,26 @@ static int alloc_outputs(dk_parquet* p, int c0, int c1, const std::vector<DColum
   return 0;
 }
 
-// Per-slice output allocation + value decode inside the open (DK_SLICE_DECODE=1; off by default
-// until measured on the GPU): the prerequisite of dk_parquet_open_async's overlap
+// Per-slice output allocation + value decode inside the open: the prerequisite of
+// dk_parquet_open_async's overlap, on for asynchronous opens (DK_SLICE_DECODE=0 turns it and with it
+// the asynchronous open off; =1 turns it on for synchronous opens too)
 static bool slice_decode_on() {
+  static const bool on = !(getenv("DK_SLICE_DECODE") && atoi(getenv("DK_SLICE_DECODE")) == 0);
+  return on;
+}
+static bool slice_decode_forced() {
   static const bool on = getenv("DK_SLICE_DECODE") && atoi(getenv("DK_SLICE_DECODE")) != 0;
   return on;
+}
+
+// hipEventQuery: 1 complete, 0 not yet, -1 an error (reported through fail): a sticky device fault
+// must end the open's polling loops with that error instead of polling forever
+static int ev_done(hipEvent_t e) {
+  const hipError_t q = hipEventQuery(e);
+  if (q == hipSuccess) return 1;
+  if (q == hipErrorNotReady) return 0;
+  fail(std::string("HIP error: ") + hipGetErrorString(q) + " (an event of the checkpoint open)");
+  return -1;
 }
 
 // Wait until file f's image copies are queued (file_ev recorded: a stream may wait for it; an event
@@ -1651,7 +1666,7 @@ static int prepare(dk_parquet* p) {
     const int64_t target = std::max<int64_t>(1, total / slices);
     int f0 = 0;
     int64_t acc = 0;
-    per_slice = adaptive && slices > 1 && slice_decode_on();
+    per_slice = adaptive && slices > 1 && (p->async_open ? slice_decode_on() : slice_decode_forced());
     std::vector<SizedSlice> sized;
     if (per_slice) {
       // string-copy tiles: a bound from the headers (PLAIN byte-array data pages and key-column
@@ -1688,17 +1703,40 @@ static int prepare(dk_parquet* p) {
           HIPOK(hipStreamWaitEvent(ss[k], tables, 0));
         }
       }
-      if (per_slice && !p->dec.s && p->dec.create(true)) return 1;
+      if (per_slice && !p->dec.s && p->dec.create(true)) { if (tables) hipEventDestroy(tables); return 1; }
+      // on any error return: drain the streams the loop queued work on, then free its events (the
+      // remaining slices' and `tables`)
+      struct LoopGuard {
+        hipEvent_t& tables; std::vector<SizedSlice>& sized; hipStream_t* ss; int nss; hipStream_t dec; bool armed = true;
+        ~LoopGuard() {
+          if (!armed) return;
+          for (int k = 0; k < nss; k++) if (ss[k]) hipStreamSynchronize(ss[k]);
+          if (dec) hipStreamSynchronize(dec);
+          for (SizedSlice& S : sized) if (S.ev) { hipEventDestroy(S.ev); S.ev = nullptr; }
+          if (tables) { hipEventDestroy(tables); tables = nullptr; }
+        }
+      } guard{tables, sized, ss, nss, p->dec.s};
       int slice = 0;
       while (f0 < nf) {
         int f1 = f0;
         acc = 0;
         // at least `target` bytes (or the rest), then every file already landed
-        while (f1 < nf && (acc < target || (is_queued(p, f1) && hipEventQuery(p->file_ev[f1]) == hipSuccess))) {
+        for (;;) {
+          if (f1 >= nf) break;
+          if (acc >= target) {
+            const int landed = is_queued(p, f1) ? ev_done(p->file_ev[f1]) : 0;
+            if (landed < 0) return 1;
+            if (!landed) break;
+          }
           // while the next file lands, finish the sized slices whose passes are done (never block
           // the loop on them: the next slice is queued as soon as its files are in)
-          while (per_slice && !(is_queued(p, f1) && hipEventQuery(p->file_ev[f1]) == hipSuccess)) {
-            if (!sized.empty() && hipEventQuery(sized.front().ev) == hipSuccess) {
+          while (per_slice) {
+            const int landed = is_queued(p, f1) ? ev_done(p->file_ev[f1]) : 0;
+            if (landed < 0) return 1;
+            if (landed) break;
+            const int sdone = sized.empty() ? 0 : ev_done(sized.front().ev);
+            if (sdone < 0) return 1;
+            if (sdone) {
               if (finish_slice(p, sized.front(), got)) return 1;
               sized.erase(sized.begin());
             } else if (p->queued && p->queued[f1].load() == 2) {
@@ -1707,7 +1745,7 @@ static int prepare(dk_parquet* p) {
               std::this_thread::sleep_for(std::chrono::microseconds(50));
             }
           }
-          if (!wait_queued(p, f1)) { if (tables) hipEventDestroy(tables); return 1; }   // parquet_open reports the read error
+          if (!wait_queued(p, f1)) return 1;     // parquet_open reports the read error
           HIPOK(hipEventSynchronize(p->file_ev[f1]));
           acc += (int64_t)p->files[f1].bytes.size();
           f1++;
@@ -1717,6 +1755,9 @@ static int prepare(dk_parquet* p) {
         if (verbose) fprintf(stderr, "[dk] sizing slice %d: files [%d, %d) %.1f MB queued at %.1f ms\n", slice - 1, f0, f1,
                              acc / 1e6, since(p->t_open0));
         for (int f = f0; f < f1; f++) HIPOK(hipStreamWaitEvent(cs, p->file_ev[f], 0));
+        // test hook (tests/test_async_open.py): an error in the middle of the sliced loop
+        static const int inject = getenv("DK_INJECT_SLICE_FAULT") ? atoi(getenv("DK_INJECT_SLICE_FAULT")) : -1;
+        if (slice - 1 == inject) return fail("injected fault in checkpoint open slice " + std::to_string(inject));
         const PRange R = file_range(p, f0, f1);
         sizing_stages(p, cs, R);
         if (per_slice) {
@@ -1729,9 +1770,12 @@ static int prepare(dk_parquet* p) {
           launch_copy_zc(S.cols.data(), p->d_cols.as<DColumn>() + R.col0, (long long)(R.col1 - R.col0) * sizeof(DColumn), cs);
           launch_copy_zc(S.pages.data(), p->d_pages.as<DPage>() + R.pa, (long long)(R.pb - R.pa) * sizeof(DPage), cs);
           HIPOK(hipEventCreateWithFlags(&S.ev, hipEventDisableTiming));
-          HIPOK(hipEventRecord(S.ev, cs));
           sized.push_back(std::move(S));
-          while (!sized.empty() && hipEventQuery(sized.front().ev) == hipSuccess) {
+          HIPOK(hipEventRecord(sized.back().ev, cs));
+          for (;;) {
+            const int sdone = sized.empty() ? 0 : ev_done(sized.front().ev);
+            if (sdone < 0) return 1;
+            if (!sdone) break;
             if (finish_slice(p, sized.front(), got)) return 1;
             sized.erase(sized.begin());
           }
@@ -1751,6 +1795,7 @@ static int prepare(dk_parquet* p) {
         HIPOK(hipEventRecord(tables, p->dec.s));
         HIPOK(hipStreamWaitEvent(s, tables, 0));
       }
+      guard.armed = false;
       if (tables) hipEventDestroy(tables);
     } else {
       for (int f = 0; f < nf; f++) {
@@ -2150,75 +2195,21 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
                         const int32_t* field_ids = nullptr, const std::function<void(dk_parquet*)>* publish = nullptr);
 
-// A process-wide pool of host worker threads behind parallel_for: a call no longer launches (and
-// joins) its own threads -- the commit P&M scan alone makes several calls, the open and the tail
-// parse one each. The caller works on its own job as well, so a parallel_for issued from inside a
-// pool task (nested) always completes, even with every worker busy; and so does one issued in a
-// forked child, which has no workers.
-struct HostPool {
-  struct Job {
-    std::function<void(int)> fn;
-    int n = 0;
-    std::atomic<int> next{0}, done{0};
-    std::mutex m;
-    std::condition_variable cv;
-  };
-  std::mutex mu;
-  std::condition_variable cv;
-  std::deque<std::shared_ptr<Job>> q;
-  explicit HostPool(int n) { for (int i = 0; i < n; i++) std::thread([this] { work(); }).detach(); }
-  size_t rr = 0;
-  static bool run_one(Job& j) {
-    const int i = j.next.fetch_add(1);
-    if (i >= j.n) return false;
-    j.fn(i);
-    if (j.done.fetch_add(1) + 1 == j.n) { std::lock_guard<std::mutex> g(j.m); j.cv.notify_all(); }
-    return true;
-  }
-  static void run(Job& j) { while (run_one(j)) {} }
-  // workers take one index at a time from the jobs in turn (concurrent callers -- the open's file
-  // reads and the commit-tail parse -- share the workers instead of queueing behind each other)
-  void work() {
-    for (;;) {
-      std::shared_ptr<Job> j;
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        for (;;) {
-          while (!q.empty() && q.front()->next.load() >= q.front()->n) q.pop_front();   // exhausted
-          if (!q.empty()) break;
-          cv.wait(lk);
-        }
-        j = q[rr++ % q.size()];
-      }
-      run_one(*j);
-    }
-  }
-  void parallel(int n, int width, std::function<void(int)> fn) {
-    auto j = std::make_shared<Job>();
-    j->fn = std::move(fn);
-    j->n = n;
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      q.push_back(j);
-    }
-    for (int k = 1; k < width; k++) cv.notify_one();
-    run(*j);
-    std::unique_lock<std::mutex> lk(j->m);
-    j->cv.wait(lk, [&] { return j->done.load() == j->n; });
-  }
-};
-static int io_threads() {
-  static const int nt = getenv("DK_IO_THREADS") && atoi(getenv("DK_IO_THREADS")) > 0 ? atoi(getenv("DK_IO_THREADS")) : 16;
-  return nt;
-}
-static HostPool& host_pool() { static HostPool* p = new HostPool(io_threads() - 1); return *p; }
-
-// fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads (the caller and the pool's)
+// fn(i) for i in [0, n) on up to DK_IO_THREADS (default 16) host threads. (A persistent pool with
+// prioritised jobs was measured against these per-call threads and lost: 188-193 / 192-206 ms with
+// per-call threads against 206-209 / 206-207 ms pooled, async / default open, same box,
+// profiles/r04/pool_ab.)
 template <class F>
 static void parallel_for(int n, F fn) {
-  const int nt = std::min(io_threads(), n);
+  int nt = 16;
+  if (const char* v = getenv("DK_IO_THREADS")) nt = atoi(v) > 0 ? atoi(v) : 1;
+  if (nt > n) nt = n;
   if (nt <= 1) { for (int i = 0; i < n; i++) fn(i); return; }
-  host_pool().parallel(n, nt, std::function<void(int)>(fn));
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++)
+    th.emplace_back([&] { for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
+  for (auto& x : th) x.join();
 }
 
 // Many small host -> device uploads gathered into one pinned block and copied by kernels
@@ -4020,7 +4011,7 @@ extern "C" int dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ck
       }
       if (!fill) { b_na[bi + 1] = ai; b_canon[bi + 1] = co; }
     };
-    parallel_for(nb, [&](int bi) { each(bi, false); });        // per block: actions, canonical bytes
+    parallel_for(nb, [&](int bi) { each(bi, false); });     // per block: actions, canonical bytes
     for (int bi = 0; bi < nb; bi++) { b_na[bi + 1] += b_na[bi]; b_canon[bi + 1] += b_canon[bi]; }
     r->acts.resize(b_na[nb]);
     r->act_row.resize(b_na[nb]);

@@ -1164,6 +1164,7 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
 template __global__ void k_snap_frag_t<false>(SnapCtx, const int2*, int);
 template __global__ void k_snap_frag_t<true>(SnapCtx, const int2*, int);
 
+
 // Serial path (pages flagged by k_snap_fix / k_snap_frag): every lane parses the same tag (uniform
 // control flow), then the wave copies the literal / back-reference 64 bytes per step. Back
 // references read bytes other lanes stored earlier, so a workgroup-scope acq_rel fence orders
@@ -4153,6 +4154,7 @@ void snap_stats(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SY
 // SX_NOWRITE | flags over the same work
 static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s) {
   static const int exp = getenv("DK_SNAP_EXP") ? atoi(getenv("DK_SNAP_EXP")) : -1;
+
   if (exp < 0) { hipLaunchKernelGGL(k_snap_frag_t<false>, dim3(n), dim3(64), 0, s, X, work, 0); return; }
   hipLaunchKernelGGL(k_snap_frag_t<false>, dim3(n), dim3(64), 0, s, X, work, 0);
   hipLaunchKernelGGL(k_snap_frag_t<true>, dim3(n), dim3(64), 0, s, X, work, exp | SX_NOWRITE);

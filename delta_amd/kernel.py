@@ -1294,8 +1294,9 @@ class GpuScan:
         t2 = time.perf_counter()
         # a plain scan (no shard, skipping or partition filter) opens the checkpoint asynchronously: the
         # grouped getScanFiles hands out the first files' batches while the later files still land
+        # (DK_ASYNC_OPEN=0: the synchronous open)
         plain = not self.shard and self.skipping is None and self.partition is None and self.predicate is None and \
-            scan_groups(len(self.ckpt_files or [])) and os.environ.get("DK_ASYNC_OPEN", "0") != "0"
+            scan_groups(len(self.ckpt_files or [])) and os.environ.get("DK_ASYNC_OPEN", "1") != "0"
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel, async_open=bool(plain)) \
             if self.ckpt_files else None
         t3 = time.perf_counter()
