@@ -554,7 +554,7 @@ def main(argv=None):
     step_gbs = step_bytes / (step_us * 1e-6) / 1e9 if step_us else None
     # roofline of the dominant kernel with a byte model (dk_parquet_kernel_traffic):
     # algorithmic bytes of one launch / its average launch time (HIP events on the replay stream)
-    modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy", "k_plain_copy", "k_probe") if k in kern]
+    modelled = [k for k in ("k_snap_frag", "k_tile_decode", "k_string_copy", "k_probe") if k in kern]
     rk = max(modelled, key=lambda k: kern[k]) if modelled else None
     # every modelled kernel's own roofline fraction (same byte models, same HIP-event averages)
     kern_roof = {}

@@ -40,13 +40,11 @@ void launch_copy_zc(void*, const void*, long long, hipStream_t);
 void launch_arrow_window(const ArrowWin&, hipStream_t);
 void launch_dv_expand(const DvCont*, int, const uint8_t*, unsigned long long*, hipStream_t);
 void launch_dv_select(const unsigned long long*, long long, const long long*, long long, uint8_t*, hipStream_t);
-void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, int, hipStream_t);
-void launch_plain_copy(const DChunk*, DPage*, const DColumn*, const uint8_t*, int32_t*, const DPosChunk*, int, int, int, int,
-                       unsigned long long*, unsigned int*, int32_t*, DState*, hipStream_t);
+void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
 void launch_tile_scan1(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
-void launch_tile_chars(const DChunk*, DPage*, const uint8_t*, const int32_t*, const Seg*, DTile*, int, int, int, hipStream_t);
+void launch_tile_chars(const DChunk*, DPage*, const uint8_t*, const int32_t*, const Seg*, DTile*, int, int, hipStream_t);
 void launch_tile_scan2(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
 void launch_tile_decode(const DChunk*, DPage*, const DColumn*, const uint8_t*, const int32_t*, const long long*, const Seg*, const DTile*, int, int, DState*, hipStream_t);
 void launch_delta_decode(const DChunk*, DPage*, int, const uint8_t*, long long*, hipStream_t);
@@ -139,8 +137,10 @@ extern "C" int dk_engine_create(const dk_config* cfg, dk_engine** out) {
   return 0;
 }
 
+static void reaper_drain_all();
 extern "C" void dk_engine_destroy(dk_engine* e) {
   if (!e) return;
+  reaper_drain_all();
   hipSetDevice(e->cfg.device);
   delete e;
 }
@@ -159,6 +159,35 @@ extern "C" void dk_engine_destroy(dk_engine* e) {
 // release inside a SyncedRelease scope once their stream is drained (object close / free), and
 // those blocks are reusable at once; any other release parks the block, and parked blocks are only
 // reused after the cache itself drains the device (when trimming).
+// Deferred release: a closed call object (dk_parquet_close, dk_json_tail_free) is deleted on a
+// background thread -- host tables, events, blocks back to the caches -- so that close returns at
+// once. A cache lookup that misses waits for pending releases before allocating afresh (the next
+// scan's blocks are usually the ones being released), and dk_engine_destroy / process exit wait for
+// all of them.
+struct Reaper {
+  std::mutex mu;
+  std::condition_variable cv;
+  int pending = 0;
+  void run(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (pending++ == 0 && !registered) { registered = true; std::atexit([] { reaper_drain(); }); }
+    }
+    std::thread([this, f] {
+      f();
+      std::lock_guard<std::mutex> g(mu);
+      if (--pending == 0) cv.notify_all();
+    }).detach();
+  }
+  bool busy() { std::lock_guard<std::mutex> g(mu); return pending > 0; }
+  void drain() { std::unique_lock<std::mutex> lk(mu); cv.wait(lk, [&] { return pending == 0; }); }
+  bool registered = false;
+  static void reaper_drain();
+};
+static Reaper& reaper() { static Reaper* r = new Reaper(); return *r; }
+void Reaper::reaper_drain() { reaper().drain(); }
+static void reaper_drain_all() { reaper().drain(); }
+
 static thread_local int t_synced = 0;
 struct SyncedRelease {
   SyncedRelease() { t_synced++; }
@@ -202,6 +231,10 @@ struct MemCache {
         *got = b.n;
         return b.p;
       }
+    }
+    if (reaper().busy()) {         // a deferred release may be returning just such a block
+      reaper().drain();
+      return get(want, got);
     }
     void* p = nullptr;
     if (raw_alloc(&p, n)) {        // out of memory: give back every cached block of this device, retry
@@ -850,13 +883,12 @@ static int phys_width(int phys, int tl) {
 // kernel timing (HIP events on the engine stream)
 // ------------------------------------------------------------------------------------------------
 struct KTimer {
-  static constexpr int K = 25;
+  static constexpr int K = 24;
   const char* names[K] = {"k_page_headers", "unused", "k_tile_count", "k_tile_scan",
                           "k_string_positions", "k_tile_decode", "k_string_copy", "k_json_canon",
                           "k_table_insert", "k_table_update", "k_json_select", "k_probe", "step_total",
                           "k_snap_walk_link", "k_delta_decode", "k_page_runs", "k_tile_chars", "k_stats_eval", "k_part_eval",
-                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", "k_owner_route", "k_owner_resolve",
-                          "k_plain_copy"};
+                          "k_snap_fix", "k_snap_frag", "k_snappy_serial", "k_owner_route", "k_owner_resolve"};
   double sum_ms[K] = {0};
   int64_t cnt[K] = {0};
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -950,7 +982,6 @@ struct dk_parquet {
   int n_ltiles = 0;
   DBuf d_pchunks;            // string-position chunks (DPosChunk)
   int n_pchunks = 0;
-  DBuf d_pstat, d_pfail, d_ptick;   // k_plain_copy: chunk look-back words, page redo flags, tickets
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
   std::vector<int> col_tile0;
@@ -1075,13 +1106,6 @@ static PRange file_range(const dk_parquet* p, int f0, int f1) {
   return R;
 }
 
-// PLAIN string pages in one pass at decode time (k_plain_copy); DK_PLAIN_FUSED=0: positions in the
-// sizing passes and k_string_copy tiles (A/B)
-static bool plain_fused() {
-  static const bool on = !(getenv("DK_PLAIN_FUSED") && atoi(getenv("DK_PLAIN_FUSED")) == 0);
-  return on;
-}
-
 // headers, snappy, runs, counts, positions, chars and the scans over one slice
 static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
   KTimer& T = p->timer;
@@ -1125,9 +1149,9 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
   };
   { KTimer::Scope sc(&T, 2, s); tiles([&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
-  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0, plain_fused(), s); }
+  { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0, s); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P + R.pa, np, arena, p->d_dbp.as<long long>(), s); }
-  { KTimer::Scope sc(&T, 16, s); tiles([&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, plain_fused(), s); }); }
+  { KTimer::Scope sc(&T, 16, s); tiles([&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
 }
 
@@ -1145,17 +1169,6 @@ static void decode_cols(dk_parquet* p, hipStream_t s, int c0, int c1) {
   const long long* dbp = p->d_dbp.as<long long>();
   DTile* LT = p->d_ltiles.as<DTile>();
   Seg* runs = p->d_runs.as<Seg>();
-  if (plain_fused()) {
-    // the columns' pages (decode ranges are whole files) and their position chunks
-    const int f0 = (int)(std::lower_bound(p->file_col0.begin(), p->file_col0.end(), c0) - p->file_col0.begin());
-    const int f1 = (int)(std::lower_bound(p->file_col0.begin(), p->file_col0.end(), c1) - p->file_col0.begin());
-    const int pa = p->file_page0[f0], pb = p->file_page0[f1];
-    const int pc0 = pa < p->n_pages ? p->h_pages[pa].pchunk0 : p->n_pchunks;
-    const int pc1 = pb < p->n_pages ? p->h_pages[pb].pchunk0 : p->n_pchunks;
-    KTimer::Scope sc(&T, 24, s);
-    launch_plain_copy(C, P, cols, arena, pos, p->d_pchunks.as<DPosChunk>(), pc0, pc1 - pc0, pa, pb - pa,
-                      p->d_pstat.as<unsigned long long>(), p->d_ptick.as<unsigned int>() + c0, p->d_pfail.as<int32_t>(), st, s);
-  }
   {
     KTimer::Scope sc(&T, 6, s);
     const int2* tiles = p->d_tiles.as<int2>();
@@ -1287,7 +1300,7 @@ static void build_tiles(dk_parquet* p, int c0, int c1, std::vector<int2>& tiles)
     const DColumn& c = p->h_cols[ci];
     for (int pi = c.first_page; pi < c.first_page + c.n_pages; pi++) {
       const DPage& pg = p->h_pages[pi];
-      if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN || plain_fused()) continue;
+      if (c.phys != PT_BYTE_ARRAY || (pg.flags & PF_DICT) || pg.enc != ENC_PLAIN) continue;
       for (int v0 = 0; v0 < pg.n_values; v0 += DK_COPY_TILE) tiles.push_back(make_int2(pi, v0));
     }
     // key column: its dictionary pages are hashed entry by entry (hash-only tiles)
@@ -1592,10 +1605,6 @@ static int prepare(dk_parquet* p) {
       pbase.push_back(pbase.back() + pg.npchunk);
     }
     p->n_pchunks = (int)pbase.back();
-    // (k_plain_copy: up to 4 status words per chunk)
-    if (p->d_pstat.alloc((size_t)p->n_pchunks * 8 * 4 + 64) || p->d_pfail.alloc(p->h_pages.size() * 4 + 64) ||
-        p->d_ptick.alloc((p->h_cols.size() + 1) * 4 + 64))
-      return 1;
     if (expand(p, us, p->d_pchunks, ppage, pbase, EX_POSCHUNK, sizeof(DPosChunk)) ||
         expand(p, us, p->d_ltiles, tpage, tbase, EX_TILE, sizeof(DTile)))
       return 1;
@@ -2756,9 +2765,8 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
       const DPage& pg = p->h_pages[pi];
       const int64_t body = pg.unc_off >= 0 ? pg.usize : pg.csize;
       const bool plain_str = c.phys == PT_BYTE_ARRAY && pg.enc == ENC_PLAIN;
-      if (k == "k_string_copy" || k == "k_plain_copy") {
-        // the value section read once; chars, the key column's hashes (+ positions, fused)
-        if (plain_str) rd += pg.vbytes, wr += pg.n_chars + (key ? 8ll * pg.n_values : 0) + (k == "k_plain_copy" ? 4ll * pg.n_values : 0);
+      if (k == "k_string_copy") {
+        if (plain_str) { rd += pg.vbytes; wr += pg.n_chars + (key ? 8ll * pg.n_values : 0); }
       } else if (k == "k_snap_frag") {
         // snappy pages: compressed body read, decompressed body written (v2 levels excluded)
         if (pg.unc_off >= 0) {
@@ -2966,13 +2974,15 @@ extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf,
 }
 
 extern "C" void dk_parquet_close(dk_parquet* p) {
-  if (p) ensure_open(p);
   if (!p) return;
-  hipSetDevice(p->eng->cfg.device);
-  hipStreamSynchronize(p->stream);
-  for (int k = 0; k < kCopyStreams; k++) if (p->copy[k].s) hipStreamSynchronize(p->copy[k].s);
-  SyncedRelease drained;                 // every buffer below is idle: back to the caches for reuse
-  delete p;
+  reaper().run([p] {
+    ensure_open(p);
+    hipSetDevice(p->eng->cfg.device);
+    hipStreamSynchronize(p->stream);
+    for (int k = 0; k < kCopyStreams; k++) if (p->copy[k].s) hipStreamSynchronize(p->copy[k].s);
+    SyncedRelease drained;               // every buffer below is idle: back to the caches for reuse
+    delete p;
+  });
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3581,7 +3591,9 @@ extern "C" int dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column*
   return 0;
 }
 
-extern "C" void dk_json_tail_free(dk_json_tail* t) { delete t; }
+extern "C" void dk_json_tail_free(dk_json_tail* t) {
+  if (t) reaper().run([t] { delete t; });
+}
 
 // One commit line's protocol / metaData action decoded with DefaultJsonRow's rules for
 // Protocol.FULL_SCHEMA / Metadata.FULL_SCHEMA (kernel-defaults/.../internal/data/DefaultJsonRow.java:
@@ -5433,7 +5445,7 @@ extern "C" int dk_replay_stats_parsed_files(dk_replay* r) {
 extern "C" int dk_replay_kernel_stats(dk_replay* r, int32_t i, const char** name, double* avg_us, int64_t* count) {
   if (i < 0 || i >= KTimer::K) return 1;
   // decode kernels are timed by the parquet object's timer, the rest by the replay's
-  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16) || (i >= 19 && i <= 21) || i == 24)) ? &r->ck->timer : &r->timer;
+  const KTimer* t = (r->ck && (i <= 6 || (i >= 13 && i <= 16) || (i >= 19 && i <= 21))) ? &r->ck->timer : &r->timer;
   *name = t->names[i];
   if (!*name) return 1;
   *count = t->cnt[i];

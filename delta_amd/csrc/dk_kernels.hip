@@ -1333,18 +1333,11 @@ __device__ __forceinline__ uint32_t pos_cand_mask(const StrRegion& S, int64_t i)
   return pos_cand_bits(q, nxt, S, i);
 }
 
-// PLAIN data pages are left to k_plain_copy (skip_plain = 1): the position passes then serve the
-// dictionary pages only
-__device__ __forceinline__ bool pos_skipped(const DPage& pg, int skip_plain) {
-  return skip_plain && !(pg.flags & PF_DICT);
-}
-
 __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                  DPosChunk* __restrict__ pcs, int skip_plain) {
+                                                  DPosChunk* __restrict__ pcs) {
   DPosChunk& C = pcs[blockIdx.x];
   const DPage pg = pages[C.page];
-  if (pos_skipped(pg, skip_plain)) return;
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   __shared__ int lds[12];
@@ -1396,10 +1389,10 @@ __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chu
 
 __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                  const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                 DPosChunk* __restrict__ pcs, int skip_plain) {
+                                                 DPosChunk* __restrict__ pcs) {
   DPage& pgw = pages[blockIdx.x];
   const DPage pg = pgw;
-  if (pg.npchunk == 0 || pos_skipped(pg, skip_plain)) return;
+  if (pg.npchunk == 0) return;
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   if (!str_region(pg, ck, arena, pos, S)) return;
@@ -1433,10 +1426,10 @@ __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chun
 
 __global__ __launch_bounds__(NT) void k_pos_write(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                  const DPosChunk* __restrict__ pcs, int skip_plain) {
+                                                  const DPosChunk* __restrict__ pcs) {
   const DPosChunk C = pcs[blockIdx.x];
   const DPage pg = pages[C.page];
-  if (pg.pos_fail || C.cnt == 0 || pos_skipped(pg, skip_plain)) return;
+  if (pg.pos_fail || C.cnt == 0) return;
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   if (!str_region(pg, ck, arena, pos, S)) return;
@@ -1461,11 +1454,11 @@ __global__ __launch_bounds__(NT) void k_pos_write(const DChunk* __restrict__ chu
 }
 
 __global__ void k_pos_fallback(const DChunk* __restrict__ chunks, DPage* __restrict__ pages, int n_pages,
-                               const uint8_t* __restrict__ arena, int32_t* __restrict__ pos, int skip_plain) {
+                               const uint8_t* __restrict__ arena, int32_t* __restrict__ pos) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_pages) return;
   const DPage pg = pages[i];
-  if (!pg.pos_fail || pg.npchunk == 0 || pos_skipped(pg, skip_plain)) return;
+  if (!pg.pos_fail || pg.npchunk == 0) return;
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   if (!str_region(pg, ck, arena, pos, S)) return;
@@ -1831,8 +1824,7 @@ __global__ __launch_bounds__(NT) void k_tile_scan1(DColumn* __restrict__ cols, D
 
 __global__ __launch_bounds__(NT) void k_tile_chars(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                    const uint8_t* __restrict__ arena, const int32_t* __restrict__ pos,
-                                                   const Seg* __restrict__ runs, DTile* __restrict__ tiles, int tile0,
-                                                   int plain_fused) {
+                                                   const Seg* __restrict__ runs, DTile* __restrict__ tiles, int tile0) {
   DTile& T = tiles[tile0 + blockIdx.x];
   const int pi = T.page;
   const DPage pg = pages[pi];
@@ -1843,14 +1835,7 @@ __global__ __launch_bounds__(NT) void k_tile_chars(const DChunk* __restrict__ ch
   const int vb = (int)(T.value_base - pg.value_base);     // page-local index of the tile's first value
   if (pg.status != PS_OK || nvt == 0) { if (t == 0) T.n_chars = 0; return; }
   if (pg.enc == ENC_PLAIN) {
-    if (t == 0 && plain_fused) {
-      // positions come later (k_plain_copy): a PLAIN page holds its value section less the 4-byte
-      // length prefixes, all counted on its first tile
-      const Layout L = page_layout(pg, ck, arena);
-      const long long nc = L.ok ? (long long)(L.val_e - L.val_p) - 4ll * pg.n_values : -1;
-      if (nc < 0) pages[pi].status = PS_BAD_VALUES;
-      T.n_chars = vb == 0 && nc > 0 ? nc : 0;
-    } else if (t == 0) {
+    if (t == 0) {
       const int32_t* P = pos + pg.pos_base;
       T.n_chars = (long long)(P[vb + nvt] - P[vb]) - 4ll * nvt;
     }
@@ -1984,16 +1969,31 @@ __global__ __launch_bounds__(NT) void k_tile_decode(const DChunk* __restrict__ c
   const int32_t* P = (is_str && pg.enc == ENC_PLAIN) ? pos + pg.pos_base : nullptr;
   __shared__ int s_fill;
   // null-only column whose def levels over the whole tile are ONE RLE run: every level is a row
-  // with the same def level and nothing but row_def is materialised -> a vectorised fill
-  if (col.null_only && !rep && ck.max_def > 0) {
+  // with the same def level and nothing but row_def is materialised -> a vectorised fill. A repeated
+  // leaf qualifies when its rep levels are one run of 0 and its def level opens no entry (a null or
+  // empty map / list per row, e.g. add.tags, or partitionValues of an unpartitioned table): its row
+  // offsets are then all the tile's entry base, filled the same way.
+  if (col.null_only && ck.max_def > 0) {
     if (t == 0) {
       RunCur c0;
       c0.init(runs + pg.run_d, pg.nrun_d, T.lvl0);
-      s_fill = (c0.cur.bp_idx < 0 && c0.next >= l_end) ? (int)c0.cur.val : -1;
+      int fill = (c0.cur.bp_idx < 0 && c0.next >= l_end) ? (int)c0.cur.val : -1;
+      if (rep && fill >= 0) {
+        if (fill >= ck.rep_def || pg.nrun_r <= 0) {
+          fill = -1;
+        } else {
+          RunCur c1;
+          c1.init(runs + pg.run_r, pg.nrun_r, T.lvl0);
+          if (!(c1.cur.bp_idx < 0 && c1.next >= l_end && c1.cur.val == 0)) fill = -1;
+        }
+      }
+      s_fill = fill;
     }
     __syncthreads();
     if (s_fill >= 0) {
       fill_bytes(col.row_def + T.row_base, l_end - T.lvl0, (uint8_t)s_fill);
+      if (rep && col.row_offs)
+        for (int i = t; i < l_end - T.lvl0; i += NT) col.row_offs[T.row_base + i] = T.entry_base;
       return;
     }
   }
@@ -2338,251 +2338,6 @@ __global__ __launch_bounds__(CT) void k_string_copy(const DChunk* __restrict__ c
     }
     __syncthreads();
     v0 += cnt;
-  }
-}
-
-// --------------------------------------------------------------------------------------------
-// K6b: a PLAIN string page's value section in one pass -- positions, chars and key hashes
-// (k_plain_copy; DK_PLAIN_FUSED=0 restores k_pos_* + k_string_copy). One workgroup per 16 KiB
-// chunk of the section (the DPosChunk list):
-//   1. stage the chunk, one block before it and a 1 KiB halo after it (the end of its last value)
-//      in LDS with dwordx4 loads -- the only read of the section;
-//   2. length-prefix candidates (pos_cand_bits), ranked by a block scan; each candidate's successor
-//      (q + 4 + len) must be the next one;
-//   3. the chunk's first value index and its predecessor's chain end by a decoupled look-back over
-//      per-chunk status words (count | chain end | flag): the chunk is taken by atomic ticket, so
-//      every chunk it waits on belongs to a workgroup that is already running, and a page's first
-//      chunk never waits; the page's last chunk checks count == n and chain end == section end;
-//   4. value v = base + k: P[v] = q, its bytes to chars at q - 4v (page-local), compacted in LDS
-//      congruent to the destination mod 16 and stored with dwordx4 (byte stores at the two edges,
-//      which neighbouring chunks share); the key column's hash from the staged bytes. A last value
-//      running past the halo is copied from global memory (hash 0: the probe recomputes it).
-// A page whose chain breaks anywhere (or runs out of bounds) is flagged and redone, whole, by
-// k_plain_fallback (one lane walks the chain; malformed pages report PS_BAD_VALUES).
-// --------------------------------------------------------------------------------------------
-#ifndef DK_PC_SPLIT
-#define DK_PC_SPLIT 2
-#endif
-constexpr int PC_SPLIT = DK_PC_SPLIT;                  // workgroups per DPosChunk (8 KiB each: ~22 KB of LDS)
-constexpr int PC_CHB = POS_CHB / PC_SPLIT;             // blocks per workgroup
-constexpr int PC_BPT = PC_CHB / NT;
-constexpr int PC_HB = 64;                              // halo blocks staged past the chunk
-constexpr int PC_NB = PC_CHB + 2 + PC_HB;              // staged blocks: 1 before, the chunk, 1 + halo after
-constexpr int PC_MAXC = DK_POS_CHUNK / PC_SPLIT / 5 + 8;   // candidate bound (a value takes >= 5 bytes)
-constexpr int PC_OUTB = PC_CHB + PC_HB + 4;            // output staging blocks
-static_assert(PC_BPT * NT == PC_CHB && PC_SPLIT <= 4, "k_plain_copy: blocks per workgroup must be a multiple of its threads (<= 4 status words per chunk)");
-constexpr unsigned long long PC_CMASK = (1ull << 29) - 1;
-
-__device__ __forceinline__ unsigned long long pc_word(unsigned flag, long long cnt, long long next) {
-  return ((unsigned long long)flag << 62) | ((unsigned long long)(next + 1) << 29) | ((unsigned long long)cnt & PC_CMASK);
-}
-
-__global__ __launch_bounds__(NT) void k_plain_copy(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
-                                                   const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
-                                                   int32_t* __restrict__ pos, const DPosChunk* __restrict__ pcs, int pc0,
-                                                   unsigned long long* __restrict__ pstat, unsigned int* __restrict__ ticket,
-                                                   int32_t* __restrict__ pfail) {
-  __shared__ uint4 lin[PC_NB];
-  __shared__ uint4 lout[PC_OUTB];
-  __shared__ int16_t cpos[PC_MAXC];
-  __shared__ int lds[12];
-  __shared__ int s_ci, s_bad, s_last;
-  __shared__ long long s_base;
-  const int t = threadIdx.x;
-  if (t == 0) { s_ci = (int)atomicAdd(ticket, 1u); s_bad = 0; s_last = -1; }
-  __syncthreads();
-  const int gi = pc0 * PC_SPLIT + s_ci;                    // sub-chunk: status word index
-  const DPosChunk C = pcs[gi / PC_SPLIT];
-  const DPage pg = pages[C.page];
-  if (pg.flags & PF_DICT) return;
-  const DChunk ck = chunks[pg.chunk];
-  StrRegion S;
-  if (!str_region(pg, ck, arena, pos, S)) return;          // a page-wide condition: none of its chunks waits
-  const int pf = pg.pchunk0 * PC_SPLIT, pl = (pg.pchunk0 + pg.npchunk) * PC_SPLIT - 1;
-  const int ci = gi;
-  const int64_t blk0 = (int64_t)C.blk0 + (gi % PC_SPLIT) * PC_CHB;
-  const bool on = blk0 < S.nblk;
-  const int64_t cstart = 16 * blk0 - S.mis;                 // region offset of the chunk's first byte
-  // 1. stage blocks [blk0 - 1, blk0 + PC_CHB + 1 + PC_HB): LDS byte b <-> region offset cstart - 16 + b
-  const uint4* gblk = (const uint4*)S.abase;
-  for (int k = t; k < PC_NB; k += NT) {
-    const int64_t i = blk0 - 1 + k;
-    lin[k] = (on && i >= 0 && i < S.nblk) ? gblk[i] : make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  const uint32_t* in32 = (const uint32_t*)lin;
-  const uint8_t* in8 = (const uint8_t*)lin;
-  const int64_t staged_end = cstart - 16 + 16ll * PC_NB;
-  // 2. candidates, in order
-  int run = 0;
-#pragma unroll
-  for (int j = 0; j < PC_BPT; j++) {
-    const int lb = j * NT + t;                              // chunk block
-    const int64_t i = blk0 + lb;
-    uint32_t m = on ? pos_cand_bits(lin[lb + 1], lin[lb + 2].x, S, i) : 0u;
-    int ex, e1, e2, tot, t1, t2;
-    block_scan3(__popc(m), 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
-    int k = run + ex;
-    const int64_t rb = 16 * i - S.mis;
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      if (k < PC_MAXC) cpos[k] = (int16_t)(rb + b - 3 - cstart);
-      k++;
-    }
-    run += tot;
-  }
-  __syncthreads();
-  const int cnt = run;
-  const bool over = cnt > PC_MAXC;
-  if (!over)
-    for (int k = t; k < cnt; k += NT) {
-      const int64_t q = cstart + cpos[k];
-      const int64_t nx = q + 4 + (int64_t)lds_u32_at(in32, (int32_t)(q - cstart + 16));
-      if (k + 1 < cnt) { if (nx != cstart + cpos[k + 1]) s_bad = 1; }
-      else s_last = nx > 0x7fffffffll ? -2 : (int)nx;
-    }
-  __syncthreads();
-  // 3. look-back (one lane)
-  if (t == 0) {
-    bool bad = over || s_bad || (cnt > 0 && s_last < 0);
-    const long long ln = cnt > 0 && s_last >= 0 ? s_last : -1;
-    long long base = 0, prev = -1;
-    if (ci != pf) {
-      __hip_atomic_store(&pstat[ci], pc_word(1, cnt, ln), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int j = ci - 1; j >= pf; j--) {
-        unsigned long long w;
-        int spin = 0;         // (bounded: a predecessor that never publishes sends the page to the fallback)
-        while (((w = __hip_atomic_load(&pstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0 &&
-               ++spin < (1 << 22))
-          __builtin_amdgcn_s_sleep(2);
-        if ((w >> 62) == 0) { bad = true; break; }
-        const long long cj = (long long)(w & PC_CMASK);
-        if (prev < 0 && cj > 0) prev = (long long)((w >> 29) & 0xffffffffull) - 1;
-        base += cj;
-        if ((w >> 62) == 2) break;
-      }
-    }
-    const long long inc = base + cnt, inc_next = cnt > 0 ? ln : prev;
-    __hip_atomic_store(&pstat[ci], pc_word(2, inc, inc_next), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (cnt > 0 && cstart + cpos[0] != (base == 0 ? 0 : prev)) bad = true;   // the chain enters here
-    if (ci == pl && (inc != S.n || (inc > 0 ? inc_next : 0) != S.R)) bad = true;
-    if (inc > S.n) bad = true;
-    if (bad) atomicOr(&pfail[C.page], 1);
-    else if (ci == pl) S.P[S.n] = (int32_t)S.R;
-    s_bad = bad;
-    s_base = base;
-  }
-  __syncthreads();
-  if (s_bad || cnt == 0) return;
-  // 4. positions, chars, hashes
-  const long long base = s_base;
-  const DColumn col = cols[ck.col];
-  uint64_t* vh = col.vhash ? col.vhash + pg.value_base : nullptr;
-  uint8_t* ob = (col.chars && pg.n_chars > 0) ? col.chars + pg.char_base : nullptr;
-  const int64_t q_last = cstart + cpos[cnt - 1];
-  const int64_t len_last = (int64_t)lds_u32_at(in32, (int32_t)(q_last - cstart + 16));
-  const bool last_long = q_last + 4 + len_last + 16 > staged_end;
-  const int64_t c_lo = (cstart + cpos[0]) - 4 * base;                 // page-local chars of the chunk
-  const int64_t c_full = q_last - 4 * (base + cnt - 1) + len_last;      // end of the last value's chars
-  const int64_t c_end = last_long ? c_full - len_last : c_full;         // ... of the staged ones
-  if (c_lo < 0 || c_full > pg.n_chars || c_end < c_lo) { if (t == 0) atomicOr(&pfail[C.page], 1); return; }
-  const int32_t opad = ob ? (int32_t)(((uintptr_t)ob + c_lo) & 15) : 0;
-  uint32_t* out32 = (uint32_t*)lout;
-  uint8_t* out8 = (uint8_t*)lout;
-  for (int k = t; k < cnt; k += NT) {
-    const long long v = base + k;
-    const int64_t q = cstart + cpos[k];
-    S.P[v] = (int32_t)q;
-    const int32_t len = (int32_t)lds_u32_at(in32, (int32_t)(q - cstart + 16));
-    if (k == cnt - 1 && last_long) { if (vh) vh[v] = 0; continue; }
-    const int32_t src = (int32_t)(q + 4 - cstart + 16);               // value bytes in `lin`
-    if (ob && len > 0) {
-      int32_t d = (int32_t)(q - 4 * v - c_lo) + opad;                  // value bytes in `lout`
-      int32_t sidx = src, kk = 0;
-      const int32_t head = min(len, (4 - (d & 3)) & 3);
-      for (; kk < head; kk++) out8[d + kk] = in8[sidx + kk];
-      d += head; sidx += head;
-      const int32_t nd = (len - head) >> 2;
-      const uint32_t sb = (uint32_t)(sidx & 3);
-      const int32_t si = sidx >> 2;
-      uint32_t lo = in32[si];
-      uint32_t* od = out32 + (d >> 2);
-      for (int32_t i = 0; i < nd; i++) {
-        const uint32_t hi = in32[si + i + 1];
-        od[i] = __builtin_amdgcn_alignbyte(hi, lo, sb);
-        lo = hi;
-      }
-      for (kk = head + 4 * nd; kk < len; kk++) out8[(int32_t)(q - 4 * v - c_lo) + opad + kk] = in8[src + kk];
-    }
-    if (vh) {
-      auto load8 = [&](int32_t j) -> uint64_t {
-        const int32_t b = src + 8 * j;
-        return (uint64_t)lds_u32_at(in32, b) | ((uint64_t)lds_u32_at(in32, b + 4) << 32);
-      };
-      uint64_t h = 0;
-      if (!simple_path_hash(len, load8, kDecodeSeed, &h)) h = 0;
-      vh[v] = h;
-    }
-  }
-  __syncthreads();
-  if (ob && c_end > c_lo) {
-    const int32_t nb = opad + (int32_t)(c_end - c_lo);                  // bytes of `lout` in use
-    uint8_t* gbase = ob + c_lo - opad;                                    // 16-aligned
-    for (int32_t q = t; q * 16 < nb; q += NT) {
-      const int32_t lo = q * 16, hi = lo + 16;
-      if (lo >= opad && hi <= nb) *(uint4*)(gbase + lo) = lout[q];
-      else for (int32_t j = max(lo, opad); j < min(hi, nb); j++) gbase[j] = out8[j];
-    }
-  }
-  if (ob && last_long) {                                                  // the last value, from global memory
-    const long long v = base + cnt - 1;
-    uint8_t* o = ob + (q_last - 4 * v);
-    for (int64_t j = t; j < len_last; j += NT) o[j] = S.r[q_last + 4 + j];
-  }
-}
-
-// Pages k_plain_copy flagged: one lane walks the length chain (positions; a malformed page reports
-// PS_BAD_VALUES), then the workgroup copies the values (a lane per value) and leaves their key
-// hashes to the probe (0).
-__global__ __launch_bounds__(NT) void k_plain_fallback(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
-                                                       const DColumn* __restrict__ cols, const uint8_t* __restrict__ arena,
-                                                       int32_t* __restrict__ pos, int page0, const int32_t* __restrict__ pfail,
-                                                       DState* __restrict__ st) {
-  const int pi = page0 + blockIdx.x;
-  if (!pfail[pi]) return;
-  const DPage pg = pages[pi];
-  if (pg.flags & PF_DICT) return;
-  const DChunk ck = chunks[pg.chunk];
-  StrRegion S;
-  if (!str_region(pg, ck, arena, pos, S)) return;
-  __shared__ int s_bad;
-  if (threadIdx.x == 0) {
-    int64_t q = 0;
-    bool bad = false;
-    for (int k = 0; k < S.n; k++) {
-      if (q + 4 > S.R) { bad = true; break; }
-      S.P[k] = (int32_t)q;
-      q += 4 + (int64_t)ld_u32(S.r + q);
-      if (q > S.R) { bad = true; break; }
-    }
-    S.P[S.n] = (int32_t)S.R;
-    if (bad || (S.R - 4ll * S.n) != pg.n_chars) {
-      pages[pi].status = PS_BAD_VALUES;
-      atomicOr(&st->err_flags, E_PAGE);
-      bad = true;
-    }
-    s_bad = bad;
-  }
-  __syncthreads();
-  if (s_bad) return;
-  const DColumn col = cols[ck.col];
-  uint64_t* vh = col.vhash ? col.vhash + pg.value_base : nullptr;
-  uint8_t* ob = (col.chars && pg.n_chars > 0) ? col.chars + pg.char_base : nullptr;
-  for (int v = threadIdx.x; v < S.n; v += NT) {
-    const int32_t q = S.P[v], len = S.P[v + 1] - q - 4;
-    if (ob) for (int32_t j = 0; j < len; j++) ob[q - 4ll * v + j] = S.r[q + 4 + j];
-    if (vh) vh[v] = 0;
   }
 }
 
@@ -4199,22 +3954,12 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
 }
 // string positions of pages [page0, page0 + n_pages) whose chunks are pcs[pc0, pc0 + npc)
 void launch_positions(const DChunk* c, DPage* p, int page0, int n_pages, const uint8_t* arena, int32_t* pos,
-                      DPosChunk* pcs, int pc0, int npc, int skip_plain, hipStream_t s) {
+                      DPosChunk* pcs, int pc0, int npc, hipStream_t s) {
   if (!npc) return;
-  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0, skip_plain);
-  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs, skip_plain);
-  hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0, skip_plain);
-  hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos, skip_plain);
-}
-void launch_plain_copy(const DChunk* c, DPage* p, const DColumn* cols, const uint8_t* arena, int32_t* pos,
-                       const DPosChunk* pcs, int pc0, int npc, int page0, int n_pages, unsigned long long* pstat,
-                       unsigned int* ticket, int32_t* pfail, DState* st, hipStream_t s) {
-  if (npc <= 0) return;
-  (void)hipMemsetAsync(pstat + (size_t)pc0 * PC_SPLIT, 0, (size_t)npc * PC_SPLIT * 8, s);
-  (void)hipMemsetAsync(pfail + page0, 0, (size_t)n_pages * 4, s);
-  (void)hipMemsetAsync(ticket, 0, 4, s);
-  hipLaunchKernelGGL(k_plain_copy, dim3(npc * PC_SPLIT), dim3(NT), 0, s, c, p, cols, arena, pos, pcs, pc0, pstat, ticket, pfail);
-  if (n_pages) hipLaunchKernelGGL(k_plain_fallback, dim3(n_pages), dim3(NT), 0, s, c, p, cols, arena, pos, page0, pfail, st);
+  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
+  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
+  hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos);
 }
 void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_page_runs, dim3((n + 63) / 64), dim3(64), 0, s, c, p, n, arena, runs);
@@ -4227,8 +3972,8 @@ void launch_tile_scan1(DColumn* cols, int ncols, DPage* p, DTile* t, DState* st,
   if (ncols) hipLaunchKernelGGL(k_tile_scan1, dim3(ncols), dim3(NT), 0, s, cols, p, t, st);
 }
 void launch_tile_chars(const DChunk* c, DPage* p, const uint8_t* arena, const int32_t* pos, const Seg* runs, DTile* t,
-                       int ntiles, int tile0, int plain_fused, hipStream_t s) {
-  if (ntiles) hipLaunchKernelGGL(k_tile_chars, dim3(ntiles), dim3(NT), 0, s, c, p, arena, pos, runs, t, tile0, plain_fused);
+                       int ntiles, int tile0, hipStream_t s) {
+  if (ntiles) hipLaunchKernelGGL(k_tile_chars, dim3(ntiles), dim3(NT), 0, s, c, p, arena, pos, runs, t, tile0);
 }
 void launch_tile_scan2(DColumn* cols, int ncols, DPage* p, DTile* t, DState* st, hipStream_t s) {
   if (ncols) hipLaunchKernelGGL(k_tile_scan2, dim3(ncols), dim3(NT), 0, s, cols, p, t, st);
@@ -4886,7 +4631,7 @@ int warm_kernels() {
       (const void*)k_snap_frag_t<false>, (const void*)k_snappy_serial, (const void*)k_pos_count,
       (const void*)k_pos_scan, (const void*)k_pos_write, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
-      (const void*)k_tile_scan2, (const void*)k_tile_decode, (const void*)k_string_copy, (const void*)k_plain_copy, (const void*)k_plain_fallback, (const void*)k_stats_eval,
+      (const void*)k_tile_scan2, (const void*)k_tile_decode, (const void*)k_string_copy, (const void*)k_stats_eval,
       (const void*)k_part_eval, (const void*)k_json_canon, (const void*)k_slots_init, (const void*)k_table_insert,
       (const void*)k_table_update, (const void*)k_json_select, (const void*)k_table_fp, (const void*)k_probe_fast,
       (const void*)k_probe_fast_all, (const void*)k_probe_cand, (const void*)k_probe_cand_all,

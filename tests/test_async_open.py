@@ -36,8 +36,8 @@ def _child(table, env):
 def test_async_open_error_reaches_consumer(tmp_path):
     from delta_amd import synth
     synth.write_table(str(tmp_path), synth.TableSpec(n_adds=40_000, n_parts=6, compression="snappy", n_commits=4))
-    got = _child(str(tmp_path), {"DK_INJECT_SLICE_FAULT": "2"})
-    assert not got["ok"] and "injected fault in checkpoint open slice 2" in got["err"], got
+    got = _child(str(tmp_path), {"DK_INJECT_SLICE_FAULT": "0"})
+    assert not got["ok"] and "injected fault in checkpoint open slice 0" in got["err"], got
     ok = _child(str(tmp_path), {})
     sync = _child(str(tmp_path), {"DK_ASYNC_OPEN": "0"})
     assert ok["ok"] and sync["ok"] and ok == sync

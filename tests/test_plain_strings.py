@@ -1,12 +1,13 @@
-"""PLAIN BYTE_ARRAY pages through the one-pass string decode (k_plain_copy: positions, chars and key
-hashes with a decoupled look-back over 16 KiB chunks; k_plain_fallback for pages whose length chain
-the candidate scan cannot follow) against the oracle decoder, bit for bit.
+"""PLAIN BYTE_ARRAY pages through the string decode (k_pos_count / scan / write: length-prefix
+candidates per 16 KiB chunk with the chain verified across chunks, k_pos_fallback for pages whose
+chain the candidate scan cannot follow; k_string_copy: chars + key hashes per 128-value tile) against
+the oracle decoder, bit for bit.
 
 The cases are the ones that stress the chunking: values straddling chunk boundaries, values longer
-than the 1 KiB halo and than a whole chunk, empty strings (4-byte values; runs of them defeat the
-zero-run candidate test), embedded NUL runs that look like length prefixes, a value of 2^24 bytes
-(its length prefix has no zero high byte), nulls in between, v1 / v2 pages, snappy and uncompressed.
-Reference: DefaultBinaryVector / parquet-mr's PLAIN BinaryColumnReader.
+than a copy tile's staging buffer and than a whole chunk, empty strings (4-byte values; runs of them
+defeat the zero-run candidate test), embedded NUL runs that look like length prefixes, a value of
+2^24 bytes (its length prefix has no zero high byte), nulls in between, v1 / v2 pages, snappy and
+uncompressed. Reference: DefaultBinaryVector / parquet-mr's PLAIN BinaryColumnReader.
 """
 import numpy as np
 import pyarrow as pa
