@@ -385,14 +385,24 @@ static int engine_warm(int device) {
   if (std::find(warmed.begin(), warmed.end(), device) != warmed.end()) return 0;
   warmed.push_back(device);
   warm_kernels();
-  StreamH sh, sh_hi;
-  if (sh.create() || sh_hi.create(replay_high_priority())) return 1;
+  // the pooled streams a checkpoint open and a replay take (own, aux, copy, side, decode; the replay's
+  // two high-priority ones), each with a first launch; the DMA engines' first copies both ways
+  constexpr int kWarmStreams = 12, kWarmHigh = 3;
+  StreamH sh[kWarmStreams], hi[kWarmHigh];
+  for (auto& x : sh) if (x.create()) return 1;
+  for (auto& x : hi) if (x.create(replay_high_priority())) return 1;
   DBuf d;
   HBuf h;
   if (d.alloc(1 << 20) || h.alloc(1 << 20)) return 1;
-  memset(h.data(), 0, 256);
-  launch_copy_zc(d.p, h.data(), 256, sh.s);
-  HIPOK(hipStreamSynchronize(sh.s));
+  memset(h.data(), 0, 1 << 20);
+  for (auto& x : sh) launch_copy_zc(d.p, h.data(), 256, x.s);
+  for (auto& x : hi) launch_copy_zc(d.p, h.data(), 256, x.s);
+  for (int k = 0; k < 4; k++) {
+    HIPOK(hipMemcpyAsync(d.p, h.data(), 1 << 20, hipMemcpyHostToDevice, sh[k].s));
+    HIPOK(hipMemcpyAsync(h.data(), d.p, 1 << 20, hipMemcpyDeviceToHost, sh[k].s));
+  }
+  for (auto& x : sh) HIPOK(hipStreamSynchronize(x.s));
+  for (auto& x : hi) HIPOK(hipStreamSynchronize(x.s));
   return 0;
 }
 

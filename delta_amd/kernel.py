@@ -887,6 +887,7 @@ class Snapshot:
         if files and (self.protocol is None or self.metadata is None):
             # only row groups whose footer statistics allow a non-null protocol / metaData row
             # (an all-null row group cannot hold the first one); files with none are not read
+            t_a = time.perf_counter()
             want = [lf for lf, need in (("protocol.minReaderVersion", self.protocol is None),
                                         ("metaData.id", self.metadata is None)) if need]
             groups = []
@@ -900,7 +901,9 @@ class Snapshot:
             groups = [g for g in groups if g]
             if not files:
                 return
+            t_b = time.perf_counter()
             ps = ParquetSet(engine, files, PM_LEAVES, groups=groups).decode()
+            t_c = time.perf_counter()
             B = self._parquet_batch_size
             for fi in range(len(files)):
                 # the first non-null protocol / metaData row of the file, found on the device; only
@@ -917,7 +920,11 @@ class Snapshot:
                     done = self._found(prot, meta)
                 if done:
                     break
+            t_d = time.perf_counter()
             ps.close()
+            # (where a cold load goes: footers, the open + device decode, the rows found and decoded)
+            self.load_ms.update(checkpoint_pm_footers=(t_b - t_a) * 1e3, checkpoint_pm_decode=(t_c - t_b) * 1e3,
+                                checkpoint_pm_rows=(t_d - t_c) * 1e3)
 
 
 def _row(ps, fi, leaf, r):
