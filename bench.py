@@ -182,6 +182,26 @@ def oracle_skipping(work, cfg):
     return node, osf.stat_types(node, schema)
 
 
+def masked_sum(v, sel):
+    """(sum(v[sel]), count of selected rows) for the JMH-shaped consumer, without numpy's branchy masked reduction on
+    irregular selections (`sum(where=)` runs 6-8x slower on a 50 % / 70 % random mask than on a
+    near-uniform one): near-uniform masks keep it, irregular ones take a branch-free blocked
+    multiply-add (the same sum)."""
+    import numpy as np
+    n = len(v)
+    k = int(np.count_nonzero(sel))
+    if k == n:
+        return int(v.sum()), k
+    if k == 0:
+        return 0, 0
+    if n - k < n // 16 or k < n // 16:              # a near-uniform mask: the masked sum predicts well
+        return int(v.sum(where=sel)), k
+    tot, B = 0, 1 << 16
+    for i in range(0, n, B):
+        tot += int(np.dot(v[i:i + B], sel[i:i + B].astype(np.int64)))
+    return tot, k
+
+
 def cpu_share():
     """CPUs this process may run on (sched_getaffinity, i.e. `nproc`) and the cgroup CPU quota, if
     any (cpu.max): the GPU box shows the whole machine's cores but grants one GPU's share."""
@@ -601,9 +621,9 @@ def main(argv=None):
                 size_sum += int(v.sum())
                 n_sel += b.size
             else:
-                # a masked reduction over the selected rows (no gather, no temporaries)
-                size_sum += int(v.sum(where=b.selection))
-                n_sel += int(np.count_nonzero(b.selection))
+                s_, k_ = masked_sum(v, b.selection)
+                size_sum += s_
+                n_sel += k_
             if cprof:
                 t_a = time.perf_counter(); t_s += t_a - t_d
             if capture_result:
@@ -668,10 +688,11 @@ def main(argv=None):
             sel = np.ones(b.size, bool) if b.selection is None else b.selection
             lens = np.diff(pc.offs[:b.size + 1])                  # path bytes per row
             nent = np.diff(kc.row_offs[:b.size + 1])              # partitionValues entries per row
-            path_bytes += int(lens.sum(where=sel))
-            pv_entries += int(nent.sum(where=sel))
-            size_sum += int(sz.fixed.view("<i8").sum(where=sel))
-            n_sel += int(np.count_nonzero(sel))
+            path_bytes += masked_sum(lens, sel)[0]
+            pv_entries += masked_sum(nent, sel)[0]
+            s_, k_ = masked_sum(sz.fixed.view("<i8"), sel)
+            size_sum += s_
+            n_sel += k_
             if b.file_index >= 0:                                 # device-decoded: the D2H of its leaves
                 d2h += sum(int(a.nbytes) for c in cols if c is not None
                            for a in (c.row_def, c.row_offs, c.entry_def, c.fixed, c.offs, c.chars) if a is not None)
