@@ -277,34 +277,44 @@ static MemCache& pinned_cache() { static MemCache* c = new MemCache(true, (size_
 
 // Non-blocking streams are pooled per device (creating one costs milliseconds): a call object takes
 // one when it is created and gives it back, drained, when it is freed.
-// High-priority streams (the replay's: the commit tail's uploads and kernels, the probes) come from
-// their own pool: HIP maps stream priorities to separate hardware queues, so their work does not
-// queue behind the decode passes an asynchronous open keeps feeding to the normal queues.
+// Three classes, each its own pool: HIP maps each stream priority to its own set of hardware queues
+// (GPU_MAX_HW_QUEUES of them, 4 by default), and work on one hardware queue runs in queue order.
+//  - normal: the open's sizing / decode passes, mirrors, readers;
+//  - high: the replay's (commit-tail uploads and kernels, probes) and the per-slice decode, so that
+//    they do not queue behind the passes an asynchronous open keeps feeding to the normal queues;
+//  - copy: the H2D image copies of an open, at the lowest priority. On a queue they shared with
+//    compute streams, a kernel would wait behind every image copy queued there before it (the first
+//    sizing pass of an open started 23 ms after its files had landed, profiles/r04/hwq/).
+enum StreamClass { kStreamNormal = 0, kStreamHigh = 1, kStreamCopy = 2 };
+static bool copy_class_on() {         // DK_COPY_PRIORITY=0: image copies on normal streams (A/B)
+  static const bool on = !(getenv("DK_COPY_PRIORITY") && atoi(getenv("DK_COPY_PRIORITY")) == 0);
+  return on;
+}
 struct StreamPool {
   std::mutex mu;
-  std::vector<std::pair<int, hipStream_t>> free_[2];
-  hipStream_t get(bool high = false) {
+  std::vector<std::pair<int, hipStream_t>> free_[3];
+  hipStream_t get(int cls = kStreamNormal) {
     int dev = 0;
     hipGetDevice(&dev);
     {
       std::lock_guard<std::mutex> lk(mu);
-      auto& F = free_[high];
+      auto& F = free_[cls];
       for (size_t i = 0; i < F.size(); i++)
         if (F[i].first == dev) { hipStream_t s = F[i].second; F.erase(F.begin() + i); return s; }
     }
     hipStream_t s = nullptr;
-    if (high) {
+    if (cls != kStreamNormal) {
       int least = 0, greatest = 0;
-      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) greatest = 0;
-      return hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest) == hipSuccess ? s : nullptr;
+      if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) least = greatest = 0;
+      return hipStreamCreateWithPriority(&s, hipStreamNonBlocking, cls == kStreamHigh ? greatest : least) == hipSuccess ? s : nullptr;
     }
     return hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess ? s : nullptr;
   }
-  void put(hipStream_t s, bool high = false) {
+  void put(hipStream_t s, int cls = kStreamNormal) {
     int dev = 0;
     hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    free_[high].push_back({dev, s});
+    free_[cls].push_back({dev, s});
   }
 };
 static StreamPool& stream_pool() { static StreamPool* p = new StreamPool(); return *p; }
@@ -360,11 +370,12 @@ struct HBuf {
 // nothing of a call runs on a stream shared through the engine.
 struct StreamH {
   hipStream_t s = nullptr;
-  bool high = false;
-  ~StreamH() { if (s) { hipStreamSynchronize(s); stream_pool().put(s, high); } }
-  int create(bool high_priority = false) {
-    high = high_priority;
-    s = stream_pool().get(high);
+  int cls = kStreamNormal;
+  ~StreamH() { if (s) { hipStreamSynchronize(s); stream_pool().put(s, cls); } }
+  int create(bool high_priority = false) { return create_class(high_priority ? kStreamHigh : kStreamNormal); }
+  int create_class(int c) {
+    cls = c;
+    s = stream_pool().get(cls);
     return s ? 0 : fail("hipStreamCreate failed");
   }
 };
@@ -388,7 +399,8 @@ static int engine_warm(int device) {
   // the pooled streams a checkpoint open and a replay take (own, aux, copy, side, decode; the replay's
   // two high-priority ones), each with a first launch; the DMA engines' first copies both ways
   constexpr int kWarmStreams = 12, kWarmHigh = 3;
-  StreamH sh[kWarmStreams], hi[kWarmHigh];
+  StreamH cp[4], sh[kWarmStreams], hi[kWarmHigh];
+  for (auto& x : cp) if (x.create_class(copy_class_on() ? kStreamCopy : kStreamNormal)) return 1;
   for (auto& x : sh) if (x.create()) return 1;
   for (auto& x : hi) if (x.create(replay_high_priority())) return 1;
   DBuf d;
@@ -398,9 +410,10 @@ static int engine_warm(int device) {
   for (auto& x : sh) launch_copy_zc(d.p, h.data(), 256, x.s);
   for (auto& x : hi) launch_copy_zc(d.p, h.data(), 256, x.s);
   for (int k = 0; k < 4; k++) {
-    HIPOK(hipMemcpyAsync(d.p, h.data(), 1 << 20, hipMemcpyHostToDevice, sh[k].s));
+    HIPOK(hipMemcpyAsync(d.p, h.data(), 1 << 20, hipMemcpyHostToDevice, cp[k].s));
     HIPOK(hipMemcpyAsync(h.data(), d.p, 1 << 20, hipMemcpyDeviceToHost, sh[k].s));
   }
+  for (auto& x : cp) HIPOK(hipStreamSynchronize(x.s));
   for (auto& x : sh) HIPOK(hipStreamSynchronize(x.s));
   for (auto& x : hi) HIPOK(hipStreamSynchronize(x.s));
   return 0;
@@ -2385,7 +2398,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   p->stream = p->own.s;
   if (p->aux.create()) return 1;
   for (int k = 0; k < copy_streams(); k++) {
-    if (p->copy[k].create()) return 1;
+    if (p->copy[k].create_class(copy_class_on() ? kStreamCopy : kStreamNormal)) return 1;
     HIPOK(hipEventCreateWithFlags(&p->copy_done[k].e, hipEventDisableTiming));
   }
   p->timer.on = (e->cfg.flags & DK_FLAG_TIMING) != 0;
@@ -2402,6 +2415,9 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   for (auto& ev : p->file_ev) HIPOK(hipEventCreateWithFlags(&ev.e, hipEventDisableTiming));
   const auto t_io0 = std::chrono::steady_clock::now();
   p->t_open0 = t_io0;
+  if (getenv("DK_VERBOSE"))     // the timeline's origin on CLOCK_MONOTONIC (Python's time.monotonic)
+    fprintf(stderr, "[dk] open of %d files starts at monotonic %.3f ms\n", n_files,
+            std::chrono::duration<double, std::milli>(t_io0.time_since_epoch()).count());
   parallel_for(n_files, [&](int fi) {
     FileM& f = p->files[fi];
     f.path = paths[fi];
@@ -2426,6 +2442,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   });
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
+  if (getenv("DK_VERBOSE")) fprintf(stderr, "[dk] footers read at %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_io0).count());
   // then only the offset indexes and page headers (pread in blocks): the page tables, and with them
   // the whole host half of prepare, are built before the column chunks are read (reading the headers
   // beside the image reads was no faster: both are CPU-bound on the box's share of cores)
@@ -2450,6 +2467,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   });
   for (int fi = 0; fi < n_files; fi++)
     if (!errs[fi].empty()) return fail(errs[fi]);
+  if (getenv("DK_VERBOSE")) fprintf(stderr, "[dk] page headers read at %.1f ms\n", std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_io0).count());
   std::vector<std::string> rerrs(n_files > 0 ? n_files : 0);   // the reader's errors
   // then the images: read into pinned memory, each going to HBM in 8 MiB pieces on a copy stream while
   // the rest of it (and the other files) are still being read -- on background threads, while prepare
@@ -2464,6 +2482,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   struct Piece { int fi; int64_t file_off, packed_off, len; };
   std::vector<Piece> pieces;
   static const bool by_piece = !getenv("DK_OPEN_PIECES") || atoi(getenv("DK_OPEN_PIECES")) != 0;
+  static const int64_t piece = (int64_t)(getenv("DK_PIECE_MB") ? std::max(1, atoi(getenv("DK_PIECE_MB"))) : 8) << 20;
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[n_files > 0 ? n_files : 1]);
   std::unique_ptr<int[]> fds(new int[n_files > 0 ? n_files : 1]);
   for (int fi = 0; fi < n_files; fi++) {
@@ -2471,8 +2490,8 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
     fds[fi] = -1;
     if (by_piece)
       for (const Span& sp : p->files[fi].spans)
-        for (int64_t o = 0; o < sp.len; o += (int64_t)8 << 20, n++)
-          pieces.push_back({fi, sp.file_off + o, sp.packed_off + o, std::min<int64_t>((int64_t)8 << 20, sp.len - o)});
+        for (int64_t o = 0; o < sp.len; o += piece, n++)
+          pieces.push_back({fi, sp.file_off + o, sp.packed_off + o, std::min<int64_t>(piece, sp.len - o)});
     left[fi].store(n);
   }
   std::thread reader([&] {
