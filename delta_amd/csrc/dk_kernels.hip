@@ -3641,11 +3641,16 @@ __device__ __forceinline__ void probe_fast_row(const ProbeCols& pc, long long r,
     // fingerprint is in the table go to k_probe_cand (C4: 30 % of the rows carry a DV). A decode-time
     // path hash exists only for the seed kDecodeSeed (the host drops it on a reseed).
     const bool has_off = pc.off_def != nullptr && pc.off_def[r] == pc.off_maxdef;
-    HashSink kd; kd.hs.init(kHashSeed(kDecodeSeed)); kd.n = 0;
-    if (dv_emit(true, pc.st_chars + pc.st_offs[r], (int32_t)(pc.st_offs[r + 1] - pc.st_offs[r]),
-                pc.pid_chars + pc.pid_offs[r], (int32_t)(pc.pid_offs[r + 1] - pc.pid_offs[r]), has_off,
-                has_off ? pc.off_vals[r] : 0, kd)) { *defer = true; return; }     // malformed: reported there
-    hd = kd.hs.final_(kd.n);
+    const uint8_t* st = pc.st_chars + pc.st_offs[r];
+    const int32_t stn = (int32_t)(pc.st_offs[r + 1] - pc.st_offs[r]);
+    const uint8_t* pid = pc.pid_chars + pc.pid_offs[r];
+    const int32_t pidn = (int32_t)(pc.pid_offs[r + 1] - pc.pid_offs[r]);
+    const int32_t off = has_off ? pc.off_vals[r] : 0;
+    if (!dv_hash_words(st, stn, pid, pidn, has_off, off, kDecodeSeed, &hd)) {
+      HashSink kd; kd.hs.init(kHashSeed(kDecodeSeed)); kd.n = 0;
+      if (dv_emit(true, st, stn, pid, pidn, has_off, off, kd)) { *defer = true; return; }   // malformed: reported there
+      hd = kd.hs.final_(kd.n);
+    }
   }
   const uint64_t h = hash_combine(hp, hd);
   const uint32_t f = slot_fp(h);

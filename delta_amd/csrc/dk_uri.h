@@ -440,6 +440,52 @@ DK_HD int dv_emit(bool has_dv, const uint8_t* st, int32_t stn, const uint8_t* pi
   return 0;
 }
 
+// The dvUniqueId hash of dv_emit + HashSink (DeletionVectorDescriptor.java:167-174), with
+// pathOrInlineDv absorbed 8 bytes at a time (aligned loads + funnel shift, appended to the partial
+// word: the stream's words are the same, so is the hash). False when storageType or pathOrInlineDv
+// holds a non-ASCII byte: dv_emit validates those (the caller falls back to it). The loads may read
+// up to 15 bytes past the string: decoded string columns carry 16 bytes of slack (alloc_outputs).
+// Host and device (tests/test_dv_hash.py checks it against dv_emit on the host).
+DK_HD bool dv_hash_words(const uint8_t* st, int32_t stn, const uint8_t* pid, int32_t pidn,
+                                              bool has_off, int32_t off, uint32_t seed, uint64_t* out) {
+  Hash64 hs; hs.init(kHashSeed(seed));
+  hs.put(1);
+  for (int32_t i = 0; i < stn; i++) { if (st[i] >= 0x80) return false; hs.put(st[i]); }
+  const uintptr_t pa = (uintptr_t)pid;
+  const uint64_t* base = (const uint64_t*)(pa & ~(uintptr_t)7);
+  const int sh = (int)(pa & 7) * 8;
+  const int32_t nw = (pidn + 7) >> 3;
+  uint64_t any = 0;
+  for (int32_t j = 0; j < nw; j++) {
+    uint64_t w = sh ? (base[j] >> sh) | (base[j + 1] << (64 - sh)) : base[j];
+    int nbytes = 8;
+    if (j == nw - 1 && (pidn & 7)) { nbytes = pidn & 7; w &= (1ull << (8 * nbytes)) - 1; }
+    any |= w;
+    const int nb = hs.nb;
+    if (nb + nbytes >= 8) {
+      hs.word(hs.buf | (w << (8 * nb)));
+      hs.buf = nb ? (w >> (64 - 8 * nb)) : 0ull;
+      hs.nb = nb + nbytes - 8;
+    } else {
+      hs.buf |= w << (8 * nb);
+      hs.nb = nb + nbytes;
+    }
+  }
+  if (any & 0x8080808080808080ull) return false;
+  uint64_t n = 1 + (uint64_t)stn + (uint64_t)pidn;
+  if (has_off) {
+    const char* pre = "@Optional[";
+    for (const char* q = pre; *q; q++) hs.put((uint8_t)*q);
+    char d[12]; int nd = 0; int64_t v = off; const bool neg = v < 0; if (neg) v = -v;
+    do { d[nd++] = (char)('0' + v % 10); v /= 10; } while (v);
+    n += 10 + nd + (neg ? 1 : 0) + 1;
+    if (neg) hs.put('-');
+    while (nd) hs.put((uint8_t)d[--nd]);
+    hs.put(']');
+  }
+  *out = hs.final_(n);
+  return true;
+}
 
 // Fast-path character class CC_SIMPLE (unreserved = alnum + "-_.!~*'()", plus "@&=+$,;/"),
 // tested 4 bytes at a time: ok(c) = LO[c & 15] & HI[c >> 4] != 0 for c < 0x80, one bit per high
