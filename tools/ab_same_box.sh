@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: same-box A/B of bench configurations (env settings, comma-separated per config), each run
+# same-box A/B of bench configurations (env settings, comma-separated per config), each run
 # twice interleaved; prints ms_per_step and the main phases
 set -o pipefail
 TAG=$1; shift

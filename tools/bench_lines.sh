@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4, call B: full bench lines with CPU baseline + full-size parity for C3 / C4 / C5, and a
+# full bench lines with CPU baseline + full-size parity for C3 / C4 / C5, and a
 # rocprofv3 kernel-trace summary of each (same command without the CPU baseline)
 set -o pipefail
 TAG=$1; shift

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4, call T: the whole GPU suite + smoke at HEAD, then the C3 / C4 / C5 bench lines (r04_b)
+# the whole GPU suite + smoke at HEAD, then the C3 / C4 / C5 bench lines (bench_lines.sh)
 set -o pipefail
 TAG=$1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT; cd $GRAFT_REPO_ROOT
@@ -8,4 +8,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $OUT/smoke.log; exit 1; }
 tail -1 $OUT/smoke.log
-bash tools/r04_b.sh $TAG
+bash tools/bench_lines.sh $TAG
