@@ -1221,10 +1221,17 @@ class GpuScan:
                 tail_box["error"] = e
 
         tail_thread = threading.Thread(target=parse_tail, daemon=True)
-        tail_thread.start()
+        started = []
+
+        def start_tail():
+            if not started:
+                started.append(1)
+                tail_thread.start()
         try:
-            self._prepare_checkpoint(engine, t0)
+            self._prepare_checkpoint(engine, t0, start_tail)
+            start_tail()
         except BaseException as e:
+            start_tail()
             tail_thread.join()
             self.tail = tail_box.get("tail")        # freed by close()
             self._rh = tail_box.get("rh")
@@ -1258,9 +1265,13 @@ class GpuScan:
             check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
         return self
 
-    def _prepare_checkpoint(self, engine, t1):
+    def _prepare_checkpoint(self, engine, t1, start_tail=lambda: None):
         """Plan the checkpoint files (row-group pruning, shards) and open them (host read + H2D +
-        the device sizing passes)."""
+        the device sizing passes). start_tail() starts the commit tail's parse beside the open: before
+        a synchronous open, after an asynchronous one has returned (it returns once the footers and
+        page headers are read; those and the tail's parse are CPU-bound on the same cores, and the
+        open's first H2D copies are on the critical path: 173 -> 166 ms at C3, profiles/r04/tail_after_open;
+        DK_TAIL_AFTER_OPEN=0 starts it first in both cases)."""
         self.prepare_ms = {}
         all_files, prunable = self.snapshot._checkpoint_files(engine, with_pruning=True)
         # row groups read per file: all, minus those the checkpoint predicate (the partition filter
@@ -1307,8 +1318,12 @@ class GpuScan:
         filtered = self.skipping is not None or self.partition is not None or self.predicate is not None
         plain = not self.shard and (not filtered or os.environ.get("DK_ASYNC_FILTERED", "1") != "0") and \
             scan_groups(len(self.ckpt_files or [])) and os.environ.get("DK_ASYNC_OPEN", "1") != "0"
+        late = bool(plain) and bool(self.ckpt_files) and os.environ.get("DK_TAIL_AFTER_OPEN", "1") != "0"
+        if not late:
+            start_tail()
         self.ckpt = ParquetSet(engine, self.ckpt_files, leaves, groups=sel, async_open=bool(plain)) \
             if self.ckpt_files else None
+        start_tail()
         t3 = time.perf_counter()
         self.prepare_ms.update({"plan_files": (t2 - t1) * 1e3, "checkpoint_open": (t3 - t2) * 1e3})
         if self.ckpt is not None and not self.ckpt.async_open:

@@ -5,7 +5,7 @@ set -o pipefail
 TAG=$1; shift
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT; cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
 for cfg in "$@"; do
 name=$(echo $cfg | tr ',=/' '___')_$rep
 env DK_VERBOSE=1 DK_CONSUME_PROFILE=1 $(echo $cfg | tr ',' ' ') timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --full-row-steps 0 --workdir /tmp/dk_c3 > $OUT/b_${name}.json 2> $OUT/b_${name}.err || { echo "bench failed"; tail -20 $OUT/b_${name}.err; exit 1; }
