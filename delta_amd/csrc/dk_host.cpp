@@ -4767,7 +4767,17 @@ extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
   const bool grouped = r->n_groups > 0 && r->xw == 0 && r->ck && !r->grp_f0.empty() && r->ev_tail;
   if (!grouped) return dk_replay_sync(r);      // no checkpoint, an ungrouped run, or exchange mode
   if (file >= (int)r->file_ready.size()) return fail("dk_replay_wait_file: bad checkpoint file index");
-  if (file >= 0 && r->file_ready[file]) return 0;
+  // every later group whose files the open has decoded already is issued now, so that its probe,
+  // selection copies and mirrors run while the consumer works on the files before it (also on the
+  // calls for files of a group that is ready: those return at once below)
+  auto issue_ready = [&]() -> int {
+    if (!r->run_lazy) return 0;
+    const int ng = (int)r->grp_f0.size() - 1;
+    while (r->grp_issued > 0 && r->grp_issued < ng && files_ready_now(r->ck, r->grp_f0[r->grp_issued + 1]))
+      if (issue_group(r)) return 1;
+    return 0;
+  };
+  if (file >= 0 && r->file_ready[file]) return issue_ready();
   if (file < 0 && r->tail_ready) return 0;
   hipEvent_t ev = r->ev_tail;
   if (file >= 0) {
@@ -4776,8 +4786,6 @@ extern "C" int dk_replay_wait_file(dk_replay* r, int32_t file) {
     while (r->grp_issued <= g) if (issue_group(r)) return 1;   // lazy runs issue groups on demand
     ev = r->grp_ev[g];
   }
-  // ... and every later group whose files the open has decoded already, so that their probes and
-  // selection copies run while the consumer works on this one
   if (r->run_lazy) {
     const int ng = (int)r->grp_f0.size() - 1;
     while (r->grp_issued < ng && files_ready_now(r->ck, r->grp_f0[r->grp_issued + 1]))
