@@ -2485,13 +2485,24 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   static const int64_t piece = (int64_t)(getenv("DK_PIECE_MB") ? std::max(1, atoi(getenv("DK_PIECE_MB"))) : 8) << 20;
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[n_files > 0 ? n_files : 1]);
   std::unique_ptr<int[]> fds(new int[n_files > 0 ? n_files : 1]);
+  // Windows (default): pieces are `piece`-byte windows of the packed image, whatever spans they
+  // cut; a window's spans are read into it, then the whole window (padding between spans included)
+  // goes to HBM in one copy. Cutting by span instead gave every small column chunk a copy of its own,
+  // which HIP runs as a blit kernel on the copy stream between the DMA transfers (160 per stream per
+  // C3 step, ~20 ms of each stream's time). DK_OPEN_WINDOWS=0: pieces cut per span.
+  static const bool windows = !getenv("DK_OPEN_WINDOWS") || atoi(getenv("DK_OPEN_WINDOWS")) != 0;
   for (int fi = 0; fi < n_files; fi++) {
     int n = 0;
     fds[fi] = -1;
-    if (by_piece)
-      for (const Span& sp : p->files[fi].spans)
+    const FileM& f = p->files[fi];
+    if (by_piece && windows) {
+      const int64_t size = f.spans.empty() ? 0 : f.spans.back().packed_off + f.spans.back().len;
+      for (int64_t o = 0; o < size; o += piece, n++) pieces.push_back({fi, -1, o, std::min<int64_t>(piece, size - o)});
+    } else if (by_piece) {
+      for (const Span& sp : f.spans)
         for (int64_t o = 0; o < sp.len; o += piece, n++)
           pieces.push_back({fi, sp.file_off + o, sp.packed_off + o, std::min<int64_t>(piece, sp.len - o)});
+    }
     left[fi].store(n);
   }
   std::thread reader([&] {
@@ -2511,9 +2522,18 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
         if (p->queued[pc.fi].load(std::memory_order_acquire) == 2) return;
         hipSetDevice(e->cfg.device);
         hipStream_t cs = p->copy[pc.fi % copy_streams()].s;
-        const bool ok = pread_full(fds[pc.fi], f.bytes.data() + pc.packed_off, pc.len, pc.file_off) == 0 &&
-                        hipMemcpyAsync(p->dfile[pc.fi].as<uint8_t>() + pc.packed_off, f.bytes.data() + pc.packed_off,
-                                       (size_t)pc.len, hipMemcpyHostToDevice, cs) == hipSuccess;
+        bool ok = true;
+        if (pc.file_off >= 0) {                       // one span's piece
+          ok = pread_full(fds[pc.fi], f.bytes.data() + pc.packed_off, pc.len, pc.file_off) == 0;
+        } else {                                      // a window: the parts of every span inside it
+          const int64_t w0 = pc.packed_off, w1 = w0 + pc.len;
+          for (const Span& sp : f.spans) {
+            const int64_t a = std::max(w0, sp.packed_off), b = std::min(w1, sp.packed_off + sp.len);
+            if (a < b && pread_full(fds[pc.fi], f.bytes.data() + a, b - a, sp.file_off + (a - sp.packed_off))) { ok = false; break; }
+          }
+        }
+        ok = ok && hipMemcpyAsync(p->dfile[pc.fi].as<uint8_t>() + pc.packed_off, f.bytes.data() + pc.packed_off,
+                                  (size_t)pc.len, hipMemcpyHostToDevice, cs) == hipSuccess;
         if (!ok) {
           static std::mutex mu;
           std::lock_guard<std::mutex> g(mu);
