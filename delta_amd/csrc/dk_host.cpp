@@ -189,6 +189,10 @@ void Reaper::reaper_drain() { reaper().drain(); }
 static void reaper_drain_all() { reaper().drain(); }
 
 static thread_local int t_synced = 0;
+// Set on the threads of an open (the opener, its image reader and their parallel_for workers): a
+// pending release may be a dk_parquet_close whose reaper job joins that very open, so a cache miss
+// there must never wait for the reaper (it allocates afresh instead).
+static thread_local int t_no_drain = 0;
 struct SyncedRelease {
   SyncedRelease() { t_synced++; }
   ~SyncedRelease() { t_synced--; }
@@ -232,7 +236,7 @@ struct MemCache {
         return b.p;
       }
     }
-    if (reaper().busy()) {         // a deferred release may be returning just such a block
+    if (!t_no_drain && reaper().busy()) {   // a deferred release may be returning just such a block
       reaper().drain();
       return get(want, got);
     }
@@ -1047,6 +1051,7 @@ struct dk_parquet {
   // after the handle is returned; files [0, files_ready) have final columns and a decode event
   // (file_dec) by then. open_state: 0 running, 1 done, 2 failed (open_err).
   std::thread opener;
+  std::atomic<bool> abort_open{false};   // dk_parquet_close before the open finished: stop reading
   std::atomic<int> open_state{1};
   std::string open_err;
   std::mutex rmu;
@@ -2239,8 +2244,9 @@ static void parallel_for(int n, F fn) {
   if (nt <= 1) { for (int i = 0; i < n; i++) fn(i); return; }
   std::atomic<int> next{0};
   std::vector<std::thread> th;
+  const int no_drain = t_no_drain;               // workers of an open stay off the reaper
   for (int t = 0; t < nt; t++)
-    th.emplace_back([&] { for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
+    th.emplace_back([&, no_drain] { t_no_drain = no_drain; for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
   for (auto& x : th) x.join();
 }
 
@@ -2505,7 +2511,9 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
     }
     left[fi].store(n);
   }
-  std::thread reader([&] {
+  const int no_drain = t_no_drain;
+  std::thread reader([&, no_drain] {
+    t_no_drain = no_drain;
     if (by_piece) {
       for (int fi = 0; fi < n_files; fi++) {
         fds[fi] = open(p->files[fi].path.c_str(), O_RDONLY);
@@ -2520,6 +2528,13 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
         const Piece& pc = pieces[k];
         FileM& f = p->files[pc.fi];
         if (p->queued[pc.fi].load(std::memory_order_acquire) == 2) return;
+        if (p->abort_open.load(std::memory_order_relaxed)) {   // closed while opening: stop reading
+          static std::mutex mu;
+          std::lock_guard<std::mutex> g(mu);
+          if (rerrs[pc.fi].empty()) rerrs[pc.fi] = "Error reading Parquet file: " + f.path + " (reader closed)";
+          p->queued[pc.fi].store(2, std::memory_order_release);
+          return;
+        }
         hipSetDevice(e->cfg.device);
         hipStream_t cs = p->copy[pc.fi % copy_streams()].s;
         bool ok = true;
@@ -2705,6 +2720,7 @@ extern "C" int dk_parquet_open_async(dk_engine* e, const char* const* paths, int
   std::function<void(dk_parquet*)> publish = [&](dk_parquet* q) { handed.set_value(q); };
   const std::vector<std::vector<int32_t>>* gp = (rg_count && !all) ? &groups : nullptr;
   std::thread t([&, gp] {
+    t_no_drain = 1;
     dk_parquet* q = nullptr;
     bool pub = false;
     std::function<void(dk_parquet*)> pub_fn = [&](dk_parquet* x) { pub = true; publish(x); };
@@ -3024,6 +3040,7 @@ extern "C" int dk_parquet_column_rows(dk_parquet* p, int32_t file, int32_t leaf,
 
 extern "C" void dk_parquet_close(dk_parquet* p) {
   if (!p) return;
+  p->abort_open.store(true);            // an open still reading stops at its next piece
   reaper().run([p] {
     ensure_open(p);
     hipSetDevice(p->eng->cfg.device);

@@ -1188,21 +1188,31 @@ class GpuScan:
         else:
             mine = commits
 
+        n_files_all = len(commits) + len(self.snapshot._json_checkpoint_parts())
+
         def parse_tail():
             # the tail, then the replay's commit-tail half (action table + key-table inputs)
             t = time.perf_counter()
             try:
-                tail = JsonTail(engine, [d.path for d in mine], [d.version for d in mine], self.read_stats,
-                                checkpoint_paths=parts)
+                try:
+                    tail = JsonTail(engine, [d.path for d in mine], [d.version for d in mine], self.read_stats,
+                                    checkpoint_paths=parts)
+                except BaseException:
+                    if owner is not None:   # the peers wait in global_steps: they raise with this rank
+                        tail_box["voted"] = "failed"
+                        owner.global_steps(np.zeros(n_files_all, np.int64), failed=True)
+                    raise
                 tail_box["tail"] = tail
                 if owner is not None:
                     files = self.tail_commits + self.tail_parts
                     steps = (C.c_int32 * max(1, len(files)))()
                     check(lib().dk_json_tail_file_steps(tail._h, steps))
-                    local = np.zeros(len(commits) + len(self.snapshot._json_checkpoint_parts()), np.int64)
+                    local = np.zeros(n_files_all, np.int64)
                     for k, j in enumerate(files):
                         local[j] = steps[k]
+                    tail_box["voted"] = "failed"        # (until the vote has gone through)
                     total = np.asarray(owner.global_steps(local), dtype=np.int64)
+                    tail_box["voted"] = "ok"
                     step0 = np.concatenate([[0], np.cumsum(total)])
                     if step0[-1] >= (1 << 31) - 1:
                         raise DkError("owner mode: more than 2^31 commit-tail batches")
@@ -1220,6 +1230,16 @@ class GpuScan:
             except BaseException as e:          # re-raised on the calling thread
                 tail_box["error"] = e
 
+        def owner_failed():
+            """This rank is about to raise from prepare: make sure its peers raise too instead of
+            waiting for it in a collective (global_steps, or the exchange's first vote)."""
+            if owner is None or tail_box.get("voted") == "failed":
+                return                      # (a failed vote: every rank raised at global_steps)
+            if not tail_box.get("voted"):
+                owner.global_steps(np.zeros(n_files_all, np.int64), failed=True)
+            else:
+                owner.abort()               # global_steps went through: the exchange's first vote
+
         tail_thread = threading.Thread(target=parse_tail, daemon=True)
         started = []
 
@@ -1231,38 +1251,46 @@ class GpuScan:
             self._prepare_checkpoint(engine, t0, start_tail)
             start_tail()
         except BaseException as e:
-            start_tail()
-            tail_thread.join()
-            self.tail = tail_box.get("tail")        # freed by close()
-            self._rh = tail_box.get("rh")
-            if "error" in tail_box:
-                raise tail_box["error"]
-            raise e
+            if started:                             # the tail's errors come first in replay order
+                tail_thread.join()
+                self.tail = tail_box.get("tail")    # freed by close()
+                self._rh = tail_box.get("rh")
+            try:
+                owner_failed()
+            finally:
+                if "error" in tail_box:
+                    raise tail_box["error"]
+                raise e
         tail_thread.join()
         if "tail" in tail_box:
             self.tail = tail_box["tail"]
         if "rh" in tail_box:
             self._rh = tail_box["rh"]
         if "error" in tail_box:
+            owner_failed()
             raise tail_box["error"]
         self.prepare_ms["commit_tail"] = tail_box["ms"]
         self.prepare_ms["replay_create_tail"] = tail_box["create_ms"]
-        t3 = time.perf_counter()
-        if self.ckpt is not None:
-            check(lib().dk_replay_attach_checkpoint(self._rh, self.ckpt._h))
-        self.prepare_ms["replay_attach"] = (time.perf_counter() - t3) * 1e3
-        if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
-            check(lib().dk_replay_set_exchange(self._rh, self.shard[0], self.shard[1]))
-        if getattr(self, "owner", None) is not None:
-            check(lib().dk_replay_set_owner(self._rh, self.shard[0], self.shard[1]))
-        if self.partition is not None:
-            from . import partitions as pp
-            pprog = pp.pack(self.partition, dk_part_program)
-            check(lib().dk_replay_set_partition_filter(self._rh, C.byref(pprog)))
-        if self.skipping is not None:
-            from . import skipping as sk
-            prog = sk.pack(self.skipping[1:], dk_skip_program)
-            check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
+        try:
+            t3 = time.perf_counter()
+            if self.ckpt is not None:
+                check(lib().dk_replay_attach_checkpoint(self._rh, self.ckpt._h))
+            self.prepare_ms["replay_attach"] = (time.perf_counter() - t3) * 1e3
+            if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
+                check(lib().dk_replay_set_exchange(self._rh, self.shard[0], self.shard[1]))
+            if getattr(self, "owner", None) is not None:
+                check(lib().dk_replay_set_owner(self._rh, self.shard[0], self.shard[1]))
+            if self.partition is not None:
+                from . import partitions as pp
+                pprog = pp.pack(self.partition, dk_part_program)
+                check(lib().dk_replay_set_partition_filter(self._rh, C.byref(pprog)))
+            if self.skipping is not None:
+                from . import skipping as sk
+                prog = sk.pack(self.skipping[1:], dk_skip_program)
+                check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
+        except BaseException:
+            owner_failed()
+            raise
         return self
 
     def _prepare_checkpoint(self, engine, t1, start_tail=lambda: None):

@@ -364,6 +364,12 @@ def exchange_local(sides):
 # No rank holds the whole commit tail; the ScanMetrics counters are summed over the ranks.
 # ------------------------------------------------------------------------------------------------
 REC_BYTES = 32                      # dk OwnerKeyRec
+COLLISION = 4                       # dk E_COLLISION: a 64-bit hash collision at an owner
+ERR_BIT = 1 << 20                   # vote bit: a rank failed at this step
+
+
+class OwnerPeerError(RuntimeError):
+    """Another rank of the owner exchange failed (its own error is raised on that rank)."""
 
 
 class OwnerSide:
@@ -513,17 +519,29 @@ class OwnerExchange:
         self.ms = {}
         self.bytes_sent = 0
 
-    def global_steps(self, local):
+    def global_steps(self, local, failed=False):
         """Batches of every commit file (replay order): this rank's counts summed over the ranks.
-        Called from the scan's commit-tail thread."""
+        Called from the scan's commit-tail thread. A rank whose commit-tail parse failed still takes
+        part (failed=True, its counts zero) so that no peer waits for it: every rank then raises
+        (in the reference every reader of the log sees the parse error)."""
         import contextlib
+        import numpy as np
         import torch
         import torch.distributed as dist
         dev = self._dev()
+        v = np.concatenate([np.asarray(local, dtype=np.int64).ravel(), [1 if failed else 0]])
         with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
-            t = torch.as_tensor(local, dtype=torch.int64).to(dev)
+            t = torch.as_tensor(v, dtype=torch.int64).to(dev)
             dist.all_reduce(t, group=self.group)
-            return t.cpu().numpy()
+            out = t.cpu().numpy()
+        if out[-1] and not failed:
+            raise OwnerPeerError("owner exchange: the commit-tail parse failed on another rank")
+        return out[:-1]
+
+    def abort(self):
+        """A rank that fails after global_steps (checkpoint open, replay setup) answers the exchange's
+        first vote with its error bit instead of running the exchange, so its peers raise too."""
+        self._any(ERR_BIT)
 
     def _dev(self):
         import torch
@@ -555,41 +573,78 @@ class OwnerExchange:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return int(t.item())
 
+    def _step(self, fn):
+        """Run this rank's local part of an exchange step, then vote on the MAX over ranks of the
+        error bit: a local error, or any peer's, raises on every rank at the same step (a rank that
+        raised before its next collective would leave its peers waiting in it)."""
+        box = {}
+        _, f = self._step_flag(lambda: box.__setitem__("out", fn()), {})
+        return box.get("out"), f
+
     def __call__(self, side):
         import time
         t0 = time.perf_counter()
         self.bytes_sent = 0
-        side.begin()
+        first = [True]
         while True:
-            recs_c, bytes_c = side.tail_counts()
-            recs, keys = side.tail_pack(int(recs_c.sum()), int(bytes_c.sum()))
+            def pack():
+                if first:
+                    side.begin()
+                    first.clear()
+                recs_c, bytes_c = side.tail_counts()
+                return (recs_c, bytes_c) + tuple(side.tail_pack(int(recs_c.sum()), int(bytes_c.sum())))
+            (recs_c, bytes_c, recs, keys), _ = self._step(pack)
             rrecs, rrc = self._a2a(recs, recs_c * REC_BYTES)
             rkeys, _ = self._a2a(keys, bytes_c)
-            ans, flag = side.tail_resolve(rrecs, rkeys)
-            if self._any(flag):                  # a hash collision at some owner: all ranks reseed
+            box = {}
+
+            def resolve():
+                box["ans"], box["flag"] = side.tail_resolve(rrecs, rkeys)
+            _, flag = self._step_flag(resolve, box)     # the collision vote carries the error bit
+            if flag & COLLISION:                 # a hash collision at some owner: all ranks reseed
                 side.reseed()
                 continue
-            back, _ = self._a2a(ans, [c // REC_BYTES for c in rrc], recs_c)
-            side.tail_finish(back)
+            back, _ = self._a2a(box["ans"], [c // REC_BYTES for c in rrc], recs_c)
             break
         t1 = time.perf_counter()
-        side.run()
-        c = side.ckpt_counts()
+
+        def run_pack():
+            side.tail_finish(back)
+            side.run()
+            c = side.ckpt_counts()
+            return c, side.ckpt_pack(int(c.sum()))
+        (c, send), _ = self._step(run_pack)
         t2 = time.perf_counter()
-        send = side.ckpt_pack(int(c.sum()))
         recv, rc = self._a2a(send, c)
-        flags = side.ckpt_lookup(recv)
+        flags, _ = self._step(lambda: side.ckpt_lookup(recv))
         back, _ = self._a2a(flags, rc, c)
-        side.ckpt_apply(back)
-        cr, cb = side.cand_counts()
-        recs, keys = side.cand_pack(int(cr.sum()), int(cb.sum()))
+
+        def apply_pack():
+            side.ckpt_apply(back)
+            cr, cb = side.cand_counts()
+            return (cr, cb) + tuple(side.cand_pack(int(cr.sum()), int(cb.sum())))
+        (cr, cb, recs, keys), _ = self._step(apply_pack)
         rrecs, rrc = self._a2a(recs, cr * REC_BYTES)
         rkeys, _ = self._a2a(keys, cb)
-        ans = side.cand_verify(rrecs, rkeys)
+        ans, _ = self._step(lambda: side.cand_verify(rrecs, rkeys))
         back, _ = self._a2a(ans, [x // REC_BYTES for x in rrc], cr)
         side.cand_finish(back)
         t3 = time.perf_counter()
         self.ms = {"tail_exchange": (t1 - t0) * 1e3, "decode_hash": (t2 - t1) * 1e3, "row_exchange": (t3 - t2) * 1e3}
+
+    def _step_flag(self, fn, box):
+        """_step whose vote also carries the collision flag fn left in box["flag"]."""
+        err = None
+        try:
+            fn()
+        except BaseException as e:       # noqa: BLE001 -- re-raised after the vote
+            err = e
+        f = self._any(ERR_BIT if err is not None else int(box.get("flag", 0)))
+        if f & ERR_BIT:
+            if err is not None:
+                raise err
+            raise OwnerPeerError("owner exchange: another rank failed")
+        return None, f
 
 
 class OwnerLoopback:
@@ -617,8 +672,11 @@ class OwnerLoopback:
         t.close()
         return cls([steps[i] for i in range(n)])
 
-    def global_steps(self, local):
+    def global_steps(self, local, failed=False):
         return self._steps
+
+    def abort(self):
+        pass
 
     def __call__(self, side):
         self.sides[side.rank] = side       # run() drives them once every rank's side has arrived

@@ -22,6 +22,20 @@ def main():
     eng = K.GpuEngine()
     snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
     mode = sys.argv[3] if len(sys.argv) > 3 else "allgather"
+    if mode == "owner_fail":     # a malformed commit only rank 1 parses: every rank must raise, none hang
+        scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerExchange()).build()
+        try:
+            scan.prepare(eng)
+            scan.run()
+            res = {"error": None}
+        except Exception as e:      # noqa: BLE001
+            res = {"error": type(e).__name__, "msg": str(e)[:300]}
+        with open(out + ".%d" % rank, "w") as fh:
+            json.dump(res, fh)
+        scan.close()
+        eng.close()
+        dist.destroy_process_group()
+        return
     if mode == "owner":      # owner-partitioned: every rank's counters are its share of the world's
         scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerExchange()).build()
     else:

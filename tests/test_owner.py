@@ -46,7 +46,7 @@ class CpuOwnerSide:
     """CPU stand-in for shard.OwnerSide: the same calls, buffers in the same layouts (CPU torch
     tensors), keys from the oracle (ref.action_key), the owner's rules restated in Python."""
 
-    def __init__(self, table, world, rank, owner, bs=1024, collide_first=False):
+    def __init__(self, table, world, rank, owner, bs=1024, collide_first=False, fail=None):
         import torch  # noqa: F401
         from delta_amd import kernel as K
         from oracle import ref
@@ -60,6 +60,10 @@ class CpuOwnerSide:
         local = np.zeros(len(commits), np.int64)
         for j in mine:
             local[j] = len(batches[j])
+        self.fail = fail
+        if fail == "parse":                      # this rank's commit parse failed: vote, then raise
+            owner.global_steps(local * 0, failed=True)
+            raise ValueError("malformed commit")
         step0 = np.concatenate([[0], np.cumsum(owner.global_steps(local))])
         self.acts = []            # (kind, step, row, key, tail row id (commit, line))
         for j in mine:
@@ -180,6 +184,8 @@ class CpuOwnerSide:
 
     def ckpt_lookup(self, recv):
         import torch
+        if self.fail == "lookup":
+            raise ValueError("lookup failed")
         hs = {_h(k, self.seed) for k in self.table}
         return torch.tensor([1 if int(np.uint64(np.int64(x))) in hs else 0 for x in recv.tolist()], dtype=torch.uint8)
 
@@ -273,6 +279,41 @@ def _gloo_worker(rank, world, port, table, out_path, bs, collide):
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def _gloo_fail_worker(rank, world, port, table, out_path, fail):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    try:
+        ex = shard.OwnerExchange()
+        err = None
+        try:
+            side = CpuOwnerSide(table, world, rank, ex, fail=fail if rank == world - 1 else None)
+            if fail == "open" and rank == world - 1:
+                ex.abort()                       # failed after global_steps (checkpoint open)
+                raise ValueError("open failed")
+            ex(side)
+        except Exception as e:                   # noqa: BLE001
+            err = type(e).__name__
+        with open(out_path + ".%d" % rank, "w") as f:
+            json.dump({"error": err}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", ["parse", "open", "lookup"])
+def test_gloo_owner_failure_on_one_rank(tmp_path, fail):
+    """A failure on the last rank -- its commit-tail parse (at the global-steps vote), its checkpoint
+    open (after it: the exchange's first vote), or an owner step inside the exchange -- raises on
+    every rank; no rank is left waiting in a collective (the spawn would hang)."""
+    import torch.multiprocessing as mp
+    table = str(tmp_path / "t")
+    synth.write_table(table, synth.TableSpec(n_adds=2_000, n_parts=2, row_group_size=500, n_commits=5,
+                                             adds_per_commit=10, removes_per_commit=10))
+    out = str(tmp_path / "res.json")
+    mp.spawn(_gloo_fail_worker, args=(3, _free_port(), table, out, fail), nprocs=3, join=True)
+    res = [json.load(open(out + ".%d" % r))["error"] for r in range(3)]
+    assert res == ["OwnerPeerError", "OwnerPeerError", "ValueError"], res
 
 
 @pytest.mark.parametrize("world,bs,collide", [(2, 1024, False), (3, 3, True)])
