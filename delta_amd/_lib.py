@@ -31,15 +31,10 @@ class dk_config(C.Structure):
                 ("device", C.c_int32), ("flags", C.c_int32)]
 
 
-class dk_part_program(C.Structure):
-    _fields_ = [("n_fields", C.c_int32), ("field_type", C.c_int32 * 8), ("name_off", C.c_int32 * 8),
-                ("name_len", C.c_int32 * 8), ("n_ops", C.c_int32), ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64),
-                ("lit", C.c_int64 * 64), ("pool", C.c_char * 4096)]
-
-
 class dk_rg_filter(C.Structure):
-    _fields_ = [("n_cols", C.c_int32), ("col_off", C.c_int32 * 8), ("col_len", C.c_int32 * 8), ("n_ops", C.c_int32),
-                ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64), ("lit", C.c_int64 * 64), ("pool", C.c_char * 2048)]
+    _fields_ = [("n_cols", C.c_int32), ("col_off", C.c_void_p), ("col_len", C.c_void_p), ("n_ops", C.c_int32),
+                ("op", C.c_void_p), ("arg", C.c_void_p), ("lit", C.c_void_p), ("pool", C.c_void_p),
+                ("pool_len", C.c_int64)]
 
 
 class dk_column(C.Structure):
@@ -50,10 +45,10 @@ class dk_column(C.Structure):
                 ("fixed", C.c_void_p), ("offs", C.c_void_p), ("chars", C.c_void_p)]
 
 
-class dk_skip_program(C.Structure):
-    _fields_ = [("n_paths", C.c_int32), ("path_type", C.c_int32 * 8), ("path_depth", C.c_int32 * 8),
-                ("name_off", (C.c_int32 * 4) * 8), ("name_len", (C.c_int32 * 4) * 8), ("names", C.c_char * 4096),
-                ("n_ops", C.c_int32), ("op", C.c_int32 * 64), ("arg", C.c_int32 * 64), ("lit", C.c_int64 * 64)]
+class dk_parsed_column(C.Structure):
+    _fields_ = [("type", C.c_int32), ("n", C.c_int64), ("validity", C.c_void_p), ("values", C.c_void_p),
+                ("values_hi", C.c_void_p), ("scale", C.c_void_p), ("wide", C.c_void_p), ("offs", C.c_void_p),
+                ("chars", C.c_void_p)]
 
 
 class dk_read_options(C.Structure):
@@ -104,8 +99,9 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_owner_reseed", "dk_replay_owner_tail_finish", "dk_replay_owner_ckpt_counts",
            "dk_replay_owner_ckpt_pack", "dk_replay_owner_ckpt_lookup", "dk_replay_owner_ckpt_apply",
            "dk_replay_owner_cand_counts", "dk_replay_owner_cand_pack", "dk_replay_owner_cand_verify",
-           "dk_replay_owner_cand_finish", "dk_json_parse_stats", "dk_parsed_stats_column", "dk_parsed_stats_eval",
-           "dk_parsed_stats_free"]
+           "dk_replay_owner_cand_finish", "dk_skip_compile", "dk_part_compile", "dk_program_describe",
+           "dk_program_free", "dk_json_parse", "dk_parsed_num_leaves", "dk_parsed_leaf_path", "dk_parsed_column_get",
+           "dk_parsed_eval", "dk_parsed_free"]
 
 
 def lib(build_if_missing=True):
@@ -205,10 +201,16 @@ def lib(build_if_missing=True):
         "dk_replay_owner_cand_pack": (C.c_int, [P, P, P]),
         "dk_replay_owner_cand_verify": (C.c_int, [P, P, I64, P, I64, P]),
         "dk_replay_owner_cand_finish": (C.c_int, [P, P]),
-        "dk_json_parse_stats": (C.c_int, [P, P, I64, P, P, P, P, I32, C.POINTER(P)]),
-        "dk_parsed_stats_column": (C.c_int, [P, I32, P, P]),
-        "dk_parsed_stats_eval": (C.c_int, [P, P, P]),
-        "dk_parsed_stats_free": (None, [P]),
+        "dk_skip_compile": (C.c_int, [C.c_char_p, C.c_char_p, C.POINTER(P)]),
+        "dk_part_compile": (C.c_int, [C.c_char_p, C.POINTER(P)]),
+        "dk_program_describe": (I64, [P, C.c_char_p, I64]),
+        "dk_program_free": (None, [P]),
+        "dk_json_parse": (C.c_int, [P, C.c_char_p, I64, P, P, P, P, I32, C.POINTER(P)]),
+        "dk_parsed_num_leaves": (I32, [P]),
+        "dk_parsed_leaf_path": (I64, [P, I32, C.c_char_p, I64]),
+        "dk_parsed_column_get": (C.c_int, [P, I32, C.POINTER(dk_parsed_column)]),
+        "dk_parsed_eval": (C.c_int, [P, P, P]),
+        "dk_parsed_free": (None, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -194,46 +194,49 @@ struct Slot {
 
 enum : int32_t { E_URI = 1, E_UTF8 = 2, E_COLLISION = 4, E_PAGE = 8, E_STATS = 16, E_PART = 32 };
 
-// Data-skipping program (layout of dk_skip_program in include/dkgpu.h): the stats fields to
-// extract from each row's add.stats JSON and a postfix program over them (delta_amd/skipping.py).
-constexpr int SK_MAX_PATHS = 8, SK_MAX_DEPTH = 4, SK_MAX_OPS = 64, SK_NAMES = 4096;
+// Data-skipping program (a dk_program compiled by dk_skip_compile, dk_expr.cpp, laid out in one device
+// buffer): the stats fields to read from each row's add.stats JSON (or add.stats_parsed columns) and
+// a postfix program over them. Any number of paths, ops and literal bytes; the evaluation stack is at
+// most SK_STACK deep (the compiler re-associates AND / OR chains to stay under it).
+constexpr int SK_STACK = 32;        // evaluation stack (dk_expr.cpp kMaxStack)
+constexpr int SK_NARROW = 8;        // programs of up to this many paths keep the values in registers
+constexpr int SK_WINDOW = 32;       // paths extracted per pass over a JSON object (one mask word)
 enum : int32_t { SK_LONG = 0, SK_INT = 1, SK_SHORT = 2, SK_BYTE = 3, SK_DATE = 4, SK_STRING = 5, SK_TIMESTAMP = 6, SK_DECIMAL = 7, SK_TIMESTAMP_NTZ = 8,
                  SK_FLOAT = 9, SK_DOUBLE = 10 };
 enum : int32_t { OP_STAT = 0, OP_LIT = 1, OP_LT = 2, OP_LE = 3, OP_GT = 4, OP_GE = 5, OP_EQ = 6, OP_AND = 7, OP_OR = 8, OP_LIT_STR = 9, OP_TIMEADD = 10, OP_LIT_DEC = 11,
                  OP_FCMP = 12 };
 enum : int32_t { FC_LT = 0, FC_LE = 1, FC_GT = 2, FC_GE = 3, FC_ALL = 4, FC_NONE = 5 };
 struct DSkipProg {
-  int32_t n_paths;
-  int32_t path_type[SK_MAX_PATHS];
-  int32_t path_depth[SK_MAX_PATHS];
-  int32_t name_off[SK_MAX_PATHS][SK_MAX_DEPTH];
-  int32_t name_len[SK_MAX_PATHS][SK_MAX_DEPTH];
-  char names[SK_NAMES];
-  int32_t n_ops;
-  int32_t op[SK_MAX_OPS];
-  int32_t arg[SK_MAX_OPS];
-  int64_t lit[SK_MAX_OPS];
+  int32_t n_paths, n_ops;
+  int32_t max_comps;               // most name components of a path
+  const int32_t* path_type;        // [n_paths] SK_*
+  const int32_t* path_comp;        // [n_paths + 1]: path p's name components are [path_comp[p], path_comp[p + 1])
+  const int32_t* comp_off;         // per component: its name in names
+  const int32_t* comp_len;
+  const int32_t* op;               // [n_ops]
+  const int32_t* arg;
+  const int64_t* lit;
+  const char* names;               // component names and literal bytes (UTF-8)
 };
 
-// Partition-pruning program (layout of dk_part_program in include/dkgpu.h; delta_amd/partitions.py):
-// the partition columns it reads (physical names, looked up in each row's partitionValues map) and
-// a postfix program over their deserialized values.
-constexpr int PP_MAX_FIELDS = 8, PP_MAX_OPS = 64, PP_POOL = 4096;
+// Partition-pruning program (a dk_program compiled by dk_part_compile): the partition columns it reads
+// (physical names, looked up in each row's partitionValues map when the program reads them) and a
+// postfix program over their deserialized values.
+constexpr int PP_STACK = 32;
 enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING = 4, PT_DATE = 5, PT_DECIMAL = 6,
                  PT_BOOL = 7, PT_F32 = 8, PT_F64 = 9, PT_TIMESTAMP = 10 };
 enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, PO_LT = 4, PO_LE = 5, PO_GT = 6,
                  PO_GE = 7, PO_EQ = 8, PO_NSEQ = 9, PO_ISNULL = 10, PO_ISNOTNULL = 11, PO_NOT = 12, PO_AND = 13,
-                 PO_OR = 14, PO_LIT_DEC = 15, PO_FCMP = 16 };
+                 PO_OR = 14, PO_LIT_DEC = 15, PO_FCMP = 16, PO_COALESCE = 17 };
 struct DPartProg {
-  int32_t n_fields;
-  int32_t field_type[PP_MAX_FIELDS];
-  int32_t name_off[PP_MAX_FIELDS];
-  int32_t name_len[PP_MAX_FIELDS];
-  int32_t n_ops;
-  int32_t op[PP_MAX_OPS];
-  int32_t arg[PP_MAX_OPS];       // PO_FIELD: field; PO_LIT_STR: length
-  int64_t lit[PP_MAX_OPS];       // PO_LIT_INT: value; PO_LIT_STR: offset into pool
-  char pool[PP_POOL];            // field names and string literals (UTF-8)
+  int32_t n_fields, n_ops;
+  const int32_t* field_type;       // [n_fields] PT_*
+  const int32_t* name_off;         // physical column name (map key) in pool
+  const int32_t* name_len;
+  const int32_t* op;               // [n_ops]
+  const int32_t* arg;              // PO_FIELD: field; PO_LIT_STR / PO_LIT_DEC: length; PO_COALESCE: operands
+  const int64_t* lit;              // PO_LIT_INT: value; PO_LIT_STR / PO_LIT_DEC: offset into pool
+  const char* pool;                // field names and literals (UTF-8)
 };
 
 // partitionValues map rows: repeated key / value leaves (row_offs over entries), per action for the
@@ -267,23 +270,37 @@ struct StatsRows {
 // timestamp millis, TP_INT96 timestamp (nanos of day + Julian day), TP_STR UTF-8 bytes, TP_DEC
 // unscaled INT32 / INT64 with a scale, TP_F32 / TP_F64 IEEE float / double
 enum : int32_t { TP_INT = 0, TP_MILLIS = 1, TP_INT96 = 2, TP_STR = 3, TP_DEC = 4, TP_F32 = 5, TP_F64 = 6 };
+struct TypedPath {
+  const uint8_t* def;
+  const uint8_t* vals;                // fixed-width values, one per row (TP_STR: null)
+  const int64_t* offs;                // TP_STR: n + 1 offsets into chars
+  const uint8_t* chars;
+  int32_t max_def;
+  int32_t width;                      // 4, 8 or 12 (INT96)
+  int32_t kind;                       // TP_*
+  int32_t scale;                      // TP_DEC: the decimal's scale
+};
 struct StatsParsedRows {
   int64_t n;
   int32_t n_paths;
   int32_t struct_def;                 // row_def >= this: add.stats_parsed is non-null
-  const uint8_t* def[8];
-  const uint8_t* vals[8];             // fixed-width values, one per row (TP_STR: null)
-  int32_t max_def[8];
-  int32_t width[8];                   // 4, 8 or 12 (INT96)
-  int32_t kind[8];                    // TP_*
-  int32_t scale[8];                   // TP_DEC: the decimal's scale
-  const int64_t* offs[8];             // TP_STR: n + 1 offsets into chars
-  const uint8_t* chars[8];
+  const TypedPath* paths;             // [n_paths], device memory, in the program's path order
   // the add.stats JSON of the same rows (column mode): the reference reads only it, so a row with a
   // null add.stats keeps its selection, and a row whose typed values cannot stand for the JSON (a
   // null stats_parsed struct, a float -0.0 -- Kernel reads "-0.0" as +0.0 but "-1e-400" as -0.0 --,
   // sub-microsecond INT96 nanos) is marked (selection byte 2) for k_stats_eval over its JSON
   StatsRows js;
+};
+
+// Per-lane scratch of the wide (> SK_NARROW paths) skipping kernels: path-major arrays of `lanes`
+// entries each (values, set words, typed kinds / scales / pointers); grids are sized to `lanes`.
+struct SkScratch {
+  long long* val;
+  uint32_t* setw;
+  int32_t* kind;
+  int32_t* scale;
+  const uint8_t** ptr;
+  long long lanes;
 };
 
 // Device-side counters and error state of one replay.

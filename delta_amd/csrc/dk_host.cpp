@@ -29,6 +29,7 @@
 #include "dk_device.h"
 #include "dk_thrift.h"
 #include "dk_uri.h"
+#include "dk_expr.h"
 
 namespace dk {
 void launch_page_headers(const DChunk*, DPage*, int, hipStream_t);
@@ -56,9 +57,9 @@ void launch_table_insert(const DJsonAction*, int, Slot*, uint64_t, hipStream_t);
 void launch_first_row(const uint8_t*, long long, int, unsigned long long*, hipStream_t);
 void launch_table_update(DJsonAction*, int, Slot*, uint64_t, const uint8_t*, DState*, hipStream_t);
 void launch_json_select(const DJsonAction*, int, const Slot*, uint64_t, const uint8_t*, uint8_t*, DState*, hipStream_t);
-void launch_stats_eval(const StatsRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
-void launch_stats_parsed(const StatsParsedRows&, const DSkipProg*, uint8_t*, DState*, hipStream_t);
-void launch_part_eval(const MapRows&, const DPartProg*, uint8_t*, DState*, hipStream_t);
+void launch_stats_eval(const StatsRows&, const DSkipProg&, const SkScratch&, uint8_t*, DState*, hipStream_t);
+void launch_stats_parsed(const StatsParsedRows&, const DSkipProg&, const SkScratch&, uint8_t*, DState*, hipStream_t);
+void launch_part_eval(const MapRows&, const DPartProg&, uint8_t*, DState*, hipStream_t);
 void launch_table_fp(const Slot*, uint32_t*, uint64_t, hipStream_t);
 void launch_probe_all(const ProbeSet&, const Slot*, const uint32_t*, uint64_t, const DJsonAction*, const uint8_t*, uint32_t, uint64_t,
                       int32_t*, unsigned int*, DState*, hipStream_t);
@@ -84,9 +85,9 @@ void launch_own_verify(const OwnerKeyRec*, long long, const int64_t*, const uint
                        const DJsonAction*, const uint8_t*, uint8_t*, hipStream_t);
 void launch_own_cand_finish(const ProbeSet&, const int32_t*, const uint8_t*, long long, DState*, hipStream_t);
 int warm_kernels();
-void launch_json_parse_stats(const uint8_t*, const int64_t*, const uint8_t*, const uint8_t*, long long, const DSkipProg*,
-                             long long*, uint32_t*, DState*, hipStream_t);
-void launch_parsed_eval(const uint8_t*, const int64_t*, long long, const DSkipProg*, const long long*, const uint32_t*,
+void launch_json_parse_stats(const uint8_t*, const int64_t*, const uint8_t*, const uint8_t*, long long, const DSkipProg&,
+                             const SkScratch&, long long*, uint32_t*, DState*, hipStream_t);
+void launch_parsed_eval(const uint8_t*, const int64_t*, long long, const DSkipProg&, long long*, uint32_t*,
                         uint8_t*, hipStream_t);
 }  // namespace dk
 
@@ -94,6 +95,7 @@ using namespace dk;
 
 static thread_local std::string g_err;
 static int fail(const std::string& m) { g_err = m; return 1; }
+namespace dk { int dk_fail(const std::string& m) { return fail(m); } }
 
 #define HIPOK(x)                                                                              \
   do {                                                                                        \
@@ -2108,10 +2110,12 @@ extern "C" int dk_parquet_prune_row_groups(const char* path, const dk_rg_filter*
   *n = (int32_t)f.rgs.size();
   for (int32_t g = 0; g < *n && g < cap; g++) keep[g] = 1;
   if (!flt) return 0;
-  if (flt->n_cols < 0 || flt->n_cols > 8 || flt->n_ops < 0 || flt->n_ops > 64) return fail("dk_parquet_prune_row_groups: bad filter");
+  if (flt->n_cols < 0 || flt->n_ops < 0 || flt->pool_len < 0 || (flt->n_cols && (!flt->col_off || !flt->col_len)) ||
+      (flt->n_ops && (!flt->op || !flt->arg || !flt->lit)) || (flt->pool_len && !flt->pool))
+    return fail("dk_parquet_prune_row_groups: bad filter");
   std::vector<int> col_leaf(flt->n_cols, -1);       // filter column -> non-repeated leaf of this file
   for (int c = 0; c < flt->n_cols; c++) {
-    if (flt->col_off[c] < 0 || flt->col_len[c] < 0 || flt->col_off[c] + flt->col_len[c] > (int)sizeof(flt->pool))
+    if (flt->col_off[c] < 0 || flt->col_len[c] < 0 || (int64_t)flt->col_off[c] + flt->col_len[c] > flt->pool_len)
       return fail("dk_parquet_prune_row_groups: bad column");
     const std::string name(flt->pool + flt->col_off[c], flt->col_len[c]);
     for (size_t li = 0; li < f.leaves.size(); li++)
@@ -2129,7 +2133,7 @@ extern "C" int dk_parquet_prune_row_groups(const char* path, const dk_rg_filter*
       PItem it; it.kind = 1; it.lt = flt->arg[k]; it.lit = flt->lit[k];
       if (it.lt == RL_STRING) {
         const int64_t off = flt->lit[k] & 0xffffffffll, len = flt->lit[k] >> 32;
-        if (off < 0 || len < 0 || off + len > (int64_t)sizeof(flt->pool)) return fail("dk_parquet_prune_row_groups: bad literal");
+        if (off < 0 || len < 0 || off + len > flt->pool_len) return fail("dk_parquet_prune_row_groups: bad literal");
         it.str.assign(flt->pool + off, (size_t)len);
       }
       st.push_back(it);
@@ -3830,6 +3834,82 @@ extern "C" int dk_log_pm_scan(const char* const* paths, int32_t n, int64_t* p_li
 // ------------------------------------------------------------------------------------------------
 // replay
 // ------------------------------------------------------------------------------------------------
+// A compiled program (dk_skip_compile / dk_part_compile) installed in device memory: its image
+// (dk_expr.h program_image) in one buffer and the kernel-argument struct of pointers into it. Wide
+// skipping programs (> SK_NARROW paths) also own the per-lane scratch their kernels keep the values
+// in (SkScratch: lanes x paths, sized to <= 256 MiB; grids are cut to the lanes).
+struct DevSkip {
+  dk_program prog;                      // host copy (paths: the stats_parsed leaves, the parsed schema)
+  DBuf img, scratch;
+  DSkipProg P{};
+  SkScratch S{};
+};
+struct DevPart {
+  dk_program prog;
+  DBuf img;
+  DPartProg P{};
+};
+static int install_skip(DevSkip& d, const dk_program& src) {
+  if (src.kind != DK_PROGRAM_SKIPPING) return fail("not a data-skipping program");
+  d.prog = src;
+  int64_t offs[8];
+  const std::string img = program_image(src, offs);
+  if (d.img.alloc(img.size())) return 1;
+  HIPOK(hipMemcpy(d.img.p, img.data(), img.size(), hipMemcpyHostToDevice));
+  const char* b = d.img.as<char>();
+  DSkipProg P{};
+  P.n_paths = (int32_t)src.path_type.size();
+  P.n_ops = (int32_t)src.op.size();
+  for (auto& p : src.paths) P.max_comps = std::max<int32_t>(P.max_comps, (int32_t)p.size());
+  P.path_type = (const int32_t*)(b + offs[0]);
+  P.path_comp = (const int32_t*)(b + offs[1]);
+  P.comp_off = (const int32_t*)(b + offs[2]);
+  P.comp_len = (const int32_t*)(b + offs[3]);
+  P.op = (const int32_t*)(b + offs[4]);
+  P.arg = (const int32_t*)(b + offs[5]);
+  P.lit = (const int64_t*)(b + offs[6]);
+  P.names = b + offs[7];
+  d.P = P;
+  d.S = SkScratch{};
+  if (P.n_paths > SK_NARROW) {
+    const long long nw = (P.n_paths + 31) / 32;
+    const long long per_lane = (long long)P.n_paths * 24 + nw * 4;
+    long long lanes = ((256ll << 20) / per_lane) / 256 * 256;
+    lanes = std::max(256ll, std::min(lanes, 65536ll));
+    const size_t v = (size_t)lanes * P.n_paths * 8, w = (size_t)lanes * nw * 4, k = (size_t)lanes * P.n_paths * 4;
+    if (d.scratch.alloc(v + w + 2 * k + v + 64)) return 1;
+    char* q = d.scratch.as<char>();
+    d.S.val = (long long*)q;
+    d.S.ptr = (const uint8_t**)(q + v);
+    d.S.setw = (uint32_t*)(q + 2 * v);
+    d.S.kind = (int32_t*)(q + 2 * v + w);
+    d.S.scale = (int32_t*)(q + 2 * v + w + k);
+    d.S.lanes = lanes;
+  }
+  return 0;
+}
+static int install_part(DevPart& d, const dk_program& src) {
+  if (src.kind != DK_PROGRAM_PARTITION) return fail("not a partition-pruning program");
+  d.prog = src;
+  int64_t offs[8];
+  const std::string img = program_image(src, offs);
+  if (d.img.alloc(img.size())) return 1;
+  HIPOK(hipMemcpy(d.img.p, img.data(), img.size(), hipMemcpyHostToDevice));
+  const char* b = d.img.as<char>();
+  DPartProg P{};
+  P.n_fields = (int32_t)src.field_type.size();
+  P.n_ops = (int32_t)src.op.size();
+  P.field_type = (const int32_t*)(b + offs[0]);
+  P.name_off = (const int32_t*)(b + offs[1]);
+  P.name_len = (const int32_t*)(b + offs[2]);
+  P.op = (const int32_t*)(b + offs[4]);
+  P.arg = (const int32_t*)(b + offs[5]);
+  P.lit = (const int64_t*)(b + offs[6]);
+  P.pool = b + offs[7];
+  d.P = P;
+  return 0;
+}
+
 struct dk_replay {
   StreamH own;                          // the replay's stream (the checkpoint decode runs on it too)
   hipStream_t stream = nullptr;
@@ -3844,14 +3924,15 @@ struct dk_replay {
   DBuf d_cand, d_cand_n;      // probe candidates (rows needing the full key path)
   // data skipping (dk_replay_set_skipping): program + the tail's stats strings per action
   bool has_skip = false;
-  DSkipProg skip{};
-  DBuf d_skip, d_part;                  // device copies of the programs
+  DevSkip skip;                         // the program in device memory
+  DevPart part;
+  DBuf typed_buf;                       // TypedPath tables of the stats_parsed files
+  std::vector<int> typed_paths;
   DBuf d_tstats_chars, d_tstats_off, d_tstats_len;
   std::vector<StatsRows> ck_stats;      // per checkpoint file (n = 0: no stats column)
   std::vector<StatsParsedRows> ck_parsed;   // per checkpoint file: stats_parsed columns (n = 0: JSON)
   // partition pruning (dk_replay_set_partition_filter): program + partitionValues maps
   bool has_part = false;
-  DPartProg part{};
   MapRows tail_maps{};
   std::vector<MapRows> ck_maps;         // per checkpoint file (n = 0: no partitionValues leaves)
   std::vector<std::unique_ptr<DBuf>> map_bufs;
@@ -4176,94 +4257,47 @@ extern "C" int dk_replay_attach_checkpoint(dk_replay* r, dk_parquet* ckpt) {
 
 
 // validate a data-skipping program (layout dk_skip_program); `who` prefixes the error
-static int check_skip_program(const DSkipProg& P, const char* who) {
-  const std::string W = who;
-  if (P.n_paths < 0 || P.n_paths > SK_MAX_PATHS || P.n_ops <= 0 || P.n_ops > SK_MAX_OPS)
-    return fail(W + ": bad program size");
-  for (int p = 0; p < P.n_paths; p++) {
-    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DOUBLE)
-      return fail(W + ": bad stats path");
-    for (int d = 0; d < P.path_depth[p]; d++)
-      if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
-        return fail(W + ": bad stats path name");
-  }
-  int depth = 0;
-  bool fstat[SK_MAX_OPS + 1] = {false};       // stack slot holds a float / double stats value
-  bool nlit[SK_MAX_OPS + 1] = {false};        // stack slot holds a null literal
-  for (int k = 0; k < P.n_ops; k++) {
-    const int op = P.op[k];
-    if (op == OP_STAT) {
-      if (P.arg[k] < 0 || P.arg[k] >= P.n_paths) return fail(W + ": bad stat");
-      const int t = P.path_type[P.arg[k]];
-      fstat[depth] = t == SK_FLOAT || t == SK_DOUBLE;
-      nlit[depth] = false;
-      depth++;
-    }
-    else if (op == OP_FCMP) {                   // only on a float / double stat, threshold in names
-      const long long off = P.lit[k] & 0xffffffffll, len = P.lit[k] >> 32;
-      if (depth < 1 || !fstat[depth - 1]) return fail(W + ": FCMP needs a float stat");
-      // (the threshold text is followed by the comparison's rank run, two int64s)
-      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len + 16 > SK_NAMES) return fail(W + ": bad FCMP");
-      fstat[depth - 1] = false;
-      nlit[depth - 1] = false;
-    }
-    else if (op == OP_LIT) { fstat[depth] = false; nlit[depth] = P.arg[k] != 0; depth++; }
-    else if (op == OP_TIMEADD) { if (depth < 1) return fail(W + ": stack underflow"); }
-    else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
-      if (P.arg[k] < 0 || P.lit[k] < 0 || P.lit[k] + P.arg[k] > SK_NAMES) return fail(W + ": bad string literal");
-      fstat[depth] = false;
-      nlit[depth] = false;
-      depth++;
-    }
-    else if (op >= OP_LT && op <= OP_OR) {
-      if (depth < 2) return fail(W + ": stack underflow");
-      // a float stat compares only through FCMP, or with a null literal (the result is null)
-      if ((fstat[depth - 1] && !nlit[depth - 2]) || (fstat[depth - 2] && !nlit[depth - 1]))
-        return fail(W + ": a float stat compares only through FCMP");
-      depth--;
-      fstat[depth - 1] = false;
-      nlit[depth - 1] = false;
-    }
-    else return fail(W + ": bad opcode");
-    if (depth > 16) return fail(W + ": program too deep");
-  }
-  if (depth != 1) return fail(W + ": program must leave one value");
-  return 0;
-}
-
 // ---- Engine plugin point 1: JsonHandler.parseJson over stats strings, and the data-skipping
 // PredicateEvaluator over the parsed result (KA/engine/JsonHandler.java:68-71,
 // KA/engine/ExpressionHandler.java:58, as ScanImpl.applyDataSkipping drives them,
 // KA/internal/ScanImpl.java:304-352) ----
-struct dk_parsed_stats {
+struct dk_parsed {
   StreamH own;
   int device = 0;
   int64_t n = 0;
-  DSkipProg schema{};
-  DBuf d_chars, d_offs, d_isnull, d_sel, d_prog, d_vals, d_set, d_state, d_out;
+  dk_program schema;                       // one path per schema leaf, no ops
+  DevSkip prog;                            // the schema as a device program (extraction only)
+  DBuf d_chars, d_offs, d_isnull, d_sel, d_vals, d_set, d_state, d_out;
   bool dev_input = false;
   const uint8_t* chars = nullptr;          // device views of the input
   const int64_t* offs = nullptr;
+  std::vector<int64_t> h_offs;             // host copies of the input (for the typed columns)
+  std::vector<uint8_t> h_chars;
+  bool host_ready = false;
+  std::vector<int64_t> h_vals;             // [leaf][n]
+  std::vector<uint32_t> h_set;             // [word][n]
+  // the typed columns handed out (dk_parsed_column_get), per leaf
+  struct Col { std::vector<uint8_t> valid; std::vector<int64_t> values, hi; std::vector<int32_t> offs, scale;
+               std::vector<uint8_t> chars, wide; bool built = false; };
+  std::vector<Col> cols;
+  std::vector<std::string> path_json;
 };
 
-extern "C" int dk_json_parse_stats(dk_engine* e, const dk_skip_program* schema, int64_t n, const int64_t* offs,
-                                   const uint8_t* chars, const uint8_t* isnull, const uint8_t* selection,
-                                   int32_t on_device, dk_parsed_stats** out) {
-  if (!e || !schema || !out || n < 0 || (n && (!offs || !chars))) return fail("dk_json_parse_stats: bad arguments");
+namespace dk { int schema_program(const char* schema_json, dk_program* out); }
+
+extern "C" int dk_json_parse(dk_engine* e, const char* schema_json, int64_t n, const int64_t* offs,
+                             const uint8_t* chars, const uint8_t* isnull, const uint8_t* selection,
+                             int32_t on_device, dk_parsed** out) {
+  if (!e || !schema_json || !out || n < 0 || (n && (!offs || !chars))) return fail("dk_json_parse: bad arguments");
+  *out = nullptr;
   hipSetDevice(e->cfg.device);
-  std::unique_ptr<dk_parsed_stats> ps(new dk_parsed_stats());
+  std::unique_ptr<dk_parsed> ps(new dk_parsed());
   ps->device = e->cfg.device;
-  memcpy(&ps->schema, schema, sizeof ps->schema);
-  // the schema is a program's path table (its ops are not used here): names and types only
-  DSkipProg P = ps->schema;
-  if (P.n_paths < 1 || P.n_paths > SK_MAX_PATHS) return fail("dk_json_parse_stats: 1..8 stats paths");
-  for (int p = 0; p < P.n_paths; p++) {
-    if (P.path_depth[p] < 1 || P.path_depth[p] > SK_MAX_DEPTH || P.path_type[p] < SK_LONG || P.path_type[p] > SK_DOUBLE)
-      return fail("dk_json_parse_stats: bad stats path");
-    for (int d = 0; d < P.path_depth[p]; d++)
-      if (P.name_off[p][d] < 0 || P.name_len[p][d] < 0 || P.name_off[p][d] + P.name_len[p][d] > SK_NAMES)
-        return fail("dk_json_parse_stats: bad stats path name");
-  }
+  if (dk::schema_program(schema_json, &ps->schema)) return 1;
+  if (install_skip(ps->prog, ps->schema)) return 1;
+  const int np = (int)ps->schema.paths.size();
+  const int nw = (np + 31) / 32;
+  ps->cols.resize(np);
   if (ps->own.create()) return 1;
   hipStream_t s = ps->own.s;
   ps->n = n;
@@ -4271,100 +4305,268 @@ extern "C" int dk_json_parse_stats(dk_engine* e, const dk_skip_program* schema, 
   if (ps->dev_input) {
     ps->chars = chars; ps->offs = offs;
   } else {
-    const int64_t nchars = n ? offs[n] : 0;
-    if (upload(ps->d_chars, chars, (size_t)nchars + 16, s) || upload(ps->d_offs, offs, (size_t)(n + 1) * 8, s)) return 1;
+    const int64_t nchars = n ? offs[n] - offs[0] : 0;
+    ps->h_offs.assign(offs, offs + n + 1);
+    for (auto& o : ps->h_offs) o -= offs[0];
+    ps->h_chars.assign(nchars + 16, 0);
+    if (nchars) memcpy(ps->h_chars.data(), chars + offs[0], (size_t)nchars);
+    if (upload(ps->d_chars, ps->h_chars.data(), ps->h_chars.size(), s) ||
+        upload(ps->d_offs, ps->h_offs.data(), (size_t)(n + 1) * 8, s)) return 1;
     ps->chars = ps->d_chars.as<uint8_t>(); ps->offs = ps->d_offs.as<int64_t>();
   }
   const uint8_t* dnull = isnull;
   const uint8_t* dsel = selection;
-  if (!ps->dev_input) {
-    if (isnull) { if (upload(ps->d_isnull, isnull, (size_t)n + 16, s)) return 1; dnull = ps->d_isnull.as<uint8_t>(); }
-    if (selection) { if (upload(ps->d_sel, selection, (size_t)n + 16, s)) return 1; dsel = ps->d_sel.as<uint8_t>(); }
+  if (!ps->dev_input) {                    // exactly n bytes each (the caller's arrays are not padded)
+    if (isnull) { if (upload(ps->d_isnull, isnull, (size_t)n, s)) return 1; dnull = ps->d_isnull.as<uint8_t>(); }
+    if (selection) { if (upload(ps->d_sel, selection, (size_t)n, s)) return 1; dsel = ps->d_sel.as<uint8_t>(); }
   }
-  if (upload(ps->d_prog, &ps->schema, sizeof(DSkipProg), s)) return 1;
-  if (ps->d_vals.alloc((size_t)P.n_paths * n * 8 + 64) || ps->d_set.alloc((size_t)n * 4 + 64) ||
+  if (ps->d_vals.alloc((size_t)std::max(np, 1) * n * 8 + 64) || ps->d_set.alloc((size_t)std::max(nw, 1) * n * 4 + 64) ||
       ps->d_state.alloc(sizeof(DState)))
     return 1;
   DState st0{};
   st0.err_row = LLONG_MAX;
   HIPOK(hipMemcpyAsync(ps->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
-  launch_json_parse_stats(ps->chars, ps->offs, dnull, dsel, n, ps->d_prog.as<DSkipProg>(), ps->d_vals.as<long long>(),
+  launch_json_parse_stats(ps->chars, ps->offs, dnull, dsel, n, ps->prog.P, ps->prog.S, ps->d_vals.as<long long>(),
                           ps->d_set.as<uint32_t>(), ps->d_state.as<DState>(), s);
   HIPOK(hipStreamSynchronize(s));
   DState h{};
   HIPOK(hipMemcpy(&h, ps->d_state.p, sizeof h, hipMemcpyDeviceToHost));
   if (h.err_flags & E_STATS)
     return fail("Parsing the JSON statistics: couldn't decode the stats of row " + std::to_string(h.err_row));
+  for (auto& p : ps->schema.paths) {
+    std::string j = "[";
+    for (size_t k = 0; k < p.size(); k++) {
+      j += k ? ",\"" : "\"";
+      for (unsigned char c : p[k]) {
+        if (c == '"' || c == '\\') { j += '\\'; j += (char)c; }
+        else if (c < 0x20) { char b[8]; snprintf(b, sizeof b, "\\u%04x", c); j += b; }
+        else j += (char)c;
+      }
+      j += "\"";
+    }
+    ps->path_json.push_back(j + "]");
+  }
   *out = ps.release();
   return 0;
 }
 
-// path p of the parsed stats on the host: present[r] (0 = null) and values[r] -- long / integer /
-// short / byte / date (epoch days) / timestamp(_ntz) (micros): the value; string / decimal / float /
-// double: the token's span in row r's string (offset | length << 32, bit 62 = JSON escapes or, for a
-// float / double, a special-value code NaN 1 / +Inf 2 / -Inf 3 in the low bits)
-extern "C" int dk_parsed_stats_column(dk_parsed_stats* ps, int32_t path, int64_t* values, uint8_t* present) {
-  if (!ps || path < 0 || path >= ps->schema.n_paths) return fail("dk_parsed_stats_column: bad path");
+extern "C" int32_t dk_parsed_num_leaves(const dk_parsed* ps) { return ps ? (int32_t)ps->schema.paths.size() : -1; }
+
+extern "C" int64_t dk_parsed_leaf_path(const dk_parsed* ps, int32_t leaf, char* buf, int64_t cap) {
+  if (!ps || leaf < 0 || leaf >= (int32_t)ps->path_json.size()) return -1;
+  const std::string& j = ps->path_json[leaf];
+  if (buf && cap > 0) {
+    const int64_t m = std::min<int64_t>((int64_t)j.size(), cap - 1);
+    memcpy(buf, j.data(), (size_t)m);
+    buf[m] = 0;
+  }
+  return (int64_t)j.size();
+}
+
+// JSON string body s[a, b) (escapes decoded as Jackson does; a lone surrogate becomes '?', as
+// String.getBytes(UTF_8) writes it) appended as UTF-8
+static void json_unescape(const uint8_t* s, int64_t a, int64_t b, std::vector<uint8_t>& o) {
+  auto put = [&](uint32_t cp) {
+    if (cp >= 0xD800 && cp <= 0xDFFF) { o.push_back('?'); return; }
+    if (cp < 0x80) o.push_back((uint8_t)cp);
+    else if (cp < 0x800) { o.push_back(0xC0 | (cp >> 6)); o.push_back(0x80 | (cp & 63)); }
+    else if (cp < 0x10000) { o.push_back(0xE0 | (cp >> 12)); o.push_back(0x80 | ((cp >> 6) & 63)); o.push_back(0x80 | (cp & 63)); }
+    else { o.push_back(0xF0 | (cp >> 18)); o.push_back(0x80 | ((cp >> 12) & 63)); o.push_back(0x80 | ((cp >> 6) & 63)); o.push_back(0x80 | (cp & 63)); }
+  };
+  auto hex4 = [&](int64_t i, uint32_t* v) {
+    if (i + 4 > b) return false;
+    uint32_t x = 0;
+    for (int k = 0; k < 4; k++) {
+      const uint8_t c = s[i + k];
+      x <<= 4;
+      if (c >= '0' && c <= '9') x |= c - '0'; else if ((c | 0x20) >= 'a' && (c | 0x20) <= 'f') x |= (c | 0x20) - 'a' + 10; else return false;
+    }
+    *v = x;
+    return true;
+  };
+  for (int64_t i = a; i < b;) {
+    if (s[i] != '\\') { o.push_back(s[i++]); continue; }
+    const uint8_t c = s[i + 1];
+    i += 2;
+    if (c == 'u') {
+      uint32_t cp = 0;
+      hex4(i, &cp);
+      i += 4;
+      if (cp >= 0xD800 && cp <= 0xDBFF && i + 6 <= b && s[i] == '\\' && s[i + 1] == 'u') {
+        uint32_t lo;
+        if (hex4(i + 2, &lo) && lo >= 0xDC00 && lo <= 0xDFFF) { cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00); i += 6; }
+      }
+      put(cp);
+    } else {
+      o.push_back(c == 'b' ? '\b' : c == 'f' ? '\f' : c == 'n' ? '\n' : c == 'r' ? '\r' : c == 't' ? '\t' : c);
+    }
+  }
+}
+
+// The typed column of one leaf (host memory, valid until dk_parsed_free), as DefaultJsonRow decodes
+// it (KD/internal/data/DefaultJsonRow.java:136-357): integral / date (epoch days) / timestamp(_ntz)
+// (micros) values; strings after JSON unescaping (int32 offsets + chars); decimals as the BigDecimal
+// of the number token (unscaled 128-bit value + scale, and the token text); float / double as the
+// IEEE bits of DecimalNode.floatValue / doubleValue (correctly rounded; "-0.0" is +0.0, as BigDecimal
+// has no negative zero; NaN / +-Infinity from their string forms).
+extern "C" int dk_parsed_column_get(dk_parsed* ps, int32_t leaf, dk_parsed_column* out) {
+  if (!ps || !out || leaf < 0 || leaf >= (int32_t)ps->schema.paths.size()) return fail("dk_parsed_column_get: bad leaf");
   hipSetDevice(ps->device);
   const int64_t n = ps->n;
-  if (!n) return 0;
-  std::vector<uint32_t> set(n);
-  HIPOK(hipMemcpy(set.data(), ps->d_set.p, n * 4, hipMemcpyDeviceToHost));
-  if (values) HIPOK(hipMemcpy(values, ps->d_vals.as<int64_t>() + (int64_t)path * n, n * 8, hipMemcpyDeviceToHost));
-  if (present) for (int64_t r = 0; r < n; r++) present[r] = (set[r] >> path) & 1;
+  const int np = (int)ps->schema.paths.size();
+  const int nw = (np + 31) / 32;
+  if (!ps->host_ready) {
+    ps->h_vals.resize((size_t)np * n);
+    ps->h_set.resize((size_t)nw * n);
+    if (n) {
+      HIPOK(hipMemcpy(ps->h_vals.data(), ps->d_vals.p, (size_t)np * n * 8, hipMemcpyDeviceToHost));
+      HIPOK(hipMemcpy(ps->h_set.data(), ps->d_set.p, (size_t)nw * n * 4, hipMemcpyDeviceToHost));
+    }
+    if (ps->dev_input && n) {               // the rows' strings, for the spans
+      ps->h_offs.resize(n + 1);
+      HIPOK(hipMemcpy(ps->h_offs.data(), ps->offs, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost));
+      const int64_t base = ps->h_offs[0];
+      ps->h_chars.assign(ps->h_offs[n] - base + 16, 0);
+      HIPOK(hipMemcpy(ps->h_chars.data(), ps->chars + base, (size_t)(ps->h_offs[n] - base), hipMemcpyDeviceToHost));
+      for (auto& o : ps->h_offs) o -= base;
+    }
+    ps->host_ready = true;
+  }
+  dk_parsed::Col& C = ps->cols[leaf];
+  const int t = ps->schema.path_type[leaf];
+  if (!C.built) {
+    C.valid.assign(n, 0);
+    C.values.assign(n, 0);
+    const bool strings = t == SK_STRING || t == SK_DECIMAL;
+    if (strings) C.offs.assign(n + 1, 0);
+    if (t == SK_DECIMAL) { C.hi.assign(n, 0); C.scale.assign(n, 0); C.wide.assign(n, 0); }
+    for (int64_t r = 0; r < n; r++) {
+      const bool present = (ps->h_set[(size_t)(leaf >> 5) * n + r] >> (leaf & 31)) & 1;
+      C.valid[r] = present;
+      const int64_t v = ps->h_vals[(size_t)leaf * n + r];
+      const uint8_t* row = ps->h_chars.data() + (n ? ps->h_offs[r] : 0);
+      if (present) {
+        if (t == SK_STRING) {
+          const int64_t a = v & 0x7fffffff, len = (v >> 32) & 0x3fffffff;
+          if ((v >> 62) & 1) json_unescape(row, a, a + len, C.chars);
+          else C.chars.insert(C.chars.end(), row + a, row + a + len);
+        } else if (t == SK_DECIMAL) {
+          const int64_t a = v & 0x7fffffff, len = v >> 32;
+          C.chars.insert(C.chars.end(), row + a, row + a + len);
+          // new BigDecimal(token): unscaled = the mantissa digits, scale = fraction digits - exponent
+          unsigned __int128 u = 0;
+          const unsigned __int128 lim = ((unsigned __int128)1 << 127) / 10;
+          bool neg = false, wide = false;
+          int64_t i = a, frac = 0, exp = 0;
+          bool dot = false;
+          if (row[i] == '-') { neg = true; i++; }
+          for (; i < a + len && row[i] != 'e' && row[i] != 'E'; i++) {
+            if (row[i] == '.') { dot = true; continue; }
+            if (u > lim) wide = true;
+            u = u * 10 + (row[i] - '0');
+            if (dot) frac++;
+          }
+          if (i < a + len) exp = strtoll(std::string((const char*)row + i + 1, (size_t)(a + len - i - 1)).c_str(), nullptr, 10);
+          const __int128 sv = neg ? -(__int128)u : (__int128)u;
+          C.values[r] = (int64_t)(uint64_t)sv;
+          C.hi[r] = (int64_t)(sv >> 64);
+          C.scale[r] = (int32_t)(frac - exp);
+          C.wide[r] = wide;
+        } else if (t == SK_FLOAT || t == SK_DOUBLE) {
+          uint64_t bits;
+          if ((v >> 62) & 1) {                    // NaN / +Infinity / -Infinity
+            const int code = (int)(v & 3);
+            bits = t == SK_FLOAT ? (code == 1 ? 0x7fc00000ull : code == 2 ? 0x7f800000ull : 0xff800000ull)
+                                 : (code == 1 ? 0x7ff8000000000000ull : code == 2 ? 0x7ff0000000000000ull : 0xfff0000000000000ull);
+          } else {
+            const int64_t a = v & 0x7fffffff, len = v >> 32;
+            const std::string tok((const char*)row + a, (size_t)len);
+            bool zero = true;                       // an exact zero (BigDecimal: no sign) -> +0.0
+            for (size_t k = 0; k < tok.size() && tok[k] != 'e' && tok[k] != 'E'; k++) zero = zero && !(tok[k] >= '1' && tok[k] <= '9');
+            if (t == SK_FLOAT) { float f = zero ? 0.0f : strtof(tok.c_str(), nullptr); uint32_t b; memcpy(&b, &f, 4); bits = b; }
+            else { double d = zero ? 0.0 : strtod(tok.c_str(), nullptr); memcpy(&bits, &d, 8); }
+          }
+          C.values[r] = (int64_t)bits;
+        } else {
+          C.values[r] = v;
+        }
+      }
+      if (strings) C.offs[r + 1] = (int32_t)C.chars.size();
+    }
+    if (C.chars.size() > (size_t)INT32_MAX) return fail("dk_parsed_column_get: strings exceed 2 GiB");
+    C.chars.push_back(0);
+    C.built = true;
+  }
+  memset(out, 0, sizeof *out);
+  out->type = t;
+  out->n = n;
+  out->validity = C.valid.data();
+  out->values = C.values.data();
+  if (t == SK_STRING || t == SK_DECIMAL) { out->offs = C.offs.data(); out->chars = C.chars.data(); }
+  if (t == SK_DECIMAL) { out->values_hi = C.hi.data(); out->scale = C.scale.data(); out->wide = C.wide.data(); }
   return 0;
 }
 
-// PredicateEvaluator.eval(parsed stats, selection) for COALESCE(prog, true): prog's stats paths must
-// be the parsed schema's (same order, names and types); selection is updated in place (host memory,
-// or device memory when the stats were parsed from device input)
-extern "C" int dk_parsed_stats_eval(dk_parsed_stats* ps, const dk_skip_program* prog, uint8_t* selection) {
-  if (!ps || !prog || (ps->n && !selection)) return fail("dk_parsed_stats_eval: bad arguments");
-  DSkipProg P;
-  memcpy(&P, prog, sizeof P);
-  if (check_skip_program(P, "dk_parsed_stats_eval")) return 1;
-  const DSkipProg& S = ps->schema;
-  bool same = P.n_paths == S.n_paths;
-  for (int p = 0; same && p < P.n_paths; p++) {
-    same = P.path_type[p] == S.path_type[p] && P.path_depth[p] == S.path_depth[p];
-    for (int d = 0; same && d < P.path_depth[p]; d++)
-      same = P.name_len[p][d] == S.name_len[p][d] &&
-             !memcmp(P.names + P.name_off[p][d], S.names + S.name_off[p][d], P.name_len[p][d]);
+// PredicateEvaluator.eval(parsed stats, selection) for COALESCE(prog, true): every stats path of the
+// program must be a leaf of the parsed schema with the same type (the program is re-indexed onto the
+// schema's leaves); selection is updated in place (host memory, or device memory when the stats were
+// parsed from device input)
+extern "C" int dk_parsed_eval(dk_parsed* ps, const dk_program* prog, uint8_t* selection) {
+  if (!ps || !prog || (ps->n && !selection)) return fail("dk_parsed_eval: bad arguments");
+  if (prog->kind != DK_PROGRAM_SKIPPING) return fail("dk_parsed_eval: not a data-skipping program");
+  dk_program P = ps->schema;               // the schema's path table, the program's ops re-indexed
+  std::vector<int32_t> map(prog->paths.size(), -1);
+  for (size_t i = 0; i < prog->paths.size(); i++) {
+    for (size_t j = 0; j < ps->schema.paths.size(); j++)
+      if (ps->schema.paths[j] == prog->paths[i]) { map[i] = (int32_t)j; break; }
+    if (map[i] < 0 || ps->schema.path_type[map[i]] != prog->path_type[i])
+      return fail("dk_parsed_eval: the predicate's stats paths are not in the parsed schema");
   }
-  if (!same) return fail("dk_parsed_stats_eval: the predicate's stats paths are not the parsed schema's");
+  // the program's pool starts with its own path names: literal offsets move by the size difference
+  int64_t names0 = 0;
+  for (auto& p : prog->paths) for (auto& c : p) names0 += (int64_t)c.size();
+  const int64_t base = (int64_t)P.pool.size();
+  P.pool += prog->pool.substr((size_t)names0);
+  P.op = prog->op; P.arg = prog->arg; P.lit = prog->lit;
+  for (size_t k = 0; k < P.op.size(); k++) {
+    const int op = P.op[k];
+    if (op == OP_STAT) P.arg[k] = map[P.arg[k]];
+    else if (op == OP_LIT_STR || op == OP_LIT_DEC) P.lit[k] += base - names0;
+    else if (op == OP_FCMP) P.lit[k] += base - names0;        // offset in the low 32 bits
+  }
+  P.stack = prog->stack;
   hipSetDevice(ps->device);
   hipStream_t s = ps->own.s;
   if (!ps->n) return 0;
-  if (upload(ps->d_prog, &P, sizeof P, s)) return 1;
+  DevSkip d;
+  if (install_skip(d, P)) return 1;
   uint8_t* dsel = selection;
   if (!ps->dev_input) {
     if (upload(ps->d_out, selection, (size_t)ps->n, s)) return 1;
     dsel = ps->d_out.as<uint8_t>();
   }
-  launch_parsed_eval(ps->chars, ps->offs, ps->n, ps->d_prog.as<DSkipProg>(), ps->d_vals.as<long long>(),
-                     ps->d_set.as<uint32_t>(), dsel, s);
+  launch_parsed_eval(ps->chars, ps->offs, ps->n, d.P, ps->d_vals.as<long long>(), ps->d_set.as<uint32_t>(), dsel, s);
   if (!ps->dev_input) HIPOK(hipMemcpyAsync(selection, dsel, (size_t)ps->n, hipMemcpyDeviceToHost, s));
   HIPOK(hipStreamSynchronize(s));
   return 0;
 }
 
-extern "C" void dk_parsed_stats_free(dk_parsed_stats* ps) {
+extern "C" void dk_parsed_free(dk_parsed* ps) {
   if (!ps) return;
   hipSetDevice(ps->device);
   hipStreamSynchronize(ps->own.s);
   delete ps;
 }
 
-extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog) {
-  static_assert(sizeof(dk_skip_program) == sizeof(DSkipProg), "dk_skip_program layout");
+extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_program* prog) {
   if (!r) return fail("null replay");
   if (!prog) { r->has_skip = false; return 0; }
-  DSkipProg P;
-  memcpy(&P, prog, sizeof P);
-  if (check_skip_program(P, "dk_replay_set_skipping")) return 1;
+  if (prog->kind != DK_PROGRAM_SKIPPING) return fail("dk_replay_set_skipping: not a data-skipping program");
   if (!r->tail || !r->tail->with_stats) return fail("dk_replay_set_skipping: the commit tail was parsed without stats");
   if (r->lazy && attach_upto(r, INT_MAX)) return 1;   // the typed stats columns of every file
-  r->skip = P;
+  if (install_skip(r->skip, *prog)) return 1;
+  const dk_program& P = r->skip.prog;
+  const int np = (int)P.paths.size();
   // add.stats_parsed fast path, per checkpoint file: every program path's typed leaf
   // add.stats_parsed.<path> was projected and decoded with a physical / logical type that holds the
   // stat's Kernel type (long: INT64; int / short / byte / date: INT32; timestamp(_ntz): INT64 micros /
@@ -4372,17 +4574,21 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
   // DOUBLE), and the file's add.stats JSON column is there for the rows the typed values cannot
   // stand for (k_stats_parsed)
   r->ck_parsed.assign(r->ck ? r->ck->files.size() : 0, StatsParsedRows{});
+  r->typed_paths.clear();
   static const bool no_parsed = getenv("DK_NO_STATS_PARSED") && atoi(getenv("DK_NO_STATS_PARSED"));
+  std::vector<TypedPath> all;
+  std::vector<size_t> at(r->ck_parsed.size(), SIZE_MAX);
   for (size_t fi = 0; fi < r->ck_parsed.size() && !no_parsed; fi++) {
     StatsParsedRows R{};
-    R.n_paths = P.n_paths;
+    R.n_paths = np;
     R.struct_def = 2;                     // add (1) . stats_parsed (2)
     R.js = fi < r->ck_stats.size() ? r->ck_stats[fi] : StatsRows{};
-    bool ok = P.n_paths > 0 && R.js.n > 0 && R.js.offs;
-    for (int q = 0; q < P.n_paths && ok; q++) {
+    bool ok = np > 0 && R.js.n > 0 && R.js.offs;
+    std::vector<TypedPath> tp(np);
+    for (int q = 0; q < np && ok; q++) {
       const int t = P.path_type[q];
       std::string leaf = "add.stats_parsed";
-      for (int d = 0; d < P.path_depth[q]; d++) leaf += "." + std::string(P.names + P.name_off[q][d], P.name_len[q][d]);
+      for (auto& c : P.paths[q]) leaf += "." + c;
       const DColumn* c = find_col(r->ck, (int)fi, leaf.c_str());
       const LeafM* L = find_leafm(r->ck, (int)fi, leaf.c_str());
       ok = c && L && c->present && !c->max_rep && c->max_def >= 3;
@@ -4405,79 +4611,35 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog)
       }
       ok = kind >= 0 && (kind == TP_STR ? (c->null_only || c->offs) : (c->null_only || c->fixed));
       if (!ok) break;
-      R.kind[q] = kind; R.scale[q] = kind == TP_DEC ? L->dec_scale : 0;
-      R.def[q] = c->row_def; R.max_def[q] = c->max_def;
-      R.vals[q] = c->null_only || kind == TP_STR ? nullptr : c->fixed; R.width[q] = c->width;
-      R.offs[q] = kind == TP_STR && !c->null_only ? c->offs : nullptr;
-      R.chars[q] = kind == TP_STR && !c->null_only ? c->chars : nullptr;
-      if (c->null_only) R.max_def[q] = 1 << 30;          // no value anywhere: always null
+      TypedPath& T = tp[q];
+      T.kind = kind; T.scale = kind == TP_DEC ? L->dec_scale : 0;
+      T.def = c->row_def; T.max_def = c->max_def;
+      T.vals = c->null_only || kind == TP_STR ? nullptr : c->fixed; T.width = c->width;
+      T.offs = kind == TP_STR && !c->null_only ? c->offs : nullptr;
+      T.chars = kind == TP_STR && !c->null_only ? c->chars : nullptr;
+      if (c->null_only) T.max_def = 1 << 30;          // no value anywhere: always null
     }
-    if (ok) { R.n = r->ck->files[fi].num_rows; r->ck_parsed[fi] = R; }
+    if (ok) {
+      R.n = r->ck->files[fi].num_rows;
+      r->ck_parsed[fi] = R;
+      at[fi] = all.size();
+      all.insert(all.end(), tp.begin(), tp.end());
+    }
   }
-  if (!r->d_skip.p && r->d_skip.alloc(sizeof(DSkipProg))) return -1;
-  if (hipMemcpy(r->d_skip.p, &r->skip, sizeof(DSkipProg), hipMemcpyHostToDevice) != hipSuccess)
-    return fail("dk_replay_set_skipping: copy failed");
+  if (!all.empty()) {                      // every file's TypedPath table in one device buffer
+    if (r->typed_buf.alloc(all.size() * sizeof(TypedPath))) return 1;
+    HIPOK(hipMemcpy(r->typed_buf.p, all.data(), all.size() * sizeof(TypedPath), hipMemcpyHostToDevice));
+    for (size_t fi = 0; fi < at.size(); fi++)
+      if (at[fi] != SIZE_MAX) r->ck_parsed[fi].paths = r->typed_buf.as<TypedPath>() + at[fi];
+  }
   r->has_skip = true;
   return 0;
 }
 
-extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_part_program* prog) {
-  static_assert(sizeof(dk_part_program) == sizeof(DPartProg), "dk_part_program layout");
+extern "C" int dk_replay_set_partition_filter(dk_replay* r, const dk_program* prog) {
   if (!r) return fail("null replay");
   if (!prog) { r->has_part = false; return 0; }
-  DPartProg P;
-  memcpy(&P, prog, sizeof P);
-  if (P.n_fields < 0 || P.n_fields > PP_MAX_FIELDS || P.n_ops <= 0 || P.n_ops > PP_MAX_OPS)
-    return fail("dk_replay_set_partition_filter: bad program size");
-  for (int f = 0; f < P.n_fields; f++)
-    if (P.field_type[f] < PT_LONG || P.field_type[f] > PT_TIMESTAMP || P.name_off[f] < 0 || P.name_len[f] < 0 ||
-        P.name_off[f] + P.name_len[f] > PP_POOL)
-      return fail("dk_replay_set_partition_filter: bad field");
-  int depth = 0;
-  bool ffield[PP_MAX_OPS + 1] = {false};      // stack slot holds a float / double field
-  bool pnull[PP_MAX_OPS + 1] = {false};       // stack slot holds a null literal
-  for (int k = 0; k < P.n_ops; k++) {
-    const int op = P.op[k];
-    if (op == PO_FIELD) {
-      if (P.arg[k] < 0 || P.arg[k] >= P.n_fields) return fail("dk_replay_set_partition_filter: bad field ref");
-      ffield[depth] = P.field_type[P.arg[k]] == PT_F32 || P.field_type[P.arg[k]] == PT_F64;
-      pnull[depth] = false;
-      depth++;
-    }
-    else if (op == PO_LIT_INT || op == PO_LIT_NULL) { ffield[depth] = false; pnull[depth] = op == PO_LIT_NULL; depth++; }
-    else if (op == PO_LIT_STR || op == PO_LIT_DEC) {
-      if (P.lit[k] < 0 || P.arg[k] < 0 || P.lit[k] + P.arg[k] > PP_POOL) return fail("dk_replay_set_partition_filter: bad literal");
-      ffield[depth] = false;
-      pnull[depth] = false;
-      depth++;
-    } else if (op == PO_FCMP) {
-      const long long off = P.lit[k] & 0xffffffffll, len = P.lit[k] >> 32;
-      if (depth < 1 || !ffield[depth - 1]) return fail("dk_replay_set_partition_filter: FCMP needs a float field");
-      if ((P.arg[k] & 15) > FC_NONE || len < 0 || off + len > PP_POOL) return fail("dk_replay_set_partition_filter: bad FCMP");
-      ffield[depth - 1] = false;
-      pnull[depth - 1] = false;
-    } else if ((op >= PO_LT && op <= PO_NSEQ) || op == PO_AND || op == PO_OR) {
-      if (depth < 2) return fail("dk_replay_set_partition_filter: stack underflow");
-      if ((op >= PO_LT && op <= PO_NSEQ) &&
-          ((ffield[depth - 1] && !pnull[depth - 2]) || (ffield[depth - 2] && !pnull[depth - 1])))
-        return fail("dk_replay_set_partition_filter: a float field compares only through FCMP");
-      depth--;
-      ffield[depth - 1] = false;
-      pnull[depth - 1] = false;
-    } else if (op == PO_ISNULL || op == PO_ISNOTNULL || op == PO_NOT) {
-      if (depth < 1) return fail("dk_replay_set_partition_filter: stack underflow");
-      ffield[depth - 1] = false;
-      pnull[depth - 1] = false;
-    } else {
-      return fail("dk_replay_set_partition_filter: bad opcode");
-    }
-    if (depth > 16) return fail("dk_replay_set_partition_filter: program too deep");
-  }
-  if (depth != 1) return fail("dk_replay_set_partition_filter: program must leave one value");
-  r->part = P;
-  if (!r->d_part.p && r->d_part.alloc(sizeof(DPartProg))) return -1;
-  if (hipMemcpy(r->d_part.p, &r->part, sizeof(DPartProg), hipMemcpyHostToDevice) != hipSuccess)
-    return fail("dk_replay_set_partition_filter: copy failed");
+  if (install_part(r->part, *prog)) return 1;
   r->has_part = true;
   return 0;
 }
@@ -4511,14 +4673,14 @@ static int replay_launch(dk_replay* r) {
   { KTimer::Scope sc(&T, 10, s); launch_json_select(A, na, S, r->mask, r->d_canon.as<uint8_t>(), r->d_jsel.as<uint8_t>(), st, s); }
   if (r->has_part && na) {                 // partition pruning on the tail's adds (before skipping)
     KTimer::Scope sc(&T, 18, s);
-    launch_part_eval(r->tail_maps, r->d_part.as<DPartProg>(), r->d_jsel.as<uint8_t>(), st, s);
+    launch_part_eval(r->tail_maps, r->part.P, r->d_jsel.as<uint8_t>(), st, s);
   }
   if (r->has_skip && na) {                 // data skipping on the tail's selected adds
     KTimer::Scope sc(&T, 17, s);
     StatsRows R{};
     R.n = na; R.soff = r->d_tstats_off.as<int64_t>(); R.slen = r->d_tstats_len.as<int32_t>();
     R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
-    launch_stats_eval(R, r->d_skip.as<DSkipProg>(), r->d_jsel.as<uint8_t>(), st, s);
+    launch_stats_eval(R, r->skip.P, r->skip.S, r->d_jsel.as<uint8_t>(), st, s);
   }
   if (r->n_groups > 0 && r->xw == 0 && r->ck) {
     const int ng = std::max(1, std::min(r->n_groups, (int)r->ck->files.size()));
@@ -4602,14 +4764,14 @@ static void replay_file_filters(dk_replay* r, size_t fi) {
   DState* st = r->d_state.as<DState>();
   if (r->has_part && fi < r->ck_maps.size()) {
     KTimer::Scope sc(&T, 18, s);
-    launch_part_eval(r->ck_maps[fi], r->d_part.as<DPartProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+    launch_part_eval(r->ck_maps[fi], r->part.P, r->d_csel[fi]->as<uint8_t>(), st, s);
   }
   if (r->has_skip && fi < r->ck_stats.size()) {
     KTimer::Scope sc(&T, 17, s);
     if (fi < r->ck_parsed.size() && r->ck_parsed[fi].n > 0)
-      launch_stats_parsed(r->ck_parsed[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+      launch_stats_parsed(r->ck_parsed[fi], r->skip.P, r->skip.S, r->d_csel[fi]->as<uint8_t>(), st, s);
     else
-      launch_stats_eval(r->ck_stats[fi], r->d_skip.as<DSkipProg>(), r->d_csel[fi]->as<uint8_t>(), st, s);
+      launch_stats_eval(r->ck_stats[fi], r->skip.P, r->skip.S, r->d_csel[fi]->as<uint8_t>(), st, s);
   }
 }
 
@@ -5125,14 +5287,14 @@ extern "C" int dk_replay_owner_tail_finish(dk_replay* r, const uint8_t* back) {
   DState* st = r->d_state.as<DState>();
   if (r->has_part && na) {                 // partition pruning on this rank's tail adds (before skipping)
     KTimer::Scope sc(&r->timer, 18, s);
-    launch_part_eval(r->tail_maps, r->d_part.as<DPartProg>(), r->d_jsel.as<uint8_t>(), st, s);
+    launch_part_eval(r->tail_maps, r->part.P, r->d_jsel.as<uint8_t>(), st, s);
   }
   if (r->has_skip && na) {                 // data skipping on this rank's selected tail adds
     KTimer::Scope sc(&r->timer, 17, s);
     StatsRows R{};
     R.n = (int64_t)na; R.soff = r->d_tstats_off.as<int64_t>(); R.slen = r->d_tstats_len.as<int32_t>();
     R.chars = r->d_tstats_chars.as<uint8_t>(); R.row_tag = -1000000000000ll;
-    launch_stats_eval(R, r->d_skip.as<DSkipProg>(), r->d_jsel.as<uint8_t>(), st, s);
+    launch_stats_eval(R, r->skip.P, r->skip.S, r->d_jsel.as<uint8_t>(), st, s);
   }
   r->ophase = OP_TAIL_DONE;
   return 0;

@@ -2385,7 +2385,7 @@ __device__ __forceinline__ void set_err(DState* st, int flag, long long row, int
 // with Kleene logic (DefaultExpressionEvaluator.visitAnd/visitOr, :384-436; comparators are null if
 // either side is null) and the row stays selected iff COALESCE(result, true).
 // --------------------------------------------------------------------------------------------
-constexpr int JS_MAXD = 16;
+constexpr int JS_MAXD = 64;            // JSON nesting levels a stats object may have
 
 __device__ __forceinline__ bool js_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
 __device__ __forceinline__ bool js_hex(uint8_t c) {
@@ -2816,21 +2816,42 @@ __device__ int fp_special(const uint8_t* s, int32_t a, int32_t b, bool esc) {
   return 0;
 }
 
-// extract the program's stats fields from one JSON object; returns false on a decode error
-__device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long long* val, uint32_t* set) {
+// The stats values of the row a lane evaluates: path p's value / typed kind / scale / pointer at index
+// p * stride and its set bit in word (p >> 5) * stride -- registers for narrow programs, the lane's
+// column of the SkScratch arrays for wide ones (any number of paths).
+struct SkSlots {
+  long long* val;
+  uint32_t* setw;
+  int32_t* kind;
+  int32_t* scale;
+  const uint8_t** ptr;
+  long long stride;
+  __device__ __forceinline__ bool has(int p) const { return (setw[(long long)(p >> 5) * stride] >> (p & 31)) & 1; }
+};
+
+// One pass over a JSON object extracting the program paths [w0, w0 + np) (np <= 32): values into
+// V.val, the paths found into *found. Returns false on a decode error (DefaultJsonRow's rules).
+__device__ bool js_extract_window(const uint8_t* s, int32_t n, const DSkipProg& P, int w0, int np, SkSlots V,
+                                  uint32_t* found) {
   uint32_t mstack[JS_MAXD];
-  uint8_t is_obj[JS_MAXD];
-  uint32_t leafmask[SK_MAX_DEPTH + 2];
-  for (int d = 0; d < SK_MAX_DEPTH + 2; d++) leafmask[d] = 0;
+  unsigned long long is_obj = 0;                     // bit d: nesting level d is an object
+  uint32_t leafmask[JS_MAXD];
+  const int maxc = P.max_comps < JS_MAXD - 1 ? P.max_comps : JS_MAXD - 1;
+  for (int d = 0; d <= maxc; d++) leafmask[d] = 0;
   uint32_t all = 0;
-  for (int p = 0; p < P.n_paths; p++) { leafmask[P.path_depth[p]] |= 1u << p; all |= 1u << p; }
-  *set = 0;
+  for (int q = 0; q < np; q++) {
+    const int p = w0 + q;
+    const int nc = P.path_comp[p + 1] - P.path_comp[p];
+    if (nc >= 1 && nc <= maxc) leafmask[nc] |= 1u << q;
+    all |= 1u << q;
+  }
+  uint32_t set = 0;
   int32_t i = 0;
   while (i < n && js_ws(s[i])) i++;
   if (i >= n || s[i] != '{') return false;          // the stats row must be an object (struct)
   i++;
   int depth = 1;
-  is_obj[1] = 1;
+  is_obj |= 2ull;
   mstack[1] = all;
   // states: 0 = key or '}' (after '{'), 1 = key (after ','), 2 = value, 3 = after value, 4 = value or ']'
   int state = 0;
@@ -2846,12 +2867,12 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
       const int32_t e = js_skip_string(s, n, i, &esc);
       if (e < 0) return false;
       m = 0;
-      const uint32_t cand = depth <= SK_MAX_DEPTH ? mstack[depth] : 0;
-      for (int p = 0; p < P.n_paths; p++)
-        if ((cand >> p) & 1) {
-          if (js_key_eq(s, i + 1, e - 1, esc, P.names + P.name_off[p][depth - 1], P.name_len[p][depth - 1]))
-            m |= 1u << p;
-        }
+      const uint32_t cand = depth <= maxc ? mstack[depth] : 0;
+      for (uint32_t cm = cand; cm; cm &= cm - 1) {
+        const int q = __builtin_ctz(cm);
+        const int ci = P.path_comp[w0 + q] + depth - 1;
+        if (js_key_eq(s, i + 1, e - 1, esc, P.names + P.comp_off[ci], P.comp_len[ci])) m |= 1u << q;
+      }
       i = e;
       while (i < n && js_ws(s[i])) i++;
       if (i >= n || s[i] != ':') return false;
@@ -2861,15 +2882,15 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
     }
     if (state == 2 || state == 4) {
       if (state == 4 && c == ']') { state = 3; goto close; }
-      const uint32_t leaf = depth <= SK_MAX_DEPTH ? (m & leafmask[depth]) : 0;
+      const uint32_t leaf = depth <= maxc ? (m & leafmask[depth]) : 0;
       const uint32_t pre = m & ~leaf;
       if (c == '{' || c == '[') {
         if (leaf) return false;                       // number expected
         if (c == '[' && pre) return false;            // struct expected
-        if (pre) *set &= ~pre;                        // a (repeated) parent object: its fields restart
+        if (pre) set &= ~pre;                         // a (repeated) parent object: its fields restart
         if (depth + 1 >= JS_MAXD) return false;       // deeper than supported
         depth++;
-        is_obj[depth] = c == '{';
+        if (c == '{') is_obj |= 1ull << depth; else is_obj &= ~(1ull << depth);
         mstack[depth] = c == '{' ? pre : 0;
         i++;
         state = c == '{' ? 0 : 4;
@@ -2881,25 +2902,23 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
         bool esc;
         const int32_t e = js_skip_string(s, n, i, &esc);
         if (e < 0) return false;
-        if (leaf) {
-          for (int p = 0; p < P.n_paths; p++)
-            if ((leaf >> p) & 1) {
-              const int t = P.path_type[p];
-              long long v;
-              if (t == SK_STRING) {                   // body span + escape flag, compared lazily
-                v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
-              } else if (t == SK_FLOAT || t == SK_DOUBLE) {
-                const int code = fp_special(s, i + 1, e - 1, esc);
-                if (!code) return false;
-                v = (1ll << 62) | code;
-              } else {
-                if ((t != SK_DATE && t != SK_TIMESTAMP && t != SK_TIMESTAMP_NTZ) || esc) return false;
-                if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v)
-                                   : js_timestamp(s, i + 1, e - 1, &v, t == SK_TIMESTAMP_NTZ))) return false;
-              }
-              val[p] = v;
-              *set |= 1u << p;
-            }
+        for (uint32_t lm = leaf; lm; lm &= lm - 1) {
+          const int q = __builtin_ctz(lm);
+          const int t = P.path_type[w0 + q];
+          long long v;
+          if (t == SK_STRING) {                       // body span + escape flag, compared lazily
+            v = (long long)(i + 1) | ((long long)(e - 2 - i) << 32) | (esc ? (1ll << 62) : 0);
+          } else if (t == SK_FLOAT || t == SK_DOUBLE) {
+            const int code = fp_special(s, i + 1, e - 1, esc);
+            if (!code) return false;
+            v = (1ll << 62) | code;
+          } else {
+            if ((t != SK_DATE && t != SK_TIMESTAMP && t != SK_TIMESTAMP_NTZ) || esc) return false;
+            if (!(t == SK_DATE ? js_date(s, i + 1, e - 1, &v)
+                               : js_timestamp(s, i + 1, e - 1, &v, t == SK_TIMESTAMP_NTZ))) return false;
+          }
+          V.val[(long long)(w0 + q) * V.stride] = v;
+          set |= 1u << q;
         }
         i = e;
       } else if (c == '-' || (c >= '0' && c <= '9')) {
@@ -2908,34 +2927,29 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
         long long v;
         const int32_t e = js_number(s, n, i, &integral, &fits, &v);
         if (e < 0) return false;
-        if (leaf) {
-          for (int p = 0; p < P.n_paths; p++)
-            if ((leaf >> p) & 1) {
-              const int t = P.path_type[p];
-              if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP || t == SK_TIMESTAMP_NTZ) return false;
-              if (t == SK_FLOAT || t == SK_DOUBLE) {   // exact token, range-checked
-                if (!fp_in_range(s, i, e, t == SK_DOUBLE)) return false;
-                val[p] = (long long)i | ((long long)(e - i) << 32);
-                *set |= 1u << p;
-                continue;
-              }
-              if (t == SK_DECIMAL) {                  // decimalValue() of the token: kept as its span
-                val[p] = (long long)i | ((long long)(e - i) << 32);
-                *set |= 1u << p;
-                continue;
-              }
-              if (t == SK_SHORT || t == SK_BYTE) {
-                if (!(integral && fits) && !js_small_exact(s, i, e, &v)) return false;
-              } else if (!integral || !fits) {
-                return false;                         // long/integer need an integral token
-              }
-              const bool in = t == SK_LONG ? true
-                            : t == SK_INT ? (v >= -2147483648ll && v <= 2147483647ll)
-                            : t == SK_SHORT ? (v >= -32768 && v <= 32767) : (v >= -128 && v <= 127);
-              if (!in) return false;
-              val[p] = v;
-              *set |= 1u << p;
+        for (uint32_t lm = leaf; lm; lm &= lm - 1) {
+          const int q = __builtin_ctz(lm);
+          const int t = P.path_type[w0 + q];
+          long long x = v;
+          if (t == SK_DATE || t == SK_STRING || t == SK_TIMESTAMP || t == SK_TIMESTAMP_NTZ) return false;
+          if (t == SK_FLOAT || t == SK_DOUBLE) {     // exact token, range-checked
+            if (!fp_in_range(s, i, e, t == SK_DOUBLE)) return false;
+            x = (long long)i | ((long long)(e - i) << 32);
+          } else if (t == SK_DECIMAL) {              // decimalValue() of the token: kept as its span
+            x = (long long)i | ((long long)(e - i) << 32);
+          } else {
+            if (t == SK_SHORT || t == SK_BYTE) {
+              if (!(integral && fits) && !js_small_exact(s, i, e, &x)) return false;
+            } else if (!integral || !fits) {
+              return false;                           // long/integer need an integral token
             }
+            const bool in = t == SK_LONG ? true
+                          : t == SK_INT ? (x >= -2147483648ll && x <= 2147483647ll)
+                          : t == SK_SHORT ? (x >= -32768 && x <= 32767) : (x >= -128 && x <= 127);
+            if (!in) return false;
+          }
+          V.val[(long long)(w0 + q) * V.stride] = x;
+          set |= 1u << q;
         }
         i = e;
       } else if (c == 't' || c == 'f' || c == 'n') {
@@ -2944,7 +2958,7 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
         if (i + ll > n) return false;
         for (int k = 0; k < ll; k++) if (s[i + k] != (uint8_t)lit[k]) return false;
         if (c != 'n' && (leaf || pre)) return false;  // boolean where a number / struct is expected
-        if (c == 'n') *set &= ~(leaf | pre);          // JSON null: the field (and its children) null
+        if (c == 'n') set &= ~(leaf | pre);           // JSON null: the field (and its children) null
         i += ll;
       } else {
         return false;
@@ -2953,15 +2967,31 @@ __device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, long
       continue;
     }
     // state 3: after a value
-    if (c == ',') { state = is_obj[depth] ? 1 : 4; i++; continue; }
-    if ((c == '}' && is_obj[depth]) || (c == ']' && !is_obj[depth])) goto close;
+    {
+      const bool obj = (is_obj >> depth) & 1;
+      if (c == ',') { state = obj ? 1 : 4; i++; continue; }
+      if ((c == '}' && obj) || (c == ']' && !obj)) goto close;
+    }
     return false;
   close:
     i++;
     depth--;
-    if (depth == 0) return true;                      // trailing content is ignored (readTree)
+    if (depth == 0) { *found = set; return true; }   // trailing content is ignored (readTree)
     state = 3;
   }
+}
+
+// extract every program path from one JSON object, 32 paths per pass; returns false on a decode error
+__device__ bool js_extract(const uint8_t* s, int32_t n, const DSkipProg& P, SkSlots V) {
+  int w0 = 0;
+  do {
+    const int np = P.n_paths - w0 < SK_WINDOW ? P.n_paths - w0 : SK_WINDOW;
+    uint32_t found = 0;
+    if (!js_extract_window(s, n, P, w0, np > 0 ? np : 0, V, &found)) return false;
+    if (np > 0) V.setw[(long long)(w0 >> 5) * V.stride] = found;
+    w0 += SK_WINDOW;
+  } while (w0 < P.n_paths);
+  return true;
 }
 
 // a typed decimal (unscaled value, scale) as the text "<unscaled>E-<scale>" (buffer >= 26 bytes)
@@ -3016,46 +3046,46 @@ __device__ int sk_strcmp(Utf8Cursor a, Utf8Cursor b) {
   }
 }
 
-// typed stats values (k_stats_parsed), per path: kind TP_*, decimal scale, string bytes (the value
-// slot then holds the string's length; a decimal's slot its unscaled value; a float's its rank in
-// the stat's format, FK_NAN for NaN)
-struct SkTyped { int32_t kind[SK_MAX_PATHS]; int32_t scale[SK_MAX_PATHS]; const uint8_t* ptr[SK_MAX_PATHS]; };
+// typed stats values (k_stats_parsed): per path the kind TP_*, decimal scale and string bytes in the
+// SkSlots arrays (the value slot then holds the string's length; a decimal's slot its unscaled value; a
+// float's its rank in the stat's format, FK_NAN for NaN)
 constexpr long long FK_NAN = 0x7fffffffffffffffll;
 
 // Kleene evaluation of the postfix program; returns 1 true, 0 false, -1 null. typed: the values are
-// add.stats_parsed's (null: the JSON stats path's packed spans).
-__device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, const uint8_t* s,
-                       const SkTyped* typed = nullptr) {
-  long long sv[16];
-  int8_t sn[16];      // -1 null, else 0/1 for booleans (values: 0 = non-null)
-  int8_t sk[16];      // slot kind (sk_cursor; 6 typed string, 7 typed decimal text, 8 typed float as double bits)
-  int32_t sl[16];     // literal string length
-  const uint8_t* sq[16];   // typed strings / decimal texts
+// add.stats_parsed's (else the JSON stats path's packed spans into s).
+__device__ int sk_eval(const DSkipProg& P, const SkSlots& V, const uint8_t* s, bool typed = false) {
+  long long sv[SK_STACK];
+  int8_t sn[SK_STACK];      // -1 null, else 0/1 for booleans (values: 0 = non-null)
+  int8_t sk[SK_STACK];      // slot kind (sk_cursor; 6 typed string, 7 typed decimal text, 8 typed float rank)
+  int32_t sl[SK_STACK];     // literal string length
+  const uint8_t* sq[SK_STACK];   // typed strings
   int sp = 0;
-  for (int k = 0; k < P.n_ops && k < SK_MAX_OPS; k++) {
+  for (int k = 0; k < P.n_ops; k++) {
     const int op = P.op[k];
     if (op == OP_STAT) {
+      if (sp >= SK_STACK) return -1;
       const int p = P.arg[k];
-      sv[sp] = val[p]; sn[sp] = ((set >> p) & 1) ? 0 : -1;
+      const long long pi = (long long)p * V.stride;
+      sv[sp] = V.val[pi]; sn[sp] = V.has(p) ? 0 : -1;
       const int pt = P.path_type[p];
       sk[sp] = pt == SK_STRING ? 1 : pt == SK_DECIMAL ? 3 : (pt == SK_FLOAT || pt == SK_DOUBLE) ? 5 : 0;
       sl[sp] = 0; sq[sp] = nullptr;
       if (typed) {
-        const int tk = typed->kind[p];
+        const int tk = V.kind[pi];
         sk[sp] = tk == TP_STR ? 6 : tk == TP_DEC ? 7 : (tk == TP_F32 || tk == TP_F64) ? 8 : 0;
-        sq[sp] = typed->ptr[p];
-        sl[sp] = typed->scale[p];
+        sq[sp] = V.ptr[pi];
+        sl[sp] = V.scale[pi];
       }
       sp++;
     } else if (op == OP_FCMP && sp > 0 && sk[sp - 1] == 8) {
       // a typed float / double stat, as its rank: the comparison holds for the ranks [lo, hi] the
-      // planner put after the threshold text (binfloat.rank_run; lo > hi: never), NaN per flag bit 4
+      // planner put after the threshold text (lo > hi: never), NaN per flag bit 4
       const int fl = P.arg[k];
       int8_t r;
       if (sn[sp - 1] < 0) r = -1;
       else if (sv[sp - 1] == FK_NAN) r = (int8_t)((fl >> 4) & 1);
       else {
-        const uint8_t* t = (const uint8_t*)P.names + (int32_t)(P.lit[k] & 0xffffffff) + (int32_t)(P.lit[k] >> 32);
+        const uint8_t* t = (const uint8_t*)P.names + (P.lit[k] & 0xffffffffll) + (P.lit[k] >> 32);
         unsigned long long lo = 0, hi = 0;
         for (int b = 0; b < 8; b++) { lo |= (unsigned long long)t[b] << (8 * b); hi |= (unsigned long long)t[8 + b] << (8 * b); }
         r = (int8_t)((long long)lo <= sv[sp - 1] && sv[sp - 1] <= (long long)hi);
@@ -3072,18 +3102,21 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       else {
         DecNum x, y;
         dec_parse(s + (int32_t)(a & 0x7fffffff), (int32_t)(a >> 32), &x);
-        dec_parse((const uint8_t*)P.names + (int32_t)(P.lit[k] & 0xffffffff), (int32_t)(P.lit[k] >> 32), &y);
+        dec_parse((const uint8_t*)P.names + (P.lit[k] & 0xffffffffll), (int32_t)(P.lit[k] >> 32), &y);
         const int c = dec_cmp(x, y);
         r = mode == FC_LT ? c < 0 : mode == FC_LE ? c <= 0 : mode == FC_GT ? c > 0 : c >= 0;
       }
       sn[sp - 1] = r; sv[sp - 1] = 0; sk[sp - 1] = 0;
     } else if (op == OP_LIT) {
+      if (sp >= SK_STACK) return -1;
       sv[sp] = P.lit[k]; sn[sp] = P.arg[k] ? -1 : 0; sk[sp] = 0; sl[sp] = 0; sq[sp] = nullptr; sp++;
     } else if (op == OP_TIMEADD) {                     // DefaultExpressionEvaluator.visitTimeAdd :593-625
       if (sp > 0 && sn[sp - 1] >= 0) sv[sp - 1] += P.lit[k];
     } else if (op == OP_LIT_STR || op == OP_LIT_DEC) {
+      if (sp >= SK_STACK) return -1;
       sv[sp] = P.lit[k]; sn[sp] = 0; sk[sp] = op == OP_LIT_STR ? 2 : 4; sl[sp] = P.arg[k]; sq[sp] = nullptr; sp++;
     } else if (op >= OP_LT && op <= OP_EQ) {
+      if (sp < 2) return -1;
       const long long b = sv[--sp]; const int8_t bn = sn[sp], bk = sk[sp]; const int32_t bl = sl[sp];
       const long long a = sv[--sp]; const int8_t an = sn[sp], ak = sk[sp]; const int32_t al = sl[sp];
       int8_t r;
@@ -3104,6 +3137,7 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
       else r = op == OP_LT ? a < b : op == OP_LE ? a <= b : op == OP_GT ? a > b : op == OP_GE ? a >= b : a == b;
       sn[sp] = r; sv[sp] = 0; sk[sp] = 0; sl[sp] = 0; sq[sp] = nullptr; sp++;
     } else {
+      if (sp < 2) return -1;
       const int8_t b = sn[--sp];
       const int8_t a = sn[--sp];
       int8_t r;
@@ -3115,11 +3149,29 @@ __device__ int sk_eval(const DSkipProg& P, const long long* val, uint32_t set, c
   return sp == 1 ? sn[0] : -1;
 }
 
+// The lane's slots: registers (narrow programs) or its column of the scratch arrays (wide ones). The
+// grid-stride loops below keep one lane index for a lane's whole life, and wide grids have exactly
+// S.lanes lanes.
+struct SkLocal {
+  long long val[SK_NARROW];
+  uint32_t setw[1];
+  int32_t kind[SK_NARROW];
+  int32_t scale[SK_NARROW];
+  const uint8_t* ptr[SK_NARROW];
+};
+__device__ __forceinline__ SkSlots sk_slots(SkLocal& L, const SkScratch& S, bool wide) {
+  if (!wide) return SkSlots{L.val, L.setw, L.kind, L.scale, L.ptr, 1};
+  const long long lane = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  return SkSlots{S.val + lane, S.setw + lane, S.kind + lane, S.scale + lane, S.ptr + lane, S.lanes};
+}
+
 // the program lives in device memory (its literal pool holds exact float thresholds of up to ~760
-// digits, too large for a kernel argument)
-__global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg* __restrict__ Pp,
+// digits); P itself is a kernel argument of pointers into it
+__global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg P, SkScratch S,
                                                    uint8_t* __restrict__ sel, DState* __restrict__ st) {
-  const DSkipProg& P = *Pp;
+  SkLocal L;
+  const bool wide = P.n_paths > SK_NARROW;
+  const SkSlots V = sk_slots(L, S, wide);
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
        r += (long long)gridDim.x * blockDim.x) {
     const uint8_t cur = sel[r];
@@ -3136,10 +3188,8 @@ __global__ __launch_bounds__(NT) void k_stats_eval(StatsRows R, const DSkipProg*
       s = R.chars + R.soff[r];
       len = R.slen[r];
     }
-    long long val[SK_MAX_PATHS];
-    uint32_t set = 0;
-    if (!js_extract(s, len, P, val, &set)) { set_err(st, E_STATS, R.row_tag + r, 0); continue; }
-    if (sk_eval(P, val, set, s) == 0) sel[r] = 0;                    // COALESCE(skip, true)
+    if (!js_extract(s, len, P, V)) { set_err(st, E_STATS, R.row_tag + r, 0); continue; }
+    if (sk_eval(P, V, s) == 0) sel[r] = 0;                          // COALESCE(skip, true)
   }
 }
 
@@ -3305,72 +3355,81 @@ struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 bool
   const uint8_t* p;
 };
 
-// 1 true, 0 false, -1 null; *err on a malformed partition value
-__device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bool* err) {
-  PVal f[PP_MAX_FIELDS];
-  for (int k = 0; k < P.n_fields && k < PP_MAX_FIELDS; k++) f[k].kind = 0;
-  if (M.row_offs && M.row_def[row] >= M.rep_def - 1) {   // the map is not null (and has entries somewhere)
-    const int64_t e0 = M.row_offs[row], e1 = M.row_offs[row + 1];
-    for (int k = 0; k < P.n_fields && k < PP_MAX_FIELDS; k++) {
-      const uint8_t* nm = (const uint8_t*)P.pool + P.name_off[k];
-      for (int64_t e = e0; e < e1; e++) {
-        const int64_t ko = M.k_offs[e];
-        if (bytes_cmp(M.k_chars + ko, (int32_t)(M.k_offs[e + 1] - ko), nm, P.name_len[k]) != 0) continue;
-        if (M.v_def[e] >= M.v_max_def) {
-          const uint8_t* vp = M.v_chars + M.v_offs[e];
-          const int32_t vl = (int32_t)(M.v_offs[e + 1] - M.v_offs[e]);
-          const int ty = P.field_type[k];
-          if (ty == PT_STRING) {
-            f[k].kind = 2; f[k].p = vp; f[k].len = vl;
-          } else if (ty == PT_DATE) {                    // PartitionValueEvaluator.java:72-73
-            if (!js_date(vp, 0, vl, &f[k].v)) { *err = true; return -1; }
-            f[k].kind = 1;
-          } else if (ty == PT_DECIMAL) {
-            DecNum dn;
-            if (!dec_parse(vp, vl, &dn)) { *err = true; return -1; }
-            f[k].kind = 4; f[k].p = vp; f[k].len = vl;
-          } else if (ty == PT_BOOL) {                 // Boolean.parseBoolean
-            const char* tr = "true";
-            bool t = vl == 4;
-            for (int q = 0; q < 4 && t; q++) t = (vp[q] | 0x20) == (uint8_t)tr[q];
-            f[k].kind = 1; f[k].v = t;
-          } else if (ty == PT_TIMESTAMP) {
-            if (!java_timestamp_valueof(vp, vl, &f[k].v)) { *err = true; return -1; }
-            f[k].kind = 1;
-          } else if (ty == PT_F32 || ty == PT_F64) {
-            int32_t fa = 0, fb = 0;
-            int sp_ = 0;
-            bool nz = false;
-            if (!java_parse_fp(vp, vl, &fa, &fb, &sp_, &nz)) { *err = true; return -1; }
-            f[k].kind = 5; f[k].p = vp + fa; f[k].len = fb - fa; f[k].v = sp_ | (nz ? 256 : 0);
-          } else {
-            const long long lo = ty == PT_LONG ? (-9223372036854775807ll - 1) : ty == PT_INT ? -2147483648ll
-                               : ty == PT_SHORT ? -32768 : -128;
-            const long long hi = ty == PT_LONG ? 9223372036854775807ll : ty == PT_INT ? 2147483647ll
-                               : ty == PT_SHORT ? 32767 : 127;
-            if (!java_parse_long(vp, vl, lo, hi, &f[k].v)) { *err = true; return -1; }
-            f[k].kind = 1;
-          }
-        }
-        break;
+// element_at(add.partitionValues, <field k's name>) of one row, deserialized as partition_value does
+// (PartitionValueEvaluator.java:50-100); kind 0 when the map or the key is absent or the value null.
+// false on a malformed value.
+__device__ bool part_field(const DPartProg& P, const MapRows& M, long long row, int k, PVal* f) {
+  f->kind = 0;
+  if (!(M.row_offs && M.row_def[row] >= M.rep_def - 1)) return true;   // a null map (or no entries anywhere)
+  const int64_t e0 = M.row_offs[row], e1 = M.row_offs[row + 1];
+  const uint8_t* nm = (const uint8_t*)P.pool + P.name_off[k];
+  const int32_t nl = P.name_len[k];
+  for (int64_t e = e0; e < e1; e++) {
+    const int64_t ko = M.k_offs[e];
+    if (bytes_cmp(M.k_chars + ko, (int32_t)(M.k_offs[e + 1] - ko), nm, nl) != 0) continue;
+    if (M.v_def[e] >= M.v_max_def) {
+      const uint8_t* vp = M.v_chars + M.v_offs[e];
+      const int32_t vl = (int32_t)(M.v_offs[e + 1] - M.v_offs[e]);
+      const int ty = P.field_type[k];
+      if (ty == PT_STRING) {
+        f->kind = 2; f->p = vp; f->len = vl;
+      } else if (ty == PT_DATE) {                    // PartitionValueEvaluator.java:72-73
+        if (!js_date(vp, 0, vl, &f->v)) return false;
+        f->kind = 1;
+      } else if (ty == PT_DECIMAL) {
+        DecNum dn;
+        if (!dec_parse(vp, vl, &dn)) return false;
+        f->kind = 4; f->p = vp; f->len = vl;
+      } else if (ty == PT_BOOL) {                 // Boolean.parseBoolean
+        const char* tr = "true";
+        bool t = vl == 4;
+        for (int q = 0; q < 4 && t; q++) t = (vp[q] | 0x20) == (uint8_t)tr[q];
+        f->kind = 1; f->v = t;
+      } else if (ty == PT_TIMESTAMP) {
+        if (!java_timestamp_valueof(vp, vl, &f->v)) return false;
+        f->kind = 1;
+      } else if (ty == PT_F32 || ty == PT_F64) {
+        int32_t fa = 0, fb = 0;
+        int sp_ = 0;
+        bool nz = false;
+        if (!java_parse_fp(vp, vl, &fa, &fb, &sp_, &nz)) return false;
+        f->kind = 5; f->p = vp + fa; f->len = fb - fa; f->v = sp_ | (nz ? 256 : 0);
+      } else {
+        const long long lo = ty == PT_LONG ? (-9223372036854775807ll - 1) : ty == PT_INT ? -2147483648ll
+                           : ty == PT_SHORT ? -32768 : -128;
+        const long long hi = ty == PT_LONG ? 9223372036854775807ll : ty == PT_INT ? 2147483647ll
+                           : ty == PT_SHORT ? 32767 : 127;
+        if (!java_parse_long(vp, vl, lo, hi, &f->v)) return false;
+        f->kind = 1;
       }
     }
+    break;                                           // the first entry with the key
   }
-  PVal st[16];
+  return true;
+}
+
+// 1 true, 0 false, -1 null; *err on a malformed partition value. Every FIELD op deserializes its
+// value, so every referenced column of every row is parsed (the reference deserializes whole vectors,
+// DefaultExpressionEvaluator does not short-circuit AND / OR).
+__device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bool* err) {
+  PVal st[PP_STACK];
   int sp = 0;
-  for (int i = 0; i < P.n_ops && i < PP_MAX_OPS; i++) {
+  for (int i = 0; i < P.n_ops; i++) {
     const int op = P.op[i];
-    if (op == PO_FIELD) {
-      st[sp++] = f[P.arg[i]];
-    } else if (op == PO_LIT_INT) {
-      st[sp].kind = 1; st[sp].v = P.lit[i]; sp++;
-    } else if (op == PO_LIT_STR) {
-      st[sp].kind = 2; st[sp].p = (const uint8_t*)P.pool + P.lit[i]; st[sp].len = P.arg[i]; sp++;
-    } else if (op == PO_LIT_DEC) {
-      st[sp].kind = 4; st[sp].p = (const uint8_t*)P.pool + P.lit[i]; st[sp].len = P.arg[i]; sp++;
-    } else if (op == PO_LIT_NULL) {
-      st[sp++].kind = 0;
+    if (op == PO_FIELD || op == PO_LIT_INT || op == PO_LIT_STR || op == PO_LIT_DEC || op == PO_LIT_NULL) {
+      if (sp >= PP_STACK) return -1;
+      PVal& t = st[sp++];
+      if (op == PO_FIELD) {
+        if (!part_field(P, M, row, P.arg[i], &t)) { *err = true; return -1; }
+      } else if (op == PO_LIT_INT) {
+        t.kind = 1; t.v = P.lit[i];
+      } else if (op == PO_LIT_NULL) {
+        t.kind = 0;
+      } else {
+        t.kind = op == PO_LIT_STR ? 2 : 4; t.p = (const uint8_t*)P.pool + P.lit[i]; t.len = P.arg[i];
+      }
     } else if (op == PO_FCMP) {                          // float / double field vs a planned threshold
+      if (sp < 1) return -1;
       PVal& a = st[sp - 1];
       if (a.kind != 0) {
         const int fl = P.arg[i], mode = fl & 15, code = (int)(a.v & 255);
@@ -3380,7 +3439,7 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
         else {
           DecNum x{}, y{};
           if (code == 4) { x.sign = 0; } else dec_parse(a.p, a.len, &x);        // code 4: underflow
-          dec_parse((const uint8_t*)P.pool + (int32_t)(P.lit[i] & 0xffffffff), (int32_t)(P.lit[i] >> 32), &y);
+          dec_parse((const uint8_t*)P.pool + (P.lit[i] & 0xffffffffll), (int32_t)(P.lit[i] >> 32), &y);
           int c = dec_cmp(x, y);
           if (c == 0 && (a.v & 256)) c = -1;                                     // -0.0 sits just below 0
           r = mode == FC_LT ? c < 0 : mode == FC_LE ? c <= 0 : mode == FC_GT ? c > 0 : c >= 0;
@@ -3388,6 +3447,7 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
         a.kind = 3; a.v = r;
       }
     } else if (op >= PO_LT && op <= PO_NSEQ) {
+      if (sp < 2) return -1;
       const PVal b = st[--sp];
       const PVal a = st[--sp];
       PVal r;
@@ -3412,16 +3472,27 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
       }
       st[sp++] = r;
     } else if (op == PO_ISNULL || op == PO_ISNOTNULL) {
+      if (sp < 1) return -1;
       PVal& a = st[sp - 1];
       const bool isnull = a.kind == 0;
       a.kind = 3; a.v = op == PO_ISNULL ? isnull : !isnull;
     } else if (op == PO_NOT) {
+      if (sp < 1) return -1;
       PVal& a = st[sp - 1];
       if (a.kind != 0) a.v = !a.v;
+    } else if (op == PO_COALESCE) {                      // the first non-null of the last arg operands
+      const int n = P.arg[i];
+      if (n < 1 || sp < n) return -1;
+      int pick = -1;
+      for (int q = sp - n; q < sp && pick < 0; q++) if (st[q].kind != 0) pick = q;
+      const PVal r = pick < 0 ? st[sp - n] : st[pick];
+      sp -= n;
+      st[sp++] = r;
     } else {                                             // AND / OR, Kleene
+      if (sp < 2) return -1;
       const PVal b = st[--sp];
       const PVal a = st[--sp];
-      const int av = a.kind == 0 ? -1 : (int)a.v, bv = b.kind == 0 ? -1 : (int)b.v;
+      const int av = a.kind == 0 ? -1 : (int)(a.v != 0), bv = b.kind == 0 ? -1 : (int)(b.v != 0);
       int rv;
       if (op == PO_AND) rv = (av == 0 || bv == 0) ? 0 : (av == 1 && bv == 1) ? 1 : -1;
       else rv = (av == 1 || bv == 1) ? 1 : (av == 0 && bv == 0) ? 0 : -1;
@@ -3434,9 +3505,8 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
   return st[0].v ? 1 : 0;
 }
 
-__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg* __restrict__ Pp,
+__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg P,
                                                   uint8_t* __restrict__ sel, DState* __restrict__ st) {
-  const DPartProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < M.n;
        r += (long long)gridDim.x * blockDim.x) {
     const long long row = M.act_row ? M.act_row[r] : r;
@@ -4230,29 +4300,32 @@ namespace dk {
 __device__ __forceinline__ long long ld_i64(const uint8_t* p) {
   return (long long)((unsigned long long)ld_u32(p) | ((unsigned long long)ld_u32(p + 4) << 32));
 }
-__global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DSkipProg* __restrict__ Pp,
+__global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DSkipProg P, SkScratch S,
                                                      uint8_t* __restrict__ sel) {
-  const DSkipProg& P = *Pp;
+  SkLocal L;
+  const bool wide = P.n_paths > SK_NARROW;
+  const SkSlots V = sk_slots(L, S, wide);
+  const int nw = (R.n_paths + 31) >> 5;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < R.n;
        r += (long long)gridDim.x * blockDim.x) {
     if (!sel[r] || R.js.row_def[r] < R.js.max_def) continue;         // null add.stats: kept
-    long long val[SK_MAX_PATHS];
-    uint32_t set = 0;
-    SkTyped T;
-    bool typed = R.def[0][r] >= R.struct_def;
+    bool typed = R.paths[0].def[r] >= R.struct_def;
+    for (int w = 0; w < nw; w++) V.setw[(long long)w * V.stride] = 0;
     for (int p = 0; p < R.n_paths && typed; p++) {
-      const int kd = R.kind[p];
-      T.kind[p] = kd; T.scale[p] = R.scale[p]; T.ptr[p] = nullptr;
-      val[p] = 0;
-      if (R.def[p][r] < R.max_def[p]) continue;
-      const uint8_t* v = R.vals[p] + r * R.width[p];
+      const TypedPath& T = R.paths[p];
+      const long long pi = (long long)p * V.stride;
+      const int kd = T.kind;
+      V.kind[pi] = kd; V.scale[pi] = T.scale; V.ptr[pi] = nullptr;
+      V.val[pi] = 0;
+      if (T.def[r] < T.max_def) continue;
+      const uint8_t* v = T.vals + r * T.width;
       long long x;
       if (kd == TP_STR) {
-        const long long o0 = R.offs[p][r];
-        T.ptr[p] = R.chars[p] + o0;
-        x = R.offs[p][r + 1] - o0;
+        const long long o0 = T.offs[r];
+        V.ptr[pi] = T.chars + o0;
+        x = T.offs[r + 1] - o0;
       } else if (kd == TP_INT || kd == TP_DEC) {
-        x = R.width[p] == 8 ? ld_i64(v) : (long long)(int32_t)ld_u32(v);
+        x = T.width == 8 ? ld_i64(v) : (long long)(int32_t)ld_u32(v);
       } else if (kd == TP_MILLIS) {
         x = ld_i64(v);
         if (x > 9223372036854775ll || x < -9223372036854775ll) { typed = false; break; }
@@ -4271,34 +4344,41 @@ __global__ __launch_bounds__(NT) void k_stats_parsed(StatsParsedRows R, const DS
         else if (mag == 0 && neg) { typed = false; break; }             // -0.0: ambiguous
         else x = neg ? -(long long)mag - 1 : (long long)mag;
       }
-      val[p] = x;
-      set |= 1u << p;
+      V.val[pi] = x;
+      V.setw[(long long)(p >> 5) * V.stride] |= 1u << (p & 31);
     }
     if (!typed) { sel[r] = 2; continue; }                                // k_stats_eval decides
-    if (sk_eval(P, val, set, (const uint8_t*)P.names, &T) == 0) sel[r] = 0;   // COALESCE(skip, true)
+    if (sk_eval(P, V, (const uint8_t*)P.names, true) == 0) sel[r] = 0;  // COALESCE(skip, true)
   }
 }
 
-void launch_stats_parsed(const StatsParsedRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {
-  if (R.n <= 0) return;
-  const long long want = (R.n + NT - 1) / NT;
-  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
-  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, sel);
-  StatsRows J = R.js;                  // the marked rows, from their JSON
-  J.marked = 1;
-  hipLaunchKernelGGL(k_stats_eval, dim3(grid), dim3(NT), 0, s, J, P, sel, st);
+// grid of a skipping launch: wide programs run exactly S.lanes lanes (one scratch column each)
+static unsigned sk_grid(long long n, const DSkipProg& P, const SkScratch& S) {
+  long long want = (n + NT - 1) / NT;
+  long long cap = 2048;
+  if (P.n_paths > SK_NARROW) cap = S.lanes / NT;
+  if (want > cap) want = cap;
+  return (unsigned)(want < 1 ? 1 : want);
 }
 
-void launch_stats_eval(const StatsRows& R, const DSkipProg* P, uint8_t* sel, DState* st, hipStream_t s) {
+void launch_stats_parsed(const StatsParsedRows& R, const DSkipProg& P, const SkScratch& S, uint8_t* sel, DState* st,
+                         hipStream_t s) {
   if (R.n <= 0) return;
-  const long long want = (R.n + NT - 1) / NT;
-  const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
-  hipLaunchKernelGGL(k_stats_eval, dim3(grid), dim3(NT), 0, s, R, P, sel, st);
+  const unsigned grid = sk_grid(R.n, P, S);
+  hipLaunchKernelGGL(k_stats_parsed, dim3(grid), dim3(NT), 0, s, R, P, S, sel);
+  StatsRows J = R.js;                  // the marked rows, from their JSON
+  J.marked = 1;
+  hipLaunchKernelGGL(k_stats_eval, dim3(grid), dim3(NT), 0, s, J, P, S, sel, st);
+}
+
+void launch_stats_eval(const StatsRows& R, const DSkipProg& P, const SkScratch& S, uint8_t* sel, DState* st, hipStream_t s) {
+  if (R.n <= 0) return;
+  hipLaunchKernelGGL(k_stats_eval, dim3(sk_grid(R.n, P, S)), dim3(NT), 0, s, R, P, S, sel, st);
 }
 }  // namespace dk
 
 namespace dk {
-void launch_part_eval(const MapRows& M, const DPartProg* P, uint8_t* sel, DState* st, hipStream_t s) {
+void launch_part_eval(const MapRows& M, const DPartProg& P, uint8_t* sel, DState* st, hipStream_t s) {
   if (M.n <= 0) return;
   const long long want = (M.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
@@ -4661,51 +4741,56 @@ namespace dk {
 // COALESCE(skip, true)).eval(batch, selection)). One lane per row.
 
 // DefaultJsonHandler.parseJson (KD/engine/DefaultJsonHandler.java:60-76): unselected and null rows are
-// all-null rows; a selected row's stats are decoded with DefaultJsonRow's rules (js_extract). vals is
-// path-major [n_paths][n]; set[r] has bit p when path p is non-null.
+// all-null rows; a selected row's stats are decoded with DefaultJsonRow's rules (js_extract). Each
+// lane extracts into its slots and copies them out path-major: vals[p * n + r], set word w of row r
+// at set[w * n + r].
 __global__ __launch_bounds__(NT) void k_json_parse_stats(const uint8_t* __restrict__ chars, const int64_t* __restrict__ offs,
                                                          const uint8_t* __restrict__ isnull, const uint8_t* __restrict__ sel,
-                                                         long long n, const DSkipProg* __restrict__ Pp,
+                                                         long long n, const DSkipProg P, SkScratch S,
                                                          long long* __restrict__ vals, uint32_t* __restrict__ set,
                                                          DState* __restrict__ st) {
-  const DSkipProg& P = *Pp;
+  SkLocal L;
+  const bool wide = P.n_paths > SK_NARROW;
+  const SkSlots V = sk_slots(L, S, wide);
+  const int nw = (P.n_paths + 31) >> 5;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
-    uint32_t m = 0;
-    long long v[SK_MAX_PATHS];
+    for (int w = 0; w < nw; w++) V.setw[(long long)w * V.stride] = 0;
     if (!((sel && !sel[r]) || (isnull && isnull[r]))) {
       const uint8_t* s = chars + offs[r];
-      if (!js_extract(s, (int32_t)(offs[r + 1] - offs[r]), P, v, &m)) { set_err(st, E_STATS, r, 0); m = 0; }
+      if (!js_extract(s, (int32_t)(offs[r + 1] - offs[r]), P, V)) {
+        set_err(st, E_STATS, r, 0);
+        for (int w = 0; w < nw; w++) V.setw[(long long)w * V.stride] = 0;
+      }
     }
-    set[r] = m;
-    for (int p = 0; p < P.n_paths; p++) vals[(long long)p * n + r] = ((m >> p) & 1) ? v[p] : 0;
+    for (int w = 0; w < nw; w++) set[(long long)w * n + r] = V.setw[(long long)w * V.stride];
+    for (int p = 0; p < P.n_paths; p++) vals[(long long)p * n + r] = V.has(p) ? V.val[(long long)p * V.stride] : 0;
   }
 }
 
 // PredicateEvaluator.eval(parsed, selection) for COALESCE(program, true): a selected row stays
 // selected unless the program is FALSE (DefaultPredicateEvaluator.java:42-72 ANDs the existing
-// selection in)
+// selection in). The parsed columns are read in place (stride n): the program's paths are the parsed
+// schema's, in its order.
 __global__ __launch_bounds__(NT) void k_parsed_eval(const uint8_t* __restrict__ chars, const int64_t* __restrict__ offs,
-                                                    long long n, const DSkipProg* __restrict__ Pp,
-                                                    const long long* __restrict__ vals, const uint32_t* __restrict__ set,
+                                                    long long n, const DSkipProg P,
+                                                    long long* __restrict__ vals, uint32_t* __restrict__ set,
                                                     uint8_t* __restrict__ sel) {
-  const DSkipProg& P = *Pp;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
     if (!sel[r]) continue;
-    long long v[SK_MAX_PATHS];
-    for (int p = 0; p < P.n_paths; p++) v[p] = vals[(long long)p * n + r];
-    if (sk_eval(P, v, set[r], chars + offs[r]) == 0) sel[r] = 0;
+    const SkSlots V{vals + r, set + r, nullptr, nullptr, nullptr, n};
+    if (sk_eval(P, V, chars + offs[r]) == 0) sel[r] = 0;
   }
 }
 
 void launch_json_parse_stats(const uint8_t* chars, const int64_t* offs, const uint8_t* isnull, const uint8_t* sel,
-                             long long n, const DSkipProg* P, long long* vals, uint32_t* set, DState* st, hipStream_t s) {
+                             long long n, const DSkipProg& P, const SkScratch& S, long long* vals, uint32_t* set, DState* st,
+                             hipStream_t s) {
   if (n <= 0) return;
-  const long long want = (n + NT - 1) / NT;
-  hipLaunchKernelGGL(k_json_parse_stats, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(NT), 0, s, chars, offs, isnull,
-                     sel, n, P, vals, set, st);
+  hipLaunchKernelGGL(k_json_parse_stats, dim3(sk_grid(n, P, S)), dim3(NT), 0, s, chars, offs, isnull,
+                     sel, n, P, S, vals, set, st);
 }
-void launch_parsed_eval(const uint8_t* chars, const int64_t* offs, long long n, const DSkipProg* P, const long long* vals,
-                        const uint32_t* set, uint8_t* sel, hipStream_t s) {
+void launch_parsed_eval(const uint8_t* chars, const int64_t* offs, long long n, const DSkipProg& P, long long* vals,
+                        uint32_t* set, uint8_t* sel, hipStream_t s) {
   if (n <= 0) return;
   const long long want = (n + NT - 1) / NT;
   hipLaunchKernelGGL(k_parsed_eval, dim3((unsigned)(want < 2048 ? want : 2048)), dim3(NT), 0, s, chars, offs, n, P, vals,

@@ -25,7 +25,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ._lib import (MAX_LEAF_DEPTH, Column, DkError, check, dk_batch, dk_column, dk_config, dk_dv_descriptor,
-                   dk_part_program, dk_read_options, dk_rg_filter, dk_skip_program, lib)
+                   dk_read_options, dk_rg_filter, lib)
 
 ADD_LEAVES = ["add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value",
               "add.size", "add.modificationTime", "add.dataChange",
@@ -1122,7 +1122,7 @@ class GpuScan:
         self.snapshot = snapshot
         self.shard = shard
         self.predicate = predicate
-        self.skipping = None          # (planner node, paths, types) when a data-skipping filter applies
+        self.skipping = None          # (planner node, compiled Program) when a data-skipping filter applies
         self._deferred_error = None
         self.partition = None
         self.partition_filter, self.data_filter = None, None
@@ -1131,11 +1131,12 @@ class GpuScan:
             md = snapshot.metadata or {}
             parts = md.get("partitionColumns") or []
             self.partition_filter, self.data_filter = sk.split_filters(predicate, parts)
-            self.partition = None     # compiled partition-pruning program (delta_amd/partitions.py)
+            self.partition = None     # compiled partition-pruning program (dk_part_compile)
             if self.partition_filter is not None:
                 from . import partitions as pp
+                from . import programs
                 try:
-                    self.partition = pp.compile_program(
+                    self.partition = programs.compile_partition(
                         self.partition_filter, pp.partition_fields(md["schemaString"], parts))
                 except sk.UnsupportedExpression as e:
                     self._deferred_error = e          # the reference fails when the scan files are read
@@ -1148,7 +1149,11 @@ class GpuScan:
                     except sk.UnsupportedExpression as e:
                         self._deferred_error = e      # the reference fails when the scan files are read
                     else:
-                        self.skipping = (node,) + sk.compile_program(node, leaves)
+                        from . import programs
+                        try:
+                            self.skipping = (node, programs.compile_skipping(node, leaves))
+                        except sk.UnsupportedExpression as e:
+                            self._deferred_error = e  # (the compiler's own type check)
         # ScanImpl.getScanFiles: shouldReadStats = hasDataSkippingFilter || includeStats (:128-130)
         self.read_stats = read_stats or self.skipping is not None
         self.metrics = ScanMetrics()
@@ -1281,13 +1286,9 @@ class GpuScan:
             if getattr(self, "owner", None) is not None:
                 check(lib().dk_replay_set_owner(self._rh, self.shard[0], self.shard[1]))
             if self.partition is not None:
-                from . import partitions as pp
-                pprog = pp.pack(self.partition, dk_part_program)
-                check(lib().dk_replay_set_partition_filter(self._rh, C.byref(pprog)))
+                check(lib().dk_replay_set_partition_filter(self._rh, self.partition.handle))
             if self.skipping is not None:
-                from . import skipping as sk
-                prog = sk.pack(self.skipping[1:], dk_skip_program)
-                check(lib().dk_replay_set_skipping(self._rh, C.byref(prog)))
+                check(lib().dk_replay_set_skipping(self._rh, self.skipping[1].handle))
         except BaseException:
             owner_failed()
             raise
@@ -1335,8 +1336,7 @@ class GpuScan:
             # the typed add.stats_parsed leaves of the program's stats paths: the engine evaluates
             # skipping over them where a checkpoint file carries them with a type that holds the stat
             # (dk_replay_set_skipping), the add.stats JSON standing in for the rows they cannot
-            _, paths, types, _ = self.skipping
-            leaves = leaves + ["add.stats_parsed." + ".".join(p) for p in paths]
+            leaves = leaves + ["add.stats_parsed." + ".".join(p) for p in self.skipping[1].paths]
         t2 = time.perf_counter()
         # a plain scan (no shard, skipping or partition filter) opens the checkpoint asynchronously: the
         # grouped getScanFiles hands out the first files' batches while the later files still land

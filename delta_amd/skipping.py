@@ -1,7 +1,9 @@
 """Data-skipping planning (host side of K11), restating
-kernel-api/.../internal/skipping/DataSkippingUtils.java:74-456 and StatsSchemaHelper.java:71-232,
-and compiling the skipping predicate into a postfix program that the GPU evaluates per scan-file
-row over the row's ``add.stats`` JSON (k_stats_eval; ScanImpl.applyDataSkipping, ScanImpl.java:304-352).
+kernel-api/.../internal/skipping/DataSkippingUtils.java:74-456 and StatsSchemaHelper.java:71-232.
+The skipping predicate it constructs is compiled behind the C ABI (delta_amd/programs.py ->
+dk_skip_compile) into the postfix program the GPU evaluates per scan-file row over the row's
+``add.stats`` JSON or ``add.stats_parsed`` columns (k_stats_eval / k_stats_parsed;
+ScanImpl.applyDataSkipping, ScanImpl.java:304-352).
 
 A skipping predicate node is one of
     ("AND", a, b) / ("OR", a, b)
@@ -12,7 +14,6 @@ as in the reference (rewriteEqualNullSafe, :528-534).
 from __future__ import annotations
 
 import json
-import struct
 
 from decimal import Decimal as _Decimal
 
@@ -225,17 +226,16 @@ def referenced_stats(node, out=None):
     return out
 
 
-# ---- device program (k_stats_eval): postfix over (value, is_null) pairs --------------------------
-OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD, OP_LIT_DEC, OP_FCMP = range(13)
-# OP_FCMP: pops a float/double stats value, pushes `x <mode> threshold` for its exact decimal value x
-# (threshold = decimal text in names), or the planned constant for NaN / +Infinity / -Infinity
-FC_LT, FC_LE, FC_GT, FC_GE, FC_ALL, FC_NONE = range(6)
-_FC_MODE = {"<": FC_LT, "<=": FC_LE, ">": FC_GT, ">=": FC_GE}
+# ---- stats types --------------------------------------------------------------------------------
+# (the predicate is compiled behind the C ABI: delta_amd/programs.compile_skipping -> dk_skip_compile)
 FLOATS = ("float", "double")
 LONG_MIN, LONG_MAX = -(1 << 63), (1 << 63) - 1
-_CMP = {"<": OP_LT, "<=": OP_LE, ">": OP_GT, ">=": OP_GE, "=": OP_EQ}
 TYPE_CODE = {"long": 0, "integer": 1, "short": 2, "byte": 3, "date": 4, "string": 5, "timestamp": 6, "decimal": 7,
              "timestamp_ntz": 8, "float": 9, "double": 10}
+_CMP = ("<", "<=", ">", ">=", "=")
+# opcodes of a compiled skipping program (dk_device.h; dk_program_describe's "ops")
+OP_STAT, OP_LIT, OP_LT, OP_LE, OP_GT, OP_GE, OP_EQ, OP_AND, OP_OR, OP_LIT_STR, OP_TIMEADD, OP_LIT_DEC, OP_FCMP = range(13)
+FC_LT, FC_LE, FC_GT, FC_GE, FC_ALL, FC_NONE = range(6)
 
 
 def stat_type(path, leaves):
@@ -247,118 +247,6 @@ def stat_type(path, leaves):
         if phys == path[1:]:
             return "decimal" if t.startswith("decimal") else t
     raise KeyError(path)
-
-
-def compile_program(node, leaves):
-    """(paths, path type codes, ops) for the device evaluator; raises UnsupportedSkipping for stats
-    types the GPU evaluator does not decode (the reference would skip with them: refusing keeps
-    results identical instead of silently keeping more files)."""
-    paths = referenced_stats(node)
-    if len(paths) > MAX_PATHS:
-        raise UnsupportedSkipping("data skipping filter references %d stats fields (max %d)" % (len(paths), MAX_PATHS))
-    for p in paths:
-        t = stat_type(p, leaves)
-        if t not in GPU_TYPES:
-            raise UnsupportedSkipping("data skipping on %s column %s is not supported by this engine build"
-                                      % (t, ".".join(p[1:])))
-    ops = []
-
-    def emit(n):
-        if n[0] in ("AND", "OR"):
-            emit(n[1])
-            emit(n[2])
-            ops.append((OP_AND if n[0] == "AND" else OP_OR, 0, 0))
-        elif n[0] == "stat":
-            ops.append((OP_STAT, paths.index(n[1]), 0))
-        elif n[0] == "lit":
-            v = n[1]
-            if v is None:
-                ops.append((OP_LIT, 1, 0))                   # null literal: comparisons yield null
-            elif isinstance(v, _Decimal):                    # BigDecimal text, compareTo on the GPU
-                if not v.is_finite():
-                    raise UnsupportedSkipping("decimal literal %s is not finite" % v)
-                ops.append((OP_LIT_DEC, 0, str(v).encode("ascii")))
-            elif isinstance(v, str):                         # compared as UTF-8 bytes (String.getBytes)
-                ops.append((OP_LIT_STR, 0, v.encode("utf-8", "replace")))
-            elif isinstance(v, bool) or not isinstance(v, int):
-                raise UnsupportedSkipping("data skipping with a %r literal is not supported" % (v,))
-            elif not -(1 << 63) <= v < (1 << 63):
-                raise UnsupportedSkipping("literal %d does not fit a long" % v)
-            else:
-                ops.append((OP_LIT, 0, int(v)))
-        elif n[0] == "timeadd":                              # max + 1 ms (StatsSchemaHelper :154-159)
-            emit(n[1])
-            ops.append((OP_TIMEADD, 0, 1000))
-        elif _float_comparison(n, leaves):
-            emit_float(n)
-        else:
-            kinds = {_operand_kind(c, leaves) for c in (n[1], n[2])} - {None}
-            if len(kinds) > 1:
-                raise UnsupportedSkipping("data skipping comparison of a string with a non-string")
-            emit(n[1])
-            emit(n[2])
-            ops.append((_CMP[n[0]], 0, 0))
-
-    def emit_float(n):
-        """A comparison in float / double (Float.compare / Double.compare after ImplicitCastExpression
-        widening), planned exactly by binfloat.plan: integral stats get integer bounds, float /
-        double stats an OP_FCMP per bound."""
-        from . import binfloat
-        op, stat, lit = n
-        if stat[0] != "stat" or lit[0] != "lit":
-            raise UnsupportedSkipping("float comparison of %r with %r" % (stat, lit))
-        st, lt = operand_type(stat, leaves), lit[2]
-        if lit[1] is None:                                    # null literal: the comparison is null
-            emit(stat)
-            ops.append((OP_LIT, 1, 0))
-            ops.append((_CMP[op], 0, 0))
-            return
-        cmp_t = st if st == lt else (lt if lt in _UP_CAST.get(st, ()) else st)
-        value_fmt = st if st in FLOATS else cmp_t
-        conds, (r_nan, r_pinf, r_ninf) = binfloat.plan(op, lit[1], lt, value_fmt, cmp_t)
-        ranks = binfloat.rank_run(op, lit[1], lt, value_fmt, cmp_t)[0]
-        if st not in FLOATS:                                   # integral stats widened to cmp_t
-            b = binfloat.integral_bounds(conds)
-            if b is None:
-                parts = [(OP_LT, LONG_MIN)]                    # never (null when the stat is null)
-            else:
-                parts = ([(OP_GE, b[0])] if b[0] > LONG_MIN else []) + ([(OP_LE, b[1])] if b[1] < LONG_MAX else [])
-                parts = parts or [(OP_GE, LONG_MIN)]           # always
-            for k, (cop, v) in enumerate(parts):
-                emit(stat)
-                ops.append((OP_LIT, 0, int(v)))
-                ops.append((cop, 0, 0))
-                if k:
-                    ops.append((OP_AND, 0, 0))
-            return
-        flags = (int(r_nan) << 4) | (int(r_pinf) << 5) | (int(r_ninf) << 6)
-        for k, c in enumerate(conds):
-            emit(stat)
-            if c in (binfloat.ALL, binfloat.NONE):
-                ops.append((OP_FCMP, flags | (FC_ALL if c == binfloat.ALL else FC_NONE), FcmpText(b"", ranks)))
-            else:
-                ops.append((OP_FCMP, flags | _FC_MODE[c[0]],
-                            FcmpText(binfloat.decimal_text(c[1], short=True).encode("ascii"), ranks)))
-            if k:
-                ops.append((OP_AND, 0, 0))
-    emit(node)
-    if len(ops) > MAX_OPS or _stack_depth(ops) > MAX_STACK:
-        raise UnsupportedSkipping("data skipping filter is too large for the device evaluator")
-    return paths, [TYPE_CODE[stat_type(p, leaves)] for p in paths], ops
-
-
-def _float_comparison(n, leaves):
-    return any(operand_type(c, leaves) in FLOATS for c in (n[1], n[2]) if c[0] in ("stat", "lit"))
-
-
-def _operand_kind(n, leaves):
-    if n[0] == "stat":
-        t = stat_type(n[1], leaves)
-        return t if t in ("string", "decimal") else "number"
-    if n[0] == "lit":
-        v = n[1]
-        return None if v is None else "string" if isinstance(v, str) else "decimal" if isinstance(v, _Decimal) else "number"
-    return "number"
 
 
 # ImplicitCastExpression.UP_CASTABLE_TYPE_TABLE (kernel-defaults/.../internal/expressions/
@@ -409,63 +297,3 @@ def check_types(node, leaves):
         check_types(node[2], leaves)
     elif node[0] in _CMP:
         check_comparable(node, leaves)
-
-
-MAX_PATHS, MAX_DEPTH, MAX_OPS, MAX_STACK, NAMES_BYTES = 8, 4, 64, 16, 4096
-
-
-class FcmpText(bytes):
-    """An OP_FCMP threshold (exact decimal text, for a stat read from the JSON) carrying the same
-    comparison as a run of value ranks (binfloat.rank_run, for a typed add.stats_parsed float):
-    pack writes the two ranks as int64s right after the text."""
-
-    def __new__(cls, text, ranks):
-        o = super().__new__(cls, text)
-        o.ranks = tuple(int(x) for x in ranks)
-        return o
-
-
-def _stack_depth(ops):
-    d = hi = 0
-    for op, _, _ in ops:
-        d += 1 if op in (OP_STAT, OP_LIT, OP_LIT_STR, OP_LIT_DEC) else 0 if op in (OP_TIMEADD, OP_FCMP) else -1
-        hi = max(hi, d)
-    return hi
-
-
-def pack(program, struct_type):
-    """Fill a dk_skip_program ctypes struct (include/dkgpu.h) from compile_program's output."""
-    paths, types, ops = program
-    prog = struct_type()
-    names = bytearray()
-    prog.n_paths = len(paths)
-    for i, (p, t) in enumerate(zip(paths, types)):
-        if not 1 <= len(p) <= MAX_DEPTH:
-            raise UnsupportedSkipping("stats field %s is nested deeper than %d" % (".".join(p), MAX_DEPTH))
-        prog.path_type[i] = t
-        prog.path_depth[i] = len(p)
-        for d, comp in enumerate(p):
-            b = comp.encode("utf-8")
-            prog.name_off[i][d] = len(names)
-            prog.name_len[i][d] = len(b)
-            names += b
-    if len(names) > NAMES_BYTES:
-        raise UnsupportedSkipping("stats field names exceed %d bytes" % NAMES_BYTES)
-    packed = []
-    for op, arg, lit in ops:
-        if op in (OP_LIT_STR, OP_LIT_DEC):                   # literal bytes follow the names
-            packed.append((op, len(lit), len(names)))
-            names += lit
-        elif op == OP_FCMP:                                  # flags; threshold text offset | length << 32
-            packed.append((op, arg, len(names) | (len(lit) << 32)))
-            names += lit + struct.pack("<qq", *getattr(lit, "ranks", (1, 0)))
-        else:
-            packed.append((op, arg, lit))
-    if len(names) > NAMES_BYTES:
-        raise UnsupportedSkipping("stats field names and string literals exceed %d bytes" % NAMES_BYTES)
-    from ._lib import put_bytes
-    put_bytes(prog, "names", bytes(names))       # (the rank runs hold NUL bytes)
-    prog.n_ops = len(ops)
-    for k, (op, arg, lit) in enumerate(packed):
-        prog.op[k], prog.arg[k], prog.lit[k] = op, arg, lit
-    return prog

@@ -116,18 +116,19 @@ int  dk_parquet_open_async(dk_engine* e, const char* const* paths, int32_t n_fil
  * columns. Converted per file as ParquetFilterUtils.toParquetFilter does and evaluated per row group
  * with parquet-mr's StatisticsFilter over the footer statistics (ParquetFileReader.java:111-132). */
 typedef struct dk_rg_filter {
-  int32_t n_cols;                  /* <= 8 leaf columns, dotted paths in pool                     */
-  int32_t col_off[8];
-  int32_t col_len[8];
-  int32_t n_ops;                   /* <= 64                                                       */
-  int32_t op[64];                  /* 0 COL(arg) 1 LIT(arg = type: 0 long 1 integer 2 short 3 byte
+  int32_t n_cols;                  /* leaf columns, dotted paths in pool (any number)               */
+  const int32_t* col_off;          /* [n_cols]                                                      */
+  const int32_t* col_len;
+  int32_t n_ops;                   /* any number                                                    */
+  const int32_t* op;               /* [n_ops]: 0 COL(arg) 1 LIT(arg = type: 0 long 1 integer 2 short 3 byte
                                       4 date 5 float 6 double 7 boolean 8 string 9 other; lit = value,
                                       float / double as the bits of a double, string: pool offset |
                                       length << 32) 2 NULL 3 = 4 < 5 <= 6 > 7 >= 8 AND 9 OR 10 NOT
                                       11 IS_NULL 12 IS_NOT_NULL 13 UNSUPPORTED (an unconvertible node) */
-  int32_t arg[64];
-  int64_t lit[64];
-  char pool[2048];
+  const int32_t* arg;
+  const int64_t* lit;
+  const char* pool;
+  int64_t pool_len;
 } dk_rg_filter;
 /* keep[g] = 0 for the row groups of `path` the filter proves empty (filter NULL: keep all). */
 int  dk_parquet_prune_row_groups(const char* path, const dk_rg_filter* filter, uint8_t* keep, int32_t cap,
@@ -266,80 +267,78 @@ int  dk_log_pm_scan(const char* const* paths, int32_t n, int64_t* p_line, int64_
 int  dk_json_tail_column(dk_json_tail* t, const char* leaf, dk_column* out);
 void dk_json_tail_free(dk_json_tail* t);
 
-/* ---- Data skipping (ScanImpl.applyDataSkipping, KA/internal/ScanImpl.java:304-352) ----
- * A skipping predicate compiled by the host planner (delta_amd/skipping.py, restating
- * DataSkippingUtils.constructDataSkippingFilter) into the stats fields to read from each selected
- * row's add.stats JSON and a postfix program over them. A row stays selected iff
- * COALESCE(program(stats), true); null / absent stats keep the row. */
-typedef struct dk_skip_program {
-  int32_t n_paths;                 /* <= 8 stats fields                                        */
-  int32_t path_type[8];            /* 0 long, 1 integer, 2 short, 3 byte, 4 date (epoch days), 5 string,
-                                      6 timestamp (micros since epoch), 7 decimal,
-                                      8 timestamp_ntz (micros, read as UTC), 9 float, 10 double */
-  int32_t path_depth[8];           /* name components, 1..4 ("maxValues","id" -> 2)             */
-  int32_t name_off[8][4];          /* component names: offsets / lengths into names (UTF-8)     */
-  int32_t name_len[8][4];
-  char names[4096];
-  int32_t n_ops;                   /* <= 64                                                     */
-  int32_t op[64];                  /* 0 STAT(arg=path), 1 LIT(arg=1: null), 2 <, 3 <=, 4 >, 5 >=, 6 =, 7 AND, 8 OR,
-                                      9 LIT_STR(UTF-8 bytes names[lit, lit + arg)), 10 TIMEADD(top += lit micros),
-                                      11 LIT_DEC(BigDecimal text names[lit, lit + arg)),
-                                      12 FCMP(pop a float/double stat x; push x <mode> threshold over its
-                                         exact decimal value: arg & 15 = 0 <, 1 <=, 2 >, 3 >=, 4 always,
-                                         5 never; arg bits 4/5/6 = the result for NaN / +Inf / -Inf;
-                                         threshold = names[lit & 0xffffffff, + (lit >> 32)), followed by
-                                         two little-endian int64 (lo, hi): the same comparison as the
-                                         run of the value format's ranks (Float/Double.compare order,
-                                         -0.0 = -1, lo > hi: never) for add.stats_parsed floats) */
-  int32_t arg[64];
-  int64_t lit[64];
-} dk_skip_program;
+/* ---- Predicates: ExpressionHandler.getPredicateEvaluator(inputSchema, predicate) for the two
+ * predicates a scan evaluates (KA/engine/ExpressionHandler.java:58), compiled once on the host into a
+ * device program (no size limits: programs live in device memory, paths / fields go through tables).
+ *  dk_skip_compile: the data-skipping predicate DataSkippingUtils.constructDataSkippingFilter built
+ *    (KA/internal/skipping/DataSkippingUtils.java:156-456) over the pruned stats schema, bare or wrapped
+ *    as ScanImpl wraps it, =(COALESCE(skip, true), ALWAYS_TRUE) (KA/internal/ScanImpl.java:304-352).
+ *    A row stays selected iff COALESCE(skip(stats), true); null / absent stats keep the row.
+ *  dk_part_compile: the partition predicate rewritten over the scan-file schema
+ *    (PartitionUtils.rewritePartitionPredicateOnScanFileSchema, KA/internal/util/PartitionUtils.java:
+ *    324-358: element_at(add.partitionValues, '<physical name>'), inside partition_value(.., '<type>')
+ *    unless the column is a string) as ScanImpl.applyPartitionPruning passes it (:245-294). A row stays
+ *    selected iff the predicate is TRUE.
+ * Both take JSON text (INTEGRATION.md "Predicate JSON"):
+ *   {"col": ["minValues", "id"]}
+ *   {"lit": <value>, "type": "<Kernel type>"}    null value = null literal; long / integer / short / byte,
+ *       date (epoch days), timestamp / timestamp_ntz (micros) as JSON integers; string as a JSON string;
+ *       decimal(p,s) as its BigDecimal text; float / double as "0x<IEEE bits>"; boolean as true / false;
+ *       binary as hex digits
+ *   {"op": "<NAME>", "args": [...]}              AND OR NOT = < <= > >= IS NOT DISTINCT FROM IS_NULL
+ *       IS_NOT_NULL COALESCE ALWAYS_TRUE ALWAYS_FALSE TIMEADD ELEMENT_AT, and
+ *       {"op": "PARTITION_VALUE", "type": "<Kernel type>", "args": [...]}
+ * and the stats schema is Kernel StructType JSON. Status 3: the reference's evaluator throws for this
+ * predicate ("Unsupported expression: ...", DefaultExpressionEvaluator.transformBinaryComparator). */
+typedef struct dk_program dk_program;
+#define DK_PROGRAM_SKIPPING 0
+#define DK_PROGRAM_PARTITION 1
+int  dk_skip_compile(const char* stats_schema_json, const char* predicate_json, dk_program** out);
+int  dk_part_compile(const char* predicate_json, dk_program** out);
+/* JSON description: {"kind", "stack", "paths": [{"type", "path": [...]}] | "fields": [{"type", "name"}],
+ * "ops": [[op, arg, lit], ...], "pool": hex}; returns its length (writes at most cap - 1 bytes + NUL).
+ * The paths are what a caller projects as the typed add.stats_parsed.<path> leaves. */
+int64_t dk_program_describe(const dk_program* p, char* buf, int64_t cap);
+void dk_program_free(dk_program* p);
 
 /* ---- Engine plugin point 1 beyond the ParquetHandler: the data-skipping hooks a
  * stock ScanImpl calls through the Engine (KA/internal/ScanImpl.java:304-352):
  *   JsonHandler.parseJson(statsVector, prunedStatsSchema, selection)   (KA/engine/JsonHandler.java:68-71)
- *     -> dk_json_parse_stats: the stats strings (n rows: offs[n + 1] into chars, isnull / selection one
- *        byte per row or NULL; host memory, or device memory when on_device -- a GPU-decoded
- *        add.stats column) parsed on the GPU with DefaultJsonRow's rules for the schema's stats paths
- *        (a dk_skip_program's path table; its ops are ignored). Unselected and null rows are all-null
- *        rows (DefaultJsonHandler.java:60-76); a row that does not decode fails the call.
+ *     -> dk_json_parse: the stats strings (n rows: offs[n + 1] into chars, isnull / selection one byte
+ *        per row or NULL; host memory, or device memory when on_device -- a GPU-decoded add.stats
+ *        column) parsed on the GPU with DefaultJsonRow's rules (KD/internal/data/DefaultJsonRow.java:
+ *        136-357) for every leaf of the output schema (Kernel StructType JSON; any number of leaves of
+ *        the stats types long, integer, short, byte, date, timestamp, timestamp_ntz, string, decimal,
+ *        float, double). Unselected and null rows are all-null rows (DefaultJsonHandler.java:60-76); a
+ *        row that does not decode fails the call.
+ *     -> dk_parsed_column_get: one leaf as a typed column with validity (host memory, valid until
+ *        dk_parsed_free), leaves in schema order (dk_parsed_leaf_path: the leaf's names as JSON).
  *   ExpressionHandler.getPredicateEvaluator(prunedStatsSchema, COALESCE(skip, true)).eval(parsed, sel)
  *                                                                       (KA/engine/ExpressionHandler.java:58)
- *     -> dk_parsed_stats_eval: the program over the parsed rows, ANDed into the selection in place
- *        (DefaultPredicateEvaluator.java:42-72); its stats paths must be the parsed schema's.
- * dk_parsed_stats_column hands one path back as (present, value) per row: integral / date (epoch
- * days) / timestamp (micros) values, or for string / decimal / float / double the token's span in the
- * row's string (offset | length << 32; bit 62: escaped string, or a float special value code). */
-typedef struct dk_parsed_stats dk_parsed_stats;
-int  dk_json_parse_stats(dk_engine* e, const dk_skip_program* schema, int64_t n, const int64_t* offs,
-                         const uint8_t* chars, const uint8_t* isnull, const uint8_t* selection, int32_t on_device,
-                         dk_parsed_stats** out);
-int  dk_parsed_stats_column(dk_parsed_stats* ps, int32_t path, int64_t* values, uint8_t* present);
-int  dk_parsed_stats_eval(dk_parsed_stats* ps, const dk_skip_program* prog, uint8_t* selection);
-void dk_parsed_stats_free(dk_parsed_stats* ps);
-
-/* Partition-pruning program (ScanImpl.applyPartitionPruning, ScanImpl.java:247-294): the predicate on
- * partition columns, rewritten over the scan file's partitionValues map
- * (PartitionUtils.rewritePartitionPredicateOnScanFileSchema, PartitionUtils.java:324-358), in postfix.
- * A row stays selected iff the predicate is TRUE (null and false drop it). */
-typedef struct dk_part_program {
-  int32_t n_fields;                /* <= 8 partition columns                                      */
-  int32_t field_type[8];           /* 0 long, 1 integer, 2 short, 3 byte, 4 string, 5 date, 6 decimal,
-                                      7 boolean, 8 float, 9 double, 10 timestamp / timestamp_ntz
-                                      (java.sql.Timestamp.valueOf, fields read as UTC) */
-  int32_t name_off[8];             /* physical column name (map key): offset / length in pool      */
-  int32_t name_len[8];
-  int32_t n_ops;                   /* <= 64                                                       */
-  int32_t op[64];                  /* 0 FIELD(arg) 1 LIT_INT(lit) 2 LIT_STR(pool[lit], arg bytes) 3 LIT_NULL
-                                      4 < 5 <= 6 > 7 >= 8 = 9 IS NOT DISTINCT FROM 10 IS_NULL
-                                      11 IS_NOT_NULL 12 NOT 13 AND 14 OR
-                                      15 LIT_DEC(BigDecimal text pool[lit], arg bytes)
-                                      16 FCMP(pop a float/double field; as dk_skip_program's FCMP,
-                                         threshold pool[lit & 0xffffffff, + (lit >> 32)))          */
-  int32_t arg[64];
-  int64_t lit[64];
-  char pool[4096];
-} dk_part_program;
+ *     -> dk_parsed_eval: a dk_skip_compile program over the parsed rows on the GPU, ANDed into the
+ *        selection in place (DefaultPredicateEvaluator.java:42-72); its stats paths must be leaves of
+ *        the parsed schema. */
+typedef struct dk_parsed dk_parsed;
+typedef struct dk_parsed_column {
+  int32_t type;            /* 0 long, 1 integer, 2 short, 3 byte, 4 date, 5 string, 6 timestamp, 7 decimal,
+                              8 timestamp_ntz, 9 float, 10 double                                    */
+  int64_t n;
+  const uint8_t* validity; /* one byte per row: 1 = non-null                                         */
+  const int64_t* values;   /* integral / date (epoch days) / timestamp(_ntz) (micros); float / double:
+                              IEEE bits; decimal: the low 64 bits of the unscaled value                */
+  const int64_t* values_hi;/* decimal: the high 64 bits of the (two's complement) unscaled value     */
+  const int32_t* scale;    /* decimal: BigDecimal scale per row                                      */
+  const uint8_t* wide;     /* decimal: 1 where the unscaled value needs more than 127 bits (use the text) */
+  const int32_t* offs;     /* string (unescaped UTF-8) / decimal (the number token): n + 1 offsets     */
+  const uint8_t* chars;
+} dk_parsed_column;
+int  dk_json_parse(dk_engine* e, const char* schema_json, int64_t n, const int64_t* offs, const uint8_t* chars,
+                   const uint8_t* isnull, const uint8_t* selection, int32_t on_device, dk_parsed** out);
+int32_t dk_parsed_num_leaves(const dk_parsed* ps);
+int64_t dk_parsed_leaf_path(const dk_parsed* ps, int32_t leaf, char* buf, int64_t cap);
+int  dk_parsed_column_get(dk_parsed* ps, int32_t leaf, dk_parsed_column* out);
+int  dk_parsed_eval(dk_parsed* ps, const dk_program* prog, uint8_t* selection);
+void dk_parsed_free(dk_parsed* ps);
 
 /* ---- Replay: reconcile the tail and the checkpoint files on the GPU ----
  * ckpt may be NULL (no checkpoint). Checkpoint files are given in replay order (multi-part:
@@ -349,18 +348,19 @@ int  dk_replay_create(dk_engine* e, dk_json_tail* tail, dk_parquet* ckpt, dk_rep
  * table, key table inputs) -- e.g. while the checkpoint files are still being opened -- and this
  * attaches the checkpoint afterwards (once per replay). */
 int  dk_replay_attach_checkpoint(dk_replay* r, dk_parquet* ckpt);
-/* install (prog != NULL) or clear the data-skipping program applied after reconciliation; the
- * tail must have been parsed with stats and the checkpoint projection must include add.stats */
-int  dk_replay_set_skipping(dk_replay* r, const dk_skip_program* prog);
+/* install (prog != NULL, a dk_skip_compile program; copied) or clear the data-skipping program applied
+ * after reconciliation; the tail must have been parsed with stats and the checkpoint projection must
+ * include add.stats */
+int  dk_replay_set_skipping(dk_replay* r, const dk_program* prog);
 /* Checkpoint files whose skipping reads the typed add.stats_parsed columns instead of the add.stats
  * JSON: those where every program path is an integral / date stat whose leaf
  * add.stats_parsed.<path> was projected (INT64 for long, INT32 otherwise). The predicate is the same;
  * the columns are Spark's from_json(stats) (JsonHandler.parseJson hook), so the
  * selection equals the JSON path's. DK_NO_STATS_PARSED=1 turns it off. */
 int  dk_replay_stats_parsed_files(dk_replay* r);
-/* install (prog != NULL) or clear the partition-pruning program, applied before data skipping; the
- * checkpoint projection must include add.partitionValues */
-int  dk_replay_set_partition_filter(dk_replay* r, const dk_part_program* prog);
+/* install (prog != NULL, a dk_part_compile program; copied) or clear the partition-pruning program,
+ * applied before data skipping; the checkpoint projection must include add.partitionValues */
+int  dk_replay_set_partition_filter(dk_replay* r, const dk_program* prog);
 int  dk_replay_run(dk_replay* r);                      /* async: key build, probe, decode */
 /* The same run with the checkpoint files in n_groups groups, each decoded, probed, filtered and its
  * selections copied to host memory in turn, so that ScanImpl.getScanFiles' batches can be handed

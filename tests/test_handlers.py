@@ -1,14 +1,18 @@
 """Engine plugin point 1 beyond the ParquetHandler (delta_amd/handlers.py over
-dk_json_parse_stats / dk_parsed_stats_eval): JsonHandler.parseJson of stats strings and the
-data-skipping PredicateEvaluator, as a stock ScanImpl.applyDataSkipping calls them
-(kernel-api/.../internal/ScanImpl.java:304-352), on the GPU.
+dk_json_parse / dk_parsed_column_get / dk_parsed_eval and dk_skip_compile): JsonHandler.parseJson of
+stats strings into the pruned stats schema's typed columns and the data-skipping PredicateEvaluator,
+as a stock ScanImpl.applyDataSkipping calls them (kernel-api/.../internal/ScanImpl.java:304-352), on
+the GPU.
 
 Each case is one of test_skipping.py's stats edge sets (integral / date / string / timestamp /
-decimal / float stats, escapes, duplicates, nulls) with its predicates. The oracle answers per row:
-unselected -> not selected; null stats -> kept; else oracle/skipping.keep with the oracle's own
-skipping predicate (oracle/skipping_filter.py). Parsed integral / date values are compared with the
-oracle's decode_stats. Decode errors fail the parse."""
+decimal / float stats, escapes, duplicates, nulls, NaN / +-Infinity) with its predicates. The oracle
+answers per row: unselected -> not selected; null stats -> kept; else oracle/skipping.keep with the
+oracle's own skipping predicate (oracle/skipping_filter.py). EVERY parsed column (every leaf of the
+pruned stats schema, every type) equals oracle/skipping.decode_stats of the row. Decode errors fail
+the parse."""
 import json
+import math
+import struct
 
 import numpy as np
 import pytest
@@ -23,7 +27,9 @@ def _schema(columns):
 
 
 def _plans(columns, predicate):
-    """(product program, oracle node, oracle types) for predicate over a table of `columns`."""
+    """(product program, pruned stats schema, oracle node, oracle types) for predicate over a table
+    of `columns`."""
+    from delta_amd import programs
     from oracle import skipping_filter as osf
     schema = _schema(columns)
     leaves = sk.data_schema_leaves(schema, [])
@@ -31,11 +37,24 @@ def _plans(columns, predicate):
     if node is None:
         return None
     sk.check_types(node, leaves)
-    prog = sk.compile_program(node, leaves)
+    prog = programs.compile_skipping(node, leaves)
+    stats_schema = programs.pruned_stats_schema(node, leaves)
     S = osf.StatsSchema(schema, [])
     onode = osf.build(predicate, S)
     osf.check(onode, S)
-    return prog, onode, osf.stat_types(onode, S)
+    return prog, stats_schema, onode, osf.stat_types(onode, S)
+
+
+def _same(a, b):
+    """Parsed value == oracle value (floats by Float.compare identity: NaN == NaN, -0.0 != 0.0;
+    decimals by value and scale)."""
+    if a is None or b is None:
+        return a is None and b is None
+    if isinstance(b, float):
+        return (a != a and b != b) or (a == b and math.copysign(1, a) == math.copysign(1, b))
+    if hasattr(b, "as_tuple"):
+        return a == b and a.as_tuple().exponent == b.as_tuple().exponent
+    return a == b
 
 
 CASES = [
@@ -65,29 +84,103 @@ def test_gpu_parse_json_and_predicate_evaluator(ci):
     eng = K.GpuEngine()
     rng = np.random.default_rng(ci)
     rows = list(stats) * 3
+    checked = 0
     for p in preds:
-        prog, onode, otypes = _plans(columns, p)
+        prog, schema, onode, otypes = _plans(columns, p)
         for trial in range(2):
             sel = np.ones(len(rows), bool) if trial == 0 else rng.random(len(rows)) < 0.6
-            parsed = GpuJsonHandler(eng).parseJson(rows, prog, sel)
+            parsed = GpuJsonHandler(eng).parseJson(rows, schema, sel)
             got = GpuPredicateEvaluator(eng, prog).eval(parsed, sel)
             want = [bool(s) and osk.keep(st, onode, otypes) for st, s in zip(rows, sel)]
             assert list(got) == want, (p, trial)
-            # parsed integral / date / timestamp values equal the oracle's decoded stats
-            paths, types = prog[0], prog[1]
-            for pi, (path, t) in enumerate(zip(paths, types)):
-                if t not in (0, 1, 2, 3, 4, 6, 8):
-                    continue
-                vals, pres = parsed.column(pi)
+            # every parsed column equals the oracle's decoded stats
+            assert sorted(parsed.leaves) == sorted(otypes), (parsed.leaves, otypes)
+            for path in parsed.leaves:
+                vals = parsed.values(path)
                 for r, st in enumerate(rows):
-                    if not sel[r] or st is None:
-                        assert not pres[r]
-                        continue
-                    want_v = osk.decode_stats(st, {path: otypes.get(path, "long")}).get(path) \
-                        if path in otypes else None
-                    if path in otypes:
-                        assert (want_v is None and not pres[r]) or (pres[r] and vals[r] == want_v), (path, r, st)
+                    want_v = None if (not sel[r] or st is None) else osk.decode_stats(st, {path: otypes[path]})[path]
+                    assert _same(vals[r], want_v), (path, r, st, vals[r], want_v)
+                    checked += 1
             parsed.close()
+    assert checked > 0
+    eng.close()
+
+
+def _wide_rows(n, n_cols, seed):
+    rng = np.random.default_rng(seed)
+    rows = []
+    for r in range(n):
+        if r % 17 == 5:
+            rows.append(None)
+            continue
+        st = {"numRecords": int(rng.integers(1, 1000)), "minValues": {}, "maxValues": {}, "nullCount": {}}
+        for c in range(n_cols):
+            if rng.random() < 0.1:
+                continue                                    # a missing stat: null
+            lo = int(rng.integers(-1000, 1000))
+            st["minValues"]["c%d" % c] = lo
+            st["maxValues"]["c%d" % c] = lo + int(rng.integers(0, 500))
+            st["nullCount"]["c%d" % c] = int(rng.integers(0, 3))
+        rows.append(json.dumps(st))
+    return rows
+
+
+@pytest.mark.gpu
+def test_gpu_parse_json_wide_schema():
+    """A pruned stats schema of 12 columns (37 leaves: past one 32-path extraction window and the
+    8-path register set) and an OR of 32 equalities over them: every parsed column and the evaluator's
+    selection equal the oracle."""
+    from delta_amd import kernel as K
+    from delta_amd.expressions import Column, Literal, Predicate
+    from delta_amd.handlers import GpuJsonHandler, GpuPredicateEvaluator
+    from oracle import skipping as osk
+    columns = [("c%d" % i, "long") for i in range(12)]
+    pred = Predicate("=", Column("c0"), Literal.ofLong(3))
+    for k in range(1, 32):
+        pred = Predicate("OR", pred, Predicate("=", Column("c%d" % (k % 12)), Literal.ofLong(k * 37 - 500)))
+    pred = Predicate("AND", pred, Predicate("IS_NOT_NULL", Column("c11")))
+    prog, schema, onode, otypes = _plans(columns, pred)
+    assert len(prog.paths) > 32
+    eng = K.GpuEngine()
+    rows = _wide_rows(3000, 12, 3)
+    sel = np.random.default_rng(4).random(len(rows)) < 0.8
+    parsed = GpuJsonHandler(eng).parseJson(rows, schema, sel)
+    got = GpuPredicateEvaluator(eng, prog).eval(parsed, sel)
+    want = [bool(s) and osk.keep(st, onode, otypes) for st, s in zip(rows, sel)]
+    assert list(got) == want
+    assert 0 < sum(want) < len(rows)
+    for path in parsed.leaves:
+        vals = parsed.values(path)
+        for r, st in enumerate(rows):
+            want_v = None if (not sel[r] or st is None) else osk.decode_stats(st, {path: otypes[path]})[path]
+            assert vals[r] == want_v, (path, r)
+    parsed.close()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_expression_handler_json_predicate():
+    """GpuExpressionHandler.getPredicateEvaluator takes ScanImpl's filterToEval as predicate JSON
+    (=(COALESCE(skip, true), ALWAYS_TRUE)) over the pruned stats schema JSON, as the JNI side passes
+    them (INTEGRATION.md)."""
+    from delta_amd import kernel as K
+    from delta_amd import programs
+    from delta_amd.handlers import GpuExpressionHandler, GpuJsonHandler
+    from oracle import skipping as osk
+    columns, stats, preds = CASES[0]
+    eng = K.GpuEngine()
+    for p in preds[:4]:
+        prog, schema, onode, otypes = _plans(columns, p)
+        leaves = sk.data_schema_leaves(_schema(columns), [])
+        node = sk.construct(p, leaves)
+        filter_to_eval = {"op": "=", "args": [{"op": "COALESCE", "args": [programs.skipping_node_json(node),
+                                                                         {"lit": True, "type": "boolean"}]},
+                                              {"op": "ALWAYS_TRUE", "args": []}]}
+        ev = GpuExpressionHandler(eng).getPredicateEvaluator(json.dumps(schema), json.dumps(filter_to_eval))
+        parsed = GpuJsonHandler(eng).parseJson(list(stats), schema)
+        got = ev.eval(parsed)
+        assert list(got) == [osk.keep(st, onode, otypes) for st in stats], p
+        parsed.close()
     eng.close()
 
 
@@ -98,10 +191,10 @@ def test_gpu_parse_json_decode_errors():
     from delta_amd._lib import DkError
     from delta_amd.handlers import GpuJsonHandler
     eng = K.GpuEngine()
-    prog = _plans((("x", "short"), ("id", "long")), T.BAD_PREDICATE)[0]
+    schema = _plans((("x", "short"), ("id", "long")), T.BAD_PREDICATE)[1]
     for bad in T.BAD_STATS:
         with pytest.raises(DkError, match="Parsing the JSON statistics"):
-            GpuJsonHandler(eng).parseJson([T.EDGE_STATS[0], bad], prog)
+            GpuJsonHandler(eng).parseJson([T.EDGE_STATS[0], bad], schema)
         # an unselected bad row is never parsed
-        GpuJsonHandler(eng).parseJson([T.EDGE_STATS[0], bad], prog, np.array([True, False])).close()
+        GpuJsonHandler(eng).parseJson([T.EDGE_STATS[0], bad], schema, np.array([True, False])).close()
     eng.close()

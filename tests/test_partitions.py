@@ -54,32 +54,56 @@ def test_partition_fields_and_compile():
         {"name": "x", "type": "long", "metadata": {}}]})
     f = pp.partition_fields(schema, ["p", "S", "d"])
     assert f == {"p": ("integer", "col-p"), "s": ("string", "s"), "d": ("date", "d")}
-    flist, ops, pool = pp.compile_program(And(cmp(">=", col("P"), Literal.ofInt(3)),
-                                              cmp("=", col("s"), Literal.ofString("a b"))), f)
-    assert [pool[o:o + n] for o, n, _ in flist] == [b"col-p", b"s"] and [t for _, _, t in flist] == [1, 4]
-    assert [o[0] for o in ops] == [pp.PO_FIELD, pp.PO_LIT_INT, pp.PO_GE, pp.PO_FIELD, pp.PO_LIT_STR, pp.PO_EQ,
-                                   pp.PO_AND]
-    flist, ops, _ = pp.compile_program(cmp("<", col("d"), Literal.ofDate(10957)), f)
-    assert [t for _, _, t in flist] == [5] and ops[1] == (pp.PO_LIT_INT, 0, 10957)
+    d = _describe(And(cmp(">=", col("P"), Literal.ofInt(3)), cmp("=", col("s"), Literal.ofString("a b"))), f)
+    assert [x["name"] for x in d["fields"]] == ["col-p", "s"] and [x["type"] for x in d["fields"]] == [1, 4]
+    assert [o[0] for o in d["ops"]] == [PO_FIELD, PO_LIT_INT, PO_GE, PO_FIELD, PO_LIT_STR, PO_EQ, PO_AND]
+    d = _describe(cmp("<", col("d"), Literal.ofDate(10957)), f)
+    assert [x["type"] for x in d["fields"]] == [5] and d["ops"][1] == [PO_LIT_INT, 0, 10957]
     # differently typed operands without an up-cast throw, as transformBinaryComparator does
     for bad in (cmp("=", col("d"), Literal.ofInt(1)), cmp("=", col("s"), Literal.ofInt(1)),
                 cmp("=", col("d"), Literal.ofString("2000-01-01")), cmp("=", col("p"), Literal.ofNull("string"))):
         with pytest.raises(sk.UnsupportedExpression, match="not comparable"):
-            pp.compile_program(bad, f)
-    pp.compile_program(cmp("=", col("p"), Literal.ofLong(1)), f)          # integer -> long up-cast
-    with pytest.raises(pp.UnsupportedPartitionFilter):
-        pp.compile_program(Predicate("STARTS_WITH", col("s"), Literal.ofString("a")), f)
+            _describe(bad, f)
+    _describe(cmp("=", col("p"), Literal.ofLong(1)), f)                # integer -> long up-cast
     with pytest.raises(ValueError):
-        pp.compile_program(cmp("=", col("zz"), Literal.ofInt(1)), f)
+        _describe(cmp("=", col("zz"), Literal.ofInt(1)), f)
+    # COALESCE / ALWAYS_TRUE / ALWAYS_FALSE compile; a predicate the device does not evaluate is refused
+    _describe(Predicate("COALESCE", cmp("=", col("p"), Literal.ofInt(1)), Predicate("ALWAYS_FALSE")), f)
+    with pytest.raises(pp.UnsupportedPartitionFilter):
+        _describe(Predicate("LIKE", col("s"), Literal.ofString("a%")), f)
 
 
-def test_pack_layout():
-    import ctypes
-    from delta_amd._lib import dk_part_program
-    assert ctypes.sizeof(dk_part_program) == 4 + 32 * 3 + 4 + 256 + 256 + 512 + 4096
-    f = {"p": ("integer", "p")}
-    prog = pp.pack(pp.compile_program(Predicate("IS_NULL", col("p")), f), dk_part_program)
-    assert prog.n_fields == 1 and prog.n_ops == 2 and bytes(prog.pool)[:1] == b"p"
+(PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LT, PO_LE, PO_GT, PO_GE, PO_EQ, PO_NSEQ, PO_ISNULL,
+ PO_ISNOTNULL, PO_NOT, PO_AND, PO_OR, PO_LIT_DEC, PO_FCMP, PO_COALESCE) = range(18)
+
+
+def _describe(pred, fields):
+    from delta_amd import programs
+    return programs.compile_partition(pred, fields).describe()
+
+
+def test_program_unbounded():
+    """No size caps: 40 partition columns, an OR of 300 equalities (re-associated under the device
+    stack), a 10 KiB string literal."""
+    f = {"c%d" % i: ("integer", "c%d" % i) for i in range(40)}
+    f["s"] = ("string", "s")
+    big = Predicate("AND", cmp(">=", col("c0"), Literal.ofInt(0)), cmp("=", col("c39"), Literal.ofInt(5)))
+    for i in range(1, 39):
+        big = Predicate("AND", big, cmp("<", col("c%d" % i), Literal.ofInt(i)))
+    d = _describe(big, f)
+    assert len(d["fields"]) == 40 and d["stack"] <= 32
+    ors = cmp("=", col("c1"), Literal.ofInt(0))
+    for i in range(1, 300):
+        ors = Predicate("OR", ors, cmp("=", col("c1"), Literal.ofInt(i)))
+    d = _describe(ors, f)
+    assert d["stack"] <= 32 and sum(o[0] == PO_OR for o in d["ops"]) == 299
+    right = cmp("=", col("c1"), Literal.ofInt(0))
+    for i in range(1, 300):                                    # right-deep: balanced by the compiler
+        right = Predicate("OR", cmp("=", col("c1"), Literal.ofInt(i)), right)
+    assert _describe(right, f)["stack"] <= 32
+    lit = "x" * 10240
+    d = _describe(cmp("=", col("s"), Literal.ofString(lit)), f)
+    assert bytes.fromhex(d["pool"]).find(lit.encode()) >= 0
 
 
 # ---------------------------------------------------------------- oracle (cross-checked)

@@ -190,35 +190,56 @@ def test_comparator_types(coltype, lit, ok):
             sk.check_types(node, leaves)
 
 
+def _compiled(node, leaves):
+    """dk_skip_compile of a constructed predicate (delta_amd/programs.py) as (paths, type codes, ops)
+    with each op's literal bytes decoded from the program's pool: (op, arg, lit, bytes | None, ranks | None)."""
+    import struct
+    from delta_amd import programs
+    d = programs.compile_skipping(node, leaves).describe()
+    pool = bytes.fromhex(d["pool"])
+    ops = []
+    for op, arg, lit in d["ops"]:
+        if op in (sk.OP_LIT_STR, sk.OP_LIT_DEC):
+            ops.append((op, arg, lit, pool[lit:lit + arg], None))
+        elif op == sk.OP_FCMP:
+            off, ln = lit & 0xffffffff, lit >> 32
+            ops.append((op, arg, lit, pool[off:off + ln], struct.unpack("<qq", pool[off + ln:off + ln + 16])))
+        else:
+            ops.append((op, arg, lit, None, None))
+    return [tuple(p["path"]) for p in d["paths"]], [p["type"] for p in d["paths"]], ops
+
+
 def test_compile_refuses_unsupported():
+    """The compiler behind the C ABI (dk_skip_compile) applies transformBinaryComparator's type check
+    itself (status 3 -> UnsupportedExpression), and compiles an equality to min <= v AND max >= v."""
     leaves = {("f",): ("float", ("f",)), ("s",): ("string", ("s",)), ("a",): ("long", ("a",))}
     for p in (cmp("=", col("s"), Literal.ofInt(1)), cmp("=", col("a"), Literal.ofString("1"))):
         node = sk.construct(p, leaves)
         assert node is not None
-        with pytest.raises(sk.UnsupportedSkipping):
-            sk.compile_program(node, leaves)
+        with pytest.raises(sk.UnsupportedExpression, match="operands are of different types"):
+            _compiled(node, leaves)
     node = sk.construct(cmp("=", col("a"), Literal.ofLong(3)), leaves)
-    paths, types, ops = sk.compile_program(node, leaves)
+    paths, types, ops = _compiled(node, leaves)
     assert paths == [("minValues", "a"), ("maxValues", "a")] and types == [0, 0]
     assert [o[0] for o in ops] == [sk.OP_STAT, sk.OP_LIT, sk.OP_LE, sk.OP_STAT, sk.OP_LIT, sk.OP_GE, sk.OP_AND]
 
 
 def test_compile_float_comparisons():
-    """Float / double comparisons compile to exact thresholds (delta_amd/binfloat.py): a float stat
-    gets OP_FCMP against the rounding-cell edge, an integral stat widened to float integer bounds."""
+    """Float / double comparisons compile to exact thresholds: a float stat gets OP_FCMP against the
+    rounding-cell edge, an integral stat widened to float integer bounds."""
     leaves = {("f",): ("float", ("f",)), ("a",): ("long", ("a",)), ("d",): ("double", ("d",))}
-    paths, types, ops = sk.compile_program(sk.construct(cmp("<", col("f"), Literal.ofFloat(1.5)), leaves), leaves)
+    paths, types, ops = _compiled(sk.construct(cmp("<", col("f"), Literal.ofFloat(1.5)), leaves), leaves)
     assert types == [9] and [o[0] for o in ops] == [sk.OP_STAT, sk.OP_FCMP]
     # round_float(x) < 1.5f  <=>  x < 1.5 - 2^-24 (the tie goes to the even neighbour 1.5)
-    assert ops[1][1] & 15 == sk.FC_LT and ops[1][2] == b"1.499999940395355224609375"
+    assert ops[1][1] & 15 == sk.FC_LT and ops[1][3] == b"1.499999940395355224609375"
     assert ops[1][1] >> 4 == 0b100                       # NaN: false, +Inf: false, -Inf: true
     # long column = float literal 2^24 + 1 (stored as 16777216f): min <= V holds for the longs that
     # round to at most 16777216f (x <= 16777217, the tie rounds to even), max >= V for x >= 16777216
-    _, _, ops = sk.compile_program(sk.construct(cmp("=", col("a"), Literal.ofFloat(16777217)), leaves), leaves)
+    _, _, ops = _compiled(sk.construct(cmp("=", col("a"), Literal.ofFloat(16777217)), leaves), leaves)
     assert [(o[0], o[2]) for o in ops if o[0] in (sk.OP_LIT, sk.OP_LE, sk.OP_GE)] == \
         [(sk.OP_LIT, 16777217), (sk.OP_LE, 0), (sk.OP_LIT, 16777216), (sk.OP_GE, 0)]
     # double column vs NaN literal: < holds for every non-NaN value
-    _, _, ops = sk.compile_program(sk.construct(cmp("<", col("d"), Literal.ofDouble(float("nan"))), leaves), leaves)
+    _, _, ops = _compiled(sk.construct(cmp("<", col("d"), Literal.ofDouble(float("nan"))), leaves), leaves)
     assert ops[1][0] == sk.OP_FCMP and ops[1][1] & 15 == sk.FC_ALL and ops[1][1] >> 4 == 0b110
 
 
@@ -242,17 +263,11 @@ def test_oracle_date_decoding_rules():
             osk.decode_stats(bad, t)
 
 
-def test_pack_layout():
-    from delta_amd._lib import dk_skip_program
-    import ctypes
-    assert ctypes.sizeof(dk_skip_program) == 4 + 32 + 32 + 128 + 128 + 4096 + 4 + 256 + 256 + 512
+def test_program_paths():
+    """A nested column-mapped stats path keeps its physical components (the add.stats_parsed leaf)."""
     leaves = {("s", "x"): ("short", ("col-s", "col-x"))}
-    prog = sk.pack(sk.compile_program(sk.construct(cmp(">", col("s", "x") if False else Column("s", "x"),
-                                                       Literal.ofShort(3)), leaves), leaves), dk_skip_program)
-    assert prog.n_paths == 1 and prog.path_depth[0] == 3 and prog.path_type[0] == 2
-    names = bytes(prog.names)
-    assert [names[prog.name_off[0][d]:prog.name_off[0][d] + prog.name_len[0][d]] for d in range(3)] == \
-        [b"maxValues", b"col-s", b"col-x"]
+    paths, types, _ = _compiled(sk.construct(cmp(">", Column("s", "x"), Literal.ofShort(3)), leaves), leaves)
+    assert paths == [("maxValues", "col-s", "col-x")] and types == [2]
 
 
 # ---------------------------------------------------------------- oracle (pinned to the reference)
@@ -1018,7 +1033,7 @@ def test_rank_run_matches_java_compare():
     import random
     import struct
     from fractions import Fraction
-    from delta_amd import binfloat as bf
+    from tests import binfloat_ref as bf
     rnd = random.Random(5)
     for fmt, pk, bits_n in (("float", "<f", 32), ("double", "<d", 64)):
         specials = [0.0, -0.0, 1.5, -1.5, float("inf"), float("-inf"), float("nan"), 16777216.0, 0.1, 1e-45, 5e-324]
@@ -1047,23 +1062,13 @@ def test_rank_run_matches_java_compare():
                     assert (a <= bf.rank(bits, fmt) <= b) == want, (fmt, lit_type, lit, op, x)
 
 
-def test_pack_keeps_rank_bytes():
+def test_program_keeps_rank_bytes():
     """The FCMP threshold text is followed by its rank run (two int64s, NUL bytes included) in the
-    packed names (a ctypes char-array assignment would stop at the first NUL)."""
-    import ctypes as C
-    import struct
-    from delta_amd import _lib
+    program's pool."""
     leaves = {("f",): ("float", ("f",))}
-    prog = sk.compile_program(sk.construct(cmp("=", col("f"), Literal.ofFloat(0.0)), leaves), leaves)
-    p = sk.pack(prog, _lib.dk_skip_program)
-    names = C.string_at(C.addressof(p) + type(p).names.offset, 4096)
-    for k in range(p.n_ops):
-        if p.op[k] == sk.OP_FCMP:
-            off, ln = p.lit[k] & 0xffffffff, p.lit[k] >> 32
-            assert struct.unpack("<qq", names[off + ln:off + ln + 16]) == prog[2][k][2].ranks
+    _, _, ops = _compiled(sk.construct(cmp("=", col("f"), Literal.ofFloat(0.0)), leaves), leaves)
     # min <= 0.0f: every rank up to +0.0 (-0.0 included); max >= 0.0f: from +0.0 (Float.compare: -0.0 < 0.0)
-    assert [prog[2][k][2].ranks for k in range(p.n_ops) if p.op[k] == sk.OP_FCMP] == \
-        [(-0x7f800001, 0), (0, 0x7f800000)]
+    assert [o[4] for o in ops if o[0] == sk.OP_FCMP] == [(-0x7f800001, 0), (0, 0x7f800000)]
 
 
 # ---------------------------------------------------------------- planner vs the oracle's own restatement
