@@ -106,7 +106,8 @@ class ParsedBatch:
                     out.append(Decimal(bytes(c["chars"][c["offs"][r]:c["offs"][r + 1]]).decode()))
                 else:
                     u = (int(c["hi"][r]) << 64) | (int(c["values"][r]) & ((1 << 64) - 1))
-                    out.append(Decimal(u).scaleb(-int(c["scale"][r])))
+                    digits = tuple(int(d) for d in str(abs(u)))     # exact: no context rounding
+                    out.append(Decimal((1 if u < 0 else 0, digits, -int(c["scale"][r]))))
             elif t == "float":
                 out.append(struct.unpack("<f", struct.pack("<I", int(c["values"][r]) & 0xffffffff))[0])
             elif t == "double":

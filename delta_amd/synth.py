@@ -654,8 +654,8 @@ def _typed_value(rng, name, n_ts):
     import decimal
     if rng.random() < 0.05:
         return None
-    if name == "l":
-        v = int(rng.integers(-10 ** 6, 10 ** 6)) * 1_000_003
+    if name == "l" or name.startswith("x"):
+        v = int(rng.integers(-10 ** 6, 10 ** 6)) * 1_000_003 if name == "l" else int(rng.integers(-200, 200))
         return str(v), v
     if name == "i":
         v = int(rng.integers(-(1 << 31), 1 << 31))
@@ -700,7 +700,7 @@ def _typed_value(rng, name, n_ts):
     return repr(v), v
 
 
-def write_typed_stats_table(root, n=3000, seed=7, ts_unit="us", n_tail=40):
+def write_typed_stats_table(root, n=3000, seed=7, ts_unit="us", n_tail=40, extra_long=0):
     """A table whose checkpoint adds carry add.stats (Delta's JSON) and add.stats_parsed (Spark's
     from_json(stats): the same values, typed) for every stats type of TYPED_STATS_COLUMNS: long, int,
     date, timestamp / timestamp_ntz (INT64 ``ts_unit`` "us" or "ms", or INT96 for "int96"), string
@@ -708,21 +708,24 @@ def write_typed_stats_table(root, n=3000, seed=7, ts_unit="us", n_tail=40):
     -0.0, which Kernel reads from "-0.0" as +0.0). Some rows have JSON stats and a null stats_parsed,
     some a null JSON and typed stats (the reference reads only the JSON: kept), some neither. A
     commit after the checkpoint adds ``n_tail`` files with JSON stats and removes a few. Returns
-    {column: [typed min values]} for building predicates."""
+    {column: [typed min values]} for building predicates. extra_long: that many more long columns
+    x0, x1, ... with small values (wide filters)."""
     import decimal
     rng = np.random.default_rng(seed)
     log = os.path.join(root, "_delta_log")
     os.makedirs(log, exist_ok=True)
-    names = [c for c, _ in TYPED_STATS_COLUMNS]
+    columns = list(TYPED_STATS_COLUMNS) + [("x%d" % k, "long") for k in range(extra_long)]
+    names = [c for c, _ in columns]
     unit = "us" if ts_unit == "int96" else ts_unit
     typ = {"l": pa.int64(), "i": pa.int32(), "d": pa.date32(), "ts": pa.timestamp(unit, tz="UTC"),
            "tz": pa.timestamp(unit), "s": STR, "dc": pa.decimal128(12, 2), "dd": pa.decimal128(6, 1),
            "f": pa.float32(), "g": pa.float64()}
+    typ.update({"x%d" % k: pa.int64() for k in range(extra_long)})
     vals_t = pa.struct([(c, typ[c]) for c in names])
     nc_t = pa.struct([(c, pa.int64()) for c in names])
     sp_t = pa.struct([("numRecords", pa.int64()), ("minValues", vals_t), ("maxValues", vals_t), ("nullCount", nc_t)])
     schema = {"type": "struct", "fields": [{"name": c, "type": t, "nullable": True, "metadata": {}}
-                                           for c, t in TYPED_STATS_COLUMNS]}
+                                           for c, t in columns]}
     proto = {"minReaderVersion": 1, "minWriterVersion": 2}
     meta = {"id": "typed-stats", "format": {"provider": "parquet", "options": {}},
             "schemaString": json.dumps(schema), "partitionColumns": [], "configuration": {}, "createdTime": 0}

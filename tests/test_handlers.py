@@ -138,7 +138,8 @@ def test_gpu_parse_json_wide_schema():
     pred = Predicate("=", Column("c0"), Literal.ofLong(3))
     for k in range(1, 32):
         pred = Predicate("OR", pred, Predicate("=", Column("c%d" % (k % 12)), Literal.ofLong(k * 37 - 500)))
-    pred = Predicate("AND", pred, Predicate("IS_NOT_NULL", Column("c11")))
+    for i in range(12):                                  # + nullCount of every column: 37 stats leaves
+        pred = Predicate("AND", pred, Predicate("IS_NOT_NULL", Column("c%d" % i)))
     prog, schema, onode, otypes = _plans(columns, pred)
     assert len(prog.paths) > 32
     eng = K.GpuEngine()

@@ -1015,6 +1015,67 @@ def test_gpu_typed_stats_parsed_equals_json(tmp_path, ts_unit):
         eng.close()
 
 
+def wide_predicates(mins):
+    """Filters past every old cap (8 stats paths, 64 ops, 4 KiB of literals): an OR of 32 equalities
+    over 14 columns, '=' on 5 columns, IS_NOT_NULL on 12 columns, 10 KiB string literals."""
+    cols = ["l", "i", "d", "s", "dc", "f", "g"] + ["x%d" % k for k in range(7)]
+
+    def lit(c, k):
+        vs = [v for v in mins[c] if v == v]
+        v = vs[k % len(vs)]
+        return {"l": Literal.ofLong, "i": Literal.ofInt, "d": Literal.ofDate, "s": Literal.ofString,
+                "f": Literal.ofFloat, "g": Literal.ofDouble}.get(c, Literal.ofLong)(v) if c != "dc" \
+            else Literal.ofDecimal(str(v), 12, 2)
+    ors = cmp("=", col(cols[0]), lit(cols[0], 0))
+    for k in range(1, 32):
+        c = cols[k % len(cols)]
+        ors = Or(ors, cmp("=", col(c), lit(c, 7 * k)))
+    five = cmp("=", col("x0"), lit("x0", 1))
+    for c in ("x1", "x2", "x3", "x4"):
+        five = And(five, cmp(">=", col(c), Literal.ofLong(-150)))
+    nn = Predicate("IS_NOT_NULL", col(cols[0]))
+    for c in cols[1:12]:
+        nn = And(nn, Predicate("IS_NOT_NULL", col(c)))
+    big_z, big_a = "z" * 10240, "a" * 5000 + "\u4e2d" * 2000
+    return [ors, five, nn, And(ors, nn), cmp("<", col("s"), Literal.ofString(big_z)),
+            cmp(">", col("s"), Literal.ofString(big_a)), cmp("=", col("s"), Literal.ofString(big_z)),
+            Or(cmp("=", col("s"), Literal.ofString(big_a)), cmp("=", col("x5"), lit("x5", 3)))]
+
+
+@pytest.mark.gpu
+def test_gpu_wide_filters(tmp_path):
+    """The filters of wide_predicates over a checkpoint with add.stats_parsed (14 typed columns:
+    k_stats_parsed with per-lane scratch) and a commit tail (k_stats_eval over the JSON, 32-path
+    extraction windows): the scan files and counters equal the oracle's."""
+    from delta_amd import kernel as K
+    from delta_amd import programs
+    root = str(tmp_path / "t")
+    mins = synth.write_typed_stats_table(root, n=3000, seed=17, extra_long=7)
+    eng = K.GpuEngine()
+    try:
+        widest = 0
+        for p in wide_predicates(mins):
+            schema, parts = table_metadata(root)
+            leaves = sk.data_schema_leaves(schema, parts)
+            widest = max(widest, len(programs.compile_skipping(sk.construct(p, leaves), leaves).paths))
+            g = _gpu_files_parsed(root, p, eng)
+            o = oracle_files(root, p)
+            assert g[1] == o[1], p
+            assert g[0] == o[0], p
+            assert g[2] == 1, p                       # the checkpoint's skipping read stats_parsed
+        assert widest > 32
+    finally:
+        eng.close()
+
+
+def test_oracle_wide_filters_discriminate(tmp_path):
+    root = str(tmp_path / "t")
+    mins = synth.write_typed_stats_table(root, n=400, seed=17, extra_long=7)
+    kept = [len(oracle_files(root, p)[0]) for p in wide_predicates(mins)]
+    live = 400 + 40 - 20
+    assert sum(0 < k < live for k in kept) >= 4, kept
+
+
 def test_oracle_typed_stats_table(tmp_path):
     """The typed-stats fixture is a valid table for the oracle, and the predicates discriminate (each
     keeps some files and drops some)."""
