@@ -227,7 +227,13 @@ enum : int32_t { PT_LONG = 0, PT_INT = 1, PT_SHORT = 2, PT_BYTE = 3, PT_STRING =
                  PT_BOOL = 7, PT_F32 = 8, PT_F64 = 9, PT_TIMESTAMP = 10 };
 enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, PO_LT = 4, PO_LE = 5, PO_GT = 6,
                  PO_GE = 7, PO_EQ = 8, PO_NSEQ = 9, PO_ISNULL = 10, PO_ISNOTNULL = 11, PO_NOT = 12, PO_AND = 13,
-                 PO_OR = 14, PO_LIT_DEC = 15, PO_FCMP = 16, PO_COALESCE = 17 };
+                 PO_OR = 14, PO_LIT_DEC = 15, PO_FCMP = 16, PO_COALESCE = 17,
+                 // string functions on the top of the stack; lit = offset | length << 32 of a pool
+                 // operand, arg = 1 for a null literal (the result is null):
+                 PO_STARTS_WITH = 18,    // String.startsWith(literal)
+                 PO_LIKE = 19,           // LIKE pattern compiled to tokens (byte pairs: 0 b literal, 1 one
+                                         // code point, 2 any run)
+                 PO_SUBSTR = 20 };       // SUBSTRING(s, pos[, len]): lit = (uint32)pos | len << 32, arg = has len
 struct DPartProg {
   int32_t n_fields, n_ops;
   const int32_t* field_type;       // [n_fields] PT_*

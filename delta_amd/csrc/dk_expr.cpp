@@ -750,7 +750,8 @@ int depth_of(const std::vector<Op>& ops, bool skipping) {
             : (o.op == OP_TIMEADD || o.op == OP_FCMP) ? 0 : -1;
     } else {
       delta = (o.op == PO_FIELD || o.op == PO_LIT_INT || o.op == PO_LIT_STR || o.op == PO_LIT_NULL || o.op == PO_LIT_DEC) ? 1
-            : (o.op == PO_ISNULL || o.op == PO_ISNOTNULL || o.op == PO_NOT || o.op == PO_FCMP) ? 0
+            : (o.op == PO_ISNULL || o.op == PO_ISNOTNULL || o.op == PO_NOT || o.op == PO_FCMP || o.op == PO_STARTS_WITH ||
+               o.op == PO_LIKE || o.op == PO_SUBSTR) ? 0
             : o.op == PO_COALESCE ? 1 - o.arg : -1;
     }
     d += delta;
@@ -983,6 +984,7 @@ struct PartCompiler {
     if (field_ref(x, &phys, &t)) return t;
     if (x.k == Ex::LIT) return x.type;
     if (x.k == Ex::CALL && x.name == "COALESCE" && !x.args.empty()) return type_of(x.args[0]);
+    if (x.k == Ex::CALL && x.name == "SUBSTRING") return "string";
     return "boolean";
   }
   // an operand (value expression); returns its comparison kind ("" for a null literal)
@@ -998,26 +1000,111 @@ struct PartCompiler {
       if (is_integral(ty) || ty == "date" || ty == "timestamp" || ty == "timestamp_ntz") { push(PO_LIT_INT, 0, x.iv); return kind_of(ty); }
       refuse("partition pruning with a " + ty + " literal is not supported");
     }
-    if (x.k == Ex::CALL && x.name == "COALESCE") {
-      if (x.args.empty()) refuse("COALESCE needs arguments");
+    if (x.k == Ex::CALL && x.name == "COALESCE") {   // DefaultExpressionEvaluator.visitCoalesce :236-257
+      if (x.args.empty()) throw Unsupported{3, "Unsupported expression: Coalesce requires at least one expression"};
       std::string k0, t0 = type_of(x.args[0]);
+      if (t0 != "boolean") throw Unsupported{3, "Unsupported expression: Coalesce is only supported for boolean type expressions"};
       for (auto& a : x.args) {
         if (type_of(a) != t0)
-          throw Unsupported{3, "Unsupported expression: COALESCE is only supported for arguments of the same type"};
+          throw Unsupported{3, "Unsupported expression: Coalesce is only supported for arguments of the same type"};
         const std::string k = is_predicate(a) ? (pred(a), "boolean") : operand(a);
         if (!k.empty()) k0 = k;
       }
       push(PO_COALESCE, (int)x.args.size());
       return k0;
     }
+    if (x.k == Ex::CALL && x.name == "SUBSTRING") {  // SubstringEvaluator.java:36-60
+      if (x.args.size() < 2 || x.args.size() > 3)
+        throw Unsupported{3, "Unsupported expression: Invalid number of inputs to SUBSTRING expression"};
+      if (type_of(x.args[0]) != "string")
+        throw Unsupported{3, "Unsupported expression: Invalid type of first input of SUBSTRING: expects STRING"};
+      for (size_t k = 1; k < x.args.size(); k++) {
+        const Ex& a = x.args[k];
+        if (!(a.k == Ex::LIT && a.type == "integer" && !a.null))
+          throw Unsupported{3, std::string("Unsupported expression: Invalid `") + (k == 1 ? "pos" : "len") +
+                               "` argument type for SUBSTRING"};
+      }
+      operand(x.args[0]);
+      const int64_t pos = (uint32_t)(int32_t)x.args[1].iv;
+      const int64_t len = x.args.size() == 3 ? x.args[2].iv : 0;
+      push(PO_SUBSTR, x.args.size() == 3 ? 1 : 0, pos | (int64_t)((uint64_t)(uint32_t)(int32_t)len << 32));
+      return "string";
+    }
     if (is_predicate(x)) { pred(x); return "boolean"; }
     refuse("partition pruning on expression " + x.name + " is not supported by this engine build");
+  }
+  // LIKE pattern -> tokens (LikeExpressionEvaluator.escapeLikeRegex :155-186): '_' one code point,
+  // '%' any run, escape + (_ | % | escape) that character, any other escape an error
+  static std::string like_tokens(const std::string& pat, uint32_t esc) {
+    std::string t;
+    std::vector<uint32_t> cps;                       // the pattern's code points (UTF-8 decoded)
+    std::vector<std::string> raw;
+    for (size_t i = 0; i < pat.size();) {
+      const unsigned char c = pat[i];
+      const size_t n = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+      uint32_t cp = n == 1 ? c : n == 2 ? (c & 31) : n == 3 ? (c & 15) : (c & 7);
+      for (size_t k = 1; k < n && i + k < pat.size(); k++) cp = (cp << 6) | (pat[i + k] & 63);
+      cps.push_back(cp);
+      raw.push_back(pat.substr(i, n));
+      i += n;
+    }
+    for (size_t i = 0; i < cps.size(); i++) {
+      if (cps[i] == esc) {
+        if (i + 1 == cps.size() || !(cps[i + 1] == '_' || cps[i + 1] == '%' || cps[i + 1] == esc))
+          throw Unsupported{3, "LIKE expression has invalid escape sequence: " + pat};
+        for (unsigned char b : raw[i + 1]) { t += '\0'; t += (char)b; }
+        i++;
+      } else if (cps[i] == '_') {
+        t += '\1'; t += '\0';
+      } else if (cps[i] == '%') {
+        t += '\2'; t += '\0';
+      } else {
+        for (unsigned char b : raw[i]) { t += '\0'; t += (char)b; }
+      }
+    }
+    return t;
+  }
+  // STARTS_WITH(s, literal) / LIKE(s, pattern[, escape]) (StartsWithExpressionEvaluator.java:38-60,
+  // LikeExpressionEvaluator.java:40-80): string inputs, literal second (and third) arguments
+  void string_pred(const Ex& x) {
+    const bool like = x.name == "LIKE";
+    if (like ? (x.args.size() < 2 || x.args.size() > 3) : x.args.size() != 2)
+      throw Unsupported{3, "Unsupported expression: Invalid number of inputs to " + x.name + " expression"};
+    for (size_t k = 0; k < 2; k++)
+      if (type_of(x.args[k]) != "string")
+        throw Unsupported{3, like ? "Unsupported expression: LIKE is only supported for string type expressions"
+                                  : "Unsupported expression: 'STARTS_WITH' expects STRING type inputs"};
+    const Ex& lit = x.args[1];
+    if (lit.k != Ex::LIT) {
+      if (!like) throw Unsupported{3, "Unsupported expression: 'STARTS_WITH' expects literal as the second input"};
+      refuse("LIKE with a non-literal pattern is not supported by this engine build");
+    }
+    uint32_t esc = '\\';
+    if (x.args.size() == 3) {
+      const Ex& e = x.args[2];
+      if (!(e.k == Ex::LIT && e.type == "string"))
+        throw Unsupported{3, "Unsupported expression: LIKE expects escape token expression to be a literal of String type"};
+      const std::string& t = e.text;             // one UTF-16 unit: a BMP code point
+      const unsigned char c = t.empty() ? 0 : t[0];
+      const size_t n = c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4;
+      if (e.null || t.empty() || t.size() != n || n == 4)
+        throw Unsupported{3, "Unsupported expression: LIKE expects escape token to be a single character"};
+      esc = n == 1 ? c : n == 2 ? (c & 31) : (c & 15);
+      for (size_t k = 1; k < n; k++) esc = (esc << 6) | (t[k] & 63);
+    }
+    operand(x.args[0]);
+    Op o;
+    o.op = like ? PO_LIKE : PO_STARTS_WITH;
+    if (lit.null) { o.arg = 1; ops.push_back(o); return; }
+    o.has_bytes = true;
+    o.bytes = like ? like_tokens(lit.text, esc) : lit.text;
+    ops.push_back(o);
   }
   static bool is_predicate(const Ex& x) {
     if (x.k != Ex::CALL) return false;
     const std::string& n = x.name;
     return n == "AND" || n == "OR" || n == "NOT" || n == "IS_NULL" || n == "IS_NOT_NULL" || is_cmp(n) ||
-           n == "ALWAYS_TRUE" || n == "ALWAYS_FALSE";
+           n == "ALWAYS_TRUE" || n == "ALWAYS_FALSE" || n == "STARTS_WITH" || n == "LIKE";
   }
   void pred(const Ex& x) {
     if (x.k == Ex::LIT && x.type == "boolean") { if (x.null) push(PO_LIT_NULL); else push(PO_LIT_INT, 0, x.iv); return; }
@@ -1027,6 +1114,7 @@ struct PartCompiler {
     const std::string& n = x.name;
     const auto& c = x.args;
     if (n == "ALWAYS_TRUE" || n == "ALWAYS_FALSE") { push(PO_LIT_INT, 0, n == "ALWAYS_TRUE"); return; }
+    if (n == "STARTS_WITH" || n == "LIKE") { string_pred(x); return; }
     if (n == "AND" || n == "OR") {
       if (c.size() != 2) refuse(n + " takes two predicates");
       pred(c[0]);
@@ -1119,7 +1207,7 @@ void finalize_ops(dk_program& P, const std::vector<Op>& ops, bool skipping) {
     int64_t lit = o.lit;
     if (o.has_bytes) {
       const int64_t off = (int64_t)P.pool.size();
-      if (o.op == (skipping ? OP_FCMP : PO_FCMP)) {
+      if (o.op == (skipping ? OP_FCMP : PO_FCMP) || (!skipping && (o.op == PO_STARTS_WITH || o.op == PO_LIKE))) {
         lit = off | ((int64_t)o.bytes.size() << 32);
         P.pool += o.bytes;
         if (o.ranks) {

@@ -3355,6 +3355,24 @@ struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 bool
   const uint8_t* p;
 };
 
+__device__ __forceinline__ int32_t utf8_len(uint8_t c) { return c < 0xC0 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4; }
+
+// String.matches of a LIKE pattern's regex (LikeExpressionEvaluator.isLike :134-140): tokens (byte pairs)
+// 0 b = literal byte b, 1 = one code point ('_'), 2 = any run ('%'); a greedy match with one
+// backtrack point (the last '%'), stepping by whole code points
+__device__ bool like_match(const uint8_t* s, int32_t n, const uint8_t* t, int32_t tn) {
+  int32_t i = 0, p = 0, star_p = -1, star_i = 0;
+  while (i < n) {
+    if (p < tn && t[p] == 0 && s[i] == t[p + 1]) { i++; p += 2; }
+    else if (p < tn && t[p] == 1) { i += utf8_len(s[i]); p += 2; }
+    else if (p < tn && t[p] == 2) { star_p = p; p += 2; star_i = i; }
+    else if (star_p >= 0) { p = star_p + 2; star_i += utf8_len(s[star_i]); i = star_i; }
+    else return false;
+  }
+  while (p < tn && t[p] == 2) p += 2;
+  return p >= tn && i == n;
+}
+
 // element_at(add.partitionValues, <field k's name>) of one row, deserialized as partition_value does
 // (PartitionValueEvaluator.java:50-100); kind 0 when the map or the key is absent or the value null.
 // false on a malformed value.
@@ -3480,6 +3498,44 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
       if (sp < 1) return -1;
       PVal& a = st[sp - 1];
       if (a.kind != 0) a.v = !a.v;
+    } else if (op == PO_STARTS_WITH || op == PO_LIKE) {  // over the string on top of the stack
+      if (sp < 1) return -1;
+      PVal& a = st[sp - 1];
+      if (a.kind != 0 && P.arg[i]) a.kind = 0;          // a null literal: null
+      if (a.kind != 0) {
+        const uint8_t* t = (const uint8_t*)P.pool + (P.lit[i] & 0xffffffffll);
+        const int32_t tn = (int32_t)(P.lit[i] >> 32);
+        a.v = op == PO_STARTS_WITH ? (a.len >= tn && bytes_cmp(a.p, tn, t, tn) == 0) : like_match(a.p, a.len, t, tn);
+        a.kind = 3;
+      }
+    } else if (op == PO_SUBSTR) {                        // SubstringEvaluator.getString (:92-121), code points
+      if (sp < 1) return -1;
+      PVal& a = st[sp - 1];
+      if (a.kind != 0) {
+        const int32_t pos = (int32_t)(P.lit[i] & 0xffffffffll), len = (int32_t)(P.lit[i] >> 32);
+        const bool has_len = P.arg[i] != 0;
+        int32_t L = 0;
+        for (int32_t k = 0; k < a.len; k += utf8_len(a.p[k])) L++;
+        if (pos > L || (has_len && len < 1)) {
+          a.len = 0;
+        } else {
+          const int32_t start = pos < 0 ? L + pos : (pos - 1 > 0 ? pos - 1 : 0);
+          const int32_t s0 = start > 0 ? start : 0;
+          int32_t s1 = L;
+          if (has_len) {
+            const int32_t e = (int32_t)((uint32_t)start + (uint32_t)len);   // Java int arithmetic
+            s1 = e > 0 ? e : 0;
+            if (s1 > L) s1 = L;
+          }
+          if (s1 < s0) { *err = true; return -1; }        // String.substring throws
+          int32_t b0 = 0, k = 0, cp = 0;
+          for (; k < a.len && cp < s0; k += utf8_len(a.p[k])) cp++;
+          b0 = k;
+          for (; k < a.len && cp < s1; k += utf8_len(a.p[k])) cp++;
+          a.p += b0;
+          a.len = k - b0;
+        }
+      }
     } else if (op == PO_COALESCE) {                      // the first non-null of the last arg operands
       const int n = P.arg[i];
       if (n < 1 || sp < n) return -1;

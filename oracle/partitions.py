@@ -186,6 +186,40 @@ def evaluate(node, pv, fields):
         return None if node.value is None else (_b(node.value) if node.type == "string" else node.value)
     n = node.name.upper()
     c = node.children
+    if n in ("ALWAYS_TRUE", "ALWAYS_FALSE"):                  # ExpressionVisitor.java:91-94
+        return n == "ALWAYS_TRUE"
+    if n == "COALESCE":                                        # DefaultExpressionEvaluator.java:577-590
+        vals = [evaluate(x, pv, fields) for x in c]            # (every argument evaluated)
+        return next((v for v in vals if v is not None), None)
+    if n == "STARTS_WITH":                                     # StartsWithExpressionEvaluator.java:62-92
+        a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
+        return None if a is None or b is None else a.decode("utf-8").startswith(b.decode("utf-8"))
+    if n == "LIKE":                                            # LikeExpressionEvaluator.java:82-186
+        a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
+        esc = evaluate(c[2], pv, fields).decode("utf-8") if len(c) == 3 else "\\"
+        if a is None or b is None:
+            return None
+        return re.fullmatch(_like_regex(b.decode("utf-8"), esc), a.decode("utf-8"), re.DOTALL) is not None
+    if n == "SUBSTRING":                                       # SubstringEvaluator.java:92-156
+        a = evaluate(c[0], pv, fields)
+        if a is None:
+            return None
+        s = a.decode("utf-8")
+        pos = c[1].value
+        length = c[2].value if len(c) == 3 else None
+        L = len(s)
+        if pos > L or (length is not None and length < 1):
+            return b""
+        start = L + pos if pos < 0 else max(pos - 1, 0)
+        si = max(start, 0)
+        if length is None:
+            return s[si:].encode("utf-8")
+        e = start + length
+        e = (e + 2 ** 31) % 2 ** 32 - 2 ** 31                 # Java int arithmetic
+        ei = min(L, max(e, 0))
+        if ei < si:
+            raise PartitionValueError("begin %d, end %d" % (si, ei))   # String.substring throws
+        return s[si:ei].encode("utf-8")
     if n in ("AND", "OR"):
         a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
         if n == "AND":
@@ -214,8 +248,26 @@ def evaluate(node, pv, fields):
     return {"<": r < 0, "<=": r <= 0, ">": r > 0, ">=": r >= 0, "=": r == 0}[n]
 
 
+def _like_regex(pattern, esc):
+    """LikeExpressionEvaluator.escapeLikeRegex (:155-186) as a Python regex."""
+    out, i = [], 0
+    while i < len(pattern):
+        ch = pattern[i]
+        if ch == esc:
+            if i == len(pattern) - 1 or pattern[i + 1] not in ("_", "%", esc):
+                raise PartitionValueError("LIKE expression has invalid escape sequence: %r" % pattern)
+            out.append(re.escape(pattern[i + 1]))
+            i += 2
+            continue
+        out.append("." if ch == "_" else ".*" if ch == "%" else re.escape(ch))
+        i += 1
+    return "".join(out)
+
+
 def _type(node, fields):
     kind = type(node).__name__
+    if kind == "Predicate" and node.name.upper() == "SUBSTRING":
+        return "string"
     if kind == "Column":
         return fields[node.names[0].lower()][0]
     if kind == "Literal":

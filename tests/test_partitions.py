@@ -69,8 +69,14 @@ def test_partition_fields_and_compile():
         _describe(cmp("=", col("zz"), Literal.ofInt(1)), f)
     # COALESCE / ALWAYS_TRUE / ALWAYS_FALSE compile; a predicate the device does not evaluate is refused
     _describe(Predicate("COALESCE", cmp("=", col("p"), Literal.ofInt(1)), Predicate("ALWAYS_FALSE")), f)
+    _describe(Predicate("LIKE", col("s"), Literal.ofString("a%")), f)
+    _describe(cmp("=", Predicate("SUBSTRING", col("s"), Literal.ofInt(2)), Literal.ofString("b")), f)
+    with pytest.raises(sk.UnsupportedExpression, match="STRING"):
+        _describe(Predicate("STARTS_WITH", col("p"), Literal.ofString("1")), f)
+    with pytest.raises(sk.UnsupportedExpression, match="single character"):
+        _describe(Predicate("LIKE", col("s"), Literal.ofString("a%"), Literal.ofString("ab")), f)
     with pytest.raises(pp.UnsupportedPartitionFilter):
-        _describe(Predicate("LIKE", col("s"), Literal.ofString("a%")), f)
+        _describe(Predicate("LIKE", col("s"), col("s")), f)
 
 
 (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LT, PO_LE, PO_GT, PO_GE, PO_EQ, PO_NSEQ, PO_ISNULL,
@@ -588,6 +594,76 @@ def test_gpu_row_group_pruning(rg_table):
     from delta_amd import kernel as K
     eng = K.GpuEngine()
     for p in RG_PREDICATES:
+        assert _gpu_files(rg_table, p, eng) == oracle_files(rg_table, p), p
+    eng.close()
+
+
+def wide_partition_predicates():
+    """Past the old caps (8 columns, 64 ops, 4 KiB pool): an OR of 40 equalities, a 10 KiB string
+    literal, COALESCE / ALWAYS_FALSE, and the three combined."""
+    ors = cmp("=", col("part"), Literal.ofInt(0))
+    for k in range(1, 40):
+        ors = Or(ors, cmp("=", col("part"), Literal.ofInt(k % 3 if k % 2 else 100 + k)))
+    big = cmp("<", col("date"), Literal.ofString("2024-06" + "z" * 10240))
+    co = Predicate("COALESCE", cmp(">", col("part"), Literal.ofInt(5)), Predicate("ALWAYS_FALSE"))
+    co1 = Predicate("COALESCE", cmp(">=", col("part"), Literal.ofInt(1)), Predicate("ALWAYS_FALSE"))
+    return [ors, big, co, And(And(ors, big), Or(co1, Predicate("IS_NULL", col("part"))))]
+
+
+def test_oracle_wide_partition_predicates(rg_table):
+    from oracle import ref
+    full = ref.replay(rg_table).counters.as_tuple()
+    kept = [len(oracle_files(rg_table, p)[0]) for p in wide_partition_predicates()]
+    assert all(0 < k < full[2] for k in kept), (kept, full)
+
+
+def string_function_predicates():
+    """STARTS_WITH / LIKE / SUBSTRING over the string partition column (ExpressionVisitor.java:118-123)."""
+    d = col("date")
+    sub = lambda *a: Predicate("SUBSTRING", d, *[Literal.ofInt(x) for x in a])   # noqa: E731
+    return [Predicate("STARTS_WITH", d, Literal.ofString("2024-0")),
+            Predicate("LIKE", d, Literal.ofString("2024-_3-%")),
+            Predicate("LIKE", d, Literal.ofString("%1_")),
+            Predicate("LIKE", d, Literal.ofString("2024-0%!%"), Literal.ofString("!")),
+            Predicate("NOT", Predicate("LIKE", d, Literal.ofString("%-0_-%"))),
+            cmp("=", sub(6, 2), Literal.ofString("03")),
+            cmp(">", sub(-2), Literal.ofString("15")),
+            cmp("=", sub(0, 4), Literal.ofString("2024")),
+            cmp("=", sub(-100, 95), Literal.ofString("")),
+            And(Predicate("STARTS_WITH", d, Literal.ofString("2024-1")), cmp(">", col("part"), Literal.ofInt(3)))]
+
+
+def test_oracle_string_function_predicates(rg_table):
+    from oracle import ref
+    full = ref.replay(rg_table).counters.as_tuple()
+    kept = [len(oracle_files(rg_table, p)[0]) for p in string_function_predicates()]
+    assert sum(0 < k < full[2] for k in kept) >= 6, kept
+    from oracle import partitions as opp
+    with pytest.raises(opp.PartitionValueError):       # an invalid escape fails the evaluation
+        oracle_files(rg_table, Predicate("LIKE", col("date"), Literal.ofString("2024!-%"), Literal.ofString("!")))
+
+
+@pytest.mark.gpu
+def test_gpu_string_function_predicates(rg_table):
+    """The string functions of string_function_predicates on the GPU equal the oracle; an invalid LIKE
+    escape fails the scan as the reference's evaluator does."""
+    from delta_amd import kernel as K
+    from delta_amd.skipping import UnsupportedExpression
+    eng = K.GpuEngine()
+    for p in string_function_predicates():
+        assert _gpu_files(rg_table, p, eng) == oracle_files(rg_table, p), p
+    with pytest.raises(UnsupportedExpression, match="invalid escape"):
+        _gpu_files(rg_table, Predicate("LIKE", col("date"), Literal.ofString("2024!-%"), Literal.ofString("!")), eng)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_wide_partition_predicates(rg_table):
+    """wide_partition_predicates on the GPU (partition pruning over add.partitionValues, and the
+    checkpoint row-group predicate over partitionValues_parsed) equal the oracle."""
+    from delta_amd import kernel as K
+    eng = K.GpuEngine()
+    for p in wide_partition_predicates():
         assert _gpu_files(rg_table, p, eng) == oracle_files(rg_table, p), p
     eng.close()
 
