@@ -1343,9 +1343,11 @@ class GpuScan:
         # (DK_ASYNC_OPEN=0: the synchronous open)
         # (data skipping, partition pruning and row-group predicates too: C4 308-310 ms against 321-327
         # synchronous, profiles/r04/c4_async_ab; DK_ASYNC_FILTERED=0 keeps them synchronous)
+        # sharded scans (a rank's row-group runs) open asynchronously too: in owner mode the commit
+        # tail's exchange overlaps the open, and the row exchanges wait for the decode (dk_replay_run)
         filtered = self.skipping is not None or self.partition is not None or self.predicate is not None
-        plain = not self.shard and (not filtered or os.environ.get("DK_ASYNC_FILTERED", "1") != "0") and \
-            scan_groups(len(self.ckpt_files or [])) and os.environ.get("DK_ASYNC_OPEN", "1") != "0"
+        plain = (not filtered or os.environ.get("DK_ASYNC_FILTERED", "1") != "0") and \
+            (scan_groups(len(self.ckpt_files or [])) or self.shard) and os.environ.get("DK_ASYNC_OPEN", "1") != "0"
         late = bool(plain) and bool(self.ckpt_files) and os.environ.get("DK_TAIL_AFTER_OPEN", "1") != "0"
         if not late:
             start_tail()

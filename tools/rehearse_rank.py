@@ -1,0 +1,173 @@
+"""One-GPU rehearsal of one rank of the N-GPU owner-partitioned scan (bench.py --gpus N, the default
+exchange=owner), for the timing of the path the driver's 8-GPU run measures.
+
+All N ranks' scans run in this process on one GPU (shard.OwnerLoopback routes the exchanges' buffers
+between them on the device): each rank opens only its contiguous run of row groups (asynchronous open)
+and parses only its commit files j = rank (mod N). Every rank is timed on its own:
+
+  open       prepare (footers, page headers, the commit-tail parse of its files + replay create)
+             until its asynchronous open has finished decoding (the ranks run one after another, so
+             each rank's H2D and decode have the GPU to themselves, as on its own GPU)
+  exchange   each of its owner-exchange calls (tail resolve, checkpoint hash routing / lookup /
+             candidates), device-synchronised, summed
+  transfer   the bytes it sends through the all-to-alls at an assumed per-GPU all-to-all bandwidth
+             (--a2a-gbs, default 300 GB/s: 7 xGMI links at ~43 GB/s each) + 30 us per collective
+  consume    its scan-file batches consumed as bench.py's JMH-shaped consumer does (sum of add.size
+             over the selected rows)
+
+per_rank_ms = open + exchange + transfer + consume; the rehearsed N-GPU step is the max over ranks.
+Usage: python tools/rehearse_rank.py --world 8 [--config c3] [--workdir DIR] > out.json
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--workdir", default=None)
+    ap.add_argument("--a2a-gbs", type=float, default=300.0)
+    ap.add_argument("--runs", type=int, default=2, help="exchange runs (the last is reported)")
+    args = ap.parse_args()
+    import bench
+    cfg = bench.CONFIGS[args.config]
+    rows = args.rows or cfg["rows"]
+    compression = cfg["spec"].get("compression", "none")
+    work = args.workdir or os.path.join(tempfile.gettempdir(), "dk_rehearse_%s_%d" % (args.config, rows))
+    marker = os.path.join(work, ".ready")
+    if not os.path.exists(marker):
+        import shutil
+        shutil.rmtree(work, ignore_errors=True)
+        t0 = time.time()
+        bench.make_table(work, rows, 20250218, compression, cfg)
+        open(marker, "w").close()
+        print("table generated in %.1fs" % (time.time() - t0), file=sys.stderr)
+
+    import numpy as np
+    import torch
+    torch.cuda.init()
+    from delta_amd import kernel as K
+    from delta_amd import shard
+    from delta_amd._lib import check, lib
+
+    class Timed:
+        """An OwnerSide whose calls are timed (each returns with the device synchronised)."""
+
+        def __init__(self, side, clock):
+            self.side, self.clock = side, clock
+            self.rank = side.rank
+
+        def __getattr__(self, name):
+            f = getattr(self.side, name)
+            if not callable(f):
+                return f
+
+            def call(*a, **k):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                out = f(*a, **k)
+                torch.cuda.synchronize()
+                self.clock[name] = self.clock.get(name, 0.0) + (time.perf_counter() - t) * 1e3
+                return out
+            return call
+
+    class TimedLoopback(shard.OwnerLoopback):
+        def __init__(self, steps):
+            super().__init__(steps)
+            self.clocks = {}
+            self.sent = {}
+            self.collectives = 0
+
+        def __call__(self, side):
+            self.sides[side.rank] = Timed(side, self.clocks.setdefault(side.rank, {}))
+
+        def _route(self, sends):
+            self.collectives += 1
+            for s, (t, cnt) in enumerate(sends):
+                own = int(sum(cnt[:s])), int(cnt[s]) if s < len(cnt) else 0
+                nbytes = t.numel() * t.element_size()
+                per = t.element_size() if t.numel() else 0
+                self.sent[s] = self.sent.get(s, 0) + nbytes - own[1] * per   # bytes leaving rank s
+            return super()._route(sends)
+
+    world = args.world
+    eng = K.GpuEngine(timing=False)
+    snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
+    lb = TimedLoopback(shard.OwnerLoopback.for_table(eng, snap)._steps)
+    scans, opened = [], {}
+    for r in range(world):
+        s = K.Table.forPath(eng, work).getLatestSnapshot(eng)
+        sc = s.getScanBuilder().withStats(cfg["stats"]).withShard(world, r, owner=lb).build()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sc.prepare(eng)
+        t1 = time.perf_counter()
+        if sc.ckpt is not None:
+            check(lib().dk_parquet_sync(sc.ckpt._h))
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        opened[r] = {"prepare_ms": (t1 - t0) * 1e3, "open_ms": (t2 - t0) * 1e3,
+                     "async_open": bool(sc.ckpt is not None and sc.ckpt.async_open),
+                     "checkpoint_rows": int(sum(sc.ckpt.num_rows(i) for i in range(len(sc.ckpt_files)))) if sc.ckpt else 0,
+                     "commit_files": len(sc.tail_commits), "tail_rows": int(sc.tail.rows),
+                     "phases_ms": {k: round(v, 2) for k, v in sc.prepare_ms.items()}}
+        scans.append(sc)
+    for run in range(args.runs):
+        lb.clocks.clear()
+        lb.sent.clear()
+        lb.collectives = 0
+        lb.run(scans)
+    counters = np.zeros(5, np.int64)
+    consume = {}
+    for r, sc in enumerate(scans):
+        counters += np.array(sc.metrics.as_tuple())
+        t0 = time.perf_counter()
+        size_sum = n_sel = 0
+        for b in sc._batches():
+            v = b.data["add.size"].fixed.view("<i8")
+            if b.selection is None:
+                size_sum += int(v.sum())
+                n_sel += b.size
+            else:
+                s_, k_ = bench.masked_sum(v, b.selection)
+                size_sum += s_
+                n_sel += k_
+        consume[r] = ((time.perf_counter() - t0) * 1e3, n_sel)
+    per_rank = {}
+    for r in range(world):
+        ex = sum(lb.clocks.get(r, {}).values())
+        tr = lb.sent.get(r, 0) / (args.a2a_gbs * 1e9) * 1e3 + lb.collectives * 0.03
+        per_rank[r] = dict(opened[r], exchange_ms=round(ex, 3), exchange_calls_ms={k: round(v, 3) for k, v in lb.clocks.get(r, {}).items()},
+                           bytes_sent=lb.sent.get(r, 0), transfer_model_ms=round(tr, 3),
+                           consume_ms=round(consume[r][0], 3), selected=consume[r][1],
+                           per_rank_ms=round(opened[r]["open_ms"] + ex + tr + consume[r][0], 2))
+    step = max(v["per_rank_ms"] for v in per_rank.values())
+    seen = int(counters[0])
+    out = {"world": world, "config": args.config, "rows": rows, "counters": [int(x) for x in counters],
+           "rehearsed_step_ms": round(step, 2), "rehearsed_actions_per_s": seen / (step * 1e-3),
+           "collectives_per_run": lb.collectives, "a2a_gbs_assumed": args.a2a_gbs, "per_rank": per_rank,
+           "note": "one process, one GPU: each rank's open ran alone (its own H2D and decode), exchanges "
+                   "through device-side loopback; transfer time modelled from the bytes each rank sends"}
+    for sc in scans:
+        sc.close()
+    plain = snap.getScanBuilder().withStats(cfg["stats"]).build()      # the unsharded scan's counters
+    for _ in plain.getScanFiles(eng):
+        pass
+    out["counters_unsharded"] = list(plain.metrics.as_tuple())
+    out["counters_match"] = out["counters_unsharded"] == out["counters"]
+    plain.close()
+    print(json.dumps(out, indent=1))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
