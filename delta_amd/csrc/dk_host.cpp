@@ -3914,6 +3914,7 @@ struct dk_replay {
   StreamH own;                          // the replay's stream (the checkpoint decode runs on it too)
   hipStream_t stream = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr;   // ordering against the checkpoint's own stream
+  hipEvent_t ev_pf = nullptr;                      // owner mode: the prefetched mirrors follow the decode
   dk_engine* eng = nullptr;
   dk_json_tail* tail = nullptr;
   dk_parquet* ck = nullptr;
@@ -5319,6 +5320,18 @@ static int owner_launch(dk_replay* r) {
     st0.err_row = LLONG_MAX;
     HIPOK(hipMemcpyAsync(p->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, s));
     if (run_pipeline(p, 1, s, false)) return 1;
+    if (!r->prefetch.empty()) {
+      // the prefetched leaves (add.size) go to host memory now, on the mirror stream, while the
+      // row exchanges run: the consumer then finds them there
+      if (p->async_open && !p->mir.s && p->mir.create()) return 1;
+      hipStream_t ms = p->async_open ? p->mir.s : p->stream;
+      if (!r->ev_pf) HIPOK(hipEventCreateWithFlags(&r->ev_pf, hipEventDisableTiming));
+      HIPOK(hipEventRecord(r->ev_pf, s));
+      HIPOK(hipStreamWaitEvent(ms, r->ev_pf, 0));
+      for (int leaf : r->prefetch)
+        for (size_t f = 0; f < p->files.size(); f++)
+          if (p->colmap[f][leaf] >= 0 && queue_mirror(p, p->colmap[f][leaf])) return 1;
+    }
     const size_t nf = r->probe.size();
     r->probe_run = r->probe;
     r->probe_row0.assign(nf + 1, 0);
@@ -5703,6 +5716,7 @@ extern "C" void dk_replay_free(dk_replay* r) {
     hipSetDevice(r->eng->cfg.device);
     if (r->ev_in) hipEventDestroy(r->ev_in);
     if (r->ev_out) hipEventDestroy(r->ev_out);
+    if (r->ev_pf) hipEventDestroy(r->ev_pf);
     if (r->ev_tail) hipEventDestroy(r->ev_tail);
     for (hipEvent_t e : r->grp_ev) hipEventDestroy(e);
     SyncedRelease drained;

@@ -1428,6 +1428,11 @@ class GpuScan:
         groups = scan_groups(len(self.ckpt_files or []))
         exchanging = (getattr(self, "exchange", None) is not None or getattr(self, "owner", None) is not None) \
             and self.shard and self.shard[0] > 1
+        if exchanging and getattr(self, "owner", None) is not None and self.ckpt is not None:
+            # owner mode: add.size goes to host memory right after the decode, beside the exchanges
+            for leaf in self.PREFETCH_LEAVES:
+                if leaf in self.ckpt.leaves:
+                    check(lib().dk_replay_prefetch_leaf(self._rh, leaf.encode()))
         if groups and not exchanging:
             # grouped: batches go out as their group of files is decoded and probed; the counters are
             # final once the iterator is exhausted (ScanImpl's metrics are read after it, too)

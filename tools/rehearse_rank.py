@@ -36,7 +36,6 @@ def main():
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--a2a-gbs", type=float, default=300.0)
-    ap.add_argument("--runs", type=int, default=2, help="exchange runs (the last is reported)")
     args = ap.parse_args()
     import bench
     cfg = bench.CONFIGS[args.config]
@@ -102,46 +101,54 @@ def main():
     world = args.world
     eng = K.GpuEngine(timing=False)
     snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
-    lb = TimedLoopback(shard.OwnerLoopback.for_table(eng, snap)._steps)
-    scans, opened = [], {}
-    for r in range(world):
-        s = K.Table.forPath(eng, work).getLatestSnapshot(eng)
-        sc = s.getScanBuilder().withStats(cfg["stats"]).withShard(world, r, owner=lb).build()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        sc.prepare(eng)
-        t1 = time.perf_counter()
-        if sc.ckpt is not None:
-            check(lib().dk_parquet_sync(sc.ckpt._h))
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        opened[r] = {"prepare_ms": (t1 - t0) * 1e3, "open_ms": (t2 - t0) * 1e3,
-                     "async_open": bool(sc.ckpt is not None and sc.ckpt.async_open),
-                     "checkpoint_rows": int(sum(sc.ckpt.num_rows(i) for i in range(len(sc.ckpt_files)))) if sc.ckpt else 0,
-                     "commit_files": len(sc.tail_commits), "tail_rows": int(sc.tail.rows),
-                     "phases_ms": {k: round(v, 2) for k, v in sc.prepare_ms.items()}}
-        scans.append(sc)
-    for run in range(args.runs):
-        lb.clocks.clear()
-        lb.sent.clear()
-        lb.collectives = 0
+    steps = shard.OwnerLoopback.for_table(eng, snap)._steps
+    # iteration 0 warms the caching allocators (every rank's blocks, as each rank's process is warm
+    # after bench.py's warm-up steps); iteration 1 is reported
+    for it in range(2):
+        lb = TimedLoopback(steps)
+        scans, opened = [], {}
+        for r in range(world):
+            s = K.Table.forPath(eng, work).getLatestSnapshot(eng)
+            sc = s.getScanBuilder().withStats(cfg["stats"]).withShard(world, r, owner=lb).build()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sc.prepare(eng)
+            t1 = time.perf_counter()
+            if sc.ckpt is not None:
+                check(lib().dk_parquet_sync(sc.ckpt._h))
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            opened[r] = {"prepare_ms": (t1 - t0) * 1e3, "open_ms": (t2 - t0) * 1e3,
+                         "async_open": bool(sc.ckpt is not None and sc.ckpt.async_open),
+                         "checkpoint_rows": int(sum(sc.ckpt.num_rows(i) for i in range(len(sc.ckpt_files)))) if sc.ckpt else 0,
+                         "commit_files": len(sc.tail_commits), "tail_rows": int(sc.tail.rows),
+                         "phases_ms": {k: round(v, 2) for k, v in sc.prepare_ms.items()}}
+            scans.append(sc)
+        for sc in scans:                        # as getScanFiles does in owner mode
+            for leaf in sc.PREFETCH_LEAVES:
+                if leaf in sc.ckpt.leaves:
+                    check(lib().dk_replay_prefetch_leaf(sc._rh, leaf.encode()))
         lb.run(scans)
-    counters = np.zeros(5, np.int64)
-    consume = {}
-    for r, sc in enumerate(scans):
-        counters += np.array(sc.metrics.as_tuple())
-        t0 = time.perf_counter()
-        size_sum = n_sel = 0
-        for b in sc._batches():
-            v = b.data["add.size"].fixed.view("<i8")
-            if b.selection is None:
-                size_sum += int(v.sum())
-                n_sel += b.size
-            else:
-                s_, k_ = bench.masked_sum(v, b.selection)
-                size_sum += s_
-                n_sel += k_
-        consume[r] = ((time.perf_counter() - t0) * 1e3, n_sel)
+        counters = np.zeros(5, np.int64)
+        consume = {}
+        for r, sc in enumerate(scans):
+            counters += np.array(sc.metrics.as_tuple())
+            t0 = time.perf_counter()
+            size_sum = n_sel = 0
+            for b in sc._batches():
+                v = b.data["add.size"].fixed.view("<i8")
+                if b.selection is None:
+                    size_sum += int(v.sum())
+                    n_sel += b.size
+                else:
+                    s_, k_ = bench.masked_sum(v, b.selection)
+                    size_sum += s_
+                    n_sel += k_
+            b = v = None
+            consume[r] = ((time.perf_counter() - t0) * 1e3, n_sel)
+        if it == 0:
+            for sc in scans:
+                sc.close()
     per_rank = {}
     for r in range(world):
         ex = sum(lb.clocks.get(r, {}).values())
@@ -155,8 +162,9 @@ def main():
     out = {"world": world, "config": args.config, "rows": rows, "counters": [int(x) for x in counters],
            "rehearsed_step_ms": round(step, 2), "rehearsed_actions_per_s": seen / (step * 1e-3),
            "collectives_per_run": lb.collectives, "a2a_gbs_assumed": args.a2a_gbs, "per_rank": per_rank,
-           "note": "one process, one GPU: each rank's open ran alone (its own H2D and decode), exchanges "
-                   "through device-side loopback; transfer time modelled from the bytes each rank sends"}
+           "note": "one process, one GPU, caches warmed by a first iteration: each rank's open ran alone "
+                   "(its own H2D and decode), exchanges through device-side loopback; transfer time modelled "
+                   "from the bytes each rank sends"}
     for sc in scans:
         sc.close()
     plain = snap.getScanBuilder().withStats(cfg["stats"]).build()      # the unsharded scan's counters
