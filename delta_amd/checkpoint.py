@@ -18,9 +18,9 @@ What runs where:
   * protocol / metaData / txn (per appId) / domainMetadata (per domain): the first seen in reverse
     log order (:256-330);
   * rows come out in the iterator's order (commits newest first, then the checkpoint, row order);
-  * the Parquet file is written on the host with pyarrow (the ParquetHandler.writeParquetFileAtomically
-    role, DefaultParquetHandler.java:115-163), atomically (a temporary file linked into place, failing
-    when the checkpoint exists), then _last_checkpoint {version, size = adds kept}.
+  * the Parquet file is encoded on the device (dk_ckpt_writer_*, the ParquetHandler.writeParquetFileAtomically
+    role, DefaultParquetHandler.java:115-163) and written atomically (a temporary file linked into
+    place, failing when the checkpoint exists), then _last_checkpoint {version, size = adds kept}.
 """
 from __future__ import annotations
 
@@ -93,54 +93,6 @@ def interval_ms(text):
             raise DkError("Error parsing '%s' to interval" % text)
         total += float(n) * _UNIT_MS[unit]
     return int(total)
-
-
-# ---- CHECKPOINT_SCHEMA as Arrow types -----------------------------------------------------------
-# Field order and nullability follow the reference definitions (paths under kernel-api/.../internal/
-# actions/): SingleAction.CHECKPOINT_SCHEMA (SingleAction.java:30-37), AddFile.FULL_SCHEMA =
-# SCHEMA_WITHOUT_STATS + stats (AddFile.java:42-70), RemoveFile.FULL_SCHEMA (RemoveFile.java:23-38),
-# DeletionVectorDescriptor.READ_SCHEMA (:84-90), Metadata.FULL_SCHEMA (Metadata.java:57-72) with
-# Format.FULL_SCHEMA (Format.java:42-48), Protocol.FULL_SCHEMA (Protocol.java:49-54),
-# SetTransaction.FULL_SCHEMA (SetTransaction.java:28-32), DomainMetadata.FULL_SCHEMA
-# (DomainMetadata.java:34-38). `nullable=False` becomes a REQUIRED Parquet field.
-def checkpoint_schema():
-    import pyarrow as pa
-    S, L, B, I = pa.string(), pa.int64(), pa.bool_(), pa.int32()
-
-    def F(name, t, nullable=True):
-        return pa.field(name, t, nullable=nullable)
-
-    def M(value_nullable=True):                 # MapType(string, string, valueContainsNull)
-        return pa.map_(F("key", S, False), F("value", S, value_nullable))
-
-    def A(contains_null):                       # ArrayType(string, containsNull)
-        return pa.list_(F("element", S, contains_null))
-
-    dv = pa.struct([F("storageType", S, False), F("pathOrInlineDv", S, False), F("offset", I),
-                    F("sizeInBytes", I, False), F("cardinality", L, False)])
-    add = pa.struct([F("path", S, False), F("partitionValues", M(), False), F("size", L, False),
-                     F("modificationTime", L, False), F("dataChange", B, False), F("deletionVector", dv),
-                     F("tags", M()), F("baseRowId", L), F("defaultRowCommitVersion", L), F("stats", S)])
-    rm = pa.struct([F("path", S, False), F("deletionTimestamp", L), F("dataChange", B, False),
-                    F("extendedFileMetadata", B), F("partitionValues", M()), F("size", L), F("stats", S),
-                    F("tags", M()), F("deletionVector", dv), F("baseRowId", L), F("defaultRowCommitVersion", L)])
-    fmt = pa.struct([F("provider", S, False), F("options", M(False))])
-    meta = pa.struct([F("id", S, False), F("name", S), F("description", S), F("format", fmt, False),
-                      F("schemaString", S, False), F("partitionColumns", A(False), False), F("createdTime", L),
-                      F("configuration", M(False), False)])
-    proto = pa.struct([F("minReaderVersion", I, False), F("minWriterVersion", I, False),
-                       F("readerFeatures", A(False)), F("writerFeatures", A(False))])
-    txn = pa.struct([F("appId", S, False), F("version", L, False), F("lastUpdated", L)])
-    dm = pa.struct([F("domain", S, False), F("configuration", S, False), F("removed", B, False)])
-    return pa.schema([("txn", txn), ("add", add), ("remove", rm), ("metaData", meta), ("protocol", proto),
-                      ("domainMetadata", dm)])
-
-
-_ADD_KEYS = ("path", "partitionValues", "size", "modificationTime", "dataChange", "stats", "tags", "deletionVector",
-             "baseRowId", "defaultRowCommitVersion")
-_RM_KEYS = ("path", "deletionTimestamp", "dataChange", "extendedFileMetadata", "partitionValues", "size", "stats",
-            "tags", "deletionVector", "baseRowId", "defaultRowCommitVersion")
-_DV_KEYS = ("storageType", "pathOrInlineDv", "offset", "sizeInBytes", "cardinality")
 
 
 def _pick(obj, keys):
@@ -396,21 +348,9 @@ def _write_gpu(engine, snap, path, now_ms, codec=1):
     return n_adds
 
 
-def _arrow_value(kind, v):
-    if v is None:
-        return None
-    if kind == "metaData":
-        return {"id": v["id"], "name": v.get("name"), "description": v.get("description"),
-                "format": {"provider": v["format"]["provider"], "options": list((v["format"].get("options") or {}).items())},
-                "schemaString": v["schemaString"], "partitionColumns": v["partitionColumns"],
-                "createdTime": v.get("createdTime"), "configuration": list((v.get("configuration") or {}).items())}
-    return v
-
-
-def write_checkpoint(engine, table_path, now_ms=None, encoder="gpu"):
-    """SnapshotManager.checkpoint at the latest version: <v>.checkpoint.parquet + _last_checkpoint.
-    encoder "gpu": the file is encoded on the device (dk_ckpt_writer_*); "host": pyarrow.
-    Returns (version, number of add actions)."""
+def write_checkpoint(engine, table_path, now_ms=None):
+    """SnapshotManager.checkpoint at the latest version: <v>.checkpoint.parquet + _last_checkpoint,
+    the file encoded on the device (dk_ckpt_writer_*). Returns (version, number of add actions)."""
     from .kernel import Table
     snap = Table.forPath(engine, table_path).getLatestSnapshot(engine)
     v = snap.getVersion()
@@ -420,25 +360,12 @@ def write_checkpoint(engine, table_path, now_ms=None, encoder="gpu"):
     if os.path.exists(final):
         raise CheckpointAlreadyExistsException("Checkpoint for given version %d already exists in the table" % v)
     tmp = os.path.join(log, ".%020d.checkpoint.parquet.%d.tmp" % (v, os.getpid()))
-    if encoder == "gpu":
-        try:
-            n_adds = _write_gpu(engine, snap, tmp, now_ms)
-        except BaseException:
-            if os.path.exists(tmp):
-                os.remove(tmp)
-            raise
-    else:
-        import pyarrow as pa
-        import pyarrow.parquet as pq
-        actions, n_adds = checkpoint_actions(engine, snap, now_ms)
-        schema = checkpoint_schema()
-        cols = {name: [] for name in schema.names}
-        for kind, val in actions:
-            for name in schema.names:
-                cols[name].append(_arrow_value(kind, val) if name == kind else None)
-        table = pa.table({name: pa.array(cols[name], type=schema.field(name).type) for name in schema.names},
-                         schema=schema)
-        pq.write_table(table, tmp, compression="snappy")
+    try:
+        n_adds = _write_gpu(engine, snap, tmp, now_ms)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise
     try:
         os.link(tmp, final)                     # atomic, and fails when the checkpoint exists
     except FileExistsError:

@@ -643,7 +643,7 @@ class Table:
     def forPath(engine, path):
         return Table(path)
 
-    def checkpoint(self, engine, version=None, now_ms=None, encoder="gpu"):
+    def checkpoint(self, engine, version=None, now_ms=None):
         """Table.checkpoint (TableImpl.java:132-140 -> SnapshotManager.checkpoint): writes the classic
         checkpoint of the latest version and _last_checkpoint (delta_amd/checkpoint.py). Returns
         (version, number of add actions written)."""
@@ -652,7 +652,7 @@ class Table:
         if version is not None and version != latest:
             raise DkError("checkpoint: this engine writes checkpoints of the latest version (%d), not %d"
                           % (latest, version))
-        return write_checkpoint(engine, self.path, now_ms, encoder=encoder)
+        return write_checkpoint(engine, self.path, now_ms)
 
     def getLatestSnapshot(self, engine):
         t0 = time.perf_counter()

@@ -10,7 +10,55 @@ import re
 
 import pytest
 
-from delta_amd.checkpoint import checkpoint_schema
+
+# ---- CHECKPOINT_SCHEMA as Arrow types -----------------------------------------------------------
+# Field order and nullability follow the reference definitions (paths under kernel-api/.../internal/
+# actions/): SingleAction.CHECKPOINT_SCHEMA (SingleAction.java:30-37), AddFile.FULL_SCHEMA =
+# SCHEMA_WITHOUT_STATS + stats (AddFile.java:42-70), RemoveFile.FULL_SCHEMA (RemoveFile.java:23-38),
+# DeletionVectorDescriptor.READ_SCHEMA (:84-90), Metadata.FULL_SCHEMA (Metadata.java:57-72) with
+# Format.FULL_SCHEMA (Format.java:42-48), Protocol.FULL_SCHEMA (Protocol.java:49-54),
+# SetTransaction.FULL_SCHEMA (SetTransaction.java:28-32), DomainMetadata.FULL_SCHEMA
+# (DomainMetadata.java:34-38). `nullable=False` becomes a REQUIRED Parquet field.
+def checkpoint_schema():
+    import pyarrow as pa
+    S, L, B, I = pa.string(), pa.int64(), pa.bool_(), pa.int32()
+
+    def F(name, t, nullable=True):
+        return pa.field(name, t, nullable=nullable)
+
+    def M(value_nullable=True):                 # MapType(string, string, valueContainsNull)
+        return pa.map_(F("key", S, False), F("value", S, value_nullable))
+
+    def A(contains_null):                       # ArrayType(string, containsNull)
+        return pa.list_(F("element", S, contains_null))
+
+    dv = pa.struct([F("storageType", S, False), F("pathOrInlineDv", S, False), F("offset", I),
+                    F("sizeInBytes", I, False), F("cardinality", L, False)])
+    add = pa.struct([F("path", S, False), F("partitionValues", M(), False), F("size", L, False),
+                     F("modificationTime", L, False), F("dataChange", B, False), F("deletionVector", dv),
+                     F("tags", M()), F("baseRowId", L), F("defaultRowCommitVersion", L), F("stats", S)])
+    rm = pa.struct([F("path", S, False), F("deletionTimestamp", L), F("dataChange", B, False),
+                    F("extendedFileMetadata", B), F("partitionValues", M()), F("size", L), F("stats", S),
+                    F("tags", M()), F("deletionVector", dv), F("baseRowId", L), F("defaultRowCommitVersion", L)])
+    fmt = pa.struct([F("provider", S, False), F("options", M(False))])
+    meta = pa.struct([F("id", S, False), F("name", S), F("description", S), F("format", fmt, False),
+                      F("schemaString", S, False), F("partitionColumns", A(False), False), F("createdTime", L),
+                      F("configuration", M(False), False)])
+    proto = pa.struct([F("minReaderVersion", I, False), F("minWriterVersion", I, False),
+                       F("readerFeatures", A(False)), F("writerFeatures", A(False))])
+    txn = pa.struct([F("appId", S, False), F("version", L, False), F("lastUpdated", L)])
+    dm = pa.struct([F("domain", S, False), F("configuration", S, False), F("removed", B, False)])
+    return pa.schema([("txn", txn), ("add", add), ("remove", rm), ("metaData", meta), ("protocol", proto),
+                      ("domainMetadata", dm)])
+
+
+_ADD_KEYS = ("path", "partitionValues", "size", "modificationTime", "dataChange", "stats", "tags", "deletionVector",
+             "baseRowId", "defaultRowCommitVersion")
+_RM_KEYS = ("path", "deletionTimestamp", "dataChange", "extendedFileMetadata", "partitionValues", "size", "stats",
+            "tags", "deletionVector", "baseRowId", "defaultRowCommitVersion")
+_DV_KEYS = ("storageType", "pathOrInlineDv", "offset", "sizeInBytes", "cardinality")
+
+
 
 ACT = "/root/reference/kernel/kernel-api/src/main/java/io/delta/kernel/internal/actions"
 

@@ -59,6 +59,122 @@ def test_oracle_checkpoint_known_answer(tmp_path):
     assert rows[6][1][0] == "a"
 
 
+# ---- the reference's own answers: CreateCheckpointSuite.scala (kernel-defaults tests) -------------------
+SUITE_NOW = 1_700_000_000_000
+
+
+def _write_commits(d, commits):
+    log = os.path.join(d, "_delta_log")
+    os.makedirs(log)
+    for v, acts in enumerate(commits):
+        with open(os.path.join(log, "%020d.json" % v), "w") as f:
+            f.write("\n".join(json.dumps(a) for a in acts) + "\n")
+    return d
+
+
+def _suite_meta(retention=None):
+    conf = {"delta.deletedFileRetentionDuration": retention} if retention else {}
+    return {"metaData": {"id": "t", "format": {"provider": "parquet", "options": {}},
+                         "schemaString": json.dumps({"type": "struct", "fields": [
+                             {"name": "c1", "type": "integer", "nullable": True, "metadata": {}}]}),
+                         "partitionColumns": [], "configuration": conf, "createdTime": 1}}
+
+
+def _suite_add(p):
+    return {"add": {"path": p, "partitionValues": {}, "size": 0, "modificationTime": 0, "dataChange": True}}
+
+
+def _suite_remove(p, ts):
+    return {"remove": {"path": p, "deletionTimestamp": ts, "dataChange": True}}
+
+
+def suite_tombstone_log(d, retention):
+    """The log of CreateCheckpointSuite.scala:224-296 ("checkpoint contains all not expired
+    tombstones"), as commits relative to a fixed now: addFiles (each commit also updates the metadata
+    with the retention setting), then removes of file8 (ts 1), file7 (-8 days), file6 (-3 days),
+    file5 (-1 s), addFiles file10-18, removes of file3 (-9 days) and file2 (-1 day); checkpoint at 7."""
+    day = 24 * 60 * 60 * 1000
+    return _write_commits(d, [
+        [{"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}, _suite_meta(retention)] +
+        [_suite_add("file%d" % i) for i in range(1, 10)],
+        [_suite_remove("file8", 1)],
+        [_suite_remove("file7", SUITE_NOW - 8 * day)],
+        [_suite_remove("file6", SUITE_NOW - 3 * day)],
+        [_suite_remove("file5", SUITE_NOW - 1000)],
+        [_suite_meta(retention)] + [_suite_add("file%d" % i) for i in range(10, 19)],
+        [_suite_remove("file3", SUITE_NOW - 9 * day)],
+        [_suite_remove("file2", SUITE_NOW - 1 * day)],
+    ])
+
+
+# the tombstones the suite asserts per retention setting (:276-290)
+SUITE_TOMBSTONES = {None: {"file6", "file5", "file2"}, "2 days": {"file5", "file2"}, "0 days": set()}
+
+
+def suite_txn_log(d):
+    """CreateCheckpointSuite.scala:178-222 ("commits with set transactions"): idempotent appends of
+    appId1 (versions 0, 2, 3), a delete, appId2 (7, 25), appId3 (7908), a plain append, appId4."""
+    txn = lambda a, v: {"txn": {"appId": a, "version": v, "lastUpdated": 1}}   # noqa: E731
+    return _write_commits(d, [
+        [{"protocol": {"minReaderVersion": 1, "minWriterVersion": 2}}, _suite_meta(), _suite_add("p0"), txn("appId1", 0)],
+        [_suite_add("p1"), txn("appId1", 2)],
+        [_suite_add("p2"), txn("appId1", 3)],
+        [_suite_remove("p0", SUITE_NOW)],
+        [_suite_add("p4"), txn("appId2", 7)],
+        [_suite_add("p5"), txn("appId2", 25)],
+        [_suite_add("p6"), txn("appId3", 7908)],
+        [_suite_add("p7")],
+        [_suite_add("p8"), txn("appId4", 12312312)],
+    ])
+
+
+SUITE_TXNS = {"appId1": 3, "appId2": 25, "appId3": 7908, "appId4": 12312312}
+
+
+@pytest.mark.parametrize("retention", [None, "2 days", "0 days"])
+def test_oracle_suite_tombstones(tmp_path, retention):
+    """The oracle writer keeps exactly the tombstones CreateCheckpointSuite asserts."""
+    d = suite_tombstone_log(str(tmp_path), retention)
+    rows, _ = ock.checkpoint_actions(d, now_ms=SUITE_NOW)
+    assert {r[1][0] for r in rows if r[0] == "remove"} == SUITE_TOMBSTONES[retention]
+
+
+def test_oracle_suite_txns(tmp_path):
+    d = suite_txn_log(str(tmp_path))
+    rows, _ = ock.checkpoint_actions(d, now_ms=SUITE_NOW)
+    assert {r[1][0]: r[1][1] for r in rows if r[0] == "txn"} == SUITE_TXNS
+    assert sum(r[0] == "txn" for r in rows) == 4 and sum(r[0] == "protocol" for r in rows) == 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("retention", [None, "2 days", "0 days"])
+def test_gpu_suite_tombstones(tmp_path, retention):
+    """Table.checkpoint on the GPU over the suite's log writes exactly the asserted tombstones (the
+    file read back with pyarrow), and the whole file equals the oracle's rows."""
+    from delta_amd import kernel as K
+    d = suite_tombstone_log(str(tmp_path), retention)
+    eng = K.GpuEngine()
+    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=SUITE_NOW)
+    assert v == 7 and n_adds == 18 - 5
+    got = ock.read_checkpoint(os.path.join(d, "_delta_log", "%020d.checkpoint.parquet" % v))
+    assert {r[1][0] for r in got if r[0] == "remove"} == SUITE_TOMBSTONES[retention]
+    assert got == ock.checkpoint_actions(d, now_ms=SUITE_NOW)[0]
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_suite_txns(tmp_path):
+    from delta_amd import kernel as K
+    d = suite_txn_log(str(tmp_path))
+    eng = K.GpuEngine()
+    v, _ = K.Table.forPath(eng, d).checkpoint(eng, now_ms=SUITE_NOW)
+    got = ock.read_checkpoint(os.path.join(d, "_delta_log", "%020d.checkpoint.parquet" % v))
+    assert {r[1][0]: r[1][1] for r in got if r[0] == "txn"} == SUITE_TXNS
+    assert [r[0] for r in got].count("protocol") == 1
+    assert got == ock.checkpoint_actions(d, now_ms=SUITE_NOW)[0]
+    eng.close()
+
+
 def _now_keep_half(ckpt_version, n_commits):
     # synth removes carry deletionTimestamp 1.7e12 + version: keep those of the newer half
     return 1_700_000_000_000 + ckpt_version + n_commits // 2 + 604_800_000
@@ -71,9 +187,8 @@ CASES = {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("encoder", ["gpu", "host"])
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_gpu_checkpoint_write(tmp_path, name, encoder):
+def test_gpu_checkpoint_write(tmp_path, name):
     from delta_amd import kernel as K
     from delta_amd import synth
     from tests.parity_util import assert_same, oracle_scan, product_scan
@@ -93,21 +208,20 @@ def test_gpu_checkpoint_write(tmp_path, name, encoder):
     before = oracle_scan(d)
     want, want_adds = ock.checkpoint_actions(d, now)
     eng = K.GpuEngine()
-    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=now, encoder=encoder)
+    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=now)
     assert v == info["version"] and n_adds == want_adds
     # read back with pyarrow (an independent Parquet reader): rows in order, and the schema's
     # repetition / nesting as the reference declares it
     got = ock.read_checkpoint(os.path.join(log, "%020d.checkpoint.parquet" % v))
-    if encoder == "gpu":
-        import pyarrow.parquet as pq
-        from tests.test_checkpoint_schema import EXPECTED
-        pf = pq.ParquetFile(os.path.join(log, "%020d.checkpoint.parquet" % v))
-        sch = pf.schema_arrow
-        assert sch.names == ["txn", "add", "remove", "metaData", "protocol", "domainMetadata"]
-        for top in ("add", "remove", "metaData", "protocol", "txn", "domainMetadata"):
-            t = sch.field(top).type
-            assert [(t.field(i).name, t.field(i).nullable) for i in range(t.num_fields)] == EXPECTED[top], top
-        assert pf.metadata.row_group(pf.metadata.num_row_groups - 1).column(0).compression == "SNAPPY"
+    import pyarrow.parquet as pq
+    from tests.test_checkpoint_schema import EXPECTED
+    pf = pq.ParquetFile(os.path.join(log, "%020d.checkpoint.parquet" % v))
+    sch = pf.schema_arrow
+    assert sch.names == ["txn", "add", "remove", "metaData", "protocol", "domainMetadata"]
+    for top in ("add", "remove", "metaData", "protocol", "txn", "domainMetadata"):
+        t = sch.field(top).type
+        assert [(t.field(i).name, t.field(i).nullable) for i in range(t.num_fields)] == EXPECTED[top], top
+    assert pf.metadata.row_group(pf.metadata.num_row_groups - 1).column(0).compression == "SNAPPY"
     assert len(got) == len(want)
     for i, (a, b) in enumerate(zip(got, want)):
         assert a == b, (i, a, b)

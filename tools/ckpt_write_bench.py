@@ -16,7 +16,7 @@ def main():
     from delta_amd import kernel as K
     from delta_amd import synth
     rows, parts = int(sys.argv[1]), int(sys.argv[2])
-    encoder = "host" if "--host" in sys.argv else "gpu"
+    encoder = "gpu"
     d = "/tmp/dk_ckw_%d_%d" % (rows, parts)
     shutil.rmtree(d, ignore_errors=True)
     spec = synth.TableSpec(n_adds=rows, n_parts=parts, compression="snappy", n_commits=100, adds_per_commit=100,
@@ -41,7 +41,7 @@ def main():
 
     before = scan_summary()
     t0 = time.perf_counter()
-    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=1_700_000_000_000 + 10**12, encoder=encoder)
+    v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=1_700_000_000_000 + 10**12)
     dt = time.perf_counter() - t0
     path = os.path.join(d, "_delta_log", "%020d.checkpoint.parquet" % v)
     pf = pq.ParquetFile(path)
