@@ -95,6 +95,13 @@ def interval_ms(text):
     return int(total)
 
 
+_ADD_KEYS = ("path", "partitionValues", "size", "modificationTime", "dataChange", "stats", "tags", "deletionVector",
+             "baseRowId", "defaultRowCommitVersion")
+_RM_KEYS = ("path", "deletionTimestamp", "dataChange", "extendedFileMetadata", "partitionValues", "size", "stats",
+            "tags", "deletionVector", "baseRowId", "defaultRowCommitVersion")
+_DV_KEYS = ("storageType", "pathOrInlineDv", "offset", "sizeInBytes", "cardinality")
+
+
 def _pick(obj, keys):
     if obj is None:
         return None

@@ -570,28 +570,6 @@ static int read_spans(FileM& f, std::vector<Span> want) {
   return 0;
 }
 
-// pread the file's spans into its pinned image; after each `chunk` bytes, sink(offset, length) may
-// start moving that part on (the H2D copy of an image overlaps the rest of its read)
-template <class Sink>
-static int read_spans_into(FileM& f, size_t chunk, Sink&& sink) {
-  const int fd = open(f.path.c_str(), O_RDONLY);
-  if (fd < 0) return fail("Error reading Parquet file: " + f.path + " (cannot open)");
-  size_t flushed = 0;
-  for (const Span& sp : f.spans) {
-    int64_t done = 0;
-    while (done < sp.len) {
-      const ssize_t k = pread(fd, f.bytes.data() + sp.packed_off + done, (size_t)(sp.len - done), sp.file_off + done);
-      if (k <= 0) { close(fd); return fail("Error reading Parquet file: " + f.path + " (short read)"); }
-      done += k;
-      const size_t at = (size_t)(sp.packed_off + done);
-      if (at - flushed >= chunk) { if (sink(flushed, at - flushed)) { close(fd); return 1; } flushed = at; }
-    }
-  }
-  close(fd);
-  if (f.bytes.size() > flushed && sink(flushed, f.bytes.size() - flushed)) return 1;
-  return 0;
-}
-
 static int parse_footer(FileM& f) {
   const std::vector<uint8_t>& b = f.footer;
   TReader t{b.data(), b.data() + b.size(), 0};
@@ -1078,29 +1056,7 @@ static int upload(DBuf& d, const void* src, size_t n, hipStream_t s) {
 }
 
 
-
-// Per-page and per-tile kernels are launched once over every page / tile, or -- with
-// DK_SPLIT_LAUNCH=1, a profiling aid -- once per column so that rocprofv3's kernel trace
-// attributes time to columns.
-static bool split_launch() {
-  static const bool split = getenv("DK_SPLIT_LAUNCH") && atoi(getenv("DK_SPLIT_LAUNCH")) != 0;
-  return split;
-}
-template <class F>
-static void per_column(const dk_parquet* p, int n, F&& f) {
-  if (!split_launch()) { f(0, n); return; }
-  int covered = 0;
-  for (const DColumn& c : p->h_cols) { f(c.first_page, c.n_pages); covered += c.n_pages; }
-  if (covered < n) f(covered, n - covered);    // dictionary pages (after every data page)
-}
-template <class F>
-static void per_column_tiles(const dk_parquet* p, F&& f) {
-  if (!split_launch()) { f(0, p->n_ltiles); return; }
-  for (const DColumn& c : p->h_cols) f(c.first_tile, c.n_tiles);
-}
-
-// Snappy page mode: DK_SNAPPY_MODE=page|frag forces it; by default page mode once the compressed
-// pages outnumber 8 waves per SIMD of the chip (k_snap_frag waves are LDS-limited to about that).
+// Snappy page mode (DK_SNAPPY_MODE=page): one wave decodes a whole page in order.
 static bool snap_page_mode(const dk_parquet* p) {
   static const char* env = getenv("DK_SNAPPY_MODE");
   (void)p;
@@ -1173,15 +1129,11 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
     { KTimer::Scope s3(&T, 21, s); launch_snappy(X, ncp, nfr, wk, 3, s); }
   }
   { KTimer::Scope sc(&T, 15, s); launch_page_runs(C, P + R.pa, np, arena, runs, s); }
-  auto tiles = [&](auto&& f) {
-    if (!split_launch()) { f(R.t0, R.t1 - R.t0); return; }
-    for (int c = R.col0; c < R.col1; c++) f(p->h_cols[c].first_tile, p->h_cols[c].n_tiles);
-  };
-  { KTimer::Scope sc(&T, 2, s); tiles([&](int a, int k) { launch_tile_count(C, P, arena, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 2, s); launch_tile_count(C, P, arena, runs, LT, R.t1 - R.t0, R.t0, s); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
   { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0, s); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P + R.pa, np, arena, p->d_dbp.as<long long>(), s); }
-  { KTimer::Scope sc(&T, 16, s); tiles([&](int a, int k) { launch_tile_chars(C, P, arena, pos, runs, LT, k, a, s); }); }
+  { KTimer::Scope sc(&T, 16, s); launch_tile_chars(C, P, arena, pos, runs, LT, R.t1 - R.t0, R.t0, s); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
 }
 
@@ -1202,25 +1154,14 @@ static void decode_cols(dk_parquet* p, hipStream_t s, int c0, int c1) {
   {
     KTimer::Scope sc(&T, 6, s);
     const int2* tiles = p->d_tiles.as<int2>();
-    if (!split_launch()) {
-      const int t0 = p->col_tile0[c0], t1 = p->col_tile0[c1];
-      if (t1 > t0) launch_string_copy(C, P, t1 - t0, cols, arena, pos, tiles, s, t0, p->copy_cb);
-    } else {
-      for (int c = c0; c < c1; c++)
-        launch_string_copy(C, P, p->col_tile0[c + 1] - p->col_tile0[c], cols, arena, pos, tiles, s, p->col_tile0[c],
-                           p->copy_cb);
-    }
+    const int t0 = p->col_tile0[c0], t1 = p->col_tile0[c1];
+    if (t1 > t0) launch_string_copy(C, P, t1 - t0, cols, arena, pos, tiles, s, t0, p->copy_cb);
   }
   {
     KTimer::Scope sc(&T, 5, s);
-    if (!split_launch()) {
-      const int a = p->h_cols[c0].first_tile;
-      const int b = c1 < p->n_cols ? p->h_cols[c1].first_tile : p->n_ltiles;
-      if (b > a) launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, b - a, a, st, s);
-    } else {
-      for (int c = c0; c < c1; c++)
-        launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, p->h_cols[c].n_tiles, p->h_cols[c].first_tile, st, s);
-    }
+    const int a = p->h_cols[c0].first_tile;
+    const int b = c1 < p->n_cols ? p->h_cols[c1].first_tile : p->n_ltiles;
+    if (b > a) launch_tile_decode(C, P, cols, arena, pos, dbp, runs, LT, b - a, a, st, s);
   }
 }
 
@@ -1403,18 +1344,6 @@ static int alloc_outputs(dk_parquet* p, int c0, int c1, const std::vector<DColum
   arena_bytes = arena_at;
   }
   return 0;
-}
-
-// Per-slice output allocation + value decode inside the open: the prerequisite of
-// dk_parquet_open_async's overlap, on for asynchronous opens (DK_SLICE_DECODE=0 turns it and with it
-// the asynchronous open off; =1 turns it on for synchronous opens too)
-static bool slice_decode_on() {
-  static const bool on = !(getenv("DK_SLICE_DECODE") && atoi(getenv("DK_SLICE_DECODE")) == 0);
-  return on;
-}
-static bool slice_decode_forced() {
-  static const bool on = getenv("DK_SLICE_DECODE") && atoi(getenv("DK_SLICE_DECODE")) != 0;
-  return on;
 }
 
 // hipEventQuery: 1 complete, 0 not yet, -1 an error (reported through fail): a sticky device fault
@@ -1665,10 +1594,8 @@ static int prepare(dk_parquet* p) {
       });
       if (upload_zc(p, p->d_pwork, pwork.data(), pwork.size() * sizeof(int2), us)) return 1;
     }
-    // page mode finds tags through a bitmap built by the speculative walk (DK_SNAP_BITS=0: the
-    // in-kernel pointer-doubling discovery instead)
-    static const bool bits = !getenv("DK_SNAP_BITS") || atoi(getenv("DK_SNAP_BITS")) != 0;
-    if (bits && (snap_page_mode(p) || snap_hybrid(p)) && p->d_tbits.alloc(((size_t)p->n_segs * (DK_SNAP_SEG / 64) + 4) * 8)) return 1;
+    // page and hybrid modes find tags through a bitmap built by the speculative walk
+    if ((snap_page_mode(p) || snap_hybrid(p)) && p->d_tbits.alloc(((size_t)p->n_segs * (DK_SNAP_SEG / 64) + 4) * 8)) return 1;
   }
   if (p->d_dbp.alloc((size_t)(dbp_n + 16) * 8)) return 1;
   p->bytes_arena = arena_n;
@@ -1694,18 +1621,17 @@ static int prepare(dk_parquet* p) {
   // previous slice is queued, at least 1/DK_OPEN_SLICES of the bytes (the host waits for more
   // files until it has that much, or the rest) -- each slice's passes have a fixed latency cost
   // (k_snap_fix's per-page chains), so fewer, larger slices once the reads have run ahead.
-  // DK_OPEN_ADAPTIVE=0: fixed slices of 1/DK_OPEN_SLICES of the bytes.
+  // Asynchronous opens also allocate the outputs and decode the values slice by slice.
   {
     const int nf = (int)p->files.size();
     int64_t total = 0;
     for (const FileM& f : p->files) total += (int64_t)f.bytes.size();
     static const int want = getenv("DK_OPEN_SLICES") ? std::max(1, atoi(getenv("DK_OPEN_SLICES"))) : 8;
-    static const bool adaptive = !getenv("DK_OPEN_ADAPTIVE") || atoi(getenv("DK_OPEN_ADAPTIVE")) != 0;
     const int slices = snap_page_mode(p) ? 1 : want;
     const int64_t target = std::max<int64_t>(1, total / slices);
     int f0 = 0;
     int64_t acc = 0;
-    per_slice = adaptive && slices > 1 && (p->async_open ? slice_decode_on() : slice_decode_forced());
+    per_slice = slices > 1 && p->async_open;
     std::vector<SizedSlice> sized;
     if (per_slice) {
       // string-copy tiles: a bound from the headers (PLAIN byte-array data pages and key-column
@@ -1726,7 +1652,7 @@ static int prepare(dk_parquet* p) {
       p->copy_cb = 0;
       p->bytes_written = 0;
     }
-    if (adaptive && slices > 1) {
+    if (slices > 1) {
       // slices touch disjoint pages / segments / tiles / columns: they rotate over up to three
       // streams (DK_OPEN_STREAMS), so one slice's latency tail (k_snap_fix / k_snap_frag's longest
       // pages) overlaps the next slice's passes; `s` joins them all at the end
@@ -1886,9 +1812,8 @@ static int prepare(dk_parquet* p) {
   }
   p->slice.assign(p->h_cols.size(), HostCol());
   p->prepared = true;
-  static const bool no_reuse = getenv("DK_NO_PREPARE_REUSE") && atoi(getenv("DK_NO_PREPARE_REUSE"));
-  p->fresh = !no_reuse;
-  p->decoded_fresh = per_slice && !no_reuse;
+  p->fresh = true;
+  p->decoded_fresh = per_slice;
   return 0;
 }
 
@@ -2481,44 +2406,35 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   std::vector<std::string> rerrs(n_files > 0 ? n_files : 0);   // the reader's errors
   // then the images: read into pinned memory, each going to HBM in 8 MiB pieces on a copy stream while
   // the rest of it (and the other files) are still being read -- on background threads, while prepare
-  // runs the sizing passes over the files whose copies have landed (DK_OPEN_OVERLAP=0: every image is
-  // read before prepare)
+  // runs the sizing passes over the files whose copies have landed
   p->queued.reset(new std::atomic<int>[n_files > 0 ? n_files : 1]);
   for (int fi = 0; fi < n_files; fi++) p->queued[fi].store(0);
-  // Pieces (default): every span cut into 8 MiB pieces, all threads working through them in file
-  // order, so files land one after another from the first milliseconds on (one file per thread
-  // would land the first file only after a sixteenth of the whole read); the thread that finishes a
-  // file's last piece records its event. DK_OPEN_PIECES=0: one file per thread.
-  struct Piece { int fi; int64_t file_off, packed_off, len; };
+  // Pieces: every image cut into 8 MiB pieces, all threads working through them in file order, so
+  // files land one after another from the first milliseconds on (one file per thread would land the
+  // first file only after a sixteenth of the whole read); the thread that finishes a file's last
+  // piece records its event.
+  struct Piece { int fi; int64_t packed_off, len; };
   std::vector<Piece> pieces;
-  static const bool by_piece = !getenv("DK_OPEN_PIECES") || atoi(getenv("DK_OPEN_PIECES")) != 0;
   static const int64_t piece = (int64_t)(getenv("DK_PIECE_MB") ? std::max(1, atoi(getenv("DK_PIECE_MB"))) : 8) << 20;
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[n_files > 0 ? n_files : 1]);
   std::unique_ptr<int[]> fds(new int[n_files > 0 ? n_files : 1]);
-  // Windows (default): pieces are `piece`-byte windows of the packed image, whatever spans they
-  // cut; a window's spans are read into it, then the whole window (padding between spans included)
-  // goes to HBM in one copy. Cutting by span instead gave every small column chunk a copy of its own,
-  // which HIP runs as a blit kernel on the copy stream between the DMA transfers (160 per stream per
-  // C3 step, ~20 ms of each stream's time). DK_OPEN_WINDOWS=0: pieces cut per span.
-  static const bool windows = !getenv("DK_OPEN_WINDOWS") || atoi(getenv("DK_OPEN_WINDOWS")) != 0;
+  // A piece is a `piece`-byte window of the packed image, whatever spans it cuts; the window's spans
+  // are read into it, then the whole window (padding between spans included) goes to HBM in one
+  // copy. Cutting by span instead gave every small column chunk a copy of its own, which HIP runs as
+  // a blit kernel on the copy stream between the DMA transfers (160 per stream per C3 step, ~20 ms
+  // of each stream's time).
   for (int fi = 0; fi < n_files; fi++) {
     int n = 0;
     fds[fi] = -1;
     const FileM& f = p->files[fi];
-    if (by_piece && windows) {
-      const int64_t size = f.spans.empty() ? 0 : f.spans.back().packed_off + f.spans.back().len;
-      for (int64_t o = 0; o < size; o += piece, n++) pieces.push_back({fi, -1, o, std::min<int64_t>(piece, size - o)});
-    } else if (by_piece) {
-      for (const Span& sp : f.spans)
-        for (int64_t o = 0; o < sp.len; o += piece, n++)
-          pieces.push_back({fi, sp.file_off + o, sp.packed_off + o, std::min<int64_t>(piece, sp.len - o)});
-    }
+    const int64_t size = f.spans.empty() ? 0 : f.spans.back().packed_off + f.spans.back().len;
+    for (int64_t o = 0; o < size; o += piece, n++) pieces.push_back({fi, o, std::min<int64_t>(piece, size - o)});
     left[fi].store(n);
   }
   const int no_drain = t_no_drain;
   std::thread reader([&, no_drain] {
     t_no_drain = no_drain;
-    if (by_piece) {
+    {
       for (int fi = 0; fi < n_files; fi++) {
         fds[fi] = open(p->files[fi].path.c_str(), O_RDONLY);
         if (fds[fi] < 0) { rerrs[fi] = "Error reading Parquet file: " + p->files[fi].path + " (cannot open)"; p->queued[fi].store(2); }
@@ -2542,14 +2458,10 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
         hipSetDevice(e->cfg.device);
         hipStream_t cs = p->copy[pc.fi % copy_streams()].s;
         bool ok = true;
-        if (pc.file_off >= 0) {                       // one span's piece
-          ok = pread_full(fds[pc.fi], f.bytes.data() + pc.packed_off, pc.len, pc.file_off) == 0;
-        } else {                                      // a window: the parts of every span inside it
-          const int64_t w0 = pc.packed_off, w1 = w0 + pc.len;
-          for (const Span& sp : f.spans) {
-            const int64_t a = std::max(w0, sp.packed_off), b = std::min(w1, sp.packed_off + sp.len);
-            if (a < b && pread_full(fds[pc.fi], f.bytes.data() + a, b - a, sp.file_off + (a - sp.packed_off))) { ok = false; break; }
-          }
+        const int64_t w0 = pc.packed_off, w1 = w0 + pc.len;   // the parts of every span inside the window
+        for (const Span& sp : f.spans) {
+          const int64_t a = std::max(w0, sp.packed_off), b = std::min(w1, sp.packed_off + sp.len);
+          if (a < b && pread_full(fds[pc.fi], f.bytes.data() + a, b - a, sp.file_off + (a - sp.packed_off))) { ok = false; break; }
         }
         ok = ok && hipMemcpyAsync(p->dfile[pc.fi].as<uint8_t>() + pc.packed_off, f.bytes.data() + pc.packed_off,
                                   (size_t)pc.len, hipMemcpyHostToDevice, cs) == hipSuccess;
@@ -2576,34 +2488,15 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
         p->queued[fi].compare_exchange_strong(expect, 2);
         if (expect == 0 && rerrs[fi].empty()) rerrs[fi] = "Error reading Parquet file: " + p->files[fi].path + " (short read)";
       }
-      return;
     }
-    parallel_for(n_files, [&](int fi) {
-      FileM& f = p->files[fi];
-      hipSetDevice(e->cfg.device);
-      hipStream_t cs = p->copy[fi % copy_streams()].s;
-      uint8_t* dst = p->dfile[fi].as<uint8_t>();
-      if (read_spans_into(f, (size_t)8 << 20, [&](size_t off, size_t len) {
-            return hipMemcpyAsync(dst + off, f.bytes.data() + off, len, hipMemcpyHostToDevice, cs) == hipSuccess
-                       ? 0 : fail("hipMemcpyAsync failed for " + f.path);
-          })) { rerrs[fi] = g_err; p->queued[fi].store(2, std::memory_order_release); return; }
-      if (hipEventRecord(p->file_ev[fi], cs) != hipSuccess) {
-        rerrs[fi] = "hipEventRecord failed";
-        p->queued[fi].store(2, std::memory_order_release);
-        return;
-      }
-      p->queued[fi].store(1, std::memory_order_release);
-    });
   });
   struct Joiner { std::thread& t; ~Joiner() { if (t.joinable()) t.join(); } } joiner{reader};
-  static const bool overlap = !getenv("DK_OPEN_OVERLAP") || atoi(getenv("DK_OPEN_OVERLAP")) != 0;
   auto read_errors = [&]() -> int {
     if (reader.joinable()) reader.join();
     for (int fi = 0; fi < n_files; fi++)
       if (!rerrs[fi].empty()) return fail(rerrs[fi]);
     return 0;
   };
-  if (!overlap && read_errors()) return 1;
   const auto t_io1 = std::chrono::steady_clock::now();
   for (int fi = 0; fi < n_files; fi++) {             // concatenate the files' tables in file order
     FileMeta& M = metas[fi];
@@ -2696,9 +2589,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
 extern "C" int dk_parquet_open_async(dk_engine* e, const char* const* paths, int32_t n_files, const char* const* leaves,
                                      int32_t n_leaves, const int32_t* rg_count, const int32_t* rg_list, dk_parquet** out) {
   *out = nullptr;
-  const bool slice_decode = slice_decode_on() &&
-                            !(getenv("DK_OPEN_ADAPTIVE") && atoi(getenv("DK_OPEN_ADAPTIVE")) == 0) &&
-                            !(getenv("DK_SNAPPY_MODE") && !strcmp(getenv("DK_SNAPPY_MODE"), "page")) &&
+  const bool slice_decode = !(getenv("DK_SNAPPY_MODE") && !strcmp(getenv("DK_SNAPPY_MODE"), "page")) &&
                             !(getenv("DK_ASYNC_OPEN") && atoi(getenv("DK_ASYNC_OPEN")) == 0) &&
                             !(getenv("DK_OPEN_SLICES") && atoi(getenv("DK_OPEN_SLICES")) <= 1);
   if (!slice_decode) return dk_parquet_open_sel(e, paths, n_files, leaves, n_leaves, rg_count, rg_list, out);
@@ -4087,8 +3978,7 @@ static int replay_attach(dk_replay* r, dk_parquet* ckpt) {
       total += ckpt->files[fi].num_rows;
     }
     // every file in one probe launch while global row numbers fit the int32 candidate list
-    static const bool per_file = getenv("DK_PROBE_PER_FILE") && atoi(getenv("DK_PROBE_PER_FILE"));
-    r->probe_all = !per_file && nf > 1 && total < (1ll << 31) - 1;
+    r->probe_all = nf > 1 && total < (1ll << 31) - 1;
     if (r->d_cand.alloc((size_t)(r->probe_all ? total : max_rows) * 4 + 64)) return 1;
     if (r->d_cand_n.alloc(64)) return 1;
     for (size_t fi = 0; fi < nf; fi++) {
@@ -4576,10 +4466,9 @@ extern "C" int dk_replay_set_skipping(dk_replay* r, const dk_program* prog) {
   // stand for (k_stats_parsed)
   r->ck_parsed.assign(r->ck ? r->ck->files.size() : 0, StatsParsedRows{});
   r->typed_paths.clear();
-  static const bool no_parsed = getenv("DK_NO_STATS_PARSED") && atoi(getenv("DK_NO_STATS_PARSED"));
   std::vector<TypedPath> all;
   std::vector<size_t> at(r->ck_parsed.size(), SIZE_MAX);
-  for (size_t fi = 0; fi < r->ck_parsed.size() && !no_parsed; fi++) {
+  for (size_t fi = 0; fi < r->ck_parsed.size(); fi++) {
     StatsParsedRows R{};
     R.n_paths = np;
     R.struct_def = 2;                     // add (1) . stats_parsed (2)
@@ -5573,11 +5462,6 @@ extern "C" int dk_replay_sync(dk_replay* r) {
                   " in checkpoint row " + std::to_string(r->h_state.err_row));
     }
     r->have_result = true;
-    if (getenv("DK_PROBE_STATS") && r->ck) {   // diagnostics: candidates of the last probed file
-      unsigned int nc = 0;
-      HIPOK(hipMemcpy(&nc, r->d_cand_n.p, sizeof nc, hipMemcpyDeviceToHost));
-      fprintf(stderr, "[dk] probe candidates (last file): %u\n", nc);
-    }
     return 0;
   }
   return fail("replay: repeated key-hash collisions");

@@ -697,12 +697,7 @@ enum : int { SX_NO_FAR = 1, SX_NO_BYTES = 2, SX_NO_RESOLVE = 4, SX_ONLY_DISCOVER
 #ifndef DK_SF_WPE
 #define DK_SF_WPE 5
 #endif
-#ifndef DK_SF_FARQ16
-#define DK_SF_FARQ16 1
-#endif
-#ifndef DK_SF_FARQ_MAX
-#define DK_SF_FARQ_MAX 8
-#endif
+constexpr int SF_FARQ_MAX = 8;             // far copies up to this long are loaded early (three dwords)
 #if DK_SF_WPE > 0
 #define SF_WPE_ATTR __attribute__((amdgpu_waves_per_eu(DK_SF_WPE)))
 #else
@@ -997,18 +992,13 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
     }
     if (__ballot(bad)) { bad = true; break; }
     SSTAT(0, 1); SSTAT(1, n); SSTAT(11, __popcll(__ballot(valid && !is_copy)));
-#if DK_SF_FARQ16
-    // far copies of <= 16 bytes (two thirds of all copies reach past the 4 KiB ring on path data):
+    // far copies of <= 8 bytes (two thirds of all copies reach past the 4 KiB ring on path data):
     // their source words are loaded here, unconditionally (no lane waits on a branch), and consumed
     // only after the byte-parallel stage, so the load latency hides behind the resolve and map work
-    const bool farq = valid && mode == SM_FAR && len <= DK_SF_FARQ_MAX && !(xf & SX_NO_FAR);
+    const bool farq = valid && mode == SM_FAR && len <= SF_FARQ_MAX && !(xf & SX_NO_FAR);
     if (farq) mode = SM_FARQ;
     const uintptr_t fa = farq ? (((uintptr_t)(out + src)) & ~(uintptr_t)3) : (((uintptr_t)in) & ~(uintptr_t)15);
     const uint32_t fw0 = ((const GAS uint32_t*)fa)[0], fw1 = ((const GAS uint32_t*)fa)[1], fw2 = ((const GAS uint32_t*)fa)[2];
-#if DK_SF_FARQ_MAX > 8
-    const uint32_t fw3 = ((const GAS uint32_t*)fa)[3], fw4 = ((const GAS uint32_t*)fa)[4];
-#endif
-#endif
     for (int round = 0; round < ((xf & SX_NO_RESOLVE) ? 0 : 6); round++) {
       const bool act = valid && mode == SM_DEP && !stuck;
       if (!__ballot(act)) break;
@@ -1035,21 +1025,6 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
       }
     }
     STIME(16);                                   // modes + resolution
-    // far sources of <= 8 bytes (most: short matches far back): the owning lane loads them with
-    // three dwords from the output this wave flushed to HBM, now, and stores them after step 5
-#if !DK_SF_FARQ16
-    const int32_t ext_f = per ? per : len;
-    if (valid && mode == SM_FAR && ext_f <= 8 && len <= 8) mode = SM_FARQ;
-    const bool farq = valid && mode == SM_FARQ;
-    uint32_t fw0 = 0, fw1 = 0, fw2 = 0;
-    if (!(xf & SX_NO_FAR) && __ballot(farq)) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (farq) {
-        const GAS uint32_t* a = (const GAS uint32_t*)(((uintptr_t)(out + src)) & ~(uintptr_t)3);
-        fw0 = a[0]; fw1 = a[1]; fw2 = a[2];
-      }
-    }
-#endif
     STIME(17);                                   // far-quick loads issued
     // ---- 5. byte-parallel production of every WIN / RING / FAR tag ----
     const int32_t CH = (xf & SX_NO_BYTES) ? 0 : (total + 63) >> 6;   // output bytes per lane (<= SF_CH)
@@ -1108,31 +1083,15 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
         for (int32_t k = 0; k < SF_CH; k++) if (sa[k] <= -2) L[(o + b0 + k) & SF_RM] = (uint8_t)gv[k];
       }
     }
-#if DK_SF_FARQ16
     if (farq) {                                    // (a far source never overlaps its copy: per = 0)
       const uint32_t sh = (uint32_t)(((uintptr_t)(out + src)) & 3);
       for (int32_t i = 0; i < len; i++) {
         const uint32_t k = sh + (uint32_t)i;
         const uint32_t q = k >> 2;
-#if DK_SF_FARQ_MAX > 8
-        const uint32_t w = q == 0 ? fw0 : q == 1 ? fw1 : q == 2 ? fw2 : q == 3 ? fw3 : fw4;
-#else
         const uint32_t w = q == 0 ? fw0 : q == 1 ? fw1 : fw2;
-#endif
         L[(ot + i) & SF_RM] = (uint8_t)(w >> (8 * (k & 3)));
       }
     }
-#else
-    if (farq) {
-      const uint32_t sh = (uint32_t)(((uintptr_t)(out + src)) & 3);
-      const uint32_t rc = small_rcp(per);
-      for (int32_t i = 0; i < len; i++) {
-        const uint32_t k = sh + (uint32_t)(per ? small_mod(i, per, rc) : i);
-        const uint32_t w = k < 4 ? fw0 : (k < 8 ? fw1 : fw2);
-        L[(ot + i) & SF_RM] = (uint8_t)(w >> (8 * (k & 3)));
-      }
-    }
-#endif
     STIME(18);                                   // bytes + far
     // ---- 6. sources straddling tags of this batch: one tag at a time, in order ----
     unsigned long long m = __ballot(valid && mode == SM_DEP);

@@ -137,6 +137,7 @@ def test_oracle_suite_tombstones(tmp_path, retention):
     d = suite_tombstone_log(str(tmp_path), retention)
     rows, _ = ock.checkpoint_actions(d, now_ms=SUITE_NOW)
     assert {r[1][0] for r in rows if r[0] == "remove"} == SUITE_TOMBSTONES[retention]
+    assert sum(r[0] == "add" for r in rows) == 18 - 6
 
 
 def test_oracle_suite_txns(tmp_path):
@@ -153,12 +154,13 @@ def test_gpu_suite_tombstones(tmp_path, retention):
     file read back with pyarrow), and the whole file equals the oracle's rows."""
     from delta_amd import kernel as K
     d = suite_tombstone_log(str(tmp_path), retention)
+    want = ock.checkpoint_actions(d, now_ms=SUITE_NOW)[0]        # (before the checkpoint exists)
     eng = K.GpuEngine()
     v, n_adds = K.Table.forPath(eng, d).checkpoint(eng, now_ms=SUITE_NOW)
-    assert v == 7 and n_adds == 18 - 5
+    assert v == 7 and n_adds == 18 - 6            # file1..file18 less the six removed
     got = ock.read_checkpoint(os.path.join(d, "_delta_log", "%020d.checkpoint.parquet" % v))
     assert {r[1][0] for r in got if r[0] == "remove"} == SUITE_TOMBSTONES[retention]
-    assert got == ock.checkpoint_actions(d, now_ms=SUITE_NOW)[0]
+    assert got == want
     eng.close()
 
 
@@ -166,12 +168,13 @@ def test_gpu_suite_tombstones(tmp_path, retention):
 def test_gpu_suite_txns(tmp_path):
     from delta_amd import kernel as K
     d = suite_txn_log(str(tmp_path))
+    want = ock.checkpoint_actions(d, now_ms=SUITE_NOW)[0]
     eng = K.GpuEngine()
     v, _ = K.Table.forPath(eng, d).checkpoint(eng, now_ms=SUITE_NOW)
     got = ock.read_checkpoint(os.path.join(d, "_delta_log", "%020d.checkpoint.parquet" % v))
     assert {r[1][0]: r[1][1] for r in got if r[0] == "txn"} == SUITE_TXNS
     assert [r[0] for r in got].count("protocol") == 1
-    assert got == ock.checkpoint_actions(d, now_ms=SUITE_NOW)[0]
+    assert got == want
     eng.close()
 
 

@@ -3,7 +3,7 @@ fragment-boundary walk of k_snap_fix was only checked end to end).
 
   default       hybrid: speculative walk + link, k_snap_fix verifies entries, rewrites the tag-start
                 bitmap and walks it to every 64 KiB fragment start; k_snap_frag decodes fragments
-  DK_SNAP_BITS=0  the same without the bitmap (k_snap_fix walks to the fragment starts tag by tag)
+  DK_SNAPPY_MODE=frag  fragments without the bitmap (k_snap_fix walks to the fragment starts tag by tag)
   DK_SNAPPY_MODE=page  one wave decodes a whole page in order (no fragments)
 
 Pages are crafted to stress the walk: long incompressible literals that cross many 2 KiB segments,
@@ -83,8 +83,8 @@ def _digest_product(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{}, {"DK_SNAP_BITS": "0"}, {"DK_SNAPPY_MODE": "page"}],
-                         ids=["hybrid-bitmap", "hybrid-no-bitmap", "page"])
+@pytest.mark.parametrize("env", [{}, {"DK_SNAPPY_MODE": "frag"}, {"DK_SNAPPY_MODE": "page"}],
+                         ids=["hybrid-bitmap", "frag-no-bitmap", "page"])
 def test_gpu_snappy_modes_equal_pyarrow(tmp_path, env):
     path = str(tmp_path / "s.parquet")
     want = _digest_expected(_write(path, 31))
