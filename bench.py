@@ -62,10 +62,11 @@ CONFIGS = {
                spec=dict(pv_keys=1, n_commits=100, adds_per_commit=50, removes_per_commit=50),
                desc="C1: %d-AddFile single-part uncompressed checkpoint per GPU, 100-commit JSON tail; "
                     "read schema add(no stats)+remove"),
-    "c2": dict(rows=10_000_000, shared=False, stats=False, predicate=None,
-               spec=dict(pv_keys=2, with_stats_parsed=True, n_commits=100, adds_per_commit=50, removes_per_commit=50),
-               desc="C2: %d-AddFile single-part checkpoint per GPU, 2-key partitionValues, stats_parsed present, "
-                    "100-commit JSON tail; read schema add(no stats)+remove"),
+    "c2": dict(rows=10_000_000, shared=False, stats=True, predicate=None,
+               spec=dict(pv_keys=2, compression="snappy", with_stats=True, with_stats_parsed=True, n_commits=100,
+                         adds_per_commit=50, removes_per_commit=50),
+               desc="C2: %d-AddFile single-part snappy checkpoint per GPU, 2-key partitionValues, stats JSON + "
+                    "stats_parsed, 100-commit JSON tail; read schema add(with stats)+remove (C2b)"),
     "c3": dict(rows=100_000_000, shared=True, stats=False, predicate=None,
                spec=dict(n_parts=64, compression="snappy", n_commits=1000, adds_per_commit=100,
                          removes_per_commit=100, readd_frac=0.1, dup_frac=0.05),
@@ -393,6 +394,8 @@ def main(argv=None):
                          "alltoall = allgather's tail, checkpoint rows pre-filtered by their path-hash owner "
                          "(DESIGN.md §6)")
     ap.add_argument("--workdir", default=None)
+    ap.add_argument("--jmh-ops", type=int, default=3,
+                    help="timed JMH-shaped operations (engine + forPath + snapshot + getScanFiles consumed)")
     args = ap.parse_args(argv)
 
     env_world = int(os.environ.get("WORLD_SIZE", "0") or 0)
@@ -746,6 +749,41 @@ def main(argv=None):
                     "partition_entries_per_step": f_pv // k,
                     "d2h_bytes_per_step": f_d2h // k, "leaves": list(FULL_LEAVES)}
 
+    # ---- beside the headline: the JMH operation itself (BenchmarkParallelCheckpointReading.java:110-139):
+    # a new engine, Table.forPath, getLatestSnapshot, getScanState, getScanFiles consumed (sum of
+    # add.size), engine closed -- one warm-up op, then --jmh-ops timed ops, average time per op ----
+    jmh = None
+    if args.jmh_ops > 0 and world == 1:
+        def jmh_op():
+            t_o = time.perf_counter()
+            e2 = K.GpuEngine()
+            sn = K.Table.forPath(e2, work).getLatestSnapshot(e2)
+            sb = sn.getScanBuilder().withStats(cfg["stats"])
+            if cfg["predicate"]:
+                from delta_amd.expressions import Column, Literal, Predicate
+                col, op, lit = cfg["predicate"]
+                sb = sb.withFilter(Predicate(op, Column(col), Literal.ofLong(lit)))
+            sc = sb.build()
+            sc.getScanState(e2)
+            size_sum = 0
+            for b in sc.getScanFiles(e2):
+                v = b.data["add.size"].fixed.view("<i8")
+                size_sum += int(v.sum()) if b.selection is None else masked_sum(v, b.selection)[0]
+            b = v = None
+            seen = sc.metrics.addFilesSeen
+            sc.close()
+            e2.close()
+            return seen, size_sum, (time.perf_counter() - t_o) * 1e3
+        jmh_op()                                                  # warm-up (JMH's warm-up iterations)
+        ops = [jmh_op() for _ in range(args.jmh_ops)]
+        ms = sum(o[2] for o in ops) / len(ops)
+        jmh = {"definition": "BenchmarkParallelCheckpointReading.benchmark: new engine + Table.forPath + "
+                             "getLatestSnapshot + getScanState + getScanFiles consumed (sum of add.size over the "
+                             "selected rows) + engine close; average time per op after one warm-up op",
+               "ms_per_op": ms, "ops": len(ops), "ops_ms": [round(o[2], 2) for o in ops],
+               "actions_per_s": ops[0][0] / (ms * 1e-3), "addFilesSeen_per_op": ops[0][0],
+               "size_sum_matches_headline": ops[0][1] == size_all // args.steps}
+
     result = {
         "metric": METRIC,
         "value": value,
@@ -788,6 +826,7 @@ def main(argv=None):
                                                for k in owner_ms[0]} if owner_ms else None),
                         "prepare_s": prepare_s},
         "full_row_consume": full_row,
+        "jmh_op": jmh,
         "snapshot_load_ms": snapshot_ms,
         "snapshot_load_cold_ms": snapshot_cold_ms,
         "engine_create_ms": engine_create_ms,

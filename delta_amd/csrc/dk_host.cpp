@@ -2766,6 +2766,16 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
   return 0;
 }
 
+// DK_MIRROR_DMA=1 (A/B): an asynchronous open's column mirrors as DMA copies on a copy-class stream
+// instead of k_copy_zc on a normal one
+static bool mirror_dma() {
+  static const bool on = getenv("DK_MIRROR_DMA") && atoi(getenv("DK_MIRROR_DMA")) != 0;
+  return on;
+}
+static int create_mirror_stream(dk_parquet* p) {
+  return mirror_dma() ? p->mir.create_class(copy_class_on() ? kStreamCopy : kStreamNormal) : p->mir.create();
+}
+
 // queue the D2H copy of decoded column ci into its pinned mirror (on the parquet stream, so it
 // follows the decode that produced the column)
 static int queue_mirror(dk_parquet* p, int ci) {
@@ -2775,7 +2785,7 @@ static int queue_mirror(dk_parquet* p, int ci) {
   // own stream (an asynchronous open keeps queueing its passes on `stream`); while the open's H2D
   // copies are in flight the copies are made by a kernel into the pinned mirror (a DMA copy would
   // queue behind them)
-  if (p->async_open && !p->mir.s && p->mir.create()) return 1;
+  if (p->async_open && !p->mir.s && create_mirror_stream(p)) return 1;
   hipStream_t s = p->async_open ? p->mir.s : p->stream;
   if (p->async_open && p->open_state.load() != 0) {   // after the decode queued on `stream`
     if (!p->mir_ev) HIPOK(hipEventCreateWithFlags(&p->mir_ev, hipEventDisableTiming));
@@ -2785,7 +2795,7 @@ static int queue_mirror(dk_parquet* p, int ci) {
   const int cf = p->col_file[ci];
   if (cf < (int)p->file_done.size() && p->file_done[cf]) HIPOK(hipStreamWaitEvent(s, p->file_done[cf], 0));
   if (cf < (int)p->file_dec.size() && p->file_dec[cf]) HIPOK(hipStreamWaitEvent(s, p->file_dec[cf], 0));
-  const bool zc = p->async_open;
+  const bool zc = p->async_open && !mirror_dma();
   auto d2h = [&](void* dst, const void* src, size_t n) -> int {
     if (!n) return 0;
     if (zc) { launch_copy_zc(dst, src, (long long)n, s); return 0; }
@@ -5212,7 +5222,7 @@ static int owner_launch(dk_replay* r) {
     if (!r->prefetch.empty()) {
       // the prefetched leaves (add.size) go to host memory now, on the mirror stream, while the
       // row exchanges run: the consumer then finds them there
-      if (p->async_open && !p->mir.s && p->mir.create()) return 1;
+      if (p->async_open && !p->mir.s && create_mirror_stream(p)) return 1;
       hipStream_t ms = p->async_open ? p->mir.s : p->stream;
       if (!r->ev_pf) HIPOK(hipEventCreateWithFlags(&r->ev_pf, hipEventDisableTiming));
       HIPOK(hipEventRecord(r->ev_pf, s));

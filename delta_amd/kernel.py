@@ -1167,6 +1167,20 @@ class GpuScan:
         """tableRoot = dataPath.toUri().toString() (ActiveAddFilesIterator.java:251)."""
         return table_root_uri(self.snapshot.table.path)
 
+    def getScanState(self, engine):
+        """Scan.getScanState (ScanImpl.java:189-218, ScanStateRow.java:35-44) as a dict: the table's
+        configuration, schema string, partition columns, protocol versions and tablePath. Host-side
+        only: the logical schema stands for the physical ones (column-mapping translation is outside
+        the scan-file path this engine accelerates)."""
+        md = self.snapshot.metadata or {}
+        pr = self.snapshot.protocol or {}
+        schema = md.get("schemaString")
+        return {"configuration": dict(md.get("configuration") or {}), "logicalSchemaString": schema,
+                "physicalSchemaString": schema, "physicalDataReadSchemaString": schema,
+                "partitionColumns": list(md.get("partitionColumns") or []),
+                "minReaderVersion": pr.get("minReaderVersion"), "minWriterVersion": pr.get("minWriterVersion"),
+                "tablePath": self.table_root()}
+
     def prepare(self, engine):
         """Host-side setup: parse the commit tail, open checkpoint files, upload to HBM."""
         if self._deferred_error is not None:
