@@ -2766,15 +2766,9 @@ extern "C" int dk_parquet_kernel_traffic(dk_parquet* p, const char* kernel, int6
   return 0;
 }
 
-// DK_MIRROR_DMA=1 (A/B): an asynchronous open's column mirrors as DMA copies on a copy-class stream
-// instead of k_copy_zc on a normal one
-static bool mirror_dma() {
-  static const bool on = getenv("DK_MIRROR_DMA") && atoi(getenv("DK_MIRROR_DMA")) != 0;
-  return on;
-}
-static int create_mirror_stream(dk_parquet* p) {
-  return mirror_dma() ? p->mir.create_class(copy_class_on() ? kStreamCopy : kStreamNormal) : p->mir.create();
-}
+// an asynchronous open's mirrors are k_copy_zc kernels on a normal stream: DMA copies on a copy-class
+// stream were no faster (profiles/r05/mirror_dma_ab)
+static int create_mirror_stream(dk_parquet* p) { return p->mir.create(); }
 
 // queue the D2H copy of decoded column ci into its pinned mirror (on the parquet stream, so it
 // follows the decode that produced the column)
@@ -2795,7 +2789,7 @@ static int queue_mirror(dk_parquet* p, int ci) {
   const int cf = p->col_file[ci];
   if (cf < (int)p->file_done.size() && p->file_done[cf]) HIPOK(hipStreamWaitEvent(s, p->file_done[cf], 0));
   if (cf < (int)p->file_dec.size() && p->file_dec[cf]) HIPOK(hipStreamWaitEvent(s, p->file_dec[cf], 0));
-  const bool zc = p->async_open && !mirror_dma();
+  const bool zc = p->async_open;
   auto d2h = [&](void* dst, const void* src, size_t n) -> int {
     if (!n) return 0;
     if (zc) { launch_copy_zc(dst, src, (long long)n, s); return 0; }
