@@ -165,10 +165,10 @@ constexpr int SNAP_REC = DK_SNAP_REC; // tag positions a walker records for the 
 #define DK_SF_RING 4096
 #endif
 #ifndef DK_SF_FW
-#define DK_SF_FW 2048
+#define DK_SF_FW 1024
 #endif
 #ifndef DK_SF_MARGIN
-#define DK_SF_MARGIN 640
+#define DK_SF_MARGIN 336
 #endif
 constexpr int SNAP_RING = DK_SF_RING; // k_snap_frag: output ring (LDS)
 constexpr int SNAP_FLUSH = 1024;      // k_snap_frag: ring -> HBM flush granule
@@ -687,15 +687,17 @@ enum : int32_t { SM_WIN = 0, SM_RING = 1, SM_FAR = 2, SM_DEP = 3, SM_FARQ = 4 };
 // k_snap_frag packs a tag's output offset inside the batch (< SF_BMAX) into 10 bits and its mode
 // into the next 3 (prm[].y): both must fit
 static_assert(SF_BMAX <= 1024, "DK_SF_BOUT too large: batch offsets are packed in 10 bits");
+static_assert(SF_BMAX % 16 == 0 && SF_BMAX >= 128, "the tag map is zeroed in 16-byte granules and holds TP");
 static_assert(SM_FARQ < 8, "snappy tag modes are packed in 3 bits");
 
 // EXP instances take experiment flags (A/B timing, tools/snap_ab.py): SX_* skip parts of the work
 // and SX_NOWRITE keeps the output of a preceding correct launch.
 enum : int { SX_NO_FAR = 1, SX_NO_BYTES = 2, SX_NO_RESOLVE = 4, SX_ONLY_DISCOVERY = 8, SX_NOWRITE = 16 };
-// 5 waves per SIMD (96 VGPRs, a few spilled bytes; the LDS allows 20 waves per CU): the kernel is
-// latency bound per wave, and 4 -> 5 waves took it from 34.0 to 29.5 ms at C3 (profiles/r02/occupancy_ab)
+// 6 waves per SIMD: <= 80 VGPRs (72 used) and a 1 KiB compressed window, 6,656 B of LDS per wave,
+// 24 waves per CU: 5 % under 5 waves with a 2 KiB window (profiles/r05/snap_occupancy_ab; 4 -> 5
+// waves took it from 34.0 to 29.5 ms at C3 in round 2, profiles/r02/occupancy_ab)
 #ifndef DK_SF_WPE
-#define DK_SF_WPE 5
+#define DK_SF_WPE 6
 #endif
 constexpr int SF_FARQ_MAX = 8;             // far copies up to this long are loaded early (three dwords)
 #if DK_SF_WPE > 0
@@ -706,14 +708,15 @@ constexpr int SF_FARQ_MAX = 8;             // far copies up to this long are loa
 template <bool EXP>
 __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const int2* __restrict__ work, int xflags) {
   const int xf = EXP ? xflags : 0;
-  // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map
-  __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX + 16) / 16];
+  // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map (the
+  // bitmap discovery's tag offsets TP share its bytes: discovery and the bytes stage never overlap)
+  __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX) / 16];
   __shared__ u32x2 prm[64];                // per-tag (src, (ot - o) | mode << 10 | per << 13)
   __shared__ uint32_t BW[SF_FW / 32 + 4];  // tag-start bits of the window's 64-byte blocks (bitmap mode)
-  __shared__ int16_t TP[64];               // bitmap discovery: offsets of the batch's tags
   uint8_t* L = (uint8_t*)lds4;
   uint32_t* W32 = (uint32_t*)(L + SNAP_RING);
   uint8_t* M = L + SNAP_RING + SF_FW + 16;
+  int16_t* TP = (int16_t*)M;               // bitmap discovery: offsets of the batch's tags
   const int2 wk = work[blockIdx.x];            // (compressed-page index, fragment)
   if (X.serial[wk.x]) return;
   const int lane = threadIdx.x;

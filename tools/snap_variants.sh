@@ -1,5 +1,6 @@
 #!/bin/bash
-# kernel-trace A/B of libdkgpu variants (DK_LIB_PATH) on the 12.5M-row C3-shaped snappy table.
+# kernel-trace A/B of libdkgpu variants (DK_LIB_PATH) on the 12.5M-row C3-shaped snappy table, one
+# synchronous single-slice open per decode (one k_snap_frag launch over every fragment).
 # Usage (via gpurun): bash tools/snap_variants.sh TAG LIB1 [LIB2 ...]   ("default" = the in-tree build)
 set -o pipefail
 TAG=$1; shift
@@ -30,12 +31,12 @@ i=0
 for lib in "$@"; do
   i=$((i+1))
   if [ "$lib" = default ]; then L="DK_VERBOSE="; elif [ "$lib" = frag ]; then L="DK_SNAP_PIPE=0"; else L="DK_LIB_PATH=$GRAFT_REPO_ROOT/$lib"; fi
-  env $L timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/v$i -o k -- python3 /tmp/snap_run.py > $OUT/v$i.log 2>&1 || { echo "run $i failed"; tail -5 $OUT/v$i.log; exit 1; }
+  env $L DK_ASYNC_OPEN=0 DK_OPEN_SLICES=1 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/v$i -o k -- python3 /tmp/snap_run.py > $OUT/v$i.log 2>&1 || { echo "run $i failed"; tail -5 $OUT/v$i.log; exit 1; }
   python3 - $OUT/v$i "$lib" <<PY
 import csv, glob, sys
 for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
         if 'snap_pipe' in r['Name'] or 'snap_frag' in r['Name']:
-            print(sys.argv[2], r['Name'][:24], r['Calls'], '%.1f us' % (float(r['AverageNs']) / 1e3), open(sys.argv[1] + '.log').read().strip().splitlines()[-1])
+            print(sys.argv[2], r['Name'][:24], r['Calls'], '%.1f us' % (float(r['AverageNs']) / 1e3), [l for l in open(sys.argv[1] + '.log').read().splitlines() if l.startswith('rows')])
 PY
 done
