@@ -1224,11 +1224,12 @@ __global__ __launch_bounds__(64) void k_snappy_serial(const DChunk* __restrict__
 // cut into 16 KiB chunks (one workgroup each, one dwordx4 per lane per step):
 //   k_pos_count    candidates per chunk, gathered in order in LDS, and the exact length chain
 //                  inside the chunk: every candidate's successor (q + 4 + len(q)) is the next one;
-//                  the chunk's first candidate and its last one's successor are kept
-//   k_pos_scan     per page: exclusive scan over its chunks; the chain across chunks (first
-//                  candidate 0, each chunk's first = the previous non-empty chunk's last
-//                  successor, the last successor = R) and count == n, else the fallback
-//   k_pos_write    candidates -> P in order
+//                  the chunk's first candidate and its last one's successor are kept; its first
+//                  value index by decoupled look-back over the page's earlier chunks, and the
+//                  candidates written to P at once (one pass over the region)
+//   k_pos_scan     per page: the chain across chunks (first candidate 0, each chunk's first = the
+//                  previous non-empty chunk's last successor, the last successor = R) and
+//                  count == n, else the fallback
 //   k_pos_fallback pages that failed: one lane walks the chain (always exact)
 // --------------------------------------------------------------------------------------------
 constexpr int POS_CHB = DK_POS_CHUNK / 16;   // aligned 16-byte blocks per chunk
@@ -1295,17 +1296,27 @@ __device__ __forceinline__ uint32_t pos_cand_mask(const StrRegion& S, int64_t i)
   return pos_cand_bits(q, nxt, S, i);
 }
 
+// One workgroup per 16 KiB chunk of a PLAIN byte-array region: the candidate length prefixes (zero
+// high bytes, pos_cand_bits), checked to chain inside the chunk (each prefix's successor is the
+// next candidate), and written out at their value index. The chunk's first value index comes from
+// its predecessors in the page by decoupled look-back over their status words (DPosChunk::pad:
+// 1 << 30 | count once counted, 2 << 30 | inclusive prefix once known; predecessors have lower
+// workgroup indices, so they are dispatched first and never wait on this one). k_pos_scan then
+// checks the chain across the chunks and resets the status words; a page whose chain does not hold
+// is rewritten serially by k_pos_fallback.
+constexpr int POS_ST_AGG = 1 << 30, POS_ST_INC = 2 << 30, POS_ST_VAL = (1 << 30) - 1;
 __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                  DPosChunk* __restrict__ pcs) {
-  DPosChunk& C = pcs[blockIdx.x];
+                                                  DPosChunk* __restrict__ pcs_all, int pc0) {
+  const int gi = pc0 + (int)blockIdx.x;
+  DPosChunk& C = pcs_all[gi];
   const DPage pg = pages[C.page];
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   __shared__ int lds[12];
   // a value takes >= 5 region bytes (4-byte prefix + content), so a chunk holds <= 3277 prefixes
   __shared__ int16_t cpos[DK_POS_CHUNK / 5 + 8];
-  __shared__ int s_bad, s_last;
+  __shared__ int s_bad, s_last, s_base;
   const bool on = str_region(pg, ck, arena, pos, S) && (int64_t)C.blk0 < S.nblk;
   const int64_t cstart = 16 * (int64_t)C.blk0 - (on ? S.mis : 0);   // region offset of the chunk start
   if (threadIdx.x == 0) { s_bad = 0; s_last = -1; }
@@ -1328,12 +1339,24 @@ __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chu
   }
   __syncthreads();
   const int cnt = run;
-  if (cnt > DK_POS_CHUNK / 5 + 8) {                 // impossible for a real chain: fallback
-    if (threadIdx.x == 0) { C.cnt = cnt; C.first = -1; C.last_next = -1; C.ok = 0; }
-    return;
+  const bool fits = cnt <= DK_POS_CHUNK / 5 + 8;    // (more is impossible for a real chain: fallback)
+  // publish the count, then add up the predecessors' (thread 0) while the others check the chain
+  if (threadIdx.x == 0) {
+    int base = 0;
+    if (gi > pg.pchunk0) {
+      __hip_atomic_store(&C.pad, POS_ST_AGG | (cnt & POS_ST_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int j = gi - 1; j >= pg.pchunk0; j--) {
+        int v;
+        do { v = __hip_atomic_load(&pcs_all[j].pad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); } while (v == 0);
+        base += v & POS_ST_VAL;
+        if (v & POS_ST_INC) break;
+      }
+    }
+    __hip_atomic_store(&C.pad, POS_ST_INC | ((base + cnt) & POS_ST_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_base = base;
   }
-  bool bad = false;
-  for (int k = threadIdx.x; k < cnt; k += NT) {
+  bool bad = !fits;
+  for (int k = threadIdx.x; fits && k < cnt; k += NT) {
     const int64_t q = cstart + cpos[k];
     const int64_t nx = q + 4 + (int64_t)ld_u32(S.r + q);
     if (k + 1 < cnt) { if (nx != cstart + cpos[k + 1]) bad = true; }
@@ -1343,10 +1366,15 @@ __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chu
   __syncthreads();
   if (threadIdx.x == 0) {
     C.cnt = cnt;
-    C.first = cnt ? (int32_t)(cstart + cpos[0]) : -1;
-    C.last_next = s_last;
+    C.base = s_base;
+    C.first = cnt && fits ? (int32_t)(cstart + cpos[0]) : -1;
+    C.last_next = fits ? s_last : -1;
     C.ok = !s_bad;
   }
+  // the positions, at their value index (a chunk whose chain breaks fails its page: k_pos_fallback)
+  if (fits && !s_bad)
+    for (int k = threadIdx.x; k < cnt; k += NT)
+      if (s_base + k < S.n) S.P[s_base + k] = (int32_t)(cstart + cpos[k]);
 }
 
 __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
@@ -1355,6 +1383,7 @@ __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chun
   DPage& pgw = pages[blockIdx.x];
   const DPage pg = pgw;
   if (pg.npchunk == 0) return;
+  for (int c = threadIdx.x; c < pg.npchunk; c += NT) pcs[pg.pchunk0 + c].pad = 0;   // k_pos_count's status words
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   if (!str_region(pg, ck, arena, pos, S)) return;
@@ -1365,7 +1394,6 @@ __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chun
     const int v = c < pg.npchunk ? pcs[pg.pchunk0 + c].cnt : 0;
     int ex, e1, e2, tot, t1, t2;
     block_scan3(v, 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
-    if (c < pg.npchunk) pcs[pg.pchunk0 + c].base = run + ex;
     run += tot;
   }
   if (threadIdx.x == 0) {
@@ -1383,35 +1411,6 @@ __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chun
     if (expect != S.R) ok = false;
     pgw.pos_fail = !ok;
     S.P[S.n] = (int32_t)S.R;
-  }
-}
-
-__global__ __launch_bounds__(NT) void k_pos_write(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
-                                                  const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                  const DPosChunk* __restrict__ pcs) {
-  const DPosChunk C = pcs[blockIdx.x];
-  const DPage pg = pages[C.page];
-  if (pg.pos_fail || C.cnt == 0) return;
-  const DChunk ck = chunks[pg.chunk];
-  StrRegion S;
-  if (!str_region(pg, ck, arena, pos, S)) return;
-  __shared__ int lds[12];
-  int run = C.base;
-#pragma unroll
-  for (int j = 0; j < POS_BPT; j++) {
-    const int64_t i = (int64_t)C.blk0 + j * NT + threadIdx.x;
-    uint32_t m = pos_cand_mask(S, i);
-    int ex, e1, e2, tot, t1, t2;
-    block_scan3(__popc(m), 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
-    int k = run + ex;
-    const int64_t rb = 16 * i - S.mis;
-    while (m) {
-      const int b = __ffs(m) - 1;
-      m &= m - 1;
-      if (k < S.n) S.P[k] = (int32_t)(rb + b - 3);
-      k++;
-    }
-    run += tot;
   }
 }
 
@@ -4049,9 +4048,8 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
 void launch_positions(const DChunk* c, DPage* p, int page0, int n_pages, const uint8_t* arena, int32_t* pos,
                       DPosChunk* pcs, int pc0, int npc, hipStream_t s) {
   if (!npc) return;
-  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
+  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs, pc0);
   hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs);
-  hipLaunchKernelGGL(k_pos_write, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs + pc0);
   hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos);
 }
 void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {
@@ -4732,7 +4730,7 @@ int warm_kernels() {
   const void* fns[] = {
       (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_link, (const void*)k_snap_fix,
       (const void*)k_snap_frag_t<false>, (const void*)k_snappy_serial, (const void*)k_pos_count,
-      (const void*)k_pos_scan, (const void*)k_pos_write, (const void*)k_pos_fallback, (const void*)k_delta_decode,
+      (const void*)k_pos_scan, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
       (const void*)k_tile_scan2, (const void*)k_tile_decode, (const void*)k_string_copy, (const void*)k_stats_eval,
       (const void*)k_part_eval, (const void*)k_json_canon, (const void*)k_slots_init, (const void*)k_table_insert,
