@@ -1300,15 +1300,20 @@ __device__ __forceinline__ uint32_t pos_cand_mask(const StrRegion& S, int64_t i)
 // high bytes, pos_cand_bits), checked to chain inside the chunk (each prefix's successor is the
 // next candidate), and written out at their value index. The chunk's first value index comes from
 // its predecessors in the page by decoupled look-back over their status words (DPosChunk::pad:
-// 1 << 30 | count once counted, 2 << 30 | inclusive prefix once known; predecessors have lower
-// workgroup indices, so they are dispatched first and never wait on this one). k_pos_scan then
-// checks the chain across the chunks and resets the status words; a page whose chain does not hold
-// is rewritten serially by k_pos_fallback.
+// 1 << 30 | count once counted, 2 << 30 | inclusive prefix once known). A workgroup takes its chunk
+// by ticket (an atomic counter per launch), not by its workgroup index: every predecessor it waits
+// for has then started already, whatever else shares the chip (concurrent launches of other slices
+// could otherwise fill the CUs with waiters whose predecessors are not yet dispatched). k_pos_scan
+// then checks the chain across the chunks and resets the status words; a page whose chain does not
+// hold is rewritten serially by k_pos_fallback.
 constexpr int POS_ST_AGG = 1 << 30, POS_ST_INC = 2 << 30, POS_ST_VAL = (1 << 30) - 1;
 __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                  DPosChunk* __restrict__ pcs_all, int pc0) {
-  const int gi = pc0 + (int)blockIdx.x;
+                                                  DPosChunk* __restrict__ pcs_all, int pc0, int* __restrict__ ticket) {
+  __shared__ int s_tk;
+  if (threadIdx.x == 0) s_tk = atomicAdd(ticket, 1);
+  __syncthreads();
+  const int gi = pc0 + s_tk;
   DPosChunk& C = pcs_all[gi];
   const DPage pg = pages[C.page];
   const DChunk ck = chunks[pg.chunk];
@@ -4046,9 +4051,10 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
 }
 // string positions of pages [page0, page0 + n_pages) whose chunks are pcs[pc0, pc0 + npc)
 void launch_positions(const DChunk* c, DPage* p, int page0, int n_pages, const uint8_t* arena, int32_t* pos,
-                      DPosChunk* pcs, int pc0, int npc, hipStream_t s) {
+                      DPosChunk* pcs, int pc0, int npc, int* ticket, hipStream_t s) {
   if (!npc) return;
-  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs, pc0);
+  (void)hipMemsetAsync(ticket, 0, sizeof(int), s);
+  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs, pc0, ticket);
   hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs);
   hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos);
 }
