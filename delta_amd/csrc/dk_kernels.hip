@@ -353,28 +353,34 @@ __device__ __forceinline__ GAS uint64_t* snap_seg_bits(const SnapCtx& X, int k) 
   return X.tbits ? (GAS uint64_t*)(X.tbits + (int64_t)k * (SNAP_SEG / 64)) : nullptr;
 }
 
-// A lane's 32-byte register window over the stream (two dwordx4 loads from a 16-byte aligned
-// address): tags parse from registers, so a walker issues one load pair per ~8 tags instead of two
-// loads per tag (its lanes walk different segments: every load is a separate cache line).
+// A lane's register window over the stream (SNAP_RW dwords from a 16-byte aligned address, in
+// dwordx4 loads): tags parse from registers, so a walker issues one load group per several tags
+// instead of two loads per tag (its lanes walk different segments: every load is a separate cache
+// line). 32 bytes: 48 and 64-byte windows were slower (k_snap_walk 498-502 -> 513 / 547 us on a
+// 12.5M-row table; selecting a dword costs a v_cndmask per window dword, profiles/r05/snap_walk_ab).
+constexpr int SNAP_RW = 8;
 struct SnapRegWin {
   const uint8_t* in;
   int64_t base = 1ll << 62;      // stream offset of w[0]
-  uint32_t w[8];
+  uint32_t w[SNAP_RW];
   __device__ __forceinline__ void load(int64_t p) {
     const uintptr_t a = ((uintptr_t)(in + p)) & ~(uintptr_t)15;
     base = p - (int64_t)((uintptr_t)(in + p) - a);
-    const u32x4 x = *(const GAS u32x4*)a, y = *(const GAS u32x4*)(a + 16);
-    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+#pragma unroll
+    for (int q = 0; q < SNAP_RW / 4; q++) {
+      const u32x4 x = *(const GAS u32x4*)(a + 16 * q);
+      w[4 * q] = x.x; w[4 * q + 1] = x.y; w[4 * q + 2] = x.z; w[4 * q + 3] = x.w;
+    }
   }
   __device__ __forceinline__ uint32_t sel(int i) const {
     uint32_t v = w[0];
 #pragma unroll
-    for (int q = 1; q < 8; q++) v = i == q ? w[q] : v;
+    for (int q = 1; q < SNAP_RW; q++) v = i == q ? w[q] : v;
     return v;
   }
-  // 8 bytes from stream offset p (p - base <= 24 after refill)
+  // 8 bytes from stream offset p (p - base <= 4 * SNAP_RW - 8 after refill)
   __device__ __forceinline__ uint64_t at(int64_t p) {
-    if (p < base || p + 5 > base + 32) load(p);
+    if (p < base || p + 5 > base + 4 * SNAP_RW) load(p);
     const int rel = (int)(p - base), i = rel >> 2;
     return ((((uint64_t)sel(i + 1)) << 32) | sel(i)) >> (8 * (rel & 3));
   }

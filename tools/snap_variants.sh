@@ -36,7 +36,7 @@ for lib in "$@"; do
 import csv, glob, sys
 for f in glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        if 'snap_pipe' in r['Name'] or 'snap_frag' in r['Name']:
+        if 'snap' in r['Name'] and 'serial' not in r['Name']:
             print(sys.argv[2], r['Name'][:24], r['Calls'], '%.1f us' % (float(r['AverageNs']) / 1e3), [l for l in open(sys.argv[1] + '.log').read().splitlines() if l.startswith('rows')])
 PY
 done
