@@ -74,6 +74,8 @@ struct SnapCtx {
   int32_t* t_exit;           // true exit (-1: malformed)
   const int32_t* fbase;      // compressed page -> first fragment (n_cpages + 1)
   int64_t* fstart;           // fragment -> compressed offset of its first tag
+  int64_t* t_ob;             // segment -> output offset of its first byte within the page (k_snap_fix)
+  int32_t* fseg;             // fragment -> segment holding its first output byte (k_snap_fix, bitmap mode)
   int32_t* serial;           // compressed page -> 1: decode on the serial path
   uint64_t* tbits;           // page mode: tag-start bitmap, DK_SNAP_SEG / 64 words per segment (or null)
   int32_t page_mode;         // 1: whole pages decode in order (no 64 KiB fragment starts needed)

@@ -980,7 +980,7 @@ struct dk_parquet {
   std::vector<int> col_file;
   DBuf d_chunks, d_pages, d_cols, d_pos, d_arena, d_state, d_dbp, d_tiles;
   // snappy: compressed pages, their 64 KiB fragment bases / work items / starts, serial flags
-  DBuf d_cpage, d_fbase, d_fwork, d_fstart, d_serial;
+  DBuf d_cpage, d_fbase, d_fwork, d_fstart, d_serial, d_snap_ob, d_fseg;
   DBuf d_sbase, d_spage, d_snapws;   // speculative-walk segments: page bases, owner page, workspace
   DBuf d_tbits;                      // page mode: tag-start bitmap (DK_SNAP_SEG / 64 words per segment)
   DBuf d_pwork;                      // page-mode work items (page, -1)
@@ -1115,6 +1115,7 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
     X.w_exit = ws; X.w_out = ws + ns; X.w_npos = ws + 2 * ns; X.t_entry = ws + 3 * ns; X.t_out = ws + 4 * ns;
     X.t_exit = ws + 5 * ns; X.w_pos = ws + 6 * ns; X.w_cum = ws + (6 + DK_SNAP_REC) * ns;
     X.fbase = p->d_fbase.as<int32_t>(); X.fstart = p->d_fstart.as<int64_t>(); X.serial = p->d_serial.as<int32_t>();
+    X.t_ob = p->d_snap_ob.as<int64_t>(); X.fseg = p->d_fseg.as<int32_t>();
     X.k0 = R.s0; X.k1 = R.s1; X.c0 = R.ca;
     // page mode (one wave decodes a whole page in order, no walk; never sliced) or the speculative
     // walk that splits pages into 64 KiB fragments
@@ -1584,7 +1585,8 @@ static int prepare(dk_parquet* p) {
         expand(p, us, p->d_fwork, none, fb, EX_FRAG, sizeof(int2)) || p->d_fstart.alloc((size_t)p->n_frags * 8) ||
         p->d_serial.alloc(cpage.size() * 4) || upload_zc(p, p->d_sbase, sbase.data(), sbase.size() * 4, us) ||
         expand(p, us, p->d_spage, none, sb, EX_SEG, 4) ||
-        p->d_snapws.alloc((size_t)sbase.back() * 4 * (6 + 2 * DK_SNAP_REC)))
+        p->d_snapws.alloc((size_t)sbase.back() * 4 * (6 + 2 * DK_SNAP_REC)) ||
+        p->d_snap_ob.alloc((size_t)sbase.back() * 8 + 8) || p->d_fseg.alloc((size_t)p->n_frags * 4 + 4))
       return 1;
     p->n_segs = sbase.back();
     if (snap_page_mode(p)) {

@@ -303,14 +303,17 @@ __device__ __forceinline__ int64_t snap_preamble(const uint8_t* in, int64_t clen
 //   k_snap_link   one lane per segment re-walks from the previous walker's exit (the true entry
 //                 whenever the previous segment's walker joined the true chain) until it meets a
 //                 recorded position -- two chains that share a tag are identical from there on --
-//                 then takes the walker's exit and output; otherwise it walks the whole segment.
+//                 then takes the walker's exit and output; otherwise it walks the whole segment. On
+//                 the way it writes the tag-start bits from its entry to the meeting point.
 //   k_snap_fix    one wave per page checks that every entry equals the previous segment's true exit
-//                 (re-walking, in order, any segment where it does not), scans the output bytes and
-//                 finds where each 64 KiB output fragment starts in the compressed stream. Google's
-//                 compressor encodes every 64 KiB of input on its own, so no tag straddles a
-//                 fragment boundary and no copy reaches back across one; a page that breaks this
-//                 (legal in the format, never written by snappy) or is malformed goes to the serial
-//                 path.
+//                 (re-walking, in order, any segment where it does not, and rewriting that segment's
+//                 bits), scans the output bytes and names the segment holding each 64 KiB output
+//                 fragment's first byte. Google's compressor encodes every 64 KiB of input on its own,
+//                 so no tag straddles a fragment boundary and no copy reaches back across one; a page
+//                 that breaks this (legal in the format, never written by snappy) or is malformed
+//                 goes to the serial path.
+//   k_snap_bounds one wave per fragment walks that segment's bitmap from its verified entry to the
+//                 fragment's first tag (all boundaries in parallel).
 //   k_snap_frag   one wave per fragment decodes it through a 4 KiB LDS output ring (back references
 //                 are served from LDS; farther ones from the flushed HBM output) and stores the
 //                 ring to HBM in 1 KiB dwordx4 granules.
@@ -486,7 +489,9 @@ __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
       tex = X.w_exit[k];
     } else {
       e = X.w_exit[k - 1];
-      snap_seg_from(X, k, j, in, clen, e, true, &tout, &tex);
+      // (the tag-start bits from e to where it meets the walker are written on the way: they are the
+      // true chain's whenever e is the true entry, which k_snap_fix checks)
+      snap_seg_from(X, k, j, in, clen, e, true, &tout, &tex, X.tbits != nullptr);
     }
   }
   X.t_entry[k] = e;
@@ -520,7 +525,6 @@ __device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets 
 
 __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
   const int ci = X.c0 + blockIdx.x, lane = threadIdx.x;
-  __shared__ int16_t TPF[64];               // bitmap boundary walk: offsets of a step's tags
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
   if (!snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
     if (lane == 0) X.serial[ci] = 1;
@@ -538,6 +542,7 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
     const int k = base + lane;
     const bool valid = k < k1;
     int32_t e = valid ? X.t_entry[k] : 0, tout = valid ? X.t_out[k] : 0, tex = valid ? X.t_exit[k] : 0;
+    bool fixed = false;
     // every entry must be the previous segment's true exit; re-walk (in order) where it is not
     while (true) {
       int32_t pv = __shfl_up(tex, 1, 64);
@@ -550,14 +555,15 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
       if (lane == L) snap_seg_from(X, base + L, base + L - k0, in, clen, eL, true, &to2, &tx2);
       to2 = __shfl(to2, L, 64);
       tx2 = __shfl(tx2, L, 64);
-      if (lane == L) { e = eL; tout = to2; tex = tx2; }
+      if (lane == L) { e = eL; tout = to2; tex = tx2; fixed = true; }
     }
     if (__ballot(valid && tex < 0)) { bad = true; break; }
-    // entries verified: each segment's tag-start bits up to where the walker joined the true chain
-    // are rewritten from its true entry (every lane its own segment)
-    if (X.tbits && valid) {
+    // entries verified: k_snap_link wrote each segment's tag-start bits from its entry to where it
+    // met the walker, so they are right wherever that entry was; a corrected segment's bits are
+    // rewritten whole from its true entry (every lane its own segment)
+    if (X.tbits && valid && fixed) {
       int32_t to3, tx3;
-      snap_seg_from(X, k, k - k0, in, clen, e, true, &to3, &tx3, true);
+      snap_seg_from(X, k, k - k0, in, clen, e, false, &to3, &tx3, true);
     }
     // output offsets: exclusive scan of tout
     int64_t x = tout;
@@ -566,59 +572,19 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
     const int64_t ob = running + x - tout;
     running += __shfl(x, 63, 64);
     prev_exit = __shfl(tex, (k1 - base) >= 64 ? 63 : (k1 - base - 1), 64);
-    // fragment starts inside this segment: walk from its entry to each 64 KiB output boundary
-    // (page mode decodes whole pages in order and needs none). With the tag-start bitmap (just
-    // rewritten to the true chain above) the wave walks one boundary at a time, 256 stream bytes per
-    // step: lanes rank the set bits of 4 bytes each, parse up to 64 tags in parallel and scan their
-    // output lengths (a dependent chain per 256 bytes instead of per tag)
+    // fragment starts inside this segment. With the tag-start bitmap (just rewritten to the true
+    // chain above) each boundary is found by its own wave afterwards (k_snap_bounds): here every
+    // segment keeps its verified entry and output base and names the fragments whose first byte it
+    // holds (page mode decodes whole pages in order and needs none)
     if (!X.page_mode && X.tbits && !bad) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");     // the bitmap words this wave wrote
-      unsigned long long mb = __ballot(valid && tout > 0 && (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG < ob + tout);
-      while (mb && !bad) {
-        const int L = __ffsll((long long)mb) - 1;
-        mb &= mb - 1;
-        const int64_t obL = __shfl(ob, L, 64);
-        const int32_t toutL = __shfl(tout, L, 64), eL = __shfl(e, L, 64);
-        const int64_t s0 = (int64_t)(base + L - k0) * SNAP_SEG;
-        const int64_t send = s0 + SNAP_SEG < clen ? s0 + SNAP_SEG : clen;
-        const GAS uint64_t* wb = snap_seg_bits(X, base + L);
-        int64_t F = (obL + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG, p = eL, o = obL;
-        while (F < obL + toutL) {
-          const int64_t q = p + 4 * lane;
-          uint32_t b4 = 0;
-          if (q < send) {
-            const int rel = (int)(q - s0), wi = rel >> 6, sh = rel & 63;
-            uint64_t w = wb[wi] >> sh;
-            if (sh > 60 && wi + 1 < SNAP_SEG / 64) w |= wb[wi + 1] << (64 - sh);
-            b4 = (uint32_t)w & 0xfu;
-            if (send - q < 4) b4 &= (1u << (send - q)) - 1u;
+      if (valid) {
+        X.t_entry[k] = e;
+        X.t_ob[k] = ob;
+        if (tout > 0)
+          for (int64_t F = (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG; F < ob + tout; F += SNAP_FRAG) {
+            const int f = (int)(F / SNAP_FRAG);
+            if (f < nf) X.fseg[f0 + f] = k; else bad = true;
           }
-          const int32_t cnt = __popc(b4), incl = dpp_scan_add(cnt);
-          const int32_t nt = __builtin_amdgcn_readlane(incl, 63);
-          int32_t r0 = incl - cnt;
-          for (int bb = 0; bb < 4; bb++)
-            if ((b4 >> bb) & 1) { if (r0 < 64) TPF[r0] = (int16_t)(4 * lane + bb); r0++; }
-          const int32_t nw = nt < 64 ? nt : 64;
-          const bool intag = lane < nw;
-          const int32_t pos = intag ? (int32_t)TPF[lane] : 0;
-          int32_t adv = 0, len = 0;
-          bool perr = false;
-          if (intag) perr = !snap_parse(in, clen, p + pos, &adv, &len);
-          if (nw == 0 || __builtin_amdgcn_readlane(pos, 0) != 0 || __ballot(perr)) { bad = true; break; }
-          const int32_t oi = dpp_scan_add(len);
-          const int32_t tot = __builtin_amdgcn_readlane(oi, nw - 1);
-          const int64_t pnext = p + __builtin_amdgcn_readlane(pos, nw - 1) + __builtin_amdgcn_readlane(adv, nw - 1);
-          if (o + tot < F) { p = pnext; o += tot; continue; }
-          const unsigned long long hit = __ballot(intag && o + oi - len == F);
-          int64_t pb;
-          if (hit) pb = p + __builtin_amdgcn_readlane(pos, __ffsll((long long)hit) - 1);
-          else if (o + tot == F) pb = pnext;
-          else { bad = true; break; }                  // a tag straddles the boundary
-          const int f = (int)(F / SNAP_FRAG);
-          if (f >= nf) { bad = true; break; }
-          if (lane == 0) X.fstart[f0 + f] = pb;
-          p = pb; o = F; F += SNAP_FRAG;
-        }
       }
     } else if (valid && tout > 0 && !X.page_mode) {
       int64_t F = (ob + SNAP_FRAG - 1) / SNAP_FRAG * SNAP_FRAG;
@@ -640,6 +606,72 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
   }
   if (running != ulen || prev_exit != (int32_t)clen) bad = true;
   if (lane == 0) X.serial[ci] = bad ? 1 : 0;
+}
+
+// One wave per 64 KiB fragment (bitmap mode): the compressed offset of the fragment's first tag,
+// walked from the verified entry of the segment holding the fragment's first output byte
+// (k_snap_fix: t_entry, t_ob, fseg) over that segment's tag-start bitmap, 256 stream bytes per step:
+// lanes rank the set bits of 4 bytes each, parse up to 64 tags in parallel and scan their output
+// lengths (a dependent chain per 256 bytes instead of per tag). A tag straddling the boundary sends
+// the page to the serial path. Every boundary is independent, so they run in parallel instead of one
+// after another inside k_snap_fix's wave per page.
+__global__ __launch_bounds__(64) void k_snap_bounds(SnapCtx X, const int2* __restrict__ work) {
+  const int2 wk = work[blockIdx.x];
+  const int ci = wk.x, f = wk.y, lane = threadIdx.x;
+  __shared__ int16_t TPF[64];
+  if (X.serial[ci]) return;
+  const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
+  if (!snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) return;
+  const int64_t F = (int64_t)f * SNAP_FRAG;
+  if (F >= ulen) return;                           // no output there (k_snap_frag returns too)
+  const int f0 = X.fbase[ci];
+  const int k = X.fseg[f0 + f];                    // assigned by k_snap_fix for every F < ulen
+  if (k < X.sbase[ci] || k >= X.sbase[ci + 1]) {   // (cannot happen on a page k_snap_fix accepted)
+    if (lane == 0) X.serial[ci] = 1;
+    return;
+  }
+  const int64_t s0 = (int64_t)(k - X.sbase[ci]) * SNAP_SEG;
+  const int64_t send = s0 + SNAP_SEG < clen ? s0 + SNAP_SEG : clen;
+  const GAS uint64_t* wb = snap_seg_bits(X, k);
+  int64_t p = X.t_entry[k], o = X.t_ob[k];
+  bool bad = p < 0 || o > F;
+  int64_t pb = -1;
+  while (!bad) {
+    const int64_t q = p + 4 * lane;
+    uint32_t b4 = 0;
+    if (q < send) {
+      const int rel = (int)(q - s0), wi = rel >> 6, sh = rel & 63;
+      uint64_t w = wb[wi] >> sh;
+      if (sh > 60 && wi + 1 < SNAP_SEG / 64) w |= wb[wi + 1] << (64 - sh);
+      b4 = (uint32_t)w & 0xfu;
+      if (send - q < 4) b4 &= (1u << (send - q)) - 1u;
+    }
+    const int32_t cnt = __popc(b4), incl = dpp_scan_add(cnt);
+    const int32_t nt = __builtin_amdgcn_readlane(incl, 63);
+    int32_t r0 = incl - cnt;
+    for (int bb = 0; bb < 4; bb++)
+      if ((b4 >> bb) & 1) { if (r0 < 64) TPF[r0] = (int16_t)(4 * lane + bb); r0++; }
+    const int32_t nw = nt < 64 ? nt : 64;
+    const bool intag = lane < nw;
+    const int32_t pos = intag ? (int32_t)TPF[lane] : 0;
+    int32_t adv = 0, len = 0;
+    bool perr = false;
+    if (intag) perr = !snap_parse(in, clen, p + pos, &adv, &len);
+    if (nw == 0 || __builtin_amdgcn_readlane(pos, 0) != 0 || __ballot(perr)) { bad = true; break; }
+    const int32_t oi = dpp_scan_add(len);
+    const int32_t tot = __builtin_amdgcn_readlane(oi, nw - 1);
+    const int64_t pnext = p + __builtin_amdgcn_readlane(pos, nw - 1) + __builtin_amdgcn_readlane(adv, nw - 1);
+    if (o + tot < F) { p = pnext; o += tot; continue; }
+    const unsigned long long hit = __ballot(intag && o + oi - len == F);
+    if (hit) pb = p + __builtin_amdgcn_readlane(pos, __ffsll((long long)hit) - 1);
+    else if (o + tot == F) pb = pnext;
+    else bad = true;                                   // a tag straddles the boundary
+    break;
+  }
+  if (lane == 0) {
+    if (bad) X.serial[ci] = 1;
+    else X.fstart[f0 + f] = pb;
+  }
 }
 
 // i mod d for 0 <= i < 64, 0 < d < 64 (d = copy offset): exact with a 16-bit reciprocal
@@ -4048,6 +4080,7 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
     }
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
+    if (X.tbits && n_frag) hipLaunchKernelGGL(k_snap_bounds, dim3(n_frag), dim3(64), 0, s, X, work);
   } else if (phase == 2) {
     if (n_frag) launch_frag(X, n_frag, work, s);
   } else {
@@ -4740,7 +4773,7 @@ namespace dk {
 // getScanFiles (round-3 cold snapshot load: 242 ms, 5 ms warm). Returns the kernels touched.
 int warm_kernels() {
   const void* fns[] = {
-      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_link, (const void*)k_snap_fix,
+      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
       (const void*)k_snap_frag_t<false>, (const void*)k_snappy_serial, (const void*)k_pos_count,
       (const void*)k_pos_scan, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
