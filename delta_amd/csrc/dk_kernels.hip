@@ -728,9 +728,6 @@ static_assert(SF_BMAX <= 1024, "DK_SF_BOUT too large: batch offsets are packed i
 static_assert(SF_BMAX % 16 == 0 && SF_BMAX >= 128, "the tag map is zeroed in 16-byte granules and holds TP");
 static_assert(SM_FARQ < 8, "snappy tag modes are packed in 3 bits");
 
-// EXP instances take experiment flags (A/B timing, tools/snap_ab.py): SX_* skip parts of the work
-// and SX_NOWRITE keeps the output of a preceding correct launch.
-enum : int { SX_NO_FAR = 1, SX_NO_BYTES = 2, SX_NO_RESOLVE = 4, SX_ONLY_DISCOVERY = 8, SX_NOWRITE = 16 };
 // 6 waves per SIMD: <= 80 VGPRs (72 used) and a 1 KiB compressed window, 6,656 B of LDS per wave,
 // 24 waves per CU: 5 % under 5 waves with a 2 KiB window (profiles/r05/snap_occupancy_ab; 4 -> 5
 // waves took it from 34.0 to 29.5 ms at C3 in round 2, profiles/r02/occupancy_ab)
@@ -743,9 +740,7 @@ constexpr int SF_FARQ_MAX = 8;             // far copies up to this long are loa
 #else
 #define SF_WPE_ATTR
 #endif
-template <bool EXP>
-__global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const int2* __restrict__ work, int xflags) {
-  const int xf = EXP ? xflags : 0;
+__global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag(SnapCtx X, const int2* __restrict__ work) {
   // LDS: [0, SNAP_RING) output ring | [SNAP_RING, +SF_FW + 16) compressed window | tag map (the
   // bitmap discovery's tag offsets TP share its bytes: discovery and the bytes stage never overlap)
   __shared__ u32x4 lds4[(SNAP_RING + SF_FW + 16 + SF_BMAX) / 16];
@@ -818,7 +813,6 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
   };
   int32_t o = o0, flushed = o0;
   auto flush_to = [&](int32_t upto) {          // ring -> HBM, 16-byte granules
-    if (xf & SX_NOWRITE) { flushed = upto; return; }
     for (int32_t u = flushed + 16 * lane; u < upto; u += 16 * 64)
       *(GAS u32x4*)(gout + u) = lds4[(u & SF_RM) >> 4];
     flushed = upto;
@@ -981,11 +975,6 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
       SSTAT(5, 1);
       continue;
     }
-    if (xf & SX_ONLY_DISCOVERY) {
-      o += outsum; p = t;
-      while (o - flushed >= SNAP_FLUSH) flush_to(flushed + SNAP_FLUSH);
-      continue;
-    }
     STIME(14);                                   // discovery
     // ---- 2. parse each tag (lane j = tag j) ----
     const bool valid = lane < n;
@@ -1036,11 +1025,11 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
     // far copies of <= 8 bytes (two thirds of all copies reach past the 4 KiB ring on path data):
     // their source words are loaded here, unconditionally (no lane waits on a branch), and consumed
     // only after the byte-parallel stage, so the load latency hides behind the resolve and map work
-    const bool farq = valid && mode == SM_FAR && len <= SF_FARQ_MAX && !(xf & SX_NO_FAR);
+    const bool farq = valid && mode == SM_FAR && len <= SF_FARQ_MAX;
     if (farq) mode = SM_FARQ;
     const uintptr_t fa = farq ? (((uintptr_t)(out + src)) & ~(uintptr_t)3) : (((uintptr_t)in) & ~(uintptr_t)15);
     const uint32_t fw0 = ((const GAS uint32_t*)fa)[0], fw1 = ((const GAS uint32_t*)fa)[1], fw2 = ((const GAS uint32_t*)fa)[2];
-    for (int round = 0; round < ((xf & SX_NO_RESOLVE) ? 0 : 6); round++) {
+    for (int round = 0; round < 6; round++) {
       const bool act = valid && mode == SM_DEP && !stuck;
       if (!__ballot(act)) break;
       SSTAT(7, 1);
@@ -1068,7 +1057,7 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
     STIME(16);                                   // modes + resolution
     STIME(17);                                   // far-quick loads issued
     // ---- 5. byte-parallel production of every WIN / RING / FAR tag ----
-    const int32_t CH = (xf & SX_NO_BYTES) ? 0 : (total + 63) >> 6;   // output bytes per lane (<= SF_CH)
+    const int32_t CH = (total + 63) >> 6;        // output bytes per lane (<= SF_CH)
     SSTAT(8, CH); SSTAT(2, __popcll(__ballot(valid && mode == SM_DEP))); SSTAT(3, __popcll(__ballot(valid && mode >= SM_FAR && mode != SM_DEP)));
     SSTAT(4, __popcll(__ballot(valid && is_copy && mode == SM_WIN))); SSTAT(10, __popcll(__ballot(valid && mode == SM_RING)));
     for (int32_t b = lane * 16; b < total; b += 64 * 16) *(uint4*)(M + b) = make_uint4(0, 0, 0, 0);
@@ -1114,7 +1103,7 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
       for (int32_t k = 0; k < SF_CH; k++) v[k] = sa[k] >= 0 ? L[sa[k]] : 0;
 #pragma unroll
       for (int32_t k = 0; k < SF_CH; k++) if (sa[k] >= 0) L[(o + b0 + k) & SF_RM] = (uint8_t)v[k];
-      if (!(xf & SX_NO_FAR) && __ballot(any_far)) {
+      if (__ballot(any_far)) {
         // far sources: bytes this wave flushed to HBM earlier (its stores complete first)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         uint32_t gv[SF_CH];
@@ -1156,13 +1145,11 @@ __global__ __launch_bounds__(64) SF_WPE_ATTR void k_snap_frag_t(SnapCtx X, const
   if (lane == 0) for (int i = 0; i < 24; i++) atomicAdd(&dk_snap_stats[i], st_[i]);
 #endif
   if (bad || o != o1 || p != ce) {
-    if (lane == 0 && !(xf & SX_NOWRITE)) X.serial[wk.x] = 1;
+    if (lane == 0) X.serial[wk.x] = 1;
     return;
   }
   flush_to(o1);
 }
-template __global__ void k_snap_frag_t<false>(SnapCtx, const int2*, int);
-template __global__ void k_snap_frag_t<true>(SnapCtx, const int2*, int);
 
 
 // Serial path (pages flagged by k_snap_fix / k_snap_frag): every lane parses the same tag (uniform
@@ -4040,14 +4027,8 @@ void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
 }
 void snap_stats(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dk_snap_stats), 24 * 8); }
 
-// DK_SNAP_EXP=<flags> (A/B timing only): a correct decode, then the timed experiment instance with
-// SX_NOWRITE | flags over the same work
 static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s) {
-  static const int exp = getenv("DK_SNAP_EXP") ? atoi(getenv("DK_SNAP_EXP")) : -1;
-
-  if (exp < 0) { hipLaunchKernelGGL(k_snap_frag_t<false>, dim3(n), dim3(64), 0, s, X, work, 0); return; }
-  hipLaunchKernelGGL(k_snap_frag_t<false>, dim3(n), dim3(64), 0, s, X, work, 0);
-  hipLaunchKernelGGL(k_snap_frag_t<true>, dim3(n), dim3(64), 0, s, X, work, exp | SX_NOWRITE);
+  hipLaunchKernelGGL(k_snap_frag, dim3(n), dim3(64), 0, s, X, work);
 }
 
 // phase 0: walk + link, 1: fix, 2: fragment decode, 3: serial fallback; n_frag < 0: page mode
@@ -4774,7 +4755,7 @@ namespace dk {
 int warm_kernels() {
   const void* fns[] = {
       (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
-      (const void*)k_snap_frag_t<false>, (const void*)k_snappy_serial, (const void*)k_pos_count,
+      (const void*)k_snap_frag, (const void*)k_snappy_serial, (const void*)k_pos_count,
       (const void*)k_pos_scan, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
       (const void*)k_tile_scan2, (const void*)k_tile_decode, (const void*)k_string_copy, (const void*)k_stats_eval,

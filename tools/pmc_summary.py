@@ -30,7 +30,7 @@ acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(args.root, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"].split("(")[0].replace("dk::", "").replace("void ", "")
-        name = name.split("<")[0].replace("k_snap_frag_t", "k_snap_frag")      # template instances
+        name = name.split("<")[0].replace("k_snap_frag_t", "k_snap_frag")      # (round-4 profiles: a template)
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 
 def big_mean(v):
