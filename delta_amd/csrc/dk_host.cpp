@@ -41,7 +41,7 @@ void launch_copy_zc(void*, const void*, long long, hipStream_t);
 void launch_arrow_window(const ArrowWin&, hipStream_t);
 void launch_dv_expand(const DvCont*, int, const uint8_t*, unsigned long long*, hipStream_t);
 void launch_dv_select(const unsigned long long*, long long, const long long*, long long, uint8_t*, hipStream_t);
-void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, int*, hipStream_t);
+void launch_positions(const DChunk*, DPage*, int, int, const uint8_t*, int32_t*, DPosChunk*, int, int, int16_t*, hipStream_t);
 void launch_page_runs(const DChunk*, DPage*, int, const uint8_t*, Seg*, hipStream_t);
 void launch_tile_count(const DChunk*, DPage*, const uint8_t*, const Seg*, DTile*, int, int, hipStream_t);
 void launch_tile_scan1(DColumn*, int, DPage*, DTile*, DState*, hipStream_t);
@@ -988,7 +988,7 @@ struct dk_parquet {
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
   int n_ltiles = 0;
   DBuf d_pchunks;            // string-position chunks (DPosChunk)
-  DBuf d_pos_tickets;        // k_pos_count's workgroup tickets, one counter per slice (at the slice's first chunk)
+  DBuf d_pos_scratch;        // k_pos_count's candidates, DK_POS_CHUNK / 5 + 8 int16 offsets per chunk
   int n_pchunks = 0;
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
@@ -1134,7 +1134,7 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
   { KTimer::Scope sc(&T, 2, s); launch_tile_count(C, P, arena, runs, LT, R.t1 - R.t0, R.t0, s); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan1(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
   { KTimer::Scope sc(&T, 4, s); launch_positions(C, P, R.pa, np, arena, pos, p->d_pchunks.as<DPosChunk>(), R.pc0, R.pc1 - R.pc0,
-                                                    p->d_pos_tickets.as<int>() + R.pc0, s); }
+                                                    p->d_pos_scratch.as<int16_t>(), s); }
   if (p->has_dbp) { KTimer::Scope sc(&T, 14, s); launch_delta_decode(C, P + R.pa, np, arena, p->d_dbp.as<long long>(), s); }
   { KTimer::Scope sc(&T, 16, s); launch_tile_chars(C, P, arena, pos, runs, LT, R.t1 - R.t0, R.t0, s); }
   { KTimer::Scope sc(&T, 3, s); launch_tile_scan2(cols + R.col0, R.col1 - R.col0, P, LT, st, s); }
@@ -1567,7 +1567,7 @@ static int prepare(dk_parquet* p) {
       pbase.push_back(pbase.back() + pg.npchunk);
     }
     p->n_pchunks = (int)pbase.back();
-    if (p->d_pos_tickets.alloc((size_t)(p->n_pchunks + 1) * 4)) return 1;
+    if (p->d_pos_scratch.alloc(((size_t)p->n_pchunks * (DK_POS_CHUNK / 5 + 8) + 8) * 2)) return 1;
     if (expand(p, us, p->d_pchunks, ppage, pbase, EX_POSCHUNK, sizeof(DPosChunk)) ||
         expand(p, us, p->d_ltiles, tpage, tbase, EX_TILE, sizeof(DTile)))
       return 1;

@@ -1249,12 +1249,12 @@ __global__ __launch_bounds__(64) void k_snappy_serial(const DChunk* __restrict__
 // cut into 16 KiB chunks (one workgroup each, one dwordx4 per lane per step):
 //   k_pos_count    candidates per chunk, gathered in order in LDS, and the exact length chain
 //                  inside the chunk: every candidate's successor (q + 4 + len(q)) is the next one;
-//                  the chunk's first candidate and its last one's successor are kept; its first
-//                  value index by decoupled look-back over the page's earlier chunks, and the
-//                  candidates written to P at once (one pass over the region)
-//   k_pos_scan     per page: the chain across chunks (first candidate 0, each chunk's first = the
-//                  previous non-empty chunk's last successor, the last successor = R) and
-//                  count == n, else the fallback
+//                  the chunk's first candidate and its last one's successor are kept, the
+//                  candidates go to the chunk's int16 scratch slot (one pass over the region)
+//   k_pos_scan     per page: exclusive scan over its chunks; the chain across chunks (first
+//                  candidate 0, each chunk's first = the previous non-empty chunk's last
+//                  successor, the last successor = R) and count == n, else the fallback; then
+//                  every chunk's scratch offsets -> P at their value index
 //   k_pos_fallback pages that failed: one lane walks the chain (always exact)
 // --------------------------------------------------------------------------------------------
 constexpr int POS_CHB = DK_POS_CHUNK / 16;   // aligned 16-byte blocks per chunk
@@ -1323,30 +1323,23 @@ __device__ __forceinline__ uint32_t pos_cand_mask(const StrRegion& S, int64_t i)
 
 // One workgroup per 16 KiB chunk of a PLAIN byte-array region: the candidate length prefixes (zero
 // high bytes, pos_cand_bits), checked to chain inside the chunk (each prefix's successor is the
-// next candidate), and written out at their value index. The chunk's first value index comes from
-// its predecessors in the page by decoupled look-back over their status words (DPosChunk::pad:
-// 1 << 30 | count once counted, 2 << 30 | inclusive prefix once known). A workgroup takes its chunk
-// by ticket (an atomic counter per launch), not by its workgroup index: every predecessor it waits
-// for has then started already, whatever else shares the chip (concurrent launches of other slices
-// could otherwise fill the CUs with waiters whose predecessors are not yet dispatched). k_pos_scan
-// then checks the chain across the chunks and resets the status words; a page whose chain does not
-// hold is rewritten serially by k_pos_fallback.
-constexpr int POS_ST_AGG = 1 << 30, POS_ST_INC = 2 << 30, POS_ST_VAL = (1 << 30) - 1;
+// next candidate), kept as chunk-relative int16 offsets in the chunk's slot of a scratch array
+// (POS_CAP per chunk). k_pos_scan then scans the page's chunk counts, checks the chain across the
+// chunks and moves every chunk's offsets to its value indexes: the region is read once (the old
+// second pass re-read it to write the positions), and no workgroup waits on another (a look-back
+// over the chunks' status words stalled when several slices' launches shared the chip).
+constexpr int POS_CAP = DK_POS_CHUNK / 5 + 8;    // a value takes >= 5 region bytes: <= 3277 per chunk
 __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                  DPosChunk* __restrict__ pcs_all, int pc0, int* __restrict__ ticket) {
-  __shared__ int s_tk;
-  if (threadIdx.x == 0) s_tk = atomicAdd(ticket, 1);
-  __syncthreads();
-  const int gi = pc0 + s_tk;
+                                                  DPosChunk* __restrict__ pcs_all, int pc0, int16_t* __restrict__ scratch) {
+  const int gi = pc0 + (int)blockIdx.x;
   DPosChunk& C = pcs_all[gi];
   const DPage pg = pages[C.page];
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   __shared__ int lds[12];
-  // a value takes >= 5 region bytes (4-byte prefix + content), so a chunk holds <= 3277 prefixes
-  __shared__ int16_t cpos[DK_POS_CHUNK / 5 + 8];
-  __shared__ int s_bad, s_last, s_base;
+  __shared__ int16_t cpos[POS_CAP];
+  __shared__ int s_bad, s_last;
   const bool on = str_region(pg, ck, arena, pos, S) && (int64_t)C.blk0 < S.nblk;
   const int64_t cstart = 16 * (int64_t)C.blk0 - (on ? S.mis : 0);   // region offset of the chunk start
   if (threadIdx.x == 0) { s_bad = 0; s_last = -1; }
@@ -1362,68 +1355,51 @@ __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chu
     while (m) {
       const int b = __ffs(m) - 1;
       m &= m - 1;
-      if (k < DK_POS_CHUNK / 5 + 8) cpos[k] = (int16_t)(rb + b - 3 - cstart);
+      if (k < POS_CAP) cpos[k] = (int16_t)(rb + b - 3 - cstart);
       k++;
     }
     run += tot;
   }
   __syncthreads();
   const int cnt = run;
-  const bool fits = cnt <= DK_POS_CHUNK / 5 + 8;    // (more is impossible for a real chain: fallback)
-  // publish the count, then add up the predecessors' (thread 0) while the others check the chain
-  if (threadIdx.x == 0) {
-    int base = 0;
-    if (gi > pg.pchunk0) {
-      __hip_atomic_store(&C.pad, POS_ST_AGG | (cnt & POS_ST_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int j = gi - 1; j >= pg.pchunk0; j--) {
-        int v;
-        do { v = __hip_atomic_load(&pcs_all[j].pad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); } while (v == 0);
-        base += v & POS_ST_VAL;
-        if (v & POS_ST_INC) break;
-      }
-    }
-    __hip_atomic_store(&C.pad, POS_ST_INC | ((base + cnt) & POS_ST_VAL), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_base = base;
-  }
+  const bool fits = cnt <= POS_CAP;                 // (more is impossible for a real chain: fallback)
   bool bad = !fits;
+  int16_t* slot = scratch + (int64_t)gi * POS_CAP;
   for (int k = threadIdx.x; fits && k < cnt; k += NT) {
     const int64_t q = cstart + cpos[k];
     const int64_t nx = q + 4 + (int64_t)ld_u32(S.r + q);
     if (k + 1 < cnt) { if (nx != cstart + cpos[k + 1]) bad = true; }
     else s_last = nx > 0x7fffffffll ? -2 : (int)nx;
+    slot[k] = cpos[k];
   }
   if (bad) s_bad = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
     C.cnt = cnt;
-    C.base = s_base;
     C.first = cnt && fits ? (int32_t)(cstart + cpos[0]) : -1;
     C.last_next = fits ? s_last : -1;
     C.ok = !s_bad;
   }
-  // the positions, at their value index (a chunk whose chain breaks fails its page: k_pos_fallback)
-  if (fits && !s_bad)
-    for (int k = threadIdx.x; k < cnt; k += NT)
-      if (s_base + k < S.n) S.P[s_base + k] = (int32_t)(cstart + cpos[k]);
 }
 
 __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chunks, DPage* __restrict__ pages,
                                                  const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
-                                                 DPosChunk* __restrict__ pcs) {
+                                                 DPosChunk* __restrict__ pcs, const int16_t* __restrict__ scratch) {
   DPage& pgw = pages[blockIdx.x];
   const DPage pg = pgw;
   if (pg.npchunk == 0) return;
-  for (int c = threadIdx.x; c < pg.npchunk; c += NT) pcs[pg.pchunk0 + c].pad = 0;   // k_pos_count's status words
   const DChunk ck = chunks[pg.chunk];
   StrRegion S;
   if (!str_region(pg, ck, arena, pos, S)) return;
   __shared__ int lds[12];
+  __shared__ int s_ok;
   int run = 0;
   for (int c0 = 0; c0 < pg.npchunk; c0 += NT) {
     const int c = c0 + threadIdx.x;
     const int v = c < pg.npchunk ? pcs[pg.pchunk0 + c].cnt : 0;
     int ex, e1, e2, tot, t1, t2;
     block_scan3(v, 0, 0, &ex, &e1, &e2, &tot, &t1, &t2, lds);
+    if (c < pg.npchunk) pcs[pg.pchunk0 + c].base = run + ex;
     run += tot;
   }
   if (threadIdx.x == 0) {
@@ -1441,6 +1417,16 @@ __global__ __launch_bounds__(NT) void k_pos_scan(const DChunk* __restrict__ chun
     if (expect != S.R) ok = false;
     pgw.pos_fail = !ok;
     S.P[S.n] = (int32_t)S.R;
+    s_ok = ok;
+  }
+  __syncthreads();
+  if (!s_ok) return;                                 // k_pos_fallback writes the page
+  // every chunk's offsets to their value indexes
+  for (int c = 0; c < pg.npchunk; c++) {
+    const DPosChunk C = pcs[pg.pchunk0 + c];
+    const int64_t cstart = 16 * (int64_t)C.blk0 - S.mis;
+    const int16_t* slot = scratch + (int64_t)(pg.pchunk0 + c) * POS_CAP;
+    for (int k = threadIdx.x; k < C.cnt; k += NT) S.P[C.base + k] = (int32_t)(cstart + slot[k]);
   }
 }
 
@@ -4071,11 +4057,10 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
 }
 // string positions of pages [page0, page0 + n_pages) whose chunks are pcs[pc0, pc0 + npc)
 void launch_positions(const DChunk* c, DPage* p, int page0, int n_pages, const uint8_t* arena, int32_t* pos,
-                      DPosChunk* pcs, int pc0, int npc, int* ticket, hipStream_t s) {
+                      DPosChunk* pcs, int pc0, int npc, int16_t* scratch, hipStream_t s) {
   if (!npc) return;
-  (void)hipMemsetAsync(ticket, 0, sizeof(int), s);
-  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs, pc0, ticket);
-  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs);
+  hipLaunchKernelGGL(k_pos_count, dim3(npc), dim3(NT), 0, s, c, p, arena, pos, pcs, pc0, scratch);
+  hipLaunchKernelGGL(k_pos_scan, dim3(n_pages), dim3(NT), 0, s, c, p + page0, arena, pos, pcs, (const int16_t*)scratch);
   hipLaunchKernelGGL(k_pos_fallback, dim3((n_pages + 63) / 64), dim3(64), 0, s, c, p + page0, n_pages, arena, pos);
 }
 void launch_page_runs(const DChunk* c, DPage* p, int n, const uint8_t* arena, Seg* runs, hipStream_t s) {
