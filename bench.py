@@ -67,6 +67,11 @@ CONFIGS = {
                          adds_per_commit=50, removes_per_commit=50),
                desc="C2: %d-AddFile single-part snappy checkpoint per GPU, 2-key partitionValues, stats JSON + "
                     "stats_parsed, 100-commit JSON tail; read schema add(with stats)+remove (C2b)"),
+    "c2a": dict(rows=10_000_000, shared=False, stats=False, predicate=None,
+                spec=dict(pv_keys=2, compression="snappy", with_stats=True, with_stats_parsed=True, n_commits=100,
+                          adds_per_commit=50, removes_per_commit=50),
+                desc="C2a: %d-AddFile single-part snappy checkpoint per GPU, 2-key partitionValues, stats JSON + "
+                     "stats_parsed, 100-commit JSON tail; read schema add(no stats)+remove"),
     "c3": dict(rows=100_000_000, shared=True, stats=False, predicate=None,
                spec=dict(n_parts=64, compression="snappy", n_commits=1000, adds_per_commit=100,
                          removes_per_commit=100, readd_frac=0.1, dup_frac=0.05),
