@@ -523,7 +523,12 @@ __device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets 
   return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
 
+__device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
 __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
+#ifdef DK_SNAP_STATS
+  const unsigned long long fc0 = clock64();
+  unsigned long long fcorr = 0, fcorr_cy = 0;
+#endif
   const int ci = X.c0 + blockIdx.x, lane = threadIdx.x;
   const uint8_t* in; uint8_t* out; int64_t clen, ulen, lv;
   if (!snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
@@ -552,7 +557,14 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
       const int L = __ffsll((long long)m) - 1;
       const int32_t eL = __shfl(pv, L, 64);
       int32_t to2 = 0, tx2 = 0;
+#ifdef DK_SNAP_STATS
+      const unsigned long long cc0 = clock64();
+      fcorr++;
+#endif
       if (lane == L) snap_seg_from(X, base + L, base + L - k0, in, clen, eL, true, &to2, &tx2);
+#ifdef DK_SNAP_STATS
+      fcorr_cy += clock64() - cc0;
+#endif
       to2 = __shfl(to2, L, 64);
       tx2 = __shfl(tx2, L, 64);
       if (lane == L) { e = eL; tout = to2; tex = tx2; fixed = true; }
@@ -606,6 +618,13 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
   }
   if (running != ulen || prev_exit != (int32_t)clen) bad = true;
   if (lane == 0) X.serial[ci] = bad ? 1 : 0;
+#ifdef DK_SNAP_STATS
+  if (lane == 0) {
+    atomicAdd(&dk_snap_stats[21], fcorr);
+    atomicAdd(&dk_snap_stats[22], clock64() - fc0);
+    atomicAdd(&dk_snap_stats[23], fcorr_cy);
+  }
+#endif
 }
 
 // One wave per 64 KiB fragment (bitmap mode): the compressed offset of the fragment's first tag,
@@ -688,7 +707,6 @@ __device__ __forceinline__ int32_t small_mod_f(int32_t i, int32_t d) {
 }
 
 
-__device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
 
 // k_snap_frag: one wave per 64 KiB output fragment, in batches of up to 64 tags (one per lane).
 //  1. tag starts: every lane parses the candidate tag at cursor + lane (LDS window); the true chain

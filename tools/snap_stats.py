@@ -1,5 +1,5 @@
 """k_snap_frag batch statistics on a bench table (needs a DK_SNAP_STATS build loaded via DK_LIB_PATH:
-DK_VARIANT_FLAGS=-DDK_SNAP_STATS python tools/build_variant.py build/libdk_stats.so).
+DK_VARIANT_FLAGS=-DDK_SNAP_STATS python tools/build_variant.py stats_lib/libdk_stats.so).
 Usage: DK_LIB_PATH=build/libdk_stats.so python tools/snap_stats.py TABLE_DIR"""
 import ctypes as C
 import sys
@@ -11,7 +11,8 @@ from delta_amd._lib import lib  # noqa: E402
 
 NAMES = ["batches", "batch_tags", "dep_tags", "far_tags", "win_copies", "big_literals", "refills",
          "resolve_rounds", "sum_CH", "fragments", "ring_tags", "literal_tags", "cand_rounds",
-         "cy_top", "cy_discovery", "cy_parse_scan", "cy_resolve", "cy_farq", "cy_bytes", "cy_dep", "cy_flush"]
+         "cy_top", "cy_discovery", "cy_parse_scan", "cy_resolve", "cy_farq", "cy_bytes", "cy_dep", "cy_flush",
+         "fix_corrections", "fix_cycles", "fix_correction_cycles"]
 eng = K.GpuEngine()
 snap = K.Table.forPath(eng, sys.argv[1]).getLatestSnapshot(eng)
 scan = snap.getScanBuilder().build()
