@@ -1,6 +1,7 @@
 #!/bin/bash
 # k_snap_pipe vs k_snap_frag on a 12.5M-row C3-shaped snappy table: kernel trace + one SQ PMC pass
-# per variant (DK_SNAP_PIPE=1 / 0). Usage (via gpurun): bash tools/snap_ab.sh TAG
+# per variant (DK_SNAP_PIPE=1 / 0: a switch of the profiles/r05/snap_pipe_ab patch only; without
+# the patch both passes run the same kernel). Usage (via gpurun): bash tools/snap_ab.sh TAG
 set -o pipefail
 TAG=$1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG; mkdir -p $OUT; cd $GRAFT_REPO_ROOT

@@ -30,7 +30,7 @@ cd /tmp
 i=0
 for lib in "$@"; do
   i=$((i+1))
-  if [ "$lib" = default ]; then L="DK_VERBOSE="; elif [ "$lib" = frag ]; then L="DK_SNAP_PIPE=0"; else L="DK_LIB_PATH=$GRAFT_REPO_ROOT/$lib"; fi
+  if [ "$lib" = default ]; then L="DK_VERBOSE="; else L="DK_LIB_PATH=$GRAFT_REPO_ROOT/$lib"; fi
   env $L DK_ASYNC_OPEN=0 DK_OPEN_SLICES=1 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/v$i -o k -- python3 /tmp/snap_run.py > $OUT/v$i.log 2>&1 || { echo "run $i failed"; tail -5 $OUT/v$i.log; exit 1; }
   python3 - $OUT/v$i "$lib" <<PY
 import csv, glob, sys
