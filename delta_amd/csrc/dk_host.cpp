@@ -183,6 +183,10 @@ struct Reaper {
   }
   bool busy() { std::lock_guard<std::mutex> g(mu); return pending > 0; }
   void drain() { std::unique_lock<std::mutex> lk(mu); cv.wait(lk, [&] { return pending == 0; }); }
+  bool drain_for(int ms) {
+    std::unique_lock<std::mutex> lk(mu);
+    return cv.wait_for(lk, std::chrono::milliseconds(ms), [&] { return pending == 0; });
+  }
   bool registered = false;
   static void reaper_drain();
 };
@@ -195,6 +199,8 @@ static thread_local int t_synced = 0;
 // pending release may be a dk_parquet_close whose reaper job joins that very open, so a cache miss
 // there must never wait for the reaper (it allocates afresh instead).
 static thread_local int t_no_drain = 0;
+static thread_local int t_drain_budget_ms = 0;   // bounded wait left to such a thread (ms)
+constexpr int kOpenDrainMs = 40;
 struct SyncedRelease {
   SyncedRelease() { t_synced++; }
   ~SyncedRelease() { t_synced--; }
@@ -238,14 +244,27 @@ struct MemCache {
         return b.p;
       }
     }
-    if (!t_no_drain && reaper().busy()) {   // a deferred release may be returning just such a block
-      reaper().drain();
+    static const bool verbose = getenv("DK_VERBOSE") != nullptr;
+    // A deferred release may be returning just such a block (the previous scan's close). Open
+    // threads wait a bounded time only: the pending release may be the close that joins this open.
+    if (reaper().busy() && !(t_no_drain && t_drain_budget_ms <= 0)) {
+      const auto t0 = std::chrono::steady_clock::now();
+      if (t_no_drain) reaper().drain_for(t_drain_budget_ms); else reaper().drain();
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (t_no_drain) t_drain_budget_ms -= (int)ms + 1;
+      if (verbose && ms > 2) fprintf(stderr, "[dk] cache %s: waited %.1f ms for pending releases\n", pinned ? "pinned" : "device", ms);
       return get(want, got);
     }
     void* p = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     if (raw_alloc(&p, n)) {        // out of memory: give back every cached block of this device, retry
       trim(dev, 0);
       if (raw_alloc(&p, n)) return nullptr;
+    }
+    if (verbose) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      if (ms > 2) fprintf(stderr, "[dk] cache %s miss: %.1f MB allocated in %.1f ms (held %.2f GB)\n", pinned ? "pinned" : "device",
+                          n / 1e6, ms, held / 1e9);
     }
     *got = n;
     return p;
@@ -261,6 +280,8 @@ struct MemCache {
   }
   void trim(int dev, size_t keep) { std::lock_guard<std::mutex> lk(mu); trim_locked(dev, keep); }
   void trim_locked(int dev, size_t keep) {
+    if (getenv("DK_VERBOSE"))
+      fprintf(stderr, "[dk] cache %s trim: %.2f GB held, keeping %.2f GB\n", pinned ? "pinned" : "device", held / 1e9, keep / 1e9);
     hipDeviceSynchronize();
     idle.insert(idle.end(), parked.begin(), parked.end());
     parked.clear();
@@ -2180,7 +2201,7 @@ static void parallel_for(int n, F fn) {
   std::vector<std::thread> th;
   const int no_drain = t_no_drain;               // workers of an open stay off the reaper
   for (int t = 0; t < nt; t++)
-    th.emplace_back([&, no_drain] { t_no_drain = no_drain; for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
+    th.emplace_back([&, no_drain] { t_no_drain = no_drain; t_drain_budget_ms = kOpenDrainMs; for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
   for (auto& x : th) x.join();
 }
 
@@ -2439,6 +2460,7 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   const int no_drain = t_no_drain;
   std::thread reader([&, no_drain] {
     t_no_drain = no_drain;
+    t_drain_budget_ms = kOpenDrainMs;
     {
       for (int fi = 0; fi < n_files; fi++) {
         fds[fi] = open(p->files[fi].path.c_str(), O_RDONLY);
@@ -2621,6 +2643,7 @@ extern "C" int dk_parquet_open_async(dk_engine* e, const char* const* paths, int
   const std::vector<std::vector<int32_t>>* gp = (rg_count && !all) ? &groups : nullptr;
   std::thread t([&, gp] {
     t_no_drain = 1;
+    t_drain_budget_ms = kOpenDrainMs;
     dk_parquet* q = nullptr;
     bool pub = false;
     std::function<void(dk_parquet*)> pub_fn = [&](dk_parquet* x) { pub = true; publish(x); };
