@@ -22,7 +22,8 @@ driver's `torch.distributed.run --nproc-per-node N bench.py --gpus N` does. C3 i
 checkpoint row groups are cut into N contiguous runs (delta_amd/shard.py). With the default
 `--exchange owner`, each rank parses only the commit files j = rank (mod N), the keys are owned by
 hash, and three RCCL all-to-alls resolve every commit-tail action and every checkpoint row at its
-key's owner (shard.OwnerExchange; `owner_exchange_ms`); each rank consumes its own scan files and
+key's owner (the protocol and its RCCL collectives inside libdkgpu: dk_replay_owner_run over
+shard.OwnerComm.rccl; `owner_exchange_ms`); each rank consumes its own scan files and
 counters and consumer sums are all-reduced. `--exchange allgather` keeps the whole commit tail on
 every rank and ends the device step with one RCCL all-gather of counters and selection bitmaps
 (shard.SelectionExchange, `exchange_ms`).
@@ -509,7 +510,7 @@ def main(argv=None):
     owner = None
     if args.exchange == "owner" and cfg["shared"] and world > 1:
         from delta_amd import shard
-        owner = shard.OwnerExchange(device="cuda")
+        owner = shard.OwnerComm.rccl()         # RCCL over xGMI, owned by libdkgpu (dk_comm_create)
     owner_ms = []
     a2a_ms = []
 

@@ -75,6 +75,41 @@ class dk_dv_descriptor(C.Structure):
 
 MAX_LEAF_DEPTH = 8
 
+# dk_comm (include/dkgpu.h): the owner exchange's collectives behind the C ABI
+COMM_ID_BYTES = 128
+STATUS_PEER = 6
+A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64))
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_int64), C.c_int32, C.c_int32)
+
+
+class dk_comm_callbacks(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("alltoallv", A2A_FN), ("allreduce_i64", ALLREDUCE_FN)]
+
+
+_U = C.c_void_p
+SIDE_FNS = [
+    ("begin", C.CFUNCTYPE(C.c_int, _U)),
+    ("tail_counts", C.CFUNCTYPE(C.c_int, _U, C.POINTER(C.c_int64), C.POINTER(C.c_int64))),
+    ("tail_pack", C.CFUNCTYPE(C.c_int, _U, C.c_void_p, C.c_void_p)),
+    ("tail_resolve", C.CFUNCTYPE(C.c_int, _U, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p,
+                                 C.POINTER(C.c_int32))),
+    ("reseed", C.CFUNCTYPE(C.c_int, _U)),
+    ("tail_finish", C.CFUNCTYPE(C.c_int, _U, C.c_void_p)),
+    ("run", C.CFUNCTYPE(C.c_int, _U)),
+    ("ckpt_counts", C.CFUNCTYPE(C.c_int, _U, C.POINTER(C.c_int64))),
+    ("ckpt_pack", C.CFUNCTYPE(C.c_int, _U, C.c_void_p)),
+    ("ckpt_lookup", C.CFUNCTYPE(C.c_int, _U, C.c_void_p, C.c_int64, C.c_void_p)),
+    ("ckpt_apply", C.CFUNCTYPE(C.c_int, _U, C.c_void_p)),
+    ("cand_counts", C.CFUNCTYPE(C.c_int, _U, C.POINTER(C.c_int64), C.POINTER(C.c_int64))),
+    ("cand_pack", C.CFUNCTYPE(C.c_int, _U, C.c_void_p, C.c_void_p)),
+    ("cand_verify", C.CFUNCTYPE(C.c_int, _U, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p)),
+    ("cand_finish", C.CFUNCTYPE(C.c_int, _U, C.c_void_p)),
+]
+
+
+class dk_owner_side(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("device_buffers", C.c_int32)] + SIDE_FNS
+
 EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy", "dk_parquet_open",
            "dk_parquet_decode", "dk_parquet_sync", "dk_parquet_num_rows", "dk_parquet_column",
            "dk_parquet_first_row", "dk_parquet_column_rows",
@@ -101,7 +136,9 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_replay_owner_cand_counts", "dk_replay_owner_cand_pack", "dk_replay_owner_cand_verify",
            "dk_replay_owner_cand_finish", "dk_skip_compile", "dk_part_compile", "dk_program_describe",
            "dk_program_free", "dk_json_parse", "dk_parsed_num_leaves", "dk_parsed_leaf_path", "dk_parsed_column_get",
-           "dk_parsed_eval", "dk_parsed_free"]
+           "dk_parsed_eval", "dk_parsed_free", "dk_comm_unique_id", "dk_comm_create", "dk_comm_create_callbacks",
+           "dk_comm_create_local", "dk_comm_world", "dk_comm_rank", "dk_comm_allreduce_i64", "dk_comm_alltoallv",
+           "dk_comm_abort", "dk_comm_last_run", "dk_comm_destroy", "dk_replay_owner_run", "dk_owner_protocol_run"]
 
 
 def lib(build_if_missing=True):
@@ -211,6 +248,18 @@ def lib(build_if_missing=True):
         "dk_parsed_column_get": (C.c_int, [P, I32, C.POINTER(dk_parsed_column)]),
         "dk_parsed_eval": (C.c_int, [P, P, P]),
         "dk_parsed_free": (None, [P]),
+        "dk_comm_unique_id": (C.c_int, [P]),
+        "dk_comm_create": (C.c_int, [P, I32, I32, I32, C.POINTER(P)]),
+        "dk_comm_create_callbacks": (C.c_int, [C.POINTER(dk_comm_callbacks), I32, I32, C.POINTER(P)]),
+        "dk_comm_create_local": (C.c_int, [I32, I32, C.POINTER(P)]),
+        "dk_comm_world": (I32, [P]), "dk_comm_rank": (I32, [P]),
+        "dk_comm_allreduce_i64": (C.c_int, [P, C.POINTER(I64), I32, I32]),
+        "dk_comm_alltoallv": (C.c_int, [P, P, C.POINTER(I64), P, C.POINTER(I64), I32]),
+        "dk_comm_abort": (C.c_int, [P]),
+        "dk_comm_last_run": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(I64)]),
+        "dk_comm_destroy": (None, [P]),
+        "dk_replay_owner_run": (C.c_int, [P, P]),
+        "dk_owner_protocol_run": (C.c_int, [C.POINTER(dk_owner_side), P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

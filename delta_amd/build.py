@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdkgpu.so")
 OBJ = os.path.join(HERE, "..", "build", "obj")   # kept between builds: only stale objects recompile
-SOURCES = ["dk_host.cpp", "dk_expr.cpp", "dk_kernels.hip", "dk_arrow.hip", "dk_dv.hip", "dk_encode.hip"]
+SOURCES = ["dk_host.cpp", "dk_expr.cpp", "dk_comm.cpp", "dk_kernels.hip", "dk_arrow.hip", "dk_dv.hip", "dk_encode.hip"]
 HEADERS = ["dk_device.h", "dk_thrift.h", "dk_uri.h", "dk_expr.h"]
 
 

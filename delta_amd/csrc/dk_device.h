@@ -235,7 +235,10 @@ enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, 
                  PO_STARTS_WITH = 18,    // String.startsWith(literal)
                  PO_LIKE = 19,           // LIKE pattern compiled to tokens (byte pairs: 0 b literal, 1 one
                                          // code point, 2 any run)
-                 PO_SUBSTR = 20 };       // SUBSTRING(s, pos[, len]): lit = (uint32)pos | len << 32, arg = has len
+                 PO_SUBSTR = 20,         // SUBSTRING(s, pos[, len]): lit = (uint32)pos | len << 32, arg = has len
+                 PO_LIKE_DYN = 21,       // LIKE(s, pattern) with the pattern a value (top) over s (below):
+                                         // arg = the escape code point (LikeExpressionEvaluator.eval)
+                 PO_TIMEADD = 22 };      // TIMEADD(ts, millis): ts (below) + millis (top) * 1000, wrapping
 struct DPartProg {
   int32_t n_fields, n_ops;
   const int32_t* field_type;       // [n_fields] PT_*

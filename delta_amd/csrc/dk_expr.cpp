@@ -985,7 +985,24 @@ struct PartCompiler {
     if (x.k == Ex::LIT) return x.type;
     if (x.k == Ex::CALL && x.name == "COALESCE" && !x.args.empty()) return type_of(x.args[0]);
     if (x.k == Ex::CALL && x.name == "SUBSTRING") return "string";
+    if (x.k == Ex::CALL && x.name == "TIMEADD" && !x.args.empty()) return type_of(x.args[0]);
     return "boolean";
+  }
+  // stack slots an expression needs as emitted (AND / OR take their deeper operand first: Kleene AND /
+  // OR are commutative and both operands are always evaluated, so any nesting -- e.g. a long chain of
+  // AND(x, NOT(AND(y, NOT(...)))) -- fits the device stack)
+  int need(const Ex& x) {
+    if (x.k != Ex::CALL) return 1;
+    const std::string& n = x.name;
+    const auto& c = x.args;
+    if (n == "PARTITION_VALUE" || n == "ELEMENT_AT" || c.empty()) return 1;
+    if ((n == "AND" || n == "OR") && c.size() == 2) {
+      const int a = need(c[0]), b = need(c[1]);
+      return a >= b ? std::max(a, b + 1) : std::max(b, a + 1);
+    }
+    int d = 0;
+    for (size_t i = 0; i < c.size(); i++) d = std::max(d, need(c[i]) + (int)i);
+    return std::max(d, 1);
   }
   // an operand (value expression); returns its comparison kind ("" for a null literal)
   std::string operand(const Ex& x) {
@@ -1012,6 +1029,17 @@ struct PartCompiler {
       }
       push(PO_COALESCE, (int)x.args.size());
       return k0;
+    }
+    if (x.k == Ex::CALL && x.name == "TIMEADD") {    // DefaultExpressionEvaluator.visitTimeAdd (:260-288, :593-626)
+      if (x.args.size() != 2)
+        throw Unsupported{3, "Unsupported expression: TIMEADD requires exactly two arguments: timestamp column and milliseconds"};
+      const std::string t0 = type_of(x.args[0]), t1 = type_of(x.args[1]);
+      if (!((t0 == "timestamp" || t0 == "timestamp_ntz") && t1 == "long"))
+        throw Unsupported{3, "TIMEADD requires a timestamp and a Long (milliseconds) to add to it"};
+      operand(x.args[0]);
+      operand(x.args[1]);
+      push(PO_TIMEADD);
+      return "timestamp";
     }
     if (x.k == Ex::CALL && x.name == "SUBSTRING") {  // SubstringEvaluator.java:36-60
       if (x.args.size() < 2 || x.args.size() > 3)
@@ -1075,10 +1103,8 @@ struct PartCompiler {
         throw Unsupported{3, like ? "Unsupported expression: LIKE is only supported for string type expressions"
                                   : "Unsupported expression: 'STARTS_WITH' expects STRING type inputs"};
     const Ex& lit = x.args[1];
-    if (lit.k != Ex::LIT) {
-      if (!like) throw Unsupported{3, "Unsupported expression: 'STARTS_WITH' expects literal as the second input"};
-      refuse("LIKE with a non-literal pattern is not supported by this engine build");
-    }
+    if (lit.k != Ex::LIT && !like)
+      throw Unsupported{3, "Unsupported expression: 'STARTS_WITH' expects literal as the second input"};
     uint32_t esc = '\\';
     if (x.args.size() == 3) {
       const Ex& e = x.args[2];
@@ -1093,6 +1119,11 @@ struct PartCompiler {
       for (size_t k = 1; k < n; k++) esc = (esc << 6) | (t[k] & 63);
     }
     operand(x.args[0]);
+    if (lit.k != Ex::LIT) {                          // a per-row pattern: tokenized on the device per row
+      operand(lit);
+      push(PO_LIKE_DYN, (int)esc);
+      return;
+    }
     Op o;
     o.op = like ? PO_LIKE : PO_STARTS_WITH;
     if (lit.null) { o.arg = 1; ops.push_back(o); return; }
@@ -1117,8 +1148,9 @@ struct PartCompiler {
     if (n == "STARTS_WITH" || n == "LIKE") { string_pred(x); return; }
     if (n == "AND" || n == "OR") {
       if (c.size() != 2) refuse(n + " takes two predicates");
-      pred(c[0]);
-      pred(c[1]);
+      const bool swap = need(c[1]) > need(c[0]);     // the deeper operand first (Sethi-Ullman order)
+      pred(c[swap ? 1 : 0]);
+      pred(c[swap ? 0 : 1]);
       push(n == "AND" ? PO_AND : PO_OR);
       return;
     }

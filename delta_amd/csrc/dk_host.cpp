@@ -5058,8 +5058,9 @@ static int owner_phase(dk_replay* r, int want, const char* who) {
 
 extern "C" int dk_replay_set_owner(dk_replay* r, int32_t world, int32_t rank) {
   if (!r) return fail("null replay");
-  if (world <= 1) { r->ow = 0; return 0; }
-  if (world > 64 || rank < 0 || rank >= world) return fail("dk_replay_set_owner: bad world / rank");
+  if (world == 0) { r->ow = 0; return 0; }        // (owner mode off)
+  // world 1 is a real owner run (one rank through a communicator, e.g. a one-GPU RCCL world)
+  if (world < 0 || world > 64 || rank < 0 || rank >= world) return fail("dk_replay_set_owner: bad world / rank");
   if (r->xw > 0) return fail("dk_replay_set_owner: the replay is in hash-exchange mode");
   r->ow = world; r->orank = rank;
   r->ophase = OP_IDLE;

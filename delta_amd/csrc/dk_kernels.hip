@@ -3368,6 +3368,64 @@ __device__ bool like_match(const uint8_t* s, int32_t n, const uint8_t* t, int32_
   return p >= tn && i == n;
 }
 
+// LIKE with a per-row pattern (LikeExpressionEvaluator.eval :86-140 with escapeLikeRegex :155-186): the
+// pattern is first checked whole (an escape must be followed by '_', '%' or the escape itself, else the
+// reference throws "LIKE expression has invalid escape sequence"), then matched as like_match does:
+// '_' one code point, '%' any run, anything else (or an escaped character) itself, one backtrack point.
+// Returns 1 / 0, -1 on an invalid escape.
+__device__ int like_match_dyn(const uint8_t* s, int32_t n, const uint8_t* pat, int32_t pn, uint32_t esc) {
+  auto cp_at = [&](int32_t k, int32_t* len) -> uint32_t {
+    const uint8_t c = pat[k];
+    int32_t l = utf8_len(c);
+    if (k + l > pn) l = pn - k;
+    uint32_t cp = l == 1 ? c : l == 2 ? (c & 31) : l == 3 ? (c & 15) : (c & 7);
+    for (int32_t q = 1; q < l; q++) cp = (cp << 6) | (pat[k + q] & 63);
+    *len = l;
+    return cp;
+  };
+  for (int32_t k = 0; k < pn;) {                     // validate the escapes
+    int32_t l;
+    const uint32_t cp = cp_at(k, &l);
+    if (cp == esc) {
+      if (k + l >= pn) return -1;
+      int32_t l2;
+      const uint32_t nx = cp_at(k + l, &l2);
+      if (!(nx == '_' || nx == '%' || nx == esc)) return -1;
+      k += l + l2;
+    } else {
+      k += l;
+    }
+  }
+  // token at pattern position p: kind 0 literal bytes [lb, lb + ll), 1 one code point, 2 any run
+  auto tok = [&](int32_t p, int* kind, int32_t* lb, int32_t* ll) -> int32_t {
+    int32_t l;
+    const uint32_t cp = cp_at(p, &l);
+    if (cp == esc) { int32_t l2; cp_at(p + l, &l2); *kind = 0; *lb = p + l; *ll = l2; return p + l + l2; }
+    *kind = cp == '_' ? 1 : cp == '%' ? 2 : 0;
+    *lb = p; *ll = l;
+    return p + l;
+  };
+  int32_t i = 0, p = 0, star_p = -1, star_i = 0;
+  while (i < n) {
+    int kind = -1;
+    int32_t lb = 0, ll = 0, np = p;
+    if (p < pn) np = tok(p, &kind, &lb, &ll);
+    if (kind == 0 && i + ll <= n && bytes_cmp(s + i, ll, pat + lb, ll) == 0) { i += ll; p = np; }
+    else if (kind == 1) { i += utf8_len(s[i]); p = np; }
+    else if (kind == 2) { star_p = np; p = np; star_i = i; }
+    else if (star_p >= 0) { p = star_p; star_i += utf8_len(s[star_i]); i = star_i; }
+    else return 0;
+  }
+  while (p < pn) {
+    int kind;
+    int32_t lb, ll;
+    const int32_t np = tok(p, &kind, &lb, &ll);
+    if (kind != 2) break;
+    p = np;
+  }
+  return p >= pn && i == n ? 1 : 0;
+}
+
 // element_at(add.partitionValues, <field k's name>) of one row, deserialized as partition_value does
 // (PartitionValueEvaluator.java:50-100); kind 0 when the map or the key is absent or the value null.
 // false on a malformed value.
@@ -3503,6 +3561,22 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
         a.v = op == PO_STARTS_WITH ? (a.len >= tn && bytes_cmp(a.p, tn, t, tn) == 0) : like_match(a.p, a.len, t, tn);
         a.kind = 3;
       }
+    } else if (op == PO_LIKE_DYN) {                      // LIKE(s, pattern value): null if either is null
+      if (sp < 2) return -1;
+      const PVal pt = st[--sp];
+      PVal& a = st[sp - 1];
+      if (a.kind != 0 && pt.kind == 0) a.kind = 0;
+      if (a.kind != 0) {
+        const int m = like_match_dyn(a.p, a.len, pt.p, pt.len, (uint32_t)P.arg[i]);
+        if (m < 0) { *err = true; return -1; }           // "LIKE expression has invalid escape sequence"
+        a.kind = 3; a.v = m;
+      }
+    } else if (op == PO_TIMEADD) {                       // DefaultExpressionEvaluator.visitTimeAdd (:593-626)
+      if (sp < 2) return -1;
+      const PVal d = st[--sp];
+      PVal& a = st[sp - 1];
+      if (d.kind == 0) a.kind = 0;
+      if (a.kind != 0) a.v = (long long)((unsigned long long)a.v + (unsigned long long)d.v * 1000ull);
     } else if (op == PO_SUBSTR) {                        // SubstringEvaluator.getString (:92-121), code points
       if (sp < 1) return -1;
       PVal& a = st[sp - 1];

@@ -1019,14 +1019,21 @@ class ScanBuilder:
         self.read_stats = flag
         return self
 
+    def withReadSchema(self, schema_json):
+        """ScanBuilderImpl.withReadSchema (ScanBuilderImpl.java:70-74): the logical schema the scan
+        state reports (Kernel StructType JSON); the scan files are the same."""
+        self.read_schema = schema_json
+        return self
+
     def withShard(self, world, rank, exchange=None, owner=None):
         """Reconcile only this rank's checkpoint row groups (delta_amd/shard.py). exchange: None (the
         probe runs against this rank's own copy of the commit-tail key table), or a callable that
         drives the hash(path)-owner exchange for this rank (shard.exchange_hash_owner over
         torch.distributed, or an in-process loopback), called with the scan's ExchangeSide after
-        every run. owner: the owner-partitioned reconciliation (shard.OwnerExchange or a loopback):
-        this rank parses only its share of the commit files, and the key table of the keys it owns
-        answers every rank's rows for them."""
+        every run. owner: the owner-partitioned reconciliation over a library communicator
+        (shard.OwnerComm: RCCL, callbacks or in-process ranks): this rank parses only its share of
+        the commit files, and the key table of the keys it owns answers every rank's rows for them;
+        the whole protocol runs in dk_replay_owner_run."""
         self.shard = (int(world), int(rank))
         self.exchange = exchange
         self.owner = owner
@@ -1036,8 +1043,10 @@ class ScanBuilder:
 
     def build(self):
         sc = GpuScan(self.snapshot, self.read_stats, self.shard, self.predicate)
+        sc.read_schema = getattr(self, "read_schema", None)
         sc.exchange = getattr(self, "exchange", None)
-        sc.owner = getattr(self, "owner", None) if self.shard and self.shard[0] > 1 else None
+        # owner mode: an explicit owner communicator (also at world 1: one RCCL rank through the ABI)
+        sc.owner = getattr(self, "owner", None) if self.shard else None
         return sc
 
 
@@ -1138,8 +1147,10 @@ class GpuScan:
                 try:
                     self.partition = programs.compile_partition(
                         self.partition_filter, pp.partition_fields(md["schemaString"], parts))
-                except sk.UnsupportedExpression as e:
-                    self._deferred_error = e          # the reference fails when the scan files are read
+                except (sk.UnsupportedExpression, pp.UnsupportedPartitionFilter) as e:
+                    # the reference fails when the scan files are read, never at build(); a filter
+                    # this engine cannot compile fails there too, loudly
+                    self._deferred_error = e
             if self.data_filter is not None:
                 leaves = sk.data_schema_leaves(md["schemaString"], parts)
                 node = sk.construct(self.data_filter, leaves)
@@ -1169,17 +1180,13 @@ class GpuScan:
 
     def getScanState(self, engine):
         """Scan.getScanState (ScanImpl.java:189-218, ScanStateRow.java:35-44) as a dict: the table's
-        configuration, schema string, partition columns, protocol versions and tablePath. Host-side
-        only: the logical schema stands for the physical ones (column-mapping translation is outside
-        the scan-file path this engine accelerates)."""
-        md = self.snapshot.metadata or {}
-        pr = self.snapshot.protocol or {}
-        schema = md.get("schemaString")
-        return {"configuration": dict(md.get("configuration") or {}), "logicalSchemaString": schema,
-                "physicalSchemaString": schema, "physicalDataReadSchemaString": schema,
-                "partitionColumns": list(md.get("partitionColumns") or []),
-                "minReaderVersion": pr.get("minReaderVersion"), "minWriterVersion": pr.get("minWriterVersion"),
-                "tablePath": self.table_root()}
+        configuration, the logical read schema, its physical equivalent under the column mapping
+        mode, the physical data read schema (no partition columns; `_metadata.row_index` when
+        deletionVectors is a reader feature), partition columns, protocol versions and tablePath;
+        schemas as the reference's JSON text (delta_amd/schema.py)."""
+        from . import schema
+        return schema.scan_state(self.snapshot.metadata or {}, self.snapshot.protocol or {}, self.table_root(),
+                                 read_schema=getattr(self, "read_schema", None))
 
     def prepare(self, engine):
         """Host-side setup: parse the commit tail, open checkpoint files, upload to HBM."""
@@ -1390,8 +1397,9 @@ class GpuScan:
         """The device step: commit-tail keys + table, checkpoint decode, probe, selection (with an
         exchange: decode + routing, the exchange, then the probe of the rows the owners flagged)."""
         if getattr(self, "owner", None) is not None:
-            from .shard import OwnerSide
-            self.owner(OwnerSide(self))            # the commit-tail exchange, dk_replay_run, the row exchanges
+            # the commit-tail exchange, dk_replay_run and the row exchanges, all in the library
+            # (dk_replay_owner_run over the owner's dk_comm)
+            self.owner.run_scan(self)
             return
         check(lib().dk_replay_run(self._rh))
         if getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1:
@@ -1440,13 +1448,21 @@ class GpuScan:
             self._detach_batches()          # the rerun reuses the pinned blocks earlier batches view
         t0 = time.perf_counter()
         groups = scan_groups(len(self.ckpt_files or []))
-        exchanging = (getattr(self, "exchange", None) is not None or getattr(self, "owner", None) is not None) \
-            and self.shard and self.shard[0] > 1
-        if exchanging and getattr(self, "owner", None) is not None and self.ckpt is not None:
-            # owner mode: add.size goes to host memory right after the decode, beside the exchanges
-            for leaf in self.PREFETCH_LEAVES:
-                if leaf in self.ckpt.leaves:
-                    check(lib().dk_replay_prefetch_leaf(self._rh, leaf.encode()))
+        owner = getattr(self, "owner", None)
+        exchanging = owner is not None or (getattr(self, "exchange", None) is not None and self.shard and self.shard[0] > 1)
+        if owner is not None and self.ckpt is not None:
+            # owner mode: add.size goes to host memory right after the decode, beside the exchanges.
+            # A failure here must still reach the peers (they are about to vote in the owner run):
+            # this rank answers the run's first vote with its error bit (owner.abort)
+            try:
+                for leaf in self.PREFETCH_LEAVES:
+                    if leaf in self.ckpt.leaves:
+                        check(lib().dk_replay_prefetch_leaf(self._rh, leaf.encode()))
+                if os.environ.get("DK_INJECT_PREFETCH_FAULT") == str(self.shard[1]):
+                    raise DkError("injected prefetch failure (DK_INJECT_PREFETCH_FAULT)")
+            except BaseException:
+                owner.abort()
+                raise
         if groups and not exchanging:
             # grouped: batches go out as their group of files is decoded and probed; the counters are
             # final once the iterator is exhausted (ScanImpl's metrics are read after it, too)

@@ -361,304 +361,112 @@ def exchange_local(sides):
 #      row (selected); the rest come back as candidates;
 #   3. the candidates' canonical keys to their owners, answered byte-exactly (selected / duplicate /
 #      tombstoned).
-# No rank holds the whole commit tail; the ScanMetrics counters are summed over the ranks.
+# The protocol and its collectives run inside libdkgpu (dk_replay_owner_run over a dk_comm,
+# delta_amd/csrc/dk_comm.cpp): RCCL over xGMI, a caller's transport through callbacks, or the ranks of
+# one process. No rank holds the whole commit tail; the ScanMetrics counters are summed over the ranks.
 # ------------------------------------------------------------------------------------------------
 REC_BYTES = 32                      # dk OwnerKeyRec
-COLLISION = 4                       # dk E_COLLISION: a 64-bit hash collision at an owner
-ERR_BIT = 1 << 20                   # vote bit: a rank failed at this step
 
 
 class OwnerPeerError(RuntimeError):
     """Another rank of the owner exchange failed (its own error is raised on that rank)."""
 
 
-class OwnerSide:
-    """One rank's side of the owner-partitioned reconciliation over a GpuScan's replay. Buffers are
-    torch uint8 / int64 tensors on the scan's GPU; every library call returns with its stream
-    drained."""
-
-    def __init__(self, scan):
-        import torch
-        self.scan = scan
-        self.world, self.rank = scan.shard
-        self.rh = scan._rh
-        self.device = torch.device("cuda", torch.cuda.current_device())
-
-    def _lib(self):
-        from ._lib import check, lib
-        return check, lib()
-
-    def _buf(self, n, dtype=None):
-        import torch
-        return torch.empty(max(1, n), dtype=dtype or torch.uint8, device=self.device)[:n]
-
-    def _in(self, t):
-        import torch
-        t = t.to(self.device).contiguous()
-        torch.cuda.current_stream().synchronize()          # the collective's data has landed
-        return t
-
-    def begin(self):
-        check, L = self._lib()
-        check(L.dk_replay_owner_begin(self.rh))
-
-    def tail_counts(self):
-        import ctypes as C
-        import numpy as np
-        check, L = self._lib()
-        recs, nbytes = np.zeros(self.world, np.int64), np.zeros(self.world, np.int64)
-        check(L.dk_replay_owner_tail_counts(self.rh, recs.ctypes.data_as(C.POINTER(C.c_int64)),
-                                            nbytes.ctypes.data_as(C.POINTER(C.c_int64))))
-        return recs, nbytes
-
-    def tail_pack(self, n, nbytes):
-        import ctypes as C
-        check, L = self._lib()
-        recs, keys = self._buf(n * REC_BYTES), self._buf(nbytes)
-        check(L.dk_replay_owner_tail_pack(self.rh, C.c_void_p(recs.data_ptr()), C.c_void_p(keys.data_ptr())))
-        return recs, keys
-
-    def tail_resolve(self, recs, keys):
-        import ctypes as C
-        check, L = self._lib()
-        recs, keys = self._in(recs), self._in(keys)
-        n = recs.numel() // REC_BYTES
-        ans, flags = self._buf(n), C.c_int32(0)
-        check(L.dk_replay_owner_tail_resolve(self.rh, C.c_void_p(recs.data_ptr()), n, C.c_void_p(keys.data_ptr()),
-                                             keys.numel(), C.c_void_p(ans.data_ptr()), C.byref(flags)))
-        return ans, int(flags.value)
-
-    def reseed(self):
-        check, L = self._lib()
-        check(L.dk_replay_owner_reseed(self.rh))
-
-    def tail_finish(self, back):
-        import ctypes as C
-        check, L = self._lib()
-        back = self._in(back)
-        check(L.dk_replay_owner_tail_finish(self.rh, C.c_void_p(back.data_ptr())))
-
-    def run(self):
-        check, L = self._lib()
-        check(L.dk_replay_run(self.rh))
-
-    def ckpt_counts(self):
-        import ctypes as C
-        import numpy as np
-        check, L = self._lib()
-        c = np.zeros(self.world, np.int64)
-        check(L.dk_replay_owner_ckpt_counts(self.rh, c.ctypes.data_as(C.POINTER(C.c_int64))))
-        return c
-
-    def ckpt_pack(self, n):
-        import ctypes as C
-        import torch
-        check, L = self._lib()
-        send = self._buf(n, torch.int64)
-        check(L.dk_replay_owner_ckpt_pack(self.rh, C.c_void_p(send.data_ptr())))
-        return send
-
-    def ckpt_lookup(self, recv):
-        import ctypes as C
-        check, L = self._lib()
-        recv = self._in(recv)
-        flags = self._buf(recv.numel())
-        check(L.dk_replay_owner_ckpt_lookup(self.rh, C.c_void_p(recv.data_ptr()), recv.numel(),
-                                            C.c_void_p(flags.data_ptr())))
-        return flags
-
-    def ckpt_apply(self, back):
-        import ctypes as C
-        check, L = self._lib()
-        back = self._in(back)
-        check(L.dk_replay_owner_ckpt_apply(self.rh, C.c_void_p(back.data_ptr())))
-
-    def cand_counts(self):
-        import ctypes as C
-        import numpy as np
-        check, L = self._lib()
-        recs, nbytes = np.zeros(self.world, np.int64), np.zeros(self.world, np.int64)
-        check(L.dk_replay_owner_cand_counts(self.rh, recs.ctypes.data_as(C.POINTER(C.c_int64)),
-                                            nbytes.ctypes.data_as(C.POINTER(C.c_int64))))
-        return recs, nbytes
-
-    def cand_pack(self, n, nbytes):
-        import ctypes as C
-        check, L = self._lib()
-        recs, keys = self._buf(n * REC_BYTES), self._buf(nbytes)
-        check(L.dk_replay_owner_cand_pack(self.rh, C.c_void_p(recs.data_ptr()), C.c_void_p(keys.data_ptr())))
-        return recs, keys
-
-    def cand_verify(self, recs, keys):
-        import ctypes as C
-        check, L = self._lib()
-        recs, keys = self._in(recs), self._in(keys)
-        n = recs.numel() // REC_BYTES
-        ans = self._buf(n)
-        check(L.dk_replay_owner_cand_verify(self.rh, C.c_void_p(recs.data_ptr()), n, C.c_void_p(keys.data_ptr()),
-                                            keys.numel(), C.c_void_p(ans.data_ptr())))
-        return ans
-
-    def cand_finish(self, back):
-        import ctypes as C
-        check, L = self._lib()
-        back = self._in(back)
-        check(L.dk_replay_owner_cand_finish(self.rh, C.c_void_p(back.data_ptr())))
+def _ptr_array(ptr, n, dtype):
+    import ctypes as C
+    import numpy as np
+    if n <= 0:
+        return np.zeros(0, dtype=dtype)
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dtype))), shape=(n,))
 
 
-class OwnerExchange:
-    """The owner-partitioned reconciliation over torch.distributed (RCCL over xGMI when `device` is
-    "cuda", gloo on the CPU): ScanBuilder.withShard(world, rank, owner=OwnerExchange(...)). Each
-    step is timed into `ms` (phase -> milliseconds of the last run)."""
+class OwnerComm:
+    """One rank's dk_comm: ScanBuilder.withShard(world, rank, owner=OwnerComm...). The scan's
+    prepare() all-reduces the commit files' batch counts through it (global_steps), run() hands the
+    replay to dk_replay_owner_run, which runs the three exchanges and their votes in the library.
+    Build with OwnerComm.rccl (RCCL over xGMI, the product), OwnerComm.over_torch (callbacks over a
+    torch.distributed group: gloo on the CPU) or OwnerComm.local (every rank in this process)."""
 
-    def __init__(self, group=None, device=None):
-        import torch
-        self.group = group
-        # "cuda" is pinned to this thread's current GPU now: global_steps runs on the scan's tail thread
-        self.device = torch.device("cuda", torch.cuda.current_device()) if device == "cuda" else device
+    def __init__(self, handle, world, rank, keep=(), steps=None):
+        self._h = handle
+        self.world, self.rank = int(world), int(rank)
+        self._keep = keep               # ctypes callbacks the library holds
+        self._steps = steps             # local ranks: the global batch counts, known up front
         self.ms = {}
         self.bytes_sent = 0
 
-    def global_steps(self, local, failed=False):
-        """Batches of every commit file (replay order): this rank's counts summed over the ranks.
-        Called from the scan's commit-tail thread. A rank whose commit-tail parse failed still takes
-        part (failed=True, its counts zero) so that no peer waits for it: every rank then raises
-        (in the reference every reader of the log sees the parse error)."""
-        import contextlib
-        import numpy as np
+    # ---- construction
+    @classmethod
+    def rccl(cls, group=None, device=None):
+        """RCCL communicator over xGMI owned by libdkgpu; the 128-byte unique id goes from the
+        group's first rank to the others over torch.distributed (a JVM host would use its own RPC)."""
+        import ctypes as C
         import torch
         import torch.distributed as dist
-        dev = self._dev()
-        v = np.concatenate([np.asarray(local, dtype=np.int64).ravel(), [1 if failed else 0]])
-        with (torch.cuda.device(dev) if dev.type == "cuda" else contextlib.nullcontext()):
-            t = torch.as_tensor(v, dtype=torch.int64).to(dev)
-            dist.all_reduce(t, group=self.group)
-            out = t.cpu().numpy()
-        if out[-1] and not failed:
-            raise OwnerPeerError("owner exchange: the commit-tail parse failed on another rank")
-        return out[:-1]
-
-    def abort(self):
-        """A rank that fails after global_steps (checkpoint open, replay setup) answers the exchange's
-        first vote with its error bit instead of running the exchange, so its peers raise too."""
-        self._any(ERR_BIT)
-
-    def _dev(self):
-        import torch
-        return torch.device(self.device) if self.device is not None else torch.device("cpu")
-
-    def _a2a(self, send, send_counts, recv_counts=None):
-        """all_to_all_single of a 1-D tensor cut into per-destination runs; recv_counts exchanged
-        first unless given. Returns (received tensor on the transport device, recv_counts)."""
-        import torch
-        import torch.distributed as dist
-        dev = self._dev()
-        send = send.to(dev)
-        sc = [int(x) for x in send_counts]
-        if recv_counts is None:
-            c = torch.tensor(sc, dtype=torch.int64, device=dev)
-            rc = torch.empty_like(c)
-            dist.all_to_all_single(rc, c, group=self.group)
-            recv_counts = [int(x) for x in rc.cpu().tolist()]
-        rcl = [int(x) for x in recv_counts]
-        recv = torch.empty(max(1, sum(rcl)), dtype=send.dtype, device=dev)[:sum(rcl)]
-        dist.all_to_all_single(recv, send, output_split_sizes=rcl, input_split_sizes=sc, group=self.group)
-        self.bytes_sent += send.numel() * send.element_size()
-        return recv, rcl
-
-    def _any(self, flag):
-        import torch
-        import torch.distributed as dist
-        t = torch.tensor([int(flag)], dtype=torch.int64, device=self._dev())
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        return int(t.item())
-
-    def _step(self, fn):
-        """Run this rank's local part of an exchange step, then vote on the MAX over ranks of the
-        error bit: a local error, or any peer's, raises on every rank at the same step (a rank that
-        raised before its next collective would leave its peers waiting in it)."""
-        box = {}
-        _, f = self._step_flag(lambda: box.__setitem__("out", fn()), {})
-        return box.get("out"), f
-
-    def __call__(self, side):
-        import time
-        t0 = time.perf_counter()
-        self.bytes_sent = 0
-        first = [True]
-        while True:
-            def pack():
-                if first:
-                    side.begin()
-                    first.clear()
-                recs_c, bytes_c = side.tail_counts()
-                return (recs_c, bytes_c) + tuple(side.tail_pack(int(recs_c.sum()), int(bytes_c.sum())))
-            (recs_c, bytes_c, recs, keys), _ = self._step(pack)
-            rrecs, rrc = self._a2a(recs, recs_c * REC_BYTES)
-            rkeys, _ = self._a2a(keys, bytes_c)
-            box = {}
-
-            def resolve():
-                box["ans"], box["flag"] = side.tail_resolve(rrecs, rkeys)
-            _, flag = self._step_flag(resolve, box)     # the collision vote carries the error bit
-            if flag & COLLISION:                 # a hash collision at some owner: all ranks reseed
-                side.reseed()
-                continue
-            back, _ = self._a2a(box["ans"], [c // REC_BYTES for c in rrc], recs_c)
-            break
-        t1 = time.perf_counter()
-
-        def run_pack():
-            side.tail_finish(back)
-            side.run()
-            c = side.ckpt_counts()
-            return c, side.ckpt_pack(int(c.sum()))
-        (c, send), _ = self._step(run_pack)
-        t2 = time.perf_counter()
-        recv, rc = self._a2a(send, c)
-        flags, _ = self._step(lambda: side.ckpt_lookup(recv))
-        back, _ = self._a2a(flags, rc, c)
-
-        def apply_pack():
-            side.ckpt_apply(back)
-            cr, cb = side.cand_counts()
-            return (cr, cb) + tuple(side.cand_pack(int(cr.sum()), int(cb.sum())))
-        (cr, cb, recs, keys), _ = self._step(apply_pack)
-        rrecs, rrc = self._a2a(recs, cr * REC_BYTES)
-        rkeys, _ = self._a2a(keys, cb)
-        ans, _ = self._step(lambda: side.cand_verify(rrecs, rkeys))
-        back, _ = self._a2a(ans, [x // REC_BYTES for x in rrc], cr)
-        side.cand_finish(back)
-        t3 = time.perf_counter()
-        self.ms = {"tail_exchange": (t1 - t0) * 1e3, "decode_hash": (t2 - t1) * 1e3, "row_exchange": (t3 - t2) * 1e3}
-
-    def _step_flag(self, fn, box):
-        """_step whose vote also carries the collision flag fn left in box["flag"]."""
-        err = None
-        try:
-            fn()
-        except BaseException as e:       # noqa: BLE001 -- re-raised after the vote
-            err = e
-        f = self._any(ERR_BIT if err is not None else int(box.get("flag", 0)))
-        if f & ERR_BIT:
-            if err is not None:
-                raise err
-            raise OwnerPeerError("owner exchange: another rank failed")
-        return None, f
-
-
-class OwnerLoopback:
-    """The owner exchange between `world` scans in ONE process (tests and single-GPU rehearsals):
-    the scans are prepared one after another (global_steps answers from the whole commit tail,
-    counted once up front), then run() drives every side's exchanges in lockstep."""
-
-    def __init__(self, global_steps):
-        import numpy as np
-        self._steps = np.asarray(global_steps, dtype=np.int64)
-        self.sides = {}
+        from ._lib import COMM_ID_BYTES, check, lib
+        single = not (dist.is_available() and dist.is_initialized())     # one rank, no process group
+        world, rank = (1, 0) if single else (dist.get_world_size(group), dist.get_rank(group))
+        uid = (C.c_uint8 * COMM_ID_BYTES)()
+        if rank == 0:
+            check(lib().dk_comm_unique_id(uid))
+        if not single:
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+            uid = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(box[0])
+        dev = torch.cuda.current_device() if device is None else int(device)
+        h = C.c_void_p()
+        check(lib().dk_comm_create(uid, world, rank, dev, C.byref(h)))
+        return cls(h, world, rank)
 
     @classmethod
-    def for_table(cls, engine, snapshot):
+    def over_torch(cls, group=None):
+        """Callback transport over a torch.distributed group, host tensors (gloo)."""
+        import ctypes as C
+        import numpy as np
+        import torch
+        import torch.distributed as dist
+        from ._lib import A2A_FN, ALLREDUCE_FN, check, dk_comm_callbacks, lib
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+
+        def a2a(_u, send, sbytes, recv, rbytes):
+            try:
+                sb = [int(sbytes[i]) for i in range(world)]
+                rb = [int(rbytes[i]) for i in range(world)]
+                st = torch.from_numpy(_ptr_array(send, sum(sb), np.uint8).copy())
+                rt = torch.empty(sum(rb), dtype=torch.uint8)
+                dist.all_to_all_single(rt, st, output_split_sizes=rb, input_split_sizes=sb, group=group)
+                if sum(rb):
+                    C.memmove(recv, rt.numpy().ctypes.data, sum(rb))
+                return 0
+            except BaseException:            # noqa: BLE001 -- reported as the callback's status
+                return 1
+
+        def allreduce(_u, vals, n, op):
+            try:
+                t = torch.from_numpy(_ptr_array(vals, n, np.int64).copy())
+                dist.all_reduce(t, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX, group=group)
+                C.memmove(vals, t.numpy().ctypes.data, 8 * n)
+                return 0
+            except BaseException:            # noqa: BLE001
+                return 1
+        cb = dk_comm_callbacks(None, A2A_FN(a2a), ALLREDUCE_FN(allreduce))
+        h = C.c_void_p()
+        check(lib().dk_comm_create_callbacks(C.byref(cb), world, rank, C.byref(h)))
+        return cls(h, world, rank, keep=(cb,))
+
+    @classmethod
+    def local(cls, world, steps=None, on_device=True):
+        """`world` ranks in this process (one thread each: run_local), exchanging through memory.
+        steps: the commit files' global batch counts (LocalOwners.for_table), as their all-reduce
+        would give them (the scans are prepared one after another)."""
+        import ctypes as C
+        from ._lib import check, lib
+        hs = (C.c_void_p * world)()
+        check(lib().dk_comm_create_local(world, 1 if on_device else 0, hs))
+        return [cls(C.c_void_p(hs[r]), world, r, steps=steps) for r in range(world)]
+
+    @staticmethod
+    def table_steps(engine, snapshot):
         """Batches of every commit file (and JSON manifest part) from one parse of the whole tail."""
         import ctypes as C
         from ._lib import check, lib
@@ -670,74 +478,177 @@ class OwnerLoopback:
         steps = (C.c_int32 * max(1, n))()
         check(lib().dk_json_tail_file_steps(t._h, steps))
         t.close()
-        return cls([steps[i] for i in range(n)])
+        return [steps[i] for i in range(n)]
+
+    # ---- the scan's calls
+    def _status(self, rc, side_error=None):
+        from ._lib import STATUS_PEER, DkError, lib
+        if rc == 0:
+            return
+        msg = lib().dk_last_error().decode("utf-8", "replace")
+        if rc == STATUS_PEER:
+            raise OwnerPeerError(msg)
+        if side_error is not None:
+            raise side_error
+        raise DkError(msg)
 
     def global_steps(self, local, failed=False):
-        return self._steps
+        """Batches of every commit file (replay order): this rank's counts summed over the ranks.
+        Called from the scan's commit-tail thread. A rank whose commit-tail parse failed still takes
+        part (failed=True, its counts zero) so that no peer waits for it: every rank then raises
+        (in the reference every reader of the log sees the parse error)."""
+        import numpy as np
+        from ._lib import lib
+        if self._steps is not None:
+            return np.asarray(self._steps, dtype=np.int64)
+        v = np.concatenate([np.asarray(local, dtype=np.int64).ravel(), [1 if failed else 0]]).astype(np.int64)
+        import ctypes as C
+        self._status(lib().dk_comm_allreduce_i64(self._h, v.ctypes.data_as(C.POINTER(C.c_int64)), len(v), 0))
+        if v[-1] and not failed:
+            raise OwnerPeerError("owner exchange: the commit-tail parse failed on another rank")
+        return v[:-1]
 
     def abort(self):
-        pass
+        """A rank that fails after global_steps (checkpoint open, replay setup) answers the owner
+        run's first vote with its error bit instead of running it, so its peers raise too."""
+        from ._lib import lib
+        if self._steps is None:
+            self._status(lib().dk_comm_abort(self._h))
 
-    def __call__(self, side):
-        self.sides[side.rank] = side       # run() drives them once every rank's side has arrived
+    def _last_run(self):
+        import ctypes as C
+        from ._lib import lib
+        ms, b = (C.c_double * 4)(), C.c_int64()
+        lib().dk_comm_last_run(self._h, ms, C.byref(b))
+        self.ms = {"tail_exchange": ms[0], "decode_hash": ms[1], "row_exchange": ms[2], "total": ms[3]}
+        self.bytes_sent = int(b.value)
 
-    @staticmethod
-    def _route(sends):
-        """sends[s] = (1-D tensor, per-destination counts) -> per destination (concatenation over
-        sources, per-source counts)."""
+    def run_scan(self, scan):
+        """The whole owner protocol of one scan run on this rank (dk_replay_owner_run)."""
+        from ._lib import lib
+        rc = lib().dk_replay_owner_run(scan._rh, self._h)
+        self._last_run()
+        self._status(rc)
+
+    def run_side(self, side):
+        """The same protocol over a Python stand-in for the device side (tests): `side` has the
+        dk_owner_side calls with CPU torch tensors (tests/test_owner.py: CpuOwnerSide)."""
+        import ctypes as C
+        from ._lib import dk_owner_side, lib
+        ad = _SideAdapter(side)
+        rc = lib().dk_owner_protocol_run(C.byref(ad.struct), self._h)
+        self._last_run()
+        self._status(rc, ad.error)
+
+    def close(self):
+        from ._lib import lib
+        if self._h:
+            lib().dk_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:                    # noqa: BLE001 -- interpreter shutdown
+            pass
+
+
+class _SideAdapter:
+    """dk_owner_side over a Python object whose calls take and return CPU torch tensors (the layout
+    of the device calls: 32-byte key records, key bytes, 8-byte row hashes, one answer byte each)."""
+
+    def __init__(self, side):
+        import ctypes as C
+        import numpy as np
         import torch
-        world = len(sends)
-        out = []
-        for d in range(world):
-            parts, counts = [], []
-            for s in range(world):
-                t, cnt = sends[s]
-                a = int(sum(cnt[:d]))
-                parts.append(t[a:a + int(cnt[d])])
-                counts.append(int(cnt[d]))
-            dev = next((p.device for p in parts if p.numel()), sends[d][0].device)
-            out.append((torch.cat([p.to(dev) for p in parts]) if parts else sends[d][0][:0], counts))
-        return out
+        from ._lib import SIDE_FNS, dk_owner_side
+        self.side, self.error = side, None
+        st = {}
 
-    def run(self, scans):
-        """Every scan's run() with this loopback as its owner, then the exchanges in lockstep."""
-        self.sides = {}
-        for sc in scans:
-            sc.run()                            # registers the side
-        sides = [self.sides[r] for r in range(len(scans))]
-        world = len(sides)
-        for s in sides:
-            s.begin()
-        while True:
-            cnts = [s.tail_counts() for s in sides]
-            packed = [s.tail_pack(int(r.sum()), int(b.sum())) for s, (r, b) in zip(sides, cnts)]
-            rrecs = self._route([(p[0], r * REC_BYTES) for p, (r, _) in zip(packed, cnts)])
-            rkeys = self._route([(p[1], b) for p, (_, b) in zip(packed, cnts)])
-            res = [sides[d].tail_resolve(rrecs[d][0], rkeys[d][0]) for d in range(world)]
-            if any(f for _, f in res):
-                for s in sides:
-                    s.reseed()
-                continue
-            back = self._route([(res[d][0], [c // REC_BYTES for c in rrecs[d][1]]) for d in range(world)])
-            for s in range(world):
-                sides[s].tail_finish(back[s][0])
-            break
-        for s in sides:
-            s.run()
-        cs = [s.ckpt_counts() for s in sides]
-        sends = [s.ckpt_pack(int(c.sum())) for s, c in zip(sides, cs)]
-        recv = self._route([(t, c) for t, c in zip(sends, cs)])
-        flags = [sides[d].ckpt_lookup(recv[d][0]) for d in range(world)]
-        back = self._route([(flags[d], recv[d][1]) for d in range(world)])
-        for s in range(world):
-            sides[s].ckpt_apply(back[s][0])
-        cc = [s.cand_counts() for s in sides]
-        packed = [s.cand_pack(int(r.sum()), int(b.sum())) for s, (r, b) in zip(sides, cc)]
-        rrecs = self._route([(p[0], r * REC_BYTES) for p, (r, _) in zip(packed, cc)])
-        rkeys = self._route([(p[1], b) for p, (_, b) in zip(packed, cc)])
-        ans = [sides[d].cand_verify(rrecs[d][0], rkeys[d][0]) for d in range(world)]
-        back = self._route([(ans[d], [c // REC_BYTES for c in rrecs[d][1]]) for d in range(world)])
-        for s in range(world):
-            sides[s].cand_finish(back[s][0])
-        for sc in scans:
-            sc.sync()
+        def guard(f):
+            def g(*a):
+                try:
+                    return int(f(*a) or 0)
+                except BaseException as e:      # noqa: BLE001 -- re-raised after the protocol returns
+                    if self.error is None:
+                        self.error = e
+                    return 1
+            return g
+
+        def put(ptr, t):
+            t = t.contiguous().view(torch.uint8).numpy() if isinstance(t, torch.Tensor) else np.asarray(t)
+            if t.nbytes:
+                C.memmove(ptr, t.ctypes.data, t.nbytes)
+
+        def u8(ptr, n):
+            return torch.from_numpy(_ptr_array(ptr, n, np.uint8).copy())
+
+        def counts2(ptr_a, ptr_b, key, fn):
+            a, b = fn()
+            st[key] = (int(np.sum(a)), int(np.sum(b)))
+            for i in range(len(a)):
+                ptr_a[i], ptr_b[i] = int(a[i]), int(b[i])
+
+        def tail_pack(_u, recs, keys):
+            r, k = side.tail_pack(*st["tail"])
+            put(recs, r); put(keys, k)
+
+        def tail_resolve(_u, recs, n, keys, nb, ans, flags):
+            a, f = side.tail_resolve(u8(recs, n * REC_BYTES), u8(keys, nb))
+            put(ans, a.to(torch.uint8))
+            flags[0] = int(f)
+
+        def ckpt_counts(_u, c):
+            v = side.ckpt_counts()
+            st["ckpt"] = int(np.sum(v))
+            for i in range(len(v)):
+                c[i] = int(v[i])
+
+        def cand_pack(_u, recs, keys):
+            r, k = side.cand_pack(*st["cand"])
+            put(recs, r); put(keys, k)
+
+        impl = {
+            "begin": lambda _u: side.begin(),
+            "tail_counts": lambda _u, a, b: counts2(a, b, "tail", side.tail_counts),
+            "tail_pack": tail_pack,
+            "tail_resolve": tail_resolve,
+            "reseed": lambda _u: side.reseed(),
+            "tail_finish": lambda _u, back: side.tail_finish(u8(back, st["tail"][0])),
+            "run": lambda _u: side.run(),
+            "ckpt_counts": ckpt_counts,
+            "ckpt_pack": lambda _u, send: put(send, side.ckpt_pack(st["ckpt"])),
+            "ckpt_lookup": lambda _u, recv, n, flags: put(flags, side.ckpt_lookup(
+                torch.from_numpy(_ptr_array(recv, n, np.int64).copy())).to(torch.uint8)),
+            "ckpt_apply": lambda _u, back: side.ckpt_apply(u8(back, st["ckpt"])),
+            "cand_counts": lambda _u, a, b: counts2(a, b, "cand", side.cand_counts),
+            "cand_pack": cand_pack,
+            "cand_verify": lambda _u, recs, n, keys, nb, ans: put(ans, side.cand_verify(
+                u8(recs, n * REC_BYTES), u8(keys, nb)).to(torch.uint8)),
+            "cand_finish": lambda _u, back: side.cand_finish(u8(back, st["cand"][0])),
+        }
+        self._fns = [ftype(guard(impl[name])) for name, ftype in SIDE_FNS]
+        self.struct = dk_owner_side(None, 0, *self._fns)
+
+
+def run_local(scans):
+    """Every scan's run() (each with its OwnerComm.local rank) on its own thread, then sync():
+    the ranks of one process exchange through the library's in-process transport."""
+    import threading
+    errs = [None] * len(scans)
+
+    def go(i):
+        try:
+            scans[i].run()
+        except BaseException as e:           # noqa: BLE001 -- re-raised below
+            errs[i] = e
+    ts = [threading.Thread(target=go, args=(i,), daemon=True) for i in range(len(scans))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    for sc in scans:
+        sc.sync()

@@ -465,6 +465,75 @@ int  dk_replay_owner_cand_pack(dk_replay* r, void* recs, void* keys);
 int  dk_replay_owner_cand_verify(dk_replay* r, const void* recs, int64_t n, const void* keys, int64_t nbytes,
                                  uint8_t* answers);
 int  dk_replay_owner_cand_finish(dk_replay* r, const uint8_t* back);
+
+/* ---- Collectives of the multi-GPU owner exchange, owned by the library (delta_amd/csrc/dk_comm.cpp).
+ * Kernel's Engine has no collective hook (KA/engine/Engine.java:30-64), so a JVM GpuScan cannot bring
+ * one: rank 0 makes an RCCL unique id (dk_comm_unique_id), the host hands its 128 bytes to every rank by
+ * any means (the JVM's own RPC, a shared file), each rank creates its communicator over xGMI
+ * (dk_comm_create) and runs the whole owner protocol of a scan in ONE call, dk_replay_owner_run (the
+ * repartition by path of spark/src/main/scala/org/apache/spark/sql/delta/Snapshot.scala:476-485, the
+ * 14 dk_replay_owner_* steps above with their collectives: 11 per run). Every step carries a vote: a
+ * rank whose local part fails returns its error, every peer returns DK_STATUS_PEER at the same step,
+ * and no rank waits in a collective for a failed one. A rank that fails after the commit-tail
+ * batch-count all-reduce but before its dk_replay_owner_run (e.g. its checkpoint open) calls
+ * dk_comm_abort instead, which answers the run's first vote.
+ * Other transports: dk_comm_create_callbacks (the caller's all-to-all / all-reduce over host memory:
+ * tests over gloo, a host with its own transport) and dk_comm_create_local (`world` communicators of
+ * one process, one thread per rank: one-GPU rehearsals). */
+typedef struct dk_comm dk_comm;
+#define DK_COMM_ID_BYTES 128
+#define DK_STATUS_PEER 6            /* another rank of the collective failed at this step */
+typedef struct dk_comm_callbacks {
+  void* user;
+  /* all-to-all of byte runs in host memory: send holds send_bytes[p] bytes for each rank p in rank
+   * order; recv receives recv_bytes[p] bytes from each rank p in rank order. 0 = OK. */
+  int (*alltoallv)(void* user, const void* send, const int64_t* send_bytes, void* recv, const int64_t* recv_bytes);
+  /* element-wise reduction of vals[0..n) over the ranks, in place: op 0 = sum, 1 = max. 0 = OK. */
+  int (*allreduce_i64)(void* user, int64_t* vals, int32_t n, int32_t op);
+} dk_comm_callbacks;
+int  dk_comm_unique_id(uint8_t id[DK_COMM_ID_BYTES]);
+int  dk_comm_create(const uint8_t id[DK_COMM_ID_BYTES], int32_t world, int32_t rank, int32_t device, dk_comm** out);
+int  dk_comm_create_callbacks(const dk_comm_callbacks* cb, int32_t world, int32_t rank, dk_comm** out);
+int  dk_comm_create_local(int32_t world, int32_t on_device, dk_comm** comms /* [world] */);
+int32_t dk_comm_world(const dk_comm* c);
+int32_t dk_comm_rank(const dk_comm* c);
+/* host values; op 0 = sum, 1 = max (the commit tail's global batch counts: dk_json_tail_file_steps) */
+int  dk_comm_allreduce_i64(dk_comm* c, int64_t* vals, int32_t n, int32_t op);
+int  dk_comm_alltoallv(dk_comm* c, const void* send, const int64_t* send_bytes, void* recv, const int64_t* recv_bytes,
+                       int32_t on_device);
+int  dk_comm_abort(dk_comm* c);
+/* the last owner run: ms[0] commit-tail exchange, ms[1] decode + row hashes, ms[2] row and candidate
+ * exchanges, ms[3] total; payload bytes this rank sent to its peers */
+int  dk_comm_last_run(const dk_comm* c, double ms[4], int64_t* bytes_sent);
+void dk_comm_destroy(dk_comm* c);
+/* dk_replay_set_owner(r, world, rank) first (world = dk_comm_world), the commit tail rebased with the
+ * all-reduced batch counts; then this call; then dk_replay_sync as usual. */
+int  dk_replay_owner_run(dk_replay* r, dk_comm* c);
+/* The same protocol over a caller's stand-in for the device side (tests of the protocol without a GPU;
+ * each member mirrors the dk_replay_owner_* call of the same name; buffers in host memory unless
+ * device_buffers). */
+typedef struct dk_owner_side {
+  void* user;
+  int32_t device_buffers;
+  int (*begin)(void* user);
+  int (*tail_counts)(void* user, int64_t* recs, int64_t* bytes);
+  int (*tail_pack)(void* user, void* recs, void* keys);
+  int (*tail_resolve)(void* user, const void* recs, int64_t n, const void* keys, int64_t nbytes, uint8_t* answers,
+                      int32_t* flags);
+  int (*reseed)(void* user);
+  int (*tail_finish)(void* user, const uint8_t* back);
+  int (*run)(void* user);
+  int (*ckpt_counts)(void* user, int64_t* counts);
+  int (*ckpt_pack)(void* user, uint64_t* send);
+  int (*ckpt_lookup)(void* user, const uint64_t* recv, int64_t n, uint8_t* flags);
+  int (*ckpt_apply)(void* user, const uint8_t* back);
+  int (*cand_counts)(void* user, int64_t* recs, int64_t* bytes);
+  int (*cand_pack)(void* user, void* recs, void* keys);
+  int (*cand_verify)(void* user, const void* recs, int64_t n, const void* keys, int64_t nbytes, uint8_t* answers);
+  int (*cand_finish)(void* user, const uint8_t* back);
+} dk_owner_side;
+int  dk_owner_protocol_run(const dk_owner_side* side, dk_comm* c);
+
 /* Checkpoint Parquet writer (Table.checkpoint's ParquetHandler.writeParquetFileAtomically,
  * DefaultParquetHandler.java:110-163): CHECKPOINT_SCHEMA (SingleAction.java:30-37), encoded on the
  * device. Rows come in iterator order as row groups: action rows built by the caller as JSON lines

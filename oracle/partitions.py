@@ -220,6 +220,12 @@ def evaluate(node, pv, fields):
         if ei < si:
             raise PartitionValueError("begin %d, end %d" % (si, ei))   # String.substring throws
         return s[si:ei].encode("utf-8")
+    if n == "TIMEADD":                                         # DefaultExpressionEvaluator.java:593-626
+        a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
+        if a is None or b is None:
+            return None
+        v = (a + ((b * 1000 + 2 ** 63) % 2 ** 64 - 2 ** 63)) % 2 ** 64          # Java long arithmetic
+        return v - 2 ** 64 if v >= 2 ** 63 else v
     if n in ("AND", "OR"):
         a, b = evaluate(c[0], pv, fields), evaluate(c[1], pv, fields)
         if n == "AND":
@@ -268,6 +274,8 @@ def _type(node, fields):
     kind = type(node).__name__
     if kind == "Predicate" and node.name.upper() == "SUBSTRING":
         return "string"
+    if kind == "Predicate" and node.name.upper() == "TIMEADD":
+        return _type(node.children[0], fields)
     if kind == "Column":
         return fields[node.names[0].lower()][0]
     if kind == "Literal":

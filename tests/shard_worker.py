@@ -22,11 +22,13 @@ def main():
     eng = K.GpuEngine()
     snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
     mode = sys.argv[3] if len(sys.argv) > 3 else "allgather"
-    if mode == "owner_fail":     # a malformed commit only rank 1 parses: every rank must raise, none hang
-        scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerExchange()).build()
+    if mode in ("owner_fail", "owner_prefetch_fail"):
+        # owner_fail: a malformed commit only rank 1 parses; owner_prefetch_fail: rank 1's add.size
+        # prefetch fails between its prepare and its owner run (DK_INJECT_PREFETCH_FAULT=1). Every
+        # rank must raise, none hang.
+        scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerComm.over_torch()).build()
         try:
-            scan.prepare(eng)
-            scan.run()
+            list(scan.getScanFiles(eng))
             res = {"error": None}
         except Exception as e:      # noqa: BLE001
             res = {"error": type(e).__name__, "msg": str(e)[:300]}
@@ -37,7 +39,7 @@ def main():
         dist.destroy_process_group()
         return
     if mode == "owner":      # owner-partitioned: every rank's counters are its share of the world's
-        scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerExchange()).build()
+        scan = snap.getScanBuilder().withShard(world, rank, owner=shard.OwnerComm.over_torch()).build()
     else:
         scan = snap.getScanBuilder().withShard(world, rank, exchange=shard.exchange_hash_owner if mode == "alltoall"
                                                else None).build()

@@ -1,18 +1,22 @@
-"""Owner-partitioned reconciliation, the multi-GPU "owner" mode (delta_amd/shard.py: OwnerExchange,
-OwnerSide, OwnerLoopback; dk_replay_owner_*).
+"""Owner-partitioned reconciliation, the multi-GPU "owner" mode (the protocol and its collectives in
+libdkgpu: dk_replay_owner_run / dk_owner_protocol_run over a dk_comm, delta_amd/csrc/dk_comm.cpp;
+delta_amd/shard.py: OwnerComm).
 
 Each rank parses only the commit files j = rank (mod world) and decodes only its row groups of the
 checkpoint; the key (URI(path), dvUniqueId) with hash h is owned by rank h mod world, which resolves
 the commit-tail actions routed to it (R2-R5, App. A) and answers every rank's checkpoint rows for its
 keys, first by hash, then byte-exactly.
 
-CPU: gloo worlds 2 and 3 drive the product's OwnerExchange (global batch steps, three all-to-all
-exchanges, the collision vote) over a CPU stand-in for the device side (CpuOwnerSide: the oracle's
-JSON decode and canonical keys, the same record layout, the owner rules restated), reassembled
-against the unsharded oracle replay. A forced collision round checks the reseed vote.
-GPU: the product's owner mode for 2 and 3 ranks simulated in one process (OwnerLoopback) equals the
-oracle -- rows in the reference order, counters -- including DV swaps, checkpoint removes, JSON
-batch boundaries inside a commit (R5) and a data-skipping filter.
+CPU: gloo worlds 2 and 3 drive the library's protocol (dk_owner_protocol_run: global batch steps,
+three all-to-all exchanges, the votes) through the callback transport (dk_comm_create_callbacks over
+gloo) over a CPU stand-in for the device side (CpuOwnerSide: the oracle's JSON decode and canonical
+keys, the same record layout, the owner rules restated), reassembled against the unsharded oracle
+replay; a forced collision round checks the reseed vote; the in-process transport
+(dk_comm_create_local) does the same with one thread per rank.
+GPU: the product's owner mode (dk_replay_owner_run) for 2 and 3 ranks in one process over the
+in-process transport equals the oracle -- rows in the reference order, counters -- including DV
+swaps, checkpoint removes, JSON batch boundaries inside a commit (R5) and a data-skipping filter; a
+one-rank RCCL communicator created through the C ABI does too.
 """
 import hashlib
 import json
@@ -244,9 +248,9 @@ def _gloo_worker(rank, world, port, table, out_path, bs, collide):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     try:
-        ex = shard.OwnerExchange()
+        ex = shard.OwnerComm.over_torch()
         side = CpuOwnerSide(table, world, rank, ex, bs=bs, collide_first=collide)
-        ex(side)
+        ex.run_side(side)
         units = []
         for f, r0, n in side.units:
             bits = np.array([side.sel[(f, r)] for r in range(r0, r0 + n)], bool)
@@ -285,14 +289,14 @@ def _gloo_fail_worker(rank, world, port, table, out_path, fail):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     try:
-        ex = shard.OwnerExchange()
+        ex = shard.OwnerComm.over_torch()
         err = None
         try:
             side = CpuOwnerSide(table, world, rank, ex, fail=fail if rank == world - 1 else None)
             if fail == "open" and rank == world - 1:
                 ex.abort()                       # failed after global_steps (checkpoint open)
                 raise ValueError("open failed")
-            ex(side)
+            ex.run_side(side)
         except Exception as e:                   # noqa: BLE001
             err = type(e).__name__
         with open(out_path + ".%d" % rank, "w") as f:
@@ -343,7 +347,7 @@ def _loopback_check(table, world, bs, predicate):
     from oracle import ref
     eng = K.GpuEngine(json_batch_size=bs)
     snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
-    lb = shard.OwnerLoopback.for_table(eng, snap)
+    comms = shard.OwnerComm.local(world, steps=shard.OwnerComm.table_steps(eng, snap))
     scans = []
     for r in range(world):
         snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
@@ -354,7 +358,7 @@ def _loopback_check(table, world, bs, predicate):
             sb = sb.withFilter(Predicate(">", Column("id"), Literal.ofLong(predicate)))
             from tests.test_skipping import oracle_skipping
             skipping = oracle_skipping(table, Predicate(">", Column("id"), Literal.ofLong(predicate)))
-        sc = sb.withShard(world, r, owner=lb).build()
+        sc = sb.withShard(world, r, owner=comms[r]).build()
         sc.prepare(eng)
         scans.append(sc)
     full = ref.replay(table, json_batch_size=bs, with_stats=bool(predicate), skipping=skipping)
@@ -362,7 +366,7 @@ def _loopback_check(table, world, bs, predicate):
     for sc in scans:                              # no rank parsed more than its share of the commits
         assert len(sc.tail_commits) <= -(-n_commits // world), (len(sc.tail_commits), n_commits)
     for step in range(2):                         # a second run reuses the replays
-        lb.run(scans)
+        shard.run_local(scans)
         counters = np.zeros(5, np.int64)
         tail, files = [], {}
         for sc in scans:
@@ -383,6 +387,8 @@ def _loopback_check(table, world, bs, predicate):
         assert rows == want, (step, len(rows), len(want))
     for sc in scans:
         sc.close()
+    for c in comms:
+        c.close()
     eng.close()
     print("ok")
 
@@ -396,11 +402,92 @@ def _loopback_check(table, world, bs, predicate):
 def test_gpu_owner_loopback(tmp_path, world, bs, spec, predicate):
     """The product's owner mode (tail records routed and resolved by their owners, every checkpoint
     row's key hash routed, candidates verified byte-exactly on the device) for `world` ranks in one
-    process: merged rows (reference order) and counters equal the oracle's."""
+    process, each rank's dk_replay_owner_run on its own thread over the in-process transport: merged
+    rows (reference order) and counters equal the oracle's."""
     synth.write_table(str(tmp_path), synth.TableSpec(n_adds=20_000, n_commits=9, adds_per_commit=30,
                                                      removes_per_commit=30, **spec))
     root = os.path.dirname(HERE)
     code = ("import sys; sys.path.insert(0, %r); from tests.test_owner import _loopback_check; "
             "_loopback_check(%r, %d, %d, %r)" % (root, str(tmp_path), world, bs, predicate))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
+
+
+def _local_worker(rank, world, comms, table, bs, results):
+    try:
+        side = CpuOwnerSide(table, world, rank, comms[rank], bs=bs)
+        comms[rank].run_side(side)
+        results[rank] = side
+    except BaseException as e:               # noqa: BLE001 -- reported by the test
+        results[rank] = e
+
+
+@pytest.mark.parametrize("world,bs", [(3, 5)])
+def test_local_transport_owner_protocol(tmp_path, world, bs):
+    """The library's in-process transport (dk_comm_create_local, host buffers), one thread per rank,
+    drives the protocol over the CPU stand-in: the merged counters and checkpoint selections equal
+    the unsharded oracle's."""
+    import threading
+    from oracle import ref
+    table = str(tmp_path / "t")
+    synth.write_table(table, synth.TableSpec(n_adds=3_000, n_parts=2, row_group_size=700, n_commits=6,
+                                             adds_per_commit=15, removes_per_commit=15, dv_frac=0.2, readd_frac=0.2))
+    seg = ref.load_log_segment(table)
+    commits = [f for f in seg.all_files_reversed() if f.kind == "commit"]
+    steps = [len(list(ref.read_json_batches(c.path, bs))) for c in commits]
+    comms = shard.OwnerComm.local(world, steps=steps, on_device=False)
+    results = [None] * world
+    ts = [threading.Thread(target=_local_worker, args=(r, world, comms, table, bs, results)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert all(isinstance(x, CpuOwnerSide) for x in results), results
+    full = results[0].full
+    counters = np.sum([x.counters for x in results], axis=0)
+    assert tuple(int(c) for c in counters) == full.counters.as_tuple()
+    sel = {}
+    for x in results:
+        sel.update(x.sel)
+    for b in full.checkpoint:
+        got = np.array([sel[(b.file_index, r)] for r in range(len(b.selected))], bool)
+        assert np.array_equal(got, b.selected.astype(bool))
+    assert all(c.bytes_sent > 0 for c in comms)
+    for c in comms:
+        c.close()
+
+
+def _rccl_world1_check(table):
+    """Body of test_gpu_rccl_world1: one RCCL rank created through the C ABI (dk_comm_unique_id +
+    dk_comm_create, no torch.distributed) runs the owner protocol of a whole scan."""
+    import torch
+    torch.cuda.init()
+    from delta_amd import kernel as K
+    from oracle import ref
+    eng = K.GpuEngine()
+    snap = K.Table.forPath(eng, table).getLatestSnapshot(eng)
+    comm = shard.OwnerComm.rccl()
+    sc = snap.getScanBuilder().withShard(1, 0, owner=comm).build()
+    batches = list(sc.getScanFiles(eng))
+    full = ref.replay(table)
+    rows = [ref.canon_add_from_cols(b.data, int(i)) + (b.table_root,) for b in batches for i in b.selected_rows()]
+    assert sc.metrics.as_tuple() == full.counters.as_tuple(), (sc.metrics.as_tuple(), full.counters.as_tuple())
+    assert rows == full.scan_files(), (len(rows), len(full.scan_files()))
+    assert comm.ms["total"] > 0
+    sc.close()
+    comm.close()
+    eng.close()
+    print("ok")
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_world1(tmp_path):
+    """A one-rank RCCL communicator owned by libdkgpu (the path a JVM GpuScan takes: unique id in,
+    dk_replay_owner_run) gives the oracle's scan files and counters."""
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=20_000, n_parts=2, row_group_size=4000, n_commits=6,
+                                                     adds_per_commit=30, removes_per_commit=30, dv_frac=0.2))
+    root = os.path.dirname(HERE)
+    code = ("import sys; sys.path.insert(0, %r); from tests.test_owner import _rccl_world1_check; "
+            "_rccl_world1_check(%r)" % (root, str(tmp_path)))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]

@@ -75,8 +75,9 @@ def test_partition_fields_and_compile():
         _describe(Predicate("STARTS_WITH", col("p"), Literal.ofString("1")), f)
     with pytest.raises(sk.UnsupportedExpression, match="single character"):
         _describe(Predicate("LIKE", col("s"), Literal.ofString("a%"), Literal.ofString("ab")), f)
-    with pytest.raises(pp.UnsupportedPartitionFilter):
-        _describe(Predicate("LIKE", col("s"), col("s")), f)
+    # a per-row LIKE pattern compiles to the device's dynamic LIKE (PO_LIKE_DYN = 21, escape in arg)
+    d = _describe(Predicate("LIKE", col("s"), col("s")), f)
+    assert [o[0] for o in d["ops"]] == [PO_FIELD, PO_FIELD, 21] and d["ops"][2][1] == ord("\\")
 
 
 (PO_FIELD, PO_LIT_INT, PO_LIT_STR, PO_LIT_NULL, PO_LT, PO_LE, PO_GT, PO_GE, PO_EQ, PO_NSEQ, PO_ISNULL,

@@ -270,25 +270,30 @@ def test_gpu_two_processes_gloo(tmp_path, mode):
 
 
 @pytest.mark.gpu
-def test_gpu_owner_failure_reaches_every_rank(tmp_path):
-    """Owner mode over gloo, two GPU processes: a malformed commit file that only rank 1 parses
-    (j = 1 of the newest-first replay order) fails rank 1's commit-tail parse; rank 0 must raise
-    too (at the global-steps vote) instead of waiting for rank 1 in a collective."""
+@pytest.mark.parametrize("mode", ["owner_fail", "owner_prefetch_fail"])
+def test_gpu_owner_failure_reaches_every_rank(tmp_path, mode):
+    """Owner mode over gloo (the library's protocol through the callback transport), two GPU
+    processes. owner_fail: a malformed commit file that only rank 1 parses (j = 1 of the newest-first
+    replay order) fails rank 1's commit-tail parse; rank 0 must raise too (at the global-steps vote).
+    owner_prefetch_fail: rank 1 fails after its prepare, before its owner run (the add.size
+    prefetch); it answers the run's first vote with its error bit and rank 0 raises there. No rank
+    waits for the other in a collective."""
     import json
     import subprocess
     import sys
     table = str(tmp_path / "t")
     synth.write_table(table, synth.TableSpec(n_adds=8_000, n_parts=2, row_group_size=2000, n_commits=4))
-    log = os.path.join(table, "_delta_log")
-    commits = sorted(f for f in os.listdir(log) if f.endswith(".json"))
-    with open(os.path.join(log, commits[-2]), "a") as f:    # second newest: replay index 1 -> rank 1
-        f.write('{"add": {"path": \n')
+    if mode == "owner_fail":
+        log = os.path.join(table, "_delta_log")
+        commits = sorted(f for f in os.listdir(log) if f.endswith(".json"))
+        with open(os.path.join(log, commits[-2]), "a") as f:    # second newest: replay index 1 -> rank 1
+            f.write('{"add": {"path": \n')
     port = _free_port()
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "shard_worker.py")
     out = str(tmp_path / "res.json")
-    procs = [subprocess.Popen([sys.executable, worker, table, out, "owner_fail"],
+    procs = [subprocess.Popen([sys.executable, worker, table, out, mode],
                               env=dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
-                                       MASTER_PORT=str(port)))
+                                       MASTER_PORT=str(port), DK_INJECT_PREFETCH_FAULT="1"))
              for r in range(2)]
     for p in procs:
         assert p.wait(timeout=300) == 0

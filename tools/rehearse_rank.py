@@ -1,15 +1,18 @@
 """One-GPU rehearsal of one rank of the N-GPU owner-partitioned scan (bench.py --gpus N, the default
 exchange=owner), for the timing of the path the driver's 8-GPU run measures.
 
-All N ranks' scans run in this process on one GPU (shard.OwnerLoopback routes the exchanges' buffers
-between them on the device): each rank opens only its contiguous run of row groups (asynchronous open)
-and parses only its commit files j = rank (mod N). Every rank is timed on its own:
+All N ranks' scans run in this process on one GPU: each rank opens only its contiguous run of row
+groups (asynchronous open) and parses only its commit files j = rank (mod N); then every rank's
+dk_replay_owner_run runs on its own thread over the library's in-process transport
+(dk_comm_create_local: the same protocol and votes as over RCCL, buffers copied device to device).
+Every rank is timed:
 
   open       prepare (footers, page headers, the commit-tail parse of its files + replay create)
              until its asynchronous open has finished decoding (the ranks run one after another, so
              each rank's H2D and decode have the GPU to themselves, as on its own GPU)
-  exchange   each of its owner-exchange calls (tail resolve, checkpoint hash routing / lookup /
-             candidates), device-synchronised, summed
+  exchange   its owner run's commit-tail exchange + row / candidate exchanges (dk_comm_last_run),
+             with all N ranks' exchange kernels sharing this one GPU at the same time (an upper
+             bound of a rank's own)
   transfer   the bytes it sends through the all-to-alls at an assumed per-GPU all-to-all bandwidth
              (--a2a-gbs, default 300 GB/s: 7 xGMI links at ~43 GB/s each) + 30 us per collective
   consume    its scan-file batches consumed as bench.py's JMH-shaped consumer does (sum of add.size
@@ -58,58 +61,19 @@ def main():
     from delta_amd import shard
     from delta_amd._lib import check, lib
 
-    class Timed:
-        """An OwnerSide whose calls are timed (each returns with the device synchronised)."""
-
-        def __init__(self, side, clock):
-            self.side, self.clock = side, clock
-            self.rank = side.rank
-
-        def __getattr__(self, name):
-            f = getattr(self.side, name)
-            if not callable(f):
-                return f
-
-            def call(*a, **k):
-                torch.cuda.synchronize()
-                t = time.perf_counter()
-                out = f(*a, **k)
-                torch.cuda.synchronize()
-                self.clock[name] = self.clock.get(name, 0.0) + (time.perf_counter() - t) * 1e3
-                return out
-            return call
-
-    class TimedLoopback(shard.OwnerLoopback):
-        def __init__(self, steps):
-            super().__init__(steps)
-            self.clocks = {}
-            self.sent = {}
-            self.collectives = 0
-
-        def __call__(self, side):
-            self.sides[side.rank] = Timed(side, self.clocks.setdefault(side.rank, {}))
-
-        def _route(self, sends):
-            self.collectives += 1
-            for s, (t, cnt) in enumerate(sends):
-                own = int(sum(cnt[:s])), int(cnt[s]) if s < len(cnt) else 0
-                nbytes = t.numel() * t.element_size()
-                per = t.element_size() if t.numel() else 0
-                self.sent[s] = self.sent.get(s, 0) + nbytes - own[1] * per   # bytes leaving rank s
-            return super()._route(sends)
-
     world = args.world
     eng = K.GpuEngine(timing=False)
     snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
-    steps = shard.OwnerLoopback.for_table(eng, snap)._steps
+    steps = shard.OwnerComm.table_steps(eng, snap)
+    comms = shard.OwnerComm.local(world, steps=steps)
+    collectives = 11                            # per owner run (delta_amd/csrc/dk_comm.cpp)
     # iteration 0 warms the caching allocators (every rank's blocks, as each rank's process is warm
     # after bench.py's warm-up steps); iteration 1 is reported
     for it in range(2):
-        lb = TimedLoopback(steps)
         scans, opened = [], {}
         for r in range(world):
             s = K.Table.forPath(eng, work).getLatestSnapshot(eng)
-            sc = s.getScanBuilder().withStats(cfg["stats"]).withShard(world, r, owner=lb).build()
+            sc = s.getScanBuilder().withStats(cfg["stats"]).withShard(world, r, owner=comms[r]).build()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             sc.prepare(eng)
@@ -128,7 +92,10 @@ def main():
             for leaf in sc.PREFETCH_LEAVES:
                 if leaf in sc.ckpt.leaves:
                     check(lib().dk_replay_prefetch_leaf(sc._rh, leaf.encode()))
-        lb.run(scans)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        shard.run_local(scans)
+        run_ms = (time.perf_counter() - t0) * 1e3
         counters = np.zeros(5, np.int64)
         consume = {}
         for r, sc in enumerate(scans):
@@ -151,22 +118,27 @@ def main():
                 sc.close()
     per_rank = {}
     for r in range(world):
-        ex = sum(lb.clocks.get(r, {}).values())
-        tr = lb.sent.get(r, 0) / (args.a2a_gbs * 1e9) * 1e3 + lb.collectives * 0.03
-        per_rank[r] = dict(opened[r], exchange_ms=round(ex, 3), exchange_calls_ms={k: round(v, 3) for k, v in lb.clocks.get(r, {}).items()},
-                           bytes_sent=lb.sent.get(r, 0), transfer_model_ms=round(tr, 3),
+        m = comms[r].ms
+        ex = m["tail_exchange"] + m["row_exchange"]
+        tr = comms[r].bytes_sent / (args.a2a_gbs * 1e9) * 1e3 + collectives * 0.03
+        per_rank[r] = dict(opened[r], exchange_ms=round(ex, 3), owner_run_ms={k: round(v, 3) for k, v in m.items()},
+                           bytes_sent=comms[r].bytes_sent, transfer_model_ms=round(tr, 3),
                            consume_ms=round(consume[r][0], 3), selected=consume[r][1],
                            per_rank_ms=round(opened[r]["open_ms"] + ex + tr + consume[r][0], 2))
     step = max(v["per_rank_ms"] for v in per_rank.values())
     seen = int(counters[0])
     out = {"world": world, "config": args.config, "rows": rows, "counters": [int(x) for x in counters],
            "rehearsed_step_ms": round(step, 2), "rehearsed_actions_per_s": seen / (step * 1e-3),
-           "collectives_per_run": lb.collectives, "a2a_gbs_assumed": args.a2a_gbs, "per_rank": per_rank,
+           "collectives_per_run": collectives, "a2a_gbs_assumed": args.a2a_gbs, "per_rank": per_rank,
+           "all_ranks_owner_run_ms": round(run_ms, 3),
            "note": "one process, one GPU, caches warmed by a first iteration: each rank's open ran alone "
-                   "(its own H2D and decode), exchanges through device-side loopback; transfer time modelled "
-                   "from the bytes each rank sends"}
+                   "(its own H2D and decode); every rank's dk_replay_owner_run concurrently on its own thread "
+                   "over the in-process transport (all ranks' exchange kernels share the GPU); transfer time "
+                   "modelled from the bytes each rank sends"}
     for sc in scans:
         sc.close()
+    for c in comms:
+        c.close()
     plain = snap.getScanBuilder().withStats(cfg["stats"]).build()      # the unsharded scan's counters
     for _ in plain.getScanFiles(eng):
         pass
