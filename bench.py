@@ -690,8 +690,11 @@ def main(argv=None):
     t0 = time.perf_counter()
     seen_tot = sel_tot = size_tot = 0
     phase_sum = {}
+    step_ms = []                                    # each timed step's wall time (this rank)
     for _ in range(args.steps):
+        ts = time.perf_counter()
         seen, n_sel, size_sum, phases = e2e_step()
+        step_ms.append((time.perf_counter() - ts) * 1e3)
         seen_tot += seen
         sel_tot += n_sel
         size_tot += size_sum
@@ -798,6 +801,11 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
+        # the spread of the timed steps (rank 0's clock): a step must not depend on the previous
+        # step's teardown (the pinned staging ring, no per-open pinning)
+        "step_ms_p50": round(float(np.percentile(step_ms, 50)), 3) if step_ms else None,
+        "step_ms_p90": round(float(np.percentile(step_ms, 90)), 3) if step_ms else None,
+        "step_ms_min_max": [round(min(step_ms), 3), round(max(step_ms), 3)] if step_ms else None,
         "higher_is_better": True,
         "scaling": "strong" if cfg["shared"] else "weak",
         "vs_baseline": None,

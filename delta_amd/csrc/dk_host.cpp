@@ -165,28 +165,39 @@ extern "C" void dk_engine_destroy(dk_engine* e) {
 // background thread -- host tables, events, blocks back to the caches -- so that close returns at
 // once. A cache lookup that misses waits for pending releases before allocating afresh (the next
 // scan's blocks are usually the ones being released), and dk_engine_destroy / process exit wait for
-// all of them.
+// all of them. Jobs are numbered: the threads of an open wait only for the jobs submitted before the
+// open started (a later job may be the close that joins this very open; older ones never wait for
+// it), so no wait needs a time limit.
 struct Reaper {
   std::mutex mu;
   std::condition_variable cv;
   int pending = 0;
+  uint64_t next_id = 0;
+  std::vector<uint64_t> live;          // ids of the jobs still running
   void run(std::function<void()> f) {
+    uint64_t id;
     {
       std::lock_guard<std::mutex> g(mu);
       if (pending++ == 0 && !registered) { registered = true; std::atexit([] { reaper_drain(); }); }
+      id = next_id++;
+      live.push_back(id);
     }
-    std::thread([this, f] {
+    std::thread([this, f, id] {
       f();
       std::lock_guard<std::mutex> g(mu);
+      live.erase(std::find(live.begin(), live.end(), id));
       if (--pending == 0) cv.notify_all();
+      else cv.notify_all();
     }).detach();
   }
-  bool busy() { std::lock_guard<std::mutex> g(mu); return pending > 0; }
-  void drain() { std::unique_lock<std::mutex> lk(mu); cv.wait(lk, [&] { return pending == 0; }); }
-  bool drain_for(int ms) {
-    std::unique_lock<std::mutex> lk(mu);
-    return cv.wait_for(lk, std::chrono::milliseconds(ms), [&] { return pending == 0; });
+  uint64_t ticket() { std::lock_guard<std::mutex> g(mu); return next_id; }
+  bool oldest_below(uint64_t t) {      // (mu held) a job submitted before ticket t is still running
+    for (uint64_t id : live) if (id < t) return true;
+    return false;
   }
+  bool busy_before(uint64_t t) { std::lock_guard<std::mutex> g(mu); return oldest_below(t); }
+  void drain_before(uint64_t t) { std::unique_lock<std::mutex> lk(mu); cv.wait(lk, [&] { return !oldest_below(t); }); }
+  void drain() { std::unique_lock<std::mutex> lk(mu); cv.wait(lk, [&] { return pending == 0; }); }
   bool registered = false;
   static void reaper_drain();
 };
@@ -195,12 +206,10 @@ void Reaper::reaper_drain() { reaper().drain(); }
 static void reaper_drain_all() { reaper().drain(); }
 
 static thread_local int t_synced = 0;
-// Set on the threads of an open (the opener, its image reader and their parallel_for workers): a
-// pending release may be a dk_parquet_close whose reaper job joins that very open, so a cache miss
-// there must never wait for the reaper (it allocates afresh instead).
-static thread_local int t_no_drain = 0;
-static thread_local int t_drain_budget_ms = 0;   // bounded wait left to such a thread (ms)
-constexpr int kOpenDrainMs = 40;
+// The reaper ticket of the open a thread works for (the opener, its image reader and their
+// parallel_for workers): a cache miss there waits only for releases submitted before that open
+// started. Other threads wait for every pending release (UINT64_MAX).
+static thread_local uint64_t t_open_ticket = UINT64_MAX;
 struct SyncedRelease {
   SyncedRelease() { t_synced++; }
   ~SyncedRelease() { t_synced--; }
@@ -212,7 +221,8 @@ struct MemCache {
   size_t held = 0;                 // bytes in idle + parked
   const bool pinned;
   const size_t cap;
-  MemCache(bool pinned_, size_t cap_) : pinned(pinned_), cap(cap_) {}
+  const bool pageable;             // plain host memory (header images): malloc / free
+  MemCache(bool pinned_, size_t cap_, bool pageable_ = false) : pinned(pinned_), cap(cap_), pageable(pageable_) {}
   static size_t round(size_t n) {
     if (n < ((size_t)1 << 20)) return (n + 4095) & ~(size_t)4095;
     int e = 63 - __builtin_clzll((unsigned long long)n);       // 2^e <= n < 2^(e+1)
@@ -220,10 +230,11 @@ struct MemCache {
     return (n + step - 1) & ~(step - 1);
   }
   int raw_alloc(void** p, size_t n) {
+    if (pageable) return (*p = malloc(n)) ? 0 : 1;
     return pinned ? (hipHostMalloc(p, n, hipHostMallocDefault) == hipSuccess ? 0 : 1)
                   : (hipMalloc(p, n) == hipSuccess ? 0 : 1);
   }
-  void raw_free(void* p) { if (pinned) hipHostFree(p); else hipFree(p); }
+  void raw_free(void* p) { if (pageable) free(p); else if (pinned) hipHostFree(p); else hipFree(p); }
   void* get(size_t want, size_t* got) {
     int dev = 0;
     hipGetDevice(&dev);
@@ -245,13 +256,12 @@ struct MemCache {
       }
     }
     static const bool verbose = getenv("DK_VERBOSE") != nullptr;
-    // A deferred release may be returning just such a block (the previous scan's close). Open
-    // threads wait a bounded time only: the pending release may be the close that joins this open.
-    if (reaper().busy() && !(t_no_drain && t_drain_budget_ms <= 0)) {
+    // A deferred release may be returning just such a block (the previous scan's close); an open's
+    // threads wait only for releases older than the open (its own close may be among the newer)
+    if (reaper().busy_before(t_open_ticket)) {
       const auto t0 = std::chrono::steady_clock::now();
-      if (t_no_drain) reaper().drain_for(t_drain_budget_ms); else reaper().drain();
+      reaper().drain_before(t_open_ticket);
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-      if (t_no_drain) t_drain_budget_ms -= (int)ms + 1;
       if (verbose && ms > 2) fprintf(stderr, "[dk] cache %s: waited %.1f ms for pending releases\n", pinned ? "pinned" : "device", ms);
       return get(want, got);
     }
@@ -274,7 +284,7 @@ struct MemCache {
     int dev = 0;
     hipGetDevice(&dev);
     std::lock_guard<std::mutex> lk(mu);
-    (t_synced ? idle : parked).push_back({p, n, dev});
+    (t_synced || pageable ? idle : parked).push_back({p, n, dev});   // (no device work reads host images)
     held += n;
     if (held > cap) trim_locked(-1, cap / 2);
   }
@@ -301,6 +311,10 @@ struct MemCache {
 };
 static MemCache& dev_cache() { static MemCache* c = new MemCache(false, (size_t)96 << 30); return *c; }
 static MemCache& pinned_cache() { static MemCache* c = new MemCache(true, (size_t)24 << 30); return *c; }
+// header images (HostImg): kept between scans so that the page-header blocks read into them land on
+// pages already faulted in (fresh pages cost ~50 ms of faults per C3 open); only touched pages are
+// resident
+static MemCache& pageable_cache() { static MemCache* c = new MemCache(false, (size_t)64 << 30, true); return *c; }
 
 // Non-blocking streams are pooled per device (creating one costs milliseconds): a call object takes
 // one when it is created and gives it back, drained, when it is freed.
@@ -367,8 +381,31 @@ struct DBuf {
   template <class T> T* as() const { return (T*)p; }
 };
 
-// Pinned host memory from the process-wide cache (file images on their way to HBM, selections and
-// column mirrors on their way back): DMA at full PCIe rate, no page faults on reuse.
+// A file's packed image layout in pageable host memory: the open reads only the page-header blocks
+// into it (the host builds the page tables from them); the column chunks themselves go to HBM
+// through the pinned staging ring (PinRing), never through here. Untouched pages cost nothing.
+struct HostImg {
+  uint8_t* p = nullptr;
+  size_t n = 0, cap = 0;
+  HostImg() = default;
+  HostImg(const HostImg&) = delete;
+  HostImg& operator=(const HostImg&) = delete;
+  HostImg(HostImg&& o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr; o.n = o.cap = 0; }
+  HostImg& operator=(HostImg&& o) noexcept { if (this != &o) { release(); p = o.p; n = o.n; cap = o.cap; o.p = nullptr; o.n = o.cap = 0; } return *this; }
+  ~HostImg() { release(); }
+  void release() { if (p) pageable_cache().put(p, cap); p = nullptr; n = cap = 0; }
+  int alloc(size_t bytes) {
+    release();
+    n = bytes;
+    p = (uint8_t*)pageable_cache().get(bytes ? bytes : 1, &cap);
+    return p ? 0 : fail("host allocation failed for " + std::to_string(bytes) + " bytes");
+  }
+  uint8_t* data() const { return p; }
+  size_t size() const { return n; }
+};
+
+// Pinned host memory from the process-wide cache (selections and column mirrors on their way back,
+// small staged uploads): DMA at full PCIe rate, no page faults on reuse.
 struct HBuf {
   uint8_t* p = nullptr;
   size_t n = 0, cap = 0;
@@ -413,6 +450,73 @@ static bool replay_high_priority() {
   return on;
 }
 
+// The pinned staging ring of the file images' way to HBM: DK_PINNED_MB (default 1024) MiB per device
+// in slots of one H2D piece (DK_PIECE_MB, default 8 MiB), allocated once. A reader thread preads a
+// piece into a free slot, queues its DMA copy to HBM and records the slot's event; the slot is reused
+// once that event has fired. Pinned memory no longer grows with the table (a scan used to pin its
+// whole projected image, 5.8 GB at C3) and an open never waits for the previous scan's release of it.
+static int64_t piece_bytes() {
+  static const int64_t piece = (int64_t)(getenv("DK_PIECE_MB") ? std::max(1, atoi(getenv("DK_PIECE_MB"))) : 8) << 20;
+  return piece;
+}
+struct PinRing {
+  struct Slot { uint8_t* p = nullptr; hipEvent_t ev = nullptr; bool used = false; };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Slot> slots;
+  std::deque<int> free_;
+  std::string err;
+  explicit PinRing(int dev) {
+    int64_t mb = getenv("DK_PINNED_MB") ? std::max(16, atoi(getenv("DK_PINNED_MB"))) : 1024;
+    const int64_t sb = piece_bytes();
+    int n = (int)std::max<int64_t>(4, (mb << 20) / sb);
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(dev);
+    uint8_t* base = nullptr;
+    if (hipHostMalloc((void**)&base, (size_t)n * sb, hipHostMallocDefault) != hipSuccess) {
+      err = "hipHostMalloc failed for the pinned staging ring";
+    } else {
+      for (int i = 0; i < n; i++) {
+        Slot s;
+        s.p = base + (size_t)i * sb;
+        if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) { err = "hipEventCreate failed"; break; }
+        slots.push_back(s);
+        free_.push_back(i);
+      }
+    }
+    hipSetDevice(cur);
+  }
+  // a slot whose previous copy has finished (blocks while every slot is in flight)
+  int acquire() {
+    int i;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return !free_.empty(); });
+      i = free_.front();
+      free_.pop_front();
+    }
+    if (slots[i].used && hipEventSynchronize(slots[i].ev) != hipSuccess) { release(i, nullptr); return -1; }
+    return i;
+  }
+  // back to the ring; its copy (queued on s) must finish before the next user writes it
+  void release(int i, hipStream_t s) {
+    if (s) slots[i].used = hipEventRecord(slots[i].ev, s) == hipSuccess;
+    std::lock_guard<std::mutex> g(mu);
+    free_.push_back(i);
+    cv.notify_one();
+  }
+};
+static PinRing* pin_ring(int dev) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, PinRing*>> rings;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& r : rings) if (r.first == dev) return r.second;
+  auto* r = new PinRing(dev);
+  rings.push_back({dev, r});
+  return r;
+}
+
 // Warm-up at engine creation (once per device and process): the code objects' lazy load, a pooled
 // stream, a first launch on it, the first device / pinned blocks -- costs the first
 // getLatestSnapshot would otherwise pay.
@@ -423,6 +527,7 @@ static int engine_warm(int device) {
   if (std::find(warmed.begin(), warmed.end(), device) != warmed.end()) return 0;
   warmed.push_back(device);
   warm_kernels();
+  if (!pin_ring(device)->err.empty()) return fail(pin_ring(device)->err);   // (the staging ring, once)
   // the pooled streams a checkpoint open and a replay take (own, aux, copy, side, decode; the replay's
   // two high-priority ones), each with a first launch; the DMA engines' first copies both ways
   constexpr int kWarmStreams = 12, kWarmHigh = 3;
@@ -489,7 +594,8 @@ struct FileM {
   std::string path;
   int64_t size = 0;
   std::vector<uint8_t> footer;            // the FileMetaData bytes
-  HBuf bytes;                             // packed column-chunk / offset-index bytes (pinned)
+  HostImg bytes;                          // packed column-chunk / offset-index layout (pageable; only
+                                          // the page-header blocks are read into it, on the host)
   std::vector<Span> spans;
   int64_t num_rows = 0;                   // rows of the selected row groups
   std::vector<int32_t> sel;               // selected row groups, ascending
@@ -2199,9 +2305,9 @@ static void parallel_for(int n, F fn) {
   if (nt <= 1) { for (int i = 0; i < n; i++) fn(i); return; }
   std::atomic<int> next{0};
   std::vector<std::thread> th;
-  const int no_drain = t_no_drain;               // workers of an open stay off the reaper
+  const uint64_t ticket = t_open_ticket;         // workers of an open wait only for older releases
   for (int t = 0; t < nt; t++)
-    th.emplace_back([&, no_drain] { t_no_drain = no_drain; t_drain_budget_ms = kOpenDrainMs; for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
+    th.emplace_back([&, ticket] { t_open_ticket = ticket; for (int i; (i = next.fetch_add(1)) < n;) fn(i); });
   for (auto& x : th) x.join();
 }
 
@@ -2352,6 +2458,13 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
                         int32_t n_leaves, const std::vector<std::vector<int32_t>>* groups, dk_parquet** out,
                         const int32_t* field_ids, const std::function<void(dk_parquet*)>* publish) {
   if (!e) return fail("null engine");
+  // this open's threads wait only for releases submitted before it started (a synchronous open on a
+  // caller's thread takes its ticket here; the asynchronous opener brought its own)
+  struct TicketScope {
+    uint64_t saved;
+    TicketScope() : saved(t_open_ticket) { if (t_open_ticket == UINT64_MAX) t_open_ticket = reaper().ticket(); }
+    ~TicketScope() { t_open_ticket = saved; }
+  } ticket_scope;
   hipSetDevice(e->cfg.device);
   std::unique_ptr<dk_parquet> p(new dk_parquet());
   p->eng = e;
@@ -2441,7 +2554,9 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
   // piece records its event.
   struct Piece { int fi; int64_t packed_off, len; };
   std::vector<Piece> pieces;
-  static const int64_t piece = (int64_t)(getenv("DK_PIECE_MB") ? std::max(1, atoi(getenv("DK_PIECE_MB"))) : 8) << 20;
+  const int64_t piece = piece_bytes();
+  PinRing* ring = pin_ring(e->cfg.device);
+  if (!ring->err.empty()) return fail(ring->err);
   std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[n_files > 0 ? n_files : 1]);
   std::unique_ptr<int[]> fds(new int[n_files > 0 ? n_files : 1]);
   // A piece is a `piece`-byte window of the packed image, whatever spans it cuts; the window's spans
@@ -2457,17 +2572,17 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
     for (int64_t o = 0; o < size; o += piece, n++) pieces.push_back({fi, o, std::min<int64_t>(piece, size - o)});
     left[fi].store(n);
   }
-  const int no_drain = t_no_drain;
-  std::thread reader([&, no_drain] {
-    t_no_drain = no_drain;
-    t_drain_budget_ms = kOpenDrainMs;
+  const uint64_t ticket = t_open_ticket;
+  std::mutex rerr_mu;                             // every write of rerrs[] by the reader's threads
+  std::thread reader([&, ticket] {
+    t_open_ticket = ticket;
     {
       for (int fi = 0; fi < n_files; fi++) {
         fds[fi] = open(p->files[fi].path.c_str(), O_RDONLY);
         if (fds[fi] < 0) { rerrs[fi] = "Error reading Parquet file: " + p->files[fi].path + " (cannot open)"; p->queued[fi].store(2); }
         else if (left[fi].load() == 0) {              // nothing projected to read
           const bool rec = hipEventRecord(p->file_ev[fi], p->copy[fi % copy_streams()].s) == hipSuccess;
-          if (!rec) rerrs[fi] = "hipEventRecord failed";
+          if (!rec) { std::lock_guard<std::mutex> g(rerr_mu); rerrs[fi] = "hipEventRecord failed"; }
           p->queued[fi].store(rec ? 1 : 2, std::memory_order_release);
         }
       }
@@ -2476,32 +2591,38 @@ static int parquet_open(dk_engine* e, const char* const* paths, int32_t n_files,
         FileM& f = p->files[pc.fi];
         if (p->queued[pc.fi].load(std::memory_order_acquire) == 2) return;
         if (p->abort_open.load(std::memory_order_relaxed)) {   // closed while opening: stop reading
-          static std::mutex mu;
-          std::lock_guard<std::mutex> g(mu);
+          std::lock_guard<std::mutex> g(rerr_mu);
           if (rerrs[pc.fi].empty()) rerrs[pc.fi] = "Error reading Parquet file: " + f.path + " (reader closed)";
           p->queued[pc.fi].store(2, std::memory_order_release);
           return;
         }
         hipSetDevice(e->cfg.device);
+        // a file's pieces share one copy stream (round-robin pieces over the streams were measured
+        // slower: 171-176 against 153-181 ms at C3, the file's readiness then waits for every
+        // stream, profiles/r06/ring_ab)
         hipStream_t cs = p->copy[pc.fi % copy_streams()].s;
-        bool ok = true;
+        const int slot = ring->acquire();             // a pinned slot whose previous copy has landed
+        bool ok = slot >= 0;
+        uint8_t* buf = ok ? ring->slots[slot].p : nullptr;
         const int64_t w0 = pc.packed_off, w1 = w0 + pc.len;   // the parts of every span inside the window
         for (const Span& sp : f.spans) {
+          if (!ok) break;
           const int64_t a = std::max(w0, sp.packed_off), b = std::min(w1, sp.packed_off + sp.len);
-          if (a < b && pread_full(fds[pc.fi], f.bytes.data() + a, b - a, sp.file_off + (a - sp.packed_off))) { ok = false; break; }
+          if (a < b && pread_full(fds[pc.fi], buf + (a - w0), b - a, sp.file_off + (a - sp.packed_off))) ok = false;
         }
-        ok = ok && hipMemcpyAsync(p->dfile[pc.fi].as<uint8_t>() + pc.packed_off, f.bytes.data() + pc.packed_off,
-                                  (size_t)pc.len, hipMemcpyHostToDevice, cs) == hipSuccess;
+        const bool copied = ok && hipMemcpyAsync(p->dfile[pc.fi].as<uint8_t>() + pc.packed_off, buf, (size_t)pc.len,
+                                                 hipMemcpyHostToDevice, cs) == hipSuccess;
+        if (slot >= 0) ring->release(slot, copied ? cs : nullptr);
+        ok = copied;
         if (!ok) {
-          static std::mutex mu;
-          std::lock_guard<std::mutex> g(mu);
+          std::lock_guard<std::mutex> g(rerr_mu);
           if (rerrs[pc.fi].empty()) rerrs[pc.fi] = "Error reading Parquet file: " + f.path + " (short read)";
           p->queued[pc.fi].store(2, std::memory_order_release);
           return;
         }
         if (left[pc.fi].fetch_sub(1) == 1) {          // the file's last piece: its copies are all queued
           const bool rec = hipEventRecord(p->file_ev[pc.fi], cs) == hipSuccess;
-          if (!rec) rerrs[pc.fi] = "hipEventRecord failed";
+          if (!rec) { std::lock_guard<std::mutex> g(rerr_mu); if (rerrs[pc.fi].empty()) rerrs[pc.fi] = "hipEventRecord failed"; }
           int expect = 0;
           p->queued[pc.fi].compare_exchange_strong(expect, rec ? 1 : 2, std::memory_order_acq_rel);
         }
@@ -2641,9 +2762,9 @@ extern "C" int dk_parquet_open_async(dk_engine* e, const char* const* paths, int
   std::string early_err;
   std::function<void(dk_parquet*)> publish = [&](dk_parquet* q) { handed.set_value(q); };
   const std::vector<std::vector<int32_t>>* gp = (rg_count && !all) ? &groups : nullptr;
-  std::thread t([&, gp] {
-    t_no_drain = 1;
-    t_drain_budget_ms = kOpenDrainMs;
+  const uint64_t ticket = reaper().ticket();     // releases older than this open
+  std::thread t([&, gp, ticket] {
+    t_open_ticket = ticket;
     dk_parquet* q = nullptr;
     bool pub = false;
     std::function<void(dk_parquet*)> pub_fn = [&](dk_parquet* x) { pub = true; publish(x); };

@@ -5,8 +5,10 @@ counts, plus one full-size C2 counter / selection check.
   (C2a) and with stats (C2b).
 * C3: 64-part snappy checkpoint + 1k commits (100 adds + 100 removes each, 10% re-adds, 5%
   duplicates), unsharded and as 8 shards (ScanBuilder.withShard, delta_amd/shard.py) merged.
-* C2 at 10M rows: ScanMetrics counters, every checkpoint selection bit, the commit-tail rows and a
-  digest of the selected checkpoint rows against the oracle.
+* C2 at 10M rows, as SURVEY §8(d) specifies it (snappy, 2-key partitionValues, `stats` +
+  `stats_parsed`, read with stats): ScanMetrics counters, every checkpoint selection bit, the
+  commit-tail rows and digests of every decoded leaf the scan files carry (path, partitionValues,
+  size, modificationTime, stats) against the oracle.
 """
 import zlib
 
@@ -68,23 +70,27 @@ def test_c3_shape_8_shards(c3_table, c3_oracle):
 
 
 def _col_digest(col):
-    """crc32 over a decoded column's buffers (row_def, offsets, chars / fixed values)."""
+    """crc32 over a decoded column's buffers (row_def, map offsets / entry levels, offsets, chars /
+    fixed values)."""
     h = zlib.crc32(np.ascontiguousarray(col.row_def))
-    for a in (col.offs, col.chars, col.fixed):
+    for a in (getattr(col, "row_offs", None), getattr(col, "entry_def", None), col.offs, col.chars, col.fixed):
         if a is not None:
             h = zlib.crc32(np.ascontiguousarray(a), h)
     return h
 
 
-@pytest.mark.timeout(600)
+C2_LEAVES = ("add.path", "add.partitionValues.key_value.key", "add.partitionValues.key_value.value", "add.size",
+             "add.modificationTime", "add.stats")
+
+
+@pytest.mark.timeout(900)
 def test_c2_full_size_10m(tmp_path):
     from delta_amd import kernel as K
     from oracle import ref
-    spec = dict(C2, with_stats=False, compression="none")
-    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=10_000_000, **spec))
+    synth.write_table(str(tmp_path), synth.TableSpec(n_adds=10_000_000, **C2))
     eng = K.GpuEngine()
     snap = K.Table.forPath(eng, str(tmp_path)).getLatestSnapshot(eng)
-    scan = snap.getScanBuilder().build()
+    scan = snap.getScanBuilder().withStats(True).build()
     got_sel, got_tail, got_dig = [], None, None
     for b in scan.getScanFiles(eng):
         rows = b.selected_rows()
@@ -92,16 +98,16 @@ def test_c2_full_size_10m(tmp_path):
             got_tail = [ref.canon_add_from_cols(b.data, int(i)) for i in rows]
             continue
         got_sel.append(np.asarray(b.selection, dtype=bool))
-        got_dig = [_col_digest(b.data[leaf]) for leaf in ("add.path", "add.size", "add.modificationTime")]
+        got_dig = [_col_digest(b.data[leaf]) for leaf in C2_LEAVES]
     counters = scan.metrics.as_tuple()
     scan.close()
     eng.close()
-    r = ref.replay(str(tmp_path))
+    r = ref.replay(str(tmp_path), with_stats=True)
     assert counters == r.counters.as_tuple()
     assert counters[0] > 10_000_000
     assert got_tail == [ref.canon_add_from_json(a) for a in r.json_rows]
     assert len(got_sel) == len(r.checkpoint) == 1
     want = r.checkpoint[0]
     assert np.array_equal(got_sel[0], want.selected.astype(bool))
-    # the selected rows' content: the decoded columns the rows come from are identical
-    assert got_dig == [_col_digest(want.cols[leaf]) for leaf in ("add.path", "add.size", "add.modificationTime")]
+    # the selected rows' content: every decoded leaf the rows come from is identical
+    assert got_dig == [_col_digest(want.cols[leaf]) for leaf in C2_LEAVES]
