@@ -508,9 +508,17 @@ def main(argv=None):
 
     a2a = args.exchange == "alltoall" and cfg["shared"] and world > 1
     owner = None
+    owner_comm_error = None
     if args.exchange == "owner" and cfg["shared"] and world > 1:
         from delta_amd import shard
-        owner = shard.OwnerComm.rccl()         # RCCL over xGMI, owned by libdkgpu (dk_comm_create)
+        try:
+            owner = shard.OwnerComm.rccl()     # RCCL over xGMI, owned by libdkgpu (dk_comm_create)
+        except Exception as e:                 # noqa: BLE001 -- every rank fails the same way here
+            # the communicator could not be created (RCCL init): run the replicated-tail mode instead
+            # and say so in the line
+            owner_comm_error = "%s: %s" % (type(e).__name__, str(e)[:200])
+            print("[rank %d] owner communicator failed (%s); exchange = allgather" % (rank, owner_comm_error),
+                  file=sys.stderr)
     owner_ms = []
     a2a_ms = []
 
@@ -821,7 +829,8 @@ def main(argv=None):
                                      "commit tail on every GPU; device step ends with one RCCL all-gather of counters "
                                      "+ selection bitmaps"))
                                    if cfg["shared"] else "weak: one table per GPU"),
-                   "exchange": args.exchange if (cfg["shared"] and world > 1) else None,
+                   "exchange": (("allgather (owner communicator failed: %s)" % owner_comm_error) if owner_comm_error
+                                else args.exchange) if (cfg["shared"] and world > 1) else None,
                    "checkpoint_rows_per_gpu": n_ckpt_rows, "json_tail_rows": n_tail,
                    "checkpoint_files_per_gpu": len(ckpt_files)},
         "value_definition": "ScanMetrics.numAddFilesSeen / getScanFiles wall time until fully consumed "

@@ -138,7 +138,7 @@ EXPORTS = ["dk_last_error", "dk_version", "dk_engine_create", "dk_engine_destroy
            "dk_program_free", "dk_json_parse", "dk_parsed_num_leaves", "dk_parsed_leaf_path", "dk_parsed_column_get",
            "dk_parsed_eval", "dk_parsed_free", "dk_comm_unique_id", "dk_comm_create", "dk_comm_create_callbacks",
            "dk_comm_create_local", "dk_comm_world", "dk_comm_rank", "dk_comm_allreduce_i64", "dk_comm_alltoallv",
-           "dk_comm_abort", "dk_comm_last_run", "dk_comm_destroy", "dk_replay_owner_run", "dk_owner_protocol_run"]
+           "dk_comm_abort", "dk_comm_last_run", "dk_comm_last_steps", "dk_comm_destroy", "dk_replay_owner_run", "dk_owner_protocol_run"]
 
 
 def lib(build_if_missing=True):
@@ -256,7 +256,8 @@ def lib(build_if_missing=True):
         "dk_comm_allreduce_i64": (C.c_int, [P, C.POINTER(I64), I32, I32]),
         "dk_comm_alltoallv": (C.c_int, [P, P, C.POINTER(I64), P, C.POINTER(I64), I32]),
         "dk_comm_abort": (C.c_int, [P]),
-        "dk_comm_last_run": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(I64)]),
+        "dk_comm_last_run": (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(I64), C.POINTER(I64)]),
+        "dk_comm_last_steps": (C.c_int, [P, C.POINTER(C.c_double)]),
         "dk_comm_destroy": (None, [P]),
         "dk_replay_owner_run": (C.c_int, [P, P]),
         "dk_owner_protocol_run": (C.c_int, [C.POINTER(dk_owner_side), P]),

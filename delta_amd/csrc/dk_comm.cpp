@@ -35,7 +35,10 @@
 
 #include "../../include/dkgpu.h"
 
-namespace dk { int dk_fail(const std::string& m); }
+namespace dk {
+int dk_fail(const std::string& m);
+hipStream_t replay_stream(dk_replay* r);
+}
 using dk::dk_fail;
 
 #define CHIP(x)                                                                                   \
@@ -131,6 +134,7 @@ struct Scratch {
 // ---- the in-process hub of local communicators ----------------------------------------------
 struct Hub {
   int world;
+  std::mutex side_mu;                         // DK_LOCAL_SERIAL=1: one rank's local step at a time
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
@@ -164,9 +168,11 @@ struct dk_comm {
   Scratch stage_send, stage_recv, small;
   // the protocol's buffers (side memory), kept between runs
   Scratch b_recs, b_keys, b_rrecs, b_rkeys, b_ans, b_back, b_cksend, b_ckrecv, b_flags, b_ckback;
-  // the last run's phases (ms) and bytes sent
-  double ms[4] = {0, 0, 0, 0};
-  int64_t bytes_sent = 0;
+  // the last run: phase wall times, local-step times per phase, time inside collectives (ms), the
+  // payload bytes sent and the number of collectives
+  double ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  double step_ms[16] = {0};                   // per local step, in dk_owner_side member order
+  int64_t bytes_sent = 0, n_coll = 0;
   bool transport_on_device() const { return kind == RCCL || (kind == LOCAL && local_device); }
 };
 
@@ -232,8 +238,9 @@ int local_a2a(dk_comm* c, const Plane* P, int np, bool device) {
       const int64_t n = src.sbytes[c->rank];
       if (n != P[k].rbytes[s]) err = dk_fail("dk_comm: send / receive sizes disagree between ranks");
       else if (n) {
-        if (device) {
-          if (hipMemcpy((uint8_t*)P[k].recv + ro, src.send + so, n, hipMemcpyDefault) != hipSuccess)
+        if (device) {                          // on this rank's copy stream (a hipMemcpy between device
+                                               // buffers may return before the copy has landed)
+          if (hipMemcpyAsync((uint8_t*)P[k].recv + ro, src.send + so, n, hipMemcpyDefault, c->stream) != hipSuccess)
             err = dk_fail("dk_comm: local all-to-all copy failed");
         } else {
           memcpy((uint8_t*)P[k].recv + ro, src.send + so, n);
@@ -241,17 +248,36 @@ int local_a2a(dk_comm* c, const Plane* P, int np, bool device) {
       }
       ro += P[k].rbytes[s];
     }
+    if (device && hipStreamSynchronize(c->stream) != hipSuccess && !err) err = dk_fail("dk_comm: local copy failed");
     H.barrier();                              // every source buffer stays valid until all have pulled
     if (err) return err;
   }
   return 0;
 }
 
+// the communicator's own stream for its device copies (created on first use)
+int comm_stream(dk_comm* c) {
+  if (c->stream) return 0;
+  CHIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  return 0;
+}
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+int comm_a2a_(dk_comm* c, const Plane* P, int np, bool device);
 // all-to-all of the planes; `device`: where the caller's buffers live
 int comm_a2a(dk_comm* c, const Plane* P, int np, bool device) {
+  const auto t = Clock::now();
+  const int rc = comm_a2a_(c, P, np, device);
+  c->ms[7] += ms_since(t);
+  c->n_coll++;
+  return rc;
+}
+int comm_a2a_(dk_comm* c, const Plane* P, int np, bool device) {
   const int W = c->world;
   for (int k = 0; k < np; k++) c->bytes_sent += total(P[k].sbytes, W) - P[k].sbytes[c->rank];
-  if (c->kind == dk_comm::LOCAL) return local_a2a(c, P, np, device);
+  if (c->kind == dk_comm::LOCAL) return (device && comm_stream(c)) ? 1 : local_a2a(c, P, np, device);
   const bool tdev = c->transport_on_device();
   std::vector<Plane> T(P, P + np);
   std::vector<int64_t> soff(np + 1, 0), roff(np + 1, 0);
@@ -262,12 +288,15 @@ int comm_a2a(dk_comm* c, const Plane* P, int np, bool device) {
     }
     void *ss, *rs;
     if (c->stage_send.get(soff[np], tdev, &ss) || c->stage_recv.get(roff[np], tdev, &rs)) return 1;
+    if (comm_stream(c)) return 1;
     for (int k = 0; k < np; k++) {
       const int64_t n = soff[k + 1] - soff[k];
-      if (n) CHIP(hipMemcpy((uint8_t*)ss + soff[k], P[k].send, n, tdev ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
+      if (n) CHIP(hipMemcpyAsync((uint8_t*)ss + soff[k], P[k].send, n, tdev ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost,
+                                 c->stream));
       T[k].send = (uint8_t*)ss + soff[k];
       T[k].recv = (uint8_t*)rs + roff[k];
     }
+    CHIP(hipStreamSynchronize(c->stream));
   }
   int rc = 0;
   if (c->kind == dk_comm::RCCL) {
@@ -278,11 +307,13 @@ int comm_a2a(dk_comm* c, const Plane* P, int np, bool device) {
         rc = dk_fail("dk_comm: the all-to-all callback failed");
   }
   if (rc) return rc;
-  if (device != tdev)
+  if (device != tdev) {
     for (int k = 0; k < np; k++) {
       const int64_t n = roff[k + 1] - roff[k];
-      if (n) CHIP(hipMemcpy(P[k].recv, T[k].recv, n, tdev ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice));
+      if (n) CHIP(hipMemcpyAsync(P[k].recv, T[k].recv, n, tdev ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice, c->stream));
     }
+    CHIP(hipStreamSynchronize(c->stream));
+  }
   return 0;
 }
 
@@ -297,7 +328,15 @@ int comm_a2a_small(dk_comm* c, const int64_t* send, int64_t* recv, int k) {
   return rc;
 }
 
+int comm_allreduce_(dk_comm* c, int64_t* vals, int n, int op);
 int comm_allreduce(dk_comm* c, int64_t* vals, int n, int op) {
+  const auto t = Clock::now();
+  const int rc = comm_allreduce_(c, vals, n, op);
+  c->ms[7] += ms_since(t);
+  c->n_coll++;
+  return rc;
+}
+int comm_allreduce_(dk_comm* c, int64_t* vals, int n, int op) {
   if (n <= 0) return 0;
   if (op != 0 && op != 1) return dk_fail("dk_comm_allreduce_i64: op must be 0 (sum) or 1 (max)");
   switch (c->kind) {
@@ -333,27 +372,53 @@ int comm_allreduce(dk_comm* c, int64_t* vals, int n, int op) {
 struct Side {
   const dk_owner_side* cs = nullptr;
   dk_replay* r = nullptr;
+  double* acc = nullptr;                        // the phase's local-step time (ms)
+  double* steps = nullptr;                      // per-step times (dk_owner_side member order)
+  std::mutex* serial = nullptr;                 // one rank's local step at a time (local transport)
   bool device() const { return r != nullptr || (cs && cs->device_buffers); }
-#define CALL(name, ...) (r ? dk_replay_owner_##name(r, ##__VA_ARGS__) : cs->name(cs->user, ##__VA_ARGS__))
-  int begin() { return r ? dk_replay_owner_begin(r) : cs->begin(cs->user); }
-  int tail_counts(int64_t* recs, int64_t* bytes) { return CALL(tail_counts, recs, bytes); }
-  int tail_pack(void* recs, void* keys) { return CALL(tail_pack, recs, keys); }
+  // every local step timed (and, with a serial lock, run alone on the device)
+  struct Timed {
+    const Side& s;
+    int k;
+    Clock::time_point t;
+    std::unique_lock<std::mutex> lk;
+    // serial (rehearsals: every rank in one process on one GPU): the step runs alone -- the device
+    // drained of the other ranks' work before it, its own work finished inside its time
+    // (the step's own stream is drained inside its time; work it queued on other streams -- the
+    // add.size mirror, which overlaps the exchanges on a rank's own GPU -- before the next step)
+    Timed(const Side& s_, int k_) : s(s_), k(k_) {
+      if (s.serial) { lk = std::unique_lock<std::mutex>(*s.serial); hipDeviceSynchronize(); }
+      t = Clock::now();
+    }
+    ~Timed() {
+      if (s.serial && s.r) hipStreamSynchronize(dk::replay_stream(s.r));
+      const double d = ms_since(t);
+      if (s.acc) *s.acc += d;
+      if (s.steps) s.steps[k] += d;
+    }
+  };
+  enum { S_BEGIN, S_TAIL_COUNTS, S_TAIL_PACK, S_TAIL_RESOLVE, S_RESEED, S_TAIL_FINISH, S_RUN, S_CKPT_COUNTS,
+         S_CKPT_PACK, S_CKPT_LOOKUP, S_CKPT_APPLY, S_CAND_COUNTS, S_CAND_PACK, S_CAND_VERIFY, S_CAND_FINISH };
+#define CALL(name, K, ...) (Timed(*this, K), r ? dk_replay_owner_##name(r, ##__VA_ARGS__) : cs->name(cs->user, ##__VA_ARGS__))
+  int begin() { Timed tm(*this, S_BEGIN); return r ? dk_replay_owner_begin(r) : cs->begin(cs->user); }
+  int tail_counts(int64_t* recs, int64_t* bytes) { return CALL(tail_counts, S_TAIL_COUNTS, recs, bytes); }
+  int tail_pack(void* recs, void* keys) { return CALL(tail_pack, S_TAIL_PACK, recs, keys); }
   int tail_resolve(const void* recs, int64_t n, const void* keys, int64_t nb, uint8_t* ans, int32_t* flags) {
-    return CALL(tail_resolve, recs, n, keys, nb, ans, flags);
+    return CALL(tail_resolve, S_TAIL_RESOLVE, recs, n, keys, nb, ans, flags);
   }
-  int reseed() { return r ? dk_replay_owner_reseed(r) : cs->reseed(cs->user); }
-  int tail_finish(const uint8_t* back) { return CALL(tail_finish, back); }
-  int run() { return r ? dk_replay_run(r) : cs->run(cs->user); }
-  int ckpt_counts(int64_t* c) { return CALL(ckpt_counts, c); }
-  int ckpt_pack(uint64_t* send) { return CALL(ckpt_pack, send); }
-  int ckpt_lookup(const uint64_t* recv, int64_t n, uint8_t* flags) { return CALL(ckpt_lookup, recv, n, flags); }
-  int ckpt_apply(const uint8_t* back) { return CALL(ckpt_apply, back); }
-  int cand_counts(int64_t* recs, int64_t* bytes) { return CALL(cand_counts, recs, bytes); }
-  int cand_pack(void* recs, void* keys) { return CALL(cand_pack, recs, keys); }
+  int reseed() { Timed tm(*this, S_RESEED); return r ? dk_replay_owner_reseed(r) : cs->reseed(cs->user); }
+  int tail_finish(const uint8_t* back) { return CALL(tail_finish, S_TAIL_FINISH, back); }
+  int run() { Timed tm(*this, S_RUN); return r ? dk_replay_run(r) : cs->run(cs->user); }
+  int ckpt_counts(int64_t* c) { return CALL(ckpt_counts, S_CKPT_COUNTS, c); }
+  int ckpt_pack(uint64_t* send) { return CALL(ckpt_pack, S_CKPT_PACK, send); }
+  int ckpt_lookup(const uint64_t* recv, int64_t n, uint8_t* flags) { return CALL(ckpt_lookup, S_CKPT_LOOKUP, recv, n, flags); }
+  int ckpt_apply(const uint8_t* back) { return CALL(ckpt_apply, S_CKPT_APPLY, back); }
+  int cand_counts(int64_t* recs, int64_t* bytes) { return CALL(cand_counts, S_CAND_COUNTS, recs, bytes); }
+  int cand_pack(void* recs, void* keys) { return CALL(cand_pack, S_CAND_PACK, recs, keys); }
   int cand_verify(const void* recs, int64_t n, const void* keys, int64_t nb, uint8_t* ans) {
-    return CALL(cand_verify, recs, n, keys, nb, ans);
+    return CALL(cand_verify, S_CAND_VERIFY, recs, n, keys, nb, ans);
   }
-  int cand_finish(const uint8_t* back) { return CALL(cand_finish, back); }
+  int cand_finish(const uint8_t* back) { return CALL(cand_finish, S_CAND_FINISH, back); }
 #undef CALL
 };
 
@@ -375,14 +440,18 @@ int vote_outcome(const StepErr& e, int64_t votes) {
   return DK_STATUS_PEER;
 }
 
-using Clock = std::chrono::steady_clock;
-double ms_since(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
-
 int run_protocol(Side& S, dk_comm* c) {
   const int W = c->world;
   const bool dev = S.device();
   if (c->device >= 0) CHIP(hipSetDevice(c->device));
   c->bytes_sent = 0;
+  c->n_coll = 0;
+  for (double& m : c->ms) m = 0;
+  for (double& m : c->step_ms) m = 0;
+  S.steps = c->step_ms;
+  static const bool serial = getenv("DK_LOCAL_SERIAL") && atoi(getenv("DK_LOCAL_SERIAL")) != 0;
+  if (c->kind == dk_comm::LOCAL && serial) S.serial = &c->hub->side_mu;
+  S.acc = &c->ms[4];
   const auto t0 = Clock::now();
   std::vector<int64_t> sv(3 * W), rv(3 * W);
   std::vector<int64_t> rc(W), bc(W), rrc(W), rbc(W), zero(W, 0), ones(W);
@@ -441,6 +510,7 @@ int run_protocol(Side& S, dk_comm* c) {
   }
   c->ms[0] = ms_since(t0);
   const auto t1 = Clock::now();
+  S.acc = &c->ms[5];
 
   // ---- 2. every checkpoint row's key hash to its owner; rows no owned tail key hashes to decide there
   void *cks = nullptr, *ckr = nullptr, *flags = nullptr, *ckb = nullptr;
@@ -455,6 +525,7 @@ int run_protocol(Side& S, dk_comm* c) {
   }
   c->ms[1] = ms_since(t1);
   const auto t2 = Clock::now();
+  S.acc = &c->ms[6];
   for (int p = 0; p < W; p++) {
     sv[2 * p] = e.set ? kErrBit : 0;
     sv[2 * p + 1] = e.set ? 0 : cc[p] * 8;
@@ -620,20 +691,25 @@ extern "C" int dk_comm_abort(dk_comm* c) {
   return comm_a2a_small(c, sv.data(), rv.data(), 3);
 }
 
-extern "C" int dk_comm_last_run(const dk_comm* c, double ms[4], int64_t* bytes_sent) {
+extern "C" int dk_comm_last_run(const dk_comm* c, double ms[8], int64_t* bytes_sent, int64_t* collectives) {
   if (!c) return dk_fail("dk_comm_last_run: null communicator");
-  if (ms) for (int i = 0; i < 4; i++) ms[i] = c->ms[i];
+  if (ms) for (int i = 0; i < 8; i++) ms[i] = c->ms[i];
   if (bytes_sent) *bytes_sent = c->bytes_sent;
+  if (collectives) *collectives = c->n_coll;
+  return 0;
+}
+
+extern "C" int dk_comm_last_steps(const dk_comm* c, double ms[16]) {
+  if (!c) return dk_fail("dk_comm_last_steps: null communicator");
+  for (int i = 0; i < 16; i++) ms[i] = c->step_ms[i];
   return 0;
 }
 
 extern "C" void dk_comm_destroy(dk_comm* c) {
   if (!c) return;
-  if (c->kind == dk_comm::RCCL) {
-    hipSetDevice(c->device);
-    if (c->nccl) rccl().destroy(c->nccl);
-    if (c->stream) hipStreamDestroy(c->stream);
-  }
+  if (c->device >= 0) hipSetDevice(c->device);
+  if (c->kind == dk_comm::RCCL && c->nccl) rccl().destroy(c->nccl);
+  if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 

@@ -76,6 +76,13 @@ void launch_own_rowhash(const ProbeSet&, uint64_t*, uint32_t, uint64_t, DState*,
 void launch_own_count(const ProbeSet&, const uint64_t*, int, unsigned long long*, unsigned long long*, hipStream_t);
 void launch_own_pack(const ProbeSet&, const uint64_t*, int, const unsigned long long*, uint64_t*, int32_t*, hipStream_t);
 void launch_own_lookup(const uint64_t*, long long, const Slot*, const uint32_t*, uint64_t, uint8_t*, hipStream_t);
+void launch_own_tail_count(const DJsonAction*, int, int, unsigned long long*, hipStream_t);
+void launch_own_tail_pack(const DJsonAction*, int, int, const unsigned long long*, const uint8_t*, OwnerKeyRec*, uint8_t*,
+                          int32_t*, hipStream_t);
+void launch_own_tail_finish(const int32_t*, const uint8_t*, long long, uint8_t*, hipStream_t);
+int own_recs_blocks(long long, long long*);
+void launch_own_recs_acts(const OwnerKeyRec*, long long, long long, unsigned long long*, int*, unsigned long long*,
+                          DJsonAction*, hipStream_t);
 void launch_own_apply(const ProbeSet&, const int32_t*, const uint8_t*, long long, int32_t*, unsigned int*, DState*, hipStream_t);
 void launch_own_cand_len(const ProbeSet&, const int32_t*, long long, const uint64_t*, int, int32_t*, int32_t*, int32_t*,
                          hipStream_t);
@@ -4002,10 +4009,10 @@ struct dk_replay {
   // rank's checkpoint rows for them
   int32_t ow = 0, orank = 0;              // ow = 0: off
   int32_t ophase = 0;                     // OP_* below
-  std::vector<DJsonAction> h_acts;        // own actions after k_json_canon (host copy)
-  std::vector<uint8_t> h_canon;
-  std::vector<int32_t> o_send_src;        // own action of each tail record, in send order
-  std::vector<int64_t> o_send_koff;       // its key bytes in the send buffer
+  DBuf d_otot;                            // tail records / key bytes per owner (k_own_tail_count)
+  DBuf d_osrc;                            // own action of each tail record, in send order
+  DBuf d_orsum;                           // owner: key bytes per record chunk, then chunk offsets (+ total, bad)
+  int64_t n_osend = 0;                    // tail records this rank sends
   DBuf d_oacts, d_ocanon, d_oslots, d_ofp, d_osel;
   int64_t n_oacts = 0;
   uint64_t omask = 0;
@@ -5188,6 +5195,8 @@ extern "C" int dk_replay_set_owner(dk_replay* r, int32_t world, int32_t rank) {
   return 0;
 }
 
+namespace dk { hipStream_t replay_stream(dk_replay* r) { return r ? r->stream : nullptr; } }
+
 extern "C" int dk_replay_owner_begin(dk_replay* r) {
   if (owner_phase(r, -1, "dk_replay_owner_begin")) return 1;
   r->have_result = false;
@@ -5195,7 +5204,9 @@ extern "C" int dk_replay_owner_begin(dk_replay* r) {
   r->n_groups = 0;
   DState st0{};
   st0.err_row = LLONG_MAX;
-  HIPOK(hipMemcpy(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice));
+  // (on the replay's stream, synchronised: a pageable hipMemcpy may return before its DMA lands)
+  HIPOK(hipMemcpyAsync(r->d_state.p, &st0, sizeof st0, hipMemcpyHostToDevice, r->stream));
+  HIPOK(hipStreamSynchronize(r->stream));
   r->ophase = OP_BEGUN;
   return 0;
 }
@@ -5209,50 +5220,33 @@ extern "C" int dk_replay_owner_tail_counts(dk_replay* r, int64_t* recs, int64_t*
     launch_json_canon(r->d_acts.as<DJsonAction>(), na, r->d_jchars.as<uint8_t>(), r->d_canon.as<uint8_t>(), r->seed,
                       r->d_state.as<DState>(), s);
   }
+  // records / key bytes per owner, counted on the device (k_own_tail_count): only 2 x world counts
+  // come back
+  if (r->d_otot.n < (size_t)r->ow * 16 + 64 && r->d_otot.alloc((size_t)r->ow * 16 + 64)) return 1;
+  launch_own_tail_count(r->d_acts.as<DJsonAction>(), na, r->ow, r->d_otot.as<unsigned long long>(), s);
+  std::vector<unsigned long long> tot(2 * (size_t)r->ow);
+  HIPOK(hipMemcpyAsync(tot.data(), r->d_otot.p, tot.size() * 8, hipMemcpyDeviceToHost, s));
   HIPOK(hipStreamSynchronize(s));
-  r->h_acts.resize(na);
-  if (na) HIPOK(hipMemcpy(r->h_acts.data(), r->d_acts.p, na * sizeof(DJsonAction), hipMemcpyDeviceToHost));
-  r->h_canon.resize(r->d_canon.n);
-  if (r->d_canon.n) HIPOK(hipMemcpy(r->h_canon.data(), r->d_canon.p, r->d_canon.n, hipMemcpyDeviceToHost));
-  std::vector<std::vector<int32_t>> by(r->ow);
-  for (int i = 0; i < na; i++) {
-    const DJsonAction& a = r->h_acts[i];
-    if (a.kind == JA_NONE || a.status) continue;       // a key error: reported by dk_replay_sync
-    by[a.h % (uint64_t)r->ow].push_back(i);
-  }
-  r->o_send_src.clear();
-  r->o_send_koff.clear();
-  int64_t koff = 0;
+  r->n_osend = 0;
   for (int o = 0; o < r->ow; o++) {
-    recs[o] = (int64_t)by[o].size();
-    bytes[o] = 0;
-    for (int32_t i : by[o]) {
-      const int64_t kl = (int64_t)r->h_acts[i].canon_len + r->h_acts[i].dv_len;
-      r->o_send_src.push_back(i);
-      r->o_send_koff.push_back(koff);
-      koff += kl;
-      bytes[o] += kl;
-    }
+    recs[o] = (int64_t)tot[o];
+    bytes[o] = (int64_t)tot[r->ow + o];
+    r->n_osend += recs[o];
   }
   r->ophase = OP_TAIL_COUNTED;
   return 0;
 }
 
+// the records and key bytes, owner-major, written by the device (k_own_tail_pack) straight into the
+// caller's send buffers
 extern "C" int dk_replay_owner_tail_pack(dk_replay* r, void* recs, void* keys) {
   if (owner_phase(r, OP_TAIL_COUNTED, "dk_replay_owner_tail_pack")) return 1;
-  const size_t n = r->o_send_src.size();
-  std::vector<OwnerKeyRec> R(n);
-  std::vector<uint8_t> K;
-  for (size_t pos = 0; pos < n; pos++) {
-    const int32_t i = r->o_send_src[pos];
-    const DJsonAction& a = r->h_acts[i];
-    OwnerKeyRec& k = R[pos];
-    k.h = a.h; k.kind = a.kind; k.step = a.step; k.row = a.row;
-    k.key_len = a.canon_len + a.dv_len; k.canon_len = a.canon_len; k.src = i;
-    K.insert(K.end(), r->h_canon.begin() + a.canon_off, r->h_canon.begin() + a.canon_off + k.key_len);
-  }
-  if (n) HIPOK(hipMemcpy(recs, R.data(), n * sizeof(OwnerKeyRec), hipMemcpyHostToDevice));
-  if (!K.empty()) HIPOK(hipMemcpy(keys, K.data(), K.size(), hipMemcpyHostToDevice));
+  hipStream_t s = r->stream;
+  if (r->d_osrc.n < (size_t)r->n_osend * 4 + 64 && r->d_osrc.alloc((size_t)r->n_osend * 4 + 64)) return 1;
+  if (r->n_osend > 0)
+    launch_own_tail_pack(r->d_acts.as<DJsonAction>(), (int)r->acts.size(), r->ow, r->d_otot.as<unsigned long long>(),
+                         r->d_canon.as<uint8_t>(), (OwnerKeyRec*)recs, (uint8_t*)keys, r->d_osrc.as<int32_t>(), s);
+  HIPOK(hipStreamSynchronize(s));                 // the records leave through the caller's collective
   r->ophase = OP_TAIL_PACKED;
   return 0;
 }
@@ -5262,28 +5256,20 @@ extern "C" int dk_replay_owner_tail_resolve(dk_replay* r, const void* recs, int6
   if (owner_phase(r, OP_TAIL_PACKED, "dk_replay_owner_tail_resolve")) return 1;
   if (n < 0 || nbytes < 0 || n > INT32_MAX / 2) return fail("dk_replay_owner_tail_resolve: bad sizes");
   hipStream_t s = r->stream;
-  std::vector<OwnerKeyRec> R(n);
-  if (n) HIPOK(hipMemcpy(R.data(), recs, n * sizeof(OwnerKeyRec), hipMemcpyDeviceToHost));
-  std::vector<DJsonAction> A(n);
-  int64_t koff = 0;
-  for (int64_t i = 0; i < n; i++) {
-    const OwnerKeyRec& k = R[i];
-    if (k.key_len < 0 || k.canon_len < 0 || k.canon_len > k.key_len || koff + k.key_len > nbytes ||
-        (k.kind != JA_ADD && k.kind != JA_REMOVE && k.kind != JA_CKADD))
-      return fail("dk_replay_owner_tail_resolve: malformed key record");
-    DJsonAction a{};
-    a.kind = k.kind; a.step = k.step; a.row = k.row;
-    a.canon_off = koff; a.canon_len = k.canon_len; a.dv_len = k.key_len - k.canon_len;
-    a.h = k.h;
-    A[i] = a;
-    koff += k.key_len;
-  }
-  if (koff != nbytes) return fail("dk_replay_owner_tail_resolve: key bytes do not match the records");
   uint64_t cap = 1024;
   while (cap < 2 * (uint64_t)n + 16) cap <<= 1;
   r->omask = cap - 1;
   r->n_oacts = n;
-  if (upload(r->d_oacts, A.data(), n * sizeof(DJsonAction), s)) return 1;
+  // the received records -> the owner's action table, on the device (k_own_recs_count / _acts)
+  long long chunk;
+  const int nb = own_recs_blocks(n, &chunk);
+  if (r->d_oacts.n < (size_t)n * sizeof(DJsonAction) + 64 && r->d_oacts.alloc((size_t)n * sizeof(DJsonAction) + 64)) return 1;
+  if (r->d_orsum.n < (size_t)nb * 8 + 64 && r->d_orsum.alloc((size_t)nb * 8 + 64)) return 1;
+  unsigned long long* bsum = r->d_orsum.as<unsigned long long>();
+  unsigned long long* total = bsum + nb;
+  int* bad = (int*)(bsum + nb + 1);
+  HIPOK(hipMemsetAsync(bsum + nb, 0, 16, s));
+  launch_own_recs_acts((const OwnerKeyRec*)recs, n, nbytes, bsum, bad, total, r->d_oacts.as<DJsonAction>(), s);
   if (r->d_ocanon.alloc(nbytes + 64)) return 1;
   if (nbytes) HIPOK(hipMemcpyAsync(r->d_ocanon.p, keys, nbytes, hipMemcpyDeviceToDevice, s));
   if (r->d_oslots.alloc(cap * sizeof(Slot)) || r->d_ofp.alloc(cap * sizeof(uint32_t)) || r->d_osel.alloc(n + 16)) return 1;
@@ -5297,9 +5283,13 @@ extern "C" int dk_replay_owner_tail_resolve(dk_replay* r, const void* recs, int6
     launch_json_select(OA, (int)n, S, r->omask, r->d_ocanon.as<uint8_t>(), r->d_osel.as<uint8_t>(), st, s); }
   launch_table_fp(S, r->d_ofp.as<uint32_t>(), cap, s);
   if (n) HIPOK(hipMemcpyAsync(answers, r->d_osel.p, n, hipMemcpyDeviceToDevice, s));
-  HIPOK(hipStreamSynchronize(s));
+  struct { unsigned long long total; int bad, pad; } chk{0, 0, 0};
   DState h{};
-  HIPOK(hipMemcpy(&h, r->d_state.p, sizeof h, hipMemcpyDeviceToHost));
+  HIPOK(hipMemcpyAsync(&chk, total, 16, hipMemcpyDeviceToHost, s));
+  HIPOK(hipMemcpyAsync(&h, r->d_state.p, sizeof h, hipMemcpyDeviceToHost, s));
+  HIPOK(hipStreamSynchronize(s));
+  if (n && chk.bad) return fail("dk_replay_owner_tail_resolve: malformed key record");
+  if ((int64_t)(n ? chk.total : 0) != nbytes) return fail("dk_replay_owner_tail_resolve: key bytes do not match the records");
   *flags = h.err_flags & E_COLLISION;
   r->ophase = OP_TAIL_RESOLVED;
   return 0;
@@ -5314,7 +5304,8 @@ extern "C" int dk_replay_owner_reseed(dk_replay* r) {
   HIPOK(hipMemcpy(&h, r->d_state.p, sizeof h, hipMemcpyDeviceToHost));
   for (int i = 0; i < 5; i++) h.counters[i] = 0;
   h.err_flags &= ~E_COLLISION;
-  HIPOK(hipMemcpy(r->d_state.p, &h, sizeof h, hipMemcpyHostToDevice));
+  HIPOK(hipMemcpyAsync(r->d_state.p, &h, sizeof h, hipMemcpyHostToDevice, r->stream));
+  HIPOK(hipStreamSynchronize(r->stream));
   if (++r->seed > 64) return fail("replay: repeated key-hash collisions");
   r->ophase = OP_BEGUN;
   return 0;
@@ -5323,11 +5314,10 @@ extern "C" int dk_replay_owner_reseed(dk_replay* r) {
 extern "C" int dk_replay_owner_tail_finish(dk_replay* r, const uint8_t* back) {
   if (owner_phase(r, OP_TAIL_RESOLVED, "dk_replay_owner_tail_finish")) return 1;
   hipStream_t s = r->stream;
-  const size_t n = r->o_send_src.size(), na = r->acts.size();
-  std::vector<uint8_t> hb(n), sel(na + 16, 0);
-  if (n) HIPOK(hipMemcpy(hb.data(), back, n, hipMemcpyDeviceToHost));
-  for (size_t pos = 0; pos < n; pos++) sel[r->o_send_src[pos]] = hb[pos] != 0;
-  if (upload(r->d_jsel, sel.data(), sel.size(), s)) return 1;
+  const size_t na = r->acts.size();
+  if (r->d_jsel.n < na + 16 && r->d_jsel.alloc(na + 16)) return 1;
+  HIPOK(hipMemsetAsync(r->d_jsel.p, 0, na + 16, s));
+  launch_own_tail_finish(r->d_osrc.as<int32_t>(), (const uint8_t*)back, r->n_osend, r->d_jsel.as<uint8_t>(), s);
   DState* st = r->d_state.as<DState>();
   if (r->has_part && na) {                 // partition pruning on this rank's tail adds (before skipping)
     KTimer::Scope sc(&r->timer, 18, s);

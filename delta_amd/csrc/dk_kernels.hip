@@ -4244,19 +4244,40 @@ __global__ __launch_bounds__(NT) void k_a2a_count(ProbeSet PS, int world, long l
 }
 
 // bc[b][o] -> exclusive offsets in owner-major order; totals[o] = records for owner o
-__global__ void k_a2a_scan(unsigned long long* __restrict__ bc, int nb, int world,
-                           unsigned long long* __restrict__ totals) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// Block-wide exclusive scan of one u64 per thread (NT threads); *total = the block's sum.
+__device__ __forceinline__ unsigned long long block_excl_scan(unsigned long long v, unsigned long long* total) {
+  __shared__ unsigned long long wsum[NT / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) { const unsigned long long y = __shfl_up(x, o, 64); if (lane >= o) x += y; }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < NT / 64; k++) { const unsigned long long t = wsum[k]; if (k < w) before += t; all += t; }
+  __syncthreads();                                   // (wsum reused by the next call)
+  *total = all;
+  return before + x - v;
+}
+
+// owner-major exclusive offsets of the per-workgroup routing counts (bc[b * world + o]): owner by
+// owner, the workgroup chunks scanned NT at a time (was one lane over every count: 2-3 ms at 12.5M
+// rows, 763 chunks x 8 owners of dependent global read-modify-writes)
+__global__ __launch_bounds__(NT) void k_a2a_scan(unsigned long long* __restrict__ bc, int nb, int world,
+                                                 unsigned long long* __restrict__ totals) {
   unsigned long long run = 0;
   for (int o = 0; o < world; o++) {
-    unsigned long long t = 0;
-    for (int b = 0; b < nb; b++) {
-      const unsigned long long c = bc[(long long)b * world + o];
-      bc[(long long)b * world + o] = run + t;
-      t += c;
+    const unsigned long long start = run;
+    for (int b0 = 0; b0 < nb; b0 += NT) {
+      const int b = b0 + threadIdx.x;
+      const unsigned long long c = b < nb ? bc[(long long)b * world + o] : 0ull;
+      unsigned long long tot;
+      const unsigned long long ex = block_excl_scan(c, &tot);
+      if (b < nb) bc[(long long)b * world + o] = run + ex;
+      run += tot;
     }
-    totals[o] = t;
-    run += t;
+    if (threadIdx.x == 0) totals[o] = run - start;
   }
 }
 
@@ -4358,7 +4379,7 @@ void launch_a2a_count(const ProbeSet& PS, int world, unsigned long long* bc, uns
   long long chunk;
   const int nb = a2a_blocks(PS.total, &chunk);
   hipLaunchKernelGGL(k_a2a_count, dim3(nb), dim3(NT), 0, s, PS, world, chunk, bc);
-  hipLaunchKernelGGL(k_a2a_scan, dim3(1), dim3(64), 0, s, bc, nb, world, totals);
+  hipLaunchKernelGGL(k_a2a_scan, dim3(1), dim3(NT), 0, s, bc, nb, world, totals);
 }
 void launch_a2a_pack(const ProbeSet& PS, int world, const unsigned long long* boff, uint64_t* send_h, int32_t* send_g,
                      int32_t* cand, unsigned int* cand_n, DState* st, hipStream_t s) {
@@ -4651,6 +4672,111 @@ __global__ __launch_bounds__(NT) void k_own_pack(ProbeSet PS, const uint64_t* __
   }
 }
 
+// Commit tail, routed on the device (was a host pass over the actions and their canonical keys,
+// 1-4 ms per rank at N = 8): workgroup o takes, in action order, every action whose key it routes to
+// owner o -- records and key bytes owner-major, the send order deterministic. The key-error actions
+// (status != 0) stay home; dk_replay_sync reports them.
+__device__ __forceinline__ bool own_tail_routed(const DJsonAction& a, int world, int o) {
+  return a.kind != JA_NONE && a.status == 0 && a2a_owner(a.h, world) == o;
+}
+__global__ __launch_bounds__(NT) void k_own_tail_count(const DJsonAction* __restrict__ acts, int na, int world,
+                                                       unsigned long long* __restrict__ tot) {
+  const int o = blockIdx.x;
+  unsigned long long nr = 0, nb = 0;
+  for (int i = threadIdx.x; i < na; i += NT) {
+    const DJsonAction& a = acts[i];
+    if (own_tail_routed(a, world, o)) { nr++; nb += (unsigned long long)(a.canon_len + a.dv_len); }
+  }
+  unsigned long long tr, tb;
+  block_excl_scan(nr, &tr);
+  block_excl_scan(nb, &tb);
+  if (threadIdx.x == 0) { tot[o] = tr; tot[world + o] = tb; }
+}
+__global__ __launch_bounds__(NT) void k_own_tail_pack(const DJsonAction* __restrict__ acts, int na, int world,
+                                                      const unsigned long long* __restrict__ tot,
+                                                      const uint8_t* __restrict__ canon, OwnerKeyRec* __restrict__ recs,
+                                                      uint8_t* __restrict__ keys, int32_t* __restrict__ send_src) {
+  const int o = blockIdx.x;
+  unsigned long long run_r = 0, run_b = 0;
+  for (int q = 0; q < o; q++) { run_r += tot[q]; run_b += tot[world + q]; }
+  for (int s0 = 0; s0 < na; s0 += NT) {
+    const int i = s0 + threadIdx.x;
+    DJsonAction a{};
+    bool own = false;
+    if (i < na) { a = acts[i]; own = own_tail_routed(a, world, o); }
+    const int32_t kl = own ? a.canon_len + a.dv_len : 0;
+    // one scan of (key bytes << 16 | records): < 2^16 records and < 2^48 bytes per NT actions
+    unsigned long long both;
+    const unsigned long long ex = block_excl_scan(own ? ((unsigned long long)kl << 16) | 1ull : 0ull, &both);
+    const unsigned long long nr = both & 0xffffull, nbytes = both >> 16;
+    if (own) {
+      const unsigned long long pos = run_r + (ex & 0xffffull), kpos = run_b + (ex >> 16);
+      OwnerKeyRec k;
+      k.h = a.h; k.kind = a.kind; k.step = a.step; k.row = a.row;
+      k.key_len = kl; k.canon_len = a.canon_len; k.src = i;
+      recs[pos] = k;
+      send_src[pos] = i;
+      const uint8_t* src = canon + a.canon_off;
+      for (int32_t b = 0; b < kl; b++) keys[kpos + b] = src[b];
+    }
+    run_r += nr;
+    run_b += nbytes;
+  }
+}
+// owner: the received tail records -> its action table (DJsonAction over the received key bytes), on
+// the device (was a host pass: records down, actions up). Chunks of records: key bytes per chunk
+// (k_own_recs_count, validating every record), owner-major scan of the chunk sums (k_a2a_scan, one
+// "owner"), then each chunk's records with their key offsets (k_own_recs_acts).
+__global__ __launch_bounds__(NT) void k_own_recs_count(const OwnerKeyRec* __restrict__ recs, long long n, long long chunk,
+                                                       unsigned long long* __restrict__ bsum, int* __restrict__ bad) {
+  const long long g0 = (long long)blockIdx.x * chunk, g1 = g0 + chunk < n ? g0 + chunk : n;
+  unsigned long long sum = 0;
+  for (long long i = g0 + threadIdx.x; i < g1; i += NT) {
+    const OwnerKeyRec k = recs[i];
+    if (k.key_len < 0 || k.canon_len < 0 || k.canon_len > k.key_len ||
+        (k.kind != JA_ADD && k.kind != JA_REMOVE && k.kind != JA_CKADD)) { atomicOr(bad, 1); continue; }
+    sum += (unsigned long long)k.key_len;
+  }
+  unsigned long long tot;
+  block_excl_scan(sum, &tot);
+  if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+// (a malformed record -- reported by the host from k_own_recs_count's flag -- or one whose key bytes
+// would fall past the received buffer becomes a JA_NONE action no table kernel reads)
+__global__ __launch_bounds__(NT) void k_own_recs_acts(const OwnerKeyRec* __restrict__ recs, long long n, long long chunk,
+                                                      const unsigned long long* __restrict__ boff, long long nbytes,
+                                                      DJsonAction* __restrict__ acts) {
+  const long long g0 = (long long)blockIdx.x * chunk, g1 = g0 + chunk < n ? g0 + chunk : n;
+  unsigned long long run = boff[blockIdx.x];
+  for (long long s0 = g0; s0 < g1; s0 += NT) {
+    const long long i = s0 + threadIdx.x;
+    OwnerKeyRec k{};
+    if (i < g1) k = recs[i];
+    const unsigned long long kl = (i < g1 && k.key_len > 0) ? (unsigned long long)k.key_len : 0ull;
+    unsigned long long tot;
+    const unsigned long long ex = block_excl_scan(kl, &tot);
+    if (i < g1) {
+      DJsonAction a{};
+      const bool ok = k.key_len >= 0 && k.canon_len >= 0 && k.canon_len <= k.key_len &&
+                      (k.kind == JA_ADD || k.kind == JA_REMOVE || k.kind == JA_CKADD) &&
+                      (long long)(run + ex) + k.key_len <= nbytes;
+      a.kind = ok ? k.kind : JA_NONE; a.step = k.step; a.row = k.row;
+      a.canon_off = ok ? (int64_t)(run + ex) : 0; a.canon_len = ok ? k.canon_len : 0;
+      a.dv_len = ok ? k.key_len - k.canon_len : 0;
+      a.h = k.h;
+      acts[i] = a;
+    }
+    run += tot;
+  }
+}
+
+// origin: the owners' answers (in send order) -> the selection byte of each own action
+__global__ __launch_bounds__(NT) void k_own_tail_finish(const int32_t* __restrict__ send_src, const uint8_t* __restrict__ back,
+                                                        long long n, uint8_t* __restrict__ jsel) {
+  for (long long i = (long long)blockIdx.x * NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT)
+    jsel[send_src[i]] = back[i] != 0;
+}
+
 // owner side, by hash: flag 1 iff a slot of this rank's commit-tail key table holds exactly h (then
 // the origin sends the row's key for the byte-exact answer), 0: the key is in neither tail set
 __global__ __launch_bounds__(NT) void k_own_lookup(const uint64_t* __restrict__ recv, long long n,
@@ -4783,13 +4909,40 @@ void launch_own_count(const ProbeSet& PS, const uint64_t* rowh, int world, unsig
   long long chunk;
   const int nb = a2a_blocks(PS.total, &chunk);
   hipLaunchKernelGGL(k_own_count, dim3(nb), dim3(NT), 0, s, PS, rowh, world, chunk, bc);
-  hipLaunchKernelGGL(k_a2a_scan, dim3(1), dim3(64), 0, s, bc, nb, world, totals);
+  hipLaunchKernelGGL(k_a2a_scan, dim3(1), dim3(NT), 0, s, bc, nb, world, totals);
 }
 void launch_own_pack(const ProbeSet& PS, const uint64_t* rowh, int world, const unsigned long long* boff, uint64_t* send_h,
                      int32_t* send_g, hipStream_t s) {
   long long chunk;
   const int nb = a2a_blocks(PS.total, &chunk);
   hipLaunchKernelGGL(k_own_pack, dim3(nb), dim3(NT), 0, s, PS, rowh, world, chunk, boff, send_h, send_g);
+}
+void launch_own_tail_count(const DJsonAction* acts, int na, int world, unsigned long long* tot, hipStream_t s) {
+  hipLaunchKernelGGL(k_own_tail_count, dim3(world), dim3(NT), 0, s, acts, na, world, tot);
+}
+void launch_own_tail_pack(const DJsonAction* acts, int na, int world, const unsigned long long* tot, const uint8_t* canon,
+                          OwnerKeyRec* recs, uint8_t* keys, int32_t* send_src, hipStream_t s) {
+  hipLaunchKernelGGL(k_own_tail_pack, dim3(world), dim3(NT), 0, s, acts, na, world, tot, canon, recs, keys, send_src);
+}
+int own_recs_blocks(long long n, long long* chunk) {
+  long long nb = (n + 4095) / 4096;                      // >= 4 Ki records per workgroup
+  if (nb > 1024) nb = 1024;
+  if (nb < 1) nb = 1;
+  *chunk = (n + nb - 1) / nb;
+  if (*chunk < 1) *chunk = 1;
+  return (int)nb;
+}
+void launch_own_recs_acts(const OwnerKeyRec* recs, long long n, long long nbytes, unsigned long long* bsum, int* bad,
+                          unsigned long long* total, DJsonAction* acts, hipStream_t s) {
+  if (n <= 0) return;
+  long long chunk;
+  const int nb = own_recs_blocks(n, &chunk);
+  hipLaunchKernelGGL(k_own_recs_count, dim3(nb), dim3(NT), 0, s, recs, n, chunk, bsum, bad);
+  hipLaunchKernelGGL(k_a2a_scan, dim3(1), dim3(NT), 0, s, bsum, nb, 1, total);
+  hipLaunchKernelGGL(k_own_recs_acts, dim3(nb), dim3(NT), 0, s, recs, n, chunk, bsum, nbytes, acts);
+}
+void launch_own_tail_finish(const int32_t* send_src, const uint8_t* back, long long n, uint8_t* jsel, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_own_tail_finish, dim3(own_grid(n)), dim3(NT), 0, s, send_src, back, n, jsel);
 }
 void launch_own_lookup(const uint64_t* recv, long long n, const Slot* slots, const uint32_t* fp, uint64_t mask,
                        uint8_t* flags, hipStream_t s) {
@@ -4843,7 +4996,9 @@ int warm_kernels() {
       (const void*)k_pack_bits, (const void*)k_a2a_count, (const void*)k_a2a_scan, (const void*)k_a2a_pack,
       (const void*)k_a2a_filter, (const void*)k_a2a_apply, (const void*)k_own_rowhash, (const void*)k_own_count,
       (const void*)k_own_pack, (const void*)k_own_lookup, (const void*)k_own_cand_len, (const void*)k_own_cand_keys,
-      (const void*)k_own_verify, (const void*)k_own_cand_finish};
+      (const void*)k_own_verify, (const void*)k_own_cand_finish, (const void*)k_own_tail_count,
+      (const void*)k_own_tail_pack, (const void*)k_own_tail_finish, (const void*)k_own_recs_count,
+      (const void*)k_own_recs_acts};
   int n = 0;
   for (const void* f : fns) {
     hipFuncAttributes a;

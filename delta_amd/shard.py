@@ -518,10 +518,17 @@ class OwnerComm:
     def _last_run(self):
         import ctypes as C
         from ._lib import lib
-        ms, b = (C.c_double * 4)(), C.c_int64()
-        lib().dk_comm_last_run(self._h, ms, C.byref(b))
-        self.ms = {"tail_exchange": ms[0], "decode_hash": ms[1], "row_exchange": ms[2], "total": ms[3]}
+        ms, b, n = (C.c_double * 8)(), C.c_int64(), C.c_int64()
+        lib().dk_comm_last_run(self._h, ms, C.byref(b), C.byref(n))
+        self.ms = {"tail_exchange": ms[0], "decode_hash": ms[1], "row_exchange": ms[2], "total": ms[3],
+                   "tail_local": ms[4], "decode_local": ms[5], "row_local": ms[6], "collectives": ms[7]}
         self.bytes_sent = int(b.value)
+        self.collectives = int(n.value)
+        st = (C.c_double * 16)()
+        lib().dk_comm_last_steps(self._h, st)
+        names = ("begin", "tail_counts", "tail_pack", "tail_resolve", "reseed", "tail_finish", "run", "ckpt_counts",
+                 "ckpt_pack", "ckpt_lookup", "ckpt_apply", "cand_counts", "cand_pack", "cand_verify", "cand_finish")
+        self.steps_ms = {k: st[i] for i, k in enumerate(names)}
 
     def run_scan(self, scan):
         """The whole owner protocol of one scan run on this rank (dk_replay_owner_run)."""

@@ -502,9 +502,14 @@ int  dk_comm_allreduce_i64(dk_comm* c, int64_t* vals, int32_t n, int32_t op);
 int  dk_comm_alltoallv(dk_comm* c, const void* send, const int64_t* send_bytes, void* recv, const int64_t* recv_bytes,
                        int32_t on_device);
 int  dk_comm_abort(dk_comm* c);
-/* the last owner run: ms[0] commit-tail exchange, ms[1] decode + row hashes, ms[2] row and candidate
- * exchanges, ms[3] total; payload bytes this rank sent to its peers */
-int  dk_comm_last_run(const dk_comm* c, double ms[4], int64_t* bytes_sent);
+/* the last owner run (ms): [0] commit-tail exchange, [1] decode + row hashes, [2] row and candidate
+ * exchanges, [3] total (wall times); [4..6] the local steps' share of [0..2]; [7] time inside
+ * collectives; the payload bytes this rank sent to its peers and the number of collectives */
+int  dk_comm_last_run(const dk_comm* c, double ms[8], int64_t* bytes_sent, int64_t* collectives);
+/* the last owner run's local steps (ms), in dk_owner_side member order: begin, tail_counts, tail_pack,
+ * tail_resolve, reseed, tail_finish, run, ckpt_counts, ckpt_pack, ckpt_lookup, ckpt_apply, cand_counts,
+ * cand_pack, cand_verify, cand_finish */
+int  dk_comm_last_steps(const dk_comm* c, double ms[16]);
 void dk_comm_destroy(dk_comm* c);
 /* dk_replay_set_owner(r, world, rank) first (world = dk_comm_world), the commit tail rebased with the
  * all-reduced batch counts; then this call; then dk_replay_sync as usual. */

@@ -398,6 +398,7 @@ def _loopback_check(table, world, bs, predicate):
     (2, 1024, dict(n_parts=3, row_group_size=3000), None),
     (3, 3, dict(n_parts=1, row_group_size=2500, dv_frac=0.2, ckpt_removes=100, readd_frac=0.2, dup_frac=0.1), None),
     (2, 5, dict(n_parts=4, row_group_size=2000, dv_frac=0.3, with_stats=True), 8_000),
+    (8, 1024, dict(n_parts=8, row_group_size=1000, compression="snappy", readd_frac=0.1, dup_frac=0.05), None),
 ])
 def test_gpu_owner_loopback(tmp_path, world, bs, spec, predicate):
     """The product's owner mode (tail records routed and resolved by their owners, every checkpoint

@@ -10,15 +10,18 @@ Every rank is timed:
   open       prepare (footers, page headers, the commit-tail parse of its files + replay create)
              until its asynchronous open has finished decoding (the ranks run one after another, so
              each rank's H2D and decode have the GPU to themselves, as on its own GPU)
-  exchange   its owner run's commit-tail exchange + row / candidate exchanges (dk_comm_last_run),
-             with all N ranks' exchange kernels sharing this one GPU at the same time (an upper
-             bound of a rank's own)
+  hash       its owner run's decode-and-hash phase: the row key hashes, the routing counts and
+             the row records packed (dk_comm_last_run's local steps of that phase)
+  exchange   the local steps of its owner run's commit-tail and row / candidate exchanges
+             (dk_comm_last_run: each step timed, and with DK_LOCAL_SERIAL=1, the default here, run
+             alone on the device, so a rank's steps do not share the GPU with its peers' as they
+             would not on its own GPU); the wall times of the concurrent run are reported beside it
   transfer   the bytes it sends through the all-to-alls at an assumed per-GPU all-to-all bandwidth
              (--a2a-gbs, default 300 GB/s: 7 xGMI links at ~43 GB/s each) + 30 us per collective
   consume    its scan-file batches consumed as bench.py's JMH-shaped consumer does (sum of add.size
              over the selected rows)
 
-per_rank_ms = open + exchange + transfer + consume; the rehearsed N-GPU step is the max over ranks.
+per_rank_ms = open + hash + exchange + transfer + consume; the rehearsed N-GPU step is the max over ranks.
 Usage: python tools/rehearse_rank.py --world 8 [--config c3] [--workdir DIR] > out.json
 """
 import argparse
@@ -39,7 +42,10 @@ def main():
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--workdir", default=None)
     ap.add_argument("--a2a-gbs", type=float, default=300.0)
+    ap.add_argument("--concurrent", action="store_true", help="ranks' local steps share the GPU (no DK_LOCAL_SERIAL)")
     args = ap.parse_args()
+    if not args.concurrent:
+        os.environ["DK_LOCAL_SERIAL"] = "1"
     import bench
     cfg = bench.CONFIGS[args.config]
     rows = args.rows or cfg["rows"]
@@ -66,7 +72,7 @@ def main():
     snap = K.Table.forPath(eng, work).getLatestSnapshot(eng)
     steps = shard.OwnerComm.table_steps(eng, snap)
     comms = shard.OwnerComm.local(world, steps=steps)
-    collectives = 11                            # per owner run (delta_amd/csrc/dk_comm.cpp)
+    collectives = 11                            # per owner run without a collision (dk_comm.cpp)
     # iteration 0 warms the caching allocators (every rank's blocks, as each rank's process is warm
     # after bench.py's warm-up steps); iteration 1 is reported
     for it in range(2):
@@ -119,12 +125,14 @@ def main():
     per_rank = {}
     for r in range(world):
         m = comms[r].ms
-        ex = m["tail_exchange"] + m["row_exchange"]
-        tr = comms[r].bytes_sent / (args.a2a_gbs * 1e9) * 1e3 + collectives * 0.03
-        per_rank[r] = dict(opened[r], exchange_ms=round(ex, 3), owner_run_ms={k: round(v, 3) for k, v in m.items()},
+        ex = m["tail_local"] + m["row_local"]
+        hs = m["decode_local"]
+        tr = comms[r].bytes_sent / (args.a2a_gbs * 1e9) * 1e3 + comms[r].collectives * 0.03
+        per_rank[r] = dict(opened[r], exchange_ms=round(ex, 3), hash_ms=round(hs, 3), owner_run_ms={k: round(v, 3) for k, v in m.items()},
+                           owner_steps_ms={k: round(v, 3) for k, v in comms[r].steps_ms.items()},
                            bytes_sent=comms[r].bytes_sent, transfer_model_ms=round(tr, 3),
                            consume_ms=round(consume[r][0], 3), selected=consume[r][1],
-                           per_rank_ms=round(opened[r]["open_ms"] + ex + tr + consume[r][0], 2))
+                           per_rank_ms=round(opened[r]["open_ms"] + hs + ex + tr + consume[r][0], 2))
     step = max(v["per_rank_ms"] for v in per_rank.values())
     seen = int(counters[0])
     out = {"world": world, "config": args.config, "rows": rows, "counters": [int(x) for x in counters],
