@@ -238,9 +238,14 @@ enum : int32_t { PO_FIELD = 0, PO_LIT_INT = 1, PO_LIT_STR = 2, PO_LIT_NULL = 3, 
                  PO_SUBSTR = 20,         // SUBSTRING(s, pos[, len]): lit = (uint32)pos | len << 32, arg = has len
                  PO_LIKE_DYN = 21,       // LIKE(s, pattern) with the pattern a value (top) over s (below):
                                          // arg = the escape code point (LikeExpressionEvaluator.eval)
-                 PO_TIMEADD = 22 };      // TIMEADD(ts, millis): ts (below) + millis (top) * 1000, wrapping
+                 PO_TIMEADD = 22,        // TIMEADD(ts, millis): ts (below) + millis (top) * 1000, wrapping
+                 PO_FCMP2 = 23 };        // two float / double / integral values compared after widening:
+                                         // arg = comparison (PO_LT..PO_NSEQ) | double-wide << 8 | form of
+                                         // the lower operand << 12 | of the upper << 16 (FF_*)
+enum : int32_t { FF_INTEGRAL = 0, FF_FLOAT = 1, FF_DOUBLE = 2 };   // a float / double literal: its IEEE bits
 struct DPartProg {
   int32_t n_fields, n_ops;
+  int32_t wide;                    // the program holds PO_FCMP2: k_part_eval_wide (digit buffers in scratch)
   const int32_t* field_type;       // [n_fields] PT_*
   const int32_t* name_off;         // physical column name (map key) in pool
   const int32_t* name_len;

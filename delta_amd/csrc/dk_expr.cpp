@@ -1169,6 +1169,28 @@ struct PartCompiler {
     if (!ka.empty() && !kb.empty() && ka != kb) refuse("comparison of " + ka + " with " + kb + " is not supported");
     push(n == "<" ? PO_LT : n == "<=" ? PO_LE : n == ">" ? PO_GT : n == ">=" ? PO_GE : n == "=" ? PO_EQ : PO_NSEQ);
   }
+  // Two float-typed values with no literal side to plan a threshold from (two columns, two literals):
+  // both operands on the stack, compared on the device after the ImplicitCastExpression widening
+  // (the wider of the two types; PO_FCMP2 parses each float value exactly to its own type).
+  void float_values_cmp(const std::string& n, const Ex& a, const Ex& b) {
+    const std::string ta = type_of(a), tb = type_of(b);
+    auto form = [&](const Ex& x, const std::string& t) {
+      if (!is_float(t) && !is_integral(t)) refuse("comparison of " + ta + " with " + tb + " is not supported");
+      if (x.k == Ex::LIT && is_float(t)) {             // IEEE bits as an integer literal
+        if (x.null) push(PO_LIT_NULL); else push(PO_LIT_INT, 0, (long long)x.bits);
+      } else {
+        operand(x);
+      }
+      return is_integral(t) ? FF_INTEGRAL : t == "float" ? FF_FLOAT : FF_DOUBLE;
+    };
+    const bool swap = need(b) > need(a);
+    int fa, fb;
+    if (swap) { fb = form(b, tb); fa = form(a, ta); } else { fa = form(a, ta); fb = form(b, tb); }
+    const std::string c = swap ? reverse_cmp(n) : n;
+    const int cop = c == "<" ? PO_LT : c == "<=" ? PO_LE : c == ">" ? PO_GT : c == ">=" ? PO_GE : c == "=" ? PO_EQ : PO_NSEQ;
+    const bool dbl = ta == "double" || tb == "double";
+    push(PO_FCMP2, cop | (int)dbl << 8 | (swap ? fb : fa) << 12 | (swap ? fa : fb) << 16);
+  }
   void float_cmp(std::string n, const Ex& l0, const Ex& r0) {
     const Ex* left = &l0;
     const Ex* right = &r0;
@@ -1176,8 +1198,7 @@ struct PartCompiler {
     const std::string ct = type_of(*left), lt = type_of(*right);
     if (!comparable(ct, lt)) unsupported_expr(n, ct, lt);
     std::string phys, tt;
-    if (!field_ref(*left, &phys, &tt) || right->k != Ex::LIT)
-      refuse("float partition comparison needs a column and a literal");
+    if (!field_ref(*left, &phys, &tt) || right->k != Ex::LIT) { float_values_cmp(n, l0, r0); return; }
     if (!is_float(ct) && !is_integral(ct)) refuse("comparison of " + ct + " with " + lt + " is not supported");
     auto cmp_code = [](const std::string& c) {
       return c == "<" ? PO_LT : c == "<=" ? PO_LE : c == ">" ? PO_GT : c == ">=" ? PO_GE : c == "=" ? PO_EQ : PO_NSEQ;

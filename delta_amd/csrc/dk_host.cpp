@@ -3957,6 +3957,7 @@ static int install_part(DevPart& d, const dk_program& src) {
   P.arg = (const int32_t*)(b + offs[5]);
   P.lit = (const int64_t*)(b + offs[6]);
   P.pool = b + offs[7];
+  for (int32_t o : src.op) P.wide |= o == PO_FCMP2;
   d.P = P;
   return 0;
 }

@@ -3344,6 +3344,167 @@ __device__ bool java_parse_fp(const uint8_t* s, int32_t n, int32_t* a, int32_t* 
   return true;
 }
 
+// Correctly rounded decimal -> IEEE binary32 / binary64 (FloatingDecimal's result: nearest, ties to
+// even, overflow to infinity, gradual underflow) for comparisons between two float-typed values, where
+// no threshold can be planned on the host. The exact decimal value 0.d1d2..dn x 10^dp is held as digits
+// (up to FD_DIGITS of them; the exact expansion of any binary64 halfway point fits, longer inputs keep
+// a sticky `trunc` bit) and scaled by binary shifts of at most 60 bits until it lies in [1/2, 1); the
+// shift count is the binary exponent, and the mantissa is the integer part of the value times
+// 2^(mantissa bits + 1), rounded on the digits that remain. Only k_part_eval_wide carries these
+// buffers (private scratch), so ordinary partition programs keep a scratch-free kernel.
+constexpr int FD_DIGITS = 800;
+struct FDec {
+  uint8_t d[FD_DIGITS];
+  int32_t nd, dp;
+  bool trunc;
+};
+
+__device__ void fd_trim(FDec& x) {
+  while (x.nd > 0 && x.d[x.nd - 1] == 0) x.nd--;
+  if (x.nd == 0) x.dp = 0;
+}
+
+// a digit span java_parse_fp accepted (sign, digits, optional fraction and exponent, no suffix)
+__device__ void fd_read(FDec& x, const uint8_t* s, int32_t n, bool* neg) {
+  int32_t i = 0;
+  *neg = false;
+  if (i < n && (s[i] == '+' || s[i] == '-')) { *neg = s[i] == '-'; i++; }
+  x.nd = 0; x.dp = 0; x.trunc = false;
+  bool dot = false;
+  for (; i < n; i++) {
+    const uint8_t c = s[i];
+    if (c == '.') { dot = true; x.dp = x.nd; continue; }
+    if (c < '0' || c > '9') break;
+    if (c == '0' && x.nd == 0) { x.dp--; continue; }        // leading zeros only move the point
+    if (x.nd < FD_DIGITS) x.d[x.nd++] = (uint8_t)(c - '0');
+    else if (c != '0') x.trunc = true;
+  }
+  if (!dot) x.dp = x.nd;
+  if (i < n && (s[i] | 0x20) == 'e') {
+    i++;
+    int sg = 1;
+    if (i < n && (s[i] == '+' || s[i] == '-')) { sg = s[i] == '-' ? -1 : 1; i++; }
+    int32_t e = 0;
+    for (; i < n && s[i] >= '0' && s[i] <= '9'; i++) if (e < 1000000) e = e * 10 + (s[i] - '0');
+    x.dp += sg * e;
+  }
+  fd_trim(x);
+}
+
+// x /= 2^k, 1 <= k <= 60
+__device__ void fd_shr(FDec& x, int k) {
+  int32_t r = 0, w = 0;
+  unsigned long long n = 0;
+  for (; (n >> k) == 0; r++) {
+    if (r >= x.nd) {
+      if (n == 0) { x.nd = 0; x.dp = 0; return; }
+      while ((n >> k) == 0) { n *= 10; r++; }
+      break;
+    }
+    n = n * 10 + x.d[r];
+  }
+  x.dp -= r - 1;
+  const unsigned long long mask = (1ull << k) - 1;
+  for (; r < x.nd; r++) {
+    const uint8_t c = x.d[r];
+    x.d[w++] = (uint8_t)(n >> k);
+    n = (n & mask) * 10 + c;
+  }
+  while (n > 0) {
+    const uint8_t dig = (uint8_t)(n >> k);
+    n &= mask;
+    if (w < FD_DIGITS) x.d[w++] = dig;
+    else if (dig > 0) x.trunc = true;
+    n *= 10;
+  }
+  x.nd = w;
+  fd_trim(x);
+}
+
+// x *= 2^k, 1 <= k <= 60: the carry out of a dry pass gives the new digit count, then the product is
+// written right to left in place (each write lands at or past the digit just read)
+__device__ void fd_shl(FDec& x, int k) {
+  unsigned long long n = 0;
+  for (int32_t r = x.nd - 1; r >= 0; r--) n = (n + ((unsigned long long)x.d[r] << k)) / 10;
+  int32_t delta = 0;
+  for (; n > 0; n /= 10) delta++;
+  int32_t w = x.nd + delta;
+  n = 0;
+  for (int32_t r = x.nd - 1; r >= 0; r--) {
+    n += (unsigned long long)x.d[r] << k;
+    const unsigned long long q = n / 10;
+    const uint8_t rem = (uint8_t)(n - q * 10);
+    if (--w < FD_DIGITS) x.d[w] = rem;
+    else if (rem) x.trunc = true;
+    n = q;
+  }
+  while (n > 0) {
+    const unsigned long long q = n / 10;
+    const uint8_t rem = (uint8_t)(n - q * 10);
+    if (--w < FD_DIGITS) x.d[w] = rem;
+    else if (rem) x.trunc = true;
+    n = q;
+  }
+  x.nd = min(x.nd + delta, FD_DIGITS);
+  x.dp += delta;
+  fd_trim(x);
+}
+
+__device__ void fd_shift(FDec& x, int k) {
+  for (; k > 60; k -= 60) fd_shr(x, 60);
+  for (; k < -60; k += 60) fd_shl(x, 60);
+  if (k > 0) fd_shr(x, k);
+  else if (k < 0) fd_shl(x, -k);
+}
+
+// the integer part, plus one when the fraction rounds up (above a half, or a half with an odd last
+// digit or sticky digits beyond the buffer)
+__device__ unsigned long long fd_round(const FDec& x) {
+  unsigned long long m = 0;
+  int32_t i = 0;
+  for (; i < x.dp && i < x.nd; i++) m = m * 10 + x.d[i];
+  for (; i < x.dp; i++) m *= 10;
+  const int32_t p = x.dp;
+  bool up = false;
+  if (p >= 0 && p < x.nd) {
+    if (x.d[p] == 5 && p + 1 == x.nd) up = x.trunc || (p > 0 && (x.d[p - 1] & 1));
+    else up = x.d[p] >= 5;
+  }
+  return m + up;
+}
+
+// IEEE bits of the digit span s[0, n): mb mantissa bits, eb exponent bits (23, 8 or 52, 11)
+__device__ unsigned long long fd_bits(FDec& x, const uint8_t* s, int32_t n, int mb, int eb) {
+  bool neg;
+  fd_read(x, s, n, &neg);
+  const int bias = -((1 << (eb - 1)) - 1);
+  const int emax = (1 << eb) - 1;
+  unsigned long long mant = 0;
+  int e = bias;
+  bool inf = false;
+  if (x.nd > 0) {
+    if (x.dp > 310) inf = true;
+    else if (x.dp >= -330) {
+      const int pw[9] = {1, 3, 6, 9, 13, 16, 19, 23, 26};   // 2^pw[i] < 10^i
+      e = 0;
+      while (x.dp > 0) { const int k = x.dp >= 9 ? 27 : pw[x.dp]; fd_shift(x, k); e += k; }
+      while (x.dp < 0 || (x.dp == 0 && x.d[0] < 5)) { const int k = -x.dp >= 9 ? 27 : pw[-x.dp]; fd_shift(x, -k); e -= k; }
+      e--;                                                  // value in [1, 2) x 2^e
+      if (e < bias + 1) { fd_shift(x, bias + 1 - e); e = bias + 1; }
+      if (e - bias >= emax) inf = true;
+      else {
+        fd_shift(x, -(mb + 1));
+        mant = fd_round(x);
+        if (mant == (2ull << mb)) { mant >>= 1; e++; if (e - bias >= emax) inf = true; }
+        if (!(mant & (1ull << mb))) e = bias;               // subnormal (or zero)
+      }
+    }
+  }
+  if (inf) { mant = 0; e = emax + bias; }
+  return (mant & ((1ull << mb) - 1)) | ((unsigned long long)((e - bias) & emax) << mb) |
+         ((unsigned long long)neg << (mb + eb));
+}
+
 struct PVal {           // stack value: kind 0 null, 1 integer, 2 string, 3 boolean, 4 decimal text,
   int32_t kind, len;    // 5 float / double (p, len: digit span; v: special code | negative zero << 8)
   long long v;
@@ -3482,6 +3643,33 @@ __device__ bool part_field(const DPartProg& P, const MapRows& M, long long row, 
 // 1 true, 0 false, -1 null; *err on a malformed partition value. Every FIELD op deserializes its
 // value, so every referenced column of every row is parsed (the reference deserializes whole vectors,
 // DefaultExpressionEvaluator does not short-circuit AND / OR).
+// one operand of PO_FCMP2 as a double: an integral value cast to the comparison type first (to float
+// when neither side is double: ImplicitCastExpression rounds long -> float directly); a float value
+// parsed to binary32 and widened exactly
+__device__ double fp_operand(const PVal& v, int form, bool dbl, FDec& x) {
+  if (form == FF_INTEGRAL) return dbl ? (double)v.v : (double)(float)v.v;
+  if (v.kind == 1)                                     // a literal: its IEEE bits
+    return form == FF_FLOAT ? (double)__uint_as_float((uint32_t)v.v) : __longlong_as_double(v.v);
+  const int code = (int)(v.v & 255);
+  if (code == 1) return __longlong_as_double(0x7ff8000000000000ll);
+  if (code == 2) return __longlong_as_double(0x7ff0000000000000ll);
+  if (code == 3) return __longlong_as_double((long long)0xfff0000000000000ull);
+  if (code == 4) return (v.v & 256) ? -0.0 : 0.0;
+  if (form == FF_FLOAT) return (double)__uint_as_float((uint32_t)fd_bits(x, v.p, v.len, 23, 8));
+  return __longlong_as_double((long long)fd_bits(x, v.p, v.len, 52, 11));
+}
+
+// Float.compare / Double.compare: NaN above everything and equal to itself, -0.0 below 0.0
+__device__ int java_fp_compare(double a, double b) {
+  const bool an = a != a, bn = b != b;
+  if (an || bn) return (int)an - (int)bn;
+  if (a < b) return -1;
+  if (a > b) return 1;
+  const bool sa = signbit(a), sb = signbit(b);
+  return sa == sb ? 0 : sa ? -1 : 1;
+}
+
+template <bool WIDE>
 __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bool* err) {
   PVal st[PP_STACK];
   int sp = 0;
@@ -3571,6 +3759,30 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
         if (m < 0) { *err = true; return -1; }           // "LIKE expression has invalid escape sequence"
         a.kind = 3; a.v = m;
       }
+    } else if (op == PO_FCMP2) {                         // float-typed values compared (widened first)
+      if constexpr (WIDE) {
+        if (sp < 2) return -1;
+        const PVal b = st[--sp];
+        const PVal a = st[--sp];
+        const int ar = P.arg[i], cop = ar & 255;
+        const bool dbl = (ar >> 8) & 1;
+        PVal r;
+        r.kind = 3;
+        if (cop == PO_NSEQ && (a.kind == 0 || b.kind == 0)) {
+          r.v = a.kind == 0 && b.kind == 0;
+        } else if (a.kind == 0 || b.kind == 0) {
+          r.kind = 0;
+        } else {
+          FDec x;
+          const double av = fp_operand(a, (ar >> 12) & 15, dbl, x);
+          const double bv = fp_operand(b, (ar >> 16) & 15, dbl, x);
+          const int c = java_fp_compare(av, bv);
+          r.v = cop == PO_LT ? c < 0 : cop == PO_LE ? c <= 0 : cop == PO_GT ? c > 0 : cop == PO_GE ? c >= 0 : c == 0;
+        }
+        st[sp++] = r;
+      } else {
+        return -1;                                       // routed to k_part_eval_wide by the host
+      }
     } else if (op == PO_TIMEADD) {                       // DefaultExpressionEvaluator.visitTimeAdd (:593-626)
       if (sp < 2) return -1;
       const PVal d = st[--sp];
@@ -3630,17 +3842,26 @@ __device__ int part_eval(const DPartProg& P, const MapRows& M, long long row, bo
   return st[0].v ? 1 : 0;
 }
 
-__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg P,
-                                                  uint8_t* __restrict__ sel, DState* __restrict__ st) {
+template <bool WIDE>
+__device__ __forceinline__ void part_eval_rows(const MapRows& M, const DPartProg& P, uint8_t* __restrict__ sel,
+                                               DState* __restrict__ st) {
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < M.n;
        r += (long long)gridDim.x * blockDim.x) {
     const long long row = M.act_row ? M.act_row[r] : r;
     if (row < 0) continue;                              // not an add action
     bool err = false;
-    const int res = part_eval(P, M, row, &err);
+    const int res = part_eval<WIDE>(P, M, row, &err);
     if (err) { set_err(st, E_PART, M.row_tag + r, 0); continue; }
     if (res != 1 && sel[r]) sel[r] = 0;
   }
+}
+__global__ __launch_bounds__(NT) void k_part_eval(MapRows M, const DPartProg P,
+                                                  uint8_t* __restrict__ sel, DState* __restrict__ st) {
+  part_eval_rows<false>(M, P, sel, st);
+}
+__global__ __launch_bounds__(NT) void k_part_eval_wide(MapRows M, const DPartProg P,
+                                                       uint8_t* __restrict__ sel, DState* __restrict__ st) {
+  part_eval_rows<true>(M, P, sel, st);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -4522,7 +4743,8 @@ void launch_part_eval(const MapRows& M, const DPartProg& P, uint8_t* sel, DState
   if (M.n <= 0) return;
   const long long want = (M.n + NT - 1) / NT;
   const unsigned grid = (unsigned)(want < 2048 ? want : 2048);
-  hipLaunchKernelGGL(k_part_eval, dim3(grid), dim3(NT), 0, s, M, P, sel, st);
+  if (P.wide) hipLaunchKernelGGL(k_part_eval_wide, dim3(grid), dim3(NT), 0, s, M, P, sel, st);
+  else hipLaunchKernelGGL(k_part_eval, dim3(grid), dim3(NT), 0, s, M, P, sel, st);
 }
 // First row whose definition level reaches min_def (LogReplay.loadTableProtocolAndMetadata takes
 // the first non-null protocol / metaData row, internal/replay/LogReplay.java:247-296): a grid-stride
