@@ -94,6 +94,9 @@ struct DPosChunk {
   int32_t pad;
 };
 constexpr int DK_POS_CHUNK = 16384;
+// candidate offsets k_pos_count keeps per chunk: a value takes >= 4 region bytes (an empty string is
+// its length prefix alone), so a chunk holds at most DK_POS_CHUNK / 4 of them
+constexpr int DK_POS_CAP = DK_POS_CHUNK / 4 + 8;
 // k_expand record kinds (per-page work lists built on the device from per-group counts)
 enum : int { EX_TILE = 0, EX_POSCHUNK = 1, EX_FRAG = 2, EX_SEG = 3 };
 

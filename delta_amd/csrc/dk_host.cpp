@@ -1122,7 +1122,7 @@ struct dk_parquet {
   DBuf d_ltiles, d_runs;     // level tiles (DTile) and hybrid-stream run tables (Seg)
   int n_ltiles = 0;
   DBuf d_pchunks;            // string-position chunks (DPosChunk)
-  DBuf d_pos_scratch;        // k_pos_count's candidates, DK_POS_CHUNK / 5 + 8 int16 offsets per chunk
+  DBuf d_pos_scratch;        // k_pos_count's candidates, DK_POS_CAP int16 offsets per chunk
   int n_pchunks = 0;
   // string-copy tile table: (page, first value) per 256-value tile of every PLAIN BYTE_ARRAY data
   // page, grouped by column (col_tile0[c] = first tile of column c; col_tile0[n_cols] = total)
@@ -1701,7 +1701,7 @@ static int prepare(dk_parquet* p) {
       pbase.push_back(pbase.back() + pg.npchunk);
     }
     p->n_pchunks = (int)pbase.back();
-    if (p->d_pos_scratch.alloc(((size_t)p->n_pchunks * (DK_POS_CHUNK / 5 + 8) + 8) * 2)) return 1;
+    if (p->d_pos_scratch.alloc(((size_t)p->n_pchunks * DK_POS_CAP + 8) * 2)) return 1;
     if (expand(p, us, p->d_pchunks, ppage, pbase, EX_POSCHUNK, sizeof(DPosChunk)) ||
         expand(p, us, p->d_ltiles, tpage, tbase, EX_TILE, sizeof(DTile)))
       return 1;

@@ -389,9 +389,8 @@ struct SnapRegWin {
   }
 };
 
-// snap_parse over a register window
-__device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_t p, int32_t* adv, int32_t* len) {
-  const uint64_t d = W.at(p);
+// one tag at p from its first 8 bytes d (low byte first)
+__device__ __forceinline__ bool snap_parse_d(uint64_t d, int64_t clen, int64_t p, int32_t* adv, int32_t* len) {
   const uint32_t tag = (uint32_t)d & 0xff;
   const int kind = tag & 3;
   if (kind == 0) {
@@ -411,6 +410,123 @@ __device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_
   *adv = hdr;
   *len = kind == 1 ? (int32_t)(((tag >> 2) & 7) + 4) : (int32_t)((tag >> 2) + 1);
   return true;
+}
+
+// snap_parse over a register window
+__device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_t p, int32_t* adv, int32_t* len) {
+  return snap_parse_d(W.at(p), clen, p, adv, len);
+}
+
+// k_snap_walk with the stream staged through LDS (the default, DK_SF_WALK_LDS): a wave's 64 lanes walk
+// 64 segments in rounds of SW_STEP stream bytes. Each round the wave loads every live segment's next
+// window (SW_STEP + 32 bytes from the segment's 16-byte aligned base, so a tag header starting in the
+// round's SW_STEP bytes is whole) with coalesced dwordx4 loads -- consecutive lanes, consecutive 16
+// bytes -- into its LDS slots, then each lane parses the tags that start in its window from LDS. Every
+// stream line is fetched once per segment, where per-lane register windows (one load per ~20 bytes
+// parsed, 64 different lines per load instruction) had each line fetched again and again once 2k
+// resident lanes per CU outgrew the L2.
+#ifndef DK_SF_WALK_LDS
+#define DK_SF_WALK_LDS 1
+#endif
+#ifndef DK_SF_WALK_PF
+#define DK_SF_WALK_PF 0             // round r + 1's loads issued before round r's parse (slower: VGPRs)
+#endif
+#ifndef DK_SF_WALK_STEP
+#define DK_SF_WALK_STEP 128
+#endif
+#ifndef DK_SF_LINK_WIN
+#define DK_SF_LINK_WIN 0             // 1: slower (415 vs 322 us, profiles/r06/walk_ab)
+#endif
+constexpr int SW_STEP = DK_SF_WALK_STEP;
+constexpr int SW_BLK = (SW_STEP + 32) / 16;      // 16-byte blocks staged per segment and round
+constexpr int SW_SLOT = SW_BLK * 16;
+
+__global__ __launch_bounds__(NT) void k_snap_walk_lds(SnapCtx X) {
+  __shared__ u32x4 win[NT / 64][64 * SW_BLK];
+  u32x4* W = win[threadIdx.x >> 6];
+  const uint32_t* W32 = (const uint32_t*)W;
+  const int lane = threadIdx.x & 63;
+  const int k = X.k0 + blockIdx.x * NT + threadIdx.x;
+  const uint8_t* in = nullptr;
+  uint8_t* out;
+  int64_t clen = 0, ulen, lv, p = 0, end = 0, s0 = 0;
+  int32_t o = 0, n = 0;
+  bool dead = false, live = false, ok = false;
+  if (k < X.k1) {
+    const int ci = X.spage[k];
+    const int j = k - X.sbase[ci];
+    s0 = (int64_t)j * SNAP_SEG;
+    if (snap_page(X, ci, &in, &clen, &out, &ulen, &lv)) {
+      ok = true;
+      p = s0;
+      end = s0 + SNAP_SEG < clen ? s0 + SNAP_SEG : clen;
+      if (j == 0) { uint64_t un; p = snap_preamble(in, clen, &un); }
+      dead = p < 0;
+      live = !dead && p < end;
+    }
+  }
+  SnapBits B{k < X.k1 ? snap_seg_bits(X, k) : nullptr, s0};
+  const uint64_t ab = ok ? ((uint64_t)(uintptr_t)(in + s0) & ~15ull) : 0;   // the window's aligned base
+  const int64_t w0 = ok ? s0 - (int64_t)((uint64_t)(uintptr_t)(in + s0) - ab) : 0;
+  const uint32_t ab_lo = (uint32_t)ab, ab_hi = (uint32_t)(ab >> 32);
+  // the blocks of round r for the segments whose lanes set `want` (coalesced: lane L, step i loads
+  // block L + 64 i of the wave's 64 windows)
+  auto stage = [&](int r, bool want, u32x4* v) {
+#pragma unroll
+    for (int i = 0; i < SW_BLK; i++) {
+      const int b = lane + 64 * i, q = b / SW_BLK, t = b - q * SW_BLK;
+      const uint64_t qa = ((uint64_t)(uint32_t)__shfl((int)ab_hi, q) << 32) | (uint32_t)__shfl((int)ab_lo, q);
+      v[i] = u32x4{0u, 0u, 0u, 0u};
+      if (__shfl((int)want, q)) v[i] = *(const GAS u32x4*)(uintptr_t)(qa + (uint64_t)r * SW_STEP + 16 * t);
+    }
+  };
+#if DK_SF_WALK_PF
+  u32x4 nx[SW_BLK];
+  stage(0, live, nx);
+#endif
+  for (int r = 0; __any(live); r++) {
+    const int64_t wr = w0 + (int64_t)r * SW_STEP;
+    const bool need = live && p < wr + SW_STEP;       // this lane parses in this round
+#if DK_SF_WALK_PF
+    // round r's blocks arrived during round r - 1's parse; round r + 1's are issued before this parse
+#pragma unroll
+    for (int i = 0; i < SW_BLK; i++) W[lane + 64 * i] = nx[i];
+    stage(r + 1, live && wr + SW_STEP < end, nx);
+#else
+    if (!__any(need)) continue;
+    {
+      u32x4 v[SW_BLK];
+      stage(r, need, v);
+#pragma unroll
+      for (int i = 0; i < SW_BLK; i++) W[lane + 64 * i] = v[i];
+    }
+#endif
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (need) {
+      const int64_t wend = wr + SW_STEP < end ? wr + SW_STEP : end;
+      while (p < wend) {
+        const int off = lane * SW_SLOT + (int)(p - wr);
+        const uint64_t d = ((((uint64_t)W32[(off >> 2) + 1]) << 32) | W32[off >> 2]) >> (8 * (off & 3));
+        int32_t adv, len;
+        if (!snap_parse_d(d, clen, p, &adv, &len)) { dead = true; break; }
+        if (n < SNAP_REC) { X.w_pos[(int64_t)n * X.nseg + k] = (int32_t)p; X.w_cum[(int64_t)n * X.nseg + k] = o; n++; }
+        B.mark(p);
+        o += len;
+        p += adv;
+      }
+      if (dead || p >= end) live = false;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (k >= X.k1) return;
+  B.finish(-1);
+  X.w_exit[k] = (!ok || dead) ? -1 : (int32_t)p;
+  X.w_out[k] = o;
+  X.w_npos[k] = n;
 }
 
 __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
@@ -445,6 +561,10 @@ __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
 
 // true exit / output of segment j entered at e (serial walk, merging with the walker's recorded
 // positions when `merge`)
+// (WIN: tags parse from a register window, one load per window instead of a dependent load pair per
+// tag -- k_snap_link, whose lanes that never meet the walker's recorded positions walk the whole
+// segment and set the kernel's duration; k_snap_fix keeps the per-tag loads, its VGPR budget is spent)
+template <bool WIN = false>
 __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, const uint8_t* in, int64_t clen, int64_t e,
                                               bool merge, int32_t* tout, int32_t* texit, bool bits = false) {
   const int64_t end = (int64_t)j * SNAP_SEG + SNAP_SEG < clen ? (int64_t)j * SNAP_SEG + SNAP_SEG : clen;
@@ -457,6 +577,7 @@ __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, co
   const int n = merge ? X.w_npos[k] : 0;
   int jj = 0;
   int32_t pj = n > 0 ? X.w_pos[k] : 0;
+  SnapRegWin W{in};
   while (true) {
     while (jj < n && pj < p) { jj++; pj = jj < n ? X.w_pos[(int64_t)jj * X.nseg + k] : 0; }
     if (jj < n && pj == p) {                 // joined the walker's chain
@@ -467,7 +588,8 @@ __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, co
     }
     if (p >= end) { *tout = o; *texit = (int32_t)p; B.finish(-1); return; }
     int32_t adv, len;
-    if (!snap_parse(in, clen, p, &adv, &len)) { *tout = o; *texit = -1; B.finish(-1); return; }
+    const bool good = WIN ? snap_parse_w(W, clen, p, &adv, &len) : snap_parse(in, clen, p, &adv, &len);
+    if (!good) { *tout = o; *texit = -1; B.finish(-1); return; }
     B.mark(p);
     o += len;
     p += adv;
@@ -491,7 +613,7 @@ __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
       e = X.w_exit[k - 1];
       // (the tag-start bits from e to where it meets the walker are written on the way: they are the
       // true chain's whenever e is the true entry, which k_snap_fix checks)
-      snap_seg_from(X, k, j, in, clen, e, true, &tout, &tex, X.tbits != nullptr);
+      snap_seg_from<DK_SF_LINK_WIN>(X, k, j, in, clen, e, true, &tout, &tex, X.tbits != nullptr);
     }
   }
   X.t_entry[k] = e;
@@ -1346,7 +1468,7 @@ __device__ __forceinline__ uint32_t pos_cand_mask(const StrRegion& S, int64_t i)
 // chunks and moves every chunk's offsets to its value indexes: the region is read once (the old
 // second pass re-read it to write the positions), and no workgroup waits on another (a look-back
 // over the chunks' status words stalled when several slices' launches shared the chip).
-constexpr int POS_CAP = DK_POS_CHUNK / 5 + 8;    // a value takes >= 5 region bytes: <= 3277 per chunk
+constexpr int POS_CAP = DK_POS_CAP;
 __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chunks, const DPage* __restrict__ pages,
                                                   const uint8_t* __restrict__ arena, int32_t* __restrict__ pos,
                                                   DPosChunk* __restrict__ pcs_all, int pc0, int16_t* __restrict__ scratch) {
@@ -1380,7 +1502,7 @@ __global__ __launch_bounds__(NT) void k_pos_count(const DChunk* __restrict__ chu
   }
   __syncthreads();
   const int cnt = run;
-  const bool fits = cnt <= POS_CAP;                 // (more is impossible for a real chain: fallback)
+  const bool fits = cnt <= POS_CAP;                 // (more is impossible for a length chain: fallback)
   bool bad = !fits;
   int16_t* slot = scratch + (int64_t)gi * POS_CAP;
   for (int k = threadIdx.x; fits && k < cnt; k += NT) {
@@ -4342,7 +4464,8 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
     if (phase == 0) {
       (void)hipMemsetAsync(X.serial + X.c0, 0, (size_t)n_cp * 4, s);
       if (X.tbits && g > 0) {             // tag-start bitmap: speculative walk + link
-        hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
+        if (DK_SF_WALK_LDS) hipLaunchKernelGGL(k_snap_walk_lds, dim3(g), dim3(NT), 0, s, X);
+        else hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
         hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
       }
     } else if (phase == 1) {
@@ -4355,7 +4478,8 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
   }
   if (phase == 0) {
     if (g > 0) {
-      hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
+      if (DK_SF_WALK_LDS) hipLaunchKernelGGL(k_snap_walk_lds, dim3(g), dim3(NT), 0, s, X);
+      else hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
       hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
     }
   } else if (phase == 1) {
@@ -5206,7 +5330,7 @@ namespace dk {
 // getScanFiles (round-3 cold snapshot load: 242 ms, 5 ms warm). Returns the kernels touched.
 int warm_kernels() {
   const void* fns[] = {
-      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
+      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_walk_lds, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
       (const void*)k_snap_frag, (const void*)k_snappy_serial, (const void*)k_pos_count,
       (const void*)k_pos_scan, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
