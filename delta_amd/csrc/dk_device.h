@@ -69,6 +69,8 @@ struct SnapCtx {
   int32_t* w_npos;           // walker: recorded positions
   int32_t* w_pos;            // [DK_SNAP_REC][nseg] tag positions
   int32_t* w_cum;            // [DK_SNAP_REC][nseg] walker output before that tag
+  int32_t* relink;           // segments k_snap_link hands to the staged relink walk (or null: no budget),
+  int32_t* relink_n;         // a launch's at relink[k0 ...], counted in relink_n[k0] (slices run concurrently)
   int32_t* t_entry;          // true entry (link: speculative; fix: verified)
   int32_t* t_out;            // true output bytes
   int32_t* t_exit;           // true exit (-1: malformed)

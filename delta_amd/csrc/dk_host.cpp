@@ -1248,6 +1248,7 @@ static void sizing_stages(dk_parquet* p, hipStream_t s, const PRange& R) {
     const int64_t ns = p->n_segs;
     X.w_exit = ws; X.w_out = ws + ns; X.w_npos = ws + 2 * ns; X.t_entry = ws + 3 * ns; X.t_out = ws + 4 * ns;
     X.t_exit = ws + 5 * ns; X.w_pos = ws + 6 * ns; X.w_cum = ws + (6 + DK_SNAP_REC) * ns;
+    X.relink = ws + (6 + 2 * DK_SNAP_REC) * ns; X.relink_n = ws + (7 + 2 * DK_SNAP_REC) * ns;
     X.fbase = p->d_fbase.as<int32_t>(); X.fstart = p->d_fstart.as<int64_t>(); X.serial = p->d_serial.as<int32_t>();
     X.t_ob = p->d_snap_ob.as<int64_t>(); X.fseg = p->d_fseg.as<int32_t>();
     X.k0 = R.s0; X.k1 = R.s1; X.c0 = R.ca;
@@ -1719,7 +1720,7 @@ static int prepare(dk_parquet* p) {
         expand(p, us, p->d_fwork, none, fb, EX_FRAG, sizeof(int2)) || p->d_fstart.alloc((size_t)p->n_frags * 8) ||
         p->d_serial.alloc(cpage.size() * 4) || upload_zc(p, p->d_sbase, sbase.data(), sbase.size() * 4, us) ||
         expand(p, us, p->d_spage, none, sb, EX_SEG, 4) ||
-        p->d_snapws.alloc((size_t)sbase.back() * 4 * (6 + 2 * DK_SNAP_REC)) ||
+        p->d_snapws.alloc((size_t)sbase.back() * 4 * (8 + 2 * DK_SNAP_REC) + 64) ||
         p->d_snap_ob.alloc((size_t)sbase.back() * 8 + 8) || p->d_fseg.alloc((size_t)p->n_frags * 4 + 4))
       return 1;
     p->n_segs = sbase.back();

@@ -429,10 +429,16 @@ __device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_
 #define DK_SF_WALK_LDS 1
 #endif
 #ifndef DK_SF_WALK_PF
-#define DK_SF_WALK_PF 0             // round r + 1's loads issued before round r's parse (slower: VGPRs)
+#define DK_SF_WALK_PF 0             // walk: round r + 1's loads issued before round r's parse (slower: VGPRs)
+#endif
+#ifndef DK_SF_RELINK_PF
+#define DK_SF_RELINK_PF 0           // relink: prefetching the next round measured equal (profiles/r06/walk_ab)
 #endif
 #ifndef DK_SF_WALK_STEP
 #define DK_SF_WALK_STEP 128
+#endif
+#ifndef DK_SF_LINK_BUDGET
+#define DK_SF_LINK_BUDGET 32         // k_snap_link tags before a segment goes to the staged relink pass
 #endif
 #ifndef DK_SF_LINK_WIN
 #define DK_SF_LINK_WIN 0             // 1: slower (415 vs 322 us, profiles/r06/walk_ab)
@@ -441,18 +447,28 @@ constexpr int SW_STEP = DK_SF_WALK_STEP;
 constexpr int SW_BLK = (SW_STEP + 32) / 16;      // 16-byte blocks staged per segment and round
 constexpr int SW_SLOT = SW_BLK * 16;
 
+// RELINK: the same staged walk from a segment's linked entry (X.t_entry) for the segments k_snap_link
+// gave up on (X.relink[k0 + i] for i < X.relink_n[k0]): their true output, exit and tag-start bits
+template <bool RELINK>
 __global__ __launch_bounds__(NT) void k_snap_walk_lds(SnapCtx X) {
   __shared__ u32x4 win[NT / 64][64 * SW_BLK];
   u32x4* W = win[threadIdx.x >> 6];
   const uint32_t* W32 = (const uint32_t*)W;
   const int lane = threadIdx.x & 63;
-  const int k = X.k0 + blockIdx.x * NT + threadIdx.x;
+  int k = X.k0 + blockIdx.x * NT + threadIdx.x;
+  bool valid = k < X.k1;
+  if (RELINK) {
+    const int idx = blockIdx.x * NT + threadIdx.x;
+    valid = idx < X.relink_n[X.k0];
+    k = valid ? X.relink[X.k0 + idx] : 0;
+  }
+  if (RELINK && !__any(valid)) return;
   const uint8_t* in = nullptr;
   uint8_t* out;
   int64_t clen = 0, ulen, lv, p = 0, end = 0, s0 = 0;
   int32_t o = 0, n = 0;
   bool dead = false, live = false, ok = false;
-  if (k < X.k1) {
+  if (valid) {
     const int ci = X.spage[k];
     const int j = k - X.sbase[ci];
     s0 = (int64_t)j * SNAP_SEG;
@@ -460,12 +476,13 @@ __global__ __launch_bounds__(NT) void k_snap_walk_lds(SnapCtx X) {
       ok = true;
       p = s0;
       end = s0 + SNAP_SEG < clen ? s0 + SNAP_SEG : clen;
-      if (j == 0) { uint64_t un; p = snap_preamble(in, clen, &un); }
+      if (RELINK) p = X.t_entry[k];
+      else if (j == 0) { uint64_t un; p = snap_preamble(in, clen, &un); }
       dead = p < 0;
       live = !dead && p < end;
     }
   }
-  SnapBits B{k < X.k1 ? snap_seg_bits(X, k) : nullptr, s0};
+  SnapBits B{valid ? snap_seg_bits(X, k) : nullptr, s0};
   const uint64_t ab = ok ? ((uint64_t)(uintptr_t)(in + s0) & ~15ull) : 0;   // the window's aligned base
   const int64_t w0 = ok ? s0 - (int64_t)((uint64_t)(uintptr_t)(in + s0) - ab) : 0;
   const uint32_t ab_lo = (uint32_t)ab, ab_hi = (uint32_t)(ab >> 32);
@@ -480,27 +497,24 @@ __global__ __launch_bounds__(NT) void k_snap_walk_lds(SnapCtx X) {
       if (__shfl((int)want, q)) v[i] = *(const GAS u32x4*)(uintptr_t)(qa + (uint64_t)r * SW_STEP + 16 * t);
     }
   };
-#if DK_SF_WALK_PF
-  u32x4 nx[SW_BLK];
-  stage(0, live, nx);
-#endif
+  constexpr bool PF = RELINK ? DK_SF_RELINK_PF : DK_SF_WALK_PF;
+  u32x4 nx[PF ? SW_BLK : 1];
+  if constexpr (PF) stage(0, live, nx);
   for (int r = 0; __any(live); r++) {
     const int64_t wr = w0 + (int64_t)r * SW_STEP;
     const bool need = live && p < wr + SW_STEP;       // this lane parses in this round
-#if DK_SF_WALK_PF
-    // round r's blocks arrived during round r - 1's parse; round r + 1's are issued before this parse
+    if constexpr (PF) {
+      // round r's blocks arrived during round r - 1's parse; round r + 1's are issued before this parse
 #pragma unroll
-    for (int i = 0; i < SW_BLK; i++) W[lane + 64 * i] = nx[i];
-    stage(r + 1, live && wr + SW_STEP < end, nx);
-#else
-    if (!__any(need)) continue;
-    {
+      for (int i = 0; i < SW_BLK; i++) W[lane + 64 * i] = nx[i];
+      stage(r + 1, live && wr + SW_STEP < end, nx);
+    } else {
+      if (!__any(need)) continue;
       u32x4 v[SW_BLK];
       stage(r, need, v);
 #pragma unroll
       for (int i = 0; i < SW_BLK; i++) W[lane + 64 * i] = v[i];
     }
-#endif
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -511,7 +525,7 @@ __global__ __launch_bounds__(NT) void k_snap_walk_lds(SnapCtx X) {
         const uint64_t d = ((((uint64_t)W32[(off >> 2) + 1]) << 32) | W32[off >> 2]) >> (8 * (off & 3));
         int32_t adv, len;
         if (!snap_parse_d(d, clen, p, &adv, &len)) { dead = true; break; }
-        if (n < SNAP_REC) { X.w_pos[(int64_t)n * X.nseg + k] = (int32_t)p; X.w_cum[(int64_t)n * X.nseg + k] = o; n++; }
+        if (!RELINK && n < SNAP_REC) { X.w_pos[(int64_t)n * X.nseg + k] = (int32_t)p; X.w_cum[(int64_t)n * X.nseg + k] = o; n++; }
         B.mark(p);
         o += len;
         p += adv;
@@ -522,8 +536,13 @@ __global__ __launch_bounds__(NT) void k_snap_walk_lds(SnapCtx X) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  if (k >= X.k1) return;
+  if (!valid) return;
   B.finish(-1);
+  if (RELINK) {
+    X.t_out[k] = o;
+    X.t_exit[k] = (!ok || dead) ? -1 : (int32_t)p;
+    return;
+  }
   X.w_exit[k] = (!ok || dead) ? -1 : (int32_t)p;
   X.w_out[k] = o;
   X.w_npos[k] = n;
@@ -564,9 +583,12 @@ __global__ __launch_bounds__(NT) void k_snap_walk(SnapCtx X) {
 // (WIN: tags parse from a register window, one load per window instead of a dependent load pair per
 // tag -- k_snap_link, whose lanes that never meet the walker's recorded positions walk the whole
 // segment and set the kernel's duration; k_snap_fix keeps the per-tag loads, its VGPR budget is spent)
+__device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS / DK_LINK_STATS builds only (tools/snap_stats.py)
+
 template <bool WIN = false>
 __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, const uint8_t* in, int64_t clen, int64_t e,
-                                              bool merge, int32_t* tout, int32_t* texit, bool bits = false) {
+                                              bool merge, int32_t* tout, int32_t* texit, bool bits = false,
+                                              int* st = nullptr, int budget = 1 << 30) {
   const int64_t end = (int64_t)j * SNAP_SEG + SNAP_SEG < clen ? (int64_t)j * SNAP_SEG + SNAP_SEG : clen;
   // bits (e verified): the bitmap words up to the join point are rewritten from the true chain (the
   // walker's words from there on are already right; without a join every word is rewritten)
@@ -578,21 +600,25 @@ __device__ __forceinline__ void snap_seg_from(const SnapCtx& X, int k, int j, co
   int jj = 0;
   int32_t pj = n > 0 ? X.w_pos[k] : 0;
   SnapRegWin W{in};
+  int nt = 0;
   while (true) {
     while (jj < n && pj < p) { jj++; pj = jj < n ? X.w_pos[(int64_t)jj * X.nseg + k] : 0; }
     if (jj < n && pj == p) {                 // joined the walker's chain
       *tout = o + X.w_out[k] - X.w_cum[(int64_t)jj * X.nseg + k];
       *texit = X.w_exit[k];
       B.finish(p);
+      if (st) { st[0] = nt; st[1] = 1; st[2] = jj; }
       return;
     }
-    if (p >= end) { *tout = o; *texit = (int32_t)p; B.finish(-1); return; }
+    if (p >= end) { *tout = o; *texit = (int32_t)p; B.finish(-1); if (st) { st[0] = nt; st[1] = 0; st[2] = n; } return; }
+    if (nt >= budget) { *texit = -2; if (st) { st[0] = nt; st[1] = 0; st[2] = jj; } return; }   // relink
     int32_t adv, len;
     const bool good = WIN ? snap_parse_w(W, clen, p, &adv, &len) : snap_parse(in, clen, p, &adv, &len);
     if (!good) { *tout = o; *texit = -1; B.finish(-1); return; }
     B.mark(p);
     o += len;
     p += adv;
+    nt++;
   }
 }
 
@@ -613,7 +639,37 @@ __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
       e = X.w_exit[k - 1];
       // (the tag-start bits from e to where it meets the walker are written on the way: they are the
       // true chain's whenever e is the true entry, which k_snap_fix checks)
-      snap_seg_from<DK_SF_LINK_WIN>(X, k, j, in, clen, e, true, &tout, &tex, X.tbits != nullptr);
+#ifdef DK_LINK_STATS
+      // (stats build, tools/link_stats.py): lanes, merged, tags walked, max, >16, >64, >256, tags of
+      // lanes > 64, lanes entering past the walker's last recorded position, clock of the walk
+      int st[3] = {0, 0, 0};
+      const unsigned long long c0 = clock64();
+      snap_seg_from<DK_SF_LINK_WIN>(X, k, j, in, clen, e, true, &tout, &tex, X.tbits != nullptr, st,
+                                    X.relink ? DK_SF_LINK_BUDGET : (1 << 30));
+      const unsigned long long cy = clock64() - c0;
+      const int nrec = X.w_npos[k];
+      atomicAdd(&dk_snap_stats[0], 1ull);
+      atomicAdd(&dk_snap_stats[1], (unsigned long long)st[1]);
+      atomicAdd(&dk_snap_stats[2], (unsigned long long)st[0]);
+      atomicMax(&dk_snap_stats[3], (unsigned long long)st[0]);
+      atomicAdd(&dk_snap_stats[4], (unsigned long long)(st[0] > 16));
+      atomicAdd(&dk_snap_stats[5], (unsigned long long)(st[0] > 64));
+      atomicAdd(&dk_snap_stats[6], (unsigned long long)(st[0] > 256));
+      if (st[0] > 64) atomicAdd(&dk_snap_stats[7], (unsigned long long)st[0]);
+      atomicAdd(&dk_snap_stats[8], (unsigned long long)(nrec > 0 && e > X.w_pos[(int64_t)(nrec - 1) * X.nseg + k]));
+      atomicMax(&dk_snap_stats[9], cy);
+      atomicAdd(&dk_snap_stats[10], cy);
+      atomicAdd(&dk_snap_stats[11], (unsigned long long)(nrec < SNAP_REC));
+      atomicAdd(&dk_snap_stats[12], (unsigned long long)(e >= (int64_t)j * SNAP_SEG + SNAP_SEG));
+#else
+      snap_seg_from<DK_SF_LINK_WIN>(X, k, j, in, clen, e, true, &tout, &tex, X.tbits != nullptr, nullptr,
+                                    X.relink ? DK_SF_LINK_BUDGET : (1 << 30));
+#endif
+      if (tex == -2) {                       // not joined within the budget: the staged relink pass
+        X.relink[X.k0 + atomicAdd(&X.relink_n[X.k0], 1)] = k;
+        X.t_entry[k] = e;
+        return;
+      }
     }
   }
   X.t_entry[k] = e;
@@ -645,7 +701,6 @@ __device__ __forceinline__ int32_t dpp_shr1(int32_t v) {         // lane i gets 
   return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
 }
 
-__device__ unsigned long long dk_snap_stats[24];   // DK_SNAP_STATS builds only (tools/snap_stats.py)
 __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
 #ifdef DK_SNAP_STATS
   const unsigned long long fc0 = clock64();
@@ -4448,6 +4503,15 @@ void launch_page_headers(const DChunk* c, DPage* p, int n, hipStream_t s) {
 }
 void snap_stats(unsigned long long* out) { (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(dk_snap_stats), 24 * 8); }
 
+// speculative walk, link, and the staged relink of the segments the link did not join within its budget
+static void snap_walk_link(const SnapCtx& X, int g, hipStream_t s) {
+  if (DK_SF_WALK_LDS) hipLaunchKernelGGL(k_snap_walk_lds<false>, dim3(g), dim3(NT), 0, s, X);
+  else hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
+  if (X.relink) (void)hipMemsetAsync(X.relink_n + X.k0, 0, 4, s);   // the slice's own counter and list
+  hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+  if (X.relink) hipLaunchKernelGGL(k_snap_walk_lds<true>, dim3(g), dim3(NT), 0, s, X);
+}
+
 static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s) {
   hipLaunchKernelGGL(k_snap_frag, dim3(n), dim3(64), 0, s, X, work);
 }
@@ -4464,9 +4528,7 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
     if (phase == 0) {
       (void)hipMemsetAsync(X.serial + X.c0, 0, (size_t)n_cp * 4, s);
       if (X.tbits && g > 0) {             // tag-start bitmap: speculative walk + link
-        if (DK_SF_WALK_LDS) hipLaunchKernelGGL(k_snap_walk_lds, dim3(g), dim3(NT), 0, s, X);
-        else hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
-        hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+        snap_walk_link(X, g, s);
       }
     } else if (phase == 1) {
       if (X.tbits) hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
@@ -4478,9 +4540,7 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
   }
   if (phase == 0) {
     if (g > 0) {
-      if (DK_SF_WALK_LDS) hipLaunchKernelGGL(k_snap_walk_lds, dim3(g), dim3(NT), 0, s, X);
-      else hipLaunchKernelGGL(k_snap_walk, dim3(g), dim3(NT), 0, s, X);
-      hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
+      snap_walk_link(X, g, s);
     }
   } else if (phase == 1) {
     hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
@@ -5330,7 +5390,7 @@ namespace dk {
 // getScanFiles (round-3 cold snapshot load: 242 ms, 5 ms warm). Returns the kernels touched.
 int warm_kernels() {
   const void* fns[] = {
-      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_walk_lds, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
+      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_walk_lds<false>, (const void*)k_snap_walk_lds<true>, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
       (const void*)k_snap_frag, (const void*)k_snappy_serial, (const void*)k_pos_count,
       (const void*)k_pos_scan, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
