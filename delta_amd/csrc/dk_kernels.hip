@@ -677,6 +677,22 @@ __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
   X.t_exit[k] = tex;
 }
 
+#ifndef DK_SF_RECHECK
+#define DK_SF_RECHECK 1              // recheck rounds
+#endif
+// segments whose linked entry differs from the previous segment's linked exit go to the relink list
+// with that exit as their entry (a -1 exit is left to k_snap_fix, which fails the page)
+__global__ __launch_bounds__(NT) void k_snap_recheck(SnapCtx X) {
+  const int k = X.k0 + blockIdx.x * NT + threadIdx.x;
+  if (k >= X.k1) return;
+  const int ci = X.spage[k];
+  if (k == X.sbase[ci]) return;                      // a page's first segment starts on the true chain
+  const int32_t pe = X.t_exit[k - 1];
+  if (pe < 0 || pe == X.t_entry[k]) return;
+  X.t_entry[k] = pe;
+  X.relink[X.k0 + atomicAdd(&X.relink_n[X.k0], 1)] = k;
+}
+
 // wave64 inclusive scans with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 / 31
 // across rows): VALU only, no LDS round trip
 __device__ __forceinline__ int32_t dpp_scan_add(int32_t v) {
@@ -4510,6 +4526,14 @@ static void snap_walk_link(const SnapCtx& X, int g, hipStream_t s) {
   if (X.relink) (void)hipMemsetAsync(X.relink_n + X.k0, 0, 4, s);   // the slice's own counter and list
   hipLaunchKernelGGL(k_snap_link, dim3(g), dim3(NT), 0, s, X);
   if (X.relink) hipLaunchKernelGGL(k_snap_walk_lds<true>, dim3(g), dim3(NT), 0, s, X);
+  // one parallel recheck: a segment whose linked entry is not its predecessor's linked exit (that
+  // predecessor's walker never joined the true chain) is walked again from that exit, so k_snap_fix's
+  // wave per page finds (almost) nothing to correct one segment after another
+  for (int it = 0; X.relink && it < DK_SF_RECHECK; it++) {
+    (void)hipMemsetAsync(X.relink_n + X.k0, 0, 4, s);
+    hipLaunchKernelGGL(k_snap_recheck, dim3(g), dim3(NT), 0, s, X);
+    hipLaunchKernelGGL(k_snap_walk_lds<true>, dim3(g), dim3(NT), 0, s, X);
+  }
 }
 
 static void launch_frag(const SnapCtx& X, int n, const int2* work, hipStream_t s) {
@@ -5390,7 +5414,7 @@ namespace dk {
 // getScanFiles (round-3 cold snapshot load: 242 ms, 5 ms warm). Returns the kernels touched.
 int warm_kernels() {
   const void* fns[] = {
-      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_walk_lds<false>, (const void*)k_snap_walk_lds<true>, (const void*)k_snap_link, (const void*)k_snap_fix, (const void*)k_snap_bounds,
+      (const void*)k_page_headers, (const void*)k_snap_walk, (const void*)k_snap_walk_lds<false>, (const void*)k_snap_walk_lds<true>, (const void*)k_snap_link, (const void*)k_snap_recheck, (const void*)k_snap_fix, (const void*)k_snap_bounds,
       (const void*)k_snap_frag, (const void*)k_snappy_serial, (const void*)k_pos_count,
       (const void*)k_pos_scan, (const void*)k_pos_fallback, (const void*)k_delta_decode,
       (const void*)k_page_runs, (const void*)k_tile_count, (const void*)k_tile_scan1, (const void*)k_tile_chars,
