@@ -45,7 +45,7 @@ mean = {k: {c: big_mean(v) for c, v in d.items()} for k, d in acc.items()}
 
 # dominant global-load width per kernel (bytes per lane per load), from the kernel source
 WIDTH = {"k_string_copy": 16, "k_pos_count": 16, "k_pos_verify": 16, "k_copy_zc": 16,
-         "k_snap_walk": 16, "k_snap_link": 4, "k_snap_fix": 4, "k_snap_frag": 4, "k_tile_decode": 4,
+         "k_snap_walk": 16, "k_snap_walk_lds": 16, "k_snap_recheck": 4, "k_snap_link": 4, "k_snap_fix": 4, "k_snap_frag": 4, "k_tile_decode": 4,
          "k_tile_count": 4, "k_tile_chars": 4, "k_probe_fast_all": 8, "k_snappy_serial": 1}
 CALIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r03", "pmc_calib.json")
 try:
