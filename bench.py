@@ -519,6 +519,11 @@ def main(argv=None):
             owner_comm_error = "%s: %s" % (type(e).__name__, str(e)[:200])
             print("[rank %d] owner communicator failed (%s); exchange = allgather" % (rank, owner_comm_error),
                   file=sys.stderr)
+        # every rank takes the same mode: a communicator that failed anywhere drops it everywhere
+        if max_over_ranks(0.0 if owner is not None else 1.0) > 0 and owner is not None:
+            owner.close()
+            owner = None
+            owner_comm_error = owner_comm_error or "a peer rank could not create its communicator"
     owner_ms = []
     a2a_ms = []
 
