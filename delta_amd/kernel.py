@@ -1352,7 +1352,11 @@ class GpuScan:
             self.ckpt_index = list(range(len(all_files)))
             sel = None
         self.ckpt_files = [all_files[i] for i in self.ckpt_index]
-        leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else []) + REMOVE_LEAVES
+        # the checkpoint's remove columns are not read: ActiveAddFilesIterator ignores every remove of a
+        # checkpoint batch (ActiveAddFilesIterator.java:158-183, `if (!isFromCheckpoint)`) and only its
+        # add rows reach the scan files, so the fused engine pushes that into the projection (the
+        # commit tail's removes are parsed by the JSON tail parser)
+        leaves = ADD_LEAVES + ([STATS_LEAF] if self.read_stats else [])
         if self.skipping is not None:
             # the typed add.stats_parsed leaves of the program's stats paths: the engine evaluates
             # skipping over them where a checkpoint file carries them with a type that holds the stat
