@@ -677,6 +677,9 @@ __global__ __launch_bounds__(NT) void k_snap_link(SnapCtx X) {
   X.t_exit[k] = tex;
 }
 
+#ifndef DK_SF_FIX_RELINK
+#define DK_SF_FIX_RELINK 1           // k_snap_fix hands corrected segments' bitmap rewrites to the relink walk
+#endif
 #ifndef DK_SF_RECHECK
 #define DK_SF_RECHECK 1              // recheck rounds
 #endif
@@ -767,8 +770,15 @@ __global__ __launch_bounds__(64) void k_snap_fix(SnapCtx X) {
     // met the walker, so they are right wherever that entry was; a corrected segment's bits are
     // rewritten whole from its true entry (every lane its own segment)
     if (X.tbits && valid && fixed) {
-      int32_t to3, tx3;
-      snap_seg_from(X, k, k - k0, in, clen, e, false, &to3, &tx3, true);
+      if (X.relink && DK_SF_FIX_RELINK && !X.page_mode) {
+        // rewritten by the staged relink walk after this kernel (its own entry is final here):
+        // the page's wave does not wait on a serial walk of the whole segment
+        X.t_entry[k] = e;
+        X.relink[X.k0 + atomicAdd(&X.relink_n[X.k0], 1)] = k;
+      } else {
+        int32_t to3, tx3;
+        snap_seg_from(X, k, k - k0, in, clen, e, false, &to3, &tx3, true);
+      }
     }
     // output offsets: exclusive scan of tout
     int64_t x = tout;
@@ -4567,7 +4577,10 @@ void launch_snappy(const SnapCtx& X, int n_cp, int n_frag, const int2* work, int
       snap_walk_link(X, g, s);
     }
   } else if (phase == 1) {
+    const bool rl = X.relink && X.tbits && DK_SF_FIX_RELINK && g > 0;
+    if (rl) (void)hipMemsetAsync(X.relink_n + X.k0, 0, 4, s);
     hipLaunchKernelGGL(k_snap_fix, dim3(n_cp), dim3(64), 0, s, X);
+    if (rl) hipLaunchKernelGGL(k_snap_walk_lds<true>, dim3(g), dim3(NT), 0, s, X);   // corrected segments' bits
     if (X.tbits && n_frag) hipLaunchKernelGGL(k_snap_bounds, dim3(n_frag), dim3(64), 0, s, X, work);
   } else if (phase == 2) {
     if (n_frag) launch_frag(X, n_frag, work, s);
