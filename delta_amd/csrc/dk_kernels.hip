@@ -438,7 +438,7 @@ __device__ __forceinline__ bool snap_parse_w(SnapRegWin& W, int64_t clen, int64_
 #define DK_SF_WALK_STEP 128
 #endif
 #ifndef DK_SF_LINK_BUDGET
-#define DK_SF_LINK_BUDGET 32         // k_snap_link tags before a segment goes to the staged relink pass
+#define DK_SF_LINK_BUDGET 16         // k_snap_link tags before a segment goes to the staged relink pass
 #endif
 #ifndef DK_SF_LINK_WIN
 #define DK_SF_LINK_WIN 0             // 1: slower (415 vs 322 us, profiles/r06/walk_ab)
